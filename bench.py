@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""Headline benchmark: TeraSort GB/s sorted (whole node) on 1..8 MI355X.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+BASELINE.json metric: "GB/sec sorted (whole node), 1 TB TeraSort at 1/2/4/8 MI355X".  The
+reference's TeraSort (DryadLINQ OSDI'08 §5) is weak-scaled: a fixed partition per machine
+(3.87 GB), 240 machines ~ 1 TB at ~3.1 GB/s.  Here each GPU owns 125 GB (1.25e9 x 100-byte
+records, 10-byte keys) so 8 GPUs sort exactly 1 TB; per-GPU work is fixed as N grows ("weak").
+
+One step = read the input table (synthetic generator store, materialised in HBM) -> sample ->
+range partition -> RCCL all-to-all-v over xGMI -> local LSD radix sort -> row gather into the
+output table.  Nothing is cached between steps; the output is validated valsort-style (global
+checksum, record count, in-rank order, cross-rank boundaries) after the timed region.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_GBPS = 3.1   # DryadLINQ TeraSort, 240 machines, ~1 TB in ~319 s
+METRIC = "GB/sec sorted (whole node), 1 TB TeraSort at 1/2/4/8 MI355X"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--records-per-gpu", type=int, default=1_250_000_000)
+    ap.add_argument("--no-validate", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    from dryad_amd.parallel.comm import init_world, shutdown
+    from dryad_amd.models.terasort import TeraSortConfig, TeraSortJob, run_steps
+
+    world = init_world(device="cuda")
+    if world.size != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world.size}", file=sys.stderr)
+    cfg = TeraSortConfig(records_per_rank=args.records_per_gpu)
+    t_alloc = time.perf_counter()
+    job = TeraSortJob(cfg, world)
+    if world.rank == 0:
+        free, total = torch.cuda.mem_get_info(world.device)
+        print(f"[bench] allocated working set in {time.perf_counter() - t_alloc:.1f}s; HBM free {free/1e9:.1f} "
+              f"/ {total/1e9:.1f} GB", file=sys.stderr, flush=True)
+    expect = None
+    if not args.no_validate:
+        expect = job.input_checksum()
+    for i in range(args.warmup):
+        t0 = time.perf_counter()
+        job.step()
+        torch.cuda.synchronize()
+        if world.rank == 0:
+            print(f"[bench] warmup {i}: {time.perf_counter() - t0:.3f}s", file=sys.stderr, flush=True)
+    secs = run_steps(job, args.steps)
+    val = None
+    if expect is not None:
+        val = job.validate(*expect)
+    total_bytes = job.bytes_per_rank * world.size
+    ms = 1e3 * secs / max(args.steps, 1)
+    gbps = total_bytes / 1e9 / (secs / max(args.steps, 1))
+    if world.rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(gbps, 3),
+            "unit": "GB/s",
+            "n_gpus": world.size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(gbps / BASELINE_GBPS, 3),
+            "dtype": "uint8",
+            "data": "synthetic (gensort-style counter-generated 100-byte records, 10-byte random keys)",
+            "config": {
+                "model": "TeraSort 100-byte records / 10-byte key (OrderBy via range-partition + radix sort)",
+                "global_batch": job.n * world.size,
+                "seq_len": 100,
+                "parallelism": f"dp{world.size}",
+                "records_per_gpu": job.n,
+                "bytes_per_gpu": job.bytes_per_rank,
+                "total_bytes": total_bytes,
+                "validated": None if val is None else val["ok"],
+            },
+        }
+        if val is not None and not val["ok"]:
+            line["validation"] = val
+        print(json.dumps(line), flush=True)
+    shutdown()
+    if val is not None and not val["ok"]:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,423 @@
+// LSD radix sort of 128-bit (hi, lo) entries + key extraction + row gather, for gfx950.
+//
+// This is the engine behind OrderBy / Sort / MergeSort / RangePartition of the vertex operator
+// library (reference: LinqToDryad/DryadLinqVertex.cs:293-423 `Sort`/`MergeSort`, and the threaded
+// `ParallelSort` at :9321-9817 which sorts 2^21-element chunks and k-way merges them).  Instead of
+// comparison sorting boxed records we sort compact 16-byte (key, row-index) entries with a stable
+// reduce-then-scan LSD radix sort and then gather whole rows once (key-pointer sort).
+//
+// Per 8-bit pass:
+//   rs_count   : G workgroups, each owns a contiguous range of 2048-entry tiles and builds a
+//                256-bin LDS histogram (one sub-histogram per wave to cut LDS atomic contention)
+//   rs_scan_*  : exclusive scan of the [digit][block] count matrix (3 tiny kernels)
+//   rs_scatter : per tile, wave-level multi-split ranking with 64-bit ballots (8 ballots per
+//                64-entry row), block-local reorder through LDS so that each digit's run is
+//                written contiguously (coalesced 16-byte stores), stable across tiles/blocks.
+#include "common.h"
+
+namespace {
+
+constexpr int kRadixBits = 8;
+constexpr int kBins = 1 << kRadixBits;
+constexpr int kItems = 8;                  // entries per thread per tile
+constexpr int kTile = kBlock * kItems;     // 2048 entries per tile
+constexpr int kMaxGrid = 1024;             // workgroups for count/scatter (4 per CU)
+constexpr int kScanChunk = 4096;           // elements per scan workgroup (16 per thread)
+
+__device__ __forceinline__ uint32_t digit_of(const E128& e, int shift) {
+  return shift >= 64 ? (uint32_t)((e.hi >> (shift - 64)) & 0xFF)
+                     : (uint32_t)((e.lo >> shift) & 0xFF);
+}
+
+__global__ __launch_bounds__(256) void rs_count(const E128* __restrict__ in, uint64_t n, int shift,
+                                                uint32_t* __restrict__ counts, uint32_t G,
+                                                uint64_t per_block) {
+  __shared__ uint32_t hist[4][kBins];
+  const int t = threadIdx.x, w = wave_id();
+  for (int i = t; i < 4 * kBins; i += kBlock) (&hist[0][0])[i] = 0;
+  __syncthreads();
+  const bool use_hi = shift >= 64;
+  const int s = use_hi ? shift - 64 : shift;
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(in) + (use_hi ? 1 : 0);
+  const uint64_t beg = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  uint64_t i = beg + t;
+  // 8 independent loads in flight per thread before the LDS atomics.
+  for (; i + 7 * kBlock < end; i += 8 * kBlock) {
+    uint64_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = src[2 * (i + k * kBlock)];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) atomicAdd(&hist[w][(v[k] >> s) & 0xFF], 1u);
+  }
+  for (; i < end; i += kBlock) atomicAdd(&hist[w][(src[2 * i] >> s) & 0xFF], 1u);
+  __syncthreads();
+  const uint32_t c = hist[0][t] + hist[1][t] + hist[2][t] + hist[3][t];
+  counts[(uint64_t)t * G + blockIdx.x] = c;
+}
+
+// --- exclusive scan of a uint32 array of length M (M <= 256 * kScanChunk) ---
+__global__ __launch_bounds__(256) void rs_scan_reduce(const uint32_t* __restrict__ a, uint32_t M,
+                                                      uint32_t* __restrict__ partial) {
+  __shared__ uint32_t sc[4];
+  const uint32_t base = blockIdx.x * kScanChunk + threadIdx.x * 16;
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) s += (base + k < M) ? a[base + k] : 0u;
+  uint32_t total;
+  block_exclusive_scan256(s, sc, total);
+  if (threadIdx.x == 0) partial[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void rs_scan_partials(uint32_t* __restrict__ partial, uint32_t S) {
+  __shared__ uint32_t sc[4];
+  const uint32_t t = threadIdx.x;
+  uint32_t v = t < S ? partial[t] : 0u;
+  uint32_t total;
+  uint32_t ex = block_exclusive_scan256(v, sc, total);
+  if (t < S) partial[t] = ex;
+}
+
+__global__ __launch_bounds__(256) void rs_scan_down(uint32_t* __restrict__ a, uint32_t M,
+                                                    const uint32_t* __restrict__ partial) {
+  __shared__ uint32_t sc[4];
+  const uint32_t base = blockIdx.x * kScanChunk + threadIdx.x * 16;
+  uint32_t v[16];
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = (base + k < M) ? a[base + k] : 0u;
+    s += v[k];
+  }
+  uint32_t total;
+  uint32_t run = block_exclusive_scan256(s, sc, total) + partial[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (base + k < M) a[base + k] = run;
+    run += v[k];
+  }
+}
+
+__global__ __launch_bounds__(256) void rs_scatter(const E128* __restrict__ in, E128* __restrict__ out,
+                                                  uint64_t n, int shift,
+                                                  const uint32_t* __restrict__ offsets, uint32_t G,
+                                                  uint64_t per_block) {
+  __shared__ E128 stage[kTile];          // 32 KiB
+  __shared__ uint32_t wcnt[4][kBins];    // per-wave digit counters, later wave prefixes
+  __shared__ uint32_t goff[kBins];       // running global output offset of each digit
+  __shared__ uint32_t bstart[kBins];     // in-tile start of each digit
+  __shared__ uint32_t sc[4];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  goff[t] = offsets[(uint64_t)t * G + blockIdx.x];
+  const uint64_t beg = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  for (uint64_t base = beg; base < end; base += kTile) {
+    const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kTile ? (end - base) : kTile);
+    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    __syncthreads();
+    E128 e[kItems];
+    uint32_t rk[kItems], dg[kItems];
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+      const bool valid = pos < cnt;
+      if (valid) e[r] = in[base + pos];
+      const uint32_t d = valid ? digit_of(e[r], shift) : 0u;
+      uint64_t peers = ballot64(valid);
+#pragma unroll
+      for (int k = 0; k < kRadixBits; ++k) {
+        const bool bit = (d >> k) & 1u;
+        const uint64_t b = ballot64(bit);
+        peers &= bit ? b : ~b;
+      }
+      const uint32_t below = popc_below(peers);
+      const uint32_t prior = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      rk[r] = prior + below;
+      dg[r] = d;
+    }
+    __syncthreads();
+    {
+      const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+      const uint32_t tot = c0 + c1 + c2 + c3;
+      wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
+      uint32_t all;
+      const uint32_t ex = block_exclusive_scan256(tot, sc, all);
+      bstart[t] = ex;
+      // stash tile totals in the upper half of `sc`-free storage: reuse goff update after use.
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < kItems; ++r) {
+        const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+        if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = e[r];
+      }
+      __syncthreads();
+      for (uint32_t j = t; j < cnt; j += kBlock) {
+        const E128 v = stage[j];
+        const uint32_t d = digit_of(v, shift);
+        out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+      }
+      __syncthreads();
+      goff[t] += tot;
+    }
+    __syncthreads();
+  }
+}
+
+void scan_inplace(uint32_t* a, uint32_t M, uint32_t* partial, hipStream_t s) {
+  const uint32_t S = (M + kScanChunk - 1) / kScanChunk;
+  rs_scan_reduce<<<S, 256, 0, s>>>(a, M, partial);
+  rs_scan_partials<<<1, 256, 0, s>>>(partial, S);
+  rs_scan_down<<<S, 256, 0, s>>>(a, M, partial);
+}
+
+inline void sort_geometry(uint64_t n, uint32_t& G, uint64_t& per_block) {
+  uint64_t tiles = (n + kTile - 1) / kTile;
+  if (tiles < 1) tiles = 1;
+  G = (uint32_t)(tiles < (uint64_t)kMaxGrid ? tiles : (uint64_t)kMaxGrid);
+  per_block = ((tiles + G - 1) / G) * kTile;
+}
+
+}  // namespace
+
+// Workspace needed by dr_sort_u128 (bytes).
+DR_API uint64_t dr_sort_u128_workspace(uint64_t n) {
+  uint32_t G; uint64_t per_block;
+  sort_geometry(n, G, per_block);
+  const uint64_t M = (uint64_t)kBins * G;
+  return (M + 1024) * sizeof(uint32_t);
+}
+
+// Stable LSD radix sort of `n` entries on composite key bits [begin_bit, end_bit) (multiples of 8;
+// bit 0 = lsb of lo, bit 64 = lsb of hi).  Ping-pongs between `keys` and `tmp`; *result_in_tmp
+// tells the caller where the sorted sequence ended up.  Returns a hipError_t.
+DR_API int dr_sort_u128(E128* keys, E128* tmp, uint64_t n, int begin_bit, int end_bit, void* ws,
+                        hipStream_t s, int* result_in_tmp) {
+  *result_in_tmp = 0;
+  if (n == 0 || begin_bit >= end_bit) return 0;
+  if ((begin_bit & 7) || (end_bit & 7) || end_bit > 128 || begin_bit < 0) return (int)hipErrorInvalidValue;
+  if (n >= (1ull << 32)) return (int)hipErrorInvalidValue;
+  uint32_t G; uint64_t per_block;
+  sort_geometry(n, G, per_block);
+  uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* partial = counts + (uint64_t)kBins * G;
+  E128* src = keys;
+  E128* dst = tmp;
+  int flips = 0;
+  for (int shift = begin_bit; shift < end_bit; shift += kRadixBits) {
+    rs_count<<<G, 256, 0, s>>>(src, n, shift, counts, G, per_block);
+    scan_inplace(counts, kBins * G, partial, s);
+    rs_scatter<<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+    E128* x = src; src = dst; dst = x;
+    flips ^= 1;
+  }
+  DR_LAUNCH_CHECK();
+  *result_in_tmp = flips;
+  return 0;
+}
+
+// Per-digit totals of one pass (used by partition ops that only need the histogram of a small
+// digit, e.g. destination ids): writes kBins uint64 totals of digit at `shift`.
+namespace {
+__global__ void rs_digit_totals(const uint32_t* __restrict__ counts_scanned, uint32_t G, uint64_t n,
+                                uint64_t* __restrict__ starts) {
+  const int t = threadIdx.x;
+  starts[t] = counts_scanned[(uint64_t)t * G];
+  if (t == 0) starts[kBins] = n;
+}
+}  // namespace
+
+// One stable counting-sort pass on the 8-bit digit at `shift`; additionally reports the start
+// offset of every digit value in `digit_starts` (kBins + 1 uint64, device).  This is the
+// partition primitive (hash / range partition by destination id).
+DR_API int dr_partition_pass_u128(const E128* in, E128* out, uint64_t n, int shift, void* ws,
+                                  uint64_t* digit_starts, hipStream_t s) {
+  if (n >= (1ull << 32) || (shift & 7) || shift > 120) return (int)hipErrorInvalidValue;
+  if (n == 0) {
+    hipMemsetAsync(digit_starts, 0, sizeof(uint64_t) * (kBins + 1), s);
+    return 0;
+  }
+  uint32_t G; uint64_t per_block;
+  sort_geometry(n, G, per_block);
+  uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* partial = counts + (uint64_t)kBins * G;
+  rs_count<<<G, 256, 0, s>>>(in, n, shift, counts, G, per_block);
+  scan_inplace(counts, kBins * G, partial, s);
+  rs_digit_totals<<<1, kBins, 0, s>>>(counts, G, n, digit_starts);
+  rs_scatter<<<G, 256, 0, s>>>(in, out, n, shift, counts, G, per_block);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Key extraction from fixed-width rows: key bytes [key_off, key_off + key_len), key_len <= 12,
+// compared as unsigned big-endian bytes (memcmp order, = TeraSort / byte-string order).
+//   hi = key bytes 0..7, lo = key bytes 8..11 in bits 63..32, row index (idx_base + i) in 31..0.
+namespace {
+__global__ __launch_bounds__(256) void extract_keys_kernel(const uint8_t* __restrict__ rows, uint64_t n,
+                                                           uint32_t stride, uint32_t key_off,
+                                                           uint32_t key_len, uint32_t idx_base,
+                                                           E128* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint8_t* r = rows + i * stride + key_off;
+    uint64_t hi = 0, lo = 0;
+    if (((stride | key_off) & 3) == 0) {
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(r);
+      uint32_t b[3] = {0, 0, 0};
+      const uint32_t nw = (key_len + 3) >> 2;
+      for (uint32_t k = 0; k < nw; ++k) b[k] = bswap32(w[k]);
+      // mask bytes beyond key_len
+      uint32_t full = key_len;
+      for (int k = 0; k < 3; ++k) {
+        const int bytes = (int)full - 4 * k;
+        if (bytes <= 0) b[k] = 0;
+        else if (bytes < 4) b[k] &= 0xFFFFFFFFu << (8 * (4 - bytes));
+      }
+      hi = ((uint64_t)b[0] << 32) | b[1];
+      lo = (uint64_t)b[2] << 32;
+    } else {
+      for (uint32_t k = 0; k < key_len; ++k) {
+        const uint64_t v = r[k];
+        if (k < 8) hi |= v << (8 * (7 - k));
+        else lo |= v << (8 * (11 - k) + 32);
+      }
+    }
+    E128 e;
+    e.hi = hi;
+    e.lo = lo | (uint32_t)(idx_base + (uint32_t)i);
+    out[i] = e;
+  }
+}
+
+// Specialisation for the TeraSort record (stride 100, 10-byte key at offset 0): three dword loads.
+__global__ __launch_bounds__(256) void extract_keys_ts(const uint32_t* __restrict__ rows, uint64_t n,
+                                                       uint32_t idx_base, E128* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t* r = rows + i * 25;
+    const uint32_t w0 = r[0], w1 = r[1], w2 = r[2];
+    E128 e;
+    e.hi = ((uint64_t)bswap32(w0) << 32) | bswap32(w1);
+    e.lo = ((uint64_t)(bswap32(w2) & 0xFFFF0000u) << 32) | (uint32_t)(idx_base + (uint32_t)i);
+    out[i] = e;
+  }
+}
+}  // namespace
+
+DR_API int dr_extract_keys(const uint8_t* rows, uint64_t n, uint32_t stride, uint32_t key_off,
+                           uint32_t key_len, uint32_t idx_base, E128* out, hipStream_t s) {
+  if (key_len == 0 || key_len > 12) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  const unsigned g = grid_for(n, 256, 16384);
+  if (stride == 100 && key_off == 0 && key_len == 10)
+    extract_keys_ts<<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows), n, idx_base, out);
+  else
+    extract_keys_kernel<<<g, 256, 0, s>>>(rows, n, stride, key_off, key_len, idx_base, out);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Row gather: out[i] = rows[idx(i)] for fixed-width rows (stride multiple of 4 bytes), where
+// idx(i) is the low 32 bits of entries[i].lo (key-pointer sort result) or an explicit int64 index.
+// A workgroup handles 256 output rows: indices staged in LDS, then the 256*W output dwords are
+// written fully coalesced; each 64-lane load instruction reads ~2.5 rows of contiguous bytes.
+namespace {
+template <int WCONST>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint32_t* __restrict__ in,
+                                                          uint32_t* __restrict__ out,
+                                                          const E128* __restrict__ ent,
+                                                          const int64_t* __restrict__ idx64,
+                                                          uint64_t n, uint32_t Wdyn) {
+  const uint32_t W = WCONST > 0 ? (uint32_t)WCONST : Wdyn;
+  __shared__ uint64_t sidx[256];
+  const int t = threadIdx.x;
+  for (uint64_t row0 = (uint64_t)blockIdx.x * 256; row0 < n; row0 += (uint64_t)gridDim.x * 256) {
+    if (row0 + t < n) sidx[t] = ent ? (uint64_t)(uint32_t)ent[row0 + t].lo : (uint64_t)idx64[row0 + t];
+    __syncthreads();
+    const uint32_t rows = (uint32_t)((n - row0) < 256 ? (n - row0) : 256);
+    const uint32_t words = rows * W;
+    uint32_t* o = out + row0 * W;
+    uint32_t j = t;
+    for (; j + 3 * 256 < words; j += 4 * 256) {
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t jj = j + k * 256;
+        const uint32_t r = jj / W, c = jj - r * W;
+        v[k] = in[sidx[r] * W + c];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[j + k * 256] = v[k];
+    }
+    for (; j < words; j += 256) {
+      const uint32_t r = j / W, c = j - r * W;
+      o[j] = in[sidx[r] * W + c];
+    }
+    __syncthreads();
+  }
+}
+}  // namespace
+
+DR_API int dr_gather_rows(const uint8_t* rows, uint8_t* out, const E128* entries, const int64_t* idx,
+                          uint64_t n, uint32_t stride, hipStream_t s) {
+  if (stride == 0 || (stride & 3)) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  const uint32_t W = stride / 4;
+  const unsigned g = grid_for(n, 256, 16384);
+  const uint32_t* in = reinterpret_cast<const uint32_t*>(rows);
+  uint32_t* o = reinterpret_cast<uint32_t*>(out);
+  if (W == 25)
+    gather_rows_kernel<25><<<g, 256, 0, s>>>(in, o, entries, idx, n, W);
+  else
+    gather_rows_kernel<0><<<g, 256, 0, s>>>(in, o, entries, idx, n, W);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Range destination: for each entry, dest = #separators strictly below its key (ascending) or
+// strictly above (descending).  Key = (hi, lo & lo_mask).  Separators live in LDS (<= 255).
+// Writes (hi = dest, lo = original lo) to `out` (may alias `in`), ready for one partition pass
+// at shift 64.  Mirrors DryadLinqVertex.RangePartition + DryadLinqUtil.BinarySearch
+// (reference LinqToDryad/DryadLinqVertex.cs:4909-5151, DryadLinqUtil.cs:112-140).
+namespace {
+__global__ __launch_bounds__(256) void range_dest_kernel(const E128* __restrict__ in, E128* __restrict__ out,
+                                                         uint64_t n, const E128* __restrict__ seps,
+                                                         uint32_t nsep, uint64_t lo_mask, int desc) {
+  __shared__ uint64_t shi[256], slo[256];
+  for (uint32_t k = threadIdx.x; k < nsep; k += blockDim.x) {
+    shi[k] = seps[k].hi;
+    slo[k] = seps[k].lo & lo_mask;
+  }
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    E128 e = in[i];
+    const uint64_t kh = e.hi, kl = e.lo & lo_mask;
+    // branchless binary search for the count of separators "before" the key
+    uint32_t lo = 0, hi = nsep;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const uint64_t sh = shi[mid], sl = slo[mid];
+      const bool before = desc ? (sh > kh || (sh == kh && sl > kl)) : (sh < kh || (sh == kh && sl < kl));
+      lo = before ? mid + 1 : lo;
+      hi = before ? hi : mid;
+    }
+    e.hi = lo;
+    out[i] = e;
+  }
+}
+}  // namespace
+
+DR_API int dr_range_dest_u128(const E128* in, E128* out, uint64_t n, const E128* seps, uint32_t nsep,
+                              uint64_t lo_mask, int descending, hipStream_t s) {
+  if (nsep > 255) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  range_dest_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(in, out, n, seps, nsep, lo_mask, descending);
+  DR_LAUNCH_CHECK();
+  return 0;
+}

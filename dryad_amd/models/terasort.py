@@ -1,0 +1,112 @@
+"""TeraSort workload (BASELINE.json headline: "GB/sec sorted (whole node), 1 TB TeraSort").
+
+The DryadLINQ TeraSort experiment (OSDI'08 §5) is a *weak-scaling* sort: every machine holds a
+fixed 3.87 GB partition of 100-byte records (10-byte key) and the table grows with the machine
+count (240 machines ~ 1 TB).  This module reproduces that job on MI355X ranks: each rank owns
+``records_per_rank`` records of the global synthetic table (default 1.25e9 = 125 GB, so 8 ranks
+= 1 TB), and one step is
+
+    FromStore(gen) -> OrderBy(r.key) -> ToStore(hbm://)
+
+executed as generate (read the input table) -> sample/range-partition -> RCCL all-to-all-v ->
+local radix sort -> row gather into the HBM output table.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+
+import torch
+
+from ..ops import recordsort as RS
+from ..ops import terasort as TS
+from ..parallel import shuffle
+from ..parallel.comm import World, get_world
+
+RECORD = TS.RECORD_BYTES
+KEYLEN = TS.KEY_BYTES
+
+
+@dataclass
+class TeraSortConfig:
+    records_per_rank: int = 1_250_000_000
+    seed: int = 0x5EED_7E4A_50A7
+    sample_target: int = 1 << 20
+    slack: float = 0.01          # receive-buffer headroom for range-partition skew
+
+
+class TeraSortJob:
+    def __init__(self, cfg: TeraSortConfig, world: World | None = None):
+        self.cfg = cfg
+        self.world = world or get_world()
+        dev = self.world.device
+        cap = cfg.records_per_rank if self.world.size == 1 else int(cfg.records_per_rank * (1 + cfg.slack))
+        self.bufs = RS.SortBuffers.allocate(cap, RECORD, dev)
+        self.n = cfg.records_per_rank
+        self.out = None
+        self.stats = RS.SortStats()
+
+    @property
+    def bytes_per_rank(self) -> int:
+        return self.n * RECORD
+
+    def generate(self):
+        first = self.world.rank * self.n
+        TS.generate(self.bufs.rows_in[: self.n], first, self.cfg.seed)
+
+    def step(self):
+        self.generate()
+        self.out = RS.distributed_sort_rows(self.bufs, self.n, 0, KEYLEN, self.world,
+                                            sample_target=self.cfg.sample_target, stats=self.stats)
+        return self.out
+
+    def input_checksum(self) -> tuple[int, int]:
+        self.generate()
+        acc = TS.check(self.bufs.rows_in[: self.n])
+        shuffle.all_reduce_(acc, "sum", self.world)
+        return int(acc[0].item()), self.n * self.world.size
+
+    def validate(self, expect_hash: int, expect_records: int) -> dict:
+        """valsort: global hash sum, record count, in-rank order and cross-rank boundaries."""
+        out = self.out
+        acc = TS.check(out)
+        cnt = torch.tensor([out.shape[0]], dtype=torch.int64, device=out.device)
+        shuffle.all_reduce_(acc, "sum", self.world)
+        shuffle.all_reduce_(cnt, "sum", self.world)
+        # boundary: last key of rank r <= first key of rank r+1 (empty ranks skipped)
+        ends = torch.zeros((1, 2 * KEYLEN + 1), dtype=torch.uint8, device=out.device)
+        if out.shape[0] > 0:
+            ends[0, 0] = 1
+            ends[0, 1:1 + KEYLEN] = out[0, :KEYLEN]
+            ends[0, 1 + KEYLEN:] = out[-1, :KEYLEN]
+        allends = shuffle.all_gather_tensor(ends, self.world).cpu().numpy()
+        boundary_ok = True
+        prev_last = None
+        for row in allends:
+            if row[0] == 0:
+                continue
+            first, last = bytes(row[1:1 + KEYLEN]), bytes(row[1 + KEYLEN:])
+            if prev_last is not None and prev_last > first:
+                boundary_ok = False
+            prev_last = last
+        h = int(acc[0].item())
+        ok = (h == expect_hash and int(acc[1].item()) == 0 and int(cnt.item()) == expect_records and boundary_ok)
+        return dict(ok=bool(ok), hash_match=h == expect_hash, violations=int(acc[1].item()),
+                    records=int(cnt.item()), boundary_ok=boundary_ok)
+
+
+def run_steps(job: TeraSortJob, steps: int) -> float:
+    """Run ``steps`` steps bracketed by barrier+synchronize; returns max-over-ranks seconds."""
+    w = job.world
+    dev = w.device
+    w.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        job.step()
+    torch.cuda.synchronize(dev)
+    w.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    shuffle.all_reduce_(t, "max", w)
+    return float(t.item())

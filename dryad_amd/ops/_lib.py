@@ -1,0 +1,115 @@
+"""ctypes binding of the gfx950 kernel library (``libdryad_kernels.so``).
+
+The library exposes an ``extern "C"`` launcher per kernel family (raw device pointers,
+sizes, ``hipStream_t``; return value = ``hipError_t``).  It is loaded lazily, *after* torch so
+the kernels bind to the HIP runtime torch already mapped.  On a machine with a GPU a missing
+library is a hard error (no silent eager fallback); on CPU-only machines the GPU operators are
+simply unavailable and the object/CPU executors are used instead.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+import torch
+
+from .._build import KERNEL_LIB
+
+_LOCK = threading.Lock()
+_LIB = None
+
+c_u64 = ctypes.c_uint64
+c_u32 = ctypes.c_uint32
+c_i32 = ctypes.c_int
+c_i64 = ctypes.c_int64
+c_f32 = ctypes.c_float
+c_f64 = ctypes.c_double
+vp = ctypes.c_void_p
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "dr_sort_u128_workspace": (c_u64, [c_u64]),
+    "dr_sort_u128": (c_i32, [vp, vp, c_u64, c_i32, c_i32, vp, vp, ctypes.POINTER(c_i32)]),
+    "dr_partition_pass_u128": (c_i32, [vp, vp, c_u64, c_i32, vp, vp, vp]),
+    "dr_extract_keys": (c_i32, [vp, c_u64, c_u32, c_u32, c_u32, c_u32, vp, vp]),
+    "dr_gather_rows": (c_i32, [vp, vp, vp, vp, c_u64, c_u32, vp]),
+    "dr_range_dest_u128": (c_i32, [vp, vp, c_u64, vp, c_u32, c_u64, c_i32, vp]),
+    "dr_terasort_gen": (c_i32, [vp, c_u64, c_u64, c_u64, vp]),
+    "dr_terasort_check": (c_i32, [vp, c_u64, vp, vp]),
+}
+
+
+class NativeKernelsMissing(RuntimeError):
+    pass
+
+
+def _register(lib, name, sig):
+    fn = getattr(lib, name)
+    fn.restype, fn.argtypes = sig
+    return fn
+
+
+def register_signatures(sigs: dict):
+    """Kernel modules add their launcher signatures here at import time."""
+    _SIGS.update(sigs)
+    if _LIB is not None:
+        for name, sig in sigs.items():
+            _register(_LIB, name, sig)
+
+
+def lib():
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        path = Path(os.environ.get("DRYAD_KERNEL_LIB", str(KERNEL_LIB)))
+        if not path.exists():
+            if os.environ.get("DRYAD_AUTOBUILD", "1") == "1":
+                from .._build import build_kernels
+                build_kernels()
+            if not path.exists():
+                raise NativeKernelsMissing(
+                    f"{path} not built: run `python -m dryad_amd._build` (hipcc --offload-arch=gfx950)")
+        l = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+        for name, sig in _SIGS.items():
+            _register(l, name, sig)
+        _LIB = l
+        return l
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except (NativeKernelsMissing, OSError, RuntimeError):
+        return False
+
+
+def stream_of(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def ptr(t: torch.Tensor | None):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"HIP kernel launcher {what} failed with hipError_t={rc}")
+
+
+def call(name: str, *args):
+    rc = getattr(lib(), name)(*args)
+    check(rc, name)
+    return rc
+
+
+def require_gpu_tensor(t: torch.Tensor, what: str):
+    if not t.is_cuda:
+        raise ValueError(f"{what}: expected a device (HBM) tensor, got {t.device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: expected a contiguous tensor")

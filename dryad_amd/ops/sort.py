@@ -1,0 +1,119 @@
+"""Sort / partition / gather operators over HBM-resident tensors (HIP kernels in csrc/kernels/sort.hip).
+
+Data model: a *sort entry* array is an ``int64`` tensor of shape ``[n, 2]`` whose rows are the
+16-byte ``E128`` structs of the kernels: column 0 = ``lo``, column 1 = ``hi``.  The composite key
+is ``(hi << 64) | lo`` compared unsigned; the row index of the record lives in the low 32 bits
+of ``lo`` (key-pointer sort).  Fixed-width record tables are ``uint8`` tensors ``[n, stride]``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import c_u32, c_u64, ptr, stream_of
+
+_WS_CACHE: dict = {}
+
+
+def _workspace(n: int, device) -> torch.Tensor:
+    nbytes = int(_lib.lib().dr_sort_u128_workspace(c_u64(max(n, 1))))
+    key = (device, nbytes)
+    ws = _WS_CACHE.get(key)
+    if ws is None:
+        # keep one workspace per (device, size); small (<= 1 MiB)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _WS_CACHE.clear()
+        _WS_CACHE[key] = ws
+    return ws
+
+
+def empty_entries(n: int, device) -> torch.Tensor:
+    return torch.empty((n, 2), dtype=torch.int64, device=device)
+
+
+def sort_entries(entries: torch.Tensor, begin_bit: int, end_bit: int,
+                 tmp: torch.Tensor | None = None) -> torch.Tensor:
+    """Stable LSD radix sort of E128 entries on composite bits [begin_bit, end_bit).
+
+    Returns the tensor holding the sorted entries (``entries`` or ``tmp``)."""
+    _lib.require_gpu_tensor(entries, "sort_entries")
+    n = entries.shape[0]
+    if n == 0 or begin_bit >= end_bit:
+        return entries
+    if tmp is None:
+        tmp = torch.empty_like(entries)
+    assert tmp.shape[0] >= n
+    ws = _workspace(n, entries.device)
+    flag = ctypes.c_int(0)
+    _lib.call("dr_sort_u128", ptr(entries), ptr(tmp), c_u64(n), begin_bit, end_bit, ptr(ws),
+              stream_of(entries), ctypes.byref(flag))
+    return tmp[:n] if flag.value else entries
+
+
+def partition_pass(entries: torch.Tensor, shift: int, out: torch.Tensor | None = None):
+    """One stable counting-sort pass on the byte digit at ``shift``.
+
+    Returns ``(out, starts)`` where ``starts`` is a device int64 tensor of 257 digit offsets."""
+    _lib.require_gpu_tensor(entries, "partition_pass")
+    n = entries.shape[0]
+    if out is None:
+        out = torch.empty_like(entries)
+    starts = torch.empty(257, dtype=torch.int64, device=entries.device)
+    ws = _workspace(n, entries.device)
+    _lib.call("dr_partition_pass_u128", ptr(entries), ptr(out), c_u64(n), shift, ptr(ws), ptr(starts),
+              stream_of(entries))
+    return out, starts
+
+
+def extract_keys(rows: torch.Tensor, key_off: int, key_len: int, idx_base: int = 0,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """Build E128 sort entries from the byte-string key of fixed-width rows (memcmp order)."""
+    _lib.require_gpu_tensor(rows, "extract_keys")
+    assert rows.dtype == torch.uint8 and rows.dim() == 2
+    n, stride = rows.shape
+    if out is None:
+        out = empty_entries(n, rows.device)
+    _lib.call("dr_extract_keys", ptr(rows), c_u64(n), c_u32(stride), c_u32(key_off), c_u32(key_len),
+              c_u32(idx_base), ptr(out), stream_of(rows))
+    return out[:n]
+
+
+def gather_rows(rows: torch.Tensor, entries: torch.Tensor | None = None, index: torch.Tensor | None = None,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    """out[i] = rows[idx(i)] with idx from the low 32 bits of ``entries[i].lo`` or from ``index``."""
+    _lib.require_gpu_tensor(rows, "gather_rows")
+    assert rows.dtype == torch.uint8 and rows.dim() == 2 and rows.shape[1] % 4 == 0
+    src = entries if entries is not None else index
+    n = src.shape[0]
+    if index is not None:
+        assert index.dtype == torch.int64 and index.is_contiguous()
+    if out is None:
+        out = torch.empty((n, rows.shape[1]), dtype=torch.uint8, device=rows.device)
+    _lib.call("dr_gather_rows", ptr(rows), ptr(out), ptr(entries), ptr(index), c_u64(n), c_u32(rows.shape[1]),
+              stream_of(rows))
+    return out[:n]
+
+
+def range_dest(entries: torch.Tensor, separators: torch.Tensor, lo_mask: int, descending: bool = False,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+    """Replace entries[i].hi by its destination partition (count of separators before the key)."""
+    _lib.require_gpu_tensor(entries, "range_dest")
+    n = entries.shape[0]
+    if out is None:
+        out = entries
+    nsep = separators.shape[0]
+    _lib.call("dr_range_dest_u128", ptr(entries), ptr(out), c_u64(n), ptr(separators), c_u32(nsep),
+              c_u64(lo_mask & 0xFFFFFFFFFFFFFFFF), int(descending), stream_of(entries))
+    return out
+
+
+def entries_to_key_int(entries: torch.Tensor, lo_keep_bits: int = 64):
+    """Host helper for tests: composite keys as Python ints (hi<<64 | lo masked)."""
+    e = entries.cpu().numpy()
+    mask = ((1 << lo_keep_bits) - 1) << (64 - lo_keep_bits) if lo_keep_bits < 64 else (1 << 64) - 1
+    out = []
+    for lo, hi in e.tolist():
+        out.append(((hi & (2**64 - 1)) << 64) | ((lo & (2**64 - 1)) & mask))
+    return out

@@ -1,0 +1,30 @@
+"""TeraSort record store kernels: synthetic generator + valsort-style checker (csrc/kernels/terasort.hip)."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import c_u64, ptr, stream_of
+
+RECORD_BYTES = 100
+KEY_BYTES = 10
+# lo-word mask that keeps the two key bytes stored in lo (bits 63..48) and drops the row index.
+LO_KEY_MASK_10 = 0xFFFF000000000000
+
+
+def generate(out: torch.Tensor, first_index: int, seed: int) -> torch.Tensor:
+    """Fill ``out`` ([n, 100] uint8, HBM) with records first_index .. first_index+n-1."""
+    _lib.require_gpu_tensor(out, "terasort.generate")
+    assert out.dtype == torch.uint8 and out.dim() == 2 and out.shape[1] == RECORD_BYTES
+    _lib.call("dr_terasort_gen", ptr(out), c_u64(out.shape[0]), c_u64(first_index), c_u64(seed & (2**64 - 1)),
+              stream_of(out))
+    return out
+
+
+def check(rows: torch.Tensor, acc: torch.Tensor | None = None) -> torch.Tensor:
+    """Accumulate [sum of record hashes mod 2^64, #adjacent order violations] into ``acc``."""
+    _lib.require_gpu_tensor(rows, "terasort.check")
+    if acc is None:
+        acc = torch.zeros(2, dtype=torch.int64, device=rows.device)
+    _lib.call("dr_terasort_check", ptr(rows), c_u64(rows.shape[0]), ptr(acc), stream_of(rows))
+    return acc

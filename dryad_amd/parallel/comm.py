@@ -1,0 +1,89 @@
+"""Process-group management: one process per GPU, RCCL over xGMI (``torch.distributed`` backend
+``"nccl"`` is RCCL on ROCm), ``gloo`` for CPU runs and tests.
+
+This replaces the reference's whole cluster plane (Peloponnese process manager, YARN AM,
+ProcessService HTTP mailboxes: SURVEY §2.4) for the single-node MI355X target: the set of
+"computers" is the set of ranks, membership is fixed for a job, and all data-plane transfers go
+through collectives on one communicator.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class World:
+    rank: int = 0
+    size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str | None = None
+
+    @property
+    def distributed(self) -> bool:
+        return self.size > 1 and dist.is_available() and dist.is_initialized()
+
+    def barrier(self):
+        if self.distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+
+_WORLD: World | None = None
+
+
+def env_world_size() -> int:
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def init_world(device: str | None = None, backend: str | None = None, timeout_s: int = 1800) -> World:
+    """Initialise (idempotently) the job's process group from torchrun-style env vars.
+
+    ``device``: "cuda" / "cpu" / None (cuda if available).  The backend defaults to nccl (RCCL) for
+    GPU ranks and gloo for CPU ranks."""
+    global _WORLD
+    if _WORLD is not None:
+        return _WORLD
+    size = env_world_size()
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_cuda = (device == "cuda") or (device is None and torch.cuda.is_available())
+    if use_cuda:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+    else:
+        dev = torch.device("cpu")
+    be = backend or ("nccl" if use_cuda else "gloo")
+    if size > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        kwargs = dict(backend=be, rank=rank, world_size=size, timeout=datetime.timedelta(seconds=timeout_s))
+        if be == "nccl":
+            kwargs["device_id"] = dev
+        dist.init_process_group(**kwargs)
+    _WORLD = World(rank=rank, size=size, local_rank=local_rank, device=dev, backend=be if size > 1 else None)
+    return _WORLD
+
+
+def set_world(w: World | None):
+    """Install an explicit world (tests, in-process executors)."""
+    global _WORLD
+    _WORLD = w
+
+
+def get_world() -> World:
+    return _WORLD if _WORLD is not None else World()
+
+
+def shutdown():
+    global _WORLD
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+    _WORLD = None

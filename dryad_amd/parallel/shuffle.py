@@ -1,0 +1,149 @@
+"""Shuffle engine: the Dryad CrossProduct channel pattern as RCCL collectives over xGMI.
+
+Reference mapping:
+  * R1 HashPartition/RangePartition -> Merge (``GraphBuilder.ConnectCrossProduct``, N x M files
+    served over HTTP) becomes a size exchange (all-to-all of int64 counts) followed by one
+    all-to-all-v of the payload.  On a fully connected 8-GPU xGMI node every GPU drives its 7
+    links concurrently, so the exchange is pairwise (alltoallv), never a ring.
+  * R2 full merge to one partition -> gather to the root.
+  * R3 Tee broadcast -> broadcast / all-gather.
+  * R4 aggregation trees -> all-reduce (dense) or all-to-all + local combine (sparse keys).
+  * R5 sampler gather -> all-gather of the samples.
+
+Large exchanges are issued in chunks (``DRYAD_SHUFFLE_CHUNK_BYTES``, default 4 GiB per peer per
+round) so that RCCL's internal staging and the int32 limits of some code paths are never hit and
+so a later version can overlap the next chunk's pack kernel with the current transfer.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+from .comm import World, get_world
+
+CHUNK_BYTES = int(os.environ.get("DRYAD_SHUFFLE_CHUNK_BYTES", str(4 << 30)))
+
+
+def exchange_counts(send_counts: torch.Tensor, world: World | None = None) -> torch.Tensor:
+    """All-to-all of per-destination counts (int64 [world]).  Returns the receive counts."""
+    w = world or get_world()
+    if w.size == 1:
+        return send_counts.clone()
+    dev = w.device if w.backend == "nccl" else torch.device("cpu")
+    s = send_counts.to(dev, torch.int64).contiguous()
+    r = torch.empty_like(s)
+    dist.all_to_all_single(r, s)
+    return r.to(send_counts.device)
+
+
+def alltoallv_bytes(send: torch.Tensor, send_counts: list[int], recv: torch.Tensor, recv_counts: list[int],
+                    world: World | None = None):
+    """All-to-all-v over flat uint8 views: ``send`` is grouped by destination with
+    ``send_counts[d]`` bytes for rank d; ``recv`` receives ``recv_counts[s]`` bytes from rank s,
+    in source-rank order."""
+    w = world or get_world()
+    assert send.dtype == torch.uint8 and recv.dtype == torch.uint8
+    if w.size == 1:
+        n = send_counts[0]
+        recv[:n].copy_(send[:n])
+        return recv
+    assert len(send_counts) == w.size and len(recv_counts) == w.size
+    total_s, total_r = sum(send_counts), sum(recv_counts)
+    assert send.numel() >= total_s and recv.numel() >= total_r
+    maxpair = max(max(send_counts), max(recv_counts))
+    if maxpair <= CHUNK_BYTES:
+        dist.all_to_all_single(recv[:total_r], send[:total_s], output_split_sizes=list(recv_counts),
+                               input_split_sizes=list(send_counts))
+        return recv
+    # chunked rounds: every round moves up to CHUNK_BYTES from each source to each destination
+    soff = [0] * w.size
+    roff = [0] * w.size
+    acc = 0
+    for d in range(w.size):
+        soff[d] = acc
+        acc += send_counts[d]
+    acc = 0
+    for s_ in range(w.size):
+        roff[s_] = acc
+        acc += recv_counts[s_]
+    done_s = [0] * w.size
+    done_r = [0] * w.size
+    while any(done_s[d] < send_counts[d] for d in range(w.size)) or any(
+            done_r[s_] < recv_counts[s_] for s_ in range(w.size)):
+        ops = []
+        for peer in range(w.size):
+            ns = min(CHUNK_BYTES, send_counts[peer] - done_s[peer])
+            nr = min(CHUNK_BYTES, recv_counts[peer] - done_r[peer])
+            if peer == w.rank:
+                if ns > 0:
+                    recv[roff[peer] + done_r[peer]: roff[peer] + done_r[peer] + nr].copy_(
+                        send[soff[peer] + done_s[peer]: soff[peer] + done_s[peer] + ns])
+            else:
+                if ns > 0:
+                    ops.append(dist.P2POp(dist.isend, send[soff[peer] + done_s[peer]: soff[peer] + done_s[peer] + ns],
+                                          peer))
+                if nr > 0:
+                    ops.append(dist.P2POp(dist.irecv, recv[roff[peer] + done_r[peer]: roff[peer] + done_r[peer] + nr],
+                                          peer))
+            done_s[peer] += max(ns, 0)
+            done_r[peer] += max(nr, 0)
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+    return recv
+
+
+def all_gather_tensor(t: torch.Tensor, world: World | None = None) -> torch.Tensor:
+    """All-gather equally shaped tensors along dim 0 (R5: sampler gather, R3 broadcast of small data)."""
+    w = world or get_world()
+    if w.size == 1:
+        return t.clone()
+    dev_ok = (w.backend == "nccl") == t.is_cuda
+    src = t if dev_ok else (t.to(w.device) if w.backend == "nccl" else t.cpu())
+    out = torch.empty((w.size * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+    dist.all_gather_into_tensor(out, src.contiguous())
+    return out.to(t.device)
+
+
+def all_gather_varlen(t: torch.Tensor, world: World | None = None) -> torch.Tensor:
+    """All-gather tensors whose dim 0 differs per rank."""
+    w = world or get_world()
+    if w.size == 1:
+        return t.clone()
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    ns = all_gather_tensor(n, w).tolist()
+    m = max(ns)
+    pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[: t.shape[0]] = t
+    g = all_gather_tensor(pad, w)
+    parts = [g[i * m: i * m + ns[i]] for i in range(w.size)]
+    return torch.cat(parts, 0)
+
+
+def all_reduce_(t: torch.Tensor, op: str = "sum", world: World | None = None) -> torch.Tensor:
+    w = world or get_world()
+    if w.size == 1:
+        return t
+    rop = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op]
+    if (w.backend == "nccl") != t.is_cuda:
+        tmp = t.to(w.device) if w.backend == "nccl" else t.cpu()
+        dist.all_reduce(tmp, op=rop)
+        t.copy_(tmp)
+    else:
+        dist.all_reduce(t, op=rop)
+    return t
+
+
+def broadcast_(t: torch.Tensor, src: int = 0, world: World | None = None) -> torch.Tensor:
+    w = world or get_world()
+    if w.size == 1:
+        return t
+    if (w.backend == "nccl") != t.is_cuda:
+        tmp = t.to(w.device) if w.backend == "nccl" else t.cpu()
+        dist.broadcast(tmp, src=src)
+        t.copy_(tmp)
+    else:
+        dist.broadcast(t, src=src)
+    return t

@@ -1,0 +1,140 @@
+"""Numerics of the sort/partition/gather HIP kernels vs plain PyTorch/numpy references."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _u64(a):
+    return a.cpu().numpy().view(np.uint64)
+
+
+def _ref_order(e, lo_mask=0xFFFFFFFFFFFFFFFF):
+    """numpy stable lexsort on (hi, lo & mask): reference permutation."""
+    a = _u64(e)
+    lo = a[:, 0] & np.uint64(lo_mask)
+    hi = a[:, 1]
+    return np.lexsort((lo, hi), axis=0)
+
+
+@pytest.mark.parametrize("n", [1, 7, 2048, 2049, 100_003, 1_000_000])
+def test_sort_entries_full_128(n):
+    from dryad_amd.ops import sort as S
+    g = torch.Generator(device="cuda").manual_seed(n)
+    e = torch.randint(-2**63, 2**63 - 1, (n, 2), dtype=torch.int64, device="cuda", generator=g)
+    ref = e.cpu().numpy()[_ref_order(e)]
+    out = S.sort_entries(e.clone(), 0, 128)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+def test_sort_entries_is_stable_on_key_bits():
+    from dryad_amd.ops import sort as S
+    n = 300_000
+    e = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    e[:, 1] = torch.randint(0, 50, (n,), device="cuda")           # few distinct hi keys
+    e[:, 0] = torch.arange(n, device="cuda")                        # row index = original order
+    out = S.sort_entries(e.clone(), 64, 128).cpu().numpy()
+    ref = e.cpu().numpy()[np.argsort(e[:, 1].cpu().numpy(), kind="stable")]
+    np.testing.assert_array_equal(out, ref)
+
+
+def test_partition_pass_starts():
+    from dryad_amd.ops import sort as S
+    n = 123_457
+    e = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    e[:, 1] = torch.randint(0, 8, (n,), device="cuda")
+    e[:, 0] = torch.arange(n, device="cuda")
+    out, starts = S.partition_pass(e, 64)
+    h = np.bincount(e[:, 1].cpu().numpy(), minlength=256)
+    exp = np.concatenate([[0], np.cumsum(h)])
+    np.testing.assert_array_equal(starts.cpu().numpy(), exp)
+    ref = e.cpu().numpy()[np.argsort(e[:, 1].cpu().numpy(), kind="stable")]
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("stride,off,klen", [(100, 0, 10), (16, 4, 8), (13, 1, 12), (24, 8, 3)])
+def test_extract_keys(stride, off, klen):
+    from dryad_amd.ops import sort as S
+    n = 5000
+    rows = torch.randint(0, 256, (n, stride), dtype=torch.uint8, device="cuda")
+    e = S.extract_keys(rows, off, klen, 0).cpu().numpy().view(np.uint64)
+    r = rows.cpu().numpy()
+    for i in [0, 1, 17, n - 1]:
+        key = bytes(r[i, off:off + klen]) + bytes(12 - klen)
+        hi = int.from_bytes(key[:8], "big")
+        lo = (int.from_bytes(key[8:12], "big") << 32) | i
+        assert int(e[i, 1]) == hi and int(e[i, 0]) == lo
+
+
+def test_gather_rows_entries_and_index():
+    from dryad_amd.ops import sort as S
+    n, stride = 10_000, 100
+    rows = torch.randint(0, 256, (n, stride), dtype=torch.uint8, device="cuda")
+    perm = torch.randperm(n, device="cuda")
+    ent = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    ent[:, 0] = perm
+    out = S.gather_rows(rows, entries=ent)
+    assert torch.equal(out, rows[perm])
+    rows2 = torch.randint(0, 256, (n, 36), dtype=torch.uint8, device="cuda")
+    out2 = S.gather_rows(rows2, index=perm.to(torch.int64))
+    assert torch.equal(out2, rows2[perm])
+
+
+def test_range_dest_matches_searchsorted():
+    from dryad_amd.ops import sort as S
+    n = 50_000
+    e = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    e[:, 1] = torch.randint(0, 1000, (n,), device="cuda")
+    e[:, 0] = torch.arange(n, device="cuda")
+    seps = torch.zeros((7, 2), dtype=torch.int64, device="cuda")
+    sv = torch.tensor([100, 200, 200, 450, 600, 800, 999], device="cuda")
+    seps[:, 1] = sv
+    out = S.range_dest(e.clone(), seps, 0)
+    ref = torch.searchsorted(sv, e[:, 1], right=False)   # count of seps strictly below key
+    assert torch.equal(out[:, 1], ref)
+    assert torch.equal(out[:, 0], e[:, 0])
+
+
+def test_terasort_generate_and_check():
+    from dryad_amd.ops import terasort as TS
+    n = 100_000
+    a = torch.empty((n, 100), dtype=torch.uint8, device="cuda")
+    b = torch.empty((2 * n, 100), dtype=torch.uint8, device="cuda")
+    TS.generate(a, n, 42)
+    TS.generate(b, 0, 42)
+    assert torch.equal(a, b[n:])                      # counter-based: slices agree
+    r = a[5].cpu().numpy().tobytes()
+    assert r[10:12] == b"\x00\x11" and r[96:] == bytes([0xCC, 0xDD, 0xEE, 0xFF])
+    assert r[12:44].decode() == format(n + 5, "032X")
+    acc = TS.check(a)
+    perm = torch.randperm(n, device="cuda")
+    acc2 = TS.check(a[perm].contiguous())
+    assert acc[0].item() == acc2[0].item()            # order-independent checksum
+
+
+def test_local_sort_rows_matches_python_sorted():
+    from dryad_amd.ops import recordsort as RS, terasort as TS
+    n = 200_000
+    bufs = RS.SortBuffers.allocate(n, 100, "cuda")
+    TS.generate(bufs.rows_in[:n], 0, 7)
+    src = bufs.rows_in[:n].cpu().numpy()
+    out = RS.distributed_sort_rows(bufs, n, 0, 10).cpu().numpy()
+    keys = [bytes(r[:10]) + i.to_bytes(4, "big") for i, r in enumerate(src)]
+    order = sorted(range(n), key=lambda i: keys[i])
+    np.testing.assert_array_equal(out, src[order])
+    acc = TS.check(torch.from_numpy(out).cuda())
+    assert acc[1].item() == 0
+
+
+def test_local_sort_descending():
+    from dryad_amd.ops import recordsort as RS
+    n = 20_000
+    rows = torch.randint(0, 256, (n, 12), dtype=torch.uint8, device="cuda")
+    out = torch.empty_like(rows)
+    ea = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    eb = torch.empty_like(ea)
+    got = RS.local_sort_rows(rows, out, ea, eb, 2, 9, descending=True).cpu().numpy()
+    src = rows.cpu().numpy()
+    order = sorted(range(n), key=lambda i: (bytes(255 - x for x in src[i, 2:11]), i))
+    np.testing.assert_array_equal(got, src[order])
