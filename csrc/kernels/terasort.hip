@@ -16,46 +16,59 @@
 
 namespace {
 
-__device__ __forceinline__ uint32_t ts_byte(uint64_t g, uint32_t p, uint64_t kA, uint64_t kB, uint64_t fil) {
-  if (p < 8) return (uint32_t)(kA >> (56 - 8 * p)) & 0xFF;
-  if (p < 10) return (uint32_t)(kB >> (56 - 8 * (p - 8))) & 0xFF;
-  if (p == 10) return 0x00;
-  if (p == 11) return 0x11;
-  if (p < 44) {
-    const uint32_t q = p - 12;
-    if (q < 16) return '0';
+__device__ __forceinline__ uint32_t hex_word(uint64_t g, uint32_t k) {
+  // bytes 4k..4k+3 of the 32-hex-digit record number field starting at byte 12 (k in 7..10)
+  uint32_t w = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const uint32_t q = 4 * k + b - 12;                    // digit index 16..31
     const uint32_t nib = (uint32_t)(g >> (4 * (31 - q))) & 0xF;
-    return nib < 10 ? '0' + nib : 'A' + nib - 10;
+    w |= (nib < 10 ? '0' + nib : 'A' + nib - 10) << (8 * b);
   }
-  if (p < 48) return 0x88 + 0x11 * (p - 44);
-  if (p < 96) return 'A' + (uint32_t)((fil >> (5 * ((p - 48) >> 2))) % 26);
-  return 0xCC + 0x11 * (p - 96);
+  return w;
 }
 
-__device__ __forceinline__ uint32_t ts_word(uint64_t seed, uint64_t g, uint32_t k) {
-  uint64_t kA = 0, kB = 0, fil = 0;
-  if (k < 3) {
-    kA = mix64(seed ^ mix64(g));
-    kB = mix64(kA ^ 0xD1B54A32D192ED03ull);
-  } else if (k >= 12 && k < 24) {
-    fil = mix64(g ^ (seed * 0x2545F4914F6CDD1Dull) ^ 0xF00DF00DF00DF00Dull);
-  }
-  const uint32_t p = 4 * k;
-  return ts_byte(g, p, kA, kB, fil) | (ts_byte(g, p + 1, kA, kB, fil) << 8) |
-         (ts_byte(g, p + 2, kA, kB, fil) << 16) | (ts_byte(g, p + 3, kA, kB, fil) << 24);
+// The 25 little-endian dwords of record g, computed directly (one hash triple per record).
+__device__ __forceinline__ void ts_record(uint64_t seed, uint64_t g, uint32_t* w) {
+  const uint64_t kA = mix64(seed ^ mix64(g));
+  const uint64_t kB = mix64(kA ^ 0xD1B54A32D192ED03ull);
+  const uint64_t fil = mix64(g ^ (seed * 0x2545F4914F6CDD1Dull) ^ 0xF00DF00DF00DF00Dull);
+  w[0] = bswap32((uint32_t)(kA >> 32));
+  w[1] = bswap32((uint32_t)kA);
+  w[2] = (uint32_t)(kB >> 56) | (((uint32_t)(kB >> 48) & 0xFF) << 8) | (0x11u << 24);
+  w[3] = w[4] = w[5] = w[6] = 0x30303030u;
+#pragma unroll
+  for (uint32_t k = 7; k < 11; ++k) w[k] = hex_word(g, k);
+  w[11] = 0xBBAA9988u;
+#pragma unroll
+  for (uint32_t i = 0; i < 12; ++i) w[12 + i] = ('A' + (uint32_t)((fil >> (5 * i)) % 26)) * 0x01010101u;
+  w[24] = 0xFFEEDDCCu;
 }
 
-// One workgroup writes 256 consecutive records = 6400 dwords, fully coalesced.
+// One workgroup generates 256 consecutive records: each thread builds one record in LDS, then
+// the block streams the 25.6 KB image out with coalesced 16-byte stores.
 __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out, uint64_t n, uint64_t first,
                                                      uint64_t seed) {
+  __shared__ __attribute__((aligned(16))) uint32_t img[256 * 25];
   for (uint64_t row0 = (uint64_t)blockIdx.x * 256; row0 < n; row0 += (uint64_t)gridDim.x * 256) {
     const uint32_t rows = (uint32_t)((n - row0) < 256 ? (n - row0) : 256);
-    const uint32_t words = rows * 25;
-    uint32_t* o = out + row0 * 25;
-    for (uint32_t j = threadIdx.x; j < words; j += 256) {
-      const uint32_t r = j / 25, k = j - r * 25;
-      o[j] = ts_word(seed, first + row0 + r, k);
+    if (threadIdx.x < rows) {
+      uint32_t w[25];
+      ts_record(seed, first + row0 + threadIdx.x, w);
+#pragma unroll
+      for (int k = 0; k < 25; ++k) img[threadIdx.x * 25 + k] = w[k];
     }
+    __syncthreads();
+    uint32_t* o = out + row0 * 25;
+    const uint32_t words = rows * 25;
+    if (rows == 256) {
+      const uint4* src = reinterpret_cast<const uint4*>(img);
+      uint4* dst = reinterpret_cast<uint4*>(o);
+      for (uint32_t j = threadIdx.x; j < 256 * 25 / 4; j += 256) dst[j] = src[j];
+    } else {
+      for (uint32_t j = threadIdx.x; j < words; j += 256) o[j] = img[j];
+    }
+    __syncthreads();
   }
 }
 

@@ -106,7 +106,7 @@ def build_runtime(verbose: bool = False, force: bool = False) -> Path:
         objs.append(o)
     target = runtime_lib_path()
     if force or _stale(target, objs):
-        _run([cxx, "-shared", *extra, *objs, "-o", target, "-lpthread", "-lz"], verbose)
+        _run([cxx, "-shared", *extra, *objs, "-o", target, "-lpthread"], verbose)
     return target
 
 

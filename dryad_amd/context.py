@@ -1,0 +1,325 @@
+"""``DryadLinqContext``: job configuration and the factory for query inputs.
+
+Reference: LinqToDryad/DryadLinqContext.cs:566-1310.  Constructors map to the MI355X node:
+
+  * ``DryadLinqContext(num_processes)``        LOCAL platform: the job manager plus
+    ``num_processes`` CPU worker processes on this host (LocalJobSubmission analog, used for the
+    WordCount plumbing config and CI without a GPU)
+  * ``DryadLinqContext(platform="gpu")``       GPU platform: SPMD over the ranks of the current
+    ``torchrun`` world, one MI355X per rank, RCCL over xGMI for shuffles
+  * ``DryadLinqContext(cluster=LocalGpuNode(n))`` explicit cluster descriptor
+
+Configuration properties keep the reference names (``JobFriendlyName``, ``EnableSpeculativeDuplication``,
+``LocalDebug``, ...) and are frozen once the context has run a job (test ContextConfigIsReadOnly).
+"""
+from __future__ import annotations
+
+import enum
+import itertools
+import os
+import threading
+
+from . import types as T
+from .errors import DryadLinqException, ErrorCode
+from .jobinfo import DryadLinqJobInfo, JobHandle, JobStatus
+from .query import Query, QNode
+
+
+class PlatformKind(enum.Enum):
+    LOCAL = "LOCAL"          # CPU worker processes on this host
+    GPU = "GPU"              # MI355X ranks of a torchrun world
+    LOCAL_DEBUG = "LOCAL_DEBUG"
+
+
+class ExecutorKind(enum.Enum):
+    DRYAD = "DRYAD"
+    LOCAL_DEBUG = "LOCAL_DEBUG"
+
+
+class CompressionScheme(enum.Enum):
+    NONE = 0
+    GZIP = 1
+    None_ = 0
+
+
+class QueryLoggingLevel(enum.IntEnum):
+    """Reference QueryTraceLevel.cs:30-37 / Constants.cs:72-112 (bit masks)."""
+    Off = 0
+    Critical = 1
+    Error = 3
+    Warning = 7
+    Information = 15
+    Verbose = 31
+
+
+class DryadLinqCluster:
+    """Cluster descriptor interface (reference DryadLinqContext.cs:76-106)."""
+    platform = PlatformKind.LOCAL
+
+    def make_context_defaults(self) -> dict:
+        return {}
+
+
+class LocalCpuCluster(DryadLinqCluster):
+    platform = PlatformKind.LOCAL
+
+    def __init__(self, num_processes: int = 2):
+        self.num_processes = int(num_processes)
+
+
+class LocalGpuNode(DryadLinqCluster):
+    """One MI355X node: ``n_gpus`` ranks (defaults to the torchrun WORLD_SIZE)."""
+    platform = PlatformKind.GPU
+
+    def __init__(self, n_gpus: int | None = None):
+        self.n_gpus = n_gpus
+
+
+_ctx_ids = itertools.count(1)
+
+_DEFAULTS = dict(
+    IntermediateDataCompressionScheme=CompressionScheme.NONE,
+    OutputDataCompressionScheme=CompressionScheme.NONE,
+    CompileForVertexDebugging=False,
+    JobFriendlyName="DryadLINQ job",
+    JobMinNodes=None,
+    JobMaxNodes=None,
+    ThreadsPerWorker=None,
+    JobRuntimeLimit=None,
+    EnableSpeculativeDuplication=True,
+    LocalDebug=False,
+    DebugBreak=False,
+    RuntimeLoggingLevel=QueryLoggingLevel.Error,
+    SelectOrderPreserving=False,
+    ForceGC=False,
+    PartitionCount=None,               # default partition count for shuffles (StaticConfig 8)
+    MaxVertexFailures=6,               # DrGraphParameters: m_maxActiveFailureCount
+    DynamicOptLevel=0x1,               # broadcast only (DryadLinqGlobals.cs:43-52)
+    HeadNode="localhost",
+    DryadHomeDirectory=None,
+    PartitionUncPath=None,
+    Queue=None,
+    NodeGroup=None,
+    ContainerMbMemory=None,
+    ApplicationMasterMbMemory=None,
+    GraphManagerNode=None,
+)
+
+_READONLY_AFTER_USE = set(_DEFAULTS) - {"LocalDebug"}
+
+
+class DryadLinqContext:
+    def __init__(self, num_processes: int | None = None, storage_set_scheme: str | None = None, *,
+                 platform: str | PlatformKind | None = None, cluster: DryadLinqCluster | None = None,
+                 temp_dir: str | None = None):
+        object.__setattr__(self, "_props", dict(_DEFAULTS))
+        object.__setattr__(self, "_frozen", False)
+        object.__setattr__(self, "_id", next(_ctx_ids))
+        self._props["JobEnvironmentVariables"] = {}
+        self._props["ResourcesToAdd"] = []
+        self._props["ResourcesToRemove"] = []
+        if isinstance(platform, str):
+            platform = PlatformKind(platform.upper())
+        if cluster is not None:
+            platform = cluster.platform
+            if isinstance(cluster, LocalCpuCluster):
+                num_processes = cluster.num_processes
+        if platform is None:
+            platform = PlatformKind.LOCAL
+        self._props["PlatformKind"] = platform
+        self._props["ExecutorKind"] = ExecutorKind.DRYAD
+        self._props["NumProcesses"] = int(num_processes) if num_processes else 2
+        self._props["StorageScheme"] = storage_set_scheme or ("hbm" if platform == PlatformKind.GPU else "partfile")
+        self._props["TempDir"] = temp_dir
+        object.__setattr__(self, "_cluster", cluster)
+        object.__setattr__(self, "_lock", threading.RLock())
+        object.__setattr__(self, "_executor", None)
+        object.__setattr__(self, "_jobs", {})
+        object.__setattr__(self, "_job_seq", itertools.count(1))
+
+    # ------------------------------------------------------------------ properties
+    def __getattr__(self, name):
+        props = object.__getattribute__(self, "_props")
+        if name in props:
+            return props[name]
+        raise AttributeError(name)
+
+    def __setattr__(self, name, value):
+        if name in self._props or name in _DEFAULTS:
+            if self._frozen and name in _READONLY_AFTER_USE:
+                raise DryadLinqException(0, f"DryadLinqContext.{name} cannot be changed after the context was used")
+            self._props[name] = value
+        else:
+            object.__setattr__(self, name, value)
+
+    @property
+    def num_partitions(self) -> int:
+        if self.PartitionCount:
+            return int(self.PartitionCount)
+        if self.PlatformKind == PlatformKind.GPU:
+            from .parallel.comm import get_world
+            return max(1, get_world().size)
+        return max(1, int(self.NumProcesses))
+
+    def _compatible(self, other) -> bool:
+        return isinstance(other, DryadLinqContext) and other._props["PlatformKind"] == self._props["PlatformKind"]
+
+    def __eq__(self, other):
+        return self is other
+
+    def __hash__(self):
+        return self._id
+
+    def Dispose(self):
+        if self._executor is not None:
+            self._executor.close()
+            object.__setattr__(self, "_executor", None)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.Dispose()
+
+    def ClientVersion(self):
+        from . import __version__
+        return __version__
+
+    # ------------------------------------------------------------------ inputs
+    def FromEnumerable(self, data, dtype=None) -> Query:
+        data = list(data)
+        if dtype is None:
+            dtype = T.infer_common_type(data[:1000]) if data else T.Int32
+        return Query(self, QNode("FromEnumerable", (), dict(data=data), dtype))
+
+    def FromStore(self, uri: str, dtype=None, deserializer=None) -> Query:
+        from .io.providers import provider_for
+        p = provider_for(str(uri))
+        if not p.exists(str(uri)):
+            raise DryadLinqException(ErrorCode.FailedToGetStreamProps, f"dataset {uri} does not exist")
+        if dtype is None:
+            dtype = T.LineRecordT if str(uri).startswith("partfile") and deserializer is None else None
+            if str(uri).startswith("gen://range"):
+                dtype = T.Int32
+            if str(uri).startswith("gen://terasort"):
+                dtype = T.Pickle
+        else:
+            dtype = T.from_annotation(dtype)
+        return Query(self, QNode("FromStore", (), dict(uri=str(uri), deserializer=deserializer), dtype))
+
+    def MakeTemporaryStreamUri(self) -> str:
+        from .io.providers import provider_for, unique_name
+        scheme = self.StorageScheme
+        return provider_for(scheme + "://x").temp_uri(unique_name("DryadLinqTemp"))
+
+    # ------------------------------------------------------------------ execution
+    def _freeze(self):
+        object.__setattr__(self, "_frozen", True)
+
+    def _get_executor(self):
+        if self._executor is None:
+            with self._lock:
+                if self._executor is None:
+                    from .runtime.executor import make_executor
+                    object.__setattr__(self, "_executor", make_executor(self))
+        return self._executor
+
+    def _local_debug(self) -> bool:
+        return bool(self.LocalDebug) or self.PlatformKind == PlatformKind.LOCAL_DEBUG
+
+    def _write_local_store(self, node: QNode, data):
+        from .io.providers import provider_for
+        uri = node.args["uri"]
+        p = provider_for(uri)
+        if p.exists(uri) and not node.args.get("delete_if_exists") and not node.args.get("_temp"):
+            raise DryadLinqException(0, f"can't output to existing table {uri}")
+        dtype = node.dtype or (T.infer_common_type(data[:1000]) if data else T.Int32)
+        node.dtype = dtype
+        p.write_table(uri, [data], dtype)
+
+    def _enumerate(self, q: Query) -> list:
+        self._freeze()
+        if self._local_debug():
+            from .localdebug import LocalEvaluator
+            return LocalEvaluator(self).eval(q.node)
+        return self._get_executor().enumerate(q)
+
+    def _execute_scalar(self, q: Query):
+        self._freeze()
+        if self._local_debug():
+            from .localdebug import LocalEvaluator
+            return LocalEvaluator(self).eval(q.node)[0]
+        res = self._get_executor().enumerate(q)
+        if len(res) != 1:
+            raise DryadLinqException(0, f"scalar query produced {len(res)} records")
+        return res[0]
+
+    def _new_handle(self) -> JobHandle:
+        return JobHandle(f"{self._id}.{next(self._job_seq)}")
+
+    def Submit(self, *queries) -> DryadLinqJobInfo:
+        """Submit one or several ``ToStore`` queries as ONE job (reference Submit(params IQueryable[]))."""
+        qs = []
+        for q in queries:
+            qs.extend(q if isinstance(q, (list, tuple)) else [q])
+        self._freeze()
+        outs = []
+        for q in qs:
+            if q.node.op != "ToStore":
+                q = q.ToStore(self.MakeTemporaryStreamUri())
+                q.node.args["_temp"] = True
+            outs.append(q)
+        # repeat submission of an executed query returns the existing job
+        key = tuple(sorted(q.node.id for q in outs))
+        prev = self._jobs.get(key)
+        if prev is not None:
+            return prev
+        h = self._new_handle()
+        info = DryadLinqJobInfo([h])
+        self._jobs[key] = info
+        if self._local_debug():
+            from .localdebug import LocalEvaluator
+            try:
+                ev = LocalEvaluator(self)
+                for q in outs:
+                    ev.eval(q.node)
+                h.finish(True)
+            except BaseException as e:  # noqa: BLE001
+                h.finish(False, e)
+            return info
+        self._get_executor().submit(outs, h)
+        return info
+
+    def SubmitAndWait(self, *queries) -> DryadLinqJobInfo:
+        info = self.Submit(*queries)
+        info.Wait()
+        return info
+
+    def _do_while(self, source: Query, body, cond) -> Query:
+        before = source
+        while True:
+            after = body(before)
+            if not self._local_debug():
+                tmp = self.MakeTemporaryStreamUri()
+                st = after.ToStore(tmp)
+                st.node.args["_temp"] = True
+                self.SubmitAndWait(st)
+                after = Query(self, QNode("Table", (), dict(uri=tmp), st.node.dtype))
+            else:
+                after = self.FromEnumerable(list(after), dtype=after.dtype)
+            more = cond(before, after)
+            val = more.Single() if isinstance(more, Query) else bool(more)
+            if not val:
+                return after
+            before = after
+
+    def Explain(self, q: Query) -> str:
+        from .compiler.planner import compile_queries
+        plan = compile_queries(self, [q])
+        return plan.explain()
+
+    # python-style aliases
+    from_enumerable = FromEnumerable
+    from_store = FromStore
+    submit = Submit
+    submit_and_wait = SubmitAndWait

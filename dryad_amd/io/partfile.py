@@ -1,0 +1,145 @@
+"""The ``partfile`` partitioned-table format (byte-compatible with the reference).
+
+Metadata file (reference GraphManager/filesystem/DrPartitionFile.cpp:59-308, client side
+LinqToDryad/DataProvider.cs:378-538):
+
+    <partBasePath>
+    <N>
+    <i>,<size>[,<machine>[:<overridePath>]]      (N lines)
+
+Partition ``i`` lives at ``<partBasePath>.%08X`` (upper-case hex of the line position).  Writers
+produce ``<partBasePath>.%08X---<vertexId>_<port>_<version>.tmp`` and the job manager commits the
+chosen version of each partition by rename once the whole job succeeded; other versions are deleted
+(DrPartitionFile.cpp:436-600).  Parts are record streams in the DryadLinqBinary format.
+"""
+from __future__ import annotations
+
+import os
+import uuid
+from dataclasses import dataclass, field
+
+
+@dataclass
+class PartEntry:
+    index: int
+    size: int
+    machine: str | None = None
+    override: str | None = None
+
+
+@dataclass
+class PartFileMeta:
+    base: str
+    parts: list = field(default_factory=list)
+
+    @property
+    def count(self) -> int:
+        return len(self.parts)
+
+    @property
+    def total_size(self) -> int:
+        return sum(p.size for p in self.parts)
+
+    def part_path(self, pos: int) -> str:
+        e = self.parts[pos]
+        if e.override:
+            return e.override
+        return f"{self.base}.{pos:08X}"
+
+    def paths(self) -> list:
+        return [self.part_path(i) for i in range(self.count)]
+
+
+def read_meta(meta_path: str) -> PartFileMeta:
+    with open(meta_path, "r", encoding="utf-8") as f:
+        lines = [ln.rstrip("\r\n") for ln in f]
+    lines = [ln for ln in lines if ln.strip() != ""] if len(lines) > 2 else lines
+    if len(lines) < 2:
+        raise ValueError(f"the partition file {meta_path} is malformed")
+    base = lines[0].strip()
+    n = int(lines[1].strip())
+    parts = []
+    for ln in lines[2:2 + n]:
+        fields = ln.split(",")
+        idx, size = int(fields[0]), int(fields[1])
+        machine = override = None
+        if len(fields) > 2 and fields[2]:
+            if ":" in fields[2]:
+                machine, override = fields[2].split(":", 1)
+            else:
+                machine = fields[2]
+        parts.append(PartEntry(idx, size, machine, override))
+    if len(parts) != n:
+        raise ValueError(f"the partition file {meta_path} is malformed: expected {n} parts, found {len(parts)}")
+    if not os.path.isabs(base):
+        base = os.path.join(os.path.dirname(os.path.abspath(meta_path)), base)
+    return PartFileMeta(base, parts)
+
+
+def write_meta(meta_path: str, meta: PartFileMeta):
+    tmp = meta_path + ".tmp-" + uuid.uuid4().hex[:8]
+    with open(tmp, "w", encoding="utf-8", newline="\n") as f:
+        f.write(meta.base + "\n")
+        f.write(f"{meta.count}\n")
+        for i, p in enumerate(meta.parts):
+            extra = ""
+            if p.machine:
+                extra = "," + p.machine + (":" + p.override if p.override else "")
+            f.write(f"{i},{p.size}{extra}\n")
+    os.replace(tmp, meta_path)
+
+
+def default_base(meta_path: str) -> str:
+    d = os.path.dirname(os.path.abspath(meta_path))
+    name = os.path.basename(meta_path)
+    return os.path.join(d, name + ".parts", "Part")
+
+
+def tmp_part_path(base: str, pos: int, vertex_id: int, port: int, version: int) -> str:
+    return f"{base}.{pos:08X}---{vertex_id}_{port}_{version}.tmp"
+
+
+def commit_parts(meta_path: str, base: str, chosen: list[str], machine: str | None = None) -> PartFileMeta:
+    """Rename the chosen temporary part files to their final names and write the metadata."""
+    os.makedirs(os.path.dirname(base), exist_ok=True)
+    parts = []
+    for pos, src in enumerate(chosen):
+        dst = f"{base}.{pos:08X}"
+        if src != dst:
+            os.replace(src, dst)
+        parts.append(PartEntry(pos, os.path.getsize(dst), machine))
+    meta = PartFileMeta(base, parts)
+    write_meta(meta_path, meta)
+    return meta
+
+
+def cleanup_tmp(base: str):
+    """Delete every uncommitted ``.tmp`` version of ``base`` (failed / duplicate vertices)."""
+    d = os.path.dirname(base)
+    if not os.path.isdir(d):
+        return
+    prefix = os.path.basename(base) + "."
+    for fn in os.listdir(d):
+        if fn.startswith(prefix) and fn.endswith(".tmp") and "---" in fn:
+            try:
+                os.remove(os.path.join(d, fn))
+            except OSError:
+                pass
+
+
+def exists(meta_path: str) -> bool:
+    return os.path.exists(meta_path)
+
+
+def delete(meta_path: str):
+    """Delete the table: every partition then the metadata (CheckExistence(deleteIfExists))."""
+    if not os.path.exists(meta_path):
+        return
+    try:
+        meta = read_meta(meta_path)
+        for p in meta.paths():
+            if os.path.exists(p):
+                os.remove(p)
+    except Exception:
+        pass
+    os.remove(meta_path)

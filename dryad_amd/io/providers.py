@@ -1,0 +1,282 @@
+"""Storage schemes (DataProvider registry).
+
+Reference: LinqToDryad/DataProvider.cs:62-682 (per-scheme GetStreamInfo / Ingress / Egress /
+CheckExistence / GetTemporaryStreamUri), DataPath.cs:39-58 (schemes partfile, hdfs, wasb,
+azureblob).  Schemes here:
+
+  * ``partfile:///abs/meta``  host partitioned files (byte-compatible, see io/partfile.py)
+  * ``hbm://name``            device-resident tables kept in HBM by the GPU executor of this process
+                              (one entry per local partition); the MI355X replacement for temp
+                              partfiles between jobs
+  * ``mem://name``            host-memory tables of this process (object executor / tests)
+  * ``gen://kind?args``       synthetic generator stores (terasort, range, uniform), partition i is
+                              a pure function of (args, i): idempotent under vertex re-execution
+
+hdfs/wasb/azureblob are not available on a single MI355X node without network; asking for them
+raises ``DryadLinqException(UnrecognizedDataSource)``.
+"""
+from __future__ import annotations
+
+import os
+import threading
+import urllib.parse
+import uuid
+
+from ..errors import DryadLinqException, ErrorCode
+from . import binary as B
+from . import partfile as PF
+
+
+def parse_uri(uri: str):
+    if "://" not in uri:
+        # plain path => partfile
+        return "partfile", os.path.abspath(uri), {}
+    scheme, rest = uri.split("://", 1)
+    scheme = scheme.lower()
+    query = {}
+    if "?" in rest:
+        rest, q = rest.split("?", 1)
+        query = {k: v[-1] for k, v in urllib.parse.parse_qs(q).items()}
+    if scheme in ("partfile", "file"):
+        path = rest
+        if path.startswith("/") and len(path) > 2 and path[2] == ":":   # partfile:///C:/x
+            path = path[1:]
+        return scheme, path, query
+    return scheme, rest, query
+
+
+class DataProvider:
+    scheme = ""
+
+    def stream_info(self, uri) -> tuple[int, int]:
+        raise NotImplementedError
+
+    def exists(self, uri) -> bool:
+        raise NotImplementedError
+
+    def check_existence(self, uri, delete_if_exists: bool):
+        if self.exists(uri):
+            if not delete_if_exists:
+                raise DryadLinqException(ErrorCode.OutputUriAlreadyExists if hasattr(ErrorCode, "OutputUriAlreadyExists")
+                                         else 0, f"can't output to existing table {uri}")
+            self.delete(uri)
+
+    def delete(self, uri):
+        raise NotImplementedError
+
+    def read_partition(self, uri, i: int, dtype):
+        raise NotImplementedError
+
+    def write_table(self, uri, partitions: list, dtype, delete_if_exists=True):
+        raise NotImplementedError
+
+    def temp_uri(self, name: str) -> str:
+        raise NotImplementedError
+
+    def read_all(self, uri, dtype):
+        n, _ = self.stream_info(uri)
+        for i in range(n):
+            yield from self.read_partition(uri, i, dtype)
+
+
+class PartfileProvider(DataProvider):
+    scheme = "partfile"
+
+    def _path(self, uri):
+        return parse_uri(uri)[1]
+
+    def stream_info(self, uri):
+        m = PF.read_meta(self._path(uri))
+        return m.count, m.total_size
+
+    def exists(self, uri):
+        return os.path.exists(self._path(uri))
+
+    def delete(self, uri):
+        PF.delete(self._path(uri))
+
+    def part_paths(self, uri):
+        return PF.read_meta(self._path(uri)).paths()
+
+    def read_partition(self, uri, i, dtype):
+        path = PF.read_meta(self._path(uri)).part_path(i)
+        with open(path, "rb") as f:
+            data = f.read()
+        return B.decode_records(dtype, data)
+
+    def read_partition_bytes(self, uri, i) -> bytes:
+        path = PF.read_meta(self._path(uri)).part_path(i)
+        with open(path, "rb") as f:
+            return f.read()
+
+    def write_table(self, uri, partitions, dtype, delete_if_exists=True):
+        """Ingress: one part file per partition (records in DryadLinqBinary)."""
+        meta_path = self._path(uri)
+        if delete_if_exists:
+            PF.delete(meta_path)
+        os.makedirs(os.path.dirname(os.path.abspath(meta_path)) or ".", exist_ok=True)
+        base = PF.default_base(meta_path)
+        os.makedirs(os.path.dirname(base), exist_ok=True)
+        tmps = []
+        for pos, recs in enumerate(partitions):
+            tmp = PF.tmp_part_path(base, pos, 0, pos, 0)
+            if isinstance(recs, (bytes, bytearray)):
+                with open(tmp, "wb") as f:
+                    f.write(recs)
+            else:
+                B.write_records(tmp, dtype, recs)
+            tmps.append(tmp)
+        return PF.commit_parts(meta_path, base, tmps)
+
+    def temp_uri(self, name):
+        root = os.environ.get("DRYAD_TEMP_DIR") or os.path.join(os.environ.get("TMPDIR", "/tmp"), "DryadLinqTemp")
+        os.makedirs(root, exist_ok=True)
+        return "partfile://" + os.path.join(root, name)
+
+
+class _MemoryTables:
+    def __init__(self):
+        self.tables = {}
+        self.lock = threading.Lock()
+
+
+_MEM = _MemoryTables()
+
+
+class MemProvider(DataProvider):
+    """Host-memory tables: ``{name: (dtype, [partition lists])}``."""
+    scheme = "mem"
+
+    def _name(self, uri):
+        return parse_uri(uri)[1]
+
+    def stream_info(self, uri):
+        t = _MEM.tables.get(self._name(uri))
+        if t is None:
+            raise DryadLinqException(0, f"no such table {uri}")
+        return len(t[1]), sum(len(p) for p in t[1])
+
+    def exists(self, uri):
+        return self._name(uri) in _MEM.tables
+
+    def delete(self, uri):
+        _MEM.tables.pop(self._name(uri), None)
+
+    def read_partition(self, uri, i, dtype):
+        return list(_MEM.tables[self._name(uri)][1][i])
+
+    def write_table(self, uri, partitions, dtype, delete_if_exists=True):
+        with _MEM.lock:
+            _MEM.tables[self._name(uri)] = (dtype, [list(p) for p in partitions])
+
+    def temp_uri(self, name):
+        return "mem://" + name
+
+
+class HbmProvider(DataProvider):
+    """Device-resident tables of this process: ``{name: (dtype, [local partition batches])}``.
+    On a GPU rank each entry holds the rank's partitions as columnar batches in HBM."""
+    scheme = "hbm"
+    tables: dict = {}
+
+    def _name(self, uri):
+        return parse_uri(uri)[1]
+
+    def stream_info(self, uri):
+        t = self.tables.get(self._name(uri))
+        if t is None:
+            raise DryadLinqException(0, f"no such HBM table {uri}")
+        return t["partitions"], t.get("bytes", 0)
+
+    def exists(self, uri):
+        return self._name(uri) in self.tables
+
+    def delete(self, uri):
+        self.tables.pop(self._name(uri), None)
+
+    def put(self, uri, entry: dict):
+        self.tables[self._name(uri)] = entry
+
+    def get(self, uri) -> dict:
+        t = self.tables.get(self._name(uri))
+        if t is None:
+            raise DryadLinqException(0, f"no such HBM table {uri}")
+        return t
+
+    def read_partition(self, uri, i, dtype):
+        t = self.get(uri)
+        b = t["local"].get(i)
+        if b is None:
+            raise DryadLinqException(0, f"partition {i} of {uri} is not resident on this rank")
+        return b.to_objects() if hasattr(b, "to_objects") else list(b)
+
+    def write_table(self, uri, partitions, dtype, delete_if_exists=True):
+        self.put(uri, {"dtype": dtype, "partitions": len(partitions), "local": dict(enumerate(partitions))})
+
+    def temp_uri(self, name):
+        return "hbm://" + name
+
+
+class GenProvider(DataProvider):
+    """Synthetic generator stores.  ``gen://range?count=N&partitions=P[&start=S]`` yields ints;
+    ``gen://terasort?records=N&partitions=P&seed=S`` yields 100-byte TeraSort records (as bytes on
+    the object path, generated directly in HBM by the GPU executor)."""
+    scheme = "gen"
+
+    def _args(self, uri):
+        _, kind, q = parse_uri(uri)
+        return kind.strip("/"), q
+
+    def stream_info(self, uri):
+        kind, q = self._args(uri)
+        p = int(q.get("partitions", 1))
+        if kind == "terasort":
+            return p, int(q.get("records", 0)) * 100
+        return p, int(q.get("count", 0)) * 4
+
+    def exists(self, uri):
+        return True
+
+    def delete(self, uri):
+        raise DryadLinqException(0, "generator stores are read-only")
+
+    def bounds(self, uri, i):
+        kind, q = self._args(uri)
+        p = int(q.get("partitions", 1))
+        n = int(q.get("records", q.get("count", 0)))
+        return (n * i) // p, (n * (i + 1)) // p
+
+    def read_partition(self, uri, i, dtype):
+        kind, q = self._args(uri)
+        lo, hi = self.bounds(uri, i)
+        if kind == "range":
+            start = int(q.get("start", 0))
+            return list(range(start + lo, start + hi))
+        if kind == "terasort":
+            from ..models.terasort_cpu import gen_records
+            return gen_records(lo, hi - lo, int(q.get("seed", 0)))
+        raise DryadLinqException(ErrorCode.UnrecognizedDataSource, f"unknown generator {kind}")
+
+    def temp_uri(self, name):
+        raise DryadLinqException(0, "generator stores are read-only")
+
+
+_PROVIDERS = {p.scheme: p for p in (PartfileProvider(), MemProvider(), HbmProvider(), GenProvider())}
+_PROVIDERS["file"] = _PROVIDERS["partfile"]
+
+
+def provider_for(uri: str) -> DataProvider:
+    scheme = parse_uri(uri)[0]
+    p = _PROVIDERS.get(scheme)
+    if p is None:
+        raise DryadLinqException(ErrorCode.UnrecognizedDataSource,
+                                 f"unsupported storage scheme '{scheme}' (available: {sorted(_PROVIDERS)})")
+    return p
+
+
+def register_provider(p: DataProvider):
+    _PROVIDERS[p.scheme] = p
+
+
+def unique_name(prefix="tmp") -> str:
+    return f"{prefix}-{uuid.uuid4().hex[:12]}"
