@@ -231,6 +231,7 @@ std::vector<std::pair<int, int>> JobGraph::on_completed(int v, int version, doub
     return cancel;
   }
   *accepted = true;
+  const bool was_running = f->second.state == VState::Running;
   f->second.state = VState::Completed;
   x.completed_version = version;
   x.bytes_read += bytes_read;
@@ -238,7 +239,7 @@ std::vector<std::pair<int, int>> JobGraph::on_completed(int v, int version, doub
   completed_++;
   Stage& s = stages_[x.stage];
   s.completed++;
-  if (f->second.start > 0) s.stats.elapsed.push_back(now - f->second.start);
+  if (was_running) s.stats.elapsed.push_back(now - f->second.start);
   reestimate(s);
   for (auto& kv : x.attempts) {
     if (kv.first != version && (kv.second.state == VState::Running || kv.second.state == VState::Ready)) {
@@ -250,7 +251,7 @@ std::vector<std::pair<int, int>> JobGraph::on_completed(int v, int version, doub
   std::ostringstream o;
   o << "{\"ev\":\"vertex\",\"t\":" << now << ",\"vertex\":" << v << ",\"stage\":\"" << jesc(s.name)
     << "\",\"partition\":" << x.partition << ",\"version\":" << version << ",\"state\":\"Completed\",\"elapsed\":"
-    << (f->second.start > 0 ? now - f->second.start : 0.0) << ",\"bytes_read\":" << bytes_read
+    << (was_running ? now - f->second.start : 0.0) << ",\"bytes_read\":" << bytes_read
     << ",\"bytes_written\":" << bytes_written << "}";
   event(o.str());
   mark_completed_downstream(v, now);
@@ -373,7 +374,7 @@ std::vector<ReadyItem> JobGraph::check_duplicates(double now) {
           has_dup |= kv.second.duplicate;
         }
       }
-      if (live == 1 && !has_dup && start > 0 && start + thr < now) {
+      if (live == 1 && !has_dup && start + thr < now) {
         enqueue(v, now, true);
         out.push_back(ready_.back());
       }

@@ -75,8 +75,9 @@ def decomposable(decomposer_cls):
 
     def deco(f):
         @functools.wraps(f)
-        def w(*a, **k):
-            return f(*a, **k)
+        def w(group, *a, **k):
+            from .compiler.decomposition import user_decomposable_call
+            return user_decomposable_call(f, decomposer_cls, group, a)
         return _mark(w, _dryad_decomposable=decomposer_cls)
     return deco
 

@@ -1,0 +1,118 @@
+"""Physical query plan: stages (vertex sets), their inputs/connections and vertex programs.
+
+Mirrors the reference XML query plan (LinqToDryad/DryadLinqQueryGen.cs:837-971,
+DryadLinqQueryNode.cs:728-827): every plan vertex has UniqueId, Type, Name, Explain, Partitions,
+ChannelType, ConnectionOperator, DynamicManager, Entry and Children.  Here a ``Stage`` is one
+vertex set; ``StageInput.kind`` is the connection operator:
+
+  * ``pointwise``  vertex p reads partition p of the source (same partition count)
+  * ``cross``      CrossProduct: vertex p reads output port p of *every* source vertex (shuffle)
+  * ``merge``      N -> 1: the single vertex reads port ``port`` of every source vertex in order
+  * ``broadcast``  every vertex reads port ``port`` of every source vertex (Tee + CrossProduct)
+  * ``offset``     vertex p reads source partition p - offset if it exists (Concat)
+
+A vertex program is a list of op dicts executed in sequence by the vertex runtime; the first op
+receives all stage inputs, later ops the previous op's single output stream.  The last op may emit
+several output ports (partitioners, Fork).
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+
+from .datasetinfo import DataSetInfo
+
+CHANNEL_TYPES = ("DiskFile", "HBM", "MemoryFIFO")
+
+
+@dataclass
+class StageInput:
+    src: int
+    kind: str = "pointwise"
+    port: int = 0
+    offset: int = 0
+    merge_sort: dict | None = None      # k-way merge of sorted source ports: {key, comparer, descending}
+
+    def to_json(self):
+        d = {"UniqueId": self.src, "ConnectionOperator": {"pointwise": "Pointwise", "cross": "CrossProduct",
+                                                         "merge": "Pointwise", "broadcast": "CrossProduct",
+                                                         "offset": "Pointwise"}[self.kind],
+             "Kind": self.kind, "Port": self.port}
+        if self.offset:
+            d["Offset"] = self.offset
+        if self.merge_sort:
+            d["MergeSort"] = True
+        return d
+
+
+@dataclass
+class Stage:
+    id: int
+    name: str
+    partitions: int
+    inputs: list = field(default_factory=list)
+    ops: list = field(default_factory=list)
+    out_ports: int = 1
+    dtype: object = None
+    info: DataSetInfo = field(default_factory=DataSetInfo)
+    output: dict | None = None          # {"uri", "delete_if_exists", "temp"} for ToStore stages
+    dynamic_manager: str | None = None
+    channel_type: str = "DiskFile"
+    explain: list = field(default_factory=list)
+    gang: bool = False                  # vertices must run together (collective exchange)
+    gpu: dict | None = None             # columnar/HIP lowering chosen by the GPU executor
+
+    @property
+    def is_output(self) -> bool:
+        return self.output is not None
+
+    def describe_ops(self) -> str:
+        return " -> ".join(op.get("explain", op["op"]) for op in self.ops)
+
+    def to_json(self):
+        return {
+            "UniqueId": self.id, "Type": self.ops[0]["op"] if self.ops else "Merge", "Name": self.name,
+            "Explain": self.explain + [self.describe_ops()], "Partitions": self.partitions,
+            "ChannelType": self.channel_type, "DynamicManager": self.dynamic_manager or "None",
+            "Entry": [op["op"] for op in self.ops], "OutputPorts": self.out_ports,
+            "Children": [i.to_json() for i in self.inputs],
+            "DataSetInfo": self.info.describe(),
+            **({"Output": {k: v for k, v in self.output.items() if k in ("uri", "delete_if_exists", "temp")}}
+               if self.output else {}),
+        }
+
+
+@dataclass
+class Plan:
+    stages: list
+    outputs: list            # stage ids that write tables (ToStore), in query order
+    globals: dict = field(default_factory=dict)
+
+    def stage(self, i) -> Stage:
+        return self.stages[i]
+
+    def consumers(self, sid: int) -> list:
+        return [s.id for s in self.stages if any(i.src == sid for i in s.inputs)]
+
+    def to_json(self) -> dict:
+        return {"Query": {**self.globals, "QueryPlan": [s.to_json() for s in self.stages],
+                          "Outputs": self.outputs}}
+
+    def dumps(self) -> str:
+        return json.dumps(self.to_json(), indent=1, default=str)
+
+    def explain(self) -> str:
+        """Human-readable per-stage explanation (reference DryadLinqQueryExplain.cs)."""
+        lines = []
+        for s in self.stages:
+            ins = ", ".join(f"{i.kind}({i.src}" + (f":{i.port}" if i.port else "") + ")" for i in s.inputs) or "-"
+            lines.append(f"Stage {s.id} [{s.name}] partitions={s.partitions} inputs={ins}"
+                         + (f" ports={s.out_ports}" if s.out_ports != 1 else "")
+                         + (f" dynamic={s.dynamic_manager}" if s.dynamic_manager else "")
+                         + (" gang" if s.gang else ""))
+            for e in s.explain:
+                lines.append(f"    {e}")
+            for op in s.ops:
+                lines.append(f"    {op.get('explain', op['op'])}")
+            lines.append(f"    => {s.info.describe()}" + (f" -> {s.output['uri']}" if s.output else ""))
+        return "\n".join(lines)

@@ -199,6 +199,9 @@ class DryadLinqContext:
             raise DryadLinqException(ErrorCode.FailedToGetStreamProps, f"dataset {uri} does not exist")
         if dtype is None:
             dtype = T.LineRecordT if str(uri).startswith("partfile") and deserializer is None else None
+            sch = p.schema(str(uri)) if hasattr(p, "schema") else None
+            if sch is not None and sch.get("dtype") is not None:
+                dtype = sch["dtype"]
             if str(uri).startswith("gen://range"):
                 dtype = T.Int32
             if str(uri).startswith("gen://terasort"):

@@ -91,7 +91,91 @@ def sort_key(key_selector, comparer=None, descending=False):
     return lambda x: K(key_selector(x))
 
 
-class Grouping(list):
+class LinqList(list):
+    """A list with LINQ-to-Objects methods (what C# code gets on IEnumerable<T>)."""
+
+    def Count(self, pred=None):
+        return Count(self, pred)
+
+    LongCount = Count
+
+    def Sum(self, sel=None):
+        return Sum(self, sel)
+
+    def Min(self, sel=None):
+        return Min(self, sel)
+
+    def Max(self, sel=None):
+        return Max(self, sel)
+
+    def Average(self, sel=None):
+        return Average(self, sel)
+
+    def Any(self, pred=None):
+        return Any(self, pred)
+
+    def All(self, pred):
+        return All(self, pred)
+
+    def Contains(self, v):
+        return Contains(self, v)
+
+    def First(self, pred=None):
+        return First(self, pred)
+
+    def FirstOrDefault(self, pred=None):
+        return FirstOrDefault(self, pred)
+
+    def Last(self, pred=None):
+        return Last(self, pred)
+
+    def LastOrDefault(self, pred=None):
+        return LastOrDefault(self, pred)
+
+    def Single(self, pred=None):
+        return Single(self, pred)
+
+    def Aggregate(self, *args):
+        if len(args) == 1:
+            return Aggregate(self, _NO, args[0])
+        return Aggregate(self, *args)
+
+    def Select(self, f):
+        return LinqList(Select(self, f, nparams_is2(f)))
+
+    def Where(self, f):
+        return LinqList(Where(self, f, nparams_is2(f)))
+
+    def SelectMany(self, f, r=None):
+        return LinqList(SelectMany(self, f, r))
+
+    def OrderBy(self, k, comparer=None):
+        return LinqList(OrderBy(self, k, comparer))
+
+    def OrderByDescending(self, k, comparer=None):
+        return LinqList(OrderBy(self, k, comparer, True))
+
+    def Distinct(self, comparer=None):
+        return LinqList(Distinct(self, comparer))
+
+    def Take(self, n):
+        return LinqList(self[:max(0, n)])
+
+    def Skip(self, n):
+        return LinqList(self[max(0, n):])
+
+    def ToList(self):
+        return list(self)
+
+    ToArray = ToList
+
+
+def nparams_is2(f):
+    from .query import nparams
+    return nparams(f) >= 2
+
+
+class Grouping(LinqList):
     """IGrouping<K, T>: a list of elements with a ``Key``."""
 
     def __init__(self, key, elements=()):

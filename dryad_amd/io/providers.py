@@ -27,6 +27,11 @@ from . import binary as B
 from . import partfile as PF
 
 
+def T_Pickle():
+    from ..types import Pickle
+    return Pickle
+
+
 def parse_uri(uri: str):
     if "://" not in uri:
         # plain path => partfile
@@ -93,15 +98,34 @@ class PartfileProvider(DataProvider):
         return os.path.exists(self._path(uri))
 
     def delete(self, uri):
-        PF.delete(self._path(uri))
+        path = self._path(uri)
+        PF.delete(path)
+        if os.path.exists(path + ".dryadtype"):
+            os.remove(path + ".dryadtype")
 
     def part_paths(self, uri):
         return PF.read_meta(self._path(uri)).paths()
+
+    def schema(self, uri):
+        from ..runtime.jobmanager import read_schema
+        return read_schema(self._path(uri))
 
     def read_partition(self, uri, i, dtype):
         path = PF.read_meta(self._path(uri)).part_path(i)
         with open(path, "rb") as f:
             data = f.read()
+        sch = self.schema(uri)
+        if sch is not None and sch.get("format") == "pickle":
+            import gzip
+            import pickle
+            if data[:2] == b"\x1f\x8b":
+                data = gzip.decompress(data)
+            return pickle.loads(data) if data else []
+        if dtype is None or dtype == T_Pickle():
+            dtype = sch["dtype"] if sch is not None else None
+        if dtype is None:
+            from ..types import LineRecordT
+            dtype = LineRecordT
         return B.decode_records(dtype, data)
 
     def read_partition_bytes(self, uri, i) -> bytes:
@@ -126,7 +150,11 @@ class PartfileProvider(DataProvider):
             else:
                 B.write_records(tmp, dtype, recs)
             tmps.append(tmp)
-        return PF.commit_parts(meta_path, base, tmps)
+        meta = PF.commit_parts(meta_path, base, tmps)
+        if dtype is not None:
+            from ..runtime.jobmanager import write_schema
+            write_schema(meta_path, dtype, "binary")
+        return meta
 
     def temp_uri(self, name):
         root = os.environ.get("DRYAD_TEMP_DIR") or os.path.join(os.environ.get("TMPDIR", "/tmp"), "DryadLinqTemp")

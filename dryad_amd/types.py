@@ -90,8 +90,15 @@ class DType:
 class _Prim(DType):
     def __init__(self, name, width, wfn, rfn, torch_dtype=None, default=0):
         self.name, self.fixed_width, self._w, self._r = name, width, wfn, rfn
-        self.torch_dtype = torch_dtype
+        self._torch_name = torch_dtype
         self._default = default
+
+    @property
+    def torch_dtype(self):
+        if self._torch_name is None:
+            return None
+        import torch
+        return getattr(torch, self._torch_name)
 
     def encode(self, w, v):
         getattr(w, self._w)(v)
@@ -104,11 +111,7 @@ class _Prim(DType):
 
 
 def _tdt(name):
-    try:
-        import torch
-        return getattr(torch, name)
-    except Exception:  # pragma: no cover
-        return None
+    return name   # resolved lazily (workers of the CPU executor never import torch)
 
 
 Byte = _Prim("Byte", 1, "write_byte", "read_byte", _tdt("uint8"))
