@@ -34,18 +34,20 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--records-per-gpu", type=int, default=1_250_000_000)
     ap.add_argument("--no-validate", action="store_true")
+    ap.add_argument("--direct", action="store_true",
+                    help="run the sort pipeline directly instead of through the DryadLINQ query API")
     args = ap.parse_args()
 
     import torch
     from dryad_amd.parallel.comm import init_world, shutdown
-    from dryad_amd.models.terasort import TeraSortConfig, TeraSortJob, run_steps
+    from dryad_amd.models.terasort import TeraSortConfig, TeraSortJob, TeraSortQueryJob, run_steps
 
     world = init_world(device="cuda")
     if world.size != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world.size}", file=sys.stderr)
     cfg = TeraSortConfig(records_per_rank=args.records_per_gpu)
     t_alloc = time.perf_counter()
-    job = TeraSortJob(cfg, world)
+    job = TeraSortJob(cfg, world) if args.direct else TeraSortQueryJob(cfg, world)
     if world.rank == 0:
         free, total = torch.cuda.mem_get_info(world.device)
         print(f"[bench] allocated working set in {time.perf_counter() - t_alloc:.1f}s; HBM free {free/1e9:.1f} "
@@ -53,6 +55,7 @@ def main():
     expect = None
     if not args.no_validate:
         expect = job.input_checksum()
+        torch.cuda.empty_cache()
     for i in range(args.warmup):
         t0 = time.perf_counter()
         job.step()
@@ -89,10 +92,14 @@ def main():
                 "bytes_per_gpu": job.bytes_per_rank,
                 "total_bytes": total_bytes,
                 "validated": None if val is None else val["ok"],
+                "path": "direct" if args.direct else "DryadLINQ query -> GPU executor (fused OrderBy gang stage)",
             },
         }
         if val is not None and not val["ok"]:
             line["validation"] = val
+        if not args.direct:
+            rep = job.executor_report()
+            print(f"[bench] executor: {json.dumps(rep, default=str)[:2000]}", file=sys.stderr, flush=True)
         print(json.dumps(line), flush=True)
     shutdown()
     if val is not None and not val["ok"]:

@@ -1,0 +1,349 @@
+// Relational kernels for the GPU vertex operator library (gfx950).
+//
+//   dr_build_keys       : up to 4 typed key columns -> order-preserving 128-bit sort entries
+//                         (normalised keys in the top bits, row index in the low 32 bits)
+//   dr_hash_dest        : hash of the key bits -> destination partition in entry.hi (HashPartition,
+//                         reference DryadLinqVertex.cs:4788-4907 port = hash % nPorts)
+//   dr_segment_flags    : 1 where the key differs from the previous sorted entry (GroupBy /
+//                         Distinct boundaries, ordered-GroupBy adjacent difference :586-760)
+//   dr_seg_reduce       : segmented sum/min/max/count over rows in sorted order, wave-level
+//                         segmented scan with 64-bit shuffles then one atomic per run tail
+//   dr_join_ranges      : for each sorted outer key, [lower, upper) among sorted inner keys
+//   dr_join_emit        : expand the ranges into (outer row, inner row) pairs (MergeJoin :898-1162)
+//   dr_scan_i64         : exclusive prefix sum of int64 (any length, reduce-then-scan)
+#include "common.h"
+
+namespace {
+
+enum KeyType : int {
+  K_U8 = 0, K_I8 = 1, K_BOOL = 2, K_I16 = 3, K_U16 = 4, K_I32 = 5, K_U32 = 6, K_I64 = 7, K_U64 = 8, K_F32 = 9,
+  K_F64 = 10
+};
+
+__device__ __forceinline__ int key_bits(int t) {
+  switch (t) {
+    case K_U8: case K_I8: case K_BOOL: return 8;
+    case K_I16: case K_U16: return 16;
+    case K_I32: case K_U32: case K_F32: return 32;
+    default: return 64;
+  }
+}
+
+// order-preserving unsigned image of one key value
+__device__ __forceinline__ uint64_t norm_key(const void* col, uint64_t i, int t) {
+  switch (t) {
+    case K_U8: case K_BOOL: return ((const uint8_t*)col)[i];
+    case K_I8: return (uint8_t)(((const int8_t*)col)[i]) ^ 0x80u;
+    case K_I16: return (uint16_t)(((const int16_t*)col)[i]) ^ 0x8000u;
+    case K_U16: return ((const uint16_t*)col)[i];
+    case K_I32: return (uint32_t)(((const int32_t*)col)[i]) ^ 0x80000000u;
+    case K_U32: return ((const uint32_t*)col)[i];
+    case K_I64: return (uint64_t)(((const int64_t*)col)[i]) ^ 0x8000000000000000ull;
+    case K_U64: return ((const uint64_t*)col)[i];
+    case K_F32: {
+      uint32_t u = ((const uint32_t*)col)[i];
+      return (u & 0x80000000u) ? (uint32_t)~u : (u | 0x80000000u);
+    }
+    case K_F64: {
+      uint64_t u = ((const uint64_t*)col)[i];
+      return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+    }
+  }
+  return 0;
+}
+
+struct KeyCols {
+  const void* col[4];
+  int type[4];
+  int desc[4];
+  int ncols;
+};
+
+__global__ __launch_bounds__(256) void build_keys_kernel(KeyCols kc, uint64_t n, uint32_t idx_base, int total_bits,
+                                                         E128* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    unsigned __int128 k = 0;
+    for (int c = 0; c < kc.ncols; ++c) {
+      const int b = key_bits(kc.type[c]);
+      uint64_t v = norm_key(kc.col[c], i, kc.type[c]);
+      if (kc.desc[c]) v = ~v & (b == 64 ? ~0ull : ((1ull << b) - 1));
+      k = (k << b) | v;
+    }
+    k <<= (128 - total_bits);
+    E128 e;
+    e.hi = (uint64_t)(k >> 64);
+    e.lo = (uint64_t)k | (uint32_t)(idx_base + (uint32_t)i);
+    out[i] = e;
+  }
+}
+
+__global__ __launch_bounds__(256) void hash_dest_kernel(E128* __restrict__ e, uint64_t n, uint64_t lo_mask,
+                                                        uint32_t nparts) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    E128 x = e[i];
+    const uint64_t h = mix64(x.hi ^ mix64(x.lo & lo_mask));
+    x.hi = (uint32_t)((h >> 32) % nparts);
+    e[i] = x;
+  }
+}
+
+__global__ __launch_bounds__(256) void segment_flags_kernel(const E128* __restrict__ e, uint64_t n, uint64_t lo_mask,
+                                                            int64_t* __restrict__ flags) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    int64_t f = 1;
+    if (i > 0) {
+      const E128 a = e[i - 1], b = e[i];
+      f = (a.hi != b.hi || (a.lo & lo_mask) != (b.lo & lo_mask)) ? 1 : 0;
+    }
+    flags[i] = f;
+  }
+}
+
+// ----- segmented reduction -------------------------------------------------------------------
+template <typename T>
+struct OpSum { __device__ static T f(T a, T b) { return a + b; } };
+template <typename T>
+struct OpMin { __device__ static T f(T a, T b) { return b < a ? b : a; } };
+template <typename T>
+struct OpMax { __device__ static T f(T a, T b) { return b > a ? b : a; } };
+
+__device__ __forceinline__ void atomic_combine(int64_t* p, int64_t v, int op) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+  if (op == 0 || op == 3) { atomicAdd(q, (unsigned long long)v); return; }
+  if (op == 1) { atomicMin(reinterpret_cast<long long*>(p), (long long)v); return; }
+  atomicMax(reinterpret_cast<long long*>(p), (long long)v);
+}
+
+__device__ __forceinline__ void atomic_combine(double* p, double v, int op) {
+  if (op == 0 || op == 3) { atomicAdd(p, v); return; }
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+  unsigned long long old = *q, assumed;
+  do {
+    assumed = old;
+    const double cur = __longlong_as_double((long long)assumed);
+    const double nv = (op == 1) ? (v < cur ? v : cur) : (v > cur ? v : cur);
+    if (nv == cur) break;
+    old = atomicCAS(q, assumed, (unsigned long long)__double_as_longlong(nv));
+  } while (assumed != old);
+}
+
+template <typename T, typename Op>
+__device__ __forceinline__ void seg_reduce_body(const T* __restrict__ vals, const E128* __restrict__ ent,
+                                                const int64_t* __restrict__ seg, uint64_t n, T* __restrict__ out,
+                                                int op, T ident) {
+  const int lane = lane_id();
+  const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const uint64_t w0 = (((uint64_t)blockIdx.x * blockDim.x) + threadIdx.x) >> 6;
+  for (uint64_t base = w0 * 64; base < n; base += waves * 64) {
+    const uint64_t i = base + lane;
+    const bool valid = i < n;
+    T v = ident;
+    int64_t s = -1;
+    if (valid) {
+      const uint32_t row = ent ? (uint32_t)ent[i].lo : (uint32_t)i;
+      v = (op == 3) ? (T)1 : vals[row];
+      s = seg[i];
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const T o = __shfl_up(v, d, 64);
+      const int64_t os = __shfl_up(s, d, 64);
+      if (lane >= d && os == s) v = Op::f(v, o);
+    }
+    const int64_t ns = __shfl_down(s, 1, 64);
+    const bool tail = valid && (lane == 63 || i + 1 >= n || ns != s);
+    if (tail) atomic_combine(&out[s], v, op);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void seg_reduce_kernel(const T* vals, const E128* ent, const int64_t* seg, uint64_t n,
+                                                         T* out, int op, T ident) {
+  if (op == 1) seg_reduce_body<T, OpMin<T>>(vals, ent, seg, n, out, op, ident);
+  else if (op == 2) seg_reduce_body<T, OpMax<T>>(vals, ent, seg, n, out, op, ident);
+  else seg_reduce_body<T, OpSum<T>>(vals, ent, seg, n, out, op, ident);
+}
+
+// ----- merge join ----------------------------------------------------------------------------
+__device__ __forceinline__ bool key_less(const E128& a, const E128& b, uint64_t m) {
+  return a.hi < b.hi || (a.hi == b.hi && (a.lo & m) < (b.lo & m));
+}
+
+__global__ __launch_bounds__(256) void join_ranges_kernel(const E128* __restrict__ outer, uint64_t no,
+                                                          const E128* __restrict__ inner, uint64_t ni, uint64_t m,
+                                                          int64_t* __restrict__ lower, int64_t* __restrict__ count) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < no; i += (uint64_t)gridDim.x * blockDim.x) {
+    const E128 k = outer[i];
+    uint64_t lo = 0, hi = ni;
+    while (lo < hi) {   // lower bound
+      const uint64_t mid = (lo + hi) >> 1;
+      if (key_less(inner[mid], k, m)) lo = mid + 1; else hi = mid;
+    }
+    uint64_t lb = lo;
+    hi = ni;
+    while (lo < hi) {   // upper bound
+      const uint64_t mid = (lo + hi) >> 1;
+      if (!key_less(k, inner[mid], m)) lo = mid + 1; else hi = mid;
+    }
+    lower[i] = (int64_t)lb;
+    count[i] = (int64_t)(lo - lb);
+  }
+}
+
+__global__ __launch_bounds__(256) void join_emit_kernel(const E128* __restrict__ outer, const E128* __restrict__ inner,
+                                                        uint64_t no, const int64_t* __restrict__ lower,
+                                                        const int64_t* __restrict__ count,
+                                                        const int64_t* __restrict__ offs,
+                                                        int64_t* __restrict__ out_outer, int64_t* __restrict__ out_inner) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < no; i += (uint64_t)gridDim.x * blockDim.x) {
+    const int64_t c = count[i], lb = lower[i], o = offs[i];
+    const int64_t orow = (int64_t)(uint32_t)outer[i].lo;
+    for (int64_t j = 0; j < c; ++j) {
+      out_outer[o + j] = orow;
+      out_inner[o + j] = (int64_t)(uint32_t)inner[lb + j].lo;
+    }
+  }
+}
+
+// ----- int64 exclusive scan ------------------------------------------------------------------
+constexpr int kChunk = 4096;   // 256 threads x 16
+
+__global__ __launch_bounds__(256) void scan_reduce_i64(const int64_t* __restrict__ a, uint64_t n,
+                                                       int64_t* __restrict__ part) {
+  __shared__ uint64_t sc[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kChunk + threadIdx.x * 16;
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) s += (base + k < n) ? a[base + k] : 0;
+  uint64_t w = wave_sum64((uint64_t)s);
+  if (lane_id() == 0) sc[wave_id()] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (int64_t)(sc[0] + sc[1] + sc[2] + sc[3]);
+}
+
+__global__ __launch_bounds__(256) void scan_down_i64(const int64_t* __restrict__ a, int64_t* __restrict__ out,
+                                                     uint64_t n, const int64_t* __restrict__ part_ex) {
+  __shared__ uint64_t sc[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kChunk + threadIdx.x * 16;
+  int64_t v[16];
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = (base + k < n) ? a[base + k] : 0;
+    s += v[k];
+  }
+  const uint64_t inc = wave_inclusive_scan64((uint64_t)s);
+  if (lane_id() == 63) sc[wave_id()] = inc;
+  __syncthreads();
+  const int w = wave_id();
+  uint64_t pre = 0;
+  for (int k = 0; k < w; ++k) pre += sc[k];
+  int64_t run = (int64_t)(pre + inc) - s + part_ex[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (base + k < n) out[base + k] = run;
+    run += v[k];
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// Returns the number of key bits (<= 96) or a negative hipError.
+DR_API int dr_build_keys(const void* const* cols, const int* types, const int* desc, int ncols, uint64_t n,
+                         uint32_t idx_base, E128* out, int* begin_bit, hipStream_t s) {
+  if (ncols < 1 || ncols > 4) return (int)hipErrorInvalidValue;
+  KeyCols kc{};
+  int bits = 0;
+  for (int c = 0; c < ncols; ++c) {
+    kc.col[c] = cols[c];
+    kc.type[c] = types[c];
+    kc.desc[c] = desc ? desc[c] : 0;
+    const int t = types[c];
+    bits += (t <= K_BOOL) ? 8 : (t <= K_U16) ? 16 : (t <= K_U32 || t == K_F32) ? 32 : 64;
+  }
+  kc.ncols = ncols;
+  if (bits > 96) return (int)hipErrorInvalidValue;
+  *begin_bit = (128 - bits) & ~7;
+  if (n == 0) return 0;
+  build_keys_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(kc, n, idx_base, bits, out);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+DR_API int dr_hash_dest(E128* e, uint64_t n, uint64_t lo_mask, uint32_t nparts, hipStream_t s) {
+  if (nparts == 0 || nparts > 256) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  hash_dest_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(e, n, lo_mask, nparts);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+DR_API int dr_segment_flags(const E128* e, uint64_t n, uint64_t lo_mask, int64_t* flags, hipStream_t s) {
+  if (n == 0) return 0;
+  segment_flags_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(e, n, lo_mask, flags);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// op: 0 sum, 1 min, 2 max, 3 count; dtype: 0 int64, 1 float64.  `out` must be pre-initialised
+// with the identity; `ent` (optional) maps sorted position -> row of `vals`.
+DR_API int dr_seg_reduce(const void* vals, const E128* ent, const int64_t* seg, uint64_t n, void* out, int op,
+                         int dtype, hipStream_t s) {
+  if (n == 0) return 0;
+  const unsigned g = grid_for(n, 256, 8192);
+  if (dtype == 0) {
+    const int64_t ident = op == 1 ? INT64_MAX : op == 2 ? INT64_MIN : 0;
+    seg_reduce_kernel<int64_t><<<g, 256, 0, s>>>((const int64_t*)vals, ent, seg, n, (int64_t*)out, op, ident);
+  } else {
+    const double ident = op == 1 ? __builtin_inf() : op == 2 ? -__builtin_inf() : 0.0;
+    seg_reduce_kernel<double><<<g, 256, 0, s>>>((const double*)vals, ent, seg, n, (double*)out, op, ident);
+  }
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+DR_API int dr_join_ranges(const E128* outer, uint64_t no, const E128* inner, uint64_t ni, uint64_t lo_mask,
+                          int64_t* lower, int64_t* count, hipStream_t s) {
+  if (no == 0) return 0;
+  join_ranges_kernel<<<grid_for(no, 256, 16384), 256, 0, s>>>(outer, no, inner, ni, lo_mask, lower, count);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+DR_API int dr_join_emit(const E128* outer, const E128* inner, uint64_t no, const int64_t* lower, const int64_t* count,
+                        const int64_t* offs, int64_t* out_outer, int64_t* out_inner, hipStream_t s) {
+  if (no == 0) return 0;
+  join_emit_kernel<<<grid_for(no, 256, 16384), 256, 0, s>>>(outer, inner, no, lower, count, offs, out_outer, out_inner);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+DR_API uint64_t dr_scan_i64_workspace(uint64_t n) {
+  uint64_t total = 0;
+  uint64_t m = n;
+  while (m > 1) {
+    m = (m + kChunk - 1) / kChunk;
+    total += m;
+  }
+  return (total + 8) * sizeof(int64_t);
+}
+
+// out[i] = sum_{j<i} a[i]  (may alias a).  Recursive reduce-then-scan.
+DR_API int dr_scan_i64(const int64_t* a, int64_t* out, uint64_t n, void* ws, hipStream_t s) {
+  if (n == 0) return 0;
+  int64_t* part = reinterpret_cast<int64_t*>(ws);
+  const uint64_t nb = (n + kChunk - 1) / kChunk;
+  if (nb == 1) {
+    hipMemsetAsync(part, 0, sizeof(int64_t), s);
+    scan_down_i64<<<1, 256, 0, s>>>(a, out, n, part);
+    DR_LAUNCH_CHECK();
+    return 0;
+  }
+  scan_reduce_i64<<<(unsigned)nb, 256, 0, s>>>(a, n, part);
+  int rc = dr_scan_i64(part, part, nb, part + nb, s);
+  if (rc) return rc;
+  scan_down_i64<<<(unsigned)nb, 256, 0, s>>>(a, out, n, part);
+  DR_LAUNCH_CHECK();
+  return 0;
+}

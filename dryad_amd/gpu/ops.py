@@ -1,0 +1,441 @@
+"""GPU implementations of the vertex operator library over HBM-resident ``DeviceTable`` partitions.
+
+Each function mirrors an op of ``runtime/vertex_ops.py`` (the object path) with the same
+signature ``fn(op, inputs, vctx)``; inputs are DeviceTables, the result a DeviceTable or a
+``Ported`` table for multi-port (partitioning) outputs.  An op raises ``NotTraceable`` when it
+cannot run on the device (opaque lambda, custom comparer, string data, ...); the executor then runs
+the object implementation for that op only.
+
+Hot paths are HIP kernels: key normalisation (dr_build_keys / dr_extract_keys), LSD radix sort
+(dr_sort_u128), hashing and partition passes (dr_hash_dest / dr_partition_pass_u128), range
+destinations (dr_range_dest_u128), segmented reductions (dr_seg_reduce), merge-join expansion
+(dr_join_ranges / dr_join_emit), row gathers (dr_gather_rows) and the synthetic TeraSort store.
+Elementwise projections/predicates are traced user lambdas executed as PyTorch-ROCm tensor ops.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..compiler.decomposition import Sym, substitute
+from ..ops import recordsort as RS
+from ..ops import relational as R
+from ..ops import sort as S
+from . import trace as TR
+from .table import DeviceTable, Ported, Shape, from_objects
+from .trace import NotTraceable
+
+E_SHAPE = Shape("tuple", ["lo", "hi"])
+
+
+def _one(inputs) -> DeviceTable:
+    ts = [t for t in inputs if t is not None]
+    if len(ts) == 1:
+        return ts[0]
+    return DeviceTable.concat(ts)
+
+
+def _check(t):
+    if not isinstance(t, DeviceTable):
+        raise NotTraceable("host partition")
+    return t
+
+
+# ---------------------------------------------------------------------------------------------
+# key handling
+def key_entries(table: DeviceTable, key_fn, comparer=None, descending=False):
+    """-> (entries [n,2], begin_bit, lo_mask).  Keys compare like the object path's default order."""
+    if comparer is not None:
+        raise NotTraceable("custom comparer")
+    if table.n == 0:
+        return torch.empty((0, 2), dtype=torch.int64, device=table.device), 64, 0
+    res = TR.call(key_fn, table)
+    kind, spec = TR.key_columns(res, table)
+    if kind == "bytes":
+        if spec.length > 12:
+            raise NotTraceable("byte key longer than 12 bytes")
+        e = S.extract_keys(table.rows, spec.off, spec.length, 0)
+        b0, _, lo_mask = RS.key_bits(spec.length)
+        if descending:
+            e[:, 1].bitwise_not_()
+            if lo_mask:
+                e[:, 0].bitwise_xor_(torch.tensor(RS._as_i64(lo_mask), dtype=torch.int64, device=e.device))
+        return e, b0, lo_mask
+    cols = spec
+    for c in cols:
+        if c.dtype not in R.KEY_TYPES:
+            raise NotTraceable(f"key dtype {c.dtype}")
+    if R.key_bit_count(cols) > 96:
+        raise NotTraceable("composite key wider than 96 bits")
+    e, b0, lo_mask = R.build_keys(cols, [descending] * len(cols))
+    return e, b0, lo_mask
+
+
+def _perm(entries: torch.Tensor) -> torch.Tensor:
+    return (entries[:, 0] & 0xFFFFFFFF).contiguous()
+
+
+def sort_perm(table, key_fn, comparer=None, descending=False):
+    e, b0, lo_mask = key_entries(table, key_fn, comparer, descending)
+    srt = S.sort_entries(e, b0, 128)
+    return srt, _perm(srt), lo_mask
+
+
+# ---------------------------------------------------------------------------------------------
+# sources / trivial ops
+def op_enumerable(op, inputs, v):
+    recs = op["chunks"][v.partition]
+    t = from_objects(recs, op.get("dtype"), v.device)
+    if t is None:
+        raise NotTraceable("non-columnar record type")
+    return t
+
+
+def op_read(op, inputs, v):
+    from ..io.providers import parse_uri, provider_for
+    uri = op["uri"]
+    scheme, path, q = parse_uri(uri)
+    if scheme == "gen":
+        kind = path.strip("/")
+        from ..io.providers import GenProvider
+        lo, hi = GenProvider().bounds(uri, v.partition)
+        if kind == "terasort":
+            from ..ops import terasort as TSK
+            rows = v.alloc_rows(hi - lo, 100)
+            TSK.generate(rows, lo, int(q.get("seed", 0)))
+            return DeviceTable(hi - lo, Shape("rows", key_off=0, key_len=10), rows=rows)
+        if kind == "range":
+            start = int(q.get("start", 0))
+            a = torch.arange(start + lo, start + hi, dtype=torch.int32 if start + hi < 2**31 else torch.int64,
+                             device=v.device)
+            return DeviceTable.from_columns({"v": a}, Shape("scalar", ["v"]))
+    if scheme == "hbm":
+        return provider_for(uri).get(uri)["local"][v.partition]
+    recs = provider_for(uri).read_partition(uri, v.partition, op.get("dtype"))
+    t = from_objects(recs, op.get("dtype"), v.device)
+    if t is None:
+        raise NotTraceable("non-columnar store records")
+    return t
+
+
+def op_identity(op, inputs, v):
+    return _one(inputs)
+
+
+def op_concat(op, inputs, v):
+    return _one(inputs)
+
+
+def op_output(op, inputs, v):
+    return _one(inputs)
+
+
+def op_where(op, inputs, v):
+    t = _check(_one(inputs))
+    if t.n == 0:
+        return t
+    return t.mask(TR.to_mask(TR.call(op["fn"], t), t))
+
+
+def op_select(op, inputs, v):
+    t = _check(_one(inputs))
+    if t.n == 0:
+        raise NotTraceable("empty partition: output type unknown")
+    return TR.to_table(TR.call(op["fn"], t), t)
+
+
+def _offset(inputs, v):
+    offs = inputs[1]
+    if isinstance(offs, DeviceTable):
+        vals = offs.cols[offs.shape.fields[0]].tolist()
+    else:
+        vals = list(offs)
+    return vals[v.partition] if v.partition < len(vals) else 0
+
+
+def op_where_idx(op, inputs, v):
+    t = _check(inputs[0])
+    if t.n == 0:
+        return t
+    return t.mask(TR.to_mask(TR.call(op["fn"], t, _offset(inputs, v)), t))
+
+
+def op_select_idx(op, inputs, v):
+    t = _check(inputs[0])
+    if t.n == 0:
+        raise NotTraceable("empty partition")
+    return TR.to_table(TR.call(op["fn"], t, _offset(inputs, v)), t)
+
+
+def op_take(op, inputs, v):
+    t = _check(_one(inputs))
+    return t.slice(0, min(t.n, max(0, op["count"])))
+
+
+def op_skip(op, inputs, v):
+    t = _check(_one(inputs))
+    return t.slice(min(t.n, max(0, op["count"])), t.n)
+
+
+def op_reverse(op, inputs, v):
+    t = _check(_one(inputs))
+    return t.take(torch.arange(t.n - 1, -1, -1, device=t.device))
+
+
+def _scalar_table(vals, dtype, device):
+    return DeviceTable.from_columns({"v": torch.tensor(vals, dtype=dtype, device=device)}, Shape("scalar", ["v"]))
+
+
+def op_count(op, inputs, v):
+    t = _check(_one(inputs))
+    return _scalar_table([t.n], torch.int64, v.device)
+
+
+def op_offsets(op, inputs, v):
+    t = _check(_one(inputs))
+    c = t.cols[t.shape.fields[0]].to(torch.int64)
+    return DeviceTable.from_columns({"v": torch.cumsum(c, 0) - c}, Shape("scalar", ["v"]))
+
+
+# ---------------------------------------------------------------------------------------------
+# sorting / partitioning
+def op_sort(op, inputs, v):
+    t = _check(_one(inputs))
+    if t.n <= 1:
+        return t
+    _, perm, _ = sort_perm(t, op["key"], op.get("comparer"), op.get("descending", False))
+    return t.take(perm)
+
+
+def op_hash_partition(op, inputs, v):
+    t = _check(_one(inputs))
+    n = op["count"]
+    if op.get("comparer") is not None:
+        raise NotTraceable("custom comparer")
+    if t.n == 0:
+        return Ported(t, [0] * (n + 1))
+    e, _, lo_mask = key_entries(t, op["key"])
+    R.hash_dest(e, lo_mask, n)
+    part, starts = S.partition_pass(e, 64)
+    st = starts[: n + 1].tolist()
+    return Ported(t.take(_perm(part)), st)
+
+
+def op_sample(op, inputs, v):
+    t = _check(_one(inputs))
+    e, b0, lo_mask = key_entries(t, op["key"], op.get("comparer"), False)
+    n = t.n
+    rate = op.get("rate", 0.001)
+    m = n if n * rate < 10 else max(1, int(n * rate))
+    stride = max(1, n // max(m, 1))
+    samp = e[::stride][:m].clone() if n else e
+    samp[:, 0] &= RS._as_i64(lo_mask)
+    return DeviceTable.from_columns({"lo": samp[:, 0].contiguous(), "hi": samp[:, 1].contiguous()}, E_SHAPE)
+
+
+def op_separators(op, inputs, v):
+    t = _check(_one(inputs))
+    n = op["count"]
+    if t.n == 0:
+        return DeviceTable.from_columns({"lo": torch.empty(0, dtype=torch.int64, device=v.device),
+                                         "hi": torch.empty(0, dtype=torch.int64, device=v.device)}, E_SHAPE)
+    e = torch.stack([t.cols["lo"], t.cols["hi"]], 1).contiguous()
+    srt = S.sort_entries(e, 0, 128)
+    pos = torch.tensor([(j * t.n) // n for j in range(1, n)], dtype=torch.int64, device=e.device)
+    s = srt.index_select(0, pos)
+    return DeviceTable.from_columns({"lo": s[:, 0].contiguous(), "hi": s[:, 1].contiguous()}, E_SHAPE)
+
+
+def op_range_partition(op, inputs, v):
+    t = _check(inputs[0])
+    n = op["count"]
+    if op.get("separators") is not None:
+        raise NotTraceable("explicit separators are host values")
+    seps_t = inputs[1] if len(inputs) > 1 else None
+    if t.n == 0:
+        return Ported(t, [0] * (n + 1))
+    e, _, lo_mask = key_entries(t, op["key"], op.get("comparer"), False)
+    if seps_t is None or seps_t.n == 0:
+        return Ported(t, [0] + [t.n] * n)
+    seps = torch.stack([seps_t.cols["lo"], seps_t.cols["hi"]], 1).contiguous()
+    S.range_dest(e, seps, lo_mask, descending=op.get("descending", False))
+    part, starts = S.partition_pass(e, 64)
+    return Ported(t.take(_perm(part)), starts[: n + 1].tolist())
+
+
+# ---------------------------------------------------------------------------------------------
+# GroupBy with decomposable aggregates (sort-based: radix sort -> segments -> segmented reduce)
+_GPU_AGGS = {"count", "sum", "min", "max", "avg", "any", "all"}
+
+
+def _agg_value(agg, t):
+    if agg.kind == "count":
+        if agg.pred is None:
+            return None
+        return TR.to_mask(TR.call(agg.pred, t), t).to(torch.int64)
+    if agg.kind in ("any", "all"):
+        if agg.pred is None:
+            return torch.ones(t.n, dtype=torch.int64, device=t.device)
+        return TR.to_mask(TR.call(agg.pred, t), t).to(torch.int64)
+    if agg.sel is None:
+        if t.shape.kind != "scalar":
+            raise NotTraceable("aggregate over non-scalar records")
+        return t.cols[t.shape.fields[0]]
+    r = TR.call(agg.sel, t)
+    if not isinstance(r, TR.Col):
+        raise NotTraceable("aggregate selector must produce a scalar field")
+    return r.t
+
+
+def _key_cols(t, key_fn):
+    res = TR.call(key_fn, t)
+    kind, spec = TR.key_columns(res, t)
+    if kind != "cols":
+        raise NotTraceable("byte-string group keys")
+    return spec, isinstance(res, tuple)
+
+
+def op_group_partial(op, inputs, v):
+    t = _check(_one(inputs))
+    d = op["decomp"]
+    if op.get("comparer") is not None or any(a.kind not in _GPU_AGGS for a in d.aggs):
+        raise NotTraceable("aggregate not supported on the device")
+    if t.n == 0:
+        raise NotTraceable("empty partition")
+    kcols, _ = _key_cols(t, op["key"])
+    e, b0, lo_mask = R.build_keys(kcols)
+    srt = S.sort_entries(e, b0, 128)
+    seg, nseg, starts = R.segment_ids(srt, lo_mask)
+    rows_at_start = _perm(srt).index_select(0, starts)
+    out = {f"k{i}": c.index_select(0, rows_at_start) for i, c in enumerate(kcols)}
+    for j, a in enumerate(d.aggs):
+        val = _agg_value(a, t)
+        if a.kind == "count":
+            out[f"a{j}"] = R.seg_reduce(val, srt, seg, nseg, R.OP_COUNT if val is None else R.OP_SUM, torch.int64)
+        elif a.kind == "sum":
+            out[f"a{j}"] = R.seg_reduce(val, srt, seg, nseg, R.OP_SUM, val.dtype)
+        elif a.kind in ("min", "max"):
+            out[f"a{j}"] = R.seg_reduce(val, srt, seg, nseg, R.OP_MIN if a.kind == "min" else R.OP_MAX, val.dtype)
+        elif a.kind == "avg":
+            out[f"a{j}"] = R.seg_reduce(val, srt, seg, nseg, R.OP_SUM, torch.float64)
+            out[f"c{j}"] = R.seg_reduce(None, srt, seg, nseg, R.OP_COUNT, torch.int64)
+        elif a.kind in ("any", "all"):
+            out[f"a{j}"] = R.seg_reduce(val, srt, seg, nseg, R.OP_MAX if a.kind == "any" else R.OP_MIN, torch.int64)
+    tb = DeviceTable.from_columns(out, Shape("tuple", list(out)))
+    tb.group_meta = dict(nkeys=len(kcols), aggs=d.aggs)
+    return tb
+
+
+def _pkey(r):   # key selector of partial-aggregate tables: the key columns
+    return tuple(getattr(r, f"k{i}") for i in range(_pkey.nkeys))
+
+
+def op_group_final(op, inputs, v):
+    t = _check(_one(inputs))
+    d = op["decomp"]
+    if t.n == 0:
+        raise NotTraceable("empty partition")
+    nkeys = sum(1 for f in t.shape.fields if f.startswith("k"))
+    kcols = [t.cols[f"k{i}"] for i in range(nkeys)]
+    e, b0, lo_mask = R.build_keys(kcols)
+    srt = S.sort_entries(e, b0, 128)
+    seg, nseg, starts = R.segment_ids(srt, lo_mask)
+    rows_at_start = _perm(srt).index_select(0, starts)
+    keys = [c.index_select(0, rows_at_start) for c in kcols]
+    vals = []
+    for j, a in enumerate(d.aggs):
+        col = t.cols[f"a{j}"]
+        if a.kind in ("count", "sum"):
+            r = R.seg_reduce(col, srt, seg, nseg, R.OP_SUM, col.dtype)
+            vals.append(r if col.dtype in (torch.int64, torch.float64) else r.to(col.dtype))
+        elif a.kind in ("min", "max"):
+            r = R.seg_reduce(col, srt, seg, nseg, R.OP_MIN if a.kind == "min" else R.OP_MAX, col.dtype)
+            vals.append(r.to(col.dtype) if col.dtype != r.dtype else r)
+        elif a.kind == "avg":
+            s_ = R.seg_reduce(col, srt, seg, nseg, R.OP_SUM, torch.float64)
+            c_ = R.seg_reduce(t.cols[f"c{j}"], srt, seg, nseg, R.OP_SUM, torch.int64)
+            vals.append(s_ / c_.to(torch.float64))
+        elif a.kind == "any":
+            vals.append(R.seg_reduce(col, srt, seg, nseg, R.OP_MAX, torch.int64).to(torch.bool))
+        elif a.kind == "all":
+            vals.append(R.seg_reduce(col, srt, seg, nseg, R.OP_MIN, torch.int64).to(torch.bool))
+    key = TR.Col(keys[0]) if nkeys == 1 else tuple(TR.Col(k) for k in keys)
+    env = {"key": key, "aggs": [TR.Col(x) for x in vals]}
+    try:
+        res = substitute(d.template, env)
+    except NotTraceable:
+        raise
+    except Exception as ex:  # noqa: BLE001
+        raise NotTraceable(f"result template: {ex}")
+    proto = DeviceTable(nseg, Shape("scalar", ["v"]), {"v": keys[0]})
+    return TR.to_table(res, proto)
+
+
+# ---------------------------------------------------------------------------------------------
+def op_distinct(op, inputs, v):
+    t = _check(_one(inputs))
+    if op.get("comparer") is not None:
+        raise NotTraceable("custom comparer")
+    if t.n <= 1:
+        return t
+    if t.rows is not None:
+        if t.rows.shape[1] > 12:
+            raise NotTraceable("wide rows")
+        e, b0, lo_mask = key_entries(t, lambda r: r[0:t.rows.shape[1]])
+    else:
+        cols = [t.cols[f] for f in t.shape.fields]
+        if R.key_bit_count(cols) > 96:
+            raise NotTraceable("record wider than 96 bits")
+        e, b0, lo_mask = R.build_keys(cols)
+    srt = S.sort_entries(e, b0, 128)
+    _, _, starts = R.segment_ids(srt, lo_mask)
+    return t.take(_perm(srt).index_select(0, starts))
+
+
+def op_hash_join(op, inputs, v):
+    outer, inner = _check(inputs[0]), _check(inputs[1])
+    if op.get("comparer") is not None:
+        raise NotTraceable("custom comparer")
+    if outer.n == 0 or inner.n == 0:
+        raise NotTraceable("empty join side: output type unknown")
+    eo, b0, lm = key_entries(outer, op["outer_key"])
+    ei, b1, lm2 = key_entries(inner, op["inner_key"])
+    if (b0, lm) != (b1, lm2):
+        raise NotTraceable("join keys of different types")
+    so = S.sort_entries(eo, b0, 128)
+    si = S.sort_entries(ei, b0, 128)
+    oo, ii, _ = R.merge_join_pairs(so, si, lm)
+    if oo.shape[0] == 0:
+        raise NotTraceable("empty join result")
+    a, b = outer.take(oo), inner.take(ii)
+    res = op["result"](TR.proxy(a), TR.proxy(b))
+    return TR.to_table(res, a)
+
+
+op_merge_join = op_hash_join
+
+
+# ---------------------------------------------------------------------------------------------
+# aggregates: partial per partition (device reductions) -> final on one vertex
+def op_agg_partial(op, inputs, v):
+    t = _check(_one(inputs))
+    s = op["spec"]
+    k = s["kind"]
+    if s.get("comparer") is not None:
+        raise NotTraceable("comparer")
+    if k == "Count":
+        if s.get("predicate") is None:
+            return _scalar_table([t.n], torch.int64, v.device)
+        if t.n == 0:
+            return _scalar_table([0], torch.int64, v.device)
+        return _scalar_table([int(TR.to_mask(TR.call(s["predicate"], t), t).sum().item())], torch.int64, v.device)
+    raise NotTraceable(f"aggregate {k} on host")
+
+
+def op_agg_final(op, inputs, v):
+    t = _check(_one(inputs))
+    if op["spec"]["kind"] == "Count":
+        return _scalar_table([int(t.cols[t.shape.fields[0]].sum().item())], torch.int64, v.device)
+    raise NotTraceable("aggregate on host")
+
+
+OPS = {k[3:]: fn for k, fn in list(globals().items()) if k.startswith("op_")}

@@ -1,0 +1,66 @@
+"""HBM working-set pool of the GPU executor.
+
+A 125 GB/GPU sort needs input rows + output rows + two entry arrays resident at once (~290 GB of
+the 309 GB on an MI355X), so the executor cannot let each vertex allocate freely: large record
+tables are carved out of one long-lived ``SortBuffers`` set that is reused job after job.  An HBM
+output table (``hbm://``) pins the buffer set its rows live in until the table is deleted
+(``ToStore(..., delete_if_exists=True)`` deletes at submission, like the reference's
+CheckExistence(deleteIfExists) in DataProvider.cs:484-538).
+"""
+from __future__ import annotations
+
+import threading
+
+import torch
+
+from ..ops import recordsort as RS
+
+
+class BufferSet:
+    def __init__(self, bufs: RS.SortBuffers, stride: int):
+        self.bufs = bufs
+        self.stride = stride
+        self.pins = 0
+        self.in_use = False
+
+    @property
+    def capacity(self):
+        return self.bufs.capacity
+
+
+class HbmPool:
+    def __init__(self, device):
+        self.device = device
+        self.sets: list = []
+        self.lock = threading.Lock()
+
+    def acquire(self, capacity: int, stride: int) -> BufferSet:
+        with self.lock:
+            for s in self.sets:
+                if not s.in_use and s.pins == 0 and s.stride == stride and s.capacity >= capacity:
+                    s.in_use = True
+                    return s
+            # drop idle sets before allocating a new one (HBM is the limit, not the allocator)
+            keep = [s for s in self.sets if s.in_use or s.pins > 0]
+            self.sets = keep
+            torch.cuda.empty_cache() if self.device.type == "cuda" else None
+            s = BufferSet(RS.SortBuffers.allocate(capacity, stride, self.device), stride)
+            s.in_use = True
+            self.sets.append(s)
+            return s
+
+    def release(self, s: BufferSet):
+        with self.lock:
+            s.in_use = False
+
+    def pin(self, s: BufferSet):
+        with self.lock:
+            s.pins += 1
+
+    def unpin(self, s: BufferSet):
+        with self.lock:
+            s.pins = max(0, s.pins - 1)
+
+    def clear(self):
+        with self.lock:
+            self.sets = [s for s in self.sets if s.in_use or s.pins > 0]

@@ -1,0 +1,200 @@
+"""Device-resident partitions for the GPU executor.
+
+A partition in HBM is a ``DeviceTable``: either
+
+  * ``rows``  — fixed-width row records (``uint8 [n, stride]``), e.g. TeraSort's 100-byte records;
+    the key is a byte-string field ``(key_off, key_len)`` compared in memcmp order, or
+  * ``cols``  — struct-of-arrays: an ordered dict of equally long 1-D tensors (one per record
+    field), with a ``shape`` describing how fields map back to Python records: a scalar, a tuple,
+    a dataclass, or a LineRecord-free fixed record.
+
+The DryadLINQ ``channel`` between two vertices on the same GPU is a DeviceTable handed over by
+reference (zero copy); across GPUs it is packed into one uint8 row buffer and moved with RCCL.
+Output ports of partitioning vertices are *one* permuted table plus port offsets (``Ported``), so
+a shuffle never materialises N small tables.
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .. import types as T
+
+
+@dataclass
+class Shape:
+    """How columns map to Python records."""
+    kind: str                         # "scalar" | "tuple" | "dataclass" | "rows"
+    fields: list = field(default_factory=list)   # column names in record order
+    pytype: object = None
+    key_off: int = 0                  # rows: default key field
+    key_len: int = 0
+
+    def describe(self):
+        if self.kind == "rows":
+            return f"rows(key=[{self.key_off},{self.key_off + self.key_len}))"
+        return f"{self.kind}({', '.join(self.fields)})"
+
+
+class DeviceTable:
+    def __init__(self, n: int, shape: Shape, cols: dict | None = None, rows: torch.Tensor | None = None):
+        self.n = int(n)
+        self.shape = shape
+        self.cols = cols if cols is not None else {}
+        self.rows = rows
+
+    # ------------------------------------------------------------------ construction
+    @staticmethod
+    def from_rows(rows: torch.Tensor, key_off=0, key_len=None) -> "DeviceTable":
+        return DeviceTable(rows.shape[0], Shape("rows", key_off=key_off, key_len=key_len or rows.shape[1]), rows=rows)
+
+    @staticmethod
+    def from_columns(cols: dict, shape: Shape) -> "DeviceTable":
+        n = next(iter(cols.values())).shape[0] if cols else 0
+        return DeviceTable(n, shape, dict(cols))
+
+    @staticmethod
+    def empty_like(t: "DeviceTable", n: int = 0) -> "DeviceTable":
+        if t.shape.kind == "rows":
+            return DeviceTable(n, t.shape, rows=t.rows.new_empty((n, t.rows.shape[1])))
+        return DeviceTable(n, t.shape, {k: v.new_empty((n,)) for k, v in t.cols.items()})
+
+    @property
+    def device(self):
+        if self.rows is not None:
+            return self.rows.device
+        for v in self.cols.values():
+            return v.device
+        return torch.device("cpu")
+
+    @property
+    def nbytes(self) -> int:
+        if self.rows is not None:
+            return self.rows.numel()
+        return sum(v.numel() * v.element_size() for v in self.cols.values())
+
+    def row_bytes(self) -> int:
+        if self.rows is not None:
+            return self.rows.shape[1]
+        return sum(v.element_size() for v in self.cols.values())
+
+    # ------------------------------------------------------------------ slicing / permutation
+    def slice(self, a: int, b: int) -> "DeviceTable":
+        if self.rows is not None:
+            return DeviceTable(b - a, self.shape, rows=self.rows[a:b])
+        return DeviceTable(b - a, self.shape, {k: v[a:b] for k, v in self.cols.items()})
+
+    def take(self, idx: torch.Tensor) -> "DeviceTable":
+        """Gather rows by an int64 index tensor (HIP row gather for row tables)."""
+        if self.rows is not None:
+            from ..ops import sort as S
+            return DeviceTable(idx.shape[0], self.shape, rows=S.gather_rows(self.rows, index=idx.contiguous()))
+        return DeviceTable(idx.shape[0], self.shape, {k: v.index_select(0, idx) for k, v in self.cols.items()})
+
+    def mask(self, m: torch.Tensor) -> "DeviceTable":
+        idx = torch.nonzero(m, as_tuple=False).flatten()
+        return self.take(idx)
+
+    @staticmethod
+    def concat(tables: list) -> "DeviceTable":
+        tables = [t for t in tables if t is not None]
+        if not tables:
+            return None
+        t0 = tables[0]
+        if len(tables) == 1:
+            return t0
+        if t0.rows is not None:
+            return DeviceTable(sum(t.n for t in tables), t0.shape, rows=torch.cat([t.rows for t in tables]))
+        return DeviceTable(sum(t.n for t in tables), t0.shape,
+                           {k: torch.cat([t.cols[k] for t in tables]) for k in t0.cols})
+
+    # ------------------------------------------------------------------ packing for RCCL
+    def pack(self) -> torch.Tensor:
+        """One uint8 [n, row_bytes] buffer (AoS) so an exchange is a single collective."""
+        if self.rows is not None:
+            return self.rows
+        parts = [v.contiguous().view(torch.uint8).reshape(self.n, v.element_size()) for v in self.cols.values()]
+        if not parts:
+            return torch.empty((self.n, 0), dtype=torch.uint8, device=self.device)
+        return torch.cat(parts, dim=1) if len(parts) > 1 else parts[0]
+
+    def unpack_like(self, buf: torch.Tensor, n: int) -> "DeviceTable":
+        if self.rows is not None:
+            return DeviceTable(n, self.shape, rows=buf.reshape(n, self.rows.shape[1]))
+        buf = buf.reshape(n, -1)
+        out, off = {}, 0
+        for k, v in self.cols.items():
+            w = v.element_size()
+            out[k] = buf[:, off:off + w].contiguous().view(v.dtype).reshape(n)
+            off += w
+        return DeviceTable(n, self.shape, out)
+
+    # ------------------------------------------------------------------ host conversion
+    def to_objects(self) -> list:
+        if self.n == 0:
+            return []
+        if self.rows is not None:
+            a = self.rows.cpu().numpy()
+            return [bytes(r) for r in a]
+        arrs = {k: v.cpu().numpy() for k, v in self.cols.items()}
+        sh = self.shape
+        if sh.kind == "scalar":
+            return arrs[sh.fields[0]].tolist()
+        lists = [arrs[f].tolist() for f in sh.fields]
+        if sh.kind == "tuple":
+            return list(zip(*lists))
+        if sh.kind == "dataclass":
+            return [sh.pytype(*vals) for vals in zip(*lists)]
+        raise ValueError(sh.kind)
+
+
+@dataclass
+class Ported:
+    """A multi-port vertex output: ``table`` permuted so port k = rows [offsets[k], offsets[k+1])."""
+    table: DeviceTable
+    offsets: list
+
+    def port(self, k: int) -> DeviceTable:
+        return self.table.slice(self.offsets[k], self.offsets[k + 1])
+
+    @property
+    def nports(self):
+        return len(self.offsets) - 1
+
+
+# ---------------------------------------------------------------------------------------------
+_NP_OF = {T.Int32: np.int32, T.Int64: np.int64, T.Float64: np.float64, T.Float32: np.float32, T.Bool: np.bool_,
+          T.Int16: np.int16, T.Byte: np.uint8, T.SByte: np.int8, T.UInt16: np.uint16}
+
+
+def columnar_dtype(dt) -> bool:
+    """Can records of this DType live as columns in HBM?"""
+    if dt in _NP_OF:
+        return True
+    if isinstance(dt, T.RecordT):
+        return all(t in _NP_OF for _, t in dt.fields) and not dt.nullable_fields
+    return False
+
+
+def from_objects(records: list, dt, device) -> DeviceTable | None:
+    """Ingress: Python records -> DeviceTable (None if the type is not columnar)."""
+    if dt is None:
+        dt = T.infer_common_type(records[:1000]) if records else T.Int32
+    if not columnar_dtype(dt):
+        return None
+    if dt in _NP_OF:
+        a = np.asarray(records, dtype=_NP_OF[dt]) if records else np.zeros(0, _NP_OF[dt])
+        return DeviceTable.from_columns({"v": torch.from_numpy(a).to(device)}, Shape("scalar", ["v"]))
+    names = [n for n, _ in dt.fields]
+    cols = {}
+    for i, (n, t) in enumerate(dt.fields):
+        if dt.pytype in (None, tuple):
+            vals = [r[i] for r in records]
+        else:
+            vals = [getattr(r, n) for r in records]
+        cols[n] = torch.from_numpy(np.asarray(vals, dtype=_NP_OF[t]) if vals else np.zeros(0, _NP_OF[t])).to(device)
+    kind = "tuple" if dt.pytype in (None, tuple) else "dataclass"
+    return DeviceTable.from_columns(cols, Shape(kind, names, None if kind == "tuple" else dt.pytype))

@@ -220,9 +220,14 @@ class HbmProvider(DataProvider):
         return self._name(uri) in self.tables
 
     def delete(self, uri):
-        self.tables.pop(self._name(uri), None)
+        ent = self.tables.pop(self._name(uri), None)
+        if ent is not None and ent.get("pool") is not None:
+            for b in ent.get("pins", []):
+                ent["pool"].unpin(b)
 
     def put(self, uri, entry: dict):
+        if self._name(uri) in self.tables:
+            self.delete(uri)
         self.tables[self._name(uri)] = entry
 
     def get(self, uri) -> dict:

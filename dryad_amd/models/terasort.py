@@ -95,7 +95,61 @@ class TeraSortJob:
                     records=int(cnt.item()), boundary_ok=boundary_ok)
 
 
-def run_steps(job: TeraSortJob, steps: int) -> float:
+class TeraSortQueryJob:
+    """The same TeraSort expressed as a DryadLINQ query and executed by the GPU executor:
+
+        ctx.FromStore("gen://terasort?...").OrderBy(r => r[0:10]).ToStore("hbm://terasort_out")
+
+    The planner emits Sample -> Separators -> RangePartition -(CrossProduct)-> Merge+Sort; the GPU
+    executor recognises the idiom and runs it as one fused gang stage on pooled HBM buffers."""
+
+    OUT = "hbm://terasort_out"
+
+    def __init__(self, cfg: TeraSortConfig, world: World | None = None):
+        import dryad_amd as D
+        self.cfg = cfg
+        self.world = world or get_world()
+        self.n = cfg.records_per_rank
+        W = self.world.size
+        self.ctx = D.DryadLinqContext(platform="gpu")
+        self.ctx.PartitionCount = W
+        self.ctx._props["ShuffleSlack"] = cfg.slack
+        self.src = f"gen://terasort?records={self.n * W}&partitions={W}&seed={cfg.seed}"
+        self.out = None
+
+    @property
+    def bytes_per_rank(self) -> int:
+        return self.n * RECORD
+
+    def query(self):
+        return (self.ctx.FromStore(self.src)
+                .OrderBy(lambda r: r[0:10])
+                .ToStore(self.OUT, delete_if_exists=True))
+
+    def step(self):
+        self.query().SubmitAndWait()
+        from ..io.providers import provider_for
+        ent = provider_for(self.OUT).get(self.OUT)
+        self.out = ent["local"][self.world.rank].rows
+        return self.out
+
+    def executor_report(self) -> dict:
+        ex = self.ctx._get_executor()
+        r = ex.last_result or {}
+        return dict(fallbacks=r.get("fallbacks"), timings=r.get("timings"))
+
+    def input_checksum(self) -> tuple[int, int]:
+        rows = torch.empty((self.n, RECORD), dtype=torch.uint8, device=self.world.device)
+        TS.generate(rows, self.world.rank * self.n, self.cfg.seed)
+        acc = TS.check(rows)
+        del rows
+        shuffle.all_reduce_(acc, "sum", self.world)
+        return int(acc[0].item()), self.n * self.world.size
+
+    validate = TeraSortJob.validate
+
+
+def run_steps(job, steps: int) -> float:
     """Run ``steps`` steps bracketed by barrier+synchronize; returns max-over-ranks seconds."""
     w = job.world
     dev = w.device

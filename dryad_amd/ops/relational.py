@@ -1,0 +1,127 @@
+"""Python wrappers of the relational HIP kernels (csrc/kernels/relational.hip)."""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import c_i32, c_u32, c_u64, ptr, stream_of, vp
+
+_lib.register_signatures({
+    "dr_build_keys": (c_i32, [ctypes.POINTER(vp), ctypes.POINTER(c_i32), ctypes.POINTER(c_i32), c_i32, c_u64, c_u32,
+                              vp, ctypes.POINTER(c_i32), vp]),
+    "dr_hash_dest": (c_i32, [vp, c_u64, c_u64, c_u32, vp]),
+    "dr_segment_flags": (c_i32, [vp, c_u64, c_u64, vp, vp]),
+    "dr_seg_reduce": (c_i32, [vp, vp, vp, c_u64, vp, c_i32, c_i32, vp]),
+    "dr_join_ranges": (c_i32, [vp, c_u64, vp, c_u64, c_u64, vp, vp, vp]),
+    "dr_join_emit": (c_i32, [vp, vp, c_u64, vp, vp, vp, vp, vp, vp]),
+    "dr_scan_i64_workspace": (c_u64, [c_u64]),
+    "dr_scan_i64": (c_i32, [vp, vp, c_u64, vp, vp]),
+})
+
+KEY_TYPES = {torch.uint8: 0, torch.int8: 1, torch.bool: 2, torch.int16: 3, torch.uint16: 4, torch.int32: 5,
+             torch.uint32: 6, torch.int64: 7, torch.uint64: 8, torch.float32: 9, torch.float64: 10}
+KEY_BITS = {0: 8, 1: 8, 2: 8, 3: 16, 4: 16, 5: 32, 6: 32, 7: 64, 8: 64, 9: 32, 10: 64}
+
+OP_SUM, OP_MIN, OP_MAX, OP_COUNT = 0, 1, 2, 3
+
+
+def key_bit_count(cols) -> int:
+    return sum(KEY_BITS[KEY_TYPES[c.dtype]] for c in cols)
+
+
+def build_keys(cols: list, descending=None, idx_base: int = 0, out: torch.Tensor | None = None):
+    """Typed key columns (<= 96 bits total) -> (E128 entries [n,2] int64, begin_bit, lo_mask)."""
+    n = cols[0].shape[0]
+    dev = cols[0].device
+    if out is None:
+        out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    cols = [c.contiguous() for c in cols]
+    arr = (vp * len(cols))(*[c.data_ptr() for c in cols])
+    ty = (c_i32 * len(cols))(*[KEY_TYPES[c.dtype] for c in cols])
+    de = (c_i32 * len(cols))(*[int(bool(d)) for d in (descending or [False] * len(cols))])
+    bb = c_i32(0)
+    _lib.call("dr_build_keys", arr, ty, de, len(cols), c_u64(n), c_u32(idx_base), ptr(out), ctypes.byref(bb),
+              stream_of(out))
+    bits = key_bit_count(cols)
+    # lo bits that hold key material (everything above the 32-bit row index)
+    key_lo_bits = max(0, bits - 64)
+    lo_mask = (((1 << key_lo_bits) - 1) << (64 - key_lo_bits)) if key_lo_bits else 0
+    return out[:n], bb.value, lo_mask
+
+
+def hash_dest(entries: torch.Tensor, lo_mask: int, nparts: int) -> torch.Tensor:
+    _lib.call("dr_hash_dest", ptr(entries), c_u64(entries.shape[0]), c_u64(lo_mask & (2**64 - 1)), c_u32(nparts),
+              stream_of(entries))
+    return entries
+
+
+def segment_flags(entries: torch.Tensor, lo_mask: int) -> torch.Tensor:
+    n = entries.shape[0]
+    flags = torch.empty(n, dtype=torch.int64, device=entries.device)
+    _lib.call("dr_segment_flags", ptr(entries), c_u64(n), c_u64(lo_mask & (2**64 - 1)), ptr(flags), stream_of(entries))
+    return flags
+
+
+def scan_exclusive(a: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    assert a.dtype == torch.int64 and a.is_contiguous()
+    n = a.shape[0]
+    if out is None:
+        out = torch.empty_like(a)
+    ws = torch.empty(int(_lib.lib().dr_scan_i64_workspace(c_u64(max(n, 1)))), dtype=torch.uint8, device=a.device)
+    _lib.call("dr_scan_i64", ptr(a), ptr(out), c_u64(n), ptr(ws), stream_of(a))
+    return out
+
+
+def segment_ids(entries: torch.Tensor, lo_mask: int):
+    """(segment id per sorted row, number of segments, segment start positions)."""
+    flags = segment_flags(entries, lo_mask)
+    ids = scan_exclusive(flags)
+    n = entries.shape[0]
+    if n == 0:
+        return ids, 0, ids
+    nseg = int(ids[-1].item() + flags[-1].item())
+    # ids are exclusive sums: segment id of row i = (#starts before i) + flag[i] - 1
+    ids = ids + flags - 1
+    starts = torch.nonzero(flags, as_tuple=False).flatten()
+    return ids, nseg, starts
+
+
+def seg_reduce(vals: torch.Tensor | None, entries: torch.Tensor | None, seg: torch.Tensor, nseg: int, op: int,
+               dtype: torch.dtype = torch.float64) -> torch.Tensor:
+    """Segmented reduction over rows in sorted order (row = entries[i].lo & 0xffffffff)."""
+    n = seg.shape[0]
+    dev = seg.device
+    dt = 0 if dtype in (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool) else 1
+    tdt = torch.int64 if dt == 0 else torch.float64
+    if op == OP_MIN:
+        init = torch.iinfo(torch.int64).max if dt == 0 else float("inf")
+    elif op == OP_MAX:
+        init = torch.iinfo(torch.int64).min if dt == 0 else float("-inf")
+    else:
+        init = 0
+    out = torch.full((nseg,), init, dtype=tdt, device=dev)
+    v = None
+    if op != OP_COUNT:
+        v = vals.to(tdt).contiguous()
+    _lib.call("dr_seg_reduce", ptr(v), ptr(entries), ptr(seg), c_u64(n), ptr(out), op, dt, stream_of(seg))
+    return out
+
+
+def merge_join_pairs(outer_sorted: torch.Tensor, inner_sorted: torch.Tensor, lo_mask: int):
+    """Row-index pairs (outer_row, inner_row) of equal keys between two sorted entry arrays,
+    grouped by outer in sorted-key order."""
+    no, ni = outer_sorted.shape[0], inner_sorted.shape[0]
+    dev = outer_sorted.device
+    lower = torch.empty(no, dtype=torch.int64, device=dev)
+    count = torch.empty(no, dtype=torch.int64, device=dev)
+    _lib.call("dr_join_ranges", ptr(outer_sorted), c_u64(no), ptr(inner_sorted), c_u64(ni),
+              c_u64(lo_mask & (2**64 - 1)), ptr(lower), ptr(count), stream_of(outer_sorted))
+    offs = scan_exclusive(count)
+    total = int((offs[-1] + count[-1]).item()) if no else 0
+    oo = torch.empty(total, dtype=torch.int64, device=dev)
+    ii = torch.empty(total, dtype=torch.int64, device=dev)
+    _lib.call("dr_join_emit", ptr(outer_sorted), ptr(inner_sorted), c_u64(no), ptr(lower), ptr(count), ptr(offs),
+              ptr(oo), ptr(ii), stream_of(outer_sorted))
+    return oo, ii, count

@@ -1,0 +1,623 @@
+"""SPMD executor for MI355X ranks: one process per GPU, every rank runs the same plan.
+
+Mapping of the Dryad runtime onto a node of GPUs:
+  * vertex placement: partition p of every stage lives on rank ``p % world`` (a GPU "computer");
+    pointwise channels between stages are zero-copy hand-offs of HBM tables
+  * CrossProduct channels (hash / range shuffles) are one RCCL all-to-all-v of packed rows over
+    xGMI per stage; merge / broadcast / remote pointwise channels are gathers / all-gathers
+  * the stage DAG executes bulk-synchronously in topological order; the native ``JobGraph``
+    tracks vertex versions — a failed vertex is re-executed in place (its inputs are still
+    resident in HBM) up to MaxVertexFailures, and a per-stage all-reduce of the status word makes
+    every rank abort together instead of hanging in the next collective (gang semantics of
+    DrCohort/DrGang: a collective exchange stage restarts as a whole)
+  * each op runs as a HIP/PyTorch device op when its lambdas trace to columns (gpu/ops.py);
+    otherwise that op alone runs on host objects (recorded in ``self.fallbacks``)
+"""
+from __future__ import annotations
+
+import json
+import os
+import pickle
+import time
+
+import torch
+import torch.distributed as dist
+
+from ..compiler.planner import compile_queries
+from ..errors import DryadLinqException, DryadLinqJobException, ErrorCode
+from ..gpu import ops as G
+from ..gpu.table import DeviceTable, Ported, from_objects
+from ..gpu.trace import NotTraceable
+from ..io.providers import parse_uri, provider_for
+from ..native import runtime as native_runtime
+from ..parallel import shuffle
+from ..parallel.comm import World, get_world, init_world
+from ..utils.log import get_logger
+from . import vertex_ops as V
+from .executor import _BaseExecutor
+
+log = get_logger("gpu_executor")
+
+
+class GpuVertexContext(V.VertexContext):
+    def __init__(self, partition, partitions, vertex_id, version, stage, device, world, runner=None):
+        super().__init__(partition, partitions, vertex_id, version, stage)
+        self.device = device
+        self.world = world
+        self.runner = runner
+
+    def alloc_rows(self, n, stride):
+        """Large row tables come from the executor's HBM pool (reused across jobs)."""
+        r = self.runner
+        if r is None or r.pool is None or self.device.type != "cuda" or n * stride < (64 << 20):
+            return torch.empty((n, stride), dtype=torch.uint8, device=self.device)
+        slack = r.ctx._props.get("ShuffleSlack", 0.01) if self.world.size > 1 else 0.0
+        bs = r.pool.acquire(int(n * (1 + slack)) + 1024, stride)
+        r.row_sets[(self.stage.id, self.partition)] = bs
+        return bs.bufs.rows_in[:n]
+
+
+def _to_objects(x):
+    if isinstance(x, DeviceTable):
+        return x.to_objects()
+    if isinstance(x, Ported):
+        return [x.port(k).to_objects() for k in range(x.nports)]
+    return x
+
+
+def _object_bytes(x) -> int:
+    return x.nbytes if isinstance(x, DeviceTable) else 0
+
+
+class GpuJobRunner:
+    def __init__(self, ctx, plan, world: World, faults=None, pool=None):
+        self.ctx, self.plan, self.world = ctx, plan, world
+        self.pool = pool
+        self.row_sets: dict = {}          # (stage, partition) -> pooled BufferSet holding its rows
+        self.fused: dict = {}             # merge stage id -> fused distributed-OrderBy descriptor
+        self.skipped: set = set()
+        self.dev = world.device
+        self.gpu_ok = self.dev.type == "cuda"
+        self.faults = faults or []
+        self.channels: dict = {}          # (stage, partition) -> DeviceTable | Ported | list | list-of-lists
+        self.fallbacks: list = []
+        self.timings: dict = {}
+        R = native_runtime()
+        p = R.Params()
+        p.max_failures = int(getattr(ctx, "MaxVertexFailures", 6) or 6)
+        p.speculative = False            # collectives: no duplicates (a straggler holds the gang anyway)
+        self.g = R.JobGraph(p)
+        self.vids = []
+        for s in plan.stages:
+            self.g.add_stage(f"{s.id}:{s.name}", s.partitions, False, s.is_output)
+            self.vids.append([self.g.add_vertex(s.id, q) for q in range(s.partitions)])
+        for s in plan.stages:
+            for q in range(s.partitions):
+                for ii, si in enumerate(s.inputs):
+                    for src in self._sources(si, q):
+                        self.g.add_edge(self.vids[si.src][src], 0, self.vids[s.id][q], ii)
+
+    def owner(self, p: int) -> int:
+        return p % self.world.size
+
+    # ------------------------------------------------------------------ fused distributed OrderBy
+    def _find_fused_orderby(self):
+        """Plan idiom Sample -> Separators -> RangePartition -(cross)-> Merge+sort over one input X.
+        For fixed-width row tables it runs as ONE gang stage: the pooled in-place distributed sort
+        (ops/recordsort.distributed_sort_rows) with no intermediate table copies."""
+        st = self.plan.stages
+        out = {}
+        for m in st:
+            if len(m.inputs) != 1 or m.inputs[0].kind != "cross" or not m.ops or m.ops[0]["op"] != "sort":
+                continue
+            rp = st[m.inputs[0].src]
+            if len(rp.ops) != 1 or rp.ops[0]["op"] != "range_partition" or rp.ops[0].get("separators") is not None:
+                continue
+            if len(rp.inputs) != 2 or rp.inputs[0].kind != "pointwise" or rp.inputs[1].kind != "broadcast":
+                continue
+            sep = st[rp.inputs[1].src]
+            if len(sep.inputs) != 1 or sep.inputs[0].kind != "merge" or sep.ops[0]["op"] != "separators":
+                continue
+            samp = st[sep.inputs[0].src]
+            x = rp.inputs[0].src
+            if len(samp.inputs) != 1 or samp.inputs[0].src != x or samp.ops[0]["op"] != "sample" or len(samp.ops) != 1:
+                continue
+            if self.plan.consumers(samp.id) != [sep.id] or self.plan.consumers(sep.id) != [rp.id] or \
+                    self.plan.consumers(rp.id) != [m.id]:
+                continue
+            if rp.partitions != st[x].partitions or m.partitions != st[x].partitions:
+                continue
+            out[m.id] = dict(x=x, stages=[samp.id, sep.id, rp.id], key=m.ops[0]["key"],
+                             desc=m.ops[0].get("descending", False), comparer=m.ops[0].get("comparer"))
+        return out
+
+    def _fused_applicable(self, f) -> bool:
+        from ..gpu import trace as TR
+        ok = self.gpu_ok and f["comparer"] is None and self.plan.stages[f["x"]].partitions == self.world.size
+        spec = None
+        if ok:
+            t = self.channels.get((f["x"], self.world.rank))
+            ok = isinstance(t, DeviceTable) and t.rows is not None and (f["x"], self.world.rank) in self.row_sets
+            if ok:
+                try:
+                    kind, spec = TR.key_columns(TR.call(f["key"], t), t)
+                    ok = kind == "bytes" and spec.length <= 12 and not f["desc"]
+                except Exception:  # noqa: BLE001
+                    ok = False
+        votes = [None] * self.world.size
+        if self.world.size > 1:
+            dist.all_gather_object(votes, (bool(ok), None if spec is None else (spec.off, spec.length)))
+        else:
+            votes = [(bool(ok), None if spec is None else (spec.off, spec.length))]
+        if all(v[0] for v in votes) and len({v[1] for v in votes}) == 1:
+            f["spec"] = votes[0][1]
+            return True
+        return False
+
+    def _run_fused(self, m, f):
+        from ..ops import recordsort as RS
+        me = self.world.rank
+        t = self.channels[(f["x"], me)]
+        bs = self.row_sets[(f["x"], me)]
+        off, ln = f["spec"]
+        stats = RS.SortStats()
+        out = RS.distributed_sort_rows(bs.bufs, t.n, off, ln, self.world, stats=stats)
+        self.row_sets[(m.id, me)] = bs
+        self.last_sort_stats = stats
+        table = DeviceTable(out.shape[0], t.shape, rows=out)
+        # the rest of the merge stage's program after the sort
+        vctx = GpuVertexContext(me, m.partitions, self.vids[m.id][me], 0, m, self.dev, self.world, self)
+        data = table
+        for op in m.ops[1:]:
+            data = self._run_op(op, [data], vctx, m)
+        return data
+
+    def _sources(self, si, p):
+        src = self.plan.stages[si.src]
+        if si.kind == "pointwise":
+            return [p]
+        if si.kind == "offset":
+            q = p - si.offset
+            return [q] if 0 <= q < src.partitions else []
+        return list(range(src.partitions))
+
+    # ------------------------------------------------------------------ channel transport
+    def _port_of(self, si, val, dst_p):
+        """Port data of one source vertex's output for a destination partition."""
+        if si.kind == "cross":
+            if isinstance(val, Ported):
+                return val.port(dst_p)
+            return val[dst_p]
+        k = si.port
+        if isinstance(val, Ported):
+            return val.port(k)
+        if isinstance(val, list) and val and isinstance(val[0], list) and self.plan.stages[si.src].out_ports > 1:
+            return val[k]
+        return val
+
+    def _gather_inputs(self, s):
+        """Deliver every input channel of every local vertex of stage s (collectives included)."""
+        W, me = self.world.size, self.world.rank
+        local = [p for p in range(s.partitions) if self.owner(p) == me]
+        inputs = {p: [[] for _ in s.inputs] for p in local}
+        for ii, si in enumerate(s.inputs):
+            src_stage = self.plan.stages[si.src]
+            if si.kind == "cross" and W > 1:
+                got = self._exchange_cross(si, src_stage, s)
+                for p in local:
+                    inputs[p][ii] = got[p]
+                continue
+            # which (src q -> dst p) items cross ranks?
+            need_remote = False
+            for p in range(s.partitions):
+                for q in self._sources(si, p):
+                    if self.owner(q) != self.owner(p):
+                        need_remote = True
+            if not need_remote:
+                for p in local:
+                    inputs[p][ii] = [self._port_of(si, self.channels[(si.src, q)], p) for q in self._sources(si, p)]
+                continue
+            # generic path: every rank publishes the port data other ranks need (host objects or
+            # packed device rows) through one all_gather_object of descriptors + payloads
+            send = {}
+            for p in range(s.partitions):
+                for q in self._sources(si, p):
+                    if self.owner(q) == me and self.owner(p) != me:
+                        send[(q, p)] = self._portable(self._port_of(si, self.channels[(si.src, q)], p))
+            gathered = [None] * W
+            dist.all_gather_object(gathered, send)
+            for p in local:
+                lst = []
+                for q in self._sources(si, p):
+                    if self.owner(q) == me:
+                        lst.append(self._port_of(si, self.channels[(si.src, q)], p))
+                    else:
+                        lst.append(self._unportable(gathered[self.owner(q)][(q, p)]))
+                inputs[p][ii] = lst
+        return inputs
+
+    def _portable(self, x):
+        if isinstance(x, DeviceTable):
+            return ("dt", x.shape, {k: v.cpu() for k, v in x.cols.items()} if x.rows is None else None,
+                    x.rows.cpu() if x.rows is not None else None, x.n)
+        return ("obj", x)
+
+    def _unportable(self, x):
+        if x[0] == "dt":
+            _, shape, cols, rows, n = x
+            if rows is not None:
+                return DeviceTable(n, shape, rows=rows.to(self.dev))
+            return DeviceTable(n, shape, {k: v.to(self.dev) for k, v in cols.items()})
+        return x[1]
+
+    def _exchange_cross(self, si, src_stage, dst_stage):
+        """CrossProduct shuffle: one all-to-all-v of packed rows (RCCL over xGMI)."""
+        W, me = self.world.size, self.world.rank
+        P_src, P_dst = src_stage.partitions, dst_stage.partitions
+        local_src = [q for q in range(P_src) if self.owner(q) == me]
+        vals = {q: self.channels[(si.src, q)] for q in local_src}
+        device_ok = all(isinstance(v, Ported) for v in vals.values())
+        # agree on the transport (all device tables with one schema, else host objects)
+        sig = None
+        if device_ok and vals:
+            t0 = next(iter(vals.values())).table
+            sig = (t0.shape.kind, tuple(t0.shape.fields), t0.rows.shape[1] if t0.rows is not None else None,
+                   tuple((k, str(v.dtype)) for k, v in t0.cols.items()))
+        sigs = [None] * W
+        dist.all_gather_object(sigs, (device_ok, sig))
+        uniform = all(ok for ok, _ in sigs) and len({s for _, s in sigs if s is not None}) <= 1
+        local_dst = [p for p in range(P_dst) if self.owner(p) == me]
+        if not uniform:
+            send = {}
+            for q, v in vals.items():
+                for p in range(P_dst):
+                    if self.owner(p) != me:
+                        send[(q, p)] = _to_objects(self._port_of(si, v, p))
+            gathered = [None] * W
+            dist.all_gather_object(gathered, send)
+            out = {}
+            for p in local_dst:
+                out[p] = [(_to_objects(self._port_of(si, self.channels[(si.src, q)], p)) if self.owner(q) == me
+                           else gathered[self.owner(q)][(q, p)]) for q in range(P_src)]
+            return out
+        # counts matrix [P_src, P_dst] (rows), all-gathered
+        cnt = torch.zeros((P_src, P_dst), dtype=torch.int64)
+        for q, v in vals.items():
+            cnt[q] = torch.tensor([v.offsets[p + 1] - v.offsets[p] for p in range(P_dst)], dtype=torch.int64)
+        allc = cnt.clone()
+        shuffle.all_reduce_(allc, "sum", self.world)
+        proto = next(iter(vals.values())).table if vals else None
+        # pack: for each destination rank, for each local src q asc, for each dst p owned by it asc
+        pieces, send_counts = [], [0] * W
+        row_bytes = None
+        for r in range(W):
+            for q in local_src:
+                t = vals[q].table
+                packed = t.pack()
+                row_bytes = packed.shape[1]
+                for p in range(P_dst):
+                    if self.owner(p) != r:
+                        continue
+                    a, b = vals[q].offsets[p], vals[q].offsets[p + 1]
+                    if b > a:
+                        pieces.append(packed[a:b])
+                    send_counts[r] += (b - a)
+        if row_bytes is None:
+            row_bytes = 0
+        rb = [None] * W
+        dist.all_gather_object(rb, row_bytes)
+        row_bytes = max(x for x in rb if x is not None)
+        recv_counts = []
+        for r in range(W):
+            c = 0
+            for q in range(P_src):
+                if self.owner(q) != r:
+                    continue
+                for p in local_dst:
+                    c += int(allc[q, p])
+            recv_counts.append(c)
+        send = torch.cat(pieces) if pieces else torch.empty((0, row_bytes), dtype=torch.uint8, device=self.dev)
+        recv = torch.empty((sum(recv_counts), row_bytes), dtype=torch.uint8, device=self.dev)
+        shuffle.alltoallv_bytes(send.reshape(-1), [c * row_bytes for c in send_counts], recv.reshape(-1),
+                                [c * row_bytes for c in recv_counts], self.world)
+        if proto is None:
+            raise DryadLinqException(0, "rank without source partitions in a device shuffle")
+        # unpack into per-(q, p) slices
+        out = {p: [None] * P_src for p in local_dst}
+        off = 0
+        for r in range(W):
+            for q in range(P_src):
+                if self.owner(q) != r:
+                    continue
+                for p in local_dst:
+                    c = int(allc[q, p])
+                    out[p][q] = proto.unpack_like(recv[off:off + c], c)
+                    off += c
+        return out
+
+    # ------------------------------------------------------------------ vertex execution
+    def _fault(self, s, p, version):
+        for f in self.faults:
+            if f.get("stage") not in (None, s.id, s.name) or f.get("partition") not in (None, p):
+                continue
+            if f.get("version") not in (None, version):
+                continue
+            return f.get("kind", "fail")
+        return None
+
+    def _merge_streams(self, si, streams):
+        if not streams:
+            return None
+        if all(isinstance(x, DeviceTable) for x in streams):
+            return DeviceTable.concat(streams)
+        objs = [x if isinstance(x, list) else _to_objects(x) for x in streams]
+        return [y for o in objs for y in o]
+
+    def run_vertex(self, s, p, version, raw_inputs):
+        fault = self._fault(s, p, version)
+        if fault == "fail":
+            raise RuntimeError(f"injected vertex failure {s.name}[{p}] v{version}")
+        vctx = GpuVertexContext(p, s.partitions, self.vids[s.id][p], version, s, self.dev, self.world, self)
+        inputs = [self._merge_streams(si, streams) for si, streams in zip(s.inputs, raw_inputs)]
+        data = None
+        for i, op in enumerate(s.ops):
+            args = inputs if i == 0 else [data]
+            data = self._run_op(op, args, vctx, s)
+        return data
+
+    def _run_op(self, op, args, vctx, s):
+        name = op["op"]
+        fn = G.OPS.get(name) if self.gpu_ok else None
+        if fn is not None and all(a is None or isinstance(a, DeviceTable) for a in args):
+            try:
+                return fn(op, [a for a in args] if args else [], vctx)
+            except NotTraceable as e:
+                self.fallbacks.append((s.name, name, str(e)))
+        elif fn is None or not self.gpu_ok:
+            self.fallbacks.append((s.name, name, "host op"))
+        objs = [(_to_objects(a) if not isinstance(a, list) else a) if a is not None else [] for a in args]
+        out = V.OPS[name](op, objs, vctx)
+        return self._maybe_device(out, s, name)
+
+    def _maybe_device(self, out, s, opname):
+        """Host op result -> device table when the records are columnar (keeps later ops on GPU)."""
+        if not self.gpu_ok or not isinstance(out, list) or not out:
+            return out
+        if isinstance(out[0], list):           # multi-port host output
+            return out
+        try:
+            t = from_objects(out, None, self.dev)
+        except Exception:  # noqa: BLE001
+            t = None
+        return t if t is not None else out
+
+    # ------------------------------------------------------------------ main loop
+    def run(self):
+        g = self.g
+        W, me = self.world.size, self.world.rank
+        t_start = time.time()
+        now = lambda: time.time() - t_start  # noqa: E731
+        g.start(now())
+        ready = {}
+
+        def refresh():
+            for it in g.take_ready(1 << 30, now()):
+                ready[it.vertex] = it.version
+
+        self.fused = self._find_fused_orderby()
+        fused_first = {f["stages"][0]: mid for mid, f in self.fused.items()}
+        active_fused = {}
+        for s in self.plan.stages:
+            t0 = time.time()
+            status, err = 0, ""
+            if s.id in fused_first:
+                mid = fused_first[s.id]
+                if self._fused_applicable(self.fused[mid]):
+                    active_fused[mid] = self.fused[mid]
+                    self.skipped.update(self.fused[mid]["stages"])
+            if s.id in self.skipped:
+                refresh()
+                for p in range(s.partitions):
+                    vid = self.vids[s.id][p]
+                    ver = ready.pop(vid)
+                    g.on_running(vid, ver, self.owner(p), now())
+                    g.on_completed(vid, ver, now(), 0, 0)
+                self.timings[f"{s.id}:{s.name}(fused)"] = 0.0
+                continue
+            if s.id in active_fused:
+                refresh()
+                vid = self.vids[s.id][me]
+                ver = ready.pop(vid)
+                g.on_running(vid, ver, me, now())
+                out = self._run_fused(s, active_fused[s.id])
+                self.channels[(s.id, me)] = out
+                g.on_completed(vid, ver, now(), 0, _object_bytes(out))
+                for p in range(s.partitions):
+                    if p != me:
+                        v2 = self.vids[s.id][p]
+                        ver2 = ready.pop(v2)
+                        g.on_running(v2, ver2, self.owner(p), now())
+                        g.on_completed(v2, ver2, now(), 0, 0)
+                self._release(s)
+                if self.gpu_ok:
+                    torch.cuda.synchronize(self.dev)
+                self.timings[f"{s.id}:{s.name}(fused OrderBy)"] = time.time() - t0
+                continue
+            raw = self._gather_inputs(s)
+            refresh()
+            for p in sorted(raw):
+                vid = self.vids[s.id][p]
+                while True:
+                    ver = ready.pop(vid)
+                    g.on_running(vid, ver, me, now())
+                    try:
+                        out = self.run_vertex(s, p, ver, raw[p])
+                        self.channels[(s.id, p)] = out if out is not None else []
+                        g.on_completed(vid, ver, now(), 0, _object_bytes(out))
+                        break
+                    except Exception as e:  # noqa: BLE001
+                        g.on_failed(vid, ver, now(), -1, f"{type(e).__name__}: {e}")
+                        self._last_exc = e
+                        if g.failed():
+                            status, err = 1, g.failure()
+                            break
+                        refresh()
+                        log.warning("vertex %s[%d] v%d failed, re-executing: %s", s.name, p, ver, e)
+                if status:
+                    break
+            # stage barrier: every rank learns whether a vertex of the stage failed for good
+            st = torch.tensor([status], dtype=torch.int64,
+                              device=self.dev if self.world.backend == "nccl" else "cpu")
+            shuffle.all_reduce_(st, "max", self.world)
+            if int(st.item()) != 0:
+                raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed,
+                                            err or f"job aborted: a vertex of stage {s.name} failed on another rank",
+                                            inner=getattr(self, "_last_exc", None))
+            for p in range(s.partitions):          # replicate remote completions into the local graph
+                if self.owner(p) != me:
+                    vid = self.vids[s.id][p]
+                    ver = ready.pop(vid)
+                    g.on_running(vid, ver, self.owner(p), now())
+                    g.on_completed(vid, ver, now(), 0, 0)
+            self._release(s)
+            if self.gpu_ok:
+                torch.cuda.synchronize(self.dev)
+            self.timings[f"{s.id}:{s.name}"] = time.time() - t0
+        committed = self._commit()
+        if self.pool is not None:
+            for b in set(self.row_sets.values()):
+                self.pool.release(b)
+        return dict(committed=committed, fallbacks=self.fallbacks, timings=self.timings,
+                    statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()])
+
+    def _release(self, s):
+        later = {i.src for st in self.plan.stages if st.id > s.id for i in st.inputs}
+        later |= {f["x"] for mid, f in self.fused.items() if mid > s.id}
+        for (sid, p) in list(self.channels):
+            if sid <= s.id and sid not in later and not self.plan.stages[sid].is_output:
+                del self.channels[(sid, p)]
+
+    # ------------------------------------------------------------------ outputs
+    def _commit(self):
+        W, me = self.world.size, self.world.rank
+        committed = {}
+        for s in self.plan.stages:
+            if not s.is_output:
+                continue
+            uri = s.output["uri"]
+            scheme, path, _ = parse_uri(uri)
+            local = {p: self.channels[(s.id, p)] for p in range(s.partitions) if self.owner(p) == me}
+            if scheme == "hbm":
+                tabs = {p: (v if isinstance(v, DeviceTable) else v) for p, v in local.items()}
+                pins = [self.row_sets[(s.id, p)] for p in local if (s.id, p) in self.row_sets]
+                for b in pins:
+                    self.pool.pin(b)
+                provider_for(uri).put(uri, {"dtype": s.dtype, "partitions": s.partitions, "local": tabs,
+                                            "owner_of": {p: self.owner(p) for p in range(s.partitions)},
+                                            "bytes": sum(_object_bytes(v) for v in tabs.values()),
+                                            "pins": pins, "pool": self.pool})
+                committed[uri] = s.partitions
+            else:
+                # host stores: every rank ships its partitions' records to rank 0, which writes them
+                objs = {p: _to_objects(v) if not isinstance(v, list) else v for p, v in local.items()}
+                gathered = [None] * W
+                if W > 1:
+                    dist.all_gather_object(gathered, objs)
+                else:
+                    gathered = [objs]
+                if me == 0:
+                    parts = {}
+                    for d in gathered:
+                        parts.update(d)
+                    ordered = [parts[p] for p in range(s.partitions)]
+                    prov = provider_for(uri)
+                    if prov.exists(uri):
+                        if s.output.get("delete_if_exists") or s.output.get("temp"):
+                            prov.delete(uri)
+                        else:
+                            raise DryadLinqException(ErrorCode.JobToCreateTableFailed, f"output {uri} exists")
+                    from .. import types as T
+                    dt = s.dtype
+                    if dt is None or dt == T.Pickle:
+                        flat = [x for part in ordered for x in part[:100]]
+                        dt = T.infer_common_type(flat) if flat else T.Int32
+                    prov.write_table(uri, ordered, dt)
+                if W > 1:
+                    self.world.barrier()
+                committed[uri] = s.partitions
+            qn = s.output.get("qnode")
+            if qn is not None:
+                qn.args["_executed"] = True
+        return committed
+
+
+class GpuExecutor(_BaseExecutor):
+    def __init__(self, ctx):
+        self.ctx = ctx
+        w = get_world()
+        if w.size == 1 and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            w = init_world(device=ctx._props.get("Device"))             # launched by torchrun
+        elif w.size == 1 and w.device.type == "cpu" and torch.cuda.is_available() \
+                and ctx._props.get("Device", "cuda") != "cpu":
+            w = World(0, 1, 0, torch.device("cuda", torch.cuda.current_device()), None)
+        self.world = w
+        self.last_result = None
+        from ..gpu.pool import HbmPool
+        self.pool = HbmPool(w.device) if w.device.type == "cuda" else None
+
+    def run_job(self, outs, handle):
+        plan = compile_queries(self.ctx, outs)
+        faults = self.ctx._props.get("FaultInjection") or []
+        for st in plan.stages:      # CheckExistence(deleteIfExists) at submission
+            if st.is_output and st.output["uri"].startswith("hbm://"):
+                prov = provider_for(st.output["uri"])
+                if prov.exists(st.output["uri"]):
+                    if st.output.get("delete_if_exists") or st.output.get("temp"):
+                        prov.delete(st.output["uri"])
+                    else:
+                        raise DryadLinqException(ErrorCode.JobToCreateTableFailed,
+                                                 f"output {st.output['uri']} already exists")
+        runner = GpuJobRunner(self.ctx, plan, self.world, faults, self.pool)
+        res = runner.run()
+        self.last_result = res
+        self.last_plan = plan
+        if handle is not None:
+            handle.events.extend(res["events"])
+        return res
+
+    def enumerate(self, q):
+        node = q.node
+        if node.op == "ToStore" and node.args.get("_executed"):
+            uri = node.args["uri"]
+            return self._read_back(uri, node.dtype)
+        if node.op == "ToStore":
+            self.ctx.SubmitAndWait(q)
+            return self._read_back(node.args["uri"], node.dtype)
+        from ..io.providers import unique_name
+        tmp = "hbm://" + unique_name("enum")
+        st = q.ToStore(tmp)
+        st.node.args["_temp"] = True
+        self.run_job([st], None)
+        try:
+            return self._read_back(tmp, st.node.dtype)
+        finally:
+            provider_for(tmp).delete(tmp)
+
+    def _read_back(self, uri, dtype):
+        if not uri.startswith("hbm://"):
+            return list(provider_for(uri).read_all(uri, dtype))
+        ent = provider_for(uri).get(uri)
+        mine = {p: _to_objects(v) if not isinstance(v, list) else v for p, v in ent["local"].items()}
+        W = self.world.size
+        if W > 1:
+            gathered = [None] * W
+            dist.all_gather_object(gathered, mine)
+            allp = {}
+            for d in gathered:
+                allp.update(d)
+        else:
+            allp = mine
+        return [x for p in range(ent["partitions"]) for x in allp.get(p, [])]
+
+    def close(self):
+        pass

@@ -1,0 +1,28 @@
+"""Multi-process SPMD execution of the GPU executor's distributed path on CPU (gloo, 2 ranks)."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("ranks,parts", [(2, 2), (2, 3)])
+def test_spmd_gloo(ranks, parts):
+    env = dict(os.environ, SPMD_DEVICE="cpu", SPMD_PARTS=str(parts), PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tests", "dist", "spmd_queries.py")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "SPMD_OK" in r.stdout
