@@ -198,10 +198,29 @@ def op_offsets(op, inputs, v):
 
 # ---------------------------------------------------------------------------------------------
 # sorting / partitioning
+def _pooled_set(t: DeviceTable, v):
+    """The executor's pooled buffer set whose rows_in holds this row table (or None)."""
+    r = getattr(v, "runner", None)
+    if r is None or t.rows is None:
+        return None
+    bs = r.row_sets.get((v.stage.id, v.partition))
+    if bs is not None and t.rows.data_ptr() == bs.bufs.rows_in.data_ptr():
+        return bs
+    return None
+
+
 def op_sort(op, inputs, v):
     t = _check(_one(inputs))
     if t.n <= 1:
         return t
+    bs = _pooled_set(t, v)
+    if bs is not None and op.get("comparer") is None:
+        # in-place key-pointer sort of pooled rows: rows_in -> rows_out, entries in the pool
+        kind, spec = TR.key_columns(TR.call(op["key"], t), t)
+        if kind == "bytes" and spec.length <= 12:
+            out = RS.local_sort_rows(t.rows, bs.bufs.rows_out, bs.bufs.ent_a, bs.bufs.ent_b, spec.off, spec.length,
+                                     descending=op.get("descending", False))
+            return DeviceTable(out.shape[0], t.shape, rows=out)
     _, perm, _ = sort_perm(t, op["key"], op.get("comparer"), op.get("descending", False))
     return t.take(perm)
 

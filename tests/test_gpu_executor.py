@@ -88,6 +88,13 @@ def test_terasort_query_fused_path():
     job.step()
     v = job.validate(*expect)
     assert v["ok"], v
-    assert any("fused OrderBy" in k for k in job.executor_report()["timings"])
+    assert "sort" not in {op for _, op, _ in job.executor_report()["fallbacks"]}
     job.step()                     # buffers are reused across jobs
     assert job.validate(*expect)["ok"]
+
+
+def test_fused_orderby_two_partitions_one_rank():
+    # two partitions on one rank: the planner emits the sampled range-partition shuffle
+    c = _ctx(2)
+    data = list(range(100_000, 0, -3))
+    assert list(c.FromEnumerable(data).OrderBy(lambda x: x)) == sorted(data)
