@@ -15,12 +15,14 @@
 //                written contiguously (coalesced 16-byte stores), stable across tiles/blocks.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int kRadixBits = 8;
 constexpr int kBins = 1 << kRadixBits;
-constexpr int kItems = 8;                  // entries per thread per tile
-constexpr int kTile = kBlock * kItems;     // 2048 entries per tile
+constexpr int kItems = 8;                  // default entries per thread per tile
+constexpr int kTile = kBlock * kItems;     // 2048 entries per tile (default geometry)
 constexpr int kMaxGrid = 1024;             // workgroups for count/scatter (4 per CU)
 constexpr int kScanChunk = 4096;           // elements per scan workgroup (16 per thread)
 
@@ -98,11 +100,14 @@ __global__ __launch_bounds__(256) void rs_scan_down(uint32_t* __restrict__ a, ui
   }
 }
 
+template <int ITEMS>
 __global__ __launch_bounds__(256) void rs_scatter(const E128* __restrict__ in, E128* __restrict__ out,
                                                   uint64_t n, int shift,
                                                   const uint32_t* __restrict__ offsets, uint32_t G,
                                                   uint64_t per_block) {
-  __shared__ E128 stage[kTile];          // 32 KiB
+  constexpr int kItems = ITEMS;
+  constexpr int kTile = kBlock * ITEMS;
+  __shared__ E128 stage[kTile];          // 32 KiB (ITEMS=8) / 64 KiB (ITEMS=16)
   __shared__ uint32_t wcnt[4][kBins];    // per-wave digit counters, later wave prefixes
   __shared__ uint32_t goff[kBins];       // running global output offset of each digit
   __shared__ uint32_t bstart[kBins];     // in-tile start of each digit
@@ -166,6 +171,86 @@ __global__ __launch_bounds__(256) void rs_scatter(const E128* __restrict__ in, E
   }
 }
 
+// v2: all of a tile's loads are issued back to back and the NEXT tile is prefetched into
+// registers while the current one is ranked and staged (software pipelining across tiles), so a
+// workgroup's global-load latency overlaps its LDS ranking / scatter work.
+template <int ITEMS>
+__global__ __launch_bounds__(256) void rs_scatter_v2(const E128* __restrict__ in, E128* __restrict__ out,
+                                                     uint64_t n, int shift,
+                                                     const uint32_t* __restrict__ offsets, uint32_t G,
+                                                     uint64_t per_block) {
+  constexpr int kTile = kBlock * ITEMS;
+  __shared__ E128 stage[kTile];
+  __shared__ uint32_t wcnt[4][kBins];
+  __shared__ uint32_t goff[kBins];
+  __shared__ uint32_t bstart[kBins];
+  __shared__ uint32_t sc[4];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  goff[t] = offsets[(uint64_t)t * G + blockIdx.x];
+  const uint64_t beg = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  E128 cur[ITEMS], nxt[ITEMS];
+  auto load_tile = [&](uint64_t base, E128* dst) {
+    const uint32_t c = (uint32_t)((end - base) < (uint64_t)kTile ? (end - base) : kTile);
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+      if (pos < c) dst[r] = in[base + pos];
+    }
+  };
+  if (beg < end) load_tile(beg, cur);
+  for (uint64_t base = beg; base < end; base += kTile) {
+    const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kTile ? (end - base) : kTile);
+    if (base + kTile < end) load_tile(base + kTile, nxt);
+    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    __syncthreads();
+    uint32_t rk[ITEMS], dg[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+      const bool valid = pos < cnt;
+      const uint32_t d = valid ? digit_of(cur[r], shift) : 0u;
+      uint64_t peers = ballot64(valid);
+#pragma unroll
+      for (int k = 0; k < kRadixBits; ++k) {
+        const bool bit = (d >> k) & 1u;
+        const uint64_t b = ballot64(bit);
+        peers &= bit ? b : ~b;
+      }
+      const uint32_t below = popc_below(peers);
+      const uint32_t prior = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      rk[r] = prior + below;
+      dg[r] = d;
+    }
+    __syncthreads();
+    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
+    uint32_t all;
+    bstart[t] = block_exclusive_scan256(tot, sc, all);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+      if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (uint32_t j = t; j < cnt; j += kBlock) {
+      const E128 v = stage[j];
+      const uint32_t d = digit_of(v, shift);
+      out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+    }
+    __syncthreads();
+    goff[t] += tot;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) cur[r] = nxt[r];
+  }
+}
+
 void scan_inplace(uint32_t* a, uint32_t M, uint32_t* partial, hipStream_t s) {
   const uint32_t S = (M + kScanChunk - 1) / kScanChunk;
   rs_scan_reduce<<<S, 256, 0, s>>>(a, M, partial);
@@ -173,14 +258,50 @@ void scan_inplace(uint32_t* a, uint32_t M, uint32_t* partial, hipStream_t s) {
   rs_scan_down<<<S, 256, 0, s>>>(a, M, partial);
 }
 
+int g_items = 0;   // 0 = not initialised; set from DRYAD_SORT_ITEMS or dr_sort_set_items
+
+inline int sort_items() {
+  if (g_items == 0) {
+    const char* e = getenv("DRYAD_SORT_ITEMS");
+    g_items = (e && atoi(e) == 16) ? 16 : 8;
+  }
+  return g_items;
+}
+
 inline void sort_geometry(uint64_t n, uint32_t& G, uint64_t& per_block) {
-  uint64_t tiles = (n + kTile - 1) / kTile;
+  const uint64_t tile = (uint64_t)kBlock * sort_items();
+  uint64_t tiles = (n + tile - 1) / tile;
   if (tiles < 1) tiles = 1;
-  G = (uint32_t)(tiles < (uint64_t)kMaxGrid ? tiles : (uint64_t)kMaxGrid);
-  per_block = ((tiles + G - 1) / G) * kTile;
+  const uint64_t maxg = sort_items() == 16 ? kMaxGrid / 2 : kMaxGrid;
+  G = (uint32_t)(tiles < maxg ? tiles : maxg);
+  per_block = ((tiles + G - 1) / G) * tile;
+}
+
+int g_scatter_v2 = -1;
+
+void launch_scatter(const E128* in, E128* out, uint64_t n, int shift, const uint32_t* offsets, uint32_t G,
+                    uint64_t per_block, hipStream_t s) {
+  if (g_scatter_v2 < 0) {
+    const char* e = getenv("DRYAD_SCATTER_V2");
+    g_scatter_v2 = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  if (g_scatter_v2) {
+    if (sort_items() == 16)
+      rs_scatter_v2<16><<<G, 256, 0, s>>>(in, out, n, shift, offsets, G, per_block);
+    else
+      rs_scatter_v2<8><<<G, 256, 0, s>>>(in, out, n, shift, offsets, G, per_block);
+    return;
+  }
+  if (sort_items() == 16)
+    rs_scatter<16><<<G, 256, 0, s>>>(in, out, n, shift, offsets, G, per_block);
+  else
+    rs_scatter<8><<<G, 256, 0, s>>>(in, out, n, shift, offsets, G, per_block);
 }
 
 }  // namespace
+
+DR_API void dr_sort_set_items(int items) { g_items = (items == 16) ? 16 : 8; }
+DR_API void dr_sort_set_scatter_v2(int on) { g_scatter_v2 = on ? 1 : 0; }
 
 // Workspace needed by dr_sort_u128 (bytes).
 DR_API uint64_t dr_sort_u128_workspace(uint64_t n) {
@@ -209,7 +330,7 @@ DR_API int dr_sort_u128(E128* keys, E128* tmp, uint64_t n, int begin_bit, int en
   for (int shift = begin_bit; shift < end_bit; shift += kRadixBits) {
     rs_count<<<G, 256, 0, s>>>(src, n, shift, counts, G, per_block);
     scan_inplace(counts, kBins * G, partial, s);
-    rs_scatter<<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+    launch_scatter(src, dst, n, shift, counts, G, per_block, s);
     E128* x = src; src = dst; dst = x;
     flips ^= 1;
   }
@@ -246,7 +367,7 @@ DR_API int dr_partition_pass_u128(const E128* in, E128* out, uint64_t n, int shi
   rs_count<<<G, 256, 0, s>>>(in, n, shift, counts, G, per_block);
   scan_inplace(counts, kBins * G, partial, s);
   rs_digit_totals<<<1, kBins, 0, s>>>(counts, G, n, digit_starts);
-  rs_scatter<<<G, 256, 0, s>>>(in, out, n, shift, counts, G, per_block);
+  launch_scatter(in, out, n, shift, counts, G, per_block, s);
   DR_LAUNCH_CHECK();
   return 0;
 }
@@ -362,8 +483,81 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const uint32_t* __rest
 }
 }  // namespace
 
+// 16-byte vectorised gather for a compile-time stride S (multiple of 4): each output uint4 chunk
+// is read from one source row (or stitched from two adjacent output rows' sources) and written
+// with one 16-byte store; ~4x fewer memory instructions than the dword path.
+namespace {
+__device__ __forceinline__ uint4 load16_a4(const uint8_t* p) {
+  uint4 v;
+  __builtin_memcpy(&v, __builtin_assume_aligned(p, 4), 16);
+  return v;
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void gather_rows_v4_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                             const E128* __restrict__ ent,
+                                                             const int64_t* __restrict__ idx64, uint64_t n) {
+  static_assert(S % 4 == 0, "stride must be a multiple of 4");
+  __shared__ uint64_t sidx[257];
+  const int t = threadIdx.x;
+  for (uint64_t row0 = (uint64_t)blockIdx.x * 256; row0 < n; row0 += (uint64_t)gridDim.x * 256) {
+    const uint32_t rows = (uint32_t)((n - row0) < 256 ? (n - row0) : 256);
+    if (t < (int)rows) sidx[t] = ent ? (uint64_t)(uint32_t)ent[row0 + t].lo : (uint64_t)idx64[row0 + t];
+    __syncthreads();
+    if (rows == 256) {
+      constexpr uint32_t chunks = 256 * S / 16;
+      uint4* o = reinterpret_cast<uint4*>(out + row0 * S);
+      for (uint32_t c = t; c < chunks; c += 256) {
+        const uint32_t b = 16 * c;
+        const uint32_t r = b / S, off = b - r * S;
+        const uint8_t* src = in + sidx[r] * S + off;
+        uint4 v;
+        if (off + 16 <= S) {
+          v = load16_a4(src);
+        } else {
+          uint32_t w[4];
+          const uint32_t k1 = (S - off) / 4;
+          const uint32_t* a = reinterpret_cast<const uint32_t*>(src);
+          const uint32_t* bnext = reinterpret_cast<const uint32_t*>(in + sidx[r + 1] * S);
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) w[k] = k < k1 ? a[k] : bnext[k - k1];
+          v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        o[c] = v;
+      }
+    } else {
+      const uint32_t W = S / 4;
+      const uint32_t words = rows * W;
+      const uint32_t* inw = reinterpret_cast<const uint32_t*>(in);
+      uint32_t* o = reinterpret_cast<uint32_t*>(out) + row0 * W;
+      for (uint32_t j = t; j < words; j += 256) {
+        const uint32_t r = j / W, c = j - r * W;
+        o[j] = inw[sidx[r] * W + c];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+int g_gather_v4 = -1;
+inline bool gather_v4_enabled() {
+  if (g_gather_v4 < 0) {
+    const char* e = getenv("DRYAD_GATHER_V4");
+    g_gather_v4 = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return g_gather_v4 == 1;
+}
+}  // namespace
+
+DR_API void dr_gather_set_v4(int on) { g_gather_v4 = on ? 1 : 0; }
+
 DR_API int dr_gather_rows(const uint8_t* rows, uint8_t* out, const E128* entries, const int64_t* idx,
                           uint64_t n, uint32_t stride, hipStream_t s) {
+  if (stride == 100 && gather_v4_enabled() && n > 0 && (((uintptr_t)out) & 15) == 0) {
+    gather_rows_v4_kernel<100><<<grid_for(n, 256, 16384), 256, 0, s>>>(rows, out, entries, idx, n);
+    DR_LAUNCH_CHECK();
+    return 0;
+  }
   if (stride == 0 || (stride & 3)) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
   const uint32_t W = stride / 4;
@@ -418,6 +612,46 @@ DR_API int dr_range_dest_u128(const E128* in, E128* out, uint64_t n, const E128*
   if (nsep > 255) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
   range_dest_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(in, out, n, seps, nsep, lo_mask, descending);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Prefix sort + tie fix-up: after a stable sort on hi only (64 key bits), runs of equal hi are
+// re-ordered by the full lo word (remaining key bytes, then row index = stable order) by one
+// thread per run.  Random keys (TeraSort) have essentially no such runs, saving two radix passes
+// for 10-byte keys; a run longer than `max_run` sets *overflow so the caller falls back to the
+// full-width sort.
+namespace {
+__global__ __launch_bounds__(256) void tie_fixup_kernel(E128* __restrict__ e, uint64_t n, uint32_t max_run,
+                                                        uint32_t* __restrict__ overflow) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t h = e[i].hi;
+    if (e[i + 1].hi != h) continue;
+    if (i > 0 && e[i - 1].hi == h) continue;   // not the run start
+    uint64_t j = i + 1;
+    while (j + 1 < n && e[j + 1].hi == h && j - i < max_run) ++j;
+    if (j - i >= max_run) {
+      atomicOr(overflow, 1u);
+      continue;
+    }
+    for (uint64_t a = i + 1; a <= j; ++a) {   // insertion sort by lo
+      const E128 x = e[a];
+      uint64_t b = a;
+      while (b > i && e[b - 1].lo > x.lo) {
+        e[b] = e[b - 1];
+        --b;
+      }
+      e[b] = x;
+    }
+  }
+}
+}  // namespace
+
+DR_API int dr_tie_fixup(E128* e, uint64_t n, uint32_t max_run, uint32_t* overflow, hipStream_t s) {
+  if (n < 2) return 0;
+  tie_fixup_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(e, n, max_run, overflow);
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -26,6 +26,9 @@ import torch
 from ..parallel.comm import World, get_world
 from ..parallel import shuffle
 from . import sort as S
+import os as _os
+
+PREFIX_SORT = _os.environ.get("DRYAD_PREFIX_SORT", "1") == "1"
 
 
 def key_bits(key_len: int) -> tuple[int, int, int]:
@@ -85,7 +88,10 @@ def local_sort_rows(rows: torch.Tensor, out: torch.Tensor, ent_a: torch.Tensor, 
             e[:, 0].bitwise_xor_(torch.tensor(lo_mask - (1 << 64) if lo_mask >= (1 << 63) else lo_mask,
                                               dtype=torch.int64, device=e.device))
     b0, b1, _ = key_bits(key_len)
-    srt = S.sort_entries(e, b0, b1, tmp=ent_b[:n])
+    if PREFIX_SORT and b0 < 64:
+        srt = S.sort_entries_prefix(e, b0, tmp=ent_b[:n])
+    else:
+        srt = S.sort_entries(e, b0, b1, tmp=ent_b[:n])
     return S.gather_rows(rows, entries=srt, out=out[:n])
 
 

@@ -12,7 +12,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import c_u32, c_u64, ptr, stream_of
+from ._lib import c_u32, c_u64, ptr, stream_of  # noqa: F401
 
 _WS_CACHE: dict = {}
 
@@ -50,6 +50,46 @@ def sort_entries(entries: torch.Tensor, begin_bit: int, end_bit: int,
     _lib.call("dr_sort_u128", ptr(entries), ptr(tmp), c_u64(n), begin_bit, end_bit, ptr(ws),
               stream_of(entries), ctypes.byref(flag))
     return tmp[:n] if flag.value else entries
+
+
+def tie_fixup(entries: torch.Tensor, max_run: int = 4096) -> bool:
+    """Re-order runs of equal ``hi`` by ``lo`` (see dr_tie_fixup).  Returns False on overflow."""
+    flag = torch.zeros(1, dtype=torch.int32, device=entries.device)
+    _lib.call("dr_tie_fixup", ptr(entries), c_u64(entries.shape[0]), c_u32(max_run), ptr(flag), stream_of(entries))
+    return int(flag.item()) == 0
+
+
+def sort_entries_prefix(entries: torch.Tensor, begin_bit: int, tmp: torch.Tensor | None = None) -> torch.Tensor:
+    """Sort on composite bits [begin_bit, 128) by sorting hi (bits 64..127) and fixing ties on lo.
+
+    Equivalent to ``sort_entries(entries, begin_bit, 128)`` (stable), two passes cheaper for
+    keys with 9-12 bytes when the first 8 key bytes are mostly distinct; falls back to the full
+    sort when long runs of equal prefixes exist."""
+    if begin_bit >= 64:
+        return sort_entries(entries, begin_bit, 128, tmp)
+    if tmp is None:
+        tmp = torch.empty_like(entries)
+    backup = None
+    srt = sort_entries(entries, 64, 128, tmp)
+    if tie_fixup(srt):
+        return srt
+    # long equal-prefix runs: redo with the full key width from the (now prefix-sorted) entries;
+    # a stable LSD sort over [begin_bit, 64) then [64, 128) restores the exact order
+    other = tmp if srt is entries else entries
+    out = sort_entries(srt, begin_bit, 64, other[: srt.shape[0]])
+    return sort_entries(out, 64, 128, (srt if out is not srt else other)[: srt.shape[0]])
+
+
+def set_sort_items(items: int):
+    _lib.lib().dr_sort_set_items(int(items))
+
+
+def set_scatter_v2(on: bool):
+    _lib.lib().dr_sort_set_scatter_v2(int(bool(on)))
+
+
+def set_gather_v4(on: bool):
+    _lib.lib().dr_gather_set_v4(int(bool(on)))
 
 
 def partition_pass(entries: torch.Tensor, shift: int, out: torch.Tensor | None = None):

@@ -138,3 +138,50 @@ def test_local_sort_descending():
     src = rows.cpu().numpy()
     order = sorted(range(n), key=lambda i: (bytes(255 - x for x in src[i, 2:11]), i))
     np.testing.assert_array_equal(got, src[order])
+
+
+@pytest.mark.parametrize("dup", [False, True])
+def test_prefix_sort_with_tie_fixup_matches_full_sort(dup):
+    from dryad_amd.ops import sort as S
+    n = 400_000
+    e = torch.randint(-2**63, 2**63 - 1, (n, 2), dtype=torch.int64, device="cuda")
+    if dup:   # long runs of equal 64-bit prefixes force the fallback path
+        e[:, 1] = torch.randint(0, 3, (n,), device="cuda")
+    else:     # a few short ties
+        e[: n // 100, 1] = e[n // 100: 2 * (n // 100), 1]
+    e[:, 0] = (e[:, 0] & ~0xFFFFFFFF) | torch.arange(n, device="cuda")
+    full = S.sort_entries(e.clone(), 32, 128).cpu().numpy()
+    pre = S.sort_entries_prefix(e.clone(), 32).cpu().numpy()
+    np.testing.assert_array_equal(pre, full)
+
+
+def test_sort_tile16_and_gather_v4_variants():
+    from dryad_amd.ops import sort as S
+    n = 300_001
+    e = torch.randint(-2**63, 2**63 - 1, (n, 2), dtype=torch.int64, device="cuda")
+    ref = S.sort_entries(e.clone(), 0, 128).cpu().numpy()
+    S.set_sort_items(16)
+    try:
+        np.testing.assert_array_equal(S.sort_entries(e.clone(), 0, 128).cpu().numpy(), ref)
+    finally:
+        S.set_sort_items(8)
+    rows = torch.randint(0, 256, (n, 100), dtype=torch.uint8, device="cuda")
+    perm = torch.randperm(n, device="cuda")
+    S.set_gather_v4(True)
+    a = S.gather_rows(rows, index=perm)
+    S.set_gather_v4(False)
+    b = S.gather_rows(rows, index=perm)
+    S.set_gather_v4(True)
+    assert torch.equal(a, rows[perm]) and torch.equal(a, b)
+
+
+def test_scatter_v1_v2_agree():
+    from dryad_amd.ops import sort as S
+    n = 250_003
+    e = torch.randint(-2**63, 2**63 - 1, (n, 2), dtype=torch.int64, device="cuda")
+    S.set_scatter_v2(False)
+    a = S.sort_entries(e.clone(), 0, 128).cpu().numpy()
+    S.set_scatter_v2(True)
+    b = S.sort_entries(e.clone(), 0, 128).cpu().numpy()
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(a, e.cpu().numpy()[_ref_order(e)])
