@@ -318,7 +318,11 @@ DR_API int dr_sort_u128(E128* keys, E128* tmp, uint64_t n, int begin_bit, int en
                         hipStream_t s, int* result_in_tmp) {
   *result_in_tmp = 0;
   if (n == 0 || begin_bit >= end_bit) return 0;
-  if ((begin_bit & 7) || (end_bit & 7) || end_bit > 128 || begin_bit < 0) return (int)hipErrorInvalidValue;
+  // passes are 8-bit digits at begin_bit, begin_bit + 8, ...; a digit may not straddle lo/hi, so
+  // unaligned ranges must lie inside hi (the caller guarantees the bits above end_bit are constant
+  // when (end_bit - begin_bit) is not a multiple of 8 or end_bit is unaligned)
+  if (end_bit > 128 || begin_bit < 0 || ((end_bit - begin_bit) & 7)) return (int)hipErrorInvalidValue;
+  if ((begin_bit & 7) && begin_bit < 64) return (int)hipErrorInvalidValue;
   if (n >= (1ull << 32)) return (int)hipErrorInvalidValue;
   uint32_t G; uint64_t per_block;
   sort_geometry(n, G, per_block);
@@ -652,6 +656,166 @@ __global__ __launch_bounds__(256) void tie_fixup_kernel(E128* __restrict__ e, ui
 DR_API int dr_tie_fixup(E128* e, uint64_t n, uint32_t max_run, uint32_t* overflow, hipStream_t s) {
   if (n < 2) return 0;
   tie_fixup_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(e, n, max_run, overflow);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Hybrid sort, phase 2: segmented in-LDS sort of runs.  After a stable LSD sort on only the top
+// window of varying key bits (3 passes for ~1e9 uniform keys instead of 8-10), entries sharing
+// those bits form short runs (expected n / 2^window ~ 75).  Each workgroup owns the runs that
+// START in its 2048-entry core and reads up to 512 more entries so a run spilling past the core
+// is finished by its owner; positions inside a run are permuted in place, which never changes the
+// run-id bits other workgroups read.  Rank of x in its run = #(y < x) + #(y == x, y before x)
+// on the masked key: a stable sort on [begin_bit, end_bit) whatever the unmasked bits hold.
+// Lanes of a wave walk the same run in lockstep, so the LDS reads are mostly broadcasts.
+// A run that does not end inside the window sets *overflow (caller falls back to full LSD).
+namespace {
+constexpr int kSegCore = 2048, kSegExt = 512, kSegWin = kSegCore + kSegExt, kSegPer = kSegWin / 256;  // 10
+
+// Comparison keys: the run is fixed by masked hi >> B (B = run_shift), so only the 64 key bits
+// right below the run bits, k = (hi << (64 - B)) | (lo >> B), plus (REST) the masked low B bits
+// of lo when the key extends that far, decide the order inside a run; position breaks ties.
+template <bool REST>
+__global__ __launch_bounds__(256) void seg_sort_kernel(E128* __restrict__ e, uint64_t n, int run_shift,
+                                                       uint64_t mh, uint64_t ml, uint32_t* __restrict__ overflow) {
+  __shared__ __attribute__((aligned(16))) uint64_t kk[kSegWin];
+  __shared__ uint64_t rest[REST ? kSegWin : 1];
+  __shared__ uint32_t rid32[kSegWin];
+  __shared__ uint16_t rid_of[kSegWin];
+  __shared__ uint16_t rstart[kSegWin + 1];
+  __shared__ uint32_t sc[4];
+  const int t = threadIdx.x;
+  const int B = run_shift;
+  const uint64_t c0 = (uint64_t)blockIdx.x * kSegCore;
+  if (c0 >= n) return;
+  const uint32_t core = (uint32_t)((n - c0) < (uint64_t)kSegCore ? (n - c0) : kSegCore);
+  const uint64_t wend = (c0 + kSegWin) < n ? c0 + kSegWin : n;
+  const uint32_t L = (uint32_t)(wend - c0);
+  const uint64_t rest_mask = B ? (ml & ((1ull << B) - 1)) : 0ull;
+  auto key64 = [&](uint64_t hi, uint64_t lo) -> uint64_t {
+    return B ? ((hi << (64 - B)) | (lo >> B)) : lo;
+  };
+  // thread t loads (and later ranks) positions t, t + 256, ...: the unmasked entries stay in
+  // registers; LDS gets the comparison keys and the low 32 bits of the run id (the window is at
+  // most 32 bits wide for n < 2^32, and every key shares the bits above it)
+  E128 mine[kSegPer];
+#pragma unroll
+  for (int k = 0; k < kSegPer; ++k) {
+    const uint32_t i = t + k * 256;
+    if (i < L) {
+      mine[k] = e[c0 + i];
+      const uint64_t h = mine[k].hi & mh, lo = mine[k].lo & ml;
+      kk[i] = key64(h, lo);
+      if (REST) rest[i] = lo & rest_mask;
+      rid32[i] = (uint32_t)(h >> B);
+    }
+  }
+  const uint32_t prev_rid = (c0 > 0) ? (uint32_t)((e[c0 - 1].hi & mh) >> B) : 0u;
+  __syncthreads();
+  uint32_t f = 0;
+#pragma unroll
+  for (int k = 0; k < kSegPer; ++k) {
+    const uint32_t p = t * kSegPer + k;
+    if (p < L) {
+      const uint32_t r = rid32[p];
+      const bool start = (p == 0) ? (c0 == 0 || prev_rid != r) : (rid32[p - 1] != r);
+      if (start) f |= 1u << k;
+    }
+  }
+  uint32_t nruns;
+  const uint32_t base = block_exclusive_scan256((uint32_t)__popc(f), sc, nruns);
+  uint32_t id = base;
+#pragma unroll
+  for (int k = 0; k < kSegPer; ++k) {
+    const uint32_t p = t * kSegPer + k;
+    if (p < L) {
+      if (f & (1u << k)) { rstart[id] = (uint16_t)p; ++id; }
+      rid_of[p] = (uint16_t)(id - 1);   // 0xFFFF: run started before this window
+    }
+  }
+  if (t == 0) rstart[nruns] = (uint16_t)L;
+  __syncthreads();
+  const bool open_end = wend < n;
+#pragma unroll
+  for (int k = 0; k < kSegPer; ++k) {
+    const uint32_t p = t + k * 256;
+    if (p >= L) continue;
+    const uint32_t r = rid_of[p];
+    if (r == 0xFFFFu) continue;
+    const uint32_t rs = rstart[r];
+    if (rs >= core) continue;                       // owned by the next workgroup
+    if (open_end && r + 1 == nruns) {               // run may continue past the window
+      atomicOr(overflow, 1u);
+      continue;
+    }
+    const uint32_t re = rstart[r + 1];
+    if (re - rs == 1) continue;
+    const uint64_t kx = kk[p];
+    const uint64_t rx = REST ? rest[p] : 0ull;
+    // rank = #{y in run : (k_y, rest_y, j) < (k_x, rest_x, p)}
+    uint32_t cnt = 0;
+    uint32_t j = rs;
+    if (!REST) {
+      for (; j < (rs & ~1u) + 2 && j < re; ++j) cnt += (kk[j] < kx || (kk[j] == kx && j < p)) ? 1u : 0u;
+      for (; j + 4 <= re; j += 4) {   // 16-byte aligned pairs: two ds_read_b128 per 4 keys
+        const ulonglong2 y0 = *reinterpret_cast<const ulonglong2*>(&kk[j]);
+        const ulonglong2 y1 = *reinterpret_cast<const ulonglong2*>(&kk[j + 2]);
+        cnt += (y0.x < kx || (y0.x == kx && j < p)) ? 1u : 0u;
+        cnt += (y0.y < kx || (y0.y == kx && j + 1 < p)) ? 1u : 0u;
+        cnt += (y1.x < kx || (y1.x == kx && j + 2 < p)) ? 1u : 0u;
+        cnt += (y1.y < kx || (y1.y == kx && j + 3 < p)) ? 1u : 0u;
+      }
+    }
+    for (; j < re; ++j) {
+      const uint64_t y = kk[j];
+      const uint64_t ry = REST ? rest[j] : 0ull;
+      cnt += (y < kx || (y == kx && (ry < rx || (ry == rx && j < p)))) ? 1u : 0u;
+    }
+    e[c0 + rs + cnt] = mine[k];
+  }
+}
+
+// [min, max] of hi over all entries (the hybrid sort skips the common prefix of all keys).
+__global__ __launch_bounds__(256) void hi_range_kernel(const E128* __restrict__ e, uint64_t n,
+                                                       unsigned long long* __restrict__ range) {
+  uint64_t mn = ~0ull, mx = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t h = e[i].hi;
+    mn = h < mn ? h : mn;
+    mx = h > mx ? h : mx;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint64_t a = __shfl_xor(mn, m, 64), b = __shfl_xor(mx, m, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if (lane_id() == 0) {
+    atomicMin(range, (unsigned long long)mn);
+    atomicMax(range + 1, (unsigned long long)mx);
+  }
+}
+}  // namespace
+
+DR_API int dr_seg_sort_runs(E128* e, uint64_t n, int run_shift, uint64_t mask_hi, uint64_t mask_lo,
+                            uint32_t* overflow, hipStream_t s) {
+  if (run_shift < 0 || run_shift > 63) return (int)hipErrorInvalidValue;
+  if (n < 2) return 0;
+  const uint64_t g = (n + kSegCore - 1) / kSegCore;
+  const bool rest = run_shift > 0 && (mask_lo & ((1ull << run_shift) - 1)) != 0;
+  if (rest)
+    seg_sort_kernel<true><<<(unsigned)g, 256, 0, s>>>(e, n, run_shift, mask_hi, mask_lo, overflow);
+  else
+    seg_sort_kernel<false><<<(unsigned)g, 256, 0, s>>>(e, n, run_shift, mask_hi, mask_lo, overflow);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// [min, max] of entries[].hi into range[0..1] (caller initialises to {~0, 0}).
+DR_API int dr_hi_range(const E128* e, uint64_t n, uint64_t* range, hipStream_t s) {
+  if (n == 0) return 0;
+  hi_range_kernel<<<grid_for(n, 256 * 8, 4096), 256, 0, s>>>(e, n, reinterpret_cast<unsigned long long*>(range));
   DR_LAUNCH_CHECK();
   return 0;
 }

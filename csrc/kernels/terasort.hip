@@ -46,10 +46,16 @@ __device__ __forceinline__ void ts_record(uint64_t seed, uint64_t g, uint32_t* w
 }
 
 // One workgroup generates 256 consecutive records: each thread builds one record in LDS, then
-// the block streams the 25.6 KB image out with coalesced 16-byte stores.
+// the block streams the 25.6 KB image out with coalesced 16-byte stores.  With KEYS the producer
+// also emits the record's 16-byte sort entry (the extract_keys_ts layout: hi = key bytes 0..7,
+// lo = key bytes 8..9 << 48 | row index) and folds [min, max] of hi into hi_range, so a sort
+// that consumes the generated table skips its key-extraction pass (one 100-byte row read each).
+template <bool KEYS>
 __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out, uint64_t n, uint64_t first,
-                                                     uint64_t seed) {
+                                                     uint64_t seed, E128* __restrict__ keys, uint32_t idx_base,
+                                                     unsigned long long* __restrict__ hi_range) {
   __shared__ __attribute__((aligned(16))) uint32_t img[256 * 25];
+  uint64_t mn = ~0ull, mx = 0;
   for (uint64_t row0 = (uint64_t)blockIdx.x * 256; row0 < n; row0 += (uint64_t)gridDim.x * 256) {
     const uint32_t rows = (uint32_t)((n - row0) < 256 ? (n - row0) : 256);
     if (threadIdx.x < rows) {
@@ -57,6 +63,14 @@ __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out,
       ts_record(seed, first + row0 + threadIdx.x, w);
 #pragma unroll
       for (int k = 0; k < 25; ++k) img[threadIdx.x * 25 + k] = w[k];
+      if (KEYS) {
+        E128 e;
+        e.hi = ((uint64_t)bswap32(w[0]) << 32) | bswap32(w[1]);
+        e.lo = ((uint64_t)(bswap32(w[2]) & 0xFFFF0000u) << 32) | (uint32_t)(idx_base + (uint32_t)(row0 + threadIdx.x));
+        keys[row0 + threadIdx.x] = e;
+        mn = e.hi < mn ? e.hi : mn;
+        mx = e.hi > mx ? e.hi : mx;
+      }
     }
     __syncthreads();
     uint32_t* o = out + row0 * 25;
@@ -69,6 +83,18 @@ __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out,
       for (uint32_t j = threadIdx.x; j < words; j += 256) o[j] = img[j];
     }
     __syncthreads();
+  }
+  if (KEYS && hi_range) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      const uint64_t a = __shfl_xor(mn, m, 64), b = __shfl_xor(mx, m, 64);
+      mn = a < mn ? a : mn;
+      mx = b > mx ? b : mx;
+    }
+    if (lane_id() == 0) {
+      atomicMin(hi_range, (unsigned long long)mn);
+      atomicMax(hi_range + 1, (unsigned long long)mx);
+    }
   }
 }
 
@@ -111,7 +137,21 @@ __global__ __launch_bounds__(256) void ts_check_kernel(const uint32_t* __restric
 
 DR_API int dr_terasort_gen(uint8_t* out, uint64_t n, uint64_t first_index, uint64_t seed, hipStream_t s) {
   if (n == 0) return 0;
-  ts_gen_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index, seed);
+  ts_gen_kernel<false><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index,
+                                                               seed, nullptr, 0, nullptr);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// Generator fused with key extraction: also writes n sort entries (row index idx_base + i) and,
+// when hi_range is non-null, min/max of the entries' hi words (caller initialises {~0, 0}).
+DR_API int dr_terasort_gen_keys(uint8_t* out, uint64_t n, uint64_t first_index, uint64_t seed, E128* keys,
+                                uint32_t idx_base, uint64_t* hi_range, hipStream_t s) {
+  if (n == 0) return 0;
+  if (n + idx_base > (1ull << 32)) return (int)hipErrorInvalidValue;
+  ts_gen_kernel<true><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index,
+                                                              seed, keys, idx_base,
+                                                              reinterpret_cast<unsigned long long*>(hi_range));
   DR_LAUNCH_CHECK();
   return 0;
 }

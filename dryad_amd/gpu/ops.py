@@ -76,7 +76,7 @@ def _perm(entries: torch.Tensor) -> torch.Tensor:
 
 def sort_perm(table, key_fn, comparer=None, descending=False):
     e, b0, lo_mask = key_entries(table, key_fn, comparer, descending)
-    srt = S.sort_entries(e, b0, 128)
+    srt = S.sort_entries_hybrid(e, b0)
     return srt, _perm(srt), lo_mask
 
 
@@ -101,8 +101,16 @@ def op_read(op, inputs, v):
         if kind == "terasort":
             from ..ops import terasort as TSK
             rows = v.alloc_rows(hi - lo, 100)
-            TSK.generate(rows, lo, int(q.get("seed", 0)))
-            return DeviceTable(hi - lo, Shape("rows", key_off=0, key_len=10), rows=rows)
+            t = DeviceTable(hi - lo, Shape("rows", key_off=0, key_len=10), rows=rows)
+            bs = _pooled_set(t, v)
+            if bs is not None:
+                # producer-side key extraction: a following OrderBy(key bytes 0..9) starts sorting
+                rng = torch.tensor([-1, 0], dtype=torch.int64, device=rows.device)
+                TSK.generate_with_keys(rows, lo, int(q.get("seed", 0)), bs.bufs.ent_a, rng)
+                bs.keys_ready = (rows.data_ptr(), hi - lo, 0, 10, rng)
+            else:
+                TSK.generate(rows, lo, int(q.get("seed", 0)))
+            return t
         if kind == "range":
             start = int(q.get("start", 0))
             a = torch.arange(start + lo, start + hi, dtype=torch.int32 if start + hi < 2**31 else torch.int64,
@@ -218,8 +226,10 @@ def op_sort(op, inputs, v):
         # in-place key-pointer sort of pooled rows: rows_in -> rows_out, entries in the pool
         kind, spec = TR.key_columns(TR.call(op["key"], t), t)
         if kind == "bytes" and spec.length <= 12:
+            bounds = bs.take_keys(t.rows, spec.off, spec.length)
             out = RS.local_sort_rows(t.rows, bs.bufs.rows_out, bs.bufs.ent_a, bs.bufs.ent_b, spec.off, spec.length,
-                                     descending=op.get("descending", False))
+                                     descending=op.get("descending", False), hi_bounds=bounds,
+                                     keys_ready=bounds is not None)
             return DeviceTable(out.shape[0], t.shape, rows=out)
     _, perm, _ = sort_perm(t, op["key"], op.get("comparer"), op.get("descending", False))
     return t.take(perm)
@@ -322,7 +332,7 @@ def op_group_partial(op, inputs, v):
         raise NotTraceable("empty partition")
     kcols, _ = _key_cols(t, op["key"])
     e, b0, lo_mask = R.build_keys(kcols)
-    srt = S.sort_entries(e, b0, 128)
+    srt = S.sort_entries_hybrid(e, b0)
     seg, nseg, starts = R.segment_ids(srt, lo_mask)
     rows_at_start = _perm(srt).index_select(0, starts)
     out = {f"k{i}": c.index_select(0, rows_at_start) for i, c in enumerate(kcols)}
@@ -356,7 +366,7 @@ def op_group_final(op, inputs, v):
     nkeys = sum(1 for f in t.shape.fields if f.startswith("k"))
     kcols = [t.cols[f"k{i}"] for i in range(nkeys)]
     e, b0, lo_mask = R.build_keys(kcols)
-    srt = S.sort_entries(e, b0, 128)
+    srt = S.sort_entries_hybrid(e, b0)
     seg, nseg, starts = R.segment_ids(srt, lo_mask)
     rows_at_start = _perm(srt).index_select(0, starts)
     keys = [c.index_select(0, rows_at_start) for c in kcols]
@@ -405,7 +415,7 @@ def op_distinct(op, inputs, v):
         if R.key_bit_count(cols) > 96:
             raise NotTraceable("record wider than 96 bits")
         e, b0, lo_mask = R.build_keys(cols)
-    srt = S.sort_entries(e, b0, 128)
+    srt = S.sort_entries_hybrid(e, b0)
     _, _, starts = R.segment_ids(srt, lo_mask)
     return t.take(_perm(srt).index_select(0, starts))
 
@@ -420,8 +430,8 @@ def op_hash_join(op, inputs, v):
     ei, b1, lm2 = key_entries(inner, op["inner_key"])
     if (b0, lm) != (b1, lm2):
         raise NotTraceable("join keys of different types")
-    so = S.sort_entries(eo, b0, 128)
-    si = S.sort_entries(ei, b0, 128)
+    so = S.sort_entries_hybrid(eo, b0)
+    si = S.sort_entries_hybrid(ei, b0)
     oo, ii, _ = R.merge_join_pairs(so, si, lm)
     if oo.shape[0] == 0:
         raise NotTraceable("empty join result")

@@ -22,6 +22,21 @@ class BufferSet:
         self.stride = stride
         self.pins = 0
         self.in_use = False
+        # set by a producer that also wrote rows_in's sort entries into bufs.ent_a:
+        # (rows_in data_ptr, n, key_off, key_len, hi_range device tensor); consumed by one sort
+        self.keys_ready = None
+
+    def take_keys(self, rows, key_off: int, key_len: int):
+        """Entries in ent_a for exactly these rows and key, or None.  One-shot: sorting reuses
+        ent_a as scratch, so the claim is dropped either way."""
+        kr, self.keys_ready = self.keys_ready, None
+        if kr is None or rows is None:
+            return None
+        ptr_, n, off, ln, rng = kr
+        if ptr_ != rows.data_ptr() or n != rows.shape[0] or off != key_off or ln != key_len:
+            return None
+        mn, mx = (int(x) & ((1 << 64) - 1) for x in rng.cpu().tolist())
+        return mn, mx
 
     @property
     def capacity(self):
@@ -39,6 +54,7 @@ class HbmPool:
             for s in self.sets:
                 if not s.in_use and s.pins == 0 and s.stride == stride and s.capacity >= capacity:
                     s.in_use = True
+                    s.keys_ready = None
                     return s
             # drop idle sets before allocating a new one (HBM is the limit, not the allocator)
             keep = [s for s in self.sets if s.in_use or s.pins > 0]

@@ -28,7 +28,9 @@ from ..parallel import shuffle
 from . import sort as S
 import os as _os
 
-PREFIX_SORT = _os.environ.get("DRYAD_PREFIX_SORT", "1") == "1"
+# local sort algorithm: "hybrid" (top-window LSD + in-LDS run sort, default), "prefix"
+# (64-bit LSD + tie fix-up) or "lsd" (full-width LSD)
+SORT_ALGO = _os.environ.get("DRYAD_SORT_ALGO", "hybrid")
 
 
 def key_bits(key_len: int) -> tuple[int, int, int]:
@@ -74,12 +76,18 @@ class SortStats:
 
 
 def local_sort_rows(rows: torch.Tensor, out: torch.Tensor, ent_a: torch.Tensor, ent_b: torch.Tensor,
-                    key_off: int, key_len: int, descending: bool = False) -> torch.Tensor:
-    """Sort fixed-width ``rows`` by their byte-string key into ``out`` (stable)."""
+                    key_off: int, key_len: int, descending: bool = False,
+                    hi_bounds: tuple[int, int] | None = None, keys_ready: bool = False) -> torch.Tensor:
+    """Sort fixed-width ``rows`` by their byte-string key into ``out`` (stable).
+
+    ``hi_bounds`` = known (min, max) of the first 8 key bytes as a big-endian integer (e.g. this
+    rank's range-partition bounds); lets the hybrid sort skip their common prefix without a pass.
+    ``keys_ready``: ``ent_a[:n]`` already holds ``extract_keys(rows, key_off, key_len)`` (the
+    producer emitted them, e.g. the fused TeraSort generator)."""
     n = rows.shape[0]
     if n == 0:
         return out[:0]
-    e = S.extract_keys(rows, key_off, key_len, 0, out=ent_a[:n])
+    e = ent_a[:n] if keys_ready else S.extract_keys(rows, key_off, key_len, 0, out=ent_a[:n])
     if descending:
         # invert the key bits (not the row index) so an ascending radix sort yields descending keys
         b0, _, lo_mask = key_bits(key_len)
@@ -88,7 +96,9 @@ def local_sort_rows(rows: torch.Tensor, out: torch.Tensor, ent_a: torch.Tensor, 
             e[:, 0].bitwise_xor_(torch.tensor(lo_mask - (1 << 64) if lo_mask >= (1 << 63) else lo_mask,
                                               dtype=torch.int64, device=e.device))
     b0, b1, _ = key_bits(key_len)
-    if PREFIX_SORT and b0 < 64:
+    if SORT_ALGO == "hybrid":
+        srt = S.sort_entries_hybrid(e, b0, b1, tmp=ent_b[:n], hi_bounds=None if descending else hi_bounds)
+    elif SORT_ALGO == "prefix" and b0 < 64:
         srt = S.sort_entries_prefix(e, b0, tmp=ent_b[:n])
     else:
         srt = S.sort_entries(e, b0, b1, tmp=ent_b[:n])
@@ -115,6 +125,14 @@ def choose_separators(entries: torch.Tensor, n: int, world: World, lo_mask: int,
     return srt.index_select(0, pos).contiguous()
 
 
+def rank_hi_bounds(seps: torch.Tensor, rank: int) -> tuple[int, int]:
+    """(min, max) of key ``hi`` words that range partition ``rank`` can receive."""
+    his = [int(x) & ((1 << 64) - 1) for x in seps[:, 1].tolist()]
+    lo = his[rank - 1] if rank > 0 else 0
+    hi = his[rank] if rank < len(his) else (1 << 64) - 1
+    return lo, hi
+
+
 def _as_i64(v: int) -> int:
     v &= (1 << 64) - 1
     return v - (1 << 64) if v >= (1 << 63) else v
@@ -122,21 +140,24 @@ def _as_i64(v: int) -> int:
 
 def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int, world: World | None = None,
                           sample_target: int = 1 << 20, seed: int = 314159,
-                          stats: SortStats | None = None) -> torch.Tensor:
+                          stats: SortStats | None = None, keys_ready: bool = False,
+                          hi_bounds: tuple[int, int] | None = None) -> torch.Tensor:
     """Globally sort the first ``n`` rows of ``bufs.rows_in`` across all ranks.
 
     On return rank r holds, in ``bufs.rows_out[:n_r]``, the r-th key range in ascending order.
-    ``bufs.rows_in`` is clobbered (it becomes the receive buffer)."""
+    ``bufs.rows_in`` is clobbered (it becomes the receive buffer).  ``keys_ready``: ``bufs.ent_a[:n]``
+    already holds the rows' sort entries; ``hi_bounds``: known hi range of the local keys."""
     w = world or get_world()
     rows = bufs.rows_in[:n]
     if w.size == 1:
-        out = local_sort_rows(rows, bufs.rows_out, bufs.ent_a, bufs.ent_b, key_off, key_len)
+        out = local_sort_rows(rows, bufs.rows_out, bufs.ent_a, bufs.ent_b, key_off, key_len,
+                              hi_bounds=hi_bounds, keys_ready=keys_ready)
         if stats is not None:
             stats.n_in = stats.n_out = n
         return out
     stride = rows.shape[1]
     b0, b1, lo_mask = key_bits(key_len)
-    ent = S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
+    ent = bufs.ent_a[:n] if keys_ready else S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
     seps = choose_separators(ent, n, w, lo_mask, sample_target, seed, bufs.ent_b)
     S.range_dest(ent, seps, lo_mask)                                    # ent.hi := destination
     part, starts = S.partition_pass(ent, 64, out=bufs.ent_b[:n])        # stable by destination
@@ -152,7 +173,8 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     recv_flat = bufs.rows_in.view(-1)
     shuffle.alltoallv_bytes(send_flat, [c * stride for c in send_counts], recv_flat,
                             [c * stride for c in recv_counts], w)
-    out = local_sort_rows(bufs.rows_in[:n_recv], bufs.rows_out, bufs.ent_a, bufs.ent_b, key_off, key_len)
+    out = local_sort_rows(bufs.rows_in[:n_recv], bufs.rows_out, bufs.ent_a, bufs.ent_b, key_off, key_len,
+                          hi_bounds=rank_hi_bounds(seps, w.rank))
     if stats is not None:
         stats.n_in, stats.n_out = n, n_recv
         stats.send_counts, stats.recv_counts = send_counts, recv_counts

@@ -80,6 +80,80 @@ def sort_entries_prefix(entries: torch.Tensor, begin_bit: int, tmp: torch.Tensor
     return sort_entries(out, 64, 128, (srt if out is not srt else other)[: srt.shape[0]])
 
 
+def hi_range(entries: torch.Tensor) -> tuple[int, int]:
+    """(min, max) of the unsigned ``hi`` words (one streaming pass)."""
+    r = torch.tensor([-1, 0], dtype=torch.int64, device=entries.device)
+    _lib.call("dr_hi_range", ptr(entries), c_u64(entries.shape[0]), ptr(r), stream_of(entries))
+    mn, mx = r.cpu().tolist()
+    return mn & _M64, mx & _M64
+
+
+_M64 = (1 << 64) - 1
+# expected run length the segmented phase is sized for (window = smallest multiple of 8 bits with
+# n / 2^window <= RUN_TARGET); overridable for tuning
+import os as _os  # noqa: E402
+RUN_TARGET = int(_os.environ.get("DRYAD_SORT_RUN_TARGET", "128"))
+
+
+def _mask_words(begin_bit: int, end_bit: int) -> tuple[int, int]:
+    m = ((1 << end_bit) - 1) ^ ((1 << begin_bit) - 1)
+    return (m >> 64) & _M64, m & _M64
+
+
+def _i64(v: int) -> int:
+    v &= _M64
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+def sort_entries_hybrid(entries: torch.Tensor, begin_bit: int, end_bit: int = 128,
+                        tmp: torch.Tensor | None = None, hi_bounds: tuple[int, int] | None = None,
+                        stats: dict | None = None) -> torch.Tensor:
+    """Stable sort on composite bits [begin_bit, end_bit) = LSD radix on only the top window of
+    *varying* key bits + an in-LDS segmented sort of the resulting short runs.
+
+    Bits of ``hi`` above the common prefix of all keys (from ``hi_bounds`` = a known (min, max)
+    of hi, e.g. the range-partition separators, or one dr_hi_range pass) are skipped; the window
+    is the smallest multiple of 8 bits making the expected run <= RUN_TARGET for uniform keys
+    (3 passes for 1e9 keys vs 10 for a full 80-bit TeraSort key).  Skewed keys (a run longer than
+    the LDS window) fall back to the full LSD sort of the remaining bits — same result."""
+    n = entries.shape[0]
+    if n < 2 or begin_bit >= end_bit:
+        return entries
+    if tmp is None:
+        tmp = torch.empty_like(entries)
+    if end_bit < 128:   # bits above end_bit are not key bits: no prefix information
+        return sort_entries(entries, begin_bit, end_bit, tmp)
+    mn, mx = hi_bounds if hi_bounds is not None else hi_range(entries)
+    P = 64 - (mn ^ mx).bit_length()            # common prefix of every hi word
+    top = 128 - P                              # composite bits >= top are constant
+    if top <= begin_bit:
+        return entries                         # all keys equal: stable order = input order
+    win = 8
+    while win < 64 and n > RUN_TARGET << win:
+        win += 8
+    span = top - begin_bit
+    if span <= win + 8 or top - win < 64:
+        # few varying bits (or the window would leave hi): plain LSD over the varying bits
+        e_ = min(128, begin_bit + ((span + 7) // 8) * 8)
+        b = e_ - ((span + 7) // 8) * 8
+        if stats is not None:
+            stats["path"] = "lsd"
+        return sort_entries(entries, b, e_, tmp)
+    srt = sort_entries(entries, top - win, top, tmp)
+    mh, ml = _mask_words(begin_bit, end_bit)
+    flag = torch.zeros(1, dtype=torch.int32, device=entries.device)
+    _lib.call("dr_seg_sort_runs", ptr(srt), c_u64(n), top - win - 64, c_u64(mh), c_u64(ml), ptr(flag),
+              stream_of(srt))
+    if int(flag.item()) == 0:
+        if stats is not None:
+            stats["path"] = f"hybrid win={win} top={top}"
+        return srt
+    if stats is not None:
+        stats["path"] = "fallback"
+    other = tmp if srt is entries else entries
+    return sort_entries(srt, begin_bit, 128, other[:n])
+
+
 def set_sort_items(items: int):
     _lib.lib().dr_sort_set_items(int(items))
 

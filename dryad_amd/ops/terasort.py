@@ -4,7 +4,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
-from ._lib import c_u64, ptr, stream_of
+from ._lib import c_u32, c_u64, ptr, stream_of
 
 RECORD_BYTES = 100
 KEY_BYTES = 10
@@ -18,6 +18,19 @@ def generate(out: torch.Tensor, first_index: int, seed: int) -> torch.Tensor:
     assert out.dtype == torch.uint8 and out.dim() == 2 and out.shape[1] == RECORD_BYTES
     _lib.call("dr_terasort_gen", ptr(out), c_u64(out.shape[0]), c_u64(first_index), c_u64(seed & (2**64 - 1)),
               stream_of(out))
+    return out
+
+
+def generate_with_keys(out: torch.Tensor, first_index: int, seed: int, keys: torch.Tensor,
+                       hi_range: torch.Tensor | None = None) -> torch.Tensor:
+    """``generate`` fused with key extraction: ``keys`` ([n, 2] int64) receives the sort entries
+    ``extract_keys(out, 0, 10)`` would build, ``hi_range`` ([2] int64, initialised to [-1, 0])
+    the unsigned min/max of their hi words.  Saves the extraction pass of a following sort."""
+    _lib.require_gpu_tensor(out, "terasort.generate_with_keys")
+    n = out.shape[0]
+    assert keys.shape[0] >= n and keys.dtype == torch.int64 and keys.is_contiguous()
+    _lib.call("dr_terasort_gen_keys", ptr(out), c_u64(n), c_u64(first_index), c_u64(seed & (2**64 - 1)),
+              ptr(keys), c_u32(0), ptr(hi_range), stream_of(out))
     return out
 
 

@@ -161,7 +161,9 @@ class GpuJobRunner:
         bs = self.row_sets[(f["x"], me)]
         off, ln = f["spec"]
         stats = RS.SortStats()
-        out = RS.distributed_sort_rows(bs.bufs, t.n, off, ln, self.world, stats=stats)
+        bounds = bs.take_keys(t.rows, off, ln)
+        out = RS.distributed_sort_rows(bs.bufs, t.n, off, ln, self.world, stats=stats,
+                                       keys_ready=bounds is not None, hi_bounds=bounds)
         self.row_sets[(m.id, me)] = bs
         self.last_sort_stats = stats
         table = DeviceTable(out.shape[0], t.shape, rows=out)

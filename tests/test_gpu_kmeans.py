@@ -1,0 +1,51 @@
+"""k-means MFMA kernel vs plain PyTorch fp32 reference."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,k", [(1, 1), (1000, 7), (50_000, 32), (100_003, 100), (40_000, 200), (20_000, 300), (30_000, 1000), (5_000, 4096)])
+def test_kmeans_step_matches_reference(n, k):
+    from dryad_amd.ops import kmeans as KM
+    x = torch.empty((n, KM.DIM), dtype=torch.float32, device="cuda")
+    KM.generate(x, 0, blobs=max(1, k // 2), seed=n)
+    c = x[torch.randperm(n, device="cuda")[: min(n, k)]].clone()
+    if c.shape[0] < k:
+        c = torch.cat([c, torch.randn((k - c.shape[0], KM.DIM), device="cuda")])
+    sums, counts, assign = KM.step(x, c)
+    rs, rc, ra, d = KM.step_reference(x, c)
+    # points whose best and second-best distances are (numerically) tied may legitimately differ
+    top2 = torch.topk(d, min(2, k), dim=1, largest=False).values
+    gap = (top2[:, 1] - top2[:, 0]) if k > 1 else torch.full((n,), 1e9, device="cuda")
+    tied = gap <= 1e-3 * top2[:, 0].abs().clamp_min(1.0)
+    mism = (assign.long() != ra.long()) & ~tied
+    assert int(mism.sum()) == 0
+    if int(tied.sum()) == 0:
+        assert torch.equal(counts, rc)
+        torch.testing.assert_close(sums, rs, rtol=1e-4, atol=1e-2)
+    assert int(counts.sum()) == n
+
+
+def test_kmeans_generate_counter_based():
+    from dryad_amd.ops import kmeans as KM
+    a = torch.empty((1000, KM.DIM), dtype=torch.float32, device="cuda")
+    b = torch.empty((3000, KM.DIM), dtype=torch.float32, device="cuda")
+    KM.generate(a, 2000, 16, 5)
+    KM.generate(b, 0, 16, 5)
+    assert torch.equal(a, b[2000:])
+
+
+def test_kmeans_converges_on_blobs():
+    from dryad_amd.ops import kmeans as KM
+    n, k = 200_000, 16
+    x = torch.empty((n, KM.DIM), dtype=torch.float32, device="cuda")
+    KM.generate(x, 0, blobs=k, seed=3)
+    c = x[:k].clone()
+    ws = KM.KMeansWorkspace(n, k, x.device)
+    for _ in range(10):
+        s, cnt, _a = KM.step(x, c, ws)
+        c = KM.update(c, s, cnt)
+    _, _, a, d = KM.step_reference(x, c)
+    inertia = d.min(1).values + (x * x).sum(1)
+    assert float(inertia.mean()) < 1.0   # blobs have per-dim noise 0.2*U(-.5,.5): within-blob MSE ~0.43

@@ -185,3 +185,52 @@ def test_scatter_v1_v2_agree():
     b = S.sort_entries(e.clone(), 0, 128).cpu().numpy()
     np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(a, e.cpu().numpy()[_ref_order(e)])
+
+
+@pytest.mark.parametrize("kind", ["uniform", "prefix", "narrow", "dups", "allsame", "small"])
+def test_hybrid_sort_matches_full_sort(kind):
+    from dryad_amd.ops import sort as S
+    n = 3000 if kind == "small" else 600_000
+    e = torch.randint(-2**63, 2**63 - 1, (n, 2), dtype=torch.int64, device="cuda")
+    if kind == "prefix":      # constant top 20 bits (range-partitioned rank)
+        e[:, 1] = (e[:, 1] & ((1 << 44) - 1)) | (0x5A5A5 << 44)
+    elif kind == "narrow":    # only 20 varying bits in hi
+        e[:, 1] = e[:, 1] & ((1 << 20) - 1)
+    elif kind == "dups":      # runs far longer than the LDS window -> fallback path
+        e[:, 1] = torch.randint(0, 5, (n,), device="cuda") << 40
+    elif kind == "allsame":
+        e[:, 1] = 77
+    e[:, 0] = (e[:, 0] & ~0xFFFFFFFF) | torch.arange(n, device="cuda")
+    for begin in (0, 48, 64, 96):
+        full = S.sort_entries(e.clone(), begin, 128).cpu().numpy()
+        st = {}
+        got = S.sort_entries_hybrid(e.clone(), begin, 128, stats=st).cpu().numpy()
+        np.testing.assert_array_equal(got, full, err_msg=f"{kind} begin={begin} {st}")
+
+
+def test_hybrid_sort_masks_bits_below_begin():
+    """Bits below begin_bit are payload: order among equal keys must be input order."""
+    from dryad_amd.ops import sort as S
+    n = 400_000
+    e = torch.randint(-2**63, 2**63 - 1, (n, 2), dtype=torch.int64, device="cuda")
+    e[:, 1] = e[:, 1] & ((1 << 62) - 1)
+    e[: n // 2, 1] = e[n // 2:, 1]          # every key appears twice
+    full = S.sort_entries(e.clone(), 64, 128).cpu().numpy()
+    got = S.sort_entries_hybrid(e.clone(), 64, 128).cpu().numpy()
+    np.testing.assert_array_equal(got, full)
+
+
+def test_terasort_generate_with_keys_matches_extract():
+    from dryad_amd.ops import sort as S, terasort as TS
+    n = 100_003
+    a = torch.empty((n, 100), dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    keys = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    rng = torch.tensor([-1, 0], dtype=torch.int64, device="cuda")
+    TS.generate_with_keys(a, 77, 5, keys, rng)
+    TS.generate(b, 77, 5)
+    assert torch.equal(a, b)
+    ref = S.extract_keys(b, 0, 10, 0)
+    assert torch.equal(keys, ref)
+    mn, mx = S.hi_range(ref)
+    assert [int(x) & (2**64 - 1) for x in rng.cpu().tolist()] == [mn, mx]
