@@ -323,8 +323,10 @@ DR_API int dr_kmeans_step(const float* X, uint64_t n, int d, const float* C, int
   return 0;
 }
 
-// Synthetic Gaussian-mixture points: point i belongs to blob (i * 2654435761) % K; coordinates
-// = blob centre (deterministic from blob id) + small deterministic noise.
+// Synthetic blob points (the k-means benchmark input, gen://points): point i belongs to blob
+// (i * 2654435761) % blobs; coordinate d = centre(blob, d) + 0.2 * (u - 0.5) with centre in
+// [-5, 5).  Every operation is explicitly rounded (no FMA contraction) so the numpy twin in
+// models/kmeans_cpu.py reproduces it bit for bit.
 namespace {
 __device__ __forceinline__ float u01(uint64_t z) { return (float)(mix64(z) >> 40) * (1.0f / 16777216.0f); }
 
@@ -332,11 +334,11 @@ __global__ __launch_bounds__(256) void kmeans_gen_kernel(float* __restrict__ X, 
                                                          int blobs, uint64_t seed) {
   for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * D; e += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t i = e / D + first;
-    const int d = (int)(e % D);
+    const uint64_t d = e % D;
     const uint64_t b = (i * 2654435761ull) % (uint64_t)blobs;
-    const float centre = 10.f * u01(seed ^ (b * 0x9E3779B97F4A7C15ull) ^ (uint64_t)d * 0x632BE59BD9B4E019ull) - 5.f;
-    const float noise = u01(seed * 31 + i * 0xD1B54A32D192ED03ull + (uint64_t)d) - 0.5f;
-    X[e] = centre + 0.2f * noise;
+    const float centre = __fsub_rn(__fmul_rn(10.f, u01(seed ^ (b * 0x9E3779B97F4A7C15ull) ^ (d * 0x632BE59BD9B4E019ull))), 5.f);
+    const float noise = __fsub_rn(u01(seed * 31 + i * 0xD1B54A32D192ED03ull + d), 0.5f);
+    X[e] = __fadd_rn(centre, __fmul_rn(0.2f, noise));
   }
 }
 }  // namespace

@@ -13,6 +13,11 @@ IAssociative.cs) as Python decorators and protocols.
 * ``@nullable`` on a dataclass field type via ``typing.Optional`` (the ``[Nullable]`` attribute).
 * ``@custom_serializer(cls)`` — ``[CustomDryadLinqSerializer]``: the class provides
   ``Write(writer, value)`` / ``Read(reader)``.
+* ``@device_function`` — (no reference equivalent: the reference's vertex code is CLR) an
+  Apply/ApplyPerPartition body that takes and returns ``gpu.table.DeviceTable`` partitions.  On
+  the GPU executor it runs on the HBM-resident tensors (HIP kernels / torch); LocalDebug and the
+  CPU executors hand it CPU-tensor tables built from the records, so one body serves every
+  executor.
 """
 from __future__ import annotations
 
@@ -96,6 +101,15 @@ def custom_serializer(serializer_cls):
         cls._dryad_serializer = serializer_cls
         return cls
     return deco
+
+
+def device_function(fn):
+    """Mark an Apply body as a DeviceTable -> DeviceTable function (see module docstring)."""
+    return _mark(fn, _dryad_device=True)
+
+
+def is_device_function(f) -> bool:
+    return bool(getattr(f, "_dryad_device", False))
 
 
 def is_homomorphic(f) -> bool:

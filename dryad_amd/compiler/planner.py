@@ -501,7 +501,8 @@ class Planner:
         func = a["func"]
         per_part = a.get("per_partition") or is_homomorphic(func)
         first_only = a.get("first_only") or is_left_homomorphic(func)
-        op = dict(op="apply", fn=func, multi=a.get("multi", False), explain="apply" + (" per partition" if per_part else ""))
+        op = dict(op="apply", fn=func, multi=a.get("multi", False), explain="apply" + (" per partition" if per_part else ""),
+                  in_dtypes=[s.dtype for s in q.sources])
         if per_part:
             lead = srcs[0]
             inputs = [StageInput(lead, "pointwise")]

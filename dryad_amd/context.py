@@ -202,10 +202,6 @@ class DryadLinqContext:
             sch = p.schema(str(uri)) if hasattr(p, "schema") else None
             if sch is not None and sch.get("dtype") is not None:
                 dtype = sch["dtype"]
-            if str(uri).startswith("gen://range"):
-                dtype = T.Int32
-            if str(uri).startswith("gen://terasort"):
-                dtype = T.Pickle
         else:
             dtype = T.from_annotation(dtype)
         return Query(self, QNode("FromStore", (), dict(uri=str(uri), deserializer=deserializer), dtype))

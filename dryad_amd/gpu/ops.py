@@ -111,6 +111,12 @@ def op_read(op, inputs, v):
             else:
                 TSK.generate(rows, lo, int(q.get("seed", 0)))
             return t
+        if kind == "points":
+            from ..ops import kmeans as KM
+            x = v.alloc_tensor((hi - lo, KM.DIM), torch.float32)
+            KM.generate(x, lo, int(q.get("blobs", 64)), int(q.get("seed", 0)))
+            from .. import types as T
+            return DeviceTable.from_columns({"x": x}, Shape("vector", ["x"], T.Vector(T.Float32, KM.DIM)))
         if kind == "range":
             start = int(q.get("start", 0))
             a = torch.arange(start + lo, start + hi, dtype=torch.int32 if start + hi < 2**31 else torch.int64,
@@ -465,6 +471,24 @@ def op_agg_final(op, inputs, v):
     if op["spec"]["kind"] == "Count":
         return _scalar_table([int(t.cols[t.shape.fields[0]].sum().item())], torch.int64, v.device)
     raise NotTraceable("aggregate on host")
+
+
+def op_apply(op, inputs, v):
+    """Apply / ApplyPerPartition: ``@device_function`` bodies run on the HBM tables; any other
+    Python body runs on the host records (NotTraceable -> host op)."""
+    from ..attributes import is_device_function
+    f = op["fn"]
+    if not is_device_function(f):
+        raise NotTraceable("Apply body is not a @device_function")
+    from .. import device_udf
+    res = device_udf.call(f, [x if x is not None else [] for x in inputs], op.get("in_dtypes") or [],
+                          bool(op.get("multi")), v.device)
+    if isinstance(res, DeviceTable):
+        return res
+    out = from_objects(list(res), None, v.device)
+    if out is None:
+        raise NotTraceable("device_function returned non-columnar records")
+    return out
 
 
 OPS = {k[3:]: fn for k, fn in list(globals().items()) if k.startswith("op_")}

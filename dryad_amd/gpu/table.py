@@ -27,7 +27,7 @@ from .. import types as T
 @dataclass
 class Shape:
     """How columns map to Python records."""
-    kind: str                         # "scalar" | "tuple" | "dataclass" | "rows"
+    kind: str                         # "scalar" | "tuple" | "dataclass" | "rows" | "vector"
     fields: list = field(default_factory=list)   # column names in record order
     pytype: object = None
     key_off: int = 0                  # rows: default key field
@@ -60,7 +60,14 @@ class DeviceTable:
     def empty_like(t: "DeviceTable", n: int = 0) -> "DeviceTable":
         if t.shape.kind == "rows":
             return DeviceTable(n, t.shape, rows=t.rows.new_empty((n, t.rows.shape[1])))
-        return DeviceTable(n, t.shape, {k: v.new_empty((n,)) for k, v in t.cols.items()})
+        return DeviceTable(n, t.shape, {k: v.new_empty((n,) + tuple(v.shape[1:])) for k, v in t.cols.items()})
+
+    def col(self, key) -> torch.Tensor:
+        """Column by name or by record position (tuple tables built from records name their
+        fields Item1..ItemN, device-built ones whatever the producer chose)."""
+        if isinstance(key, int):
+            return self.cols[self.shape.fields[key]]
+        return self.cols[key]
 
     @property
     def device(self):
@@ -79,7 +86,7 @@ class DeviceTable:
     def row_bytes(self) -> int:
         if self.rows is not None:
             return self.rows.shape[1]
-        return sum(v.element_size() for v in self.cols.values())
+        return sum(_width(v) for v in self.cols.values())
 
     # ------------------------------------------------------------------ slicing / permutation
     def slice(self, a: int, b: int) -> "DeviceTable":
@@ -116,7 +123,7 @@ class DeviceTable:
         """One uint8 [n, row_bytes] buffer (AoS) so an exchange is a single collective."""
         if self.rows is not None:
             return self.rows
-        parts = [v.contiguous().view(torch.uint8).reshape(self.n, v.element_size()) for v in self.cols.values()]
+        parts = [v.contiguous().view(torch.uint8).reshape(self.n, _width(v)) for v in self.cols.values()]
         if not parts:
             return torch.empty((self.n, 0), dtype=torch.uint8, device=self.device)
         return torch.cat(parts, dim=1) if len(parts) > 1 else parts[0]
@@ -127,8 +134,8 @@ class DeviceTable:
         buf = buf.reshape(n, -1)
         out, off = {}, 0
         for k, v in self.cols.items():
-            w = v.element_size()
-            out[k] = buf[:, off:off + w].contiguous().view(v.dtype).reshape(n)
+            w = _width(v)
+            out[k] = buf[:, off:off + w].contiguous().view(v.dtype).reshape((n,) + tuple(v.shape[1:]))
             off += w
         return DeviceTable(n, self.shape, out)
 
@@ -143,12 +150,22 @@ class DeviceTable:
         sh = self.shape
         if sh.kind == "scalar":
             return arrs[sh.fields[0]].tolist()
-        lists = [arrs[f].tolist() for f in sh.fields]
+        if sh.kind == "vector":
+            return [tuple(r) for r in arrs[sh.fields[0]].tolist()]
+        lists = [[tuple(r) for r in arrs[f].tolist()] if arrs[f].ndim > 1 else arrs[f].tolist() for f in sh.fields]
         if sh.kind == "tuple":
             return list(zip(*lists))
         if sh.kind == "dataclass":
             return [sh.pytype(*vals) for vals in zip(*lists)]
         raise ValueError(sh.kind)
+
+
+def _width(v: torch.Tensor) -> int:
+    """Bytes per record of a column ([n] scalars or [n, d] vectors)."""
+    per = 1
+    for d in v.shape[1:]:
+        per *= d
+    return per * v.element_size()
 
 
 @dataclass
@@ -174,8 +191,11 @@ def columnar_dtype(dt) -> bool:
     """Can records of this DType live as columns in HBM?"""
     if dt in _NP_OF:
         return True
+    if isinstance(dt, T.VectorT):
+        return dt.elem in _NP_OF
     if isinstance(dt, T.RecordT):
-        return all(t in _NP_OF for _, t in dt.fields) and not dt.nullable_fields
+        return all(t in _NP_OF or (isinstance(t, T.VectorT) and t.elem in _NP_OF) for _, t in dt.fields) \
+            and not dt.nullable_fields
     return False
 
 
@@ -185,6 +205,10 @@ def from_objects(records: list, dt, device) -> DeviceTable | None:
         dt = T.infer_common_type(records[:1000]) if records else T.Int32
     if not columnar_dtype(dt):
         return None
+    if isinstance(dt, T.VectorT):
+        npt = _NP_OF[dt.elem]
+        a = np.asarray(records, dtype=npt).reshape(len(records), dt.dim) if records else np.zeros((0, dt.dim), npt)
+        return DeviceTable.from_columns({"x": torch.from_numpy(a).to(device)}, Shape("vector", ["x"], dt))
     if dt in _NP_OF:
         a = np.asarray(records, dtype=_NP_OF[dt]) if records else np.zeros(0, _NP_OF[dt])
         return DeviceTable.from_columns({"v": torch.from_numpy(a).to(device)}, Shape("scalar", ["v"]))
@@ -195,6 +219,11 @@ def from_objects(records: list, dt, device) -> DeviceTable | None:
             vals = [r[i] for r in records]
         else:
             vals = [getattr(r, n) for r in records]
+        if isinstance(t, T.VectorT):
+            npt = _NP_OF[t.elem]
+            a = np.asarray(vals, dtype=npt).reshape(len(vals), t.dim) if vals else np.zeros((0, t.dim), npt)
+            cols[n] = torch.from_numpy(a).to(device)
+            continue
         cols[n] = torch.from_numpy(np.asarray(vals, dtype=_NP_OF[t]) if vals else np.zeros(0, _NP_OF[t])).to(device)
     kind = "tuple" if dt.pytype in (None, tuple) else "dataclass"
     return DeviceTable.from_columns(cols, Shape(kind, names, None if kind == "tuple" else dt.pytype))

@@ -253,7 +253,9 @@ class HbmProvider(DataProvider):
 class GenProvider(DataProvider):
     """Synthetic generator stores.  ``gen://range?count=N&partitions=P[&start=S]`` yields ints;
     ``gen://terasort?records=N&partitions=P&seed=S`` yields 100-byte TeraSort records (as bytes on
-    the object path, generated directly in HBM by the GPU executor)."""
+    the object path, generated directly in HBM by the GPU executor);
+    ``gen://points?count=N&partitions=P&blobs=B&seed=S`` yields 128-dim float32 blob points
+    (tuples on the object path, one [n, 128] HBM tensor on the GPU executor)."""
     scheme = "gen"
 
     def _args(self, uri):
@@ -265,10 +267,18 @@ class GenProvider(DataProvider):
         p = int(q.get("partitions", 1))
         if kind == "terasort":
             return p, int(q.get("records", 0)) * 100
+        if kind == "points":
+            return p, int(q.get("count", 0)) * 4 * 128
         return p, int(q.get("count", 0)) * 4
 
     def exists(self, uri):
         return True
+
+    def schema(self, uri):
+        from .. import types as T
+        kind, _ = self._args(uri)
+        dt = {"range": T.Int32, "terasort": T.Pickle, "points": T.Vector(T.Float32, 128)}.get(kind)
+        return {"dtype": dt}
 
     def delete(self, uri):
         raise DryadLinqException(0, "generator stores are read-only")
@@ -288,6 +298,9 @@ class GenProvider(DataProvider):
         if kind == "terasort":
             from ..models.terasort_cpu import gen_records
             return gen_records(lo, hi - lo, int(q.get("seed", 0)))
+        if kind == "points":
+            from ..models.kmeans_cpu import gen_point_records
+            return gen_point_records(lo, hi - lo, int(q.get("blobs", 64)), int(q.get("seed", 0)))
         raise DryadLinqException(ErrorCode.UnrecognizedDataSource, f"unknown generator {kind}")
 
     def temp_uri(self, name):

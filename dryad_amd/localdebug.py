@@ -103,6 +103,10 @@ class LocalEvaluator:
             return s0
         if op == "Apply":
             f = a["func"]
+            from .attributes import is_device_function
+            if is_device_function(f):
+                from .device_udf import call_on_records
+                return call_on_records(f, srcs, [s.dtype for s in n.sources], bool(a.get("multi")))
             if a.get("multi"):
                 return f([s0] + srcs[1:]) if len(srcs) > 1 else f([s0])
             return f(*srcs)

@@ -92,7 +92,7 @@ _M64 = (1 << 64) - 1
 # expected run length the segmented phase is sized for (window = smallest multiple of 8 bits with
 # n / 2^window <= RUN_TARGET); overridable for tuning
 import os as _os  # noqa: E402
-RUN_TARGET = int(_os.environ.get("DRYAD_SORT_RUN_TARGET", "128"))
+RUN_TARGET = int(_os.environ.get("DRYAD_SORT_RUN_TARGET", "16"))
 
 
 def _mask_words(begin_bit: int, end_bit: int) -> tuple[int, int]:

@@ -26,6 +26,7 @@ import torch.distributed as dist
 from ..compiler.planner import compile_queries
 from ..errors import DryadLinqException, DryadLinqJobException, ErrorCode
 from ..gpu import ops as G
+from ..attributes import is_device_function
 from ..gpu.table import DeviceTable, Ported, from_objects
 from ..gpu.trace import NotTraceable
 from ..io.providers import parse_uri, provider_for
@@ -45,6 +46,10 @@ class GpuVertexContext(V.VertexContext):
         self.device = device
         self.world = world
         self.runner = runner
+
+    def alloc_tensor(self, shape, dtype):
+        """Plain device allocation for a vertex's own (non-row) tables."""
+        return torch.empty(shape, dtype=dtype, device=self.device)
 
     def alloc_rows(self, n, stride):
         """Large row tables come from the executor's HBM pool (reused across jobs)."""
@@ -370,7 +375,8 @@ class GpuJobRunner:
     def _run_op(self, op, args, vctx, s):
         name = op["op"]
         fn = G.OPS.get(name) if self.gpu_ok else None
-        if fn is not None and all(a is None or isinstance(a, DeviceTable) for a in args):
+        device_apply = name == "apply" and is_device_function(op["fn"])
+        if fn is not None and (device_apply or all(a is None or isinstance(a, DeviceTable) for a in args)):
             try:
                 return fn(op, [a for a in args] if args else [], vctx)
             except NotTraceable as e:

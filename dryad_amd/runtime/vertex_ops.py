@@ -472,6 +472,10 @@ def op_range_partition(op, inputs, v):
 # ---------------------------------------------------------------------------------------------
 def op_apply(op, inputs, v):
     f = op["fn"]
+    from ..attributes import is_device_function
+    if is_device_function(f):
+        from ..device_udf import call_on_records
+        return call_on_records(f, list(inputs), op.get("in_dtypes") or [], bool(op.get("multi")))
     if op.get("multi"):
         res = f(list(inputs))
     else:

@@ -187,6 +187,38 @@ class ArrayT(DType):
         return []
 
 
+class VectorT(DType):
+    """Fixed-dimension numeric vector (a k-means point, an embedding): the record is a tuple of
+    ``dim`` numbers.  Wire format = the reference's serialization of a ``float[]``/``double[]``
+    field (int32 length, then raw little-endian elements), so it is byte-compatible with an
+    ArrayT of the same element type.  In HBM a vector column is one ``[n, dim]`` tensor."""
+
+    def __init__(self, elem: DType, dim: int):
+        self.elem = elem
+        self.dim = int(dim)
+        self.name = f"Vector[{elem!r},{self.dim}]"
+        self.fixed_width = 4 + self.dim * elem.fixed_width if elem.fixed_width else None
+
+    def encode(self, w, v):
+        if len(v) != self.dim:
+            raise ValueError(f"{self.name}: got {len(v)} elements")
+        w.write_int32(self.dim)
+        for x in v:
+            self.elem.encode(w, x)
+
+    def decode(self, r):
+        n = r.read_int32()
+        return tuple(self.elem.decode(r) for _ in range(n))
+
+    def default(self):
+        return tuple(self.elem.default() for _ in range(self.dim))
+
+
+
+def Vector(elem: DType, dim: int) -> VectorT:
+    return VectorT(elem, dim)
+
+
 class RecordT(DType):
     """A user-defined record (dataclass or tuple): fields in declaration order.  If any field is
     a nullable reference type, a BitVector of null flags precedes the fields and null fields are
@@ -304,6 +336,9 @@ def record_type(cls) -> RecordT:
     return RecordT(fields, cls, nullable)
 
 
+VECTOR_MIN_DIM = 16
+
+
 def infer_type(v) -> DType:
     """Infer the DType of a Python value (ints default to Int32 when they fit, like C# literals)."""
     if isinstance(v, bool):
@@ -327,7 +362,19 @@ def infer_type(v) -> DType:
     if dataclasses.is_dataclass(v) and not isinstance(v, type):
         return record_type(type(v))
     if isinstance(v, tuple) and not hasattr(v, "_fields"):
+        # a wide homogeneous float tuple is a vector (k-means points, embeddings), not a record
+        if len(v) >= VECTOR_MIN_DIM and all(type(x) is float for x in v):
+            return VectorT(Float64, len(v))
         return RecordT([(f"Item{i + 1}", infer_type(x)) for i, x in enumerate(v)], tuple)
+    try:
+        import numpy as _np
+        if isinstance(v, _np.ndarray) and v.ndim == 1:
+            et = {_np.dtype("float32"): Float32, _np.dtype("float64"): Float64,
+                  _np.dtype("int32"): Int32, _np.dtype("int64"): Int64}.get(v.dtype)
+            if et is not None:
+                return VectorT(et, v.shape[0])
+    except ImportError:  # pragma: no cover
+        pass
     return Pickle
 
 

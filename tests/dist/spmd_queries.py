@@ -46,6 +46,15 @@ def main():
         b = list(build(g))
         ok = (a == b) if ordered else (canon(a) == canon(b))
         assert ok, f"rank {w.rank} {name}: {a[:8]} != {b[:8]}"
+    # one k-means iteration: device_function Apply with a broadcast centroid table + merge Apply
+    from dryad_amd.models.kmeans import step_query, POINT_T
+    from dryad_amd.models.kmeans_cpu import gen_points
+    cents = [tuple(r) for r in gen_points(0, 4, 5, 9).tolist()]
+    km = lambda c: step_query(c.FromStore("gen://points?count=3000&partitions=%d&blobs=5&seed=9" % g.PartitionCount),  # noqa: E731
+                              c.FromEnumerable(cents, dtype=POINT_T))
+    a, b = list(km(l)), list(km(g))
+    assert len(a) == len(b) == 4 and max(abs(x - y) for ra, rb in zip(a, b) for x, y in zip(ra, rb)) < 1e-5, \
+        f"rank {w.rank} kmeans"
     for name, f in [("count", lambda c: c.FromEnumerable(data).Count()),
                     ("sum", lambda c: c.FromEnumerable(data).Sum()),
                     ("max", lambda c: c.FromEnumerable(data).Max())]:

@@ -98,3 +98,14 @@ def test_fused_orderby_two_partitions_one_rank():
     c = _ctx(2)
     data = list(range(100_000, 0, -3))
     assert list(c.FromEnumerable(data).OrderBy(lambda x: x)) == sorted(data)
+
+
+def test_kmeans_job_on_device_matches_reference():
+    import numpy as np
+    from dryad_amd.models.kmeans import KMeansConfig, KMeansJob, reference
+    cfg = KMeansConfig(points_per_partition=150_000, k=16, blobs=16, iterations=4)
+    c = _ctx(2)
+    r = KMeansJob(c, cfg, partitions=2).run()
+    assert "apply" not in _fallback_ops(c), c._get_executor().last_result["fallbacks"]
+    ref = reference(cfg, 2, r.iterations)
+    np.testing.assert_allclose(r.centroids, ref, rtol=0, atol=2e-4)
