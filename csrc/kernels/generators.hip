@@ -1,0 +1,33 @@
+// Synthetic columnar stores for the secondary BASELINE configs (GroupBy-Aggregate, hash join).
+//
+// gen://records64: 64-byte records = 8 int64 fields (Key, V1..V7), record i of a global table:
+//   Key = mix64(seed ^ (i * G)) % nkeys            (uniform keys; nkeys sets the group count)
+//   Vj  = mix64((seed + j * H) ^ i) >> 33           (non-negative 31-bit values: sums of 2^32
+//                                                    records cannot overflow int64)
+// Counter based, so every rank materialises exactly its slice in HBM and a re-executed input
+// vertex regenerates identical data.  models/records_cpu.py is the numpy twin.
+#include "common.h"
+
+namespace {
+constexpr uint64_t kG = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t kH = 0xD1B54A32D192ED03ull;
+
+__global__ __launch_bounds__(256) void gen_records64_kernel(int64_t* const* __restrict__ cols, int ncols, uint64_t n,
+                                                            uint64_t first, uint64_t nkeys, uint64_t seed) {
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = first + r;
+    cols[0][r] = (int64_t)(mix64(seed ^ (i * kG)) % nkeys);
+    for (int j = 1; j < ncols; ++j) cols[j][r] = (int64_t)(mix64((seed + (uint64_t)j * kH) ^ i) >> 33);
+  }
+}
+}  // namespace
+
+// cols: device array of ncols (<= 8) device pointers to int64 columns of length n.
+DR_API int dr_gen_records64(int64_t* const* cols, int ncols, uint64_t n, uint64_t first, uint64_t nkeys,
+                            uint64_t seed, hipStream_t s) {
+  if (ncols < 1 || ncols > 8 || nkeys == 0) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  gen_records64_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(cols, ncols, n, first, nkeys, seed);
+  DR_LAUNCH_CHECK();
+  return 0;
+}

@@ -312,6 +312,9 @@ class Planner:
         key, elem, res, cmp = a["key_selector"], a.get("element_selector"), a.get("result_selector"), a.get("comparer")
         gb = dict(op="group_by", key=key, elem=elem, result=res, comparer=cmp, explain="group_by")
         if src.info.partition.is_partitioned_by(key, cmp):
+            d = decompose(res, elem) if res is not None else None
+            if d is not None:   # lets the device run it as one partial-aggregation pass
+                gb["decomp"] = d
             return self.pointwise(src, "GroupBy", [gb], DataSetInfo(src.info.partition if res is None else
                                                                     PartitionInfo.random(src.partitions)))
         n = self.P

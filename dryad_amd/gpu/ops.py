@@ -117,6 +117,14 @@ def op_read(op, inputs, v):
             KM.generate(x, lo, int(q.get("blobs", 64)), int(q.get("seed", 0)))
             from .. import types as T
             return DeviceTable.from_columns({"x": x}, Shape("vector", ["x"], T.Vector(T.Float32, KM.DIM)))
+        if kind == "records64":
+            from ..ops import relational as R
+            from ..models.records_cpu import FIELDS
+            ncols = int(q.get("cols", 8))
+            cols = [v.alloc_tensor((hi - lo,), torch.int64) for _ in range(ncols)]
+            R.gen_records64(cols, lo, int(q.get("keys", 1 << 20)), int(q.get("seed", 0)))
+            names = FIELDS[:ncols]
+            return DeviceTable.from_columns(dict(zip(names, cols)), Shape("tuple", names))
         if kind == "range":
             start = int(q.get("start", 0))
             a = torch.arange(start + lo, start + hi, dtype=torch.int32 if start + hi < 2**31 else torch.int64,
@@ -393,6 +401,12 @@ def op_group_final(op, inputs, v):
             vals.append(R.seg_reduce(col, srt, seg, nseg, R.OP_MAX, torch.int64).to(torch.bool))
         elif a.kind == "all":
             vals.append(R.seg_reduce(col, srt, seg, nseg, R.OP_MIN, torch.int64).to(torch.bool))
+    return _group_result(d, keys, vals, nseg)
+
+
+def _group_result(d, keys, vals, nseg):
+    """Substitute the per-group key/aggregate columns into the result-selector template."""
+    nkeys = len(keys)
     key = TR.Col(keys[0]) if nkeys == 1 else tuple(TR.Col(k) for k in keys)
     env = {"key": key, "aggs": [TR.Col(x) for x in vals]}
     try:
@@ -403,6 +417,27 @@ def op_group_final(op, inputs, v):
         raise NotTraceable(f"result template: {ex}")
     proto = DeviceTable(nseg, Shape("scalar", ["v"]), {"v": keys[0]})
     return TR.to_table(res, proto)
+
+
+def op_group_by(op, inputs, v):
+    """GroupBy over an already key-partitioned input (e.g. one partition): with a decomposable
+    result selector the partial aggregation pass is already the whole answer."""
+    d = op.get("decomp")
+    if d is None or op.get("elem") is not None:
+        raise NotTraceable("non-decomposable GroupBy")
+    tb = op_group_partial(dict(op, decomp=d), inputs, v)
+    nkeys = tb.group_meta["nkeys"]
+    keys = [tb.cols[f"k{i}"] for i in range(nkeys)]
+    vals = []
+    for j, a in enumerate(d.aggs):
+        col = tb.cols[f"a{j}"]
+        if a.kind == "avg":
+            vals.append(col / tb.cols[f"c{j}"].to(torch.float64))
+        elif a.kind in ("any", "all"):
+            vals.append(col.to(torch.bool))
+        else:
+            vals.append(col)
+    return _group_result(d, keys, vals, tb.n)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -255,7 +255,9 @@ class GenProvider(DataProvider):
     ``gen://terasort?records=N&partitions=P&seed=S`` yields 100-byte TeraSort records (as bytes on
     the object path, generated directly in HBM by the GPU executor);
     ``gen://points?count=N&partitions=P&blobs=B&seed=S`` yields 128-dim float32 blob points
-    (tuples on the object path, one [n, 128] HBM tensor on the GPU executor)."""
+    (tuples on the object path, one [n, 128] HBM tensor on the GPU executor);
+    ``gen://records64?count=N&partitions=P&keys=K&seed=S[&cols=C]`` yields 64-byte records of 8
+    int64 fields (Key uniform in [0, K), V1..V7 31-bit values), columnar in HBM."""
     scheme = "gen"
 
     def _args(self, uri):
@@ -269,6 +271,8 @@ class GenProvider(DataProvider):
             return p, int(q.get("records", 0)) * 100
         if kind == "points":
             return p, int(q.get("count", 0)) * 4 * 128
+        if kind == "records64":
+            return p, int(q.get("count", 0)) * 8 * int(q.get("cols", 8))
         return p, int(q.get("count", 0)) * 4
 
     def exists(self, uri):
@@ -278,6 +282,10 @@ class GenProvider(DataProvider):
         from .. import types as T
         kind, _ = self._args(uri)
         dt = {"range": T.Int32, "terasort": T.Pickle, "points": T.Vector(T.Float32, 128)}.get(kind)
+        if kind == "records64":
+            from ..models.records_cpu import FIELDS
+            ncols = int(self._args(uri)[1].get("cols", 8))
+            dt = T.RecordT([(f, T.Int64) for f in FIELDS[:ncols]], tuple)
         return {"dtype": dt}
 
     def delete(self, uri):
@@ -301,6 +309,10 @@ class GenProvider(DataProvider):
         if kind == "points":
             from ..models.kmeans_cpu import gen_point_records
             return gen_point_records(lo, hi - lo, int(q.get("blobs", 64)), int(q.get("seed", 0)))
+        if kind == "records64":
+            from ..models.records_cpu import gen_records
+            return gen_records(lo, hi - lo, int(q.get("keys", 1 << 20)), int(q.get("seed", 0)),
+                               int(q.get("cols", 8)))
         raise DryadLinqException(ErrorCode.UnrecognizedDataSource, f"unknown generator {kind}")
 
     def temp_uri(self, name):

@@ -125,3 +125,18 @@ def merge_join_pairs(outer_sorted: torch.Tensor, inner_sorted: torch.Tensor, lo_
     _lib.call("dr_join_emit", ptr(outer_sorted), ptr(inner_sorted), c_u64(no), ptr(lower), ptr(count), ptr(offs),
               ptr(oo), ptr(ii), stream_of(outer_sorted))
     return oo, ii, count
+
+
+_lib.register_signatures({"dr_gen_records64": (c_i32, [vp, c_i32, c_u64, c_u64, c_u64, c_u64, vp])})
+
+
+def gen_records64(cols: list, first: int, nkeys: int, seed: int):
+    """Fill int64 HBM columns (Key, V1..) with records first.. of gen://records64."""
+    n = cols[0].shape[0]
+    for c in cols:
+        _lib.require_gpu_tensor(c, "gen_records64")
+        assert c.dtype == torch.int64 and c.shape[0] == n
+    ptrs = torch.tensor([c.data_ptr() for c in cols], dtype=torch.int64, device=cols[0].device)
+    _lib.call("dr_gen_records64", ptr(ptrs), len(cols), c_u64(n), c_u64(first), c_u64(nkeys),
+              c_u64(seed & (2**64 - 1)), stream_of(cols[0]))
+    return cols

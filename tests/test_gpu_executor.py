@@ -109,3 +109,29 @@ def test_kmeans_job_on_device_matches_reference():
     assert "apply" not in _fallback_ops(c), c._get_executor().last_result["fallbacks"]
     ref = reference(cfg, 2, r.iterations)
     np.testing.assert_allclose(r.centroids, ref, rtol=0, atol=2e-4)
+
+
+def test_records64_generator_matches_numpy_twin():
+    import numpy as np
+    from dryad_amd.models.records_cpu import gen_columns
+    from dryad_amd.ops import relational as R
+    cols = [torch.empty(10_001, dtype=torch.int64, device="cuda") for _ in range(8)]
+    R.gen_records64(cols, 123, 1000, 7)
+    ref = gen_columns(123, 10_001, 1000, 7)
+    for c, r in zip(cols, ref):
+        np.testing.assert_array_equal(c.cpu().numpy(), r)
+
+
+def test_groupby_records64_on_device():
+    src = "gen://records64?count=300000&partitions=2&keys=5000&seed=3"
+    _same(lambda c: c.FromStore(src).GroupBy(
+        lambda r: r[0], lambda k, g: (k, g.Count(), g.Sum(lambda r: r[1]), g.Min(lambda r: r[2]),
+                                      g.Max(lambda r: r[3]))), parts=2,
+        device_ops=("read", "group_partial", "group_final"))
+
+
+def test_groupby_single_partition_on_device():
+    src = "gen://records64?count=200000&partitions=1&keys=3000&seed=5"
+    _same(lambda c: c.FromStore(src).GroupBy(
+        lambda r: r[0], lambda k, g: (k, g.Count(), g.Sum(lambda r: r[1]), g.Average(lambda r: r[2]),
+                                      g.Max(lambda r: r[3]))), parts=1, device_ops=("read", "group_by"))
