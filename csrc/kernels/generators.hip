@@ -4,6 +4,11 @@
 //   Key = mix64(seed ^ (i * G)) % nkeys            (uniform keys; nkeys sets the group count)
 //   Vj  = mix64((seed + j * H) ^ i) >> 33           (non-negative 31-bit values: sums of 2^32
 //                                                    records cannot overflow int64)
+// gen://records64?...&mode=dim: a "dimension table" whose keys are a bijection of [0, nkeys)
+//   Key = (i * A + seed) % nkeys   (A odd, coprime with nkeys — the caller picks it)
+//   Vj  = mix64((seed + j * H) ^ Key) >> 33        (payload is a function of the key, so a join's
+//                                                    expected result can be computed from the probe
+//                                                    side alone)
 // Counter based, so every rank materialises exactly its slice in HBM and a re-executed input
 // vertex regenerates identical data.  models/records_cpu.py is the numpy twin.
 #include "common.h"
@@ -13,21 +18,56 @@ constexpr uint64_t kG = 0x9E3779B97F4A7C15ull;
 constexpr uint64_t kH = 0xD1B54A32D192ED03ull;
 
 __global__ __launch_bounds__(256) void gen_records64_kernel(int64_t* const* __restrict__ cols, int ncols, uint64_t n,
-                                                            uint64_t first, uint64_t nkeys, uint64_t seed) {
+                                                            uint64_t first, uint64_t nkeys, uint64_t seed,
+                                                            uint64_t dim_mult) {
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t i = first + r;
-    cols[0][r] = (int64_t)(mix64(seed ^ (i * kG)) % nkeys);
-    for (int j = 1; j < ncols; ++j) cols[j][r] = (int64_t)(mix64((seed + (uint64_t)j * kH) ^ i) >> 33);
+    if (dim_mult) {
+      const uint64_t key = (uint64_t)(((unsigned __int128)i * dim_mult + seed) % nkeys);
+      cols[0][r] = (int64_t)key;
+      for (int j = 1; j < ncols; ++j) cols[j][r] = (int64_t)(mix64((seed + (uint64_t)j * kH) ^ key) >> 33);
+    } else {
+      cols[0][r] = (int64_t)(mix64(seed ^ (i * kG)) % nkeys);
+      for (int j = 1; j < ncols; ++j) cols[j][r] = (int64_t)(mix64((seed + (uint64_t)j * kH) ^ i) >> 33);
+    }
+  }
+}
+
+// Row-major twin: out[r * ncols + j] (a 64-byte row store when ncols = 8).
+__global__ __launch_bounds__(256) void gen_records64_rows_kernel(int64_t* __restrict__ out, int ncols, uint64_t n,
+                                                                 uint64_t first, uint64_t nkeys, uint64_t seed,
+                                                                 uint64_t dim_mult) {
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = first + r;
+    int64_t* o = out + r * ncols;
+    if (dim_mult) {
+      const uint64_t key = (uint64_t)(((unsigned __int128)i * dim_mult + seed) % nkeys);
+      o[0] = (int64_t)key;
+      for (int j = 1; j < ncols; ++j) o[j] = (int64_t)(mix64((seed + (uint64_t)j * kH) ^ key) >> 33);
+    } else {
+      o[0] = (int64_t)(mix64(seed ^ (i * kG)) % nkeys);
+      for (int j = 1; j < ncols; ++j) o[j] = (int64_t)(mix64((seed + (uint64_t)j * kH) ^ i) >> 33);
+    }
   }
 }
 }  // namespace
 
 // cols: device array of ncols (<= 8) device pointers to int64 columns of length n.
+// dim_mult != 0 selects the dimension-table mode (key = (i * dim_mult + seed) % nkeys).
 DR_API int dr_gen_records64(int64_t* const* cols, int ncols, uint64_t n, uint64_t first, uint64_t nkeys,
-                            uint64_t seed, hipStream_t s) {
+                            uint64_t seed, uint64_t dim_mult, hipStream_t s) {
   if (ncols < 1 || ncols > 8 || nkeys == 0) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
-  gen_records64_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(cols, ncols, n, first, nkeys, seed);
+  gen_records64_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(cols, ncols, n, first, nkeys, seed, dim_mult);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+DR_API int dr_gen_records64_rows(int64_t* out, int ncols, uint64_t n, uint64_t first, uint64_t nkeys, uint64_t seed,
+                                 uint64_t dim_mult, hipStream_t s) {
+  if (ncols < 1 || ncols > 8 || nkeys == 0) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  gen_records64_rows_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(out, ncols, n, first, nkeys, seed, dim_mult);
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -122,7 +122,9 @@ def op_read(op, inputs, v):
             from ..models.records_cpu import FIELDS
             ncols = int(q.get("cols", 8))
             cols = [v.alloc_tensor((hi - lo,), torch.int64) for _ in range(ncols)]
-            R.gen_records64(cols, lo, int(q.get("keys", 1 << 20)), int(q.get("seed", 0)))
+            from ..models.records_cpu import dim_multiplier
+            nk = int(q.get("keys", 1 << 20))
+            R.gen_records64(cols, lo, nk, int(q.get("seed", 0)), dim_multiplier(nk) if q.get("mode") == "dim" else 0)
             names = FIELDS[:ncols]
             return DeviceTable.from_columns(dict(zip(names, cols)), Shape("tuple", names))
         if kind == "range":

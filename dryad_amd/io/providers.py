@@ -257,7 +257,8 @@ class GenProvider(DataProvider):
     ``gen://points?count=N&partitions=P&blobs=B&seed=S`` yields 128-dim float32 blob points
     (tuples on the object path, one [n, 128] HBM tensor on the GPU executor);
     ``gen://records64?count=N&partitions=P&keys=K&seed=S[&cols=C]`` yields 64-byte records of 8
-    int64 fields (Key uniform in [0, K), V1..V7 31-bit values), columnar in HBM."""
+    int64 fields (Key uniform in [0, K), V1..V7 31-bit values), columnar in HBM; ``&mode=dim``
+    makes it a dimension table (keys a bijection of [0, K), payload a function of the key)."""
     scheme = "gen"
 
     def _args(self, uri):
@@ -311,8 +312,10 @@ class GenProvider(DataProvider):
             return gen_point_records(lo, hi - lo, int(q.get("blobs", 64)), int(q.get("seed", 0)))
         if kind == "records64":
             from ..models.records_cpu import gen_records
-            return gen_records(lo, hi - lo, int(q.get("keys", 1 << 20)), int(q.get("seed", 0)),
-                               int(q.get("cols", 8)))
+            from ..models.records_cpu import dim_multiplier
+            nk = int(q.get("keys", 1 << 20))
+            return gen_records(lo, hi - lo, nk, int(q.get("seed", 0)), int(q.get("cols", 8)),
+                               dim_multiplier(nk) if q.get("mode") == "dim" else 0)
         raise DryadLinqException(ErrorCode.UnrecognizedDataSource, f"unknown generator {kind}")
 
     def temp_uri(self, name):

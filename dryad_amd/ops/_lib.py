@@ -120,3 +120,65 @@ def require_gpu_tensor(t: torch.Tensor, what: str):
         raise ValueError(f"{what}: expected a device (HBM) tensor, got {t.device}")
     if not t.is_contiguous():
         raise ValueError(f"{what}: expected a contiguous tensor")
+
+
+_HIP = None
+
+
+def hip_runtime():
+    """The HIP runtime torch already mapped (same SONAME as /opt/rocm's)."""
+    global _HIP
+    if _HIP is None:
+        try:
+            _HIP = ctypes.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL)
+        except OSError:
+            _HIP = ctypes.CDLL(str(Path(torch.__file__).parent / "lib" / "libamdhip64.so"), mode=os.RTLD_GLOBAL)
+        _HIP.hipHostRegister.restype = c_i32
+        _HIP.hipHostRegister.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint]
+        _HIP.hipHostUnregister.restype = c_i32
+        _HIP.hipHostUnregister.argtypes = [vp]
+        _HIP.hipMemcpyAsync.restype = c_i32
+        _HIP.hipMemcpyAsync.argtypes = [vp, vp, ctypes.c_size_t, c_i32, vp]
+    return _HIP
+
+
+HIP_MEMCPY_H2D, HIP_MEMCPY_D2H = 1, 2
+
+
+def memcpy_async(dst: torch.Tensor, src: torch.Tensor, stream) -> None:
+    """Raw DMA copy between a device tensor and a registered (page-locked) host tensor on
+    ``stream`` (a torch stream).  torch does not know hipHostRegister'ed memory is pinned and
+    would stage such copies through a bounce buffer."""
+    n = src.numel() * src.element_size()
+    assert dst.numel() * dst.element_size() == n
+    if n == 0:
+        return
+    kind = HIP_MEMCPY_D2H if src.is_cuda else HIP_MEMCPY_H2D
+    check(hip_runtime().hipMemcpyAsync(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()), n, kind,
+                                       ctypes.c_void_p(stream.cuda_stream)), "hipMemcpyAsync")
+
+
+class PinnedHostBuffer:
+    """Exact-size page-locked host memory: a plain CPU tensor registered with hipHostRegister
+    (torch's pinned allocator rounds requests up to a power of two, which for 100 GB spill
+    buffers would double the host footprint)."""
+
+    def __init__(self, shape, dtype=torch.uint8):
+        self.tensor = torch.empty(shape, dtype=dtype)
+        nbytes = self.tensor.numel() * self.tensor.element_size()
+        self.registered = False
+        if nbytes:
+            check(hip_runtime().hipHostRegister(ctypes.c_void_p(self.tensor.data_ptr()), nbytes, 0), "hipHostRegister")
+            self.registered = True
+
+    def release(self):
+        if self.registered:
+            hip_runtime().hipHostUnregister(ctypes.c_void_p(self.tensor.data_ptr()))
+            self.registered = False
+        self.tensor = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:  # noqa: BLE001
+            pass

@@ -127,16 +127,27 @@ def merge_join_pairs(outer_sorted: torch.Tensor, inner_sorted: torch.Tensor, lo_
     return oo, ii, count
 
 
-_lib.register_signatures({"dr_gen_records64": (c_i32, [vp, c_i32, c_u64, c_u64, c_u64, c_u64, vp])})
+_lib.register_signatures({"dr_gen_records64": (c_i32, [vp, c_i32, c_u64, c_u64, c_u64, c_u64, c_u64, vp]),
+                          "dr_gen_records64_rows": (c_i32, [vp, c_i32, c_u64, c_u64, c_u64, c_u64, c_u64, vp])})
 
 
-def gen_records64(cols: list, first: int, nkeys: int, seed: int):
-    """Fill int64 HBM columns (Key, V1..) with records first.. of gen://records64."""
+def gen_records64_rows(out: torch.Tensor, first: int, nkeys: int, seed: int, dim_mult: int = 0):
+    """Row-major gen://records64: ``out`` int64 [n, ncols] (a [n, 64]-byte row store for 8 columns)."""
+    _lib.require_gpu_tensor(out, "gen_records64_rows")
+    assert out.dtype == torch.int64 and out.dim() == 2
+    _lib.call("dr_gen_records64_rows", ptr(out), out.shape[1], c_u64(out.shape[0]), c_u64(first), c_u64(nkeys),
+              c_u64(seed & (2**64 - 1)), c_u64(dim_mult), stream_of(out))
+    return out
+
+
+def gen_records64(cols: list, first: int, nkeys: int, seed: int, dim_mult: int = 0):
+    """Fill int64 HBM columns (Key, V1..) with records first.. of gen://records64
+    (``dim_mult`` != 0: dimension-table mode, key = (i * dim_mult + seed) % nkeys)."""
     n = cols[0].shape[0]
     for c in cols:
         _lib.require_gpu_tensor(c, "gen_records64")
         assert c.dtype == torch.int64 and c.shape[0] == n
     ptrs = torch.tensor([c.data_ptr() for c in cols], dtype=torch.int64, device=cols[0].device)
     _lib.call("dr_gen_records64", ptr(ptrs), len(cols), c_u64(n), c_u64(first), c_u64(nkeys),
-              c_u64(seed & (2**64 - 1)), stream_of(cols[0]))
+              c_u64(seed & (2**64 - 1)), c_u64(dim_mult), stream_of(cols[0]))
     return cols

@@ -1,5 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_gpu_executor.py -x -q > gpurun_out/t.log 2>&1; rc=$?; tail -3 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python benchmarks/groupby.py --records-per-gpu 1e8 --steps 2 > gpurun_out/gb_small.log 2>&1; rc=$?; tail -2 gpurun_out/gb_small.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python benchmarks/groupby.py --steps 2 > gpurun_out/gb_full.log 2>&1; rc=$?; tail -2 gpurun_out/gb_full.log; exit $rc
+timeout -k 10 600 python -m pytest tests/test_gpu_grace.py -x -q > gpurun_out/t.log 2>&1; rc=$?; tail -15 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python benchmarks/join.py --table-gb 4 --steps 2 --hbm-budget-gb 4 > gpurun_out/join_small_spill.log 2>&1; rc=$?; tail -1 gpurun_out/join_small_spill.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 900 python benchmarks/join.py --steps 2 > gpurun_out/join_full.log 2>&1; rc=$?; tail -2 gpurun_out/join_full.log; exit $rc
