@@ -43,6 +43,8 @@ def _check(t):
 # ---------------------------------------------------------------------------------------------
 # key handling
 def key_entries(table: DeviceTable, key_fn, comparer=None, descending=False):
+    if table.heap is not None:
+        raise NotTraceable("string keys")
     """-> (entries [n,2], begin_bit, lo_mask).  Keys compare like the object path's default order."""
     if comparer is not None:
         raise NotTraceable("custom comparer")
@@ -134,6 +136,18 @@ def op_read(op, inputs, v):
             return DeviceTable.from_columns({"v": a}, Shape("scalar", ["v"]))
     if scheme == "hbm":
         return provider_for(uri).get(uri)["local"][v.partition]
+    if scheme == "text":
+        # raw bytes -> HBM heap -> line (offset, length) pairs on the device
+        from ..ops import text as TX
+        from .table import text_table
+        from .. import types as T
+        data = provider_for(uri).read_partition_bytes(uri, v.partition)
+        heap = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(v.device) if data else \
+            torch.zeros(0, dtype=torch.uint8, device=v.device)
+        off, ln = TX.lines(heap)
+        t = text_table(heap, off, ln, T.LineRecord)
+        t.whole_heap = True           # every line of the heap, in order (tokenise the heap directly)
+        return t
     recs = provider_for(uri).read_partition(uri, v.partition, op.get("dtype"))
     t = from_objects(recs, op.get("dtype"), v.device)
     if t is None:
@@ -445,6 +459,8 @@ def op_group_by(op, inputs, v):
 # ---------------------------------------------------------------------------------------------
 def op_distinct(op, inputs, v):
     t = _check(_one(inputs))
+    if t.heap is not None:
+        raise NotTraceable("string records")
     if op.get("comparer") is not None:
         raise NotTraceable("custom comparer")
     if t.n <= 1:
@@ -522,10 +538,9 @@ def op_apply(op, inputs, v):
                           bool(op.get("multi")), v.device)
     if isinstance(res, DeviceTable):
         return res
-    out = from_objects(list(res), None, v.device)
-    if out is None:
-        raise NotTraceable("device_function returned non-columnar records")
-    return out
+    res = list(res)
+    out = from_objects(res, None, v.device) if res else None
+    return out if out is not None else res      # non-columnar results travel as host records
 
 
 OPS = {k[3:]: fn for k, fn in list(globals().items()) if k.startswith("op_")}

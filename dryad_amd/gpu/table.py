@@ -6,7 +6,9 @@ A partition in HBM is a ``DeviceTable``: either
     the key is a byte-string field ``(key_off, key_len)`` compared in memcmp order, or
   * ``cols``  — struct-of-arrays: an ordered dict of equally long 1-D tensors (one per record
     field), with a ``shape`` describing how fields map back to Python records: a scalar, a tuple,
-    a dataclass, or a LineRecord-free fixed record.
+    a dataclass, or a LineRecord-free fixed record, or
+  * ``text``  — strings / LineRecords: one UTF-8 byte ``heap`` plus ``off``/``len`` columns (line
+    splitting and tokenising happen on the heap in place: ops/text.py).
 
 The DryadLINQ ``channel`` between two vertices on the same GPU is a DeviceTable handed over by
 reference (zero copy); across GPUs it is packed into one uint8 row buffer and moved with RCCL.
@@ -40,11 +42,13 @@ class Shape:
 
 
 class DeviceTable:
-    def __init__(self, n: int, shape: Shape, cols: dict | None = None, rows: torch.Tensor | None = None):
+    def __init__(self, n: int, shape: Shape, cols: dict | None = None, rows: torch.Tensor | None = None,
+                 heap: torch.Tensor | None = None):
         self.n = int(n)
         self.shape = shape
         self.cols = cols if cols is not None else {}
         self.rows = rows
+        self.heap = heap              # text tables: the byte heap the off/len columns point into
 
     # ------------------------------------------------------------------ construction
     @staticmethod
@@ -92,14 +96,15 @@ class DeviceTable:
     def slice(self, a: int, b: int) -> "DeviceTable":
         if self.rows is not None:
             return DeviceTable(b - a, self.shape, rows=self.rows[a:b])
-        return DeviceTable(b - a, self.shape, {k: v[a:b] for k, v in self.cols.items()})
+        return DeviceTable(b - a, self.shape, {k: v[a:b] for k, v in self.cols.items()}, heap=self.heap)
 
     def take(self, idx: torch.Tensor) -> "DeviceTable":
         """Gather rows by an int64 index tensor (HIP row gather for row tables)."""
         if self.rows is not None:
             from ..ops import sort as S
             return DeviceTable(idx.shape[0], self.shape, rows=S.gather_rows(self.rows, index=idx.contiguous()))
-        return DeviceTable(idx.shape[0], self.shape, {k: v.index_select(0, idx) for k, v in self.cols.items()})
+        return DeviceTable(idx.shape[0], self.shape, {k: v.index_select(0, idx) for k, v in self.cols.items()},
+                           heap=self.heap)
 
     def mask(self, m: torch.Tensor) -> "DeviceTable":
         idx = torch.nonzero(m, as_tuple=False).flatten()
@@ -115,12 +120,22 @@ class DeviceTable:
             return t0
         if t0.rows is not None:
             return DeviceTable(sum(t.n for t in tables), t0.shape, rows=torch.cat([t.rows for t in tables]))
+        if t0.heap is not None:
+            offs, base = [], 0
+            for t in tables:
+                offs.append(t.cols["off"] + base)
+                base += t.heap.shape[0]
+            return DeviceTable(sum(t.n for t in tables), t0.shape,
+                               {"off": torch.cat(offs), "len": torch.cat([t.cols["len"] for t in tables])},
+                               heap=torch.cat([t.heap for t in tables]))
         return DeviceTable(sum(t.n for t in tables), t0.shape,
                            {k: torch.cat([t.cols[k] for t in tables]) for k in t0.cols})
 
     # ------------------------------------------------------------------ packing for RCCL
     def pack(self) -> torch.Tensor:
         """One uint8 [n, row_bytes] buffer (AoS) so an exchange is a single collective."""
+        if self.heap is not None:
+            raise TypeError("text tables are exchanged as records")
         if self.rows is not None:
             return self.rows
         parts = [v.contiguous().view(torch.uint8).reshape(self.n, _width(v)) for v in self.cols.values()]
@@ -146,6 +161,13 @@ class DeviceTable:
         if self.rows is not None:
             a = self.rows.cpu().numpy()
             return [bytes(r) for r in a]
+        if self.heap is not None:
+            from ..ops.text import gather_strings
+            strs = gather_strings(self.heap, self.cols["off"], self.cols["len"]) if self.heap.is_cuda else \
+                _host_strings(self.heap, self.cols["off"], self.cols["len"])
+            if self.shape.pytype is not None and self.shape.pytype is not str:
+                return [self.shape.pytype(x) for x in strs]
+            return strs
         arrs = {k: v.cpu().numpy() for k, v in self.cols.items()}
         sh = self.shape
         if sh.kind == "scalar":
@@ -158,6 +180,16 @@ class DeviceTable:
         if sh.kind == "dataclass":
             return [sh.pytype(*vals) for vals in zip(*lists)]
         raise ValueError(sh.kind)
+
+
+def _host_strings(heap, off, ln) -> list:
+    b = heap.numpy().tobytes()
+    return [b[o:o + n].decode("utf-8", "replace") for o, n in zip(off.tolist(), ln.tolist())]
+
+
+def text_table(heap: torch.Tensor, off: torch.Tensor, ln: torch.Tensor, pytype=None) -> "DeviceTable":
+    """A text (string / LineRecord) table over a byte heap."""
+    return DeviceTable(off.shape[0], Shape("text", ["off", "len"], pytype), {"off": off, "len": ln}, heap=heap)
 
 
 def _width(v: torch.Tensor) -> int:
@@ -203,6 +235,15 @@ def from_objects(records: list, dt, device) -> DeviceTable | None:
     """Ingress: Python records -> DeviceTable (None if the type is not columnar)."""
     if dt is None:
         dt = T.infer_common_type(records[:1000]) if records else T.Int32
+    if dt in (T.LineRecordT, T.String):
+        strs = [r.Line if isinstance(r, T.LineRecord) else r for r in records]
+        enc = [x.encode("utf-8") for x in strs]
+        ln = np.asarray([len(x) for x in enc], dtype=np.int64)
+        off = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.int64) if len(enc) else np.zeros(0, np.int64)
+        heap = torch.frombuffer(bytearray(b"".join(enc)), dtype=torch.uint8) if enc and ln.sum() else \
+            torch.zeros(0, dtype=torch.uint8)
+        return text_table(heap.to(device), torch.from_numpy(off).to(device), torch.from_numpy(ln).to(device),
+                          T.LineRecord if dt == T.LineRecordT else str)
     if not columnar_dtype(dt):
         return None
     if isinstance(dt, T.VectorT):

@@ -173,6 +173,8 @@ class RecProxy:
 
 
 def proxy(table: DeviceTable):
+    if table.shape.kind in ("text", "vector"):
+        raise NotTraceable(f"lambdas over {table.shape.kind} records run on the host")
     if table.shape.kind == "rows":
         return RowProxy(table)
     if table.shape.kind == "scalar":

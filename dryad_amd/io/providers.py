@@ -322,7 +322,104 @@ class GenProvider(DataProvider):
         raise DryadLinqException(0, "generator stores are read-only")
 
 
-_PROVIDERS = {p.scheme: p for p in (PartfileProvider(), MemProvider(), HbmProvider(), GenProvider())}
+class TextProvider(DataProvider):
+    """Plain text files as LineRecord tables (reference A-8: LineRecord text I/O).
+
+    ``text:///path/to/file.txt?partitions=P`` splits one file into P byte ranges cut at line
+    boundaries; ``text:///path/to/dir`` (or a glob ``text:///path/part-*``) is one partition per
+    file.  Lines end at '\n' (a trailing '\r' is dropped).  Written tables are a directory of
+    part files ``part-%08X.txt``."""
+    scheme = "text"
+
+    def _spec(self, uri):
+        _, path, q = parse_uri(uri)
+        return path, q
+
+    def _files(self, uri):
+        import glob as _glob
+        path, _ = self._spec(uri)
+        if os.path.isdir(path):
+            return sorted(os.path.join(path, f) for f in os.listdir(path) if not f.startswith("."))
+        if any(ch in path for ch in "*?["):
+            return sorted(_glob.glob(path))
+        return [path]
+
+    def ranges(self, uri):
+        """[(file, start, end)] per partition, cut after a '\n'."""
+        files = self._files(uri)
+        _, q = self._spec(uri)
+        p = int(q.get("partitions", 0) or 0)
+        if len(files) != 1 or p <= 1:
+            return [(f, 0, os.path.getsize(f)) for f in files]
+        f = files[0]
+        size = os.path.getsize(f)
+        cuts = [0]
+        with open(f, "rb") as fh:
+            for k in range(1, p):
+                pos = max(cuts[-1], (size * k) // p)
+                fh.seek(pos)
+                if pos > 0:
+                    fh.seek(pos - 1)
+                    if fh.read(1) != b"\n":
+                        fh.readline()
+                cuts.append(min(size, fh.tell()))
+        cuts.append(size)
+        return [(f, cuts[i], cuts[i + 1]) for i in range(p)]
+
+    def stream_info(self, uri):
+        r = self.ranges(uri)
+        return len(r), sum(b - a for _, a, b in r)
+
+    def exists(self, uri):
+        return bool(self._files(uri)) and all(os.path.exists(f) for f in self._files(uri))
+
+    def delete(self, uri):
+        import shutil
+        path, _ = self._spec(uri)
+        if os.path.isdir(path):
+            shutil.rmtree(path)
+        elif os.path.exists(path):
+            os.remove(path)
+
+    def schema(self, uri):
+        from ..types import LineRecordT
+        return {"dtype": LineRecordT}
+
+    def read_partition_bytes(self, uri, i) -> bytes:
+        f, a, b = self.ranges(uri)[i]
+        with open(f, "rb") as fh:
+            fh.seek(a)
+            return fh.read(b - a)
+
+    def read_partition(self, uri, i, dtype):
+        from ..types import LineRecord
+        data = self.read_partition_bytes(uri, i)
+        if not data:
+            return []
+        lines = data.split(b"\n")
+        if lines and lines[-1] == b"":
+            lines.pop()
+        return [LineRecord(x[:-1].decode("utf-8", "replace") if x.endswith(b"\r") else x.decode("utf-8", "replace"))
+                for x in lines]
+
+    def write_table(self, uri, partitions, dtype, delete_if_exists=True):
+        path, _ = self._spec(uri)
+        if delete_if_exists:
+            self.delete(uri)
+        os.makedirs(path, exist_ok=True)
+        for i, recs in enumerate(partitions):
+            tmp = os.path.join(path, f".part-{i:08X}.tmp")
+            with open(tmp, "wb") as fh:
+                for r in recs:
+                    fh.write((r.Line if hasattr(r, "Line") else str(r)).encode("utf-8") + b"\n")
+            os.replace(tmp, os.path.join(path, f"part-{i:08X}.txt"))
+
+    def temp_uri(self, name):
+        root = os.environ.get("DRYAD_TEMP_DIR") or os.path.join(os.environ.get("TMPDIR", "/tmp"), "DryadLinqTemp")
+        return "text://" + os.path.join(root, name)
+
+
+_PROVIDERS = {p.scheme: p for p in (PartfileProvider(), MemProvider(), HbmProvider(), GenProvider(), TextProvider())}
 _PROVIDERS["file"] = _PROVIDERS["partfile"]
 
 

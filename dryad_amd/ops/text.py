@@ -1,0 +1,112 @@
+"""Device text operators (csrc/kernels/text.hip): line splitting and WordCount tokenisation.
+
+A partition's text lives in HBM as one byte heap; lines and tokens are (offset, length) int64
+pairs.  Whitespace = ' ', '\\t', '\\r', '\\n' (String.Split() with no arguments, which is what the
+reference's WordCount sample uses)."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from . import relational as R
+from . import sort as S
+from ._lib import c_u64, ptr, stream_of, vp, c_i32
+
+_lib.register_signatures({
+    "dr_text_marks": (c_i32, [vp, c_u64, vp, vp]),
+    "dr_token_hash": (c_i32, [vp, vp, vp, c_u64, vp, vp]),
+    "dr_token_verify": (c_i32, [vp, vp, vp, vp, c_u64, vp, vp]),
+})
+
+SPACE = b" \t\r\n"
+
+
+def marks(buf: torch.Tensor) -> torch.Tensor:
+    _lib.require_gpu_tensor(buf, "text.marks")
+    m = torch.empty(buf.shape[0], dtype=torch.uint8, device=buf.device)
+    _lib.call("dr_text_marks", ptr(buf), c_u64(buf.shape[0]), ptr(m), stream_of(buf))
+    return m
+
+
+def lines(buf: torch.Tensor, m: torch.Tensor | None = None):
+    """(offset, length) of every '\\n'-terminated line (a trailing '\\r' is dropped)."""
+    n = buf.shape[0]
+    if n == 0:
+        z = torch.empty(0, dtype=torch.int64, device=buf.device)
+        return z, z
+    m = marks(buf) if m is None else m
+    st = torch.nonzero(m & 1, as_tuple=False).flatten()
+    nxt = torch.cat([st[1:], torch.tensor([n], dtype=torch.int64, device=buf.device)])
+    ln = nxt - st
+    last_nl = torch.cat([(buf[st[1:] - 1] == 10), (buf[n - 1:n] == 10)])
+    ln = ln - last_nl.to(torch.int64)
+    # drop a trailing '\r' (CRLF files)
+    end = st + ln - 1
+    cr = (ln > 0) & (buf[end.clamp_min(0)] == 13)
+    ln = ln - cr.to(torch.int64)
+    return st, ln
+
+
+def tokens(buf: torch.Tensor, m: torch.Tensor | None = None):
+    """(offset, length) of every whitespace-separated token, in text order."""
+    if buf.shape[0] == 0:
+        z = torch.empty(0, dtype=torch.int64, device=buf.device)
+        return z, z
+    m = marks(buf) if m is None else m
+    st = torch.nonzero(m & 2, as_tuple=False).flatten()
+    en = torch.nonzero(m & 4, as_tuple=False).flatten()
+    return st, en - st + 1
+
+
+def token_hash(buf, off, ln) -> torch.Tensor:
+    out = torch.empty(off.shape[0], dtype=torch.int64, device=buf.device)
+    _lib.call("dr_token_hash", ptr(buf), ptr(off.contiguous()), ptr(ln.contiguous()), c_u64(off.shape[0]), ptr(out),
+              stream_of(buf))
+    return out
+
+
+def gather_strings(buf: torch.Tensor, off: torch.Tensor, ln: torch.Tensor) -> list:
+    """Host strings for (offset, length) pairs (one ragged device gather + one copy)."""
+    if off.numel() == 0:
+        return []
+    tot = int(ln.sum().item())
+    base = torch.repeat_interleave(off, ln)
+    starts = torch.cumsum(ln, 0) - ln
+    pos = base + (torch.arange(tot, device=buf.device) - torch.repeat_interleave(starts, ln))
+    data = buf.index_select(0, pos).cpu().numpy().tobytes()
+    lens = ln.cpu().tolist()
+    out, p = [], 0
+    for L in lens:
+        out.append(data[p:p + L].decode("utf-8", errors="replace"))
+        p += L
+    return out
+
+
+def word_count(buf: torch.Tensor) -> list:
+    """[(word, count)] of the whitespace tokens in ``buf`` (device hash-group + exact check)."""
+    off, ln = tokens(buf)
+    nt = off.shape[0]
+    if nt == 0:
+        return []
+    h = token_hash(buf, off, ln)
+    e = torch.empty((nt, 2), dtype=torch.int64, device=buf.device)
+    e[:, 1] = h
+    e[:, 0] = torch.arange(nt, dtype=torch.int64, device=buf.device)
+    srt = S.sort_entries_hybrid(e, 64)
+    seg, nseg, starts = R.segment_ids(srt, 0)
+    order = srt[:, 0] & 0xFFFFFFFF
+    rep_sorted = order.index_select(0, starts).index_select(0, seg)      # representative per sorted token
+    rep = torch.empty_like(rep_sorted)
+    rep[order] = rep_sorted
+    bad = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    _lib.call("dr_token_verify", ptr(buf), ptr(off), ptr(ln), ptr(rep), c_u64(nt), ptr(bad), stream_of(buf))
+    if int(bad.item()):
+        # 64-bit hash collision between different words: exact host path (never seen in practice)
+        from collections import Counter
+        words = gather_strings(buf, off, ln)
+        return list(Counter(words).items())
+    ends = torch.cat([starts[1:], torch.tensor([nt], dtype=torch.int64, device=buf.device)])
+    counts = (ends - starts).cpu().tolist()
+    reps = order.index_select(0, starts)
+    words = gather_strings(buf, off.index_select(0, reps), ln.index_select(0, reps))
+    return list(zip(words, counts))

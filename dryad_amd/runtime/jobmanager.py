@@ -252,16 +252,18 @@ class JobRunner:
                     dtype = _resolve_dtype(dtypes, fmt)
                 write_schema(path, dtype, fmt)
                 committed[uri] = meta
-            elif scheme in ("mem", "hbm"):
+            else:
+                # any other provider (mem, hbm, text, user-registered): hand it the records
                 from .worker import read_channel
                 parts = []
                 for p, v in enumerate(vids):
                     recs, _ = read_channel(self.output_part_path(s, p, v, self.g.completed_version(v)), -1)
                     parts.append(recs)
-                provider_for(uri).write_table(uri, parts, dtype)
+                prov = provider_for(uri)
+                if not hasattr(prov, "write_table"):
+                    raise DryadLinqException(ErrorCode.UnrecognizedDataSource, f"cannot write to {uri}")
+                prov.write_table(uri, parts, dtype)
                 committed[uri] = len(parts)
-            else:
-                raise DryadLinqException(ErrorCode.UnrecognizedDataSource, f"cannot write to {uri}")
             qn = s.output.get("qnode")
             if qn is not None and qn.dtype is None:
                 qn.dtype = dtype

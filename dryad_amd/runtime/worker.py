@@ -95,7 +95,10 @@ def write_output_part(stage, records, path: str, compress=False):
     if dtype is None or dtype == T.Pickle:
         dtype = T.infer_common_type(records[:1000]) if records else None
     uri = stage.output["uri"]
-    if stage.output.get("temp") or uri.startswith(("mem://", "hbm://")) or dtype is None or dtype == T.Pickle:
+    from ..io.providers import parse_uri
+    if stage.output.get("temp") or parse_uri(uri)[0] not in ("partfile", "file") or dtype is None \
+            or dtype == T.Pickle:
+        # non-partfile stores are committed by their provider from the channel records
         n = write_channel(path, records, compress)
         return n, (dtype.name if dtype is not None else None), "pickle"
     ser = stage.output.get("serializer")
