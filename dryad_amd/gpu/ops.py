@@ -148,7 +148,20 @@ def op_read(op, inputs, v):
         t = text_table(heap, off, ln, T.LineRecord)
         t.whole_heap = True           # every line of the heap, in order (tokenise the heap directly)
         return t
-    recs = provider_for(uri).read_partition(uri, v.partition, op.get("dtype"))
+    prov = provider_for(uri)
+    if scheme in ("partfile", "file") and v.device.type == "cuda":
+        # binary part of fixed-width records: bytes -> HBM -> columns with the device codec
+        from ..ops import codec as CD
+        sch = prov.schema(uri) or {}
+        dt = op.get("dtype") or sch.get("dtype")
+        if sch.get("format", "binary") == "binary" and dt is not None and CD.layout(dt) is not None:
+            data = prov.read_partition_bytes(uri, v.partition)
+            buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(v.device) if data else \
+                torch.zeros(0, dtype=torch.uint8, device=v.device)
+            t = CD.decode(buf, dt)
+            if t is not None:
+                return t
+    recs = prov.read_partition(uri, v.partition, op.get("dtype"))
     t = from_objects(recs, op.get("dtype"), v.device)
     if t is None:
         raise NotTraceable("non-columnar store records")

@@ -527,6 +527,8 @@ class GpuJobRunner:
                                             "bytes": sum(_object_bytes(v) for v in tabs.values()),
                                             "pins": pins, "pool": self.pool})
                 committed[uri] = s.partitions
+            elif scheme in ("partfile", "file") and self._commit_partfile(s, uri, path, local):
+                committed[uri] = s.partitions
             else:
                 # host stores: every rank ships its partitions' records to rank 0, which writes them
                 objs = {p: _to_objects(v) if not isinstance(v, list) else v for p, v in local.items()}
@@ -559,6 +561,59 @@ class GpuJobRunner:
             if qn is not None:
                 qn.args["_executed"] = True
         return committed
+
+
+def _commit_partfile_impl(runner, s, uri, path, local):
+    """Partfile output written in parallel: every rank encodes its own partitions (device codec
+    for fixed-width columnar tables, host encoder otherwise) into tmp part files, rank 0 commits
+    the metadata by rename (reference DrPartitionFile.cpp:463-600).  Returns False when the
+    record type has to be inferred from the data on the host (then rank 0 writes everything)."""
+    from .. import types as T
+    from ..io import binary as B
+    from ..io import partfile as PF
+    from ..ops import codec as CD
+    from .jobmanager import write_schema
+    W, me = runner.world.size, runner.world.rank
+    dt = s.dtype
+    if dt is None or dt == T.Pickle:
+        return False
+    prov = provider_for(uri)
+    if me == 0 and prov.exists(uri):
+        if s.output.get("delete_if_exists") or s.output.get("temp"):
+            prov.delete(uri)
+        else:
+            raise DryadLinqException(ErrorCode.JobToCreateTableFailed, f"output {uri} exists")
+    if W > 1:
+        runner.world.barrier()
+    base = PF.default_base(path)
+    os.makedirs(os.path.dirname(base) or ".", exist_ok=True)
+    mine = {}
+    for p, v in local.items():
+        tmp = PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, 0)
+        data = CD.encode(v, dt) if isinstance(v, DeviceTable) and v.device.type == "cuda" else None
+        if data is not None:
+            with open(tmp, "wb") as f:
+                f.write(data.cpu().numpy().tobytes())
+        else:
+            B.write_records(tmp, dt, _to_objects(v) if not isinstance(v, list) else v)
+        mine[p] = tmp
+    gathered = [None] * W
+    if W > 1:
+        dist.all_gather_object(gathered, mine)
+    else:
+        gathered = [mine]
+    if me == 0:
+        parts = {}
+        for d in gathered:
+            parts.update(d)
+        PF.commit_parts(path, base, [parts[p] for p in range(s.partitions)])
+        write_schema(path, dt, "binary")
+    if W > 1:
+        runner.world.barrier()
+    return True
+
+
+GpuJobRunner._commit_partfile = lambda self, s, uri, path, local: _commit_partfile_impl(self, s, uri, path, local)
 
 
 class GpuExecutor(_BaseExecutor):
