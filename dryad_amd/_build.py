@@ -110,9 +110,22 @@ def build_runtime(verbose: bool = False, force: bool = False) -> Path:
     return target
 
 
+LAUNCHER = NATIVE_DIR / "dryad-launch"
+
+
+def build_launcher(verbose: bool = False, force: bool = False) -> Path:
+    """The native per-GPU process launcher (csrc/launcher/dryad_launch.cpp)."""
+    NATIVE_DIR.mkdir(parents=True, exist_ok=True)
+    src = CSRC / "launcher" / "dryad_launch.cpp"
+    if force or _stale(LAUNCHER, [src]):
+        _run([os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", src, "-o", LAUNCHER], verbose)
+    return LAUNCHER
+
+
 def build_all(verbose: bool = False, force: bool = False):
     k = build_kernels(verbose, force)
     r = build_runtime(verbose, force)
+    build_launcher(verbose, force)
     return k, r
 
 
