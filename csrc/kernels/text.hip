@@ -21,7 +21,8 @@ __global__ __launch_bounds__(256) void text_marks_kernel(const uint8_t* __restri
     const uint8_t p = i ? buf[i - 1] : (uint8_t)'\n';
     const uint8_t q = (i + 1 < n) ? buf[i + 1] : (uint8_t)'\n';
     uint8_t m = 0;
-    if (p == '\n') m |= 1;                        // a line starts after every '\n' (and at 0)
+    // a line starts at 0 and after every "\n", "\r\n" or lone "\r" (DryadLinqTextReader.cs:217-240)
+    if (p == '\n' || (p == '\r' && c != '\n')) m |= 1;
     if (!is_space(c) && is_space(p)) m |= 2;
     if (!is_space(c) && is_space(q)) m |= 4;
     marks[i] = m;

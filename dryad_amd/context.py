@@ -103,6 +103,7 @@ _DEFAULTS = dict(
     ContainerMbMemory=None,
     ApplicationMasterMbMemory=None,
     GraphManagerNode=None,
+    FaultInjection=None,          # [{stage, partition, version, kind}] (SURVEY §5.3 FaultInjector)
 )
 
 _READONLY_AFTER_USE = set(_DEFAULTS) - {"LocalDebug"}
@@ -294,20 +295,59 @@ class DryadLinqContext:
         info.Wait()
         return info
 
-    def _do_while(self, source: Query, body, cond) -> Query:
+    def _do_while(self, source: Query, body, cond, checkpoint: str | None = None) -> Query:
+        """Client loop of DoWhile.  Every iteration is materialised (reference
+        DryadLinqQueryable.cs:1297-1305); with ``checkpoint`` (a partfile/text/hbm uri prefix) the
+        iterations are persistent tables ``<checkpoint>.iter<k>`` plus a state file, and a rerun
+        of the same loop resumes after the last completed iteration."""
+        import json as _json
         before = source
+        k = 0
+        state_path = None
+        if checkpoint is not None:
+            from .io.providers import parse_uri
+            scheme, path, _ = parse_uri(checkpoint)
+            if scheme in ("partfile", "file", "text"):
+                state_path = path + ".dowhile.json"
+            else:
+                state_path = os.path.join(os.environ.get("TMPDIR", "/tmp"),
+                                          "dryad-dowhile-" + checkpoint.replace("/", "_").replace(":", "_") + ".json")
+            if os.path.exists(state_path):
+                with open(state_path) as f:
+                    st = _json.load(f)
+                before = self.FromStore(st["table"])
+                k = st["iteration"]
+                if st.get("done"):
+                    return before
         while True:
             after = body(before)
             if not self._local_debug():
-                tmp = self.MakeTemporaryStreamUri()
-                st = after.ToStore(tmp)
-                st.node.args["_temp"] = True
+                if checkpoint is not None:
+                    tmp = f"{checkpoint}.iter{k + 1}"
+                    st = after.ToStore(tmp, delete_if_exists=True)
+                else:
+                    tmp = self.MakeTemporaryStreamUri()
+                    st = after.ToStore(tmp)
+                    st.node.args["_temp"] = True
                 self.SubmitAndWait(st)
                 after = Query(self, QNode("Table", (), dict(uri=tmp), st.node.dtype))
             else:
                 after = self.FromEnumerable(list(after), dtype=after.dtype)
             more = cond(before, after)
             val = more.Single() if isinstance(more, Query) else bool(more)
+            k += 1
+            if state_path is not None and not self._local_debug():
+                prev = before.node.args.get("uri") if before.node.op in ("Table", "FromStore") else None
+                tmp_state = state_path + ".tmp"
+                with open(tmp_state, "w") as f:
+                    _json.dump(dict(iteration=k, table=after.node.args["uri"], done=not val), f)
+                os.replace(tmp_state, state_path)          # commit the iteration
+                if prev and prev.startswith(f"{checkpoint}.iter"):
+                    from .io.providers import provider_for
+                    try:
+                        provider_for(prev).delete(prev)
+                    except Exception:  # noqa: BLE001
+                        pass
             if not val:
                 return after
             before = after

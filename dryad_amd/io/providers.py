@@ -327,7 +327,7 @@ class TextProvider(DataProvider):
 
     ``text:///path/to/file.txt?partitions=P`` splits one file into P byte ranges cut at line
     boundaries; ``text:///path/to/dir`` (or a glob ``text:///path/part-*``) is one partition per
-    file.  Lines end at '\n' (a trailing '\r' is dropped).  Written tables are a directory of
+    file.  Lines end at '\\n', '\\r\\n' or a lone '\\r' (Appendix C).  Written tables are a directory of
     part files ``part-%08X.txt``."""
     scheme = "text"
 
@@ -396,11 +396,11 @@ class TextProvider(DataProvider):
         data = self.read_partition_bytes(uri, i)
         if not data:
             return []
-        lines = data.split(b"\n")
+        import re
+        lines = re.split(rb"\r\n|\r|\n", data)
         if lines and lines[-1] == b"":
             lines.pop()
-        return [LineRecord(x[:-1].decode("utf-8", "replace") if x.endswith(b"\r") else x.decode("utf-8", "replace"))
-                for x in lines]
+        return [LineRecord(x.decode("utf-8", "replace")) for x in lines]
 
     def write_table(self, uri, partitions, dtype, delete_if_exists=True):
         path, _ = self._spec(uri)

@@ -29,7 +29,7 @@ def marks(buf: torch.Tensor) -> torch.Tensor:
 
 
 def lines(buf: torch.Tensor, m: torch.Tensor | None = None):
-    """(offset, length) of every '\\n'-terminated line (a trailing '\\r' is dropped)."""
+    """(offset, length) of every line ('\\n', '\\r\\n' or '\\r' separated, Appendix C)."""
     n = buf.shape[0]
     if n == 0:
         z = torch.empty(0, dtype=torch.int64, device=buf.device)
@@ -38,12 +38,12 @@ def lines(buf: torch.Tensor, m: torch.Tensor | None = None):
     st = torch.nonzero(m & 1, as_tuple=False).flatten()
     nxt = torch.cat([st[1:], torch.tensor([n], dtype=torch.int64, device=buf.device)])
     ln = nxt - st
-    last_nl = torch.cat([(buf[st[1:] - 1] == 10), (buf[n - 1:n] == 10)])
-    ln = ln - last_nl.to(torch.int64)
-    # drop a trailing '\r' (CRLF files)
-    end = st + ln - 1
-    cr = (ln > 0) & (buf[end.clamp_min(0)] == 13)
-    ln = ln - cr.to(torch.int64)
+    # strip the terminator: "\n", "\r\n" or a lone "\r" (the last line may have none)
+    last = buf[(nxt - 1).clamp_min(0)]
+    term = ((last == 10) | (last == 13)).to(torch.int64)
+    prev = buf[(nxt - 2).clamp_min(0)]
+    term = term + ((last == 10) & (prev == 13) & (ln >= 2)).to(torch.int64)
+    ln = ln - term
     return st, ln
 
 

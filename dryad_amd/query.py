@@ -426,10 +426,11 @@ class Query:
             raise DryadLinqException(0, "SlidingWindow requires windowSize >= 2")
         return self._q("SlidingWindow", func=func, window_size=int(window_size))
 
-    def DoWhile(self, body: Callable, cond: Callable) -> "Query":
+    def DoWhile(self, body: Callable, cond: Callable, checkpoint: str | None = None) -> "Query":
         """Client-side loop (reference DryadLinqQueryable.cs:1280-1306): materialise body(before)
-        each iteration; stop when cond(before, after) yields False."""
-        return self._ctx._do_while(self, body, cond)
+        each iteration; stop when cond(before, after) yields False.  ``checkpoint``: persist each
+        iteration under that uri prefix so a rerun resumes after the last completed iteration."""
+        return self._ctx._do_while(self, body, cond, checkpoint)
 
     def Fork(self, mapper, keys=None, per_record: bool = False):
         """Fork(mapper) -> MultiQuery with .First/.Second[/.Third]; Fork(keySel, keys) -> keyed."""

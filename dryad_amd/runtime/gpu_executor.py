@@ -33,6 +33,7 @@ from ..io.providers import parse_uri, provider_for
 from ..native import runtime as native_runtime
 from ..parallel import shuffle
 from ..parallel.comm import World, get_world, init_world
+from ..utils import trace as TRC
 from ..utils.log import get_logger
 from . import vertex_ops as V
 from .executor import _BaseExecutor
@@ -369,9 +370,11 @@ class GpuJobRunner:
         vctx = GpuVertexContext(p, s.partitions, self.vids[s.id][p], version, s, self.dev, self.world, self)
         inputs = [self._merge_streams(si, streams) for si, streams in zip(s.inputs, raw_inputs)]
         data = None
-        for i, op in enumerate(s.ops):
-            args = inputs if i == 0 else [data]
-            data = self._run_op(op, args, vctx, s)
+        with TRC.range(f"vertex {s.id}:{s.name}[{p}] v{version}"):
+            for i, op in enumerate(s.ops):
+                args = inputs if i == 0 else [data]
+                with TRC.range(op["op"]):
+                    data = self._run_op(op, args, vctx, s)
         return data
 
     def _run_op(self, op, args, vctx, s):
@@ -643,12 +646,51 @@ class GpuExecutor(_BaseExecutor):
                         raise DryadLinqException(ErrorCode.JobToCreateTableFailed,
                                                  f"output {st.output['uri']} already exists")
         runner = GpuJobRunner(self.ctx, plan, self.world, faults, self.pool)
-        res = runner.run()
+        job_dir = self._job_dir(plan) if self.world.rank == 0 else None
+        t0 = time.time()
+        res = None
+        try:
+            res = runner.run()
+        except BaseException as e:
+            if job_dir:
+                with open(os.path.join(job_dir, "log", "error.txt"), "w") as f:
+                    f.write(str(e))
+            raise
+        finally:
+            if job_dir:
+                evs = res["events"] if res else [json.loads(e) for e in runner.g.drain_events()]
+                with open(os.path.join(job_dir, "log", "events.jsonl"), "w") as f:
+                    for e in evs:
+                        f.write(json.dumps(e) + "\n")
+        if job_dir:
+            st = dict(res.get("statistics") or {})
+            st.update(executor="gpu", ranks=self.world.size, elapsed_s=time.time() - t0,
+                      stage_seconds=res.get("timings"), host_fallbacks=res.get("fallbacks"))
+            with open(os.path.join(job_dir, "statistics.json"), "w") as f:
+                json.dump(st, f, indent=1, default=str)
+        self.last_job_dir = job_dir
         self.last_result = res
         self.last_plan = plan
         if handle is not None:
             handle.events.extend(res["events"])
         return res
+
+    _seq = 0
+
+    def _job_dir(self, plan):
+        """LocalJobs-style job directory (plan, explain, Calypso-style events, statistics) so
+        ``python -m dryad_amd.tools.jobbrowser`` works on GPU jobs too."""
+        if not self.ctx._props.get("KeepJobDirectories", True):
+            return None
+        from .executor import dryad_home
+        GpuExecutor._seq += 1
+        d = os.path.join(dryad_home(self.ctx), "LocalJobs", f"gpu-{os.getpid()}-{int(time.time() * 1000) % 10**9}-{GpuExecutor._seq}")
+        os.makedirs(os.path.join(d, "log"), exist_ok=True)
+        with open(os.path.join(d, "plan.json"), "w") as f:
+            f.write(plan.dumps())
+        with open(os.path.join(d, "QueryGraph.txt"), "w") as f:
+            f.write(plan.explain())
+        return d
 
     def enumerate(self, q):
         node = q.node

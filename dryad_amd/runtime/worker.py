@@ -95,6 +95,12 @@ def write_output_part(stage, records, path: str, compress=False):
     if dtype is None or dtype == T.Pickle:
         dtype = T.infer_common_type(records[:1000]) if records else None
     uri = stage.output["uri"]
+    if not records and (dtype is None or dtype == T.Pickle) and not stage.output.get("temp"):
+        # an empty partition of an untyped output: a 0-byte part reads back as [] in every format,
+        # so it must not force the whole table to the pickle format
+        with open(path, "wb"):
+            pass
+        return 0, None, None
     from ..io.providers import parse_uri
     if stage.output.get("temp") or parse_uri(uri)[0] not in ("partfile", "file") or dtype is None \
             or dtype == T.Pickle:

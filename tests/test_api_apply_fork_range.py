@@ -131,3 +131,43 @@ def test_dowhile():
     for c in (local_ctx(), cluster_ctx()):
         r = sorted(c.FromEnumerable([1, 2, 3]).DoWhile(body, cond))
         assert r == [512, 1024, 1536]
+
+
+def test_do_while_checkpoint_resumes(tmp_path):
+    import dryad_amd as D
+    ck = f"partfile://{tmp_path}/loop"
+    calls = {"n": 0}
+
+    def body(q):
+        calls["n"] += 1
+        return q.Select(lambda x: x + 1)
+
+    def cond_stop_at(limit):
+        return lambda before, after: min(after) < limit
+
+    c = D.DryadLinqContext(2)
+    r1 = sorted(c.FromEnumerable([0, 10]).DoWhile(body, cond_stop_at(3), checkpoint=ck))
+    assert r1 == [3, 13] and calls["n"] == 3
+    # a rerun of the finished loop returns the committed result without executing the body
+    c2 = D.DryadLinqContext(2)
+    assert sorted(c2.FromEnumerable([0, 10]).DoWhile(body, cond_stop_at(3), checkpoint=ck)) == [3, 13]
+    assert calls["n"] == 3
+    # crash after 2 iterations, then resume: only the remaining iteration runs
+    ck2 = f"partfile://{tmp_path}/loop2"
+    calls["n"] = 0
+
+    def crashing(limit):
+        def cond(before, after):
+            if max(after) == 2:
+                raise RuntimeError("client crashed")
+            return max(after) < limit
+        return cond
+    try:
+        D.DryadLinqContext(2).FromEnumerable([0]).DoWhile(body, crashing(5), checkpoint=ck2)
+    except RuntimeError:
+        pass
+    assert calls["n"] == 2
+    calls["n"] = 0
+    # the state file still points at iteration 1 (the crash happened before committing 2)
+    r = list(D.DryadLinqContext(2).FromEnumerable([0]).DoWhile(body, cond_stop_at(5), checkpoint=ck2))
+    assert r == [5] and calls["n"] == 4

@@ -11,15 +11,15 @@ def _heap(s: bytes):
     return torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda()
 
 
-@pytest.mark.parametrize("text", [b"a b\r\nc  d\te\n\nlast", b"one\n", b"   \n\n", b"x", b""])
+@pytest.mark.parametrize("text", [b"a b\r\nc  d\te\n\nlast", b"one\n", b"   \n\n", b"x", b"", b"mac\rlines\r\rend\r"])
 def test_lines_and_tokens_match_python(text):
     from dryad_amd.ops import text as TX
     h = _heap(text) if text else torch.zeros(0, dtype=torch.uint8, device="cuda")
     off, ln = TX.lines(h)
-    exp_lines = text.split(b"\n")
+    import re
+    exp_lines = re.split(rb"\r\n|\r|\n", text)
     if exp_lines and exp_lines[-1] == b"":
         exp_lines.pop()
-    exp_lines = [x[:-1] if x.endswith(b"\r") else x for x in exp_lines]
     got = [text[o:o + n] for o, n in zip(off.tolist(), ln.tolist())]
     assert got == exp_lines
     to, tl = TX.tokens(h)
