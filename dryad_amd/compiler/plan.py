@@ -32,16 +32,19 @@ class StageInput:
     port: int = 0
     offset: int = 0
     merge_sort: dict | None = None      # k-way merge of sorted source ports: {key, comparer, descending}
+    group: int = 0                      # kind "group": partition j reads source partitions [j*g, (j+1)*g)
 
     def to_json(self):
         d = {"UniqueId": self.src, "ConnectionOperator": {"pointwise": "Pointwise", "cross": "CrossProduct",
                                                          "merge": "Pointwise", "broadcast": "CrossProduct",
-                                                         "offset": "Pointwise"}[self.kind],
+                                                         "offset": "Pointwise", "group": "Pointwise"}[self.kind],
              "Kind": self.kind, "Port": self.port}
         if self.offset:
             d["Offset"] = self.offset
         if self.merge_sort:
             d["MergeSort"] = True
+        if self.group:
+            d["GroupSize"] = self.group
         return d
 
 

@@ -95,6 +95,8 @@ _DEFAULTS = dict(
     PartitionCount=None,               # default partition count for shuffles (StaticConfig 8)
     MaxVertexFailures=6,               # DrGraphParameters: m_maxActiveFailureCount
     DynamicOptLevel=0x1,               # broadcast only (DryadLinqGlobals.cs:43-52)
+    AggregationTreeMaxInputs=150,      # aggregation tree: max inputs per vertex (DryadLinqApplication.cs:173-175)
+    AggregationTreeGroup=32,           # ... and partials folded per interior vertex
     HeadNode="localhost",
     DryadHomeDirectory=None,
     PartitionUncPath=None,

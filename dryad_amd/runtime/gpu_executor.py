@@ -187,6 +187,8 @@ class GpuJobRunner:
         if si.kind == "offset":
             q = p - si.offset
             return [q] if 0 <= q < src.partitions else []
+        if si.kind == "group":
+            return list(range(p * si.group, min(src.partitions, (p + 1) * si.group)))
         return list(range(src.partitions))
 
     # ------------------------------------------------------------------ channel transport

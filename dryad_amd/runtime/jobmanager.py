@@ -75,6 +75,9 @@ class JobRunner:
                     elif si.kind == "offset":
                         q = p - si.offset
                         pairs = [(self.vids[si.src][q], si.port)] if 0 <= q < src_stage.partitions else []
+                    elif si.kind == "group":
+                        pairs = [(self.vids[si.src][q], si.port)
+                                 for q in range(p * si.group, min(src_stage.partitions, (p + 1) * si.group))]
                     else:
                         raise DryadLinqException(0, f"unknown connection {si.kind}")
                     for src, port in pairs:

@@ -402,6 +402,46 @@ def op_agg_final(op, inputs, v):
     raise DryadLinqException(ErrorCode.OperatorNotSupported, f"aggregate {k}")
 
 
+def op_agg_combine(op, inputs, v):
+    """Fold a group of partial aggregates into ONE partial of the same shape (aggregation-tree
+    interior vertex: RecursiveAccumulate without FinalReduce)."""
+    s = op["spec"]
+    k = s["kind"]
+    parts = _one(inputs)
+    if k in ("Count", "Sum"):
+        tot = 0
+        for p in parts:
+            tot = tot + p
+        return [tot]
+    if k in ("Min", "Max"):
+        vals = [p for p in parts if p != _NONE]
+        if not vals:
+            return [_NONE]
+        return [E.Min(vals, None, s.get("comparer")) if k == "Min" else E.Max(vals, None, s.get("comparer"))]
+    if k == "Average":
+        return [(sum(p[0] for p in parts), sum(p[1] for p in parts))]
+    if k in ("Any", "Contains"):
+        return [any(parts)]
+    if k == "All":
+        return [all(parts)]
+    if k in ("First", "FirstOrDefault", "Last", "LastOrDefault"):
+        found = [p for p in parts if p[0]]
+        if not found:
+            return [(False, None)]
+        return [found[0] if k.startswith("First") else found[-1]]
+    if k in ("Single", "SingleOrDefault"):
+        n = sum(c for c, _ in parts)
+        x = next((x for c, x in parts if c), None)
+        return [(n, x)]
+    if k == "Aggregate":
+        assoc = s["assoc"]
+        acc = assoc.Seed()
+        for p in parts:
+            acc = assoc.RecursiveAccumulate(acc, p)
+        return [acc]
+    raise DryadLinqException(ErrorCode.OperatorNotSupported, f"aggregate {k}")
+
+
 def op_aggregate_seq(op, inputs, v):
     from ..localdebug import eval_scalar
     s = op["spec"]

@@ -227,3 +227,24 @@ def test_shared_subquery_tee():
 
 def test_sliding_window():
     both(lambda c: c.FromEnumerable(N[:20]).SlidingWindow(lambda w: sum(w), 3), ordered=True)
+
+
+def test_aggregation_tree_for_wide_aggregates():
+    import dryad_amd as D
+    c = D.DryadLinqContext(2)
+    c.PartitionCount = 40
+    c.AggregationTreeMaxInputs = 6
+    c.AggregationTreeGroup = 4
+    data = list(range(1, 2001))
+    q = c.FromEnumerable(data)
+    plan = c.Explain(q.Select(lambda x: x * 2).Where(lambda x: x % 3 == 0))
+    assert plan
+    assert q.Sum() == sum(data)
+    assert q.Count() == len(data)
+    assert q.Min() == 1 and q.Max() == 2000
+    assert abs(q.Average() - sum(data) / len(data)) < 1e-9
+    assert q.First(lambda x: x > 1500) == 1501 and q.Last(lambda x: x < 10) == 9
+    assert q.Any(lambda x: x == 1999) and not q.All(lambda x: x < 1000)
+    from dryad_amd.compiler.planner import compile_queries
+    p = compile_queries(c, [q.SumAsQuery()])
+    assert any("Combine" in s.name for s in p.stages)
