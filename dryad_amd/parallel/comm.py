@@ -55,12 +55,18 @@ def init_world(device: str | None = None, backend: str | None = None, timeout_s:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_cuda = (device == "cuda") or (device is None and torch.cuda.is_available())
+    # DRYAD_DIST_BACKEND=gloo with GPU ranks: collectives staged through host memory.  Lets
+    # several ranks share one GPU (RCCL needs distinct devices) so the multi-rank GPU data path
+    # can be tested on a single-GPU box.
+    be = backend or os.environ.get("DRYAD_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
     if use_cuda:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        idx = local_rank
+        if be != "nccl":
+            idx = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(idx)
+        dev = torch.device("cuda", idx)
     else:
         dev = torch.device("cpu")
-    be = backend or ("nccl" if use_cuda else "gloo")
     if size > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")

@@ -52,6 +52,14 @@ def alltoallv_bytes(send: torch.Tensor, send_counts: list[int], recv: torch.Tens
     assert len(send_counts) == w.size and len(recv_counts) == w.size
     total_s, total_r = sum(send_counts), sum(recv_counts)
     assert send.numel() >= total_s and recv.numel() >= total_r
+    if w.backend != "nccl" and (send.is_cuda or recv.is_cuda):
+        # gloo transport for device buffers (tests / shared-GPU ranks): stage through host memory
+        s_cpu = send[:total_s].cpu()
+        r_cpu = torch.empty(total_r, dtype=torch.uint8)
+        dist.all_to_all_single(r_cpu, s_cpu, output_split_sizes=list(recv_counts),
+                               input_split_sizes=list(send_counts))
+        recv[:total_r].copy_(r_cpu)
+        return recv
     maxpair = max(max(send_counts), max(recv_counts))
     if maxpair <= CHUNK_BYTES:
         dist.all_to_all_single(recv[:total_r], send[:total_s], output_split_sizes=list(recv_counts),

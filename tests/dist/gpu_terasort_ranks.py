@@ -1,0 +1,45 @@
+"""Multi-rank TeraSort through the query API on GPU ranks (run by tests/test_gpu_multirank.py
+with DRYAD_DIST_BACKEND=gloo so two ranks can share one GPU): sampling, separators, range_dest,
+partition pass, packed all-to-all-v, hybrid local sort with rank hi-bounds, validation."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+import torch  # noqa: E402
+
+from dryad_amd.models.terasort import TeraSortConfig, TeraSortQueryJob  # noqa: E402
+from dryad_amd.parallel.comm import init_world, shutdown  # noqa: E402
+
+
+def main():
+    w = init_world(device="cuda")
+    job = TeraSortQueryJob(TeraSortConfig(records_per_rank=int(os.environ.get("TS_RECORDS", "2000000"))), w)
+    expect = job.input_checksum()
+    for _ in range(2):
+        job.step()
+        v = job.validate(*expect)
+        assert v["ok"], (w.rank, v)
+    rep = job.executor_report()
+    assert "sort" not in {op for _, op, _ in rep["fallbacks"]}, rep["fallbacks"]
+    # a GroupBy with a cross shuffle and a join on device tables across ranks
+    import dryad_amd as D
+    g = D.DryadLinqContext(platform="gpu")
+    g.PartitionCount = w.size
+    src = "gen://records64?count=200000&partitions=%d&keys=1000&seed=3" % w.size
+    got = sorted(g.FromStore(src).GroupBy(lambda r: r[0], lambda k, gr: (k, gr.Count(), gr.Sum(lambda r: r[1]))))
+    l = D.DryadLinqContext(1)
+    l.LocalDebug = True
+    exp = sorted(l.FromStore(src).GroupBy(lambda r: r[0], lambda k, gr: (k, gr.Count(), gr.Sum(lambda r: r[1]))))
+    assert got == exp
+    fb = {op for _, op, _ in g._get_executor().last_result["fallbacks"]}
+    assert "group_partial" not in fb and "group_final" not in fb, fb
+    w.barrier()
+    if w.rank == 0:
+        print("MULTIRANK_OK", w.size, flush=True)
+    torch.cuda.synchronize()
+    shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,22 @@
+"""Two GPU ranks sharing one MI355X (gloo transport staged through the host): exercises the
+multi-rank GPU code paths (fused distributed OrderBy, cross shuffles of device tables) that the
+8-GPU RCCL run uses, on a single-GPU box."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.timeout(600)
+def test_two_ranks_share_one_gpu():
+    env = dict(os.environ, DRYAD_DIST_BACKEND="gloo", PYTHONPATH=ROOT, TS_RECORDS="2000000")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                          "--master-addr", "127.0.0.1", "--master-port", "29633",
+                          os.path.join(ROOT, "tests", "dist", "gpu_terasort_ranks.py")],
+                         capture_output=True, text=True, timeout=560, env=env, cwd=ROOT)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
+    assert "MULTIRANK_OK 2" in out.stdout
