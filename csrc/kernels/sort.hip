@@ -664,14 +664,14 @@ DR_API int dr_tie_fixup(E128* e, uint64_t n, uint32_t max_run, uint32_t* overflo
 // Hybrid sort, phase 2: segmented in-LDS sort of runs.  After a stable LSD sort on only the top
 // window of varying key bits (3 passes for ~1e9 uniform keys instead of 8-10), entries sharing
 // those bits form short runs (expected n / 2^window ~ 75).  Each workgroup owns the runs that
-// START in its 2048-entry core and reads up to 512 more entries so a run spilling past the core
+// START in its 2048-entry core and reads up to 256 more entries so a run spilling past the core
 // is finished by its owner; positions inside a run are permuted in place, which never changes the
 // run-id bits other workgroups read.  Rank of x in its run = #(y < x) + #(y == x, y before x)
 // on the masked key: a stable sort on [begin_bit, end_bit) whatever the unmasked bits hold.
 // Lanes of a wave walk the same run in lockstep, so the LDS reads are mostly broadcasts.
 // A run that does not end inside the window sets *overflow (caller falls back to full LSD).
 namespace {
-constexpr int kSegCore = 2048, kSegExt = 512, kSegWin = kSegCore + kSegExt, kSegPer = kSegWin / 256;  // 10
+constexpr int kSegCore = 2048, kSegExt = 256, kSegWin = kSegCore + kSegExt, kSegPer = kSegWin / 256;  // 9
 
 // Comparison keys: the run is fixed by masked hi >> B (B = run_shift), so only the 64 key bits
 // right below the run bits, k = (hi << (64 - B)) | (lo >> B), plus (REST) the masked low B bits
