@@ -164,6 +164,90 @@ __global__ __launch_bounds__(256) void seg_reduce_kernel(const T* vals, const E1
   else seg_reduce_body<T, OpSum<T>>(vals, ent, seg, n, out, op, ident);
 }
 
+// ----- fused multi-aggregate segmented reduction ------------------------------------------------
+// One pass over the sorted entries computes up to 8 aggregates (GroupBy's Count/Sum/Min/Max of
+// several columns): the segmented-scan predicates are computed once per wave and shared by all
+// aggregates, and a segment that starts and ends inside one wave (the common case: most groups
+// are short) is written with a plain store; only segments crossing a wave boundary use atomics.
+enum MultiOp : int { M_SUM_I = 0, M_MIN_I = 1, M_MAX_I = 2, M_COUNT = 3, M_SUM_F = 4, M_MIN_F = 5, M_MAX_F = 6 };
+constexpr int kMaxAggs = 8;
+struct AggSpecs {
+  int op[kMaxAggs];
+  const uint64_t* vals[kMaxAggs];
+  uint64_t* out[kMaxAggs];
+};
+
+__device__ __forceinline__ uint64_t m_combine(uint64_t a, uint64_t b, int op) {
+  switch (op) {
+    case M_SUM_I: case M_COUNT: return a + b;
+    case M_MIN_I: return (int64_t)b < (int64_t)a ? b : a;
+    case M_MAX_I: return (int64_t)b > (int64_t)a ? b : a;
+    case M_SUM_F: return (uint64_t)__double_as_longlong(__longlong_as_double((long long)a) + __longlong_as_double((long long)b));
+    case M_MIN_F: {
+      const double x = __longlong_as_double((long long)a), y = __longlong_as_double((long long)b);
+      return y < x ? b : a;
+    }
+    default: {
+      const double x = __longlong_as_double((long long)a), y = __longlong_as_double((long long)b);
+      return y > x ? b : a;
+    }
+  }
+}
+
+__device__ __forceinline__ void m_atomic(uint64_t* p, uint64_t v, int op) {
+  switch (op) {
+    case M_SUM_I: case M_COUNT: atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v); break;
+    case M_MIN_I: atomicMin(reinterpret_cast<long long*>(p), (long long)v); break;
+    case M_MAX_I: atomicMax(reinterpret_cast<long long*>(p), (long long)v); break;
+    case M_SUM_F: atomicAdd(reinterpret_cast<double*>(p), __longlong_as_double((long long)v)); break;
+    default: atomic_combine(reinterpret_cast<double*>(p), __longlong_as_double((long long)v), op == M_MIN_F ? 1 : 2);
+  }
+}
+
+__global__ __launch_bounds__(256) void seg_reduce_multi_kernel(const E128* __restrict__ ent,
+                                                               const int64_t* __restrict__ seg, uint64_t n,
+                                                               int nagg, AggSpecs sp) {
+  const int lane = lane_id();
+  const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const uint64_t w0 = (((uint64_t)blockIdx.x * blockDim.x) + threadIdx.x) >> 6;
+  for (uint64_t base = w0 * 64; base < n; base += waves * 64) {
+    const uint64_t i = base + lane;
+    const bool valid = i < n;
+    const int64_t s = valid ? seg[i] : -1 - (int64_t)lane;
+    const uint32_t row = valid ? (ent ? (uint32_t)ent[i].lo : (uint32_t)i) : 0u;
+    // same-segment predicates of the 6 scan steps, shared by every aggregate
+    uint32_t same = 0;
+#pragma unroll
+    for (int k = 0, d = 1; d < 64; d <<= 1, ++k) {
+      const int64_t os = __shfl_up(s, d, 64);
+      if (lane >= d && os == s) same |= 1u << k;
+    }
+    const int64_t prev = __shfl_up(s, 1, 64), next = __shfl_down(s, 1, 64);
+    bool head = lane > 0 ? prev != s : (i == 0 || !valid || seg[i - 1] != s);
+    bool end = lane < 63 ? next != s : true;
+    if (lane == 63 && valid && i + 1 < n) end = seg[i + 1] != s;
+    if (valid && i + 1 >= n) end = true;
+    const int64_t s0 = __shfl(s, 0, 64);
+    const bool h0 = __shfl(head, 0, 64);
+    const bool tail = valid && (lane == 63 || i + 1 >= n || next != s);
+    const bool plain = tail && end && (s != s0 || h0);
+    for (int a = 0; a < nagg; ++a) {
+      const int op = sp.op[a];
+      uint64_t v = 0;
+      if (valid) v = (op == M_COUNT) ? 1ull : sp.vals[a][row];
+#pragma unroll
+      for (int k = 0, d = 1; d < 64; d <<= 1, ++k) {
+        const uint64_t o = __shfl_up(v, d, 64);
+        if (same & (1u << k)) v = m_combine(v, o, op);
+      }
+      if (tail) {
+        if (plain) sp.out[a][s] = v;
+        else m_atomic(sp.out[a] + s, v, op);
+      }
+    }
+  }
+}
+
 // ----- merge join ----------------------------------------------------------------------------
 __device__ __forceinline__ bool key_less(const E128& a, const E128& b, uint64_t m) {
   return a.hi < b.hi || (a.hi == b.hi && (a.lo & m) < (b.lo & m));
@@ -299,6 +383,23 @@ DR_API int dr_seg_reduce(const void* vals, const E128* ent, const int64_t* seg, 
     const double ident = op == 1 ? __builtin_inf() : op == 2 ? -__builtin_inf() : 0.0;
     seg_reduce_kernel<double><<<g, 256, 0, s>>>((const double*)vals, ent, seg, n, (double*)out, op, ident);
   }
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// Fused multi-aggregate segmented reduce (see seg_reduce_multi_kernel).  ops/vals/outs: host
+// arrays of nagg (<= 8) entries; outputs must be pre-filled with each op's identity.
+DR_API int dr_seg_reduce_multi(const E128* ent, const int64_t* seg, uint64_t n, int nagg, const int* ops,
+                               const void* const* vals, void* const* outs, hipStream_t s) {
+  if (nagg < 1 || nagg > kMaxAggs) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  AggSpecs sp;
+  for (int a = 0; a < nagg; ++a) {
+    sp.op[a] = ops[a];
+    sp.vals[a] = reinterpret_cast<const uint64_t*>(vals[a]);
+    sp.out[a] = reinterpret_cast<uint64_t*>(outs[a]);
+  }
+  seg_reduce_multi_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(ent, seg, n, nagg, sp);
   DR_LAUNCH_CHECK();
   return 0;
 }

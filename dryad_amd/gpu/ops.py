@@ -379,19 +379,24 @@ def op_group_partial(op, inputs, v):
     seg, nseg, starts = R.segment_ids(srt, lo_mask)
     rows_at_start = _perm(srt).index_select(0, starts)
     out = {f"k{i}": c.index_select(0, rows_at_start) for i, c in enumerate(kcols)}
+    # every aggregate in one fused segmented-reduce pass
+    specs, names = [], []
     for j, a in enumerate(d.aggs):
         val = _agg_value(a, t)
         if a.kind == "count":
-            out[f"a{j}"] = R.seg_reduce(val, srt, seg, nseg, R.OP_COUNT if val is None else R.OP_SUM, torch.int64)
-        elif a.kind == "sum":
-            out[f"a{j}"] = R.seg_reduce(val, srt, seg, nseg, R.OP_SUM, val.dtype)
-        elif a.kind in ("min", "max"):
-            out[f"a{j}"] = R.seg_reduce(val, srt, seg, nseg, R.OP_MIN if a.kind == "min" else R.OP_MAX, val.dtype)
+            specs.append(("count", None, torch.int64) if val is None else ("sum", val, torch.int64))
+            names.append(f"a{j}")
+        elif a.kind in ("sum", "min", "max"):
+            specs.append((a.kind, val, val.dtype))
+            names.append(f"a{j}")
         elif a.kind == "avg":
-            out[f"a{j}"] = R.seg_reduce(val, srt, seg, nseg, R.OP_SUM, torch.float64)
-            out[f"c{j}"] = R.seg_reduce(None, srt, seg, nseg, R.OP_COUNT, torch.int64)
+            specs += [("sum", val, torch.float64), ("count", None, torch.int64)]
+            names += [f"a{j}", f"c{j}"]
         elif a.kind in ("any", "all"):
-            out[f"a{j}"] = R.seg_reduce(val, srt, seg, nseg, R.OP_MAX if a.kind == "any" else R.OP_MIN, torch.int64)
+            specs.append(("max" if a.kind == "any" else "min", val, torch.int64))
+            names.append(f"a{j}")
+    for nm, res in zip(names, R.seg_reduce_multi(srt, seg, nseg, specs)):
+        out[nm] = res
     tb = DeviceTable.from_columns(out, Shape("tuple", list(out)))
     tb.group_meta = dict(nkeys=len(kcols), aggs=d.aggs)
     return tb
@@ -413,23 +418,28 @@ def op_group_final(op, inputs, v):
     seg, nseg, starts = R.segment_ids(srt, lo_mask)
     rows_at_start = _perm(srt).index_select(0, starts)
     keys = [c.index_select(0, rows_at_start) for c in kcols]
-    vals = []
+    specs = []
     for j, a in enumerate(d.aggs):
         col = t.cols[f"a{j}"]
         if a.kind in ("count", "sum"):
-            r = R.seg_reduce(col, srt, seg, nseg, R.OP_SUM, col.dtype)
-            vals.append(r if col.dtype in (torch.int64, torch.float64) else r.to(col.dtype))
+            specs.append(("sum", col, col.dtype))
         elif a.kind in ("min", "max"):
-            r = R.seg_reduce(col, srt, seg, nseg, R.OP_MIN if a.kind == "min" else R.OP_MAX, col.dtype)
-            vals.append(r.to(col.dtype) if col.dtype != r.dtype else r)
+            specs.append((a.kind, col, col.dtype))
         elif a.kind == "avg":
-            s_ = R.seg_reduce(col, srt, seg, nseg, R.OP_SUM, torch.float64)
-            c_ = R.seg_reduce(t.cols[f"c{j}"], srt, seg, nseg, R.OP_SUM, torch.int64)
-            vals.append(s_ / c_.to(torch.float64))
-        elif a.kind == "any":
-            vals.append(R.seg_reduce(col, srt, seg, nseg, R.OP_MAX, torch.int64).to(torch.bool))
-        elif a.kind == "all":
-            vals.append(R.seg_reduce(col, srt, seg, nseg, R.OP_MIN, torch.int64).to(torch.bool))
+            specs += [("sum", col, torch.float64), ("sum", t.cols[f"c{j}"], torch.int64)]
+        elif a.kind in ("any", "all"):
+            specs.append(("max" if a.kind == "any" else "min", col, torch.int64))
+    res = iter(R.seg_reduce_multi(srt, seg, nseg, specs))
+    vals = []
+    for j, a in enumerate(d.aggs):
+        col = t.cols[f"a{j}"]
+        r = next(res)
+        if a.kind in ("count", "sum", "min", "max"):
+            vals.append(r if col.dtype in (torch.int64, torch.float64) else r.to(col.dtype))
+        elif a.kind == "avg":
+            vals.append(r / next(res).to(torch.float64))
+        else:
+            vals.append(r.to(torch.bool))
     return _group_result(d, keys, vals, nseg)
 
 

@@ -151,3 +151,45 @@ def gen_records64(cols: list, first: int, nkeys: int, seed: int, dim_mult: int =
     _lib.call("dr_gen_records64", ptr(ptrs), len(cols), c_u64(n), c_u64(first), c_u64(nkeys),
               c_u64(seed & (2**64 - 1)), c_u64(dim_mult), stream_of(cols[0]))
     return cols
+
+
+_lib.register_signatures({"dr_seg_reduce_multi": (c_i32, [vp, vp, c_u64, c_i32, vp, vp, vp, vp])})
+
+_MOPS = {("sum", 0): 0, ("min", 0): 1, ("max", 0): 2, ("count", 0): 3, ("sum", 1): 4, ("min", 1): 5, ("max", 1): 6}
+
+
+def seg_reduce_multi(entries: torch.Tensor | None, seg: torch.Tensor, nseg: int, specs: list) -> list:
+    """Several segmented reductions in ONE pass over the sorted entries.
+
+    ``specs``: [(op, vals, dtype)] with op in sum/min/max/count, vals a column in original row
+    order (None for count) and dtype torch.int64 or torch.float64.  Returns one [nseg] tensor per
+    spec."""
+    n = seg.shape[0]
+    dev = seg.device
+    outs, keep = [], []
+    ops = (ctypes.c_int * max(1, len(specs)))()
+    vps = (ctypes.c_void_p * max(1, len(specs)))()
+    ops_p = (ctypes.c_void_p * max(1, len(specs)))()
+    for a, (op, vals, dtype) in enumerate(specs):
+        f = 0 if dtype in (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool) else 1
+        tdt = torch.int64 if f == 0 else torch.float64
+        if op == "count":
+            f, tdt = 0, torch.int64
+        init = {"sum": 0, "count": 0,
+                "min": torch.iinfo(torch.int64).max if f == 0 else float("inf"),
+                "max": torch.iinfo(torch.int64).min if f == 0 else float("-inf")}[op]
+        out = torch.full((nseg,), init, dtype=tdt, device=dev)
+        v = None if op == "count" else vals.to(tdt).contiguous()
+        keep.append(v)
+        outs.append(out)
+        ops[a] = _MOPS[(op, f)]
+        vps[a] = v.data_ptr() if v is not None else 0
+        ops_p[a] = out.data_ptr()
+    if n and specs:
+        for k in range(0, len(specs), 8):     # kernel takes 8 aggregates per pass
+            m = min(8, len(specs) - k)
+            o8 = (ctypes.c_int * m)(*[ops[k + j] for j in range(m)])
+            v8 = (ctypes.c_void_p * m)(*[vps[k + j] for j in range(m)])
+            p8 = (ctypes.c_void_p * m)(*[ops_p[k + j] for j in range(m)])
+            _lib.call("dr_seg_reduce_multi", ptr(entries), ptr(seg), c_u64(n), m, o8, v8, p8, stream_of(seg))
+    return outs

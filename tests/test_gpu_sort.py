@@ -234,3 +234,29 @@ def test_terasort_generate_with_keys_matches_extract():
     assert torch.equal(keys, ref)
     mn, mx = S.hi_range(ref)
     assert [int(x) & (2**64 - 1) for x in rng.cpu().tolist()] == [mn, mx]
+
+
+@pytest.mark.parametrize("nkeys", [1, 7, 1000, 300_000])
+def test_seg_reduce_multi_matches_torch(nkeys):
+    from dryad_amd.ops import relational as R, sort as S
+    n = 500_003
+    k = torch.randint(0, nkeys, (n,), device="cuda", dtype=torch.int64)
+    vi = torch.randint(-10**6, 10**6, (n,), device="cuda", dtype=torch.int64)
+    vf = torch.randn(n, device="cuda", dtype=torch.float64)
+    e, b0, lo_mask = R.build_keys([k])
+    srt = S.sort_entries_hybrid(e, b0)
+    seg, nseg, starts = R.segment_ids(srt, lo_mask)
+    cnt, si, mn, mx, sf, mnf, mxf = R.seg_reduce_multi(srt, seg, nseg, [
+        ("count", None, torch.int64), ("sum", vi, torch.int64), ("min", vi, torch.int64), ("max", vi, torch.int64),
+        ("sum", vf, torch.float64), ("min", vf, torch.float64), ("max", vf, torch.float64)])
+    keys = k.index_select(0, (srt[:, 0] & 0xFFFFFFFF).index_select(0, starts))
+    uk, inv = torch.unique(k, return_inverse=True)
+    assert torch.equal(keys, uk)
+    assert torch.equal(cnt, torch.bincount(inv, minlength=uk.numel()))
+    assert torch.equal(si, torch.zeros_like(uk).index_add_(0, inv, vi))
+    ref_min = torch.full_like(uk, 2**62).scatter_reduce(0, inv, vi, "amin")
+    ref_max = torch.full_like(uk, -2**62).scatter_reduce(0, inv, vi, "amax")
+    assert torch.equal(mn, ref_min) and torch.equal(mx, ref_max)
+    torch.testing.assert_close(sf, torch.zeros(uk.numel(), dtype=torch.float64, device="cuda").index_add_(0, inv, vf))
+    assert torch.equal(mnf, torch.full((uk.numel(),), 1e300, dtype=torch.float64, device="cuda").scatter_reduce(0, inv, vf, "amin"))
+    assert torch.equal(mxf, torch.full((uk.numel(),), -1e300, dtype=torch.float64, device="cuda").scatter_reduce(0, inv, vf, "amax"))
