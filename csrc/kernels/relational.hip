@@ -175,6 +175,7 @@ struct AggSpecs {
   int op[kMaxAggs];
   const uint64_t* vals[kMaxAggs];
   uint64_t* out[kMaxAggs];
+  uint32_t stride[kMaxAggs];   // elements between consecutive records (1 = column, k = AoS row)
 };
 
 __device__ __forceinline__ uint64_t m_combine(uint64_t a, uint64_t b, int op) {
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(256) void seg_reduce_multi_kernel(const E128* __res
     for (int a = 0; a < nagg; ++a) {
       const int op = sp.op[a];
       uint64_t v = 0;
-      if (valid) v = (op == M_COUNT) ? 1ull : sp.vals[a][row];
+      if (valid) v = (op == M_COUNT) ? 1ull : sp.vals[a][(uint64_t)row * sp.stride[a]];
 #pragma unroll
       for (int k = 0, d = 1; d < 64; d <<= 1, ++k) {
         const uint64_t o = __shfl_up(v, d, 64);
@@ -389,8 +390,10 @@ DR_API int dr_seg_reduce(const void* vals, const E128* ent, const int64_t* seg, 
 
 // Fused multi-aggregate segmented reduce (see seg_reduce_multi_kernel).  ops/vals/outs: host
 // arrays of nagg (<= 8) entries; outputs must be pre-filled with each op's identity.
+// strides: host array of nagg element strides (nullptr = all 1); with ent == nullptr the values
+// are already in sorted order (row = position).
 DR_API int dr_seg_reduce_multi(const E128* ent, const int64_t* seg, uint64_t n, int nagg, const int* ops,
-                               const void* const* vals, void* const* outs, hipStream_t s) {
+                               const void* const* vals, void* const* outs, const uint32_t* strides, hipStream_t s) {
   if (nagg < 1 || nagg > kMaxAggs) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
   AggSpecs sp;
@@ -398,6 +401,7 @@ DR_API int dr_seg_reduce_multi(const E128* ent, const int64_t* seg, uint64_t n, 
     sp.op[a] = ops[a];
     sp.vals[a] = reinterpret_cast<const uint64_t*>(vals[a]);
     sp.out[a] = reinterpret_cast<uint64_t*>(outs[a]);
+    sp.stride[a] = strides ? strides[a] : 1u;
   }
   seg_reduce_multi_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(ent, seg, n, nagg, sp);
   DR_LAUNCH_CHECK();

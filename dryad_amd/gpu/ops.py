@@ -402,10 +402,6 @@ def op_group_partial(op, inputs, v):
     return tb
 
 
-def _pkey(r):   # key selector of partial-aggregate tables: the key columns
-    return tuple(getattr(r, f"k{i}") for i in range(_pkey.nkeys))
-
-
 def op_group_final(op, inputs, v):
     t = _check(_one(inputs))
     d = op["decomp"]

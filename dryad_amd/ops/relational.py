@@ -153,7 +153,7 @@ def gen_records64(cols: list, first: int, nkeys: int, seed: int, dim_mult: int =
     return cols
 
 
-_lib.register_signatures({"dr_seg_reduce_multi": (c_i32, [vp, vp, c_u64, c_i32, vp, vp, vp, vp])})
+_lib.register_signatures({"dr_seg_reduce_multi": (c_i32, [vp, vp, c_u64, c_i32, vp, vp, vp, vp, vp])})
 
 _MOPS = {("sum", 0): 0, ("min", 0): 1, ("max", 0): 2, ("count", 0): 3, ("sum", 1): 4, ("min", 1): 5, ("max", 1): 6}
 
@@ -191,5 +191,5 @@ def seg_reduce_multi(entries: torch.Tensor | None, seg: torch.Tensor, nseg: int,
             o8 = (ctypes.c_int * m)(*[ops[k + j] for j in range(m)])
             v8 = (ctypes.c_void_p * m)(*[vps[k + j] for j in range(m)])
             p8 = (ctypes.c_void_p * m)(*[ops_p[k + j] for j in range(m)])
-            _lib.call("dr_seg_reduce_multi", ptr(entries), ptr(seg), c_u64(n), m, o8, v8, p8, stream_of(seg))
+            _lib.call("dr_seg_reduce_multi", ptr(entries), ptr(seg), c_u64(n), m, o8, v8, p8, None, stream_of(seg))
     return outs
