@@ -111,16 +111,19 @@ __global__ __launch_bounds__(512) void kmeans_step_kernel(const float* __restric
         stage(c0, CT, ctile, cn);
         __syncthreads();
       }
-      f32x16 acc = {};
+      // two independent accumulation chains (even / odd k-steps) keep the matrix pipe busy
+      // instead of serialising 64 dependent MFMAs on one accumulator
+      f32x16 acc = {}, acc2 = {};
       const float* brow = tb + r * LDW + 64 * h;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const float4 b = *reinterpret_cast<const float4*>(brow + 4 * q);
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(b.x, a[4 * q + 0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(b.y, a[4 * q + 1], acc, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(b.y, a[4 * q + 1], acc2, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(b.z, a[4 * q + 2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(b.w, a[4 * q + 3], acc, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(b.w, a[4 * q + 3], acc2, 0, 0, 0);
       }
+      acc += acc2;
 #pragma unroll
       for (int q4 = 0; q4 < 4; ++q4) {
         const float4 cv = *reinterpret_cast<const float4*>(tn + 8 * q4 + 4 * h);

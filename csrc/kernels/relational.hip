@@ -249,6 +249,107 @@ __global__ __launch_bounds__(256) void seg_reduce_multi_kernel(const E128* __res
   }
 }
 
+// Thread-serial variant: each lane reduces PER consecutive sorted elements on its own (segments
+// that start and end inside the lane are written directly), and only the per-lane tail partials
+// take part in a 64-lane segmented scan — 1/PER of the cross-lane traffic of the per-element
+// scan above.  Segments touching the chunk boundary are combined with atomics.
+template <int PER>
+__global__ __launch_bounds__(256) void seg_reduce_multi_serial(const E128* __restrict__ ent,
+                                                               const int64_t* __restrict__ seg, uint64_t n,
+                                                               int nagg, AggSpecs sp) {
+  constexpr uint64_t kChunkElems = 64 * PER;
+  const int lane = lane_id();
+  const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const uint64_t w0 = (((uint64_t)blockIdx.x * blockDim.x) + threadIdx.x) >> 6;
+  for (uint64_t cbase = w0 * kChunkElems; cbase < n; cbase += waves * kChunkElems) {
+    const uint64_t first = cbase + (uint64_t)lane * PER;
+    int64_t sid[PER];
+    uint32_t row[PER];
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint64_t i = first + k;
+      if (i < n) {
+        sid[k] = seg[i];
+        row[k] = ent ? (uint32_t)ent[i].lo : (uint32_t)i;
+        cnt = k + 1;
+      } else {
+        sid[k] = INT64_MIN + (int64_t)(lane * PER + k);   // unique, never matches
+        row[k] = 0;
+      }
+    }
+    const uint64_t cend = (cbase + kChunkElems < n) ? cbase + kChunkElems : n;
+    // segments continuing across the chunk boundary must be combined atomically
+    const int64_t chunk_first = seg[cbase];
+    const int64_t chunk_last = seg[cend - 1];
+    const bool open_left = cbase > 0 && seg[cbase - 1] == chunk_first;
+    const bool open_right = cend < n && seg[cend] == chunk_last;
+    const int64_t head_id = sid[0], tail_id = sid[PER - 1];
+    const int64_t prev_tail = __shfl_up(tail_id, 1, 64);
+    const int64_t next_head = __shfl_down(head_id, 1, 64);
+    const bool carry_in = lane > 0 && prev_tail == head_id;
+    const bool tail_continues = (lane < 63) ? (next_head == tail_id) : false;
+    // lane-level scan predicates (key equality of tail ids), shared by all aggregates
+    uint32_t same = 0;
+#pragma unroll
+    for (int k = 0, d = 1; d < 64; d <<= 1, ++k) {
+      const int64_t o = __shfl_up(tail_id, d, 64);
+      if (lane >= d && o == tail_id) same |= 1u << k;
+    }
+    for (int a = 0; a < nagg; ++a) {
+      const int op = sp.op[a];
+      uint64_t v[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k)
+        v[k] = (k < cnt) ? ((op == M_COUNT) ? 1ull : sp.vals[a][(uint64_t)row[k] * sp.stride[a]]) : 0ull;
+      // serial pass over the lane's runs
+      uint64_t acc = v[0];
+      uint64_t head_val = 0;
+      bool head_done = false;
+#pragma unroll
+      for (int k = 1; k < PER; ++k) {
+        if (k < cnt && sid[k] == sid[k - 1]) {
+          acc = m_combine(acc, v[k], op);
+        } else {
+          if (!head_done) {           // first run of the lane ends at k-1
+            head_val = acc;
+            head_done = true;
+          } else if (k - 1 < cnt) {   // an interior run, entirely inside this lane
+            const int64_t s_ = sid[k - 1];
+            if ((s_ == chunk_first && open_left) || (s_ == chunk_last && open_right)) m_atomic(sp.out[a] + s_, acc, op);
+            else sp.out[a][s_] = acc;
+          }
+          acc = v[k];
+        }
+      }
+      const uint64_t tail_val = acc;   // last run of the lane (== first run if the lane has one run)
+      // inclusive segmented scan of tail partials across lanes
+      uint64_t S = tail_val;
+#pragma unroll
+      for (int k = 0, d = 1; d < 64; d <<= 1, ++k) {
+        const uint64_t o = __shfl_up(S, d, 64);
+        if (same & (1u << k)) S = m_combine(S, o, op);
+      }
+      const uint64_t carry = __shfl_up(S, 1, 64);
+      if (cnt == 0) continue;
+      if (head_done) {
+        // the lane's first run ends inside the lane: carry (if any) + head partial
+        const uint64_t hv = carry_in ? m_combine(carry, head_val, op) : head_val;
+        if ((head_id == chunk_first && open_left) || (head_id == chunk_last && open_right)) m_atomic(sp.out[a] + head_id, hv, op);
+        else sp.out[a][head_id] = hv;
+      }
+      // the lane's last run: written by the lane where the segment ends (S already includes
+      // every earlier lane's share of it)
+      // (a lane cut short by the end of the array already wrote all its runs in the serial pass)
+      if (cnt == PER && !tail_continues) {
+        const int64_t s_ = tail_id;
+        if ((s_ == chunk_first && open_left) || (s_ == chunk_last && open_right)) m_atomic(sp.out[a] + s_, S, op);
+        else sp.out[a][s_] = S;
+      }
+    }
+  }
+}
+
 // ----- merge join ----------------------------------------------------------------------------
 __device__ __forceinline__ bool key_less(const E128& a, const E128& b, uint64_t m) {
   return a.hi < b.hi || (a.hi == b.hi && (a.lo & m) < (b.lo & m));
@@ -403,7 +504,15 @@ DR_API int dr_seg_reduce_multi(const E128* ent, const int64_t* seg, uint64_t n, 
     sp.out[a] = reinterpret_cast<uint64_t*>(outs[a]);
     sp.stride[a] = strides ? strides[a] : 1u;
   }
-  seg_reduce_multi_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(ent, seg, n, nagg, sp);
+  static int serial = -1;
+  if (serial < 0) {
+    const char* e = getenv("DRYAD_SEGRED_SERIAL");
+    serial = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  if (serial)
+    seg_reduce_multi_serial<8><<<grid_for(n, 256 * 8, 8192), 256, 0, s>>>(ent, seg, n, nagg, sp);
+  else
+    seg_reduce_multi_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(ent, seg, n, nagg, sp);
   DR_LAUNCH_CHECK();
   return 0;
 }

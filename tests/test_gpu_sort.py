@@ -260,3 +260,28 @@ def test_seg_reduce_multi_matches_torch(nkeys):
     torch.testing.assert_close(sf, torch.zeros(uk.numel(), dtype=torch.float64, device="cuda").index_add_(0, inv, vf))
     assert torch.equal(mnf, torch.full((uk.numel(),), 1e300, dtype=torch.float64, device="cuda").scatter_reduce(0, inv, vf, "amin"))
     assert torch.equal(mxf, torch.full((uk.numel(),), -1e300, dtype=torch.float64, device="cuda").scatter_reduce(0, inv, vf, "amax"))
+
+
+@pytest.mark.parametrize("serial", ["0", "1"])
+def test_seg_reduce_multi_variants_agree(serial, monkeypatch):
+    import subprocess, sys, os
+    code = (
+        "import torch\n"
+        "from dryad_amd.ops import relational as R\n"
+        "torch.manual_seed(1)\n"
+        "for n, nk in ((1, 1), (511, 3), (513, 600), (4097, 2), (1_000_003, 50), (2_000_000, 1_500_000)):\n"
+        "    k = torch.sort(torch.randint(0, nk, (n,), device='cuda'))[0]\n"
+        "    flags = torch.ones(n, dtype=torch.int64, device='cuda'); flags[1:] = (k[1:] != k[:-1]).long()\n"
+        "    seg = torch.cumsum(flags, 0) - 1; nseg = int(seg[-1]) + 1\n"
+        "    vi = torch.randint(-10**6, 10**6, (n,), device='cuda'); vf = torch.randn(n, device='cuda', dtype=torch.float64)\n"
+        "    c, s, mn, mxf = R.seg_reduce_multi(None, seg, nseg, [('count', None, torch.int64), ('sum', vi, torch.int64),\n"
+        "                                        ('min', vi, torch.int64), ('max', vf, torch.float64)])\n"
+        "    assert torch.equal(c, torch.bincount(seg, minlength=nseg))\n"
+        "    assert torch.equal(s, torch.zeros(nseg, dtype=torch.int64, device='cuda').index_add_(0, seg, vi))\n"
+        "    assert torch.equal(mn, torch.full((nseg,), 2**62, device='cuda').scatter_reduce(0, seg, vi, 'amin'))\n"
+        "    assert torch.equal(mxf, torch.full((nseg,), -1e300, dtype=torch.float64, device='cuda').scatter_reduce(0, seg, vf, 'amax'))\n"
+        "print('OK')\n")
+    env = dict(os.environ, DRYAD_SEGRED_SERIAL=serial)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0 and "OK" in out.stdout, out.stderr[-3000:]

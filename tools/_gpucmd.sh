@@ -1,5 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_gb3 -o run -- python3 $GRAFT_REPO_ROOT/benchmarks/groupby.py --steps 1 --warmup 1 > $GRAFT_REPO_ROOT/gpurun_out/gb_prof.log 2>&1; rc=$?
-tail -1 $GRAFT_REPO_ROOT/gpurun_out/gb_prof.log; exit $rc
+timeout -k 10 500 python -m pytest tests/test_gpu_sort.py tests/test_gpu_executor.py tests/test_gpu_kmeans.py -x -q > gpurun_out/t.log 2>&1; rc=$?; tail -25 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
+for d in 0 1; do DRYAD_KM_DEBUG=$d timeout -k 10 100 python tools/microbench_kmeans.py 20000000 16,64,128,256,1024 2>/dev/null | sed "s/^/dbg=$d /" || exit 1; done
+timeout -k 10 600 python benchmarks/groupby.py --steps 2 > gpurun_out/gb_full.log 2>&1; rc=$?; tail -1 gpurun_out/gb_full.log; exit $rc
