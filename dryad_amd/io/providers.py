@@ -126,12 +126,20 @@ class PartfileProvider(DataProvider):
         if dtype is None:
             from ..types import LineRecordT
             dtype = LineRecordT
+        if data[:2] == b"\x1f\x8b":       # gzip-compressed record stream (OutputDataCompressionScheme)
+            import gzip
+            data = gzip.decompress(data)
         return B.decode_records(dtype, data)
 
     def read_partition_bytes(self, uri, i) -> bytes:
+        """The decoded record-stream bytes of part i (gzip-compressed parts are inflated)."""
         path = PF.read_meta(self._path(uri)).part_path(i)
         with open(path, "rb") as f:
-            return f.read()
+            data = f.read()
+        if data[:2] == b"\x1f\x8b":
+            import gzip
+            data = gzip.decompress(data)
+        return data
 
     def write_table(self, uri, partitions, dtype, delete_if_exists=True):
         """Ingress: one part file per partition (records in DryadLinqBinary)."""

@@ -596,9 +596,15 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     for p, v in local.items():
         tmp = PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, 0)
         data = CD.encode(v, dt) if isinstance(v, DeviceTable) and v.device.type == "cuda" else None
-        if data is not None:
+        raw = data.cpu().numpy().tobytes() if data is not None else None
+        if runner.ctx.OutputDataCompressionScheme.value != 0:
+            import gzip
+            if raw is None:
+                raw = B.encode_records(dt, _to_objects(v) if not isinstance(v, list) else v)
+            raw = gzip.compress(raw, compresslevel=6)
+        if raw is not None:
             with open(tmp, "wb") as f:
-                f.write(data.cpu().numpy().tobytes())
+                f.write(raw)
         else:
             B.write_records(tmp, dt, _to_objects(v) if not isinstance(v, list) else v)
         mine[p] = tmp

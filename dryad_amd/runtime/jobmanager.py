@@ -49,6 +49,7 @@ class JobRunner:
         self.inputs_of: dict = {}    # vid -> [[(src_vid, src_port, edge_id), ...] per stage input]
         self.events = []
         self.compress = ctx.IntermediateDataCompressionScheme.value != 0
+        self.output_gzip = ctx.OutputDataCompressionScheme.value != 0
         self._build()
 
     # ------------------------------------------------------------------ graph construction
@@ -113,7 +114,7 @@ class JobRunner:
             inputs.append([(self.chan_path(src, g.completed_version(src), port), e) for src, port, e in lst])
         cmd = dict(job=self.job_dir, stage=sid, partition=part, vertex=vid, version=version, inputs=inputs,
                    outputs=[self.chan_path(vid, version, k) for k in range(stage.out_ports)],
-                   faults=self.faults, compress=self.compress)
+                   faults=self.faults, compress=self.compress, output_gzip=self.output_gzip)
         if stage.is_output:
             cmd["output_part"] = self.output_part_path(stage, part, vid, version)
         return cmd

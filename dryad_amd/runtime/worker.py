@@ -87,7 +87,7 @@ def _merge_inputs(stage_input, streams):
     return [x for s in streams for x in s]
 
 
-def write_output_part(stage, records, path: str, compress=False):
+def write_output_part(stage, records, path: str, compress=False, output_gzip=False):
     """Write an output partition in the DryadLinqBinary record format (typed) or pickle."""
     from .. import types as T
     from ..io import binary as B
@@ -112,6 +112,13 @@ def write_output_part(stage, records, path: str, compress=False):
         with open(path, "wb") as f:
             ser(records, f)
         return os.path.getsize(path), dtype.name, "custom"
+    if output_gzip:
+        # whole-stream gzip of the record stream (CompressionScheme.Gzip,
+        # DryadLinqBlockStream.cs:198-225); readers detect the gzip magic
+        data = gzip.compress(B.encode_records(dtype, records), compresslevel=6)
+        with open(path, "wb") as f:
+            f.write(data)
+        return len(data), dtype.name, "binary"
     n = B.write_records(path, dtype, records)
     return n, dtype.name, "binary"
 
@@ -146,7 +153,7 @@ def execute_vertex(cmd: dict, plan=None) -> dict:
         compress = bool(cmd.get("compress"))
         if stage.is_output:
             recs = ports[0]
-            nb, dt, fmt = write_output_part(stage, recs, cmd["output_part"], compress)
+            nb, dt, fmt = write_output_part(stage, recs, cmd["output_part"], compress, bool(cmd.get("output_gzip")))
             res.update(bytes_written=nb, dtype=dt, fmt=fmt, records_out=len(recs))
         else:
             for k, path in enumerate(cmd["outputs"]):

@@ -174,3 +174,19 @@ def test_rabin_fingerprint_matches_definition():
     v = 0x0123456789ABCDEF
     assert r.extend_u64(poly, v) == r.extend(poly, v.to_bytes(8, "little"))
     assert r.extend_u32(poly, 0xDEADBEEF) == r.extend(poly, (0xDEADBEEF).to_bytes(4, "little"))
+
+
+def test_output_gzip_compression_roundtrip(tmp_path):
+    import gzip
+    import dryad_amd as D
+    from dryad_amd.context import CompressionScheme
+    from dryad_amd.io import partfile as PF
+    c = D.DryadLinqContext(2)
+    c.OutputDataCompressionScheme = CompressionScheme.GZIP
+    uri = f"partfile://{tmp_path}/z.pt"
+    data = [(i, i * 0.25) for i in range(5000)]
+    c.FromEnumerable(data).ToStore(uri).SubmitAndWait()
+    part = PF.read_meta(str(tmp_path / "z.pt")).part_path(0)
+    raw = open(part, "rb").read()
+    assert raw[:2] == b"\x1f\x8b" and len(gzip.decompress(raw)) > len(raw)
+    assert sorted(D.DryadLinqContext(2).FromStore(uri)) == data
