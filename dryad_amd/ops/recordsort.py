@@ -158,8 +158,16 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     stride = rows.shape[1]
     b0, b1, lo_mask = key_bits(key_len)
     ent = bufs.ent_a[:n] if keys_ready else S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
-    seps = choose_separators(ent, n, w, lo_mask, sample_target, seed, bufs.ent_b)
-    S.range_dest(ent, seps, lo_mask)                                    # ent.hi := destination
+    part_mask = lo_mask
+    if key_len <= 10 and w.size < (1 << 16):
+        # skew: equal keys must not all land on one rank.  Bits 47..32 of lo are free for keys of
+        # <= 10 bytes; with the rank there (and the row index below it) every entry is unique, so
+        # the sampled separators split runs of equal keys across ranks while the global order
+        # (key, rank, row) stays a valid OrderBy order.
+        ent[:, 0].bitwise_or_(w.rank << 32)
+        part_mask = (1 << 64) - 1
+    seps = choose_separators(ent, n, w, part_mask, sample_target, seed, bufs.ent_b)
+    S.range_dest(ent, seps, part_mask)                                   # ent.hi := destination
     part, starts = S.partition_pass(ent, 64, out=bufs.ent_b[:n])        # stable by destination
     S.gather_rows(rows, entries=part, out=bufs.rows_out[:n])            # pack send buffer
     st = starts[: w.size + 1].cpu().tolist()

@@ -34,6 +34,16 @@ def main():
     assert got == exp
     fb = {op for _, op, _ in g._get_executor().last_result["fallbacks"]}
     assert "group_partial" not in fb and "group_final" not in fb, fb
+    # skew: every key equal -> the (key, rank, row) tie-break still balances the ranks
+    from dryad_amd.ops import recordsort as RS
+    n = 300_000
+    bufs = RS.SortBuffers.allocate(n, 16, w.device, slack=0.05)
+    bufs.rows_in[:n].fill_(7)
+    bufs.rows_in[:n, 8:] = torch.randint(0, 256, (n, 8), dtype=torch.uint8, device=w.device)
+    st = RS.SortStats()
+    out = RS.distributed_sort_rows(bufs, n, 0, 8, w, stats=st)
+    assert abs(st.n_out - n) <= 0.05 * n, (w.rank, st.n_out)
+    assert torch.equal(out[:, :8], torch.full_like(out[:, :8], 7))
     w.barrier()
     if w.rank == 0:
         print("MULTIRANK_OK", w.size, flush=True)
