@@ -498,6 +498,75 @@ def op_distinct(op, inputs, v):
     return t.take(_perm(srt).index_select(0, starts))
 
 
+def _record_entries(t):
+    if t.rows is not None:
+        if t.rows.shape[1] > 12:
+            raise NotTraceable("wide rows")
+        return key_entries(t, lambda r: r[0:t.rows.shape[1]])
+    cols = [t.cols[f] for f in t.shape.fields]
+    if R.key_bit_count(cols) > 96:
+        raise NotTraceable("record wider than 96 bits")
+    e, b0, lo_mask = R.build_keys(cols)
+    return e, b0, lo_mask
+
+
+def _set_op(kind, op, inputs):
+    """Union / Intersect / Except (K10): sort the concatenation, segment equal records and keep
+    one representative per segment according to which sides the segment contains."""
+    if op.get("comparer") is not None:
+        raise NotTraceable("custom comparer")
+    a, b = _check(inputs[0]), _check(inputs[1])
+    if a.heap is not None or b.heap is not None:
+        raise NotTraceable("string records")
+    if a.shape.kind != b.shape.kind or a.shape.fields != b.shape.fields or a.row_bytes() != b.row_bytes():
+        raise NotTraceable("operands have different layouts")
+    both = DeviceTable.concat([a, b])
+    if both.n == 0:
+        return both
+    e, b0, lo_mask = _record_entries(both)
+    srt = S.sort_entries_hybrid(e, b0)
+    seg, nseg, starts = R.segment_ids(srt, lo_mask)
+    first = _perm(srt).index_select(0, starts)
+    if kind == "union":
+        return both.take(first)
+    side = (torch.arange(both.n, device=both.device) >= a.n).to(torch.int64)   # 0 = left, 1 = right
+    lo_side, hi_side = R.seg_reduce_multi(srt, seg, nseg, [("min", side, torch.int64), ("max", side, torch.int64)])
+    keep = (lo_side == 0) & (hi_side == 1) if kind == "intersect" else (hi_side == 0)
+    return both.take(first[keep])
+
+
+def op_union(op, inputs, v):
+    return _set_op("union", op, inputs)
+
+
+def op_intersect(op, inputs, v):
+    return _set_op("intersect", op, inputs)
+
+
+def op_except(op, inputs, v):
+    return _set_op("except", op, inputs)
+
+
+def _while_cut(op, t):
+    m = TR.to_mask(TR.call(op["fn"], t, 0 if op.get("indexed") else None), t)
+    bad = torch.nonzero(~m, as_tuple=False)
+    return int(bad[0].item()) if bad.numel() else t.n
+
+
+def op_take_while(op, inputs, v):
+    t = _check(_one(inputs))
+    if t.n == 0:
+        return t
+    return t.slice(0, _while_cut(op, t))
+
+
+def op_skip_while(op, inputs, v):
+    t = _check(_one(inputs))
+    if t.n == 0:
+        return t
+    return t.slice(_while_cut(op, t), t.n)
+
+
 def op_hash_join(op, inputs, v):
     outer, inner = _check(inputs[0]), _check(inputs[1])
     if op.get("comparer") is not None:

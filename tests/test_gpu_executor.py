@@ -135,3 +135,15 @@ def test_groupby_single_partition_on_device():
     _same(lambda c: c.FromStore(src).GroupBy(
         lambda r: r[0], lambda k, g: (k, g.Count(), g.Sum(lambda r: r[1]), g.Average(lambda r: r[2]),
                                       g.Max(lambda r: r[3]))), parts=1, device_ops=("read", "group_by"))
+
+
+def test_set_ops_and_while_on_device():
+    a = [(i * 7) % 500 for i in range(3000)]
+    b = [(i * 11) % 700 for i in range(2000)]
+    for name in ("Union", "Intersect", "Except"):
+        _same(lambda c, n=name: getattr(c.FromEnumerable(a), n)(c.FromEnumerable(b)), parts=1,
+              device_ops=(name.lower(),))
+    _same(lambda c: c.FromEnumerable(list(range(1000))).TakeWhile(lambda x: x < 377), ordered=True,
+          device_ops=("take_while",))
+    _same(lambda c: c.FromEnumerable(list(range(1000))).SkipWhile(lambda x: x < 377), ordered=True,
+          device_ops=("skip_while",))
