@@ -366,20 +366,8 @@ def _key_cols(t, key_fn):
     return spec, isinstance(res, tuple)
 
 
-def op_group_partial(op, inputs, v):
-    t = _check(_one(inputs))
-    d = op["decomp"]
-    if op.get("comparer") is not None or any(a.kind not in _GPU_AGGS for a in d.aggs):
-        raise NotTraceable("aggregate not supported on the device")
-    if t.n == 0:
-        raise NotTraceable("empty partition")
-    kcols, _ = _key_cols(t, op["key"])
-    e, b0, lo_mask = R.build_keys(kcols)
-    srt = S.sort_entries_hybrid(e, b0)
-    seg, nseg, starts = R.segment_ids(srt, lo_mask)
-    rows_at_start = _perm(srt).index_select(0, starts)
-    out = {f"k{i}": c.index_select(0, rows_at_start) for i, c in enumerate(kcols)}
-    # every aggregate in one fused segmented-reduce pass
+def _group_specs(d, t):
+    """Aggregate specs (op, column, dtype) + output column names of a decomposed GroupBy."""
     specs, names = [], []
     for j, a in enumerate(d.aggs):
         val = _agg_value(a, t)
@@ -395,6 +383,37 @@ def op_group_partial(op, inputs, v):
         elif a.kind in ("any", "all"):
             specs.append(("max" if a.kind == "any" else "min", val, torch.int64))
             names.append(f"a{j}")
+    return specs, names
+
+
+def op_group_partial(op, inputs, v):
+    t = _check(_one(inputs))
+    d = op["decomp"]
+    if op.get("comparer") is not None or any(a.kind not in _GPU_AGGS for a in d.aggs):
+        raise NotTraceable("aggregate not supported on the device")
+    if t.n == 0:
+        raise NotTraceable("empty partition")
+    kcols, _ = _key_cols(t, op["key"])
+    specs, names = _group_specs(d, t)
+    # low-cardinality integer keys: one streaming pass into LDS hash tables (no sort)
+    if len(kcols) == 1 and not kcols[0].is_floating_point() and t.n >= (1 << 16):
+        nd, m = R.estimate_distinct(kcols[0])
+        if nd <= R.HASH_AGG_MAX_KEYS and nd * 8 < m:
+            got = R.hash_aggregate(kcols[0], specs)
+            if got is not None:
+                keys, res = got
+                out = {"k0": keys}
+                for nm, r in zip(names, res):
+                    out[nm] = r
+                tb = DeviceTable.from_columns(out, Shape("tuple", list(out)))
+                tb.group_meta = dict(nkeys=1, aggs=d.aggs)
+                return tb
+    e, b0, lo_mask = R.build_keys(kcols)
+    srt = S.sort_entries_hybrid(e, b0)
+    seg, nseg, starts = R.segment_ids(srt, lo_mask)
+    rows_at_start = _perm(srt).index_select(0, starts)
+    out = {f"k{i}": c.index_select(0, rows_at_start) for i, c in enumerate(kcols)}
+    # every aggregate in one fused segmented-reduce pass
     for nm, res in zip(names, R.seg_reduce_multi(srt, seg, nseg, specs)):
         out[nm] = res
     tb = DeviceTable.from_columns(out, Shape("tuple", list(out)))

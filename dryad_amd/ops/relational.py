@@ -193,3 +193,69 @@ def seg_reduce_multi(entries: torch.Tensor | None, seg: torch.Tensor, nseg: int,
             p8 = (ctypes.c_void_p * m)(*[ops_p[k + j] for j in range(m)])
             _lib.call("dr_seg_reduce_multi", ptr(entries), ptr(seg), c_u64(n), m, o8, v8, p8, None, stream_of(seg))
     return outs
+
+
+_lib.register_signatures({"dr_hash_aggregate": (c_i32, [vp, c_u64, c_i32, vp, vp, vp, vp, c_u64, vp, vp])})
+
+HASH_AGG_MAX_KEYS = 1 << 15
+
+
+def estimate_distinct(col: torch.Tensor, sample: int = 1 << 16) -> tuple[int, int]:
+    """(distinct keys in an evenly strided sample, sample size)."""
+    n = col.shape[0]
+    if n == 0:
+        return 0, 0
+    step = max(1, n // sample)
+    s_ = col[::step][:sample]
+    return int(torch.unique(s_).numel()), int(s_.numel())
+
+
+def hash_aggregate(key: torch.Tensor, specs: list, capacity: int | None = None):
+    """Low-cardinality GroupBy in one streaming pass (csrc/kernels/hashagg.hip).
+
+    ``key``: integer column; ``specs`` as for seg_reduce_multi.  Returns (keys, outs) for the
+    distinct keys (unordered), or None when the table overflowed (caller falls back to sorting)."""
+    n = key.shape[0]
+    dev = key.device
+    k64 = key.to(torch.int64).contiguous()
+    if capacity is None:
+        d, m = estimate_distinct(k64)
+        capacity = max(1024, 1 << (max(1, 4 * d) - 1).bit_length())
+    gkeys = torch.full((capacity,), -2**63, dtype=torch.int64, device=dev)
+    ops, vals, outs, keep = [], [], [], []
+    for op, v, dtype in specs:
+        f = 0 if dtype in (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool) else 1
+        if op == "count":
+            f = 0
+        tdt = torch.int64 if f == 0 else torch.float64
+        init = {"sum": 0, "count": 0,
+                "min": torch.iinfo(torch.int64).max if f == 0 else float("inf"),
+                "max": torch.iinfo(torch.int64).min if f == 0 else float("-inf")}[op]
+        out = torch.full((capacity + 1,), init, dtype=tdt, device=dev)
+        vv = None if op == "count" else v.to(tdt).contiguous()
+        keep.append(vv)
+        ops.append(_MOPS[(op, f)])
+        vals.append(vv.data_ptr() if vv is not None else 0)
+        outs.append(out)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    m = len(specs)
+    _lib.call("dr_hash_aggregate", ptr(k64), c_u64(n), m, (ctypes.c_int * m)(*ops), (ctypes.c_void_p * m)(*vals),
+              (ctypes.c_void_p * m)(*[o.data_ptr() for o in outs]), ptr(gkeys), c_u64(capacity), ptr(flag),
+              stream_of(k64))
+    if int(flag.item()):
+        return None
+    used = torch.nonzero(gkeys != -2**63, as_tuple=False).flatten()
+    keys_out = gkeys.index_select(0, used)
+    res = [o.index_select(0, used) for o in outs]
+    # the INT64_MIN key lives in the extra slot `capacity`
+    cnt_special = None
+    for (op, _, _), o in zip(specs, outs):
+        if op == "count":
+            cnt_special = int(o[capacity].item())
+            break
+    if cnt_special is None:
+        cnt_special = int((k64 == -2**63).sum().item())
+    if cnt_special:
+        keys_out = torch.cat([keys_out, torch.tensor([-2**63], dtype=torch.int64, device=dev)])
+        res = [torch.cat([r, o[capacity:capacity + 1]]) for r, o in zip(res, outs)]
+    return keys_out.to(key.dtype), res

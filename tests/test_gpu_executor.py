@@ -147,3 +147,25 @@ def test_set_ops_and_while_on_device():
           device_ops=("take_while",))
     _same(lambda c: c.FromEnumerable(list(range(1000))).SkipWhile(lambda x: x < 377), ordered=True,
           device_ops=("skip_while",))
+
+
+def test_groupby_low_cardinality_hash_path():
+    import dryad_amd.ops.relational as R
+    src = "gen://records64?count=400000&partitions=2&keys=300&seed=9"
+    c = _same(lambda c: c.FromStore(src).GroupBy(
+        lambda r: r[0], lambda k, g: (k, g.Count(), g.Sum(lambda r: r[1]), g.Min(lambda r: r[2]),
+                                      g.Max(lambda r: r[3]), g.Average(lambda r: r[4]))), parts=2,
+        device_ops=("group_partial", "group_final"))
+    # direct kernel check incl. negative keys and the INT64_MIN sentinel value
+    k = torch.randint(-50, 50, (300_000,), device="cuda", dtype=torch.int64)
+    k[::997] = -2**63
+    v = torch.randn(300_000, device="cuda", dtype=torch.float64)
+    keys, (cnt, s, mx) = R.hash_aggregate(k, [("count", None, torch.int64), ("sum", v, torch.float64),
+                                              ("max", v, torch.float64)])
+    order = torch.argsort(keys)
+    uk, inv = torch.unique(k, return_inverse=True)
+    assert torch.equal(keys[order], uk)
+    assert torch.equal(cnt[order], torch.bincount(inv))
+    torch.testing.assert_close(s[order], torch.zeros(uk.numel(), dtype=torch.float64, device="cuda").index_add_(0, inv, v))
+    assert torch.equal(mx[order], torch.full((uk.numel(),), -1e300, dtype=torch.float64, device="cuda")
+                       .scatter_reduce(0, inv, v, "amax"))
