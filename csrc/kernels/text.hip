@@ -55,7 +55,40 @@ __global__ __launch_bounds__(256) void token_verify_kernel(const uint8_t* __rest
   }
 }
 
+// mode 0: s == pat, 1: s.startswith(pat), 2: s.endswith(pat), 3: pat in s (substring)
+__global__ __launch_bounds__(256) void str_match_kernel(const uint8_t* __restrict__ heap, const int64_t* __restrict__ off,
+                                                        const int64_t* __restrict__ len, uint64_t n,
+                                                        const uint8_t* __restrict__ pat, int64_t plen, int mode,
+                                                        bool* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint8_t* s = heap + off[i];
+    const int64_t L = len[i];
+    bool ok;
+    if (mode == 0 || mode == 1 || mode == 2) {
+      ok = (mode == 0) ? (L == plen) : (L >= plen);
+      const int64_t base = (mode == 2) ? L - plen : 0;
+      for (int64_t k = 0; ok && k < plen; ++k) ok = s[base + k] == pat[k];
+    } else {
+      ok = false;
+      for (int64_t st = 0; !ok && st + plen <= L; ++st) {
+        bool m = true;
+        for (int64_t k = 0; m && k < plen; ++k) m = s[st + k] == pat[k];
+        ok = m;
+      }
+    }
+    out[i] = ok;
+  }
+}
+
 }  // namespace
+
+DR_API int dr_str_match(const uint8_t* heap, const int64_t* off, const int64_t* len, uint64_t n, const uint8_t* pat,
+                        int64_t plen, int mode, bool* out, hipStream_t s) {
+  if (n == 0) return 0;
+  str_match_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(heap, off, len, n, pat, plen, mode, out);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
 
 DR_API int dr_text_marks(const uint8_t* buf, uint64_t n, uint8_t* marks, hipStream_t s) {
   if (n == 0) return 0;

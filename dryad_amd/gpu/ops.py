@@ -497,7 +497,7 @@ def op_group_by(op, inputs, v):
 # ---------------------------------------------------------------------------------------------
 def op_distinct(op, inputs, v):
     t = _check(_one(inputs))
-    if t.heap is not None:
+    if t.heap is not None or t.strs:
         raise NotTraceable("string records")
     if op.get("comparer") is not None:
         raise NotTraceable("custom comparer")
@@ -518,6 +518,8 @@ def op_distinct(op, inputs, v):
 
 
 def _record_entries(t):
+    if t.strs:
+        raise NotTraceable("records with string fields")
     if t.rows is not None:
         if t.rows.shape[1] > 12:
             raise NotTraceable("wide rows")

@@ -43,12 +43,15 @@ class Shape:
 
 class DeviceTable:
     def __init__(self, n: int, shape: Shape, cols: dict | None = None, rows: torch.Tensor | None = None,
-                 heap: torch.Tensor | None = None):
+                 heap: torch.Tensor | None = None, strs: dict | None = None):
         self.n = int(n)
         self.shape = shape
         self.cols = cols if cols is not None else {}
         self.rows = rows
         self.heap = heap              # text tables: the byte heap the off/len columns point into
+        # string fields of record tables: field -> UTF-8 heap; cols[field] holds the byte offsets
+        # and cols[field + "#len"] the byte lengths
+        self.strs = strs or {}
 
     # ------------------------------------------------------------------ construction
     @staticmethod
@@ -96,7 +99,8 @@ class DeviceTable:
     def slice(self, a: int, b: int) -> "DeviceTable":
         if self.rows is not None:
             return DeviceTable(b - a, self.shape, rows=self.rows[a:b])
-        return DeviceTable(b - a, self.shape, {k: v[a:b] for k, v in self.cols.items()}, heap=self.heap)
+        return DeviceTable(b - a, self.shape, {k: v[a:b] for k, v in self.cols.items()}, heap=self.heap,
+                           strs=self.strs)
 
     def take(self, idx: torch.Tensor) -> "DeviceTable":
         """Gather rows by an int64 index tensor (HIP row gather for row tables)."""
@@ -104,7 +108,7 @@ class DeviceTable:
             from ..ops import sort as S
             return DeviceTable(idx.shape[0], self.shape, rows=S.gather_rows(self.rows, index=idx.contiguous()))
         return DeviceTable(idx.shape[0], self.shape, {k: v.index_select(0, idx) for k, v in self.cols.items()},
-                           heap=self.heap)
+                           heap=self.heap, strs=self.strs)
 
     def mask(self, m: torch.Tensor) -> "DeviceTable":
         idx = torch.nonzero(m, as_tuple=False).flatten()
@@ -128,14 +132,25 @@ class DeviceTable:
             return DeviceTable(sum(t.n for t in tables), t0.shape,
                                {"off": torch.cat(offs), "len": torch.cat([t.cols["len"] for t in tables])},
                                heap=torch.cat([t.heap for t in tables]))
+        if t0.strs:
+            cols = {k: torch.cat([t.cols[k] for t in tables]) for k in t0.cols}
+            strs = {}
+            for f in t0.strs:
+                offs, base = [], 0
+                for t in tables:
+                    offs.append(t.cols[f] + base)
+                    base += t.strs[f].shape[0]
+                cols[f] = torch.cat(offs)
+                strs[f] = torch.cat([t.strs[f] for t in tables])
+            return DeviceTable(sum(t.n for t in tables), t0.shape, cols, strs=strs)
         return DeviceTable(sum(t.n for t in tables), t0.shape,
                            {k: torch.cat([t.cols[k] for t in tables]) for k in t0.cols})
 
     # ------------------------------------------------------------------ packing for RCCL
     def pack(self) -> torch.Tensor:
         """One uint8 [n, row_bytes] buffer (AoS) so an exchange is a single collective."""
-        if self.heap is not None:
-            raise TypeError("text tables are exchanged as records")
+        if self.heap is not None or self.strs:
+            raise TypeError("tables with strings are exchanged as records")
         if self.rows is not None:
             return self.rows
         parts = [v.contiguous().view(torch.uint8).reshape(self.n, _width(v)) for v in self.cols.values()]
@@ -168,7 +183,13 @@ class DeviceTable:
             if self.shape.pytype is not None and self.shape.pytype is not str:
                 return [self.shape.pytype(x) for x in strs]
             return strs
-        arrs = {k: v.cpu().numpy() for k, v in self.cols.items()}
+        arrs = {k: v.cpu().numpy() for k, v in self.cols.items() if not k.endswith("#len")}
+        for f, hp in self.strs.items():
+            if hp.is_cuda:
+                from ..ops.text import gather_strings
+                arrs[f] = _ObjArr(gather_strings(hp, self.cols[f], self.cols[f + "#len"]))
+            else:
+                arrs[f] = _ObjArr(_host_strings(hp, self.cols[f], self.cols[f + "#len"]))
         sh = self.shape
         if sh.kind == "scalar":
             return arrs[sh.fields[0]].tolist()
@@ -180,6 +201,14 @@ class DeviceTable:
         if sh.kind == "dataclass":
             return [sh.pytype(*vals) for vals in zip(*lists)]
         raise ValueError(sh.kind)
+
+
+class _ObjArr(list):
+    """A list standing in for a numpy column of strings in to_objects."""
+    ndim = 1
+
+    def tolist(self):
+        return list(self)
 
 
 def _host_strings(heap, off, ln) -> list:
@@ -226,8 +255,8 @@ def columnar_dtype(dt) -> bool:
     if isinstance(dt, T.VectorT):
         return dt.elem in _NP_OF
     if isinstance(dt, T.RecordT):
-        return all(t in _NP_OF or (isinstance(t, T.VectorT) and t.elem in _NP_OF) for _, t in dt.fields) \
-            and not dt.nullable_fields
+        return all(t in _NP_OF or t == T.String or (isinstance(t, T.VectorT) and t.elem in _NP_OF)
+                   for _, t in dt.fields) and not dt.nullable_fields
     return False
 
 
@@ -254,12 +283,18 @@ def from_objects(records: list, dt, device) -> DeviceTable | None:
         a = np.asarray(records, dtype=_NP_OF[dt]) if records else np.zeros(0, _NP_OF[dt])
         return DeviceTable.from_columns({"v": torch.from_numpy(a).to(device)}, Shape("scalar", ["v"]))
     names = [n for n, _ in dt.fields]
-    cols = {}
+    cols, strs = {}, {}
     for i, (n, t) in enumerate(dt.fields):
         if dt.pytype in (None, tuple):
             vals = [r[i] for r in records]
         else:
             vals = [getattr(r, n) for r in records]
+        if t == T.String:
+            heap, off, ln = _encode_strings(vals)
+            strs[n] = heap.to(device)
+            cols[n] = off.to(device)
+            cols[n + "#len"] = ln.to(device)
+            continue
         if isinstance(t, T.VectorT):
             npt = _NP_OF[t.elem]
             a = np.asarray(vals, dtype=npt).reshape(len(vals), t.dim) if vals else np.zeros((0, t.dim), npt)
@@ -267,4 +302,15 @@ def from_objects(records: list, dt, device) -> DeviceTable | None:
             continue
         cols[n] = torch.from_numpy(np.asarray(vals, dtype=_NP_OF[t]) if vals else np.zeros(0, _NP_OF[t])).to(device)
     kind = "tuple" if dt.pytype in (None, tuple) else "dataclass"
-    return DeviceTable.from_columns(cols, Shape(kind, names, None if kind == "tuple" else dt.pytype))
+    t = DeviceTable.from_columns(cols, Shape(kind, names, None if kind == "tuple" else dt.pytype))
+    t.strs = strs
+    return t
+
+
+def _encode_strings(vals: list):
+    enc = [("" if v is None else str(v)).encode("utf-8") for v in vals]
+    ln = np.asarray([len(x) for x in enc], dtype=np.int64)
+    off = (np.concatenate([[0], np.cumsum(ln)[:-1]]) if len(enc) else np.zeros(0)).astype(np.int64)
+    blob = b"".join(enc)
+    heap = torch.frombuffer(bytearray(blob), dtype=torch.uint8) if blob else torch.zeros(0, dtype=torch.uint8)
+    return heap, torch.from_numpy(off), torch.from_numpy(ln)

@@ -141,6 +141,55 @@ class RowProxy:
         raise NotTraceable("branch on a record")
 
 
+class StrCol:
+    """A string field of a record table: (heap, offset, length) per record.  Supports ordinal
+    comparisons with constants (==, !=, startswith, endswith, `in`) on the device and can be
+    projected into a new table; anything else runs on the host."""
+    __slots__ = ("heap", "off", "len")
+
+    def __init__(self, heap, off, ln):
+        self.heap, self.off, self.len = heap, off, ln
+
+    def _match(self, pat, mode):
+        if not isinstance(pat, str):
+            raise NotTraceable("string compared with a non-constant")
+        from ..ops.text import str_match
+        return Col(str_match(self.heap, self.off, self.len, pat, mode))
+
+    def __eq__(self, o):
+        return self._match(o, 0)
+
+    def __ne__(self, o):
+        return Col(~self._match(o, 0).t)
+
+    def startswith(self, p):
+        return self._match(p, 1)
+
+    def endswith(self, p):
+        return self._match(p, 2)
+
+    def __contains__(self, p):
+        raise NotTraceable("`in` on a string field must produce a column")   # bool() forces a host value
+
+    def __bool__(self):
+        raise NotTraceable("branch on a string field")
+
+    def __hash__(self):
+        raise NotTraceable("hash of a string field")
+
+    def __len__(self):
+        raise NotTraceable("len() of a string field")
+
+    def __getattr__(self, name):
+        raise NotTraceable(f"string method {name}")
+
+
+def _field(t, name):
+    if name in t.strs:
+        return StrCol(t.strs[name], t.cols[name], t.cols[name + "#len"])
+    return Col(t.cols[name])
+
+
 class RecProxy:
     """Proxy for a columnar tuple / dataclass record."""
 
@@ -150,7 +199,7 @@ class RecProxy:
     def __getattr__(self, name):
         t = object.__getattribute__(self, "_t")
         if name in t.cols:
-            return Col(t.cols[name])
+            return _field(t, name)
         raise NotTraceable(f"unknown field {name}")
 
     def __getitem__(self, i):
@@ -158,12 +207,12 @@ class RecProxy:
         if isinstance(i, int):
             f = t.shape.fields
             if -len(f) <= i < len(f):
-                return Col(t.cols[f[i]])
+                return _field(t, f[i])
         raise NotTraceable("record index")
 
     def __iter__(self):
         t = object.__getattribute__(self, "_t")
-        return iter([Col(t.cols[f]) for f in t.shape.fields])
+        return iter([_field(t, f) for f in t.shape.fields])
 
     def __len__(self):
         return len(object.__getattribute__(self, "_t").shape.fields)
@@ -221,16 +270,30 @@ def to_table(res, table: DeviceTable) -> DeviceTable:
         if res.off == 0 and res.length == table.rows.shape[1]:
             return table
         return DeviceTable.from_rows(table.rows[:, res.off:res.off + res.length].contiguous())
+    if isinstance(res, StrCol):
+        from .table import text_table
+        return text_table(res.heap, res.off, res.len, str)
     if isinstance(res, (Col, int, float, bool)):
         return DeviceTable.from_columns({"v": _as_col(res, n, dev)}, Shape("scalar", ["v"]))
     if isinstance(res, tuple) and not hasattr(res, "_fields"):
-        cols = {f"Item{i + 1}": _as_col(v, n, dev) for i, v in enumerate(res)}
-        return DeviceTable.from_columns(cols, Shape("tuple", list(cols)))
+        names = [f"Item{i + 1}" for i in range(len(res))]
+        return _record_table(dict(zip(names, res)), Shape("tuple", names), n, dev)
     if dataclasses.is_dataclass(res) and not isinstance(res, type):
         names = [f.name for f in dataclasses.fields(res)]
-        cols = {k: _as_col(getattr(res, k), n, dev) for k in names}
-        return DeviceTable.from_columns(cols, Shape("dataclass", names, type(res)))
+        return _record_table({k: getattr(res, k) for k in names}, Shape("dataclass", names, type(res)), n, dev)
     raise NotTraceable(f"projection result of type {type(res).__name__}")
+
+
+def _record_table(vals: dict, shape, n, dev) -> DeviceTable:
+    cols, strs = {}, {}
+    for k, v in vals.items():
+        if isinstance(v, StrCol):
+            cols[k], cols[k + "#len"], strs[k] = v.off, v.len, v.heap
+        else:
+            cols[k] = _as_col(v, n, dev)
+    t = DeviceTable.from_columns(cols, shape)
+    t.strs = strs
+    return t
 
 
 def to_mask(res, table: DeviceTable) -> torch.Tensor:
@@ -250,7 +313,13 @@ def key_columns(res, table: DeviceTable):
     if isinstance(res, Col):
         return "cols", [_as_col(res, table.n, table.device)]
     if isinstance(res, RecProxy):
+        if table.strs:
+            raise NotTraceable("string keys")
         return "cols", [table.cols[f] for f in table.shape.fields]
     if isinstance(res, tuple):
+        if any(isinstance(v, StrCol) for v in res):
+            raise NotTraceable("string keys")
         return "cols", [_as_col(v, table.n, table.device) for v in res]
+    if isinstance(res, StrCol):
+        raise NotTraceable("string keys")
     raise NotTraceable(f"key of type {type(res).__name__}")

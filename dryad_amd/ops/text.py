@@ -5,6 +5,8 @@ pairs.  Whitespace = ' ', '\\t', '\\r', '\\n' (String.Split() with no arguments,
 reference's WordCount sample uses)."""
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -16,7 +18,25 @@ _lib.register_signatures({
     "dr_text_marks": (c_i32, [vp, c_u64, vp, vp]),
     "dr_token_hash": (c_i32, [vp, vp, vp, c_u64, vp, vp]),
     "dr_token_verify": (c_i32, [vp, vp, vp, vp, c_u64, vp, vp]),
+    "dr_str_match": (c_i32, [vp, vp, vp, c_u64, vp, ctypes.c_int64, c_i32, vp, vp]),
 })
+
+MATCH_EQ, MATCH_PREFIX, MATCH_SUFFIX, MATCH_CONTAINS = 0, 1, 2, 3
+
+
+def str_match(heap, off, ln, pattern: str, mode: int) -> torch.Tensor:
+    """Boolean mask of strings (heap, off, len) that equal / start with / end with / contain
+    ``pattern`` (UTF-8 byte comparison, i.e. ordinal string semantics)."""
+    n = off.shape[0]
+    out = torch.empty(n, dtype=torch.bool, device=off.device)
+    pat = pattern.encode("utf-8")
+    pt = torch.frombuffer(bytearray(pat), dtype=torch.uint8).to(off.device) if pat else \
+        torch.zeros(1, dtype=torch.uint8, device=off.device)
+    if heap.numel() == 0:
+        heap = torch.zeros(1, dtype=torch.uint8, device=off.device)
+    _lib.call("dr_str_match", ptr(heap), ptr(off.contiguous()), ptr(ln.contiguous()), c_u64(n), ptr(pt),
+              ctypes.c_int64(len(pat)), mode, ptr(out), stream_of(off))
+    return out
 
 SPACE = b" \t\r\n"
 

@@ -247,7 +247,7 @@ class GpuJobRunner:
         return inputs
 
     def _portable(self, x):
-        if isinstance(x, DeviceTable) and x.heap is not None:
+        if isinstance(x, DeviceTable) and (x.heap is not None or x.strs):
             return ("obj", x.to_objects())
         if isinstance(x, DeviceTable):
             return ("dt", x.shape, {k: v.cpu() for k, v in x.cols.items()} if x.rows is None else None,
@@ -268,7 +268,7 @@ class GpuJobRunner:
         P_src, P_dst = src_stage.partitions, dst_stage.partitions
         local_src = [q for q in range(P_src) if self.owner(q) == me]
         vals = {q: self.channels[(si.src, q)] for q in local_src}
-        device_ok = all(isinstance(v, Ported) and v.table.heap is None for v in vals.values())
+        device_ok = all(isinstance(v, Ported) and v.table.heap is None and not v.table.strs for v in vals.values())
         # agree on the transport (all device tables with one schema, else host objects)
         sig = None
         if device_ok and vals:

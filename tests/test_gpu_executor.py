@@ -169,3 +169,15 @@ def test_groupby_low_cardinality_hash_path():
     torch.testing.assert_close(s[order], torch.zeros(uk.numel(), dtype=torch.float64, device="cuda").index_add_(0, inv, v))
     assert torch.equal(mx[order], torch.full((uk.numel(),), -1e300, dtype=torch.float64, device="cuda")
                        .scatter_reduce(0, inv, v, "amax"))
+
+
+def test_records_with_string_fields_on_device():
+    people = [(("alice", "bob", "carol", "dave", "eve")[i % 5] + str(i % 7), i, float(i) / 3) for i in range(20_000)]
+    _same(lambda c: c.FromEnumerable(people).Where(lambda r: r[0] == "bob1"), device_ops=("where",))
+    _same(lambda c: c.FromEnumerable(people).Where(lambda r: r[0].startswith("ca") & (r[1] > 100)),
+          device_ops=("where",))
+    _same(lambda c: c.FromEnumerable(people).Where(lambda r: r[0].endswith("3")).Select(lambda r: (r[1] * 2, r[0])),
+          device_ops=("where", "select"))
+    _same(lambda c: c.FromEnumerable(people).Select(lambda r: r[0]).Take(50), ordered=True, device_ops=("select",))
+    # string keys still work (host path), results identical
+    _same(lambda c: c.FromEnumerable(people).GroupBy(lambda r: r[0], lambda k, g: (k, g.Count())), parts=2)

@@ -1,5 +1,9 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 500 python -m pytest tests/test_gpu_executor.py -x -q > gpurun_out/t.log 2>&1; rc=$?; tail -30 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python benchmarks/groupby.py --steps 2 --keys 1000 > gpurun_out/gb_1k.log 2>&1; rc=$?; tail -1 gpurun_out/gb_1k.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python benchmarks/groupby.py --steps 2 > gpurun_out/gb_full.log 2>&1; rc=$?; tail -1 gpurun_out/gb_full.log; exit $rc
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/p_gb -o run -- python3 $R/benchmarks/groupby.py --steps 1 --warmup 1 > $R/gpurun_out/p_gb.log 2>&1 || exit 1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/p_gb1k -o run -- python3 $R/benchmarks/groupby.py --steps 1 --warmup 1 --keys 1000 > $R/gpurun_out/p_gb1k.log 2>&1 || exit 1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/p_km -o run -- python3 $R/benchmarks/kmeans.py --iters 3 --warmup 1 > $R/gpurun_out/p_km.log 2>&1 || exit 1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/p_join -o run -- python3 $R/benchmarks/join.py --steps 1 --warmup 1 > $R/gpurun_out/p_join.log 2>&1 || exit 1
+grep -h metric $R/gpurun_out/p_*.log | cut -c1-200
