@@ -21,7 +21,7 @@ from ..ops import recordsort as RS
 from ..ops import relational as R
 from ..ops import sort as S
 from . import trace as TR
-from .table import DeviceTable, Ported, Shape, from_objects
+from .table import DeviceTable, PartialMeta, Ported, Shape, from_objects
 from .trace import NotTraceable
 
 E_SHAPE = Shape("tuple", ["lo", "hi"])
@@ -43,9 +43,9 @@ def _check(t):
 # ---------------------------------------------------------------------------------------------
 # key handling
 def key_entries(table: DeviceTable, key_fn, comparer=None, descending=False):
+    """-> (entries [n,2], begin_bit, lo_mask).  Keys compare like the object path's default order."""
     if table.heap is not None:
         raise NotTraceable("string keys")
-    """-> (entries [n,2], begin_bit, lo_mask).  Keys compare like the object path's default order."""
     if comparer is not None:
         raise NotTraceable("custom comparer")
     if table.n == 0:
@@ -70,6 +70,33 @@ def key_entries(table: DeviceTable, key_fn, comparer=None, descending=False):
         raise NotTraceable("composite key wider than 96 bits")
     e, b0, lo_mask = R.build_keys(cols, [descending] * len(cols))
     return e, b0, lo_mask
+
+
+def eq_key_entries(table: DeviceTable, key_fn, comparer=None):
+    """Entries for equality-only consumers (HashPartition, Join): like key_entries, but string
+    fields are keyed by their Rabin-64 fingerprints.  -> (entries, begin_bit, lo_mask, skeys)."""
+    if table.heap is not None:
+        raise NotTraceable("text records")
+    if comparer is not None:
+        raise NotTraceable("custom comparer")
+    if table.n == 0:
+        return torch.empty((0, 2), dtype=torch.int64, device=table.device), 64, 0, []
+    res = TR.call(key_fn, table)
+    try:
+        kind, spec = TR.key_columns(res, table)
+    except NotTraceable:
+        kind = "str"
+    if kind != "str":
+        e, b0, lo_mask = key_entries(table, key_fn, comparer)
+        return e, b0, lo_mask, []
+    cols, skeys = TR.eq_key_columns(res, table)
+    for c in cols:
+        if c.dtype not in R.KEY_TYPES:
+            raise NotTraceable(f"key dtype {c.dtype}")
+    if R.key_bit_count(cols) > 96:
+        raise NotTraceable("composite key wider than 96 bits")
+    e, b0, lo_mask = R.build_keys(cols)
+    return e, b0, lo_mask, skeys
 
 
 def _perm(entries: torch.Tensor) -> torch.Tensor:
@@ -285,7 +312,7 @@ def op_hash_partition(op, inputs, v):
         raise NotTraceable("custom comparer")
     if t.n == 0:
         return Ported(t, [0] * (n + 1))
-    e, _, lo_mask = key_entries(t, op["key"])
+    e, _, lo_mask, _ = eq_key_entries(t, op["key"])
     R.hash_dest(e, lo_mask, n)
     part, starts = S.partition_pass(e, 64)
     st = starts[: n + 1].tolist()
@@ -359,11 +386,64 @@ def _agg_value(agg, t):
 
 
 def _key_cols(t, key_fn):
+    """Group key columns; string fields become Rabin fingerprints (skeys[i] = their StrCol).
+    Also returns how the host path represents the key ("single" or "tuple")."""
     res = TR.call(key_fn, t)
-    kind, spec = TR.key_columns(res, t)
-    if kind != "cols":
-        raise NotTraceable("byte-string group keys")
-    return spec, isinstance(res, tuple)
+    if isinstance(res, TR.RecProxy) and t.shape.kind == "dataclass":
+        raise NotTraceable("record-valued group key")
+    cols, skeys = TR.eq_key_columns(res, t)
+    form = "tuple" if isinstance(res, (tuple, TR.RecProxy)) else "single"
+    return cols, skeys, form
+
+
+def _partial_table(out, strs, d, nkeys, form):
+    names = [f for f in out if not f.endswith("#len")]
+    meta = PartialMeta(nkeys, tuple(a.kind for a in d.aggs), form)
+    tb = DeviceTable.from_columns(out, Shape("partial", names, meta))
+    tb.strs = strs
+    return tb
+
+
+def _group_keys(kcols, skeys):
+    """Sort by the key columns -> (srt, seg, nseg, rows_at_start).  With string keys, every row is
+    checked against its group's representative so a fingerprint collision can never merge two
+    different strings (the operator falls back to the host if one ever occurs)."""
+    e, b0, lo_mask = R.build_keys(kcols)
+    srt = S.sort_entries_hybrid(e, b0)
+    seg, nseg, starts = R.segment_ids(srt, lo_mask)
+    perm = _perm(srt)
+    rows_at_start = perm.index_select(0, starts)
+    if any(sk is not None for sk in skeys):
+        from ..ops.fingerprint import strings_differ
+        rep = rows_at_start.index_select(0, seg)          # representative row, in sorted order
+        for sk in skeys:
+            if sk is not None:
+                trip = (sk.heap, sk.off, sk.len)
+                if strings_differ(trip, perm, trip, rep):
+                    raise NotTraceable("string key fingerprint collision")
+    return srt, seg, nseg, rows_at_start
+
+
+def _key_outputs(kcols, skeys, rows_at_start):
+    """Per-group key columns (string keys keep their heap) -> (cols, strs)."""
+    out, strs = {}, {}
+    for i, (c, sk) in enumerate(zip(kcols, skeys)):
+        if sk is None:
+            out[f"k{i}"] = c.index_select(0, rows_at_start)
+        else:
+            out[f"k{i}"] = sk.off.index_select(0, rows_at_start)
+            out[f"k{i}#len"] = sk.len.index_select(0, rows_at_start)
+            strs[f"k{i}"] = sk.heap
+    return out, strs
+
+
+def _key_values(tb, nkeys):
+    """Key columns of a group table as traced values (StrCol for string keys)."""
+    vals = []
+    for i in range(nkeys):
+        f = f"k{i}"
+        vals.append(TR.StrCol(tb.strs[f], tb.cols[f], tb.cols[f + "#len"]) if f in tb.strs else tb.cols[f])
+    return vals
 
 
 def _group_specs(d, t):
@@ -393,10 +473,10 @@ def op_group_partial(op, inputs, v):
         raise NotTraceable("aggregate not supported on the device")
     if t.n == 0:
         raise NotTraceable("empty partition")
-    kcols, _ = _key_cols(t, op["key"])
+    kcols, skeys, form = _key_cols(t, op["key"])
     specs, names = _group_specs(d, t)
     # low-cardinality integer keys: one streaming pass into LDS hash tables (no sort)
-    if len(kcols) == 1 and not kcols[0].is_floating_point() and t.n >= (1 << 16):
+    if len(kcols) == 1 and skeys[0] is None and not kcols[0].is_floating_point() and t.n >= (1 << 16):
         nd, m = R.estimate_distinct(kcols[0])
         if nd <= R.HASH_AGG_MAX_KEYS and nd * 8 < m:
             got = R.hash_aggregate(kcols[0], specs)
@@ -405,20 +485,13 @@ def op_group_partial(op, inputs, v):
                 out = {"k0": keys}
                 for nm, r in zip(names, res):
                     out[nm] = r
-                tb = DeviceTable.from_columns(out, Shape("tuple", list(out)))
-                tb.group_meta = dict(nkeys=1, aggs=d.aggs)
-                return tb
-    e, b0, lo_mask = R.build_keys(kcols)
-    srt = S.sort_entries_hybrid(e, b0)
-    seg, nseg, starts = R.segment_ids(srt, lo_mask)
-    rows_at_start = _perm(srt).index_select(0, starts)
-    out = {f"k{i}": c.index_select(0, rows_at_start) for i, c in enumerate(kcols)}
+                return _partial_table(out, {}, d, 1, form)
+    srt, seg, nseg, rows_at_start = _group_keys(kcols, skeys)
+    out, strs = _key_outputs(kcols, skeys, rows_at_start)
     # every aggregate in one fused segmented-reduce pass
     for nm, res in zip(names, R.seg_reduce_multi(srt, seg, nseg, specs)):
         out[nm] = res
-    tb = DeviceTable.from_columns(out, Shape("tuple", list(out)))
-    tb.group_meta = dict(nkeys=len(kcols), aggs=d.aggs)
-    return tb
+    return _partial_table(out, strs, d, len(kcols), form)
 
 
 def op_group_final(op, inputs, v):
@@ -426,13 +499,14 @@ def op_group_final(op, inputs, v):
     d = op["decomp"]
     if t.n == 0:
         raise NotTraceable("empty partition")
-    nkeys = sum(1 for f in t.shape.fields if f.startswith("k"))
-    kcols = [t.cols[f"k{i}"] for i in range(nkeys)]
-    e, b0, lo_mask = R.build_keys(kcols)
-    srt = S.sort_entries_hybrid(e, b0)
-    seg, nseg, starts = R.segment_ids(srt, lo_mask)
-    rows_at_start = _perm(srt).index_select(0, starts)
-    keys = [c.index_select(0, rows_at_start) for c in kcols]
+    if t.shape.kind != "partial":
+        raise NotTraceable("group_final input is not a device partial table")
+    nkeys = t.shape.pytype.nkeys
+    kcols, skeys = TR.eq_key_columns(tuple(TR.Col(v) if isinstance(v, torch.Tensor) else v
+                                           for v in _key_values(t, nkeys)), t)
+    srt, seg, nseg, rows_at_start = _group_keys(kcols, skeys)
+    kout, kstrs = _key_outputs(kcols, skeys, rows_at_start)
+    keys = _key_values(DeviceTable(nseg, Shape("tuple", list(kout)), kout, strs=kstrs), nkeys)
     specs = []
     for j, a in enumerate(d.aggs):
         col = t.cols[f"a{j}"]
@@ -455,13 +529,14 @@ def op_group_final(op, inputs, v):
             vals.append(r / next(res).to(torch.float64))
         else:
             vals.append(r.to(torch.bool))
-    return _group_result(d, keys, vals, nseg)
+    return _group_result(d, keys, vals, nseg, t.shape.pytype.key_form)
 
 
-def _group_result(d, keys, vals, nseg):
+def _group_result(d, keys, vals, nseg, form="single"):
     """Substitute the per-group key/aggregate columns into the result-selector template."""
     nkeys = len(keys)
-    key = TR.Col(keys[0]) if nkeys == 1 else tuple(TR.Col(k) for k in keys)
+    kv = [k if isinstance(k, TR.StrCol) else TR.Col(k) for k in keys]
+    key = kv[0] if nkeys == 1 and form == "single" else tuple(kv)
     env = {"key": key, "aggs": [TR.Col(x) for x in vals]}
     try:
         res = substitute(d.template, env)
@@ -469,7 +544,8 @@ def _group_result(d, keys, vals, nseg):
         raise
     except Exception as ex:  # noqa: BLE001
         raise NotTraceable(f"result template: {ex}")
-    proto = DeviceTable(nseg, Shape("scalar", ["v"]), {"v": keys[0]})
+    k0 = keys[0].off if isinstance(keys[0], TR.StrCol) else keys[0]
+    proto = DeviceTable(nseg, Shape("scalar", ["v"]), {"v": k0})
     return TR.to_table(res, proto)
 
 
@@ -480,8 +556,8 @@ def op_group_by(op, inputs, v):
     if d is None or op.get("elem") is not None:
         raise NotTraceable("non-decomposable GroupBy")
     tb = op_group_partial(dict(op, decomp=d), inputs, v)
-    nkeys = tb.group_meta["nkeys"]
-    keys = [tb.cols[f"k{i}"] for i in range(nkeys)]
+    nkeys = tb.shape.pytype.nkeys
+    keys = _key_values(tb, nkeys)
     vals = []
     for j, a in enumerate(d.aggs):
         col = tb.cols[f"a{j}"]
@@ -491,7 +567,7 @@ def op_group_by(op, inputs, v):
             vals.append(col.to(torch.bool))
         else:
             vals.append(col)
-    return _group_result(d, keys, vals, tb.n)
+    return _group_result(d, keys, vals, tb.n, tb.shape.pytype.key_form)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -594,15 +670,21 @@ def op_hash_join(op, inputs, v):
         raise NotTraceable("custom comparer")
     if outer.n == 0 or inner.n == 0:
         raise NotTraceable("empty join side: output type unknown")
-    eo, b0, lm = key_entries(outer, op["outer_key"])
-    ei, b1, lm2 = key_entries(inner, op["inner_key"])
-    if (b0, lm) != (b1, lm2):
+    eo, b0, lm, so_keys = eq_key_entries(outer, op["outer_key"])
+    ei, b1, lm2, si_keys = eq_key_entries(inner, op["inner_key"])
+    if (b0, lm) != (b1, lm2) or [k is None for k in so_keys] != [k is None for k in si_keys]:
         raise NotTraceable("join keys of different types")
     so = S.sort_entries_hybrid(eo, b0)
     si = S.sort_entries_hybrid(ei, b0)
     oo, ii, _ = R.merge_join_pairs(so, si, lm)
     if oo.shape[0] == 0:
         raise NotTraceable("empty join result")
+    if so_keys:
+        # string keys matched by fingerprint: every emitted pair must hold equal strings
+        from ..ops.fingerprint import strings_differ
+        for a, b in zip(so_keys, si_keys):
+            if a is not None and strings_differ((a.heap, a.off, a.len), oo, (b.heap, b.off, b.len), ii):
+                raise NotTraceable("string key fingerprint collision")
     a, b = outer.take(oo), inner.take(ii)
     res = op["result"](TR.proxy(a), TR.proxy(b))
     return TR.to_table(res, a)

@@ -29,7 +29,8 @@ from .. import types as T
 @dataclass
 class Shape:
     """How columns map to Python records."""
-    kind: str                         # "scalar" | "tuple" | "dataclass" | "rows" | "vector"
+    kind: str                         # "scalar" | "tuple" | "dataclass" | "rows" | "vector" | "text"
+    #                                   | "partial" (GroupBy partial aggregates: pytype = PartialMeta)
     fields: list = field(default_factory=list)   # column names in record order
     pytype: object = None
     key_off: int = 0                  # rows: default key field
@@ -39,6 +40,17 @@ class Shape:
         if self.kind == "rows":
             return f"rows(key=[{self.key_off},{self.key_off + self.key_len}))"
         return f"{self.kind}({', '.join(self.fields)})"
+
+
+@dataclass(frozen=True)
+class PartialMeta:
+    """Layout of a device GroupBy partial-aggregate table: key columns k0..k{nkeys-1} then the
+    accumulator columns of each aggregate (a{j}, plus c{j} for averages).  Only plain data, so
+    the shape pickles across ranks.  ``key_form`` = "single" | "tuple" (how the host path
+    represents the group key)."""
+    nkeys: int
+    kinds: tuple
+    key_form: str = "single"
 
 
 class DeviceTable:
@@ -200,7 +212,26 @@ class DeviceTable:
             return list(zip(*lists))
         if sh.kind == "dataclass":
             return [sh.pytype(*vals) for vals in zip(*lists)]
+        if sh.kind == "partial":
+            return _partial_objects(sh.pytype, arrs)
         raise ValueError(sh.kind)
+
+
+def _partial_objects(meta: PartialMeta, arrs: dict) -> list:
+    """Partial-aggregate table -> the host path's (key, [acc per aggregate]) pairs
+    (runtime/vertex_ops.op_group_partial), so a host group_final can consume device partials."""
+    keys = [arrs[f"k{i}"].tolist() for i in range(meta.nkeys)]
+    kv = keys[0] if meta.nkeys == 1 and meta.key_form == "single" else list(zip(*keys))
+    accs = []
+    for j, kind in enumerate(meta.kinds):
+        a = arrs[f"a{j}"].tolist()
+        if kind == "avg":
+            accs.append(list(zip(a, arrs[f"c{j}"].tolist())))
+        elif kind in ("any", "all"):
+            accs.append([bool(x) for x in a])
+        else:
+            accs.append(a)
+    return [(k, [acc[i] for acc in accs]) for i, k in enumerate(kv)]
 
 
 class _ObjArr(list):

@@ -296,6 +296,34 @@ def _record_table(vals: dict, shape, n, dev) -> DeviceTable:
     return t
 
 
+def eq_key_columns(res, table: DeviceTable):
+    """Key columns for equality-only consumers (GroupBy, HashPartition, Join): a string field is
+    replaced by its Rabin-64 fingerprint column (ops/fingerprint.py).  Returns (cols, strkeys)
+    with strkeys[i] the StrCol behind cols[i] (None for plain columns); callers must verify that
+    rows sharing a fingerprint hold equal strings.  Byte-string row keys stay NotTraceable here."""
+    if isinstance(res, RecProxy) and table.strs:
+        items = [_field(table, f) for f in table.shape.fields]
+    elif isinstance(res, StrCol):
+        items = [res]
+    elif isinstance(res, tuple) and any(isinstance(v, StrCol) for v in res):
+        items = list(res)
+    else:
+        kind, spec = key_columns(res, table)
+        if kind != "cols":
+            raise NotTraceable("byte-string key")
+        return spec, [None] * len(spec)
+    from ..ops.fingerprint import rabin_strings
+    cols, skeys = [], []
+    for v in items:
+        if isinstance(v, StrCol):
+            cols.append(rabin_strings(v.heap, v.off, v.len))
+            skeys.append(v)
+        else:
+            cols.append(_as_col(v, table.n, table.device))
+            skeys.append(None)
+    return cols, skeys
+
+
 def to_mask(res, table: DeviceTable) -> torch.Tensor:
     if isinstance(res, bool):
         return torch.full((table.n,), res, dtype=torch.bool, device=table.device)

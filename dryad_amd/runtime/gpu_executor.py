@@ -248,13 +248,40 @@ class GpuJobRunner:
 
     def _portable(self, x):
         if isinstance(x, DeviceTable) and (x.heap is not None or x.strs):
-            return ("obj", x.to_objects())
+            return self._ship(x)
         if isinstance(x, DeviceTable):
             return ("dt", x.shape, {k: v.cpu() for k, v in x.cols.items()} if x.rows is None else None,
                     x.rows.cpu() if x.rows is not None else None, x.n)
         return ("obj", x)
 
+    @staticmethod
+    def _ship(x):
+        """A port for the object transport: string-bearing device tables travel as host copies of
+        their columns and heaps (so field names, partial-aggregate layouts and the device path on
+        the receiving rank survive); everything else as records."""
+        if isinstance(x, DeviceTable) and (x.heap is not None or x.strs):
+            return ("dts", x.shape, {k: v.cpu() for k, v in x.cols.items()},
+                    x.heap.cpu() if x.heap is not None else None, {f: h.cpu() for f, h in x.strs.items()}, x.n)
+        return ("obj", _to_objects(x))
+
+    @staticmethod
+    def _keep(x):
+        """A local port on the object transport (string tables stay on the device)."""
+        if isinstance(x, DeviceTable) and (x.heap is not None or x.strs):
+            return x
+        return _to_objects(x)
+
+    def _unship(self, x):
+        if x[0] == "dts":
+            _, shape, cols, heap, strs, n = x
+            return DeviceTable(n, shape, {k: v.to(self.dev) for k, v in cols.items()},
+                               heap=heap.to(self.dev) if heap is not None else None,
+                               strs={f: h.to(self.dev) for f, h in strs.items()})
+        return x[1]
+
     def _unportable(self, x):
+        if x[0] == "dts":
+            return self._unship(x)
         if x[0] == "dt":
             _, shape, cols, rows, n = x
             if rows is not None:
@@ -284,13 +311,14 @@ class GpuJobRunner:
             for q, v in vals.items():
                 for p in range(P_dst):
                     if self.owner(p) != me:
-                        send[(q, p)] = _to_objects(self._port_of(si, v, p))
+                        send[(q, p)] = self._ship(self._port_of(si, v, p))
             gathered = [None] * W
             dist.all_gather_object(gathered, send)
             out = {}
             for p in local_dst:
-                out[p] = [(_to_objects(self._port_of(si, self.channels[(si.src, q)], p)) if self.owner(q) == me
-                           else gathered[self.owner(q)][(q, p)]) for q in range(P_src)]
+                out[p] = [self._keep(self._port_of(si, self.channels[(si.src, q)], p))
+                          if self.owner(q) == me else self._unship(gathered[self.owner(q)][(q, p)])
+                          for q in range(P_src)]
             return out
         # counts matrix [P_src, P_dst] (rows), all-gathered
         cnt = torch.zeros((P_src, P_dst), dtype=torch.int64)

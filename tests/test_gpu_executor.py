@@ -179,5 +179,22 @@ def test_records_with_string_fields_on_device():
     _same(lambda c: c.FromEnumerable(people).Where(lambda r: r[0].endswith("3")).Select(lambda r: (r[1] * 2, r[0])),
           device_ops=("where", "select"))
     _same(lambda c: c.FromEnumerable(people).Select(lambda r: r[0]).Take(50), ordered=True, device_ops=("select",))
-    # string keys still work (host path), results identical
-    _same(lambda c: c.FromEnumerable(people).GroupBy(lambda r: r[0], lambda k, g: (k, g.Count())), parts=2)
+    # string keys: Rabin fingerprints on the device, verified against the strings
+    _same(lambda c: c.FromEnumerable(people).GroupBy(lambda r: r[0], lambda k, g: (k, g.Count())), parts=2,
+          device_ops=("group_partial", "group_final", "hash_partition"))
+
+
+def test_string_keys_on_device():
+    people = [(("alice", "bob", "carol", "dave", "eve", "")[i % 6] + "x" * (i % 23), i % 50, float(i) / 3)
+              for i in range(30_000)]
+    _same(lambda c: c.FromEnumerable(people).GroupBy(
+        lambda r: r[0], lambda k, g: (k, g.Count(), g.Sum(lambda r: r[1]), g.Max(lambda r: r[2]))), parts=1,
+        device_ops=("group_by", "group_partial"))
+    # composite key (string, int) across two partitions
+    _same(lambda c: c.FromEnumerable(people).GroupBy(
+        lambda r: (r[0], r[1] % 3), lambda k, g: (k[0], k[1], g.Average(lambda r: r[1]))), parts=2,
+        device_ops=("group_partial", "group_final", "hash_partition"))
+    names = [(("alice", "bob", "carol", "dave")[i % 4] + "x" * (i % 23), i) for i in range(5_000)]
+    ages = [(("alice", "bob", "carol", "zed")[i % 4] + "x" * (i % 11), i * 10) for i in range(400)]
+    _same(lambda c: c.FromEnumerable(names).Join(c.FromEnumerable(ages), lambda a: a[0], lambda b: b[0],
+                                                 lambda a, b: (a[1], b[1])), parts=1, device_ops=("hash_join",))
