@@ -585,7 +585,8 @@ DR_API int dr_gather_rows(const uint8_t* rows, uint8_t* out, const E128* entries
 namespace {
 __global__ __launch_bounds__(256) void range_dest_kernel(const E128* __restrict__ in, E128* __restrict__ out,
                                                          uint64_t n, const E128* __restrict__ seps,
-                                                         uint32_t nsep, uint64_t lo_mask, int desc) {
+                                                         uint32_t nsep, uint64_t lo_mask, int desc,
+                                                         uint32_t subs, uint32_t ranks) {
   __shared__ uint64_t shi[256], slo[256];
   for (uint32_t k = threadIdx.x; k < nsep; k += blockDim.x) {
     shi[k] = seps[k].hi;
@@ -605,17 +606,140 @@ __global__ __launch_bounds__(256) void range_dest_kernel(const E128* __restrict_
       lo = before ? mid + 1 : lo;
       hi = before ? hi : mid;
     }
-    e.hi = lo;
+    // sub-range pipelining: key range g = rank * subs + sub is renumbered sub-major
+    // (sub * ranks + rank) so that one partition pass lays out round `sub` of the exchange as one
+    // contiguous destination-ordered block
+    e.hi = subs > 1 ? (uint64_t)((lo % subs) * ranks + lo / subs) : (uint64_t)lo;
     out[i] = e;
   }
 }
 }  // namespace
 
 DR_API int dr_range_dest_u128(const E128* in, E128* out, uint64_t n, const E128* seps, uint32_t nsep,
-                              uint64_t lo_mask, int descending, hipStream_t s) {
+                              uint64_t lo_mask, int descending, uint32_t subs, uint32_t ranks,
+                              hipStream_t s) {
   if (nsep > 255) return (int)hipErrorInvalidValue;
+  if (subs > 1 && (uint64_t)subs * ranks != (uint64_t)nsep + 1) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
-  range_dest_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(in, out, n, seps, nsep, lo_mask, descending);
+  range_dest_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(in, out, n, seps, nsep, lo_mask, descending,
+                                                            subs, ranks);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Bucket scatter of whole rows (the send-buffer pack of a range / hash shuffle): rows[i] goes to
+// its bucket's contiguous region, bucket = low byte of entries[i].hi (from dr_range_dest_u128 or
+// a hash destination), stable within a bucket.  Replaces "partition the entries, then gather the
+// rows through them": that gather reads every 100-byte row at a scattered address (the partition
+// interleaves up to 256 streams); here each 512-row tile is read coalesced into LDS, ranked by
+// bucket with the radix-scatter ballots, and each bucket's rows are written as one contiguous run.
+namespace {
+constexpr int kBsTile = 512;
+constexpr int kBsMaxW = 32;   // dwords per row held in LDS (stride <= 128 bytes)
+
+template <int WC>
+__global__ __launch_bounds__(256) void bucket_scatter_rows_kernel(const E128* __restrict__ ent,
+                                                                  const uint32_t* __restrict__ rows,
+                                                                  uint32_t* __restrict__ out, uint64_t n,
+                                                                  uint32_t Wdyn,
+                                                                  const uint32_t* __restrict__ offsets,
+                                                                  uint32_t G, uint64_t per_block) {
+  constexpr int ITEMS = kBsTile / kBlock;
+  constexpr int LW = WC > 0 ? WC : kBsMaxW;
+  const uint32_t W = WC > 0 ? (uint32_t)WC : Wdyn;
+  __shared__ uint32_t srow[kBsTile * LW];
+  __shared__ uint16_t perm[kBsTile];
+  __shared__ uint8_t dslot[kBsTile];
+  __shared__ uint32_t wcnt[4][kBins];
+  __shared__ uint32_t goff[kBins];
+  __shared__ uint32_t bstart[kBins];
+  __shared__ uint32_t sc[4];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  goff[t] = offsets[(uint64_t)t * G + blockIdx.x];
+  const uint64_t beg = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  for (uint64_t base = beg; base < end; base += kBsTile) {
+    const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kBsTile ? (end - base) : kBsTile);
+    const uint32_t words = cnt * W;
+    const uint32_t* src = rows + base * W;
+    for (uint32_t j = t; j < words; j += kBlock) srow[j] = src[j];
+    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    __syncthreads();
+    uint32_t rk[ITEMS], dg[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kBsTile / 4) + r * 64 + l;
+      const bool valid = pos < cnt;
+      const uint32_t d = valid ? (uint32_t)(ent[base + pos].hi & 0xFF) : 0u;
+      uint64_t peers = ballot64(valid);
+#pragma unroll
+      for (int k = 0; k < kRadixBits; ++k) {
+        const bool bit = (d >> k) & 1u;
+        const uint64_t b = ballot64(bit);
+        peers &= bit ? b : ~b;
+      }
+      const uint32_t below = popc_below(peers);
+      const uint32_t prior = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      rk[r] = prior + below;
+      dg[r] = d;
+    }
+    __syncthreads();
+    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
+    uint32_t all;
+    bstart[t] = block_exclusive_scan256(tot, sc, all);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kBsTile / 4) + r * 64 + l;
+      if (pos < cnt) {
+        const uint32_t slot = bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
+        perm[slot] = (uint16_t)pos;
+        dslot[slot] = (uint8_t)dg[r];
+      }
+    }
+    __syncthreads();
+    // slot-major dword copy: consecutive lanes write consecutive dwords of consecutive slots, and
+    // consecutive slots of one bucket are consecutive rows of the output
+    for (uint32_t q = t; q < words; q += kBlock) {
+      const uint32_t j = q / W, c = q - j * W;
+      const uint32_t d = dslot[j];
+      out[((uint64_t)goff[d] + (j - bstart[d])) * W + c] = srow[(uint32_t)perm[j] * W + c];
+    }
+    __syncthreads();
+    goff[t] += tot;
+  }
+}
+}  // namespace
+
+// Stable bucket scatter of `n` fixed-width rows (stride % 4 == 0, stride <= 128) by the low byte
+// of entries[i].hi; `bucket_starts` (kBins + 1 uint64, device) receives every bucket's offset.
+DR_API int dr_bucket_scatter_rows(const E128* ent, const uint8_t* rows, uint8_t* out, uint64_t n,
+                                  uint32_t stride, void* ws, uint64_t* bucket_starts, hipStream_t s) {
+  if (stride == 0 || (stride & 3) || stride > 4 * kBsMaxW || n >= (1ull << 32)) return (int)hipErrorInvalidValue;
+  if (n == 0) {
+    hipMemsetAsync(bucket_starts, 0, sizeof(uint64_t) * (kBins + 1), s);
+    return 0;
+  }
+  uint32_t G; uint64_t per_block;
+  sort_geometry(n, G, per_block);
+  uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* partial = counts + (uint64_t)kBins * G;
+  rs_count<<<G, 256, 0, s>>>(ent, n, 64, counts, G, per_block);
+  scan_inplace(counts, kBins * G, partial, s);
+  rs_digit_totals<<<1, kBins, 0, s>>>(counts, G, n, bucket_starts);
+  const uint32_t W = stride / 4;
+  const uint32_t* in = reinterpret_cast<const uint32_t*>(rows);
+  uint32_t* o = reinterpret_cast<uint32_t*>(out);
+  if (W == 25)
+    bucket_scatter_rows_kernel<25><<<G, 256, 0, s>>>(ent, in, o, n, W, counts, G, per_block);
+  else
+    bucket_scatter_rows_kernel<0><<<G, 256, 0, s>>>(ent, in, o, n, W, counts, G, per_block);
   DR_LAUNCH_CHECK();
   return 0;
 }

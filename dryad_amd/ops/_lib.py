@@ -35,7 +35,8 @@ _SIGS = {
     "dr_partition_pass_u128": (c_i32, [vp, vp, c_u64, c_i32, vp, vp, vp]),
     "dr_extract_keys": (c_i32, [vp, c_u64, c_u32, c_u32, c_u32, c_u32, vp, vp]),
     "dr_gather_rows": (c_i32, [vp, vp, vp, vp, c_u64, c_u32, vp]),
-    "dr_range_dest_u128": (c_i32, [vp, vp, c_u64, vp, c_u32, c_u64, c_i32, vp]),
+    "dr_range_dest_u128": (c_i32, [vp, vp, c_u64, vp, c_u32, c_u64, c_i32, c_u32, c_u32, vp]),
+    "dr_bucket_scatter_rows": (c_i32, [vp, vp, vp, c_u64, c_u32, vp, vp, vp]),
     "dr_terasort_gen": (c_i32, [vp, c_u64, c_u64, c_u64, vp]),
     "dr_terasort_check": (c_i32, [vp, c_u64, vp, vp]),
     "dr_terasort_gen_keys": (c_i32, [vp, c_u64, c_u64, c_u64, vp, c_u32, vp, vp]),

@@ -8,13 +8,16 @@ channels) + ``MergeSort``/``Sort`` (LinqToDryad/DryadLinqQueryGen.cs:2362-2474 C
   1. extract   — key bytes -> 16-byte (key, row) entries              [HIP: dr_extract_keys]
   2. sample    — deterministic per-rank sample (seeded by rank = vertex id, so idempotent under
                  re-execution), all-gather, sort, pick world-1 evenly spaced separators
-  3. range-dest— per entry destination by binary search of the separators   [HIP: dr_range_dest_u128]
-  4. partition — one stable counting pass on the destination byte            [HIP: dr_partition_pass_u128]
-  5. pack      — gather rows into destination-contiguous send buffer        [HIP: dr_gather_rows]
-  6. exchange  — count all-to-all + payload all-to-all-v over xGMI          [RCCL]
-  7. local sort— extract + 80/96-bit LSD radix sort + row gather            [HIP]
+  3. range-dest— per entry key range (W * B ranges, B per destination rank) by binary search of
+                 the separators, numbered round-major                       [HIP: dr_range_dest_u128]
+  4. pack      — one stable LDS-staged bucket scatter of whole rows into a
+                 round-major send buffer                                    [HIP: dr_bucket_scatter_rows]
+  5. exchange  — count all-to-all + B payload all-to-all-v rounds over xGMI, all queued up front
+                                                                            [RCCL]
+  6. local sort— per received key range, while later rounds are in flight: extract + hybrid
+                 radix sort + row gather                                    [HIP]
 
-With world size 1 steps 2-6 are skipped.  All buffers are preallocated by the caller so a step does
+With world size 1 steps 2-5 are skipped.  All buffers are preallocated by the caller so a step does
 no HBM allocation (everything stays resident; 288 GB per GPU holds in + out + entries).
 """
 from __future__ import annotations
@@ -31,6 +34,11 @@ import os as _os
 # local sort algorithm: "hybrid" (top-window LSD + in-LDS run sort, default), "prefix"
 # (64-bit LSD + tie fix-up) or "lsd" (full-width LSD)
 SORT_ALGO = _os.environ.get("DRYAD_SORT_ALGO", "hybrid")
+# pipelined exchange of the multi-rank sort: key sub-ranges per destination rank (0 = from the
+# data size) and the target bytes per (source, destination) pair and round
+PIPE_SUBS = int(_os.environ.get("DRYAD_SHUFFLE_SUBS", "0"))
+PIPE_ROUND_BYTES = int(_os.environ.get("DRYAD_SHUFFLE_ROUND_BYTES", str(1 << 30)))
+_M64 = (1 << 64) - 1
 
 
 def key_bits(key_len: int) -> tuple[int, int, int]:
@@ -71,6 +79,7 @@ class SortBuffers:
 class SortStats:
     n_in: int = 0
     n_out: int = 0
+    rounds: int = 1
     send_counts: list = field(default_factory=list)
     recv_counts: list = field(default_factory=list)
 
@@ -106,10 +115,11 @@ def local_sort_rows(rows: torch.Tensor, out: torch.Tensor, ent_a: torch.Tensor, 
 
 
 def choose_separators(entries: torch.Tensor, n: int, world: World, lo_mask: int, sample_target: int,
-                      seed: int, tmp: torch.Tensor) -> torch.Tensor:
+                      seed: int, tmp: torch.Tensor, parts: int | None = None) -> torch.Tensor:
     """Sampler (reference DryadLinqSampler.cs:38-246): per-rank stride sample at ~0.001 (at least
-    min(n, 16) keys, at most sample_target), all-gathered, sorted on the GPU, world-1 separators at
-    evenly spaced ranks.  Deterministic given (rank, n, seed)."""
+    min(n, 16) keys, at most sample_target), all-gathered, sorted on the GPU, ``parts``-1
+    (default world-1) separators at evenly spaced ranks.  Deterministic given (rank, n, seed)."""
+    parts = parts or world.size
     m = max(1, min(n, max(16, min(sample_target, n // 1000 if n >= 16000 else n))))
     stride = max(1, n // m)
     off = (seed + world.rank * 7919) % stride if stride > 1 else 0
@@ -120,22 +130,53 @@ def choose_separators(entries: torch.Tensor, n: int, world: World, lo_mask: int,
     total = allsamp.shape[0]
     scratch = torch.empty_like(allsamp)
     srt = S.sort_entries(allsamp.contiguous(), 0, 128, tmp=scratch)
-    pos = torch.tensor([(j * total) // world.size for j in range(1, world.size)], dtype=torch.int64,
+    pos = torch.tensor([(j * total) // parts for j in range(1, parts)], dtype=torch.int64,
                        device=srt.device)
     return srt.index_select(0, pos).contiguous()
 
 
 def rank_hi_bounds(seps: torch.Tensor, rank: int) -> tuple[int, int]:
     """(min, max) of key ``hi`` words that range partition ``rank`` can receive."""
-    his = [int(x) & ((1 << 64) - 1) for x in seps[:, 1].tolist()]
-    lo = his[rank - 1] if rank > 0 else 0
-    hi = his[rank] if rank < len(his) else (1 << 64) - 1
-    return lo, hi
+    return _range_hi_bounds([int(x) & _M64 for x in seps[:, 1].tolist()], rank)
 
 
 def _as_i64(v: int) -> int:
     v &= (1 << 64) - 1
     return v - (1 << 64) if v >= (1 << 63) else v
+
+
+def pipeline_subs(max_rank_bytes: int, world_size: int) -> int:
+    """Key sub-ranges per destination rank of the pipelined exchange: about PIPE_ROUND_BYTES per
+    (source, destination) pair and round, at least 4 (small jobs run the same pipeline), and
+    world * subs <= 256 (one radix digit of bucket ids)."""
+    cap = max(1, 256 // world_size)
+    if PIPE_SUBS:
+        return max(1, min(PIPE_SUBS, cap))
+    want = -(-max_rank_bytes // max(1, world_size * PIPE_ROUND_BYTES))
+    b = 4
+    while b < want:
+        b <<= 1
+    return min(b, cap)
+
+
+def _range_hi_bounds(seps_hi: list, g: int) -> tuple[int, int]:
+    """(min, max) of the key ``hi`` words that key range ``g`` (between separators g-1 and g) holds."""
+    lo = seps_hi[g - 1] if g > 0 else 0
+    hi = seps_hi[g] if g < len(seps_hi) else (1 << 64) - 1
+    return lo, hi
+
+
+def _sort_keys(rows: torch.Tensor, ent: torch.Tensor, tmp: torch.Tensor, key_off: int, key_len: int,
+               hi_bounds) -> torch.Tensor:
+    """Extract + sort the entries of ``rows`` (row indices relative to ``rows``); returns the
+    tensor holding the sorted entries (``ent`` or ``tmp``)."""
+    e = S.extract_keys(rows, key_off, key_len, 0, out=ent)
+    b0, b1, _ = key_bits(key_len)
+    if SORT_ALGO == "hybrid":
+        return S.sort_entries_hybrid(e, b0, b1, tmp=tmp, hi_bounds=hi_bounds)
+    if SORT_ALGO == "prefix" and b0 < 64:
+        return S.sort_entries_prefix(e, b0, tmp=tmp)
+    return S.sort_entries(e, b0, b1, tmp=tmp)
 
 
 def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int, world: World | None = None,
@@ -146,7 +187,17 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
 
     On return rank r holds, in ``bufs.rows_out[:n_r]``, the r-th key range in ascending order.
     ``bufs.rows_in`` is clobbered (it becomes the receive buffer).  ``keys_ready``: ``bufs.ent_a[:n]``
-    already holds the rows' sort entries; ``hi_bounds``: known hi range of the local keys."""
+    already holds the rows' sort entries; ``hi_bounds``: known hi range of the local keys.
+
+    With several ranks the exchange is pipelined with the local sort.  The sampled separators cut
+    the key space into ``W * B`` ranges, B consecutive ones per destination rank.  One bucket
+    scatter packs the rows round-major (round b = every rank's b-th range), and the B rounds are
+    queued as RCCL all-to-all-v collectives up front.  Rank r receives round b as one contiguous
+    block holding ALL rows of its key range b, so it extracts + radix-sorts range b while rounds
+    b+1.. are still on the wire, and gathers the sorted rows into ``rows_out`` as soon as the
+    send region under them has gone out.  Only the last range's sort is exposed after the
+    exchange (reference: the sampler + RangePartition + MergeSort stages of
+    DryadLinqQueryGen.cs:2362-2474, CrossProduct channels GraphBuilder.cs:481-504)."""
     w = world or get_world()
     rows = bufs.rows_in[:n]
     if w.size == 1:
@@ -155,35 +206,58 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
         if stats is not None:
             stats.n_in = stats.n_out = n
         return out
-    stride = rows.shape[1]
-    b0, b1, lo_mask = key_bits(key_len)
+    W, stride = w.size, rows.shape[1]
     ent = bufs.ent_a[:n] if keys_ready else S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
+    _, _, lo_mask = key_bits(key_len)
     part_mask = lo_mask
-    if key_len <= 10 and w.size < (1 << 16):
+    if key_len <= 10 and W < (1 << 16):
         # skew: equal keys must not all land on one rank.  Bits 47..32 of lo are free for keys of
         # <= 10 bytes; with the rank there (and the row index below it) every entry is unique, so
         # the sampled separators split runs of equal keys across ranks while the global order
         # (key, rank, row) stays a valid OrderBy order.
         ent[:, 0].bitwise_or_(w.rank << 32)
         part_mask = (1 << 64) - 1
-    seps = choose_separators(ent, n, w, part_mask, sample_target, seed, bufs.ent_b)
-    S.range_dest(ent, seps, part_mask)                                   # ent.hi := destination
-    part, starts = S.partition_pass(ent, 64, out=bufs.ent_b[:n])        # stable by destination
-    S.gather_rows(rows, entries=part, out=bufs.rows_out[:n])            # pack send buffer
-    st = starts[: w.size + 1].cpu().tolist()
-    send_counts = [st[i + 1] - st[i] for i in range(w.size)]
-    recv_t = shuffle.exchange_counts(torch.tensor(send_counts, dtype=torch.int64), w)
-    recv_counts = [int(x) for x in recv_t.tolist()]
-    n_recv = sum(recv_counts)
+    nmax = torch.tensor([n], dtype=torch.int64, device=w.device)
+    shuffle.all_reduce_(nmax, "max", w)
+    B = pipeline_subs(int(nmax.item()) * stride, W)
+    seps = choose_separators(ent, n, w, part_mask, sample_target, seed, bufs.ent_b, parts=W * B)
+    seps_hi = [int(x) & _M64 for x in seps[:, 1].tolist()]
+    S.range_dest(ent, seps, part_mask, subs=B, ranks=W)                  # ent.hi := b * W + rank
+    st = S.bucket_scatter_rows(ent, rows, bufs.rows_out)                 # send buffer, round-major
+    send = [[st[b * W + r + 1] - st[b * W + r] for r in range(W)] for b in range(B)]
+    sc = torch.tensor([[send[b][r] for b in range(B)] for r in range(W)], dtype=torch.int64)
+    rc = shuffle.exchange_counts(sc.flatten(), w).view(W, B).tolist()    # rc[src][b]
+    off = [0]
+    for b in range(B):
+        off.append(off[-1] + sum(rc[s][b] for s in range(W)))
+    n_recv = off[-1]
     if n_recv > bufs.capacity:
         raise RuntimeError(f"range partition skew: rank {w.rank} receives {n_recv} rows > capacity {bufs.capacity}")
-    send_flat = bufs.rows_out.view(-1)
-    recv_flat = bufs.rows_in.view(-1)
-    shuffle.alltoallv_bytes(send_flat, [c * stride for c in send_counts], recv_flat,
-                            [c * stride for c in recv_counts], w)
-    out = local_sort_rows(bufs.rows_in[:n_recv], bufs.rows_out, bufs.ent_a, bufs.ent_b, key_off, key_len,
-                          hi_bounds=rank_hi_bounds(seps, w.rank))
+    send_flat, recv_flat = bufs.rows_out.view(-1), bufs.rows_in.view(-1)
+    handles = [shuffle.alltoallv_bytes_async(
+        send_flat[st[b * W] * stride: st[(b + 1) * W] * stride], [c * stride for c in send[b]],
+        recv_flat[off[b] * stride: off[b + 1] * stride], [rc[s][b] * stride for s in range(W)], w)
+        for b in range(B)]
+    out = bufs.rows_out
+    pending = []
+    for b in range(B):
+        shuffle.wait(handles[b])
+        a, z = off[b], off[b + 1]
+        if z > a:
+            srt = _sort_keys(bufs.rows_in[a:z], bufs.ent_a[a:z], bufs.ent_b[a:z], key_off, key_len,
+                             _range_hi_bounds(seps_hi, w.rank * B + b))
+            pending.append((a, z, srt))
+        # rows_out[:sent] has been sent (rounds <= b are complete); rows_out[n:] never held data
+        sent = st[(b + 1) * W]
+        keep = []
+        for a2, z2, s2 in pending:
+            if b == B - 1 or z2 <= sent or a2 >= n:
+                S.gather_rows(bufs.rows_in[a2:z2], entries=s2, out=out[a2:z2])
+            else:
+                keep.append((a2, z2, s2))
+        pending = keep
     if stats is not None:
-        stats.n_in, stats.n_out = n, n_recv
-        stats.send_counts, stats.recv_counts = send_counts, recv_counts
-    return out
+        stats.n_in, stats.n_out, stats.rounds = n, n_recv, B
+        stats.send_counts = [sum(send[b][r] for b in range(B)) for r in range(W)]
+        stats.recv_counts = [sum(rc[s]) for s in range(W)]
+    return out[:n_recv]

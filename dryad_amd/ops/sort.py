@@ -211,16 +211,39 @@ def gather_rows(rows: torch.Tensor, entries: torch.Tensor | None = None, index: 
 
 
 def range_dest(entries: torch.Tensor, separators: torch.Tensor, lo_mask: int, descending: bool = False,
-               out: torch.Tensor | None = None) -> torch.Tensor:
-    """Replace entries[i].hi by its destination partition (count of separators before the key)."""
+               out: torch.Tensor | None = None, subs: int = 1, ranks: int = 1) -> torch.Tensor:
+    """Replace entries[i].hi by its destination partition (count of separators before the key).
+
+    With ``subs`` > 1 the ``ranks * subs`` key ranges are renumbered sub-range-major
+    (range ``r * subs + b`` -> ``b * ranks + r``): one partition pass then lays out round ``b`` of a
+    pipelined exchange as a contiguous, destination-ordered block."""
     _lib.require_gpu_tensor(entries, "range_dest")
     n = entries.shape[0]
     if out is None:
         out = entries
     nsep = separators.shape[0]
     _lib.call("dr_range_dest_u128", ptr(entries), ptr(out), c_u64(n), ptr(separators), c_u32(nsep),
-              c_u64(lo_mask & 0xFFFFFFFFFFFFFFFF), int(descending), stream_of(entries))
+              c_u64(lo_mask & 0xFFFFFFFFFFFFFFFF), int(descending), c_u32(subs), c_u32(ranks), stream_of(entries))
     return out
+
+
+def bucket_scatter_rows(entries: torch.Tensor, rows: torch.Tensor, out: torch.Tensor) -> list:
+    """Stable scatter of fixed-width ``rows`` into bucket order, bucket = low byte of
+    ``entries[i].hi`` (row i <-> entry i), into ``out``.  Returns the 257 bucket start offsets
+    (host list).  One coalesced LDS-staged pass over the rows (dr_bucket_scatter_rows) instead of
+    a partition pass of the entries plus a row gather through them."""
+    _lib.require_gpu_tensor(rows, "bucket_scatter_rows")
+    assert rows.dtype == torch.uint8 and rows.dim() == 2 and out.shape[0] >= rows.shape[0]
+    n, stride = rows.shape
+    if stride % 4 or stride > 128:
+        part, starts = partition_pass(entries[:n], 64)
+        gather_rows(rows, entries=part, out=out[:n])
+        return starts.tolist()
+    starts = torch.empty(257, dtype=torch.int64, device=rows.device)
+    ws = _workspace(n, rows.device)
+    _lib.call("dr_bucket_scatter_rows", ptr(entries), ptr(rows), ptr(out), c_u64(n), c_u32(stride), ptr(ws),
+              ptr(starts), stream_of(rows))
+    return starts.tolist()
 
 
 def entries_to_key_int(entries: torch.Tensor, lo_keep_bits: int = 64):

@@ -103,6 +103,29 @@ def alltoallv_bytes(send: torch.Tensor, send_counts: list[int], recv: torch.Tens
     return recv
 
 
+def alltoallv_bytes_async(send: torch.Tensor, send_counts: list[int], recv: torch.Tensor, recv_counts: list[int],
+                          world: World | None = None):
+    """``alltoallv_bytes`` that does not wait: over RCCL the collective is queued on the
+    communicator's stream and the caller's stream keeps running; ``wait(handle)`` later makes the
+    caller's stream wait for it (the pipelined range shuffle sorts sub-range b while round b+1 is
+    on the wire).  Other transports (gloo staging through the host, rounds chunked past
+    CHUNK_BYTES per peer) complete before returning and give ``None``."""
+    w = world or get_world()
+    if (w.size > 1 and w.backend == "nccl" and send.is_cuda and recv.is_cuda
+            and max(max(send_counts), max(recv_counts)) <= CHUNK_BYTES):
+        ts, tr = sum(send_counts), sum(recv_counts)
+        return dist.all_to_all_single(recv[:tr], send[:ts], output_split_sizes=list(recv_counts),
+                                      input_split_sizes=list(send_counts), async_op=True)
+    alltoallv_bytes(send, send_counts, recv, recv_counts, w)
+    return None
+
+
+def wait(handle) -> None:
+    """Make the current stream wait for an ``alltoallv_bytes_async`` handle."""
+    if handle is not None:
+        handle.wait()
+
+
 def all_gather_tensor(t: torch.Tensor, world: World | None = None) -> torch.Tensor:
     """All-gather equally shaped tensors along dim 0 (R5: sampler gather, R3 broadcast of small data)."""
     w = world or get_world()

@@ -44,6 +44,29 @@ def main():
     out = RS.distributed_sort_rows(bufs, n, 0, 8, w, stats=st)
     assert abs(st.n_out - n) <= 0.05 * n, (w.rank, st.n_out)
     assert torch.equal(out[:, :8], torch.full_like(out[:, :8], 7))
+    # uneven inputs per rank through the pipelined exchange (several key sub-ranges per rank):
+    # checksum, record count, in-rank order and cross-rank boundaries
+    from dryad_amd.ops import terasort as TS
+    from dryad_amd.parallel import shuffle
+    for subs in (0, 3):
+        RS.PIPE_SUBS = subs
+        n = 150_000 if w.rank == 0 else 40_000
+        bufs = RS.SortBuffers.allocate(190_000, 100, w.device)
+        TS.generate(bufs.rows_in[:n], w.rank * 1_000_000, 99)
+        acc_in = TS.check(bufs.rows_in[:n]).clone()
+        st = RS.SortStats()
+        out = RS.distributed_sort_rows(bufs, n, 0, 10, w, stats=st)
+        assert st.rounds == (RS.pipeline_subs(150_000 * 100, w.size) if subs == 0 else subs), st.rounds
+        acc_out = TS.check(out)
+        tot = torch.stack([acc_in[0], acc_out[0], acc_out[1], torch.tensor(out.shape[0], device=w.device)])
+        shuffle.all_reduce_(tot, "sum", w)
+        assert int(tot[0]) == int(tot[1]) and int(tot[2]) == 0 and int(tot[3]) == 190_000, tot.tolist()
+        ends = torch.zeros((1, 20), dtype=torch.uint8, device=w.device)
+        ends[0, :10], ends[0, 10:] = out[0, :10], out[-1, :10]
+        allends = shuffle.all_gather_tensor(ends, w).cpu().numpy()
+        for r in range(w.size - 1):
+            assert bytes(allends[r, 10:]) <= bytes(allends[r + 1, :10]), r
+    RS.PIPE_SUBS = 0
     w.barrier()
     if w.rank == 0:
         print("MULTIRANK_OK", w.size, flush=True)

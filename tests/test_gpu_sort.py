@@ -96,6 +96,39 @@ def test_range_dest_matches_searchsorted():
     assert torch.equal(out[:, 0], e[:, 0])
 
 
+def test_range_dest_sub_major_numbering():
+    from dryad_amd.ops import sort as S
+    n = 40_000
+    e = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    e[:, 1] = torch.randint(0, 800, (n,), device="cuda")
+    e[:, 0] = torch.arange(n, device="cuda")
+    sv = torch.tensor([100, 200, 300, 400, 500, 600, 700], device="cuda")   # 8 ranges = 2 ranks x 4 subs
+    seps = torch.zeros((7, 2), dtype=torch.int64, device="cuda")
+    seps[:, 1] = sv
+    out = S.range_dest(e.clone(), seps, 0, subs=4, ranks=2)
+    g = torch.searchsorted(sv, e[:, 1], right=False)                  # range r * 4 + b
+    assert torch.equal(out[:, 1], (g % 4) * 2 + g // 4)
+    assert torch.equal(out[:, 0], e[:, 0])
+
+
+@pytest.mark.parametrize("n,stride,nb", [(1, 100, 8), (5000, 100, 3), (300_001, 100, 128), (70_000, 16, 256),
+                                         (4097, 36, 17), (100_000, 128, 64), (20_000, 132, 5)])
+def test_bucket_scatter_rows_is_a_stable_partition(n, stride, nb):
+    from dryad_amd.ops import sort as S
+    g = torch.Generator(device="cuda").manual_seed(n + stride)
+    rows = torch.randint(0, 256, (n, stride), dtype=torch.uint8, device="cuda", generator=g)
+    e = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    e[:, 1] = torch.randint(0, nb, (n,), device="cuda", generator=g)
+    e[:, 0] = torch.arange(n, device="cuda")
+    out = torch.empty_like(rows)
+    st = S.bucket_scatter_rows(e, rows, out)
+    d = e[:, 1].cpu().numpy()
+    order = np.argsort(d, kind="stable")
+    np.testing.assert_array_equal(out.cpu().numpy(), rows.cpu().numpy()[order])
+    h = np.bincount(d, minlength=256)
+    np.testing.assert_array_equal(np.array(st), np.concatenate([[0], np.cumsum(h)]))
+
+
 def test_terasort_generate_and_check():
     from dryad_amd.ops import terasort as TS
     n = 100_000
