@@ -288,7 +288,8 @@ def GroupJoin(outer, inner, outer_key, inner_key, result_sel, comparer=None):
         table.setdefault(wrap(k), []).append(y)
     for x in outer:
         k = outer_key(x)
-        yield result_sel(x, list(table.get(wrap(k), ())) if k is not None else [])
+        # the group is an IEnumerable<TInner> in the reference: LINQ methods (g.Count(), g.Sum(...))
+        yield result_sel(x, LinqList(table.get(wrap(k), ())) if k is not None else LinqList())
 
 
 def Distinct(src, comparer=None):

@@ -9,7 +9,8 @@ the object implementation for that op only.
 Hot paths are HIP kernels: key normalisation (dr_build_keys / dr_extract_keys), LSD radix sort
 (dr_sort_u128), hashing and partition passes (dr_hash_dest / dr_partition_pass_u128), range
 destinations (dr_range_dest_u128), segmented reductions (dr_seg_reduce), merge-join expansion
-(dr_join_ranges / dr_join_emit), row gathers (dr_gather_rows) and the synthetic TeraSort store.
+(dr_join_ranges / dr_join_emit), the hash join (dr_hj_*), whole-partition aggregates
+(dr_reduce_multi), row gathers (dr_gather_rows) and the synthetic TeraSort store.
 Elementwise projections/predicates are traced user lambdas executed as PyTorch-ROCm tensor ops.
 """
 from __future__ import annotations
@@ -72,31 +73,73 @@ def key_entries(table: DeviceTable, key_fn, comparer=None, descending=False):
     return e, b0, lo_mask
 
 
+def _wide(cols) -> bool:
+    """Key columns that do not fit one 128-bit sort entry (96 key bits + the 32-bit row index)."""
+    return len(cols) > 4 or R.key_bit_count(cols) > 96
+
+
+def _wide_key(cols):
+    """Wide key columns -> (int64 Rabin-64 fingerprint of each row's packed key bytes, the packed
+    bytes).  -0.0 and 0.0 pack alike (one key, as in Python)."""
+    from ..ops.fingerprint import rabin_rows
+    parts = []
+    for c in cols:
+        if c.is_floating_point():
+            c = c + 0.0
+        parts.append(c.contiguous().view(torch.uint8).reshape(c.shape[0], -1))
+    packed = torch.cat(parts, 1).contiguous()
+    return rabin_rows(packed), packed
+
+
+def _rows_differ(pa, ia, pb, ib) -> bool:
+    """True if some packed byte row pa[ia[i]] differs from pb[ib[i]] (ia None = identity)."""
+    from ..ops.fingerprint import strings_differ
+
+    def trip(p):
+        w = p.shape[1]
+        off = torch.arange(p.shape[0], dtype=torch.int64, device=p.device) * w
+        return p.reshape(-1), off, torch.full_like(off, w)
+    return strings_differ(trip(pa), ia, trip(pb), ib)
+
+
 def eq_key_entries(table: DeviceTable, key_fn, comparer=None):
     """Entries for equality-only consumers (HashPartition, Join): like key_entries, but string
-    fields are keyed by their Rabin-64 fingerprints.  -> (entries, begin_bit, lo_mask, skeys)."""
+    fields are keyed by their Rabin-64 fingerprints, and keys wider than one 96-bit entry (or byte
+    keys longer than 12 bytes) by the fingerprint of their packed bytes.
+    -> (entries, begin_bit, lo_mask, skeys, wide): ``wide`` = (packed key bytes, key layout) for a
+    fingerprinted wide key (callers that pair rows verify the bytes), else None."""
     if table.heap is not None:
         raise NotTraceable("text records")
     if comparer is not None:
         raise NotTraceable("custom comparer")
     if table.n == 0:
-        return torch.empty((0, 2), dtype=torch.int64, device=table.device), 64, 0, []
+        return torch.empty((0, 2), dtype=torch.int64, device=table.device), 64, 0, [], None
     res = TR.call(key_fn, table)
     try:
         kind, spec = TR.key_columns(res, table)
     except NotTraceable:
         kind = "str"
-    if kind != "str":
-        e, b0, lo_mask = key_entries(table, key_fn, comparer)
-        return e, b0, lo_mask, []
-    cols, skeys = TR.eq_key_columns(res, table)
+    if kind == "bytes":
+        if spec.length <= 12:
+            e, b0, lo_mask = key_entries(table, key_fn, comparer)
+            return e, b0, lo_mask, [], None
+        from ..ops.fingerprint import rabin_rows
+        packed = table.rows[:, spec.off:spec.off + spec.length].contiguous()
+        e, b0, lo_mask = R.build_keys([rabin_rows(packed)])
+        return e, b0, lo_mask, [], (packed, ("bytes", spec.length))
+    if kind == "cols":
+        cols, skeys = spec, [None] * len(spec)
+    else:
+        cols, skeys = TR.eq_key_columns(res, table)
     for c in cols:
-        if c.dtype not in R.KEY_TYPES:
+        if c.dtype not in R.KEY_TYPES or c.dim() != 1:
             raise NotTraceable(f"key dtype {c.dtype}")
-    if R.key_bit_count(cols) > 96:
-        raise NotTraceable("composite key wider than 96 bits")
+    if _wide(cols):
+        fp, packed = _wide_key(cols)
+        e, b0, lo_mask = R.build_keys([fp])
+        return e, b0, lo_mask, skeys, (packed, tuple(str(c.dtype) for c in cols))
     e, b0, lo_mask = R.build_keys(cols)
-    return e, b0, lo_mask, skeys
+    return e, b0, lo_mask, skeys, None
 
 
 def _perm(entries: torch.Tensor) -> torch.Tensor:
@@ -312,7 +355,7 @@ def op_hash_partition(op, inputs, v):
         raise NotTraceable("custom comparer")
     if t.n == 0:
         return Ported(t, [0] * (n + 1))
-    e, _, lo_mask, _ = eq_key_entries(t, op["key"])
+    e, _, lo_mask, _, _ = eq_key_entries(t, op["key"])
     R.hash_dest(e, lo_mask, n)
     part, starts = S.partition_pass(e, 64)
     st = starts[: n + 1].tolist()
@@ -405,14 +448,24 @@ def _partial_table(out, strs, d, nkeys, form):
 
 
 def _group_keys(kcols, skeys):
-    """Sort by the key columns -> (srt, seg, nseg, rows_at_start).  With string keys, every row is
-    checked against its group's representative so a fingerprint collision can never merge two
-    different strings (the operator falls back to the host if one ever occurs)."""
-    e, b0, lo_mask = R.build_keys(kcols)
+    """Sort by the key columns -> (srt, seg, nseg, rows_at_start, starts).  String keys and keys
+    wider than one 96-bit entry are sorted by Rabin-64 fingerprints; every row is then checked
+    against its group's representative so a fingerprint collision can never merge two different
+    keys (the operator falls back to the host if one ever occurs)."""
+    if any(c.dtype not in R.KEY_TYPES or c.dim() != 1 for c in kcols):
+        raise NotTraceable("group key of a non-key dtype")
+    packed = None
+    if _wide(kcols):
+        fp, packed = _wide_key(kcols)
+        e, b0, lo_mask = R.build_keys([fp])
+    else:
+        e, b0, lo_mask = R.build_keys(kcols)
     srt = S.sort_entries_hybrid(e, b0)
     seg, nseg, starts = R.segment_ids(srt, lo_mask)
     perm = _perm(srt)
     rows_at_start = perm.index_select(0, starts)
+    if packed is not None and _rows_differ(packed, perm, packed, rows_at_start.index_select(0, seg)):
+        raise NotTraceable("wide key fingerprint collision")
     if any(sk is not None for sk in skeys):
         from ..ops.fingerprint import strings_differ
         rep = rows_at_start.index_select(0, seg)          # representative row, in sorted order
@@ -421,12 +474,17 @@ def _group_keys(kcols, skeys):
                 trip = (sk.heap, sk.off, sk.len)
                 if strings_differ(trip, perm, trip, rep):
                     raise NotTraceable("string key fingerprint collision")
-    return srt, seg, nseg, rows_at_start
+    return srt, seg, nseg, rows_at_start, starts
 
 
-def _key_outputs(kcols, skeys, rows_at_start):
-    """Per-group key columns (string keys keep their heap) -> (cols, strs)."""
+def _key_outputs(kcols, skeys, rows_at_start, srt=None, starts=None):
+    """Per-group key columns (string keys keep their heap) -> (cols, strs).  A single int64 key
+    is decoded from the sorted entries at the group starts (hi = key ^ sign bit, a near-sequential
+    read) instead of a random gather of the key column."""
     out, strs = {}, {}
+    if srt is not None and len(kcols) == 1 and skeys[0] is None and kcols[0].dtype == torch.int64:
+        out["k0"] = srt[:, 1].index_select(0, starts).bitwise_xor_(-(1 << 63))
+        return out, strs
     for i, (c, sk) in enumerate(zip(kcols, skeys)):
         if sk is None:
             out[f"k{i}"] = c.index_select(0, rows_at_start)
@@ -486,8 +544,8 @@ def op_group_partial(op, inputs, v):
                 for nm, r in zip(names, res):
                     out[nm] = r
                 return _partial_table(out, {}, d, 1, form)
-    srt, seg, nseg, rows_at_start = _group_keys(kcols, skeys)
-    out, strs = _key_outputs(kcols, skeys, rows_at_start)
+    srt, seg, nseg, rows_at_start, starts = _group_keys(kcols, skeys)
+    out, strs = _key_outputs(kcols, skeys, rows_at_start, srt, starts)
     # every aggregate in one fused segmented-reduce pass
     for nm, res in zip(names, R.seg_reduce_multi(srt, seg, nseg, specs)):
         out[nm] = res
@@ -504,8 +562,8 @@ def op_group_final(op, inputs, v):
     nkeys = t.shape.pytype.nkeys
     kcols, skeys = TR.eq_key_columns(tuple(TR.Col(v) if isinstance(v, torch.Tensor) else v
                                            for v in _key_values(t, nkeys)), t)
-    srt, seg, nseg, rows_at_start = _group_keys(kcols, skeys)
-    kout, kstrs = _key_outputs(kcols, skeys, rows_at_start)
+    srt, seg, nseg, rows_at_start, starts = _group_keys(kcols, skeys)
+    kout, kstrs = _key_outputs(kcols, skeys, rows_at_start, srt, starts)
     keys = _key_values(DeviceTable(nseg, Shape("tuple", list(kout)), kout, strs=kstrs), nkeys)
     specs = []
     for j, a in enumerate(d.aggs):
@@ -573,38 +631,48 @@ def op_group_by(op, inputs, v):
 # ---------------------------------------------------------------------------------------------
 def op_distinct(op, inputs, v):
     t = _check(_one(inputs))
-    if t.heap is not None or t.strs:
-        raise NotTraceable("string records")
     if op.get("comparer") is not None:
         raise NotTraceable("custom comparer")
     if t.n <= 1:
         return t
-    if t.rows is not None:
-        if t.rows.shape[1] > 12:
-            raise NotTraceable("wide rows")
-        e, b0, lo_mask = key_entries(t, lambda r: r[0:t.rows.shape[1]])
-    else:
-        cols = [t.cols[f] for f in t.shape.fields]
-        if R.key_bit_count(cols) > 96:
-            raise NotTraceable("record wider than 96 bits")
-        e, b0, lo_mask = R.build_keys(cols)
+    e, b0, lo_mask, packed = _record_entries(t)
     srt = S.sort_entries_hybrid(e, b0)
-    _, _, starts = R.segment_ids(srt, lo_mask)
+    seg, _, starts = R.segment_ids(srt, lo_mask)
+    _verify_segments(packed, srt, seg, starts)
     return t.take(_perm(srt).index_select(0, starts))
 
 
 def _record_entries(t):
-    if t.strs:
+    """Whole-record keys for Distinct / set operations -> (entries, begin_bit, lo_mask, packed):
+    records up to 96 bits (rows up to 12 bytes) are their own sort key; wider fixed-width records
+    are keyed by the Rabin-64 fingerprint of their packed bytes (``packed`` is returned for the
+    byte-for-byte segment check)."""
+    if t.heap is not None or t.strs:
         raise NotTraceable("records with string fields")
     if t.rows is not None:
-        if t.rows.shape[1] > 12:
-            raise NotTraceable("wide rows")
-        return key_entries(t, lambda r: r[0:t.rows.shape[1]])
-    cols = [t.cols[f] for f in t.shape.fields]
-    if R.key_bit_count(cols) > 96:
-        raise NotTraceable("record wider than 96 bits")
-    e, b0, lo_mask = R.build_keys(cols)
-    return e, b0, lo_mask
+        if t.rows.shape[1] <= 12:
+            e, b0, lm = key_entries(t, lambda r: r[0:t.rows.shape[1]])
+            return e, b0, lm, None
+        packed = t.rows.contiguous()
+    else:
+        cols = [t.cols[f] for f in t.shape.fields]
+        if all(c.dim() == 1 and c.dtype in R.KEY_TYPES for c in cols) and not _wide(cols):
+            e, b0, lm = R.build_keys(cols)
+            return e, b0, lm, None
+        packed = torch.cat([(c + 0.0 if c.is_floating_point() else c).contiguous().view(torch.uint8)
+                            .reshape(t.n, -1) for c in cols], 1).contiguous()
+    from ..ops.fingerprint import rabin_rows
+    e, b0, lm = R.build_keys([rabin_rows(packed)])
+    return e, b0, lm, packed
+
+
+def _verify_segments(packed, srt, seg, starts):
+    """NotTraceable if two different records share a fingerprint segment."""
+    if packed is None:
+        return
+    perm = _perm(srt)
+    if _rows_differ(packed, perm, packed, perm.index_select(0, starts).index_select(0, seg)):
+        raise NotTraceable("record fingerprint collision")
 
 
 def _set_op(kind, op, inputs):
@@ -620,9 +688,10 @@ def _set_op(kind, op, inputs):
     both = DeviceTable.concat([a, b])
     if both.n == 0:
         return both
-    e, b0, lo_mask = _record_entries(both)
+    e, b0, lo_mask, packed = _record_entries(both)
     srt = S.sort_entries_hybrid(e, b0)
     seg, nseg, starts = R.segment_ids(srt, lo_mask)
+    _verify_segments(packed, srt, seg, starts)
     first = _perm(srt).index_select(0, starts)
     if kind == "union":
         return both.take(first)
@@ -664,57 +733,302 @@ def op_skip_while(op, inputs, v):
     return t.slice(_while_cut(op, t), t.n)
 
 
-def op_hash_join(op, inputs, v):
-    outer, inner = _check(inputs[0]), _check(inputs[1])
+def _join_pairs(op, outer, inner, hashed):
+    """(outer_row, inner_row, per-outer match counts) of equal keys.  ``hashed``: device hash
+    table on the inner keys probed in outer row order (hashjoin.hip: LINQ Join order); else
+    radix-sorted entries + merge-path ranges (key order).  Pairs matched through fingerprints
+    (string / wide keys) are verified byte for byte."""
     if op.get("comparer") is not None:
         raise NotTraceable("custom comparer")
-    if outer.n == 0 or inner.n == 0:
-        raise NotTraceable("empty join side: output type unknown")
-    eo, b0, lm, so_keys = eq_key_entries(outer, op["outer_key"])
-    ei, b1, lm2, si_keys = eq_key_entries(inner, op["inner_key"])
-    if (b0, lm) != (b1, lm2) or [k is None for k in so_keys] != [k is None for k in si_keys]:
+    eo, b0, lm, so_keys, wo = eq_key_entries(outer, op["outer_key"])
+    ei, b1, lm2, si_keys, wi = eq_key_entries(inner, op["inner_key"])
+    if (b0, lm) != (b1, lm2) or [k is None for k in so_keys] != [k is None for k in si_keys] or \
+            (wo is None) != (wi is None) or (wo is not None and wo[1] != wi[1]):
         raise NotTraceable("join keys of different types")
-    so = S.sort_entries_hybrid(eo, b0)
-    si = S.sort_entries_hybrid(ei, b0)
-    oo, ii, _ = R.merge_join_pairs(so, si, lm)
-    if oo.shape[0] == 0:
-        raise NotTraceable("empty join result")
-    if so_keys:
-        # string keys matched by fingerprint: every emitted pair must hold equal strings
+    if hashed:
+        oo, ii, cnt = R.hash_join_pairs(eo, ei, lm)
+    else:
+        so = S.sort_entries_hybrid(eo, b0)
+        si = S.sort_entries_hybrid(ei, b0)
+        oo, ii, cnt = R.merge_join_pairs(so, si, lm)
+    if oo.shape[0]:
         from ..ops.fingerprint import strings_differ
         for a, b in zip(so_keys, si_keys):
             if a is not None and strings_differ((a.heap, a.off, a.len), oo, (b.heap, b.off, b.len), ii):
                 raise NotTraceable("string key fingerprint collision")
+        if wo is not None and _rows_differ(wo[0], oo, wi[0], ii):
+            raise NotTraceable("wide key fingerprint collision")
+    return oo, ii, cnt
+
+
+def _join(op, inputs, hashed):
+    outer, inner = _check(inputs[0]), _check(inputs[1])
+    if outer.n == 0 or inner.n == 0:
+        raise NotTraceable("empty join side: output type unknown")
+    oo, ii, _ = _join_pairs(op, outer, inner, hashed)
+    if oo.shape[0] == 0:
+        raise NotTraceable("empty join result")
     a, b = outer.take(oo), inner.take(ii)
-    res = op["result"](TR.proxy(a), TR.proxy(b))
-    return TR.to_table(res, a)
+    return _result_table(_traced(op["result"], TR.proxy(a), TR.proxy(b)), a)
 
 
-op_merge_join = op_hash_join
+def op_hash_join(op, inputs, v):
+    """Join (K8; reference HashJoin DryadLinqVertex.cs:852-897): a device hash table on the inner
+    keys, probed in outer row order (csrc/kernels/hashjoin.hip)."""
+    return _join(op, inputs, True)
+
+
+def op_merge_join(op, inputs, v):
+    """Join of key-ordered inputs (K9; reference MergeJoin DryadLinqVertex.cs:898-1070)."""
+    return _join(op, inputs, False)
+
+
+def op_hash_group_join(op, inputs, v):
+    """GroupJoin whose result selector only folds the group with decomposable aggregates
+    (Count / Sum / Min / Max / Average / Any / All; reference HashGroupJoin DryadLinqVertex.cs:
+    1071-1116): hash-join pairs in outer row order -> per-outer-row segmented reductions over the
+    matched inner rows -> the result template evaluated over the outer records' columns."""
+    from ..compiler.decomposition import decompose
+    outer, inner = _check(inputs[0]), _check(inputs[1])
+    if outer.n == 0 or inner.n == 0:
+        raise NotTraceable("empty GroupJoin side")
+    d = decompose(op["result"])
+    if d is None or any(a.kind not in ("count", "sum", "min", "max", "avg", "any", "all") for a in d.aggs):
+        raise NotTraceable("GroupJoin result selector does not decompose into device aggregates")
+    oo, ii, cnt = _join_pairs(op, outer, inner, True)
+    if any(a.kind in ("min", "max", "avg") for a in d.aggs) and bool((cnt == 0).any()):
+        raise NotTraceable("Min / Max / Average over an empty group")
+    specs, plan = [], []
+    for a in d.aggs:
+        val = _agg_value(a, inner)
+        if a.kind == "count" and val is None:
+            plan.append(("count", None))
+            continue
+        if a.kind in ("count", "any", "all"):
+            specs.append(("sum", val, torch.int64))
+        elif a.kind == "avg":
+            specs.append(("sum", val, torch.float64))
+        else:
+            specs.append((a.kind, val, val.dtype))
+        plan.append((a.kind, len(specs) - 1))
+    ent = torch.stack([ii, torch.zeros_like(ii)], 1).contiguous()
+    red = R.seg_reduce_multi(ent, oo, outer.n, specs) if specs else []
+    vals = []
+    for kind, j in plan:
+        r = cnt if j is None else red[j]
+        if kind == "avg":
+            r = r / cnt.to(torch.float64)
+        elif kind == "any":
+            r = r > 0
+        elif kind == "all":
+            r = r == cnt
+        vals.append(r)
+    env = {"key": TR.proxy(outer), "aggs": [TR.Col(x) for x in vals]}
+    try:
+        res = substitute(d.template, env)
+    except NotTraceable:
+        raise
+    except Exception as ex:  # noqa: BLE001
+        raise NotTraceable(f"result template: {ex}")
+    return _result_table(res, outer)
+
+
+op_merge_group_join = op_hash_group_join
 
 
 # ---------------------------------------------------------------------------------------------
-# aggregates: partial per partition (device reductions) -> final on one vertex
+# aggregates (K11): the partial of every partition is ONE pass of the reduce kernel over its HBM
+# columns (ops/reduce.py, csrc/kernels/reduce.hip); partials are host scalars in the object
+# path's format, so the final vertex (one value per partition) folds them with the object code
+_EMPTY_PARTIAL = {"Count": 0, "Sum": 0, "Average": (0, 0), "Any": False, "All": True, "Contains": False,
+                  "First": (False, None), "FirstOrDefault": (False, None), "Last": (False, None),
+                  "LastOrDefault": (False, None), "Single": (0, None), "SingleOrDefault": (0, None)}
+
+
+def _agg_column(sel, t):
+    """The numeric column an aggregate folds: the records themselves or the traced selector."""
+    if sel is None:
+        if t.shape.kind != "scalar":
+            raise NotTraceable("aggregate over non-scalar records")
+        c = t.cols[t.shape.fields[0]]
+    else:
+        r = TR.call(sel, t)
+        if not isinstance(r, TR.Col):
+            raise NotTraceable("aggregate selector must produce a numeric field")
+        c = r.t.expand(t.n) if r.t.dim() == 0 else r.t
+    if c.dim() != 1 or c.is_complex():
+        raise NotTraceable("aggregate over a non-scalar field")
+    return c
+
+
+def _record_at(t, i):
+    return t.slice(i, i + 1).to_objects()[0]
+
+
 def op_agg_partial(op, inputs, v):
+    from ..ops import reduce as RD
+    from ..runtime.vertex_ops import _NONE
     t = _check(_one(inputs))
     s = op["spec"]
     k = s["kind"]
     if s.get("comparer") is not None:
-        raise NotTraceable("comparer")
+        raise NotTraceable("custom comparer")
+    if k not in _EMPTY_PARTIAL and k not in ("Min", "Max"):
+        raise NotTraceable(f"{k} with a user accumulator runs on the host")
+    n, dev = t.n, t.device
+    if n == 0:
+        return [_NONE if k in ("Min", "Max") else _EMPTY_PARTIAL[k]]
+    pred = s.get("predicate")
+    mask = TR.to_mask(TR.call(pred, t), t) if pred is not None else None
     if k == "Count":
-        if s.get("predicate") is None:
-            return _scalar_table([t.n], torch.int64, v.device)
-        if t.n == 0:
-            return _scalar_table([0], torch.int64, v.device)
-        return _scalar_table([int(TR.to_mask(TR.call(s["predicate"], t), t).sum().item())], torch.int64, v.device)
-    raise NotTraceable(f"aggregate {k} on host")
+        return [n if mask is None else RD.reduce_multi(n, [(RD.COUNT, None, mask)], dev)[0]]
+    if k in ("Any", "All"):
+        c = n if mask is None else RD.reduce_multi(n, [(RD.COUNT, None, mask)], dev)[0]
+        return [c > 0] if k == "Any" else [c == n]
+    if k in ("Sum", "Average", "Min", "Max"):
+        col = _agg_column(s.get("selector"), t)
+        rop = {"Sum": RD.SUM, "Average": RD.SUM, "Min": RD.MIN, "Max": RD.MAX}[k]
+        r = RD.reduce_multi(n, [(rop, col, None)], dev)[0]
+        if k == "Average":
+            return [(r, n)]
+        return [bool(r) if col.dtype == torch.bool and k != "Sum" else r]
+    if k == "Contains":
+        val = s.get("value")
+        if t.shape.kind != "scalar" or isinstance(val, bool) or not isinstance(val, (int, float)):
+            raise NotTraceable("Contains of a non-numeric value")
+        hit = t.cols[t.shape.fields[0]] == val
+        return [RD.reduce_multi(n, [(RD.COUNT, None, hit)], dev)[0] > 0]
+    if k.startswith("First") or k.startswith("Last"):
+        first = k.startswith("First")
+        i = (0 if first else n - 1) if mask is None else \
+            RD.reduce_multi(n, [(RD.FIRST if first else RD.LAST, None, mask)], dev)[0]
+        return [(False, None)] if i is None else [(True, _record_at(t, i))]
+    # Single / SingleOrDefault: the number of matches and the first one
+    c, i = (n, 0) if mask is None else RD.reduce_multi(n, [(RD.COUNT, None, mask), (RD.FIRST, None, mask)], dev)
+    return [(c, _record_at(t, i) if c else None)]
+
+
+def _host_partials(inputs) -> list:
+    out = []
+    for x in inputs:
+        if isinstance(x, DeviceTable):
+            out.extend(x.to_objects())
+        elif isinstance(x, list):
+            out.extend(x)
+    return out
 
 
 def op_agg_final(op, inputs, v):
+    """Fold the per-partition partials (one host value per partition, the reference's final
+    aggregate vertex) with the object implementation; device-table partials are read back."""
+    from ..runtime import vertex_ops as VO
+    return VO.op_agg_final(op, [_host_partials(inputs)], v)
+
+
+def op_agg_combine(op, inputs, v):
+    """Aggregation-tree interior vertex: partials in, one partial out (object implementation)."""
+    from ..runtime import vertex_ops as VO
+    return VO.op_agg_combine(op, [_host_partials(inputs)], v)
+
+
+# ---------------------------------------------------------------------------------------------
+# Zip / SelectMany / SlidingWindow / keyed Fork on traced columns
+def _traced(fn, *args):
+    try:
+        return fn(*args)
+    except NotTraceable:
+        raise
+    except (TypeError, AttributeError, RuntimeError, IndexError, ValueError) as e:
+        raise NotTraceable(f"{type(e).__name__}: {e}")
+
+
+def _result_table(res, proto):
+    """TR.to_table, except that a record proxy stands for its own table."""
+    if isinstance(res, (TR.RecProxy, TR.RowProxy)):
+        return object.__getattribute__(res, "_t")
+    if isinstance(res, TR.ByteField):
+        raise NotTraceable("byte-string projection of a proxied row")
+    return TR.to_table(res, proto)
+
+
+def op_zip(op, inputs, v):
+    a, b = _check(inputs[0]), _check(inputs[1])
+    n = min(a.n, b.n)
+    if n == 0:
+        raise NotTraceable("empty Zip input: output type unknown")
+    a, b = a.slice(0, n), b.slice(0, n)
+    return _result_table(_traced(op["fn"], TR.proxy(a), TR.proxy(b)), a)
+
+
+def _interleave(tabs):
+    """Tables t_0..t_{L-1} of n rows -> n * L rows t_0[0], t_1[0], .., t_0[1], .. (SelectMany order)."""
+    t0, L = tabs[0], len(tabs)
+    if any(t.heap is not None or t.strs for t in tabs):
+        raise NotTraceable("SelectMany over string fields")
+    if t0.rows is not None:
+        if any(t.rows is None or t.rows.shape[1] != t0.rows.shape[1] for t in tabs):
+            raise NotTraceable("SelectMany elements of different layouts")
+        return DeviceTable(t0.n * L, t0.shape, rows=torch.stack([t.rows for t in tabs], 1).reshape(t0.n * L, -1))
+    for t in tabs[1:]:
+        if t.rows is not None or t.shape.kind != t0.shape.kind or t.shape.fields != t0.shape.fields or \
+                t.shape.pytype is not t0.shape.pytype or \
+                any(t.cols[k].dtype != c.dtype or t.cols[k].shape[1:] != c.shape[1:] for k, c in t0.cols.items()):
+            raise NotTraceable("SelectMany elements of different layouts")
+    cols = {k: torch.stack([t.cols[k] for t in tabs], 1).reshape((t0.n * L,) + tuple(c.shape[1:]))
+            for k, c in t0.cols.items()}
+    return DeviceTable(t0.n * L, t0.shape, cols)
+
+
+def op_select_many(op, inputs, v):
+    """SelectMany whose selector returns a fixed-length list / tuple of traced values: every
+    element is a column table, interleaved in record order (one stack per field)."""
     t = _check(_one(inputs))
-    if op["spec"]["kind"] == "Count":
-        return _scalar_table([int(t.cols[t.shape.fields[0]].sum().item())], torch.int64, v.device)
-    raise NotTraceable("aggregate on host")
+    if t.n == 0:
+        raise NotTraceable("empty partition: output type unknown")
+    res = TR.call(op["fn"], t)
+    if not isinstance(res, (list, tuple)) or hasattr(res, "_fields") or not res:
+        raise NotTraceable("SelectMany selector must return a fixed-length list of traced values")
+    r = op.get("result")
+    x = TR.proxy(t)
+    return _interleave([_result_table(_traced(r, x, e) if r is not None else e, t) for e in res])
+
+
+def op_sliding_window(op, inputs, v):
+    """SlidingWindow(f, w): f sees a list of w proxies over shifted slices of the partition."""
+    t = _check(_one(inputs))
+    w = int(op["window"])
+    m = t.n - w + 1
+    if m <= 0:
+        raise NotTraceable("window longer than the input: output type unknown")
+    wins = [TR.proxy(t.slice(j, j + m)) for j in range(w)]
+    return _result_table(_traced(op["fn"], wins), t.slice(0, m))
+
+
+def op_fork(op, inputs, v):
+    """Keyed Fork (IKeyedMultiQueryable): one stable pass routes each record to the port of its
+    key (a repeated key routes to its last index, like the object path's dict)."""
+    t = _check(_one(inputs))
+    keys = op.get("keys")
+    if keys is None:
+        raise NotTraceable("ForkTuple mappers run on the host")
+    if t.n == 0:
+        raise NotTraceable("empty partition")
+    if any(isinstance(k, bool) or not isinstance(k, (int, float)) for k in keys):
+        raise NotTraceable("non-numeric fork keys")
+    kc = TR.call(op["mapper"], t)
+    if not isinstance(kc, TR.Col):
+        raise NotTraceable("fork key must be a scalar field")
+    col = kc.t.expand(t.n) if kc.t.dim() == 0 else kc.t
+    K = len(keys)
+    dest = torch.full((t.n,), K, dtype=torch.int64, device=t.device)
+    for i, k in enumerate(keys):
+        dest.masked_fill_(col == k, i)
+    order = torch.argsort(dest, stable=True)
+    counts = torch.bincount(dest, minlength=K + 1)[:K].tolist()
+    offs = [0]
+    for c in counts:
+        offs.append(offs[-1] + c)
+    return Ported(t.take(order), offs)
 
 
 def op_apply(op, inputs, v):

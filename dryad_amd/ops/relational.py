@@ -109,6 +109,47 @@ def seg_reduce(vals: torch.Tensor | None, entries: torch.Tensor | None, seg: tor
     return out
 
 
+_lib.register_signatures({
+    "dr_hj_slots": (c_i32, [vp, c_u64, c_u64, c_i32, vp, vp, vp]),
+    "dr_hj_gather": (c_i32, [vp, c_u64, vp, vp, vp]),
+    "dr_hj_probe": (c_i32, [vp, c_u64, vp, vp, c_i32, c_u64, vp, vp, vp, vp, c_i32, vp]),
+})
+
+
+def hash_join_pairs(outer: torch.Tensor, inner: torch.Tensor, lo_mask: int):
+    """Row-index pairs (outer_row, inner_row) of equal keys through a device hash table built on
+    the inner entries (csrc/kernels/hashjoin.hip).  Pairs come in outer row order and, per outer
+    row, in inner row order (LINQ Join order); ``count[o]`` = matches of outer row o.  Entries must
+    be in row order (row index = position), as build_keys / extract_keys produce them."""
+    from . import sort as S
+    no, ni = outer.shape[0], inner.shape[0]
+    dev = outer.device
+    lm = c_u64(lo_mask & (2**64 - 1))
+    log_cap = max(1, (2 * max(ni, 1) - 1).bit_length())
+    slots = torch.empty((ni, 2), dtype=torch.int64, device=dev)
+    hist = torch.zeros((1 << log_cap) + 1, dtype=torch.int64, device=dev)
+    st = stream_of(hist)
+    _lib.call("dr_hj_slots", ptr(inner), c_u64(ni), lm, log_cap, ptr(slots), ptr(hist), st)
+    srt = S.sort_entries(slots, 64, 64 + 8 * ((log_cap + 7) // 8)) if ni else slots
+    starts = scan_exclusive(hist)
+    keys = torch.empty((ni, 2), dtype=torch.int64, device=dev)
+    _lib.call("dr_hj_gather", ptr(srt), c_u64(ni), ptr(inner), ptr(keys), st)
+    count = torch.empty(no, dtype=torch.int64, device=dev)
+    _lib.call("dr_hj_probe", ptr(outer), c_u64(no), ptr(keys), ptr(starts), log_cap, lm, ptr(count), None, None,
+              None, 0, st)
+    if no == 0:
+        z = torch.empty(0, dtype=torch.int64, device=dev)
+        return z, z, count
+    offs = scan_exclusive(count)
+    total = int((offs[-1] + count[-1]).item())
+    oo = torch.empty(total, dtype=torch.int64, device=dev)
+    ii = torch.empty(total, dtype=torch.int64, device=dev)
+    if total:
+        _lib.call("dr_hj_probe", ptr(outer), c_u64(no), ptr(keys), ptr(starts), log_cap, lm, None, ptr(offs),
+                  ptr(oo), ptr(ii), 1, st)
+    return oo, ii, count
+
+
 def merge_join_pairs(outer_sorted: torch.Tensor, inner_sorted: torch.Tensor, lo_mask: int):
     """Row-index pairs (outer_row, inner_row) of equal keys between two sorted entry arrays,
     grouped by outer in sorted-key order."""
@@ -156,6 +197,10 @@ def gen_records64(cols: list, first: int, nkeys: int, seed: int, dim_mult: int =
 _lib.register_signatures({"dr_seg_reduce_multi": (c_i32, [vp, vp, c_u64, c_i32, vp, vp, vp, vp, vp])})
 
 _MOPS = {("sum", 0): 0, ("min", 0): 1, ("max", 0): 2, ("count", 0): 3, ("sum", 1): 4, ("min", 1): 5, ("max", 1): 6}
+# value columns of a permuted segmented reduction over at least this many rows are first packed
+# row-major ([n, m] 64-bit words): the permuted reads then touch one row segment per sorted entry
+# instead of one random cache line per column (the dominant cost of a high-cardinality GroupBy)
+AOS_MIN_ROWS = 1 << 20
 
 
 def seg_reduce_multi(entries: torch.Tensor | None, seg: torch.Tensor, nseg: int, specs: list) -> list:
@@ -163,13 +208,15 @@ def seg_reduce_multi(entries: torch.Tensor | None, seg: torch.Tensor, nseg: int,
 
     ``specs``: [(op, vals, dtype)] with op in sum/min/max/count, vals a column in original row
     order (None for count) and dtype torch.int64 or torch.float64.  Returns one [nseg] tensor per
-    spec."""
+    spec.  With a row permutation (``entries``), several value columns and many rows, the columns
+    are packed into one row-major buffer first (the kernel reads strided values)."""
     n = seg.shape[0]
     dev = seg.device
     outs, keep = [], []
     ops = (ctypes.c_int * max(1, len(specs)))()
     vps = (ctypes.c_void_p * max(1, len(specs)))()
     ops_p = (ctypes.c_void_p * max(1, len(specs)))()
+    strides = (ctypes.c_uint32 * max(1, len(specs)))(*([1] * max(1, len(specs))))
     for a, (op, vals, dtype) in enumerate(specs):
         f = 0 if dtype in (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool) else 1
         tdt = torch.int64 if f == 0 else torch.float64
@@ -185,13 +232,22 @@ def seg_reduce_multi(entries: torch.Tensor | None, seg: torch.Tensor, nseg: int,
         ops[a] = _MOPS[(op, f)]
         vps[a] = v.data_ptr() if v is not None else 0
         ops_p[a] = out.data_ptr()
+    cols = [a for a, v in enumerate(keep) if v is not None]
+    if entries is not None and n >= AOS_MIN_ROWS and len(cols) >= 2:
+        # one streaming pass packs the columns row-major (64-bit words; float bits unchanged)
+        aos = torch.stack([keep[a].view(torch.int64) for a in cols], 1)
+        keep.append(aos)
+        for j, a in enumerate(cols):
+            vps[a] = aos[:, j].data_ptr()
+            strides[a] = len(cols)
     if n and specs:
         for k in range(0, len(specs), 8):     # kernel takes 8 aggregates per pass
             m = min(8, len(specs) - k)
             o8 = (ctypes.c_int * m)(*[ops[k + j] for j in range(m)])
             v8 = (ctypes.c_void_p * m)(*[vps[k + j] for j in range(m)])
             p8 = (ctypes.c_void_p * m)(*[ops_p[k + j] for j in range(m)])
-            _lib.call("dr_seg_reduce_multi", ptr(entries), ptr(seg), c_u64(n), m, o8, v8, p8, None, stream_of(seg))
+            s8 = (ctypes.c_uint32 * m)(*[strides[k + j] for j in range(m)])
+            _lib.call("dr_seg_reduce_multi", ptr(entries), ptr(seg), c_u64(n), m, o8, v8, p8, s8, stream_of(seg))
     return outs
 
 

@@ -264,7 +264,7 @@ def op_merge_join(op, inputs, v):
 
 def op_merge_group_join(op, inputs, v):
     r = op["result"]
-    return [r(x, g) for x, g in _merge_join_iter(inputs[0], inputs[1], op["outer_key"], op["inner_key"],
+    return [r(x, E.LinqList(g)) for x, g in _merge_join_iter(inputs[0], inputs[1], op["outer_key"], op["inner_key"],
                                                   op.get("comparer"))]
 
 
