@@ -6,7 +6,7 @@
 // DryadLinqVertex.cs:1673-4697 (Count, Sum, Min, Max, Average, Any, All, First, Last, Single ...)
 // as one C# loop per aggregate over the deserialised records.  Here every aggregate of a
 // partition is one slot of a register accumulator array: each lane walks the columns with a
-// grid-stride loop (4 independent loads in flight per column per lane), the wave folds its lanes
+// grid-stride loop (8 consecutive rows per lane per trip: 16-byte vector loads), the wave folds its lanes
 // with xor shuffles, the workgroup folds its 4 waves in LDS, and a second single-workgroup
 // kernel folds the per-workgroup partials in a fixed order (bit-reproducible float sums for a
 // given partition size, no float atomics).
@@ -29,6 +29,8 @@ struct RedSpec {
   int vt[kMaxAgg];
   const void* val[kMaxAgg];
   const uint8_t* mask[kMaxAgg];
+  int vsame[kMaxAgg];   // slot reads the same value column as the slot before it (reuse the registers)
+  int msame[kMaxAgg];   // same mask as the slot before it
 };
 
 __device__ __forceinline__ bool is_f(int vt) { return vt == V_F64 || vt == V_F32; }
@@ -73,33 +75,91 @@ __device__ __forceinline__ int64_t element(int op, int vt, const void* p, uint64
   }
 }
 
+typedef long long ll2_t __attribute__((ext_vector_type(2)));
+typedef int i4_t __attribute__((ext_vector_type(4)));
+typedef float f4_t __attribute__((ext_vector_type(4)));
+
+// Rows base..base+7 of one slot's value column with 16-byte vector loads (the caller guarantees
+// 16-byte aligned columns and base % 8 == 0).
+__device__ __forceinline__ void load8(int op, int vt, const void* p, uint64_t base, int64_t* x) {
+  if (op == R_COUNT) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = 1;
+    return;
+  }
+  if (op == R_FIRST || op == R_LAST) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = (int64_t)(base + k);
+    return;
+  }
+  switch (vt) {
+    case V_I64:
+    case V_F64: {
+      const ll2_t* q = reinterpret_cast<const ll2_t*>(static_cast<const int64_t*>(p) + base);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const ll2_t v = q[j];
+        x[2 * j] = v.x;
+        x[2 * j + 1] = v.y;
+      }
+      break;
+    }
+    case V_I32: {
+      const i4_t* q = reinterpret_cast<const i4_t*>(static_cast<const int32_t*>(p) + base);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const i4_t v = q[j];
+        x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
+      }
+      break;
+    }
+    case V_F32: {
+      const f4_t* q = reinterpret_cast<const f4_t*>(static_cast<const float*>(p) + base);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f4_t v = q[j];
+        x[4 * j] = as_i((double)v.x); x[4 * j + 1] = as_i((double)v.y);
+        x[4 * j + 2] = as_i((double)v.z); x[4 * j + 3] = as_i((double)v.w);
+      }
+      break;
+    }
+    default: {
+      const uint64_t w = *reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(p) + base);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = (int64_t)((w >> (8 * k)) & 0xFF);
+    }
+  }
+}
+
 template <int M>
 __global__ __launch_bounds__(256) void reduce_partial_kernel(RedSpec s, uint64_t n, int64_t* __restrict__ part) {
   int64_t acc[M];
 #pragma unroll
   for (int a = 0; a < M; ++a) acc[a] = identity(s.op[a], is_f(s.vt[a]));
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // 4 rows per lane per trip: independent loads keep HBM busy
-  for (; i + 3 * stride < n; i += 4 * stride) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t n8 = n & ~7ull;
+  // 8 consecutive rows per lane per trip: 16-byte loads of every slot's column, one 8-byte load
+  // of its mask bytes
+  // (Sum / Min / Max of one column, or several slots under one predicate, load it once)
+  for (uint64_t base = tid * 8; base < n8; base += nthr * 8) {
+    int64_t x[8];
+    uint64_t mw = 0;
 #pragma unroll
     for (int a = 0; a < M; ++a) {
-      const int op = s.op[a], vt = s.vt[a];
-      const bool f = is_f(vt);
-      int64_t x[4];
-      bool ok[4];
+      const int op = s.op[a];
+      const bool f = is_f(s.vt[a]);
+      if (!(a > 0 && s.vsame[a])) load8(op, s.vt[a], s.val[a], base, x);
+      if (!(a > 0 && s.msame[a]))
+        mw = s.mask[a] ? *reinterpret_cast<const uint64_t*>(s.mask[a] + base) : 0x0101010101010101ull;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint64_t r = i + k * stride;
-        ok[k] = s.mask[a] == nullptr || s.mask[a][r] != 0;
-        x[k] = element(op, vt, s.val[a], r);
+      for (int k = 0; k < 8; ++k) {
+        const int64_t c = combine(op, f, acc[a], x[k]);
+        acc[a] = ((mw >> (8 * k)) & 0xFF) ? c : acc[a];
       }
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (ok[k]) acc[a] = combine(op, f, acc[a], x[k]);
     }
   }
-  for (; i < n; i += stride) {
+  for (uint64_t i = n8 + tid; i < n; i += nthr) {
 #pragma unroll
     for (int a = 0; a < M; ++a) {
       if (s.mask[a] != nullptr && s.mask[a][i] == 0) continue;
@@ -179,7 +239,14 @@ DR_API int dr_reduce_multi(int m, const int* ops, const int* vts, const void* co
     if ((s.op[a] == R_SUM || s.op[a] == R_MIN || s.op[a] == R_MAX) && (s.vt[a] == V_NONE || s.val[a] == nullptr))
       return (int)hipErrorInvalidValue;
   }
-  const unsigned g = grid_for(n, kBlock * 4, kMaxBlocks);
+  for (int a = 1; a < kMaxAgg; ++a) {
+    const bool valued = s.op[a] == R_SUM || s.op[a] == R_MIN || s.op[a] == R_MAX;
+    const bool pvalued = s.op[a - 1] == R_SUM || s.op[a - 1] == R_MIN || s.op[a - 1] == R_MAX;
+    s.vsame[a] = (valued && pvalued && s.val[a] == s.val[a - 1] && s.vt[a] == s.vt[a - 1]) ||
+                 (s.op[a] == s.op[a - 1] && !valued);
+    s.msame[a] = s.mask[a] == s.mask[a - 1];
+  }
+  const unsigned g = grid_for(n, kBlock * 8, kMaxBlocks);
   int64_t* part = static_cast<int64_t*>(ws);
   switch (m) {
     case 1: launch_partial<1>(s, n, g, part, st); break;

@@ -296,12 +296,22 @@ __global__ __launch_bounds__(256) void seg_reduce_multi_serial(const E128* __res
       const int64_t o = __shfl_up(tail_id, d, 64);
       if (lane >= d && o == tail_id) same |= 1u << k;
     }
+    // software pipeline over the aggregates: the permuted (random) loads of aggregate a + 1 are
+    // issued before aggregate a's scan and stores, so two columns' loads are in flight per lane
+    uint64_t vnext[PER];
+    auto load_vals = [&](int a, uint64_t* dst) {
+      const int op = sp.op[a];
+#pragma unroll
+      for (int k = 0; k < PER; ++k)
+        dst[k] = (k < cnt) ? ((op == M_COUNT) ? 1ull : sp.vals[a][(uint64_t)row[k] * sp.stride[a]]) : 0ull;
+    };
+    load_vals(0, vnext);
     for (int a = 0; a < nagg; ++a) {
       const int op = sp.op[a];
       uint64_t v[PER];
 #pragma unroll
-      for (int k = 0; k < PER; ++k)
-        v[k] = (k < cnt) ? ((op == M_COUNT) ? 1ull : sp.vals[a][(uint64_t)row[k] * sp.stride[a]]) : 0ull;
+      for (int k = 0; k < PER; ++k) v[k] = vnext[k];
+      if (a + 1 < nagg) load_vals(a + 1, vnext);
       // serial pass over the lane's runs
       uint64_t acc = v[0];
       uint64_t head_val = 0;

@@ -36,16 +36,22 @@ def _workspace(dev) -> torch.Tensor:
     return ws
 
 
+def _aligned(t: torch.Tensor) -> torch.Tensor:
+    """The kernel reads 8 rows per lane with 16-byte vector loads: columns start 16-byte aligned."""
+    t = t.contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
 def _value_column(v: torch.Tensor) -> torch.Tensor:
     if v.dtype == torch.bool:
-        return v.contiguous().view(torch.uint8)
+        return _aligned(v).view(torch.uint8)
     if v.dtype not in _VT:
         v = v.to(torch.float64 if v.is_floating_point() else torch.int64)
-    return v.contiguous()
+    return _aligned(v)
 
 
 def _mask_column(m: torch.Tensor) -> torch.Tensor:
-    return m.contiguous().view(torch.uint8) if m.dtype == torch.bool else (m != 0).contiguous().view(torch.uint8)
+    return _aligned(m if m.dtype == torch.bool else m != 0).view(torch.uint8)
 
 
 def reduce_multi(n: int, slots: list, device) -> list:

@@ -197,10 +197,11 @@ def gen_records64(cols: list, first: int, nkeys: int, seed: int, dim_mult: int =
 _lib.register_signatures({"dr_seg_reduce_multi": (c_i32, [vp, vp, c_u64, c_i32, vp, vp, vp, vp, vp])})
 
 _MOPS = {("sum", 0): 0, ("min", 0): 1, ("max", 0): 2, ("count", 0): 3, ("sum", 1): 4, ("min", 1): 5, ("max", 1): 6}
-# value columns of a permuted segmented reduction over at least this many rows are first packed
-# row-major ([n, m] 64-bit words): the permuted reads then touch one row segment per sorted entry
-# instead of one random cache line per column (the dominant cost of a high-cardinality GroupBy)
-AOS_MIN_ROWS = 1 << 20
+# optional: value columns of a permuted segmented reduction over at least this many rows are first
+# packed row-major ([n, m] 64-bit words) so the permuted reads touch one row segment per sorted
+# entry.  Off by default: on 1.25e9 rows x 3 columns the torch.stack packing pass costs more
+# (~47 ms) than the segmented pass saves (105 -> 81 ms); measured in profiles/README.md
+AOS_MIN_ROWS = int(__import__("os").environ.get("DRYAD_SEGRED_AOS_MIN_ROWS", str(1 << 62)))
 
 
 def seg_reduce_multi(entries: torch.Tensor | None, seg: torch.Tensor, nseg: int, specs: list) -> list:
