@@ -18,6 +18,26 @@ struct __attribute__((aligned(16))) E128 {
   uint64_t hi;
 };
 
+// 256-bit sort entry: an E128 key (same digit layout) carrying two more payload words, so a sort
+// can move up to three 8-byte values with the key instead of leaving a row permutation to gather
+// through (GroupBy with decomposable aggregates: sequential segmented reduction afterwards).
+struct __attribute__((aligned(16))) E256 {
+  uint64_t lo;
+  uint64_t hi;
+  uint64_t p0;
+  uint64_t p1;
+};
+
+// 320-bit variant (four payload words) for the final stage of a distributed GroupBy, whose
+// partial counts are one more column to fold.
+struct __attribute__((aligned(8))) E320 {
+  uint64_t lo;
+  uint64_t hi;
+  uint64_t p0;
+  uint64_t p1;
+  uint64_t p2;
+};
+
 static constexpr int kWave = 64;
 static constexpr int kBlock = 256;
 

@@ -253,10 +253,10 @@ __global__ __launch_bounds__(256) void seg_reduce_multi_kernel(const E128* __res
 // that start and end inside the lane are written directly), and only the per-lane tail partials
 // take part in a 64-lane segmented scan — 1/PER of the cross-lane traffic of the per-element
 // scan above.  Segments touching the chunk boundary are combined with atomics.
-template <int PER>
+template <int PER, int NAGG>
 __global__ __launch_bounds__(256) void seg_reduce_multi_serial(const E128* __restrict__ ent,
                                                                const int64_t* __restrict__ seg, uint64_t n,
-                                                               int nagg, AggSpecs sp) {
+                                                               AggSpecs sp) {
   constexpr uint64_t kChunkElems = 64 * PER;
   const int lane = lane_id();
   const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -296,22 +296,20 @@ __global__ __launch_bounds__(256) void seg_reduce_multi_serial(const E128* __res
       const int64_t o = __shfl_up(tail_id, d, 64);
       if (lane >= d && o == tail_id) same |= 1u << k;
     }
-    // software pipeline over the aggregates: the permuted (random) loads of aggregate a + 1 are
-    // issued before aggregate a's scan and stores, so two columns' loads are in flight per lane
-    uint64_t vnext[PER];
-    auto load_vals = [&](int a, uint64_t* dst) {
+    // every aggregate's permuted (random) loads are issued up front, PER x NAGG per lane in flight
+    // (with packed rows the NAGG loads of one row hit the same 32-byte sector together)
+    uint64_t vv[NAGG][PER];
+#pragma unroll
+    for (int a = 0; a < NAGG; ++a) {
       const int op = sp.op[a];
 #pragma unroll
       for (int k = 0; k < PER; ++k)
-        dst[k] = (k < cnt) ? ((op == M_COUNT) ? 1ull : sp.vals[a][(uint64_t)row[k] * sp.stride[a]]) : 0ull;
-    };
-    load_vals(0, vnext);
-    for (int a = 0; a < nagg; ++a) {
-      const int op = sp.op[a];
-      uint64_t v[PER];
+        vv[a][k] = (k < cnt) ? ((op == M_COUNT) ? 1ull : sp.vals[a][(uint64_t)row[k] * sp.stride[a]]) : 0ull;
+    }
 #pragma unroll
-      for (int k = 0; k < PER; ++k) v[k] = vnext[k];
-      if (a + 1 < nagg) load_vals(a + 1, vnext);
+    for (int a = 0; a < NAGG; ++a) {
+      const int op = sp.op[a];
+      const uint64_t* v = vv[a];
       // serial pass over the lane's runs
       uint64_t acc = v[0];
       uint64_t head_val = 0;
@@ -513,14 +511,27 @@ DR_API int dr_seg_reduce_multi(const E128* ent, const int64_t* seg, uint64_t n, 
     sp.vals[a] = reinterpret_cast<const uint64_t*>(vals[a]);
     sp.out[a] = reinterpret_cast<uint64_t*>(outs[a]);
     sp.stride[a] = strides ? strides[a] : 1u;
+    // a missing output, or a value column missing for a value-reading op, would fault the device
+    if (sp.out[a] == nullptr || (sp.op[a] != M_COUNT && sp.vals[a] == nullptr)) return (int)hipErrorInvalidValue;
   }
   static int serial = -1;
   if (serial < 0) {
     const char* e = getenv("DRYAD_SEGRED_SERIAL");
     serial = (e && atoi(e) == 0) ? 0 : 1;
   }
-  if (serial)
-    seg_reduce_multi_serial<8><<<grid_for(n, 256 * 8, 8192), 256, 0, s>>>(ent, seg, n, nagg, sp);
+  if (serial) {
+    const unsigned g = grid_for(n, 256 * 8, 8192);
+    switch (nagg) {
+      case 1: seg_reduce_multi_serial<8, 1><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
+      case 2: seg_reduce_multi_serial<8, 2><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
+      case 3: seg_reduce_multi_serial<8, 3><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
+      case 4: seg_reduce_multi_serial<8, 4><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
+      case 5: seg_reduce_multi_serial<8, 5><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
+      case 6: seg_reduce_multi_serial<8, 6><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
+      case 7: seg_reduce_multi_serial<8, 7><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
+      default: seg_reduce_multi_serial<8, 8><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
+    }
+  }
   else
     seg_reduce_multi_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(ent, seg, n, nagg, sp);
   DR_LAUNCH_CHECK();

@@ -26,12 +26,14 @@ constexpr int kTile = kBlock * kItems;     // 2048 entries per tile (default geo
 constexpr int kMaxGrid = 1024;             // workgroups for count/scatter (4 per CU)
 constexpr int kScanChunk = 4096;           // elements per scan workgroup (16 per thread)
 
-__device__ __forceinline__ uint32_t digit_of(const E128& e, int shift) {
+template <typename T>
+__device__ __forceinline__ uint32_t digit_of(const T& e, int shift) {
   return shift >= 64 ? (uint32_t)((e.hi >> (shift - 64)) & 0xFF)
                      : (uint32_t)((e.lo >> shift) & 0xFF);
 }
 
-__global__ __launch_bounds__(256) void rs_count(const E128* __restrict__ in, uint64_t n, int shift,
+template <typename T>
+__global__ __launch_bounds__(256) void rs_count(const T* __restrict__ in, uint64_t n, int shift,
                                                 uint32_t* __restrict__ counts, uint32_t G,
                                                 uint64_t per_block) {
   __shared__ uint32_t hist[4][kBins];
@@ -40,6 +42,7 @@ __global__ __launch_bounds__(256) void rs_count(const E128* __restrict__ in, uin
   __syncthreads();
   const bool use_hi = shift >= 64;
   const int s = use_hi ? shift - 64 : shift;
+  constexpr int W = sizeof(T) / 8;   // 64-bit words per entry
   const uint64_t* src = reinterpret_cast<const uint64_t*>(in) + (use_hi ? 1 : 0);
   const uint64_t beg = (uint64_t)blockIdx.x * per_block;
   const uint64_t end = beg + per_block < n ? beg + per_block : n;
@@ -48,11 +51,11 @@ __global__ __launch_bounds__(256) void rs_count(const E128* __restrict__ in, uin
   for (; i + 7 * kBlock < end; i += 8 * kBlock) {
     uint64_t v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = src[2 * (i + k * kBlock)];
+    for (int k = 0; k < 8; ++k) v[k] = src[W * (i + k * kBlock)];
 #pragma unroll
     for (int k = 0; k < 8; ++k) atomicAdd(&hist[w][(v[k] >> s) & 0xFF], 1u);
   }
-  for (; i < end; i += kBlock) atomicAdd(&hist[w][(src[2 * i] >> s) & 0xFF], 1u);
+  for (; i < end; i += kBlock) atomicAdd(&hist[w][(src[W * i] >> s) & 0xFF], 1u);
   __syncthreads();
   const uint32_t c = hist[0][t] + hist[1][t] + hist[2][t] + hist[3][t];
   counts[(uint64_t)t * G + blockIdx.x] = c;
@@ -174,13 +177,13 @@ __global__ __launch_bounds__(256) void rs_scatter(const E128* __restrict__ in, E
 // v2: all of a tile's loads are issued back to back and the NEXT tile is prefetched into
 // registers while the current one is ranked and staged (software pipelining across tiles), so a
 // workgroup's global-load latency overlaps its LDS ranking / scatter work.
-template <int ITEMS>
-__global__ __launch_bounds__(256) void rs_scatter_v2(const E128* __restrict__ in, E128* __restrict__ out,
+template <typename T, int ITEMS>
+__global__ __launch_bounds__(256) void rs_scatter_v2(const T* __restrict__ in, T* __restrict__ out,
                                                      uint64_t n, int shift,
                                                      const uint32_t* __restrict__ offsets, uint32_t G,
                                                      uint64_t per_block) {
   constexpr int kTile = kBlock * ITEMS;
-  __shared__ E128 stage[kTile];
+  __shared__ T stage[kTile];
   __shared__ uint32_t wcnt[4][kBins];
   __shared__ uint32_t goff[kBins];
   __shared__ uint32_t bstart[kBins];
@@ -189,8 +192,8 @@ __global__ __launch_bounds__(256) void rs_scatter_v2(const E128* __restrict__ in
   goff[t] = offsets[(uint64_t)t * G + blockIdx.x];
   const uint64_t beg = (uint64_t)blockIdx.x * per_block;
   const uint64_t end = beg + per_block < n ? beg + per_block : n;
-  E128 cur[ITEMS], nxt[ITEMS];
-  auto load_tile = [&](uint64_t base, E128* dst) {
+  T cur[ITEMS], nxt[ITEMS];
+  auto load_tile = [&](uint64_t base, T* dst) {
     const uint32_t c = (uint32_t)((end - base) < (uint64_t)kTile ? (end - base) : kTile);
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
@@ -240,7 +243,7 @@ __global__ __launch_bounds__(256) void rs_scatter_v2(const E128* __restrict__ in
     __syncthreads();
 #pragma unroll 4
     for (uint32_t j = t; j < cnt; j += kBlock) {
-      const E128 v = stage[j];
+      const T v = stage[j];
       const uint32_t d = digit_of(v, shift);
       out[(uint64_t)goff[d] + (j - bstart[d])] = v;
     }
@@ -287,9 +290,9 @@ void launch_scatter(const E128* in, E128* out, uint64_t n, int shift, const uint
   }
   if (g_scatter_v2) {
     if (sort_items() == 16)
-      rs_scatter_v2<16><<<G, 256, 0, s>>>(in, out, n, shift, offsets, G, per_block);
+      rs_scatter_v2<E128, 16><<<G, 256, 0, s>>>(in, out, n, shift, offsets, G, per_block);
     else
-      rs_scatter_v2<8><<<G, 256, 0, s>>>(in, out, n, shift, offsets, G, per_block);
+      rs_scatter_v2<E128, 8><<<G, 256, 0, s>>>(in, out, n, shift, offsets, G, per_block);
     return;
   }
   if (sort_items() == 16)
@@ -942,4 +945,116 @@ DR_API int dr_hi_range(const E128* e, uint64_t n, uint64_t* range, hipStream_t s
   hi_range_kernel<<<grid_for(n, 256 * 8, 4096), 256, 0, s>>>(e, n, reinterpret_cast<unsigned long long*>(range));
   DR_LAUNCH_CHECK();
   return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Payload-carrying sort (32-byte E256 / 40-byte E320 entries).  A GroupBy whose aggregates fold
+// at most three (four) 8-byte columns sorts the values WITH the key: 4 LSD passes move 2x the bytes of a key-pointer
+// sort, but the segmented reduction afterwards streams the sorted array instead of gathering
+// every value column through a random row permutation (which runs at the HBM line-rate limit:
+// one 128-byte line per 8-byte value).
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(256) void pack_wide_kernel(const int64_t* __restrict__ key, int64_t bias,
+                                                        const uint64_t* __restrict__ v0, const uint64_t* __restrict__ v1,
+                                                        const uint64_t* __restrict__ v2, const uint64_t* __restrict__ v3,
+                                                        uint64_t n, T* __restrict__ out) {
+  constexpr int W = sizeof(T) / 8;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t w[W];
+    w[1] = key ? (uint64_t)key[i] - (uint64_t)bias : 0ull;   // key - min: >= 0, unsigned order = signed order
+    w[0] = v0 ? v0[i] : 0ull;
+    w[2] = v1 ? v1[i] : 0ull;
+    w[3] = v2 ? v2[i] : 0ull;
+    if constexpr (W > 4) w[4] = v3 ? v3[i] : 0ull;
+    uint64_t* o = reinterpret_cast<uint64_t*>(out + i);
+#pragma unroll
+    for (int k = 0; k < W; ++k) o[k] = w[k];
+  }
+}
+
+// flags[i] = 1 where hi differs from the previous entry's (entries `words` 64-bit words apart)
+__global__ __launch_bounds__(256) void hi_flags_kernel(const uint64_t* __restrict__ e, uint32_t words, uint64_t n,
+                                                       int64_t* __restrict__ flags) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    flags[i] = (i == 0 || e[(i - 1) * words + 1] != e[i * words + 1]) ? 1 : 0;
+}
+
+}  // namespace
+
+// Wide sort entries (words = 4: E256, 5: E320) from an int64 key column (hi = key - bias, bias =
+// the column minimum; key == nullptr leaves hi zero: a row-major value buffer) and up to
+// words - 1 8-byte value columns (nullptr = absent) in lo, p0, ...
+DR_API int dr_pack_wide(int words, const int64_t* key, int64_t bias, const uint64_t* v0, const uint64_t* v1,
+                        const uint64_t* v2, const uint64_t* v3, uint64_t n, void* out, hipStream_t s) {
+  if (n == 0) return 0;
+  const unsigned g = grid_for(n, 256, 16384);
+  if (words == 4) pack_wide_kernel<E256><<<g, 256, 0, s>>>(key, bias, v0, v1, v2, nullptr, n, static_cast<E256*>(out));
+  else if (words == 5) pack_wide_kernel<E320><<<g, 256, 0, s>>>(key, bias, v0, v1, v2, v3, n, static_cast<E320*>(out));
+  else return (int)hipErrorInvalidValue;
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+DR_API int dr_hi_flags(const uint64_t* entries, uint32_t words, uint64_t n, int64_t* flags, hipStream_t s) {
+  if (n == 0) return 0;
+  if (words < 2 || words > 5) return (int)hipErrorInvalidValue;
+  hi_flags_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(entries, words, n, flags);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+namespace {
+
+// ITEMS entries per thread per tile: E256 8 (2048-entry tile, 64 KiB LDS stage, ~256 contiguous
+// output bytes per digit run), E320 4 (40 KiB stage, three workgroups per CU)
+template <typename T, int ITEMS>
+int sort_wide(T* keys, T* tmp, uint64_t n, int begin_bit, int end_bit, void* ws, hipStream_t s, int* result_in_tmp) {
+  const uint64_t tile = (uint64_t)kBlock * ITEMS;
+  uint64_t tiles = (n + tile - 1) / tile;
+  if (tiles < 1) tiles = 1;
+  const uint32_t G = (uint32_t)(tiles < (uint64_t)kMaxGrid ? tiles : (uint64_t)kMaxGrid);
+  const uint64_t per_block = ((tiles + G - 1) / G) * tile;
+  uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* partial = counts + (uint64_t)kBins * G;
+  T* src = keys;
+  T* dst = tmp;
+  int flips = 0;
+  for (int shift = begin_bit; shift < end_bit; shift += kRadixBits) {
+    rs_count<<<G, 256, 0, s>>>(src, n, shift, counts, G, per_block);
+    scan_inplace(counts, kBins * G, partial, s);
+    rs_scatter_v2<T, ITEMS><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+    T* x = src; src = dst; dst = x;
+    flips ^= 1;
+  }
+  DR_LAUNCH_CHECK();
+  *result_in_tmp = flips;
+  return 0;
+}
+
+}  // namespace
+
+// Stable LSD radix sort of wide entries (words = 4: E256, 5: E320) on composite key bits
+// [begin_bit, end_bit) of (hi, lo); same contract as dr_sort_u128, workspace
+// dr_sort_u256_workspace(n).
+DR_API int dr_sort_wide(int words, void* keys, void* tmp, uint64_t n, int begin_bit, int end_bit, void* ws,
+                        hipStream_t s, int* result_in_tmp) {
+  *result_in_tmp = 0;
+  if (n == 0 || begin_bit >= end_bit) return 0;
+  if (end_bit > 128 || begin_bit < 0 || ((end_bit - begin_bit) & 7)) return (int)hipErrorInvalidValue;
+  if ((begin_bit & 7) && begin_bit < 64) return (int)hipErrorInvalidValue;
+  if (n >= (1ull << 32)) return (int)hipErrorInvalidValue;
+  if (words == 4)
+    return sort_wide<E256, 8>(static_cast<E256*>(keys), static_cast<E256*>(tmp), n, begin_bit, end_bit, ws, s,
+                              result_in_tmp);
+  if (words == 5)
+    return sort_wide<E320, 4>(static_cast<E320*>(keys), static_cast<E320*>(tmp), n, begin_bit, end_bit, ws, s,
+                              result_in_tmp);
+  return (int)hipErrorInvalidValue;
+}
+
+DR_API uint64_t dr_sort_u256_workspace(uint64_t n) {
+  (void)n;
+  return ((uint64_t)kBins * kMaxGrid + 1024) * sizeof(uint32_t);
 }

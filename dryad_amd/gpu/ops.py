@@ -524,6 +524,21 @@ def _group_specs(d, t):
     return specs, names
 
 
+_INT_KEYS = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8)
+
+
+def _payload_groups(kcols, skeys, specs, n):
+    """R.payload_groups for a single plain integer key on a large partition, else None.  Keys come
+    back in the key column's dtype."""
+    if len(kcols) != 1 or skeys[0] is not None or kcols[0].dtype not in _INT_KEYS or n < R.PAYLOAD_SORT_MIN_ROWS:
+        return None
+    k = kcols[0]
+    got = R.payload_groups(k.to(torch.int64), specs)
+    if got is None or k.dtype == torch.int64:
+        return got
+    return got[0].to(k.dtype), got[1]
+
+
 def op_group_partial(op, inputs, v):
     t = _check(_one(inputs))
     d = op["decomp"]
@@ -544,6 +559,13 @@ def op_group_partial(op, inputs, v):
                 for nm, r in zip(names, res):
                     out[nm] = r
                 return _partial_table(out, {}, d, 1, form)
+    # one int64 key folding <= 3 columns: the values ride in the sort entries (no random gather)
+    got = _payload_groups(kcols, skeys, specs, t.n)
+    if got is not None:
+        out = {"k0": got[0]}
+        for nm, r in zip(names, got[1]):
+            out[nm] = r
+        return _partial_table(out, {}, d, 1, form)
     srt, seg, nseg, rows_at_start, starts = _group_keys(kcols, skeys)
     out, strs = _key_outputs(kcols, skeys, rows_at_start, srt, starts)
     # every aggregate in one fused segmented-reduce pass
@@ -562,9 +584,6 @@ def op_group_final(op, inputs, v):
     nkeys = t.shape.pytype.nkeys
     kcols, skeys = TR.eq_key_columns(tuple(TR.Col(v) if isinstance(v, torch.Tensor) else v
                                            for v in _key_values(t, nkeys)), t)
-    srt, seg, nseg, rows_at_start, starts = _group_keys(kcols, skeys)
-    kout, kstrs = _key_outputs(kcols, skeys, rows_at_start, srt, starts)
-    keys = _key_values(DeviceTable(nseg, Shape("tuple", list(kout)), kout, strs=kstrs), nkeys)
     specs = []
     for j, a in enumerate(d.aggs):
         col = t.cols[f"a{j}"]
@@ -576,7 +595,14 @@ def op_group_final(op, inputs, v):
             specs += [("sum", col, torch.float64), ("sum", t.cols[f"c{j}"], torch.int64)]
         elif a.kind in ("any", "all"):
             specs.append(("max" if a.kind == "any" else "min", col, torch.int64))
-    res = iter(R.seg_reduce_multi(srt, seg, nseg, specs))
+    got = _payload_groups(kcols, skeys, specs, t.n)
+    if got is not None:
+        keys, nseg, res = [got[0]], got[0].shape[0], iter(got[1])
+    else:
+        srt, seg, nseg, rows_at_start, starts = _group_keys(kcols, skeys)
+        kout, kstrs = _key_outputs(kcols, skeys, rows_at_start, srt, starts)
+        keys = _key_values(DeviceTable(nseg, Shape("tuple", list(kout)), kout, strs=kstrs), nkeys)
+        res = iter(R.seg_reduce_multi(srt, seg, nseg, specs))
     vals = []
     for j, a in enumerate(d.aggs):
         col = t.cols[f"a{j}"]

@@ -2,11 +2,12 @@
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
 from . import _lib
-from ._lib import c_i32, c_u32, c_u64, ptr, stream_of, vp
+from ._lib import c_i32, c_i64, c_u32, c_u64, ptr, stream_of, vp
 
 _lib.register_signatures({
     "dr_build_keys": (c_i32, [ctypes.POINTER(vp), ctypes.POINTER(c_i32), ctypes.POINTER(c_i32), c_i32, c_u64, c_u32,
@@ -76,9 +77,12 @@ def scan_exclusive(a: torch.Tensor, out: torch.Tensor | None = None) -> torch.Te
 
 def segment_ids(entries: torch.Tensor, lo_mask: int):
     """(segment id per sorted row, number of segments, segment start positions)."""
-    flags = segment_flags(entries, lo_mask)
+    return _ids_from_flags(segment_flags(entries, lo_mask))
+
+
+def _ids_from_flags(flags: torch.Tensor):
     ids = scan_exclusive(flags)
-    n = entries.shape[0]
+    n = flags.shape[0]
     if n == 0:
         return ids, 0, ids
     nseg = int(ids[-1].item() + flags[-1].item())
@@ -197,11 +201,11 @@ def gen_records64(cols: list, first: int, nkeys: int, seed: int, dim_mult: int =
 _lib.register_signatures({"dr_seg_reduce_multi": (c_i32, [vp, vp, c_u64, c_i32, vp, vp, vp, vp, vp])})
 
 _MOPS = {("sum", 0): 0, ("min", 0): 1, ("max", 0): 2, ("count", 0): 3, ("sum", 1): 4, ("min", 1): 5, ("max", 1): 6}
-# optional: value columns of a permuted segmented reduction over at least this many rows are first
-# packed row-major ([n, m] 64-bit words) so the permuted reads touch one row segment per sorted
-# entry.  Off by default: on 1.25e9 rows x 3 columns the torch.stack packing pass costs more
-# (~47 ms) than the segmented pass saves (105 -> 81 ms); measured in profiles/README.md
-AOS_MIN_ROWS = int(__import__("os").environ.get("DRYAD_SEGRED_AOS_MIN_ROWS", str(1 << 62)))
+# value columns of a permuted segmented reduction over at least this many rows are first packed
+# into 32- / 40-byte rows (dr_pack_wide) so each sorted entry costs one sector-aligned random read
+# instead of one cache line per column: GroupBy of 1.25e9 rows x 3 columns 249.4 -> 238.7 ms per
+# step (the torch.stack packing tried first cost 47 ms and lost; profiles/README.md)
+AOS_MIN_ROWS = int(os.environ.get("DRYAD_SEGRED_AOS_MIN_ROWS", str(1 << 24)))
 
 
 def seg_reduce_multi(entries: torch.Tensor | None, seg: torch.Tensor, nseg: int, specs: list) -> list:
@@ -227,20 +231,32 @@ def seg_reduce_multi(entries: torch.Tensor | None, seg: torch.Tensor, nseg: int,
                 "min": torch.iinfo(torch.int64).max if f == 0 else float("inf"),
                 "max": torch.iinfo(torch.int64).min if f == 0 else float("-inf")}[op]
         out = torch.full((nseg,), init, dtype=tdt, device=dev)
-        v = None if op == "count" else vals.to(tdt).contiguous()
-        keep.append(v)
         outs.append(out)
         ops[a] = _MOPS[(op, f)]
-        vps[a] = v.data_ptr() if v is not None else 0
         ops_p[a] = out.data_ptr()
+        if isinstance(vals, StridedCol) and op != "count":
+            keep.append(None)      # already in the reduced dtype, inside a row-major buffer
+            vps[a] = vals.base.data_ptr() + 8 * vals.word
+            strides[a] = vals.stride
+            continue
+        v = None if op == "count" else vals.to(tdt).contiguous()
+        keep.append(v)
+        vps[a] = v.data_ptr() if v is not None else 0
     cols = [a for a, v in enumerate(keep) if v is not None]
-    if entries is not None and n >= AOS_MIN_ROWS and len(cols) >= 2:
-        # one streaming pass packs the columns row-major (64-bit words; float bits unchanged)
-        aos = torch.stack([keep[a].view(torch.int64) for a in cols], 1)
+    distinct = list({keep[a].data_ptr(): keep[a] for a in cols}.values())
+    if entries is not None and n >= AOS_MIN_ROWS and 2 <= len(distinct) <= 4:
+        # one streaming pass packs the distinct columns into 32- / 40-byte rows (the wide sort
+        # entry layout with no key: words lo, p0, p1[, p2]), so each permuted row costs one
+        # sector-aligned read instead of one cache line per column
+        words = 4 if len(distinct) <= 3 else 5
+        aos = torch.empty((n, words), dtype=torch.int64, device=dev)
+        vp4 = [c.data_ptr() for c in distinct] + [0] * (4 - len(distinct))
+        _lib.call("dr_pack_wide", words, vp(0), c_i64(0), *[vp(x) for x in vp4], c_u64(n), ptr(aos), stream_of(aos))
         keep.append(aos)
-        for j, a in enumerate(cols):
-            vps[a] = aos[:, j].data_ptr()
-            strides[a] = len(cols)
+        slot = {c.data_ptr(): _PAYLOAD_WORDS[j] for j, c in enumerate(distinct)}
+        for a in cols:
+            vps[a] = aos.data_ptr() + 8 * slot[keep[a].data_ptr()]
+            strides[a] = words
     if n and specs:
         for k in range(0, len(specs), 8):     # kernel takes 8 aggregates per pass
             m = min(8, len(specs) - k)
@@ -250,6 +266,86 @@ def seg_reduce_multi(entries: torch.Tensor | None, seg: torch.Tensor, nseg: int,
             s8 = (ctypes.c_uint32 * m)(*[strides[k + j] for j in range(m)])
             _lib.call("dr_seg_reduce_multi", ptr(entries), ptr(seg), c_u64(n), m, o8, v8, p8, s8, stream_of(seg))
     return outs
+
+
+class StridedCol:
+    """A 64-bit column stored as word ``word`` of every ``stride``-word row of ``base``."""
+
+    def __init__(self, base: torch.Tensor, word: int, stride: int):
+        self.base, self.word, self.stride = base, word, stride
+
+
+_lib.register_signatures({
+    "dr_pack_wide": (c_i32, [c_i32, vp, c_i64, vp, vp, vp, vp, c_u64, vp, vp]),
+    "dr_hi_flags": (c_i32, [vp, c_u32, c_u64, vp, vp]),
+    "dr_sort_wide": (c_i32, [c_i32, vp, vp, c_u64, c_i32, c_i32, vp, vp, ctypes.POINTER(c_i32)]),
+    "dr_sort_u256_workspace": (c_u64, [c_u64]),
+})
+
+# payload sort: GroupBy on one int64 key folding <= 4 value columns, on at least this many rows
+# and keys spanning <= 32 varying bits (4 radix passes).  Off by default: on the 1.25e9-row
+# GroupBy benchmark it measured 260.6 ms against 251.2 ms for the key-pointer sort — the E256
+# scatter passes (26 ms each vs 12 for E128) and their count passes cost more than the random
+# gathers they remove (profiles/README.md)
+PAYLOAD_SORT_MIN_ROWS = int(os.environ.get("DRYAD_PAYLOAD_SORT_MIN_ROWS", str(1 << 62)))
+PAYLOAD_SORT_MAX_PASSES = 4
+_PAYLOAD_WORDS = (0, 2, 3, 4)      # payload words of an E256 / E320 entry: lo, p0, p1, p2 (hi = key)
+
+
+def payload_groups(key: torch.Tensor, specs: list):
+    """Sort-based GroupBy that carries the aggregated values in the sort entries (32-byte E256:
+    key - min(key) in hi, up to three 8-byte values in lo / p0 / p1, or a 40-byte E320 with a
+    fourth in p2; csrc/kernels/sort.hip dr_sort_wide),
+    then one sequential segmented reduction over the sorted array — no random gather through a
+    row permutation.  ``specs`` as for seg_reduce_multi.  Returns (keys, outs) in ascending key
+    order (the order of the key-pointer path), or None when the shape does not suit it."""
+    from . import reduce as RD
+    n = key.shape[0]
+    dev = key.device
+    if key.dtype != torch.int64 or key.dim() != 1 or n < 2 or n >= (1 << 32):
+        return None
+    cols, where = [], []
+    for op, vals, dtype in specs:
+        if op == "count":
+            where.append(None)
+            continue
+        f = dtype not in (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool)
+        v = vals.to(torch.float64 if f else torch.int64).contiguous()
+        j = next((j for j, c in enumerate(cols) if c.data_ptr() == v.data_ptr() and c.dtype == v.dtype), None)
+        if j is None:
+            if len(cols) == 4:
+                return None
+            cols.append(v)
+            j = len(cols) - 1
+        where.append(j)
+    mn, mx = RD.reduce_multi(n, [(RD.MIN, key, None), (RD.MAX, key, None)], dev)
+    span = (mx - mn).bit_length()      # entries hold key - min (order-preserving, >= 0)
+    passes = (span + 7) // 8
+    if passes > PAYLOAD_SORT_MAX_PASSES:
+        return None
+    k = key.contiguous()
+    words = 4 if len(cols) <= 3 else 5
+    e = torch.empty((n, words), dtype=torch.int64, device=dev)
+    vp4 = [c.data_ptr() for c in cols] + [0] * (4 - len(cols))
+    _lib.call("dr_pack_wide", words, ptr(k), c_i64(mn), *[vp(x) for x in vp4], c_u64(n), ptr(e), stream_of(e))
+    del cols
+    if passes:
+        tmp = torch.empty_like(e)
+        ws = torch.empty(int(_lib.lib().dr_sort_u256_workspace(c_u64(n))), dtype=torch.uint8, device=dev)
+        flag = ctypes.c_int32(0)
+        _lib.call("dr_sort_wide", words, ptr(e), ptr(tmp), c_u64(n), 64, 64 + 8 * passes, ptr(ws), stream_of(e),
+                  ctypes.byref(flag))
+        if flag.value:
+            e = tmp
+        del tmp
+    flags = torch.empty(n, dtype=torch.int64, device=dev)
+    _lib.call("dr_hi_flags", ptr(e), c_u32(words), c_u64(n), ptr(flags), stream_of(e))
+    seg, nseg, starts = _ids_from_flags(flags)
+    del flags
+    keys = e[:, 1].index_select(0, starts).add_(mn)
+    sp = [(op, None if w is None else StridedCol(e, _PAYLOAD_WORDS[w], words), dtype)
+          for (op, _, dtype), w in zip(specs, where)]
+    return keys, seg_reduce_multi(None, seg, nseg, sp)
 
 
 _lib.register_signatures({"dr_hash_aggregate": (c_i32, [vp, c_u64, c_i32, vp, vp, vp, vp, c_u64, vp, vp])})

@@ -195,3 +195,60 @@ def test_seg_reduce_aos_packing_matches_columns(aos, monkeypatch):
     torch.testing.assert_close(sf, torch.zeros(uk.numel(), dtype=torch.float64, device="cuda").index_add_(0, inv, vf))
     # the group keys decoded from the sorted entries equal the gathered key column
     assert torch.equal(srt[:, 1].index_select(0, starts).bitwise_xor_(-(1 << 63)), uk)
+
+
+@pytest.mark.parametrize("n,span", [(2, 8), (4097, 12), (5000, 1), (3_000_001, 30), (1 << 20, 20)])
+def test_payload_sort_groups_match_torch(n, span):
+    """E256 payload sort + sequential segmented reduction against a torch fp64/int64 reference."""
+    from dryad_amd.ops import relational as R
+    torch.manual_seed(n + span)
+    key = torch.randint(-(1 << (span - 1)) if span > 1 else 0, 1 << (span - 1) if span > 1 else 2, (n,),
+                        dtype=torch.int64, device="cuda")
+    a = torch.randint(-10**9, 10**9, (n,), dtype=torch.int64, device="cuda")
+    f = torch.randn(n, dtype=torch.float64, device="cuda")
+    i32 = (a % 1000).to(torch.int32)
+    specs = [("count", None, torch.int64), ("sum", a, torch.int64), ("min", f, torch.float64),
+             ("max", f, torch.float64), ("max", i32, torch.int64), ("sum", a, torch.float64),
+             ("min", a + 1, torch.int64)]
+    assert R.payload_groups(key, specs) is None   # five distinct (column, dtype) payloads
+    if n % 2:
+        specs = specs[:6]   # four payloads: 40-byte E320 entries
+    else:
+        specs = specs[:5]   # three payloads: 32-byte E256 entries
+    keys, outs = R.payload_groups(key, specs)
+    uk, inv = torch.unique(key, sorted=True, return_inverse=True)
+    assert torch.equal(keys, uk)
+    g = uk.shape[0]
+    cnt = torch.bincount(inv, minlength=g)
+    s = torch.zeros(g, dtype=torch.int64, device="cuda").index_add_(0, inv, a)
+    mn = torch.full((g,), float("inf"), dtype=torch.float64, device="cuda").scatter_reduce(0, inv, f, "amin")
+    mx = torch.full((g,), float("-inf"), dtype=torch.float64, device="cuda").scatter_reduce(0, inv, f, "amax")
+    mi = torch.full((g,), -2**63, dtype=torch.int64, device="cuda").scatter_reduce(0, inv, i32.to(torch.int64), "amax")
+    ref = [cnt, s, mn, mx, mi]
+    if len(specs) == 6:
+        ref.append(torch.zeros(g, dtype=torch.float64, device="cuda").index_add_(0, inv, a.to(torch.float64)))
+    for j, (o, r) in enumerate(zip(outs, ref)):
+        if j == 5:
+            torch.testing.assert_close(o, r, rtol=1e-12, atol=1e-3)
+        else:
+            assert torch.equal(o, r)
+
+
+def test_payload_sort_rejects_wide_key_span():
+    from dryad_amd.ops import relational as R
+    key = torch.tensor([0, 1 << 40, 5], dtype=torch.int64, device="cuda")
+    assert R.payload_groups(key, [("count", None, torch.int64)]) is None
+
+
+@pytest.mark.parametrize("parts", [1, 3])
+def test_groupby_payload_path_matches_localdebug(parts, monkeypatch):
+    from dryad_amd.ops import relational as R
+    monkeypatch.setattr(R, "PAYLOAD_SORT_MIN_ROWS", 0)
+    calls = []
+    orig = R.payload_groups
+    monkeypatch.setattr(R, "payload_groups", lambda *a: calls.append(1) or orig(*a))
+    _same(lambda c: c.FromEnumerable(PAIRS).GroupBy(
+        lambda p: p[0] * 1000 - 7, lambda k, g: (k, g.Count(), g.Sum(lambda p: p[0]), g.Min(lambda p: p[1]),
+                                                 g.Max(lambda p: p[0]), g.Average(lambda p: p[0]))),
+        parts=parts, device_ops=("group_partial", "group_final", "group_by"))
+    assert calls, "payload path not taken"
