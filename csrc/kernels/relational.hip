@@ -582,3 +582,75 @@ DR_API int dr_scan_i64(const int64_t* a, int64_t* out, uint64_t n, void* ws, hip
   DR_LAUNCH_CHECK();
   return 0;
 }
+
+namespace {
+
+// ----- fused segment ids -----------------------------------------------------------------------
+// flag(i) = 1 where sorted entry i starts a new key (hi or masked lo differs from entry i - 1)
+__device__ __forceinline__ int64_t seg_flag(const E128* __restrict__ e, uint64_t i, uint64_t lo_mask) {
+  if (i == 0) return 1;
+  const E128 a = e[i - 1], b = e[i];
+  return (a.hi != b.hi || ((a.lo ^ b.lo) & lo_mask) != 0) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void seg_count_kernel(const E128* __restrict__ e, uint64_t n, uint64_t lo_mask,
+                                                        int64_t* __restrict__ part) {
+  __shared__ uint64_t sc[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kChunk + threadIdx.x * 16;
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) s += (base + k < n) ? seg_flag(e, base + k, lo_mask) : 0;
+  uint64_t w = wave_sum64((uint64_t)s);
+  if (lane_id() == 0) sc[wave_id()] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (int64_t)(sc[0] + sc[1] + sc[2] + sc[3]);
+}
+
+// ids[i] = (number of segment starts at or before i) - 1; starts[id] = i at every start
+__global__ __launch_bounds__(256) void seg_ids_kernel(const E128* __restrict__ e, uint64_t n, uint64_t lo_mask,
+                                                      const int64_t* __restrict__ part_ex, int64_t* __restrict__ ids,
+                                                      int64_t* __restrict__ starts) {
+  __shared__ uint64_t sc[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kChunk + threadIdx.x * 16;
+  int64_t v[16];
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = (base + k < n) ? seg_flag(e, base + k, lo_mask) : 0;
+    s += v[k];
+  }
+  const uint64_t inc = wave_inclusive_scan64((uint64_t)s);
+  if (lane_id() == 63) sc[wave_id()] = inc;
+  __syncthreads();
+  const int w = wave_id();
+  uint64_t pre = 0;
+  for (int k = 0; k < w; ++k) pre += sc[k];
+  int64_t run = (int64_t)(pre + inc) - s + part_ex[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    run += v[k];
+    if (base + k < n) {
+      ids[base + k] = run - 1;
+      if (v[k]) starts[run - 1] = (int64_t)(base + k);
+    }
+  }
+}
+
+}  // namespace
+
+// Segment ids of sorted entries in two passes over the entries (no flag array): ids[i] = segment
+// of entry i, starts[g] = first position of segment g (starts needs room for n values); the
+// segment count is ids[n - 1] + 1.  ws: dr_scan_i64_workspace(n) bytes.
+DR_API int dr_segment_ids(const E128* e, uint64_t n, uint64_t lo_mask, int64_t* ids, int64_t* starts, void* ws,
+                          hipStream_t s) {
+  if (n == 0) return 0;
+  int64_t* part = reinterpret_cast<int64_t*>(ws);
+  const uint64_t nb = (n + kChunk - 1) / kChunk;
+  seg_count_kernel<<<(unsigned)nb, 256, 0, s>>>(e, n, lo_mask, part);
+  int rc = dr_scan_i64(part, part, nb, part + nb, s);
+  if (rc) return rc;
+  seg_ids_kernel<<<(unsigned)nb, 256, 0, s>>>(e, n, lo_mask, part, ids, starts);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+

@@ -75,9 +75,26 @@ def scan_exclusive(a: torch.Tensor, out: torch.Tensor | None = None) -> torch.Te
     return out
 
 
+_lib.register_signatures({"dr_segment_ids": (c_i32, [vp, c_u64, c_u64, vp, vp, vp, vp])})
+
+
 def segment_ids(entries: torch.Tensor, lo_mask: int):
-    """(segment id per sorted row, number of segments, segment start positions)."""
-    return _ids_from_flags(segment_flags(entries, lo_mask))
+    """(segment id per sorted row, number of segments, segment start positions): two fused passes
+    over the sorted entries (dr_segment_ids), no flag array."""
+    n = entries.shape[0]
+    dev = entries.device
+    ids = torch.empty(n, dtype=torch.int64, device=dev)
+    if n == 0:
+        return ids, 0, ids
+    starts = torch.empty(n, dtype=torch.int64, device=dev)
+    ws = torch.empty(int(_lib.lib().dr_scan_i64_workspace(c_u64(n))), dtype=torch.uint8, device=dev)
+    _lib.call("dr_segment_ids", ptr(entries), c_u64(n), c_u64(lo_mask & (2**64 - 1)), ptr(ids), ptr(starts), ptr(ws),
+              stream_of(entries))
+    nseg = int(ids[-1].item()) + 1
+    starts = starts[:nseg]
+    if nseg * 2 < n:
+        starts = starts.clone()      # release the n-row buffer
+    return ids, nseg, starts
 
 
 def _ids_from_flags(flags: torch.Tensor):

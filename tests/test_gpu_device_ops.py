@@ -252,3 +252,19 @@ def test_groupby_payload_path_matches_localdebug(parts, monkeypatch):
                                                  g.Max(lambda p: p[0]), g.Average(lambda p: p[0]))),
         parts=parts, device_ops=("group_partial", "group_final", "group_by"))
     assert calls, "payload path not taken"
+
+
+@pytest.mark.parametrize("n", [1, 4096, 4097, 1_000_003])
+def test_fused_segment_ids_match_flag_scan(n):
+    from dryad_amd.ops import relational as R
+    from dryad_amd.ops import sort as S
+    torch.manual_seed(n)
+    k = torch.randint(0, max(2, n // 3), (n,), dtype=torch.int64, device="cuda")
+    k2 = torch.randint(0, 3, (n,), dtype=torch.int32, device="cuda")
+    e, b0, lm = R.build_keys([k, k2])
+    srt = S.sort_entries_hybrid(e, b0)
+    ids, nseg, starts = R.segment_ids(srt, lm)
+    ref_ids, ref_n, ref_starts = R._ids_from_flags(R.segment_flags(srt, lm))
+    assert nseg == ref_n
+    assert torch.equal(ids, ref_ids)
+    assert torch.equal(starts, ref_starts)
