@@ -176,6 +176,8 @@ struct AggSpecs {
   const uint64_t* vals[kMaxAggs];
   uint64_t* out[kMaxAggs];
   uint32_t stride[kMaxAggs];   // elements between consecutive records (1 = column, k = AoS row)
+  const uint64_t* rows;        // packed 32-byte rows shared by every value aggregate (or nullptr):
+  uint32_t word[kMaxAggs];     // then aggregate a reads word[a] of row r, loaded as two 16-byte vectors
 };
 
 __device__ __forceinline__ uint64_t m_combine(uint64_t a, uint64_t b, int op) {
@@ -253,7 +255,7 @@ __global__ __launch_bounds__(256) void seg_reduce_multi_kernel(const E128* __res
 // that start and end inside the lane are written directly), and only the per-lane tail partials
 // take part in a 64-lane segmented scan — 1/PER of the cross-lane traffic of the per-element
 // scan above.  Segments touching the chunk boundary are combined with atomics.
-template <int PER, int NAGG>
+template <int PER, int NAGG, bool PACKED>
 __global__ __launch_bounds__(256) void seg_reduce_multi_serial(const E128* __restrict__ ent,
                                                                const int64_t* __restrict__ seg, uint64_t n,
                                                                AggSpecs sp) {
@@ -298,18 +300,47 @@ __global__ __launch_bounds__(256) void seg_reduce_multi_serial(const E128* __res
     }
     // every aggregate's permuted (random) loads are issued up front, PER x NAGG per lane in flight
     // (with packed rows the NAGG loads of one row hit the same 32-byte sector together)
-    uint64_t vv[NAGG][PER];
+    typedef unsigned long long u2_t __attribute__((ext_vector_type(2)));
+    // PACKED: one 32-byte row per sorted entry, 2 vector loads instead of one load per aggregate;
+    // else every aggregate's permuted loads.  Either way all loads are issued up front.
+    u2_t r0[PACKED ? PER : 1], r1[PACKED ? PER : 1];
+    uint64_t vv[PACKED ? 1 : NAGG][PER];
+    if constexpr (PACKED) {
 #pragma unroll
-    for (int a = 0; a < NAGG; ++a) {
-      const int op = sp.op[a];
+      for (int k = 0; k < PER; ++k) {
+        if (k < cnt) {
+          const u2_t* q = reinterpret_cast<const u2_t*>(sp.rows + (uint64_t)row[k] * 4);
+          r0[k] = q[0];
+          r1[k] = q[1];
+        } else {
+          r0[k] = u2_t{0ull, 0ull};
+          r1[k] = u2_t{0ull, 0ull};
+        }
+      }
+    } else {
 #pragma unroll
-      for (int k = 0; k < PER; ++k)
-        vv[a][k] = (k < cnt) ? ((op == M_COUNT) ? 1ull : sp.vals[a][(uint64_t)row[k] * sp.stride[a]]) : 0ull;
+      for (int a = 0; a < NAGG; ++a) {
+        const int op = sp.op[a];
+#pragma unroll
+        for (int k = 0; k < PER; ++k)
+          vv[a][k] = (k < cnt) ? ((op == M_COUNT) ? 1ull : sp.vals[a][(uint64_t)row[k] * sp.stride[a]]) : 0ull;
+      }
     }
 #pragma unroll
     for (int a = 0; a < NAGG; ++a) {
       const int op = sp.op[a];
-      const uint64_t* v = vv[a];
+      uint64_t v[PER];
+      if constexpr (PACKED) {
+        const uint32_t wd = sp.word[a];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+          const uint64_t x = wd == 0 ? r0[k].x : wd == 1 ? r0[k].y : wd == 2 ? r1[k].x : r1[k].y;
+          v[k] = (k < cnt) ? ((op == M_COUNT) ? 1ull : x) : 0ull;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) v[k] = vv[a][k];
+      }
       // serial pass over the lane's runs
       uint64_t acc = v[0];
       uint64_t head_val = 0;
@@ -514,6 +545,28 @@ DR_API int dr_seg_reduce_multi(const E128* ent, const int64_t* seg, uint64_t n, 
     // a missing output, or a value column missing for a value-reading op, would fault the device
     if (sp.out[a] == nullptr || (sp.op[a] != M_COUNT && sp.vals[a] == nullptr)) return (int)hipErrorInvalidValue;
   }
+  // packed-row mode: every value aggregate reads a word of the same 16-byte-aligned 4-word rows
+  sp.rows = nullptr;
+  {
+    uintptr_t base = UINTPTR_MAX;
+    bool packed = ent != nullptr;
+    int nval = 0;
+    for (int a = 0; a < nagg; ++a) {
+      if (sp.op[a] == M_COUNT) continue;
+      ++nval;
+      packed = packed && sp.stride[a] == 4;
+      base = reinterpret_cast<uintptr_t>(sp.vals[a]) < base ? reinterpret_cast<uintptr_t>(sp.vals[a]) : base;
+    }
+    packed = packed && nval > 0 && (base & 15) == 0;
+    for (int a = 0; a < nagg && packed; ++a) {
+      sp.word[a] = 0;
+      if (sp.op[a] == M_COUNT) continue;
+      const uintptr_t d = reinterpret_cast<uintptr_t>(sp.vals[a]) - base;
+      if (d % 8 != 0 || d / 8 > 3) packed = false;
+      else sp.word[a] = (uint32_t)(d / 8);
+    }
+    if (packed) sp.rows = reinterpret_cast<const uint64_t*>(base);
+  }
   static int serial = -1;
   if (serial < 0) {
     const char* e = getenv("DRYAD_SEGRED_SERIAL");
@@ -521,16 +574,17 @@ DR_API int dr_seg_reduce_multi(const E128* ent, const int64_t* seg, uint64_t n, 
   }
   if (serial) {
     const unsigned g = grid_for(n, 256 * 8, 8192);
+#define DR_SEGRED_CASE(N)                                                             \
+      case N:                                                                          \
+        if (sp.rows) seg_reduce_multi_serial<8, N, true><<<g, 256, 0, s>>>(ent, seg, n, sp);  \
+        else seg_reduce_multi_serial<8, N, false><<<g, 256, 0, s>>>(ent, seg, n, sp);       \
+        break;
     switch (nagg) {
-      case 1: seg_reduce_multi_serial<8, 1><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
-      case 2: seg_reduce_multi_serial<8, 2><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
-      case 3: seg_reduce_multi_serial<8, 3><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
-      case 4: seg_reduce_multi_serial<8, 4><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
-      case 5: seg_reduce_multi_serial<8, 5><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
-      case 6: seg_reduce_multi_serial<8, 6><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
-      case 7: seg_reduce_multi_serial<8, 7><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
-      default: seg_reduce_multi_serial<8, 8><<<g, 256, 0, s>>>(ent, seg, n, sp); break;
+      DR_SEGRED_CASE(1) DR_SEGRED_CASE(2) DR_SEGRED_CASE(3) DR_SEGRED_CASE(4)
+      DR_SEGRED_CASE(5) DR_SEGRED_CASE(6) DR_SEGRED_CASE(7)
+      default: DR_SEGRED_CASE(8)
     }
+#undef DR_SEGRED_CASE
   }
   else
     seg_reduce_multi_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(ent, seg, n, nagg, sp);
