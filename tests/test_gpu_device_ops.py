@@ -268,3 +268,31 @@ def test_fused_segment_ids_match_flag_scan(n):
     assert nseg == ref_n
     assert torch.equal(ids, ref_ids)
     assert torch.equal(starts, ref_starts)
+
+
+@pytest.mark.parametrize("ncols", [2, 3, 4, 5])
+def test_seg_reduce_packed_rows_any_width(ncols, monkeypatch):
+    """Packed value rows: 2-3 distinct columns -> 32-byte rows (vector loads), 4 -> 40-byte rows
+    (strided loads), 5 -> not packed; every layout against a torch reference."""
+    from dryad_amd.ops import relational as R, sort as S
+    monkeypatch.setattr(R, "AOS_MIN_ROWS", 0)
+    torch.manual_seed(ncols)
+    n = 300_007
+    k = torch.randint(0, 50_000, (n,), device="cuda", dtype=torch.int64)
+    cols = [torch.randint(-10**6, 10**6, (n,), device="cuda", dtype=torch.int64) for _ in range(ncols)]
+    e, b0, lo_mask = R.build_keys([k])
+    srt = S.sort_entries_hybrid(e, b0)
+    seg, nseg, _ = R.segment_ids(srt, lo_mask)
+    ops = ["sum", "min", "max", "sum", "max"]
+    specs = [("count", None, torch.int64)] + [(ops[j], c, torch.int64) for j, c in enumerate(cols)] + \
+        [("min", cols[0], torch.int64)]
+    got = R.seg_reduce_multi(srt, seg, nseg, specs)
+    uk, inv = torch.unique(k, return_inverse=True)
+    g = uk.numel()
+    assert torch.equal(got[0], torch.bincount(inv, minlength=g))
+    red = {"sum": lambda c: torch.zeros(g, dtype=torch.int64, device="cuda").index_add_(0, inv, c),
+           "min": lambda c: torch.full((g,), 2**62, dtype=torch.int64, device="cuda").scatter_reduce(0, inv, c, "amin"),
+           "max": lambda c: torch.full((g,), -2**62, dtype=torch.int64, device="cuda").scatter_reduce(0, inv, c, "amax")}
+    for j, c in enumerate(cols):
+        assert torch.equal(got[1 + j], red[ops[j]](c)), j
+    assert torch.equal(got[-1], red["min"](cols[0]))
