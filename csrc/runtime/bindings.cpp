@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include "codec.h"
+#include "fifo.h"
 #include "jobgraph.h"
 #include "workqueue.h"
 
@@ -255,4 +256,35 @@ PYBIND11_MODULE(_dryad_native, m) {
     py::gil_scoped_release nogil;
     write_file_atomic(path, reinterpret_cast<const uint8_t*>(bi.ptr), (size_t)bi.size * bi.itemsize);
   });
+
+  // FIFO channel (C-5).  put/get return a status code (0 ok, 1 timeout, 2 closed, 3 aborted);
+  // both release the GIL while they wait so producer and consumer threads run concurrently.
+  py::class_<BlockFifo>(m, "BlockFifo")
+      .def(py::init<uint64_t>(), py::arg("capacity_bytes"))
+      .def("put", [](BlockFifo& f, py::buffer b, int64_t timeout_ms) {
+            py::buffer_info bi = b.request();
+            const auto* p = reinterpret_cast<const uint8_t*>(bi.ptr);
+            BlockFifo::Block blk(p, p + (size_t)bi.size * bi.itemsize);
+            py::gil_scoped_release nogil;
+            return (int)f.put(std::move(blk), timeout_ms);
+          }, py::arg("block"), py::arg("timeout_ms") = -1)
+      .def("get", [](BlockFifo& f, int64_t timeout_ms) -> py::tuple {
+            BlockFifo::Block blk;
+            BlockFifo::Status st;
+            {
+              py::gil_scoped_release nogil;
+              st = f.get(blk, timeout_ms);
+            }
+            if (st != BlockFifo::Status::Ok) return py::make_tuple((int)st, py::none());
+            return py::make_tuple(0, as_bytes(blk));
+          }, py::arg("timeout_ms") = -1)
+      .def("close", &BlockFifo::close)
+      .def("abort", &BlockFifo::abort)
+      .def("error", &BlockFifo::error)
+      .def("queued_bytes", &BlockFifo::queued_bytes)
+      .def("queued_blocks", &BlockFifo::queued_blocks)
+      .def("peak_bytes", &BlockFifo::peak_bytes)
+      .def("blocks_written", &BlockFifo::blocks_written)
+      .def("capacity", &BlockFifo::capacity)
+      .def("closed", &BlockFifo::closed);
 }
