@@ -462,11 +462,14 @@ def _group_keys(kcols, skeys):
         e, b0, lo_mask = R.build_keys(kcols)
     srt = S.sort_entries_hybrid(e, b0)
     seg, nseg, starts = R.segment_ids(srt, lo_mask)
-    perm = _perm(srt)
-    rows_at_start = perm.index_select(0, starts)
+    # group representatives straight from the sorted entries (nseg reads); the full row
+    # permutation is only materialised when fingerprinted keys must be verified
+    rows_at_start = srt[:, 0].index_select(0, starts).bitwise_and_(0xFFFFFFFF)
+    verify_str = any(sk is not None for sk in skeys)
+    perm = _perm(srt) if (packed is not None or verify_str) else None
     if packed is not None and _rows_differ(packed, perm, packed, rows_at_start.index_select(0, seg)):
         raise NotTraceable("wide key fingerprint collision")
-    if any(sk is not None for sk in skeys):
+    if verify_str:
         from ..ops.fingerprint import strings_differ
         rep = rows_at_start.index_select(0, seg)          # representative row, in sorted order
         for sk in skeys:
