@@ -40,12 +40,19 @@ __device__ __forceinline__ uint64_t norm_key(const void* col, uint64_t i, int t)
     case K_U32: return ((const uint32_t*)col)[i];
     case K_I64: return (uint64_t)(((const int64_t*)col)[i]) ^ 0x8000000000000000ull;
     case K_U64: return ((const uint64_t*)col)[i];
+    // -0.0 folds into +0.0 and every NaN into one canonical NaN, so equality consumers
+    // (GroupBy / Distinct / Join) see the host's notion of equal floats
     case K_F32: {
       uint32_t u = ((const uint32_t*)col)[i];
+      if (u == 0x80000000u) u = 0;
+      if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu)) u = 0x7FC00000u;
       return (u & 0x80000000u) ? (uint32_t)~u : (u | 0x80000000u);
     }
     case K_F64: {
       uint64_t u = ((const uint64_t*)col)[i];
+      if (u == 0x8000000000000000ull) u = 0;
+      if ((u & 0x7FF0000000000000ull) == 0x7FF0000000000000ull && (u & 0x000FFFFFFFFFFFFFull))
+        u = 0x7FF8000000000000ull;
       return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
     }
   }

@@ -43,6 +43,11 @@ class PartitionInfo:
     comparer: object = None
     separators: list | None = None
     descending: bool = False
+    # the range_partition op that produced this partitioning.  A consumer that relies on equal
+    # keys being co-located marks it ``keep_ties``; otherwise the GPU executor's fused OrderBy may
+    # split long runs of equal keys over several ranks (skew), which keeps the global order but
+    # not the co-location.
+    origin: dict | None = field(default=None, compare=False, repr=False)
 
     @staticmethod
     def random(count: int) -> "PartitionInfo":
@@ -53,15 +58,25 @@ class PartitionInfo:
         return PartitionInfo(PartitionType.HASH, count, key, comparer)
 
     @staticmethod
-    def range(key, count, separators=None, descending=False, comparer=None) -> "PartitionInfo":
-        return PartitionInfo(PartitionType.RANGE, count, key, comparer, separators, descending)
+    def range(key, count, separators=None, descending=False, comparer=None, origin=None) -> "PartitionInfo":
+        return PartitionInfo(PartitionType.RANGE, count, key, comparer, separators, descending, origin)
+
+    def rely_on_colocation(self):
+        """A consumer elides a shuffle because equal keys share a partition: the producing range
+        partition must then keep runs of equal keys together."""
+        if self.kind == PartitionType.RANGE and self.origin is not None:
+            self.origin["keep_ties"] = True
 
     def is_partitioned_by(self, key, comparer=None) -> bool:
-        """Records with equal keys are guaranteed to be in the same partition."""
+        """Records with equal keys are guaranteed to be in the same partition (a True answer
+        marks the producing range partition keep_ties, see ``origin``)."""
         if self.count == 1:
             return True
         if self.kind in (PartitionType.HASH, PartitionType.RANGE, PartitionType.HASH_OR_RANGE):
-            return same_key(self.key, key) and (comparer is None or comparer is self.comparer)
+            ok = same_key(self.key, key) and (comparer is None or comparer is self.comparer)
+            if ok:
+                self.rely_on_colocation()
+            return ok
         return False
 
     def is_same_partition(self, other: "PartitionInfo") -> bool:
@@ -73,8 +88,12 @@ class PartitionInfo:
         if self.kind == PartitionType.HASH and other.kind == PartitionType.HASH:
             return True   # same hash function and count; keys compared by the caller
         if self.kind == PartitionType.RANGE and other.kind == PartitionType.RANGE:
-            return (self.separators is not None and self.separators == other.separators
-                    and self.descending == other.descending)
+            ok = (self.separators is not None and self.separators == other.separators
+                  and self.descending == other.descending)
+            if ok:
+                self.rely_on_colocation()
+                other.rely_on_colocation()
+            return ok
         return False
 
 

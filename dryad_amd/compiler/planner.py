@@ -116,7 +116,7 @@ class Planner:
                              [dict(op="range_partition", key=key, comparer=comparer, descending=descending,
                                    separators=None, count=n, explain=f"range_partition(n={n}, sampled)")])
         part.out_ports = n
-        info = DataSetInfo(PartitionInfo.range(key, n, separators, descending, comparer))
+        info = DataSetInfo(PartitionInfo.range(key, n, separators, descending, comparer, origin=part.ops[-1]))
         m = self._new("Merge", n, [StageInput(part, "cross")], [], info, dtype=src.dtype)
         m.gang = True
         return m

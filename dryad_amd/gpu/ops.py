@@ -43,8 +43,15 @@ def _check(t):
 
 # ---------------------------------------------------------------------------------------------
 # key handling
+def _row_index_fits(n: int):
+    """Sort entries carry a 32-bit row index (low word of ``lo``)."""
+    if n >= (1 << 32):
+        raise NotTraceable("partition of 2^32 rows or more (32-bit row index in the sort entries)")
+
+
 def key_entries(table: DeviceTable, key_fn, comparer=None, descending=False):
     """-> (entries [n,2], begin_bit, lo_mask).  Keys compare like the object path's default order."""
+    _row_index_fits(table.n)
     if table.heap is not None:
         raise NotTraceable("string keys")
     if comparer is not None:
@@ -108,6 +115,7 @@ def eq_key_entries(table: DeviceTable, key_fn, comparer=None):
     keys longer than 12 bytes) by the fingerprint of their packed bytes.
     -> (entries, begin_bit, lo_mask, skeys, wide): ``wide`` = (packed key bytes, key layout) for a
     fingerprinted wide key (callers that pair rows verify the bytes), else None."""
+    _row_index_fits(table.n)
     if table.heap is not None:
         raise NotTraceable("text records")
     if comparer is not None:
@@ -348,6 +356,66 @@ def op_sort(op, inputs, v):
     return t.take(perm)
 
 
+def hash_keys(table: DeviceTable, key_fn):
+    """Key selector -> (HashKey fields, tuple_form) for stable_hash_dest: the key VALUE the host
+    partitioner would hash (runtime/vertex_ops.stable_hash), whatever column widths this
+    partition inferred."""
+    res = TR.call(key_fn, table)
+
+    def field(v):
+        if isinstance(v, TR.StrCol):
+            return R.HashKey.string(v.heap, v.off, v.len)
+        if isinstance(v, TR.ByteField):
+            return R.HashKey.bytes_field(table.rows, v.off, v.length)
+        c = TR._as_col(v, table.n, table.device)
+        if c.dtype not in R.KEY_TYPES or c.dim() != 1:
+            raise NotTraceable(f"hash key of dtype {c.dtype}")
+        return R.HashKey.column(c)
+
+    if isinstance(res, TR.RowProxy):
+        return [R.HashKey.bytes_field(table.rows, 0, table.rows.shape[1])], False
+    if isinstance(res, TR.RecProxy):
+        sh = table.shape
+        if sh.kind == "scalar":
+            return [field(TR._field(table, sh.fields[0]))], False
+        if sh.kind not in ("tuple", "dataclass"):
+            raise NotTraceable(f"hash of a {sh.kind} record")
+        items = [TR._field(table, f) for f in sh.fields]
+        if len(items) > R.MAX_HASH_COLS:
+            raise NotTraceable("record key with more than 8 fields")
+        return [field(x) for x in items], True
+    if isinstance(res, tuple):
+        if not res or len(res) > R.MAX_HASH_COLS:
+            raise NotTraceable("tuple key of 0 or more than 8 fields")
+        if any(isinstance(x, tuple) for x in res):
+            raise NotTraceable("nested tuple key")
+        return [field(x) for x in res], True
+    return [field(res)], False
+
+
+def hash_partition_perm(table: DeviceTable, key_fn, n: int):
+    """-> (row permutation grouping rows by destination, n+1 port offsets).  The destination is
+    the host partitioner's (hash & 0x7FFFFFFF) % n of the key value, so device and host vertices
+    of one stage always agree.  n > 256 takes one stable 8-bit pass per destination byte."""
+    if n > (1 << 24):
+        raise NotTraceable("more than 2^24 hash partitions")
+    if table.n >= (1 << 32):
+        raise NotTraceable("hash partition of 2^32 rows or more")
+    keys, tup = hash_keys(table, key_fn)
+    e, _ = R.stable_hash_dest(keys, table.n, n, tup, table.device)
+    shift = 64
+    while True:
+        e, starts = S.partition_pass(e, shift)
+        shift += 8
+        if n <= (1 << (shift - 64)):
+            break
+    if n <= 256:
+        st = starts[: n + 1]
+    else:
+        st = torch.searchsorted(e[:, 1].contiguous(), torch.arange(n + 1, dtype=torch.int64, device=e.device))
+    return _perm(e), st.tolist()
+
+
 def op_hash_partition(op, inputs, v):
     t = _check(_one(inputs))
     n = op["count"]
@@ -355,11 +423,8 @@ def op_hash_partition(op, inputs, v):
         raise NotTraceable("custom comparer")
     if t.n == 0:
         return Ported(t, [0] * (n + 1))
-    e, _, lo_mask, _, _ = eq_key_entries(t, op["key"])
-    R.hash_dest(e, lo_mask, n)
-    part, starts = S.partition_pass(e, 64)
-    st = starts[: n + 1].tolist()
-    return Ported(t.take(_perm(part)), st)
+    perm, st = hash_partition_perm(t, op["key"], n)
+    return Ported(t.take(perm), st)
 
 
 def op_sample(op, inputs, v):
@@ -454,6 +519,7 @@ def _group_keys(kcols, skeys):
     keys (the operator falls back to the host if one ever occurs)."""
     if any(c.dtype not in R.KEY_TYPES or c.dim() != 1 for c in kcols):
         raise NotTraceable("group key of a non-key dtype")
+    _row_index_fits(kcols[0].shape[0] if kcols else 0)
     packed = None
     if _wide(kcols):
         fp, packed = _wide_key(kcols)

@@ -182,12 +182,15 @@ def _sort_keys(rows: torch.Tensor, ent: torch.Tensor, tmp: torch.Tensor, key_off
 def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int, world: World | None = None,
                           sample_target: int = 1 << 20, seed: int = 314159,
                           stats: SortStats | None = None, keys_ready: bool = False,
-                          hi_bounds: tuple[int, int] | None = None) -> torch.Tensor:
+                          hi_bounds: tuple[int, int] | None = None, split_ties: bool = True) -> torch.Tensor:
     """Globally sort the first ``n`` rows of ``bufs.rows_in`` across all ranks.
 
     On return rank r holds, in ``bufs.rows_out[:n_r]``, the r-th key range in ascending order.
     ``bufs.rows_in`` is clobbered (it becomes the receive buffer).  ``keys_ready``: ``bufs.ent_a[:n]``
     already holds the rows' sort entries; ``hi_bounds``: known hi range of the local keys.
+    ``split_ties``: runs of equal keys may be split over ranks (skew); keeps the global order but
+    not the co-location of equal keys, so the planner turns it off (keep_ties) when a consumer
+    relies on the output being partitioned by the key.
 
     With several ranks the exchange is pipelined with the local sort.  The sampled separators cut
     the key space into ``W * B`` ranges, B consecutive ones per destination rank.  One bucket
@@ -210,7 +213,7 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     ent = bufs.ent_a[:n] if keys_ready else S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
     _, _, lo_mask = key_bits(key_len)
     part_mask = lo_mask
-    if key_len <= 10 and W < (1 << 16):
+    if split_ties and key_len <= 10 and W < (1 << 16):
         # skew: equal keys must not all land on one rank.  Bits 47..32 of lo are free for keys of
         # <= 10 bytes; with the rank there (and the row index below it) every entry is unique, so
         # the sampled separators split runs of equal keys across ranks while the global order

@@ -35,6 +35,8 @@ def key_bit_count(cols) -> int:
 def build_keys(cols: list, descending=None, idx_base: int = 0, out: torch.Tensor | None = None):
     """Typed key columns (<= 96 bits total) -> (E128 entries [n,2] int64, begin_bit, lo_mask)."""
     n = cols[0].shape[0]
+    if n + idx_base >= (1 << 32):
+        raise ValueError("build_keys: row index does not fit the 32-bit index field")
     dev = cols[0].device
     if out is None:
         out = torch.empty((n, 2), dtype=torch.int64, device=dev)
@@ -53,6 +55,10 @@ def build_keys(cols: list, descending=None, idx_base: int = 0, out: torch.Tensor
 
 
 def hash_dest(entries: torch.Tensor, lo_mask: int, nparts: int) -> torch.Tensor:
+    """Internal bucket hash (grace join buckets; both join sides use it).  Not the partitioner
+    hash: keyed shuffles use stable_hash_dest, which matches the host path."""
+    if not 0 < nparts <= 256:
+        raise ValueError(f"hash_dest: {nparts} buckets (1..256)")
     _lib.call("dr_hash_dest", ptr(entries), c_u64(entries.shape[0]), c_u64(lo_mask & (2**64 - 1)), c_u32(nparts),
               stream_of(entries))
     return entries
@@ -429,3 +435,68 @@ def hash_aggregate(key: torch.Tensor, specs: list, capacity: int | None = None):
         keys_out = torch.cat([keys_out, torch.tensor([-2**63], dtype=torch.int64, device=dev)])
         res = [torch.cat([r, o[capacity:capacity + 1]]) for r, o in zip(res, outs)]
     return keys_out.to(key.dtype), res
+
+
+# ---------------------------------------------------------------------------------------------
+# Device image of the host partitioner hash (csrc/kernels/stablehash.hip)
+_lib.register_signatures({
+    "dr_stable_hash_dest": (c_i32, [ctypes.POINTER(c_i32), ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                    ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), c_i32, c_i32,
+                                    c_u64, c_u32, vp, vp, vp]),
+})
+
+H_BYTES, H_STR = 20, 21
+MAX_HASH_COLS = 8
+
+
+class HashKey:
+    """One field of a key for stable_hash_dest: a typed column, a byte-string field of fixed-width
+    rows, or a string field (heap, offsets, lengths)."""
+    __slots__ = ("kind", "t", "off", "len", "stride", "boff", "blen")
+
+    def __init__(self, kind, t, off=None, ln=None, stride=0, boff=0, blen=0):
+        self.kind, self.t, self.off, self.len = kind, t, off, ln
+        self.stride, self.boff, self.blen = stride, boff, blen
+
+    @staticmethod
+    def column(c: torch.Tensor) -> "HashKey":
+        if c.dtype not in KEY_TYPES or c.dim() != 1:
+            raise TypeError(f"hash key column of dtype {c.dtype} / dim {c.dim()}")
+        return HashKey(KEY_TYPES[c.dtype], c.contiguous())
+
+    @staticmethod
+    def bytes_field(rows: torch.Tensor, off: int, length: int) -> "HashKey":
+        assert rows.dtype == torch.uint8 and rows.dim() == 2 and rows.is_contiguous()
+        assert 0 <= off and off + length <= rows.shape[1]
+        return HashKey(H_BYTES, rows, stride=rows.shape[1], boff=off, blen=length)
+
+    @staticmethod
+    def string(heap: torch.Tensor, off: torch.Tensor, ln: torch.Tensor) -> "HashKey":
+        if heap.numel() == 0:
+            heap = torch.zeros(8, dtype=torch.uint8, device=off.device)
+        return HashKey(H_STR, heap, off.to(torch.int64).contiguous(), ln.to(torch.int64).contiguous())
+
+
+def stable_hash_dest(keys: list, n: int, nparts: int, tuple_form: bool, device,
+                     want_hash: bool = False):
+    """Destination partition of every record under the host partitioner hash
+    (runtime/vertex_ops.stable_hash): -> (E128 entries {lo = row, hi = port} or None,
+    int64 hashes or None).  ``tuple_form``: the key is a tuple/record of ``keys``."""
+    if not keys or len(keys) > MAX_HASH_COLS or (not tuple_form and len(keys) != 1):
+        raise ValueError("stable_hash_dest: 1..8 key fields (exactly 1 unless tuple_form)")
+    if n >= (1 << 32):
+        raise ValueError("stable_hash_dest: partition of 2^32 rows or more")
+    k = len(keys)
+    kinds = (c_i32 * k)(*[x.kind for x in keys])
+    ptrs = (vp * k)(*[x.t.data_ptr() for x in keys])
+    offs = (vp * k)(*[x.off.data_ptr() if x.off is not None else 0 for x in keys])
+    lens = (vp * k)(*[x.len.data_ptr() if x.len is not None else 0 for x in keys])
+    strides = (c_u32 * k)(*[x.stride for x in keys])
+    boffs = (c_u32 * k)(*[x.boff for x in keys])
+    blens = (c_u32 * k)(*[x.blen for x in keys])
+    ent = torch.empty((n, 2), dtype=torch.int64, device=device) if nparts else None
+    hs = torch.empty(n, dtype=torch.int64, device=device) if want_hash else None
+    _lib.call("dr_stable_hash_dest", kinds, ptrs, offs, lens, strides, boffs, blens, k, int(bool(tuple_form)),
+              c_u64(n), c_u32(nparts), ptr(ent) if ent is not None else None,
+              ptr(hs) if hs is not None else None, stream_of(keys[0].t))
+    return ent, hs

@@ -134,7 +134,8 @@ class GpuJobRunner:
             if rp.partitions != st[x].partitions or m.partitions != st[x].partitions:
                 continue
             out[m.id] = dict(x=x, stages=[samp.id, sep.id, rp.id], key=m.ops[0]["key"],
-                             desc=m.ops[0].get("descending", False), comparer=m.ops[0].get("comparer"))
+                             desc=m.ops[0].get("descending", False), comparer=m.ops[0].get("comparer"),
+                             keep_ties=bool(rp.ops[0].get("keep_ties", False)))
         return out
 
     def _fused_applicable(self, f) -> bool:
@@ -169,7 +170,8 @@ class GpuJobRunner:
         stats = RS.SortStats()
         bounds = bs.take_keys(t.rows, off, ln)
         out = RS.distributed_sort_rows(bs.bufs, t.n, off, ln, self.world, stats=stats,
-                                       keys_ready=bounds is not None, hi_bounds=bounds)
+                                       keys_ready=bounds is not None, hi_bounds=bounds,
+                                       split_ties=not f.get("keep_ties", False))
         self.row_sets[(m.id, me)] = bs
         self.last_sort_stats = stats
         table = DeviceTable(out.shape[0], t.shape, rows=out)

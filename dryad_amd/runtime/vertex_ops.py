@@ -18,6 +18,7 @@ import dataclasses
 import functools
 import heapq
 import itertools
+import math
 import random
 import struct
 from collections import OrderedDict
@@ -69,7 +70,10 @@ def _h(k) -> int:
         x ^= x >> 33
         return x
     if isinstance(k, float):
-        if k == int(k) and abs(k) < 2**63:
+        # mirrored bit for bit by the device partitioner (csrc/kernels/stablehash.hip)
+        if k != k:
+            return _fnv(struct.pack("<Q", 0x7FF8000000000000))
+        if math.isfinite(k) and abs(k) < 2**63 and k == int(k):
             return _h(int(k))
         return _fnv(struct.pack("<d", k))
     if isinstance(k, str):

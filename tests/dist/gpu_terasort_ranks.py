@@ -34,6 +34,14 @@ def main():
     assert got == exp
     fb = {op for _, op, _ in g._get_executor().last_result["fallbacks"]}
     assert "group_partial" not in fb and "group_final" not in fb, fb
+    # OrderBy(k).GroupBy(k) with heavily duplicated keys: GroupBy elides its shuffle, so the fused
+    # distributed OrderBy must keep equal keys on one rank (planner keep_ties)
+    ts = "gen://terasort?records=200000&partitions=%d&seed=5" % w.size
+    k1 = lambda r: r[0:1]  # noqa: E731
+    got = sorted(g.FromStore(ts).OrderBy(k1).GroupBy(k1, lambda k, gr: (k, gr.Count())))
+    exp = sorted(l.FromStore(ts).OrderBy(k1).GroupBy(k1, lambda k, gr: (k, gr.Count())))
+    assert got == exp, (len(got), len(exp))
+    assert len(got) == 256
     # skew: every key equal -> the (key, rank, row) tie-break still balances the ranks
     from dryad_amd.ops import recordsort as RS
     n = 300_000
