@@ -18,6 +18,12 @@ struct __attribute__((aligned(16))) E128 {
   uint64_t hi;
 };
 
+// 64-bit sort entry of the compact row sort: a 32-bit window of the key (the 32 key bits right
+// below the common prefix of all keys) in the high word, a 32-bit row index in the low word.
+struct __attribute__((aligned(8))) E64 {
+  uint64_t v;
+};
+
 // 256-bit sort entry: an E128 key (same digit layout) carrying two more payload words, so a sort
 // can move up to three 8-byte values with the key instead of leaving a row permutation to gather
 // through (GroupBy with decomposable aggregates: sequential segmented reduction afterwards).

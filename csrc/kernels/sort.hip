@@ -32,6 +32,10 @@ __device__ __forceinline__ uint32_t digit_of(const T& e, int shift) {
                      : (uint32_t)((e.lo >> shift) & 0xFF);
 }
 
+__device__ __forceinline__ uint32_t digit_of(const E64& e, int shift) {
+  return (uint32_t)((e.v >> shift) & 0xFF);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void rs_count(const T* __restrict__ in, uint64_t n, int shift,
                                                 uint32_t* __restrict__ counts, uint32_t G,
@@ -1057,4 +1061,221 @@ DR_API int dr_sort_wide(int words, void* keys, void* tmp, uint64_t n, int begin_
 DR_API uint64_t dr_sort_u256_workspace(uint64_t n) {
   (void)n;
   return ((uint64_t)kBins * kMaxGrid + 1024) * sizeof(uint32_t);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Compact row sort (fixed-width rows, byte-string key in memcmp order).
+//
+// The 16-byte key-pointer entries of the hybrid sort move 40 GB per LSD pass at 1.25e9 rows.  Here
+// an entry is 8 bytes: the 32 key bits right below the common prefix of all keys (the "window")
+// and the 32-bit row index.  A stable LSD sort over the window (4 passes at 1e9 rows, 20 GB each)
+// leaves runs of equal windows (mean n / 2^32 ~ 0.3 extra entries per run for uniform keys); the
+// row gather then finishes those runs itself: it reads the full keys of the rows of a
+// multi-entry run (which it fetches anyway), ranks them in LDS and writes every row at its final
+// position.  A run longer than the gather's LDS window sets *overflow (the caller falls back to
+// the full-key hybrid sort).
+namespace {
+
+__device__ __forceinline__ void load_key128(const uint8_t* r, uint32_t key_len, bool aligned, uint64_t& k0,
+                                            uint64_t& k1) {
+  uint32_t b[4] = {0, 0, 0, 0};
+  if (aligned) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(r);
+    const uint32_t nw = (key_len + 3) >> 2;
+    for (uint32_t k = 0; k < nw; ++k) b[k] = bswap32(w[k]);
+  } else {
+    for (uint32_t k = 0; k < key_len; ++k) b[k >> 2] |= (uint32_t)r[k] << (8 * (3 - (k & 3)));
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int bytes = (int)key_len - 4 * k;
+    if (bytes <= 0) b[k] = 0;
+    else if (bytes < 4) b[k] &= 0xFFFFFFFFu << (8 * (4 - bytes));
+  }
+  k0 = ((uint64_t)b[0] << 32) | b[1];
+  k1 = ((uint64_t)b[2] << 32) | b[3];
+}
+
+// window = composite key bits [P, P + 32) counted from the most significant end
+__device__ __forceinline__ uint32_t key_window(uint64_t k0, uint64_t k1, uint32_t P) {
+  const unsigned __int128 k = ((unsigned __int128)k0 << 64) | k1;
+  return P >= 128 ? 0u : (uint32_t)((k << P) >> 96);
+}
+
+__global__ __launch_bounds__(256) void extract_keys64_kernel(const uint8_t* __restrict__ rows, uint64_t n,
+                                                             uint32_t stride, uint32_t key_off, uint32_t key_len,
+                                                             uint32_t P, uint32_t idx_base, E64* __restrict__ out) {
+  const bool aligned = ((stride | key_off) & 3) == 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t k0, k1;
+    load_key128(rows + i * stride + key_off, key_len, aligned, k0, k1);
+    E64 e;
+    e.v = ((uint64_t)key_window(k0, k1, P) << 32) | (uint32_t)(idx_base + (uint32_t)i);
+    out[i] = e;
+  }
+}
+
+constexpr int kGfCore = 256, kGfExt = 64, kGfWin = kGfCore + kGfExt;
+
+// One workgroup per 256 output positions (grid-stride): owns the runs that START in its core and
+// finishes them up to 64 positions past it; positions of a run started by the previous workgroup
+// are left to that workgroup.  Rows are copied dword-wise, output-coalesced (gather_rows_kernel).
+template <int WC>
+__global__ __launch_bounds__(256) void gather_fixup_kernel(const uint32_t* __restrict__ rows, uint32_t* __restrict__ out,
+                                                           const E64* __restrict__ ent, uint64_t n, uint32_t Wdyn,
+                                                           uint32_t key_off, uint32_t key_len, int run_shift,
+                                                           uint32_t* __restrict__ overflow) {
+  const uint32_t W = WC > 0 ? (uint32_t)WC : Wdyn;
+  __shared__ uint32_t rid[kGfWin + 1];     // rid[p + 1] = run id of window position p; rid[0] = position -1
+  __shared__ uint32_t idx[kGfWin];
+  __shared__ uint32_t sidx[kGfWin];
+  __shared__ uint64_t kk0[kGfWin], kk1[kGfWin];
+  __shared__ uint32_t own[2];
+  const int t = threadIdx.x;
+  const uint8_t* rbytes = reinterpret_cast<const uint8_t*>(rows);
+  const bool aligned = (((W * 4) | key_off) & 3) == 0;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * kGfCore; c0 < n; c0 += (uint64_t)gridDim.x * kGfCore) {
+    const uint32_t L = (uint32_t)((n - c0) < (uint64_t)kGfWin ? (n - c0) : kGfWin);
+    const uint32_t core = L < (uint32_t)kGfCore ? L : (uint32_t)kGfCore;
+    for (uint32_t p = t; p < L; p += kBlock) {
+      const uint64_t v = ent[c0 + p].v;
+      rid[p + 1] = (uint32_t)(v >> run_shift);
+      idx[p] = (uint32_t)v;
+    }
+    if (t == 0) {
+      rid[0] = c0 > 0 ? (uint32_t)(ent[c0 - 1].v >> run_shift) : 0u;
+      own[0] = 0xFFFFFFFFu;
+      own[1] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    for (uint32_t p = t; p < L; p += kBlock) {
+      const bool start = (c0 + p == 0) || rid[p + 1] != rid[p];
+      if (start) atomicMin(&own[p < core ? 0 : 1], p);
+    }
+    __syncthreads();
+    const uint32_t ob = own[0];
+    uint32_t oe = own[1];
+    if (oe == 0xFFFFFFFFu && c0 + L == n) oe = L;
+    if (ob == 0xFFFFFFFFu) {           // the whole core continues a run owned by a previous workgroup
+      __syncthreads();
+      continue;
+    }
+    if (oe == 0xFFFFFFFFu) {           // a run owned here does not end inside the window
+      if (t == 0) atomicOr(overflow, 1u);
+      __syncthreads();
+      continue;
+    }
+    // phase A: keys of the rows in multi-entry runs
+    for (uint32_t p = ob + t; p < oe; p += kBlock) {
+      const bool multi = (p > ob && rid[p + 1] == rid[p]) || (p + 1 < oe && rid[p + 2] == rid[p + 1]);
+      if (multi) {
+        uint64_t k0, k1;
+        load_key128(rbytes + (uint64_t)idx[p] * (W * 4) + key_off, key_len, aligned, k0, k1);
+        kk0[p] = k0;
+        kk1[p] = k1;
+      } else {
+        sidx[p - ob] = idx[p];
+      }
+    }
+    __syncthreads();
+    // phase B: rank inside each run: (key, position) order = stable
+    for (uint32_t p = ob + t; p < oe; p += kBlock) {
+      const uint32_t r = rid[p + 1];
+      const bool multi = (p > ob && rid[p] == r) || (p + 1 < oe && rid[p + 2] == r);
+      if (!multi) continue;
+      uint32_t rs = p, re = p + 1;
+      while (rs > ob && rid[rs] == r) --rs;
+      while (re < oe && rid[re + 1] == r) ++re;
+      const uint64_t a0 = kk0[p], a1 = kk1[p];
+      uint32_t cnt = 0;
+      for (uint32_t q = rs; q < re; ++q) {
+        const uint64_t b0 = kk0[q], b1 = kk1[q];
+        cnt += (b0 < a0 || (b0 == a0 && (b1 < a1 || (b1 == a1 && q < p)))) ? 1u : 0u;
+      }
+      sidx[rs + cnt - ob] = idx[p];
+    }
+    __syncthreads();
+    const uint32_t words = (oe - ob) * W;
+    uint32_t* o = out + (c0 + ob) * W;
+    uint32_t j = t;
+    for (; j + 3 * kBlock < words; j += 4 * kBlock) {
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t jj = j + k * kBlock;
+        const uint32_t r = jj / W, c = jj - r * W;
+        v[k] = rows[(uint64_t)sidx[r] * W + c];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[j + k * kBlock] = v[k];
+    }
+    for (; j < words; j += kBlock) {
+      const uint32_t r = j / W, c = j - r * W;
+      o[j] = rows[(uint64_t)sidx[r] * W + c];
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+DR_API int dr_extract_keys64(const uint8_t* rows, uint64_t n, uint32_t stride, uint32_t key_off, uint32_t key_len,
+                             uint32_t prefix_bits, uint32_t idx_base, E64* out, hipStream_t s) {
+  if (key_len == 0 || key_len > 16 || key_off + key_len > stride) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  if (n + idx_base > (1ull << 32)) return (int)hipErrorInvalidValue;
+  extract_keys64_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(rows, n, stride, key_off, key_len, prefix_bits,
+                                                                idx_base, out);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// Stable LSD radix sort of E64 entries on bits [begin_bit, end_bit) (multiples of 8, < 64 = the
+// window); 16 entries per thread per tile (128 contiguous output bytes per digit run).
+DR_API int dr_sort_u64(E64* keys, E64* tmp, uint64_t n, int begin_bit, int end_bit, void* ws, hipStream_t s,
+                       int* result_in_tmp) {
+  *result_in_tmp = 0;
+  if (n == 0 || begin_bit >= end_bit) return 0;
+  if (end_bit > 64 || begin_bit < 0 || (begin_bit & 7) || (end_bit & 7)) return (int)hipErrorInvalidValue;
+  if (n >= (1ull << 32)) return (int)hipErrorInvalidValue;
+  constexpr int ITEMS = 16;
+  const uint64_t tile = (uint64_t)kBlock * ITEMS;
+  uint64_t tiles = (n + tile - 1) / tile;
+  if (tiles < 1) tiles = 1;
+  const uint32_t G = (uint32_t)(tiles < (uint64_t)kMaxGrid ? tiles : (uint64_t)kMaxGrid);
+  const uint64_t per_block = ((tiles + G - 1) / G) * tile;
+  uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* partial = counts + (uint64_t)kBins * G;
+  E64* src = keys;
+  E64* dst = tmp;
+  int flips = 0;
+  for (int shift = begin_bit; shift < end_bit; shift += kRadixBits) {
+    rs_count<<<G, 256, 0, s>>>(src, n, shift, counts, G, per_block);
+    scan_inplace(counts, kBins * G, partial, s);
+    rs_scatter_v2<E64, ITEMS><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+    E64* x = src; src = dst; dst = x;
+    flips ^= 1;
+  }
+  DR_LAUNCH_CHECK();
+  *result_in_tmp = flips;
+  return 0;
+}
+
+// Row gather + run fix-up of the compact sort: out = rows in (window, full key, position) order.
+// run_shift = 64 - (window bits the LSD sort covered).  stride % 4 == 0, key_len <= 16.
+DR_API int dr_gather_fixup(const uint8_t* rows, uint8_t* out, const E64* ent, uint64_t n, uint32_t stride,
+                           uint32_t key_off, uint32_t key_len, int run_shift, uint32_t* overflow, hipStream_t s) {
+  if (stride == 0 || (stride & 3) || key_len == 0 || key_len > 16 || key_off + key_len > stride) return (int)hipErrorInvalidValue;
+  if (run_shift < 32 || run_shift > 63) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  const unsigned g = grid_for(n, kGfCore, 16384);
+  const uint32_t W = stride / 4;
+  const uint32_t* in = reinterpret_cast<const uint32_t*>(rows);
+  uint32_t* o = reinterpret_cast<uint32_t*>(out);
+  if (W == 25)
+    gather_fixup_kernel<25><<<g, 256, 0, s>>>(in, o, ent, n, W, key_off, key_len, run_shift, overflow);
+  else
+    gather_fixup_kernel<0><<<g, 256, 0, s>>>(in, o, ent, n, W, key_off, key_len, run_shift, overflow);
+  DR_LAUNCH_CHECK();
+  return 0;
 }

@@ -50,9 +50,11 @@ __device__ __forceinline__ void ts_record(uint64_t seed, uint64_t g, uint32_t* w
 // also emits the record's 16-byte sort entry (the extract_keys_ts layout: hi = key bytes 0..7,
 // lo = key bytes 8..9 << 48 | row index) and folds [min, max] of hi into hi_range, so a sort
 // that consumes the generated table skips its key-extraction pass (one 100-byte row read each).
-template <bool KEYS>
+// KEYS: 0 = rows only, 1 = E128 entries (full 80-bit key), 2 = E64 entries of the compact row
+// sort (key bits 0..31 in the high word: the window for a zero common prefix).
+template <int KEYS>
 __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out, uint64_t n, uint64_t first,
-                                                     uint64_t seed, E128* __restrict__ keys, uint32_t idx_base,
+                                                     uint64_t seed, void* __restrict__ keys, uint32_t idx_base,
                                                      unsigned long long* __restrict__ hi_range) {
   __shared__ __attribute__((aligned(16))) uint32_t img[256 * 25];
   uint64_t mn = ~0ull, mx = 0;
@@ -64,12 +66,18 @@ __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out,
 #pragma unroll
       for (int k = 0; k < 25; ++k) img[threadIdx.x * 25 + k] = w[k];
       if (KEYS) {
-        E128 e;
-        e.hi = ((uint64_t)bswap32(w[0]) << 32) | bswap32(w[1]);
-        e.lo = ((uint64_t)(bswap32(w[2]) & 0xFFFF0000u) << 32) | (uint32_t)(idx_base + (uint32_t)(row0 + threadIdx.x));
-        keys[row0 + threadIdx.x] = e;
-        mn = e.hi < mn ? e.hi : mn;
-        mx = e.hi > mx ? e.hi : mx;
+        const uint64_t hi = ((uint64_t)bswap32(w[0]) << 32) | bswap32(w[1]);
+        const uint32_t idx = idx_base + (uint32_t)(row0 + threadIdx.x);
+        if (KEYS == 1) {
+          E128 e;
+          e.hi = hi;
+          e.lo = ((uint64_t)(bswap32(w[2]) & 0xFFFF0000u) << 32) | idx;
+          static_cast<E128*>(keys)[row0 + threadIdx.x] = e;
+        } else {
+          static_cast<uint64_t*>(keys)[row0 + threadIdx.x] = (hi & 0xFFFFFFFF00000000ull) | idx;
+        }
+        mn = hi < mn ? hi : mn;
+        mx = hi > mx ? hi : mx;
       }
     }
     __syncthreads();
@@ -137,8 +145,8 @@ __global__ __launch_bounds__(256) void ts_check_kernel(const uint32_t* __restric
 
 DR_API int dr_terasort_gen(uint8_t* out, uint64_t n, uint64_t first_index, uint64_t seed, hipStream_t s) {
   if (n == 0) return 0;
-  ts_gen_kernel<false><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index,
-                                                               seed, nullptr, 0, nullptr);
+  ts_gen_kernel<0><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index,
+                                                           seed, nullptr, 0, nullptr);
   DR_LAUNCH_CHECK();
   return 0;
 }
@@ -149,9 +157,21 @@ DR_API int dr_terasort_gen_keys(uint8_t* out, uint64_t n, uint64_t first_index, 
                                 uint32_t idx_base, uint64_t* hi_range, hipStream_t s) {
   if (n == 0) return 0;
   if (n + idx_base > (1ull << 32)) return (int)hipErrorInvalidValue;
-  ts_gen_kernel<true><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index,
-                                                              seed, keys, idx_base,
-                                                              reinterpret_cast<unsigned long long*>(hi_range));
+  ts_gen_kernel<1><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index,
+                                                           seed, keys, idx_base,
+                                                           reinterpret_cast<unsigned long long*>(hi_range));
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// Same, emitting the 8-byte entries of the compact row sort (dr_extract_keys64 with prefix 0).
+DR_API int dr_terasort_gen_keys64(uint8_t* out, uint64_t n, uint64_t first_index, uint64_t seed, E64* keys,
+                                  uint32_t idx_base, uint64_t* hi_range, hipStream_t s) {
+  if (n == 0) return 0;
+  if (n + idx_base > (1ull << 32)) return (int)hipErrorInvalidValue;
+  ts_gen_kernel<2><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index,
+                                                           seed, keys, idx_base,
+                                                           reinterpret_cast<unsigned long long*>(hi_range));
   DR_LAUNCH_CHECK();
   return 0;
 }

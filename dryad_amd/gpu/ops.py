@@ -186,8 +186,14 @@ def op_read(op, inputs, v):
             if bs is not None:
                 # producer-side key extraction: a following OrderBy(key bytes 0..9) starts sorting
                 rng = torch.tensor([-1, 0], dtype=torch.int64, device=rows.device)
-                TSK.generate_with_keys(rows, lo, int(q.get("seed", 0)), bs.bufs.ent_a, rng)
-                bs.keys_ready = (rows.data_ptr(), hi - lo, 0, 10, rng)
+                if v.world.size == 1 and S.compact_sort_ok(rows, 10):
+                    # one rank: the sort takes the compact 8-byte entries
+                    TSK.generate_with_keys64(rows, lo, int(q.get("seed", 0)), bs.bufs.ent_a.view(-1), rng)
+                    fmt = "e64"
+                else:
+                    TSK.generate_with_keys(rows, lo, int(q.get("seed", 0)), bs.bufs.ent_a, rng)
+                    fmt = "e128"
+                bs.keys_ready = (rows.data_ptr(), hi - lo, 0, 10, rng, fmt)
             else:
                 TSK.generate(rows, lo, int(q.get("seed", 0)))
             return t
@@ -347,10 +353,11 @@ def op_sort(op, inputs, v):
         # in-place key-pointer sort of pooled rows: rows_in -> rows_out, entries in the pool
         kind, spec = TR.key_columns(TR.call(op["key"], t), t)
         if kind == "bytes" and spec.length <= 12:
-            bounds = bs.take_keys(t.rows, spec.off, spec.length)
+            kr = bs.take_keys(t.rows, spec.off, spec.length)
             out = RS.local_sort_rows(t.rows, bs.bufs.rows_out, bs.bufs.ent_a, bs.bufs.ent_b, spec.off, spec.length,
-                                     descending=op.get("descending", False), hi_bounds=bounds,
-                                     keys_ready=bounds is not None)
+                                     descending=op.get("descending", False),
+                                     hi_bounds=None if kr is None else kr[:2], keys_ready=kr is not None,
+                                     keys_fmt="e128" if kr is None else kr[2])
             return DeviceTable(out.shape[0], t.shape, rows=out)
     _, perm, _ = sort_perm(t, op["key"], op.get("comparer"), op.get("descending", False))
     return t.take(perm)

@@ -23,20 +23,21 @@ class BufferSet:
         self.pins = 0
         self.in_use = False
         # set by a producer that also wrote rows_in's sort entries into bufs.ent_a:
-        # (rows_in data_ptr, n, key_off, key_len, hi_range device tensor); consumed by one sort
+        # (rows_in data_ptr, n, key_off, key_len, hi_range device tensor, entry format "e64" |
+        # "e128"); consumed by one sort
         self.keys_ready = None
 
     def take_keys(self, rows, key_off: int, key_len: int):
-        """Entries in ent_a for exactly these rows and key, or None.  One-shot: sorting reuses
-        ent_a as scratch, so the claim is dropped either way."""
+        """(hi min, hi max, entry format) of the entries in ent_a for exactly these rows and key,
+        or None.  One-shot: sorting reuses ent_a as scratch, so the claim is dropped either way."""
         kr, self.keys_ready = self.keys_ready, None
         if kr is None or rows is None:
             return None
-        ptr_, n, off, ln, rng = kr
+        ptr_, n, off, ln, rng, fmt = kr
         if ptr_ != rows.data_ptr() or n != rows.shape[0] or off != key_off or ln != key_len:
             return None
         mn, mx = (int(x) & ((1 << 64) - 1) for x in rng.cpu().tolist())
-        return mn, mx
+        return mn, mx, fmt
 
     @property
     def capacity(self):

@@ -86,16 +86,29 @@ class SortStats:
 
 def local_sort_rows(rows: torch.Tensor, out: torch.Tensor, ent_a: torch.Tensor, ent_b: torch.Tensor,
                     key_off: int, key_len: int, descending: bool = False,
-                    hi_bounds: tuple[int, int] | None = None, keys_ready: bool = False) -> torch.Tensor:
+                    hi_bounds: tuple[int, int] | None = None, keys_ready: bool = False,
+                    keys_fmt: str = "e128", stats: dict | None = None) -> torch.Tensor:
     """Sort fixed-width ``rows`` by their byte-string key into ``out`` (stable).
 
+    Ascending sorts take the compact path (8-byte entries + run fix-up in the row gather,
+    ops/sort.sort_rows_compact); descending sorts, and keys so duplicated that a run of equal
+    32-bit windows outgrows the gather's LDS window, take the 16-byte-entry hybrid sort.
     ``hi_bounds`` = known (min, max) of the first 8 key bytes as a big-endian integer (e.g. this
-    rank's range-partition bounds); lets the hybrid sort skip their common prefix without a pass.
-    ``keys_ready``: ``ent_a[:n]`` already holds ``extract_keys(rows, key_off, key_len)`` (the
-    producer emitted them, e.g. the fused TeraSort generator)."""
+    rank's range-partition bounds); lets the sort skip their common prefix without a pass.
+    ``keys_ready``: ``ent_a`` already holds the entries of ``rows`` in ``keys_fmt`` ("e64": the
+    compact entries for prefix 0, "e128": ``extract_keys(rows, key_off, key_len)``), emitted by
+    the producer (the fused TeraSort generator)."""
     n = rows.shape[0]
     if n == 0:
         return out[:0]
+    if not descending and S.compact_sort_ok(rows, key_len):
+        r = S.sort_rows_compact(rows, out, ent_a.view(-1), ent_b.view(-1), key_off, key_len, hi_bounds=hi_bounds,
+                                keys_ready=keys_ready and keys_fmt == "e64", stats=stats)
+        if r is not None:
+            return r
+        keys_ready = False          # the compact attempt reused ent_a
+    if keys_fmt != "e128":
+        keys_ready = False
     e = ent_a[:n] if keys_ready else S.extract_keys(rows, key_off, key_len, 0, out=ent_a[:n])
     if descending:
         # invert the key bits (not the row index) so an ascending radix sort yields descending keys
@@ -182,7 +195,8 @@ def _sort_keys(rows: torch.Tensor, ent: torch.Tensor, tmp: torch.Tensor, key_off
 def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int, world: World | None = None,
                           sample_target: int = 1 << 20, seed: int = 314159,
                           stats: SortStats | None = None, keys_ready: bool = False,
-                          hi_bounds: tuple[int, int] | None = None, split_ties: bool = True) -> torch.Tensor:
+                          hi_bounds: tuple[int, int] | None = None, split_ties: bool = True,
+                          keys_fmt: str = "e128") -> torch.Tensor:
     """Globally sort the first ``n`` rows of ``bufs.rows_in`` across all ranks.
 
     On return rank r holds, in ``bufs.rows_out[:n_r]``, the r-th key range in ascending order.
@@ -205,11 +219,13 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     rows = bufs.rows_in[:n]
     if w.size == 1:
         out = local_sort_rows(rows, bufs.rows_out, bufs.ent_a, bufs.ent_b, key_off, key_len,
-                              hi_bounds=hi_bounds, keys_ready=keys_ready)
+                              hi_bounds=hi_bounds, keys_ready=keys_ready, keys_fmt=keys_fmt)
         if stats is not None:
             stats.n_in = stats.n_out = n
         return out
     W, stride = w.size, rows.shape[1]
+    if keys_fmt != "e128":
+        keys_ready = False
     ent = bufs.ent_a[:n] if keys_ready else S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
     _, _, lo_mask = key_bits(key_len)
     part_mask = lo_mask
@@ -242,23 +258,46 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
         recv_flat[off[b] * stride: off[b + 1] * stride], [rc[s][b] * stride for s in range(W)], w)
         for b in range(B)]
     out = bufs.rows_out
-    pending = []
+    pending, fixups = [], []
+    e64a, e64b = bufs.ent_a.view(-1), bufs.ent_b.view(-1)
+    compact = S.compact_sort_ok(bufs.rows_in[:2], key_len)
     for b in range(B):
         shuffle.wait(handles[b])
         a, z = off[b], off[b + 1]
         if z > a:
-            srt = _sort_keys(bufs.rows_in[a:z], bufs.ent_a[a:z], bufs.ent_b[a:z], key_off, key_len,
-                             _range_hi_bounds(seps_hi, w.rank * B + b))
-            pending.append((a, z, srt))
+            hb = _range_hi_bounds(seps_hi, w.rank * B + b)
+            if compact and z - a >= 2:
+                # compact sort of this key range; its gather (with the run fix-up) is deferred
+                # like the full-key path's
+                r = bufs.rows_in[a:z]
+                P = min(S.common_prefix_bits(*hb), 8 * key_len)
+                e = S.extract_keys64(r, key_off, key_len, P, e64a[a:z])
+                win = min(S.window_bits64(z - a), max(8, ((8 * key_len - P + 7) // 8) * 8), 32)
+                pending.append((a, z, ("e64", S.sort_entries64(e, e64b[a:z], win), win)))
+            else:
+                srt = _sort_keys(bufs.rows_in[a:z], bufs.ent_a[a:z], bufs.ent_b[a:z], key_off, key_len, hb)
+                pending.append((a, z, ("e128", srt, 0)))
         # rows_out[:sent] has been sent (rounds <= b are complete); rows_out[n:] never held data
         sent = st[(b + 1) * W]
         keep = []
-        for a2, z2, s2 in pending:
+        for a2, z2, (fmt, s2, win) in pending:
             if b == B - 1 or z2 <= sent or a2 >= n:
-                S.gather_rows(bufs.rows_in[a2:z2], entries=s2, out=out[a2:z2])
+                if fmt == "e64":
+                    flag = torch.zeros(1, dtype=torch.int32, device=out.device)
+                    S.gather_fixup(bufs.rows_in[a2:z2], s2, out[a2:z2], key_off, key_len, win, flag)
+                    fixups.append((a2, z2, flag))
+                else:
+                    S.gather_rows(bufs.rows_in[a2:z2], entries=s2, out=out[a2:z2])
             else:
-                keep.append((a2, z2, s2))
+                keep.append((a2, z2, (fmt, s2, win)))
         pending = keep
+    if fixups:
+        flags = torch.cat([f for _, _, f in fixups]).tolist()
+        for (a2, z2, _), bad in zip(fixups, flags):
+            if bad:     # a run of equal windows too long for the fix-up: full-key sort of the range
+                srt = _sort_keys(bufs.rows_in[a2:z2], bufs.ent_a[a2:z2], bufs.ent_b[a2:z2], key_off, key_len,
+                                 None)
+                S.gather_rows(bufs.rows_in[a2:z2], entries=srt, out=out[a2:z2])
     if stats is not None:
         stats.n_in, stats.n_out, stats.rounds = n, n_recv, B
         stats.send_counts = [sum(send[b][r] for b in range(B)) for r in range(W)]

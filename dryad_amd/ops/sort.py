@@ -254,3 +254,105 @@ def entries_to_key_int(entries: torch.Tensor, lo_keep_bits: int = 64):
     for lo, hi in e.tolist():
         out.append(((hi & (2**64 - 1)) << 64) | ((lo & (2**64 - 1)) & mask))
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Compact row sort: 8-byte (32-bit key window, 32-bit row) entries + run fix-up in the row gather
+# (csrc/kernels/sort.hip dr_extract_keys64 / dr_sort_u64 / dr_gather_fixup).
+_lib.register_signatures({
+    "dr_extract_keys64": (ctypes.c_int, [ctypes.c_void_p, c_u64, c_u32, c_u32, c_u32, c_u32, c_u32, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
+    "dr_sort_u64": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u64, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
+    "dr_gather_fixup": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_u64, c_u32, c_u32, c_u32,
+                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+})
+# expected entries per run the compact sort sizes its window for (window = smallest multiple of 8
+# bits, at most 32, with n <= RUN_TARGET64 * 2^window)
+RUN_TARGET64 = float(_os.environ.get("DRYAD_SORT64_RUN_TARGET", "1"))
+COMPACT_SORT = _os.environ.get("DRYAD_COMPACT_SORT", "1") == "1"
+
+
+def common_prefix_bits(mn: int, mx: int) -> int:
+    """Leading bits shared by every 64-bit value in [mn, mx]."""
+    return 64 - ((mn ^ mx) & _M64).bit_length()
+
+
+def extract_keys64(rows: torch.Tensor, key_off: int, key_len: int, prefix_bits: int,
+                   out: torch.Tensor) -> torch.Tensor:
+    """E64 entries (int64 [n]): key bits [prefix_bits, prefix_bits + 32) << 32 | row index."""
+    _lib.require_gpu_tensor(rows, "extract_keys64")
+    n, stride = rows.shape
+    _lib.call("dr_extract_keys64", ptr(rows), c_u64(n), c_u32(stride), c_u32(key_off), c_u32(key_len),
+              c_u32(prefix_bits), c_u32(0), ptr(out), stream_of(rows))
+    return out[:n]
+
+
+def window_bits64(n: int) -> int:
+    win = 8
+    while win < 32 and n > RUN_TARGET64 * (1 << win):
+        win += 8
+    return win
+
+
+def sort_entries64(e: torch.Tensor, tmp: torch.Tensor, win: int) -> torch.Tensor:
+    """Stable LSD sort of E64 entries on their top ``win`` window bits."""
+    n = e.shape[0]
+    ws = _workspace(n, e.device)
+    flag = ctypes.c_int(0)
+    _lib.call("dr_sort_u64", ptr(e), ptr(tmp), c_u64(n), 64 - win, 64, ptr(ws), stream_of(e), ctypes.byref(flag))
+    return tmp[:n] if flag.value else e
+
+
+def gather_fixup(rows: torch.Tensor, srt: torch.Tensor, out: torch.Tensor, key_off: int, key_len: int,
+                 win: int, flag: torch.Tensor):
+    n, stride = rows.shape
+    _lib.call("dr_gather_fixup", ptr(rows), ptr(out), ptr(srt), c_u64(n), c_u32(stride), c_u32(key_off),
+              c_u32(key_len), 64 - win, ptr(flag), stream_of(rows))
+
+
+def compact_sort_ok(rows: torch.Tensor, key_len: int) -> bool:
+    n, stride = rows.shape
+    return COMPACT_SORT and 2 <= n < (1 << 32) and stride % 4 == 0 and 1 <= key_len <= 16
+
+
+def sort_rows_compact(rows: torch.Tensor, out: torch.Tensor, ent: torch.Tensor, tmp: torch.Tensor,
+                      key_off: int, key_len: int, hi_bounds: tuple[int, int] | None = None,
+                      keys_ready: bool = False, stats: dict | None = None):
+    """Stable sort of fixed-width ``rows`` by the byte-string key into ``out[:n]`` through 8-byte
+    entries.  ``ent``/``tmp``: int64 scratch of >= n elements each.  ``hi_bounds``: (min, max) of
+    the first 8 key bytes (big-endian) of all rows, used to skip their common prefix; with
+    ``keys_ready`` ``ent[:n]`` already holds the entries for prefix 0 (fused generator).
+    Returns ``out[:n]``, or None when a run of equal windows is too long for the gather's fix-up
+    (heavily duplicated keys): the caller then sorts on full keys."""
+    n = rows.shape[0]
+    if hi_bounds is None:
+        e = extract_keys64(rows, key_off, key_len, 0, ent)
+        hi_bounds = _hi_range64(e)
+        P = common_prefix_bits(hi_bounds[0] & ~0xFFFFFFFF, hi_bounds[1] | 0xFFFFFFFF)
+        if P:
+            e = extract_keys64(rows, key_off, key_len, P, ent)
+    else:
+        P = min(common_prefix_bits(*hi_bounds), 8 * key_len)
+        if keys_ready and P == 0:
+            e = ent[:n]
+        else:
+            e = extract_keys64(rows, key_off, key_len, P, ent)
+    win = min(window_bits64(n), max(8, ((8 * key_len - P + 7) // 8) * 8), 32)
+    srt = sort_entries64(e, tmp, win)
+    flag = torch.zeros(1, dtype=torch.int32, device=rows.device)
+    gather_fixup(rows, srt, out, key_off, key_len, win, flag)
+    if stats is not None:
+        stats["path"] = f"compact win={win} prefix={P}"
+    if int(flag.item()) != 0:
+        if stats is not None:
+            stats["path"] += " overflow"
+        return None
+    return out[:n]
+
+
+def _hi_range64(e: torch.Tensor) -> tuple[int, int]:
+    """(min, max) of the E64 window words, as hi-word bounds (window bits in the top 32)."""
+    w = (e >> 32) & 0xFFFFFFFF                 # unsigned window (>> is arithmetic on int64)
+    mn, mx = int(w.min().item()), int(w.max().item())
+    return mn << 32, mx << 32

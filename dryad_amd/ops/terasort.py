@@ -34,6 +34,18 @@ def generate_with_keys(out: torch.Tensor, first_index: int, seed: int, keys: tor
     return out
 
 
+def generate_with_keys64(out: torch.Tensor, first_index: int, seed: int, keys: torch.Tensor,
+                         hi_range: torch.Tensor | None = None) -> torch.Tensor:
+    """``generate`` fused with the 8-byte entries of the compact row sort (key bytes 0..3 << 32 |
+    row index, ``keys`` int64 [>= n]) and the min/max of the key's first 8 bytes."""
+    _lib.require_gpu_tensor(out, "terasort.generate_with_keys64")
+    n = out.shape[0]
+    assert keys.numel() >= n and keys.dtype == torch.int64 and keys.is_contiguous()
+    _lib.call("dr_terasort_gen_keys64", ptr(out), c_u64(n), c_u64(first_index), c_u64(seed & (2**64 - 1)),
+              ptr(keys), c_u32(0), ptr(hi_range), stream_of(out))
+    return out
+
+
 def check(rows: torch.Tensor, acc: torch.Tensor | None = None) -> torch.Tensor:
     """Accumulate [sum of record hashes mod 2^64, #adjacent order violations] into ``acc``."""
     _lib.require_gpu_tensor(rows, "terasort.check")

@@ -168,10 +168,11 @@ class GpuJobRunner:
         bs = self.row_sets[(f["x"], me)]
         off, ln = f["spec"]
         stats = RS.SortStats()
-        bounds = bs.take_keys(t.rows, off, ln)
+        kr = bs.take_keys(t.rows, off, ln)
         out = RS.distributed_sort_rows(bs.bufs, t.n, off, ln, self.world, stats=stats,
-                                       keys_ready=bounds is not None, hi_bounds=bounds,
-                                       split_ties=not f.get("keep_ties", False))
+                                       keys_ready=kr is not None, hi_bounds=None if kr is None else kr[:2],
+                                       split_ties=not f.get("keep_ties", False),
+                                       keys_fmt="e128" if kr is None else kr[2])
         self.row_sets[(m.id, me)] = bs
         self.last_sort_stats = stats
         table = DeviceTable(out.shape[0], t.shape, rows=out)

@@ -1,0 +1,83 @@
+"""Compact row sort (8-byte window entries + run fix-up inside the row gather,
+csrc/kernels/sort.hip dr_extract_keys64 / dr_sort_u64 / dr_gather_fixup) against a numpy
+stable lexicographic sort of the key bytes."""
+import numpy as np
+import pytest
+import torch
+
+from dryad_amd.ops import recordsort as RS
+from dryad_amd.ops import sort as S
+from dryad_amd.ops import terasort as TS
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _ref_order(rows: np.ndarray, off: int, ln: int) -> np.ndarray:
+    k = rows[:, off:off + ln]
+    return np.lexsort(tuple(k[:, j] for j in reversed(range(ln))))
+
+
+def _sort(rows_t, off, ln, hi_bounds=None, keys_ready=False, ent=None):
+    n, stride = rows_t.shape
+    out = torch.empty_like(rows_t)
+    ent = ent if ent is not None else torch.empty(n, dtype=torch.int64, device=DEV)
+    tmp = torch.empty(n, dtype=torch.int64, device=DEV)
+    st = {}
+    r = S.sort_rows_compact(rows_t, out, ent, tmp, off, ln, hi_bounds=hi_bounds, keys_ready=keys_ready, stats=st)
+    return r, st
+
+
+@pytest.mark.parametrize("n,stride,off,ln", [(1000, 16, 0, 8), (200_003, 100, 0, 10), (70_000, 32, 4, 12),
+                                             (50_000, 20, 2, 3), (100_000, 24, 5, 16), (3, 8, 0, 1)])
+def test_random_keys(n, stride, off, ln):
+    g = torch.Generator().manual_seed(n)
+    rows = torch.randint(0, 256, (n, stride), dtype=torch.uint8, generator=g)
+    r, st = _sort(rows.to(DEV), off, ln)
+    assert r is not None, st
+    ref = rows.numpy()[_ref_order(rows.numpy(), off, ln)]
+    assert np.array_equal(r.cpu().numpy(), ref), st
+
+
+def test_shared_prefix_and_duplicates():
+    n = 300_000
+    g = torch.Generator().manual_seed(7)
+    rows = torch.randint(0, 256, (n, 16), dtype=torch.uint8, generator=g)
+    rows[:, :5] = 0x5A                                  # 40 shared leading key bits
+    rows[:, 8] = rows[:, 8] % 4                         # a few duplicates of the whole key
+    rows[:, 9:12] = 0
+    r, st = _sort(rows.to(DEV), 0, 12)
+    assert r is not None, st
+    assert "prefix=" in st["path"]
+    ref = rows.numpy()[_ref_order(rows.numpy(), 0, 12)]
+    assert np.array_equal(r.cpu().numpy(), ref), st
+
+
+def test_long_runs_overflow_then_full_key_fallback():
+    n = 100_000
+    rows = torch.zeros((n, 16), dtype=torch.uint8)
+    rows[:, 8:] = torch.randint(0, 256, (n, 8), dtype=torch.uint8)     # key 0..7 all equal: one run
+    r, st = _sort(rows.to(DEV), 0, 8)
+    assert r is None and "overflow" in st["path"]
+    # local_sort_rows falls back to the 16-byte hybrid sort and stays stable
+    ent_a = torch.empty((n, 2), dtype=torch.int64, device=DEV)
+    ent_b = torch.empty_like(ent_a)
+    out = torch.empty((n, 16), dtype=torch.uint8, device=DEV)
+    got = RS.local_sort_rows(rows.to(DEV), out, ent_a, ent_b, 0, 8)
+    assert torch.equal(got.cpu(), rows)
+
+
+def test_generator_fused_e64_keys():
+    n = 1 << 20
+    rows = torch.empty((n, 100), dtype=torch.uint8, device=DEV)
+    ent = torch.empty(n, dtype=torch.int64, device=DEV)
+    rng = torch.tensor([-1, 0], dtype=torch.int64, device=DEV)
+    TS.generate_with_keys64(rows, 0, 42, ent, rng)
+    ref_e = S.extract_keys64(rows, 0, 10, 0, torch.empty(n, dtype=torch.int64, device=DEV))
+    assert torch.equal(ent, ref_e)
+    mn, mx = (int(x) & ((1 << 64) - 1) for x in rng.cpu().tolist())
+    acc_in = TS.check(rows).clone()
+    r, st = _sort(rows, 0, 10, hi_bounds=(mn, mx), keys_ready=True, ent=ent)
+    assert r is not None, st
+    acc = TS.check(r)
+    assert int(acc[1]) == 0 and int(acc[0]) == int(acc_in[0])
