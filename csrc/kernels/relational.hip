@@ -503,6 +503,26 @@ DR_API int dr_build_keys(const void* const* cols, const int* types, const int* d
   return 0;
 }
 
+namespace {
+// E64 entries of a narrow integer key: ((norm(key) - bias) << 32) | (idx_base + i); the caller
+// guarantees norm(key) - bias < 2^32 for every row (bias = norm(min key)).
+__global__ __launch_bounds__(256) void build_keys64_kernel(const void* __restrict__ col, int type, uint64_t n,
+                                                           uint64_t bias, uint32_t idx_base, uint64_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = ((norm_key(col, i, type) - bias) << 32) | (uint32_t)(idx_base + (uint32_t)i);
+}
+}  // namespace
+
+DR_API int dr_build_keys64(const void* col, int type, uint64_t n, uint64_t bias, uint32_t idx_base, uint64_t* out,
+                           hipStream_t s) {
+  if (type < K_U8 || type > K_U64) return (int)hipErrorInvalidValue;   // integer keys only
+  if (n == 0) return 0;
+  if (n + idx_base > (1ull << 32)) return (int)hipErrorInvalidValue;
+  build_keys64_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(col, type, n, bias, idx_base, out);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
 DR_API int dr_hash_dest(E128* e, uint64_t n, uint64_t lo_mask, uint32_t nparts, hipStream_t s) {
   if (nparts == 0 || nparts > 256) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;

@@ -181,11 +181,13 @@ __global__ __launch_bounds__(256) void rs_scatter(const E128* __restrict__ in, E
 // v2: all of a tile's loads are issued back to back and the NEXT tile is prefetched into
 // registers while the current one is ranked and staged (software pipelining across tiles), so a
 // workgroup's global-load latency overlaps its LDS ranking / scatter work.
-template <typename T, int ITEMS>
+// EXPAND (T = E64 only): the pass writes 16-byte E128 entries {lo = row index, hi = window +
+// bias} instead, so a compact sort of narrow integer keys hands consumers the usual E128 layout.
+template <typename T, int ITEMS, bool EXPAND = false>
 __global__ __launch_bounds__(256) void rs_scatter_v2(const T* __restrict__ in, T* __restrict__ out,
                                                      uint64_t n, int shift,
                                                      const uint32_t* __restrict__ offsets, uint32_t G,
-                                                     uint64_t per_block) {
+                                                     uint64_t per_block, uint64_t bias = 0) {
   constexpr int kTile = kBlock * ITEMS;
   __shared__ T stage[kTile];
   __shared__ uint32_t wcnt[4][kBins];
@@ -249,7 +251,15 @@ __global__ __launch_bounds__(256) void rs_scatter_v2(const T* __restrict__ in, T
     for (uint32_t j = t; j < cnt; j += kBlock) {
       const T v = stage[j];
       const uint32_t d = digit_of(v, shift);
-      out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+      if constexpr (EXPAND) {
+        const uint64_t w = reinterpret_cast<const uint64_t&>(v);
+        E128 x;
+        x.lo = (uint32_t)w;
+        x.hi = (w >> 32) + bias;
+        reinterpret_cast<E128*>(out)[(uint64_t)goff[d] + (j - bstart[d])] = x;
+      } else {
+        out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+      }
     }
     __syncthreads();
     goff[t] += tot;
@@ -1230,6 +1240,11 @@ DR_API int dr_extract_keys64(const uint8_t* rows, uint64_t n, uint32_t stride, u
   return 0;
 }
 
+namespace {
+int g_items64 = -1;   // entries per thread per tile of the E64 scatter (8 / 16 / 32)
+}
+DR_API void dr_sort64_set_items(int items) { g_items64 = (items == 8 || items == 32) ? items : 16; }
+
 // Stable LSD radix sort of E64 entries on bits [begin_bit, end_bit) (multiples of 8, < 64 = the
 // window); 16 entries per thread per tile (128 contiguous output bytes per digit run).
 DR_API int dr_sort_u64(E64* keys, E64* tmp, uint64_t n, int begin_bit, int end_bit, void* ws, hipStream_t s,
@@ -1238,7 +1253,12 @@ DR_API int dr_sort_u64(E64* keys, E64* tmp, uint64_t n, int begin_bit, int end_b
   if (n == 0 || begin_bit >= end_bit) return 0;
   if (end_bit > 64 || begin_bit < 0 || (begin_bit & 7) || (end_bit & 7)) return (int)hipErrorInvalidValue;
   if (n >= (1ull << 32)) return (int)hipErrorInvalidValue;
-  constexpr int ITEMS = 16;
+  if (g_items64 < 0) {
+    const char* ev = getenv("DRYAD_SORT64_ITEMS");
+    g_items64 = ev ? atoi(ev) : 16;
+    if (g_items64 != 8 && g_items64 != 16 && g_items64 != 32) g_items64 = 16;
+  }
+  const int ITEMS = g_items64;
   const uint64_t tile = (uint64_t)kBlock * ITEMS;
   uint64_t tiles = (n + tile - 1) / tile;
   if (tiles < 1) tiles = 1;
@@ -1252,12 +1272,52 @@ DR_API int dr_sort_u64(E64* keys, E64* tmp, uint64_t n, int begin_bit, int end_b
   for (int shift = begin_bit; shift < end_bit; shift += kRadixBits) {
     rs_count<<<G, 256, 0, s>>>(src, n, shift, counts, G, per_block);
     scan_inplace(counts, kBins * G, partial, s);
-    rs_scatter_v2<E64, ITEMS><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+    if (ITEMS == 32)
+      rs_scatter_v2<E64, 32><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+    else if (ITEMS == 8)
+      rs_scatter_v2<E64, 8><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+    else
+      rs_scatter_v2<E64, 16><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
     E64* x = src; src = dst; dst = x;
     flips ^= 1;
   }
   DR_LAUNCH_CHECK();
   *result_in_tmp = flips;
+  return 0;
+}
+
+// Stable LSD sort of E64 entries on bits [begin_bit, end_bit) whose LAST pass writes E128 entries
+// {lo = row index, hi = (entry >> 32) + bias} to `out` (n x 16 bytes, not aliasing keys/tmp): the
+// sort of a narrow integer key (span < 2^32; entries = (norm key - norm min) << 32 | row) at half
+// the traffic of the 16-byte sort, handing the E128 layout to segment / join consumers.
+DR_API int dr_sort_u64_expand(E64* keys, E64* tmp, E128* out, uint64_t n, int begin_bit, int end_bit, uint64_t bias,
+                              void* ws, hipStream_t s) {
+  if (n == 0) return 0;
+  if (end_bit > 64 || begin_bit < 32 || (begin_bit & 7) || (end_bit & 7) || begin_bit >= end_bit)
+    return (int)hipErrorInvalidValue;
+  if (n >= (1ull << 32)) return (int)hipErrorInvalidValue;
+  constexpr int ITEMS = 16;
+  const uint64_t tile = (uint64_t)kBlock * ITEMS;
+  uint64_t tiles = (n + tile - 1) / tile;
+  if (tiles < 1) tiles = 1;
+  const uint32_t G = (uint32_t)(tiles < (uint64_t)kMaxGrid ? tiles : (uint64_t)kMaxGrid);
+  const uint64_t per_block = ((tiles + G - 1) / G) * tile;
+  uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* partial = counts + (uint64_t)kBins * G;
+  E64* src = keys;
+  E64* dst = tmp;
+  for (int shift = begin_bit; shift < end_bit; shift += kRadixBits) {
+    rs_count<<<G, 256, 0, s>>>(src, n, shift, counts, G, per_block);
+    scan_inplace(counts, kBins * G, partial, s);
+    if (shift + kRadixBits >= end_bit) {
+      rs_scatter_v2<E64, ITEMS, true><<<G, 256, 0, s>>>(src, reinterpret_cast<E64*>(out), n, shift, counts, G,
+                                                        per_block, bias);
+    } else {
+      rs_scatter_v2<E64, ITEMS><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+      E64* x = src; src = dst; dst = x;
+    }
+  }
+  DR_LAUNCH_CHECK();
   return 0;
 }
 

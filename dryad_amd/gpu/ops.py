@@ -528,12 +528,16 @@ def _group_keys(kcols, skeys):
         raise NotTraceable("group key of a non-key dtype")
     _row_index_fits(kcols[0].shape[0] if kcols else 0)
     packed = None
-    if _wide(kcols):
+    srt = R.int_key_sort(kcols[0]) if len(kcols) == 1 else None
+    if srt is not None:
+        lo_mask = 0                     # narrow integer key: compact sort, E128 {row, norm key}
+    elif _wide(kcols):
         fp, packed = _wide_key(kcols)
         e, b0, lo_mask = R.build_keys([fp])
     else:
         e, b0, lo_mask = R.build_keys(kcols)
-    srt = S.sort_entries_hybrid(e, b0)
+    if srt is None:
+        srt = S.sort_entries_hybrid(e, b0)
     seg, nseg, starts = R.segment_ids(srt, lo_mask)
     # group representatives straight from the sorted entries (nseg reads); the full row
     # permutation is only materialised when fingerprinted keys must be verified

@@ -500,3 +500,52 @@ def stable_hash_dest(keys: list, n: int, nparts: int, tuple_form: bool, device,
               c_u64(n), c_u32(nparts), ptr(ent) if ent is not None else None,
               ptr(hs) if hs is not None else None, stream_of(keys[0].t))
     return ent, hs
+
+
+# ---------------------------------------------------------------------------------------------
+# Narrow integer keys: compact 8-byte sort whose last pass expands to E128
+_lib.register_signatures({
+    "dr_build_keys64": (c_i32, [vp, c_i32, c_u64, c_u64, c_u32, vp, vp]),
+    "dr_sort_u64_expand": (c_i32, [vp, vp, vp, c_u64, c_i32, c_i32, c_u64, vp, vp]),
+})
+_INT_BITS = {torch.uint8: 8, torch.int8: 8, torch.bool: 8, torch.int16: 16, torch.uint16: 16, torch.int32: 32,
+             torch.uint32: 32, torch.int64: 64, torch.uint64: 64}
+_SIGNED = {torch.int8, torch.int16, torch.int32, torch.int64}
+INT_KEY_SORT = os.environ.get("DRYAD_INT_KEY_SORT", "1") == "1"
+
+
+def _norm_int(v: int, dtype) -> int:
+    """Order-preserving unsigned image of an integer key (relational.hip norm_key)."""
+    b = _INT_BITS[dtype]
+    v &= (1 << b) - 1
+    return v ^ (1 << (b - 1)) if dtype in _SIGNED else v
+
+
+def int_key_sort(col: torch.Tensor):
+    """Stable sort of one integer key column whose value span is below 2^32, through 8-byte
+    entries ((key - min) << 32 | row; half the bytes per radix pass of the 16-byte sort).  Returns
+    E128 entries {lo = row, hi = normalised key} (segment_ids / seg_reduce layout, lo_mask 0), or
+    None when the column does not qualify."""
+    from . import reduce as RD
+    from . import sort as S
+    n = col.shape[0]
+    if not INT_KEY_SORT or col.dtype not in _INT_BITS or col.dim() != 1 or n < 2 or n >= (1 << 32):
+        return None
+    col = col.contiguous()
+    c = col.to(torch.int64) if col.dtype in (torch.bool, torch.uint16, torch.uint32) else col
+    mn, mx = RD.reduce_multi(n, [(RD.MIN, c, None), (RD.MAX, c, None)], col.device)
+    span = int(mx) - int(mn)
+    if span >= (1 << 32):
+        return None
+    passes = max(1, (span.bit_length() + 7) // 8)
+    bias = _norm_int(int(mn), col.dtype)
+    dev = col.device
+    e = torch.empty(n, dtype=torch.int64, device=dev)
+    tmp = torch.empty(n, dtype=torch.int64, device=dev)
+    out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    _lib.call("dr_build_keys64", ptr(col), KEY_TYPES[col.dtype], c_u64(n), c_u64(bias), c_u32(0), ptr(e),
+              stream_of(col))
+    ws = S._workspace(n, dev)
+    _lib.call("dr_sort_u64_expand", ptr(e), ptr(tmp), ptr(out), c_u64(n), 32, 32 + 8 * passes, c_u64(bias), ptr(ws),
+              stream_of(col))
+    return out

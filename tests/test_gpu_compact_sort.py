@@ -81,3 +81,25 @@ def test_generator_fused_e64_keys():
     assert r is not None, st
     acc = TS.check(r)
     assert int(acc[1]) == 0 and int(acc[0]) == int(acc_in[0])
+
+
+@pytest.mark.parametrize("dtype,lo,hi", [(torch.int64, -(1 << 40), -(1 << 40) + (1 << 30)), (torch.int32, -5, 300),
+                                         (torch.int64, 7, 8), (torch.int16, -30000, 30000),
+                                         (torch.uint8, 0, 256), (torch.int64, 0, 1 << 31)])
+def test_int_key_sort_matches_stable_argsort(dtype, lo, hi):
+    from dryad_amd.ops import relational as R
+    n = 500_000
+    col = torch.randint(lo, hi, (n,), dtype=torch.int64).to(dtype).to(DEV)
+    srt = R.int_key_sort(col)
+    assert srt is not None
+    perm = (srt[:, 0] & 0xFFFFFFFF).cpu()
+    ref = torch.sort(col.cpu().to(torch.int64), stable=True).indices
+    assert torch.equal(perm, ref)
+    if dtype == torch.int64:
+        assert torch.equal(srt[:, 1].cpu() ^ (-(1 << 63)), col.cpu()[ref])
+
+
+def test_int_key_sort_declines_wide_spans():
+    from dryad_amd.ops import relational as R
+    col = torch.tensor([0, 1 << 40, 5], dtype=torch.int64, device=DEV)
+    assert R.int_key_sort(col) is None
