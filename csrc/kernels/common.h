@@ -116,6 +116,14 @@ __device__ __host__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// x mod d for any 64-bit x, given m = ~0ull / d (host-precomputed): q = mulhi(x, m) undershoots
+// the true quotient by at most one, so a single correction makes the result exact.
+__device__ __forceinline__ uint64_t fast_mod64(uint64_t x, uint64_t d, uint64_t m) {
+  const uint64_t q = __umul64hi(x, m);
+  const uint64_t r = x - q * d;
+  return r >= d ? r - d : r;
+}
+
 // Grid sizing for streaming kernels: enough workgroups to fill 256 CUs several times over.
 static inline unsigned grid_for(uint64_t work_items, unsigned per_block, unsigned cap = 8192) {
   uint64_t g = (work_items + per_block - 1) / per_block;

@@ -18,36 +18,45 @@ constexpr uint64_t kG = 0x9E3779B97F4A7C15ull;
 constexpr uint64_t kH = 0xD1B54A32D192ED03ull;
 
 __global__ __launch_bounds__(256) void gen_records64_kernel(int64_t* const* __restrict__ cols, int ncols, uint64_t n,
-                                                            uint64_t first, uint64_t nkeys, uint64_t seed,
-                                                            uint64_t dim_mult) {
+                                                            uint64_t first, uint64_t nkeys, uint64_t mkeys,
+                                                            uint64_t seed, uint64_t dim_mult, bool wide) {
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t i = first + r;
     if (dim_mult) {
-      const uint64_t key = (uint64_t)(((unsigned __int128)i * dim_mult + seed) % nkeys);
+      const uint64_t key = wide ? (uint64_t)(((unsigned __int128)i * dim_mult + seed) % nkeys)
+                                : fast_mod64(i * dim_mult + seed, nkeys, mkeys);
       cols[0][r] = (int64_t)key;
       for (int j = 1; j < ncols; ++j) cols[j][r] = (int64_t)(mix64((seed + (uint64_t)j * kH) ^ key) >> 33);
     } else {
-      cols[0][r] = (int64_t)(mix64(seed ^ (i * kG)) % nkeys);
+      cols[0][r] = (int64_t)fast_mod64(mix64(seed ^ (i * kG)), nkeys, mkeys);
       for (int j = 1; j < ncols; ++j) cols[j][r] = (int64_t)(mix64((seed + (uint64_t)j * kH) ^ i) >> 33);
     }
   }
 }
 
-// Row-major twin: out[r * ncols + j] (a 64-byte row store when ncols = 8).
-__global__ __launch_bounds__(256) void gen_records64_rows_kernel(int64_t* __restrict__ out, int ncols, uint64_t n,
-                                                                 uint64_t first, uint64_t nkeys, uint64_t seed,
-                                                                 uint64_t dim_mult) {
-  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+// Row-major twin: out[r * ncols + j] (a 64-byte row store when ncols = 8).  One lane per field,
+// so a wave writes 8 consecutive 64-byte rows with coalesced 8-byte stores; the key modulo is a
+// multiply-high reduction (fast_mod64) instead of a 64- or 128-bit software division.  WIDE: the
+// dimension-table product i * dim_mult + seed may pass 2^64 (then 128-bit arithmetic is needed).
+template <int NC, bool WIDE>
+__global__ __launch_bounds__(256) void gen_records64_rows_kernel(int64_t* __restrict__ out, uint64_t n,
+                                                                 uint64_t first, uint64_t nkeys, uint64_t mkeys,
+                                                                 uint64_t seed, uint64_t dim_mult) {
+  const uint64_t total = n * NC;
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = e / NC;
+    const int j = (int)(e - r * NC);
     const uint64_t i = first + r;
-    int64_t* o = out + r * ncols;
+    uint64_t v;
     if (dim_mult) {
-      const uint64_t key = (uint64_t)(((unsigned __int128)i * dim_mult + seed) % nkeys);
-      o[0] = (int64_t)key;
-      for (int j = 1; j < ncols; ++j) o[j] = (int64_t)(mix64((seed + (uint64_t)j * kH) ^ key) >> 33);
+      uint64_t key;
+      if (WIDE) key = (uint64_t)(((unsigned __int128)i * dim_mult + seed) % nkeys);
+      else key = fast_mod64(i * dim_mult + seed, nkeys, mkeys);
+      v = j == 0 ? key : (mix64((seed + (uint64_t)j * kH) ^ key) >> 33);
     } else {
-      o[0] = (int64_t)(mix64(seed ^ (i * kG)) % nkeys);
-      for (int j = 1; j < ncols; ++j) o[j] = (int64_t)(mix64((seed + (uint64_t)j * kH) ^ i) >> 33);
+      v = j == 0 ? fast_mod64(mix64(seed ^ (i * kG)), nkeys, mkeys) : (mix64((seed + (uint64_t)j * kH) ^ i) >> 33);
     }
+    out[e] = (int64_t)v;
   }
 }
 }  // namespace
@@ -58,7 +67,9 @@ DR_API int dr_gen_records64(int64_t* const* cols, int ncols, uint64_t n, uint64_
                             uint64_t seed, uint64_t dim_mult, hipStream_t s) {
   if (ncols < 1 || ncols > 8 || nkeys == 0) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
-  gen_records64_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(cols, ncols, n, first, nkeys, seed, dim_mult);
+  const unsigned __int128 top = (unsigned __int128)(first + n) * dim_mult + seed;
+  gen_records64_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(cols, ncols, n, first, nkeys, ~0ull / nkeys, seed,
+                                                               dim_mult, dim_mult && (top >> 64) != 0);
   DR_LAUNCH_CHECK();
   return 0;
 }
@@ -67,7 +78,27 @@ DR_API int dr_gen_records64_rows(int64_t* out, int ncols, uint64_t n, uint64_t f
                                  uint64_t dim_mult, hipStream_t s) {
   if (ncols < 1 || ncols > 8 || nkeys == 0) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
-  gen_records64_rows_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(out, ncols, n, first, nkeys, seed, dim_mult);
+  const uint64_t m = ~0ull / nkeys;
+  // the dimension-table key needs 128-bit arithmetic once (first + n) * dim_mult + seed can pass 2^64
+  const unsigned __int128 top = (unsigned __int128)(first + n) * dim_mult + seed;
+  const bool wide = dim_mult && (top >> 64) != 0;
+  const unsigned g = grid_for(n * (uint64_t)ncols, 256, 16384);
+#define DR_GEN_ROWS(NCV)                                                                              \
+  do {                                                                                                \
+    if (wide) gen_records64_rows_kernel<NCV, true><<<g, 256, 0, s>>>(out, n, first, nkeys, m, seed, dim_mult); \
+    else gen_records64_rows_kernel<NCV, false><<<g, 256, 0, s>>>(out, n, first, nkeys, m, seed, dim_mult);    \
+  } while (0)
+  switch (ncols) {
+    case 1: DR_GEN_ROWS(1); break;
+    case 2: DR_GEN_ROWS(2); break;
+    case 3: DR_GEN_ROWS(3); break;
+    case 4: DR_GEN_ROWS(4); break;
+    case 5: DR_GEN_ROWS(5); break;
+    case 6: DR_GEN_ROWS(6); break;
+    case 7: DR_GEN_ROWS(7); break;
+    default: DR_GEN_ROWS(8); break;
+  }
+#undef DR_GEN_ROWS
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -6,11 +6,12 @@ Tables (gen://records64, 64-byte rows = 8 int64 fields, row store):
   * S  "fact":      keys uniform in [0, |R|), so every S row matches exactly one R row.
 Query:  R.Join(S, r => r.Key, s => s.Key, (r, s) => r.V1 + s.V1).Sum()  (plus the match count).
 
-Per rank: both tables are produced in HBM-sized chunks and grace-partitioned (ops/grace.py) into
-(rank, bucket) order; rank ranges move over xGMI (RCCL all-to-all-v), bucket slices spill to
-pinned host DRAM when the working set exceeds the HBM budget, then every bucket pair is
-sort-merge joined on the device.  The expected answer is computed from S alone (validation,
-outside the timed region).
+Per rank: both tables are produced in chunks and grace-partitioned (ops/grace.py): rows move to
+their rank over xGMI (RCCL all-to-all-v), then straight into per-bucket HBM stores; the buckets
+that do not fit the HBM budget spill to pinned host DRAM.  Every bucket pair is then hash joined
+on the device (open-addressing table over R's bucket, S streamed through it) with the Sum/Count
+of the result selector fused into the probe.  The expected answer is computed from S alone
+(validation, outside the timed region).
 """
 from __future__ import annotations
 
@@ -88,7 +89,7 @@ class HashJoinJob:
         cfg = self.cfg
         # per-rank receive estimate: an even share of both tables
         self.grace = G.GraceHashJoin(self.w, 64, 0, 8, {"R": self.r_hi - self.r_lo, "S": self.s_hi - self.s_lo},
-                                     cfg.chunk_rows, cfg.hbm_budget, cfg.buckets)
+                                     cfg.chunk_rows, cfg.hbm_budget, cfg.buckets, build="R")
 
     def release(self):
         if self.grace is not None:
@@ -106,17 +107,14 @@ class HashJoinJob:
             for a, b in self._chunks(lo, hi, tot):
                 self.grace.add_chunk(t, self._produce(t, a, b))
         t1 = time.perf_counter()
-        acc = torch.zeros(2, dtype=torch.int64, device=self.w.device)
+        acc = torch.zeros(3, dtype=torch.int64, device=self.w.device)
         for _, lr, rr in self.grace.buckets("R", "S"):
-            oo, ii = G.sort_merge_join_pairs(lr, rr, 0, 8)
-            if oo.numel():
-                v = lr.view(torch.int64).reshape(-1, 8)[:, 1].index_select(0, oo) + \
-                    rr.view(torch.int64).reshape(-1, 8)[:, 1].index_select(0, ii)
-                acc[0] += oo.numel()
-                acc[1] += v.sum()
+            # (r, s) => r.V1 + s.V1, then Count/Sum: fused into the probe (V1 = bytes 8..15)
+            G.join_sum(lr, rr, 0, 8, 8, 8, acc, self.grace.table, self.grace.log_cap)
         if W > 1:
             dist.all_reduce(acc)
-        res = acc.tolist()
+        a = acc.tolist()
+        res = [a[0], a[1] + a[2]]
         self.last = dict(matches=res[0], sum=res[1], partition_s=t1 - t0, spilled_bytes=self.grace.stats.spilled_bytes,
                          buckets=self.grace.B, in_hbm=self.grace.in_hbm)
         return res

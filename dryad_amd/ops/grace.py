@@ -1,221 +1,359 @@
-"""Out-of-core (grace) hash join of fixed-width row tables: HBM -> pinned host DRAM spill.
+"""Partitioned (grace) hash join of fixed-width row tables: HBM first, pinned host DRAM spill.
 
-SURVEY §5.7: the reference scales data size by partitioning every stage and spilling sorted
-runs to temp files when RAM runs out (DryadLinqVertex.cs:9584-9615); its HashJoin vertex
-(DryadLinqVertex.cs:852-897) builds a hash table of the (co-partitioned) inner side.  On a GPU
-node the tiers are HBM -> pinned host DRAM (PCIe) -> NVMe, and the join becomes a grace join:
+SURVEY §5.7: the reference scales data size by partitioning every stage and spilling to temp
+files when RAM runs out (DryadLinqVertex.cs:9584-9615); its HashJoin vertex
+(DryadLinqVertex.cs:852-897, ParallelHashJoin :6703-7315) builds a hash lookup of the
+co-partitioned inner side and streams the outer side through it.  On a GPU node the memory tiers
+are HBM (288 GB) -> pinned host DRAM (PCIe) and the join is a grace join:
 
-  pass A (per table, streamed in chunks that fit HBM):
-     rows chunk -> key entries [HIP extract_keys] -> dest = hash(key) % (W * B) [HIP hash_dest]
-       -> stable partition pass on dest [HIP] -> rows gathered into (rank, bucket) order [HIP]
-       -> W > 1: RCCL all-to-all-v of the rank ranges (xGMI)
-       -> per bucket: device -> pinned host copy on a side stream (spill), overlapping the next
-          chunk's compute; or kept in HBM when the whole working set fits the budget
-  pass B (per bucket b): both tables' bucket b back to HBM (the next bucket's copies run on the
-     side stream while bucket b joins), sort-merge join [HIP radix sort + merge-path ranges]
-     and the join's reduction on the device.
+  pass A (per table, streamed in chunks):
+     W > 1: rows -> rank by hash(key) [HIP dr_grace_partition, contiguous send layout]
+            -> RCCL all-to-all-v over xGMI
+     rows -> bucket by hash(key) [HIP dr_grace_partition]: each bucket's rows land directly in
+            its HBM bucket store (device fill counters, no host round trip), or — for the buckets
+            that do not fit the HBM budget — in a staging area that a side stream copies to pinned
+            host DRAM while the next chunk is partitioned
+  pass B (per bucket pair): spilled buckets stream back to HBM on the side stream (one bucket
+     ahead); build an open-addressing table over the build side's bucket (sized for the Infinity
+     Cache), probe with the other side [HIP dr_ht_build / dr_ht_probe_*].
 
-Buckets are sized so one bucket pair plus join scratch fits comfortably in HBM.
+Buckets are sized by the build side (<= ~6M rows, a 134 MB table) and as many as fit the HBM
+budget stay resident; only the remainder is spilled (hybrid hash join).
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass, field
 
 import torch
 
+from . import _lib
+from ._lib import c_i32, c_u32, c_u64, ptr, stream_of, vp
 from ..parallel import shuffle
 from ..parallel.comm import World
 from . import relational as R
 from . import sort as S
+
+_lib.register_signatures({
+    "dr_grace_workspace": (c_u64, [c_u64, c_u32, c_u32]),
+    "dr_grace_partition": (c_i32, [vp, c_u64, c_u32, c_u32, c_u32, c_u64, c_i32, c_u32, vp, vp, vp, c_u32, vp, vp,
+                                   vp, vp, vp]),
+    "dr_ht_build": (c_i32, [vp, c_u64, c_u32, c_u32, c_u32, c_u64, vp, c_i32, vp]),
+    "dr_ht_probe_sum_workspace": (c_u64, []),
+    "dr_ht_probe_sum": (c_i32, [vp, c_u64, c_u32, c_u32, c_u32, c_u64, vp, c_i32, vp, c_u32, c_u32, c_u32, vp, vp,
+                                vp]),
+    "dr_ht_probe_pairs": (c_i32, [vp, c_u64, c_u32, c_u32, c_u32, c_u64, vp, c_i32, vp, vp, vp, vp, c_i32, vp]),
+})
+
+HASH_SEED = 0x6A09E667F3BCC908
+MAX_BUCKETS = 256
+BUILD_ROWS_PER_BUCKET = 6_000_000     # table of 2^23 16-byte slots (134 MB) at load <= 0.72
+SLACK = 1.02                          # per-bucket capacity over the even share
+
+
+class Partitioner:
+    """Device state of one partitioning target: nb destinations with row pointers, fill counters
+    and capacities (device arrays), reused chunk after chunk."""
+
+    def __init__(self, nb: int, device):
+        self.nb = nb
+        self.dev = device
+        self.ptrs = torch.zeros(nb, dtype=torch.int64, device=device)
+        self.fill = torch.zeros(nb, dtype=torch.int64, device=device)
+        self.cap = torch.zeros(nb, dtype=torch.int64, device=device)
+        self.counts = torch.zeros(nb, dtype=torch.int64, device=device)
+        self.bases = torch.zeros(nb, dtype=torch.int64, device=device)
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
+        self._ws = None
+
+    def workspace(self, n: int, stride: int) -> torch.Tensor:
+        need = int(_lib.lib().dr_grace_workspace(c_u64(max(n, 1)), c_u32(stride), c_u32(self.nb)))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.dev)
+        return self._ws
+
+
+def partition_rows(rows: torch.Tensor, key_off: int, key_len: int, part: Partitioner, shift: int = 0,
+                   contig_from: int | None = None, seed: int = HASH_SEED):
+    """Scatter ``rows`` [n, stride] uint8 by hash(key) into ``part``'s destinations.  Buckets below
+    ``contig_from`` (default: all) append at their fill counters (bounded by cap, overflow flagged);
+    buckets from ``contig_from`` on are laid out back to back from row 0 of their pointer.
+    ``part.counts`` / ``part.bases`` receive this call's rows and first row per destination."""
+    _lib.require_gpu_tensor(rows, "partition_rows")
+    n, stride = rows.shape
+    cf = part.nb if contig_from is None else contig_from
+    ws = part.workspace(n, stride)
+    _lib.call("dr_grace_partition", ptr(rows), c_u64(n), c_u32(stride), c_u32(key_off), c_u32(key_len),
+              c_u64(seed & (2**64 - 1)), shift, c_u32(part.nb), ptr(part.ptrs), ptr(part.fill), ptr(part.cap),
+              c_u32(cf), ptr(part.counts), ptr(part.bases), ptr(part.overflow), ptr(ws), stream_of(rows))
+
+
+def split_by_rank(rows: torch.Tensor, key_off: int, key_len: int, part: Partitioner, out: torch.Tensor) -> list:
+    """Rows grouped by destination rank (hash bits 32..63) into ``out``; returns per-rank counts."""
+    part.ptrs.fill_(out.data_ptr())
+    partition_rows(rows, key_off, key_len, part, shift=32, contig_from=0)
+    return part.counts.tolist()
 
 
 @dataclass
 class SpillStats:
     spilled_bytes: int = 0
     buckets: int = 0
+    resident: int = 0
     in_hbm: bool = False
     rows: dict = field(default_factory=dict)
 
 
-class BucketStore:
-    """Per-bucket append-only row stores: buckets [0, resident) live in HBM, the rest in
-    page-locked host DRAM (hybrid hash join: only what does not fit is spilled)."""
+class _TableStore:
+    """One table's buckets: [0, resident) in one HBM tensor, the rest in pinned host DRAM."""
 
-    def __init__(self, nbuckets: int, capacity_rows: int, stride: int, device, resident: int):
-        self.B, self.stride = nbuckets, stride
-        self.cap = capacity_rows
-        self.resident = min(resident, nbuckets)
-        self._pinned = []
-        self.bufs = []
-        for b in range(nbuckets):
-            if b < self.resident:
-                self.bufs.append(torch.empty((capacity_rows, stride), dtype=torch.uint8, device=device))
-            else:
-                from ._lib import PinnedHostBuffer
-                p = PinnedHostBuffer((capacity_rows, stride))
-                self._pinned.append(p)
-                self.bufs.append(p.tensor)
-        self.fill = [0] * nbuckets
-
-    def on_host(self, b: int) -> bool:
-        return b >= self.resident
-
-    def append(self, b: int, rows: torch.Tensor, stream):
-        n = rows.shape[0]
-        if n == 0:
-            return
-        f = self.fill[b]
-        if f + n > self.cap:
-            raise RuntimeError(f"grace bucket {b} overflow ({f + n} > {self.cap} rows): skewed keys")
-        if self.on_host(b):
-            from ._lib import memcpy_async
-            memcpy_async(self.bufs[b][f:f + n], rows, stream)
-        else:
-            with torch.cuda.stream(stream):
-                self.bufs[b][f:f + n].copy_(rows, non_blocking=True)
-        self.fill[b] = f + n
-
-    def get(self, b: int):
-        return self.bufs[b][: self.fill[b]]
+    def __init__(self, nb, cap_rows, stride, resident, device):
+        self.nb, self.cap, self.stride, self.resident = nb, cap_rows, stride, resident
+        self.hbm = torch.empty((max(resident, 0) * cap_rows, stride), dtype=torch.uint8, device=device)
+        self.host = None
+        if nb > resident:
+            from ._lib import PinnedHostBuffer
+            self.host = PinnedHostBuffer(((nb - resident) * cap_rows, stride))
+        self.part = Partitioner(nb, device)
+        base = self.hbm.data_ptr()
+        rb = cap_rows * stride
+        self._init_fill = torch.tensor([b * cap_rows for b in range(nb)], dtype=torch.int64)
+        self.part.cap.copy_(torch.tensor([(b + 1) * cap_rows for b in range(nb)], dtype=torch.int64))
+        self._hbm_base, self._rb = base, rb
+        self.part.ptrs.fill_(base)
+        self.host_fill = [0] * nb
+        self.fill = None          # host copy of the final fills (rows per bucket) after pass A
+        self.reset()
 
     def reset(self):
-        self.fill = [0] * self.B
+        self.part.fill.copy_(self._init_fill)
+        self.part.overflow.zero_()
+        self.host_fill = [0] * self.nb
+        self.fill = None
+
+    def set_staging(self, staging: torch.Tensor):
+        ptrs = [self._hbm_base if b < self.resident else staging.data_ptr() for b in range(self.nb)]
+        self.part.ptrs.copy_(torch.tensor(ptrs, dtype=torch.int64))
+
+    def host_rows(self, b):
+        k = b - self.resident
+        return self.host.tensor[k * self.cap: k * self.cap + self.host_fill[b]]
+
+    def finish(self):
+        if int(self.part.overflow.item()):
+            raise RuntimeError("grace join bucket overflow: a bucket received more than its capacity (skewed keys)")
+        f = self.part.fill.tolist()
+        self.fill = [f[b] - b * self.cap if b < self.resident else self.host_fill[b] for b in range(self.nb)]
+
+    def hbm_rows(self, b):
+        return self.hbm[b * self.cap: b * self.cap + self.fill[b]]
 
     def release(self):
-        for p in self._pinned:
-            p.release()
-        self._pinned, self.bufs = [], []
-
-
-def _partition_rows(rows: torch.Tensor, key_off: int, key_len: int, nparts: int, ent_a, ent_b, out):
-    """rows -> rows permuted by hash(key) % nparts (stable) + host list of nparts+1 offsets."""
-    n = rows.shape[0]
-    e = S.extract_keys(rows, key_off, key_len, 0, out=ent_a[:n])
-    R.hash_dest(e, 0, nparts)
-    part, starts = S.partition_pass(e, 64, out=ent_b[:n])
-    S.gather_rows(rows, entries=part, out=out[:n])
-    return out[:n], starts[: nparts + 1].cpu().tolist()
+        if self.host is not None:
+            self.host.release()
+            self.host = None
+        self.hbm = None
 
 
 class GraceHashJoin:
-    """Grace join of two row tables produced chunk by chunk (``produce(table, chunk_index)``)."""
+    """Grace join of two row tables produced chunk by chunk (``add_chunk(table, rows)``), then
+    joined bucket by bucket (``buckets(build, probe)`` yields HBM row views)."""
 
     def __init__(self, world: World, stride: int, key_off: int, key_len: int, rows_per_rank: dict,
-                 chunk_rows: int, hbm_budget: int | None = None, buckets: int | None = None):
+                 chunk_rows: int, hbm_budget: int | None = None, buckets: int | None = None,
+                 build: str | None = None):
         self.w, self.stride, self.key_off, self.key_len = world, stride, key_off, key_len
         dev = world.device
         self.dev = dev
-        free = torch.cuda.mem_get_info(dev)[0] if dev.type == "cuda" else 1 << 40
-        self.budget = int(hbm_budget if hbm_budget is not None else free * 0.85)
-        total = sum(rows_per_rank.values()) * stride
-        self.stats = SpillStats()
-        scratch_a = chunk_rows * (2 * stride + 40)              # caller's chunk + packed copy + entries
-        join_scratch = lambda nbytes: nbytes // stride * 96     # noqa: E731  (sort entries x2, pairs, sums)
         W = world.size
-        if total * 1.05 + scratch_a + join_scratch(total) < self.budget:
-            nb, resident = 1, 1                                  # everything stays in HBM
+        free = torch.cuda.mem_get_info(dev)[0]
+        self.budget = int(hbm_budget if hbm_budget is not None else free * 0.92)
+        names = list(rows_per_rank)
+        self.build_name = build or names[0]
+        nbuild = rows_per_rank[self.build_name]
+        nb = buckets or max(1, min(MAX_BUCKETS, -(-nbuild // BUILD_ROWS_PER_BUCKET)))
+        caps = {t: int(n / nb * SLACK) + 4096 for t, n in rows_per_rank.items()}
+        pair = sum(caps.values()) * stride                     # one bucket of every table
+        self.log_cap = max(4, math.ceil(math.log2(caps[self.build_name] / 0.7)))
+        table_bytes = (1 << self.log_cap) * 16
+        exch = (chunk_rows * stride + int(chunk_rows * 1.3 + 4096) * stride) if W > 1 else 0
+        fixed = table_bytes + exch
+        if pair * nb + fixed <= self.budget:
+            resident = nb
         else:
-            pair = max(self.budget // 10, 1 << 20)              # one bucket of both tables
-            nb = buckets or max(2, -(-int(total * 1.05) // pair))
-            nb = min(nb, 256 // W)
-            pair_bytes = total * 1.05 / nb
-            room = self.budget - scratch_a - 2 * pair_bytes - join_scratch(int(pair_bytes))
-            resident = max(0, int(room // pair_bytes))
-        self.B = nb
+            if buckets is None:
+                nb = max(nb, 16)
+                caps = {t: int(n / nb * SLACK) + 4096 for t, n in rows_per_rank.items()}
+                pair = sum(caps.values()) * stride
+                self.log_cap = max(4, math.ceil(math.log2(caps[self.build_name] / 0.7)))
+                fixed = (1 << self.log_cap) * 16 + exch
+            # spilled buckets need two staging areas (partitioning) and two stream-in pairs
+            fixed += 2 * chunk_rows * stride + 2 * pair
+            resident = max(0, min(nb, int((self.budget - fixed) // pair)))
+        self.B, self.resident = nb, resident
         self.in_hbm = resident >= nb
-        self.chunk = chunk_rows
-        cap = lambda n: int(n / nb * 1.05) + 65536   # noqa: E731
-        self.stores = {t: BucketStore(nb, cap(n), stride, dev, resident) for t, n in rows_per_rank.items()}
-        self.stats.buckets, self.stats.in_hbm = nb, self.in_hbm
-        self.ent_a = torch.empty((chunk_rows, 2), dtype=torch.int64, device=dev)
-        self.ent_b = torch.empty_like(self.ent_a)
-        self.pbuf = torch.empty((chunk_rows, stride), dtype=torch.uint8, device=dev)
-        self.rbuf = torch.empty((int(chunk_rows * 1.3) + 4096 if world.size > 1 else 0, stride), dtype=torch.uint8,
-                                device=dev)
-        self.copy_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self.caps = caps
+        self.stores = {t: _TableStore(nb, caps[t], stride, resident, dev) for t in rows_per_rank}
+        self.stats = SpillStats(buckets=nb, resident=resident, in_hbm=self.in_hbm)
+        self.table = torch.empty((1 << self.log_cap) * 2, dtype=torch.int64, device=dev)
+        self.copy_stream = torch.cuda.Stream(dev)
+        self.staging, self.staging_ev = [], []
+        if not self.in_hbm:
+            self.staging = [torch.empty((chunk_rows, stride), dtype=torch.uint8, device=dev) for _ in range(2)]
+            self.staging_ev = [None, None]
+            self.stream_bufs = [{t: torch.empty((caps[t], stride), dtype=torch.uint8, device=dev)
+                                 for t in rows_per_rank} for _ in range(2)]
+        self._turn = 0
+        if W > 1:
+            self.rank_part = Partitioner(W, dev)
+            self.sbuf = torch.empty((chunk_rows, stride), dtype=torch.uint8, device=dev)
+            self.rbuf = torch.empty((int(chunk_rows * 1.3) + 4096, stride), dtype=torch.uint8, device=dev)
 
     def reset(self):
-        """Empty every bucket for the next join (host buffers stay allocated and registered:
-        page-locking 100 GB costs seconds, so it is done once per job, not per step)."""
         for st in self.stores.values():
             st.reset()
-        self.stats = SpillStats(buckets=self.B, in_hbm=self.in_hbm)
+        self.stats = SpillStats(buckets=self.B, resident=self.resident, in_hbm=self.in_hbm)
 
     # -------------------------------------------------------------- pass A
     def add_chunk(self, table: str, rows: torch.Tensor):
-        W, B = self.w.size, self.B
-        if self.copy_stream is not None:
-            # pbuf / rbuf are about to be overwritten: wait for the previous chunk's spill copies
-            torch.cuda.current_stream(self.dev).wait_stream(self.copy_stream)
-        part, st = _partition_rows(rows, self.key_off, self.key_len, W * B, self.ent_a, self.ent_b, self.pbuf)
+        W = self.w.size
         if W > 1:
-            # dest = rank * B + bucket: rank ranges are contiguous; exchange (rank, bucket) counts
-            cnt = torch.tensor([st[i + 1] - st[i] for i in range(W * B)], dtype=torch.int64).view(W, B)
-            send_counts = cnt.sum(1).tolist()
-            allc = shuffle.all_gather_tensor(cnt.flatten().to(self.w.device), self.w).view(W, W, B).cpu()
-            recv_by_src = allc[:, self.w.rank, :]                      # [src, bucket]
-            recv_counts = recv_by_src.sum(1).tolist()
-            n_recv = sum(recv_counts)
+            send = split_by_rank(rows, self.key_off, self.key_len, self.rank_part, self.sbuf)
+            recv = shuffle.exchange_counts(torch.tensor(send, dtype=torch.int64), self.w).tolist()
+            n_recv = sum(recv)
             if n_recv > self.rbuf.shape[0]:
                 self.rbuf = torch.empty((int(n_recv * 1.2), self.stride), dtype=torch.uint8, device=self.dev)
-            shuffle.alltoallv_bytes(part.reshape(-1), [c * self.stride for c in send_counts],
-                                    self.rbuf.reshape(-1), [c * self.stride for c in recv_counts], self.w)
-            if self.copy_stream is not None:
-                self.copy_stream.wait_stream(torch.cuda.current_stream(self.dev))
+            shuffle.alltoallv_bytes(self.sbuf.view(-1)[: sum(send) * self.stride], [c * self.stride for c in send],
+                                    self.rbuf.view(-1)[: n_recv * self.stride], [c * self.stride for c in recv], self.w)
+            rows = self.rbuf[:n_recv]
+        st = self.stores[table]
+        main = torch.cuda.current_stream(self.dev)
+        if not self.in_hbm:
+            k = self._turn
+            self._turn ^= 1
+            if self.staging_ev[k] is not None:
+                main.wait_event(self.staging_ev[k])      # its previous chunk's spill copies are done
+            st.set_staging(self.staging[k])
+        partition_rows(rows, self.key_off, self.key_len, st.part, shift=0, contig_from=st.resident)
+        if not self.in_hbm:
+            counts = st.part.counts.tolist()          # one small D2H per chunk
+            self.copy_stream.wait_stream(main)
             off = 0
-            for src in range(W):
-                for b in range(B):
-                    c = int(recv_by_src[src, b])
-                    self.stores[table].append(b, self.rbuf[off:off + c], self.copy_stream)
-                    if self.stores[table].on_host(b):
-                        self.stats.spilled_bytes += c * self.stride
-                    off += c
-            moved = n_recv
-        else:
-            if self.copy_stream is not None:
-                self.copy_stream.wait_stream(torch.cuda.current_stream(self.dev))
-            for b in range(B):
-                self.stores[table].append(b, part[st[b]:st[b + 1]], self.copy_stream)
-                if self.stores[table].on_host(b):
-                    self.stats.spilled_bytes += (st[b + 1] - st[b]) * self.stride
-            moved = part.shape[0]
-        self.stats.rows[table] = self.stats.rows.get(table, 0) + moved
+            for b in range(st.resident, self.B):
+                c = counts[b]
+                if c:
+                    if st.host_fill[b] + c > st.cap:
+                        raise RuntimeError(f"grace join bucket {b} overflow ({st.host_fill[b] + c} > {st.cap} rows)")
+                    kk = b - st.resident
+                    dst = st.host.tensor[kk * st.cap + st.host_fill[b]: kk * st.cap + st.host_fill[b] + c]
+                    _lib.memcpy_async(dst, self.staging[k][off: off + c], self.copy_stream)
+                    st.host_fill[b] += c
+                    self.stats.spilled_bytes += c * self.stride
+                off += c
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+            self.staging_ev[k] = ev
+        self.stats.rows[table] = self.stats.rows.get(table, 0) + rows.shape[0]
 
     def finish_partitioning(self):
-        if self.copy_stream is not None:
-            torch.cuda.current_stream(self.dev).wait_stream(self.copy_stream)
+        torch.cuda.current_stream(self.dev).wait_stream(self.copy_stream)
+        for st in self.stores.values():
+            st.finish()
 
     # -------------------------------------------------------------- pass B
-    def buckets(self, left: str, right: str):
-        """Yield (b, left_rows_b, right_rows_b) in HBM; with spilled stores the next bucket's
-        host->device copies overlap the caller's work on the current one."""
+    def buckets(self, build: str, probe: str):
+        """Yield (b, build_rows_b, probe_rows_b) in HBM; spilled buckets stream in on the side
+        stream one bucket ahead of the caller's work."""
         self.finish_partitioning()
-        L, Rs = self.stores[left], self.stores[right]
+        Bs, Ps = self.stores[build], self.stores[probe]
+        main = torch.cuda.current_stream(self.dev)
         pending = None
         for b in range(self.B):
-            if not L.on_host(b):
-                yield b, L.get(b), Rs.get(b)
+            if b < self.resident:
+                yield b, Bs.hbm_rows(b), Ps.hbm_rows(b)
                 continue
-            cur = pending if pending is not None else self.stream_in(left, right, b)
-            torch.cuda.current_stream(self.dev).wait_stream(self.copy_stream)
-            pending = self.stream_in(left, right, b + 1) if b + 1 < self.B else None
+            cur = pending if pending is not None else self._stream_in(build, probe, b, 0)
+            main.wait_stream(self.copy_stream)
+            pending = self._stream_in(build, probe, b + 1, (b + 1 - self.resident) & 1) if b + 1 < self.B else None
             yield b, cur[0], cur[1]
 
-    def stream_in(self, left, right, b):
-        out = []
+    def _stream_in(self, build, probe, b, slot):
         main = torch.cuda.current_stream(self.dev)
-        for t in (left, right):
-            h = self.stores[t].get(b)
-            d = torch.empty(h.shape, dtype=torch.uint8, device=self.dev)   # allocated on the main stream
-            self.copy_stream.wait_stream(main)                             # ... whose earlier work may reuse it
-            from ._lib import memcpy_async
-            memcpy_async(d, h, self.copy_stream)
+        self.copy_stream.wait_stream(main)         # the slot's previous bucket has been consumed
+        out = []
+        for t in (build, probe):
+            h = self.stores[t].host_rows(b)
+            d = self.stream_bufs[slot][t][: h.shape[0]]
+            _lib.memcpy_async(d, h, self.copy_stream)
             out.append(d)
         return out
+
+    def clear_table(self):
+        self.table.fill_(-1)
 
     def release(self):
         for st in self.stores.values():
             st.release()
+
+
+def ht_log_cap(n_build: int) -> int:
+    return max(4, math.ceil(math.log2(max(n_build, 1) / 0.7)))
+
+
+def join_sum(build_rows: torch.Tensor, probe_rows: torch.Tensor, key_off: int, key_len: int, col_build: int,
+             col_probe: int, acc: torch.Tensor, table: torch.Tensor, log_cap: int, seed: int = HASH_SEED):
+    """acc (int64[3]) += (matches, sum of probe int64 column at byte col_probe over matches, sum of
+    the matched build rows' int64 column at byte col_build): the decomposable aggregate of a join
+    whose result selector is linear in one column per side, fused into the probe."""
+    nb, sb = build_rows.shape
+    npr, sp = probe_rows.shape
+    assert nb * 10 <= 9 * (1 << log_cap) and table.numel() * 8 >= (1 << log_cap) * 16
+    table[: (1 << log_cap) * 2].fill_(-1)
+    s = stream_of(probe_rows)
+    ws = _probe_ws(probe_rows.device)
+    _lib.call("dr_ht_build", ptr(build_rows), c_u64(nb), c_u32(sb), c_u32(key_off), c_u32(key_len),
+              c_u64(seed & (2**64 - 1)), ptr(table), log_cap, s)
+    _lib.call("dr_ht_probe_sum", ptr(probe_rows), c_u64(npr), c_u32(sp), c_u32(key_off), c_u32(key_len),
+              c_u64(seed & (2**64 - 1)), ptr(table), log_cap, ptr(build_rows), c_u32(sb), c_u32(col_probe),
+              c_u32(col_build), ptr(acc), ptr(ws), s)
+    return acc
+
+
+_PROBE_WS = {}
+
+
+def _probe_ws(dev):
+    t = _PROBE_WS.get(dev)
+    if t is None:
+        t = _PROBE_WS[dev] = torch.empty(int(_lib.lib().dr_ht_probe_sum_workspace()), dtype=torch.uint8, device=dev)
+    return t
+
+
+def hash_join_pairs(build_rows: torch.Tensor, probe_rows: torch.Tensor, key_off: int, key_len: int,
+                    seed: int = HASH_SEED):
+    """(probe row, build row) index pairs of equal keys, grouped by probe row in probe order."""
+    nb, sb = build_rows.shape
+    npr, sp = probe_rows.shape
+    dev = probe_rows.device
+    if nb == 0 or npr == 0:
+        z = torch.empty(0, dtype=torch.int64, device=dev)
+        return z, z
+    lc = ht_log_cap(nb)
+    table = torch.full(((1 << lc) * 2,), -1, dtype=torch.int64, device=dev)
+    s = stream_of(probe_rows)
+    sd = c_u64(seed & (2**64 - 1))
+    _lib.call("dr_ht_build", ptr(build_rows), c_u64(nb), c_u32(sb), c_u32(key_off), c_u32(key_len), sd, ptr(table),
+              lc, s)
+    count = torch.empty(npr, dtype=torch.int64, device=dev)
+    _lib.call("dr_ht_probe_pairs", ptr(probe_rows), c_u64(npr), c_u32(sp), c_u32(key_off), c_u32(key_len), sd,
+              ptr(table), lc, ptr(count), ptr(None), ptr(None), ptr(None), 0, s)
+    offs = R.scan_exclusive(count)
+    total = int((offs[-1] + count[-1]).item())
+    po = torch.empty(total, dtype=torch.int64, device=dev)
+    bo = torch.empty(total, dtype=torch.int64, device=dev)
+    _lib.call("dr_ht_probe_pairs", ptr(probe_rows), c_u64(npr), c_u32(sp), c_u32(key_off), c_u32(key_len), sd,
+              ptr(table), lc, ptr(count), ptr(offs), ptr(po), ptr(bo), 1, s)
+    return po, bo
 
 
 def sort_merge_join_pairs(left: torch.Tensor, right: torch.Tensor, key_off: int, key_len: int):
