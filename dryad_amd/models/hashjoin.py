@@ -19,10 +19,10 @@ import time
 from dataclasses import dataclass
 
 import torch
-import torch.distributed as dist
 
 from ..ops import grace as G
 from ..ops import relational as R
+from ..parallel import shuffle
 from ..parallel.comm import World
 from .records_cpu import dim_multiplier
 
@@ -112,7 +112,7 @@ class HashJoinJob:
             # (r, s) => r.V1 + s.V1, then Count/Sum: fused into the probe (V1 = bytes 8..15)
             G.join_sum(lr, rr, 0, 8, 8, 8, acc, self.grace.table, self.grace.log_cap)
         if W > 1:
-            dist.all_reduce(acc)
+            shuffle.all_reduce_(acc, "sum", self.w)
         a = acc.tolist()
         res = [a[0], a[1] + a[2]]
         self.last = dict(matches=res[0], sum=res[1], partition_s=t1 - t0, spilled_bytes=self.grace.stats.spilled_bytes,
@@ -129,5 +129,5 @@ class HashJoinJob:
             acc[0] += key.numel()
             acc[1] += (f + rows[:, 1]).sum()
         if self.w.size > 1:
-            dist.all_reduce(acc)
+            shuffle.all_reduce_(acc, "sum", self.w)
         return acc.tolist()

@@ -199,7 +199,8 @@ class GraceHashJoin:
         self.copy_stream = torch.cuda.Stream(dev)
         self.staging, self.staging_ev = [], []
         if not self.in_hbm:
-            self.staging = [torch.empty((chunk_rows, stride), dtype=torch.uint8, device=dev) for _ in range(2)]
+            srows = int(chunk_rows * 1.3) + 4096 if W > 1 else chunk_rows
+            self.staging = [torch.empty((srows, stride), dtype=torch.uint8, device=dev) for _ in range(2)]
             self.staging_ev = [None, None]
             self.stream_bufs = [{t: torch.empty((caps[t], stride), dtype=torch.uint8, device=dev)
                                  for t in rows_per_rank} for _ in range(2)]
@@ -233,6 +234,9 @@ class GraceHashJoin:
             self._turn ^= 1
             if self.staging_ev[k] is not None:
                 main.wait_event(self.staging_ev[k])      # its previous chunk's spill copies are done
+            if self.staging[k].shape[0] < rows.shape[0]:  # a received chunk can exceed chunk_rows
+                self.staging[k] = torch.empty((int(rows.shape[0] * 1.2), self.stride), dtype=torch.uint8,
+                                              device=self.dev)
             st.set_staging(self.staging[k])
         partition_rows(rows, self.key_off, self.key_len, st.part, shift=0, contig_from=st.resident)
         if not self.in_hbm:

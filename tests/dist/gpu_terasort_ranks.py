@@ -75,6 +75,15 @@ def main():
         for r in range(w.size - 1):
             assert bytes(allends[r, 10:]) <= bytes(allends[r + 1, :10]), r
     RS.PIPE_SUBS = 0
+    # grace hash join across ranks: rank split + all-to-all-v, bucket stores, fused probe; once in
+    # HBM and once with a budget that spills buckets to pinned host memory
+    from dryad_amd.models.hashjoin import HashJoinConfig, HashJoinJob
+    for budget in (None, 1 << 24):
+        job = HashJoinJob(w, HashJoinConfig(rows_r=200_000, rows_s=300_000, chunk_rows=50_000, hbm_budget=budget))
+        res = job.step()
+        assert res == job.expected() and res[0] == 300_000, (w.rank, res)
+        assert (job.last["spilled_bytes"] > 0) == (budget is not None), job.last
+        job.release()
     w.barrier()
     if w.rank == 0:
         print("MULTIRANK_OK", w.size, flush=True)
