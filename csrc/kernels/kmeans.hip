@@ -19,6 +19,9 @@
 // centroid tile with 16-byte LDS loads.  C/D: col j = l & 31, row = (reg & 3) + 8 (reg >> 2) + 4 h.
 #include "common.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -248,6 +251,312 @@ __global__ void sq_norms_kernel(const float* __restrict__ C, int K, float* __res
   if (threadIdx.x == 0) out[j] = s;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// K <= 64: the whole step on bf16 MFMA (mode 3).
+//
+// Distances.  x.c with x = xh + xm (+ 2^-16-relative rest), c = ch + cm split into bf16 parts:
+// xh.ch + xh.cm + xm.ch = three v_mfma_f32_32x32x16_bf16 per 16 dims, 5.3x fewer matrix-core
+// cycles than the exact-f32 v_mfma_f32_32x32x2_f32 path, with |error| <= ~1.1e-4 |x| max|c| on a
+// distance.  Every point whose best and second-best estimates are closer than twice that bound
+// is re-ranked with exact f32 dot products, so the assignment is the f32 nearest centroid.
+//
+// Sums.  S[c][d] += sum_p onehot[p][c] x[p][d] is a GEMM: A = one-hot (exact in bf16), B = the
+// point tile split EXACTLY into three bf16 parts (x = xh + xm + xl), f32 accumulation in the
+// matrix core's accumulators, flushed to the f64 global sums every `flush` tiles.  No LDS
+// read-modify-write and no per-point serial loop.
+//
+// A wave owns 32-point tiles: it loads a tile (lane (r, h) = point r's dims 16s + 8h .. +7, the
+// distance MFMA's B operand), prefetches the next one, stages the tile in LDS for the transposed
+// (point-major) reads of the sum MFMA, and keeps the K x 128 sums in 8 accumulator tiles.
+// Lane map (32x32x16 bf16): A[row r][k = 8h + j], B[k = 8h + j][col r], C col = l & 31,
+// row = (g & 3) + 8 (g >> 2) + 4 h.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int kCRow = 136;   // bf16 per centroid row in LDS (272 B: b128 reads spread over banks)
+constexpr int kXRow = 132;   // floats per point row of the LDS tile
+// |estimate - f32 distance| <= kKmTol |x| max|c|: bf16 split residuals 3 * 2^-16 plus f32
+// accumulation over 384 products (2.3e-5), both relative to sum |x_i c_i| <= |x| |c|, doubled.
+constexpr float kKmTol = 1.5e-4f;
+
+// DBG (profiling builds only): bit0 skips the sum MFMAs, bit1 the distance MFMAs, bit2 the
+// near-tie listing.
+template <int KT, int DBG>
+__global__ __launch_bounds__(256) void kmeans_mfma_kernel(const float* __restrict__ X, uint64_t n,
+                                                          const float* __restrict__ C, const float* __restrict__ cnorm,
+                                                          int K, int32_t* __restrict__ assign,
+                                                          double* __restrict__ gsum, unsigned long long* __restrict__ gcnt,
+                                                          int flush_tiles) {
+  constexpr int KP = 32 * KT;
+  __shared__ __attribute__((aligned(16))) __bf16 chi[KP * kCRow];
+  __shared__ __attribute__((aligned(16))) __bf16 cmd[KP * kCRow];
+  __shared__ float cn[KP];
+  __shared__ float cmax_s;
+  __shared__ __attribute__((aligned(16))) float xs[4][32 * kXRow];
+  __shared__ __attribute__((aligned(16))) int bjs[4][32];
+  __shared__ unsigned int wcnt[4][KP];
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
+  for (int i = t; i < KP * D; i += 256) {
+    const int c = i / D, d = i % D;
+    const float v = c < K ? C[(uint64_t)c * D + d] : 0.f;
+    const __bf16 vh = (__bf16)v;
+    chi[c * kCRow + d] = vh;
+    cmd[c * kCRow + d] = (__bf16)(v - (float)vh);
+  }
+  for (int c = t; c < KP; c += 256) cn[c] = c < K ? cnorm[c] : __builtin_inff();
+  for (int i = t; i < 4 * KP; i += 256) (&wcnt[0][0])[i] = 0u;
+  if (t == 0) {
+    float m = 0.f;
+    for (int c = 0; c < K; ++c) m = fmaxf(m, cnorm[c]);
+    cmax_s = sqrtf(m);
+  }
+  __syncthreads();
+  const float cmax = cmax_s;
+  float* xw = xs[w];
+  const uint64_t tiles = (n + 31) / 32;
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + w, GW = (uint64_t)gridDim.x * 4;
+  f32x16 S[KT][4];
+#pragma unroll
+  for (int ct = 0; ct < KT; ++ct)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S[ct][q] = f32x16{};
+  float xr[64];
+  auto load = [&](uint64_t tile, float* dst) {
+    const uint64_t p = tile * 32 + r;
+    const bool ok = p < n;
+    const float4* src = reinterpret_cast<const float4*>(X + (ok ? p : 0) * D + 8 * h);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const float4 a = ok ? src[4 * s] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 b = ok ? src[4 * s + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+      dst[8 * s + 0] = a.x; dst[8 * s + 1] = a.y; dst[8 * s + 2] = a.z; dst[8 * s + 3] = a.w;
+      dst[8 * s + 4] = b.x; dst[8 * s + 5] = b.y; dst[8 * s + 6] = b.z; dst[8 * s + 7] = b.w;
+    }
+  };
+  // flush: one centroid tile at a time through the wave's LDS tile area (32 x 128 floats), then
+  // f64 atomics on consecutive addresses (128 distinct addresses computed in registers would be
+  // hoisted out of the loop and pin 256 VGPRs)
+  auto flush = [&]() {
+#pragma unroll
+    for (int ct = 0; ct < KT; ++ct) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int g = 0; g < 16; ++g) xw[((g & 3) + 8 * (g >> 2) + 4 * h) * D + 32 * q + r] = S[ct][q][g];
+        S[ct][q] = f32x16{};
+      }
+      double* gs = gsum + (uint64_t)ct * 32 * D;
+      const int rows = K - ct * 32 < 32 ? K - ct * 32 : 32;
+      for (int i = l; i < rows * D; i += 64) {
+        const float v = xw[i];
+        if (v != 0.f) atomicAdd(gs + i, (double)v);
+      }
+    }
+    for (int c = l; c < KP; c += 64) {
+      const unsigned int v = wcnt[w][c];
+      if (v) {
+        atomicAdd(gcnt + c, (unsigned long long)v);
+        wcnt[w][c] = 0u;
+      }
+    }
+  };
+  int since = 0;
+  if (gw < tiles) load(gw, xr);
+  for (uint64_t tile = gw; tile < tiles; tile += GW) {
+    // the centroid fragments are re-read from LDS every tile: hoisted out of the loop they would
+    // pin 128 VGPRs and push the sum accumulators into scratch
+    asm volatile("" ::: "memory");
+    const uint64_t p = tile * 32 + r;
+    const bool pvalid = p < n;
+    // stage the tile for the point-major reads of the sum MFMA (a wave's LDS ops run in order)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      *reinterpret_cast<float4*>(xw + r * kXRow + 16 * s + 8 * h) = make_float4(xr[8 * s], xr[8 * s + 1], xr[8 * s + 2], xr[8 * s + 3]);
+      *reinterpret_cast<float4*>(xw + r * kXRow + 16 * s + 8 * h + 4) =
+          make_float4(xr[8 * s + 4], xr[8 * s + 5], xr[8 * s + 6], xr[8 * s + 7]);
+    }
+    // distances: Dt[c][p] = c . x_p over 8 k-steps of 16 dims
+    f32x16 Dt[KT];
+#pragma unroll
+    for (int ct = 0; ct < KT; ++ct) Dt[ct] = f32x16{};
+    float xx = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      bf16x8 xh, xm;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = xr[8 * s + j];
+        xx = fmaf(v, v, xx);
+        xh[j] = (__bf16)v;
+        xm[j] = (__bf16)(v - (float)xh[j]);
+      }
+#pragma unroll
+      for (int ct = 0; ct < KT; ++ct) {
+        if constexpr ((DBG & 2) != 0) continue;
+        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(chi + (ct * 32 + r) * kCRow + 16 * s + 8 * h);
+        const bf16x8 am = *reinterpret_cast<const bf16x8*>(cmd + (ct * 32 + r) * kCRow + 16 * s + 8 * h);
+        Dt[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xh, Dt[ct], 0, 0, 0);
+        Dt[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xm, Dt[ct], 0, 0, 0);
+        Dt[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, xh, Dt[ct], 0, 0, 0);
+      }
+    }
+    // xr is dead from here on (the re-rank reads the LDS copy): prefetch the next tile into it,
+    // overlapping the load with the argmin and the sum MFMAs
+    if (tile + GW < tiles) load(tile + GW, xr);
+    // argmin with the runner-up, merged across the two lane halves
+    float bd = __builtin_inff(), sd = __builtin_inff();
+    int bj = 0;
+#pragma unroll
+    for (int ct = 0; ct < KT; ++ct)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int c = ct * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
+        const float d = fmaf(-2.f, Dt[ct][g], cn[c]);
+        // c increases along the loop, so a strict < keeps the lowest index of equal values
+        sd = fminf(sd, fmaxf(bd, d));
+        bj = d < bd ? c : bj;
+        bd = fminf(bd, d);
+      }
+    {
+      const float obd = __shfl_xor(bd, 32, 64), osd = __shfl_xor(sd, 32, 64);
+      const int obj = __shfl_xor(bj, 32, 64);
+      xx += __shfl_xor(xx, 32, 64);
+      if (obd < bd || (obd == bd && obj < bj)) {
+        sd = fminf(bd, osd);
+        bd = obd;
+        bj = obj;
+      } else {
+        sd = fminf(sd, obd);
+      }
+    }
+    // near ties (estimates of the best and the runner-up closer than the error bound): flagged in
+    // bit 31 of the point's assignment; kmeans_near_list + kmeans_rerank_kernel re-rank them with
+    // exact f32 distances afterwards and move the point's contribution if the estimate was wrong
+    // (no atomics or ballots in this loop).
+    const bool near = (DBG & 4) == 0 && K > 1 && (sd - bd) <= 2.f * kKmTol * sqrtf(xx) * cmax;
+    if (!pvalid) bj = -1;
+    if (h == 0) {
+      bjs[w][r] = bj;
+      if (pvalid) {
+        atomicAdd(&wcnt[w][bj], 1u);
+        assign[p] = near ? (int32_t)((uint32_t)bj | 0x80000000u) : bj;
+      }
+    }
+    // sums: S[ct][q] += onehot^T (centroids x 16 points) . X (16 points x 32 dims), x in 3 exact parts
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int4 b0 = *reinterpret_cast<const int4*>(&bjs[w][16 * s + 8 * h]);
+      const int4 b1 = *reinterpret_cast<const int4*>(&bjs[w][16 * s + 8 * h + 4]);
+      const int bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      bf16x8 oh[KT];
+#pragma unroll
+      for (int ct = 0; ct < KT; ++ct)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) oh[ct][j] = (bv[j] == ct * 32 + r) ? (__bf16)1.0f : (__bf16)0.0f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bf16x8 ph, pm, pl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = xw[(16 * s + 8 * h + j) * kXRow + 32 * q + r];
+          const __bf16 a0 = (__bf16)v;
+          const float r1 = v - (float)a0;
+          const __bf16 a1 = (__bf16)r1;
+          ph[j] = a0;
+          pm[j] = a1;
+          pl[j] = (__bf16)(r1 - (float)a1);
+        }
+#pragma unroll
+        for (int ct = 0; ct < KT; ++ct) {
+          if constexpr ((DBG & 1) != 0) continue;
+          S[ct][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oh[ct], ph, S[ct][q], 0, 0, 0);
+          S[ct][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oh[ct], pm, S[ct][q], 0, 0, 0);
+          S[ct][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oh[ct], pl, S[ct][q], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one dim tile's operands live at a time
+      }
+    }
+    if (++since == flush_tiles) {
+      since = 0;
+      flush();
+    }
+  }
+  flush();
+}
+
+
+// Compaction of the near-tie flags (bit 31 of assign) into (point, estimate) pairs; clears the flag.
+__global__ __launch_bounds__(256) void kmeans_near_list(int32_t* __restrict__ assign, uint64_t n,
+                                                        uint32_t* __restrict__ near_cnt, uint32_t* __restrict__ near_list) {
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x; b < n; b += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t p = b + threadIdx.x;
+    const int32_t a = p < n ? assign[p] : 0;
+    const bool near = a < 0;
+    const uint64_t m = __ballot(near);
+    if (m) {
+      const int l = threadIdx.x & 63;
+      const int first = __builtin_ctzll(m);
+      uint32_t base = 0;
+      if (l == first) base = atomicAdd(near_cnt, (uint32_t)__popcll(m));
+      base = __shfl(base, first, 64);
+      if (near) {
+        const uint32_t o = base + popc_below(m);
+        const uint32_t est = (uint32_t)a & 0x7FFFFFFFu;
+        near_list[2 * (uint64_t)o] = (uint32_t)p;
+        near_list[2 * (uint64_t)o + 1] = est;
+        assign[p] = (int32_t)est;
+      }
+    }
+  }
+}
+
+// Exact f32 re-rank of the near-tie points listed by kmeans_near_list: one wave per point, lane
+// c computes the f32 distance to centroid c; if the estimate's choice was wrong the point's
+// coordinates and count move to the right centroid.  The grid drains the device-side count.
+__global__ __launch_bounds__(64) void kmeans_rerank_kernel(const float* __restrict__ X, const float* __restrict__ C,
+                                                           const float* __restrict__ cnorm, int K,
+                                                           const uint32_t* __restrict__ near_cnt,
+                                                           const uint32_t* __restrict__ near_list,
+                                                           int32_t* __restrict__ assign, double* __restrict__ gsum,
+                                                           unsigned long long* __restrict__ gcnt) {
+  const uint32_t total = *near_cnt;
+  const int l = threadIdx.x;
+  for (uint32_t i = blockIdx.x; i < total; i += gridDim.x) {
+    const uint64_t p = near_list[2 * (uint64_t)i];
+    const int est = (int)near_list[2 * (uint64_t)i + 1];
+    const float4* xr = reinterpret_cast<const float4*>(X + p * D);
+    float d = __builtin_inff();
+    if (l < K) {
+      const float4* cr = reinterpret_cast<const float4*>(C + (uint64_t)l * D);
+      float a0 = 0.f, a1 = 0.f;
+      for (int k = 0; k < D / 4; k += 2) {
+        const float4 x0 = xr[k], x1 = xr[k + 1], c0 = cr[k], c1 = cr[k + 1];
+        a0 = fmaf(x0.x, c0.x, fmaf(x0.y, c0.y, fmaf(x0.z, c0.z, fmaf(x0.w, c0.w, a0))));
+        a1 = fmaf(x1.x, c1.x, fmaf(x1.y, c1.y, fmaf(x1.z, c1.z, fmaf(x1.w, c1.w, a1))));
+      }
+      d = cnorm[l] - 2.f * (a0 + a1);
+    }
+    int bj = l;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      const float od = __shfl_xor(d, m, 64);
+      const int oj = __shfl_xor(bj, m, 64);
+      if (od < d || (od == d && oj < bj)) { d = od; bj = oj; }
+    }
+    if (bj != est) {
+      const float v0 = X[p * D + l], v1 = X[p * D + 64 + l];
+      atomicAdd(gsum + (uint64_t)est * D + l, -(double)v0);
+      atomicAdd(gsum + (uint64_t)est * D + 64 + l, -(double)v1);
+      atomicAdd(gsum + (uint64_t)bj * D + l, (double)v0);
+      atomicAdd(gsum + (uint64_t)bj * D + 64 + l, (double)v1);
+      if (l == 0) {
+        atomicAdd(gcnt + est, ~0ull);          // -1
+        atomicAdd(gcnt + bj, 1ull);
+        assign[p] = bj;
+      }
+    }
+  }
+}
+
 uint32_t step_smem(int K, bool cres, bool slab) {
   const int Kc = cres ? ((K + CT - 1) / CT) * CT : CT;
   return (uint32_t)((Kc * LDW + Kc + 2 * kPts) * 4 + (slab ? (uint32_t)K * D * 4 + (uint32_t)K * 4 : 0));
@@ -273,17 +582,28 @@ void set_smem(F kern, uint32_t bytes) {
 }  // namespace
 
 // Mode chosen for K (exposed for tests/benchmarks): 0 = centroids + slab resident,
-// 1 = streamed centroid tiles + slab, 2 = assignment pass + sliced accumulation.
+// 1 = streamed centroid tiles + slab, 2 = assignment pass + sliced accumulation,
+// 3 = K <= 64 on bf16 MFMA (split-precision distances with exact re-rank, MFMA one-hot sums).
+int g_km_f32 = -1;   // DRYAD_KM_F32=1: keep the exact-f32 MFMA distance path for every K
+
 DR_API int dr_kmeans_mode(int K) {
+  if (g_km_f32 < 0) {
+    const char* e = getenv("DRYAD_KM_F32");
+    g_km_f32 = (e && atoi(e) == 1) ? 1 : 0;
+  }
+  if (K <= 64 && !g_km_f32) return 3;
   if (step_smem(K, true, true) <= kLdsBudget) return 0;
   if (step_smem(K, false, true) <= kLdsBudget) return 1;
   return 2;
 }
 
 // One k-means step over n points of dimension 128.  gsum (K*D f64) and gcnt (K u64) accumulate;
-// the caller zeroes them.  assign (n int32) may be null unless K needs mode 2.
+// the caller zeroes them.  assign (n int32) may be null unless K needs mode 2; near_ws (mode 3)
+// holds dr_kmeans_near_workspace(n) bytes.
+DR_API uint64_t dr_kmeans_near_workspace(uint64_t n) { return 8 * n + 16; }
+
 DR_API int dr_kmeans_step(const float* X, uint64_t n, int d, const float* C, int K, float* cnorm_ws,
-                          int32_t* assign, double* gsum, unsigned long long* gcnt, hipStream_t s) {
+                          int32_t* assign, double* gsum, unsigned long long* gcnt, void* near_ws, hipStream_t s) {
   if (d != D || K < 1 || K > 4096) return (int)hipErrorInvalidValue;
   sq_norms_kernel<<<K, 64, 0, s>>>(C, K, cnorm_ws);
   if (n == 0) return 0;
@@ -292,6 +612,40 @@ DR_API int dr_kmeans_step(const float* X, uint64_t n, int d, const float* C, int
   if (dbg < 0) {
     const char* e = getenv("DRYAD_KM_DEBUG");
     dbg = e ? atoi(e) : 0;
+  }
+  if (mode == 3) {
+    // near_ws: [0] = count, then 2 words per listed point (point, estimated centroid); 8 n + 16
+    // bytes (dr_kmeans_near_workspace)
+    if (!near_ws || !assign) return (int)hipErrorInvalidValue;
+    const uint64_t wt = (n + 31) / 32;
+    const uint64_t blocks = (wt + 3) / 4;
+    const unsigned g3 = (unsigned)(blocks < (uint64_t)num_cus() ? blocks : (uint64_t)num_cus());
+    uint32_t* near_cnt = reinterpret_cast<uint32_t*>(near_ws);
+    uint32_t* near_list = near_cnt + 4;
+    hipMemsetAsync(near_cnt, 0, 16, s);
+#define DR_KM3(KTV, DB) kmeans_mfma_kernel<KTV, DB><<<g3, 256, 0, s>>>(X, n, C, cnorm_ws, K, assign, gsum, gcnt, 256)
+    if (K <= 32) {
+      DR_KM3(1, 0);
+    } else {
+      switch (dbg & 7) {
+        case 1: DR_KM3(2, 1); break;
+        case 4: DR_KM3(2, 4); break;
+        case 6: DR_KM3(2, 6); break;
+        case 7: DR_KM3(2, 7); break;
+        default: DR_KM3(2, 0); break;
+      }
+    }
+#undef DR_KM3
+    kmeans_near_list<<<grid_for(n, 256, 4096), 256, 0, s>>>(assign, n, near_cnt, near_list);
+    kmeans_rerank_kernel<<<1024, 64, 0, s>>>(X, C, cnorm_ws, K, near_cnt, near_list, assign, gsum, gcnt);
+    DR_LAUNCH_CHECK();
+    if (dbg & 8) {
+      uint32_t v = 0;
+      hipMemcpyAsync(&v, near_cnt, 4, hipMemcpyDeviceToHost, s);
+      hipStreamSynchronize(s);
+      fprintf(stderr, "[kmeans] near-tie points re-ranked: %u of %llu\n", v, (unsigned long long)n);
+    }
+    return 0;
   }
   const uint64_t tiles = (n + kPts - 1) / kPts;
   const uint64_t cap = (uint64_t)num_cus() * (mode == 2 ? 2 : 1);

@@ -18,7 +18,8 @@ DIM = 128
 
 _lib.register_signatures({
     "dr_kmeans_mode": (c_i32, [c_i32]),
-    "dr_kmeans_step": (c_i32, [vp, c_u64, c_i32, vp, c_i32, vp, vp, vp, vp, vp]),
+    "dr_kmeans_step": (c_i32, [vp, c_u64, c_i32, vp, c_i32, vp, vp, vp, vp, vp, vp]),
+    "dr_kmeans_near_workspace": (c_u64, [c_u64]),
     "dr_kmeans_gen": (c_i32, [vp, c_u64, c_i32, c_u64, c_i32, c_u64, vp]),
 })
 
@@ -32,10 +33,14 @@ class KMeansWorkspace:
         self.assign = torch.empty(n, dtype=torch.int32, device=device)
         self.sums = torch.empty((k, DIM), dtype=torch.float64, device=device)
         self.counts = torch.empty(k, dtype=torch.int64, device=device)
+        # near-tie list of the K <= 64 bf16-MFMA path (count + (point, estimate) pairs)
+        self.near = torch.empty(int(_lib.lib().dr_kmeans_near_workspace(c_u64(n))) if k <= 64 else 16,
+                                dtype=torch.uint8, device=device)
 
 
 def mode(k: int) -> int:
-    """0: centroids + accumulator slab in LDS; 1: streamed centroid tiles + slab; 2: two-pass."""
+    """0: centroids + accumulator slab in LDS; 1: streamed centroid tiles + slab; 2: two-pass;
+    3: K <= 64 on bf16 MFMA (split-precision distances, exact re-rank of near ties, MFMA sums)."""
     return int(_lib.lib().dr_kmeans_mode(k))
 
 
@@ -60,7 +65,7 @@ def step(points: torch.Tensor, centroids: torch.Tensor, ws: KMeansWorkspace | No
     ws.sums.zero_()
     ws.counts.zero_()
     _lib.call("dr_kmeans_step", ptr(points), c_u64(n), DIM, ptr(centroids), k, ptr(ws.cnorm), ptr(ws.assign),
-              ptr(ws.sums), ptr(ws.counts), stream_of(points))
+              ptr(ws.sums), ptr(ws.counts), ptr(ws.near), stream_of(points))
     return ws.sums, ws.counts, ws.assign[:n]
 
 

@@ -49,3 +49,28 @@ def test_kmeans_converges_on_blobs():
     _, _, a, d = KM.step_reference(x, c)
     inertia = d.min(1).values + (x * x).sum(1)
     assert float(inertia.mean()) < 1.0   # blobs have per-dim noise 0.2*U(-.5,.5): within-blob MSE ~0.43
+
+
+@pytest.mark.parametrize("k", [2, 40])
+def test_kmeans_mfma_near_ties_rerank_exactly(k):
+    """Points just off the bisector of two close centroids: the split-bf16 distance estimate
+    cannot order them (its error bound is ~100x the margin), the exact f32 re-rank must."""
+    from dryad_amd.ops import kmeans as KM
+    g = torch.Generator().manual_seed(1)
+    c = (torch.rand((k, KM.DIM), generator=g, dtype=torch.float64) * 10 - 5)
+    u = torch.randn(KM.DIM, generator=g, dtype=torch.float64)
+    u /= u.norm()
+    c[1] = c[0] + u
+    n = 4096
+    eps = (torch.rand(n, generator=g, dtype=torch.float64) - 0.5) * 0.04
+    eps[eps.abs() < 0.004] = 0.004
+    x = (c[0] + c[1]) / 2 + eps[:, None] * u[None, :]
+    xf, cf = x.float().cuda(), c.float().cuda()
+    assert KM.mode(k) == 3
+    sums, counts, assign = KM.step(xf, cf)
+    d = ((xf.double()[:, None, :] - cf.double()[None, :, :]) ** 2).sum(-1)
+    exp = torch.argmin(d, 1)
+    assert torch.equal(assign.long().cpu(), exp.cpu())
+    assert int(counts.sum()) == n
+    ref = torch.zeros((k, KM.DIM), dtype=torch.float64, device="cuda").index_add_(0, exp, xf.double())
+    torch.testing.assert_close(sums, ref, rtol=1e-5, atol=1e-3)
