@@ -106,6 +106,8 @@ _DEFAULTS = dict(
     ApplicationMasterMbMemory=None,
     GraphManagerNode=None,
     FaultInjection=None,          # [{stage, partition, version, kind}] (SURVEY §5.3 FaultInjector)
+    HbmBudgetBytes=None,          # HBM an out-of-core operator may use per GPU (None: 80% of free HBM)
+    ExternalSort=None,            # out-of-core OrderBy to host:// (None: when the data exceeds the budget)
 )
 
 _READONLY_AFTER_USE = set(_DEFAULTS) - {"LocalDebug"}

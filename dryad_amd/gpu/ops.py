@@ -220,6 +220,19 @@ def op_read(op, inputs, v):
             return DeviceTable.from_columns({"v": a}, Shape("scalar", ["v"]))
     if scheme == "hbm":
         return provider_for(uri).get(uri)["local"][v.partition]
+    if scheme == "host":
+        from ..io.hosttable import HostRows
+        from ..ops.extsort import _copy
+        b = provider_for(uri).get(uri)["local"].get(v.partition)
+        if isinstance(b, HostRows):
+            # pinned host tier -> HBM (one DMA; a following OrderBy sorts the pooled rows in place)
+            rows = v.alloc_rows(b.n, b.stride)
+            _copy(rows, b.rows, None)
+            return DeviceTable(b.n, Shape("rows", key_off=b.key_off, key_len=b.key_len), rows=rows)
+        t = from_objects(list(b or []), op.get("dtype"), v.device)
+        if t is None:
+            raise NotTraceable("non-columnar host records")
+        return t
     if scheme == "text":
         # raw bytes -> HBM heap -> line (offset, length) pairs on the device
         from ..ops import text as TX

@@ -1,0 +1,82 @@
+"""Pinned host tier of the storage hierarchy: fixed-width row tables in page-locked host DRAM.
+
+SURVEY §5.4/§5.7 plan the channel tiers HBM -> pinned host -> disk.  HBM tables
+(``hbm://``, gpu/table.DeviceTable) hold what fits on the GPUs; a ``HostRows`` table holds a
+partition that does not (the output of an out-of-core sort, a spilled intermediate) in memory the
+DMA engines can read and write directly, so PCIe copies run at full rate in both directions
+without a bounce buffer.  The reference's equivalent is the spill of sorted runs to temp files in
+``ParallelSort`` (LinqToDryad/DryadLinqVertex.cs:9584-9615, FileEnumerable :10733) — here the
+"file" is a page-locked host buffer and the runs are range buckets (ops/extsort.py).
+"""
+from __future__ import annotations
+
+import torch
+
+_PINNED: dict = {}        # data_ptr -> nbytes of the page-locked tables alive in this process
+
+
+def is_registered(t: torch.Tensor) -> bool:
+    """True if ``t`` lies inside a page-locked HostRows buffer (DMA-able without staging)."""
+    p = t.data_ptr()
+    return any(a <= p < a + nb for a, nb in _PINNED.items())
+
+
+class HostRows:
+    """``n`` fixed-width rows of ``stride`` bytes in (when a GPU is present) page-locked host memory.
+
+    ``rows`` is a CPU uint8 tensor ``[n, stride]``; records read back as ``bytes`` objects like the
+    rows of a device row table (gpu/table.DeviceTable.to_objects)."""
+
+    def __init__(self, n: int, stride: int, key_off: int = 0, key_len: int | None = None, pinned: bool | None = None):
+        self.n, self.stride = int(n), int(stride)
+        self.key_off, self.key_len = key_off, key_len or stride
+        if pinned is None:
+            pinned = torch.cuda.is_available()
+        self._buf = None
+        if pinned and self.n * self.stride > 0:
+            from ..ops._lib import PinnedHostBuffer
+            self._buf = PinnedHostBuffer((self.n, self.stride))
+            self.rows = self._buf.tensor
+            _PINNED[self.rows.data_ptr()] = self.n * self.stride
+        else:
+            self.rows = torch.empty((self.n, self.stride), dtype=torch.uint8)
+        self.pinned = self._buf is not None
+
+    @staticmethod
+    def from_tensor(rows: torch.Tensor, key_off: int = 0, key_len: int | None = None, pinned: bool | None = None):
+        """Copy a [n, stride] uint8 tensor (host or device) into a new host table."""
+        h = HostRows(rows.shape[0], rows.shape[1], key_off, key_len, pinned)
+        if h.n:
+            h.rows.copy_(rows)
+        return h
+
+    def view(self, n: int) -> "HostRows":
+        """A non-owning table over the first ``n`` rows (reusing a preallocated output)."""
+        v = HostRows.__new__(HostRows)
+        v.n, v.stride, v.key_off, v.key_len = int(n), self.stride, self.key_off, self.key_len
+        v._buf, v.rows, v.pinned = None, self.rows[:n], self.pinned
+        return v
+
+    @property
+    def nbytes(self) -> int:
+        return self.n * self.stride
+
+    def slice(self, a: int, b: int) -> torch.Tensor:
+        return self.rows[a:b]
+
+    def to_objects(self) -> list:
+        if self.n == 0:
+            return []
+        a = self.rows.numpy()
+        return [bytes(r) for r in a]
+
+    def release(self):
+        if self._buf is not None:
+            _PINNED.pop(self.rows.data_ptr(), None)
+            self._buf.release()
+            self._buf = None
+        self.rows = None
+        self.n = 0
+
+    def __len__(self):
+        return self.n

@@ -258,6 +258,62 @@ class HbmProvider(DataProvider):
         return "hbm://" + name
 
 
+class HostProvider(DataProvider):
+    """Pinned-host tables (the tier between HBM and disk, io/hosttable.py): ``{name: entry}`` with
+    ``entry["local"][p]`` = a ``HostRows`` row table or a record list for each partition this
+    process holds.  Out-of-core sorts (ops/extsort.py) write their output here; on the object
+    executors ``host://`` behaves like ``mem://``."""
+    scheme = "host"
+    tables: dict = {}
+
+    def _name(self, uri):
+        return parse_uri(uri)[1]
+
+    def stream_info(self, uri):
+        t = self.get(uri)
+        return t["partitions"], sum(getattr(v, "nbytes", 0) for v in t["local"].values())
+
+    def exists(self, uri):
+        return self._name(uri) in self.tables
+
+    def delete(self, uri):
+        ent = self.tables.pop(self._name(uri), None)
+        if ent is not None:
+            for v in ent["local"].values():
+                if hasattr(v, "release"):
+                    v.release()
+
+    def put(self, uri, entry: dict):
+        if self._name(uri) in self.tables:
+            self.delete(uri)
+        self.tables[self._name(uri)] = entry
+
+    def get(self, uri) -> dict:
+        t = self.tables.get(self._name(uri))
+        if t is None:
+            raise DryadLinqException(0, f"no such host table {uri}")
+        return t
+
+    def local_rows(self, uri, i):
+        """The ``HostRows`` of partition i (None if it is held as records)."""
+        from .hosttable import HostRows
+        v = self.get(uri)["local"].get(i)
+        return v if isinstance(v, HostRows) else None
+
+    def read_partition(self, uri, i, dtype):
+        b = self.get(uri)["local"].get(i)
+        if b is None:
+            raise DryadLinqException(0, f"partition {i} of {uri} is not resident in this process")
+        return b.to_objects() if hasattr(b, "to_objects") else list(b)
+
+    def write_table(self, uri, partitions, dtype, delete_if_exists=True):
+        self.put(uri, {"dtype": dtype, "partitions": len(partitions),
+                       "local": {i: list(p) for i, p in enumerate(partitions)}})
+
+    def temp_uri(self, name):
+        return "host://" + name
+
+
 class GenProvider(DataProvider):
     """Synthetic generator stores.  ``gen://range?count=N&partitions=P[&start=S]`` yields ints;
     ``gen://terasort?records=N&partitions=P&seed=S`` yields 100-byte TeraSort records (as bytes on
@@ -427,7 +483,8 @@ class TextProvider(DataProvider):
         return "text://" + os.path.join(root, name)
 
 
-_PROVIDERS = {p.scheme: p for p in (PartfileProvider(), MemProvider(), HbmProvider(), GenProvider(), TextProvider())}
+_PROVIDERS = {p.scheme: p for p in (PartfileProvider(), MemProvider(), HbmProvider(), HostProvider(), GenProvider(),
+                                    TextProvider())}
 _PROVIDERS["file"] = _PROVIDERS["partfile"]
 
 

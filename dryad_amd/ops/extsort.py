@@ -1,0 +1,466 @@
+"""Out-of-core distributed sort of fixed-width row tables: HBM -> pinned host DRAM spill.
+
+The in-HBM OrderBy (ops/recordsort.distributed_sort_rows) needs input rows + output rows + entry
+arrays resident at once, ~2.3x the data.  A partition larger than that (the 1- and 2-GPU points of
+a 1 TB TeraSort) is sorted here in range buckets that each fit the HBM budget.  The
+reference does the same job on the CPU with sorted 2M-element runs spilled to temp files and a
+<=16-way merge (``ParallelSort`` + ``FileEnumerable``, LinqToDryad/DryadLinqVertex.cs:9366-9367,
+9584-9615, 10733); on MI355X a *sample-partition* external sort is cheaper than a merge: every row
+crosses PCIe exactly twice in each direction and each bucket is one in-HBM radix sort.
+
+Per rank (one process per GPU, W ranks):
+
+  0. sample    — deterministic strided sample of the local rows (host sources: read straight out of
+                 host memory; generator sources: one generate pass), all-gathered and sorted on the
+                 GPU; W*P-1 separators cut the key space into P buckets per rank, each sized to ~70%
+                 of what one in-HBM sort can hold                                   [HIP + RCCL]
+  1. count     — stream the input chunk by chunk (host -> HBM DMA or the fused generator): extract
+                 the key entries, range destination, histogram per (chunk, bucket); all-gathered, so
+                 every rank knows every piece's size and final host offset up front      [HIP]
+  2. partition — stream the input again: LDS-staged bucket scatter of whole rows
+                 (dr_bucket_scatter_rows); W > 1: one all-to-all-v per chunk over xGMI; the bucket
+                 pieces go straight to their final host region by DMA on a copy stream that runs
+                 under the next chunk's kernels                                  [HIP + RCCL + DMA]
+  3. sort      — per bucket: host -> HBM, hybrid/compact radix sort + row gather, HBM -> host in
+                 place; the next bucket's upload and the previous bucket's download overlap the
+                 sort (two copy streams, both PCIe directions busy)                     [HIP + DMA]
+
+Equal keys are split across buckets (and ranks) by a (chunk, rank, row) tie tag in the spare entry
+bits, so skewed keys still fit; the order is then the source order, i.e. the sort is stable.  With
+``keep_ties`` the rank boundaries keep every run of equal keys on one rank (the planner's
+partitioned-by-key guarantee, DataSetInfo), only the buckets inside a rank split them.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from ..io.hosttable import HostRows, is_registered
+from ..parallel import shuffle
+from ..parallel.comm import World, get_world
+from . import _lib
+from . import recordsort as RS
+from . import sort as S
+
+_M64 = (1 << 64) - 1
+FILL_TARGET = 0.7            # planned bucket size as a fraction of one in-HBM sort's capacity
+
+
+def _i64(v: int) -> int:
+    v &= _M64
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+@dataclass
+class ExtSortStats:
+    n_in: int = 0
+    n_out: int = 0
+    chunks: int = 0
+    chunk_rows: int = 0
+    buckets: int = 0
+    bucket_cap: int = 0
+    max_bucket: int = 0
+    bytes_h2d: int = 0
+    bytes_d2h: int = 0
+    seconds: dict = field(default_factory=dict)
+
+
+# ------------------------------------------------------------------------------------------------
+# chunked sources
+class ChunkSource:
+    """A partition read chunk by chunk into HBM.  ``fill(lo, hi, out, copy_stream)`` writes rows
+    [lo, hi) into ``out`` (device rows) and returns the stream the data is ready on
+    (``None`` = the current stream)."""
+    n: int = 0
+    stride: int = 0
+    dma = False          # fill is a host -> device copy (counts toward bytes_h2d)
+
+    def fill(self, lo: int, hi: int, out: torch.Tensor, copy_stream):
+        raise NotImplementedError
+
+    def sample_rows(self, idx: torch.Tensor, scratch: torch.Tensor, chunk_rows: int) -> torch.Tensor:
+        """Device rows at the sorted local indices ``idx`` (int64, host).  Default: stream every
+        chunk that holds a sampled row through ``scratch`` and pick the rows on the device."""
+        dev = scratch.device
+        parts = []
+        for c0 in range(0, self.n, chunk_rows):
+            c1 = min(self.n, c0 + chunk_rows)
+            sel = idx[(idx >= c0) & (idx < c1)]
+            if sel.numel() == 0:
+                continue
+            st = self.fill(c0, c1, scratch[: c1 - c0], None)
+            if st is not None:
+                torch.cuda.current_stream(dev).wait_stream(st)
+            parts.append(scratch.index_select(0, (sel - c0).to(dev)))
+        if not parts:
+            return torch.empty((0, self.stride), dtype=torch.uint8, device=dev)
+        return torch.cat(parts)
+
+
+class GenTeraSortSource(ChunkSource):
+    """``gen://terasort`` rows [first, first + n) produced by the HIP generator in place."""
+
+    def __init__(self, first: int, n: int, seed: int):
+        from . import terasort as TS
+        self.TS = TS
+        self.first, self.n, self.seed, self.stride = first, n, seed, TS.RECORD_BYTES
+
+    def fill(self, lo, hi, out, copy_stream):
+        self.TS.generate(out[: hi - lo], self.first + lo, self.seed)
+        return None
+
+
+class HostRowsSource(ChunkSource):
+    """A ``HostRows`` table (pinned host memory): chunks arrive by DMA on the copy stream."""
+    dma = True
+
+    def __init__(self, rows: HostRows):
+        self.rows, self.n, self.stride = rows, rows.n, rows.stride
+
+    def fill(self, lo, hi, out, copy_stream):
+        _copy(out[: hi - lo], self.rows.rows[lo:hi], copy_stream)
+        return copy_stream
+
+    def sample_rows(self, idx, scratch, chunk_rows):
+        return self.rows.rows.index_select(0, idx).to(scratch.device)
+
+
+def _copy(dst: torch.Tensor, src: torch.Tensor, stream):
+    """DMA between a device tensor and a host tensor on ``stream`` (page-locked host memory goes
+    through hipMemcpyAsync directly; anything else through torch)."""
+    host = src if dst.is_cuda else dst
+    if stream is None:
+        stream = torch.cuda.current_stream(dst.device if dst.is_cuda else src.device)
+    if host.numel() == 0:
+        return
+    if is_registered(host) or host.is_pinned():
+        _lib.memcpy_async(dst, src, stream)
+    else:
+        with torch.cuda.stream(stream):
+            dst.copy_(src, non_blocking=False)
+
+
+class _Arena:
+    """One HBM allocation carved into the phase's working buffers (phases reuse the same bytes, so
+    the caching allocator never holds two phases' layouts at once)."""
+
+    def __init__(self, nbytes: int, device):
+        self.buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+        self.off = 0
+
+    def reset(self):
+        self.off = 0
+
+    def take(self, shape, dtype=torch.uint8) -> torch.Tensor:
+        esz = torch.empty(0, dtype=dtype).element_size()
+        nb = esz * math.prod(shape)
+        a = (self.off + 255) & ~255
+        if a + nb > self.buf.numel():
+            raise MemoryError("extsort arena overflow")
+        self.off = a + nb
+        return self.buf[a:a + nb].view(dtype).view(*shape)
+
+
+def default_budget(device) -> int:
+    free, _ = torch.cuda.mem_get_info(device)
+    return int(free * 0.8)
+
+
+def plan_geometry(n_rank_max: int, n_total: int, stride: int, W: int, budget: int):
+    """(chunk_rows, bucket_cap, buckets per rank) for a budget of ``budget`` HBM bytes."""
+    usable = max(budget - (1 << 16), 1 << 16)             # alignment padding of the carved buffers
+    crow = 4 * stride + 16 + (3 * stride if W > 1 else 0)
+    chunk_rows = max(1, min(usable // crow, (1 << 31) - 1, max(n_rank_max, 1)))
+    bucket_cap = max(2, usable // (4 * stride + 32))
+    per_rank = -(-n_total // W)
+    P = max(1, math.ceil(per_rank / (FILL_TARGET * bucket_cap)))
+    if W * P > 256:
+        raise RuntimeError(f"external sort: {n_total} rows of {stride} B need {W * P} range buckets with "
+                           f"a {budget / 1e9:.1f} GB HBM budget (at most 256); raise the budget")
+    return chunk_rows, bucket_cap, P
+
+
+def _separators(srt: torch.Tensor, W: int, P: int, tie_bits: bool, lo_key_mask: int, part_mask: int):
+    """W*P-1 ascending separators from the sorted sample: W-1 rank boundaries at even sample
+    quantiles, then P-1 bucket boundaries at even quantiles of each rank's own share of the sample
+    (so a rank that keeps a long run of equal keys still gets evenly filled buckets).
+    ``tie_bits``: the rank boundaries take every tuple of their key (tie tag all ones)."""
+    dev, T = srt.device, srt.shape[0]
+    none = torch.zeros((0, 2), dtype=torch.int64, device=dev)
+    rsep = srt.index_select(0, torch.tensor([(r * T) // W for r in range(1, W)], dtype=torch.int64,
+                                            device=dev)).clone() if W > 1 else none
+    if tie_bits and W > 1:
+        rsep[:, 0] |= _i64(_M64 & ~lo_key_mask)
+    # each sample's rank = #rank separators strictly below it (the kernel's own comparison)
+    bounds = [0] * (W + 1)
+    bounds[W] = T
+    if W > 1:
+        d = S.range_dest(srt.clone(), rsep, part_mask)[:, 1]
+        cnt = torch.bincount(d, minlength=W).tolist()
+        for r in range(W):
+            bounds[r + 1] = bounds[r] + cnt[r]
+    parts = []
+    for r in range(W):
+        a, b = bounds[r], bounds[r + 1]
+        if P > 1 and b > a:
+            idx = [a + (j * (b - a)) // P for j in range(1, P)]
+            parts.append(srt.index_select(0, torch.tensor(idx, dtype=torch.int64, device=dev)))
+        elif P > 1:       # no sample in this rank's range: its buckets are empty
+            fill = rsep[r:r + 1] if r < W - 1 else (rsep[r - 1:r] if r > 0 else srt[T - 1:T])
+            parts.append(fill.expand(P - 1, 2))
+        if r < W - 1:
+            parts.append(rsep[r:r + 1])
+    return torch.cat(parts).contiguous() if parts else none
+
+
+def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | None = None,
+                  budget: int | None = None, keep_ties: bool = False, sample_target: int = 1 << 20,
+                  seed: int = 314159, stats: ExtSortStats | None = None,
+                  out: HostRows | None = None) -> HostRows:
+    """Globally sort the rows of ``src`` (this rank's partition) by the byte-string key
+    [key_off, key_off + key_len) (memcmp order, key_len <= 12).  Rank r returns the r-th key range
+    as a ``HostRows`` table in pinned host memory.  ``budget``: HBM bytes the sort may use
+    (default 80% of free HBM).  ``out``: a preallocated host table to write into when it is large
+    enough (the result is then a view of its first rows)."""
+    w = world or get_world()
+    W, me = w.size, w.rank
+    dev = w.device if w.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
+    stats = stats if stats is not None else ExtSortStats()
+    stride, n = src.stride, src.n
+    if not 1 <= key_len <= 12 or key_off + key_len > stride:
+        raise ValueError("external_sort: key must be 1..12 bytes inside the row")
+    t_all = time.perf_counter()
+    budget = int(budget or default_budget(dev))
+    tot = torch.tensor([n, n], dtype=torch.int64, device=dev if w.backend == "nccl" else "cpu")
+    nmax = tot[:1].clone()
+    shuffle.all_reduce_(tot[:1], "sum", w)
+    shuffle.all_reduce_(nmax, "max", w)
+    n_total, n_rank_max = int(tot[0]), int(nmax[0])
+    chunk_rows, bucket_cap, P = plan_geometry(n_rank_max, n_total, stride, W, budget)
+    C = max(1, -(-n_rank_max // chunk_rows))
+    C_local = -(-n // chunk_rows)
+    _, _, lo_key_mask = RS.key_bits(key_len)
+    split = key_len <= 10 and C * W < (1 << 16)
+    part_mask = _M64 if split else lo_key_mask
+    stats.n_in, stats.chunks, stats.chunk_rows, stats.buckets, stats.bucket_cap = n, C, chunk_rows, P, bucket_cap
+    arena = _Arena(budget, dev)
+    comp = torch.cuda.current_stream(dev)
+    h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    tag_of = lambda c: ((c * W + me) << 32)  # noqa: E731
+
+    # ---------------------------------------------------------------- 0. sample + separators
+    t0 = time.perf_counter()
+    G = W * P
+    m = min(n, max(256 * G, min(sample_target, max(n // 1000, 16))))
+    seps, srows = None, None
+    arena.reset()
+    scratch = arena.take((chunk_rows, stride))
+    ent = arena.take((chunk_rows, 2), torch.int64)
+    if m > 0:
+        stride_s = max(1, n // m)
+        off = (seed + me * 7919) % stride_s if stride_s > 1 else 0
+        idx = torch.arange(off, n, stride_s, dtype=torch.int64)[:m]
+        srows = src.sample_rows(idx, scratch, chunk_rows)
+        samp = S.extract_keys(srows.contiguous(), key_off, key_len, 0)
+        if split:
+            c_idx = idx // chunk_rows
+            tag = ((c_idx * W + me) << 32) | (idx - c_idx * chunk_rows)
+            samp[:, 0] = (samp[:, 0] & _i64(lo_key_mask)) | tag.to(dev)
+        samp[:, 0] &= _i64(part_mask)
+    else:
+        samp = torch.empty((0, 2), dtype=torch.int64, device=dev)
+    allsamp = shuffle.all_gather_varlen(samp, w)
+    if allsamp.shape[0] == 0:
+        allsamp = torch.zeros((1, 2), dtype=torch.int64, device=dev)
+    srt = S.sort_entries(allsamp.contiguous(), 0, 128, tmp=torch.empty_like(allsamp))
+    seps = _separators(srt, W, P, keep_ties and split, lo_key_mask, part_mask)
+    seps_hi = [int(x) & _M64 for x in seps[:, 1].tolist()]
+    del srows, samp, allsamp, srt
+    stats.seconds["sample"] = time.perf_counter() - t0
+
+    def entries(c, rows_c, out_e):
+        e = S.extract_keys(rows_c, key_off, key_len, 0, out=out_e)
+        if split:
+            e[:, 0].bitwise_or_(tag_of(c))
+        S.range_dest(e, seps, part_mask)
+        return e
+
+    # ---------------------------------------------------------------- 1. count pass
+    t0 = time.perf_counter()
+    counts = torch.zeros((C, G), dtype=torch.int64, device=dev)
+    for c in range(C_local):
+        lo, hi = c * chunk_rows, min(n, (c + 1) * chunk_rows)
+        if src.dma:
+            h2d.wait_stream(comp)          # the previous chunk's extraction has read scratch
+        st = src.fill(lo, hi, scratch, h2d)
+        if st is not None:
+            comp.wait_stream(st)
+            stats.bytes_h2d += (hi - lo) * stride
+        e = entries(c, scratch[: hi - lo], ent[: hi - lo])
+        counts[c] = torch.bincount(e[:, 1], minlength=G)
+    allc = shuffle.all_gather_tensor(counts.unsqueeze(0), w).view(W, C, G).cpu()   # [src, chunk, range]
+    stats.seconds["count"] = time.perf_counter() - t0
+
+    mine = allc[:, :, me * P:(me + 1) * P]                      # [src, chunk, bucket] rows for me
+    rows_b = mine.sum(dim=(0, 1))
+    stats.max_bucket = int(rows_b.max()) if P else 0
+    if stats.max_bucket > bucket_cap:
+        raise RuntimeError(f"external sort: a range bucket holds {stats.max_bucket} rows > {bucket_cap} "
+                           f"(key skew with keep_ties, or too small a sample); raise the HBM budget")
+    n_out = int(rows_b.sum())
+    bucket_off = torch.cumsum(rows_b, 0) - rows_b
+    # host position of piece (s, c, b): bucket start + rows of earlier chunks + earlier sources
+    flat = mine.permute(1, 0, 2).reshape(C * W, P)              # (chunk, src) major order
+    piece_pos = (torch.cumsum(flat, 0) - flat + bucket_off.unsqueeze(0)).view(C, W, P)
+    out = out.view(n_out) if out is not None and out.n >= n_out and out.stride == stride else \
+        HostRows(n_out, stride, key_off, key_len)
+    try:
+        # ------------------------------------------------------------ 2. partition pass
+        t0 = time.perf_counter()
+        arena.reset()
+        rin = [arena.take((chunk_rows, stride)) for _ in range(2)]
+        rout = [arena.take((chunk_rows, stride)) for _ in range(2)]
+        ent = arena.take((chunk_rows, 2), torch.int64)
+        recv = rout
+        if W > 1:
+            rmax = int(mine.sum(dim=2).sum(dim=0).max())        # rows received in one round
+            recv = []
+            for _ in range(2):
+                try:
+                    recv.append(arena.take((max(rmax, 1), stride)))
+                except MemoryError:
+                    recv.append(torch.empty((max(rmax, 1), stride), dtype=torch.uint8, device=dev))
+        ev_in = [torch.cuda.Event() for _ in range(2)]       # rows_in[k] consumed
+        ev_ready = [None, None]                              # rows_in[k] filled (copy stream)
+        ev_out = [torch.cuda.Event() for _ in range(2)]      # scatter / exchange of round k done
+        ev_d2h = [torch.cuda.Event() for _ in range(2)]      # round k's pieces downloaded
+        for k in range(2):
+            ev_in[k].record(comp)
+            ev_d2h[k].record(d2h)
+
+        def prefetch(c):
+            if c >= C_local:
+                return
+            k = c % 2
+            lo, hi = c * chunk_rows, min(n, (c + 1) * chunk_rows)
+            if src.dma:
+                h2d.wait_event(ev_in[k])
+                src.fill(lo, hi, rin[k], h2d)
+                ev = torch.cuda.Event()
+                ev.record(h2d)
+                ev_ready[k] = ev
+                stats.bytes_h2d += (hi - lo) * stride
+            else:
+                src.fill(lo, hi, rin[k], None)
+                ev_ready[k] = None
+
+        prefetch(0)
+        for c in range(C):
+            k = c % 2
+            prefetch(c + 1)
+            cn = min(n, (c + 1) * chunk_rows) - c * chunk_rows if c < C_local else 0
+            if ev_ready[k] is not None:
+                comp.wait_event(ev_ready[k])
+                ev_ready[k] = None
+            comp.wait_event(ev_d2h[k])
+            if cn > 0:
+                e = entries(c, rin[k][:cn], ent[:cn])
+                S.bucket_scatter_rows(e, rin[k][:cn], rout[k], sync=False)
+            ev_in[k].record(comp)
+            if W > 1:
+                sc = allc[me, c].view(W, P).sum(1).tolist()
+                rc = allc[:, c, me * P:(me + 1) * P].sum(1).tolist()
+                shuffle.alltoallv_bytes(rout[k].view(-1), [x * stride for x in sc], recv[k].view(-1),
+                                        [x * stride for x in rc], w)
+            ev_out[k].record(comp)
+            d2h.wait_event(ev_out[k])
+            # pieces of round c: W == 1 -> bucket b of the local chunk; W > 1 -> (src, bucket)
+            a = 0
+            for s_ in range(W):
+                for b in range(P):
+                    cnt = int(mine[s_, c, b])
+                    if cnt:
+                        p0 = int(piece_pos[c, s_, b])
+                        _copy(out.rows[p0:p0 + cnt], recv[k][a:a + cnt], d2h)
+                        stats.bytes_d2h += cnt * stride
+                    a += cnt
+            ev_d2h[k].record(d2h)
+        torch.cuda.synchronize(dev)
+        stats.seconds["partition"] = time.perf_counter() - t0
+
+        # ------------------------------------------------------------ 3. sort each bucket
+        t0 = time.perf_counter()
+        arena.reset()
+        cap = max(2, stats.max_bucket)
+        bin_ = [arena.take((cap, stride)) for _ in range(2)]
+        bout = [arena.take((cap, stride)) for _ in range(2)]
+        ea = arena.take((cap, 2), torch.int64)
+        eb = arena.take((cap, 2), torch.int64)
+        ev_up = [None, None]
+        ev_sorted = [torch.cuda.Event() for _ in range(2)]
+        ev_down = [torch.cuda.Event() for _ in range(2)]
+        for k in range(2):
+            ev_sorted[k].record(comp)
+            ev_down[k].record(d2h)
+        sizes = [int(x) for x in rows_b.tolist()]
+        offs = [int(x) for x in bucket_off.tolist()]
+
+        def upload(b):
+            if b >= P or sizes[b] == 0:
+                return
+            k = b % 2
+            h2d.wait_event(ev_sorted[k])
+            _copy(bin_[k][: sizes[b]], out.rows[offs[b]: offs[b] + sizes[b]], h2d)
+            ev = torch.cuda.Event()
+            ev.record(h2d)
+            ev_up[k] = ev
+            stats.bytes_h2d += sizes[b] * stride
+
+        upload(0)
+        for b in range(P):
+            k = b % 2
+            upload(b + 1)
+            mb = sizes[b]
+            if mb == 0:
+                continue
+            comp.wait_event(ev_up[k])
+            comp.wait_event(ev_down[k])
+            hb = RS._range_hi_bounds(seps_hi, me * P + b)
+            res = RS.local_sort_rows(bin_[k][:mb], bout[k], ea, eb, key_off, key_len, hi_bounds=hb)
+            ev_sorted[k].record(comp)
+            d2h.wait_event(ev_sorted[k])
+            _copy(out.rows[offs[b]: offs[b] + mb], res[:mb], d2h)
+            ev_down[k].record(d2h)
+            stats.bytes_d2h += mb * stride
+        torch.cuda.synchronize(dev)
+        stats.seconds["sort"] = time.perf_counter() - t0
+    finally:
+        del arena
+    stats.n_out = n_out
+    stats.seconds["total"] = time.perf_counter() - t_all
+    return out
+
+
+def check_terasort_host(out: HostRows, chunk_rows: int = 1 << 24) -> tuple[int, int, bytes, bytes]:
+    """valsort over a host TeraSort table: (hash sum mod 2^64, order violations incl. chunk
+    boundaries, first key, last key), streamed through HBM in chunks."""
+    from . import terasort as TS
+    dev = torch.device("cuda", torch.cuda.current_device())
+    acc = torch.zeros(2, dtype=torch.int64, device=dev)
+    buf = torch.empty((min(max(out.n, 1), chunk_rows), out.stride), dtype=torch.uint8, device=dev)
+    prev, bad = None, 0
+    for a in range(0, out.n, chunk_rows):
+        b = min(out.n, a + chunk_rows)
+        _copy(buf[: b - a], out.rows[a:b], None)
+        TS.check(buf[: b - a], acc)
+        first = bytes(out.rows[a, :TS.KEY_BYTES].numpy())
+        if prev is not None and prev > first:
+            bad += 1
+        prev = bytes(out.rows[b - 1, :TS.KEY_BYTES].numpy())
+    torch.cuda.synchronize(dev)
+    h, v = acc.tolist()
+    first = bytes(out.rows[0, :TS.KEY_BYTES].numpy()) if out.n else b""
+    return h & _M64, v + bad, first, prev or b""

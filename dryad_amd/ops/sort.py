@@ -227,23 +227,24 @@ def range_dest(entries: torch.Tensor, separators: torch.Tensor, lo_mask: int, de
     return out
 
 
-def bucket_scatter_rows(entries: torch.Tensor, rows: torch.Tensor, out: torch.Tensor) -> list:
+def bucket_scatter_rows(entries: torch.Tensor, rows: torch.Tensor, out: torch.Tensor, sync: bool = True):
     """Stable scatter of fixed-width ``rows`` into bucket order, bucket = low byte of
     ``entries[i].hi`` (row i <-> entry i), into ``out``.  Returns the 257 bucket start offsets
-    (host list).  One coalesced LDS-staged pass over the rows (dr_bucket_scatter_rows) instead of
-    a partition pass of the entries plus a row gather through them."""
+    (host list; ``sync=False``: the device int64 tensor, no host synchronisation).  One coalesced
+    LDS-staged pass over the rows (dr_bucket_scatter_rows) instead of a partition pass of the
+    entries plus a row gather through them."""
     _lib.require_gpu_tensor(rows, "bucket_scatter_rows")
     assert rows.dtype == torch.uint8 and rows.dim() == 2 and out.shape[0] >= rows.shape[0]
     n, stride = rows.shape
     if stride % 4 or stride > 128:
         part, starts = partition_pass(entries[:n], 64)
         gather_rows(rows, entries=part, out=out[:n])
-        return starts.tolist()
+        return starts.tolist() if sync else starts
     starts = torch.empty(257, dtype=torch.int64, device=rows.device)
     ws = _workspace(n, rows.device)
     _lib.call("dr_bucket_scatter_rows", ptr(entries), ptr(rows), ptr(out), c_u64(n), c_u32(stride), ptr(ws),
               ptr(starts), stream_of(rows))
-    return starts.tolist()
+    return starts.tolist() if sync else starts
 
 
 def entries_to_key_int(entries: torch.Tensor, lo_keep_bits: int = 64):

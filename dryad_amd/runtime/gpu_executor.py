@@ -29,6 +29,8 @@ from ..gpu import ops as G
 from ..attributes import is_device_function
 from ..gpu.table import DeviceTable, Ported, from_objects
 from ..gpu.trace import NotTraceable
+from ..io.hosttable import HostRows
+from ..ops import extsort as EX
 from ..io.providers import parse_uri, provider_for
 from ..native import runtime as native_runtime
 from ..parallel import shuffle
@@ -182,6 +184,95 @@ class GpuJobRunner:
         for op in m.ops[1:]:
             data = self._run_op(op, [data], vctx, m)
         return data
+
+    # ------------------------------------------------------------------ out-of-core OrderBy
+    def _plan_external(self):
+        """OrderBy jobs whose partitions do not fit the HBM budget: ``read -> sort -> output`` (one
+        partition per rank) or the distributed idiom over such a read, writing a ``host://``
+        table.  They run as ops/extsort.external_sort, streaming the source through HBM in chunks
+        and spilling range buckets to pinned host memory (the reference's ParallelSort spill,
+        DryadLinqVertex.cs:9584-9615).  ``ExternalSort`` (context property) forces (True) or
+        forbids (False) the path; otherwise it is taken when rows in + out + entries would exceed
+        ``HbmBudgetBytes`` (default 80% of free HBM)."""
+        props = self.ctx._props
+        force = props.get("ExternalSort")
+        if force is False or not self.gpu_ok:
+            return {}
+        st, W = self.plan.stages, self.world.size
+        cands = {}
+        for s in st:
+            if (not s.inputs and len(s.ops) >= 2 and s.ops[0]["op"] == "read" and s.ops[1]["op"] == "sort"
+                    and all(op["op"] == "output" for op in s.ops[2:]) and s.is_output and s.partitions == W):
+                cands[s.id] = dict(read=s.ops[0], sort=s.ops[1], skip=[], keep_ties=False)
+        for mid, f in self.fused.items():
+            m, x = st[mid], st[f["x"]]
+            if (not x.inputs and len(x.ops) == 1 and x.ops[0]["op"] == "read" and m.is_output
+                    and all(op["op"] == "output" for op in m.ops[1:]) and x.partitions == W
+                    and set(self.plan.consumers(x.id)) == {f["stages"][0], f["stages"][2]}):
+                cands[mid] = dict(read=x.ops[0], sort=m.ops[0], skip=[x.id] + f["stages"], keep_ties=f["keep_ties"])
+        out = {}
+        for sid, c in sorted(cands.items()):
+            sort = c["sort"]
+            ok = parse_uri(st[sid].output["uri"])[0] == "host" and sort.get("comparer") is None \
+                and not sort.get("descending", False)
+            src = self._chunk_source(c["read"]) if ok else None
+            spec = None
+            if src is not None:
+                spec = self._external_key(src, c["read"], sort["key"])
+                budget = props.get("HbmBudgetBytes")
+                need = src.n * (2 * src.stride + 32) * 1.05
+                ok = spec is not None and (force is True or need > int(budget or EX.default_budget(self.dev)))
+            else:
+                ok = False
+            votes = [(ok, spec)]
+            if W > 1:
+                votes = [None] * W
+                dist.all_gather_object(votes, (ok, spec))
+            if all(v[0] for v in votes) and len({v[1] for v in votes}) == 1:
+                out[sid] = dict(c, source=src, spec=spec)
+        return out
+
+    def _chunk_source(self, op):
+        uri = op["uri"]
+        scheme, path, q = parse_uri(uri)
+        me = self.world.rank
+        if scheme == "gen" and path.strip("/") == "terasort":
+            from ..io.providers import GenProvider
+            lo, hi = GenProvider().bounds(uri, me)
+            return EX.GenTeraSortSource(lo, hi - lo, int(q.get("seed", 0)))
+        if scheme == "host":
+            prov = provider_for(uri)
+            h = prov.local_rows(uri, me) if prov.exists(uri) else None
+            return EX.HostRowsSource(h) if h is not None and h.stride % 4 == 0 else None
+        return None
+
+    def _external_key(self, src, read_op, key):
+        """(key offset, key length) of a byte-string key selector over the source's rows."""
+        from ..gpu import trace as TR
+        from ..gpu.table import Shape
+        k = max(1, min(src.n, 2))
+        rows = torch.zeros((k, src.stride), dtype=torch.uint8, device=self.dev)
+        if src.n:
+            src.fill(0, k, rows, None)
+        h = getattr(src, "rows", None)
+        shape = Shape("rows", key_off=h.key_off, key_len=h.key_len) if h is not None else \
+            Shape("rows", key_off=0, key_len=10)
+        try:
+            kind, spec = TR.key_columns(TR.call(key, DeviceTable(k, shape, rows=rows)), DeviceTable(k, shape, rows=rows))
+        except Exception:  # noqa: BLE001
+            return None
+        return (spec.off, spec.length) if kind == "bytes" and spec.length <= 12 else None
+
+    def _run_external(self, s, e):
+        if self.pool is not None:
+            self.pool.clear()           # idle pooled sort buffers give their HBM back
+            torch.cuda.empty_cache()
+        off, ln = e["spec"]
+        st = EX.ExtSortStats()
+        out = EX.external_sort(e["source"], off, ln, self.world, budget=self.ctx._props.get("HbmBudgetBytes"),
+                               keep_ties=e["keep_ties"], stats=st)
+        self.extsort_stats = st
+        return out
 
     def _sources(self, si, p):
         src = self.plan.stages[si.src]
@@ -451,6 +542,10 @@ class GpuJobRunner:
                 ready[it.vertex] = it.version
 
         self.fused = self._find_fused_orderby()
+        self.external = self._plan_external()
+        for sid, e in self.external.items():
+            self.fused.pop(sid, None)
+            self.skipped.update(e["skip"])
         fused_first = {f["stages"][0]: mid for mid, f in self.fused.items()}
         active_fused = {}
         for s in self.plan.stages:
@@ -469,6 +564,23 @@ class GpuJobRunner:
                     g.on_running(vid, ver, self.owner(p), now())
                     g.on_completed(vid, ver, now(), 0, 0)
                 self.timings[f"{s.id}:{s.name}(fused)"] = 0.0
+                continue
+            if s.id in self.external:
+                refresh()
+                vid = self.vids[s.id][me]
+                ver = ready.pop(vid)
+                g.on_running(vid, ver, me, now())
+                out = self._run_external(s, self.external[s.id])
+                self.channels[(s.id, me)] = out
+                g.on_completed(vid, ver, now(), 0, out.nbytes)
+                for p in range(s.partitions):
+                    if p != me:
+                        v2 = self.vids[s.id][p]
+                        ver2 = ready.pop(v2)
+                        g.on_running(v2, ver2, self.owner(p), now())
+                        g.on_completed(v2, ver2, now(), 0, 0)
+                self._release(s)
+                self.timings[f"{s.id}:{s.name}(out-of-core OrderBy)"] = time.time() - t0
                 continue
             if s.id in active_fused:
                 refresh()
@@ -534,7 +646,8 @@ class GpuJobRunner:
             for b in set(self.row_sets.values()):
                 self.pool.release(b)
         return dict(committed=committed, fallbacks=self.fallbacks, timings=self.timings,
-                    statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()])
+                    statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()],
+                    external_sort=getattr(self, "extsort_stats", None))
 
     def _release(self, s):
         later = {i.src for st in self.plan.stages if st.id > s.id for i in st.inputs}
@@ -562,6 +675,18 @@ class GpuJobRunner:
                                             "owner_of": {p: self.owner(p) for p in range(s.partitions)},
                                             "bytes": sum(_object_bytes(v) for v in tabs.values()),
                                             "pins": pins, "pool": self.pool})
+                committed[uri] = s.partitions
+            elif scheme == "host":
+                tabs = {}
+                for p, v in local.items():
+                    if isinstance(v, HostRows):
+                        tabs[p] = v
+                    elif isinstance(v, DeviceTable) and v.rows is not None and v.device.type == "cuda":
+                        tabs[p] = HostRows.from_tensor(v.rows, v.shape.key_off, v.shape.key_len)
+                    else:
+                        tabs[p] = _to_objects(v) if not isinstance(v, list) else v
+                provider_for(uri).put(uri, {"dtype": s.dtype, "partitions": s.partitions, "local": tabs,
+                                            "owner_of": {p: self.owner(p) for p in range(s.partitions)}})
                 committed[uri] = s.partitions
             elif scheme in ("partfile", "file") and self._commit_partfile(s, uri, path, local):
                 committed[uri] = s.partitions
@@ -676,7 +801,7 @@ class GpuExecutor(_BaseExecutor):
         plan = compile_queries(self.ctx, outs)
         faults = self.ctx._props.get("FaultInjection") or []
         for st in plan.stages:      # CheckExistence(deleteIfExists) at submission
-            if st.is_output and st.output["uri"].startswith("hbm://"):
+            if st.is_output and st.output["uri"].startswith(("hbm://", "host://")):
                 prov = provider_for(st.output["uri"])
                 if prov.exists(st.output["uri"]):
                     if st.output.get("delete_if_exists") or st.output.get("temp"):
@@ -750,7 +875,7 @@ class GpuExecutor(_BaseExecutor):
             provider_for(tmp).delete(tmp)
 
     def _read_back(self, uri, dtype):
-        if not uri.startswith("hbm://"):
+        if not uri.startswith(("hbm://", "host://")):
             return list(provider_for(uri).read_all(uri, dtype))
         ent = provider_for(uri).get(uri)
         mine = {p: _to_objects(v) if not isinstance(v, list) else v for p, v in ent["local"].items()}

@@ -84,6 +84,46 @@ def main():
         assert res == job.expected() and res[0] == 300_000, (w.rank, res)
         assert (job.last["spilled_bytes"] > 0) == (budget is not None), job.last
         job.release()
+    # out-of-core sort across ranks: one all-to-all-v per chunk round, buckets spilled to pinned host
+    # memory and sorted bucket by bucket; checksum, count, in-rank order and rank boundaries
+    import numpy as np
+    from dryad_amd.ops import extsort as EX
+    m64 = (1 << 64) - 1
+    s64 = lambda v: (v & m64) - (1 << 64) if (v & m64) >= (1 << 63) else (v & m64)  # noqa: E731
+    n = 300_000 if w.rank == 0 else 200_000
+    st = EX.ExtSortStats()
+    out = EX.external_sort(EX.GenTeraSortSource(w.rank * 1_000_000, n, 99), 0, 10, w, budget=16 << 20, stats=st)
+    assert st.chunks > 1 and st.buckets > 1, st
+    h, bad, first, last = EX.check_terasort_host(out, 100_000)
+    rows = torch.empty((n, 100), dtype=torch.uint8, device=w.device)
+    TS.generate(rows, w.rank * 1_000_000, 99)
+    hin = int(TS.check(rows)[0].item())
+    del rows
+    tot = torch.tensor([s64(hin), s64(h), out.n, bad], dtype=torch.int64, device=w.device)
+    shuffle.all_reduce_(tot, "sum", w)
+    assert int(tot[0]) == int(tot[1]) and int(tot[2]) == 500_000 and int(tot[3]) == 0, tot.tolist()
+    ends = torch.zeros((1, 20), dtype=torch.uint8, device=w.device)
+    ends[0, :10] = torch.frombuffer(bytearray(first), dtype=torch.uint8)
+    ends[0, 10:] = torch.frombuffer(bytearray(last), dtype=torch.uint8)
+    allends = shuffle.all_gather_tensor(ends, w).cpu().numpy()
+    for r in range(w.size - 1):
+        assert bytes(allends[r, 10:]) <= bytes(allends[r + 1, :10]), r
+    # keep_ties: every run of equal keys stays on one rank (a following GroupBy skips its shuffle)
+    from dryad_amd.io.hosttable import HostRows
+    g = np.random.default_rng(w.rank + 1)
+    a = g.integers(0, 256, size=(120_000, 16), dtype=np.uint8)
+    a[:, :10] = g.integers(0, 5, size=(120_000, 1), dtype=np.uint8)
+    out = EX.external_sort(EX.HostRowsSource(HostRows.from_tensor(torch.from_numpy(a), 0, 10)), 0, 10, w,
+                           budget=2 << 20, keep_ties=True)
+    mine = sorted({bytes(r) for r in out.rows[:, :10].numpy()})
+    got = [None] * w.size
+    import torch.distributed as dist
+    dist.all_gather_object(got, mine)
+    seen = [k for ks in got for k in ks]
+    assert len(seen) == len(set(seen)) and len(seen) == 5, got
+    cnt = torch.tensor([out.n], dtype=torch.int64, device=w.device)
+    shuffle.all_reduce_(cnt, "sum", w)
+    assert int(cnt) == 120_000 * w.size
     w.barrier()
     if w.rank == 0:
         print("MULTIRANK_OK", w.size, flush=True)
