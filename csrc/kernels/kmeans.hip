@@ -320,17 +320,19 @@ __global__ __launch_bounds__(256) void kmeans_mfma_kernel(const float* __restric
 #pragma unroll
     for (int q = 0; q < 4; ++q) S[ct][q] = f32x16{};
   float xr[64];
-  auto load = [&](uint64_t tile, float* dst) {
+  // the 8 dims 16 s + 8 h .. + 7 of point r of `tile` into dst[8 s .. 8 s + 7]
+  auto load_part = [&](uint64_t tile, int s, float* dst) {
     const uint64_t p = tile * 32 + r;
     const bool ok = p < n;
     const float4* src = reinterpret_cast<const float4*>(X + (ok ? p : 0) * D + 8 * h);
+    const float4 a = ok ? src[4 * s] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 b = ok ? src[4 * s + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+    dst[8 * s + 0] = a.x; dst[8 * s + 1] = a.y; dst[8 * s + 2] = a.z; dst[8 * s + 3] = a.w;
+    dst[8 * s + 4] = b.x; dst[8 * s + 5] = b.y; dst[8 * s + 6] = b.z; dst[8 * s + 7] = b.w;
+  };
+  auto load = [&](uint64_t tile, float* dst) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const float4 a = ok ? src[4 * s] : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4 b = ok ? src[4 * s + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
-      dst[8 * s + 0] = a.x; dst[8 * s + 1] = a.y; dst[8 * s + 2] = a.z; dst[8 * s + 3] = a.w;
-      dst[8 * s + 4] = b.x; dst[8 * s + 5] = b.y; dst[8 * s + 6] = b.z; dst[8 * s + 7] = b.w;
-    }
+    for (int s = 0; s < 8; ++s) load_part(tile, s, dst);
   };
   // flush: one centroid tile at a time through the wave's LDS tile area (32 x 128 floats), then
   // f64 atomics on consecutive addresses (128 distinct addresses computed in registers would be
@@ -379,6 +381,7 @@ __global__ __launch_bounds__(256) void kmeans_mfma_kernel(const float* __restric
 #pragma unroll
     for (int ct = 0; ct < KT; ++ct) Dt[ct] = f32x16{};
     float xx = 0.f;
+    const bool more = tile + GW < tiles;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       bf16x8 xh, xm;
@@ -389,6 +392,9 @@ __global__ __launch_bounds__(256) void kmeans_mfma_kernel(const float* __restric
         xh[j] = (__bf16)v;
         xm[j] = (__bf16)(v - (float)xh[j]);
       }
+      // these 8 registers are dead now: the next tile's dims of this k-step go in flight under
+      // the distance MFMAs, the argmin and the sum MFMAs (the re-rank reads the LDS copy)
+      if (more) load_part(tile + GW, s, xr);
 #pragma unroll
       for (int ct = 0; ct < KT; ++ct) {
         if constexpr ((DBG & 2) != 0) continue;
@@ -399,9 +405,6 @@ __global__ __launch_bounds__(256) void kmeans_mfma_kernel(const float* __restric
         Dt[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, xh, Dt[ct], 0, 0, 0);
       }
     }
-    // xr is dead from here on (the re-rank reads the LDS copy): prefetch the next tile into it,
-    // overlapping the load with the argmin and the sum MFMAs
-    if (tile + GW < tiles) load(tile + GW, xr);
     // argmin with the runner-up, merged across the two lane halves
     float bd = __builtin_inff(), sd = __builtin_inff();
     int bj = 0;
