@@ -145,18 +145,28 @@ __global__ __launch_bounds__(256) void gp_offsets_kernel(uint32_t* __restrict__ 
   }
 }
 
-// Stable bucket scatter of whole rows.  ITEMS rows per thread per tile (tile = 256 * ITEMS rows of
-// <= 64 KiB), WC = dwords per row when known at compile time (0: runtime), VEC: 16-byte copies.
-template <int ITEMS, int WC, bool VEC>
+// Stable bucket scatter of rows.  ITEMS rows per thread per tile (tile = 256 * ITEMS rows of
+// <= 64 KiB), WC = dwords per input row when known at compile time (0: runtime), VEC: 16-byte
+// copies.  Projection: the destination rows are input dwords [PO, PO + OW) (column pruning before
+// the shuffle: only the columns the join's key and result selector read travel), OWC = OW when
+// known at compile time.
+// STAGE_PROJ (VEC, OWC > 0, key inside the projection): the LDS image holds only the projected
+// dwords of each row, so a 64 KiB tile carries 64 / OWC * 256 rows and each bucket's output run is
+// that many times longer (16-byte rows of 64-byte inputs: 4096-row tiles, ~256-byte runs).
+template <int ITEMS, int WC, int OWC, bool VEC, bool STAGE_PROJ = false>
 __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restrict__ rows, uint64_t n, uint32_t Wdyn,
                                                          uint32_t kw, int key_len, uint64_t seed, int shift, uint32_t nb,
                                                          const uint32_t* __restrict__ prefix,
                                                          const int64_t* __restrict__ base,
                                                          const uint64_t* __restrict__ dst_ptr,
                                                          const int64_t* __restrict__ cap, uint32_t contig_from,
-                                                         uint32_t G, uint64_t per_block) {
+                                                         uint32_t G, uint64_t per_block, uint32_t OWdyn, uint32_t PO) {
   constexpr int TILE = kBlock * ITEMS;
   const uint32_t W = WC > 0 ? (uint32_t)WC : Wdyn;
+  const uint32_t OW = OWC > 0 ? (uint32_t)OWC : OWdyn;
+  const uint32_t LW = STAGE_PROJ ? OW : W;            // dwords per row in the LDS image
+  const uint32_t LPO = STAGE_PROJ ? 0u : PO;          // projection offset inside the LDS image
+  const uint32_t lkw = STAGE_PROJ ? kw - PO : kw;     // key offset inside the LDS image
   __shared__ __attribute__((aligned(16))) uint32_t srow[16384];   // 64 KiB of rows
   __shared__ uint16_t perm[TILE];
   __shared__ uint8_t dslot[TILE];
@@ -176,7 +186,16 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
   const uint64_t end = beg + per_block < n ? beg + per_block : n;
   for (uint64_t tb = beg; tb < end; tb += TILE) {
     const uint32_t cnt = (uint32_t)((end - tb) < (uint64_t)TILE ? (end - tb) : TILE);
-    if (VEC) {
+    if (STAGE_PROJ) {
+      const uint32_t C = W / 4, OC = OW / 4, P4 = PO / 4;
+      const uint32_t chunks = cnt * OC;
+      const uint4* src = reinterpret_cast<const uint4*>(rows + tb * W);
+      uint4* dst = reinterpret_cast<uint4*>(srow);
+      for (uint32_t q = t; q < chunks; q += kBlock) {
+        const uint32_t j = q / OC, c = q - j * OC;
+        dst[q] = src[(uint64_t)j * C + P4 + c];
+      }
+    } else if (VEC) {
       const uint32_t chunks = cnt * W / 4;
       const uint4* src = reinterpret_cast<const uint4*>(rows + tb * W);
       uint4* dst = reinterpret_cast<uint4*>(srow);
@@ -197,7 +216,7 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
       if (valid) {
         uint64_t k0;
         uint32_t k1;
-        row_key(srow + pos * W + kw, key_len, k0, k1);
+        row_key(srow + pos * LW + lkw, key_len, k0, k1);
         d = dest_of(key_hash(k0, k1, seed), shift, nb);
       }
       uint64_t peers = ballot64(valid);
@@ -235,22 +254,24 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
     // slot-major copy: consecutive lanes write consecutive pieces of consecutive slots, and the
     // slots of one bucket are consecutive rows of its destination
     if (VEC) {
-      const uint32_t C = W / 4;
-      const uint32_t chunks = cnt * C;
+      const uint32_t LC = LW / 4, OC = OW / 4, P4 = LPO / 4;
+      const uint32_t chunks = cnt * OC;
       const uint4* s4 = reinterpret_cast<const uint4*>(srow);
       for (uint32_t q = t; q < chunks; q += kBlock) {
-        const uint32_t j = q / C, c = q - j * C;
+        const uint32_t j = q / OC, c = q - j * OC;
         const uint32_t d = dslot[j];
         const int64_t row = goff[d] + (int64_t)(j - bstart[d]);
-        if (row < scap[d]) reinterpret_cast<uint4*>(sptr[d])[(uint64_t)row * C + c] = s4[(uint32_t)perm[j] * C + c];
+        if (row < scap[d])
+          reinterpret_cast<uint4*>(sptr[d])[(uint64_t)row * OC + c] = s4[(uint32_t)perm[j] * LC + P4 + c];
       }
     } else {
-      const uint32_t words = cnt * W;
+      const uint32_t words = cnt * OW;
       for (uint32_t q = t; q < words; q += kBlock) {
-        const uint32_t j = q / W, c = q - j * W;
+        const uint32_t j = q / OW, c = q - j * OW;
         const uint32_t d = dslot[j];
         const int64_t row = goff[d] + (int64_t)(j - bstart[d]);
-        if (row < scap[d]) reinterpret_cast<uint32_t*>(sptr[d])[(uint64_t)row * W + c] = srow[(uint32_t)perm[j] * W + c];
+        if (row < scap[d])
+          reinterpret_cast<uint32_t*>(sptr[d])[(uint64_t)row * OW + c] = srow[(uint32_t)perm[j] * LW + LPO + c];
       }
     }
     __syncthreads();
@@ -388,12 +409,14 @@ bool key_ok(uint32_t stride, uint32_t key_off, uint32_t key_len) {
 // Workspace (bytes) of dr_grace_partition for n rows of `stride` bytes into nb destinations.
 DR_API uint64_t dr_grace_workspace(uint64_t n, uint32_t stride, uint32_t nb) {
   uint32_t G; uint64_t per_block;
-  geometry(n, stride <= 64 ? 1024 : 512, G, per_block);
+  geometry(n, stride <= 64 ? 1024 : 512, G, per_block);     // the most workgroups any tile size gives
   return (uint64_t)nb * G * 4 + (uint64_t)nb * 8 * 2 + 256;
 }
 
 // Partition `n` rows (stride % 4 == 0, <= 128 bytes) by dest = fastrange(32 bits of hash(key) at
-// `shift`, nb) into per-destination runs at dst_ptr[d] (device array of nb row pointers).
+// `shift`, nb) into per-destination runs at dst_ptr[d] (device array of nb row pointers).  The
+// destination rows are bytes [proj_off, proj_off + out_stride) of the input rows (out_stride =
+// stride, proj_off = 0: whole rows).
 // Destinations d < contig_from append at their device fill counter fill[d] (advanced by this call;
 // rows past cap[d] are dropped and *overflow set); destinations d >= contig_from are laid out back
 // to back from row 0 of dst_ptr[d].  chunk_counts[d] / bases[d] receive this call's rows and first
@@ -401,17 +424,24 @@ DR_API uint64_t dr_grace_workspace(uint64_t n, uint32_t stride, uint32_t nb) {
 DR_API int dr_grace_partition(const uint8_t* rows, uint64_t n, uint32_t stride, uint32_t key_off, uint32_t key_len,
                               uint64_t seed, int shift, uint32_t nb, const uint64_t* dst_ptr, int64_t* fill,
                               const int64_t* cap, uint32_t contig_from, int64_t* chunk_counts, int64_t* bases,
-                              uint32_t* overflow, void* ws, hipStream_t s) {
+                              uint32_t* overflow, void* ws, uint32_t out_stride, uint32_t proj_off, hipStream_t s) {
   if (!key_ok(stride, key_off, key_len) || stride > 128 || nb < 1 || nb > kMaxBuckets || n >= (1ull << 32) ||
       (shift != 0 && shift != 32))
+    return (int)hipErrorInvalidValue;
+  if (out_stride == 0 || (out_stride & 3) || (proj_off & 3) || proj_off + out_stride > stride)
     return (int)hipErrorInvalidValue;
   if (n == 0) {
     hipMemsetAsync(chunk_counts, 0, sizeof(int64_t) * nb, s);
     return 0;
   }
   const bool small = stride <= 64;
+  const bool vec0 = (stride & 15) == 0 && (out_stride & 15) == 0 && (proj_off & 15) == 0 &&
+                    (((uintptr_t)rows) & 15) == 0;
+  // 16-byte projection holding the key: stage only the projected slice (4096-row tiles)
+  const bool stage_proj = vec0 && out_stride == 16 && stride > 16 && key_off >= proj_off &&
+                          key_off + key_len <= proj_off + out_stride;
   uint32_t G; uint64_t per_block;
-  geometry(n, small ? 1024 : 512, G, per_block);
+  geometry(n, stage_proj ? 4096 : (small ? 1024 : 512), G, per_block);
   uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
   uint64_t* totals = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(ws) + (((uint64_t)nb * G * 4 + 15) & ~15ull));
   const uint32_t W = stride / 4, kw = key_off / 4;
@@ -419,17 +449,21 @@ DR_API int dr_grace_partition(const uint8_t* rows, uint64_t n, uint32_t stride, 
   gp_count_kernel<<<G, 256, 0, s>>>(in, n, W, kw, (int)key_len, seed, shift, nb, counts, G, per_block);
   gp_totals_kernel<<<nb, 256, 0, s>>>(counts, G, totals);
   gp_offsets_kernel<<<nb, 256, 0, s>>>(counts, G, totals, fill, cap, contig_from, bases, chunk_counts, overflow);
-  const bool vec = (stride & 15) == 0 && (((uintptr_t)rows) & 15) == 0;
-#define DR_GP_SCATTER(IT, WCV, VECV)                                                                   \
-  gp_scatter_kernel<IT, WCV, VECV><<<G, 256, 0, s>>>(in, n, W, kw, (int)key_len, seed, shift, nb, counts, bases, \
-                                                     dst_ptr, cap, contig_from, G, per_block)
-  if (small) {
-    if (stride == 64 && vec) DR_GP_SCATTER(4, 16, true);
-    else if (vec) DR_GP_SCATTER(4, 0, true);
-    else DR_GP_SCATTER(4, 0, false);
+  const bool vec = vec0;
+  const uint32_t OW = out_stride / 4, PO = proj_off / 4;
+#define DR_GP_SCATTER(IT, WCV, OWCV, VECV)                                                               \
+  gp_scatter_kernel<IT, WCV, OWCV, VECV><<<G, 256, 0, s>>>(in, n, W, kw, (int)key_len, seed, shift, nb, counts, \
+                                                           bases, dst_ptr, cap, contig_from, G, per_block, OW, PO)
+  if (stage_proj) {
+    gp_scatter_kernel<16, 0, 4, true, true><<<G, 256, 0, s>>>(in, n, W, kw, (int)key_len, seed, shift, nb, counts,
+                                                              bases, dst_ptr, cap, contig_from, G, per_block, OW, PO);
+  } else if (small) {
+    if (stride == 64 && out_stride == 64 && vec) DR_GP_SCATTER(4, 16, 16, true);
+    else if (vec) DR_GP_SCATTER(4, 0, 0, true);
+    else DR_GP_SCATTER(4, 0, 0, false);
   } else {
-    if (vec) DR_GP_SCATTER(2, 0, true);
-    else DR_GP_SCATTER(2, 0, false);
+    if (vec) DR_GP_SCATTER(2, 0, 0, true);
+    else DR_GP_SCATTER(2, 0, 0, false);
   }
 #undef DR_GP_SCATTER
   DR_LAUNCH_CHECK();

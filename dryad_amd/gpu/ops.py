@@ -247,6 +247,15 @@ def op_read(op, inputs, v):
         return t
     prov = provider_for(uri)
     if scheme in ("partfile", "file") and v.device.type == "cuda":
+        rp = prov.rows_part(uri, v.partition)
+        if rp is not None:
+            # raw fixed-width rows (e.g. an out-of-core sort's output): one copy into pooled HBM
+            import numpy as np
+            mm, ko, kl = rp
+            rows = v.alloc_rows(mm.shape[0], mm.shape[1])
+            if mm.shape[0]:
+                rows.copy_(torch.from_numpy(np.ascontiguousarray(mm)))
+            return DeviceTable(mm.shape[0], Shape("rows", key_off=ko, key_len=kl), rows=rows)
         # binary part of fixed-width records: bytes -> HBM -> columns with the device codec
         from ..ops import codec as CD
         sch = prov.schema(uri) or {}

@@ -115,6 +115,9 @@ class PartfileProvider(DataProvider):
         with open(path, "rb") as f:
             data = f.read()
         sch = self.schema(uri)
+        if sch is not None and sch.get("format") == "rows":
+            st = int(sch["stride"])
+            return [data[i:i + st] for i in range(0, len(data), st)]
         if sch is not None and sch.get("format") == "pickle":
             import gzip
             import pickle
@@ -168,6 +171,19 @@ class PartfileProvider(DataProvider):
         root = os.environ.get("DRYAD_TEMP_DIR") or os.path.join(os.environ.get("TMPDIR", "/tmp"), "DryadLinqTemp")
         os.makedirs(root, exist_ok=True)
         return "partfile://" + os.path.join(root, name)
+
+    def rows_part(self, uri, i):
+        """(memory map [n, stride] uint8, key_off, key_len) of part i of a raw-rows table, or None."""
+        import numpy as np
+        sch = self.schema(uri)
+        if sch is None or sch.get("format") != "rows":
+            return None
+        path = PF.read_meta(self._path(uri)).part_path(i)
+        st = int(sch["stride"])
+        size = os.path.getsize(path)
+        mm = np.memmap(path, dtype=np.uint8, mode="r", shape=(size // st, st)) if size else \
+            np.zeros((0, st), dtype=np.uint8)
+        return mm, int(sch.get("key_off", 0)), int(sch.get("key_len", st))
 
 
 class _MemoryTables:

@@ -37,6 +37,7 @@ class HashJoinConfig:
     chunk_rows: int = 1 << 27         # 8 GB chunks
     hbm_budget: int | None = None
     buckets: int | None = None
+    prune: bool = True                # carry only Key + V1 through the grace partitioning
 
 
 def _i64(v):
@@ -88,8 +89,11 @@ class HashJoinJob:
         """Allocate the bucket stores (HBM or page-locked host) once; reused by every step."""
         cfg = self.cfg
         # per-rank receive estimate: an even share of both tables
+        # column pruning: the key selectors read Key and the result selector V1 (bytes 0..15 of
+        # both tables), so only those 16 of the 64 bytes travel through the partitioning
         self.grace = G.GraceHashJoin(self.w, 64, 0, 8, {"R": self.r_hi - self.r_lo, "S": self.s_hi - self.s_lo},
-                                     cfg.chunk_rows, cfg.hbm_budget, cfg.buckets, build="R")
+                                     cfg.chunk_rows, cfg.hbm_budget, cfg.buckets, build="R",
+                                     proj=(0, 16) if cfg.prune else None)
 
     def release(self):
         if self.grace is not None:

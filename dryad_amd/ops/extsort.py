@@ -119,6 +119,7 @@ class HostRowsSource(ChunkSource):
 
     def __init__(self, rows: HostRows):
         self.rows, self.n, self.stride = rows, rows.n, rows.stride
+        self.key_spec = (rows.key_off, rows.key_len)
 
     def fill(self, lo, hi, out, copy_stream):
         _copy(out[: hi - lo], self.rows.rows[lo:hi], copy_stream)
@@ -126,6 +127,32 @@ class HostRowsSource(ChunkSource):
 
     def sample_rows(self, idx, scratch, chunk_rows):
         return self.rows.rows.index_select(0, idx).to(scratch.device)
+
+
+class MappedRowsSource(ChunkSource):
+    """Raw fixed-width rows of a partfile part (``format: rows``), memory-mapped: each chunk is
+    copied from the page cache / disk into a pinned staging buffer, then DMA'd to HBM."""
+    dma = True
+
+    def __init__(self, mm, key_off: int = 0, key_len: int | None = None):
+        self.mm, self.n, self.stride = mm, mm.shape[0], mm.shape[1]
+        self.key_spec = (key_off, key_len or self.stride)
+        self._stage = None
+
+    def fill(self, lo, hi, out, copy_stream):
+        if self._stage is None or self._stage.n < hi - lo:
+            if self._stage is not None:
+                self._stage.release()
+            self._stage = HostRows(hi - lo, self.stride)
+        if copy_stream is not None:
+            copy_stream.synchronize()          # the previous chunk has left the staging buffer
+        self._stage.rows[: hi - lo].numpy()[:] = self.mm[lo:hi]
+        _copy(out[: hi - lo], self._stage.rows[: hi - lo], copy_stream)
+        return copy_stream
+
+    def sample_rows(self, idx, scratch, chunk_rows):
+        import numpy as np
+        return torch.from_numpy(np.ascontiguousarray(self.mm[idx.numpy()])).to(scratch.device)
 
 
 def _copy(dst: torch.Tensor, src: torch.Tensor, stream):

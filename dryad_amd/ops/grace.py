@@ -37,7 +37,7 @@ from . import sort as S
 _lib.register_signatures({
     "dr_grace_workspace": (c_u64, [c_u64, c_u32, c_u32]),
     "dr_grace_partition": (c_i32, [vp, c_u64, c_u32, c_u32, c_u32, c_u64, c_i32, c_u32, vp, vp, vp, c_u32, vp, vp,
-                                   vp, vp, vp]),
+                                   vp, vp, c_u32, c_u32, vp]),
     "dr_ht_build": (c_i32, [vp, c_u64, c_u32, c_u32, c_u32, c_u64, vp, c_i32, vp]),
     "dr_ht_probe_sum_workspace": (c_u64, []),
     "dr_ht_probe_sum": (c_i32, [vp, c_u64, c_u32, c_u32, c_u32, c_u64, vp, c_i32, vp, c_u32, c_u32, c_u32, vp, vp,
@@ -74,24 +74,30 @@ class Partitioner:
 
 
 def partition_rows(rows: torch.Tensor, key_off: int, key_len: int, part: Partitioner, shift: int = 0,
-                   contig_from: int | None = None, seed: int = HASH_SEED):
+                   contig_from: int | None = None, seed: int = HASH_SEED, proj: tuple[int, int] | None = None):
     """Scatter ``rows`` [n, stride] uint8 by hash(key) into ``part``'s destinations.  Buckets below
     ``contig_from`` (default: all) append at their fill counters (bounded by cap, overflow flagged);
     buckets from ``contig_from`` on are laid out back to back from row 0 of their pointer.
-    ``part.counts`` / ``part.bases`` receive this call's rows and first row per destination."""
+    ``part.counts`` / ``part.bases`` receive this call's rows and first row per destination.
+    ``proj = (byte offset, bytes)``: the destination rows are that slice of every row (column
+    pruning in the same pass)."""
     _lib.require_gpu_tensor(rows, "partition_rows")
     n, stride = rows.shape
+    po, ow = proj if proj is not None else (0, stride)
     cf = part.nb if contig_from is None else contig_from
     ws = part.workspace(n, stride)
     _lib.call("dr_grace_partition", ptr(rows), c_u64(n), c_u32(stride), c_u32(key_off), c_u32(key_len),
               c_u64(seed & (2**64 - 1)), shift, c_u32(part.nb), ptr(part.ptrs), ptr(part.fill), ptr(part.cap),
-              c_u32(cf), ptr(part.counts), ptr(part.bases), ptr(part.overflow), ptr(ws), stream_of(rows))
+              c_u32(cf), ptr(part.counts), ptr(part.bases), ptr(part.overflow), ptr(ws), c_u32(ow), c_u32(po),
+              stream_of(rows))
 
 
-def split_by_rank(rows: torch.Tensor, key_off: int, key_len: int, part: Partitioner, out: torch.Tensor) -> list:
-    """Rows grouped by destination rank (hash bits 32..63) into ``out``; returns per-rank counts."""
+def split_by_rank(rows: torch.Tensor, key_off: int, key_len: int, part: Partitioner, out: torch.Tensor,
+                  proj: tuple[int, int] | None = None) -> list:
+    """Rows (or their ``proj`` slice) grouped by destination rank (hash bits 32..63) into ``out``;
+    returns per-rank counts."""
     part.ptrs.fill_(out.data_ptr())
-    partition_rows(rows, key_off, key_len, part, shift=32, contig_from=0)
+    partition_rows(rows, key_off, key_len, part, shift=32, contig_from=0, proj=proj)
     return part.counts.tolist()
 
 
@@ -157,11 +163,22 @@ class _TableStore:
 
 class GraceHashJoin:
     """Grace join of two row tables produced chunk by chunk (``add_chunk(table, rows)``), then
-    joined bucket by bucket (``buckets(build, probe)`` yields HBM row views)."""
+    joined bucket by bucket (``buckets(build, probe)`` yields HBM row views).
+
+    ``stride`` / ``key_off`` describe the input rows.  ``proj = (byte offset, bytes)`` prunes
+    every row to the columns the join reads in the first partitioning pass (before the xGMI
+    exchange, the bucket stores and any spill), so the stored rows are ``proj[1]`` bytes with the
+    key at ``key_off - proj[0]``."""
 
     def __init__(self, world: World, stride: int, key_off: int, key_len: int, rows_per_rank: dict,
                  chunk_rows: int, hbm_budget: int | None = None, buckets: int | None = None,
-                 build: str | None = None):
+                 build: str | None = None, proj: tuple[int, int] | None = None):
+        if proj is not None and not (proj[0] <= key_off and key_off + key_len <= proj[0] + proj[1] <= stride):
+            raise ValueError("grace join projection must keep the key bytes")
+        self.proj = proj
+        self.key_off_in = key_off
+        if proj is not None:
+            stride, key_off = proj[1], key_off - proj[0]
         self.w, self.stride, self.key_off, self.key_len = world, stride, key_off, key_len
         dev = world.device
         self.dev = dev
@@ -218,8 +235,10 @@ class GraceHashJoin:
     # -------------------------------------------------------------- pass A
     def add_chunk(self, table: str, rows: torch.Tensor):
         W = self.w.size
+        key_off, proj = self.key_off_in, self.proj
         if W > 1:
-            send = split_by_rank(rows, self.key_off, self.key_len, self.rank_part, self.sbuf)
+            send = split_by_rank(rows, key_off, self.key_len, self.rank_part, self.sbuf, proj)
+            key_off, proj = self.key_off, None          # received rows are already pruned
             recv = shuffle.exchange_counts(torch.tensor(send, dtype=torch.int64), self.w).tolist()
             n_recv = sum(recv)
             if n_recv > self.rbuf.shape[0]:
@@ -238,7 +257,7 @@ class GraceHashJoin:
                 self.staging[k] = torch.empty((int(rows.shape[0] * 1.2), self.stride), dtype=torch.uint8,
                                               device=self.dev)
             st.set_staging(self.staging[k])
-        partition_rows(rows, self.key_off, self.key_len, st.part, shift=0, contig_from=st.resident)
+        partition_rows(rows, key_off, self.key_len, st.part, shift=0, contig_from=st.resident, proj=proj)
         if not self.in_hbm:
             counts = st.part.counts.tolist()          # one small D2H per chunk
             self.copy_stream.wait_stream(main)

@@ -213,7 +213,7 @@ class GpuJobRunner:
         out = {}
         for sid, c in sorted(cands.items()):
             sort = c["sort"]
-            ok = parse_uri(st[sid].output["uri"])[0] == "host" and sort.get("comparer") is None \
+            ok = parse_uri(st[sid].output["uri"])[0] in ("host", "partfile", "file") and sort.get("comparer") is None \
                 and not sort.get("descending", False)
             src = self._chunk_source(c["read"]) if ok else None
             spec = None
@@ -244,6 +244,10 @@ class GpuJobRunner:
             prov = provider_for(uri)
             h = prov.local_rows(uri, me) if prov.exists(uri) else None
             return EX.HostRowsSource(h) if h is not None and h.stride % 4 == 0 else None
+        if scheme in ("partfile", "file"):
+            prov = provider_for(uri)
+            r = prov.rows_part(uri, me) if prov.exists(uri) else None
+            return EX.MappedRowsSource(*r) if r is not None and r[0].shape[1] % 4 == 0 else None
         return None
 
     def _external_key(self, src, read_op, key):
@@ -254,9 +258,8 @@ class GpuJobRunner:
         rows = torch.zeros((k, src.stride), dtype=torch.uint8, device=self.dev)
         if src.n:
             src.fill(0, k, rows, None)
-        h = getattr(src, "rows", None)
-        shape = Shape("rows", key_off=h.key_off, key_len=h.key_len) if h is not None else \
-            Shape("rows", key_off=0, key_len=10)
+        ko, kl = getattr(src, "key_spec", (0, 10))
+        shape = Shape("rows", key_off=ko, key_len=kl)
         try:
             kind, spec = TR.key_columns(TR.call(key, DeviceTable(k, shape, rows=rows)), DeviceTable(k, shape, rows=rows))
         except Exception:  # noqa: BLE001
@@ -736,7 +739,8 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     from .jobmanager import write_schema
     W, me = runner.world.size, runner.world.rank
     dt = s.dtype
-    if dt is None or dt == T.Pickle:
+    rows_fmt = any(isinstance(v, HostRows) for v in local.values())
+    if not rows_fmt and (dt is None or dt == T.Pickle):
         return False
     prov = provider_for(uri)
     if me == 0 and prov.exists(uri):
@@ -748,9 +752,19 @@ def _commit_partfile_impl(runner, s, uri, path, local):
         runner.world.barrier()
     base = PF.default_base(path)
     os.makedirs(os.path.dirname(base) or ".", exist_ok=True)
-    mine = {}
+    mine, fmt_extra = {}, None
     for p, v in local.items():
         tmp = PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, 0)
+        if rows_fmt:
+            # raw fixed-width rows straight from the pinned host tier (out-of-core sort output)
+            if not isinstance(v, HostRows):
+                v = HostRows.from_tensor(v.rows, v.shape.key_off, v.shape.key_len, pinned=False)
+            with open(tmp, "wb") as f:
+                if v.n:
+                    f.write(memoryview(v.rows.numpy()).cast("B"))
+            fmt_extra = dict(stride=v.stride, key_off=v.key_off, key_len=v.key_len)
+            mine[p] = tmp
+            continue
         data = CD.encode(v, dt) if isinstance(v, DeviceTable) and v.device.type == "cuda" else None
         raw = data.cpu().numpy().tobytes() if data is not None else None
         if runner.ctx.OutputDataCompressionScheme.value != 0:
@@ -765,8 +779,10 @@ def _commit_partfile_impl(runner, s, uri, path, local):
             B.write_records(tmp, dt, _to_objects(v) if not isinstance(v, list) else v)
         mine[p] = tmp
     gathered = [None] * W
+    gathered_fmt = [None] * W
     if W > 1:
         dist.all_gather_object(gathered, mine)
+        dist.all_gather_object(gathered_fmt, fmt_extra)
     else:
         gathered = [mine]
     if me == 0:
@@ -774,7 +790,11 @@ def _commit_partfile_impl(runner, s, uri, path, local):
         for d in gathered:
             parts.update(d)
         PF.commit_parts(path, base, [parts[p] for p in range(s.partitions)])
-        write_schema(path, dt, "binary")
+        if rows_fmt:
+            extras = [x for x in gathered_fmt if x] if W > 1 else [fmt_extra]
+            write_schema(path, dt, "rows", **(extras[0] if extras and extras[0] else {}))
+        else:
+            write_schema(path, dt, "binary")
     if W > 1:
         runner.world.barrier()
     return True

@@ -288,10 +288,12 @@ def schema_path(meta_path: str) -> str:
     return meta_path + ".dryadtype"
 
 
-def write_schema(meta_path: str, dtype, fmt: str):
+def write_schema(meta_path: str, dtype, fmt: str, **extra):
+    """Sidecar of a partfile table: record type and part format ("binary" DryadLinqBinary records,
+    "pickle", or "rows" = raw fixed-width rows with ``stride`` / ``key_off`` / ``key_len``)."""
     import cloudpickle
     with open(schema_path(meta_path), "wb") as f:
-        cloudpickle.dump({"dtype": dtype, "format": fmt}, f)
+        cloudpickle.dump({"dtype": dtype, "format": fmt, **extra}, f)
 
 
 def read_schema(meta_path: str):

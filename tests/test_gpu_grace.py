@@ -10,18 +10,19 @@ def _world():
     return World(0, 1, 0, torch.device("cuda", 0), None)
 
 
-@pytest.mark.parametrize("budget", [None, 1 << 25, 1 << 20])    # in HBM / hybrid / everything spilled
-def test_grace_join_matches_expected(budget):
+@pytest.mark.parametrize("budget,prune", [(None, False), (1 << 25, False), (1 << 20, False),   # in HBM / hybrid /
+                                          (1 << 23, True), (1 << 18, True)])                 # all spilled
+def test_grace_join_matches_expected(budget, prune):
     from dryad_amd.models.hashjoin import HashJoinConfig, HashJoinJob
-    cfg = HashJoinConfig(rows_r=300_000, rows_s=450_000, chunk_rows=100_000, hbm_budget=budget)
+    cfg = HashJoinConfig(rows_r=300_000, rows_s=450_000, chunk_rows=100_000, hbm_budget=budget, prune=prune)
     job = HashJoinJob(_world(), cfg)
     res = job.step()
     assert res == job.expected()
     assert res[0] == 450_000
-    total = (300_000 + 450_000) * 64
+    total = (300_000 + 450_000) * (16 if prune else 64)
     if budget is None:
         assert job.last["in_hbm"] and job.last["spilled_bytes"] == 0
-    elif budget == 1 << 25:
+    elif budget in (1 << 25, 1 << 23):
         assert not job.last["in_hbm"] and 0 < job.last["spilled_bytes"] < total and job.last["buckets"] > 1
     else:
         assert job.last["spilled_bytes"] == total
@@ -165,3 +166,35 @@ def test_join_sum_fused_aggregate():
     pos = {k: j for j, k in enumerate(bk)}
     m = [(i, pos[k]) for i, k in enumerate(pk) if k in pos]
     assert acc.tolist() == [len(m), sum(3 * i + 1 for i, _ in m), sum(3 * j + 1 for _, j in m)]
+
+
+@pytest.mark.parametrize("proj", [(0, 16), (8, 16), (4, 8)])
+def test_partition_rows_projection(proj):
+    """Column pruning in the partition pass: destination rows are bytes [po, po + ow) of the rows,
+    bucketed exactly like the whole rows."""
+    from dryad_amd.ops import grace as G
+    g = torch.Generator().manual_seed(11)
+    keys = torch.randint(0, 9000, (50_000,), generator=g).tolist()
+    rows = _rows(keys)
+    po, ow = proj
+    nb = 7
+    whole, pruned = G.Partitioner(nb, rows.device), G.Partitioner(nb, rows.device)
+    a = torch.zeros((50_000, 64), dtype=torch.uint8, device="cuda")
+    b = torch.zeros((50_000, ow), dtype=torch.uint8, device="cuda")
+    whole.ptrs.fill_(a.data_ptr())
+    pruned.ptrs.fill_(b.data_ptr())
+    G.partition_rows(rows, 0, 8, whole, contig_from=0)
+    G.partition_rows(rows, 0, 8, pruned, contig_from=0, proj=proj)
+    assert whole.counts.tolist() == pruned.counts.tolist()
+    assert torch.equal(a[:, po:po + ow], b)
+
+
+@pytest.mark.parametrize("prune", [True, False])
+def test_hash_join_job_pruned_columns(prune):
+    from dryad_amd.models.hashjoin import HashJoinConfig, HashJoinJob
+    from dryad_amd.parallel.comm import World
+    w = World(0, 1, 0, torch.device("cuda", 0), None)
+    job = HashJoinJob(w, HashJoinConfig(rows_r=300_000, rows_s=500_000, chunk_rows=100_000, prune=prune))
+    res = job.step()
+    assert res == job.expected() and res[0] == 500_000
+    job.release()
