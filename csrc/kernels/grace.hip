@@ -35,6 +35,26 @@ struct __attribute__((aligned(16))) HSlot {
   uint32_t idx;
 };
 
+// Tile of up to 16 * 256 16-byte pieces into LDS: every load of the thread is issued before the
+// first LDS store (one wait for all of them instead of one HBM round trip per piece).  idx(q) maps
+// a piece to its global 16-byte index.
+template <int N = 16, typename F>
+__device__ __forceinline__ void tile_to_lds(uint4* __restrict__ lds, const uint4* __restrict__ src, uint32_t pieces,
+                                            F idx) {
+  uint4 v[N];
+  const uint32_t last = pieces ? pieces - 1 : 0;   // clamped, unconditional loads: v stays in VGPRs
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint32_t q = threadIdx.x + i * kBlock;
+    v[i] = src[idx(q < pieces ? q : last)];
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint32_t q = threadIdx.x + i * kBlock;
+    if (q < pieces) lds[q] = v[i];
+  }
+}
+
 __device__ __forceinline__ uint32_t keep_mask(int bytes) {
   return bytes >= 4 ? 0xFFFFFFFFu : (bytes <= 0 ? 0u : ((1u << (8 * bytes)) - 1u));
 }
@@ -153,21 +173,27 @@ __global__ __launch_bounds__(256) void gp_offsets_kernel(uint32_t* __restrict__ 
 // STAGE_PROJ (VEC, OWC > 0, key inside the projection): the LDS image holds only the projected
 // dwords of each row, so a 64 KiB tile carries 64 / OWC * 256 rows and each bucket's output run is
 // that many times longer (16-byte rows of 64-byte inputs: 4096-row tiles, ~256-byte runs).
-template <int ITEMS, int WC, int OWC, bool VEC, bool STAGE_PROJ = false>
+// ATOMIC (every destination appends at its fill counter, row order inside a destination free):
+// no count pass; each tile reserves its rows per destination with one atomicAdd on the fill
+// counter (a join's buckets do not need the input order).  Rows past cap are dropped and flagged.
+template <int ITEMS, int WC, int OWC, bool VEC, bool STAGE_PROJ = false, bool ATOMIC = false>
 __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restrict__ rows, uint64_t n, uint32_t Wdyn,
                                                          uint32_t kw, int key_len, uint64_t seed, int shift, uint32_t nb,
                                                          const uint32_t* __restrict__ prefix,
                                                          const int64_t* __restrict__ base,
                                                          const uint64_t* __restrict__ dst_ptr,
                                                          const int64_t* __restrict__ cap, uint32_t contig_from,
-                                                         uint32_t G, uint64_t per_block, uint32_t OWdyn, uint32_t PO) {
+                                                         uint32_t G, uint64_t per_block, uint32_t OWdyn, uint32_t PO,
+                                                         int64_t* __restrict__ fill = nullptr,
+                                                         uint32_t* __restrict__ overflow = nullptr) {
   constexpr int TILE = kBlock * ITEMS;
+  constexpr int LDS_DW = STAGE_PROJ ? 8192 : 16384;  // projected tiles: 32 KiB, three workgroups per CU
   const uint32_t W = WC > 0 ? (uint32_t)WC : Wdyn;
   const uint32_t OW = OWC > 0 ? (uint32_t)OWC : OWdyn;
   const uint32_t LW = STAGE_PROJ ? OW : W;            // dwords per row in the LDS image
   const uint32_t LPO = STAGE_PROJ ? 0u : PO;          // projection offset inside the LDS image
   const uint32_t lkw = STAGE_PROJ ? kw - PO : kw;     // key offset inside the LDS image
-  __shared__ __attribute__((aligned(16))) uint32_t srow[16384];   // 64 KiB of rows
+  __shared__ __attribute__((aligned(16))) uint32_t srow[LDS_DW];
   __shared__ uint16_t perm[TILE];
   __shared__ uint8_t dslot[TILE];
   __shared__ uint32_t wcnt[4][kMaxBuckets];
@@ -178,7 +204,7 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
   __shared__ uint32_t sc[4];
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   if ((uint32_t)t < nb) {
-    goff[t] = base[t] + (int64_t)prefix[(uint64_t)t * G + blockIdx.x];
+    goff[t] = ATOMIC ? 0 : base[t] + (int64_t)prefix[(uint64_t)t * G + blockIdx.x];
     sptr[t] = dst_ptr[t];
     scap[t] = (cap && (uint32_t)t < contig_from) ? cap[t] : (int64_t)0x7FFFFFFFFFFFFFFFll;
   }
@@ -188,18 +214,14 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
     const uint32_t cnt = (uint32_t)((end - tb) < (uint64_t)TILE ? (end - tb) : TILE);
     if (STAGE_PROJ) {
       const uint32_t C = W / 4, OC = OW / 4, P4 = PO / 4;
-      const uint32_t chunks = cnt * OC;
-      const uint4* src = reinterpret_cast<const uint4*>(rows + tb * W);
-      uint4* dst = reinterpret_cast<uint4*>(srow);
-      for (uint32_t q = t; q < chunks; q += kBlock) {
-        const uint32_t j = q / OC, c = q - j * OC;
-        dst[q] = src[(uint64_t)j * C + P4 + c];
-      }
+      tile_to_lds<TILE * 4 / kBlock / 4>(reinterpret_cast<uint4*>(srow), reinterpret_cast<const uint4*>(rows + tb * W), cnt * OC,
+                  [=](uint32_t q) {
+                    const uint32_t j = q / OC, c = q - j * OC;
+                    return (uint64_t)j * C + P4 + c;
+                  });
     } else if (VEC) {
-      const uint32_t chunks = cnt * W / 4;
-      const uint4* src = reinterpret_cast<const uint4*>(rows + tb * W);
-      uint4* dst = reinterpret_cast<uint4*>(srow);
-      for (uint32_t j = t; j < chunks; j += kBlock) dst[j] = src[j];
+      tile_to_lds(reinterpret_cast<uint4*>(srow), reinterpret_cast<const uint4*>(rows + tb * W), cnt * W / 4,
+                  [](uint32_t q) { return (uint64_t)q; });
     } else {
       const uint32_t words = cnt * W;
       const uint32_t* src = rows + tb * W;
@@ -240,6 +262,8 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
     wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
     uint32_t all;
     bstart[t] = block_exclusive_scan256(tot, sc, all);
+    if (ATOMIC && (uint32_t)t < nb && tot)
+      goff[t] = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(fill + t), (unsigned long long)tot);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
@@ -250,6 +274,7 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
         dslot[slot] = (uint8_t)dg[r];
       }
     }
+    if (ATOMIC && (uint32_t)t < nb && tot && goff[t] + (int64_t)tot > scap[t]) atomicOr(overflow, 1u);
     __syncthreads();
     // slot-major copy: consecutive lanes write consecutive pieces of consecutive slots, and the
     // slots of one bucket are consecutive rows of its destination
@@ -275,7 +300,7 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
       }
     }
     __syncthreads();
-    if ((uint32_t)t < nb) goff[t] += tot;
+    if (!ATOMIC && (uint32_t)t < nb) goff[t] += tot;
     __syncthreads();
   }
 }
@@ -424,7 +449,8 @@ DR_API uint64_t dr_grace_workspace(uint64_t n, uint32_t stride, uint32_t nb) {
 DR_API int dr_grace_partition(const uint8_t* rows, uint64_t n, uint32_t stride, uint32_t key_off, uint32_t key_len,
                               uint64_t seed, int shift, uint32_t nb, const uint64_t* dst_ptr, int64_t* fill,
                               const int64_t* cap, uint32_t contig_from, int64_t* chunk_counts, int64_t* bases,
-                              uint32_t* overflow, void* ws, uint32_t out_stride, uint32_t proj_off, hipStream_t s) {
+                              uint32_t* overflow, void* ws, uint32_t out_stride, uint32_t proj_off, int unordered,
+                              hipStream_t s) {
   if (!key_ok(stride, key_off, key_len) || stride > 128 || nb < 1 || nb > kMaxBuckets || n >= (1ull << 32) ||
       (shift != 0 && shift != 32))
     return (int)hipErrorInvalidValue;
@@ -441,11 +467,20 @@ DR_API int dr_grace_partition(const uint8_t* rows, uint64_t n, uint32_t stride, 
   const bool stage_proj = vec0 && out_stride == 16 && stride > 16 && key_off >= proj_off &&
                           key_off + key_len <= proj_off + out_stride;
   uint32_t G; uint64_t per_block;
-  geometry(n, stage_proj ? 4096 : (small ? 1024 : 512), G, per_block);
+  geometry(n, stage_proj ? 2048 : (small ? 1024 : 512), G, per_block);
   uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
   uint64_t* totals = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(ws) + (((uint64_t)nb * G * 4 + 15) & ~15ull));
   const uint32_t W = stride / 4, kw = key_off / 4;
   const uint32_t* in = reinterpret_cast<const uint32_t*>(rows);
+  if (unordered && stage_proj && contig_from >= nb) {
+    // every destination appends at its fill counter: no count pass, one reservation per tile
+    gp_scatter_kernel<8, 0, 4, true, true, true><<<G, 256, 0, s>>>(in, n, W, kw, (int)key_len, seed, shift, nb,
+                                                                    nullptr, nullptr, dst_ptr, cap, contig_from, G,
+                                                                    per_block, out_stride / 4, proj_off / 4, fill,
+                                                                    overflow);
+    DR_LAUNCH_CHECK();
+    return 0;
+  }
   gp_count_kernel<<<G, 256, 0, s>>>(in, n, W, kw, (int)key_len, seed, shift, nb, counts, G, per_block);
   gp_totals_kernel<<<nb, 256, 0, s>>>(counts, G, totals);
   gp_offsets_kernel<<<nb, 256, 0, s>>>(counts, G, totals, fill, cap, contig_from, bases, chunk_counts, overflow);
@@ -455,8 +490,8 @@ DR_API int dr_grace_partition(const uint8_t* rows, uint64_t n, uint32_t stride, 
   gp_scatter_kernel<IT, WCV, OWCV, VECV><<<G, 256, 0, s>>>(in, n, W, kw, (int)key_len, seed, shift, nb, counts, \
                                                            bases, dst_ptr, cap, contig_from, G, per_block, OW, PO)
   if (stage_proj) {
-    gp_scatter_kernel<16, 0, 4, true, true><<<G, 256, 0, s>>>(in, n, W, kw, (int)key_len, seed, shift, nb, counts,
-                                                              bases, dst_ptr, cap, contig_from, G, per_block, OW, PO);
+    gp_scatter_kernel<8, 0, 4, true, true><<<G, 256, 0, s>>>(in, n, W, kw, (int)key_len, seed, shift, nb, counts,
+                                                             bases, dst_ptr, cap, contig_from, G, per_block, OW, PO);
   } else if (small) {
     if (stride == 64 && out_stride == 64 && vec) DR_GP_SCATTER(4, 16, 16, true);
     else if (vec) DR_GP_SCATTER(4, 0, 0, true);
@@ -521,6 +556,356 @@ DR_API int dr_ht_probe_pairs(const uint8_t* prow, uint64_t np, uint32_t stride_p
   else
     ht_probe_pairs_kernel<false><<<g, 256, 0, s>>>(p, np, stride_p / 4, key_off_p / 4, (int)key_len, seed, tb,
                                                    (1ull << log_cap) - 1, count, offs, po, bo);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Radix join: the bucket pairs of the grace partitioning are split further, by two more digits
+// of the same key hash, into partitions whose build side fits an LDS hash table; every
+// partition pair is then joined by one workgroup entirely in LDS (no global atomics, no random
+// HBM / Infinity-Cache reads).  This is the radix-partitioned hash join of the main-memory join
+// literature mapped onto CDNA4: partition until the working set is on-chip, then build + probe
+// on-chip.  Rows are fixed-width (RW dwords, 16 or 32 bytes) with an 8-byte-or-shorter key.
+//
+//   rp_count   per tile (a tile never crosses a segment): digit histogram in LDS
+//   rp_scan    per segment: digit totals, digit starts, per-tile destination offsets
+//   rp_scatter per tile: rows staged in LDS, ranked by digit with wave ballots (stable), every
+//              digit's rows written as one contiguous run
+//   rj_join_sum per partition pair: LDS open-addressing table over the build rows (64-bit CAS),
+//              probe rows streamed through it with the Count/Sum aggregate fused in; partitions
+//              too large for the LDS table (key skew) are listed for the global-table path.
+namespace {
+
+// 32 KiB tiles (2048 16-byte rows): ~42 KiB of LDS per workgroup, three workgroups per CU to
+// hide each one's load / rank / store latency chain (one 64 KiB-tile workgroup per CU ran at half
+// the rate); 16 rows per digit run at 7-bit digits.
+constexpr uint32_t kRpTileBytes = 32768;
+constexpr uint64_t kRjEmpty = 0xFFFFFFFFFFFFFFFFull;
+constexpr uint32_t kRjCap = 2048;                 // LDS slots (16 B each: 32 KiB, 4 workgroups per CU)
+constexpr int kRjPer = 6;                         // rows per thread held in registers (1536 >= 0.75 cap)
+
+__device__ __forceinline__ uint32_t rp_seg_of(const int64_t* __restrict__ tile_base, uint32_t nseg, uint64_t t) {
+  uint32_t lo = 0, hi = nseg;                      // last s with tile_base[s] <= t
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((uint64_t)tile_base[mid] <= t) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+template <int RW>
+__device__ __forceinline__ uint32_t rp_digit(const uint32_t* r, int key_len, uint64_t seed, int shift, uint32_t dmask) {
+  uint64_t k0;
+  uint32_t k1;
+  row_key(r, key_len, k0, k1);
+  return (uint32_t)(key_hash(k0, k1, seed) >> shift) & dmask;
+}
+
+template <int RW>
+__global__ __launch_bounds__(256) void rp_count_kernel(const uint32_t* __restrict__ rows,
+                                                       const int64_t* __restrict__ seg_begin,
+                                                       const int64_t* __restrict__ seg_len,
+                                                       const int64_t* __restrict__ tile_base, uint32_t nseg,
+                                                       uint64_t ntiles, uint32_t kw, int key_len, uint64_t seed,
+                                                       int shift, int bits, uint32_t* __restrict__ counts) {
+  constexpr uint32_t TILE = kRpTileBytes / (4 * RW);
+  const uint32_t D = 1u << bits, dmask = D - 1;
+  __shared__ uint32_t hist[4][256];
+  const int t = threadIdx.x, w = wave_id();
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (int i = t; i < 4 * 256; i += kBlock) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t s = rp_seg_of(tile_base, nseg, tile);
+    const uint64_t r0 = (tile - (uint64_t)tile_base[s]) * TILE;
+    const uint64_t left = (uint64_t)seg_len[s] - r0;
+    const uint32_t cnt = left < TILE ? (uint32_t)left : TILE;
+    const uint32_t* base = rows + ((uint64_t)seg_begin[s] + r0) * RW;
+    for (uint32_t i = t; i < cnt; i += kBlock)
+      atomicAdd(&hist[w][rp_digit<RW>(base + (uint64_t)i * RW + kw, key_len, seed, shift, dmask)], 1u);
+    __syncthreads();
+    for (uint32_t d = t; d < D; d += kBlock) counts[tile * D + d] = hist[0][d] + hist[1][d] + hist[2][d] + hist[3][d];
+    __syncthreads();
+  }
+}
+
+// one workgroup per segment, thread = digit: totals, digit starts (part_start / part_len of the
+// segment's D partitions) and each tile's absolute destination row per digit (in place)
+__global__ __launch_bounds__(256) void rp_scan_kernel(const int64_t* __restrict__ seg_begin,
+                                                      const int64_t* __restrict__ tile_base, int bits,
+                                                      uint32_t* __restrict__ counts, int64_t* __restrict__ part_start,
+                                                      int64_t* __restrict__ part_len) {
+  __shared__ uint32_t sc[4];
+  const uint32_t s = blockIdx.x, d = threadIdx.x, D = 1u << bits;
+  const uint64_t t0 = (uint64_t)tile_base[s], t1 = (uint64_t)tile_base[s + 1];
+  uint64_t tot = 0;
+  if (d < D)
+    for (uint64_t t = t0; t < t1; ++t) tot += counts[t * D + d];
+  uint32_t all;
+  const uint32_t ex = block_exclusive_scan256((uint32_t)tot, sc, all);
+  if (d < D) {
+    uint64_t run = (uint64_t)seg_begin[s] + ex;
+    part_start[(uint64_t)s * D + d] = (int64_t)run;
+    part_len[(uint64_t)s * D + d] = (int64_t)tot;
+    for (uint64_t t = t0; t < t1; ++t) {
+      const uint32_t c = counts[t * D + d];
+      counts[t * D + d] = (uint32_t)run;          // rows < 2^32 (checked by the launcher)
+      run += c;
+    }
+  }
+}
+
+template <int RW>
+__global__ __launch_bounds__(256) void rp_scatter_kernel(const uint32_t* __restrict__ rows, uint32_t* __restrict__ out,
+                                                         const int64_t* __restrict__ seg_begin,
+                                                         const int64_t* __restrict__ seg_len,
+                                                         const int64_t* __restrict__ tile_base, uint32_t nseg,
+                                                         uint64_t ntiles, uint32_t kw, int key_len, uint64_t seed,
+                                                         int shift, int bits, const uint32_t* __restrict__ offsets) {
+  constexpr uint32_t TILE = kRpTileBytes / (4 * RW);
+  constexpr int ITEMS = TILE / kBlock;
+  constexpr uint32_t C = RW / 4;                    // 16-byte pieces per row
+  const uint32_t D = 1u << bits, dmask = D - 1;
+  __shared__ __attribute__((aligned(16))) uint4 srow[TILE * C];
+  __shared__ uint16_t perm[TILE];
+  __shared__ uint8_t dslot[TILE];
+  __shared__ uint32_t wcnt[4][256];
+  __shared__ uint32_t bstart[256];
+  __shared__ uint32_t goff[256];
+  __shared__ uint32_t sc[4];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint32_t s = rp_seg_of(tile_base, nseg, tile);
+    const uint64_t r0 = (tile - (uint64_t)tile_base[s]) * TILE;
+    const uint64_t left = (uint64_t)seg_len[s] - r0;
+    const uint32_t cnt = left < TILE ? (uint32_t)left : TILE;
+    tile_to_lds<TILE * C / kBlock>(srow, reinterpret_cast<const uint4*>(rows + ((uint64_t)seg_begin[s] + r0) * RW),
+                                   cnt * C, [](uint32_t q) { return (uint64_t)q; });
+    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    if ((uint32_t)t < D) goff[t] = offsets[tile * D + t];
+    __syncthreads();
+    uint32_t rk[ITEMS], dg[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (TILE / 4) + r * 64 + l;
+      const bool valid = pos < cnt;
+      const uint32_t d = valid ? rp_digit<RW>(reinterpret_cast<const uint32_t*>(srow) + pos * RW + kw, key_len, seed,
+                                              shift, dmask)
+                               : 0u;
+      uint64_t peers = ballot64(valid);
+      for (int k = 0; k < bits; ++k) {
+        const bool bit = (d >> k) & 1u;
+        const uint64_t bb = ballot64(bit);
+        peers &= bit ? bb : ~bb;
+      }
+      const uint32_t below = popc_below(peers);
+      const uint32_t prior = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      rk[r] = prior + below;
+      dg[r] = d;
+    }
+    __syncthreads();
+    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+    wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
+    uint32_t all;
+    bstart[t] = block_exclusive_scan256(c0 + c1 + c2 + c3, sc, all);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (TILE / 4) + r * 64 + l;
+      if (pos < cnt) {
+        const uint32_t slot = bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
+        perm[slot] = (uint16_t)pos;
+        dslot[slot] = (uint8_t)dg[r];
+      }
+    }
+    __syncthreads();
+    uint4* o4 = reinterpret_cast<uint4*>(out);
+    for (uint32_t q = t; q < cnt * C; q += kBlock) {
+      const uint32_t j = q / C, c = q - j * C;
+      const uint32_t d = dslot[j];
+      o4[((uint64_t)goff[d] + (j - bstart[d])) * C + c] = srow[(uint32_t)perm[j] * C + c];
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ uint32_t dword_of(const uint4& x, uint32_t i) {
+  return i == 0 ? x.x : (i == 1 ? x.y : (i == 2 ? x.z : x.w));
+}
+
+// key (<= 8 bytes at dword kw) and the int64 at dword vw of a 16-byte row held in registers
+__device__ __forceinline__ void row16(const uint4& x, uint32_t kw, int key_len, uint32_t vw, uint64_t& k0,
+                                      uint64_t& v) {
+  const uint32_t d0 = dword_of(x, kw) & keep_mask(key_len);
+  const uint32_t d1 = key_len > 4 ? (dword_of(x, kw + 1) & keep_mask(key_len - 4)) : 0u;
+  k0 = (uint64_t)d0 | ((uint64_t)d1 << 32);
+  v = (uint64_t)dword_of(x, vw) | ((uint64_t)dword_of(x, vw + 1) << 32);
+}
+
+// one workgroup per partition pair (grid-stride): LDS table over the build rows, probe, fused
+// Count / Sum(probe int64 at byte col_p) / Sum(build int64 at byte col_b) per match.  16-byte rows
+// (key <= 8 bytes): a partition's build rows and its first probe rows are loaded into registers in
+// one batch before the table is built, so the two HBM round trips overlap.
+__global__ __launch_bounds__(256) void rj_join_sum_kernel(const uint4* __restrict__ brows,
+                                                          const int64_t* __restrict__ bstart,
+                                                          const int64_t* __restrict__ blen,
+                                                          const uint4* __restrict__ prows,
+                                                          const int64_t* __restrict__ pstart,
+                                                          const int64_t* __restrict__ plen, uint64_t nparts,
+                                                          uint32_t kw, int key_len, uint64_t seed, uint32_t col_b,
+                                                          uint32_t col_p, uint32_t* __restrict__ ovf_count,
+                                                          uint32_t* __restrict__ ovf_list, uint64_t* __restrict__ partial) {
+  __shared__ unsigned long long keys[kRjCap];
+  __shared__ uint64_t vals[kRjCap];
+  __shared__ uint32_t bad;
+  __shared__ uint64_t red[3][4];
+  const int t = threadIdx.x;
+  const uint32_t vb = col_b / 4, vp = col_p / 4;
+  uint64_t cnt = 0, sp = 0, sb = 0;
+  auto probe = [&](const uint4& x, uint64_t mask) {
+    uint64_t k0, v;
+    row16(x, kw, key_len, vp, k0, v);
+    uint64_t sl = slot_of(key_hash(k0, 0u, seed), mask);
+    for (;;) {
+      const uint64_t k = keys[sl];
+      if (k == kRjEmpty) break;
+      if (k == k0) {
+        ++cnt;
+        sp += v;
+        sb += vals[sl];
+      }
+      sl = (sl + 1) & mask;
+    }
+  };
+  for (uint64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
+    const uint64_t nb = (uint64_t)blen[p], np = (uint64_t)plen[p];
+    if (nb == 0 || np == 0) continue;
+    if (nb * 4 > (uint64_t)kRjCap * 3) {           // load > 0.75: the global-table path joins it
+      if (t == 0) ovf_list[atomicAdd(ovf_count, 1u)] = (uint32_t)p;
+      continue;
+    }
+    const uint4* b0 = brows + bstart[p];
+    const uint4* p0 = prows + pstart[p];
+    uint4 bx[kRjPer], px[kRjPer];
+#pragma unroll
+    for (int k = 0; k < kRjPer; ++k) {             // clamped, unconditional: registers, no scratch
+      const uint64_t i = t + (uint64_t)k * kBlock;
+      bx[k] = b0[i < nb ? i : nb - 1];
+      px[k] = p0[i < np ? i : np - 1];
+    }
+    uint32_t cap = 64;                             // load <= 0.5 below kRjCap, <= 0.75 at it
+    while (cap < 2 * nb && cap < kRjCap) cap <<= 1;
+    const uint64_t mask = cap - 1;
+    for (uint32_t i = t; i < cap; i += kBlock) keys[i] = kRjEmpty;
+    if (t == 0) bad = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kRjPer; ++k) {
+      if (t + (uint64_t)k * kBlock >= nb) continue;
+      uint64_t k0, v;
+      row16(bx[k], kw, key_len, vb, k0, v);
+      if (k0 == kRjEmpty) {
+        bad = 1;
+        continue;
+      }
+      uint64_t sl = slot_of(key_hash(k0, 0u, seed), mask);
+      while (atomicCAS(&keys[sl], kRjEmpty, (unsigned long long)k0) != kRjEmpty) sl = (sl + 1) & mask;
+      vals[sl] = v;
+    }
+    __syncthreads();
+    if (bad) {                                     // the empty-slot sentinel is a real key here
+      if (t == 0) ovf_list[atomicAdd(ovf_count, 1u)] = (uint32_t)p;
+      __syncthreads();
+      continue;
+    }
+#pragma unroll
+    for (int k = 0; k < kRjPer; ++k)
+      if (t + (uint64_t)k * kBlock < np) probe(px[k], mask);
+    for (uint64_t j = t + (uint64_t)kRjPer * kBlock; j < np; j += kBlock) probe(p0[j], mask);
+    __syncthreads();
+  }
+  cnt = wave_sum64(cnt);
+  sp = wave_sum64(sp);
+  sb = wave_sum64(sb);
+  const int w = wave_id();
+  if (lane_id() == 0) {
+    red[0][w] = cnt;
+    red[1][w] = sp;
+    red[2][w] = sb;
+  }
+  __syncthreads();
+  if (t < 3) partial[(uint64_t)blockIdx.x * 3 + t] = red[t][0] + red[t][1] + red[t][2] + red[t][3];
+}
+
+constexpr unsigned kRpGrid = 2048;
+constexpr unsigned kRjGrid = 4096;
+
+}  // namespace
+
+// One stable radix-partition pass over segments of fixed-width rows (row_bytes 16 or 32, key <= 8
+// bytes at a 4-aligned offset): segment s = rows [seg_begin[s], seg_begin[s] + seg_len[s]) of
+// `rows` is split by digit d = (hash(key) >> shift) & (2^bits - 1) into `out` at the same
+// segment position, digit-major; part_start / part_len (nseg * 2^bits) receive every new
+// partition.  tile_base (nseg + 1, device) = exclusive scan of the segments' tile counts
+// (dr_radix_tile_rows rows per tile); counts = ntiles * 2^bits uint32 of scratch.
+DR_API uint32_t dr_radix_tile_rows(uint32_t row_bytes) { return kRpTileBytes / row_bytes; }
+
+DR_API int dr_radix_partition(const uint8_t* rows, uint8_t* out, uint32_t row_bytes, uint32_t key_off, uint32_t key_len,
+                              uint64_t seed, int shift, int bits, const int64_t* seg_begin, const int64_t* seg_len,
+                              const int64_t* tile_base, uint32_t nseg, uint64_t ntiles, uint64_t total_rows,
+                              uint32_t* counts, int64_t* part_start, int64_t* part_len, hipStream_t s) {
+  if ((row_bytes != 16 && row_bytes != 32) || !key_ok(row_bytes, key_off, key_len) || key_len > 8 || bits < 1 ||
+      bits > 8 || shift < 0 || shift + bits > 64 || total_rows >= (1ull << 32) || nseg == 0)
+    return (int)hipErrorInvalidValue;
+  if (ntiles == 0) {
+    hipMemsetAsync(part_len, 0, sizeof(int64_t) * ((uint64_t)nseg << bits), s);
+    rp_scan_kernel<<<nseg, 256, 0, s>>>(seg_begin, tile_base, bits, counts, part_start, part_len);
+    return 0;
+  }
+  const uint32_t* in = reinterpret_cast<const uint32_t*>(rows);
+  uint32_t* o = reinterpret_cast<uint32_t*>(out);
+  const unsigned g = (unsigned)(ntiles < kRpGrid ? ntiles : kRpGrid);
+  const uint32_t kw = key_off / 4;
+  if (row_bytes == 16) {
+    rp_count_kernel<4><<<g, 256, 0, s>>>(in, seg_begin, seg_len, tile_base, nseg, ntiles, kw, (int)key_len, seed,
+                                         shift, bits, counts);
+    rp_scan_kernel<<<nseg, 256, 0, s>>>(seg_begin, tile_base, bits, counts, part_start, part_len);
+    rp_scatter_kernel<4><<<g, 256, 0, s>>>(in, o, seg_begin, seg_len, tile_base, nseg, ntiles, kw, (int)key_len, seed,
+                                           shift, bits, counts);
+  } else {
+    rp_count_kernel<8><<<g, 256, 0, s>>>(in, seg_begin, seg_len, tile_base, nseg, ntiles, kw, (int)key_len, seed,
+                                         shift, bits, counts);
+    rp_scan_kernel<<<nseg, 256, 0, s>>>(seg_begin, tile_base, bits, counts, part_start, part_len);
+    rp_scatter_kernel<8><<<g, 256, 0, s>>>(in, o, seg_begin, seg_len, tile_base, nseg, ntiles, kw, (int)key_len, seed,
+                                           shift, bits, counts);
+  }
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// Join of aligned partition pairs (build / probe partitions p from the same radix passes) in LDS;
+// acc (3 int64) += (matches, sum of probe int64 at col_p per match, sum of build int64 at col_b
+// per match).  Partitions the LDS table cannot take are appended to ovf_list (ovf_count, device)
+// for the caller's global-table path.  ws = dr_radix_join_workspace() bytes.
+DR_API uint64_t dr_radix_join_workspace() { return (uint64_t)kRjGrid * 3 * 8; }
+
+DR_API int dr_radix_join_sum(const uint8_t* brows, const int64_t* bstart, const int64_t* blen, const uint8_t* prows,
+                             const int64_t* pstart, const int64_t* plen, uint64_t nparts, uint32_t row_bytes,
+                             uint32_t key_off, uint32_t key_len, uint64_t seed, uint32_t col_b, uint32_t col_p,
+                             uint32_t* ovf_count, uint32_t* ovf_list, int64_t* acc, void* ws, hipStream_t s) {
+  if (row_bytes != 16 || !key_ok(row_bytes, key_off, key_len) || key_len > 8 || (col_b & 7) || (col_p & 7) ||
+      col_b + 8 > row_bytes || col_p + 8 > row_bytes || (((uintptr_t)brows | (uintptr_t)prows) & 15))
+    return (int)hipErrorInvalidValue;
+  if (nparts == 0) return 0;
+  const unsigned g = (unsigned)(nparts < kRjGrid ? nparts : kRjGrid);
+  uint64_t* partial = reinterpret_cast<uint64_t*>(ws);
+  rj_join_sum_kernel<<<g, 256, 0, s>>>(reinterpret_cast<const uint4*>(brows), bstart, blen,
+                                       reinterpret_cast<const uint4*>(prows), pstart, plen, nparts, key_off / 4,
+                                       (int)key_len, seed, col_b, col_p, ovf_count, ovf_list, partial);
+  ht_sum_partials<<<1, 256, 0, s>>>(partial, g, reinterpret_cast<unsigned long long*>(acc));
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -38,6 +38,7 @@ class HashJoinConfig:
     hbm_budget: int | None = None
     buckets: int | None = None
     prune: bool = True                # carry only Key + V1 through the grace partitioning
+    radix: bool = True                # LDS radix join of the resident buckets
 
 
 def _i64(v):
@@ -112,9 +113,11 @@ class HashJoinJob:
                 self.grace.add_chunk(t, self._produce(t, a, b))
         t1 = time.perf_counter()
         acc = torch.zeros(3, dtype=torch.int64, device=self.w.device)
-        for _, lr, rr in self.grace.buckets("R", "S"):
-            # (r, s) => r.V1 + s.V1, then Count/Sum: fused into the probe (V1 = bytes 8..15)
-            G.join_sum(lr, rr, 0, 8, 8, 8, acc, self.grace.table, self.grace.log_cap)
+        # (r, s) => r.V1 + s.V1, then Count/Sum: fused into the probe (V1 = bytes 8..15); all
+        # buckets at once through the LDS radix join when they are resident, else bucket by bucket
+        if not (cfg.radix and self.grace.join_sum_all("R", "S", 8, 8, acc)):
+            for _, lr, rr in self.grace.buckets("R", "S"):
+                G.join_sum(lr, rr, 0, 8, 8, 8, acc, self.grace.table, self.grace.log_cap)
         if W > 1:
             shuffle.all_reduce_(acc, "sum", self.w)
         a = acc.tolist()

@@ -37,7 +37,7 @@ from . import sort as S
 _lib.register_signatures({
     "dr_grace_workspace": (c_u64, [c_u64, c_u32, c_u32]),
     "dr_grace_partition": (c_i32, [vp, c_u64, c_u32, c_u32, c_u32, c_u64, c_i32, c_u32, vp, vp, vp, c_u32, vp, vp,
-                                   vp, vp, c_u32, c_u32, vp]),
+                                   vp, vp, c_u32, c_u32, c_i32, vp]),
     "dr_ht_build": (c_i32, [vp, c_u64, c_u32, c_u32, c_u32, c_u64, vp, c_i32, vp]),
     "dr_ht_probe_sum_workspace": (c_u64, []),
     "dr_ht_probe_sum": (c_i32, [vp, c_u64, c_u32, c_u32, c_u32, c_u64, vp, c_i32, vp, c_u32, c_u32, c_u32, vp, vp,
@@ -45,7 +45,19 @@ _lib.register_signatures({
     "dr_ht_probe_pairs": (c_i32, [vp, c_u64, c_u32, c_u32, c_u32, c_u64, vp, c_i32, vp, vp, vp, vp, c_i32, vp]),
 })
 
+_lib.register_signatures({
+    "dr_radix_tile_rows": (c_u32, [c_u32]),
+    "dr_radix_partition": (c_i32, [vp, vp, c_u32, c_u32, c_u32, c_u64, c_i32, c_i32, vp, vp, vp, c_u32, c_u64, c_u64,
+                                   vp, vp, vp, vp]),
+    "dr_radix_join_workspace": (c_u64, []),
+    "dr_radix_join_sum": (c_i32, [vp, vp, vp, vp, vp, vp, c_u64, c_u32, c_u32, c_u32, c_u64, c_u32, c_u32, vp, vp, vp,
+                                  vp, vp]),
+})
+
 HASH_SEED = 0x6A09E667F3BCC908
+# radix join: two more digits of the same 64-bit key hash (the grace buckets use its low word)
+# split every bucket into 2^13 partitions whose build side fits a 64 KiB LDS table
+RADIX_PASSES = ((32, 7), (39, 6))
 MAX_BUCKETS = 256
 BUILD_ROWS_PER_BUCKET = 6_000_000     # table of 2^23 16-byte slots (134 MB) at load <= 0.72
 SLACK = 1.02                          # per-bucket capacity over the even share
@@ -74,13 +86,16 @@ class Partitioner:
 
 
 def partition_rows(rows: torch.Tensor, key_off: int, key_len: int, part: Partitioner, shift: int = 0,
-                   contig_from: int | None = None, seed: int = HASH_SEED, proj: tuple[int, int] | None = None):
+                   contig_from: int | None = None, seed: int = HASH_SEED, proj: tuple[int, int] | None = None,
+                   unordered: bool = False):
     """Scatter ``rows`` [n, stride] uint8 by hash(key) into ``part``'s destinations.  Buckets below
     ``contig_from`` (default: all) append at their fill counters (bounded by cap, overflow flagged);
     buckets from ``contig_from`` on are laid out back to back from row 0 of their pointer.
     ``part.counts`` / ``part.bases`` receive this call's rows and first row per destination.
     ``proj = (byte offset, bytes)``: the destination rows are that slice of every row (column
-    pruning in the same pass)."""
+    pruning in the same pass).  ``unordered``: rows of a destination may land in any order, so when
+    every destination appends at its fill counter the count pass is skipped (one atomic
+    reservation per tile and destination); ``part.counts`` / ``part.bases`` are then not written."""
     _lib.require_gpu_tensor(rows, "partition_rows")
     n, stride = rows.shape
     po, ow = proj if proj is not None else (0, stride)
@@ -89,7 +104,7 @@ def partition_rows(rows: torch.Tensor, key_off: int, key_len: int, part: Partiti
     _lib.call("dr_grace_partition", ptr(rows), c_u64(n), c_u32(stride), c_u32(key_off), c_u32(key_len),
               c_u64(seed & (2**64 - 1)), shift, c_u32(part.nb), ptr(part.ptrs), ptr(part.fill), ptr(part.cap),
               c_u32(cf), ptr(part.counts), ptr(part.bases), ptr(part.overflow), ptr(ws), c_u32(ow), c_u32(po),
-              stream_of(rows))
+              int(unordered), stream_of(rows))
 
 
 def split_by_rank(rows: torch.Tensor, key_off: int, key_len: int, part: Partitioner, out: torch.Tensor,
@@ -103,6 +118,7 @@ def split_by_rank(rows: torch.Tensor, key_off: int, key_len: int, part: Partitio
 
 @dataclass
 class SpillStats:
+    radix_overflow: int = 0           # radix-join partitions joined through the global table
     spilled_bytes: int = 0
     buckets: int = 0
     resident: int = 0
@@ -222,6 +238,7 @@ class GraceHashJoin:
             self.stream_bufs = [{t: torch.empty((caps[t], stride), dtype=torch.uint8, device=dev)
                                  for t in rows_per_rank} for _ in range(2)]
         self._turn = 0
+        self._scratch = None              # radix join: one store-sized buffer, allocated on first use
         if W > 1:
             self.rank_part = Partitioner(W, dev)
             self.sbuf = torch.empty((chunk_rows, stride), dtype=torch.uint8, device=dev)
@@ -257,7 +274,9 @@ class GraceHashJoin:
                 self.staging[k] = torch.empty((int(rows.shape[0] * 1.2), self.stride), dtype=torch.uint8,
                                               device=self.dev)
             st.set_staging(self.staging[k])
-        partition_rows(rows, key_off, self.key_len, st.part, shift=0, contig_from=st.resident, proj=proj)
+        # a join does not need the input order inside a bucket: resident buckets fill without a count pass
+        partition_rows(rows, key_off, self.key_len, st.part, shift=0, contig_from=st.resident, proj=proj,
+                       unordered=True)
         if not self.in_hbm:
             counts = st.part.counts.tolist()          # one small D2H per chunk
             self.copy_stream.wait_stream(main)
@@ -311,12 +330,103 @@ class GraceHashJoin:
             out.append(d)
         return out
 
+    def join_sum_all(self, build: str, probe: str, col_b: int, col_p: int, acc: torch.Tensor) -> bool:
+        """Every bucket pair at once through the LDS radix join (radix_join_sum) when all buckets
+        are resident in HBM and the rows are narrow (pruned); False when the per-bucket path has
+        to run instead."""
+        if not self.in_hbm or self.stride not in (16, 32) or self.key_len > 8 or self.key_off % 4:
+            return False
+        self.finish_partitioning()
+        Bs, Ps = self.stores[build], self.stores[probe]
+        rows = max(Bs.hbm.shape[0], Ps.hbm.shape[0])
+        if self._scratch is None or self._scratch.shape[0] < rows:
+            free = torch.cuda.mem_get_info(self.dev)[0]
+            if rows * self.stride > free * 0.9:
+                return False
+            self._scratch = torch.empty((rows, self.stride), dtype=torch.uint8, device=self.dev)
+        segs = []
+        for st in (Bs, Ps):
+            segs.append((torch.arange(self.B, dtype=torch.int64, device=self.dev) * st.cap,
+                         torch.tensor(st.fill, dtype=torch.int64, device=self.dev)))
+        self.stats.radix_overflow = radix_join_sum(Bs.hbm, segs[0], Ps.hbm, segs[1], self.key_off, self.key_len,
+                                                   col_b, col_p, acc, self._scratch)
+        return True
+
     def clear_table(self):
         self.table.fill_(-1)
 
     def release(self):
         for st in self.stores.values():
             st.release()
+        self._scratch = None
+
+
+_RADIX_SCRATCH: dict = {}
+
+
+def _counts_buf(n: int, dev) -> torch.Tensor:
+    t = _RADIX_SCRATCH.get(("counts", dev))
+    if t is None or t.numel() < n:
+        t = _RADIX_SCRATCH[("counts", dev)] = torch.empty(max(n, 1 << 20), dtype=torch.int32, device=dev)
+    return t
+
+
+def radix_partition(rows: torch.Tensor, out: torch.Tensor, seg_begin: torch.Tensor, seg_len: torch.Tensor,
+                    key_off: int, key_len: int, shift: int, bits: int, seed: int = HASH_SEED):
+    """One stable radix-partition pass (dr_radix_partition): each segment [begin, begin + len) of
+    ``rows`` is split by hash digit into ``out`` at the same rows.  Returns the new partitions'
+    (start, len) device int64 tensors, segment-major (nseg * 2^bits)."""
+    dev = rows.device
+    rb = rows.shape[1]
+    nseg = seg_begin.numel()
+    T = int(_lib.lib().dr_radix_tile_rows(c_u32(rb)))
+    tiles = (seg_len + (T - 1)) // T
+    tile_base = torch.zeros(nseg + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(tiles, 0, out=tile_base[1:])
+    ntiles = int(tile_base[-1].item())
+    counts = _counts_buf(ntiles << bits, dev)
+    ps = torch.empty(nseg << bits, dtype=torch.int64, device=dev)
+    pl = torch.empty(nseg << bits, dtype=torch.int64, device=dev)
+    _lib.call("dr_radix_partition", ptr(rows), ptr(out), c_u32(rb), c_u32(key_off), c_u32(key_len),
+              c_u64(seed & (2**64 - 1)), shift, bits, ptr(seg_begin), ptr(seg_len), ptr(tile_base), c_u32(nseg),
+              c_u64(ntiles), c_u64(rows.shape[0]), ptr(counts), ptr(ps), ptr(pl), stream_of(rows))
+    return ps, pl
+
+
+def radix_join_sum(brows: torch.Tensor, bseg, prows: torch.Tensor, pseg, key_off: int, key_len: int, col_b: int,
+                   col_p: int, acc: torch.Tensor, scratch: torch.Tensor, seed: int = HASH_SEED):
+    """``join_sum`` of every aligned segment pair at once: both sides radix-partitioned further
+    (RADIX_PASSES, through ``scratch`` and back, so ``brows`` / ``prows`` are reordered within
+    their segments) into partitions joined in LDS (dr_radix_join_sum).  Partitions too large for
+    the LDS table (key skew) go through the global hash table.  ``bseg`` / ``pseg`` = (begin, len)
+    device int64 tensors of the segments (e.g. the grace buckets)."""
+    dev = brows.device
+    parts = []
+    for rows, (sb, sl) in ((brows, bseg), (prows, pseg)):
+        tmp = scratch[: rows.shape[0]]
+        (s1, b1), (s2, b2) = RADIX_PASSES
+        ps, pl = radix_partition(rows, tmp, sb, sl, key_off, key_len, s1, b1, seed)
+        ps, pl = radix_partition(tmp, rows, ps, pl, key_off, key_len, s2, b2, seed)
+        parts.append((ps, pl))
+    (bs, bl), (ps, pl) = parts
+    nparts = bs.numel()
+    ovf_count = torch.zeros(1, dtype=torch.int32, device=dev)
+    ovf_list = torch.empty(nparts, dtype=torch.int32, device=dev)
+    ws = _RADIX_SCRATCH.get(("ws", dev))
+    if ws is None:
+        ws = _RADIX_SCRATCH[("ws", dev)] = torch.empty(int(_lib.lib().dr_radix_join_workspace()), dtype=torch.uint8,
+                                                       device=dev)
+    _lib.call("dr_radix_join_sum", ptr(brows), ptr(bs), ptr(bl), ptr(prows), ptr(ps), ptr(pl), c_u64(nparts),
+              c_u32(brows.shape[1]), c_u32(key_off), c_u32(key_len), c_u64(seed & (2**64 - 1)), c_u32(col_b),
+              c_u32(col_p), ptr(ovf_count), ptr(ovf_list), ptr(acc), ptr(ws), stream_of(brows))
+    n_ovf = int(ovf_count.item())
+    if n_ovf:
+        for p in sorted(ovf_list[:n_ovf].tolist()):
+            b0, nb_, p0, np_ = (int(x) for x in (bs[p], bl[p], ps[p], pl[p]))
+            lc = ht_log_cap(nb_)
+            table = torch.empty((1 << lc) * 2, dtype=torch.int64, device=dev)
+            join_sum(brows[b0:b0 + nb_], prows[p0:p0 + np_], key_off, key_len, col_b, col_p, acc, table, lc, seed)
+    return n_ovf
 
 
 def ht_log_cap(n_build: int) -> int:

@@ -198,3 +198,92 @@ def test_hash_join_job_pruned_columns(prune):
     res = job.step()
     assert res == job.expected() and res[0] == 500_000
     job.release()
+
+
+def _kv_rows(keys, vals):
+    r = torch.stack([torch.tensor(keys, dtype=torch.int64), torch.tensor(vals, dtype=torch.int64)], 1)
+    return r.view(torch.uint8).reshape(len(keys), 16).cuda()
+
+
+@pytest.mark.parametrize("case", ["unique", "dups", "skew"])
+def test_radix_join_sum_matches_global_table(case):
+    """LDS radix join over segmented (gapped) stores == the global-table join_sum, including
+    many-to-many keys, a key run too large for the LDS table and the empty-slot sentinel key."""
+    from dryad_amd.ops import grace as G
+    g = torch.Generator().manual_seed({"unique": 1, "dups": 2, "skew": 3}[case])
+    nb_, np_ = 400_000, 600_000
+    if case == "unique":
+        bk = torch.randperm(2_000_000, generator=g)[:nb_]
+    else:
+        bk = torch.randint(0, 150_000, (nb_,), generator=g)
+    pk = torch.randint(0, 2_000_000 if case == "unique" else 150_000, (np_,), generator=g)
+    if case == "skew":
+        bk[:9000] = 77                 # one key's build run > the LDS table
+        pk[:50] = 77
+        bk[9000] = -1                  # the LDS table's empty-slot sentinel as a real key
+        pk[50:53] = -1
+    bv = torch.randint(0, 1 << 40, (nb_,), generator=g)
+    pv = torch.randint(0, 1 << 40, (np_,), generator=g)
+    b, p = _kv_rows(bk.tolist(), bv.tolist()), _kv_rows(pk.tolist(), pv.tolist())
+    lc = G.ht_log_cap(nb_)
+    table = torch.empty((1 << lc) * 2, dtype=torch.int64, device="cuda")
+    ref = torch.zeros(3, dtype=torch.int64, device="cuda")
+    G.join_sum(b, p, 0, 8, 8, 8, ref, table, lc)
+    # the same rows as 3 gapped segments per side, bucketed like the grace pass would not need to be
+    # (any split works: partitions only have to agree between the sides through the hash digits)
+    def segmented(rows, cuts, gap=1000):
+        n = rows.shape[0]
+        out = torch.zeros((n + gap * len(cuts), 16), dtype=torch.uint8, device="cuda")
+        begins, lens, at, prev = [], [], 0, 0
+        for c in list(cuts) + [n]:
+            out[at:at + c - prev] = rows[prev:c]
+            begins.append(at)
+            lens.append(c - prev)
+            at += c - prev + gap
+            prev = c
+        return out, (torch.tensor(begins, device="cuda"), torch.tensor(lens, device="cuda"))
+    # segments must hold every occurrence of a key on one side (like grace buckets): split by key hash
+    hb = (torch.tensor(bk.tolist()) * 0x9E3779B97F4A7C15) >> 62 & 3
+    hp = (torch.tensor(pk.tolist()) * 0x9E3779B97F4A7C15) >> 62 & 3
+    ob, op = torch.argsort(hb, stable=True), torch.argsort(hp, stable=True)
+    cb = torch.bincount(hb, minlength=4).cumsum(0)[:-1].tolist()
+    cp = torch.bincount(hp, minlength=4).cumsum(0)[:-1].tolist()
+    bs, bseg = segmented(b[ob.cuda()], cb)
+    ps, pseg = segmented(p[op.cuda()], cp)
+    scratch = torch.empty((max(bs.shape[0], ps.shape[0]), 16), dtype=torch.uint8, device="cuda")
+    acc = torch.zeros(3, dtype=torch.int64, device="cuda")
+    n_ovf = G.radix_join_sum(bs, bseg, ps, pseg, 0, 8, 8, 8, acc, scratch)
+    assert acc.tolist() == ref.tolist()
+    assert (n_ovf > 0) == (case == "skew")
+
+
+@pytest.mark.parametrize("radix", [True, False])
+def test_hash_join_job_radix(radix):
+    from dryad_amd.models.hashjoin import HashJoinConfig, HashJoinJob
+    job = HashJoinJob(_world(), HashJoinConfig(rows_r=700_000, rows_s=900_000, chunk_rows=300_000, radix=radix))
+    res = job.step()
+    assert res == job.expected() and res[0] == 900_000
+    assert job.step() == res
+    job.release()
+
+
+def test_partition_rows_unordered_matches_ordered_as_multisets():
+    from dryad_amd.ops import grace as G
+    g = torch.Generator().manual_seed(21)
+    keys = torch.randint(0, 7000, (90_000,), generator=g).tolist()
+    rows = _rows(keys)
+    nb, cap = 9, 20_000
+    outs = []
+    for unordered in (False, True):
+        part = G.Partitioner(nb, rows.device)
+        store = torch.zeros((nb * cap, 16), dtype=torch.uint8, device="cuda")
+        part.ptrs.fill_(store.data_ptr())
+        part.fill.copy_(torch.tensor([b * cap for b in range(nb)], dtype=torch.int64))
+        part.cap.copy_(torch.tensor([(b + 1) * cap for b in range(nb)], dtype=torch.int64))
+        G.partition_rows(rows[:40_000], 0, 8, part, proj=(0, 16), unordered=unordered)
+        G.partition_rows(rows[40_000:], 0, 8, part, proj=(0, 16), unordered=unordered)
+        fill = part.fill.tolist()
+        assert int(part.overflow.item()) == 0
+        outs.append([sorted(map(tuple, store[b * cap: fill[b]].view(torch.int64).reshape(-1, 2).tolist()))
+                     for b in range(nb)])
+    assert outs[0] == outs[1]
