@@ -188,6 +188,7 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
                                                          uint32_t* __restrict__ overflow = nullptr) {
   constexpr int TILE = kBlock * ITEMS;
   constexpr int LDS_DW = STAGE_PROJ ? 8192 : 16384;  // projected tiles: 32 KiB, three workgroups per CU
+  static_assert(!STAGE_PROJ || OWC == 4, "staged projections are one 16-byte piece per row");
   const uint32_t W = WC > 0 ? (uint32_t)WC : Wdyn;
   const uint32_t OW = OWC > 0 ? (uint32_t)OWC : OWdyn;
   const uint32_t LW = STAGE_PROJ ? OW : W;            // dwords per row in the LDS image
@@ -210,15 +211,32 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
   }
   const uint64_t beg = (uint64_t)blockIdx.x * per_block;
   const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  // STAGE_PROJ: one 16-byte piece per row, ITEMS per thread, the next tile's loads in flight
+  // while this tile is ranked and written out
+  static_assert(!STAGE_PROJ || ITEMS == 8, "staged projections: 8 pieces per thread");
+  // STAGE_PROJ: the next tile's 8 pieces per thread in 8 named registers (an array is placed in
+  // scratch), in flight while this tile is ranked and written out
+  uint4 p0, p1, p2, p3, p4, p5, p6, p7;
+  const uint32_t pC = W / 4, pP4 = PO / 4;
+  auto issue = [&](uint64_t tb2) {
+    const uint32_t pieces = (uint32_t)((end - tb2) < (uint64_t)TILE ? (end - tb2) : TILE);
+    const uint32_t last = pieces ? pieces - 1 : 0;
+    const uint4* src = reinterpret_cast<const uint4*>(rows + tb2 * W);
+#define DR_GP_LD(I, P) { const uint32_t q = t + (I) * kBlock; P = src[(uint64_t)(q < pieces ? q : last) * pC + pP4]; }
+    DR_GP_LD(0, p0) DR_GP_LD(1, p1) DR_GP_LD(2, p2) DR_GP_LD(3, p3)
+    DR_GP_LD(4, p4) DR_GP_LD(5, p5) DR_GP_LD(6, p6) DR_GP_LD(7, p7)
+#undef DR_GP_LD
+  };
+  if (STAGE_PROJ && beg < end) issue(beg);
   for (uint64_t tb = beg; tb < end; tb += TILE) {
     const uint32_t cnt = (uint32_t)((end - tb) < (uint64_t)TILE ? (end - tb) : TILE);
     if (STAGE_PROJ) {
-      const uint32_t C = W / 4, OC = OW / 4, P4 = PO / 4;
-      tile_to_lds<TILE * 4 / kBlock / 4>(reinterpret_cast<uint4*>(srow), reinterpret_cast<const uint4*>(rows + tb * W), cnt * OC,
-                  [=](uint32_t q) {
-                    const uint32_t j = q / OC, c = q - j * OC;
-                    return (uint64_t)j * C + P4 + c;
-                  });
+      uint4* s4 = reinterpret_cast<uint4*>(srow);
+#define DR_GP_ST(I, P) { const uint32_t q = t + (I) * kBlock; if (q < cnt) s4[q] = P; }
+      DR_GP_ST(0, p0) DR_GP_ST(1, p1) DR_GP_ST(2, p2) DR_GP_ST(3, p3)
+      DR_GP_ST(4, p4) DR_GP_ST(5, p5) DR_GP_ST(6, p6) DR_GP_ST(7, p7)
+#undef DR_GP_ST
+      if (tb + TILE < end) issue(tb + TILE);
     } else if (VEC) {
       tile_to_lds(reinterpret_cast<uint4*>(srow), reinterpret_cast<const uint4*>(rows + tb * W), cnt * W / 4,
                   [](uint32_t q) { return (uint64_t)q; });
@@ -674,13 +692,43 @@ __global__ __launch_bounds__(256) void rp_scatter_kernel(const uint32_t* __restr
   __shared__ uint32_t goff[256];
   __shared__ uint32_t sc[4];
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  auto locate = [&](uint64_t tile, uint32_t& cnt) -> const uint4* {
     const uint32_t s = rp_seg_of(tile_base, nseg, tile);
     const uint64_t r0 = (tile - (uint64_t)tile_base[s]) * TILE;
     const uint64_t left = (uint64_t)seg_len[s] - r0;
-    const uint32_t cnt = left < TILE ? (uint32_t)left : TILE;
-    tile_to_lds<TILE * C / kBlock>(srow, reinterpret_cast<const uint4*>(rows + ((uint64_t)seg_begin[s] + r0) * RW),
-                                   cnt * C, [](uint32_t q) { return (uint64_t)q; });
+    cnt = left < TILE ? (uint32_t)left : TILE;
+    return reinterpret_cast<const uint4*>(rows + ((uint64_t)seg_begin[s] + r0) * RW);
+  };
+  static_assert(TILE * C / kBlock == 8, "8 staged 16-byte pieces per thread");
+  // the next tile's 8 pieces per thread live in 8 named registers across the loop (an array here
+  // was placed in scratch)
+  uint4 p0, p1, p2, p3, p4, p5, p6, p7;
+  const uint4* nsrc = nullptr;
+  uint32_t ncnt = 0;
+  auto issue = [&](const uint4* src, uint32_t pieces) {
+    const uint32_t last = pieces ? pieces - 1 : 0;
+#define DR_RP_LD(I, P) { const uint32_t q = t + (I) * kBlock; P = src[q < pieces ? q : last]; }
+    DR_RP_LD(0, p0) DR_RP_LD(1, p1) DR_RP_LD(2, p2) DR_RP_LD(3, p3)
+    DR_RP_LD(4, p4) DR_RP_LD(5, p5) DR_RP_LD(6, p6) DR_RP_LD(7, p7)
+#undef DR_RP_LD
+  };
+  if ((uint64_t)blockIdx.x < ntiles) {
+    nsrc = locate(blockIdx.x, ncnt);
+    issue(nsrc, ncnt * C);
+  }
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint32_t cnt = ncnt;
+    {
+      const uint32_t pieces = cnt * C;
+#define DR_RP_ST(I, P) { const uint32_t q = t + (I) * kBlock; if (q < pieces) srow[q] = P; }
+      DR_RP_ST(0, p0) DR_RP_ST(1, p1) DR_RP_ST(2, p2) DR_RP_ST(3, p3)
+      DR_RP_ST(4, p4) DR_RP_ST(5, p5) DR_RP_ST(6, p6) DR_RP_ST(7, p7)
+#undef DR_RP_ST
+    }
+    if (tile + gridDim.x < ntiles) {               // the next tile's rows are in flight from here on
+      nsrc = locate(tile + gridDim.x, ncnt);
+      issue(nsrc, ncnt * C);
+    }
     wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
     if ((uint32_t)t < D) goff[t] = offsets[tile * D + t];
     __syncthreads();
