@@ -262,10 +262,17 @@ __global__ __launch_bounds__(256) void seg_reduce_multi_kernel(const E128* __res
 // that start and end inside the lane are written directly), and only the per-lane tail partials
 // take part in a 64-lane segmented scan — 1/PER of the cross-lane traffic of the per-element
 // scan above.  Segments touching the chunk boundary are combined with atomics.
-template <int PER, int NAGG, bool PACKED>
+// KEYS (fused segment ids): no segment-id array.  The entries are sorted E128 {lo = row, hi =
+// key} (lo_mask 0, one 64-bit key word); a lane derives its elements' segment ids from key changes
+// + a wave prefix of its start counts + chunk_base[chunk] (exclusive scan of
+// dr_group_chunk_starts), and writes every group's key (hi ^ key_xor) at its start.
+template <int PER, int NAGG, bool PACKED, bool KEYS = false>
 __global__ __launch_bounds__(256) void seg_reduce_multi_serial(const E128* __restrict__ ent,
                                                                const int64_t* __restrict__ seg, uint64_t n,
-                                                               AggSpecs sp) {
+                                                               AggSpecs sp,
+                                                               const int64_t* __restrict__ chunk_base = nullptr,
+                                                               uint64_t key_xor = 0,
+                                                               uint64_t* __restrict__ keys_out = nullptr) {
   constexpr uint64_t kChunkElems = 64 * PER;
   const int lane = lane_id();
   const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -275,24 +282,72 @@ __global__ __launch_bounds__(256) void seg_reduce_multi_serial(const E128* __res
     int64_t sid[PER];
     uint32_t row[PER];
     int cnt = 0;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const uint64_t i = first + k;
-      if (i < n) {
-        sid[k] = seg[i];
-        row[k] = ent ? (uint32_t)ent[i].lo : (uint32_t)i;
-        cnt = k + 1;
-      } else {
-        sid[k] = INT64_MIN + (int64_t)(lane * PER + k);   // unique, never matches
-        row[k] = 0;
-      }
-    }
     const uint64_t cend = (cbase + kChunkElems < n) ? cbase + kChunkElems : n;
-    // segments continuing across the chunk boundary must be combined atomically
-    const int64_t chunk_first = seg[cbase];
-    const int64_t chunk_last = seg[cend - 1];
-    const bool open_left = cbase > 0 && seg[cbase - 1] == chunk_first;
-    const bool open_right = cend < n && seg[cend] == chunk_last;
+    int64_t chunk_first, chunk_last;
+    bool open_left, open_right;
+    if constexpr (KEYS) {
+      uint64_t kh[PER];
+      uint32_t f[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const uint64_t i = first + k;
+        if (i < n) {
+          const E128 x = ent[i];
+          kh[k] = x.hi;
+          row[k] = (uint32_t)x.lo;
+          cnt = k + 1;
+        } else {
+          kh[k] = 0;
+          row[k] = 0;
+        }
+      }
+      // key of the element before the lane's first: the previous lane's last (lane 0: a load)
+      uint64_t prev = __shfl_up(kh[PER - 1], 1, 64);
+      if (lane == 0 && first > 0) prev = ent[first - 1].hi;
+      uint32_t c = 0;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const uint64_t pk = k == 0 ? prev : kh[k - 1];
+        f[k] = (k < cnt && (first + k == 0 || kh[k] != pk)) ? 1u : 0u;
+        c += f[k];
+      }
+      const uint64_t incl = wave_inclusive_scan64((uint64_t)c);
+      const int64_t b0 = chunk_base[cbase / kChunkElems] + (int64_t)(incl - c);
+      uint32_t run = 0;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        run += f[k];
+        if (k < cnt) {
+          sid[k] = b0 + (int64_t)run - 1;
+          if (f[k]) keys_out[sid[k]] = kh[k] ^ key_xor;
+        } else {
+          sid[k] = INT64_MIN + (int64_t)(lane * PER + k);   // unique, never matches
+        }
+      }
+      const uint64_t total = __shfl(incl, 63, 64);
+      chunk_first = __shfl(sid[0], 0, 64);
+      chunk_last = chunk_base[cbase / kChunkElems] + (int64_t)total - 1;
+      open_left = cbase > 0 && __shfl(f[0], 0, 64) == 0u;
+      open_right = cend < n && ent[cend].hi == ent[cend - 1].hi;
+    } else {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const uint64_t i = first + k;
+        if (i < n) {
+          sid[k] = seg[i];
+          row[k] = ent ? (uint32_t)ent[i].lo : (uint32_t)i;
+          cnt = k + 1;
+        } else {
+          sid[k] = INT64_MIN + (int64_t)(lane * PER + k);   // unique, never matches
+          row[k] = 0;
+        }
+      }
+      // segments continuing across the chunk boundary must be combined atomically
+      chunk_first = seg[cbase];
+      chunk_last = seg[cend - 1];
+      open_left = cbase > 0 && seg[cbase - 1] == chunk_first;
+      open_right = cend < n && seg[cend] == chunk_last;
+    }
     const int64_t head_id = sid[0], tail_id = sid[PER - 1];
     const int64_t prev_tail = __shfl_up(tail_id, 1, 64);
     const int64_t next_head = __shfl_down(head_id, 1, 64);
@@ -615,6 +670,97 @@ DR_API int dr_seg_reduce_multi(const E128* ent, const int64_t* seg, uint64_t n, 
   }
   else
     seg_reduce_multi_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(ent, seg, n, nagg, sp);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+namespace {
+// group starts per 512-entry wave chunk of sorted E128 entries keyed by hi alone (lo_mask 0)
+__global__ __launch_bounds__(256) void group_chunk_starts_kernel(const E128* __restrict__ e, uint64_t n,
+                                                                 int64_t* __restrict__ cnt) {
+  constexpr int PER = 8;
+  constexpr uint64_t kChunkElems = 64 * PER;
+  const int lane = lane_id();
+  const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const uint64_t w0 = (((uint64_t)blockIdx.x * blockDim.x) + threadIdx.x) >> 6;
+  for (uint64_t cbase = w0 * kChunkElems; cbase < n; cbase += waves * kChunkElems) {
+    const uint64_t first = cbase + (uint64_t)lane * PER;
+    uint64_t kh[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) kh[k] = first + k < n ? e[first + k].hi : 0;
+    uint64_t prev = __shfl_up(kh[PER - 1], 1, 64);
+    if (lane == 0 && first > 0) prev = e[first - 1].hi;
+    uint64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      c += (first + k < n && (first + k == 0 || kh[k] != (k == 0 ? prev : kh[k - 1]))) ? 1 : 0;
+    c = wave_sum64(c);
+    if (lane == 0) cnt[cbase / kChunkElems] = (int64_t)c;
+  }
+}
+}  // namespace
+
+// Group starts per 512-entry chunk (cnt: ceil(n / 512) int64) of sorted {row, key} entries.
+DR_API uint32_t dr_group_chunk_elems() { return 512; }
+
+DR_API int dr_group_chunk_starts(const E128* e, uint64_t n, int64_t* cnt, hipStream_t s) {
+  if (n == 0) return 0;
+  group_chunk_starts_kernel<<<grid_for(n, 256 * 8, 8192), 256, 0, s>>>(e, n, cnt);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// dr_seg_reduce_multi with fused segment ids (see seg_reduce_multi_serial KEYS): chunk_base =
+// exclusive scan of dr_group_chunk_starts, keys_out[g] = hi ^ key_xor of group g.
+DR_API int dr_seg_reduce_multi_keys(const E128* ent, uint64_t n, const int64_t* chunk_base, uint64_t key_xor,
+                                    uint64_t* keys_out, int nagg, const int* ops, const void* const* vals,
+                                    void* const* outs, const uint32_t* strides, hipStream_t s) {
+  if (nagg < 1 || nagg > kMaxAggs || ent == nullptr || chunk_base == nullptr || keys_out == nullptr)
+    return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  AggSpecs sp;
+  for (int a = 0; a < nagg; ++a) {
+    sp.op[a] = ops[a];
+    sp.vals[a] = reinterpret_cast<const uint64_t*>(vals[a]);
+    sp.out[a] = reinterpret_cast<uint64_t*>(outs[a]);
+    sp.stride[a] = strides ? strides[a] : 1u;
+    if (sp.out[a] == nullptr || (sp.op[a] != M_COUNT && sp.vals[a] == nullptr)) return (int)hipErrorInvalidValue;
+  }
+  sp.rows = nullptr;
+  {
+    uintptr_t base = UINTPTR_MAX;
+    bool packed = true;
+    int nval = 0;
+    for (int a = 0; a < nagg; ++a) {
+      if (sp.op[a] == M_COUNT) continue;
+      ++nval;
+      packed = packed && sp.stride[a] == 4;
+      base = reinterpret_cast<uintptr_t>(sp.vals[a]) < base ? reinterpret_cast<uintptr_t>(sp.vals[a]) : base;
+    }
+    packed = packed && nval > 0 && (base & 15) == 0;
+    for (int a = 0; a < nagg && packed; ++a) {
+      sp.word[a] = 0;
+      if (sp.op[a] == M_COUNT) continue;
+      const uintptr_t d = reinterpret_cast<uintptr_t>(sp.vals[a]) - base;
+      if (d % 8 != 0 || d / 8 > 3) packed = false;
+      else sp.word[a] = (uint32_t)(d / 8);
+    }
+    if (packed) sp.rows = reinterpret_cast<const uint64_t*>(base);
+  }
+  const unsigned g = grid_for(n, 256 * 8, 8192);
+#define DR_SEGRED_KCASE(N)                                                                                    \
+  case N:                                                                                                     \
+    if (sp.rows) seg_reduce_multi_serial<8, N, true, true><<<g, 256, 0, s>>>(ent, nullptr, n, sp, chunk_base, \
+                                                                             key_xor, keys_out);             \
+    else seg_reduce_multi_serial<8, N, false, true><<<g, 256, 0, s>>>(ent, nullptr, n, sp, chunk_base,        \
+                                                                      key_xor, keys_out);                    \
+    break;
+  switch (nagg) {
+    DR_SEGRED_KCASE(1) DR_SEGRED_KCASE(2) DR_SEGRED_KCASE(3) DR_SEGRED_KCASE(4)
+    DR_SEGRED_KCASE(5) DR_SEGRED_KCASE(6) DR_SEGRED_KCASE(7)
+    default: DR_SEGRED_KCASE(8)
+  }
+#undef DR_SEGRED_KCASE
   DR_LAUNCH_CHECK();
   return 0;
 }

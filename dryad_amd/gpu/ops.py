@@ -641,6 +641,17 @@ def _payload_groups(kcols, skeys, specs, n):
     return got[0].to(k.dtype), got[1]
 
 
+def _fused_int64_groups(kcols, skeys, specs):
+    """(keys, aggregate columns) through R.group_reduce_sorted for one plain int64 key, else None."""
+    if not R.FUSED_GROUP_KEYS or len(kcols) != 1 or skeys[0] is not None or kcols[0].dtype != torch.int64:
+        return None
+    _row_index_fits(kcols[0].shape[0])
+    srt = R.int_key_sort(kcols[0])
+    if srt is None:
+        return None
+    return R.group_reduce_sorted(srt, specs, -(1 << 63))
+
+
 def op_group_partial(op, inputs, v):
     t = _check(_one(inputs))
     d = op["decomp"]
@@ -661,6 +672,14 @@ def op_group_partial(op, inputs, v):
                 for nm, r in zip(names, res):
                     out[nm] = r
                 return _partial_table(out, {}, d, 1, form)
+    # one int64 key: sort through 8-byte entries, then one reduction pass that finds the groups
+    # itself (no segment-id array, keys written at the group starts)
+    fused = _fused_int64_groups(kcols, skeys, specs)
+    if fused is not None:
+        out = {"k0": fused[0]}
+        for nm, r in zip(names, fused[1]):
+            out[nm] = r
+        return _partial_table(out, {}, d, 1, form)
     # one int64 key folding <= 3 columns: the values ride in the sort entries (no random gather)
     got = _payload_groups(kcols, skeys, specs, t.n)
     if got is not None:

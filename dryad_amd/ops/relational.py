@@ -221,7 +221,10 @@ def gen_records64(cols: list, first: int, nkeys: int, seed: int, dim_mult: int =
     return cols
 
 
-_lib.register_signatures({"dr_seg_reduce_multi": (c_i32, [vp, vp, c_u64, c_i32, vp, vp, vp, vp, vp])})
+_lib.register_signatures({"dr_seg_reduce_multi": (c_i32, [vp, vp, c_u64, c_i32, vp, vp, vp, vp, vp]),
+                          "dr_group_chunk_elems": (c_u32, []),
+                          "dr_group_chunk_starts": (c_i32, [vp, c_u64, vp, vp]),
+                          "dr_seg_reduce_multi_keys": (c_i32, [vp, c_u64, vp, c_u64, vp, c_i32, vp, vp, vp, vp, vp])})
 
 _MOPS = {("sum", 0): 0, ("min", 0): 1, ("max", 0): 2, ("count", 0): 3, ("sum", 1): 4, ("min", 1): 5, ("max", 1): 6}
 # value columns of a permuted segmented reduction over at least this many rows are first packed
@@ -231,15 +234,37 @@ _MOPS = {("sum", 0): 0, ("min", 0): 1, ("max", 0): 2, ("count", 0): 3, ("sum", 1
 AOS_MIN_ROWS = int(os.environ.get("DRYAD_SEGRED_AOS_MIN_ROWS", str(1 << 24)))
 
 
-def seg_reduce_multi(entries: torch.Tensor | None, seg: torch.Tensor, nseg: int, specs: list) -> list:
+FUSED_GROUP_KEYS = os.environ.get("DRYAD_FUSED_GROUP_KEYS", "1") == "1"
+
+
+def group_reduce_sorted(srt: torch.Tensor, specs: list, key_xor: int):
+    """GroupBy over entries sorted by one 64-bit key word (``int_key_sort`` layout: lo = row, hi =
+    normalised key) without materialising segment ids: a chunk pass counts the group starts per
+    512 entries, and the multi-aggregate reduction derives every element's group from key changes
+    and writes each group's key (hi ^ key_xor) itself.  Returns (keys int64 [nseg], outs)."""
+    n = srt.shape[0]
+    dev = srt.device
+    ch = int(_lib.lib().dr_group_chunk_elems())
+    cnt = torch.empty(-(-n // ch), dtype=torch.int64, device=dev)
+    _lib.call("dr_group_chunk_starts", ptr(srt), c_u64(n), ptr(cnt), stream_of(srt))
+    base = scan_exclusive(cnt)
+    nseg = int((base[-1] + cnt[-1]).item())
+    keys = torch.empty(nseg, dtype=torch.int64, device=dev)
+    outs = seg_reduce_multi(srt, None, nseg, specs, fused=(base, key_xor, keys))
+    return keys, outs
+
+
+def seg_reduce_multi(entries: torch.Tensor | None, seg: torch.Tensor | None, nseg: int, specs: list,
+                     fused: tuple | None = None) -> list:
     """Several segmented reductions in ONE pass over the sorted entries.
 
     ``specs``: [(op, vals, dtype)] with op in sum/min/max/count, vals a column in original row
     order (None for count) and dtype torch.int64 or torch.float64.  Returns one [nseg] tensor per
     spec.  With a row permutation (``entries``), several value columns and many rows, the columns
-    are packed into one row-major buffer first (the kernel reads strided values)."""
-    n = seg.shape[0]
-    dev = seg.device
+    are packed into one row-major buffer first (the kernel reads strided values).  ``fused =
+    (chunk_base, key_xor, keys_out)``: no ``seg`` array (group_reduce_sorted)."""
+    n = entries.shape[0] if fused is not None else seg.shape[0]
+    dev = entries.device if fused is not None else seg.device
     outs, keep = [], []
     ops = (ctypes.c_int * max(1, len(specs)))()
     vps = (ctypes.c_void_p * max(1, len(specs)))()
@@ -287,7 +312,13 @@ def seg_reduce_multi(entries: torch.Tensor | None, seg: torch.Tensor, nseg: int,
             v8 = (ctypes.c_void_p * m)(*[vps[k + j] for j in range(m)])
             p8 = (ctypes.c_void_p * m)(*[ops_p[k + j] for j in range(m)])
             s8 = (ctypes.c_uint32 * m)(*[strides[k + j] for j in range(m)])
-            _lib.call("dr_seg_reduce_multi", ptr(entries), ptr(seg), c_u64(n), m, o8, v8, p8, s8, stream_of(seg))
+            if fused is not None:
+                base, kx, keys_out = fused
+                _lib.call("dr_seg_reduce_multi_keys", ptr(entries), c_u64(n), ptr(base),
+                          c_u64(kx & (2**64 - 1)), ptr(keys_out), m, o8, v8, p8, s8, stream_of(entries))
+            else:
+                _lib.call("dr_seg_reduce_multi", ptr(entries), ptr(seg), c_u64(n), m, o8, v8, p8, s8,
+                          stream_of(seg))
     return outs
 
 

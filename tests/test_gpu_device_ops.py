@@ -296,3 +296,34 @@ def test_seg_reduce_packed_rows_any_width(ncols, monkeypatch):
     for j, c in enumerate(cols):
         assert torch.equal(got[1 + j], red[ops[j]](c)), j
     assert torch.equal(got[-1], red["min"](cols[0]))
+
+
+@pytest.mark.parametrize("n,span,skew", [(1, 8, False), (513, 4, False), (5000, 1, False), (1_000_003, 30, False),
+                                          (2_000_000, 24, True), (300_000, 12, False)])
+def test_group_reduce_sorted_fused_ids_match_torch(n, span, skew):
+    """GroupBy over int_key_sort entries with segment ids derived in the reduction (no id array):
+    keys, Count, int64 Sum/Min, f64 Min/Max/Sum against torch, incl. groups spanning many chunks."""
+    from dryad_amd.ops import relational as R
+    torch.manual_seed(n * 7 + span)
+    lo = -(1 << (span - 1)) if span > 1 else 0
+    key = torch.randint(lo, max(lo + 2, 1 << (span - 1)), (n,), dtype=torch.int64, device="cuda")
+    if skew:
+        key[: n // 3] = 12345                        # one group over ~1300 chunks
+    a = torch.randint(-10**9, 10**9, (n,), dtype=torch.int64, device="cuda")
+    f = torch.randn(n, dtype=torch.float64, device="cuda")
+    specs = [("count", None, torch.int64), ("sum", a, torch.int64), ("min", f, torch.float64),
+             ("max", f, torch.float64), ("min", a, torch.int64)]
+    srt = R.int_key_sort(key)
+    if srt is None:
+        pytest.skip("n < 2")
+    keys, outs = R.group_reduce_sorted(srt, specs, -(1 << 63))
+    uk, inv = torch.unique(key, sorted=True, return_inverse=True)
+    assert torch.equal(keys, uk)
+    g = uk.shape[0]
+    ref = [torch.bincount(inv, minlength=g),
+           torch.zeros(g, dtype=torch.int64, device="cuda").index_add_(0, inv, a),
+           torch.full((g,), float("inf"), dtype=torch.float64, device="cuda").scatter_reduce(0, inv, f, "amin"),
+           torch.full((g,), float("-inf"), dtype=torch.float64, device="cuda").scatter_reduce(0, inv, f, "amax"),
+           torch.full((g,), 2**63 - 1, dtype=torch.int64, device="cuda").scatter_reduce(0, inv, a, "amin")]
+    for o, r in zip(outs, ref):
+        assert torch.equal(o, r)
