@@ -1207,42 +1207,21 @@ __global__ __launch_bounds__(256) void gather_fixup_kernel(const uint32_t* __res
     __syncthreads();
     const uint32_t words = (oe - ob) * W;
     uint32_t* o = out + (c0 + ob) * W;
-    if constexpr (WC > 0) {
-      // every dword of the window's rows in flight at once (WC * 320 / 256 loads per thread): the
-      // random row reads are latency-bound, not bandwidth-bound, with 4 loads in flight per thread.
-      // Clamped unconditional loads keep v[] in VGPRs.
-      constexpr int U = (kGfWin * WC + kBlock - 1) / kBlock;
-      uint32_t v[U];
-      const uint32_t lastw = words - 1;
+    uint32_t j = t;
+    for (; j + 3 * kBlock < words; j += 4 * kBlock) {
+      uint32_t v[4];
 #pragma unroll
-      for (int k = 0; k < U; ++k) {
-        const uint32_t jj0 = t + k * kBlock;
-        const uint32_t jj = jj0 < words ? jj0 : lastw;
-        const uint32_t r = jj / WC, c = jj - r * WC;
-        v[k] = rows[(uint64_t)sidx[r] * WC + c];
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t jj = j + k * kBlock;
+        const uint32_t r = jj / W, c = jj - r * W;
+        v[k] = rows[(uint64_t)sidx[r] * W + c];
       }
 #pragma unroll
-      for (int k = 0; k < U; ++k) {
-        const uint32_t jj = t + k * kBlock;
-        if (jj < words) o[jj] = v[k];
-      }
-    } else {
-      uint32_t j = t;
-      for (; j + 3 * kBlock < words; j += 4 * kBlock) {
-        uint32_t v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t jj = j + k * kBlock;
-          const uint32_t r = jj / W, c = jj - r * W;
-          v[k] = rows[(uint64_t)sidx[r] * W + c];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) o[j + k * kBlock] = v[k];
-      }
-      for (; j < words; j += kBlock) {
-        const uint32_t r = j / W, c = j - r * W;
-        o[j] = rows[(uint64_t)sidx[r] * W + c];
-      }
+      for (int k = 0; k < 4; ++k) o[j + k * kBlock] = v[k];
+    }
+    for (; j < words; j += kBlock) {
+      const uint32_t r = j / W, c = j - r * W;
+      o[j] = rows[(uint64_t)sidx[r] * W + c];
     }
     __syncthreads();
   }
