@@ -487,6 +487,220 @@ __global__ __launch_bounds__(256) void kmeans_mfma_kernel(const float* __restric
 }
 
 
+// K <= 64 on 16x16x32 bf16 MFMA, two workgroups per CU (mode 3, default).
+//
+// The 32x32 kernel above holds a wave's whole K x 128 sum tile in registers (496 VGPR+AGPR) and a
+// 32-point LDS tile per wave, so a CU runs one wave per SIMD and the wave's MFMA, VALU and HBM
+// waits serialise.  Here a workgroup steps over 64 points (16 per wave):
+//   distances  each wave: its 16 points x 16-centroid tiles, 3 split-bf16 MFMAs per 32 dims, the
+//              next step's loads issued per k-step as their registers free up; argmin + runner-up
+//              merged over the 4 lanes that share a point; near ties flagged as before
+//   sums       every wave: the block's 64 points (one-hot x exact 3-part split of x, K = 32 points
+//              per MFMA) for its own 32-dim slice, so a wave keeps K x 32 sums (32 registers)
+// LDS: the block's 64 staged points (34 KB) + split centroids (35 KB at K = 64) -> two workgroups
+// per CU, two waves per SIMD.  Lane map (16x16x32): A[row l&15][k = 8(l>>4) + j],
+// B[k = 8(l>>4) + j][col l&15], C col = l&15, row = 4(l>>4) + reg.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kM16Pts = 64;         // points per workgroup step
+// staged point rows: 130 floats, so the sum MFMAs' transposed reads (16 lanes = 16 consecutive
+// dims of one point, 4 lane groups 8 points apart) hit 64 distinct banks; rows are 8-byte aligned,
+// so staging uses 64-bit LDS writes (a 16-byte write off its alignment replays at 64 cycles)
+constexpr int kXRow16 = 130;
+
+template <int KT>
+__global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __restrict__ X, uint64_t n,
+                                                               const float* __restrict__ C,
+                                                               const float* __restrict__ cnorm, int K,
+                                                               int32_t* __restrict__ assign, double* __restrict__ gsum,
+                                                               unsigned long long* __restrict__ gcnt, int flush_steps) {
+  constexpr int KP = 16 * KT;
+  __shared__ __attribute__((aligned(16))) __bf16 chi[KP * kCRow];
+  __shared__ __attribute__((aligned(16))) __bf16 cmd[KP * kCRow];
+  __shared__ float cn[KP];
+  __shared__ float cmax_s;
+  __shared__ __attribute__((aligned(16))) float xs[kM16Pts * kXRow16];
+  __shared__ int bjs[kM16Pts];
+  __shared__ unsigned int wcnt[KP];
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 15, g = l >> 4;
+  for (int i = t; i < KP * D; i += 256) {
+    const int c = i / D, d = i % D;
+    const float v = c < K ? C[(uint64_t)c * D + d] : 0.f;
+    const __bf16 vh = (__bf16)v;
+    chi[c * kCRow + d] = vh;
+    cmd[c * kCRow + d] = (__bf16)(v - (float)vh);
+  }
+  for (int c = t; c < KP; c += 256) {
+    cn[c] = c < K ? cnorm[c] : __builtin_inff();
+    wcnt[c] = 0u;
+  }
+  if (t == 0) {
+    float m = 0.f;
+    for (int c = 0; c < K; ++c) m = fmaxf(m, cnorm[c]);
+    cmax_s = sqrtf(m);
+  }
+  __syncthreads();
+  const float cmax = cmax_s;
+  const uint64_t steps = (n + kM16Pts - 1) / kM16Pts;
+  f32x4 S[KT][2];
+#pragma unroll
+  for (int ct = 0; ct < KT; ++ct) {
+    S[ct][0] = f32x4{};
+    S[ct][1] = f32x4{};
+  }
+  // lane (r, g) holds point r's dims 32 s + 8 g .. + 7, s < 4
+  float xr[32];
+  auto load_part = [&](uint64_t step, int s_, float* dst) {
+    // clamped, unconditional: a point past n re-reads point n - 1 (its row is finite, its one-hot
+    // is zero since bjs = -1, and it writes no assignment), so no branch wraps the loads
+    const uint64_t p = min(step * kM16Pts + 16 * w + r, n - 1);
+    const float4* src = reinterpret_cast<const float4*>(X + p * D + 32 * s_ + 8 * g);
+    const float4 a = src[0];
+    const float4 b = src[1];
+    dst[8 * s_ + 0] = a.x; dst[8 * s_ + 1] = a.y; dst[8 * s_ + 2] = a.z; dst[8 * s_ + 3] = a.w;
+    dst[8 * s_ + 4] = b.x; dst[8 * s_ + 5] = b.y; dst[8 * s_ + 6] = b.z; dst[8 * s_ + 7] = b.w;
+  };
+  if ((uint64_t)blockIdx.x < steps) {
+#pragma unroll
+    for (int s_ = 0; s_ < 4; ++s_) load_part(blockIdx.x, s_, xr);
+  }
+  auto flush = [&]() {
+#pragma unroll
+    for (int ct = 0; ct < KT; ++ct)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = ct * 16 + 4 * g + q;
+          const float v = S[ct][dt][q];
+          if (c < K && v != 0.f) atomicAdd(gsum + (uint64_t)c * D + 32 * w + 16 * dt + r, (double)v);
+        }
+        S[ct][dt] = f32x4{};
+      }
+  };
+  int since = 0;
+  for (uint64_t step = blockIdx.x; step < steps; step += gridDim.x) {
+    const uint64_t p = step * kM16Pts + 16 * w + r;
+    const bool pvalid = p < n;
+    // stage the wave's 16 points for the sum MFMAs of every wave (point-major rows)
+    float* xrow = xs + (16 * w + r) * kXRow16;
+#pragma unroll
+    for (int s_ = 0; s_ < 4; ++s_)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<float2*>(xrow + 32 * s_ + 8 * g + 2 * q) = make_float2(xr[8 * s_ + 2 * q], xr[8 * s_ + 2 * q + 1]);
+    f32x4 Dt[KT];
+#pragma unroll
+    for (int ct = 0; ct < KT; ++ct) Dt[ct] = f32x4{};
+    float xx = 0.f;
+    const bool more = step + gridDim.x < steps;
+#pragma unroll
+    for (int s_ = 0; s_ < 4; ++s_) {
+      bf16x8 xh, xm;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = xr[8 * s_ + j];
+        xx = fmaf(v, v, xx);
+        xh[j] = (__bf16)v;
+        xm[j] = (__bf16)(v - (float)xh[j]);
+      }
+      if (more) load_part(step + gridDim.x, s_, xr);     // registers free: next step in flight
+      bf16x8 ah[KT], am[KT];                              // every fragment read before the MFMAs
+#pragma unroll
+      for (int ct = 0; ct < KT; ++ct) {
+        ah[ct] = *reinterpret_cast<const bf16x8*>(chi + (ct * 16 + r) * kCRow + 32 * s_ + 8 * g);
+        am[ct] = *reinterpret_cast<const bf16x8*>(cmd + (ct * 16 + r) * kCRow + 32 * s_ + 8 * g);
+      }
+#pragma unroll
+      for (int ct = 0; ct < KT; ++ct) {
+        Dt[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[ct], xh, Dt[ct], 0, 0, 0);
+        Dt[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[ct], xm, Dt[ct], 0, 0, 0);
+        Dt[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[ct], xh, Dt[ct], 0, 0, 0);
+      }
+    }
+    // argmin with the runner-up over this lane's 4 KT centroids, then over the 4 lanes of the point
+    float bd = __builtin_inff(), sd = __builtin_inff();
+    int bj = 0;
+#pragma unroll
+    for (int ct = 0; ct < KT; ++ct)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = ct * 16 + 4 * g + q;
+        const float d = fmaf(-2.f, Dt[ct][q], cn[c]);
+        sd = fminf(sd, fmaxf(bd, d));
+        bj = d < bd ? c : bj;
+        bd = fminf(bd, d);
+      }
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) {
+      const float obd = __shfl_xor(bd, m, 64), osd = __shfl_xor(sd, m, 64);
+      const int obj = __shfl_xor(bj, m, 64);
+      xx += __shfl_xor(xx, m, 64);
+      if (obd < bd || (obd == bd && obj < bj)) {
+        sd = fminf(bd, osd);
+        bd = obd;
+        bj = obj;
+      } else {
+        sd = fminf(sd, obd);
+      }
+    }
+    const bool near = K > 1 && (sd - bd) <= 2.f * kKmTol * sqrtf(xx) * cmax;
+    if (g == 0) {
+      bjs[16 * w + r] = pvalid ? bj : -1;
+      if (pvalid) {
+        atomicAdd(&wcnt[bj], 1u);
+        assign[p] = near ? (int32_t)((uint32_t)bj | 0x80000000u) : bj;
+      }
+    }
+    __syncthreads();
+    // sums over the block's 64 points for this wave's dims 32 w .. 32 w + 31
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int4 b0 = *reinterpret_cast<const int4*>(&bjs[32 * ks + 8 * g]);
+      const int4 b1 = *reinterpret_cast<const int4*>(&bjs[32 * ks + 8 * g + 4]);
+      const int bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      bf16x8 oh[KT];
+#pragma unroll
+      for (int ct = 0; ct < KT; ++ct)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) oh[ct][j] = (bv[j] == ct * 16 + r) ? (__bf16)1.0f : (__bf16)0.0f;
+      float xv[2][8];                                     // both dim tiles' values read up front
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[dt][j] = xs[(32 * ks + 8 * g + j) * kXRow16 + 32 * w + 16 * dt + r];
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        bf16x8 ph, pm, pl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = xv[dt][j];
+          const __bf16 a0 = (__bf16)v;
+          const float r1 = v - (float)a0;
+          const __bf16 a1 = (__bf16)r1;
+          ph[j] = a0;
+          pm[j] = a1;
+          pl[j] = (__bf16)(r1 - (float)a1);
+        }
+#pragma unroll
+        for (int ct = 0; ct < KT; ++ct) {
+          S[ct][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oh[ct], ph, S[ct][dt], 0, 0, 0);
+          S[ct][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oh[ct], pm, S[ct][dt], 0, 0, 0);
+          S[ct][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oh[ct], pl, S[ct][dt], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();                          // xs / bjs are rewritten by the next step
+    if (++since == flush_steps) {
+      since = 0;
+      flush();
+    }
+  }
+  flush();
+  __syncthreads();
+  for (int c = t; c < K; c += 256)
+    if (wcnt[c]) atomicAdd(gcnt + c, (unsigned long long)wcnt[c]);
+}
+
 // Compaction of the near-tie flags (bit 31 of assign) into (point, estimate) pairs; clears the flag.
 __global__ __launch_bounds__(256) void kmeans_near_list(int32_t* __restrict__ assign, uint64_t n,
                                                         uint32_t* __restrict__ near_cnt, uint32_t* __restrict__ near_list) {
@@ -627,7 +841,22 @@ DR_API int dr_kmeans_step(const float* X, uint64_t n, int d, const float* C, int
     uint32_t* near_list = near_cnt + 4;
     hipMemsetAsync(near_cnt, 0, 16, s);
 #define DR_KM3(KTV, DB) kmeans_mfma_kernel<KTV, DB><<<g3, 256, 0, s>>>(X, n, C, cnorm_ws, K, assign, gsum, gcnt, 256)
-    if (K <= 32) {
+    static int m16 = -1;      // DRYAD_KM_MFMA16=0: the 32x32 one-workgroup-per-CU kernel
+    if (m16 < 0) {
+      const char* e = getenv("DRYAD_KM_MFMA16");
+      m16 = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    if (m16 && dbg == 0) {
+      const uint64_t st = (n + kM16Pts - 1) / kM16Pts;
+      const uint64_t cap = 2 * (uint64_t)num_cus();
+      const unsigned g16 = (unsigned)(st < cap ? st : cap);
+#define DR_KM16(KTV) kmeans_mfma16_kernel<KTV><<<g16, 256, 0, s>>>(X, n, C, cnorm_ws, K, assign, gsum, gcnt, 128)
+      if (K <= 16) DR_KM16(1);
+      else if (K <= 32) DR_KM16(2);
+      else if (K <= 48) DR_KM16(3);
+      else DR_KM16(4);
+#undef DR_KM16
+    } else if (K <= 32) {
       DR_KM3(1, 0);
     } else {
       switch (dbg & 7) {
