@@ -519,7 +519,11 @@ __global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __re
   __shared__ float cn[KP];
   __shared__ float cmax_s;
   __shared__ __attribute__((aligned(16))) float xs[kM16Pts * kXRow16];
-  __shared__ int bjs[kM16Pts];
+  // one-hot assignment matrix [centroid][point] in bf16, kept in LDS: each point's owner lane sets
+  // its single 1.0 and clears it again next step, so no lane compares every (centroid, point) pair.
+  // 16-byte slots of a row are XOR-swizzled by (row >> 1) & 7: the A-fragment reads (16 rows x
+  // 2 slots per lane group) then hit 16 distinct bank slots.
+  __shared__ __attribute__((aligned(16))) __bf16 ohs[KP * kM16Pts];
   __shared__ unsigned int wcnt[KP];
   const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 15, g = l >> 4;
   for (int i = t; i < KP * D; i += 256) {
@@ -529,6 +533,7 @@ __global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __re
     chi[c * kCRow + d] = vh;
     cmd[c * kCRow + d] = (__bf16)(v - (float)vh);
   }
+  for (int i = t; i < KP * kM16Pts; i += 256) ohs[i] = (__bf16)0.f;
   for (int c = t; c < KP; c += 256) {
     cn[c] = c < K ? cnorm[c] : __builtin_inff();
     wcnt[c] = 0u;
@@ -550,8 +555,8 @@ __global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __re
   // lane (r, g) holds point r's dims 32 s + 8 g .. + 7, s < 4
   float xr[32];
   auto load_part = [&](uint64_t step, int s_, float* dst) {
-    // clamped, unconditional: a point past n re-reads point n - 1 (its row is finite, its one-hot
-    // is zero since bjs = -1, and it writes no assignment), so no branch wraps the loads
+    // clamped, unconditional: a point past n re-reads point n - 1 (its row is finite, it sets no
+    // one-hot entry and writes no assignment), so no branch wraps the loads
     const uint64_t p = min(step * kM16Pts + 16 * w + r, n - 1);
     const float4* src = reinterpret_cast<const float4*>(X + p * D + 32 * s_ + 8 * g);
     const float4 a = src[0];
@@ -577,7 +582,8 @@ __global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __re
         S[ct][dt] = f32x4{};
       }
   };
-  int since = 0;
+  auto oh_at = [](int c, int pt) { return c * kM16Pts + 8 * ((pt >> 3) ^ ((c >> 1) & 7)) + (pt & 7); };
+  int since = 0, marked = -1;   // marked: the centroid whose one-hot entry this lane set last step
   for (uint64_t step = blockIdx.x; step < steps; step += gridDim.x) {
     const uint64_t p = step * kM16Pts + 16 * w + r;
     const bool pvalid = p < n;
@@ -645,8 +651,10 @@ __global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __re
     }
     const bool near = K > 1 && (sd - bd) <= 2.f * kKmTol * sqrtf(xx) * cmax;
     if (g == 0) {
-      bjs[16 * w + r] = pvalid ? bj : -1;
+      if (marked >= 0) ohs[oh_at(marked, 16 * w + r)] = (__bf16)0.f;
+      marked = pvalid ? bj : -1;
       if (pvalid) {
+        ohs[oh_at(bj, 16 * w + r)] = (__bf16)1.f;
         atomicAdd(&wcnt[bj], 1u);
         assign[p] = near ? (int32_t)((uint32_t)bj | 0x80000000u) : bj;
       }
@@ -655,14 +663,9 @@ __global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __re
     // sums over the block's 64 points for this wave's dims 32 w .. 32 w + 31
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int4 b0 = *reinterpret_cast<const int4*>(&bjs[32 * ks + 8 * g]);
-      const int4 b1 = *reinterpret_cast<const int4*>(&bjs[32 * ks + 8 * g + 4]);
-      const int bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
       bf16x8 oh[KT];
 #pragma unroll
-      for (int ct = 0; ct < KT; ++ct)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) oh[ct][j] = (bv[j] == ct * 16 + r) ? (__bf16)1.0f : (__bf16)0.0f;
+      for (int ct = 0; ct < KT; ++ct) oh[ct] = *reinterpret_cast<const bf16x8*>(ohs + oh_at(ct * 16 + r, 32 * ks + 8 * g));
       float xv[2][8];                                     // both dim tiles' values read up front
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
@@ -689,7 +692,7 @@ __global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __re
         }
       }
     }
-    __syncthreads();                          // xs / bjs are rewritten by the next step
+    __syncthreads();                          // xs / ohs are rewritten by the next step
     if (++since == flush_steps) {
       since = 0;
       flush();

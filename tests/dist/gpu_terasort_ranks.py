@@ -78,8 +78,10 @@ def main():
     # grace hash join across ranks: rank split + all-to-all-v, bucket stores, fused probe; once in
     # HBM and once with a budget that spills buckets to pinned host memory
     from dryad_amd.models.hashjoin import HashJoinConfig, HashJoinJob
-    for budget in (None, 1 << 24):
-        job = HashJoinJob(w, HashJoinConfig(rows_r=200_000, rows_s=300_000, chunk_rows=50_000, hbm_budget=budget))
+    # (pruned rows are 16 of 64 bytes: the pruned spill case needs the smaller budget)
+    for budget, prune in ((None, True), (1 << 24, False), (1 << 21, True)):
+        job = HashJoinJob(w, HashJoinConfig(rows_r=200_000, rows_s=300_000, chunk_rows=50_000, hbm_budget=budget,
+                                            prune=prune))
         res = job.step()
         assert res == job.expected() and res[0] == 300_000, (w.rank, res)
         assert (job.last["spilled_bytes"] > 0) == (budget is not None), job.last
