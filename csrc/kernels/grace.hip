@@ -957,3 +957,461 @@ DR_API int dr_radix_join_sum(const uint8_t* brows, const int64_t* bstart, const 
   DR_LAUNCH_CHECK();
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Radix aggregation: high-cardinality GroupBy on one 8-byte key (K6; the reference's partial +
+// final hash GroupBy vertices, DryadLinqVertex.cs:437-585, with the partitioning of
+// DryadLinqQueryGen.cs:1638-1700).  The same plan as the radix join: split the rows by digits of
+// the key hash until a partition's distinct keys fit an LDS table, then fold every partition on
+// chip.  Per GroupBy:
+//
+//   ra_cols_count / ra_cols_scatter  pass A over the key and value COLUMNS: every row is packed
+//              into a 16- or 32-byte row (key, up to three 8-byte values) while it is split by the
+//              first digit, so packing costs no pass of its own
+//   dr_radix_partition               passes B, C, ... (the join's segmented passes) on the rows
+//   ra_agg     one workgroup per partition: LDS open-addressing table (64-bit CAS on the key,
+//              ds atomics on a count and up to three accumulators), then the groups are written
+//              to the shared output through chunk reservations (one global atomic per 16K groups;
+//              a partition may straddle two chunks).  Only the last chunk of each workgroup can
+//              end partly empty; the caller closes those holes by moving the tail groups in.
+//              Partitions whose table fills (or that hold the empty-slot key) are listed for the
+//              caller's fallback.  Group order is unspecified, as for the LDS hash-agg path.
+namespace {
+
+constexpr int kRaAcc = 3;
+constexpr uint32_t kRaCap = 2048;          // 16 KB keys + 8 KB counts + 48 KB accumulators
+constexpr uint32_t kRaChunk = 16384;       // output groups per reservation
+constexpr unsigned kRaGrid = 1024;         // 2 workgroups per CU (72 KB of LDS each)
+constexpr unsigned long long kRaEmpty = 0x8000000000000000ull;
+enum RaOp : int { RA_SUM_I = 0, RA_MIN_I = 1, RA_MAX_I = 2, RA_SUM_F = 4, RA_MIN_F = 5, RA_MAX_F = 6 };
+
+struct RaCols {
+  const uint64_t* key;
+  const uint64_t* val[kRaAcc];
+  int nval;
+};
+
+struct RaSpec {
+  int nacc;
+  int op[kRaAcc];
+  int word[kRaAcc];        // 8-byte word of the packed row that holds the folded value (1..3)
+};
+
+struct RaOut {
+  int64_t* key;
+  int64_t* cnt;
+  uint64_t* acc[kRaAcc];
+};
+
+__device__ __forceinline__ unsigned long long ra_identity(int op) {
+  switch (op) {
+    case RA_MIN_I: return 0x7FFFFFFFFFFFFFFFull;
+    case RA_MAX_I: return 0x8000000000000000ull;
+    case RA_MIN_F: return (unsigned long long)__double_as_longlong(__builtin_inf());
+    case RA_MAX_F: return (unsigned long long)__double_as_longlong(-__builtin_inf());
+    default: return 0ull;
+  }
+}
+
+__device__ __noinline__ void ra_fminmax(unsigned long long* p, double v, bool is_min) {
+  unsigned long long old = *p, assumed;
+  do {
+    assumed = old;
+    const double cur = __longlong_as_double((long long)assumed);
+    if (is_min ? !(v < cur) : !(v > cur)) break;
+    old = atomicCAS(p, assumed, (unsigned long long)__double_as_longlong(v));
+  } while (assumed != old);
+}
+
+__device__ __forceinline__ void ra_fold(unsigned long long* p, uint64_t v, int op) {
+  switch (op) {
+    case RA_SUM_I: atomicAdd(p, (unsigned long long)v); break;
+    case RA_MIN_I: atomicMin(reinterpret_cast<long long*>(p), (long long)v); break;
+    case RA_MAX_I: atomicMax(reinterpret_cast<long long*>(p), (long long)v); break;
+    case RA_SUM_F: atomicAdd(reinterpret_cast<double*>(p), __longlong_as_double((long long)v)); break;
+    case RA_MIN_F: ra_fminmax(p, __longlong_as_double((long long)v), true); break;
+    default: ra_fminmax(p, __longlong_as_double((long long)v), false); break;
+  }
+}
+
+// pass A histogram: the digit of every key of a tile (tiles of the packed row width)
+template <int RW>
+__global__ __launch_bounds__(256) void ra_cols_count_kernel(const uint64_t* __restrict__ key, uint64_t n,
+                                                            uint64_t ntiles, uint64_t seed, int shift, int bits,
+                                                            uint32_t* __restrict__ counts) {
+  constexpr uint32_t TILE = kRpTileBytes / (4 * RW);
+  const uint32_t D = 1u << bits, dmask = D - 1;
+  __shared__ uint32_t hist[4][256];
+  const int t = threadIdx.x, w = wave_id();
+  const uint64_t hs = mix64(seed);               // key_hash(k, 0, seed) of the row passes
+  // one histogram per workgroup over its contiguous tile range (ra_cols_scatter walks the same
+  // range in order), so the digit scan runs over gridDim.x entries instead of every tile
+  const uint64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const uint64_t t0 = blockIdx.x * per, t1 = t0 + per < ntiles ? t0 + per : ntiles;
+  for (int i = t; i < 4 * 256; i += kBlock) (&hist[0][0])[i] = 0;
+  __syncthreads();
+  const uint64_t r_end = t1 * TILE < n ? t1 * TILE : n;
+  for (uint64_t i = t0 * TILE + t; i < r_end; i += kBlock)
+    atomicAdd(&hist[w][(uint32_t)(mix64(key[i] ^ hs) >> shift) & dmask], 1u);
+  __syncthreads();
+  for (uint32_t d = t; d < D; d += kBlock)
+    counts[(uint64_t)blockIdx.x * D + d] = hist[0][d] + hist[1][d] + hist[2][d] + hist[3][d];
+}
+
+// pass A scatter: a tile's key / value columns are loaded (the next tile's while this one is
+// ranked and written), packed into LDS rows, ranked by digit with wave ballots (stable) and
+// written digit-major at the offsets of rp_scan
+template <int RW>
+__global__ __launch_bounds__(256) void ra_cols_scatter_kernel(RaCols in, uint64_t n, uint64_t ntiles, uint64_t seed,
+                                                              int shift, int bits, const uint32_t* __restrict__ offsets,
+                                                              uint32_t* __restrict__ out) {
+  constexpr uint32_t TILE = kRpTileBytes / (4 * RW);
+  constexpr int ITEMS = TILE / kBlock;
+  constexpr uint32_t C = RW / 4;
+  const uint32_t D = 1u << bits, dmask = D - 1;
+  __shared__ __attribute__((aligned(16))) uint4 srow[TILE * C];
+  __shared__ uint16_t perm[TILE];
+  __shared__ uint8_t dslot[TILE];
+  __shared__ uint32_t wcnt[4][256];
+  __shared__ uint32_t bstart[256];
+  __shared__ uint32_t goff[256];
+  __shared__ uint32_t sc[4];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const uint64_t hs = mix64(seed);
+  uint64_t kr[ITEMS], v0[ITEMS], v1[ITEMS], v2[ITEMS];
+#define DR_RA_ISSUE(TL)                                                                   \
+  {                                                                                       \
+    const uint64_t r0_ = (TL) * TILE;                                                     \
+    _Pragma("unroll") for (int r = 0; r < ITEMS; ++r) {                                   \
+      uint64_t i_ = r0_ + w * (TILE / 4) + r * 64 + l;                                    \
+      i_ = i_ < n ? i_ : n - 1;                   /* clamped, unconditional */            \
+      kr[r] = in.key[i_];                                                                 \
+      v0[r] = in.nval > 0 ? in.val[0][i_] : 0ull;                                         \
+      v1[r] = (RW == 8 && in.nval > 1) ? in.val[1][i_] : 0ull;                            \
+      v2[r] = (RW == 8 && in.nval > 2) ? in.val[2][i_] : 0ull;                            \
+    }                                                                                     \
+  }
+  const uint64_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const uint64_t t0 = blockIdx.x * per, t1 = t0 + per < ntiles ? t0 + per : ntiles;
+  if ((uint32_t)t < D) goff[t] = offsets[(uint64_t)blockIdx.x * D + t];   // advanced tile by tile
+  if (t0 < t1) DR_RA_ISSUE(t0)
+  for (uint64_t tile = t0; tile < t1; ++tile) {
+    const uint64_t r0 = tile * TILE;
+    const uint32_t cnt = n - r0 < TILE ? (uint32_t)(n - r0) : TILE;
+    uint32_t dg[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (TILE / 4) + r * 64 + l;
+      dg[r] = (uint32_t)(mix64(kr[r] ^ hs) >> shift) & dmask;
+      if (pos < cnt) {
+        srow[pos * C] = make_uint4((uint32_t)kr[r], (uint32_t)(kr[r] >> 32), (uint32_t)v0[r], (uint32_t)(v0[r] >> 32));
+        if constexpr (C == 2)
+          srow[pos * C + 1] = make_uint4((uint32_t)v1[r], (uint32_t)(v1[r] >> 32), (uint32_t)v2[r], (uint32_t)(v2[r] >> 32));
+      }
+    }
+    if (tile + 1 < t1) DR_RA_ISSUE(tile + 1)
+    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    __syncthreads();
+    uint32_t rk[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (TILE / 4) + r * 64 + l;
+      const bool valid = pos < cnt;
+      const uint32_t d = valid ? dg[r] : 0u;
+      uint64_t peers = ballot64(valid);
+      for (int k = 0; k < bits; ++k) {
+        const bool bit = (d >> k) & 1u;
+        const uint64_t bb = ballot64(bit);
+        peers &= bit ? bb : ~bb;
+      }
+      const uint32_t below = popc_below(peers);
+      const uint32_t prior = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      rk[r] = prior + below;
+      dg[r] = d;
+    }
+    __syncthreads();
+    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+    const uint32_t mine = c0 + c1 + c2 + c3;
+    wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
+    uint32_t all;
+    bstart[t] = block_exclusive_scan256(mine, sc, all);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (TILE / 4) + r * 64 + l;
+      if (pos < cnt) {
+        const uint32_t slot = bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
+        perm[slot] = (uint16_t)pos;
+        dslot[slot] = (uint8_t)dg[r];
+      }
+    }
+    __syncthreads();
+    uint4* o4 = reinterpret_cast<uint4*>(out);
+    for (uint32_t q = t; q < cnt * C; q += kBlock) {
+      const uint32_t j = q / C, c = q - j * C;
+      const uint32_t d = dslot[j];
+      o4[((uint64_t)goff[d] + (j - bstart[d])) * C + c] = srow[(uint32_t)perm[j] * C + c];
+    }
+    __syncthreads();
+    if ((uint32_t)t < D) goff[t] += mine;
+  }
+#undef DR_RA_ISSUE
+}
+
+__device__ __forceinline__ uint64_t ra_word(const uint4& a, const uint4& b, int wi) {
+  switch (wi) {
+    case 1: return (uint64_t)a.z | ((uint64_t)a.w << 32);
+    case 2: return (uint64_t)b.x | ((uint64_t)b.y << 32);
+    default: return (uint64_t)b.z | ((uint64_t)b.w << 32);
+  }
+}
+
+// one workgroup per partition (grid-stride).  The table is sized to the partition (1.5 slots per
+// row, multiple of 64, <= kRaCap; slot = fast range of a second hash), so a small partition clears
+// and scans only its own slots.  A partition's first kRaPer * 256 rows are in registers before its
+// table is built: they were loaded while the previous partition's groups were written out.
+constexpr int kRaPer = 6;
+
+template <int RW>
+__global__ __launch_bounds__(256, 2) void ra_agg_kernel(const uint4* __restrict__ rows, const int64_t* __restrict__ pstart,
+                                                        const int64_t* __restrict__ plen, uint64_t nparts,
+                                                        uint64_t seed, RaSpec sp, RaOut o, uint64_t out_cap,
+                                                        unsigned long long* __restrict__ head,
+                                                        uint32_t* __restrict__ ovf_count, uint32_t* __restrict__ ovf_list,
+                                                        unsigned long long* __restrict__ tails) {
+  constexpr uint32_t C = RW / 4;
+  __shared__ unsigned long long keys[kRaCap];
+  __shared__ uint32_t cnts[kRaCap];
+  __shared__ unsigned long long acc[kRaAcc][kRaCap];
+  __shared__ uint32_t used, bad, lidx;
+  __shared__ unsigned long long ccur, cend, s_first, s_second, s_rem;
+  const int t = threadIdx.x, l = lane_id();
+  const uint64_t hs = mix64(seed);
+  if (t == 0) {
+    ccur = 0;
+    cend = 0;
+  }
+  uint4 ra[kRaPer], rb[kRaPer];
+  // a macro, not a lambda: arrays captured by a lambda were placed in scratch
+#define DR_RA_BATCH(P)                                                                    \
+  {                                                                                       \
+    const uint64_t len_ = (uint64_t)plen[P];                                              \
+    const uint4* base_ = rows + (uint64_t)pstart[P] * C;                                  \
+    const uint64_t last_ = len_ ? len_ - 1 : 0;                                           \
+    _Pragma("unroll") for (int k = 0; k < kRaPer; ++k) { /* clamped, unconditional */     \
+      uint64_t r_ = t + (uint64_t)k * kBlock;                                             \
+      r_ = r_ < len_ ? r_ : last_;                                                        \
+      ra[k] = base_[r_ * C];                                                              \
+      rb[k] = C == 2 ? base_[r_ * C + 1] : make_uint4(0u, 0u, 0u, 0u);                    \
+    }                                                                                     \
+  }
+  auto insert = [&](uint4 a, uint4 b, uint32_t cap) {
+    const unsigned long long k = (unsigned long long)a.x | ((unsigned long long)a.y << 32);
+    if (k == kRaEmpty) {
+      bad = 1;
+      return;
+    }
+    uint32_t sl = (uint32_t)((mix64(mix64(k ^ hs) ^ kSlotMix) >> 32) * (uint64_t)cap >> 32);
+    bool ok = false;
+    for (uint32_t probes = 0; probes < cap; ++probes) {
+      const unsigned long long cur = keys[sl];
+      if (cur == k) {
+        ok = true;
+        break;
+      }
+      if (cur == kRaEmpty) {
+        const unsigned long long prev = atomicCAS(&keys[sl], kRaEmpty, k);
+        if (prev == kRaEmpty) atomicAdd(&used, 1u);
+        if (prev == kRaEmpty || prev == k) {
+          ok = true;
+          break;
+        }
+      }
+      sl = sl + 1 == cap ? 0 : sl + 1;
+    }
+    if (!ok) {                                      // table full
+      bad = 1;
+      return;
+    }
+    atomicAdd(&cnts[sl], 1u);
+#pragma unroll
+    for (int j = 0; j < kRaAcc; ++j)
+      if (j < sp.nacc) ra_fold(&acc[j][sl], ra_word(a, b, sp.word[j]), sp.op[j]);
+  };
+  if ((uint64_t)blockIdx.x < nparts) DR_RA_BATCH(blockIdx.x)
+  for (uint64_t p = blockIdx.x; p < nparts; p += gridDim.x) {
+    const uint64_t len = (uint64_t)plen[p];
+    const uint4* base = rows + (uint64_t)pstart[p] * C;
+    const uint64_t nxt = p + gridDim.x;
+    if (len == 0) {
+      if (nxt < nparts) DR_RA_BATCH(nxt)
+      continue;
+    }
+    uint64_t c64 = ((len + len / 2 + 63) / 64) * 64;
+    const uint32_t cap = c64 < kRaCap ? (uint32_t)c64 : kRaCap;
+    for (uint32_t i = t; i < cap; i += kBlock) {
+      keys[i] = kRaEmpty;
+      cnts[i] = 0;
+#pragma unroll
+      for (int j = 0; j < kRaAcc; ++j)
+        if (j < sp.nacc) acc[j][i] = ra_identity(sp.op[j]);
+    }
+    if (t == 0) {
+      used = 0;
+      bad = 0;
+      lidx = 0;
+    }
+    __syncthreads();
+    // one inlined copy of insert: the batch rotates through ra[0] / rb[0] (constant indices keep
+    // it in registers; an unrolled loop put six copies of the probe + fold code in the kernel)
+#pragma unroll 1
+    for (int k = 0; k < kRaPer; ++k) {
+      if (t + (uint64_t)k * kBlock < len) insert(ra[0], rb[0], cap);
+#pragma unroll
+      for (int q = 0; q + 1 < kRaPer; ++q) {
+        ra[q] = ra[q + 1];
+        rb[q] = rb[q + 1];
+      }
+    }
+    for (uint64_t r = t + (uint64_t)kRaPer * kBlock; r < len; r += kBlock) {
+      const uint4 a = base[r * C];
+      uint4 b = make_uint4(0u, 0u, 0u, 0u);
+      if constexpr (C == 2) b = base[r * C + 1];
+      insert(a, b, cap);
+    }
+    __syncthreads();
+    if (nxt < nparts) DR_RA_BATCH(nxt)             // the next partition's rows arrive meanwhile
+    if (bad) {
+      if (t == 0) ovf_list[atomicAdd(ovf_count, 1u)] = (uint32_t)p;
+      __syncthreads();
+      continue;
+    }
+    if (t == 0) {                                   // output space: rest of the chunk + a new one
+      const unsigned long long ng = used, c = ccur, rem = cend - ccur;
+      s_first = c;
+      s_rem = rem;
+      if (rem >= ng) {
+        ccur = c + ng;
+        s_second = 0;
+      } else {
+        const unsigned long long nb = atomicAdd(head, (unsigned long long)kRaChunk);
+        s_second = nb;
+        ccur = nb + (ng - rem);
+        cend = nb + kRaChunk;
+      }
+    }
+    __syncthreads();
+    const unsigned long long first = s_first, second = s_second, rem = s_rem;
+    for (uint32_t b0 = 0; b0 < cap; b0 += kBlock) {
+      const uint32_t i = b0 + t;
+      const unsigned long long k = i < cap ? keys[i] : kRaEmpty;
+      const bool occ = k != kRaEmpty;
+      const uint64_t m = ballot64(occ);
+      uint32_t wb = 0;
+      if (l == 0 && m) wb = atomicAdd(&lidx, (uint32_t)__popcll(m));
+      wb = __shfl(wb, 0, 64);
+      if (occ) {
+        const unsigned long long li = wb + popc_below(m);
+        const unsigned long long pos = li < rem ? first + li : second + (li - rem);
+        if (pos < out_cap) {
+          o.key[pos] = (int64_t)k;
+          o.cnt[pos] = (int64_t)cnts[i];
+#pragma unroll
+          for (int j = 0; j < kRaAcc; ++j)
+            if (j < sp.nacc) o.acc[j][pos] = acc[j][i];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    tails[2 * (uint64_t)blockIdx.x] = ccur;
+    tails[2 * (uint64_t)blockIdx.x + 1] = cend;
+  }
+#undef DR_RA_BATCH
+}
+
+}  // namespace
+
+// Pass A of the radix aggregation: key column (int64) + nval <= 3 value columns (8-byte words)
+// -> rows of row_bytes (16: key + 1 value, 32: key + 3 values; missing values zero) split by
+// digit (hash(key) >> shift) & (2^bits - 1) into `out`; part_start / part_len (2^bits) receive the
+// partitions.  counts: dr_radix_agg_pack_grid(n, row_bytes) * 2^bits uint32 of scratch;
+// seg_tile (3 int64, device) = {0, 0, that grid}: rp_scan's segment begin and "tile" bases of the
+// one input segment.
+DR_API int dr_radix_agg_pack(const int64_t* key, const void* const* vals, int nval, uint64_t n, uint32_t row_bytes,
+                             uint64_t seed, int shift, int bits, const int64_t* seg_tile, uint32_t* counts,
+                             int64_t* part_start, int64_t* part_len, uint8_t* out, hipStream_t s) {
+  if ((row_bytes != 16 && row_bytes != 32) || nval < 0 || nval > (row_bytes == 16 ? 1 : 3) || bits < 1 || bits > 8 ||
+      shift < 0 || shift + bits > 64 || n == 0 || n >= (1ull << 32))
+    return (int)hipErrorInvalidValue;
+  RaCols in{};
+  in.key = reinterpret_cast<const uint64_t*>(key);
+  for (int j = 0; j < nval; ++j) in.val[j] = reinterpret_cast<const uint64_t*>(vals[j]);
+  in.nval = nval;
+  const uint32_t tile = kRpTileBytes / row_bytes;
+  const uint64_t ntiles = (n + tile - 1) / tile;
+  const unsigned g = (unsigned)(ntiles < kRpGrid ? ntiles : kRpGrid);
+  // counts / offsets per workgroup (its contiguous tile range), so rp_scan's "tiles" are the g
+  // workgroups: seg_tile = {seg_begin = 0, 0, g}
+  if (row_bytes == 16) {
+    ra_cols_count_kernel<4><<<g, 256, 0, s>>>(in.key, n, ntiles, seed, shift, bits, counts);
+    rp_scan_kernel<<<1, 256, 0, s>>>(seg_tile, seg_tile + 1, bits, counts, part_start, part_len);
+    ra_cols_scatter_kernel<4><<<g, 256, 0, s>>>(in, n, ntiles, seed, shift, bits, counts,
+                                                reinterpret_cast<uint32_t*>(out));
+  } else {
+    ra_cols_count_kernel<8><<<g, 256, 0, s>>>(in.key, n, ntiles, seed, shift, bits, counts);
+    rp_scan_kernel<<<1, 256, 0, s>>>(seg_tile, seg_tile + 1, bits, counts, part_start, part_len);
+    ra_cols_scatter_kernel<8><<<g, 256, 0, s>>>(in, n, ntiles, seed, shift, bits, counts,
+                                                reinterpret_cast<uint32_t*>(out));
+  }
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+DR_API uint32_t dr_radix_agg_pack_grid(uint64_t n, uint32_t row_bytes) {
+  const uint64_t ntiles = (n + kRpTileBytes / row_bytes - 1) / (kRpTileBytes / row_bytes);
+  return (uint32_t)(ntiles < kRpGrid ? (ntiles ? ntiles : 1) : kRpGrid);
+}
+
+DR_API uint32_t dr_radix_agg_grid(uint64_t nparts) { return (uint32_t)(nparts < kRaGrid ? (nparts ? nparts : 1) : kRaGrid); }
+DR_API uint32_t dr_radix_agg_chunk() { return kRaChunk; }
+
+// Fold of the final partitions: ops[j] (RaOp) of the 8-byte word words[j] (1..3) of each row,
+// nacc <= 3, plus a count per group.  Groups go to okey / ocnt / oacc[j] at positions reserved
+// from *head (zeroed by the caller) in chunks of dr_radix_agg_chunk(); tails (2 per workgroup of
+// dr_radix_agg_grid(nparts)) receive each workgroup's unused chunk end [cur, end).  out_cap must
+// be >= n + (grid + 1) * chunk.  Partitions the LDS table cannot hold go to ovf_list.
+DR_API int dr_radix_agg(const uint8_t* rows, uint32_t row_bytes, const int64_t* pstart, const int64_t* plen,
+                        uint64_t nparts, uint64_t seed, int nacc, const int* ops, const int* words,
+                        unsigned long long* head, uint64_t out_cap, int64_t* okey, int64_t* ocnt, void* const* oacc,
+                        uint32_t* ovf_count, uint32_t* ovf_list, unsigned long long* tails, hipStream_t s) {
+  if ((row_bytes != 16 && row_bytes != 32) || nacc < 0 || nacc > kRaAcc || ((uintptr_t)rows & 15))
+    return (int)hipErrorInvalidValue;
+  RaSpec sp{};
+  RaOut o{};
+  sp.nacc = nacc;
+  for (int j = 0; j < nacc; ++j) {
+    if (words[j] < 1 || words[j] > (row_bytes == 16 ? 1 : 3) ||
+        !(ops[j] == RA_SUM_I || ops[j] == RA_MIN_I || ops[j] == RA_MAX_I || ops[j] == RA_SUM_F ||
+          ops[j] == RA_MIN_F || ops[j] == RA_MAX_F))
+      return (int)hipErrorInvalidValue;
+    sp.op[j] = ops[j];
+    sp.word[j] = words[j];
+    o.acc[j] = reinterpret_cast<uint64_t*>(oacc[j]);
+  }
+  o.key = okey;
+  o.cnt = ocnt;
+  if (nparts == 0) return 0;
+  const unsigned g = dr_radix_agg_grid(nparts);
+  const uint4* r4 = reinterpret_cast<const uint4*>(rows);
+  if (row_bytes == 16)
+    ra_agg_kernel<4><<<g, 256, 0, s>>>(r4, pstart, plen, nparts, seed, sp, o, out_cap, head, ovf_count, ovf_list, tails);
+  else
+    ra_agg_kernel<8><<<g, 256, 0, s>>>(r4, pstart, plen, nparts, seed, sp, o, out_cap, head, ovf_count, ovf_list, tails);
+  DR_LAUNCH_CHECK();
+  return 0;
+}

@@ -641,6 +641,19 @@ def _payload_groups(kcols, skeys, specs, n):
     return got[0].to(k.dtype), got[1]
 
 
+def _radix_groups(kcols, skeys, specs, n, nd=None):
+    """(keys, aggregate columns) through ops/radixagg.py for one plain integer key on a large
+    partition, else None.  Keys come back in the key column's dtype."""
+    from ..ops import radixagg as RA
+    if len(kcols) != 1 or skeys[0] is not None or kcols[0].dtype not in _INT_KEYS or not RA.wanted(kcols[0]):
+        return None
+    k = kcols[0]
+    got = RA.radix_aggregate(k, specs, nd_est=nd)
+    if got is None or k.dtype == torch.int64:
+        return got
+    return got[0].to(k.dtype), got[1]
+
+
 def _fused_int64_groups(kcols, skeys, specs):
     """(keys, aggregate columns) through R.group_reduce_sorted for one plain int64 key, else None."""
     if not R.FUSED_GROUP_KEYS or len(kcols) != 1 or skeys[0] is not None or kcols[0].dtype != torch.int64:
@@ -662,8 +675,11 @@ def op_group_partial(op, inputs, v):
     kcols, skeys, form = _key_cols(t, op["key"])
     specs, names = _group_specs(d, t)
     # low-cardinality integer keys: one streaming pass into LDS hash tables (no sort)
+    nd_est = None
     if len(kcols) == 1 and skeys[0] is None and not kcols[0].is_floating_point() and t.n >= (1 << 16):
         nd, m = R.estimate_distinct(kcols[0])
+        from ..ops.radixagg import distinct_upper_estimate
+        nd_est = distinct_upper_estimate(nd, m, t.n)
         if nd <= R.HASH_AGG_MAX_KEYS and nd * 8 < m:
             got = R.hash_aggregate(kcols[0], specs)
             if got is not None:
@@ -672,6 +688,13 @@ def op_group_partial(op, inputs, v):
                 for nm, r in zip(names, res):
                     out[nm] = r
                 return _partial_table(out, {}, d, 1, form)
+    # one integer key, many distinct keys: radix-partitioned LDS aggregation (no sort, no gather)
+    got = _radix_groups(kcols, skeys, specs, t.n, nd_est)
+    if got is not None:
+        out = {"k0": got[0]}
+        for nm, r in zip(names, got[1]):
+            out[nm] = r
+        return _partial_table(out, {}, d, 1, form)
     # one int64 key: sort through 8-byte entries, then one reduction pass that finds the groups
     # itself (no segment-id array, keys written at the group starts)
     fused = _fused_int64_groups(kcols, skeys, specs)
@@ -716,7 +739,9 @@ def op_group_final(op, inputs, v):
             specs += [("sum", col, torch.float64), ("sum", t.cols[f"c{j}"], torch.int64)]
         elif a.kind in ("any", "all"):
             specs.append(("max" if a.kind == "any" else "min", col, torch.int64))
-    got = _payload_groups(kcols, skeys, specs, t.n)
+    got = _radix_groups(kcols, skeys, specs, t.n)
+    if got is None:
+        got = _payload_groups(kcols, skeys, specs, t.n)
     if got is not None:
         keys, nseg, res = [got[0]], got[0].shape[0], iter(got[1])
     else:

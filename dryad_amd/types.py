@@ -378,17 +378,40 @@ def infer_type(v) -> DType:
     return Pickle
 
 
+_WIDEN = [Int32, Int64, Float64]
+
+
+def _widen(t: DType, tv: DType) -> DType | None:
+    """Common type of two inferred types: numbers widen Int32 -> Int64 -> Float64, tuple records
+    widen field by field (a tuple stream whose first key fits 32 bits and later keys do not is
+    still an Int64 column); None when they do not combine."""
+    if t == tv:
+        return t
+    if t in _WIDEN and tv in _WIDEN:
+        return _WIDEN[max(_WIDEN.index(t), _WIDEN.index(tv))]
+    if isinstance(t, RecordT) and isinstance(tv, RecordT) and t.pytype is tv.pytype and \
+            len(t.fields) == len(tv.fields) and not t.nullable_fields and not tv.nullable_fields and \
+            all(a == b for (a, _), (b, _) in zip(t.fields, tv.fields)):
+        fields = []
+        for (n, a), (_, b) in zip(t.fields, tv.fields):
+            w = _widen(a, b)
+            if w is None:
+                return None
+            fields.append((n, w))
+        return RecordT(fields, t.pytype)
+    return None
+
+
 def infer_common_type(values) -> DType:
-    """Widen the inferred type over a sample of values (Int32 -> Int64 -> Float64)."""
+    """Widen the inferred type over a sample of values (Int32 -> Int64 -> Float64, per field of
+    tuple records)."""
     t = None
     for v in values:
         tv = infer_type(v)
         if t is None:
             t = tv
         elif t != tv:
-            order = [Int32, Int64, Float64]
-            if t in order and tv in order:
-                t = order[max(order.index(t), order.index(tv))]
-            else:
+            t = _widen(t, tv)
+            if t is None:
                 return Pickle
     return t or Int32
