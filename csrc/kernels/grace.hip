@@ -979,9 +979,9 @@ DR_API int dr_radix_join_sum(const uint8_t* brows, const int64_t* bstart, const 
 namespace {
 
 constexpr int kRaAcc = 3;
-constexpr uint32_t kRaCap = 2048;          // 16 KB keys + 8 KB counts + 48 KB accumulators
+constexpr uint32_t kRaCap = 1024;          // 8 KB keys + 4 KB counts + 24 KB accumulators: 4 workgroups per CU
 constexpr uint32_t kRaChunk = 16384;       // output groups per reservation
-constexpr unsigned kRaGrid = 1024;         // 2 workgroups per CU (72 KB of LDS each)
+constexpr unsigned kRaGrid = 2048;         // 4 workgroups per CU (36 KB of LDS each)
 constexpr unsigned long long kRaEmpty = 0x8000000000000000ull;
 enum RaOp : int { RA_SUM_I = 0, RA_MIN_I = 1, RA_MAX_I = 2, RA_SUM_F = 4, RA_MIN_F = 5, RA_MAX_F = 6 };
 
@@ -1169,14 +1169,17 @@ __device__ __forceinline__ uint64_t ra_word(const uint4& a, const uint4& b, int 
   }
 }
 
-// one workgroup per partition (grid-stride).  The table is sized to the partition (1.5 slots per
+// one workgroup per partition (grid-stride).  The table is sized to the partition (3 slots per
 // row, multiple of 64, <= kRaCap; slot = fast range of a second hash), so a small partition clears
 // and scans only its own slots.  A partition's first kRaPer * 256 rows are in registers before its
 // table is built: they were loaded while the previous partition's groups were written out.
-constexpr int kRaPer = 6;
+constexpr int kRaPer = 3;
+#ifndef RA_SLOTS_PER_ROW
+#define RA_SLOTS_PER_ROW 3          // table load <= 1/3 (all-distinct keys): ~1.2 probes per insert
+#endif
 
 template <int RW>
-__global__ __launch_bounds__(256, 2) void ra_agg_kernel(const uint4* __restrict__ rows, const int64_t* __restrict__ pstart,
+__global__ __launch_bounds__(256, 4) void ra_agg_kernel(const uint4* __restrict__ rows, const int64_t* __restrict__ pstart,
                                                         const int64_t* __restrict__ plen, uint64_t nparts,
                                                         uint64_t seed, RaSpec sp, RaOut o, uint64_t out_cap,
                                                         unsigned long long* __restrict__ head,
@@ -1250,7 +1253,7 @@ __global__ __launch_bounds__(256, 2) void ra_agg_kernel(const uint4* __restrict_
       if (nxt < nparts) DR_RA_BATCH(nxt)
       continue;
     }
-    uint64_t c64 = ((len + len / 2 + 63) / 64) * 64;
+    uint64_t c64 = ((RA_SLOTS_PER_ROW * len + 63) / 64) * 64;
     const uint32_t cap = c64 < kRaCap ? (uint32_t)c64 : kRaCap;
     for (uint32_t i = t; i < cap; i += kBlock) {
       keys[i] = kRaEmpty;
@@ -1265,17 +1268,11 @@ __global__ __launch_bounds__(256, 2) void ra_agg_kernel(const uint4* __restrict_
       lidx = 0;
     }
     __syncthreads();
-    // one inlined copy of insert: the batch rotates through ra[0] / rb[0] (constant indices keep
-    // it in registers; an unrolled loop put six copies of the probe + fold code in the kernel)
-#pragma unroll 1
-    for (int k = 0; k < kRaPer; ++k) {
-      if (t + (uint64_t)k * kBlock < len) insert(ra[0], rb[0], cap);
+    // unrolled: the batch's probe chains overlap (a rolled loop over a rotating register window
+    // was 1.6x slower)
 #pragma unroll
-      for (int q = 0; q + 1 < kRaPer; ++q) {
-        ra[q] = ra[q + 1];
-        rb[q] = rb[q + 1];
-      }
-    }
+    for (int k = 0; k < kRaPer; ++k)
+      if (t + (uint64_t)k * kBlock < len) insert(ra[k], rb[k], cap);
     for (uint64_t r = t + (uint64_t)kRaPer * kBlock; r < len; r += kBlock) {
       const uint4 a = base[r * C];
       uint4 b = make_uint4(0u, 0u, 0u, 0u);

@@ -14,7 +14,7 @@ value.  Here the rows are hash-partitioned instead, the way the radix join parti
    accumulators) and appends its groups to the output (chunk reservations, one global atomic per
    16K groups), so the data crosses HBM ~2x per pass and never through a random gather.
 
-The number of digits comes from the sampled distinct-key estimate (~600 distinct keys per
+The number of digits comes from the sampled distinct-key estimate (~300 distinct keys per
 partition; an overestimate only makes partitions smaller).  Partitions whose table fills, or that
 hold the table's empty-slot key (INT64_MIN), are folded by a torch fallback.  Group order is
 unspecified (LINQ leaves the order of a distributed GroupBy to the partitioning), like the LDS
@@ -47,8 +47,8 @@ _lib.register_signatures({
 MODE = os.environ.get("DRYAD_RADIX_AGG", "auto")
 ENABLED = MODE != "0"
 MIN_ROWS = 1 << 22                 # below this the sort-based path is as fast
-KEYS_PER_PART = int(os.environ.get("DRYAD_RADIX_AGG_KPP", "600"))   # target distinct keys per final
-#                                  partition (LDS table: up to 2048 slots, 1.5 per row)
+KEYS_PER_PART = int(os.environ.get("DRYAD_RADIX_AGG_KPP", "300"))   # target distinct keys per final
+#                                  partition (LDS table: up to 1024 slots, 3 per row)
 MIN_BITS = 11                      # >= 2048 partitions: enough workgroups to fill the chip
 MAX_BITS = 24
 _OPS = {("sum", 0): 0, ("min", 0): 1, ("max", 0): 2, ("sum", 1): 4, ("min", 1): 5, ("max", 1): 6}
@@ -73,10 +73,11 @@ def distinct_upper_estimate(d: int, m: int, n: int) -> int:
 
 
 def plan_bits(nd: int) -> list[int]:
-    """Digit widths of the passes: ~KEYS_PER_PART distinct keys per final partition, <= 8 bits per
-    pass (7 where possible: the partition kernels write 16-row runs per digit at 7 bits)."""
+    """Digit widths of the passes: ~KEYS_PER_PART distinct keys per final partition, as few passes
+    of <= 8 bits as cover them (a pass costs ~2x the rows' bytes of HBM traffic; a narrower digit
+    saves less than that)."""
     bits = max(MIN_BITS, min(MAX_BITS, math.ceil(math.log2(max(nd, 1) / KEYS_PER_PART))))
-    npass = max(1, math.ceil(bits / 7))
+    npass = max(1, math.ceil(bits / 8))
     base, extra = divmod(bits, npass)
     return [base + (1 if i < extra else 0) for i in range(npass)]
 

@@ -6,7 +6,7 @@ from dryad_amd.ops import radixagg as RA
 
 
 def test_plan_bits_targets_lds_table():
-    assert RA.plan_bits(738_000_000) == [7, 7, 7]
+    assert RA.plan_bits(738_000_000) == [8, 7, 7]
     assert sum(RA.plan_bits(10)) == RA.MIN_BITS
     assert all(w <= 8 for w in RA.plan_bits(1 << 40)) and sum(RA.plan_bits(1 << 40)) == RA.MAX_BITS
 
