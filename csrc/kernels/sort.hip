@@ -732,6 +732,115 @@ __global__ __launch_bounds__(256) void bucket_scatter_rows_kernel(const E128* __
     goff[t] += tot;
   }
 }
+// 100-byte rows (TeraSort records): the same scatter with the tile moved as 16-byte pieces and
+// the next tile's pieces and bucket bytes loaded into registers while the current tile is ranked
+// and written (the dword-at-a-time load above exposes one HBM round trip per few dwords).
+constexpr int kBs25Pieces = (kBsTile * 25 / 4 + kBlock - 1) / kBlock;   // 13 per thread
+
+__global__ __launch_bounds__(256) void bucket_scatter_rows25_kernel(const E128* __restrict__ ent,
+                                                                    const uint32_t* __restrict__ rows,
+                                                                    uint32_t* __restrict__ out, uint64_t n,
+                                                                    const uint32_t* __restrict__ offsets,
+                                                                    uint32_t G, uint64_t per_block) {
+  constexpr int ITEMS = kBsTile / kBlock;
+  constexpr uint32_t W = 25;
+  __shared__ __attribute__((aligned(16))) uint32_t srow[kBsTile * W];
+  __shared__ uint16_t perm[kBsTile];
+  __shared__ uint8_t dslot[kBsTile];
+  __shared__ uint32_t wcnt[4][kBins];
+  __shared__ uint32_t goff[kBins];
+  __shared__ uint32_t bstart[kBins];
+  __shared__ uint32_t sc[4];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  goff[t] = offsets[(uint64_t)t * G + blockIdx.x];
+  const uint64_t beg = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  static_assert(kBs25Pieces == 13 && ITEMS == 2, "13 named piece registers, 2 bucket bytes");
+  // named registers (an array here was placed in scratch)
+  uint4 p0, p1, p2, p3, p4, p5, p6, p7, p8, p9, p10, p11, p12;
+  uint32_t dn0, dn1;
+#define DR_BS25_ALL(M) M(0, p0) M(1, p1) M(2, p2) M(3, p3) M(4, p4) M(5, p5) M(6, p6) M(7, p7) M(8, p8) \
+  M(9, p9) M(10, p10) M(11, p11) M(12, p12)
+  // a macro, not a lambda: arrays captured by a lambda are placed in scratch
+#define DR_BS25_LD(I, P) { const uint32_t q_ = t + (I) * kBlock; P = s4_[q_ < pcs_ ? q_ : lp_]; }
+#define DR_BS25_ISSUE(BASE)                                                                   \
+  {                                                                                           \
+    const uint64_t b_ = (BASE);                                                               \
+    const uint32_t c_ = (uint32_t)((end - b_) < (uint64_t)kBsTile ? (end - b_) : kBsTile);    \
+    const uint32_t pcs_ = c_ * W / 4;                                                         \
+    const uint4* s4_ = reinterpret_cast<const uint4*>(rows + b_ * W);                         \
+    const uint32_t lp_ = pcs_ ? pcs_ - 1 : 0;                                                 \
+    DR_BS25_ALL(DR_BS25_LD)                      /* clamped, unconditional */                 \
+    const uint32_t pa_ = w * (kBsTile / 4) + l, pb_ = pa_ + 64;                               \
+    dn0 = (uint32_t)(ent[b_ + (pa_ < c_ ? pa_ : c_ - 1)].hi & 0xFF);                          \
+    dn1 = (uint32_t)(ent[b_ + (pb_ < c_ ? pb_ : c_ - 1)].hi & 0xFF);                          \
+  }
+  if (beg >= end) return;                         // uniform: the whole workgroup leaves
+  DR_BS25_ISSUE(beg)
+  for (uint64_t base = beg; base < end; base += kBsTile) {
+    const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kBsTile ? (end - base) : kBsTile);
+    const uint32_t words = cnt * W, pieces = words / 4;
+    uint4* s4 = reinterpret_cast<uint4*>(srow);
+#define DR_BS25_ST(I, P) { const uint32_t q = t + (I) * kBlock; if (q < pieces) s4[q] = P; }
+    DR_BS25_ALL(DR_BS25_ST)
+#undef DR_BS25_ST
+    for (uint32_t j = pieces * 4 + t; j < words; j += kBlock) srow[j] = rows[base * W + j];   // <= 3 tail dwords
+    uint32_t dg[ITEMS] = {dn0, dn1};
+    // unconditional (the last tile re-reads itself): an array assigned under a branch in the
+    // loop was placed in scratch
+    DR_BS25_ISSUE(base + kBsTile < end ? base + kBsTile : base)
+    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    __syncthreads();
+    uint32_t rk[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kBsTile / 4) + r * 64 + l;
+      const bool valid = pos < cnt;
+      const uint32_t d = valid ? dg[r] : 0u;
+      uint64_t peers = ballot64(valid);
+#pragma unroll
+      for (int k = 0; k < kRadixBits; ++k) {
+        const bool bit = (d >> k) & 1u;
+        const uint64_t b = ballot64(bit);
+        peers &= bit ? b : ~b;
+      }
+      const uint32_t below = popc_below(peers);
+      const uint32_t prior = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      rk[r] = prior + below;
+      dg[r] = d;
+    }
+    __syncthreads();
+    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
+    uint32_t all;
+    bstart[t] = block_exclusive_scan256(tot, sc, all);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kBsTile / 4) + r * 64 + l;
+      if (pos < cnt) {
+        const uint32_t slot = bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
+        perm[slot] = (uint16_t)pos;
+        dslot[slot] = (uint8_t)dg[r];
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = t; q < words; q += kBlock) {
+      const uint32_t j = q / W, c = q - j * W;
+      const uint32_t d = dslot[j];
+      out[((uint64_t)goff[d] + (j - bstart[d])) * W + c] = srow[(uint32_t)perm[j] * W + c];
+    }
+    __syncthreads();
+    goff[t] += tot;
+  }
+#undef DR_BS25_ISSUE
+#undef DR_BS25_LD
+#undef DR_BS25_ALL
+}
 }  // namespace
 
 // Stable bucket scatter of `n` fixed-width rows (stride % 4 == 0, stride <= 128) by the low byte
@@ -753,7 +862,14 @@ DR_API int dr_bucket_scatter_rows(const E128* ent, const uint8_t* rows, uint8_t*
   const uint32_t W = stride / 4;
   const uint32_t* in = reinterpret_cast<const uint32_t*>(rows);
   uint32_t* o = reinterpret_cast<uint32_t*>(out);
-  if (W == 25)
+  static int v2 = -1;   // DRYAD_BUCKET_SCATTER_V2=0: the dword-load kernel (A/B measurements)
+  if (v2 < 0) {
+    const char* e = getenv("DRYAD_BUCKET_SCATTER_V2");
+    v2 = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  if (W == 25 && v2 && (((uintptr_t)rows) & 15) == 0)
+    bucket_scatter_rows25_kernel<<<G, 256, 0, s>>>(ent, in, o, n, counts, G, per_block);
+  else if (W == 25)
     bucket_scatter_rows_kernel<25><<<G, 256, 0, s>>>(ent, in, o, n, W, counts, G, per_block);
   else
     bucket_scatter_rows_kernel<0><<<G, 256, 0, s>>>(ent, in, o, n, W, counts, G, per_block);

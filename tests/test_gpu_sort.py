@@ -111,7 +111,8 @@ def test_range_dest_sub_major_numbering():
     assert torch.equal(out[:, 0], e[:, 0])
 
 
-@pytest.mark.parametrize("n,stride,nb", [(1, 100, 8), (5000, 100, 3), (300_001, 100, 128), (70_000, 16, 256),
+@pytest.mark.parametrize("n,stride,nb", [(1, 100, 8), (5000, 100, 3), (300_001, 100, 128), (3_000_003, 100, 256),
+                                         (70_000, 16, 256),
                                          (4097, 36, 17), (100_000, 128, 64), (20_000, 132, 5)])
 def test_bucket_scatter_rows_is_a_stable_partition(n, stride, nb):
     from dryad_amd.ops import sort as S
