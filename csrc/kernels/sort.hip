@@ -14,6 +14,7 @@
 //                64-entry row), block-local reorder through LDS so that each digit's run is
 //                written contiguously (coalesced 16-byte stores), stable across tiles/blocks.
 #include "common.h"
+#include "terasort_gen.h"
 
 #include <cstdlib>
 
@@ -198,22 +199,27 @@ __global__ __launch_bounds__(256) void rs_scatter_v2(const T* __restrict__ in, T
   goff[t] = offsets[(uint64_t)t * G + blockIdx.x];
   const uint64_t beg = (uint64_t)blockIdx.x * per_block;
   const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  if (beg >= end) return;                          // uniform: the whole workgroup leaves
   T cur[ITEMS], nxt[ITEMS];
-  auto load_tile = [&](uint64_t base, T* dst) {
-    const uint32_t c = (uint32_t)((end - base) < (uint64_t)kTile ? (end - base) : kTile);
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
-      if (pos < c) dst[r] = in[base + pos];
-    }
-  };
-  if (beg < end) load_tile(beg, cur);
+  // clamped, unconditional loads in a macro (a lambda writing these arrays, or a load under a
+  // branch inside the loop, put them in scratch for the wide entry types); a position past the
+  // tile re-reads its last entry and is masked by `valid`
+#define DR_RS_LOAD(BASE, DST)                                                                   \
+  {                                                                                             \
+    const uint64_t b_ = (BASE);                                                                 \
+    const uint32_t c_ = (uint32_t)((end - b_) < (uint64_t)kTile ? (end - b_) : kTile);          \
+    _Pragma("unroll") for (int r = 0; r < ITEMS; ++r) {                                         \
+      const uint32_t pos_ = w * (kTile / 4) + r * 64 + l;                                       \
+      DST[r] = in[b_ + (pos_ < c_ ? pos_ : c_ - 1)];                                            \
+    }                                                                                           \
+  }
+  DR_RS_LOAD(beg, cur)
   for (uint64_t base = beg; base < end; base += kTile) {
     const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kTile ? (end - base) : kTile);
-    if (base + kTile < end) load_tile(base + kTile, nxt);
+    DR_RS_LOAD(base + kTile < end ? base + kTile : base, nxt)
     wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
     __syncthreads();
-    uint32_t rk[ITEMS], dg[ITEMS];
+    uint32_t rd[ITEMS];                              // in-wave rank | digit << 16 (one VGPR each)
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
       const uint32_t pos = w * (kTile / 4) + r * 64 + l;
@@ -231,8 +237,7 @@ __global__ __launch_bounds__(256) void rs_scatter_v2(const T* __restrict__ in, T
       __builtin_amdgcn_wave_barrier();
       if (valid && below == 0) wcnt[w][d] = prior + (uint32_t)__popcll(peers);
       __builtin_amdgcn_wave_barrier();
-      rk[r] = prior + below;
-      dg[r] = d;
+      rd[r] = (prior + below) | (d << 16);
     }
     __syncthreads();
     const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
@@ -244,7 +249,8 @@ __global__ __launch_bounds__(256) void rs_scatter_v2(const T* __restrict__ in, T
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
       const uint32_t pos = w * (kTile / 4) + r * 64 + l;
-      if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
+      const uint32_t d = rd[r] >> 16;
+      if (pos < cnt) stage[bstart[d] + wcnt[w][d] + (rd[r] & 0xFFFFu)] = cur[r];
     }
     __syncthreads();
 #pragma unroll 4
@@ -266,6 +272,7 @@ __global__ __launch_bounds__(256) void rs_scatter_v2(const T* __restrict__ in, T
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) cur[r] = nxt[r];
   }
+#undef DR_RS_LOAD
 }
 
 void scan_inplace(uint32_t* a, uint32_t M, uint32_t* partial, hipStream_t s) {
@@ -841,6 +848,106 @@ __global__ __launch_bounds__(256) void bucket_scatter_rows25_kernel(const E128* 
 #undef DR_BS25_LD
 #undef DR_BS25_ALL
 }
+// The same bucket scatter with the rows GENERATED in place (gensort-style TeraSort records,
+// record first + i for entry i): the send side of a distributed TeraSort over a generated input
+// never stores the input table nor reads it back; each record is built in LDS and written once,
+// into its bucket.
+__global__ __launch_bounds__(256) void bucket_scatter_gen_kernel(const E128* __restrict__ ent, uint64_t first,
+                                                                 uint64_t seed, uint32_t* __restrict__ out, uint64_t n,
+                                                                 const uint32_t* __restrict__ offsets, uint32_t G,
+                                                                 uint64_t per_block) {
+  constexpr int ITEMS = kBsTile / kBlock;
+  constexpr uint32_t W = 25;
+  static_assert(ITEMS == 2, "two records per thread per tile");
+  __shared__ __attribute__((aligned(16))) uint32_t srow[kBsTile * W];
+  __shared__ uint16_t perm[kBsTile];
+  __shared__ uint8_t dslot[kBsTile];
+  __shared__ uint32_t wcnt[4][kBins];
+  __shared__ uint32_t goff[kBins];
+  __shared__ uint32_t bstart[kBins];
+  __shared__ uint32_t sc[4];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const uint64_t beg = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  if (beg >= end) return;                          // uniform: the whole workgroup leaves
+  goff[t] = offsets[(uint64_t)t * G + blockIdx.x];
+  const uint32_t pa = w * (kBsTile / 4) + l, pb = pa + 64;
+  uint32_t dn0, dn1;
+#define DR_BSG_DEST(BASE)                                                                      \
+  {                                                                                            \
+    const uint64_t b_ = (BASE);                                                                \
+    const uint32_t c_ = (uint32_t)((end - b_) < (uint64_t)kBsTile ? (end - b_) : kBsTile);     \
+    dn0 = (uint32_t)(ent[b_ + (pa < c_ ? pa : c_ - 1)].hi & 0xFF);                             \
+    dn1 = (uint32_t)(ent[b_ + (pb < c_ ? pb : c_ - 1)].hi & 0xFF);                             \
+  }
+  DR_BSG_DEST(beg)
+  for (uint64_t base = beg; base < end; base += kBsTile) {
+    const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kBsTile ? (end - base) : kBsTile);
+    const uint32_t words = cnt * W;
+    uint32_t dg[ITEMS] = {dn0, dn1};
+    DR_BSG_DEST(base + kBsTile < end ? base + kBsTile : base)   // next tile's buckets in flight
+    // this thread's two records, built straight into the tile image (stride 25 dwords: odd, so
+    // the 64 lanes' stores hit distinct banks)
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = r == 0 ? pa : pb;
+      if (pos < cnt) {
+        uint32_t rec[25];
+        dr_ts::ts_record(seed, first + base + pos, rec);
+#pragma unroll
+        for (int k = 0; k < 25; ++k) srow[pos * W + k] = rec[k];
+      }
+    }
+    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    __syncthreads();
+    uint32_t rk[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kBsTile / 4) + r * 64 + l;
+      const bool valid = pos < cnt;
+      const uint32_t d = valid ? dg[r] : 0u;
+      uint64_t peers = ballot64(valid);
+#pragma unroll
+      for (int k = 0; k < kRadixBits; ++k) {
+        const bool bit = (d >> k) & 1u;
+        const uint64_t b = ballot64(bit);
+        peers &= bit ? b : ~b;
+      }
+      const uint32_t below = popc_below(peers);
+      const uint32_t prior = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      rk[r] = prior + below;
+      dg[r] = d;
+    }
+    __syncthreads();
+    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
+    uint32_t all;
+    bstart[t] = block_exclusive_scan256(tot, sc, all);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kBsTile / 4) + r * 64 + l;
+      if (pos < cnt) {
+        const uint32_t slot = bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
+        perm[slot] = (uint16_t)pos;
+        dslot[slot] = (uint8_t)dg[r];
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = t; q < words; q += kBlock) {
+      const uint32_t j = q / W, c = q - j * W;
+      const uint32_t d = dslot[j];
+      out[((uint64_t)goff[d] + (j - bstart[d])) * W + c] = srow[(uint32_t)perm[j] * W + c];
+    }
+    __syncthreads();
+    goff[t] += tot;
+  }
+#undef DR_BSG_DEST
+}
 }  // namespace
 
 // Stable bucket scatter of `n` fixed-width rows (stride % 4 == 0, stride <= 128) by the low byte
@@ -873,6 +980,28 @@ DR_API int dr_bucket_scatter_rows(const E128* ent, const uint8_t* rows, uint8_t*
     bucket_scatter_rows_kernel<25><<<G, 256, 0, s>>>(ent, in, o, n, W, counts, G, per_block);
   else
     bucket_scatter_rows_kernel<0><<<G, 256, 0, s>>>(ent, in, o, n, W, counts, G, per_block);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// dr_bucket_scatter_rows for the rows of a generated TeraSort input that were never stored:
+// entry i (in row order) stands for record first + i of gen://terasort with `seed`.
+DR_API int dr_bucket_scatter_gen_terasort(const E128* ent, uint64_t first, uint64_t seed, uint8_t* out, uint64_t n,
+                                          void* ws, uint64_t* bucket_starts, hipStream_t s) {
+  if (n >= (1ull << 32)) return (int)hipErrorInvalidValue;
+  if (n == 0) {
+    hipMemsetAsync(bucket_starts, 0, sizeof(uint64_t) * (kBins + 1), s);
+    return 0;
+  }
+  uint32_t G; uint64_t per_block;
+  sort_geometry(n, G, per_block);
+  uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* partial = counts + (uint64_t)kBins * G;
+  rs_count<<<G, 256, 0, s>>>(ent, n, 64, counts, G, per_block);
+  scan_inplace(counts, kBins * G, partial, s);
+  rs_digit_totals<<<1, kBins, 0, s>>>(counts, G, n, bucket_starts);
+  bucket_scatter_gen_kernel<<<G, 256, 0, s>>>(ent, first, seed, reinterpret_cast<uint32_t*>(out), n, counts, G,
+                                              per_block);
   DR_LAUNCH_CHECK();
   return 0;
 }

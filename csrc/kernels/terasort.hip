@@ -13,37 +13,11 @@
 //   [48,96)  filler: 12 runs of 4 identical letters
 //   [96,100) 0xCC 0xDD 0xEE 0xFF
 #include "common.h"
+#include "terasort_gen.h"
 
 namespace {
 
-__device__ __forceinline__ uint32_t hex_word(uint64_t g, uint32_t k) {
-  // bytes 4k..4k+3 of the 32-hex-digit record number field starting at byte 12 (k in 7..10)
-  uint32_t w = 0;
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    const uint32_t q = 4 * k + b - 12;                    // digit index 16..31
-    const uint32_t nib = (uint32_t)(g >> (4 * (31 - q))) & 0xF;
-    w |= (nib < 10 ? '0' + nib : 'A' + nib - 10) << (8 * b);
-  }
-  return w;
-}
-
-// The 25 little-endian dwords of record g, computed directly (one hash triple per record).
-__device__ __forceinline__ void ts_record(uint64_t seed, uint64_t g, uint32_t* w) {
-  const uint64_t kA = mix64(seed ^ mix64(g));
-  const uint64_t kB = mix64(kA ^ 0xD1B54A32D192ED03ull);
-  const uint64_t fil = mix64(g ^ (seed * 0x2545F4914F6CDD1Dull) ^ 0xF00DF00DF00DF00Dull);
-  w[0] = bswap32((uint32_t)(kA >> 32));
-  w[1] = bswap32((uint32_t)kA);
-  w[2] = (uint32_t)(kB >> 56) | (((uint32_t)(kB >> 48) & 0xFF) << 8) | (0x11u << 24);
-  w[3] = w[4] = w[5] = w[6] = 0x30303030u;
-#pragma unroll
-  for (uint32_t k = 7; k < 11; ++k) w[k] = hex_word(g, k);
-  w[11] = 0xBBAA9988u;
-#pragma unroll
-  for (uint32_t i = 0; i < 12; ++i) w[12 + i] = ('A' + (uint32_t)((fil >> (5 * i)) % 26)) * 0x01010101u;
-  w[24] = 0xFFEEDDCCu;
-}
+using dr_ts::ts_record;
 
 // One workgroup generates 256 consecutive records: each thread builds one record in LDS, then
 // the block streams the 25.6 KB image out with coalesced 16-byte stores.  With KEYS the producer
@@ -52,7 +26,7 @@ __device__ __forceinline__ void ts_record(uint64_t seed, uint64_t g, uint32_t* w
 // that consumes the generated table skips its key-extraction pass (one 100-byte row read each).
 // KEYS: 0 = rows only, 1 = E128 entries (full 80-bit key), 2 = E64 entries of the compact row
 // sort (key bits 0..31 in the high word: the window for a zero common prefix).
-template <int KEYS>
+template <int KEYS, bool ROWS = true>
 __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out, uint64_t n, uint64_t first,
                                                      uint64_t seed, void* __restrict__ keys, uint32_t idx_base,
                                                      unsigned long long* __restrict__ hi_range) {
@@ -63,8 +37,10 @@ __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out,
     if (threadIdx.x < rows) {
       uint32_t w[25];
       ts_record(seed, first + row0 + threadIdx.x, w);
+      if (ROWS) {
 #pragma unroll
-      for (int k = 0; k < 25; ++k) img[threadIdx.x * 25 + k] = w[k];
+        for (int k = 0; k < 25; ++k) img[threadIdx.x * 25 + k] = w[k];
+      }
       if (KEYS) {
         const uint64_t hi = ((uint64_t)bswap32(w[0]) << 32) | bswap32(w[1]);
         const uint32_t idx = idx_base + (uint32_t)(row0 + threadIdx.x);
@@ -80,6 +56,7 @@ __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out,
         mx = hi > mx ? hi : mx;
       }
     }
+    if (!ROWS) continue;                       // keys only: no record image to store
     __syncthreads();
     uint32_t* o = out + row0 * 25;
     const uint32_t words = rows * 25;
@@ -172,6 +149,18 @@ DR_API int dr_terasort_gen_keys64(uint8_t* out, uint64_t n, uint64_t first_index
   ts_gen_kernel<2><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index,
                                                            seed, keys, idx_base,
                                                            reinterpret_cast<unsigned long long*>(hi_range));
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// Entries only (the E128 layout of dr_terasort_gen_keys), no records: the distributed sort's
+// send side generates the records straight into their buckets (dr_bucket_scatter_gen_terasort).
+DR_API int dr_terasort_gen_keys_only(uint64_t n, uint64_t first_index, uint64_t seed, E128* keys, uint32_t idx_base,
+                                     uint64_t* hi_range, hipStream_t s) {
+  if (n == 0) return 0;
+  if (n + idx_base > (1ull << 32)) return (int)hipErrorInvalidValue;
+  ts_gen_kernel<1, false><<<grid_for(n, 256, 16384), 256, 0, s>>>(nullptr, n, first_index, seed, keys, idx_base,
+                                                                  reinterpret_cast<unsigned long long*>(hi_range));
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -186,6 +186,13 @@ def op_read(op, inputs, v):
             if bs is not None:
                 # producer-side key extraction: a following OrderBy(key bytes 0..9) starts sorting
                 rng = torch.tensor([-1, 0], dtype=torch.int64, device=rows.device)
+                if v.world.size > 1 and v.stage.id in getattr(v.runner, "lazy_gen_stages", ()):
+                    # only a fused distributed OrderBy reads this table: entries now, records
+                    # generated straight into the send buckets (or materialised if it is not fused)
+                    TSK.generate_keys_only(hi - lo, lo, int(q.get("seed", 0)), bs.bufs.ent_a, rng)
+                    bs.keys_ready = (rows.data_ptr(), hi - lo, 0, 10, rng, "e128")
+                    bs.lazy_gen = (lo, int(q.get("seed", 0)))
+                    return t
                 if v.world.size == 1 and S.compact_sort_ok(rows, 10):
                     # one rank: the sort takes the compact 8-byte entries
                     TSK.generate_with_keys64(rows, lo, int(q.get("seed", 0)), bs.bufs.ent_a.view(-1), rng)

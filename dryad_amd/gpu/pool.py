@@ -26,6 +26,18 @@ class BufferSet:
         # (rows_in data_ptr, n, key_off, key_len, hi_range device tensor, entry format "e64" |
         # "e128"); consumed by one sort
         self.keys_ready = None
+        # (first record, seed): rows_in holds gen://terasort records first.. that were NOT written
+        # (only their sort entries were); the distributed sort generates them straight into its
+        # send buckets, any other consumer must call materialize() first
+        self.lazy_gen = None
+
+    def materialize(self, n: int):
+        """Write the records a lazy gen://terasort read skipped (no-op otherwise)."""
+        if self.lazy_gen is not None:
+            from ..ops import terasort as TS
+            first, seed = self.lazy_gen
+            TS.generate(self.bufs.rows_in[:n], first, seed)
+            self.lazy_gen = None
 
     def take_keys(self, rows, key_off: int, key_len: int):
         """(hi min, hi max, entry format) of the entries in ent_a for exactly these rows and key,

@@ -37,10 +37,12 @@ _SIGS = {
     "dr_gather_rows": (c_i32, [vp, vp, vp, vp, c_u64, c_u32, vp]),
     "dr_range_dest_u128": (c_i32, [vp, vp, c_u64, vp, c_u32, c_u64, c_i32, c_u32, c_u32, vp]),
     "dr_bucket_scatter_rows": (c_i32, [vp, vp, vp, c_u64, c_u32, vp, vp, vp]),
+    "dr_bucket_scatter_gen_terasort": (c_i32, [vp, c_u64, c_u64, vp, c_u64, vp, vp, vp]),
     "dr_terasort_gen": (c_i32, [vp, c_u64, c_u64, c_u64, vp]),
     "dr_terasort_check": (c_i32, [vp, c_u64, vp, vp]),
     "dr_terasort_gen_keys": (c_i32, [vp, c_u64, c_u64, c_u64, vp, c_u32, vp, vp]),
     "dr_terasort_gen_keys64": (c_i32, [vp, c_u64, c_u64, c_u64, vp, c_u32, vp, vp]),
+    "dr_terasort_gen_keys_only": (c_i32, [c_u64, c_u64, c_u64, vp, c_u32, vp, vp]),
     "dr_tie_fixup": (c_i32, [vp, c_u64, c_u32, vp, vp]),
     "dr_sort_set_items": (None, [c_i32]),
     "dr_gather_set_v4": (None, [c_i32]),

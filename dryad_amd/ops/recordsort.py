@@ -196,7 +196,7 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
                           sample_target: int = 1 << 20, seed: int = 314159,
                           stats: SortStats | None = None, keys_ready: bool = False,
                           hi_bounds: tuple[int, int] | None = None, split_ties: bool = True,
-                          keys_fmt: str = "e128") -> torch.Tensor:
+                          keys_fmt: str = "e128", gen: tuple[int, int] | None = None) -> torch.Tensor:
     """Globally sort the first ``n`` rows of ``bufs.rows_in`` across all ranks.
 
     On return rank r holds, in ``bufs.rows_out[:n_r]``, the r-th key range in ascending order.
@@ -204,7 +204,9 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     already holds the rows' sort entries; ``hi_bounds``: known hi range of the local keys.
     ``split_ties``: runs of equal keys may be split over ranks (skew); keeps the global order but
     not the co-location of equal keys, so the planner turns it off (keep_ties) when a consumer
-    relies on the output being partitioned by the key.
+    relies on the output being partitioned by the key.  ``gen = (first, seed)``: ``rows_in`` was
+    never written; row i is gen://terasort record first + i (``keys_ready`` E128 entries required),
+    generated by the send-buffer pack itself.
 
     With several ranks the exchange is pipelined with the local sort.  The sampled separators cut
     the key space into ``W * B`` ranges, B consecutive ones per destination rank.  One bucket
@@ -217,6 +219,10 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     DryadLinqQueryGen.cs:2362-2474, CrossProduct channels GraphBuilder.cs:481-504)."""
     w = world or get_world()
     rows = bufs.rows_in[:n]
+    if gen is not None and (w.size == 1 or not keys_ready or keys_fmt != "e128"):
+        from . import terasort as TS
+        TS.generate(rows, gen[0], gen[1])       # the fused pack needs the E128 entries of a real exchange
+        gen = None
     if w.size == 1:
         out = local_sort_rows(rows, bufs.rows_out, bufs.ent_a, bufs.ent_b, key_off, key_len,
                               hi_bounds=hi_bounds, keys_ready=keys_ready, keys_fmt=keys_fmt)
@@ -242,7 +248,10 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     seps = choose_separators(ent, n, w, part_mask, sample_target, seed, bufs.ent_b, parts=W * B)
     seps_hi = [int(x) & _M64 for x in seps[:, 1].tolist()]
     S.range_dest(ent, seps, part_mask, subs=B, ranks=W)                  # ent.hi := b * W + rank
-    st = S.bucket_scatter_rows(ent, rows, bufs.rows_out)                 # send buffer, round-major
+    if gen is not None:                                                  # send buffer, round-major
+        st = S.bucket_scatter_gen_terasort(ent, n, gen[0], gen[1], bufs.rows_out)
+    else:
+        st = S.bucket_scatter_rows(ent, rows, bufs.rows_out)
     send = [[st[b * W + r + 1] - st[b * W + r] for r in range(W)] for b in range(B)]
     sc = torch.tensor([[send[b][r] for b in range(B)] for r in range(W)], dtype=torch.int64)
     rc = shuffle.exchange_counts(sc.flatten(), w).view(W, B).tolist()    # rc[src][b]

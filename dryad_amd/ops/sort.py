@@ -247,6 +247,20 @@ def bucket_scatter_rows(entries: torch.Tensor, rows: torch.Tensor, out: torch.Te
     return starts.tolist() if sync else starts
 
 
+def bucket_scatter_gen_terasort(entries: torch.Tensor, n: int, first: int, seed: int, out: torch.Tensor,
+                                sync: bool = True):
+    """``bucket_scatter_rows`` for a gen://terasort input whose records were never stored: entry i
+    (row order) stands for record ``first + i``, which the kernel generates straight into its
+    bucket of ``out`` (dr_bucket_scatter_gen_terasort)."""
+    _lib.require_gpu_tensor(out, "bucket_scatter_gen_terasort")
+    assert out.dtype == torch.uint8 and out.shape[1] == 100 and out.shape[0] >= n and entries.shape[0] >= n
+    starts = torch.empty(257, dtype=torch.int64, device=out.device)
+    ws = _workspace(n, out.device)
+    _lib.call("dr_bucket_scatter_gen_terasort", ptr(entries), c_u64(first), c_u64(seed & (2**64 - 1)), ptr(out),
+              c_u64(n), ptr(ws), ptr(starts), stream_of(out))
+    return starts.tolist() if sync else starts
+
+
 def entries_to_key_int(entries: torch.Tensor, lo_keep_bits: int = 64):
     """Host helper for tests: composite keys as Python ints (hi<<64 | lo masked)."""
     e = entries.cpu().numpy()

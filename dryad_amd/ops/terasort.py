@@ -34,6 +34,17 @@ def generate_with_keys(out: torch.Tensor, first_index: int, seed: int, keys: tor
     return out
 
 
+def generate_keys_only(n: int, first_index: int, seed: int, keys: torch.Tensor,
+                       hi_range: torch.Tensor | None = None) -> torch.Tensor:
+    """The sort entries of ``generate_with_keys`` without the records themselves (a distributed
+    sort then generates each record straight into its send bucket: sort.bucket_scatter_gen_terasort)."""
+    _lib.require_gpu_tensor(keys, "terasort.generate_keys_only")
+    assert keys.shape[0] >= n and keys.dtype == torch.int64 and keys.is_contiguous()
+    _lib.call("dr_terasort_gen_keys_only", c_u64(n), c_u64(first_index), c_u64(seed & (2**64 - 1)), ptr(keys),
+              c_u32(0), ptr(hi_range), stream_of(keys))
+    return keys
+
+
 def generate_with_keys64(out: torch.Tensor, first_index: int, seed: int, keys: torch.Tensor,
                          hi_range: torch.Tensor | None = None) -> torch.Tensor:
     """``generate`` fused with the 8-byte entries of the compact row sort (key bytes 0..3 << 32 |

@@ -163,6 +163,29 @@ class GpuJobRunner:
             return True
         return False
 
+    def _lazy_gen_reads(self) -> set:
+        """gen://terasort read stages whose table only a fused distributed OrderBy consumes: their
+        op_read writes just the sort entries (ops/gpu: lazy_gen) and the records are generated
+        straight into the exchange's send buckets."""
+        st, out = self.plan.stages, set()
+        if self.world.size < 2 or not self.gpu_ok:
+            return out
+        for f in self.fused.values():
+            x = st[f["x"]]
+            if (not x.inputs and len(x.ops) == 1 and x.ops[0]["op"] == "read"
+                    and parse_uri(x.ops[0]["uri"])[0] == "gen" and parse_uri(x.ops[0]["uri"])[1].strip("/") == "terasort"
+                    and set(self.plan.consumers(x.id)) == {f["stages"][0], f["stages"][2]}):
+                out.add(x.id)
+        return out
+
+    def _materialize(self, sid: int):
+        """Write the records of lazy gen reads of stage sid (its consumers are not fused after all)."""
+        for p in range(self.plan.stages[sid].partitions):
+            bs = self.row_sets.get((sid, p))
+            t = self.channels.get((sid, p))
+            if bs is not None and bs.lazy_gen is not None and isinstance(t, DeviceTable):
+                bs.materialize(t.n)
+
     def _run_fused(self, m, f):
         from ..ops import recordsort as RS
         me = self.world.rank
@@ -171,10 +194,15 @@ class GpuJobRunner:
         off, ln = f["spec"]
         stats = RS.SortStats()
         kr = bs.take_keys(t.rows, off, ln)
+        gen, bs.lazy_gen = bs.lazy_gen, None
+        if gen is not None and kr is None:         # entries were not claimed: records are needed
+            bs.lazy_gen = gen
+            bs.materialize(t.n)
+            gen = None
         out = RS.distributed_sort_rows(bs.bufs, t.n, off, ln, self.world, stats=stats,
                                        keys_ready=kr is not None, hi_bounds=None if kr is None else kr[:2],
                                        split_ties=not f.get("keep_ties", False),
-                                       keys_fmt="e128" if kr is None else kr[2])
+                                       keys_fmt="e128" if kr is None else kr[2], gen=gen)
         self.row_sets[(m.id, me)] = bs
         self.last_sort_stats = stats
         table = DeviceTable(out.shape[0], t.shape, rows=out)
@@ -549,6 +577,7 @@ class GpuJobRunner:
         for sid, e in self.external.items():
             self.fused.pop(sid, None)
             self.skipped.update(e["skip"])
+        self.lazy_gen_stages = self._lazy_gen_reads()
         fused_first = {f["stages"][0]: mid for mid, f in self.fused.items()}
         active_fused = {}
         for s in self.plan.stages:
@@ -559,6 +588,8 @@ class GpuJobRunner:
                 if self._fused_applicable(self.fused[mid]):
                     active_fused[mid] = self.fused[mid]
                     self.skipped.update(self.fused[mid]["stages"])
+                else:
+                    self._materialize(self.fused[mid]["x"])
             if s.id in self.skipped:
                 refresh()
                 for p in range(s.partitions):

@@ -319,3 +319,24 @@ def test_seg_reduce_multi_variants_agree(serial, monkeypatch):
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300,
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert out.returncode == 0 and "OK" in out.stdout, out.stderr[-3000:]
+
+
+@pytest.mark.parametrize("n,nb", [(1, 4), (5000, 3), (300_001, 200)])
+def test_bucket_scatter_gen_terasort_matches_stored_rows(n, nb):
+    """Records generated straight into their buckets == the bucket scatter of the stored records."""
+    from dryad_amd.ops import sort as S
+    from dryad_amd.ops import terasort as TS
+    first, seed = 12345, 99
+    rows = torch.empty((n, 100), dtype=torch.uint8, device="cuda")
+    keys = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    TS.generate_with_keys(rows, first, seed, keys)
+    k2 = torch.empty_like(keys)
+    TS.generate_keys_only(n, first, seed, k2)
+    assert torch.equal(keys, k2)
+    g = torch.Generator(device="cuda").manual_seed(n)
+    keys[:, 1] = torch.randint(0, nb, (n,), device="cuda", generator=g)
+    a, b = torch.empty_like(rows), torch.empty_like(rows)
+    sa = S.bucket_scatter_rows(keys, rows, a)
+    sb = S.bucket_scatter_gen_terasort(keys, n, first, seed, b)
+    assert sa == sb
+    assert torch.equal(a, b)
