@@ -199,27 +199,22 @@ __global__ __launch_bounds__(256) void rs_scatter_v2(const T* __restrict__ in, T
   goff[t] = offsets[(uint64_t)t * G + blockIdx.x];
   const uint64_t beg = (uint64_t)blockIdx.x * per_block;
   const uint64_t end = beg + per_block < n ? beg + per_block : n;
-  if (beg >= end) return;                          // uniform: the whole workgroup leaves
   T cur[ITEMS], nxt[ITEMS];
-  // clamped, unconditional loads in a macro (a lambda writing these arrays, or a load under a
-  // branch inside the loop, put them in scratch for the wide entry types); a position past the
-  // tile re-reads its last entry and is masked by `valid`
-#define DR_RS_LOAD(BASE, DST)                                                                   \
-  {                                                                                             \
-    const uint64_t b_ = (BASE);                                                                 \
-    const uint32_t c_ = (uint32_t)((end - b_) < (uint64_t)kTile ? (end - b_) : kTile);          \
-    _Pragma("unroll") for (int r = 0; r < ITEMS; ++r) {                                         \
-      const uint32_t pos_ = w * (kTile / 4) + r * 64 + l;                                       \
-      DST[r] = in[b_ + (pos_ < c_ ? pos_ : c_ - 1)];                                            \
-    }                                                                                           \
-  }
-  DR_RS_LOAD(beg, cur)
+  auto load_tile = [&](uint64_t base, T* dst) {
+    const uint32_t c = (uint32_t)((end - base) < (uint64_t)kTile ? (end - base) : kTile);
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+      if (pos < c) dst[r] = in[base + pos];
+    }
+  };
+  if (beg < end) load_tile(beg, cur);
   for (uint64_t base = beg; base < end; base += kTile) {
     const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kTile ? (end - base) : kTile);
-    DR_RS_LOAD(base + kTile < end ? base + kTile : base, nxt)
+    if (base + kTile < end) load_tile(base + kTile, nxt);
     wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
     __syncthreads();
-    uint32_t rd[ITEMS];                              // in-wave rank | digit << 16 (one VGPR each)
+    uint32_t rk[ITEMS], dg[ITEMS];
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
       const uint32_t pos = w * (kTile / 4) + r * 64 + l;
@@ -237,7 +232,8 @@ __global__ __launch_bounds__(256) void rs_scatter_v2(const T* __restrict__ in, T
       __builtin_amdgcn_wave_barrier();
       if (valid && below == 0) wcnt[w][d] = prior + (uint32_t)__popcll(peers);
       __builtin_amdgcn_wave_barrier();
-      rd[r] = (prior + below) | (d << 16);
+      rk[r] = prior + below;
+      dg[r] = d;
     }
     __syncthreads();
     const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
@@ -249,8 +245,7 @@ __global__ __launch_bounds__(256) void rs_scatter_v2(const T* __restrict__ in, T
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
       const uint32_t pos = w * (kTile / 4) + r * 64 + l;
-      const uint32_t d = rd[r] >> 16;
-      if (pos < cnt) stage[bstart[d] + wcnt[w][d] + (rd[r] & 0xFFFFu)] = cur[r];
+      if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
     }
     __syncthreads();
 #pragma unroll 4
@@ -272,7 +267,6 @@ __global__ __launch_bounds__(256) void rs_scatter_v2(const T* __restrict__ in, T
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) cur[r] = nxt[r];
   }
-#undef DR_RS_LOAD
 }
 
 void scan_inplace(uint32_t* a, uint32_t M, uint32_t* partial, hipStream_t s) {
