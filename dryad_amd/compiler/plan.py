@@ -18,6 +18,7 @@ several output ports (partitioners, Fork).
 from __future__ import annotations
 
 import json
+import xml.etree.ElementTree as ET
 from dataclasses import dataclass, field
 
 from .datasetinfo import DataSetInfo
@@ -103,6 +104,61 @@ class Plan:
 
     def dumps(self) -> str:
         return json.dumps(self.to_json(), indent=1, default=str)
+
+    # reference vertex Type names (DryadLinqQueryNode.QueryNodeType) of the plan's first op
+    _XML_TYPE = {"read": "InputTable", "output": "OutputTable", "sort": "OrderBy", "hash_partition": "HashPartition",
+                 "range_partition": "RangePartition", "group_partial": "GroupBy", "group_final": "GroupBy",
+                 "group_by": "GroupBy", "where": "Where", "select": "Select", "select_many": "SelectMany",
+                 "join": "Join", "hash_join": "Join", "group_join": "GroupJoin", "distinct": "Distinct",
+                 "union": "Union", "intersect": "Intersect", "except": "Except", "concat": "Concat",
+                 "sample": "Dynamic", "separators": "Dynamic", "apply": "Apply", "fork": "Fork",
+                 "merge": "Merge", "enumerable": "InputTable", "take": "Take", "skip": "Skip"}
+
+    def to_xml(self) -> str:
+        """The plan as the reference's query-plan XML document (DryadLinqQueryGen.cs:837-971,
+        DryadLinqQueryNode.cs:769-827): global <Query> properties, then one <Vertex> per stage with
+        UniqueId / Type / Name / Explain (CDATA) / Partitions / ChannelType / ConnectionOperator /
+        DynamicManager / Entry and <Children> (<Child> UniqueId + AffinityConstraint)."""
+        root = ET.Element("Query")
+        g = self.globals
+        for k in ("DryadLinqVersion", "ClusterName", "MinimumComputeNodes", "MaximumComputeNodes",
+                  "IntermediateDataCompression", "EnableSpeculativeDuplication"):
+            ET.SubElement(root, k).text = str(g.get(k, ""))
+        ET.SubElement(root, "Visualization").text = "none"
+        ET.SubElement(root, "QueryName").text = str(g.get("QueryName") or "")
+        ET.SubElement(root, "XmlExecHostArgs")
+        ET.SubElement(root, "Resources")
+        qp = ET.SubElement(root, "QueryPlan")
+        cdata = {}
+        for st in self.stages:
+            v = ET.SubElement(qp, "Vertex")
+            ET.SubElement(v, "UniqueId").text = str(st.id)
+            first = st.ops[0]["op"] if st.ops else "merge"
+            # a stage fusing several operators is the reference's "Super" node
+            ET.SubElement(v, "Type").text = "Super" if len(st.ops) > 1 else self._XML_TYPE.get(first, first)
+            ET.SubElement(v, "Name").text = st.name
+            mark = f"@@CDATA{st.id}@@"
+            ET.SubElement(v, "Explain").text = mark
+            cdata[mark] = "\n".join(st.explain + [st.describe_ops()])
+            ET.SubElement(v, "Partitions").text = str(st.partitions)
+            ET.SubElement(v, "ChannelType").text = st.channel_type
+            con = st.inputs[0].to_json()["ConnectionOperator"] if st.inputs else "Pointwise"
+            ET.SubElement(v, "ConnectionOperator").text = con
+            dm = ET.SubElement(v, "DynamicManager")
+            ET.SubElement(dm, "Type").text = st.dynamic_manager or "None"
+            ET.SubElement(v, "Entry").text = ".".join(op["op"] for op in st.ops)
+            if st.output:
+                ET.SubElement(v, "StorageSet").text = str(st.output.get("uri", ""))
+            ch = ET.SubElement(v, "Children")
+            for i in st.inputs:
+                c = ET.SubElement(ch, "Child")
+                ET.SubElement(c, "UniqueId").text = str(i.src)
+                ET.SubElement(c, "AffinityConstraint").text = "UseDefault"
+        ET.indent(root)
+        text = ET.tostring(root, encoding="unicode")
+        for mark, body in cdata.items():
+            text = text.replace(mark, "<![CDATA[" + body.replace("]]>", "]]]]><![CDATA[>") + "]]>")
+        return '<?xml version="1.0" encoding="utf-8"?>\n' + text + "\n"
 
     def explain(self) -> str:
         """Human-readable per-stage explanation (reference DryadLinqQueryExplain.cs)."""

@@ -108,6 +108,8 @@ class LocalExecutor(_BaseExecutor):
                 cloudpickle.dump(plan, f)
             with open(os.path.join(job_dir, "plan.json"), "w") as f:
                 f.write(plan.dumps())
+            with open(os.path.join(job_dir, "QueryPlan.xml"), "w") as f:   # the reference job directory's plan
+                f.write(plan.to_xml())
             with open(os.path.join(job_dir, "QueryGraph.txt"), "w") as f:
                 f.write(plan.explain())
             if self.thread_pool:

@@ -903,6 +903,8 @@ class GpuExecutor(_BaseExecutor):
         os.makedirs(os.path.join(d, "log"), exist_ok=True)
         with open(os.path.join(d, "plan.json"), "w") as f:
             f.write(plan.dumps())
+        with open(os.path.join(d, "QueryPlan.xml"), "w") as f:   # the reference job directory's plan
+            f.write(plan.to_xml())
         with open(os.path.join(d, "QueryGraph.txt"), "w") as f:
             f.write(plan.explain())
         return d

@@ -104,6 +104,7 @@ def test_wordcount_local_job_submission_processes(tmp_path):
     c = D.DryadLinqContext(3)        # process pool (VertexHost programs)
     out = f"partfile://{tmp_path}/wc"
     info = _wordcount(c, src, out).SubmitAndWait()
+    wc_dir = c._get_executor().last_job_dir
     got = sorted(l.Line for l in c.FromStore(out, D.types.LineRecordT))
     from collections import Counter
     exp = sorted(f"{w}: {n}" for w, n in Counter(w for t in text for w in t.split(" ")).items())
@@ -113,4 +114,17 @@ def test_wordcount_local_job_submission_processes(tmp_path):
     assert os.path.exists(os.path.join(ex.last_job_dir, "log", "events.jsonl"))
     assert os.path.exists(os.path.join(ex.last_job_dir, "statistics.json"))
     assert any(e.get("ev") == "job_stop" for e in info.events)
+    # ... and the reference-format query plan (DryadLinqQueryGen.cs:837-971)
+    import xml.etree.ElementTree as ET
+    root = ET.parse(os.path.join(wc_dir, "QueryPlan.xml")).getroot()
+    assert root.tag == "Query" and root.find("DryadLinqVersion") is not None
+    verts = root.findall("./QueryPlan/Vertex")
+    assert len(verts) >= 2
+    ids = {v.findtext("UniqueId") for v in verts}
+    for v in verts:
+        assert {e.tag for e in v} >= {"UniqueId", "Type", "Name", "Explain", "Partitions", "ChannelType",
+                                      "ConnectionOperator", "DynamicManager", "Entry", "Children"}
+        for ch in v.findall("./Children/Child"):
+            assert ch.findtext("UniqueId") in ids and ch.findtext("AffinityConstraint") == "UseDefault"
+    assert any(v.findtext("ConnectionOperator") == "CrossProduct" for v in verts)    # the word shuffle
     c.Dispose()
