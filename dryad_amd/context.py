@@ -108,6 +108,8 @@ _DEFAULTS = dict(
     FaultInjection=None,          # [{stage, partition, version, kind}] (SURVEY §5.3 FaultInjector)
     HbmBudgetBytes=None,          # HBM an out-of-core operator may use per GPU (None: 80% of free HBM)
     ExternalSort=None,            # out-of-core OrderBy to host:// (None: when the data exceeds the budget)
+    ExternalSortToDisk=None,      # its partfile:// output written through a memory-mapped part file
+    #                               (None: when the output exceeds half of the available host memory)
 )
 
 _READONLY_AFTER_USE = set(_DEFAULTS) - {"LocalDebug"}

@@ -6,7 +6,9 @@ partition that does not (the output of an out-of-core sort, a spilled intermedia
 DMA engines can read and write directly, so PCIe copies run at full rate in both directions
 without a bounce buffer.  The reference's equivalent is the spill of sorted runs to temp files in
 ``ParallelSort`` (LinqToDryad/DryadLinqVertex.cs:9584-9615, FileEnumerable :10733) — here the
-"file" is a page-locked host buffer and the runs are range buckets (ops/extsort.py).
+"file" is a page-locked host buffer and the runs are range buckets (ops/extsort.py).  Below it,
+``HostRows.mapped`` puts a table in a memory-mapped file (the disk tier) for outputs larger than
+host memory.
 """
 from __future__ import annotations
 
@@ -43,6 +45,31 @@ class HostRows:
         self.pinned = self._buf is not None
 
     @staticmethod
+    def mapped(path: str, n: int, stride: int, key_off: int = 0, key_len: int | None = None) -> "HostRows":
+        """A table backed by a memory-mapped file (the disk tier below pinned DRAM): the page cache
+        holds what is in use and writes the rest back, so the table may exceed host memory.  The
+        file (``path``) stays when the table is released; PCIe copies to and from it are staged
+        by the driver (pageable memory)."""
+        import numpy as np
+        h = HostRows.__new__(HostRows)
+        h.n, h.stride = int(n), int(stride)
+        h.key_off, h.key_len = key_off, key_len or stride
+        h._buf, h.pinned, h.path = None, False, path
+        if h.n * h.stride == 0:
+            open(path, "wb").close()
+            h._mm, h.rows = None, torch.empty((h.n, h.stride), dtype=torch.uint8)
+        else:
+            h._mm = np.memmap(path, dtype=np.uint8, mode="w+", shape=(h.n, h.stride))
+            h.rows = torch.from_numpy(h._mm)
+        return h
+
+    def flush(self):
+        """Write a mapped table's dirty pages back to its file (no-op for DRAM tables)."""
+        mm = getattr(self, "_mm", None)
+        if mm is not None:
+            mm.flush()
+
+    @staticmethod
     def from_tensor(rows: torch.Tensor, key_off: int = 0, key_len: int | None = None, pinned: bool | None = None):
         """Copy a [n, stride] uint8 tensor (host or device) into a new host table."""
         h = HostRows(rows.shape[0], rows.shape[1], key_off, key_len, pinned)
@@ -55,6 +82,7 @@ class HostRows:
         v = HostRows.__new__(HostRows)
         v.n, v.stride, v.key_off, v.key_len = int(n), self.stride, self.key_off, self.key_len
         v._buf, v.rows, v.pinned = None, self.rows[:n], self.pinned
+        v._mm, v.path = getattr(self, "_mm", None), getattr(self, "path", None)
         return v
 
     @property
@@ -71,6 +99,9 @@ class HostRows:
         return [bytes(r) for r in a]
 
     def release(self):
+        if getattr(self, "_mm", None) is not None:
+            self._mm.flush()
+            self._mm = None
         if self._buf is not None:
             _PINNED.pop(self.rows.data_ptr(), None)
             self._buf.release()

@@ -65,6 +65,7 @@ class ExtSortStats:
     max_bucket: int = 0
     bytes_h2d: int = 0
     bytes_d2h: int = 0
+    tier: str = "dram"           # where the output rows live: "dram" (pinned) or "disk" (mapped file)
     seconds: dict = field(default_factory=dict)
 
 
@@ -246,12 +247,14 @@ def _separators(srt: torch.Tensor, W: int, P: int, tie_bits: bool, lo_key_mask: 
 def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | None = None,
                   budget: int | None = None, keep_ties: bool = False, sample_target: int = 1 << 20,
                   seed: int = 314159, stats: ExtSortStats | None = None,
-                  out: HostRows | None = None) -> HostRows:
+                  out: HostRows | None = None, out_factory=None) -> HostRows:
     """Globally sort the rows of ``src`` (this rank's partition) by the byte-string key
     [key_off, key_off + key_len) (memcmp order, key_len <= 12).  Rank r returns the r-th key range
     as a ``HostRows`` table in pinned host memory.  ``budget``: HBM bytes the sort may use
     (default 80% of free HBM).  ``out``: a preallocated host table to write into when it is large
-    enough (the result is then a view of its first rows)."""
+    enough (the result is then a view of its first rows); ``out_factory(n_out)``: builds the
+    output table once this rank's row count is known (e.g. a memory-mapped part file,
+    ``HostRows.mapped``, for outputs larger than host memory)."""
     w = world or get_world()
     W, me = w.size, w.rank
     dev = w.device if w.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
@@ -342,8 +345,13 @@ def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | N
     # host position of piece (s, c, b): bucket start + rows of earlier chunks + earlier sources
     flat = mine.permute(1, 0, 2).reshape(C * W, P)              # (chunk, src) major order
     piece_pos = (torch.cumsum(flat, 0) - flat + bucket_off.unsqueeze(0)).view(C, W, P)
-    out = out.view(n_out) if out is not None and out.n >= n_out and out.stride == stride else \
-        HostRows(n_out, stride, key_off, key_len)
+    if out is not None and out.n >= n_out and out.stride == stride:
+        out = out.view(n_out)
+    elif out_factory is not None:
+        out = out_factory(n_out)
+        stats.tier = "disk" if getattr(out, "path", None) else "dram"
+    else:
+        out = HostRows(n_out, stride, key_off, key_len)
     try:
         # ------------------------------------------------------------ 2. partition pass
         t0 = time.perf_counter()

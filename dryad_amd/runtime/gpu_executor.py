@@ -300,10 +300,30 @@ class GpuJobRunner:
             torch.cuda.empty_cache()
         off, ln = e["spec"]
         st = EX.ExtSortStats()
+        factory = self._disk_output(s, e["source"], off, ln)
         out = EX.external_sort(e["source"], off, ln, self.world, budget=self.ctx._props.get("HbmBudgetBytes"),
-                               keep_ties=e["keep_ties"], stats=st)
+                               keep_ties=e["keep_ties"], stats=st, out_factory=factory)
         self.extsort_stats = st
         return out
+
+    def _disk_output(self, s, src, off, ln):
+        """Disk tier for an out-of-core OrderBy writing ``partfile://``: a factory that places this
+        rank's sorted rows in a memory-mapped file next to the output (renamed into the part file
+        at commit), so the output need not fit host memory.  ``ExternalSortToDisk`` forces / forbids
+        it; by default it is used when the rank's output would take over half the available RAM."""
+        scheme, path, _ = parse_uri(s.output["uri"])
+        if scheme not in ("partfile", "file"):
+            return None
+        force = self.ctx._props.get("ExternalSortToDisk")
+        if force is False:
+            return None
+        if force is None:
+            import psutil
+            if src.n * src.stride * 1.1 < 0.5 * psutil.virtual_memory().available:
+                return None
+        tmp = f"{os.path.abspath(path)}.extsort.{self.world.rank}.{os.getpid()}.tmp"
+        os.makedirs(os.path.dirname(tmp) or ".", exist_ok=True)
+        return lambda n_out: HostRows.mapped(tmp, n_out, src.stride, off, ln)
 
     def _sources(self, si, p):
         src = self.plan.stages[si.src]
@@ -790,9 +810,16 @@ def _commit_partfile_impl(runner, s, uri, path, local):
             # raw fixed-width rows straight from the pinned host tier (out-of-core sort output)
             if not isinstance(v, HostRows):
                 v = HostRows.from_tensor(v.rows, v.shape.key_off, v.shape.key_len, pinned=False)
-            with open(tmp, "wb") as f:
-                if v.n:
-                    f.write(memoryview(v.rows.numpy()).cast("B"))
+            if getattr(v, "path", None) and os.path.exists(v.path):
+                # disk tier: the rows already are a file; flush it and rename it into place
+                v.flush()
+                if v.n * v.stride != os.path.getsize(v.path):
+                    os.truncate(v.path, v.n * v.stride)
+                os.replace(v.path, tmp)
+            else:
+                with open(tmp, "wb") as f:
+                    if v.n:
+                        f.write(memoryview(v.rows.numpy()).cast("B"))
             fmt_extra = dict(stride=v.stride, key_off=v.key_off, key_len=v.key_len)
             mine[p] = tmp
             continue

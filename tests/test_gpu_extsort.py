@@ -88,3 +88,28 @@ def test_query_out_of_core_orderby_to_host_table():
     cnt = ctx.FromStore("host://ooc_sorted").Where(lambda r: r[0] < 128).Count()
     assert cnt == int((h.rows[:, 0] < 128).sum())
     provider_for("host://ooc_sorted").delete("host://ooc_sorted")
+
+
+def test_query_out_of_core_orderby_to_disk_partfile(tmp_path):
+    """FromStore(gen) -> OrderBy -> ToStore(partfile://) with the disk tier forced: the sorted rows
+    are written through a memory-mapped file that becomes the part file (no host-DRAM copy of the
+    output), and read back equal to the in-HBM sort."""
+    import os
+    import numpy as np
+    import dryad_amd as D
+    from dryad_amd.io.providers import provider_for
+    n = 600_000
+    ctx = D.DryadLinqContext(platform="gpu")
+    ctx.HbmBudgetBytes = 40 << 20
+    ctx.ExternalSort = True
+    ctx.ExternalSortToDisk = True
+    out = f"partfile://{tmp_path}/sorted"
+    src = f"gen://terasort?records={n}&partitions=1&seed=5"
+    ctx.FromStore(src).OrderBy(lambda r: r[0:10]).ToStore(out, delete_if_exists=True).SubmitAndWait()
+    res = ctx._get_executor().last_result
+    assert res["external_sort"] is not None and res["external_sort"].buckets > 1
+    assert res["external_sort"].tier == "disk"
+    mm, off, ln = provider_for(out).rows_part(out, 0)
+    assert (off, ln) == (0, 10)
+    assert np.array_equal(np.asarray(mm), _in_hbm_sorted(_gen_rows(n, 0, 5)).numpy())
+    assert not [f for f in os.listdir(tmp_path) if ".extsort." in f]

@@ -75,3 +75,20 @@ def test_external_sort_geometry_fits_budget():
     assert chunk8 * (7 * 100 + 16) <= budget and P8 * 8 <= 256
     with pytest.raises(RuntimeError):
         plan_geometry(10**12, 10**12, 100, 1, 10**9)    # would need > 256 range buckets
+
+
+def test_mapped_host_rows_are_a_file(tmp_path):
+    """The disk tier: a memory-mapped HostRows writes through to its file and survives release."""
+    import numpy as np
+    from dryad_amd.io.hosttable import HostRows
+    path = str(tmp_path / "rows.bin")
+    h = HostRows.mapped(path, 1000, 16, 0, 8)
+    src = torch.randint(0, 256, (1000, 16), dtype=torch.uint8)
+    h.rows.copy_(src)
+    v = h.view(600)
+    assert v.path == path and torch.equal(v.rows, src[:600])
+    h.release()
+    got = np.fromfile(path, dtype=np.uint8).reshape(1000, 16)
+    assert np.array_equal(got, src.numpy())
+    e = HostRows.mapped(str(tmp_path / "empty.bin"), 0, 16)
+    assert e.n == 0 and (tmp_path / "empty.bin").exists()
