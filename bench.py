@@ -93,6 +93,12 @@ def main():
                 "total_bytes": total_bytes,
                 "validated": None if val is None else val["ok"],
                 "path": "direct" if args.direct else "DryadLINQ query -> GPU executor (fused OrderBy gang stage)",
+                # the input read: every record is generated once per step; with one rank into the
+                # HBM input table the local sort gathers from, with several ranks straight into
+                # the all-to-all send buckets (the read stage fused with the range partition)
+                "input": "gen://terasort, generated in the timed step" + (
+                    " into the send buckets (read fused with the range partition)" if world.size > 1 and not args.direct
+                    else " into the HBM input table"),
             },
         }
         if val is not None and not val["ok"]:
