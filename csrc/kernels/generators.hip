@@ -59,6 +59,44 @@ __global__ __launch_bounds__(256) void gen_records64_rows_kernel(int64_t* __rest
     out[e] = (int64_t)v;
   }
 }
+// One row per thread, staged: each thread computes its row's NC fields (the key once, not once
+// per field lane) into an LDS image of 256 rows, which the block then streams out with 16-byte
+// stores (the per-field-lane kernel above issues eight 8-byte stores per row and recomputes the
+// dimension-table key in every lane).
+template <int NC, bool WIDE>
+__global__ __launch_bounds__(256) void gen_records64_rows_lds_kernel(int64_t* __restrict__ out, uint64_t n,
+                                                                     uint64_t first, uint64_t nkeys, uint64_t mkeys,
+                                                                     uint64_t seed, uint64_t dim_mult) {
+  __shared__ __attribute__((aligned(16))) int64_t img[256 * NC];
+  for (uint64_t row0 = (uint64_t)blockIdx.x * 256; row0 < n; row0 += (uint64_t)gridDim.x * 256) {
+    const uint32_t rows = (uint32_t)((n - row0) < 256 ? (n - row0) : 256);
+    if (threadIdx.x < rows) {
+      const uint64_t i = first + row0 + threadIdx.x;
+      uint64_t key;
+      if (dim_mult) {
+        if (WIDE) key = (uint64_t)(((unsigned __int128)i * dim_mult + seed) % nkeys);
+        else key = fast_mod64(i * dim_mult + seed, nkeys, mkeys);
+      } else {
+        key = fast_mod64(mix64(seed ^ (i * kG)), nkeys, mkeys);
+      }
+      const uint64_t src = dim_mult ? key : i;
+      img[threadIdx.x * NC] = (int64_t)key;
+#pragma unroll
+      for (int j = 1; j < NC; ++j) img[threadIdx.x * NC + j] = (int64_t)(mix64((seed + (uint64_t)j * kH) ^ src) >> 33);
+    }
+    __syncthreads();
+    const uint32_t words = rows * NC;                // int64 words of this block's rows
+    int64_t* o = out + row0 * NC;
+    if ((words & 1) == 0 && (((uintptr_t)o) & 15) == 0) {
+      const uint4* s4 = reinterpret_cast<const uint4*>(img);
+      uint4* d4 = reinterpret_cast<uint4*>(o);
+      for (uint32_t q = threadIdx.x; q < words / 2; q += 256) d4[q] = s4[q];
+    } else {
+      for (uint32_t q = threadIdx.x; q < words; q += 256) o[q] = img[q];
+    }
+    __syncthreads();
+  }
+}
 }  // namespace
 
 // cols: device array of ncols (<= 8) device pointers to int64 columns of length n.
@@ -82,11 +120,22 @@ DR_API int dr_gen_records64_rows(int64_t* out, int ncols, uint64_t n, uint64_t f
   // the dimension-table key needs 128-bit arithmetic once (first + n) * dim_mult + seed can pass 2^64
   const unsigned __int128 top = (unsigned __int128)(first + n) * dim_mult + seed;
   const bool wide = dim_mult && (top >> 64) != 0;
-  const unsigned g = grid_for(n * (uint64_t)ncols, 256, 16384);
+  static int staged = -1;    // DRYAD_GEN_ROWS_LDS=0: the one-lane-per-field kernel
+  if (staged < 0) {
+    const char* e = getenv("DRYAD_GEN_ROWS_LDS");
+    staged = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  const unsigned g = staged ? grid_for(n, 256, 8192) : grid_for(n * (uint64_t)ncols, 256, 16384);
 #define DR_GEN_ROWS(NCV)                                                                              \
   do {                                                                                                \
-    if (wide) gen_records64_rows_kernel<NCV, true><<<g, 256, 0, s>>>(out, n, first, nkeys, m, seed, dim_mult); \
-    else gen_records64_rows_kernel<NCV, false><<<g, 256, 0, s>>>(out, n, first, nkeys, m, seed, dim_mult);    \
+    if (staged) {                                                                                     \
+      if (wide) gen_records64_rows_lds_kernel<NCV, true><<<g, 256, 0, s>>>(out, n, first, nkeys, m, seed, dim_mult); \
+      else gen_records64_rows_lds_kernel<NCV, false><<<g, 256, 0, s>>>(out, n, first, nkeys, m, seed, dim_mult);    \
+    } else if (wide) {                                                                                \
+      gen_records64_rows_kernel<NCV, true><<<g, 256, 0, s>>>(out, n, first, nkeys, m, seed, dim_mult); \
+    } else {                                                                                          \
+      gen_records64_rows_kernel<NCV, false><<<g, 256, 0, s>>>(out, n, first, nkeys, m, seed, dim_mult); \
+    }                                                                                                 \
   } while (0)
   switch (ncols) {
     case 1: DR_GEN_ROWS(1); break;
