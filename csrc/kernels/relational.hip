@@ -277,6 +277,24 @@ __global__ __launch_bounds__(256) void seg_reduce_multi_serial(const E128* __res
   const int lane = lane_id();
   const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   const uint64_t w0 = (((uint64_t)blockIdx.x * blockDim.x) + threadIdx.x) >> 6;
+  // KEYS: the next chunk's sorted entries are loaded while this chunk's permuted rows are in
+  // flight (clamped, unconditional loads: an element past n re-reads entry n - 1 and is masked by
+  // cnt), so a wave waits for one HBM round trip per chunk instead of two
+  uint64_t pk[KEYS ? PER : 1];
+  uint32_t pr[KEYS ? PER : 1];
+  auto prefetch = [&](uint64_t cb) {
+    if constexpr (KEYS) {
+      const uint64_t f0 = cb + (uint64_t)lane * PER;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const uint64_t i = f0 + k < n ? f0 + k : n - 1;
+        const E128 x = ent[i];
+        pk[k] = x.hi;
+        pr[k] = (uint32_t)x.lo;
+      }
+    }
+  };
+  if (KEYS && n) prefetch(w0 * kChunkElems < n ? w0 * kChunkElems : 0);
   for (uint64_t cbase = w0 * kChunkElems; cbase < n; cbase += waves * kChunkElems) {
     const uint64_t first = cbase + (uint64_t)lane * PER;
     int64_t sid[PER];
@@ -288,18 +306,11 @@ __global__ __launch_bounds__(256) void seg_reduce_multi_serial(const E128* __res
     if constexpr (KEYS) {
       uint64_t kh[PER];
       uint32_t f[PER];
+      cnt = first < n ? (int)((n - first) < (uint64_t)PER ? (n - first) : (uint64_t)PER) : 0;
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
-        const uint64_t i = first + k;
-        if (i < n) {
-          const E128 x = ent[i];
-          kh[k] = x.hi;
-          row[k] = (uint32_t)x.lo;
-          cnt = k + 1;
-        } else {
-          kh[k] = 0;
-          row[k] = 0;
-        }
+        kh[k] = pk[k];
+        row[k] = pr[k];
       }
       // key of the element before the lane's first: the previous lane's last (lane 0: a load)
       uint64_t prev = __shfl_up(kh[PER - 1], 1, 64);
@@ -378,6 +389,10 @@ __global__ __launch_bounds__(256) void seg_reduce_multi_serial(const E128* __res
           r0[k] = u2_t{0ull, 0ull};
           r1[k] = u2_t{0ull, 0ull};
         }
+      }
+      if constexpr (KEYS) {
+        const uint64_t nb = cbase + waves * kChunkElems;
+        prefetch(nb < n ? nb : cbase);
       }
     } else {
 #pragma unroll
