@@ -475,8 +475,16 @@ def op_sample(op, inputs, v):
     return DeviceTable.from_columns({"lo": samp[:, 0].contiguous(), "hi": samp[:, 1].contiguous()}, E_SHAPE)
 
 
+def _entries_table(t):
+    """A sample / separator table of sort entries (the device sample's layout).  A partition whose
+    sample ran on the host delivers key values instead: the consumer falls back to the host too."""
+    if not isinstance(t, DeviceTable) or "lo" not in t.cols or "hi" not in t.cols:
+        raise NotTraceable("sample keys came from the host path")
+    return t
+
+
 def op_separators(op, inputs, v):
-    t = _check(_one(inputs))
+    t = _entries_table(_check(_one(inputs)))
     n = op["count"]
     if t.n == 0:
         return DeviceTable.from_columns({"lo": torch.empty(0, dtype=torch.int64, device=v.device),
@@ -499,6 +507,7 @@ def op_range_partition(op, inputs, v):
     e, _, lo_mask = key_entries(t, op["key"], op.get("comparer"), False)
     if seps_t is None or seps_t.n == 0:
         return Ported(t, [0] + [t.n] * n)
+    seps_t = _entries_table(seps_t)
     seps = torch.stack([seps_t.cols["lo"], seps_t.cols["hi"]], 1).contiguous()
     S.range_dest(e, seps, lo_mask, descending=op.get("descending", False))
     part, starts = S.partition_pass(e, 64)

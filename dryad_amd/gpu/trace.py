@@ -132,7 +132,13 @@ class RowProxy:
             if st != 1:
                 raise NotTraceable("strided byte slice")
             return ByteField(a, b - a)
-        raise NotTraceable("single byte of a row record")
+        if isinstance(k, int):
+            w = self._t.rows.shape[1]
+            i = k + w if k < 0 else k
+            if not 0 <= i < w:
+                raise NotTraceable("row byte index out of range")
+            return Col(self._t.rows[:, i].to(torch.int64))     # bytes[i] is an int in 0..255
+        raise NotTraceable("row record index")
 
     def __getattr__(self, name):
         raise NotTraceable(f"attribute {name} of a row record")

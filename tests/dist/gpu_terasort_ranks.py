@@ -126,6 +126,21 @@ def main():
     cnt = torch.tensor([out.n], dtype=torch.int64, device=w.device)
     shuffle.all_reduce_(cnt, "sum", w)
     assert int(cnt) == 120_000 * w.size
+    # a gen://terasort read feeding only a distributed OrderBy is generated lazily (entries only);
+    # with a key the fused sort cannot take (not a byte-string slice) the records must be
+    # materialised before the ordinary sample / range-partition path reads them
+    ts = "gen://terasort?records=60000&partitions=%d&seed=21" % w.size
+    kint = lambda r: r[3] * 256 + r[4]  # noqa: E731
+    gctx = D.DryadLinqContext(platform="gpu")
+    gctx.PartitionCount = w.size
+    lctx = D.DryadLinqContext(1)
+    lctx.LocalDebug = True
+    got = list(gctx.FromStore(ts).OrderBy(kint).Select(lambda r: r[0:10]))
+    exp = list(lctx.FromStore(ts).OrderBy(kint).Select(lambda r: r[0:10]))
+    assert [kint(bytes(x) + bytes(90)) for x in got] == [kint(bytes(x) + bytes(90)) for x in exp]
+    assert sorted(map(bytes, got)) == sorted(map(bytes, exp))
+    fb = {op for _, op, _ in gctx._get_executor().last_result["fallbacks"]}
+    assert not fb & {"sample", "separators", "range_partition", "sort"}, fb
     w.barrier()
     if w.rank == 0:
         print("MULTIRANK_OK", w.size, flush=True)

@@ -198,3 +198,12 @@ def test_string_keys_on_device():
     ages = [(("alice", "bob", "carol", "zed")[i % 4] + "x" * (i % 11), i * 10) for i in range(400)]
     _same(lambda c: c.FromEnumerable(names).Join(c.FromEnumerable(ages), lambda a: a[0], lambda b: b[0],
                                                  lambda a, b: (a[1], b[1])), parts=1, device_ops=("hash_join",))
+
+
+def test_row_record_byte_index_on_device():
+    """r[i] of a fixed-width row record is an int column on the device (bytes[i] semantics)."""
+    src = "gen://terasort?records=20000&partitions=1&seed=3"
+    _same(lambda c: c.FromStore(src).Where(lambda r: r[0] < 100).Select(lambda r: r[5] * 256 + r[-1]),
+          device_ops=("where", "select"))
+    _same(lambda c: c.FromStore(src).OrderBy(lambda r: r[3] * 256 + r[4]).Select(lambda r: r[0:10]), ordered=False,
+          device_ops=("sort",))
