@@ -20,3 +20,14 @@ def test_two_ranks_share_one_gpu():
                          capture_output=True, text=True, timeout=560, env=env, cwd=ROOT)
     assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
     assert "MULTIRANK_OK 2" in out.stdout
+
+
+@pytest.mark.timeout(600)
+def test_query_sweep_two_ranks():
+    env = dict(os.environ, DRYAD_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                          "--master-addr", "127.0.0.1", "--master-port", "29634",
+                          os.path.join(ROOT, "tests", "dist", "gpu_query_sweep_ranks.py")],
+                         capture_output=True, text=True, timeout=560, env=env, cwd=ROOT)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
+    assert "SWEEP_OK 2" in out.stdout
