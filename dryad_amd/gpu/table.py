@@ -173,6 +173,9 @@ class DeviceTable:
     def unpack_like(self, buf: torch.Tensor, n: int) -> "DeviceTable":
         if self.rows is not None:
             return DeviceTable(n, self.shape, rows=buf.reshape(n, self.rows.shape[1]))
+        if n == 0:                             # a rank that receives nothing (no byte views of empty slices)
+            return DeviceTable(0, self.shape, {k: torch.empty((0,) + tuple(v.shape[1:]), dtype=v.dtype,
+                                                              device=buf.device) for k, v in self.cols.items()})
         buf = buf.reshape(n, -1)
         out, off = {}, 0
         for k, v in self.cols.items():

@@ -23,11 +23,12 @@ def test_two_ranks_share_one_gpu():
 
 
 @pytest.mark.timeout(600)
-def test_query_sweep_two_ranks():
+@pytest.mark.parametrize("ranks", [2, 4, 8])
+def test_query_sweep_ranks(ranks):
     env = dict(os.environ, DRYAD_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
-    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                          "--master-addr", "127.0.0.1", "--master-port", "29634",
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+                          "--master-addr", "127.0.0.1", "--master-port", str(29634 + ranks),
                           os.path.join(ROOT, "tests", "dist", "gpu_query_sweep_ranks.py")],
                          capture_output=True, text=True, timeout=560, env=env, cwd=ROOT)
     assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
-    assert "SWEEP_OK 2" in out.stdout
+    assert f"SWEEP_OK {ranks}" in out.stdout
