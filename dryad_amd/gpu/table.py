@@ -165,6 +165,9 @@ class DeviceTable:
             raise TypeError("tables with strings are exchanged as records")
         if self.rows is not None:
             return self.rows
+        if self.n == 0:                        # (an empty, possibly expanded column has no byte view)
+            return torch.empty((0, sum(_width(v) for v in self.cols.values())), dtype=torch.uint8,
+                               device=self.device)
         parts = [v.contiguous().view(torch.uint8).reshape(self.n, _width(v)) for v in self.cols.values()]
         if not parts:
             return torch.empty((self.n, 0), dtype=torch.uint8, device=self.device)

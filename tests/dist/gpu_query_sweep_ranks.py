@@ -44,6 +44,42 @@ def queries():
         "terasort_where_take": (lambda c, W: c.FromStore(ts % W).Where(lambda r: r[0] < 16).Select(lambda r: r[0:4]),
                                 False),
         "hash_partition": (lambda c, W: c.FromEnumerable(DATA).HashPartition(lambda x: x % 37, 4), False),
+        # edge cases: empty results, zero-match joins, aggregates over nothing
+        "empty_where": (lambda c, W: c.FromEnumerable(DATA).Where(lambda x: x < 0).Select(lambda x: x + 1), False),
+        "empty_groupby": (lambda c, W: c.FromEnumerable(PAIRS).Where(lambda t: t[0] > 1000).GroupBy(
+            lambda t: t[0], lambda k, g: (k, g.Count())), False),
+        "empty_orderby": (lambda c, W: c.FromEnumerable(DATA).Where(lambda x: x < 0).OrderBy(lambda x: x), True),
+        "join_no_match": (lambda c, W: c.FromEnumerable(PAIRS[:3000]).Join(c.FromEnumerable([500, 501, 502]),
+                                                                           lambda t: t[0], lambda k: k,
+                                                                           lambda t, k: (k, t[1])), False),
+        "count_empty": (lambda c, W: [c.FromEnumerable(DATA).Where(lambda x: x < 0).Count()], True),
+        # more operators across ranks
+        "groupby_avg_any": (lambda c, W: c.FromEnumerable(PAIRS).GroupBy(
+            lambda t: t[0] % 13, lambda k, g: (k, g.Average(lambda t: t[1]), g.Any(lambda t: t[1] > 990.0))),
+            False),
+        "groupby_composite": (lambda c, W: c.FromEnumerable(PEOPLE).GroupBy(
+            lambda r: (r[0], r[1] % 3), lambda k, g: (k[0], k[1], g.Count(), g.Max(lambda r: r[2]))), False),
+        "join_strings": (lambda c, W: c.FromEnumerable(PEOPLE[:3000]).Join(
+            c.FromEnumerable([("bob1", 1), ("carol2", 2), ("eve4", 4)]), lambda a: a[0], lambda b: b[0],
+            lambda a, b: (a[1], b[1])), False),
+        "distinct_strings": (lambda c, W: c.FromEnumerable(PEOPLE).Select(lambda r: r[0]).Distinct(), False),
+        "except": (lambda c, W: c.FromEnumerable([x % 300 for x in DATA]).Except(
+            c.FromEnumerable([x % 200 for x in DATA[:500]])), False),
+        "concat": (lambda c, W: c.FromEnumerable(DATA[:4000]).Concat(c.FromEnumerable(DATA[4000:7000])), False),
+        "orderby_strings": (lambda c, W: c.FromEnumerable(PEOPLE).OrderBy(lambda r: r[0]).Select(lambda r: r[0]),
+                            True),
+        "orderby_tuple": (lambda c, W: c.FromEnumerable(PAIRS[:6000]).OrderBy(lambda t: (t[0], -t[1])), True),
+        "orderby_groupby_ties": (lambda c, W: c.FromStore(ts % W).OrderBy(lambda r: r[0:1]).GroupBy(
+            lambda r: r[0:1], lambda k, g: (k, g.Count())), False),
+        "select_many_fixed": (lambda c, W: c.FromEnumerable(DATA[:5000]).SelectMany(lambda x: (x, -x)), False),
+        "scalar_aggs": (lambda c, W: [c.FromEnumerable(PAIRS).Max(lambda t: t[1]),
+                                      c.FromEnumerable(PAIRS).Min(lambda t: t[0]),
+                                      c.FromEnumerable(PAIRS).Average(lambda t: t[1])], True),
+        "group_join": (lambda c, W: c.FromEnumerable(list(range(0, 101, 7))).GroupJoin(
+            c.FromEnumerable(PAIRS[:9000]), lambda k: k, lambda t: t[0], lambda k, g: (k, g.Count())), False),
+        "three_parts_two_ranks": (lambda c, W: c.FromStore("gen://records64?count=30000&partitions=%d&keys=97&seed=6"
+                                                           % (W + 1)).GroupBy(lambda r: r[0], lambda k, g: (k, g.Count())),
+                                  False),
     }
 
 

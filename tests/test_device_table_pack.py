@@ -18,3 +18,9 @@ def test_pack_unpack_round_trip_and_empty_receive():
     assert e.n == 0 and e.cols["v"].shape == (0, 3) and e.cols["b"].dtype == torch.float64
     rows = DeviceTable(3, Shape("rows", key_off=0, key_len=4), rows=torch.zeros((3, 16), dtype=torch.uint8))
     assert rows.unpack_like(torch.empty(0, dtype=torch.uint8), 0).rows.shape == (0, 16)
+
+
+def test_pack_of_empty_expanded_column():
+    t = DeviceTable.from_columns({"a": torch.zeros(1, dtype=torch.int32).expand(0), "b": torch.empty(0)},
+                                 Shape("tuple", ["a", "b"]))
+    assert t.pack().shape == (0, 8)
