@@ -183,7 +183,11 @@ class DeviceTable:
         out, off = {}, 0
         for k, v in self.cols.items():
             w = _width(v)
-            out[k] = buf[:, off:off + w].contiguous().view(v.dtype).reshape((n,) + tuple(v.shape[1:]))
+            # a fresh [n, w] buffer: contiguous() / clone() keep a one-row slice's offset and stride,
+            # which a byte -> wider dtype view rejects
+            piece = torch.empty((n, w), dtype=torch.uint8, device=buf.device)
+            piece.copy_(buf[:, off:off + w])
+            out[k] = piece.view(v.dtype).reshape((n,) + tuple(v.shape[1:]))
             off += w
         return DeviceTable(n, self.shape, out)
 

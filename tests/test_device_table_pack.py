@@ -24,3 +24,11 @@ def test_pack_of_empty_expanded_column():
     t = DeviceTable.from_columns({"a": torch.zeros(1, dtype=torch.int32).expand(0), "b": torch.empty(0)},
                                  Shape("tuple", ["a", "b"]))
     assert t.pack().shape == (0, 8)
+
+
+def test_unpack_single_row():
+    t = DeviceTable.from_columns({"i": torch.tensor([7], dtype=torch.int32), "d": torch.tensor([2.5]),
+                                  "j": torch.tensor([-3], dtype=torch.int64), "e": torch.tensor([1.5])},
+                                 Shape("tuple", ["i", "d", "j", "e"]))
+    u = t.unpack_like(t.pack().reshape(-1), 1)
+    assert [u.cols[k].tolist() for k in "idje"] == [[7], [2.5], [-3], [1.5]]

@@ -32,3 +32,13 @@ def test_query_sweep_ranks(ranks):
                          capture_output=True, text=True, timeout=560, env=env, cwd=ROOT)
     assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
     assert f"SWEEP_OK {ranks}" in out.stdout
+
+
+@pytest.mark.timeout(300)
+def test_query_sweep_single_rank():
+    """The same sweep on one rank (no cross-rank transport: the local shuffle paths)."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "dist", "gpu_query_sweep_ranks.py")],
+                         capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
+    assert "SWEEP_OK 1" in out.stdout
