@@ -89,7 +89,7 @@ def run(q, c, W):
 
 
 def main():
-    w = init_world(device="cuda")
+    w = init_world(device=os.environ.get("SPMD_DEVICE", "cuda"))
     W = w.size
     g = D.DryadLinqContext(platform="gpu")
     g.PartitionCount = W

@@ -26,3 +26,14 @@ def test_spmd_gloo(ranks, parts):
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "SPMD_OK" in r.stdout
+
+
+def test_query_sweep_cpu_two_ranks():
+    """The GPU-executor sweep (tests/dist/gpu_query_sweep_ranks.py) on CPU ranks over gloo."""
+    env = dict(os.environ, SPMD_DEVICE="cpu", DRYAD_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tests", "dist", "gpu_query_sweep_ranks.py")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "SWEEP_OK 2" in r.stdout
