@@ -80,6 +80,27 @@ def queries():
         "three_parts_two_ranks": (lambda c, W: c.FromStore("gen://records64?count=30000&partitions=%d&keys=97&seed=6"
                                                            % (W + 1)).GroupBy(lambda r: r[0], lambda k, g: (k, g.Count())),
                                   False),
+        # ordered / positional operators across ranks
+        "take_skip": (lambda c, W: c.FromEnumerable(DATA).OrderBy(lambda x: x).Skip(100).Take(250), True),
+        "zip": (lambda c, W: c.FromEnumerable(DATA[:3000]).Zip(c.FromEnumerable(DATA[5000:8000]),
+                                                               lambda a, b: a - b), True),
+        "reverse": (lambda c, W: c.FromEnumerable(DATA[:4000]).Reverse(), True),
+        "element_first_last": (lambda c, W: [c.FromEnumerable(DATA).First(), c.FromEnumerable(DATA).Last(),
+                                             c.FromEnumerable(DATA).First(lambda x: x > 99_000)], True),
+        "any_all_contains": (lambda c, W: [c.FromEnumerable(DATA).Any(lambda x: x == 55), c.FromEnumerable(DATA).All(
+            lambda x: x >= 0), c.FromEnumerable(DATA).Contains(7919), c.FromEnumerable(DATA).LongCount()], True),
+        "aggregate_fold": (lambda c, W: [c.FromEnumerable(DATA[:5000]).Aggregate(0, lambda a, x: (a + x) % 1_000_003)],
+                           True),
+        "sequence_equal": (lambda c, W: [c.FromEnumerable(DATA).SequenceEqual(c.FromEnumerable(list(DATA)))], True),
+        "groupby_element": (lambda c, W: c.FromEnumerable(PAIRS[:5000]).GroupBy(
+            lambda t: t[0] % 7, lambda t: t[1]).Select(lambda g: (g.Key, len(list(g)))), False),
+        "join_tuple_key": (lambda c, W: c.FromEnumerable([(i % 17, i % 5, i) for i in range(3000)]).Join(
+            c.FromEnumerable([(i % 17, i % 5, -i) for i in range(200)]), lambda a: (a[0], a[1]),
+            lambda b: (b[0], b[1]), lambda a, b: (a[2], b[2])), False),
+        "sliding_window": (lambda c, W: c.FromEnumerable(list(range(2000))).SlidingWindow(lambda w: sum(w), 3), True),
+        "apply_per_partition": (lambda c, W: c.FromEnumerable(DATA).ApplyPerPartition(
+            lambda xs: [x % 7 for x in xs if x % 3]).Select(lambda x: x * 2), False),
+        "range_partition": (lambda c, W: c.FromEnumerable(DATA).RangePartition(lambda x: x, 3), False),
     }
 
 
