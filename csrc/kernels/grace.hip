@@ -639,8 +639,26 @@ __global__ __launch_bounds__(256) void rp_count_kernel(const uint32_t* __restric
     const uint64_t left = (uint64_t)seg_len[s] - r0;
     const uint32_t cnt = left < TILE ? (uint32_t)left : TILE;
     const uint32_t* base = rows + ((uint64_t)seg_begin[s] + r0) * RW;
-    for (uint32_t i = t; i < cnt; i += kBlock)
-      atomicAdd(&hist[w][rp_digit<RW>(base + (uint64_t)i * RW + kw, key_len, seed, shift, dmask)], 1u);
+    // every key word of the thread's rows in flight before the first digit (clamped,
+    // unconditional loads: one HBM round trip per tile instead of one per row)
+    constexpr int PER = TILE / kBlock;
+    uint32_t k0[PER], k1[PER], k2[PER];
+    const uint32_t last = cnt ? cnt - 1 : 0;
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      const uint32_t i = t + r * kBlock;
+      const uint32_t* q = base + (uint64_t)(i < cnt ? i : last) * RW + kw;
+      k0[r] = q[0];
+      k1[r] = key_len > 4 ? q[1] : 0u;
+      k2[r] = key_len > 8 ? q[2] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      if (t + r * kBlock < cnt) {
+        const uint32_t kk[3] = {k0[r], k1[r], k2[r]};
+        atomicAdd(&hist[w][rp_digit<RW>(kk, key_len, seed, shift, dmask)], 1u);
+      }
+    }
     __syncthreads();
     for (uint32_t d = t; d < D; d += kBlock) counts[tile * D + d] = hist[0][d] + hist[1][d] + hist[2][d] + hist[3][d];
     __syncthreads();
