@@ -19,7 +19,6 @@ __global__ void read_rows(const uint4* __restrict__ in, uint64_t rows, int piece
 
 int main() {
   const uint64_t bytes = 32ull << 30;              // 32 GB table of 64-byte rows
-  const uint64_t rows = bytes / 64;
   uint4* buf;
   unsigned long long* sink;
   if (hipMalloc(&buf, bytes) != hipSuccess || hipMalloc(&sink, 8) != hipSuccess) return 1;
@@ -27,19 +26,22 @@ int main() {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  for (int pieces : {4, 2, 1}) {
+  for (int cfg = 0; cfg < 6; ++cfg) {
+    const int row_pieces = cfg < 3 ? 4 : 8;                    // 64- or 128-byte rows
+    const int pieces = cfg < 3 ? (4 >> cfg) : (8 >> (cfg - 3));
+    const uint64_t nr = bytes / (16 * row_pieces);
     float best = 1e9f;
     for (int it = 0; it < 4; ++it) {
       hipEventRecord(a);
-      read_rows<<<8192, 256>>>(buf, rows, pieces, 4, sink);
+      read_rows<<<8192, 256>>>(buf, nr, pieces, row_pieces, sink);
       hipEventRecord(b);
       hipEventSynchronize(b);
       float ms;
       hipEventElapsedTime(&ms, a, b);
       if (it && ms < best) best = ms;
     }
-    printf("read %2d of 64 bytes per row: %.2f ms, %.0f GB/s of touched bytes, %.0f GB/s of table\n", 16 * pieces,
-           best, rows * 16.0 * pieces / best / 1e6, bytes / best / 1e6);
+    printf("read %3d of %3d bytes per row: %.2f ms, %.0f GB/s of touched bytes, %.0f GB/s of table\n", 16 * pieces,
+           16 * row_pieces, best, nr * 16.0 * pieces / best / 1e6, bytes / best / 1e6);
   }
   return 0;
 }
