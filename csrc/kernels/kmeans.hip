@@ -705,6 +705,14 @@ __global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __re
 }
 
 // Compaction of the near-tie flags (bit 31 of assign) into (point, estimate) pairs; clears the flag.
+// Zeroes the near-tie count + pad (4 words) before a step.  A kernel rather than a memset node so
+// that a captured step (runtime/hipgraph.py) resets it on every replay like an eager run does.
+__global__ void kmeans_near_reset(uint32_t* __restrict__ near_cnt) {
+  if (threadIdx.x < 4) near_cnt[threadIdx.x] = 0u;
+}
+
+// Lists the points flagged near-tie by the step kernel (capacity n entries: each point is listed
+// at most once per step; writes past it are dropped so a missed reset cannot overrun the list).
 __global__ __launch_bounds__(256) void kmeans_near_list(int32_t* __restrict__ assign, uint64_t n,
                                                         uint32_t* __restrict__ near_cnt, uint32_t* __restrict__ near_list) {
   for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x; b < n; b += (uint64_t)gridDim.x * blockDim.x) {
@@ -721,8 +729,10 @@ __global__ __launch_bounds__(256) void kmeans_near_list(int32_t* __restrict__ as
       if (near) {
         const uint32_t o = base + popc_below(m);
         const uint32_t est = (uint32_t)a & 0x7FFFFFFFu;
-        near_list[2 * (uint64_t)o] = (uint32_t)p;
-        near_list[2 * (uint64_t)o + 1] = est;
+        if (o < n) {
+          near_list[2 * (uint64_t)o] = (uint32_t)p;
+          near_list[2 * (uint64_t)o + 1] = est;
+        }
         assign[p] = (int32_t)est;
       }
     }
@@ -737,8 +747,8 @@ __global__ __launch_bounds__(64) void kmeans_rerank_kernel(const float* __restri
                                                            const uint32_t* __restrict__ near_cnt,
                                                            const uint32_t* __restrict__ near_list,
                                                            int32_t* __restrict__ assign, double* __restrict__ gsum,
-                                                           unsigned long long* __restrict__ gcnt) {
-  const uint32_t total = *near_cnt;
+                                                           unsigned long long* __restrict__ gcnt, uint64_t n) {
+  const uint32_t total = (uint64_t)*near_cnt < n ? *near_cnt : (uint32_t)n;
   const int l = threadIdx.x;
   for (uint32_t i = blockIdx.x; i < total; i += gridDim.x) {
     const uint64_t p = near_list[2 * (uint64_t)i];
@@ -842,7 +852,7 @@ DR_API int dr_kmeans_step(const float* X, uint64_t n, int d, const float* C, int
     const unsigned g3 = (unsigned)(blocks < (uint64_t)num_cus() ? blocks : (uint64_t)num_cus());
     uint32_t* near_cnt = reinterpret_cast<uint32_t*>(near_ws);
     uint32_t* near_list = near_cnt + 4;
-    hipMemsetAsync(near_cnt, 0, 16, s);
+    kmeans_near_reset<<<1, 64, 0, s>>>(near_cnt);
 #define DR_KM3(KTV, DB) kmeans_mfma_kernel<KTV, DB><<<g3, 256, 0, s>>>(X, n, C, cnorm_ws, K, assign, gsum, gcnt, 256)
     static int m16 = -1;      // DRYAD_KM_MFMA16=0: the 32x32 one-workgroup-per-CU kernel
     if (m16 < 0) {
@@ -872,7 +882,7 @@ DR_API int dr_kmeans_step(const float* X, uint64_t n, int d, const float* C, int
     }
 #undef DR_KM3
     kmeans_near_list<<<grid_for(n, 256, 4096), 256, 0, s>>>(assign, n, near_cnt, near_list);
-    kmeans_rerank_kernel<<<1024, 64, 0, s>>>(X, C, cnorm_ws, K, near_cnt, near_list, assign, gsum, gcnt);
+    kmeans_rerank_kernel<<<1024, 64, 0, s>>>(X, C, cnorm_ws, K, near_cnt, near_list, assign, gsum, gcnt, n);
     DR_LAUNCH_CHECK();
     if (dbg & 8) {
       uint32_t v = 0;
