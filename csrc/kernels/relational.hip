@@ -698,17 +698,30 @@ __global__ __launch_bounds__(256) void group_chunk_starts_kernel(const E128* __r
   const int lane = lane_id();
   const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   const uint64_t w0 = (((uint64_t)blockIdx.x * blockDim.x) + threadIdx.x) >> 6;
+  // lane-adjacent loads (element cbase + 64 k + lane): each load instruction covers 1 KB of
+  // consecutive entries instead of one 16-byte word in each of 64 lines; the chunk (and so the
+  // count) is the same 512 consecutive entries either way
   for (uint64_t cbase = w0 * kChunkElems; cbase < n; cbase += waves * kChunkElems) {
-    const uint64_t first = cbase + (uint64_t)lane * PER;
     uint64_t kh[PER];
 #pragma unroll
-    for (int k = 0; k < PER; ++k) kh[k] = first + k < n ? e[first + k].hi : 0;
-    uint64_t prev = __shfl_up(kh[PER - 1], 1, 64);
-    if (lane == 0 && first > 0) prev = e[first - 1].hi;
+    for (int k = 0; k < PER; ++k) {
+      const uint64_t i = cbase + (uint64_t)(64 * k + lane);
+      kh[k] = i < n ? e[i].hi : 0;
+    }
+    const uint64_t before = (lane == 0 && cbase > 0) ? e[cbase - 1].hi : 0;
     uint64_t c = 0;
 #pragma unroll
-    for (int k = 0; k < PER; ++k)
-      c += (first + k < n && (first + k == 0 || kh[k] != (k == 0 ? prev : kh[k - 1]))) ? 1 : 0;
+    for (int k = 0; k < PER; ++k) {
+      const uint64_t i = cbase + (uint64_t)(64 * k + lane);
+      uint64_t prev = __shfl_up(kh[k], 1, 64);
+      if (k > 0) {
+        const uint64_t wrap = __shfl(kh[k > 0 ? k - 1 : 0], 63, 64);   // lane 63 of step k-1
+        if (lane == 0) prev = wrap;
+      } else if (lane == 0) {
+        prev = before;
+      }
+      c += (i < n && (i == 0 || kh[k] != prev)) ? 1 : 0;
+    }
     c = wave_sum64(c);
     if (lane == 0) cnt[cbase / kChunkElems] = (int64_t)c;
   }
