@@ -22,7 +22,7 @@ from ..ops import recordsort as RS
 from ..ops import relational as R
 from ..ops import sort as S
 from . import trace as TR
-from .table import DeviceTable, PartialMeta, Ported, Shape, from_objects
+from .table import DeviceTable, PartialMeta, Ported, PortTables, Shape, from_objects
 from .trace import NotTraceable
 
 E_SHAPE = Shape("tuple", ["lo", "hi"])
@@ -1105,6 +1105,89 @@ def op_agg_partial(op, inputs, v):
     return [(c, _record_at(t, i) if c else None)]
 
 
+class _AccFold:
+    """Symbolic accumulator of a user ``Aggregate(seed, func)``: tracing ``func(acc, x)`` with
+    ``acc`` bound to this object records ``acc + T(x)`` (or ``acc - T(x)``, ``T(x) + acc``, ``acc
+    + T(x) + c``, ...).  A fold whose step only adds a per-record term is ``seed + sum_i T(x_i)``,
+    so the sequential vertex becomes one device reduction.  Any other use of ``acc`` (products,
+    comparisons, branches, attribute access) is not a sum fold and raises NotTraceable."""
+    __slots__ = ("term",)
+
+    def __init__(self, term=0):
+        self.term = term
+
+    def __add__(self, o):
+        if isinstance(o, _AccFold):
+            raise NotTraceable("accumulator used twice in the fold step")
+        return _AccFold(self.term + (o if isinstance(o, (TR.Col, int, float)) else TR.Col(o)))
+
+    __radd__ = __add__
+
+    def __sub__(self, o):
+        if isinstance(o, _AccFold):
+            raise NotTraceable("accumulator used twice in the fold step")
+        return _AccFold(self.term - (o if isinstance(o, (TR.Col, int, float)) else TR.Col(o)))
+
+    def __getattr__(self, name):
+        raise NotTraceable(f"accumulator used as {name}: not a sum fold")
+
+    def __bool__(self):
+        raise NotTraceable("branch on the accumulator")
+
+    def _no(self, *a):
+        raise NotTraceable("accumulator in a non-additive expression")
+
+    __mul__ = __rmul__ = __rsub__ = __truediv__ = __rtruediv__ = __floordiv__ = __mod__ = __pow__ = _no
+    __and__ = __or__ = __xor__ = __lt__ = __le__ = __gt__ = __ge__ = __eq__ = __ne__ = __neg__ = _no
+    __hash__ = None
+
+
+def op_aggregate_seq(op, inputs, v):
+    """Non-associative ``Aggregate(seed, func[, result])`` on the merged partition
+    (reference: DryadLinqQueryGen Aggregate without [Associative] runs as one vertex folding the
+    whole input, DryadLinqQueryGen.cs:3384-3395).  When ``func`` traces to ``acc + T(x)`` the fold
+    is ``seed + sum(T(x))``: one device reduction instead of a host loop over every record.
+    Integer folds are exact; float folds are re-associated like the device ``Sum``.  Without a
+    seed the first record seeds the fold (scalar records only)."""
+    from ..ops import reduce as RD
+    from ..query import _NOSEED
+    t = _check(_one(inputs))
+    s = op["spec"]
+    if t.n == 0:
+        raise NotTraceable("empty partition")
+    seed = s.get("seed", _NOSEED)
+    rows = t
+    if seed is _NOSEED:
+        if t.shape.kind != "scalar":
+            raise NotTraceable("seedless Aggregate over non-scalar records")
+        first = t.cols[t.shape.fields[0]][:1].tolist()[0]
+        if t.n == 1:
+            r = s.get("result_selector")
+            return [r(first) if r else first]
+        rows, seed = t.slice(1, t.n), first
+    elif isinstance(seed, bool) or not isinstance(seed, (int, float)):
+        raise NotTraceable("non-numeric Aggregate seed")
+    res = _traced(s["func"], _AccFold(), TR.proxy(rows))
+    if isinstance(res, TR.Col) and isinstance(res.t, _AccFold):     # T(x) + acc via a tensor operand
+        res = res.t
+    if not isinstance(res, _AccFold):
+        raise NotTraceable("Aggregate step is not acc + f(x)")
+    term = res.term
+    if isinstance(term, (int, float)) and not isinstance(term, bool):
+        acc = seed + term * rows.n
+    else:
+        if not isinstance(term, TR.Col) or not isinstance(term.t, torch.Tensor):
+            raise NotTraceable("Aggregate term is not a numeric field")
+        col = term.t.expand(rows.n) if term.t.dim() == 0 else term.t
+        if col.dim() != 1 or col.is_complex():
+            raise NotTraceable("Aggregate term is not a scalar field")
+        if col.dtype == torch.bool:
+            col = col.to(torch.int64)
+        acc = seed + RD.reduce_multi(rows.n, [(RD.SUM, col.contiguous(), None)], t.device)[0]
+    r = s.get("result_selector")
+    return [r(acc) if r else acc]
+
+
 def _host_partials(inputs) -> list:
     out = []
     for x in inputs:
@@ -1207,7 +1290,7 @@ def op_fork(op, inputs, v):
     t = _check(_one(inputs))
     keys = op.get("keys")
     if keys is None:
-        raise NotTraceable("ForkTuple mappers run on the host")
+        return _fork_tuple(op, t)
     if t.n == 0:
         raise NotTraceable("empty partition")
     if any(isinstance(k, bool) or not isinstance(k, (int, float)) for k in keys):
@@ -1226,6 +1309,37 @@ def op_fork(op, inputs, v):
     for c in counts:
         offs.append(offs[-1] + c)
     return Ported(t.take(order), offs)
+
+
+def _fork_tuple(op, t):
+    """Per-record ForkTuple mapper (reference ForkTuple.cs / DryadLinqEnumerable Fork): the mapper
+    is traced once over the partition; port k holds ``Value`` of slot k (a traced field or record)
+    for the records whose ``HasValue`` is true, in record order.  Ports may differ in record type,
+    so the output is one table per port (PortTables); an unused slot is an empty port."""
+    from ..types import ForkTuple, ForkValue
+    if not op.get("per_record"):
+        raise NotTraceable("ForkTuple mapper over the whole sequence runs on the host")
+    if t.n == 0:
+        raise NotTraceable("empty partition")
+    res = TR.call(op["mapper"], t)
+    if not isinstance(res, ForkTuple):
+        raise NotTraceable("Fork mapper did not return a ForkTuple")
+    tables = []
+    for fv in (res.First, res.Second, res.Third):
+        if not isinstance(fv, ForkValue):
+            raise NotTraceable("ForkTuple slot is not a ForkValue")
+        hv = fv.HasValue
+        if hv is False or (isinstance(hv, TR.Col) and hv.t.dim() == 0 and not bool(hv.t)):
+            tables.append([])
+            continue
+        tab = _result_table(_traced(lambda: fv.Value), t)
+        if hv is True:
+            tables.append(tab)
+            continue
+        if not isinstance(hv, TR.Col) or hv.t.dtype != torch.bool:
+            raise NotTraceable("ForkValue.HasValue must be a bool or a boolean field")
+        tables.append(tab if hv.t.dim() == 0 else tab.mask(hv.t))
+    return PortTables(tables)
 
 
 def op_apply(op, inputs, v):

@@ -284,6 +284,20 @@ class Ported:
         return len(self.offsets) - 1
 
 
+@dataclass
+class PortTables:
+    """A multi-port vertex output whose ports are separate tables (ForkTuple ports may hold
+    different record types); an empty, untyped port is an empty host list."""
+    tables: list
+
+    def port(self, k: int):
+        return self.tables[k]
+
+    @property
+    def nports(self):
+        return len(self.tables)
+
+
 # ---------------------------------------------------------------------------------------------
 _NP_OF = {T.Int32: np.int32, T.Int64: np.int64, T.Float64: np.float64, T.Float32: np.float32, T.Bool: np.bool_,
           T.Int16: np.int16, T.Byte: np.uint8, T.SByte: np.int8, T.UInt16: np.uint16}

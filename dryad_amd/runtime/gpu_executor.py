@@ -27,7 +27,7 @@ from ..compiler.planner import compile_queries
 from ..errors import DryadLinqException, DryadLinqJobException, ErrorCode
 from ..gpu import ops as G
 from ..attributes import is_device_function
-from ..gpu.table import DeviceTable, Ported, from_objects
+from ..gpu.table import DeviceTable, PortTables, Ported, from_objects
 from ..gpu.trace import NotTraceable
 from ..io.hosttable import HostRows
 from ..ops import extsort as EX
@@ -68,8 +68,8 @@ class GpuVertexContext(V.VertexContext):
 def _to_objects(x):
     if isinstance(x, DeviceTable):
         return x.to_objects()
-    if isinstance(x, Ported):
-        return [x.port(k).to_objects() for k in range(x.nports)]
+    if isinstance(x, (Ported, PortTables)):
+        return [_to_objects(x.port(k)) for k in range(x.nports)]
     return x
 
 
@@ -344,7 +344,7 @@ class GpuJobRunner:
                 return val.port(dst_p)
             return val[dst_p]
         k = si.port
-        if isinstance(val, Ported):
+        if isinstance(val, (Ported, PortTables)):
             return val.port(k)
         if isinstance(val, list) and val and isinstance(val[0], list) and self.plan.stages[si.src].out_ports > 1:
             return val[k]

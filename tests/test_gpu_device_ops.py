@@ -101,6 +101,32 @@ def test_aggregates_on_device_match_localdebug(parts):
         assert not bad, (name, bad)
 
 
+@pytest.mark.parametrize("parts", [1, 3])
+def test_user_aggregate_sum_fold_on_device(parts):
+    """Aggregate(seed, func) whose step is acc + f(x) folds on the device (one reduction);
+    any other step still runs on the host and gives the oracle's answer."""
+    cases = {
+        "seed": (lambda c: c.FromEnumerable(INTS).Aggregate(5, lambda a, x: a + x * 3 - 1), True),
+        "term_first": (lambda c: c.FromEnumerable(INTS).Aggregate(0, lambda a, x: (x % 11) + a), True),
+        "minus": (lambda c: c.FromEnumerable(INTS).Aggregate(100, lambda a, x: a - x), True),
+        "tuple_result": (lambda c: c.FromEnumerable(PAIRS).Aggregate(
+            0.5, lambda a, p: a + p[1] * 2, lambda a: round(a, 6)), True),
+        "seedless": (lambda c: c.FromEnumerable(INTS).Aggregate(lambda a, x: a + x), True),
+        "bool_term": (lambda c: c.FromEnumerable(INTS).Aggregate(0, lambda a, x: a + (x > 0)), True),
+        "product_host": (lambda c: c.FromEnumerable(INTS[:50]).Aggregate(1, lambda a, x: a * (x % 3 + 1)), False),
+        "max_host": (lambda c: c.FromEnumerable(INTS).Aggregate(0, lambda a, x: a if a > x else x), False),
+    }
+    for name, (q, on_device) in cases.items():
+        c = _ctx(parts)
+        exp, got = q(_local()), q(c)
+        if isinstance(exp, float):
+            assert got == pytest.approx(exp, rel=1e-9), name
+        else:
+            assert got == exp, name
+        fb = {f[1] for f in _fallbacks(c)}
+        assert ("aggregate_seq" not in fb) == on_device, (name, _fallbacks(c))
+
+
 def test_hash_join_pairs_match_python_join():
     from dryad_amd.ops import relational as R
     torch.manual_seed(0)
@@ -173,6 +199,27 @@ def test_zip_selectmany_window_fork_on_device():
         for k in (0, 3, 4):
             assert sorted(kf[k]) == sorted(kl[k])
             assert "fork" not in {op for _, op, _ in _fallbacks(c)}, _fallbacks(c)
+
+
+@pytest.mark.parametrize("parts", [1, 2])
+def test_fork_tuple_mapper_on_device(parts):
+    """Per-record ForkTuple mapper traced once: ports of different record types (scalar, tuple),
+    a masked port and an unused slot, each consumed by a further device op."""
+    def mapper(p):
+        return D.ForkTuple(D.ForkValue(p[0] * 2, True), D.ForkValue((p[0], p[1] + 1.0), p[0] % 3 == 1),
+                           D.ForkValue(None, False))
+    c, l = _ctx(parts), _local()
+    fc, fl = c.FromEnumerable(PAIRS[:20000]).Fork(mapper, per_record=True), \
+        l.FromEnumerable(PAIRS[:20000]).Fork(mapper, per_record=True)
+    assert sorted(fc.First.Where(lambda x: x > 10)) == sorted(fl.First.Where(lambda x: x > 10))
+    assert "fork" not in {op for _, op, _ in _fallbacks(c)}, _fallbacks(c)
+    assert sorted(fc.Second.Select(lambda t: (t[0], t[1] * 2))) == sorted(fl.Second.Select(lambda t: (t[0], t[1] * 2)))
+    assert "fork" not in {op for _, op, _ in _fallbacks(c)}, _fallbacks(c)
+    assert list(fc.Third) == list(fl.Third) == []
+    # an untraceable mapper still answers correctly on the host
+    hc = c.FromEnumerable(PAIRS[:500]).Fork(lambda p: D.ForkTuple(D.ForkValue(str(p[0]), True)), per_record=True)
+    hl = l.FromEnumerable(PAIRS[:500]).Fork(lambda p: D.ForkTuple(D.ForkValue(str(p[0]), True)), per_record=True)
+    assert sorted(hc.First) == sorted(hl.First)
 
 
 @pytest.mark.parametrize("aos", [False, True])
