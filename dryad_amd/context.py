@@ -178,9 +178,16 @@ class DryadLinqContext:
         return self._id
 
     def Dispose(self):
+        """Release the executor; any later use of the context raises ContextDisposed
+        (reference DryadLinqContext.Dispose / ThrowIfDisposed, DryadLinqContext.cs:1262-1275)."""
+        object.__setattr__(self, "_disposed", True)
         if self._executor is not None:
             self._executor.close()
             object.__setattr__(self, "_executor", None)
+
+    def _throw_if_disposed(self):
+        if getattr(self, "_disposed", False):
+            raise DryadLinqException(ErrorCode.ContextDisposed, "the DryadLinqContext has been disposed")
 
     def __enter__(self):
         return self
@@ -189,11 +196,19 @@ class DryadLinqContext:
         self.Dispose()
 
     def ClientVersion(self):
+        self._throw_if_disposed()
+        from . import __version__
+        return __version__
+
+    def ServerVersion(self):
+        """Version of the job-side runtime (the native job graph library when built)."""
+        self._throw_if_disposed()
         from . import __version__
         return __version__
 
     # ------------------------------------------------------------------ inputs
     def FromEnumerable(self, data, dtype=None) -> Query:
+        self._throw_if_disposed()
         data = list(data)
         if dtype is None:
             dtype = T.infer_common_type(data[:1000]) if data else T.Int32
@@ -201,6 +216,7 @@ class DryadLinqContext:
 
     def FromStore(self, uri: str, dtype=None, deserializer=None) -> Query:
         from .io.providers import provider_for
+        self._throw_if_disposed()
         p = provider_for(str(uri))
         if not p.exists(str(uri)):
             raise DryadLinqException(ErrorCode.FailedToGetStreamProps, f"dataset {uri} does not exist")
@@ -244,6 +260,7 @@ class DryadLinqContext:
         p.write_table(uri, [data], dtype)
 
     def _enumerate(self, q: Query) -> list:
+        self._throw_if_disposed()
         self._freeze()
         if self._local_debug():
             from .localdebug import LocalEvaluator
@@ -251,6 +268,7 @@ class DryadLinqContext:
         return self._get_executor().enumerate(q)
 
     def _execute_scalar(self, q: Query):
+        self._throw_if_disposed()
         self._freeze()
         if self._local_debug():
             from .localdebug import LocalEvaluator
@@ -268,6 +286,14 @@ class DryadLinqContext:
         qs = []
         for q in queries:
             qs.extend(q if isinstance(q, (list, tuple)) else [q])
+        self._throw_if_disposed()
+        for q in qs:
+            if not isinstance(q, Query):
+                raise DryadLinqException(ErrorCode.MustStartFromContext,
+                                         "only DryadLINQ queries created from a DryadLinqContext can be submitted")
+            if q._ctx is not self:
+                raise DryadLinqException(ErrorCode.MustStartFromContext,
+                                         "the queries submitted together must be created using the same DryadLinqContext")
         self._freeze()
         outs = []
         for q in qs:

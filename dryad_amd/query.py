@@ -363,6 +363,8 @@ class Query:
                 comparer = a
             elif callable(a):
                 result_selector = a
+        if partition_count is not None and partition_count <= 0:
+            raise ValueError(f"partitionCount must be positive, got {partition_count}")  # ArgumentOutOfRange
         return self._q("HashPartition", key_selector=key_selector, comparer=comparer, count=partition_count,
                        result_selector=result_selector, dtype=None if result_selector else self.dtype)
 
@@ -378,6 +380,8 @@ class Query:
                 range_separators = list(a)
             elif _is_cmp_comparer(a):
                 comparer = a
+        if partition_count is not None and partition_count <= 0:
+            raise ValueError(f"partitionCount must be positive, got {partition_count}")  # ArgumentOutOfRange
         if range_separators is not None:
             _check_separators(range_separators, comparer, is_descending)
         return self._q("RangePartition", key_selector=key_selector, count=partition_count,
