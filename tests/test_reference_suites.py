@@ -232,3 +232,142 @@ def test_GroupByWithAnonymousTypes_Pipeline_and_Nested():
                                                  lambda k, g: (k, g.Count())))
     both(lambda c: c.FromEnumerable(data).GroupBy(lambda t: [t[0], t[1]] and (t[0], t[1]),
                                                  lambda k, g: (k, [x[2] for x in g][:2])))
+
+
+# ------------------------------------------------------------------ GroupByReduceTests.cs
+def _gbr(c):
+    return c.FromEnumerable(GBR).HashPartition(lambda x: x % 7, 3)
+
+
+def _decomposed(build):
+    c = cluster_ctx()
+    return "group_partial" in c.Explain(build(c))
+
+
+def test_Decomposition_Average_and_BuiltInCountIsDistributable():
+    for sel in (lambda k, g: (k, g.Average()), lambda k, g: (k, g.Count())):
+        b = lambda c, sel=sel: _gbr(c).GroupBy(lambda x: x % 10, sel)
+        both(b)
+        assert _decomposed(b)
+
+
+def test_DistributiveResultSelector_and_Select():
+    b = lambda c: _gbr(c).GroupBy(lambda x: x % 10, lambda k, g: g.Sum() * 2 + k)
+    both(b)
+    assert _decomposed(b)
+    both(lambda c: _gbr(c).GroupBy(lambda x: x % 10).Select(lambda g: (g.Key, g.Max(), g.Min())))
+
+
+def test_Bug12078_GroupByReduceWithResultSelectingAggregate():
+    both(lambda c: _gbr(c).GroupBy(lambda x: x % 10, lambda k, g: (k, g.Sum(lambda x: x * 3), g.Count(lambda x: x > 50))))
+
+
+class _Max2(D.IDecomposable):
+    """Distributable combiner whose accumulator type (a pair) differs from the result type."""
+    def Seed(self, x):
+        return (x, 1)
+
+    def Accumulate(self, a, x):
+        return (max(a[0], x), a[1] + 1)
+
+    def RecursiveAccumulate(self, a, b):
+        return (max(a[0], b[0]), a[1] + b[1])
+
+    def FinalReduce(self, a):
+        return f"{a[0]}/{a[1]}"
+
+
+class _SumNoFinal(D.IDecomposable):
+    def Seed(self, x):
+        return x
+
+    def Accumulate(self, a, x):
+        return a + x
+
+    def RecursiveAccumulate(self, a, b):
+        return a + b
+
+    def FinalReduce(self, a):
+        return a
+
+
+@D.decomposable(_Max2)
+def _max_count(g):
+    xs = list(g)
+    return f"{max(xs)}/{len(xs)}"
+
+
+@D.decomposable(_SumNoFinal)
+def _sum_nf(g):
+    return sum(g)
+
+
+def test_GroupByReduceWithCustomDecomposableFunction_DistributableCombiner_DifferingTypes_NoFinalizer():
+    for f in (_max_count, _sum_nf):
+        b = lambda c, f=f: _gbr(c).GroupBy(lambda x: x % 9, lambda k, g: (k, f(g)))
+        both(b)
+        assert _decomposed(b)
+
+
+def test_GroupByReduceWithCustomDecomposableFunction_NonDistributableCombiner():
+    # a plain Python function of the group is not decomposable: the planner keeps the full groups
+    b = lambda c: _gbr(c).GroupBy(lambda x: x % 9, lambda k, g: (k, sorted(g)[len(list(g)) // 2]))
+    both(b)
+    assert not _decomposed(b)
+
+
+def test_GroupByReduce_UseAllInternalDecomposables_and_SameDecomposableUsedTwice():
+    b = lambda c: _gbr(c).GroupBy(lambda x: x % 6, lambda k, g: (
+        k, g.Count(), g.Sum(), g.Min(), g.Max(), g.Average(), g.Any(lambda x: x > 90), g.All(lambda x: x >= 0),
+        g.Contains(50), g.Sum(), _sum_nf(g), _sum_nf(g)))
+    both(b)
+    assert _decomposed(b)
+
+
+def test_GroupByReduce_BuiltIn_First():
+    # First depends on the record order inside a group: compare on a source-ordered input
+    both(lambda c: c.FromEnumerable(GBR).GroupBy(lambda x: x % 5, lambda k, g: (k, g.First())))
+
+
+def test_GroupByReduce_ResultSelector_ComplexNewExpression_and_ListInitializer():
+    both(lambda c: _gbr(c).GroupBy(lambda x: x % 4, lambda k, g: {"key": k, "stats": (g.Count(), [g.Min(), g.Max()]),
+                                                                  "mean": g.Average()}))
+    both(lambda c: _gbr(c).GroupBy(lambda x: x % 4, lambda k, g: [k, g.Sum(), g.Count()]))
+    both(lambda c: _gbr(c).GroupBy(lambda x: x % 4, lambda k, g: [_sum_nf(g), _max_count(g)]))
+
+
+def test_GroupByReduce_ProgrammingManualExample():
+    words = ["the", "quick", "brown", "fox", "the", "lazy", "dog", "the", "fox"] * 7
+    r = both(lambda c: c.FromEnumerable(words).GroupBy(lambda w: w, lambda k, g: (k, g.Count()))
+             .OrderByDescending(lambda t: t[1]).Take(3), ordered=True)
+    assert r[0] == ("the", 21)
+
+
+def test_GroupByReduce_BitwiseNegationOperator():
+    both(lambda c: _gbr(c).GroupBy(lambda x: x % 8, lambda k, g: (~k, ~g.Sum(), g.Count() & 0xF)))
+
+
+# ------------------------------------------------------------------ ApplyAndForkTests.cs
+def test_Aggregate_WithCombiner():
+    class AddAssoc:
+        def Seed(self):
+            return 0
+
+        def RecursiveAccumulate(self, a, b):
+            return a + b
+
+    @D.associative(AddAssoc)
+    def add(a, x):
+        return a + x
+
+    c = cluster_ctx()
+    q = _gbr(c)
+    assert both(lambda c: _gbr(c).Aggregate(0, add)) == sum(GBR)
+    assert "(partial)" in c.Explain(q.AggregateAsQuery(0, add))      # per-partition partials + combine
+
+
+def test_FullHomomorphicBinaryApply_IdenticalDataSets():
+    def pairsum(a, b):
+        return [x + y for x, y in zip(a, b)]
+    r = both(lambda c: _simple(c).Apply(_simple(c), D.homomorphic(pairsum)))
+    assert sorted(r) == sorted(2 * x for x in SIMPLE)
