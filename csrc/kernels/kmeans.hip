@@ -495,7 +495,7 @@ __global__ __launch_bounds__(256) void kmeans_mfma_kernel(const float* __restric
 //   distances  each wave: its 16 points x 16-centroid tiles, 3 split-bf16 MFMAs per 32 dims, the
 //              next step's loads issued per k-step as their registers free up; argmin + runner-up
 //              merged over the 4 lanes that share a point; near ties flagged as before
-//   sums       every wave: the block's 64 points (one-hot x exact 3-part split of x, K = 32 points
+//   sums       every wave: the block's 64 points (one-hot x 2-part bf16 split of x, K = 32 points
 //              per MFMA) for its own 32-dim slice, so a wave keeps K x 32 sums (32 registers)
 // LDS: the block's 64 staged points (34 KB) + split centroids (35 KB at K = 64) -> two workgroups
 // per CU, two waves per SIMD.  Lane map (16x16x32): A[row l&15][k = 8(l>>4) + j],
@@ -673,22 +673,22 @@ __global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __re
         for (int j = 0; j < 8; ++j) xv[dt][j] = xs[(32 * ks + 8 * g + j) * kXRow16 + 32 * w + 16 * dt + r];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
-        bf16x8 ph, pm, pl;
+        // two-part split (x = xh + xm + rest, |rest| <= 2^-16 |x|, unbiased round-to-nearest):
+        // the sums' per-point error averages down over a cluster to far below the f32 rounding
+        // of the centroid, so the third part (a third of these MFMAs and ~3 VALU per element,
+        // the kernel's binding units) is not computed
+        bf16x8 ph, pm;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float v = xv[dt][j];
           const __bf16 a0 = (__bf16)v;
-          const float r1 = v - (float)a0;
-          const __bf16 a1 = (__bf16)r1;
           ph[j] = a0;
-          pm[j] = a1;
-          pl[j] = (__bf16)(r1 - (float)a1);
+          pm[j] = (__bf16)(v - (float)a0);
         }
 #pragma unroll
         for (int ct = 0; ct < KT; ++ct) {
           S[ct][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oh[ct], ph, S[ct][dt], 0, 0, 0);
           S[ct][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oh[ct], pm, S[ct][dt], 0, 0, 0);
-          S[ct][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oh[ct], pl, S[ct][dt], 0, 0, 0);
         }
       }
     }
