@@ -9,7 +9,7 @@ for ctr in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "kmeans_mfma" \
     -d gpurun_out/pmc_km/p$i -o run --output-format csv -- python3 tools/microbench_kmeans.py 50e6 64 \
-    > gpurun_out/pmc_km/p$i.log 2>&1 || { tail -5 gpurun_out/pmc_km/p$i.log; echo "pass $i failed"; }
+    > gpurun_out/pmc_km/p$i.log 2>&1 || { tail -5 gpurun_out/pmc_km/p$i.log; echo "pass $i failed"; exit 1; }
 done
-timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/pmc_km/trace -o run --output-format csv -- python3 tools/microbench_kmeans.py 50e6 64 > gpurun_out/pmc_km/trace.log 2>&1 || echo trace failed
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/pmc_km/trace -o run --output-format csv -- python3 tools/microbench_kmeans.py 50e6 64 > gpurun_out/pmc_km/trace.log 2>&1 || { echo trace failed; exit 1; }
 echo PMC_DONE
