@@ -1158,9 +1158,11 @@ def op_aggregate_seq(op, inputs, v):
     seed = s.get("seed", _NOSEED)
     rows = t
     if seed is _NOSEED:
-        if t.shape.kind != "scalar":
-            raise NotTraceable("seedless Aggregate over non-scalar records")
+        if t.shape.kind != "scalar" or t.heap is not None or t.strs or t.shape.fields[0] not in t.cols:
+            raise NotTraceable("seedless Aggregate over non-numeric records")
         first = t.cols[t.shape.fields[0]][:1].tolist()[0]
+        if isinstance(first, bool) or not isinstance(first, (int, float)):
+            raise NotTraceable("seedless Aggregate over non-numeric records")
         if t.n == 1:
             r = s.get("result_selector")
             return [r(first) if r else first]
