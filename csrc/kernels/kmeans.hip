@@ -598,7 +598,6 @@ __global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __re
 #pragma unroll
     for (int ct = 0; ct < KT; ++ct) Dt[ct] = f32x4{};
     float xx = 0.f;
-    const bool more = step + gridDim.x < steps;
 #pragma unroll
     for (int s_ = 0; s_ < 4; ++s_) {
       bf16x8 xh, xm;
@@ -609,7 +608,8 @@ __global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __re
         xh[j] = (__bf16)v;
         xm[j] = (__bf16)(v - (float)xh[j]);
       }
-      if (more) load_part(step + gridDim.x, s_, xr);     // registers free: next step in flight
+      load_part(step + gridDim.x, s_, xr);   // next step in flight; unconditional (clamped rows) so
+                                             // the loaded registers need no loop-carried copy
       bf16x8 ah[KT], am[KT];                              // every fragment read before the MFMAs
 #pragma unroll
       for (int ct = 0; ct < KT; ++ct) {
