@@ -27,6 +27,23 @@ BASELINE_GBPS = 3.1   # DryadLINQ TeraSort, 240 machines, ~1 TB in 
 METRIC = "GB/sec sorted (whole node), 1 TB TeraSort at 1/2/4/8 MI355X"
 
 
+# DRYAD_* variables a measured run may carry: logging / paths only.  Anything else is an A/B,
+# debug or transport override of the kernels or the executor, so a headline number taken with it
+# would not be the product's (``--rehearsal`` admits DRYAD_DIST_BACKEND for the shared-GPU gloo
+# rehearsal of the multi-rank path and marks the line as such).
+ALLOWED_ENV = {"DRYAD_LOGGING_LEVEL", "DRYAD_HOME", "DRYAD_TEMP_DIR", "DRYAD_ROCTX"}
+
+
+def check_env(rehearsal: bool) -> dict:
+    knobs = {k: v for k, v in os.environ.items() if k.startswith("DRYAD_") and k not in ALLOWED_ENV}
+    if rehearsal:
+        knobs.pop("DRYAD_DIST_BACKEND", None)
+    if knobs:
+        print(f"[bench] refusing to measure with engine overrides set: {knobs}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    return {k: v for k, v in os.environ.items() if k.startswith("DRYAD_")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -36,7 +53,10 @@ def main():
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--direct", action="store_true",
                     help="run the sort pipeline directly instead of through the DryadLINQ query API")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="shared-GPU gloo rehearsal of the multi-rank path (admits DRYAD_DIST_BACKEND)")
     args = ap.parse_args()
+    env = check_env(args.rehearsal)
 
     import torch
     from dryad_amd.parallel.comm import init_world, shutdown
@@ -92,6 +112,8 @@ def main():
                 "bytes_per_gpu": job.bytes_per_rank,
                 "total_bytes": total_bytes,
                 "validated": None if val is None else val["ok"],
+                "env": env,
+                "rehearsal": bool(args.rehearsal),
                 "path": "direct" if args.direct else "DryadLINQ query -> GPU executor (fused OrderBy gang stage)",
                 # the input read: every record is generated once per step; with one rank into the
                 # HBM input table the local sort gathers from, with several ranks straight into

@@ -120,11 +120,7 @@ DR_API int dr_gen_records64_rows(int64_t* out, int ncols, uint64_t n, uint64_t f
   // the dimension-table key needs 128-bit arithmetic once (first + n) * dim_mult + seed can pass 2^64
   const unsigned __int128 top = (unsigned __int128)(first + n) * dim_mult + seed;
   const bool wide = dim_mult && (top >> 64) != 0;
-  static int staged = -1;    // DRYAD_GEN_ROWS_LDS=0: the one-lane-per-field kernel
-  if (staged < 0) {
-    const char* e = getenv("DRYAD_GEN_ROWS_LDS");
-    staged = (e && atoi(e) == 0) ? 0 : 1;
-  }
+  const bool staged = true;  // LDS-staged rows (the one-lane-per-field kernel is kept for reference)
   const unsigned g = staged ? grid_for(n, 256, 8192) : grid_for(n * (uint64_t)ncols, 256, 16384);
 #define DR_GEN_ROWS(NCV)                                                                              \
   do {                                                                                                \

@@ -1220,7 +1220,8 @@ __global__ __launch_bounds__(256, 4) void ra_agg_kernel(const uint4* __restrict_
 #define DR_RA_BATCH(P)                                                                    \
   {                                                                                       \
     const uint64_t len_ = (uint64_t)plen[P];                                              \
-    const uint4* base_ = rows + (uint64_t)pstart[P] * C;                                  \
+    /* an empty partition (a trailing one starts at n) reads row 0, never past the end */ \
+    const uint4* base_ = len_ ? rows + (uint64_t)pstart[P] * C : rows;                    \
     const uint64_t last_ = len_ ? len_ - 1 : 0;                                           \
     _Pragma("unroll") for (int k = 0; k < kRaPer; ++k) { /* clamped, unconditional */     \
       uint64_t r_ = t + (uint64_t)k * kBlock;                                             \

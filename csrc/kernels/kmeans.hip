@@ -814,13 +814,15 @@ void set_smem(F kern, uint32_t bytes) {
 // Mode chosen for K (exposed for tests/benchmarks): 0 = centroids + slab resident,
 // 1 = streamed centroid tiles + slab, 2 = assignment pass + sliced accumulation,
 // 3 = K <= 64 on bf16 MFMA (split-precision distances with exact re-rank, MFMA one-hot sums).
-int g_km_f32 = -1;   // DRYAD_KM_F32=1: keep the exact-f32 MFMA distance path for every K
+int g_km_f32 = 0;    // dr_kmeans_set_variant: keep the exact-f32 MFMA distance path for every K
+int g_km_mfma16 = 1;  // dr_kmeans_set_variant: 0 = the 32x32 one-workgroup-per-CU kernel (tests)
+
+DR_API void dr_kmeans_set_variant(int f32_only, int mfma16) {
+  g_km_f32 = f32_only ? 1 : 0;
+  g_km_mfma16 = mfma16 ? 1 : 0;
+}
 
 DR_API int dr_kmeans_mode(int K) {
-  if (g_km_f32 < 0) {
-    const char* e = getenv("DRYAD_KM_F32");
-    g_km_f32 = (e && atoi(e) == 1) ? 1 : 0;
-  }
   if (K <= 64 && !g_km_f32) return 3;
   if (step_smem(K, true, true) <= kLdsBudget) return 0;
   if (step_smem(K, false, true) <= kLdsBudget) return 1;
@@ -838,11 +840,7 @@ DR_API int dr_kmeans_step(const float* X, uint64_t n, int d, const float* C, int
   sq_norms_kernel<<<K, 64, 0, s>>>(C, K, cnorm_ws);
   if (n == 0) return 0;
   const int mode = dr_kmeans_mode(K);
-  static int dbg = -1;   // DRYAD_KM_DEBUG: bit0 skip accumulation, bit1 skip distances (profiling only)
-  if (dbg < 0) {
-    const char* e = getenv("DRYAD_KM_DEBUG");
-    dbg = e ? atoi(e) : 0;
-  }
+  constexpr int dbg = 0;     // the kernels' phase-skip bits stay off in the library (no env knob)
   if (mode == 3) {
     // near_ws: [0] = count, then 2 words per listed point (point, estimated centroid); 8 n + 16
     // bytes (dr_kmeans_near_workspace)
@@ -854,12 +852,7 @@ DR_API int dr_kmeans_step(const float* X, uint64_t n, int d, const float* C, int
     uint32_t* near_list = near_cnt + 4;
     kmeans_near_reset<<<1, 64, 0, s>>>(near_cnt);
 #define DR_KM3(KTV, DB) kmeans_mfma_kernel<KTV, DB><<<g3, 256, 0, s>>>(X, n, C, cnorm_ws, K, assign, gsum, gcnt, 256)
-    static int m16 = -1;      // DRYAD_KM_MFMA16=0: the 32x32 one-workgroup-per-CU kernel
-    if (m16 < 0) {
-      const char* e = getenv("DRYAD_KM_MFMA16");
-      m16 = (e && atoi(e) == 0) ? 0 : 1;
-    }
-    if (m16 && dbg == 0) {
+    if (g_km_mfma16) {
       const uint64_t st = (n + kM16Pts - 1) / kM16Pts;
       const uint64_t cap = 2 * (uint64_t)num_cus();
       const unsigned g16 = (unsigned)(st < cap ? st : cap);

@@ -625,6 +625,13 @@ DR_API int dr_seg_reduce(const void* vals, const E128* ent, const int64_t* seg, 
   return 0;
 }
 
+// seg_reduce_multi_serial (one thread walks each chunk of rows) is the default; the variant that
+// reduces each segment across a wave is kept for tests (dr_seg_reduce_set_serial(0)).
+namespace {
+int g_segred_serial = 1;
+}
+DR_API void dr_seg_reduce_set_serial(int on) { g_segred_serial = on ? 1 : 0; }
+
 // Fused multi-aggregate segmented reduce (see seg_reduce_multi_kernel).  ops/vals/outs: host
 // arrays of nagg (<= 8) entries; outputs must be pre-filled with each op's identity.
 // strides: host array of nagg element strides (nullptr = all 1); with ent == nullptr the values
@@ -664,12 +671,7 @@ DR_API int dr_seg_reduce_multi(const E128* ent, const int64_t* seg, uint64_t n, 
     }
     if (packed) sp.rows = reinterpret_cast<const uint64_t*>(base);
   }
-  static int serial = -1;
-  if (serial < 0) {
-    const char* e = getenv("DRYAD_SEGRED_SERIAL");
-    serial = (e && atoi(e) == 0) ? 0 : 1;
-  }
-  if (serial) {
+  if (g_segred_serial) {
     const unsigned g = grid_for(n, 256 * 8, 8192);
 #define DR_SEGRED_CASE(N)                                                             \
       case N:                                                                          \

@@ -276,15 +276,9 @@ void scan_inplace(uint32_t* a, uint32_t M, uint32_t* partial, hipStream_t s) {
   rs_scan_down<<<S, 256, 0, s>>>(a, M, partial);
 }
 
-int g_items = 0;   // 0 = not initialised; set from DRYAD_SORT_ITEMS or dr_sort_set_items
+int g_items = 8;   // items per thread of the radix passes (dr_sort_set_items: 16, measurements only)
 
-inline int sort_items() {
-  if (g_items == 0) {
-    const char* e = getenv("DRYAD_SORT_ITEMS");
-    g_items = (e && atoi(e) == 16) ? 16 : 8;
-  }
-  return g_items;
-}
+inline int sort_items() { return g_items; }
 
 inline void sort_geometry(uint64_t n, uint32_t& G, uint64_t& per_block) {
   const uint64_t tile = (uint64_t)kBlock * sort_items();
@@ -295,14 +289,10 @@ inline void sort_geometry(uint64_t n, uint32_t& G, uint64_t& per_block) {
   per_block = ((tiles + G - 1) / G) * tile;
 }
 
-int g_scatter_v2 = -1;
+int g_scatter_v2 = 1;   // dr_sort_set_scatter_v2(0): the first scatter kernel (tests / A-B only)
 
 void launch_scatter(const E128* in, E128* out, uint64_t n, int shift, const uint32_t* offsets, uint32_t G,
                     uint64_t per_block, hipStream_t s) {
-  if (g_scatter_v2 < 0) {
-    const char* e = getenv("DRYAD_SCATTER_V2");
-    g_scatter_v2 = (e && atoi(e) == 0) ? 0 : 1;
-  }
   if (g_scatter_v2) {
     if (sort_items() == 16)
       rs_scatter_v2<E128, 16><<<G, 256, 0, s>>>(in, out, n, shift, offsets, G, per_block);
@@ -561,14 +551,8 @@ __global__ __launch_bounds__(256) void gather_rows_v4_kernel(const uint8_t* __re
   }
 }
 
-int g_gather_v4 = -1;
-inline bool gather_v4_enabled() {
-  if (g_gather_v4 < 0) {
-    const char* e = getenv("DRYAD_GATHER_V4");
-    g_gather_v4 = (e && atoi(e) == 0) ? 0 : 1;
-  }
-  return g_gather_v4 == 1;
-}
+int g_gather_v4 = 1;   // dr_gather_set_v4(0): the dword gather (tests / A-B only)
+inline bool gather_v4_enabled() { return g_gather_v4 == 1; }
 }  // namespace
 
 DR_API void dr_gather_set_v4(int on) { g_gather_v4 = on ? 1 : 0; }
@@ -963,12 +947,7 @@ DR_API int dr_bucket_scatter_rows(const E128* ent, const uint8_t* rows, uint8_t*
   const uint32_t W = stride / 4;
   const uint32_t* in = reinterpret_cast<const uint32_t*>(rows);
   uint32_t* o = reinterpret_cast<uint32_t*>(out);
-  static int v2 = -1;   // DRYAD_BUCKET_SCATTER_V2=0: the dword-load kernel (A/B measurements)
-  if (v2 < 0) {
-    const char* e = getenv("DRYAD_BUCKET_SCATTER_V2");
-    v2 = (e && atoi(e) == 0) ? 0 : 1;
-  }
-  if (W == 25 && v2 && (((uintptr_t)rows) & 15) == 0)
+  if (W == 25 && (((uintptr_t)rows) & 15) == 0)
     bucket_scatter_rows25_kernel<<<G, 256, 0, s>>>(ent, in, o, n, counts, G, per_block);
   else if (W == 25)
     bucket_scatter_rows_kernel<25><<<G, 256, 0, s>>>(ent, in, o, n, W, counts, G, per_block);
@@ -1480,7 +1459,7 @@ DR_API int dr_extract_keys64(const uint8_t* rows, uint64_t n, uint32_t stride, u
 }
 
 namespace {
-int g_items64 = -1;   // entries per thread per tile of the E64 scatter (8 / 16 / 32)
+int g_items64 = 16;   // entries per thread per tile of the E64 scatter (8 / 16 / 32)
 }
 DR_API void dr_sort64_set_items(int items) { g_items64 = (items == 8 || items == 32) ? items : 16; }
 
@@ -1492,11 +1471,6 @@ DR_API int dr_sort_u64(E64* keys, E64* tmp, uint64_t n, int begin_bit, int end_b
   if (n == 0 || begin_bit >= end_bit) return 0;
   if (end_bit > 64 || begin_bit < 0 || (begin_bit & 7) || (end_bit & 7)) return (int)hipErrorInvalidValue;
   if (n >= (1ull << 32)) return (int)hipErrorInvalidValue;
-  if (g_items64 < 0) {
-    const char* ev = getenv("DRYAD_SORT64_ITEMS");
-    g_items64 = ev ? atoi(ev) : 16;
-    if (g_items64 != 8 && g_items64 != 16 && g_items64 != 32) g_items64 = 16;
-  }
   const int ITEMS = g_items64;
   const uint64_t tile = (uint64_t)kBlock * ITEMS;
   uint64_t tiles = (n + tile - 1) / tile;

@@ -108,6 +108,8 @@ _DEFAULTS = dict(
     FaultInjection=None,          # [{stage, partition, version, kind}] (SURVEY §5.3 FaultInjector)
     HbmBudgetBytes=None,          # HBM an out-of-core operator may use per GPU (None: 80% of free HBM)
     ExternalSort=None,            # out-of-core OrderBy to host:// (None: when the data exceeds the budget)
+    AllowHostFallback=False,      # GPU executor: an op whose lambdas do not trace may run on host
+    HostFallbackMaxBytes=256 << 20,  # ... records only up to this many partition bytes unless allowed
     ExternalSortToDisk=None,      # its partfile:// output written through a memory-mapped part file
     #                               (None: when the output exceeds half of the available host memory)
 )
@@ -154,7 +156,7 @@ class DryadLinqContext:
     def __setattr__(self, name, value):
         if name in self._props or name in _DEFAULTS:
             if self._frozen and name in _READONLY_AFTER_USE:
-                raise DryadLinqException(0, f"DryadLinqContext.{name} cannot be changed after the context was used")
+                raise DryadLinqException(ErrorCode.Unspecified, f"DryadLinqContext.{name} cannot be changed after the context was used")
             self._props[name] = value
         else:
             object.__setattr__(self, name, value)
@@ -254,7 +256,7 @@ class DryadLinqContext:
         uri = node.args["uri"]
         p = provider_for(uri)
         if p.exists(uri) and not node.args.get("delete_if_exists") and not node.args.get("_temp"):
-            raise DryadLinqException(0, f"can't output to existing table {uri}")
+            raise DryadLinqException(ErrorCode.StreamAlreadyExists, f"can't output to existing table {uri}")
         dtype = node.dtype or (T.infer_common_type(data[:1000]) if data else T.Int32)
         node.dtype = dtype
         p.write_table(uri, [data], dtype)
@@ -275,7 +277,7 @@ class DryadLinqContext:
             return LocalEvaluator(self).eval(q.node)[0]
         res = self._get_executor().enumerate(q)
         if len(res) != 1:
-            raise DryadLinqException(0, f"scalar query produced {len(res)} records")
+            raise DryadLinqException(ErrorCode.SingleMoreThanOneElement, f"scalar query produced {len(res)} records")
         return res[0]
 
     def _new_handle(self) -> JobHandle:

@@ -22,8 +22,15 @@ from .errors import DryadLinqException, ErrorCode
 
 
 class InvalidOperationException(DryadLinqException):
-    def __init__(self, msg):
-        super().__init__(0, msg)
+    """LINQ's InvalidOperationException for empty / ambiguous sequences, carrying the vertex
+    runtime code the reference reports for the same condition (DryadLinqFaultCodes.cs:140-166)."""
+
+    def __init__(self, msg, code=None):
+        if code is None:
+            m = msg.lower()
+            code = (ErrorCode.SingleMoreThanOneElement if "more than one" in m else
+                    ErrorCode.FirstNoElementsFirst if "matching" in m else ErrorCode.AggregateNoElements)
+        super().__init__(code, msg)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -522,7 +529,7 @@ def ApplyWithPartitionIndex(src, func):
 
 def SlidingWindow(src, func, window_size):
     if window_size < 2:
-        raise DryadLinqException(ErrorCode.Unknown if hasattr(ErrorCode, "Unknown") else 0,
+        raise DryadLinqException(ErrorCode.Unspecified,  # SR.WindowSizeMustyBeGTOne (message-only ctor)
                                  "windowSize must be at least 2")
     win = deque(maxlen=window_size)
     for x in src:
@@ -547,7 +554,7 @@ def Fork(src, mapper, keys=None):
     outs = None
     for t in mapper(src):
         if not isinstance(t, ForkTuple):
-            raise DryadLinqException(0, "Fork mapper must yield ForkTuple values")
+            raise DryadLinqException(ErrorCode.FailureInUserApplyFunction, "Fork mapper must yield ForkTuple values")
         vals = (t.First, t.Second, t.Third)
         if outs is None:
             outs = [[], [], []]

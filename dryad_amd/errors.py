@@ -167,6 +167,9 @@ _TABLE = {
     'CreatingDscDataFromLocalDebugFailed': ('LocalDebug', 0),
     'UnknownError': ('Unknown', 0),
 }
+# The reference's message-only ``DryadLinqException(string)`` constructor leaves the code at 0
+# (DryadLinqException.cs:42); raise sites that mirror such a throw use ErrorCode.Unspecified.
+_UNSPECIFIED = 0
 
 
 class _Codes:
@@ -175,6 +178,7 @@ class _Codes:
     def __init__(self):
         for name, (cat, off) in _TABLE.items():
             setattr(self, name, CATEGORY_BASE[cat] + off)
+        self.Unspecified = _UNSPECIFIED
 
     def name_of(self, code: int) -> str:
         for name, (cat, off) in _TABLE.items():

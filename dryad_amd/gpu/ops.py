@@ -1147,7 +1147,8 @@ def op_aggregate_seq(op, inputs, v):
     (reference: DryadLinqQueryGen Aggregate without [Associative] runs as one vertex folding the
     whole input, DryadLinqQueryGen.cs:3384-3395).  When ``func`` traces to ``acc + T(x)`` the fold
     is ``seed + sum(T(x))``: one device reduction instead of a host loop over every record.
-    Integer folds are exact; float folds are re-associated like the device ``Sum``.  Without a
+    Integer folds are exact (a fold that could leave the int64 range, judged from the column's
+    min / max, runs on the host with Python ints); float folds are re-associated like ``Sum``.  Without a
     seed the first record seeds the fold (scalar records only)."""
     from ..ops import reduce as RD
     from ..query import _NOSEED
@@ -1185,6 +1186,13 @@ def op_aggregate_seq(op, inputs, v):
             raise NotTraceable("Aggregate term is not a scalar field")
         if col.dtype == torch.bool:
             col = col.to(torch.int64)
+        if not col.is_floating_point():
+            # the host fold uses Python ints: refuse a device sum that could wrap past int64
+            mn, mx = RD.reduce_multi(rows.n, [(RD.MIN, col.contiguous(), None), (RD.MAX, col.contiguous(), None)],
+                                     t.device)
+            lim = (1 << 63) - 1 - abs(int(seed))
+            if max(abs(int(mn)), abs(int(mx))) * rows.n > lim:
+                raise NotTraceable("integer Aggregate could overflow int64 on the device")
         acc = seed + RD.reduce_multi(rows.n, [(RD.SUM, col.contiguous(), None)], t.device)[0]
     r = s.get("result_selector")
     return [r(acc) if r else acc]

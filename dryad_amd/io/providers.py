@@ -62,8 +62,7 @@ class DataProvider:
     def check_existence(self, uri, delete_if_exists: bool):
         if self.exists(uri):
             if not delete_if_exists:
-                raise DryadLinqException(ErrorCode.OutputUriAlreadyExists if hasattr(ErrorCode, "OutputUriAlreadyExists")
-                                         else 0, f"can't output to existing table {uri}")
+                raise DryadLinqException(ErrorCode.StreamAlreadyExists, f"can't output to existing table {uri}")
             self.delete(uri)
 
     def delete(self, uri):
@@ -121,6 +120,12 @@ class PartfileProvider(DataProvider):
         if sch is not None and sch.get("format") == "pickle":
             import gzip
             import pickle
+            from ..runtime.jobmanager import pickled_table_trusted
+            if not pickled_table_trusted(self._path(uri)):
+                raise DryadLinqException(
+                    ErrorCode.FailedToDeserialize,
+                    f"{uri} holds pickled records written by another process; loading them would run "
+                    "code from the file (set DRYAD_TRUST_PICKLED_TABLES=1 to allow it)")
             if data[:2] == b"\x1f\x8b":
                 data = gzip.decompress(data)
             return pickle.loads(data) if data else []
@@ -205,7 +210,7 @@ class MemProvider(DataProvider):
     def stream_info(self, uri):
         t = _MEM.tables.get(self._name(uri))
         if t is None:
-            raise DryadLinqException(0, f"no such table {uri}")
+            raise DryadLinqException(ErrorCode.StreamDoesNotExist, f"no such table {uri}")
         return len(t[1]), sum(len(p) for p in t[1])
 
     def exists(self, uri):
@@ -237,7 +242,7 @@ class HbmProvider(DataProvider):
     def stream_info(self, uri):
         t = self.tables.get(self._name(uri))
         if t is None:
-            raise DryadLinqException(0, f"no such HBM table {uri}")
+            raise DryadLinqException(ErrorCode.StreamDoesNotExist, f"no such HBM table {uri}")
         return t["partitions"], t.get("bytes", 0)
 
     def exists(self, uri):
@@ -257,14 +262,14 @@ class HbmProvider(DataProvider):
     def get(self, uri) -> dict:
         t = self.tables.get(self._name(uri))
         if t is None:
-            raise DryadLinqException(0, f"no such HBM table {uri}")
+            raise DryadLinqException(ErrorCode.StreamDoesNotExist, f"no such HBM table {uri}")
         return t
 
     def read_partition(self, uri, i, dtype):
         t = self.get(uri)
         b = t["local"].get(i)
         if b is None:
-            raise DryadLinqException(0, f"partition {i} of {uri} is not resident on this rank")
+            raise DryadLinqException(ErrorCode.FailedToGetReadPathsForStream, f"partition {i} of {uri} is not resident on this rank")
         return b.to_objects() if hasattr(b, "to_objects") else list(b)
 
     def write_table(self, uri, partitions, dtype, delete_if_exists=True):
@@ -307,7 +312,7 @@ class HostProvider(DataProvider):
     def get(self, uri) -> dict:
         t = self.tables.get(self._name(uri))
         if t is None:
-            raise DryadLinqException(0, f"no such host table {uri}")
+            raise DryadLinqException(ErrorCode.StreamDoesNotExist, f"no such host table {uri}")
         return t
 
     def local_rows(self, uri, i):
@@ -319,7 +324,7 @@ class HostProvider(DataProvider):
     def read_partition(self, uri, i, dtype):
         b = self.get(uri)["local"].get(i)
         if b is None:
-            raise DryadLinqException(0, f"partition {i} of {uri} is not resident in this process")
+            raise DryadLinqException(ErrorCode.FailedToGetReadPathsForStream, f"partition {i} of {uri} is not resident in this process")
         return b.to_objects() if hasattr(b, "to_objects") else list(b)
 
     def write_table(self, uri, partitions, dtype, delete_if_exists=True):
@@ -370,7 +375,7 @@ class GenProvider(DataProvider):
         return {"dtype": dt}
 
     def delete(self, uri):
-        raise DryadLinqException(0, "generator stores are read-only")
+        raise DryadLinqException(ErrorCode.AttemptToReadFromAWriteStream, "generator stores are read-only")
 
     def bounds(self, uri, i):
         kind, q = self._args(uri)
@@ -399,7 +404,7 @@ class GenProvider(DataProvider):
         raise DryadLinqException(ErrorCode.UnrecognizedDataSource, f"unknown generator {kind}")
 
     def temp_uri(self, name):
-        raise DryadLinqException(0, "generator stores are read-only")
+        raise DryadLinqException(ErrorCode.AttemptToReadFromAWriteStream, "generator stores are read-only")
 
 
 class TextProvider(DataProvider):

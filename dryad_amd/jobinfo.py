@@ -75,11 +75,9 @@ class DryadLinqJobInfo:
     def Wait(self, timeout: float | None = None):
         for h in self._handles:
             if not h.wait(timeout):
-                raise DryadLinqJobException(ErrorCode.JobStatusQueryError if hasattr(ErrorCode, "JobStatusQueryError")
-                                            else 0, f"timed out waiting for job {h.job_id}")
+                raise DryadLinqJobException(ErrorCode.JobStatusQueryError, f"timed out waiting for job {h.job_id}")
             if h.status != JobStatus.Success:
-                raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed if hasattr(ErrorCode, "JobToCreateTableFailed")
-                                            else 0, f"job {h.job_id} {h.status.name}: {h.error}", inner=h.error)
+                raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed, f"job {h.job_id} {h.status.name}: {h.error}", inner=h.error)
         return self
 
     def CancelJob(self):

@@ -25,8 +25,9 @@ Per rank (one process per GPU, W ranks):
                  place; the next bucket's upload and the previous bucket's download overlap the
                  sort (two copy streams, both PCIe directions busy)                     [HIP + DMA]
 
-Equal keys are split across buckets (and ranks) by a (chunk, rank, row) tie tag in the spare entry
-bits, so skewed keys still fit; the order is then the source order, i.e. the sort is stable.  With
+Equal keys are split across buckets (and ranks) by a (rank, chunk, row) tie tag in the spare entry
+bits, so skewed keys still fit; the order is then the source order (rank 0's rows first, each rank
+in row order), i.e. the sort is stable.  With
 ``keep_ties`` the rank boundaries keep every run of equal keys on one rank (the planner's
 partitioned-by-key guarantee, DataSetInfo), only the buckets inside a rank split them.
 """
@@ -139,16 +140,19 @@ class MappedRowsSource(ChunkSource):
         self.mm, self.n, self.stride = mm, mm.shape[0], mm.shape[1]
         self.key_spec = (key_off, key_len or self.stride)
         self._stage = None
+        self._last = None                      # stream of the last DMA out of the staging buffer
 
     def fill(self, lo, hi, out, copy_stream):
+        if self._last is not None:
+            self._last.synchronize()           # the previous chunk has left the staging buffer
         if self._stage is None or self._stage.n < hi - lo:
             if self._stage is not None:
                 self._stage.release()
             self._stage = HostRows(hi - lo, self.stride)
-        if copy_stream is not None:
-            copy_stream.synchronize()          # the previous chunk has left the staging buffer
         self._stage.rows[: hi - lo].numpy()[:] = self.mm[lo:hi]
-        _copy(out[: hi - lo], self._stage.rows[: hi - lo], copy_stream)
+        st = copy_stream if copy_stream is not None else torch.cuda.current_stream(out.device)
+        _copy(out[: hi - lo], self._stage.rows[: hi - lo], st)
+        self._last = st
         return copy_stream
 
     def sample_rows(self, idx, scratch, chunk_rows):
@@ -279,7 +283,7 @@ def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | N
     arena = _Arena(budget, dev)
     comp = torch.cuda.current_stream(dev)
     h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    tag_of = lambda c: ((c * W + me) << 32)  # noqa: E731
+    tag_of = lambda c: ((me * C + c) << 32)  # noqa: E731  (rank-major: the global source order)
 
     # ---------------------------------------------------------------- 0. sample + separators
     t0 = time.perf_counter()
@@ -297,7 +301,7 @@ def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | N
         samp = S.extract_keys(srows.contiguous(), key_off, key_len, 0)
         if split:
             c_idx = idx // chunk_rows
-            tag = ((c_idx * W + me) << 32) | (idx - c_idx * chunk_rows)
+            tag = ((me * C + c_idx) << 32) | (idx - c_idx * chunk_rows)
             samp[:, 0] = (samp[:, 0] & _i64(lo_key_mask)) | tag.to(dev)
         samp[:, 0] &= _i64(part_mask)
     else:

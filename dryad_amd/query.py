@@ -96,14 +96,12 @@ class Query:
 
     def _q(self, op, sources=None, dtype=None, **args) -> "Query":
         srcs = [self._node] + [s._node if isinstance(s, Query) else s for s in (sources or [])]
-        for s in srcs:
-            pass
         return Query(self._ctx, QNode(op, srcs, args, dtype))
 
     def _other(self, other) -> QNode:
         if isinstance(other, Query):
             if other._ctx is not self._ctx and not self._ctx._compatible(other._ctx):
-                raise DryadLinqException(ErrorCode.Unknown if False else 0,
+                raise DryadLinqException(ErrorCode.MustStartFromContext,
                                          "queries from different DryadLinqContexts cannot be combined")
             return other._node
         # a plain Python iterable: lift it
@@ -129,7 +127,7 @@ class Query:
         for x in self:
             k = key_selector(x)
             if k in out:
-                raise DryadLinqException(0, f"duplicate key {k!r}")
+                raise DryadLinqException(ErrorCode.TooManyItems, f"duplicate key {k!r}")
             out[k] = element_selector(x) if element_selector else x
         return out
 
@@ -427,7 +425,7 @@ class Query:
 
     def SlidingWindow(self, func, window_size: int):
         if window_size < 2:
-            raise DryadLinqException(0, "SlidingWindow requires windowSize >= 2")
+            raise DryadLinqException(ErrorCode.Unspecified, "SlidingWindow requires windowSize >= 2")  # SR.WindowSizeMustyBeGTOne
         return self._q("SlidingWindow", func=func, window_size=int(window_size))
 
     def DoWhile(self, body: Callable, cond: Callable, checkpoint: str | None = None) -> "Query":
@@ -533,8 +531,8 @@ def _check_separators(seps, comparer, descending):
     for a, b in zip(seps, seps[1:]):
         c = cmp(a, b)
         if (c > 0 and not descending) or (c < 0 and descending):
-            raise DryadLinqException(ErrorCode.RangePartitionKeysMissing if hasattr(ErrorCode, "RangePartitionKeysMissing")
-                                     else 0, "range separators are not sorted in the partition order")
+            raise DryadLinqException(ErrorCode.PartitionKeysAreNotConsistentlyOrdered,
+                                     "range separators are not sorted in the partition order")
 
 
 # snake_case aliases for every public operator

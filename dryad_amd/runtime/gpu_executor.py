@@ -77,6 +77,17 @@ def _object_bytes(x) -> int:
     return x.nbytes if isinstance(x, DeviceTable) else 0
 
 
+def _device_bytes(x) -> int:
+    """HBM bytes behind a vertex input (tables, their string heaps, multi-port outputs)."""
+    if isinstance(x, DeviceTable):
+        return x.nbytes + (x.heap.numel() if x.heap is not None else 0) + sum(h.numel() for h in x.strs.values())
+    if isinstance(x, Ported):
+        return _device_bytes(x.table)
+    if isinstance(x, PortTables):
+        return sum(_device_bytes(t) for t in x.tables)
+    return 0
+
+
 class GpuJobRunner:
     def __init__(self, ctx, plan, world: World, faults=None, pool=None):
         self.ctx, self.plan, self.world = ctx, plan, world
@@ -506,7 +517,7 @@ class GpuJobRunner:
         shuffle.alltoallv_bytes(send.reshape(-1), [c * row_bytes for c in send_counts], recv.reshape(-1),
                                 [c * row_bytes for c in recv_counts], self.world)
         if proto is None:
-            raise DryadLinqException(0, "rank without source partitions in a device shuffle")
+            raise DryadLinqException(ErrorCode.Internal, "rank without source partitions in a device shuffle")
         # unpack into per-(q, p) slices
         out = {p: [None] * P_src for p in local_dst}
         off = 0
@@ -560,12 +571,26 @@ class GpuJobRunner:
             try:
                 return fn(op, [a for a in args] if args else [], vctx)
             except NotTraceable as e:
-                self.fallbacks.append((s.name, name, str(e)))
+                self._fallback(s, name, str(e), args)
         elif fn is None or not self.gpu_ok:
-            self.fallbacks.append((s.name, name, "host op"))
+            self._fallback(s, name, "host op", args)
         objs = [(_to_objects(a) if not isinstance(a, list) else a) if a is not None else [] for a in args]
         out = V.OPS[name](op, objs, vctx)
         return self._maybe_device(out, s, name)
+
+    def _fallback(self, s, name, why, args):
+        """Record a host fallback; refuse one that would pull more than HostFallbackMaxBytes of
+        device data into Python objects (a silent cliff on a 100 GB partition) unless the context
+        allows it (AllowHostFallback)."""
+        nb = sum(_device_bytes(a) for a in args)
+        self.fallbacks.append((s.name, name, why))
+        props = self.ctx._props
+        if self.gpu_ok and nb > int(props.get("HostFallbackMaxBytes") or 0) and not props.get("AllowHostFallback"):
+            raise DryadLinqException(
+                ErrorCode.OperatorNotSupported,
+                f"{s.name}: operator {name} cannot run on the device ({why}) and its host fallback would move "
+                f"{nb / 1e6:.1f} MB of HBM data into Python objects (> HostFallbackMaxBytes); set "
+                f"AllowHostFallback=True to run it on the host anyway")
 
     def _maybe_device(self, out, s, opname):
         """Host op result -> device table when the records are columnar (keeps later ops on GPU)."""

@@ -11,7 +11,6 @@ from __future__ import annotations
 
 import json
 import os
-import pickle
 import shutil
 import threading
 import time
@@ -80,7 +79,7 @@ class JobRunner:
                         pairs = [(self.vids[si.src][q], si.port)
                                  for q in range(p * si.group, min(src_stage.partitions, (p + 1) * si.group))]
                     else:
-                        raise DryadLinqException(0, f"unknown connection {si.kind}")
+                        raise DryadLinqException(ErrorCode.Internal, f"unknown connection {si.kind}")
                     for src, port in pairs:
                         g.add_edge(src, port, dst, ii)
                         lst.append((src, port, edge_count))
@@ -288,12 +287,28 @@ def schema_path(meta_path: str) -> str:
     return meta_path + ".dryadtype"
 
 
+_TRUSTED_PICKLED: set = set()
+
+
+def pickled_table_trusted(meta_path: str) -> bool:
+    """Opaque-record ("pickle" format) tables are only decoded when this process wrote them (the
+    object executor's own temporaries) or the user opted in with DRYAD_TRUST_PICKLED_TABLES=1."""
+    return os.path.abspath(meta_path) in _TRUSTED_PICKLED or os.environ.get("DRYAD_TRUST_PICKLED_TABLES") == "1"
+
+
 def write_schema(meta_path: str, dtype, fmt: str, **extra):
     """Sidecar of a partfile table: record type and part format ("binary" DryadLinqBinary records,
-    "pickle", or "rows" = raw fixed-width rows with ``stride`` / ``key_off`` / ``key_len``)."""
-    import cloudpickle
-    with open(schema_path(meta_path), "wb") as f:
-        cloudpickle.dump({"dtype": dtype, "format": fmt, **extra}, f)
+    "pickle", or "rows" = raw fixed-width rows with ``stride`` / ``key_off`` / ``key_len``).
+    Declarative JSON (types.dtype_to_json), so reading a foreign table's schema executes nothing;
+    a type without a descriptor is stored as ``null`` (readers then infer from the records)."""
+    try:
+        d = T.dtype_to_json(dtype)
+    except TypeError:
+        d = None
+    if fmt == "pickle":
+        _TRUSTED_PICKLED.add(os.path.abspath(meta_path))
+    with open(schema_path(meta_path), "w") as f:
+        json.dump({"dtype": d, "format": fmt, **extra}, f)
 
 
 def read_schema(meta_path: str):
@@ -301,4 +316,11 @@ def read_schema(meta_path: str):
     if not os.path.exists(p):
         return None
     with open(p, "rb") as f:
-        return pickle.load(f)
+        raw = f.read()
+    try:
+        d = json.loads(raw.decode("utf-8"))
+    except (UnicodeDecodeError, ValueError):
+        log.warning("ignoring non-JSON schema sidecar %s (older pickled format is not loaded)", p)
+        return None
+    d["dtype"] = T.dtype_from_json(d.get("dtype"))
+    return d

@@ -415,3 +415,67 @@ def infer_common_type(values) -> DType:
             if t is None:
                 return Pickle
     return t or Int32
+
+
+# ---------------------------------------------------------------------------------------------
+# Declarative type descriptors (the ``.dryadtype`` sidecar of a partfile table).  Plain JSON, like
+# the reference's plain-text partfile metadata: reading a table's schema never runs code.  A
+# record's Python class is looked up by ``module:qualname`` among modules already imported by the
+# reader (never imported on its behalf); an unknown class reads back as tuple records.
+def dtype_to_json(dt):
+    if dt is None:
+        return None
+    if isinstance(dt, _Prim) or dt is LineRecordT:
+        return {"t": dt.name}
+    if isinstance(dt, Nullable):
+        return {"t": "Nullable", "inner": dtype_to_json(dt.inner)}
+    if isinstance(dt, VectorT):
+        return {"t": "Vector", "elem": dtype_to_json(dt.elem), "dim": dt.dim}
+    if isinstance(dt, ArrayT):
+        return {"t": "Array", "elem": dtype_to_json(dt.elem)}
+    if isinstance(dt, RecordT):
+        py = None
+        if dt.pytype is tuple or dt.pytype is None:
+            py = "tuple"
+        else:
+            py = f"{dt.pytype.__module__}:{dt.pytype.__qualname__}"
+        return {"t": "Record", "fields": [[n, dtype_to_json(t)] for n, t in dt.fields],
+                "nullable": sorted(dt.nullable_fields), "pytype": py}
+    if isinstance(dt, PickleT):
+        return {"t": "Pickle"}
+    raise TypeError(f"no declarative descriptor for {dt!r}")
+
+
+def _lookup_class(spec: str):
+    import sys
+    mod, _, qual = spec.partition(":")
+    obj = sys.modules.get(mod)
+    for part in qual.split("."):
+        if obj is None or part == "<locals>":
+            return None
+        obj = getattr(obj, part, None)
+    return obj if isinstance(obj, type) else None
+
+
+def dtype_from_json(o):
+    if o is None:
+        return None
+    t = o["t"]
+    if t in PRIMITIVES:
+        return PRIMITIVES[t]
+    if t == "Nullable":
+        return Nullable(dtype_from_json(o["inner"]))
+    if t == "Vector":
+        return VectorT(dtype_from_json(o["elem"]), int(o["dim"]))
+    if t == "Array":
+        return ArrayT(dtype_from_json(o["elem"]))
+    if t == "Record":
+        py = o.get("pytype")
+        cls = tuple if py in (None, "tuple") else _lookup_class(py)
+        fields = [(n, dtype_from_json(x)) for n, x in o["fields"]]
+        if cls is None or (cls is not tuple and not dataclasses.is_dataclass(cls)):
+            cls = tuple
+        return RecordT(fields, cls, set(o.get("nullable") or ()))
+    if t == "Pickle":
+        return Pickle
+    raise ValueError(f"unknown type descriptor {t!r}")

@@ -207,3 +207,35 @@ def test_row_record_byte_index_on_device():
           device_ops=("where", "select"))
     _same(lambda c: c.FromStore(src).OrderBy(lambda r: r[3] * 256 + r[4]).Select(lambda r: r[0:10]), ordered=False,
           device_ops=("sort",))
+
+
+def test_host_fallback_refused_past_limit():
+    """A non-traceable operator over more than HostFallbackMaxBytes of HBM data is refused with a
+    real error code instead of silently pulling the partition into Python objects."""
+    from dryad_amd.errors import DryadLinqException, ErrorCode
+    data = list(range(20_000))
+    c = _ctx()
+    c.HostFallbackMaxBytes = 1024
+    with pytest.raises(DryadLinqException) as ei:
+        c.FromEnumerable(data).Aggregate(1, lambda a, x: (a * 31 + x) % 1_000_003)
+    assert ei.value.error_code == ErrorCode.OperatorNotSupported
+    c2 = _ctx()
+    c2.HostFallbackMaxBytes = 1024
+    c2.AllowHostFallback = True
+    exp = _local().FromEnumerable(data).Aggregate(1, lambda a, x: (a * 31 + x) % 1_000_003)
+    assert c2.FromEnumerable(data).Aggregate(1, lambda a, x: (a * 31 + x) % 1_000_003) == exp
+    assert "aggregate_seq" in _fallback_ops(c2) or _fallback_ops(c2)
+
+
+def test_additive_aggregate_overflow_goes_to_host():
+    """acc + x folds run as one device sum unless the int64 sum could wrap (then the exact host fold)."""
+    big = [2**61 + i for i in range(16)]
+    c = _ctx()
+    c.AllowHostFallback = True
+    got = c.FromEnumerable(big).Aggregate(0, lambda a, x: a + x)
+    assert got == sum(big)
+    assert _fallback_ops(c)
+    small = list(range(100_000))
+    c2 = _ctx()
+    assert c2.FromEnumerable(small).Aggregate(7, lambda a, x: a + x) == 7 + sum(small)
+    assert not _fallback_ops(c2)

@@ -62,6 +62,20 @@ def test_radix_aggregate_one_value_16_byte_rows_and_narrow_key():
     _check(k, specs, RA.radix_aggregate(k, specs, force=True))
 
 
+def test_radix_aggregate_few_keys_many_empty_partitions():
+    """~10 distinct keys: almost every radix partition, the trailing ones included, is empty
+    (ra_agg_kernel's prefetch of an empty partition must stay inside the row buffer)."""
+    from dryad_amd.ops import radixagg as RA
+    g = torch.Generator(device="cuda").manual_seed(5)
+    k = torch.randint(0, 10, (1_000_000,), device="cuda", generator=g) * (1 << 40)
+    v = torch.randint(-2**40, 2**40, (1_000_000,), device="cuda", generator=g)
+    specs = [("count", None, I64), ("sum", v, I64), ("max", v, I64)]
+    _check(k, specs, RA.radix_aggregate(k, specs, force=True))
+    _check(k[:1000], [(o, None if x is None else x[:1000], d) for o, x, d in specs],
+           RA.radix_aggregate(k[:1000], [(o, None if x is None else x[:1000], d) for o, x, d in specs],
+                              force=True))
+
+
 def test_radix_aggregate_float():
     from dryad_amd.ops import radixagg as RA
     g = torch.Generator(device="cuda").manual_seed(11)

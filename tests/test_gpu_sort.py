@@ -301,7 +301,8 @@ def test_seg_reduce_multi_variants_agree(serial, monkeypatch):
     import subprocess, sys, os
     code = (
         "import torch\n"
-        "from dryad_amd.ops import relational as R\n"
+        "from dryad_amd.ops import relational as R, _lib\n"
+        f"_lib.lib().dr_seg_reduce_set_serial({int(serial)})\n"
         "torch.manual_seed(1)\n"
         "for n, nk in ((1, 1), (511, 3), (513, 600), (4097, 2), (1_000_003, 50), (2_000_000, 1_500_000)):\n"
         "    k = torch.sort(torch.randint(0, nk, (n,), device='cuda'))[0]\n"
@@ -315,7 +316,7 @@ def test_seg_reduce_multi_variants_agree(serial, monkeypatch):
         "    assert torch.equal(mn, torch.full((nseg,), 2**62, device='cuda').scatter_reduce(0, seg, vi, 'amin'))\n"
         "    assert torch.equal(mxf, torch.full((nseg,), -1e300, dtype=torch.float64, device='cuda').scatter_reduce(0, seg, vf, 'amax'))\n"
         "print('OK')\n")
-    env = dict(os.environ, DRYAD_SEGRED_SERIAL=serial)
+    env = dict(os.environ)
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300,
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert out.returncode == 0 and "OK" in out.stdout, out.stderr[-3000:]
