@@ -1,0 +1,250 @@
+// Channel kernels: the send side of a hash / range shuffle between GPUs, for columnar tables.
+//
+// A Dryad CrossProduct channel (GraphBuilder.cs:481-504, DryadLinqVertex.cs:4788-4907
+// HashPartition) becomes: destination of every record (stable_hash_dest / range_dest, one E128
+// entry per row with the port in the low byte of .hi), then ONE pass that moves every column of
+// the table into port-grouped order, then one RCCL all-to-all-v per column (parallel/exchange.py).
+// The grouped table is both the local output ports and the send buffer: when the ports are
+// numbered rank-major (the LUT below), the rows for destination rank r are one contiguous slice of
+// every column, so nothing is packed again per destination.
+//
+//   pc_count_kernel    per-(bucket, workgroup) histogram of the (LUT-mapped) ports
+//   pc_scatter_kernel  stable multi-column bucket scatter: each 512-row tile is ranked by bucket
+//                      with wave64 ballot multisplits, then every column is staged through LDS
+//                      (coalesced loads) and written as one contiguous run per bucket
+//   copy_segments      variable-length string bytes into a compact heap in row order (the string
+//                      heap of the rows sent to each rank, sent by a second all-to-all-v)
+#include "common.h"
+
+namespace {
+constexpr int kPcTile = 512;
+constexpr int kPcItems = kPcTile / kBlock;   // rows ranked per thread per tile
+constexpr int kPcMaxCols = 16;
+constexpr int kPcChunk = 8;                  // dwords per row staged per column pass
+
+struct PcCols {
+  const uint8_t* in[kPcMaxCols];
+  uint8_t* out[kPcMaxCols];
+  uint32_t width[kPcMaxCols];   // bytes per row: 1, 2 or a multiple of 4
+  uint32_t ncols;
+};
+
+__global__ __launch_bounds__(256) void pc_count_kernel(const E128* __restrict__ ent, uint64_t n,
+                                                       const uint8_t* __restrict__ lut, uint32_t* __restrict__ counts,
+                                                       uint32_t G, uint64_t per_block) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint8_t slut[256];
+  const int t = threadIdx.x;
+  hist[t] = 0;
+  slut[t] = lut ? lut[t] : (uint8_t)t;
+  __syncthreads();
+  const uint64_t beg = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  for (uint64_t i = beg + t; i < end; i += kBlock) atomicAdd(&hist[slut[ent[i].hi & 0xFF]], 1u);
+  __syncthreads();
+  counts[(uint64_t)t * G + blockIdx.x] = hist[t];
+}
+
+__device__ __forceinline__ uint32_t pc_load_narrow(const uint8_t* p, uint64_t row, uint32_t w) {
+  return w == 1 ? (uint32_t)p[row] : (uint32_t)reinterpret_cast<const uint16_t*>(p)[row];
+}
+
+__device__ __forceinline__ void pc_store_narrow(uint8_t* p, uint64_t row, uint32_t w, uint32_t v) {
+  if (w == 1) p[row] = (uint8_t)v;
+  else reinterpret_cast<uint16_t*>(p)[row] = (uint16_t)v;
+}
+
+__global__ __launch_bounds__(256) void pc_scatter_kernel(const E128* __restrict__ ent, uint64_t n,
+                                                         const uint8_t* __restrict__ lut, PcCols cols,
+                                                         const int64_t* __restrict__ offsets, uint32_t G,
+                                                         uint64_t per_block) {
+  __shared__ uint32_t buf[kPcTile * kPcChunk];
+  __shared__ uint16_t perm[kPcTile];
+  __shared__ uint8_t dslot[kPcTile];
+  __shared__ uint32_t wcnt[4][256];
+  __shared__ int64_t goff[256];
+  __shared__ uint32_t bstart[256];
+  __shared__ uint32_t sc[4];
+  __shared__ uint8_t slut[256];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const uint64_t beg = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  if (beg >= end) return;                                    // uniform: the whole workgroup leaves
+  slut[t] = lut ? lut[t] : (uint8_t)t;
+  goff[t] = offsets[(uint64_t)t * G + blockIdx.x];
+  __syncthreads();
+  for (uint64_t base = beg; base < end; base += kPcTile) {
+    const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kPcTile ? (end - base) : kPcTile);
+    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    __syncthreads();
+    uint32_t rk[kPcItems], dg[kPcItems];
+#pragma unroll
+    for (int r = 0; r < kPcItems; ++r) {
+      const uint32_t pos = w * (kPcTile / 4) + r * 64 + l;
+      const bool valid = pos < cnt;
+      const uint32_t d = valid ? (uint32_t)slut[ent[base + pos].hi & 0xFF] : 0u;
+      uint64_t peers = ballot64(valid);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool bit = (d >> k) & 1u;
+        const uint64_t b = ballot64(bit);
+        peers &= bit ? b : ~b;
+      }
+      const uint32_t below = popc_below(peers);
+      const uint32_t prior = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      rk[r] = prior + below;
+      dg[r] = d;
+    }
+    __syncthreads();
+    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
+    uint32_t all;
+    bstart[t] = block_exclusive_scan256(tot, sc, all);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kPcItems; ++r) {
+      const uint32_t pos = w * (kPcTile / 4) + r * 64 + l;
+      if (pos < cnt) {
+        const uint32_t slot = bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
+        perm[slot] = (uint16_t)pos;
+        dslot[slot] = (uint8_t)dg[r];
+      }
+    }
+    __syncthreads();
+    // every column through LDS: coalesced tile loads, then slot-major stores (consecutive slots of
+    // one bucket are consecutive output rows)
+    for (uint32_t k = 0; k < cols.ncols; ++k) {
+      const uint32_t wb = cols.width[k];
+      const uint8_t* src = cols.in[k];
+      uint8_t* dst = cols.out[k];
+      if (wb < 4) {
+        for (uint32_t j = t; j < cnt; j += kBlock) buf[j] = pc_load_narrow(src, base + j, wb);
+        __syncthreads();
+        for (uint32_t j = t; j < cnt; j += kBlock) {
+          const uint32_t d = dslot[j];
+          pc_store_narrow(dst, (uint64_t)(goff[d] + (int64_t)(j - bstart[d])), wb, buf[perm[j]]);
+        }
+        __syncthreads();
+        continue;
+      }
+      const uint32_t wpr = wb >> 2;
+      const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+      uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+      for (uint32_t cw0 = 0; cw0 < wpr; cw0 += kPcChunk) {
+        const uint32_t cw = wpr - cw0 < (uint32_t)kPcChunk ? wpr - cw0 : (uint32_t)kPcChunk;
+        const uint32_t words = cnt * cw;
+        if (cw == 1) {
+          for (uint32_t q = t; q < words; q += kBlock) buf[q] = s32[(base + q) * wpr + cw0];
+        } else if (cw == 2) {
+          for (uint32_t q = t; q < words; q += kBlock) buf[q] = s32[(base + (q >> 1)) * wpr + cw0 + (q & 1)];
+        } else {
+          for (uint32_t q = t; q < words; q += kBlock) {
+            const uint32_t r = q / cw, c = q - r * cw;
+            buf[q] = s32[(base + r) * wpr + cw0 + c];
+          }
+        }
+        __syncthreads();
+        for (uint32_t q = t; q < words; q += kBlock) {
+          const uint32_t j = cw == 1 ? q : (cw == 2 ? (q >> 1) : q / cw);
+          const uint32_t c = q - j * cw;
+          const uint32_t d = dslot[j];
+          const uint64_t row = (uint64_t)(goff[d] + (int64_t)(j - bstart[d]));
+          d32[row * wpr + cw0 + c] = buf[(uint32_t)perm[j] * cw + c];
+        }
+        __syncthreads();
+      }
+    }
+    goff[t] += tot;
+    __syncthreads();
+  }
+}
+
+// One wave per 64 consecutive rows: the wave's strings form one contiguous destination range of
+// T bytes; lane b copies bytes b, b+64, ... after a 6-step search of the row that holds it.
+__global__ __launch_bounds__(256) void copy_segments_kernel(const uint8_t* __restrict__ src,
+                                                            const int64_t* __restrict__ soff,
+                                                            const int64_t* __restrict__ len,
+                                                            const int64_t* __restrict__ doff, uint64_t n,
+                                                            uint8_t* __restrict__ dst) {
+  __shared__ int64_t ends[4][64];
+  __shared__ int64_t srcs[4][64];
+  const int w = wave_id(), l = lane_id();
+  const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+  for (uint64_t g = (uint64_t)blockIdx.x * 4 + w; g * 64 < n; g += nwaves) {
+    const uint64_t r0 = g * 64;
+    const uint64_t rows = n - r0 < 64 ? n - r0 : 64;
+    const int64_t base = doff[r0];
+    int64_t e = 0, so = 0, st = 0;
+    if ((uint64_t)l < rows) {
+      st = doff[r0 + l] - base;
+      e = st + len[r0 + l];
+      so = soff[r0 + l] - st;          // source byte of destination byte b in this row: so + b
+    } else {
+      st = e = doff[r0 + rows - 1] - base + len[r0 + rows - 1];
+    }
+    ends[w][l] = e;
+    srcs[w][l] = so;
+    __builtin_amdgcn_wave_barrier();
+    const int64_t T = __shfl(e, 63, 64);
+    for (int64_t b = l; b < T; b += 64) {
+      int lo = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1)
+        if (lo + step <= 63 && ends[w][lo + step - 1] <= b) lo += step;
+      dst[base + b] = src[srcs[w][lo] + b];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+}  // namespace
+
+// Geometry shared by the count and scatter launches (the caller sizes `counts` as 256 * G).
+DR_API uint32_t dr_pc_grid(uint64_t n, uint64_t* per_block) {
+  uint64_t tiles = (n + kPcTile - 1) / kPcTile;
+  if (tiles < 1) tiles = 1;
+  // 1024 workgroups x 4 waves fill the 256 CUs; more only grows the [256][G] offset matrix
+  const uint64_t G = tiles < 1024 ? tiles : 1024;
+  *per_block = ((tiles + G - 1) / G) * kPcTile;
+  return (uint32_t)G;
+}
+
+DR_API int dr_pc_count(const E128* ent, uint64_t n, const uint8_t* lut, uint32_t* counts, uint32_t G,
+                       uint64_t per_block, hipStream_t s) {
+  if (n == 0) return 0;
+  pc_count_kernel<<<G, 256, 0, s>>>(ent, n, lut, counts, G, per_block);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// offsets: int64 [256 * G], exclusive prefix of the bucket-major counts (destination row of each
+// workgroup's first row of each bucket).  in/out/width: ncols (<= 16) device columns.
+DR_API int dr_pc_scatter(const E128* ent, uint64_t n, const uint8_t* lut, const void* const* in, void* const* out,
+                         const uint32_t* width, uint32_t ncols, const int64_t* offsets, uint32_t G, uint64_t per_block,
+                         hipStream_t s) {
+  if (ncols > (uint32_t)kPcMaxCols || n >= (1ull << 40)) return (int)hipErrorInvalidValue;
+  if (n == 0 || ncols == 0) return 0;
+  PcCols c;
+  for (uint32_t k = 0; k < ncols; ++k) {
+    const uint32_t wb = width[k];
+    if (wb == 0 || (wb > 2 && (wb & 3))) return (int)hipErrorInvalidValue;
+    c.in[k] = static_cast<const uint8_t*>(in[k]);
+    c.out[k] = static_cast<uint8_t*>(out[k]);
+    c.width[k] = wb;
+  }
+  c.ncols = ncols;
+  pc_scatter_kernel<<<G, 256, 0, s>>>(ent, n, lut, c, offsets, G, per_block);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+DR_API int dr_copy_segments(const uint8_t* src, const int64_t* soff, const int64_t* len, const int64_t* doff,
+                            uint64_t n, uint8_t* dst, hipStream_t s) {
+  if (n == 0) return 0;
+  copy_segments_kernel<<<grid_for((n + 63) / 64, 4, 8192), 256, 0, s>>>(src, soff, len, doff, n, dst);
+  DR_LAUNCH_CHECK();
+  return 0;
+}

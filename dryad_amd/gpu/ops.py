@@ -452,6 +452,43 @@ def hash_partition_perm(table: DeviceTable, key_fn, n: int):
     return _perm(e), st.tolist()
 
 
+def _port_order(n: int, world_size: int):
+    """Bucket order of a partition vertex's ports: rank-major for a multi-rank job (port p lives
+    on rank p % W), so each destination rank's rows are one contiguous slice -> (order, LUT)."""
+    if world_size <= 1 or n <= 1:
+        return None, None
+    order = sorted(range(n), key=lambda p: (p % world_size, p))
+    if order == list(range(n)):
+        return None, None
+    lut = [0] * 256
+    for i, p in enumerate(order):
+        lut[p] = i
+    return order, lut
+
+
+def partition_by_entries(t: DeviceTable, e: torch.Tensor, n: int, world_size: int = 1):
+    """Port-grouped copy of ``t``: row i goes to port ``e[i, 1]`` (< n <= 256), stable within a
+    port, every column moved in one pass (ops/channel.scatter_columns, csrc/kernels/channel.hip).
+    None when the table's columns do not fit that kernel."""
+    from ..ops import channel as CH
+    if n > 256:
+        return None
+    cols = [t.rows] if t.rows is not None else list(t.cols.values())
+    if not cols or not CH.kernel_ok(cols):
+        return None
+    order, lut = _port_order(n, world_size)
+    lut_t = torch.tensor(lut, dtype=torch.uint8, device=t.device) if lut is not None else None
+    outs, cnt = CH.scatter_columns(e, t.n, cols, lut_t)
+    offs = [0]
+    for c in cnt[:n].tolist():
+        offs.append(offs[-1] + int(c))
+    if t.rows is not None:
+        nt = DeviceTable(t.n, t.shape, rows=outs[0])
+    else:
+        nt = DeviceTable(t.n, t.shape, dict(zip(t.cols.keys(), outs)), heap=t.heap, strs=t.strs)
+    return Ported(nt, offs, order)
+
+
 def op_hash_partition(op, inputs, v):
     t = _check(_one(inputs))
     n = op["count"]
@@ -459,6 +496,12 @@ def op_hash_partition(op, inputs, v):
         raise NotTraceable("custom comparer")
     if t.n == 0:
         return Ported(t, [0] * (n + 1))
+    if n <= 256 and t.n < (1 << 32):
+        keys, tup = hash_keys(t, op["key"])
+        e, _ = R.stable_hash_dest(keys, t.n, n, tup, t.device)
+        out = partition_by_entries(t, e, n, v.world.size)
+        if out is not None:
+            return out
     perm, st = hash_partition_perm(t, op["key"], n)
     return Ported(t.take(perm), st)
 
@@ -510,6 +553,9 @@ def op_range_partition(op, inputs, v):
     seps_t = _entries_table(seps_t)
     seps = torch.stack([seps_t.cols["lo"], seps_t.cols["hi"]], 1).contiguous()
     S.range_dest(e, seps, lo_mask, descending=op.get("descending", False))
+    out = partition_by_entries(t, e, n, v.world.size)
+    if out is not None:
+        return out
     part, starts = S.partition_pass(e, 64)
     return Ported(t.take(_perm(part)), starts[: n + 1].tolist())
 

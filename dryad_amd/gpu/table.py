@@ -134,6 +134,9 @@ class DeviceTable:
         t0 = tables[0]
         if len(tables) == 1:
             return t0
+        adj = DeviceTable._adjacent(tables)
+        if adj is not None:
+            return adj
         if t0.rows is not None:
             return DeviceTable(sum(t.n for t in tables), t0.shape, rows=torch.cat([t.rows for t in tables]))
         if t0.heap is not None:
@@ -157,6 +160,31 @@ class DeviceTable:
             return DeviceTable(sum(t.n for t in tables), t0.shape, cols, strs=strs)
         return DeviceTable(sum(t.n for t in tables), t0.shape,
                            {k: torch.cat([t.cols[k] for t in tables]) for k in t0.cols})
+
+    @staticmethod
+    def _adjacent(tables: list):
+        """Tables that are consecutive row slices of one table (e.g. the pieces one exchange
+        delivered for a partition): one view instead of a copy."""
+        from ..parallel.exchange import _span
+        t0 = tables[0]
+        if t0.heap is not None and any(t.heap is not t0.heap for t in tables):
+            return None
+        if any(t.strs.keys() != t0.strs.keys() or any(t.strs[f] is not t0.strs[f] for f in t0.strs) for t in tables):
+            return None
+        if t0.rows is not None:
+            if any(t.rows is None for t in tables):
+                return None
+            r = _span([t.rows for t in tables])
+            return None if r is None else DeviceTable(r.shape[0], t0.shape, rows=r)
+        if any(t.rows is not None or t.cols.keys() != t0.cols.keys() for t in tables):
+            return None
+        cols = {}
+        for k in t0.cols:
+            v = _span([t.cols[k] for t in tables])
+            if v is None:
+                return None
+            cols[k] = v
+        return DeviceTable(sum(t.n for t in tables), t0.shape, cols, heap=t0.heap, strs=t0.strs)
 
     # ------------------------------------------------------------------ packing for RCCL
     def pack(self) -> torch.Tensor:
@@ -272,12 +300,31 @@ def _width(v: torch.Tensor) -> int:
 
 @dataclass
 class Ported:
-    """A multi-port vertex output: ``table`` permuted so port k = rows [offsets[k], offsets[k+1])."""
+    """A multi-port vertex output: ``table`` grouped by port, bucket i = rows
+    [offsets[i], offsets[i+1]) holding port ``order[i]`` (``order`` None: bucket i is port i).
+    Partitioning vertices of a multi-rank job number the buckets rank-major (every port of rank 0,
+    then rank 1, ...), so each destination rank's rows are one contiguous slice of every column
+    and the table itself is the all-to-all send buffer (parallel/exchange.py)."""
     table: DeviceTable
     offsets: list
+    order: list | None = None
+
+    def _bucket(self, k: int) -> int:
+        if self.order is None:
+            return k
+        pos = self.__dict__.get("_pos")
+        if pos is None:
+            pos = {p: i for i, p in enumerate(self.order)}
+            self.__dict__["_pos"] = pos
+        return pos[k]
 
     def port(self, k: int) -> DeviceTable:
-        return self.table.slice(self.offsets[k], self.offsets[k + 1])
+        i = self._bucket(k)
+        return self.table.slice(self.offsets[i], self.offsets[i + 1])
+
+    def port_rows(self, k: int) -> int:
+        i = self._bucket(k)
+        return self.offsets[i + 1] - self.offsets[i]
 
     @property
     def nports(self):

@@ -1,0 +1,214 @@
+"""Device channels between ranks: DeviceTables moved by RCCL all-to-all-v, column by column.
+
+The reference moves every cross-vertex channel as a file served over HTTP
+(``DrOutputGenerator.cpp:216-224``, ``ProcessService/HttpServer.cs:622-660``); a CrossProduct
+shuffle is N x M such files (``GraphBuilder.cs:481-504``).  Here a channel between GPUs is a slice
+of an HBM table, and one stage's worth of channels is ONE exchange:
+
+  * a manifest all-gather (piece row counts, string-heap bytes, the table schema: a few hundred
+    bytes per rank) so every rank sizes its receive buffers and agrees on column types
+    (partitions whose inferred widths differ, e.g. Int32 vs Int64 columns, are promoted);
+  * one all-to-all-v per column over xGMI (RCCL ``all_to_all_single``; the send side is a view of
+    the producer's port-grouped columns whenever the pieces for consecutive ranks are adjacent,
+    which is what the rank-major partition order of ``gpu/ops`` guarantees, so nothing is packed);
+  * one more all-to-all-v per string field: the pieces' string bytes compacted in row order
+    (``ops/channel.compact_heap``); receivers rebuild offsets as the prefix sum of the lengths.
+
+No record ever becomes a Python object, and no rank receives data it does not consume.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..gpu.table import DeviceTable, Shape
+from ..ops import channel as CH
+from . import shuffle
+from .comm import World
+
+
+class SchemaMismatch(Exception):
+    """Ranks hold structurally different tables: the caller has to use the object transport."""
+
+
+# ------------------------------------------------------------------------------------------------
+def _string_specs(t: DeviceTable) -> list:
+    """(offset column, length column, heap key) of every variable-length field."""
+    if t.heap is not None:
+        return [("off", "len", None)]
+    return [(f, f + "#len", f) for f in t.strs]
+
+
+def _columns(t: DeviceTable) -> dict:
+    if t.rows is not None:
+        return {"__rows__": t.rows}
+    return t.cols
+
+
+def signature(t: DeviceTable):
+    """(structure, dtypes): the structure must match across ranks, dtypes may be promoted."""
+    cols = _columns(t)
+    sh = t.shape
+    struct = (sh.kind, tuple(sh.fields), sh.pytype, sh.key_off, sh.key_len,
+              tuple((k, tuple(v.shape[1:])) for k, v in cols.items()), tuple(_string_specs(t)))
+    return struct, tuple(str(v.dtype) for v in cols.values())
+
+
+def _dtype(name: str) -> torch.dtype:
+    return getattr(torch, name.split(".")[-1])
+
+
+def _dense(t: torch.Tensor) -> bool:
+    """Row-major with the standard strides in EVERY dim (is_contiguous() accepts any stride on a
+    dim of size 1, e.g. a one-row slice of an entries column, which a byte view cannot take)."""
+    exp = 1
+    for d in range(t.dim() - 1, -1, -1):
+        if t.stride(d) != exp:
+            return False
+        exp *= t.shape[d]
+    return True
+
+
+def _span(ts: list):
+    """A view covering tensors that are consecutive contiguous slices of one storage, else None."""
+    if not ts:
+        return None
+    base = ts[0]
+    try:
+        st = base.untyped_storage()
+    except RuntimeError:
+        return None
+    pos = base.storage_offset()
+    end = pos
+    for t in ts:
+        if t.dtype != base.dtype or not _dense(t) or t.untyped_storage().data_ptr() != st.data_ptr() \
+                or t.storage_offset() != end or t.shape[1:] != base.shape[1:]:
+            return None
+        end += t.numel()
+    out = torch.empty(0, dtype=base.dtype, device=base.device)
+    tail = tuple(base.shape[1:])
+    per = 1
+    for d in tail:
+        per *= d
+    out.set_(st, pos, ((end - pos) // max(per, 1),) + tail)
+    return out
+
+
+def _cat(ts: list, like: torch.Tensor):
+    if not ts:
+        return like.new_empty((0,) + tuple(like.shape[1:]))
+    nonempty = [t for t in ts if t.shape[0] > 0]
+    if not nonempty:
+        return ts[0]
+    if len(nonempty) == 1:
+        return nonempty[0]
+    sp = _span(nonempty)
+    return sp if sp is not None else torch.cat([t.contiguous() for t in nonempty])
+
+
+def _bytes(t: torch.Tensor) -> torch.Tensor:
+    if t.numel() == 0:
+        return torch.empty(0, dtype=torch.uint8, device=t.device)
+    if not _dense(t):
+        t = torch.empty(t.shape, dtype=t.dtype, device=t.device).copy_(t)
+    return t.reshape(-1).view(torch.uint8)
+
+
+class ExchangeStats:
+    def __init__(self):
+        self.bytes_sent = 0
+        self.bytes_received = 0
+        self.collectives = 0
+
+
+def exchange(world: World, sends: list, stats: ExchangeStats | None = None) -> list:
+    """``sends[r]``: DeviceTables (pieces) for rank r, in order.  Returns ``recv[s]``: the pieces
+    rank s sent to this rank, in its order.  Collective: every rank calls it with W send lists.
+    Raises SchemaMismatch (on every rank) when the ranks' tables are structurally different."""
+    W, me = world.size, world.rank
+    assert len(sends) == W
+    proto = next((p for lst in sends for p in lst if p is not None), None)
+    sig = signature(proto) if proto is not None else None
+    manifest = []
+    for lst in sends:
+        manifest.append([(p.n, [int(p.cols[lc][:p.n].sum()) if p.n else 0 for _, lc, _ in _string_specs(p)])
+                         for p in lst])
+    gathered = [None] * W
+    dist.all_gather_object(gathered, (sig, manifest))
+    sigs = [g[0] for g in gathered if g[0] is not None]
+    if not sigs:                      # nobody holds a piece
+        return [[] for _ in range(W)]
+    structs = {s[0] for s in sigs}
+    if len(structs) != 1:
+        raise SchemaMismatch(f"ranks hold different table structures: {structs}")
+    struct = sigs[0][0]
+    kind, fields, pytype, key_off, key_len, colspecs, strspecs = struct
+    dtypes = []
+    for j in range(len(colspecs)):
+        dt = _dtype(sigs[0][1][j])
+        for s in sigs[1:]:
+            dt = torch.promote_types(dt, _dtype(s[1][j]))
+        dtypes.append(dt)
+    shape = Shape(kind, list(fields), pytype, key_off, key_len)
+    dev = world.device if world.device.type == "cuda" else (proto.device if proto is not None else torch.device("cpu"))
+    recv_rows = [sum(n for n, _ in gathered[s][1][me]) for s in range(W)]
+    send_rows = [sum(p.n for p in sends[r]) for r in range(W)]
+    total_r = sum(recv_rows)
+    out_cols = {name: None for name, _ in colspecs}
+    offset_cols = {oc for oc, _, _ in strspecs}        # rebuilt from the lengths on arrival
+    for (name, tail), dt in zip(colspecs, dtypes):
+        if name in offset_cols:
+            out_cols[name] = dt
+            continue
+        per = torch.empty((0,) + tuple(tail), dtype=dt).element_size()
+        for d in tail:
+            per *= d
+        pieces = [_columns(p)[name][:p.n] for lst in sends for p in lst]
+        pieces = [x if x.dtype == dt else x.to(dt) for x in pieces]
+        like = torch.empty((0,) + tuple(tail), dtype=dt, device=dev)
+        send = _bytes(_cat(pieces, like)) if pieces else torch.empty(0, dtype=torch.uint8, device=dev)
+        recv = torch.empty(total_r * per, dtype=torch.uint8, device=dev)
+        shuffle.alltoallv_bytes(send, [c * per for c in send_rows], recv, [c * per for c in recv_rows], world)
+        out_cols[name] = recv.view(dt).view((total_r,) + tuple(tail))
+        if stats is not None:
+            stats.bytes_sent += sum(send_rows) * per
+            stats.bytes_received += total_r * per
+            stats.collectives += 1
+    heaps = {}
+    for j, (oc, lc, hk) in enumerate(strspecs):
+        parts, send_b = [], []
+        for lst in sends:
+            nb = 0
+            for p in lst:
+                if p.n == 0:
+                    continue
+                heap = p.heap if hk is None else p.strs[hk]
+                h, _ = CH.compact_heap(heap, p.cols[oc][:p.n], p.cols[lc][:p.n])
+                parts.append(h)
+                nb += h.numel()
+            send_b.append(nb)
+        recv_b = [sum(m[1][j] for m in gathered[s][1][me]) for s in range(W)]
+        send = torch.cat(parts) if len(parts) > 1 else (parts[0] if parts else torch.empty(0, dtype=torch.uint8,
+                                                                                                device=dev))
+        recv = torch.empty(sum(recv_b), dtype=torch.uint8, device=dev)
+        shuffle.alltoallv_bytes(send, send_b, recv, recv_b, world)
+        ln = out_cols[lc].to(torch.int64)
+        out_cols[oc] = (torch.cumsum(ln, 0) - ln).to(out_cols[oc])
+        heaps[hk] = recv
+        if stats is not None:
+            stats.bytes_sent += sum(send_b)
+            stats.bytes_received += recv.numel()
+            stats.collectives += 1
+    if "__rows__" in out_cols:
+        big = DeviceTable(total_r, shape, rows=out_cols["__rows__"])
+    else:
+        big = DeviceTable(total_r, shape, out_cols, heap=heaps.get(None),
+                          strs={k: v for k, v in heaps.items() if k is not None})
+    res, a = [], 0
+    for s in range(W):
+        lst = []
+        for n, _ in gathered[s][1][me]:
+            lst.append(big.slice(a, a + n))
+            a += n
+        res.append(lst)
+    return res

@@ -100,6 +100,7 @@ class GpuJobRunner:
         self.faults = faults or []
         self.channels: dict = {}          # (stage, partition) -> DeviceTable | Ported | list | list-of-lists
         self.fallbacks: list = []
+        self.transports: list = []      # (stage, edge kind, "device" | "object", bytes / reason)
         self.timings: dict = {}
         R = native_runtime()
         p = R.Params()
@@ -383,32 +384,52 @@ class GpuJobRunner:
                 for p in local:
                     inputs[p][ii] = [self._port_of(si, self.channels[(si.src, q)], p) for q in self._sources(si, p)]
                 continue
-            # generic path: every rank publishes the port data other ranks need (host objects or
-            # packed device rows) through one all_gather_object of descriptors + payloads
-            send = {}
-            for p in range(s.partitions):
-                for q in self._sources(si, p):
-                    if self.owner(q) == me and self.owner(p) != me:
-                        send[(q, p)] = self._portable(self._port_of(si, self.channels[(si.src, q)], p))
-            gathered = [None] * W
-            dist.all_gather_object(gathered, send)
+            # merge / broadcast / remote pointwise edges: every rank sends each port value another
+            # rank needs once (a q feeding several of its partitions travels once)
+            need = [sorted({q for p in range(s.partitions) if self.owner(p) == r for q in self._sources(si, p)
+                            if self.owner(q) != r}) for r in range(W)]
+            mine = {q: self._port_of(si, self.channels[(si.src, q)], None) for r in range(W) for q in need[r]
+                    if self.owner(q) == me}
+            sends = [[mine[q] for q in need[r] if self.owner(q) == me] for r in range(W)]
+            got = self._transport(s, si, sends, [[q for q in need[me] if self.owner(q) == r] for r in range(W)])
+            recv = {q: x for r in range(W) for q, x in got[r].items()}
             for p in local:
-                lst = []
-                for q in self._sources(si, p):
-                    if self.owner(q) == me:
-                        lst.append(self._port_of(si, self.channels[(si.src, q)], p))
-                    else:
-                        lst.append(self._unportable(gathered[self.owner(q)][(q, p)]))
-                inputs[p][ii] = lst
+                inputs[p][ii] = [self._port_of(si, self.channels[(si.src, q)], p) if self.owner(q) == me
+                                 else recv[q] for q in self._sources(si, p)]
         return inputs
 
-    def _portable(self, x):
-        if isinstance(x, DeviceTable) and (x.heap is not None or x.strs):
-            return self._ship(x)
-        if isinstance(x, DeviceTable):
-            return ("dt", x.shape, {k: v.cpu() for k, v in x.cols.items()} if x.rows is None else None,
-                    x.rows.cpu() if x.rows is not None else None, x.n)
-        return ("obj", x)
+    # ------------------------------------------------------------------ channel transport
+    def _transport(self, s, si, sends, recv_ids):
+        """Move port values between ranks: ``sends[r]`` = values for rank r (in ``recv_ids`` order on
+        the receiving side).  Device tables of one schema go through parallel/exchange (RCCL
+        all-to-all-v per column, string heaps included); anything else (host records left by a
+        fallback, structurally different tables) through the object transport, recorded in
+        ``self.transports``.  Returns, per source rank, {source partition: value}."""
+        from ..parallel import exchange as EXC
+        W = self.world.size
+        dev_ok = all(isinstance(x, DeviceTable) for lst in sends for x in lst)
+        votes = [None] * W
+        dist.all_gather_object(votes, dev_ok)
+        if all(votes):
+            try:
+                st = EXC.ExchangeStats()
+                got = EXC.exchange(self.world, sends, st)
+                self.transports.append((s.name, si.kind, "device", st.bytes_sent))
+                return [dict(zip(recv_ids[r], got[r])) for r in range(W)]
+            except EXC.SchemaMismatch as e:
+                why = str(e)
+        else:
+            why = "host records on the channel"
+        gathered = [None] * W
+        payload = [[self._ship(x) for x in lst] for lst in sends]
+        dist.all_gather_object(gathered, payload)
+        # one host value per partition (aggregate partials: the reference's final-aggregate
+        # vertex input) is control-plane sized; anything bigger is a data-plane object transfer
+        scalar = all(isinstance(x, list) and len(x) <= 1 for lst in sends for x in lst)
+        self.transports.append((s.name, si.kind, "scalar" if scalar and not why.startswith("ranks") else "object",
+                                why))
+        me = self.world.rank
+        return [dict(zip(recv_ids[r], [self._unship(x) for x in gathered[r][me]])) for r in range(W)]
 
     @staticmethod
     def _ship(x):
@@ -420,13 +441,6 @@ class GpuJobRunner:
                     x.heap.cpu() if x.heap is not None else None, {f: h.cpu() for f, h in x.strs.items()}, x.n)
         return ("obj", _to_objects(x))
 
-    @staticmethod
-    def _keep(x):
-        """A local port on the object transport (string tables stay on the device)."""
-        if isinstance(x, DeviceTable) and (x.heap is not None or x.strs):
-            return x
-        return _to_objects(x)
-
     def _unship(self, x):
         if x[0] == "dts":
             _, shape, cols, heap, strs, n = x
@@ -435,101 +449,48 @@ class GpuJobRunner:
                                strs={f: h.to(self.dev) for f, h in strs.items()})
         return x[1]
 
-    def _unportable(self, x):
-        if x[0] == "dts":
-            return self._unship(x)
-        if x[0] == "dt":
-            _, shape, cols, rows, n = x
-            if rows is not None:
-                return DeviceTable(n, shape, rows=rows.to(self.dev))
-            return DeviceTable(n, shape, {k: v.to(self.dev) for k, v in cols.items()})
-        return x[1]
-
     def _exchange_cross(self, si, src_stage, dst_stage):
-        """CrossProduct shuffle: one all-to-all-v of packed rows (RCCL over xGMI)."""
+        """CrossProduct shuffle (HashPartition/RangePartition -> Merge): ONE exchange of the port
+        slices.  Send order per destination rank: local source partitions ascending, then that
+        rank's partitions ascending; with one partition per rank and rank-major port order
+        (gpu/ops.partition_by_entries) each rank's pieces are one slice of the producer's columns
+        and the pieces a partition receives arrive adjacent, so neither side copies."""
         W, me = self.world.size, self.world.rank
         P_src, P_dst = src_stage.partitions, dst_stage.partitions
         local_src = [q for q in range(P_src) if self.owner(q) == me]
-        vals = {q: self.channels[(si.src, q)] for q in local_src}
-        device_ok = all(isinstance(v, Ported) and v.table.heap is None and not v.table.strs for v in vals.values())
-        # agree on the transport (all device tables with one schema, else host objects)
-        sig = None
-        if device_ok and vals:
-            t0 = next(iter(vals.values())).table
-            sig = (t0.shape.kind, tuple(t0.shape.fields), t0.rows.shape[1] if t0.rows is not None else None,
-                   tuple((k, str(v.dtype)) for k, v in t0.cols.items()))
-        sigs = [None] * W
-        dist.all_gather_object(sigs, (device_ok, sig))
-        uniform = all(ok for ok, _ in sigs) and len({s for _, s in sigs if s is not None}) <= 1
         local_dst = [p for p in range(P_dst) if self.owner(p) == me]
-        if not uniform:
-            send = {}
-            for q, v in vals.items():
-                for p in range(P_dst):
-                    if self.owner(p) != me:
-                        send[(q, p)] = self._ship(self._port_of(si, v, p))
-            gathered = [None] * W
-            dist.all_gather_object(gathered, send)
-            out = {}
-            for p in local_dst:
-                out[p] = [self._keep(self._port_of(si, self.channels[(si.src, q)], p))
-                          if self.owner(q) == me else self._unship(gathered[self.owner(q)][(q, p)])
-                          for q in range(P_src)]
-            return out
-        # counts matrix [P_src, P_dst] (rows), all-gathered
-        cnt = torch.zeros((P_src, P_dst), dtype=torch.int64)
-        for q, v in vals.items():
-            cnt[q] = torch.tensor([v.offsets[p + 1] - v.offsets[p] for p in range(P_dst)], dtype=torch.int64)
-        allc = cnt.clone()
-        shuffle.all_reduce_(allc, "sum", self.world)
-        proto = next(iter(vals.values())).table if vals else None
-        # pack: for each destination rank, for each local src q asc, for each dst p owned by it asc
-        pieces, send_counts = [], [0] * W
-        row_bytes = None
+        sends, ids = [], []
         for r in range(W):
+            lst = []
             for q in local_src:
-                t = vals[q].table
-                packed = t.pack()
-                row_bytes = packed.shape[1]
+                v = self.channels[(si.src, q)]
                 for p in range(P_dst):
-                    if self.owner(p) != r:
-                        continue
-                    a, b = vals[q].offsets[p], vals[q].offsets[p + 1]
-                    if b > a:
-                        pieces.append(packed[a:b])
-                    send_counts[r] += (b - a)
-        if row_bytes is None:
-            row_bytes = 0
-        rb = [None] * W
-        dist.all_gather_object(rb, row_bytes)
-        row_bytes = max(x for x in rb if x is not None)
-        recv_counts = []
+                    if self.owner(p) == r:
+                        lst.append(self._port_of(si, v, p))
+            sends.append(lst)
         for r in range(W):
-            c = 0
-            for q in range(P_src):
-                if self.owner(q) != r:
-                    continue
-                for p in local_dst:
-                    c += int(allc[q, p])
-            recv_counts.append(c)
-        send = torch.cat(pieces) if pieces else torch.empty((0, row_bytes), dtype=torch.uint8, device=self.dev)
-        recv = torch.empty((sum(recv_counts), row_bytes), dtype=torch.uint8, device=self.dev)
-        shuffle.alltoallv_bytes(send.reshape(-1), [c * row_bytes for c in send_counts], recv.reshape(-1),
-                                [c * row_bytes for c in recv_counts], self.world)
-        if proto is None:
-            raise DryadLinqException(ErrorCode.Internal, "rank without source partitions in a device shuffle")
-        # unpack into per-(q, p) slices
+            ids.append([(q, p) for q in range(P_src) if self.owner(q) == r for p in local_dst])
+        got = self._transport(dst_stage, si, sends, ids)
         out = {p: [None] * P_src for p in local_dst}
-        off = 0
         for r in range(W):
-            for q in range(P_src):
-                if self.owner(q) != r:
-                    continue
-                for p in local_dst:
-                    c = int(allc[q, p])
-                    out[p][q] = proto.unpack_like(recv[off:off + c], c)
-                    off += c
+            for (q, p), x in got[r].items():
+                out[p][q] = x
+        self._drop_consumed(si.src, dst_stage.id)
         return out
+
+    def _drop_consumed(self, src_id, consumer_id):
+        """The exchange delivered copies: free the producer's tables now (not at the end of the
+        consumer stage) when nothing else reads them, so a shuffle holds send + receive only
+        while it runs and receive + output afterwards."""
+        st = self.plan.stages
+        if st[src_id].is_output or any(f["x"] == src_id for f in self.fused.values()):
+            return
+        if any(src_id == i.src for t in st if t.id != consumer_id and t.id > src_id for i in t.inputs):
+            return
+        if sum(1 for i in st[consumer_id].inputs if i.src == src_id) > 1:
+            return
+        for key in [k for k in self.channels if k[0] == src_id]:
+            del self.channels[key]
 
     # ------------------------------------------------------------------ vertex execution
     def _fault(self, s, p, version):
@@ -586,11 +547,13 @@ class GpuJobRunner:
         self.fallbacks.append((s.name, name, why))
         props = self.ctx._props
         if self.gpu_ok and nb > int(props.get("HostFallbackMaxBytes") or 0) and not props.get("AllowHostFallback"):
-            raise DryadLinqException(
+            e = DryadLinqException(
                 ErrorCode.OperatorNotSupported,
                 f"{s.name}: operator {name} cannot run on the device ({why}) and its host fallback would move "
                 f"{nb / 1e6:.1f} MB of HBM data into Python objects (> HostFallbackMaxBytes); set "
                 f"AllowHostFallback=True to run it on the host anyway")
+            e.retriable = False
+            raise e
 
     def _maybe_device(self, out, s, opname):
         """Host op result -> device table when the records are columnar (keeps later ops on GPU)."""
@@ -695,6 +658,9 @@ class GpuJobRunner:
                     except Exception as e:  # noqa: BLE001
                         g.on_failed(vid, ver, now(), -1, f"{type(e).__name__}: {e}")
                         self._last_exc = e
+                        if getattr(e, "retriable", True) is False:
+                            status, err = 2, str(e)      # deterministic refusal: re-running cannot help
+                            break
                         if g.failed():
                             status, err = 1, g.failure()
                             break
@@ -707,6 +673,8 @@ class GpuJobRunner:
                               device=self.dev if self.world.backend == "nccl" else "cpu")
             shuffle.all_reduce_(st, "max", self.world)
             if int(st.item()) != 0:
+                if status == 2:
+                    raise self._last_exc
                 raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed,
                                             err or f"job aborted: a vertex of stage {s.name} failed on another rank",
                                             inner=getattr(self, "_last_exc", None))
@@ -724,7 +692,7 @@ class GpuJobRunner:
         if self.pool is not None:
             for b in set(self.row_sets.values()):
                 self.pool.release(b)
-        return dict(committed=committed, fallbacks=self.fallbacks, timings=self.timings,
+        return dict(committed=committed, fallbacks=self.fallbacks, timings=self.timings, transports=self.transports,
                     statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()],
                     external_sort=getattr(self, "extsort_stats", None))
 

@@ -117,8 +117,24 @@ def main():
     loc = D.DryadLinqContext(1)
     loc.LocalDebug = True
     bad = []
+    ex = g._get_executor()
+    jobs = []
+    orig = ex.run_job
+
+    def run_job(outs, handle):
+        res = orig(outs, handle)
+        jobs.append(res)
+        return res
+    ex.run_job = run_job
     for name, (q, ordered) in queries().items():
+        jobs.clear()
         got = run(q, g, W)
+        for res in jobs:
+            # a channel may only go through the object transport when a host fallback left host
+            # records on it: device tables always take the RCCL / gloo device exchange
+            obj = [t for t in res.get("transports", []) if t[2] == "object"]
+            if obj and not res.get("fallbacks") and w.device.type == "cuda":
+                bad.append(f"{name}: object transport {obj}")
         if w.rank == 0:
             exp = run(q, loc, W)
             norm = (lambda x: [bytes(v) if isinstance(v, (bytes, bytearray, memoryview)) else v for v in x])
@@ -127,10 +143,44 @@ def main():
             if not ok:
                 bad.append(name)
             print(f"[sweep] {name}: {'ok' if ok else 'MISMATCH'} ({len(a)} rows)", flush=True)
-    w.barrier()
+    if w.device.type == "cuda" and W > 1:
+        bad += memory_check(g, w)
+    allbad = [None] * W
+    import torch.distributed as dist
+    dist.all_gather_object(allbad, bad)
     if w.rank == 0:
-        assert not bad, bad
+        flat = [x for b in allbad for x in b]
+        assert not flat, flat
         print("SWEEP_OK", W, flush=True)
+
+
+def memory_check(g, w):
+    """A shuffle of 2M 64-byte records per rank must peak at <= 2.5x the partition's bytes
+    (partitioned send columns + receive columns; no per-destination packs)."""
+    import torch
+    W = w.size
+    n = 2_000_000
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats()
+    base = torch.cuda.memory_allocated()
+    q = g.FromStore(f"gen://records64?count={n * W}&partitions={W}&keys=1000000&seed=3").HashPartition(
+        lambda r: r[0], W).ToStore("hbm://sweep_memcheck", delete_if_exists=True)
+    q.SubmitAndWait()
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated() - base
+    ratio = peak / (n * 64)
+    tr = g._get_executor().last_result.get("transports", [])
+    print(f"[sweep] memcheck rank {w.rank}: peak {peak / 1e6:.1f} MB = {ratio:.2f}x partition; transports {tr}",
+          flush=True)
+    out = []
+    if ratio > 2.5:
+        out.append(f"shuffle peak {ratio:.2f}x the partition bytes on rank {w.rank}")
+    if not tr or any(t[2] != "device" for t in tr):
+        out.append(f"memcheck transports {tr}")
+    from dryad_amd.io.providers import provider_for
+    provider_for("hbm://sweep_memcheck").delete("hbm://sweep_memcheck")
+    return out
 
 
 if __name__ == "__main__":

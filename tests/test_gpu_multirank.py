@@ -11,6 +11,14 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _dump(name, out):
+    """Full output of a failed multi-rank run under gpurun_out/ (the assertion shows only a tail)."""
+    if out.returncode != 0:
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(ROOT, "gpurun_out", f"fail_{name}.log"), "w") as f:
+            f.write(out.stdout + "\n---- stderr ----\n" + out.stderr)
+
+
 @pytest.mark.timeout(600)
 def test_two_ranks_share_one_gpu():
     env = dict(os.environ, DRYAD_DIST_BACKEND="gloo", PYTHONPATH=ROOT, TS_RECORDS="2000000")
@@ -18,6 +26,7 @@ def test_two_ranks_share_one_gpu():
                           "--master-addr", "127.0.0.1", "--master-port", "29633",
                           os.path.join(ROOT, "tests", "dist", "gpu_terasort_ranks.py")],
                          capture_output=True, text=True, timeout=560, env=env, cwd=ROOT)
+    _dump(os.path.basename(out.args[-1]) + str(len(out.args)), out)
     assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
     assert "MULTIRANK_OK 2" in out.stdout
 
@@ -30,6 +39,7 @@ def test_query_sweep_ranks(ranks):
                           "--master-addr", "127.0.0.1", "--master-port", str(29634 + ranks),
                           os.path.join(ROOT, "tests", "dist", "gpu_query_sweep_ranks.py")],
                          capture_output=True, text=True, timeout=560, env=env, cwd=ROOT)
+    _dump(os.path.basename(out.args[-1]) + str(len(out.args)), out)
     assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
     assert f"SWEEP_OK {ranks}" in out.stdout
 
@@ -40,5 +50,21 @@ def test_query_sweep_single_rank():
     env = dict(os.environ, PYTHONPATH=ROOT)
     out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "dist", "gpu_query_sweep_ranks.py")],
                          capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    _dump(os.path.basename(out.args[-1]) + str(len(out.args)), out)
     assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
     assert "SWEEP_OK 1" in out.stdout
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_exchange_ranks_share_one_gpu(ranks):
+    """parallel/exchange.py with device tables on GPU ranks (gloo staging between the ranks):
+    the HIP partition kernel's rank-major ports and every table layout, strings included."""
+    env = dict(os.environ, DRYAD_DIST_BACKEND="gloo", PYTHONPATH=ROOT, SPMD_DEVICE="cuda")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+                          "--master-addr", "127.0.0.1", "--master-port", str(29660 + ranks),
+                          os.path.join(ROOT, "tests", "dist", "exchange_ranks.py")],
+                         capture_output=True, text=True, timeout=380, env=env, cwd=ROOT)
+    _dump(os.path.basename(out.args[-1]) + str(len(out.args)), out)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
+    assert f"EXCHANGE_OK {ranks}" in out.stdout

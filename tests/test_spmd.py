@@ -37,3 +37,15 @@ def test_query_sweep_cpu_two_ranks():
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "SWEEP_OK 2" in r.stdout
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_exchange_gloo(ranks):
+    """Device-channel exchange (parallel/exchange.py) of every table layout over gloo ranks."""
+    env = dict(os.environ, SPMD_DEVICE="cpu", PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tests", "dist", "exchange_ranks.py")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert f"EXCHANGE_OK {ranks}" in r.stdout
