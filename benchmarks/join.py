@@ -1,11 +1,19 @@
 """Hash-join benchmark: GB/s of input joined, two 100 GB tables of 64-byte rows
 (BASELINE.json config "Hash-join two 100 GB tables, spill HBM -> host DRAM").
 
-Strong scaling: the two 100 GB tables are split over the N GPUs (1 GPU: 200 GB of input with
-the grace partitions spilled to pinned host DRAM; 8 GPUs: 25 GB per GPU, buckets stay in HBM).
-The timed step is the whole join: input generation, grace partitioning (+ xGMI exchange, + host
-spill), per-bucket sort-merge joins and the reduction.  Validated against the answer computed
-from the probe table alone.
+The query goes through the DryadLINQ API:
+
+    R.Join(S, r => r.Key, s => s.Key, (r, s) => r.V1 + s.V1).Sum()
+
+R is a dimension table (keys a bijection of [0, |R|)), S a fact table (keys uniform in [0, |R|)),
+both ``gen://records64`` stores.  The GPU executor plans it as the fused grace / radix join stage
+(dryad_amd/runtime/fused_join.py): column pruning derived from the traced selectors (Key + V1 of
+each side), hash routing over xGMI, HBM-resident buckets up to ``--hbm-budget-gb`` with the rest
+spilled to pinned host DRAM, the Sum fused into the probe.  Strong scaling: the two 100 GB tables
+are split over the N GPUs.  The timed step is one whole job (planning, input generation = the
+read, partitioning, spill, bucket joins, final aggregate).  Validated against the answer computed
+independently from S alone (models/hashjoin.HashJoinJob.expected).  ``--direct`` times the
+hand-assembled pipeline (models/hashjoin.py) instead, for comparison.
 """
 from __future__ import annotations
 
@@ -19,37 +27,63 @@ def main():
     ap.add_argument("--table-gb", type=float, default=100.0)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--chunk-rows", type=float, default=float(1 << 27))
     ap.add_argument("--hbm-budget-gb", type=float, default=None)
+    ap.add_argument("--direct", action="store_true")
     ap.add_argument("--no-validate", action="store_true")
     a = ap.parse_args()
     w = world()
-    from dryad_amd.models.hashjoin import HashJoinConfig, HashJoinJob
+    import dryad_amd as D
+    from dryad_amd.models.hashjoin import SEED_R, SEED_S, HashJoinConfig, HashJoinJob
     rows = int(a.table_gb * 1e9 / 64)
-    cfg = HashJoinConfig(rows_r=rows, rows_s=rows, chunk_rows=int(a.chunk_rows),
-                         hbm_budget=None if a.hbm_budget_gb is None else int(a.hbm_budget_gb * 1e9))
-    job = HashJoinJob(w, cfg)
+    budget = None if a.hbm_budget_gb is None else int(a.hbm_budget_gb * 1e9)
+    cfg = HashJoinConfig(rows_r=rows, rows_s=rows, hbm_budget=budget)
+    job = HashJoinJob(w, cfg) if a.direct else None
+    ctx = D.DryadLinqContext(platform="gpu")
+    ctx.PartitionCount = w.size
+    if budget is not None:
+        ctx.HbmBudgetBytes = budget
+    R = f"gen://records64?count={rows}&partitions={w.size}&keys={rows}&seed={SEED_R}&mode=dim"
+    S = f"gen://records64?count={rows}&partitions={w.size}&keys={rows}&seed={SEED_S}"
+
+    def api_step():
+        total = ctx.FromStore(R).Join(ctx.FromStore(S), lambda r: r[0], lambda s: s[0],
+                                      lambda r, s: r[1] + s[1]).Sum()
+        return [ctx._get_executor().last_result["join"]["matches"], total]
+
+    step = job.step if a.direct else api_step
+    if a.direct:
+        job.prepare()
     for _ in range(a.warmup):
-        job.step()
+        step()
     times, res = [], None
     for _ in range(a.steps):
-        dt, res = timed(w, job.step)
+        dt, res = timed(w, step)
         times.append(dt)
     ok = None
     if not a.no_validate:
-        ok = res == job.expected()
+        if job is None:
+            job = HashJoinJob(w, cfg)
+        exp = job.expected()
+        ok = res[0] == exp[0] and res[1] == exp[1]
     med = sorted(times)[len(times) // 2]
     total = 2 * rows * 64
+    if a.direct:
+        js = dict(job.last)
+        fallbacks = []
+    else:
+        last = ctx._get_executor().last_result
+        js, fallbacks = dict(last["join"] or {}), last["fallbacks"]
+        js["stage_seconds"] = {k: round(v, 4) for k, v in last["timings"].items()}
     report(w, {
         "metric": "Hash-join GB/s of input (two 100 GB tables, spill HBM -> host DRAM)",
         "value": round(total / med / 1e9, 3), "unit": "GB/s", "n_gpus": w.size, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(med * 1e3, 2), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "int64", "data": "synthetic gen://records64 row tables (dimension x fact)",
         "validated": ok, "matches": res[0] if res else None, "all_step_ms": [round(t * 1e3, 1) for t in times],
-        "spilled_bytes_per_rank": job.last.get("spilled_bytes"), "buckets": job.last.get("buckets"),
-        "partition_s": round(job.last.get("partition_s", 0), 3),
+        "path": "direct (models/hashjoin.py)" if a.direct else "DryadLINQ query -> fused grace join stage",
+        "fallbacks": fallbacks, "join": js,
         "config": {"model": "R.Join(S, Key).Select(r.V1 + s.V1).Sum() (grace hash join)", "rows_per_table": rows,
-                   "row_bytes": 64, "parallelism": f"dp{w.size}"}})
+                   "row_bytes": 64, "hbm_budget_gb": a.hbm_budget_gb, "parallelism": f"dp{w.size}"}})
 
 
 if __name__ == "__main__":

@@ -186,3 +186,47 @@ class PinnedHostBuffer:
             self.release()
         except Exception:  # noqa: BLE001
             pass
+
+
+# ------------------------------------------------------------------------------------------------
+# Pinned host buffers reused across jobs: page-locking 25-100 GB costs seconds, so a spill tier is
+# registered once per process and leased by every job that needs it (the executor's HbmPool does
+# the same for HBM).
+_PINNED_FREE: list = []
+PINNED_KEEP = 2
+
+
+class PinnedLease:
+    """A ``shape`` view into a pooled page-locked buffer; ``release()`` returns it to the pool."""
+
+    def __init__(self, buf: PinnedHostBuffer, shape, dtype):
+        self._buf = buf
+        n = 1
+        for d in shape:
+            n *= d
+        esz = torch.empty(0, dtype=dtype).element_size()
+        self.tensor = buf.tensor[: n * esz].view(dtype).view(*shape)
+
+    def release(self):
+        if self._buf is not None:
+            _PINNED_FREE.append(self._buf)
+            while len(_PINNED_FREE) > PINNED_KEEP:
+                _PINNED_FREE.pop(0).release()
+            self._buf = None
+        self.tensor = None
+
+
+def pinned_lease(shape, dtype=torch.uint8) -> PinnedLease:
+    n = torch.empty(0, dtype=dtype).element_size()
+    for d in shape:
+        n *= d
+    best = None
+    for b in _PINNED_FREE:
+        cap = b.tensor.numel()
+        if n <= cap <= 2 * max(n, 1 << 20) and (best is None or cap < best.tensor.numel()):
+            best = b
+    if best is not None:
+        _PINNED_FREE.remove(best)
+    else:
+        best = PinnedHostBuffer((max(n, 1),))
+    return PinnedLease(best, shape, dtype)

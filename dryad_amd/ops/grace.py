@@ -134,8 +134,8 @@ class _TableStore:
         self.hbm = torch.empty((max(resident, 0) * cap_rows, stride), dtype=torch.uint8, device=device)
         self.host = None
         if nb > resident:
-            from ._lib import PinnedHostBuffer
-            self.host = PinnedHostBuffer(((nb - resident) * cap_rows, stride))
+            from ._lib import pinned_lease
+            self.host = pinned_lease(((nb - resident) * cap_rows, stride))
         self.part = Partitioner(nb, device)
         base = self.hbm.data_ptr()
         rb = cap_rows * stride
@@ -334,7 +334,7 @@ class GraceHashJoin:
         """Every bucket pair at once through the LDS radix join (radix_join_sum) when all buckets
         are resident in HBM and the rows are narrow (pruned); False when the per-bucket path has
         to run instead."""
-        if not self.in_hbm or self.stride not in (16, 32) or self.key_len > 8 or self.key_off % 4:
+        if not self.in_hbm or self.stride != 16 or self.key_len > 8 or self.key_off % 4:   # dr_radix_join_sum
             return False
         self.finish_partitioning()
         Bs, Ps = self.stores[build], self.stores[probe]
@@ -350,6 +350,41 @@ class GraceHashJoin:
                          torch.tensor(st.fill, dtype=torch.int64, device=self.dev)))
         self.stats.radix_overflow = radix_join_sum(Bs.hbm, segs[0], Ps.hbm, segs[1], self.key_off, self.key_len,
                                                    col_b, col_p, acc, self._scratch)
+        return True
+
+    def join_sum_hybrid(self, build: str, probe: str, col_b: int, col_p: int, acc: torch.Tensor) -> bool:
+        """The LDS radix join for a hybrid (partly spilled) join of 16-byte rows: the resident
+        buckets all at once, then every spilled bucket pair as it streams back from host DRAM
+        (the next pair's upload overlaps this pair's join).  False when the rows do not suit it."""
+        if self.in_hbm or self.stride != 16 or self.key_len > 8 or self.key_off % 4:
+            return False
+        self.finish_partitioning()
+        Bs, Ps = self.stores[build], self.stores[probe]
+        cap = max(Bs.cap, Ps.cap)
+        # scratch of the radix passes: a group of resident buckets at a time (whatever HBM is left)
+        free = torch.cuda.mem_get_info(self.dev)[0] + (0 if self._scratch is None else self._scratch.numel())
+        group = max(1, min(max(self.resident, 1), int(free * 0.8) // (cap * self.stride)))
+        rows = group * cap
+        if self._scratch is None or self._scratch.shape[0] < rows:
+            self._scratch = None
+            self._scratch = torch.empty((rows, self.stride), dtype=torch.uint8, device=self.dev)
+        ovf = 0
+        for g0 in range(0, self.resident, group):
+            g1 = min(self.resident, g0 + group)
+            segs = []
+            for st in (Bs, Ps):
+                segs.append((torch.arange(g1 - g0, dtype=torch.int64, device=self.dev) * st.cap,
+                             torch.tensor(st.fill[g0:g1], dtype=torch.int64, device=self.dev)))
+            ovf += radix_join_sum(Bs.hbm[g0 * Bs.cap: g1 * Bs.cap], segs[0], Ps.hbm[g0 * Ps.cap: g1 * Ps.cap],
+                                  segs[1], self.key_off, self.key_len, col_b, col_p, acc, self._scratch)
+        zero = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        for b, br, pr in self.buckets(build, probe):
+            if b < self.resident or br.shape[0] == 0 or pr.shape[0] == 0:
+                continue
+            ovf += radix_join_sum(br, (zero, torch.tensor([br.shape[0]], dtype=torch.int64, device=self.dev)),
+                                  pr, (zero, torch.tensor([pr.shape[0]], dtype=torch.int64, device=self.dev)),
+                                  self.key_off, self.key_len, col_b, col_p, acc, self._scratch)
+        self.stats.radix_overflow = ovf
         return True
 
     def clear_table(self):

@@ -37,6 +37,7 @@ from ..parallel import shuffle
 from ..parallel.comm import World, get_world, init_world
 from ..utils import trace as TRC
 from ..utils.log import get_logger
+from . import fused_join as FJ
 from . import vertex_ops as V
 from .executor import _BaseExecutor
 
@@ -588,9 +589,33 @@ class GpuJobRunner:
         self.lazy_gen_stages = self._lazy_gen_reads()
         fused_first = {f["stages"][0]: mid for mid, f in self.fused.items()}
         active_fused = {}
+        self.fused_joins = FJ.find(self.plan) if self.gpu_ok else {}
+        join_first = {min(d["stages"]): jid for jid, d in self.fused_joins.items()}
+        precomputed = {}
         for s in self.plan.stages:
             t0 = time.time()
             status, err = 0, ""
+            if s.id in join_first:
+                out = self._try_fused_join(self.fused_joins[join_first[s.id]])
+                if out is not None:
+                    precomputed[join_first[s.id]] = out
+                    self.skipped.update(self.fused_joins[join_first[s.id]]["stages"])
+                    self.timings[f"{join_first[s.id]}:Join(fused grace join)"] = time.time() - t0
+            if s.id in precomputed:
+                refresh()
+                rest = self.fused_joins[s.id]["rest"]
+                for p, v in precomputed.pop(s.id).items():
+                    vctx = GpuVertexContext(p, s.partitions, self.vids[s.id][p], 0, s, self.dev, self.world, self)
+                    for op in rest:                 # the join stage's program after the aggregate
+                        v = self._run_op(op, [v], vctx, s)
+                    self.channels[(s.id, p)] = v
+                for p in range(s.partitions):
+                    vid = self.vids[s.id][p]
+                    ver = ready.pop(vid)
+                    g.on_running(vid, ver, self.owner(p), now())
+                    g.on_completed(vid, ver, now(), 0, 0)
+                self._release(s)
+                continue
             if s.id in fused_first:
                 mid = fused_first[s.id]
                 if self._fused_applicable(self.fused[mid]):
@@ -694,7 +719,25 @@ class GpuJobRunner:
                 self.pool.release(b)
         return dict(committed=committed, fallbacks=self.fallbacks, timings=self.timings, transports=self.transports,
                     statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()],
-                    external_sort=getattr(self, "extsort_stats", None))
+                    external_sort=getattr(self, "extsort_stats", None), join=getattr(self, "join_stats", None))
+
+    def _try_fused_join(self, desc):
+        """Run a Join + aggregate idiom as one fused grace join stage (runtime/fused_join.py) when
+        every rank can; None (the plan's stages run as compiled) otherwise."""
+        lay = FJ.vote(desc, self)
+        if lay is None:
+            return None
+        out, err = None, None
+        try:
+            out = FJ.run(desc, self, lay)
+        except Exception as e:  # noqa: BLE001
+            err = e
+            log.warning("fused grace join failed, running the compiled stages: %s", e)
+        ok = [err is None]
+        if self.world.size > 1:
+            ok = [None] * self.world.size
+            dist.all_gather_object(ok, err is None)
+        return out if all(ok) else None
 
     def _release(self, s):
         later = {i.src for st in self.plan.stages if st.id > s.id for i in st.inputs}

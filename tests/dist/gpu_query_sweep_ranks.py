@@ -101,6 +101,11 @@ def queries():
         "apply_per_partition": (lambda c, W: c.FromEnumerable(DATA).ApplyPerPartition(
             lambda xs: [x % 7 for x in xs if x % 3]).Select(lambda x: x * 2), False),
         "range_partition": (lambda c, W: c.FromEnumerable(DATA).RangePartition(lambda x: x, 3), False),
+        # the fused grace join stage (runtime/fused_join.py): rank routing over the exchange
+        "join_sum_fused": (lambda c, W: [c.FromStore("gen://records64?count=80000&partitions=%d&keys=80000&seed=41"
+                                                     "&mode=dim" % W).Join(
+            c.FromStore("gen://records64?count=120000&partitions=%d&keys=80000&seed=42" % W), lambda r: r[0],
+            lambda s: s[0], lambda r, s: r[1] + 2 * s[1]).Sum()], True),
     }
 
 

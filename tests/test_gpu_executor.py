@@ -239,3 +239,60 @@ def test_additive_aggregate_overflow_goes_to_host():
     c2 = _ctx()
     assert c2.FromEnumerable(small).Aggregate(7, lambda a, x: a + x) == 7 + sum(small)
     assert not _fallback_ops(c2)
+
+
+def _join_stats(c):
+    return c._get_executor().last_result.get("join")
+
+
+@pytest.mark.parametrize("budget", [None, 1 << 20])
+def test_fused_grace_join_sum_matches_oracle(budget):
+    """Join(...).Sum() over generator tables runs as ONE fused grace / radix join stage (selectors
+    traced to the key and value fields), with every bucket spilled to host DRAM when the HBM budget
+    is tiny; the result equals the LocalDebug oracle's."""
+    R = "gen://records64?count=300000&partitions=1&keys=300000&seed=11&mode=dim"
+    S = "gen://records64?count=500000&partitions=1&keys=300000&seed=12"
+
+    def q(c):
+        return c.FromStore(R).Join(c.FromStore(S), lambda r: r[0], lambda s: s[0], lambda r, s: r[1] + s[1]).Sum()
+    c = _ctx()
+    if budget:
+        c.HbmBudgetBytes = budget
+    assert q(c) == q(_local())
+    st = _join_stats(c)
+    assert st is not None and st["matches"] == 500000, st
+    if budget:
+        assert st["spilled_bytes"] > 0 and not st["in_hbm"], st
+    assert not c._get_executor().last_result["fallbacks"]
+
+
+def test_fused_grace_join_aggregates_and_layouts():
+    """Count / Average / composed Select + Sum selectors, different key and value fields per side
+    (key+value row layout), and a tuple-table hbm:// source; all against the oracle."""
+    R = "gen://records64?count=120000&partitions=2&keys=50000&seed=21"
+    S = "gen://records64?count=90000&partitions=2&keys=50000&seed=22"
+    cases = [
+        lambda c: c.FromStore(R).Join(c.FromStore(S), lambda r: r[0], lambda s: s[0], lambda r, s: r[2]).Count(),
+        lambda c: c.FromStore(R).Join(c.FromStore(S), lambda r: r[0], lambda s: s[0],
+                                      lambda r, s: 3 * r[5] - s[2] + 7).Sum(),
+        lambda c: c.FromStore(R).Join(c.FromStore(S), lambda r: r[0], lambda s: s[0],
+                                      lambda r, s: r[1] - s[1]).Select(lambda x: x * 2).Sum(lambda x: x + 1),
+        lambda c: c.FromStore(R).Join(c.FromStore(S), lambda r: r[0], lambda s: s[0], lambda r, s: s[3]).Average(),
+    ]
+    for build in cases:
+        c = _ctx(2)
+        got, exp = build(c), build(_local())
+        assert got == exp or abs(got - exp) <= 1e-9 * abs(exp), (got, exp)
+        assert _join_stats(c) is not None
+
+
+def test_fused_join_falls_back_for_non_linear_selector():
+    R = "gen://records64?count=20000&partitions=1&keys=5000&seed=31"
+    S = "gen://records64?count=20000&partitions=1&keys=5000&seed=32"
+
+    def q(c):
+        return c.FromStore(R).Join(c.FromStore(S), lambda r: r[0], lambda s: s[0],
+                                   lambda r, s: r[1] * s[1] % 1000).Sum()
+    c = _ctx()
+    assert q(c) == q(_local())
+    assert _join_stats(c) is None
