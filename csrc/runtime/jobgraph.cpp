@@ -152,6 +152,8 @@ void JobGraph::on_running(int v, int version, int worker, double now) {
   Vertex& x = vertices_.at(v);
   auto f = x.attempts.find(version);
   if (f == x.attempts.end()) return;
+  // an attempt cancelled meanwhile (gang restart, lost duplicate) stays cancelled
+  if (f->second.state == VState::Cancelled || f->second.state == VState::Failed) return;
   f->second.state = VState::Running;
   f->second.worker = worker;
   f->second.start = now;

@@ -56,6 +56,35 @@ class BufferSet:
         return self.bufs.capacity
 
 
+# HBM kept free next to a sort working set: RCCL's own buffers are allocated at communicator
+# creation (before this check runs), this covers the sampler, separators, kernel workspaces and
+# the caching allocator's rounding
+RESERVE_BYTES = 2 << 30
+
+
+def working_set_bytes(capacity: int, stride: int) -> int:
+    cap = int(capacity) + 1024
+    return cap * (2 * stride + 32)
+
+
+def check_fits(capacity: int, stride: int, device) -> None:
+    """Refuse, with a clear error, an in-HBM sort working set (rows in + rows out + two entry
+    arrays) that cannot fit this GPU; e.g. 1.25e9 TeraSort rows per GPU need 293 GB of the 309 GB.
+    Larger partitions go through the out-of-core OrderBy (ops/extsort.py: ``ExternalSort=True``
+    with a host:// or partfile:// output)."""
+    if device.type != "cuda":
+        return
+    free, total = torch.cuda.mem_get_info(device)
+    need = working_set_bytes(capacity, stride)
+    if need + RESERVE_BYTES > free:
+        from ..errors import DryadLinqException, ErrorCode
+        raise DryadLinqException(
+            ErrorCode.FailedToAllocateNewNativeBuffer,
+            f"in-HBM sort of {capacity} rows x {stride} B needs {need / 1e9:.1f} GB (+{RESERVE_BYTES / 1e9:.1f} GB "
+            f"reserve) but only {free / 1e9:.1f} of {total / 1e9:.1f} GB HBM are free on {device}; use the "
+            f"out-of-core OrderBy (ExternalSort=True, host:// or partfile:// output) or more GPUs")
+
+
 class HbmPool:
     def __init__(self, device):
         self.device = device
@@ -73,6 +102,7 @@ class HbmPool:
             keep = [s for s in self.sets if s.in_use or s.pins > 0]
             self.sets = keep
             torch.cuda.empty_cache() if self.device.type == "cuda" else None
+            check_fits(capacity, stride, self.device)
             s = BufferSet(RS.SortBuffers.allocate(capacity, stride, self.device), stride)
             s.in_use = True
             self.sets.append(s)

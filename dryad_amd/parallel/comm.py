@@ -43,11 +43,19 @@ def env_world_size() -> int:
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
-def init_world(device: str | None = None, backend: str | None = None, timeout_s: int = 1800) -> World:
+# Collective timeout: a rank that dies mid-exchange is detected by its peers' RCCL watchdog within
+# this bound (the reference's process abort timeout is 30 s, DrGraphParameters.cpp:51; a 125 GB
+# all-to-all-v round takes seconds, so the bound is minutes, not the 30 of torch's default).
+COLLECTIVE_TIMEOUT_S = 300
+
+
+def init_world(device: str | None = None, backend: str | None = None, timeout_s: int = COLLECTIVE_TIMEOUT_S) -> World:
     """Initialise (idempotently) the job's process group from torchrun-style env vars.
 
     ``device``: "cuda" / "cpu" / None (cuda if available).  The backend defaults to nccl (RCCL) for
-    GPU ranks and gloo for CPU ranks."""
+    GPU ranks and gloo for CPU ranks.  RCCL runs with asynchronous error handling in tear-down mode:
+    a collective error or timeout aborts the communicator and ends the rank, so the launcher
+    (dryad-launch / torchrun) stops the whole gang instead of leaving the peers blocked."""
     global _WORLD
     if _WORLD is not None:
         return _WORLD
@@ -73,6 +81,7 @@ def init_world(device: str | None = None, backend: str | None = None, timeout_s:
         kwargs = dict(backend=be, rank=rank, world_size=size, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kwargs["device_id"] = dev
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         dist.init_process_group(**kwargs)
     _WORLD = World(rank=rank, size=size, local_rank=local_rank, device=dev, backend=be if size > 1 else None)
     return _WORLD

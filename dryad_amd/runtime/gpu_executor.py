@@ -44,6 +44,18 @@ from .executor import _BaseExecutor
 log = get_logger("gpu_executor")
 
 
+class ChannelReadError(Exception):
+    """A vertex could not read one of its input channels: the producer is blamed (DrGraph.cpp:397-413)."""
+
+    def __init__(self, edge: int, msg: str):
+        super().__init__(msg)
+        self.edge = edge
+
+
+class VertexCrash(RuntimeError):
+    """A vertex attempt died (its output is discarded and it is re-executed)."""
+
+
 class GpuVertexContext(V.VertexContext):
     def __init__(self, partition, partitions, vertex_id, version, stage, device, world, runner=None):
         super().__init__(partition, partitions, vertex_id, version, stage)
@@ -109,14 +121,26 @@ class GpuJobRunner:
         p.speculative = False            # collectives: no duplicates (a straggler holds the gang anyway)
         self.g = R.JobGraph(p)
         self.vids = []
+        self.part_of, self.stage_of = {}, {}
         for s in plan.stages:
             self.g.add_stage(f"{s.id}:{s.name}", s.partitions, False, s.is_output)
             self.vids.append([self.g.add_vertex(s.id, q) for q in range(s.partitions)])
+            for q, v in enumerate(self.vids[-1]):
+                self.part_of[v], self.stage_of[v] = q, s.id
+        self.edge_ids = {}               # (src vertex, dst vertex, input) -> JobGraph edge id
         for s in plan.stages:
             for q in range(s.partitions):
                 for ii, si in enumerate(s.inputs):
                     for src in self._sources(si, q):
+                        self.edge_ids[(self.vids[si.src][src], self.vids[s.id][q], ii)] = len(self.edge_ids)
                         self.g.add_edge(self.vids[si.src][src], 0, self.vids[s.id][q], ii)
+        # gangs (DrGang, DrCohort.cpp:852): the members of one collective exchange restart together
+        self.gang_stages = set()
+        for s in plan.stages:
+            if any(si.kind == "cross" for si in s.inputs) and s.partitions > 1:
+                self.g.set_gang(self.vids[s.id])
+                self.gang_stages.add(s.id)
+        self.recovery: list = []         # recovery actions taken (tests / statistics)
 
     def owner(self, p: int) -> int:
         return p % self.world.size
@@ -363,21 +387,32 @@ class GpuJobRunner:
             return val[k]
         return val
 
-    def _gather_inputs(self, s):
-        """Deliver every input channel of every local vertex of stage s (collectives included)."""
+    def _gather_inputs(self, s, only=None, recover=False):
+        """Deliver every input channel of every local vertex of stage s (collectives included);
+        ``only``: just these partitions (re-execution).  Source channels released after an earlier
+        delivery are rebuilt from lineage first (all ranks release in lockstep)."""
         W, me = self.world.size, self.world.rank
-        local = [p for p in range(s.partitions) if self.owner(p) == me]
+        local = [p for p in range(s.partitions) if self.owner(p) == me and (only is None or p in only)]
         inputs = {p: [[] for _ in s.inputs] for p in local}
         for ii, si in enumerate(s.inputs):
             src_stage = self.plan.stages[si.src]
+            if recover:      # (collective vote: a rank that owns no source partition still takes part)
+                mine = [q for q in range(src_stage.partitions) if self.owner(q) == me]
+                miss = [any((si.src, q) not in self.channels for q in mine)]
+                if W > 1:
+                    miss = [None] * W
+                    dist.all_gather_object(miss, any((si.src, q) not in self.channels for q in mine))
+                if any(miss):
+                    self._rematerialize(si.src)
             if si.kind == "cross" and W > 1:
                 got = self._exchange_cross(si, src_stage, s)
                 for p in local:
                     inputs[p][ii] = got[p]
                 continue
             # which (src q -> dst p) items cross ranks?
+            dst_parts = range(s.partitions) if only is None else only
             need_remote = False
-            for p in range(s.partitions):
+            for p in dst_parts:
                 for q in self._sources(si, p):
                     if self.owner(q) != self.owner(p):
                         need_remote = True
@@ -387,7 +422,7 @@ class GpuJobRunner:
                 continue
             # merge / broadcast / remote pointwise edges: every rank sends each port value another
             # rank needs once (a q feeding several of its partitions travels once)
-            need = [sorted({q for p in range(s.partitions) if self.owner(p) == r for q in self._sources(si, p)
+            need = [sorted({q for p in dst_parts if self.owner(p) == r for q in self._sources(si, p)
                             if self.owner(q) != r}) for r in range(W)]
             mine = {q: self._port_of(si, self.channels[(si.src, q)], None) for r in range(W) for q in need[r]
                     if self.owner(q) == me}
@@ -511,10 +546,17 @@ class GpuJobRunner:
         objs = [x if isinstance(x, list) else _to_objects(x) for x in streams]
         return [y for o in objs for y in o]
 
-    def run_vertex(self, s, p, version, raw_inputs):
-        fault = self._fault(s, p, version)
+    def run_vertex(self, s, p, version, raw_inputs, inject=True):
+        fault = self._fault(s, p, version) if inject else None
         if fault == "fail":
             raise RuntimeError(f"injected vertex failure {s.name}[{p}] v{version}")
+        if fault and fault.startswith("slow"):
+            time.sleep(float(fault.split(":")[1]) if ":" in fault else 1.0)
+        if fault == "read_error" and s.inputs:
+            q = next(iter(self._sources(s.inputs[0], p)), None)
+            if q is not None:
+                raise ChannelReadError(self.edge_ids[(self.vids[s.inputs[0].src][q], self.vids[s.id][p], 0)],
+                                       f"injected read error on the channel {s.inputs[0].src}[{q}] -> {s.id}[{p}]")
         vctx = GpuVertexContext(p, s.partitions, self.vids[s.id][p], version, s, self.dev, self.world, self)
         inputs = [self._merge_streams(si, streams) for si, streams in zip(s.inputs, raw_inputs)]
         data = None
@@ -523,6 +565,8 @@ class GpuJobRunner:
                 args = inputs if i == 0 else [data]
                 with TRC.range(op["op"]):
                     data = self._run_op(op, args, vctx, s)
+        if fault == "crash":        # the attempt dies after doing its work: its output must not be used
+            raise VertexCrash(f"injected crash of {s.name}[{p}] v{version} (output discarded)")
         return data
 
     def _run_op(self, op, args, vctx, s):
@@ -668,47 +712,7 @@ class GpuJobRunner:
                     torch.cuda.synchronize(self.dev)
                 self.timings[f"{s.id}:{s.name}(fused OrderBy)"] = time.time() - t0
                 continue
-            raw = self._gather_inputs(s)
-            refresh()
-            for p in sorted(raw):
-                vid = self.vids[s.id][p]
-                while True:
-                    ver = ready.pop(vid)
-                    g.on_running(vid, ver, me, now())
-                    try:
-                        out = self.run_vertex(s, p, ver, raw[p])
-                        self.channels[(s.id, p)] = out if out is not None else []
-                        g.on_completed(vid, ver, now(), 0, _object_bytes(out))
-                        break
-                    except Exception as e:  # noqa: BLE001
-                        g.on_failed(vid, ver, now(), -1, f"{type(e).__name__}: {e}")
-                        self._last_exc = e
-                        if getattr(e, "retriable", True) is False:
-                            status, err = 2, str(e)      # deterministic refusal: re-running cannot help
-                            break
-                        if g.failed():
-                            status, err = 1, g.failure()
-                            break
-                        refresh()
-                        log.warning("vertex %s[%d] v%d failed, re-executing: %s", s.name, p, ver, e)
-                if status:
-                    break
-            # stage barrier: every rank learns whether a vertex of the stage failed for good
-            st = torch.tensor([status], dtype=torch.int64,
-                              device=self.dev if self.world.backend == "nccl" else "cpu")
-            shuffle.all_reduce_(st, "max", self.world)
-            if int(st.item()) != 0:
-                if status == 2:
-                    raise self._last_exc
-                raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed,
-                                            err or f"job aborted: a vertex of stage {s.name} failed on another rank",
-                                            inner=getattr(self, "_last_exc", None))
-            for p in range(s.partitions):          # replicate remote completions into the local graph
-                if self.owner(p) != me:
-                    vid = self.vids[s.id][p]
-                    ver = ready.pop(vid)
-                    g.on_running(vid, ver, self.owner(p), now())
-                    g.on_completed(vid, ver, now(), 0, 0)
+            self._run_stage(s, ready, refresh, now)
             self._release(s)
             if self.gpu_ok:
                 torch.cuda.synchronize(self.dev)
@@ -719,7 +723,123 @@ class GpuJobRunner:
                 self.pool.release(b)
         return dict(committed=committed, fallbacks=self.fallbacks, timings=self.timings, transports=self.transports,
                     statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()],
-                    external_sort=getattr(self, "extsort_stats", None), join=getattr(self, "join_stats", None))
+                    external_sort=getattr(self, "extsort_stats", None), join=getattr(self, "join_stats", None),
+                    recovery=self.recovery)
+
+    # ------------------------------------------------------------------ fault-tolerant stage execution
+    def _run_stage(self, s, ready, refresh, now):
+        """Run every vertex of stage s to completion, SPMD.  Rounds: each rank runs one attempt of
+        each of its ready vertices, the attempt reports are all-gathered and every rank replays all
+        of them, in rank order, on its JobGraph, so the version state machine (DrVertex.cpp:1042-1171,
+        DrGraph.cpp:392-456) reaches identical decisions everywhere without further messages:
+
+          * a failed attempt is re-executed from the same delivered inputs (HBM-resident), up to
+            MaxVertexFailures, then the job aborts on every rank;
+          * a failure inside a gang stage (a collective exchange's consumers) restarts every member;
+          * a read error blames the producing vertex: its completed version is invalidated and it
+            is re-executed on its owner (its own inputs re-delivered, released channels rebuilt from
+            lineage), then the channel is delivered again.
+        """
+        g, W, me = self.g, self.world.size, self.world.rank
+        local = [p for p in range(s.partitions) if self.owner(p) == me]
+        raw, need_gather = None, True
+        while True:
+            if need_gather:
+                raw = self._gather_inputs(s, recover=raw is not None)
+                need_gather = False
+            refresh()
+            results, report = {}, []
+            for p in local:
+                vid = self.vids[s.id][p]
+                if g.completed_version(vid) >= 0 or vid not in ready:
+                    continue
+                ver = ready[vid]
+                try:
+                    results[vid] = self.run_vertex(s, p, ver, raw[p])
+                    report.append((vid, ver, "ok", -1, "", True))
+                except ChannelReadError as e:
+                    report.append((vid, ver, "read_error", e.edge, str(e), True))
+                except Exception as e:  # noqa: BLE001
+                    self._last_exc = e
+                    report.append((vid, ver, "fail", -1, f"{type(e).__name__}: {e}",
+                                   getattr(e, "retriable", True) is not False))
+            reports = [report]
+            if W > 1:
+                reports = [None] * W
+                dist.all_gather_object(reports, report)
+            fatal, blamed = None, []
+            for r in range(W):
+                for vid, ver, kind, edge, err, retriable in reports[r]:
+                    ready.pop(vid, None)
+                    g.on_running(vid, ver, r, now())
+                    if kind == "ok":
+                        accepted, _ = g.on_completed(vid, ver, now(), 0, 0)
+                        if accepted and r == me:
+                            out = results[vid]
+                            self.channels[(s.id, self.part_of[vid])] = out if out is not None else []
+                        continue
+                    if not retriable and fatal is None:
+                        fatal = (r, err)
+                    o = g.on_failed(vid, ver, now(), edge, err)
+                    if o.action == 1:
+                        blamed.append(o.invalidated_vertex)
+                        self.recovery.append(("upstream", s.name, self.part_of[vid], o.invalidated_vertex))
+                    elif s.id in self.gang_stages:
+                        self.recovery.append(("gang_restart", s.name, self.part_of[vid]))
+                    else:
+                        self.recovery.append(("retry", s.name, self.part_of[vid]))
+                    log.warning("vertex %s[%d] v%d failed (%s): %s", s.name, self.part_of[vid], ver, kind, err)
+            if fatal is not None:
+                if fatal[0] == me:
+                    raise self._last_exc
+                raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed,
+                                            f"job aborted: a vertex of stage {s.name} failed on rank {fatal[0]}: "
+                                            f"{fatal[1]}")
+            if g.failed():
+                raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed, g.failure(),
+                                            inner=getattr(self, "_last_exc", None))
+            for pv in sorted(set(blamed)):
+                self._reexecute(pv, ready, refresh, now)
+                need_gather = True
+            if all(g.completed_version(v) >= 0 for v in self.vids[s.id]):
+                return
+
+    def _reexecute(self, vid, ready, refresh, now):
+        """Collective: re-run one invalidated producer vertex on its owner (DrVertex.cpp:1135-1158),
+        its inputs delivered again (and rebuilt from lineage where they were released)."""
+        st, p = self.plan.stages[self.stage_of[vid]], self.part_of[vid]
+        me = self.world.rank
+        raw = self._gather_inputs(st, only=[p], recover=True)
+        refresh()
+        ver = ready.pop(vid)
+        self.g.on_running(vid, ver, self.owner(p), now())
+        ok, err = True, ""
+        if self.owner(p) == me:
+            try:
+                out = self.run_vertex(st, p, ver, raw[p])
+                self.channels[(st.id, p)] = out if out is not None else []
+            except Exception as e:  # noqa: BLE001
+                ok, err = False, f"{type(e).__name__}: {e}"
+        oks = [(ok, err)]
+        if self.world.size > 1:
+            oks = [None] * self.world.size
+            dist.all_gather_object(oks, (ok, err))
+        bad = next((x for x in oks if not x[0]), None)
+        if bad is not None:
+            raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed,
+                                        f"re-execution of {st.name}[{p}] after a read error failed: {bad[1]}")
+        self.g.on_completed(vid, ver, now(), 0, 0)
+
+    def _rematerialize(self, sid):
+        """Collective: rebuild a stage's released output channels from lineage (its inputs, rebuilt
+        recursively) so an input can be delivered again after a read error.  A cache refill, not a
+        new vertex version: no JobGraph attempt is recorded."""
+        st = self.plan.stages[sid]
+        raw = self._gather_inputs(st, recover=True)
+        for p, streams in raw.items():
+            self.channels[(sid, p)] = self.run_vertex(st, p, max(0, self.g.completed_version(self.vids[sid][p])),
+                                                      streams, inject=False)
+        self.recovery.append(("rematerialize", st.name))
 
     def _try_fused_join(self, desc):
         """Run a Join + aggregate idiom as one fused grace join stage (runtime/fused_join.py) when

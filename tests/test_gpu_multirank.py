@@ -68,3 +68,18 @@ def test_exchange_ranks_share_one_gpu(ranks):
     _dump(os.path.basename(out.args[-1]) + str(len(out.args)), out)
     assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
     assert f"EXCHANGE_OK {ranks}" in out.stdout
+
+
+@pytest.mark.timeout(500)
+@pytest.mark.parametrize("ranks", [1, 2])
+def test_fault_kinds_on_gpu_ranks(ranks):
+    """fail / read_error / crash / slow injected into the GPU executor on GPU ranks (device tables,
+    device exchange): oracle-equal results and the expected recovery mechanism."""
+    env = dict(os.environ, DRYAD_DIST_BACKEND="gloo", PYTHONPATH=ROOT, SPMD_DEVICE="cuda")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+                          "--master-addr", "127.0.0.1", "--master-port", str(29680 + ranks),
+                          os.path.join(ROOT, "tests", "dist", "gpu_faults_ranks.py")],
+                         capture_output=True, text=True, timeout=480, env=env, cwd=ROOT)
+    _dump("faults%d" % ranks, out)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
+    assert f"FAULTS_OK {ranks}" in out.stdout

@@ -49,3 +49,16 @@ def test_exchange_gloo(ranks):
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert f"EXCHANGE_OK {ranks}" in r.stdout
+
+
+@pytest.mark.parametrize("ranks", [1, 2])
+def test_gpu_executor_fault_kinds_gloo(ranks):
+    """Every fault kind (fail, read_error, crash, slow) on the SPMD GPU executor's stage machinery
+    (CPU ranks over gloo): oracle-equal results and the expected recovery mechanism."""
+    env = dict(os.environ, SPMD_DEVICE="cpu", DRYAD_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tests", "dist", "gpu_faults_ranks.py")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert f"FAULTS_OK {ranks}" in r.stdout
