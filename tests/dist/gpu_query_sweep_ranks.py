@@ -150,9 +150,11 @@ def main():
             print(f"[sweep] {name}: {'ok' if ok else 'MISMATCH'} ({len(a)} rows)", flush=True)
     if w.device.type == "cuda" and W > 1:
         bad += memory_check(g, w)
-    allbad = [None] * W
-    import torch.distributed as dist
-    dist.all_gather_object(allbad, bad)
+    allbad = [bad]
+    if W > 1:
+        import torch.distributed as dist
+        allbad = [None] * W
+        dist.all_gather_object(allbad, bad)
     if w.rank == 0:
         flat = [x for b in allbad for x in b]
         assert not flat, flat
