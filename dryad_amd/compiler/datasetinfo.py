@@ -48,6 +48,9 @@ class PartitionInfo:
     # split long runs of equal keys over several ranks (skew), which keeps the global order but
     # not the co-location.
     origin: dict | None = field(default=None, compare=False, repr=False)
+    # sampled range partitions: identity of the separator stage that cut the key space (two data
+    # sets range-partitioned by the SAME sampled separators are co-partitioned)
+    seps_id: int | None = field(default=None, compare=False, repr=False)
 
     @staticmethod
     def random(count: int) -> "PartitionInfo":
@@ -58,8 +61,9 @@ class PartitionInfo:
         return PartitionInfo(PartitionType.HASH, count, key, comparer)
 
     @staticmethod
-    def range(key, count, separators=None, descending=False, comparer=None, origin=None) -> "PartitionInfo":
-        return PartitionInfo(PartitionType.RANGE, count, key, comparer, separators, descending, origin)
+    def range(key, count, separators=None, descending=False, comparer=None, origin=None,
+              seps_id=None) -> "PartitionInfo":
+        return PartitionInfo(PartitionType.RANGE, count, key, comparer, separators, descending, origin, seps_id)
 
     def rely_on_colocation(self):
         """A consumer elides a shuffle because equal keys share a partition: the producing range
@@ -88,8 +92,9 @@ class PartitionInfo:
         if self.kind == PartitionType.HASH and other.kind == PartitionType.HASH:
             return True   # same hash function and count; keys compared by the caller
         if self.kind == PartitionType.RANGE and other.kind == PartitionType.RANGE:
-            ok = (self.separators is not None and self.separators == other.separators
-                  and self.descending == other.descending)
+            same = (self.separators is not None and self.separators == other.separators) or (
+                self.seps_id is not None and self.seps_id == other.seps_id)
+            ok = same and self.descending == other.descending
             if ok:
                 self.rely_on_colocation()
                 other.rely_on_colocation()

@@ -69,6 +69,7 @@ class Planner:
         self.memo: dict = {}
         self.nodes: list = []
         self.outputs: list = []
+        self.seps_nodes: dict = {}        # id -> separator PNode of each sampled range partition
 
     # ------------------------------------------------------------------ node helpers
     def _new(self, name, partitions, inputs=(), ops=(), info=None, out_ports=1, dtype=None) -> PNode:
@@ -99,7 +100,22 @@ class Planner:
         m.gang = True
         return m
 
-    def range_shuffle(self, src: PNode, key, comparer, descending, n, separators=None, name="RangePartition"):
+    def range_shuffle(self, src: PNode, key, comparer, descending, n, separators=None, name="RangePartition",
+                      seps_node: PNode | None = None):
+        """Range partition (two-phase sampling unless ``separators`` are given).  ``seps_node``:
+        reuse another data set's sampled separators (co-range partitioning for a join / set
+        operation against a range-partitioned input, DryadLinqQueryGen.cs:1487-1512)."""
+        if seps_node is not None:
+            part = self._new(name, src.partitions, [StageInput(src, "pointwise"), StageInput(seps_node, "broadcast")],
+                             [dict(op="range_partition", key=key, comparer=comparer, descending=descending,
+                                   separators=None, count=n, keep_ties=True,
+                                   explain=f"range_partition(n={n}, separators of stage '{seps_node.name}')")])
+            part.out_ports = n
+            info = DataSetInfo(PartitionInfo.range(key, n, None, descending, comparer, origin=part.ops[-1],
+                                                   seps_id=id(seps_node)))
+            m = self._new("Merge", n, [StageInput(part, "cross")], [], info, dtype=src.dtype)
+            m.gang = True
+            return m
         if separators is not None:
             n = len(separators) + 1
             part = self.pointwise(src, name, [dict(op="range_partition", key=key, comparer=comparer,
@@ -115,11 +131,32 @@ class Planner:
             part = self._new(name, src.partitions, [StageInput(src, "pointwise"), StageInput(seps, "broadcast")],
                              [dict(op="range_partition", key=key, comparer=comparer, descending=descending,
                                    separators=None, count=n, explain=f"range_partition(n={n}, sampled)")])
+            self.seps_nodes[id(seps)] = seps
         part.out_ports = n
-        info = DataSetInfo(PartitionInfo.range(key, n, separators, descending, comparer, origin=part.ops[-1]))
+        info = DataSetInfo(PartitionInfo.range(key, n, separators, descending, comparer, origin=part.ops[-1],
+                                               seps_id=id(seps) if separators is None else None))
         m = self._new("Merge", n, [StageInput(part, "cross")], [], info, dtype=src.dtype)
         m.gang = True
         return m
+
+    def range_like(self, src: PNode, key, part: PartitionInfo) -> PNode:
+        """Range-partition ``src`` by ``key`` exactly like the range-partitioned data set ``part``
+        (its explicit separators, or its sampled separator stage broadcast to this partition step)."""
+        part.rely_on_colocation()
+        if part.separators is not None:
+            return self.range_shuffle(src, key, part.comparer, part.descending, part.count, list(part.separators))
+        seps = self.seps_nodes.get(part.seps_id)
+        if seps is None:
+            return None
+        return self.range_shuffle(src, key, part.comparer, part.descending, part.count, seps_node=seps)
+
+    def local_sort(self, src: PNode, key, cmp, desc, why) -> PNode:
+        """Sort each partition (no shuffle): the other side of an ordered (merge) operator."""
+        n = self.pointwise(src, "OrderBy", [dict(op="sort", key=key, comparer=cmp, descending=desc,
+                                                 explain=f"sort{' desc' if desc else ''} per partition ({why})")],
+                           DataSetInfo(src.info.partition, OrderInfo(key, cmp, desc), src.info.distinct),
+                           dtype=src.dtype)
+        return n
 
     # ------------------------------------------------------------------ compile
     def compile(self) -> Plan:
@@ -129,6 +166,7 @@ class Planner:
             pn = self.visit(r2)
             outs.append(pn)
         self._fuse()
+        self._cleanup()
         stages = self._emit()
         plan = Plan(stages, [s.id for s in stages if s.is_output], self._globals())
         return plan
@@ -315,8 +353,17 @@ class Planner:
             d = decompose(res, elem) if res is not None else None
             if d is not None:   # lets the device run it as one partial-aggregation pass
                 gb["decomp"] = d
-            return self.pointwise(src, "GroupBy", [gb], DataSetInfo(src.info.partition if res is None else
-                                                                    PartitionInfo.random(src.partitions)))
+            why = []
+            if src.partitions > 1:
+                why.append(f"input {src.info.partition.kind.value}-partitioned by the key: no shuffle")
+            if src.info.order is not None and src.info.order.is_ordered_by(key, cmp, src.info.order.descending):
+                # OrderedGroupBy (DryadLinqQueryGen.cs:2098-2100): groups are runs of the sorted input
+                gb.update(op="ordered_group_by", explain="ordered_group_by (runs of equal keys, no hash table / sort)")
+                why.append("input ordered by the key: no sort")
+            n = self.pointwise(src, "GroupBy", [gb], DataSetInfo(src.info.partition if res is None else
+                                                                 PartitionInfo.random(src.partitions)))
+            n.explain.extend(why)
+            return n
         n = self.P
         d = decompose(res, elem) if res is not None else None
         if d is not None:
@@ -351,23 +398,61 @@ class Planner:
         return self._new(name, l.partitions, [StageInput(l, "pointwise"), StageInput(r, "pointwise")], [op],
                          info or DataSetInfo(PartitionInfo.random(l.partitions)))
 
+    def _range_copartition(self, left: PNode, lkey, right: PNode, rkey, cmp):
+        """Co-partition against a side that is already range-partitioned by its key (reference
+        DryadLinqQueryGen.cs:1487-1512: range-distribute the other side with the same
+        separators); None when neither side is."""
+        lp, rp = left.info.partition, right.info.partition
+        if lp.count > 1 and lp.kind == PartitionType.RANGE and lp.is_partitioned_by(lkey, cmp):
+            if rp.kind == PartitionType.RANGE and rp.is_partitioned_by(rkey, cmp) and lp.is_same_partition(rp):
+                return left, right, "both sides range-partitioned alike: no shuffle"
+            r2 = self.range_like(right, rkey, lp)
+            if r2 is not None:
+                return left, r2, "outer range-partitioned by the key: inner range-partitioned alike"
+        if rp.count > 1 and rp.kind == PartitionType.RANGE and rp.is_partitioned_by(rkey, cmp):
+            l2 = self.range_like(left, lkey, rp)
+            if l2 is not None:
+                return l2, right, "inner range-partitioned by the key: outer range-partitioned alike"
+        return None
+
+    def _ordered_pair(self, l: PNode, lkey, r: PNode, rkey, cmp):
+        """Merge strategy (DryadLinqQueryGen.cs:1574-1597, 1862-1880): when either side is sorted by
+        its key within each partition, sort the other side per partition -> (l, r, note) or None."""
+        lo, ro = l.info.order, r.info.order
+        if lo is not None and lo.is_ordered_by(lkey, cmp, lo.descending):
+            if ro is None or not ro.is_ordered_by(rkey, cmp, lo.descending):
+                return l, self.local_sort(r, rkey, cmp, lo.descending, "merge with the ordered outer"), \
+                    "outer ordered by the key: inner sorted per partition, merge"
+            return l, r, "both sides ordered by the key: merge (no sort)"
+        if ro is not None and ro.is_ordered_by(rkey, cmp, ro.descending):
+            return self.local_sort(l, lkey, cmp, ro.descending, "merge with the ordered inner"), r, \
+                "inner ordered by the key: outer sorted per partition, merge"
+        return None
+
     def v_Join(self, q, a, group=False):
         outer = self.visit(q.sources[0])
         inner = self.visit(q.sources[1])
         ok, ik, cmp = a["outer_key"], a["inner_key"], a.get("comparer")
-        lo, li = outer.info.order, inner.info.order
-        merge = (lo is not None and li is not None and lo.is_ordered_by(ok, cmp) and li.is_ordered_by(ik, cmp)
-                 and outer.info.partition.is_same_partition(inner.info.partition)
-                 and outer.info.partition.kind == PartitionType.RANGE)
-        if merge:
-            l, r = outer, inner
-            kind = "merge_group_join" if group else "merge_join"
+        notes = []
+        co = self._range_copartition(outer, ok, inner, ik, cmp)
+        if co is not None:
+            l, r, why = co
+            notes.append(why)
         else:
             l, r = self._copartition(outer, ok, inner, ik, cmp)
+        od = self._ordered_pair(l, ok, r, ik, cmp) if cmp is None else None
+        if od is not None:
+            l, r, why = od
+            notes.append(why)
+            kind = "merge_group_join" if group else "merge_join"
+        else:
             kind = "hash_group_join" if group else "hash_join"
-        return self._binary("GroupJoin" if group else "Join", l, r,
-                            dict(op=kind, outer_key=ok, inner_key=ik, result=a["result_selector"], comparer=cmp,
-                                 explain=kind))
+        jop = dict(op=kind, outer_key=ok, inner_key=ik, result=a["result_selector"], comparer=cmp, explain=kind)
+        if od is not None:
+            jop["descending"] = l.info.order.descending
+        node = self._binary("GroupJoin" if group else "Join", l, r, jop)
+        node.explain.extend(notes)
+        return node
 
     def v_GroupJoin(self, q, a):
         return self.v_Join(q, a, group=True)
@@ -378,11 +463,18 @@ class Planner:
         cmp = a.get("comparer")
         if src.info.distinct:
             return src
+        ordered = cmp is None and src.info.order is not None and \
+            src.info.order.is_ordered_by(_identity, None, src.info.order.descending)
         if src.info.partition.is_partitioned_by(_identity, cmp):
-            return self.pointwise(src, "Distinct", [dict(op="distinct", comparer=cmp, explain="distinct")],
-                                  DataSetInfo(src.info.partition, src.info.order, True), dtype=src.dtype)
+            op = dict(op="ordered_distinct", comparer=cmp, explain="ordered_distinct (drop adjacent duplicates)") \
+                if ordered else dict(op="distinct", comparer=cmp, explain="distinct")
+            n = self.pointwise(src, "Distinct", [op], DataSetInfo(src.info.partition, src.info.order, True),
+                               dtype=src.dtype)
+            if src.partitions > 1:
+                n.explain.append("input partitioned by the record: no shuffle")
+            return n
         partial = self.pointwise(src, "Distinct", [dict(op="distinct", comparer=cmp, explain="distinct (partial)")],
-                                 dtype=src.dtype)
+                                 DataSetInfo(src.info.partition, src.info.order, True), dtype=src.dtype)
         sh = self.hash_shuffle(partial, _identity, cmp, self.P)
         info = DataSetInfo(sh.info.partition, None, True)
         return self.pointwise(sh, "Distinct", [dict(op="distinct", comparer=cmp, explain="distinct")], info,
@@ -393,11 +485,31 @@ class Planner:
         r = self.visit(q.sources[1])
         cmp = a.get("comparer")
         if kind == "union":
-            l = self.pointwise(l, "Distinct", [dict(op="distinct", comparer=cmp, explain="distinct (partial)")], dtype=l.dtype)
-            r = self.pointwise(r, "Distinct", [dict(op="distinct", comparer=cmp, explain="distinct (partial)")], dtype=r.dtype)
-        l2, r2 = self._copartition(l, _identity, r, _identity, cmp)
-        info = DataSetInfo(l2.info.partition, None, True)
-        return self._binary(kind.capitalize(), l2, r2, dict(op=kind, comparer=cmp, explain=kind), info)
+            l = self.pointwise(l, "Distinct", [dict(op="distinct", comparer=cmp, explain="distinct (partial)")],
+                               DataSetInfo(l.info.partition, l.info.order, True), dtype=l.dtype)
+            r = self.pointwise(r, "Distinct", [dict(op="distinct", comparer=cmp, explain="distinct (partial)")],
+                               DataSetInfo(r.info.partition, r.info.order, True), dtype=r.dtype)
+        notes = []
+        co = self._range_copartition(l, _identity, r, _identity, cmp)
+        if co is not None:
+            l2, r2, why = co
+            notes.append(why)
+        else:
+            l2, r2 = self._copartition(l, _identity, r, _identity, cmp)
+        od = self._ordered_pair(l2, _identity, r2, _identity, cmp) if cmp is None else None
+        order = None
+        if od is not None:
+            l2, r2, why = od
+            notes.append(why)
+            order = l2.info.order
+            op = dict(op="ordered_" + kind, comparer=cmp, descending=order.descending,
+                      explain=f"ordered_{kind} (merge of sorted inputs)")
+        else:
+            op = dict(op=kind, comparer=cmp, explain=kind)
+        info = DataSetInfo(l2.info.partition, order, True)
+        node = self._binary(kind.capitalize(), l2, r2, op, info)
+        node.explain.extend(notes)
+        return node
 
     def v_Union(self, q, a):
         return self._setop(q, a, "union")
@@ -603,7 +715,28 @@ class Planner:
                 changed = True
                 break
 
-    # ------------------------------------------------------------------ Phase 3: emit
+    # ------------------------------------------------------------------ Phase 3: cleanup + emit
+    def _cleanup(self):
+        """Remove useless Merge nodes (DryadLinqQueryGen.cs:474-500): an op-less Merge between a
+        CrossProduct exchange and its only consumer (a Join / set operation / Apply with several
+        inputs, which fusion could not absorb) -> the consumer takes the exchange directly (one
+        vertex hop and one HBM channel fewer per partition)."""
+        for n in list(self.nodes):
+            if n.ops or n.output is not None or len(n.inputs) != 1 or n.inputs[0].kind != "cross":
+                continue
+            cons = [(m, i) for m in self.nodes for i in m.inputs if i.src is n]
+            if len(cons) != 1 or n in self.outputs:
+                continue
+            m, i = cons[0]
+            if i.kind != "pointwise" or i.port != 0 or m.partitions != n.partitions:
+                continue
+            src_in = n.inputs[0]
+            i.src, i.kind, i.port, i.merge_sort = src_in.src, "cross", src_in.port, src_in.merge_sort
+            m.gang = True
+            m.explain.append(f"{n.name} vertex elided: the exchange feeds this stage directly")
+            self.nodes.remove(n)
+
+
     def _emit(self) -> list:
         # topological order (inputs before consumers)
         order, seen = [], set()

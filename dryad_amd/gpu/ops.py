@@ -847,7 +847,56 @@ def op_group_by(op, inputs, v):
     d = op.get("decomp")
     if d is None or op.get("elem") is not None:
         raise NotTraceable("non-decomposable GroupBy")
-    tb = op_group_partial(dict(op, decomp=d), inputs, v)
+    return _finish_group(d, op_group_partial(dict(op, decomp=d), inputs, v))
+
+
+def _ordered_group_keys(kcols, skeys):
+    """Segments of an input already sorted by the key (K7, OrderedGroupBy): entries in row order,
+    groups = runs of equal keys found by adjacent comparison, no sort -> like _group_keys."""
+    if any(c.dtype not in R.KEY_TYPES or c.dim() != 1 for c in kcols):
+        raise NotTraceable("group key of a non-key dtype")
+    _row_index_fits(kcols[0].shape[0] if kcols else 0)
+    packed = None
+    if _wide(kcols):
+        fp, packed = _wide_key(kcols)
+        e, _, lo_mask = R.build_keys([fp])
+    else:
+        e, _, lo_mask = R.build_keys(kcols)
+    seg, nseg, starts = R.segment_ids(e, lo_mask)
+    rows_at_start = starts
+    if packed is not None or any(sk is not None for sk in skeys):
+        rep = rows_at_start.index_select(0, seg)
+        idx = torch.arange(e.shape[0], device=e.device)
+        if packed is not None and _rows_differ(packed, idx, packed, rep):
+            raise NotTraceable("wide key fingerprint collision")
+        from ..ops.fingerprint import strings_differ
+        for sk in skeys:
+            if sk is not None and strings_differ((sk.heap, sk.off, sk.len), idx, (sk.heap, sk.off, sk.len), rep):
+                raise NotTraceable("string key fingerprint collision")
+    return e, seg, nseg, rows_at_start, starts
+
+
+def op_ordered_group_by(op, inputs, v):
+    """OrderedGroupBy (reference DryadLinqVertex.cs:586-760): the partition is sorted by the key,
+    so every group is a run: one adjacent-difference pass + one segmented reduction."""
+    d = op.get("decomp")
+    if d is None or op.get("elem") is not None:
+        raise NotTraceable("non-decomposable GroupBy")
+    t = _check(_one(inputs))
+    if op.get("comparer") is not None or any(a.kind not in _GPU_AGGS for a in d.aggs):
+        raise NotTraceable("aggregate not supported on the device")
+    if t.n == 0:
+        raise NotTraceable("empty partition")
+    kcols, skeys, form = _key_cols(t, op["key"])
+    specs, names = _group_specs(d, t)
+    srt, seg, nseg, rows_at_start, starts = _ordered_group_keys(kcols, skeys)
+    out, strs = _key_outputs(kcols, skeys, rows_at_start, srt, starts)
+    for nm, res in zip(names, R.seg_reduce_multi(srt, seg, nseg, specs)):
+        out[nm] = res
+    return _finish_group(d, _partial_table(out, strs, d, len(kcols), form))
+
+
+def _finish_group(d, tb):
     nkeys = tb.shape.pytype.nkeys
     keys = _key_values(tb, nkeys)
     vals = []
@@ -937,6 +986,44 @@ def _set_op(kind, op, inputs):
 
 def op_union(op, inputs, v):
     return _set_op("union", op, inputs)
+
+
+def op_ordered_distinct(op, inputs, v):
+    """Distinct of a partition sorted by the record: keep the first of every run (no sort)."""
+    t = _check(_one(inputs))
+    if op.get("comparer") is not None:
+        raise NotTraceable("custom comparer")
+    if t.n <= 1:
+        return t
+    e, _, lo_mask, packed = _record_entries(t)
+    seg, _, starts = R.segment_ids(e, lo_mask)
+    _verify_segments(packed, e, seg, starts)
+    return t.take(starts)
+
+
+def _ordered_set(kind, op, inputs):
+    """Ordered set operations: the device set operation emits records in ascending key order,
+    which is the order the planner promised for ascending, non-fingerprinted records."""
+    if op.get("descending"):
+        raise NotTraceable("descending ordered set operation")
+    a = _check(inputs[0])
+    cols = [a.cols[f] for f in a.shape.fields] if a.rows is None else []
+    if a.rows is not None and a.rows.shape[1] > 12 or a.rows is None and (_wide(cols) or any(
+            c.dim() != 1 or c.dtype not in R.KEY_TYPES for c in cols)):
+        raise NotTraceable("fingerprinted records: key order is not record order")
+    return _set_op(kind, op, inputs)
+
+
+def op_ordered_union(op, inputs, v):
+    return _ordered_set("union", op, inputs)
+
+
+def op_ordered_intersect(op, inputs, v):
+    return _ordered_set("intersect", op, inputs)
+
+
+def op_ordered_except(op, inputs, v):
+    return _ordered_set("except", op, inputs)
 
 
 def op_intersect(op, inputs, v):

@@ -150,11 +150,19 @@ def find(plan) -> dict:
             continue
         if j.ops[k]["spec"].get("predicate") is not None or j.ops[0].get("comparer") is not None:
             continue
-        if len(j.inputs) != 2 or any(i.kind != "pointwise" for i in j.inputs):
+        if len(j.inputs) != 2:
             continue
         sides = []
         for inp in j.inputs:
             m = st[inp.src]
+            if inp.kind == "cross":           # Merge vertex elided by the planner's cleanup
+                if [o["op"] for o in m.ops] != ["read", "hash_partition"] or m.inputs or \
+                        plan.consumers(m.id) != [j.id]:
+                    break
+                sides.append((m, None))
+                continue
+            if inp.kind != "pointwise":
+                break
             if [o["op"] for o in m.ops] == ["read"] and not m.inputs and plan.consumers(m.id) == [j.id] \
                     and not m.is_output:
                 sides.append((m, None))

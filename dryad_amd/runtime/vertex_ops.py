@@ -242,8 +242,9 @@ def op_hash_group_join(op, inputs, v):
     return list(E.GroupJoin(inputs[0], inputs[1], op["outer_key"], op["inner_key"], op["result"], op.get("comparer")))
 
 
-def _merge_join_iter(outer, inner, ok, ik, cmp):
-    c = E.compare_fn(cmp)
+def _merge_join_iter(outer, inner, ok, ik, cmp, descending=False):
+    c0 = E.compare_fn(cmp)
+    c = (lambda a, b: -c0(a, b)) if descending else c0
     j = 0
     n = len(inner)
     for x in outer:
@@ -260,7 +261,8 @@ def _merge_join_iter(outer, inner, ok, ik, cmp):
 
 def op_merge_join(op, inputs, v):
     out, r = [], op["result"]
-    for x, group in _merge_join_iter(inputs[0], inputs[1], op["outer_key"], op["inner_key"], op.get("comparer")):
+    for x, group in _merge_join_iter(inputs[0], inputs[1], op["outer_key"], op["inner_key"], op.get("comparer"),
+                                     op.get("descending", False)):
         for y in group:
             out.append(r(x, y))
     return out
@@ -269,7 +271,7 @@ def op_merge_join(op, inputs, v):
 def op_merge_group_join(op, inputs, v):
     r = op["result"]
     return [r(x, E.LinqList(g)) for x, g in _merge_join_iter(inputs[0], inputs[1], op["outer_key"], op["inner_key"],
-                                                  op.get("comparer"))]
+                                                  op.get("comparer"), op.get("descending", False))]
 
 
 # ---------------------------------------------------------------------------------------------
@@ -288,6 +290,63 @@ def op_intersect(op, inputs, v):
 
 def op_except(op, inputs, v):
     return list(E.Except(inputs[0], inputs[1], op.get("comparer")))
+
+
+# ordered strategies (reference OrderedGroupBy / OrderedDistinct / Ordered* set operations,
+# DryadLinqVertex.cs:586-760, 1232-1597): the inputs are sorted by the key (record), so groups
+# are runs and set operations are merges; no hash table, output stays sorted
+def op_ordered_group_by(op, inputs, v):
+    key, elem, res, cmp = op["key"], op.get("elem"), op.get("result"), op.get("comparer")
+    wrap = E.eq_wrapper(cmp)
+    out, cur, wk = [], None, None
+    for x in _one(inputs):
+        k = key(x)
+        w = wrap(k)
+        if cur is None or w != wk:
+            cur, wk = E.Grouping(k), w
+            out.append(cur)
+        cur.append(elem(x) if elem is not None else x)
+    return out if res is None else [res(g.Key, g) for g in out]
+
+
+def op_ordered_distinct(op, inputs, v):
+    out, last, first = [], None, True
+    for x in _one(inputs):
+        if first or x != last:
+            out.append(x)
+        last, first = x, False
+    return out
+
+
+def _ordered_merge(a, b, descending):
+    """(x, in_a, in_b) over the distinct records of two sorted sequences, in their order."""
+    c0 = E.compare_fn(None)
+    c = (lambda x, y: -c0(x, y)) if descending else c0
+    a, b = op_ordered_distinct(None, [a], None), op_ordered_distinct(None, [b], None)
+    i = j = 0
+    while i < len(a) or j < len(b):
+        if j >= len(b) or (i < len(a) and c(a[i], b[j]) < 0):
+            yield a[i], True, False
+            i += 1
+        elif i >= len(a) or c(a[i], b[j]) > 0:
+            yield b[j], False, True
+            j += 1
+        else:
+            yield a[i], True, True
+            i += 1
+            j += 1
+
+
+def op_ordered_union(op, inputs, v):
+    return [x for x, _, _ in _ordered_merge(inputs[0], inputs[1], op.get("descending", False))]
+
+
+def op_ordered_intersect(op, inputs, v):
+    return [x for x, ia, ib in _ordered_merge(inputs[0], inputs[1], op.get("descending", False)) if ia and ib]
+
+
+def op_ordered_except(op, inputs, v):
+    return [x for x, ia, ib in _ordered_merge(inputs[0], inputs[1], op.get("descending", False)) if ia and not ib]
 
 
 def op_zip(op, inputs, v):

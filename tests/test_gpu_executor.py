@@ -296,3 +296,20 @@ def test_fused_join_falls_back_for_non_linear_selector():
     c = _ctx()
     assert q(c) == q(_local())
     assert _join_stats(c) is None
+
+
+def test_ordered_strategies_on_device():
+    """OrderBy(k).GroupBy(k) -> ordered_group_by (runs, no sort), Distinct / Union of sorted input ->
+    ordered ops, one-sided merge join: on the device, equal to the oracle, no host fallback."""
+    pairs = [(i % 61, i) for i in range(40_000)]
+    data = [(i * 7919) % 5003 for i in range(30_000)]
+    _same(lambda c: c.FromEnumerable(pairs).OrderBy(lambda t: t[0]).GroupBy(
+        lambda t: t[0], lambda k, g: (k, g.Count(), g.Sum(lambda t: t[1]))), parts=2,
+        device_ops=("ordered_group_by", "sort"))
+    _same(lambda c: c.FromEnumerable([x % 300 for x in data]).OrderBy(lambda x: x).Distinct(), parts=2,
+          device_ops=("ordered_distinct",))
+    _same(lambda c: c.FromEnumerable([x % 400 for x in data]).OrderBy(lambda x: x).Union(
+        c.FromEnumerable([x % 250 for x in data[:3000]])), parts=2, device_ops=("ordered_union",))
+    _same(lambda c: c.FromEnumerable(pairs).OrderBy(lambda t: t[0]).Join(
+        c.FromEnumerable([(k, k * 10) for k in range(0, 61, 2)]), lambda t: t[0], lambda u: u[0],
+        lambda t, u: (t[1], u[1])), parts=2, device_ops=("merge_join",))
