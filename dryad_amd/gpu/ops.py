@@ -539,15 +539,47 @@ def op_separators(op, inputs, v):
     return DeviceTable.from_columns({"lo": s[:, 0].contiguous(), "hi": s[:, 1].contiguous()}, E_SHAPE)
 
 
+def _separator_entries(t: DeviceTable, key_fn, seps: list) -> torch.Tensor:
+    """User range separators (host key values, RangePartition(keySelector, rangeSeparators)) as
+    sort entries in the encoding of this partition's key columns, so the device range_dest
+    compares them exactly like the host's bisect over the same keys."""
+    if len(seps) > 255:
+        raise NotTraceable("more than 255 range separators")
+    kind, spec = TR.key_columns(TR.call(key_fn, t), t)
+    if kind == "bytes":
+        if any(not isinstance(x, (bytes, bytearray)) or len(x) != spec.length for x in seps):
+            raise NotTraceable("byte-key separators of another length")
+        rows = torch.tensor([list(x) for x in seps], dtype=torch.uint8, device=t.device).reshape(len(seps), spec.length)
+        return S.extract_keys(rows.contiguous(), 0, spec.length, 0)
+    k = len(spec)
+    cols = []
+    for j, c in enumerate(spec):
+        vals = [x[j] if k > 1 else x for x in seps]
+        if k > 1 and any(not isinstance(x, tuple) or len(x) != k for x in seps):
+            raise NotTraceable("separators do not match the composite key")
+        col = torch.tensor(vals, dtype=c.dtype, device=t.device)
+        if any(float(a) != float(b) for a, b in zip(vals, col.tolist())):
+            raise NotTraceable("separator not representable in the key column type")
+        cols.append(col)
+    e, _, _ = R.build_keys(cols, [False] * k)
+    return e
+
+
 def op_range_partition(op, inputs, v):
     t = _check(inputs[0])
     n = op["count"]
-    if op.get("separators") is not None:
-        raise NotTraceable("explicit separators are host values")
     seps_t = inputs[1] if len(inputs) > 1 else None
     if t.n == 0:
         return Ported(t, [0] * (n + 1))
     e, _, lo_mask = key_entries(t, op["key"], op.get("comparer"), False)
+    if op.get("separators") is not None:
+        seps = _separator_entries(t, op["key"], list(op["separators"]))
+        S.range_dest(e, seps, lo_mask, descending=op.get("descending", False))
+        out = partition_by_entries(t, e, n, v.world.size)
+        if out is not None:
+            return out
+        part, starts = S.partition_pass(e, 64)
+        return Ported(t.take(_perm(part)), starts[: n + 1].tolist())
     if seps_t is None or seps_t.n == 0:
         return Ported(t, [0] + [t.n] * n)
     seps_t = _entries_table(seps_t)

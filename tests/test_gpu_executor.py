@@ -313,3 +313,16 @@ def test_ordered_strategies_on_device():
     _same(lambda c: c.FromEnumerable(pairs).OrderBy(lambda t: t[0]).Join(
         c.FromEnumerable([(k, k * 10) for k in range(0, 61, 2)]), lambda t: t[0], lambda u: u[0],
         lambda t, u: (t[1], u[1])), parts=2, device_ops=("merge_join",))
+
+
+def test_range_partition_with_user_separators_on_device():
+    """RangePartition(key, separators[, descending]) with host separator values runs on the device
+    (separators encoded like the key columns; reference DryadLinqVertex.cs:4909-5151)."""
+    data = [(i * 7919) % 100_003 for i in range(50_000)]
+    pairs = [(i % 977, float(i)) for i in range(20_000)]
+    for build in (
+        lambda c: c.FromEnumerable(data).RangePartition(lambda x: x, [10_000, 50_000, 50_001, 90_000]),
+        lambda c: c.FromEnumerable(data).RangePartition(lambda x: x, [90_000, 50_000, 10_000], True),
+        lambda c: c.FromEnumerable(pairs).RangePartition(lambda t: t[0], [100, 500, 900]),
+    ):
+        c = _same(build, ordered=True, parts=2, device_ops=("range_partition",))
