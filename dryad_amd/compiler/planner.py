@@ -550,8 +550,16 @@ class Planner:
             spec["assoc"] = assoc()
         partial = self.pointwise(src, kind, [dict(op="agg_partial", spec=spec, explain=f"{kind} (partial)")])
         partial = self._aggregation_tree(partial, kind, spec)
-        return self.merge_one(partial, kind, [dict(op="agg_final", spec=spec, explain=f"{kind} (final)")]) \
-            if partial.partitions > 1 else self._append(partial, dict(op="agg_final", spec=spec, explain=f"{kind} (final)"))
+        if partial.partitions <= 1:
+            return self._append(partial, dict(op="agg_final", spec=spec, explain=f"{kind} (final)"))
+        final = self.merge_one(partial, kind, [dict(op="agg_final", spec=spec, explain=f"{kind} (final)")])
+        if kind == "Aggregate" and is_expensive(a["func"]):
+            # expensive associative fold: a dynamic aggregation tree (DryadLinqQueryNode.cs:2866-2871
+            # FullAggregator, AggregationLevels = 2; DrDynamicAggregateManager) folds the partials
+            # of each machine (GPU rank) into one before the final vertex
+            final.dynamic_manager = "FullAggregator"
+            final.explain.append("dynamic FullAggregator: partials folded per rank before the final aggregate")
+        return final
 
     def _aggregation_tree(self, partial: PNode, kind, spec) -> PNode:
         """Aggregation tree (reference DrDynamicAggregateManager, GraphBuilder.cs:633-703;

@@ -110,6 +110,7 @@ _DEFAULTS = dict(
     ExternalSort=None,            # out-of-core OrderBy to host:// (None: when the data exceeds the budget)
     AllowHostFallback=False,      # GPU executor: an op whose lambdas do not trace may run on host
     HostFallbackMaxBytes=256 << 20,  # ... records only up to this many partition bytes unless allowed
+    RerunInputsMaxBytes=1 << 30,  # inputs a failed GPU vertex's restart record may persist
     ExternalSortToDisk=None,      # its partfile:// output written through a memory-mapped part file
     #                               (None: when the output exceeds half of the available host memory)
 )

@@ -373,6 +373,14 @@ class GpuJobRunner:
             return list(range(p * si.group, min(src.partitions, (p + 1) * si.group)))
         return list(range(src.partitions))
 
+    def _combine_local(self, s, si, parts):
+        """One partial folding this rank's partials of the source stage (agg_combine)."""
+        vals = [self._port_of(si, self.channels[(si.src, q)], None) for q in parts]
+        vals = [_to_objects(v) if not isinstance(v, list) else v for v in vals]
+        vctx = GpuVertexContext(0, 1, -1, 0, s, self.dev, self.world, self)
+        return V.OPS["agg_combine"](dict(op="agg_combine", spec=s.ops[0]["spec"]), [[x for v in vals for x in v]],
+                                    vctx)
+
     # ------------------------------------------------------------------ channel transport
     def _port_of(self, si, val, dst_p):
         """Port data of one source vertex's output for a destination partition."""
@@ -419,6 +427,18 @@ class GpuJobRunner:
             if not need_remote:
                 for p in local:
                     inputs[p][ii] = [self._port_of(si, self.channels[(si.src, q)], p) for q in self._sources(si, p)]
+                continue
+            if si.kind == "merge" and s.dynamic_manager == "FullAggregator" and only is None \
+                    and s.ops and s.ops[0]["op"] == "agg_final":
+                # dynamic aggregation level 1 (DrDynamicAggregateManager machine grouping): each rank
+                # folds the partials of its own source partitions into one before the final vertex
+                mine = [q for q in range(src_stage.partitions) if self.owner(q) == me]
+                got = self._transport(s, si, [[self._combine_local(s, si, mine)] if self.owner(0) == r else []
+                                              for r in range(W)],
+                                      [[("rank", r)] if self.owner(0) == me else [] for r in range(W)])
+                for p in local:
+                    inputs[p][ii] = [x for r in range(W) for x in got[r].values()]
+                self.recovery.append(("dynamic_aggregate", s.name, len(mine)))
                 continue
             # merge / broadcast / remote pointwise edges: every rank sends each port value another
             # rank needs once (a q feeding several of its partitions travels once)
@@ -759,10 +779,12 @@ class GpuJobRunner:
                     report.append((vid, ver, "ok", -1, "", True))
                 except ChannelReadError as e:
                     report.append((vid, ver, "read_error", e.edge, str(e), True))
+                    self._dump_restart(s, p, ver, raw[p], str(e))
                 except Exception as e:  # noqa: BLE001
                     self._last_exc = e
                     report.append((vid, ver, "fail", -1, f"{type(e).__name__}: {e}",
                                    getattr(e, "retriable", True) is not False))
+                    self._dump_restart(s, p, ver, raw[p], f"{type(e).__name__}: {e}")
             reports = [report]
             if W > 1:
                 reports = [None] * W
@@ -803,6 +825,25 @@ class GpuJobRunner:
                 need_gather = True
             if all(g.completed_version(v) >= 0 for v in self.vids[s.id]):
                 return
+
+    def _dump_restart(self, s, p, ver, streams, error):
+        """Restart record of a failed GPU vertex attempt (DumpRestartCommand, dvertexpncontrol.cpp:
+        348-736): its delivered inputs persisted under ``log/rerun/vertex-V.v/`` (device tables as
+        tensor files + JSON layout, host records pickled) with the plan, so
+        ``python -m dryad_amd.tools.replay`` re-runs this one vertex standalone.  Skipped past
+        ``RerunInputsMaxBytes`` (default 1 GiB) of input."""
+        jd = getattr(self, "job_dir", None)
+        if not jd and getattr(self, "job_dir_factory", None) is not None:
+            jd = self.job_dir = self.job_dir_factory()
+        if not jd:
+            return
+        try:
+            from ..tools import replay as RP
+            nb = sum(_device_bytes(x) for inp in streams for x in inp)
+            limit = int(self.ctx._props.get("RerunInputsMaxBytes") or (1 << 30))
+            RP.dump(jd, self.plan, s, p, self.vids[s.id][p], ver, streams if nb <= limit else None, error)
+        except Exception as e:  # noqa: BLE001 (a diagnostic aid must never fail the job)
+            log.warning("could not write the restart record of %s[%d]: %s", s.name, p, e)
 
     def _reexecute(self, vid, ready, refresh, now):
         """Collective: re-run one invalidated producer vertex on its owner (DrVertex.cpp:1135-1158),
@@ -1045,6 +1086,10 @@ class GpuExecutor(_BaseExecutor):
                                                  f"output {st.output['uri']} already exists")
         runner = GpuJobRunner(self.ctx, plan, self.world, faults, self.pool)
         job_dir = self._job_dir(plan) if self.world.rank == 0 else None
+        runner.job_dir = job_dir
+        self.last_job_dir = job_dir
+        if self.ctx._props.get("KeepJobDirectories", True):
+            runner.job_dir_factory = lambda: self._rank_job_dir(plan)    # restart records of rank > 0
         t0 = time.time()
         res = None
         try:
@@ -1063,7 +1108,8 @@ class GpuExecutor(_BaseExecutor):
         if job_dir:
             st = dict(res.get("statistics") or {})
             st.update(executor="gpu", ranks=self.world.size, elapsed_s=time.time() - t0,
-                      stage_seconds=res.get("timings"), host_fallbacks=res.get("fallbacks"))
+                      stage_seconds=res.get("timings"), host_fallbacks=res.get("fallbacks"),
+                      transports=res.get("transports"), recovery=res.get("recovery"))
             with open(os.path.join(job_dir, "statistics.json"), "w") as f:
                 json.dump(st, f, indent=1, default=str)
         self.last_job_dir = job_dir
@@ -1090,6 +1136,14 @@ class GpuExecutor(_BaseExecutor):
             f.write(plan.to_xml())
         with open(os.path.join(d, "QueryGraph.txt"), "w") as f:
             f.write(plan.explain())
+        return d
+
+    def _rank_job_dir(self, plan):
+        """Job directory of a non-zero rank (only for restart records of injected-fault runs)."""
+        from .executor import dryad_home
+        d = os.path.join(dryad_home(self.ctx), "LocalJobs",
+                         f"gpu-rank{self.world.rank}-{os.getpid()}-{int(time.time() * 1000) % 10**9}")
+        os.makedirs(os.path.join(d, "log"), exist_ok=True)
         return d
 
     def enumerate(self, q):

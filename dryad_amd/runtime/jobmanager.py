@@ -118,6 +118,15 @@ class JobRunner:
             cmd["output_part"] = self.output_part_path(stage, part, vid, version)
         return cmd
 
+    def _dump_restart(self, cmd):
+        """Restart record of one vertex attempt (reference DVertexPnController::DumpRestartCommand,
+        dvertexpncontrol.cpp:348-736): the full command, so the vertex can be re-run on its own
+        from its persisted input channels with ``python -m dryad_amd.runtime.vertexhost --cmd``."""
+        d = os.path.join(self.job_dir, "log", "rerun")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"vertex-{cmd['vertex']}.{cmd['version']}.json"), "w") as f:
+            json.dump(cmd, f, indent=1, default=str)
+
     def _inputs_complete(self, vid) -> bool:
         return all(self.g.completed_version(src) >= 0 for lst in self.inputs_of[vid] for src, _, _ in lst)
 
@@ -157,6 +166,7 @@ class JobRunner:
                         still.append(it)
                         continue
                     cmd = self.command(it.vertex, it.version)
+                    self._dump_restart(cmd)
                     g.on_running(it.vertex, it.version, slot, now())
                     self.pool.send(slot, cmd)
                     running[(it.vertex, it.version)] = slot

@@ -69,16 +69,73 @@ def executions(events: list) -> list:
     return sorted(runs.values(), key=lambda r: (r["start"] if r["start"] is not None else 1e30, r["vertex"]))
 
 
+# failure classes (JobBrowser Diagnosis.cs:36-929: vertex failure diagnosis, deterministic input
+# failures, read failures per producer, aborts after too many failures, serialization errors)
+_CLASSES = [
+    ("out of memory", ("out of memory", "hipErrorOutOfMemory", "OutOfMemory", "FailedToAllocateNewNativeBuffer"),
+     "a vertex ran out of GPU memory: raise PartitionCount, lower HbmBudgetBytes, or let OrderBy go "
+     "out of core (ExternalSort=True)"),
+    ("host fallback refused", ("HostFallbackMaxBytes",),
+     "an operator could not run on the device and its input was too large for the host path: rewrite the "
+     "lambda with traceable column arithmetic or set AllowHostFallback=True"),
+    ("serialization", ("FailedToDeserialize", "UnpicklingError", "PicklingError", "GeneralSerializeFailure",
+                       "cannot serialize", "not serializable"),
+     "records could not be (de)serialized: check the record type / custom serializer"),
+    ("read failure", ("read error", "ChannelReadError", "ChannelReadFailed", "failed to read"),
+     "a vertex could not read an input channel: the producer was re-executed"),
+    ("collective / rank failure", ("NCCL", "RCCL", "ProcessGroup", "Watchdog", "timed out"),
+     "a collective exchange failed or timed out: a rank died or stalled (see the other ranks' logs)"),
+    ("user code exception", ("Error", "Exception"), "an exception was raised by a user lambda or operator"),
+]
+
+
+def _classify(err: str):
+    for name, pats, advice in _CLASSES:
+        if any(p in err for p in pats):
+            return name, advice
+    return "unknown", ""
+
+
 def diagnose(job: dict) -> list:
-    """Failure / straggler findings (JobBrowser Diagnosis.cs analogue)."""
+    """Failure / straggler findings (JobBrowser Diagnosis.cs analogue), most important first:
+    the job abort reason, per failing vertex its failure class and whether it is deterministic
+    (every attempt failed the same way = a bug, not a transient fault), read failures grouped by
+    the blamed producer, recovery actions, stragglers, and the restart records to replay."""
     out = []
-    if job["error"]:
-        out.append(f"job failed: {job['error'].strip()[:500]}")
+    err = (job["error"] or "").strip()
+    if err:
+        out.append(f"job failed: {err[:500]}")
+        if "failed" in err and "times" in err:
+            out.append("  the job was aborted because one vertex exhausted MaxVertexFailures (see below)")
+        cls, advice = _classify(err)
+        if advice:
+            out.append(f"  class: {cls}: {advice}")
     runs = executions(job["events"])
     failed = [r for r in runs if r["state"] == "Failed"]
+    by_vertex = {}
     for r in failed:
-        out.append(f"vertex {r['vertex']} ({r['stage']}[{r['partition']}]) v{r['version']} failed on worker "
-                   f"{r['worker']}: {r.get('error', '?')}")
+        by_vertex.setdefault((r["vertex"], r["stage"], r["partition"]), []).append(r)
+    for (v, st, p), rs in sorted(by_vertex.items(), key=lambda kv: -len(kv[1])):
+        errs = [x.get("error", "?") for x in rs]
+        cls, advice = _classify(errs[-1])
+        det = len(rs) > 1 and len({e.split(" v")[0] for e in errs}) == 1
+        out.append(f"vertex {v} ({st}[{p}]) failed {len(rs)}x [{cls}]"
+                   + (" - deterministic (identical error on every attempt)" if det else "") + f": {errs[-1][:300]}")
+        if advice:
+            out.append(f"  {advice}")
+    reads = {}
+    for e in job["events"]:
+        if e.get("ev") == "vertex" and e.get("state") == "Invalidated":
+            reads.setdefault((e.get("stage"), e.get("partition")), 0)
+            reads[(e.get("stage"), e.get("partition"))] += 1
+    for (st, p), n in reads.items():
+        out.append(f"read failures blamed producer {st}[{p}] {n}x: it was invalidated and re-executed")
+    rec = job["stats"].get("recovery") if isinstance(job.get("stats"), dict) else None
+    if rec:
+        kinds = {}
+        for r in rec:
+            kinds[r[0]] = kinds.get(r[0], 0) + 1
+        out.append("recovery actions: " + ", ".join(f"{k} x{n}" for k, n in sorted(kinds.items())))
     by_stage = {}
     for r in runs:
         if r["start"] is not None and r["end"] is not None and r["state"] == "Completed":
@@ -94,6 +151,15 @@ def diagnose(job: dict) -> list:
     reexec = {r["vertex"] for r in runs if r["version"] > 0}
     if reexec:
         out.append(f"{len(reexec)} vertices were re-executed (versions > 0)")
+    rr = sorted(glob.glob(os.path.join(job["dir"], "log", "rerun", "vertex-*")))
+    gpu = [x for x in rr if os.path.isdir(x)]
+    if gpu:
+        out.append(f"{len(gpu)} failed GPU vertex attempts can be replayed: python -m dryad_amd.tools.replay {gpu[0]}")
+    elif failed and rr:
+        v = failed[-1]
+        cand = os.path.join(job["dir"], "log", "rerun", f"vertex-{v['vertex']}.{v['version']}.json")
+        if os.path.exists(cand):
+            out.append(f"replay the failed vertex: python -m dryad_amd.runtime.vertexhost --cmd {cand}")
     return out
 
 

@@ -15,6 +15,20 @@ DATA = [(i * 7919) % 100_003 for i in range(30_000)]
 PEOPLE = [(("alice", "bob", "carol", "dave", "eve")[i % 5] + str(i % 7), i, float(i) / 3) for i in range(12_000)]
 
 
+class _AddAssoc:
+    def Seed(self):
+        return 0
+
+    def RecursiveAccumulate(self, a, b):
+        return a + b
+
+
+@D.resource(is_expensive=True)
+@D.associative(_AddAssoc)
+def _expensive_add(a, x):
+    return a + x
+
+
 def queries():
     rec = "gen://records64?count=200000&partitions=%d&keys=3000&seed=4"
     ts = "gen://terasort?records=50000&partitions=%d&seed=8"
@@ -101,6 +115,8 @@ def queries():
         "apply_per_partition": (lambda c, W: c.FromEnumerable(DATA).ApplyPerPartition(
             lambda xs: [x % 7 for x in xs if x % 3]).Select(lambda x: x * 2), False),
         "range_partition": (lambda c, W: c.FromEnumerable(DATA).RangePartition(lambda x: x, 3), False),
+        # expensive associative Aggregate: dynamic FullAggregator (per-rank fold, then final)
+        "aggregate_full_aggregator": (lambda c, W: [c.FromEnumerable(DATA).Aggregate(0, _expensive_add)], True),
         # the fused grace join stage (runtime/fused_join.py): rank routing over the exchange
         "join_sum_fused": (lambda c, W: [c.FromStore("gen://records64?count=80000&partitions=%d&keys=80000&seed=41"
                                                      "&mode=dim" % W).Join(

@@ -106,3 +106,24 @@ def test_merge_join_descending_order(desc):
         return outer.Join(c.FromEnumerable([(k, -k) for k in range(0, 61, 3)]), lambda t: t[0], lambda u: u[0],
                           lambda t, u: (t[1], u[1]))
     _check(q)
+
+
+def test_expensive_associative_aggregate_gets_full_aggregator():
+    class AddAssoc:
+        def Seed(self):
+            return 0
+
+        def RecursiveAccumulate(self, a, b):
+            return a + b
+
+    @D.resource(is_expensive=True)
+    @D.associative(AddAssoc)
+    def add(a, x):
+        return a + x
+    c = _ctx("proc")
+    p = compile_queries(c, [c.FromEnumerable(DATA).AggregateAsQuery(0, add).ToStore("mem://fa", delete_if_exists=True)])
+    final = next(s for s in p.stages if any(o["op"] == "agg_final" for o in s.ops))
+    assert final.dynamic_manager == "FullAggregator"
+    assert "<Type>FullAggregator</Type>" in p.to_xml()
+    assert all(list(c2.FromEnumerable(DATA).Aggregate(0, add) for c2 in [_ctx(k)])[0] == sum(DATA)
+               for k in ("local", "proc", "spmd"))
