@@ -318,11 +318,23 @@ def test_ordered_strategies_on_device():
 def test_range_partition_with_user_separators_on_device():
     """RangePartition(key, separators[, descending]) with host separator values runs on the device
     (separators encoded like the key columns; reference DryadLinqVertex.cs:4909-5151)."""
+    import bisect
     data = [(i * 7919) % 100_003 for i in range(50_000)]
     pairs = [(i % 977, float(i)) for i in range(20_000)]
-    for build in (
-        lambda c: c.FromEnumerable(data).RangePartition(lambda x: x, [10_000, 50_000, 50_001, 90_000]),
-        lambda c: c.FromEnumerable(data).RangePartition(lambda x: x, [90_000, 50_000, 10_000], True),
-        lambda c: c.FromEnumerable(pairs).RangePartition(lambda t: t[0], [100, 500, 900]),
+    for key, seps, desc, src in (
+        (lambda x: x, [10_000, 50_000, 50_001, 90_000], False, data),
+        (lambda x: x, [90_000, 50_000, 10_000], True, data),
+        (lambda t: t[0], [100, 500, 900], False, pairs),
     ):
-        c = _same(build, ordered=True, parts=2, device_ops=("range_partition",))
+        def build(c, key=key, seps=seps, desc=desc, src=src):
+            q = c.FromEnumerable(src)
+            return q.RangePartition(key, seps, True) if desc else q.RangePartition(key, seps)
+        # LocalDebug does not partition, so only the multiset is compared with it; the device
+        # result (partitions read in order) must walk the separator ranges monotonically
+        c = _same(build, parts=2, device_ops=("range_partition",))
+        sg = [-s for s in seps] if desc else list(seps)
+        cur = 0
+        for row in build(c):
+            k = -key(row) if desc else key(row)
+            cur = max(cur, bisect.bisect_left(sg, k))
+            assert cur <= bisect.bisect_right(sg, k), (row, seps, desc)
