@@ -1,0 +1,444 @@
+// Dense-key GroupBy aggregation: partition packed rows by key bits, then aggregate each
+// partition in an LDS table addressed directly by the key's low bits (no sort, no hashing, no
+// gather through a permutation).
+//
+// BASELINE config "GroupBy-Aggregate 10B x 64-byte records" with keys uniform over 2^30: almost
+// every key is its own group (738M groups per 1.25e9 rows), so a partial aggregation shrinks
+// nothing and the sort-based path pays 4 radix passes plus a random-row gather (45 ms of 32-byte
+// reads through the permutation, profiles/r2_kernels_gb.csv).  The reference's ParallelHashGroupBy
+// (DryadLinqVertex.cs:5342-6417) hashes every record into a per-thread dictionary; on MI355X the
+// dictionary becomes a 2^11-slot LDS table per workgroup, reached after two stable partition
+// passes over 16-byte rows:
+//
+//   row          key - kmin (kbits) | v0 - vmin0 | v1 - vmin1 | v2 - vmin2, bit-packed into 128 bits
+//                (the caller derives the widths from column bounds: generator metadata or a pass)
+//   pass 1       columns -> rows, stable partition by key bits [tb, tb + d1)     (dg_scatter<true>)
+//   pass 2       rows -> rows, stable partition by key bits [tb + d1, kbits)    (dg_scatter<false>)
+//                => rows ordered by key >> tb: every run of equal key >> tb is one LDS table
+//   aggregate    one workgroup per (pass-2 bucket, piece of pass-1 digits): finds each run with a
+//                64-ary wave search, folds it into the table with LDS integer atomics (count,
+//                sum / min / max of the offsets), emits the occupied slots (global output cursor)
+//
+// Each partition pass is count (per-workgroup histograms, bucket-major) + exclusive scan (host
+// side, torch) + scatter: a workgroup ranks a 2048-row tile by digit with wave64 ballot
+// multisplits, writes the rows into LDS in bucket order and stores every bucket's run contiguously.
+#include "common.h"
+
+namespace {
+constexpr int kDgTile = 2048;
+constexpr int kDgItems = kDgTile / kBlock;    // rows per thread per tile
+constexpr int kDgMaxDigit = 10;               // digit bits per pass (1024 buckets)
+constexpr int kDgTableBits = 11;              // LDS table slots per run: 2048
+constexpr int kDgSlots = 1 << kDgTableBits;
+constexpr int kDgMaxCols = 3;
+
+typedef unsigned __int128 u128;
+
+struct DgPack {
+  const int64_t* key;
+  const int64_t* col[kDgMaxCols];
+  int64_t kmin;
+  int64_t vmin[kDgMaxCols];
+  uint32_t kbits;
+  uint32_t vbits[kDgMaxCols];
+  uint32_t ncols;
+};
+
+__device__ __forceinline__ u128 dg_pack_row(const DgPack& p, uint64_t i) {
+  u128 r = (u128)(uint64_t)(p.key[i] - p.kmin);
+  uint32_t off = p.kbits;
+#pragma unroll
+  for (int j = 0; j < kDgMaxCols; ++j) {
+    if (j < (int)p.ncols) {
+      r |= (u128)(uint64_t)(p.col[j][i] - p.vmin[j]) << off;
+      off += p.vbits[j];
+    }
+  }
+  return r;
+}
+
+__device__ __forceinline__ uint64_t dg_field(u128 r, uint32_t off, uint32_t bits) {
+  const uint64_t v = (uint64_t)(r >> off);
+  return bits >= 64 ? v : (v & ((1ull << bits) - 1));
+}
+
+// per-(bucket, workgroup) histogram of digit = (key offset >> shift) & (2^dbits - 1), either from
+// the int64 key column (ROWS = false) or from the packed rows (ROWS = true)
+template <bool ROWS>
+__global__ __launch_bounds__(256) void dg_count_kernel(const int64_t* __restrict__ key, const uint4* __restrict__ rows,
+                                                       uint64_t n, int64_t kmin, uint32_t kbits, uint32_t shift,
+                                                       uint32_t dbits, uint32_t* __restrict__ counts, uint32_t G,
+                                                       uint64_t per_block) {
+  __shared__ uint32_t hist[1 << kDgMaxDigit];
+  const int t = threadIdx.x;
+  const uint32_t nb = 1u << dbits, mask = nb - 1;
+  for (uint32_t i = t; i < nb; i += kBlock) hist[i] = 0;
+  __syncthreads();
+  const uint64_t beg = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  const uint64_t kmask = kbits >= 64 ? ~0ull : ((1ull << kbits) - 1);
+  for (uint64_t i = beg + t; i < end; i += kBlock) {
+    uint64_t ko;
+    if constexpr (ROWS) {
+      const uint4 r = rows[i];
+      ko = (((uint64_t)r.y << 32) | r.x) & kmask;
+    } else {
+      ko = (uint64_t)(key[i] - kmin);
+    }
+    atomicAdd(&hist[(ko >> shift) & mask], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < nb; i += kBlock) counts[(uint64_t)i * G + blockIdx.x] = hist[i];
+}
+
+// Stable partition of rows [beg, end) of each workgroup by digit; offsets[d * G + b] = first output
+// row of workgroup b's bucket d (exclusive prefix of the bucket-major counts).
+template <bool FROM_COLS>
+__global__ __launch_bounds__(256) void dg_scatter_kernel(DgPack pk, const uint4* __restrict__ in, uint64_t n,
+                                                         uint32_t shift, uint32_t dbits,
+                                                         const int64_t* __restrict__ offsets, uint32_t G,
+                                                         uint64_t per_block, uint4* __restrict__ out) {
+  __shared__ uint4 tile[kDgTile];
+  __shared__ uint16_t dslot[kDgTile];
+  __shared__ uint32_t wcnt[4][1 << kDgMaxDigit];
+  __shared__ int64_t goff[1 << kDgMaxDigit];
+  __shared__ uint32_t bstart[1 << kDgMaxDigit];
+  __shared__ uint32_t sc[4];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const uint32_t nb = 1u << dbits, mask = nb - 1;
+  constexpr int kPer = (1 << kDgMaxDigit) / kBlock;   // buckets per thread in the scans
+  const uint64_t beg = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  if (beg >= end) return;                              // uniform: the whole workgroup leaves
+  const uint64_t kmask = pk.kbits >= 64 ? ~0ull : ((1ull << pk.kbits) - 1);
+  for (uint32_t i = t; i < nb; i += kBlock) goff[i] = offsets[(uint64_t)i * G + blockIdx.x];
+  for (uint64_t base = beg; base < end; base += kDgTile) {
+    const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kDgTile ? (end - base) : kDgTile);
+    for (uint32_t i = t; i < 4 * nb; i += kBlock) (&wcnt[0][0])[(i / nb) * (1 << kDgMaxDigit) + (i % nb)] = 0;
+    __syncthreads();
+    uint4 rv[kDgItems];
+    uint32_t rk[kDgItems], dg[kDgItems];
+#pragma unroll
+    for (int r = 0; r < kDgItems; ++r) {
+      const uint32_t pos = w * (kDgTile / 4) + r * 64 + l;
+      const bool valid = pos < cnt;
+      uint4 row = make_uint4(0u, 0u, 0u, 0u);
+      if (valid) {
+        if constexpr (FROM_COLS) {
+          const u128 v = dg_pack_row(pk, base + pos);
+          row = make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96));
+        } else {
+          row = in[base + pos];
+        }
+      }
+      const uint64_t ko = (((uint64_t)row.y << 32) | row.x) & kmask;
+      const uint32_t d = valid ? (uint32_t)((ko >> shift) & mask) : 0u;
+      // wave64 multisplit: the lanes holding the same digit, by one ballot per digit bit
+      uint64_t peers = ballot64(valid);
+      for (uint32_t k = 0; k < dbits; ++k) {
+        const bool bit = (d >> k) & 1u;
+        const uint64_t b = ballot64(bit);
+        peers &= bit ? b : ~b;
+      }
+      const uint32_t below = popc_below(peers);
+      const uint32_t prior = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      rk[r] = prior + below;
+      dg[r] = d;
+      rv[r] = row;
+    }
+    __syncthreads();
+    // bucket totals, wave offsets inside each bucket, and the bucket starts inside the tile
+    uint32_t tot[kPer], run = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const uint32_t b = t * kPer + q;
+      tot[q] = 0;
+      if (b < nb) {
+        const uint32_t c0 = wcnt[0][b], c1 = wcnt[1][b], c2 = wcnt[2][b], c3 = wcnt[3][b];
+        tot[q] = c0 + c1 + c2 + c3;
+        wcnt[0][b] = 0; wcnt[1][b] = c0; wcnt[2][b] = c0 + c1; wcnt[3][b] = c0 + c1 + c2;
+      }
+      run += tot[q];
+    }
+    uint32_t all;
+    uint32_t pre = block_exclusive_scan256(run, sc, all);
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const uint32_t b = t * kPer + q;
+      if (b < nb) bstart[b] = pre;
+      pre += tot[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kDgItems; ++r) {
+      const uint32_t pos = w * (kDgTile / 4) + r * 64 + l;
+      if (pos < cnt) {
+        const uint32_t slot = bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
+        tile[slot] = rv[r];
+        dslot[slot] = (uint16_t)dg[r];
+      }
+    }
+    __syncthreads();
+    // consecutive slots of one bucket are consecutive output rows
+    for (uint32_t j = t; j < cnt; j += kBlock) {
+      const uint32_t d = dslot[j];
+      out[goff[d] + (int64_t)(j - bstart[d])] = tile[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const uint32_t b = t * kPer + q;
+      if (b < nb) goff[b] += tot[q];
+    }
+    __syncthreads();
+  }
+}
+
+struct DgAgg {
+  uint32_t nacc;
+  uint32_t op[kDgMaxCols];       // 0 = sum, 1 = min, 2 = max (of the column's offsets)
+  uint32_t field_off[kDgMaxCols];
+  uint32_t field_bits[kDgMaxCols];
+  int64_t vmin[kDgMaxCols];
+};
+
+// First row in [lo, hi) whose run id (key offset >> kDgTableBits) is >= target; rows in [lo, hi)
+// are ordered by run id.  64-ary search by one wave: 3 steps cover 2^18 rows.
+__device__ __forceinline__ uint64_t dg_lower_bound(const uint4* __restrict__ rows, uint64_t lo, uint64_t hi,
+                                                   uint64_t kmask, uint64_t target) {
+  const int l = lane_id();
+  while (hi - lo > 64) {
+    const uint64_t step = (hi - lo + 63) / 64;
+    const uint64_t pos = lo + (uint64_t)l * step;
+    bool ge = true;
+    if (pos < hi) {
+      const uint4 r = rows[pos];
+      ge = (((((uint64_t)r.y << 32) | r.x) & kmask) >> kDgTableBits) >= target;
+    }
+    const uint64_t m = ballot64(ge);                  // lanes at and past the answer (monotone)
+    const int first = m ? __builtin_ctzll(m) : 64;
+    // the answer lies in (pos(first - 1), pos(first)]
+    const uint64_t nlo = first == 0 ? lo : lo + (uint64_t)(first - 1) * step + 1;
+    const uint64_t nhi = first == 64 ? hi : (lo + (uint64_t)first * step < hi ? lo + (uint64_t)first * step : hi);
+    lo = nlo;
+    hi = nhi;
+    if (first == 0) return lo;
+  }
+  const uint64_t pos = lo + l;
+  bool ge = true;
+  if (pos < hi) {
+    const uint4 r = rows[pos];
+    ge = (((((uint64_t)r.y << 32) | r.x) & kmask) >> kDgTableBits) >= target;
+  }
+  const uint64_t m = ballot64(ge || pos >= hi);
+  return lo + (uint64_t)(m ? __builtin_ctzll(m) : (int)(hi - lo));
+}
+
+// One workgroup per (bucket b of the last partition pass, piece q): rows [bstart[b], bstart[b+1])
+// are ordered by run id; the piece covers the runs b * runs_per_bucket + [q * rpp, (q + 1) * rpp).
+__global__ __launch_bounds__(256) void dg_agg_kernel(const uint4* __restrict__ rows, const int64_t* __restrict__ bstart,
+                                                     uint32_t nbuckets, uint32_t pieces, uint64_t runs_per_bucket,
+                                                     uint32_t kbits, int64_t kmin, DgAgg ag,
+                                                     unsigned long long* __restrict__ head, int64_t* __restrict__ okey,
+                                                     int64_t* __restrict__ ocnt, int64_t* __restrict__ oacc0,
+                                                     int64_t* __restrict__ oacc1, int64_t* __restrict__ oacc2) {
+  __shared__ uint32_t cnt[kDgSlots];
+  __shared__ unsigned long long acc[kDgMaxCols][kDgSlots];
+  __shared__ uint64_t bounds[2];
+  __shared__ uint32_t sc[4];
+  __shared__ unsigned long long obase;
+  const int t = threadIdx.x, w = wave_id();
+  const uint64_t kmask = kbits >= 64 ? ~0ull : ((1ull << kbits) - 1);
+  int64_t* const oacc[3] = {oacc0, oacc1, oacc2};
+  constexpr int kSlotsPer = kDgSlots / kBlock;
+  auto reset = [&]() {
+#pragma unroll
+    for (int q = 0; q < kSlotsPer; ++q) {
+      const int s = t + q * kBlock;
+      cnt[s] = 0;
+#pragma unroll
+      for (int a = 0; a < kDgMaxCols; ++a)
+        if (a < (int)ag.nacc) acc[a][s] = ag.op[a] == 1 ? ~0ull : 0ull;
+    }
+  };
+  reset();
+  const uint64_t rpp = (runs_per_bucket + pieces - 1) / pieces;
+  for (uint64_t item = blockIdx.x; item < (uint64_t)nbuckets * pieces; item += gridDim.x) {
+    const uint32_t b = (uint32_t)(item / pieces), q = (uint32_t)(item % pieces);
+    const uint64_t blo = (uint64_t)bstart[b], bhi = (uint64_t)bstart[b + 1];
+    const uint64_t run0 = (uint64_t)b * runs_per_bucket + (uint64_t)q * rpp;
+    const uint64_t run1 = (uint64_t)b * runs_per_bucket + ((uint64_t)(q + 1) * rpp < runs_per_bucket
+                                                               ? (uint64_t)(q + 1) * rpp : runs_per_bucket);
+    if (blo == bhi || run0 >= run1) continue;          // uniform
+    // this piece's rows, then run by run
+    if (w == 0) {
+      const uint64_t s0 = dg_lower_bound(rows, blo, bhi, kmask, run0);
+      const uint64_t s1 = dg_lower_bound(rows, s0, bhi, kmask, run1);
+      if (lane_id() == 0) { bounds[0] = s0; bounds[1] = s1; }
+    }
+    __syncthreads();
+    uint64_t pos = bounds[0];
+    const uint64_t pend = bounds[1];
+    __syncthreads();
+    while (pos < pend) {
+      // the run of the row at pos: rows up to the first row of the next run
+      uint64_t run;
+      {
+        const uint4 r = rows[pos];
+        run = ((((uint64_t)r.y << 32) | r.x) & kmask) >> kDgTableBits;
+      }
+      if (w == 0) {
+        const uint64_t e = dg_lower_bound(rows, pos, pend, kmask, run + 1);
+        if (lane_id() == 0) bounds[1] = e;
+      }
+      __syncthreads();
+      const uint64_t rend = bounds[1];
+      for (uint64_t i = pos + t; i < rend; i += kBlock) {
+        const uint4 rr = rows[i];
+        const u128 v = (u128)rr.x | ((u128)rr.y << 32) | ((u128)rr.z << 64) | ((u128)rr.w << 96);
+        const uint32_t s = (uint32_t)((uint64_t)v & (kDgSlots - 1));
+        atomicAdd(&cnt[s], 1u);
+#pragma unroll
+        for (int a = 0; a < kDgMaxCols; ++a) {
+          if (a < (int)ag.nacc) {
+            const unsigned long long f = dg_field(v, ag.field_off[a], ag.field_bits[a]);
+            if (ag.op[a] == 0) atomicAdd(&acc[a][s], f);
+            else if (ag.op[a] == 1) atomicMin(&acc[a][s], f);
+            else atomicMax(&acc[a][s], f);
+          }
+        }
+      }
+      __syncthreads();
+      // emit the occupied slots: count, reserve a range of the output, write, reset
+      uint32_t occ = 0;
+#pragma unroll
+      for (int q2 = 0; q2 < kSlotsPer; ++q2) occ += cnt[t * kSlotsPer + q2] != 0;
+      uint32_t total;
+      uint32_t pre = block_exclusive_scan256(occ, sc, total);
+      if (t == 0) obase = atomicAdd(head, (unsigned long long)total);
+      __syncthreads();
+      const uint64_t o0 = obase;
+#pragma unroll
+      for (int q2 = 0; q2 < kSlotsPer; ++q2) {
+        const int s = t * kSlotsPer + q2;
+        const uint32_t c = cnt[s];
+        if (c) {
+          const uint64_t o = o0 + pre++;
+          okey[o] = kmin + (int64_t)((run << kDgTableBits) | (uint64_t)s);
+          ocnt[o] = c;
+#pragma unroll
+          for (int a = 0; a < kDgMaxCols; ++a) {
+            if (a < (int)ag.nacc) {
+              const int64_t av = (int64_t)acc[a][s];
+              oacc[a][o] = ag.op[a] == 0 ? av + (int64_t)c * ag.vmin[a] : av + ag.vmin[a];
+            }
+          }
+        }
+        cnt[s] = 0;
+#pragma unroll
+        for (int a = 0; a < kDgMaxCols; ++a)
+          if (a < (int)ag.nacc) acc[a][s] = ag.op[a] == 1 ? ~0ull : 0ull;
+      }
+      pos = rend;
+      __syncthreads();
+    }
+  }
+}
+}  // namespace
+
+DR_API uint32_t dr_dg_table_bits() { return kDgTableBits; }
+DR_API uint32_t dr_dg_max_digit() { return kDgMaxDigit; }
+
+// Workgroups and rows per workgroup of a partition pass (counts are sized (1 << dbits) * G).
+DR_API uint32_t dr_dg_grid(uint64_t n, uint64_t* per_block) {
+  uint64_t tiles = (n + kDgTile - 1) / kDgTile;
+  if (tiles < 1) tiles = 1;
+  const uint64_t G = tiles < 1024 ? tiles : 1024;
+  *per_block = ((tiles + G - 1) / G) * kDgTile;
+  return (uint32_t)G;
+}
+
+static int dg_pack_from(DgPack* p, const int64_t* key, const int64_t* const* cols, const int64_t* vmin,
+                        const uint32_t* vbits, uint32_t ncols, int64_t kmin, uint32_t kbits) {
+  if (ncols > (uint32_t)kDgMaxCols || kbits == 0 || kbits > 64) return 1;
+  uint32_t tot = kbits;
+  p->key = key;
+  p->kmin = kmin;
+  p->kbits = kbits;
+  p->ncols = ncols;
+  for (uint32_t j = 0; j < (uint32_t)kDgMaxCols; ++j) {
+    p->col[j] = j < ncols ? cols[j] : nullptr;
+    p->vmin[j] = j < ncols ? vmin[j] : 0;
+    p->vbits[j] = j < ncols ? vbits[j] : 0;
+    tot += p->vbits[j];
+    if (j < ncols && (vbits[j] == 0 || vbits[j] > 64)) return 1;
+  }
+  return tot > 128 ? 1 : 0;
+}
+
+// rows == null: histogram of the key column; else of the packed rows.
+DR_API int dr_dg_count(const int64_t* key, const void* rows, uint64_t n, int64_t kmin, uint32_t kbits, uint32_t shift,
+                       uint32_t dbits, uint32_t* counts, uint32_t G, uint64_t per_block, hipStream_t s) {
+  if (dbits == 0 || dbits > (uint32_t)kDgMaxDigit) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  if (rows)
+    dg_count_kernel<true><<<G, 256, 0, s>>>(nullptr, static_cast<const uint4*>(rows), n, kmin, kbits, shift, dbits,
+                                             counts, G, per_block);
+  else
+    dg_count_kernel<false><<<G, 256, 0, s>>>(key, nullptr, n, kmin, kbits, shift, dbits, counts, G, per_block);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// in == null: rows packed from key + cols; else partition the packed rows `in`.
+DR_API int dr_dg_scatter(const int64_t* key, const int64_t* const* cols, const int64_t* vmin, const uint32_t* vbits,
+                         uint32_t ncols, int64_t kmin, uint32_t kbits, const void* in, uint64_t n, uint32_t shift,
+                         uint32_t dbits, const int64_t* offsets, uint32_t G, uint64_t per_block, void* out,
+                         hipStream_t s) {
+  if (dbits == 0 || dbits > (uint32_t)kDgMaxDigit) return (int)hipErrorInvalidValue;
+  DgPack p;
+  if (dg_pack_from(&p, key, cols, vmin, vbits, ncols, kmin, kbits)) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  if (in)
+    dg_scatter_kernel<false><<<G, 256, 0, s>>>(p, static_cast<const uint4*>(in), n, shift, dbits, offsets, G,
+                                                per_block, static_cast<uint4*>(out));
+  else
+    dg_scatter_kernel<true><<<G, 256, 0, s>>>(p, nullptr, n, shift, dbits, offsets, G, per_block,
+                                               static_cast<uint4*>(out));
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// rows: n packed rows ordered by run id (key offset >> table bits) inside each of the nbuckets
+// ranges [bstart[b], bstart[b + 1]); bucket b holds the runs b * runs_per_bucket + [0, runs_per_bucket).
+// ops / off / bits / vmin: nacc accumulators over packed fields.  head (u64, zeroed) receives the
+// group count; outputs are sized by the caller (>= the number of groups).
+DR_API int dr_dg_aggregate(const void* rows, const int64_t* bstart, uint32_t nbuckets, uint64_t runs_per_bucket,
+                           uint32_t kbits, int64_t kmin, uint32_t nacc, const uint32_t* ops, const uint32_t* off,
+                           const uint32_t* bits, const int64_t* vmin, unsigned long long* head, int64_t* okey,
+                           int64_t* ocnt, int64_t* const* oacc, hipStream_t s) {
+  if (nacc > (uint32_t)kDgMaxCols || nbuckets == 0) return (int)hipErrorInvalidValue;
+  DgAgg ag;
+  ag.nacc = nacc;
+  for (uint32_t a = 0; a < (uint32_t)kDgMaxCols; ++a) {
+    ag.op[a] = a < nacc ? ops[a] : 0;
+    ag.field_off[a] = a < nacc ? off[a] : 0;
+    ag.field_bits[a] = a < nacc ? bits[a] : 0;
+    ag.vmin[a] = a < nacc ? vmin[a] : 0;
+    if (a < nacc && (ag.op[a] > 2 || ag.field_bits[a] == 0 || ag.field_off[a] + ag.field_bits[a] > 128))
+      return (int)hipErrorInvalidValue;
+  }
+  // pieces: about 4 workgroups' worth of runs per resident workgroup
+  uint32_t pieces = 1;
+  while ((uint64_t)nbuckets * pieces < 2048 && pieces < runs_per_bucket) pieces <<= 1;
+  const uint64_t items = (uint64_t)nbuckets * pieces;
+  const unsigned grid = (unsigned)(items < 4096 ? items : 4096);
+  dg_agg_kernel<<<grid, 256, 0, s>>>(static_cast<const uint4*>(rows), bstart, nbuckets, pieces, runs_per_bucket, kbits,
+                                     kmin, ag, head, okey, ocnt, nacc > 0 ? oacc[0] : nullptr,
+                                     nacc > 1 ? oacc[1] : nullptr, nacc > 2 ? oacc[2] : nullptr);
+  DR_LAUNCH_CHECK();
+  return 0;
+}

@@ -218,6 +218,12 @@ def op_read(op, inputs, v):
             from ..models.records_cpu import dim_multiplier
             nk = int(q.get("keys", 1 << 20))
             R.gen_records64(cols, lo, nk, int(q.get("seed", 0)), dim_multiplier(nk) if q.get("mode") == "dim" else 0)
+            # the generator's value contract (models/records_cpu.py): keys in [0, nk), payloads
+            # mix64(..) >> 33, i.e. 31-bit -- column statistics for operators that pack by width
+            from . import stats
+            stats.set_bounds(cols[0], 0, nk - 1)
+            for c in cols[1:]:
+                stats.set_bounds(c, 0, (1 << 31) - 1)
             names = FIELDS[:ncols]
             return DeviceTable.from_columns(dict(zip(names, cols)), Shape("tuple", names))
         if kind == "range":
@@ -748,6 +754,16 @@ def _radix_groups(kcols, skeys, specs, n, nd=None):
     return got[0].to(k.dtype), got[1]
 
 
+def _dense_groups(kcols, skeys, specs, n):
+    """(keys, aggregate columns) through ops/densegroup.py (partition by key bits + LDS tables
+    addressed by the low key bits) for one plain integer key whose span needs 12..31 bits and
+    integer aggregates that pack with it into 16-byte rows, else None."""
+    from ..ops import densegroup as DG
+    if len(kcols) != 1 or skeys[0] is not None or kcols[0].dtype not in _INT_KEYS or n < DG.MIN_ROWS:
+        return None
+    return DG.dense_aggregate(kcols[0], specs)
+
+
 def _fused_int64_groups(kcols, skeys, specs):
     """(keys, aggregate columns) through R.group_reduce_sorted for one plain int64 key, else None."""
     if not R.FUSED_GROUP_KEYS or len(kcols) != 1 or skeys[0] is not None or kcols[0].dtype != torch.int64:
@@ -782,6 +798,14 @@ def op_group_partial(op, inputs, v):
                 for nm, r in zip(names, res):
                     out[nm] = r
                 return _partial_table(out, {}, d, 1, form)
+    # one integer key over a span of <= 2^31 values: partition by key bits, then LDS tables
+    # addressed by the low key bits (no sort, no hash, no gather)
+    got = _dense_groups(kcols, skeys, specs, t.n)
+    if got is not None:
+        out = {"k0": got[0]}
+        for nm, r in zip(names, got[1]):
+            out[nm] = r
+        return _partial_table(out, {}, d, 1, form)
     # one integer key, many distinct keys: radix-partitioned LDS aggregation (no sort, no gather)
     got = _radix_groups(kcols, skeys, specs, t.n, nd_est)
     if got is not None:
@@ -833,7 +857,9 @@ def op_group_final(op, inputs, v):
             specs += [("sum", col, torch.float64), ("sum", t.cols[f"c{j}"], torch.int64)]
         elif a.kind in ("any", "all"):
             specs.append(("max" if a.kind == "any" else "min", col, torch.int64))
-    got = _radix_groups(kcols, skeys, specs, t.n)
+    got = _dense_groups(kcols, skeys, specs, t.n)
+    if got is None:
+        got = _radix_groups(kcols, skeys, specs, t.n)
     if got is None:
         got = _payload_groups(kcols, skeys, specs, t.n)
     if got is not None:

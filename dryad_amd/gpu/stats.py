@@ -1,0 +1,45 @@
+"""Column value bounds (min / max) of device columns, cached per tensor.
+
+Operators that pack rows by value width (ops/densegroup.py) need bounds, not exact extremes:
+lo <= every value <= hi.  Sources that know them for free register them when they build a column
+(the gen:// generators: a key column over [0, keys), 31-bit payloads), the way a columnar file
+format keeps per-column statistics in its footer; any other column gets one fused min/max pass
+(ops/reduce.reduce_multi, up to 8 columns per pass) the first time it is asked for.  An entry dies
+with its tensor and is ignored once the tensor has been modified in place.
+"""
+from __future__ import annotations
+
+import torch
+from torch.utils.weak import WeakIdKeyDictionary
+
+_BOUNDS = WeakIdKeyDictionary()
+
+
+def set_bounds(col: torch.Tensor, lo: int, hi: int) -> None:
+    """Declare lo <= col[i] <= hi for every row (integer columns)."""
+    _BOUNDS[col] = (int(lo), int(hi), col._version)
+
+
+def known(col: torch.Tensor):
+    e = _BOUNDS.get(col)
+    if e is None or e[2] != col._version:
+        return None
+    return e[0], e[1]
+
+
+def bounds(cols: list) -> list:
+    """[(lo, hi)] for integer columns (one device pass over those without registered bounds)."""
+    out = [known(c) for c in cols]
+    missing = [i for i, b in enumerate(out) if b is None]
+    if missing:
+        from ..ops import reduce as RD
+        n = cols[missing[0]].shape[0]
+        slots = []
+        for i in missing:
+            c = cols[i] if cols[i].dtype == torch.int64 else cols[i].to(torch.int64)
+            slots += [(RD.MIN, c, None), (RD.MAX, c, None)]
+        got = RD.reduce_multi(n, slots, cols[missing[0]].device)
+        for j, i in enumerate(missing):
+            out[i] = (int(got[2 * j]), int(got[2 * j + 1]))
+            set_bounds(cols[i], *out[i])
+    return out

@@ -1,0 +1,173 @@
+"""Dense-key GroupBy aggregation (csrc/kernels/densegroup.hip): two stable partition passes over
+bit-packed 16-byte rows by key bits, then one LDS table per run of 2^11 consecutive keys.
+
+Applies to one integer key whose value span needs 12..31 bits (2^11 < span <= 2^31: at most two
+partition passes of <= 10 bits) and <= 3 integer value columns whose spans, with the key's, pack
+into 128 bits; count / sum / min / max aggregates.  Reference: the partial / full hash GroupBy of
+DryadLinqVertex.cs:5342-6417 (ParallelHashGroupBy) -- here the hash table is an LDS table addressed
+directly by the low key bits, reached by partitioning on the high ones.
+
+Returns (keys int64, [per-spec int64 column]) in unspecified group order, or None when the shape
+does not apply (the caller then takes the radix-aggregation or sort path).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import c_i32, c_i64, c_u32, c_u64, ptr, stream_of, vp
+
+_lib.register_signatures({
+    "dr_dg_table_bits": (c_u32, []),
+    "dr_dg_max_digit": (c_u32, []),
+    "dr_dg_grid": (c_u32, [c_u64, ctypes.POINTER(c_u64)]),
+    "dr_dg_count": (c_i32, [vp, vp, c_u64, c_i64, c_u32, c_u32, c_u32, vp, c_u32, c_u64, vp]),
+    "dr_dg_scatter": (c_i32, [vp, ctypes.POINTER(vp), ctypes.POINTER(c_i64), ctypes.POINTER(c_u32), c_u32, c_i64,
+                              c_u32, vp, c_u64, c_u32, c_u32, vp, c_u32, c_u64, vp, vp]),
+    "dr_dg_aggregate": (c_i32, [vp, vp, c_u32, c_u64, c_u32, c_i64, c_u32, ctypes.POINTER(c_u32),
+                                ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), ctypes.POINTER(c_i64), vp, vp, vp,
+                                ctypes.POINTER(vp), vp]),
+})
+
+TABLE_BITS = 11
+MAX_DIGIT = 10
+MIN_ROWS = 1 << 20
+_INT = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8)
+_OP = {"sum": 0, "min": 1, "max": 2}
+
+
+def plan(kspan_bits: int, vbits: list) -> list | None:
+    """Digit widths of the partition passes (low digit first) for a key offset of ``kspan_bits``
+    bits, or None when the dense path does not apply."""
+    d = kspan_bits - TABLE_BITS
+    if d < 1 or d > 2 * MAX_DIGIT or kspan_bits + sum(vbits) > 128:
+        return None
+    if d <= MAX_DIGIT:
+        return [d]
+    lo = (d + 1) // 2
+    return [lo, d - lo]
+
+
+def _bits(span: int) -> int:
+    return max(1, int(span).bit_length())
+
+
+def applicable(key: torch.Tensor, specs: list) -> bool:
+    return _prepare(key, specs) is not None
+
+
+def _prepare(key: torch.Tensor, specs: list):
+    from ..gpu import stats
+    n = key.shape[0]
+    if key.dim() != 1 or key.dtype not in _INT or n < 2 or n >= (1 << 32):
+        return None
+    cols, accs, where = [], [], []
+    for op, vals, dtype in specs:
+        if op == "count":
+            where.append(("count", None))
+            continue
+        if op not in _OP or vals is None or vals.dtype not in _INT or dtype not in _INT:
+            return None
+        j = next((j for j, c in enumerate(cols) if c is vals), None)
+        if j is None:
+            if len(cols) == 3:
+                return None
+            cols.append(vals)
+            j = len(cols) - 1
+        a = (_OP[op], j)
+        if a not in accs:
+            if len(accs) == 3:
+                return None
+            accs.append(a)
+        where.append(("acc", accs.index(a)))
+    bnds = stats.bounds([key] + cols)
+    (kmin, kmax), vb = bnds[0], bnds[1:]
+    kbits = _bits(kmax - kmin)
+    vbits = [_bits(hi - lo) for lo, hi in vb]
+    widths = plan(kbits, vbits)
+    if widths is None:
+        return None
+    # int64 results: a sum's magnitude is bounded by n * max|v|
+    for (op, j) in accs:
+        lo, hi = vb[j]
+        if op == 0 and n * max(abs(lo), abs(hi)) >= (1 << 63):
+            return None
+    return cols, accs, where, kmin, kbits, [lo for lo, _ in vb], vbits, widths
+
+
+def _partition(key64, cols64, vmin, vbits, kmin, kbits, src, n, shift, dbits, dev, st):
+    """One stable partition pass -> (rows, bucket totals int64 [2^dbits] on the device)."""
+    pb = c_u64(0)
+    G = int(_lib.lib().dr_dg_grid(c_u64(n), ctypes.byref(pb)))
+    nb = 1 << dbits
+    counts = torch.empty(nb * G, dtype=torch.int32, device=dev)
+    _lib.call("dr_dg_count", ptr(key64) if src is None else None, ptr(src), c_u64(n), c_i64(kmin), c_u32(kbits),
+              c_u32(shift), c_u32(dbits), ptr(counts), c_u32(G), pb, st)
+    c64 = counts.to(torch.int64)
+    del counts
+    offs = torch.cumsum(c64, 0)
+    offs -= c64
+    out = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    k = len(cols64)
+    cp = (vp * 3)(*([c.data_ptr() for c in cols64] + [0] * (3 - k)))
+    vm = (c_i64 * 3)(*(list(vmin) + [0] * (3 - k)))
+    vbt = (c_u32 * 3)(*(list(vbits) + [0] * (3 - k)))
+    _lib.call("dr_dg_scatter", ptr(key64), cp, vm, vbt, c_u32(k), c_i64(kmin), c_u32(kbits), ptr(src), c_u64(n),
+              c_u32(shift), c_u32(dbits), ptr(offs), c_u32(G), pb, ptr(out), st)
+    return out, c64.view(nb, G).sum(1)
+
+
+def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
+    """GroupBy on one integer key column through the dense-key path; see the module docstring."""
+    n = key.shape[0]
+    if not key.is_cuda or (not force and n < MIN_ROWS):
+        return None
+    prep = _prepare(key, specs)
+    if prep is None:
+        return None
+    cols, accs, where, kmin, kbits, vmin, vbits, widths = prep
+    dev = key.device
+    st = stream_of(key)
+    key64 = key if key.dtype == torch.int64 else key.to(torch.int64)
+    key64 = key64.contiguous()
+    cols64 = [(c if c.dtype == torch.int64 else c.to(torch.int64)).contiguous() for c in cols]
+    # pass 1 packs the columns (low digit), pass 2 (if any) re-partitions the rows (high digit)
+    rows, tot = _partition(key64, cols64, vmin, vbits, kmin, kbits, None, n, TABLE_BITS, widths[0], dev, st)
+    runs_per_bucket = 1
+    if len(widths) == 2:
+        nxt, tot = _partition(key64, cols64, vmin, vbits, kmin, kbits, rows, n, TABLE_BITS + widths[0], widths[1],
+                              dev, st)
+        del rows
+        rows = nxt
+        runs_per_bucket = 1 << widths[0]
+    nb = tot.shape[0]
+    bstart = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(tot, 0, out=bstart[1:])
+    # field offsets of the accumulated columns inside the packed row
+    foff, o = [], kbits
+    for b in vbits:
+        foff.append(o)
+        o += b
+    head = torch.zeros(1, dtype=torch.int64, device=dev)
+    okey = torch.empty(n, dtype=torch.int64, device=dev)
+    ocnt = torch.empty(n, dtype=torch.int64, device=dev)
+    oacc = [torch.empty(n, dtype=torch.int64, device=dev) for _ in accs]
+    na = len(accs)
+    ops = (c_u32 * 3)(*([a[0] for a in accs] + [0] * (3 - na)))
+    offs = (c_u32 * 3)(*([foff[a[1]] for a in accs] + [0] * (3 - na)))
+    bts = (c_u32 * 3)(*([vbits[a[1]] for a in accs] + [0] * (3 - na)))
+    vms = (c_i64 * 3)(*([vmin[a[1]] for a in accs] + [0] * (3 - na)))
+    optr = (vp * 3)(*([t.data_ptr() for t in oacc] + [0] * (3 - na)))
+    _lib.call("dr_dg_aggregate", ptr(rows), ptr(bstart), c_u32(nb), c_u64(runs_per_bucket), c_u32(kbits),
+              c_i64(kmin), c_u32(na), ops, offs, bts, vms, ptr(head), ptr(okey), ptr(ocnt), optr, st)
+    del rows
+    g = int(head.item())
+    keys, cnt = okey[:g], ocnt[:g]
+    outs = []
+    for kind, i in where:
+        outs.append(cnt if kind == "count" else oacc[i][:g])
+    if key.dtype != torch.int64:
+        keys = keys.to(key.dtype)
+    return keys, outs

@@ -1,5 +1,12 @@
 """k-means step on MFMA (HIP kernels in csrc/kernels/kmeans.hip).
 
+K <= 64 (the benchmark's K = 64) runs on split planes: the static point table is split once into
+three exact bf16 parts (``SplitPoints``, cached per point tensor) and every iteration reads the
+xh/xm planes only (512 B per point, as many bytes as the f32 row, no conversion work in the loop);
+the third part's per-cluster sums follow the assignment incrementally (only points whose
+assignment changed move theirs).  Larger K, or planes that do not fit in free HBM, use the f32
+kernels.
+
 BASELINE config: "k-means on 1B x 128-dim points (Apply/Fork iterative DAG, MFMA reductions)".
 The reference runs k-means as a DoWhile over per-partition Apply bodies that compute nearest
 centroids and partial sums on the CPU, then a final aggregation stage (reference samples under
@@ -8,6 +15,8 @@ assignment (f32 MFMA distance tiles + argmin) and the LDS-privatised partial sum
 reduction is one RCCL all-reduce of K*(D+1) values.
 """
 from __future__ import annotations
+
+import weakref
 
 import torch
 
@@ -21,7 +30,13 @@ _lib.register_signatures({
     "dr_kmeans_step": (c_i32, [vp, c_u64, c_i32, vp, c_i32, vp, vp, vp, vp, vp, vp]),
     "dr_kmeans_near_workspace": (c_u64, [c_u64]),
     "dr_kmeans_gen": (c_i32, [vp, c_u64, c_i32, c_u64, c_i32, c_u64, vp]),
+    "dr_kmeans_split": (c_i32, [vp, c_u64, vp, vp, vp]),
+    "dr_kmeans_step_planes": (c_i32, [vp, vp, c_u64, vp, c_i32, vp, vp, vp, vp, vp, vp, vp, vp]),
 })
+
+PLANES_MAX_K = 64
+# free HBM kept beyond the planes (the step's workspace and whatever the job allocates next)
+PLANES_HEADROOM = 4 << 30
 
 
 class KMeansWorkspace:
@@ -36,6 +51,84 @@ class KMeansWorkspace:
         # near-tie list of the K <= 64 bf16-MFMA path (count + (point, estimate) pairs)
         self.near = torch.empty(int(_lib.lib().dr_kmeans_near_workspace(c_u64(n))) if k <= 64 else 16,
                                 dtype=torch.uint8, device=device)
+
+
+class SplitPoints:
+    """Exact three-part bf16 split of an [n, 128] f32 point table: planes [3, n, 128] (xh, xm, xl
+    with x = xh + xm + xl), |x| per point, and the state that carries the xl part's per-cluster
+    sums across steps (``prev``: last final assignment, -1 = none; ``sxl``: K x 128 f64)."""
+
+    def __init__(self, x: torch.Tensor):
+        n = x.shape[0]
+        self.n = n
+        self.version = x._version
+        self.planes = torch.empty((3, n, DIM), dtype=torch.bfloat16, device=x.device)
+        self.xnorm = torch.empty(n, dtype=torch.float32, device=x.device)
+        self.prev = torch.full((n,), -1, dtype=torch.int32, device=x.device)
+        self.sxl = None
+        if x.is_cuda:
+            _lib.call("dr_kmeans_split", ptr(x), c_u64(n), ptr(self.planes), ptr(self.xnorm), stream_of(x))
+        else:
+            h, m, lo = split_reference(x)
+            self.planes[0], self.planes[1], self.planes[2] = h, m, lo
+            self.xnorm.copy_(x.double().norm(dim=1).float())
+
+    def state_for(self, k: int) -> torch.Tensor:
+        """The xl sums for ``k`` clusters; a new K restarts them (every point moves again)."""
+        if self.sxl is None or self.sxl.shape[0] != k:
+            self.sxl = torch.zeros((k, DIM), dtype=torch.float64, device=self.planes.device)
+            self.prev.fill_(-1)
+        return self.sxl
+
+
+# (device, data_ptr, n) -> SplitPoints.  The entry lives as long as the tensor that owns the
+# points' memory (the base of whatever view the caller passes: a table column handed out as a new
+# view every iteration still hits), and is checked against that owner and its version counter.
+_SPLITS: dict = {}
+
+
+def split_bytes(n: int) -> int:
+    return n * (3 * DIM * 2 + 4 + 4)
+
+
+def split_points(x: torch.Tensor, create: bool = True) -> SplitPoints | None:
+    """The cached split of ``x`` (recomputed if ``x`` was modified in place since).  Returns None
+    when the planes do not fit in free HBM (the caller then runs the f32 kernels)."""
+    base = x if x._base is None else x._base
+    key = (str(x.device), x.data_ptr(), x.shape[0])
+    sp = _SPLITS.get(key)
+    if sp is not None and sp.owner() is base and sp.version == x._version:
+        return sp
+    if not create:
+        return None
+    _SPLITS.pop(key, None)
+    if x.is_cuda:
+        free, _total = torch.cuda.mem_get_info(x.device)
+        cached = torch.cuda.memory_reserved(x.device) - torch.cuda.memory_allocated(x.device)
+        if split_bytes(x.shape[0]) + PLANES_HEADROOM > free + cached:
+            return None
+    sp = SplitPoints(x)
+
+    def _drop(ref, key=key):
+        cur = _SPLITS.get(key)
+        if cur is not None and cur.owner is ref:
+            del _SPLITS[key]
+
+    sp.owner = weakref.ref(base, _drop)
+    _SPLITS[key] = sp
+    return sp
+
+
+def split_reference(x: torch.Tensor):
+    """torch twin of kmeans_split_kernel: x = xh + xm + xl, each a round-to-nearest bf16 of the
+    remainder so far (exact: the remainders are exact in f32 and 3 x 8 significand bits cover 24;
+    for |x| >= 2^-100, where the remainders stay normal numbers)."""
+    x = x.float()
+    h = x.bfloat16()
+    r1 = x - h.float()
+    m = r1.bfloat16()
+    lo = (r1 - m.float()).bfloat16()
+    return h, m, lo
 
 
 def mode(k: int) -> int:
@@ -53,8 +146,12 @@ def generate(points: torch.Tensor, first: int = 0, blobs: int = 64, seed: int = 
     return points
 
 
-def step(points: torch.Tensor, centroids: torch.Tensor, ws: KMeansWorkspace | None = None):
-    """One assignment + partial-sum pass.  Returns (sums f64 [K,D], counts i64 [K], assign i32 [n])."""
+def step(points: torch.Tensor, centroids: torch.Tensor, ws: KMeansWorkspace | None = None,
+         planes: bool | None = None):
+    """One assignment + partial-sum pass.  Returns (sums f64 [K,D], counts i64 [K], assign i32 [n]).
+
+    ``planes``: None = split planes when K <= 64 and they fit (the default), False = the f32
+    kernels, True = split planes or an error."""
     _lib.require_gpu_tensor(points, "kmeans.step")
     _lib.require_gpu_tensor(centroids, "kmeans.step")
     assert points.dtype == torch.float32 and centroids.dtype == torch.float32
@@ -64,6 +161,19 @@ def step(points: torch.Tensor, centroids: torch.Tensor, ws: KMeansWorkspace | No
         ws = KMeansWorkspace(n, k, points.device)
     ws.sums.zero_()
     ws.counts.zero_()
+    sp = None
+    if planes is not False and 1 <= k <= PLANES_MAX_K and n > 0:
+        sp = split_points(points)
+        if sp is None and planes:
+            raise MemoryError(f"kmeans.step: split planes of {n} points ({split_bytes(n) >> 20} MiB) do not fit")
+    elif planes:
+        raise ValueError(f"kmeans.step: split planes need 1 <= K <= {PLANES_MAX_K} (K = {k})")
+    if sp is not None:
+        sxl = sp.state_for(k)
+        _lib.call("dr_kmeans_step_planes", ptr(sp.planes), ptr(sp.xnorm), c_u64(n), ptr(centroids), k,
+                  ptr(ws.cnorm), ptr(ws.assign), ptr(sp.prev), ptr(sxl), ptr(ws.sums), ptr(ws.counts),
+                  ptr(ws.near), stream_of(points))
+        return ws.sums, ws.counts, ws.assign[:n]
     _lib.call("dr_kmeans_step", ptr(points), c_u64(n), DIM, ptr(centroids), k, ptr(ws.cnorm), ptr(ws.assign),
               ptr(ws.sums), ptr(ws.counts), ptr(ws.near), stream_of(points))
     return ws.sums, ws.counts, ws.assign[:n]

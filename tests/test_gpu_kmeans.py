@@ -27,6 +27,88 @@ def test_kmeans_step_matches_reference(n, k):
     assert int(counts.sum()) == n
 
 
+@pytest.mark.parametrize("planes", [True, False])
+@pytest.mark.parametrize("n,k", [(1, 1), (1000, 7), (50_003, 64)])
+def test_kmeans_step_both_paths_match_reference(n, k, planes):
+    """K <= 64: the split-plane kernel (default) and the f32-input kernel agree with the f64 oracle."""
+    from dryad_amd.ops import kmeans as KM
+    x = torch.empty((n, KM.DIM), dtype=torch.float32, device="cuda")
+    KM.generate(x, 0, blobs=max(1, k // 2), seed=n + 7)
+    c = x[torch.randperm(n, device="cuda")[:k]].clone()
+    if c.shape[0] < k:
+        c = torch.cat([c, torch.randn((k - c.shape[0], KM.DIM), device="cuda")])
+    sums, counts, assign = KM.step(x, c, planes=planes)
+    rs, rc, ra, d = KM.step_reference(x, c)
+    top2 = torch.topk(d, min(2, k), dim=1, largest=False).values
+    tied = (top2[:, 1] - top2[:, 0] <= 1e-3 * top2[:, 0].abs().clamp_min(1.0)) if k > 1 else torch.zeros(n, dtype=torch.bool, device="cuda")
+    assert int(((assign.long() != ra.long()) & ~tied).sum()) == 0
+    if int(tied.sum()) == 0:
+        assert torch.equal(counts, rc)
+        torch.testing.assert_close(sums, rs, rtol=2e-5, atol=1e-3)
+
+
+def test_kmeans_split_planes_exact():
+    """The once-per-table split: x == (xh + xm) + xl bit for bit, equal to the torch twin (magnitudes
+    that keep the remainders normal: the device flushes f32 denormals)."""
+    from dryad_amd.ops import kmeans as KM
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn((4099, KM.DIM), generator=g) * torch.logspace(-20, 20, 4099)[:, None]).cuda()
+    sp = KM.split_points(x)
+    h, m, lo = sp.planes[0].float(), sp.planes[1].float(), sp.planes[2].float()
+    assert torch.equal((h + m) + lo, x)
+    th, tm, tl = KM.split_reference(x)
+    assert torch.equal(sp.planes[0], th) and torch.equal(sp.planes[1], tm) and torch.equal(sp.planes[2], tl)
+    ok = x.abs().amax(1) < 1e17          # |x|^2 of larger rows overflows f32 (the near-tie bound
+    torch.testing.assert_close(sp.xnorm[ok], x[ok].double().norm(dim=1).float(), rtol=1e-5, atol=0)
+    big = x.abs().amax(1) > 1e20
+    assert bool(torch.isinf(sp.xnorm[big]).all())   # becomes inf: such points are always re-ranked)
+    assert KM.split_points(x) is sp                     # cached across steps
+    x.mul_(2)
+    assert KM.split_points(x) is not sp                 # an in-place change re-splits
+
+
+@pytest.mark.parametrize("planes", [True, False])
+def test_kmeans_sums_exact_on_24bit_points(planes):
+    """Coordinates using all 24 significand bits (a two-part bf16 split drops their low bits):
+    one point per cluster, so f32 accumulation is exact and the sums must equal the points bit
+    for bit, also after every point changes cluster (the xl part moves with it)."""
+    from dryad_amd.ops import kmeans as KM
+    g = torch.Generator().manual_seed(5)
+    k = 64
+    x = torch.randint(1 << 23, 1 << 24, (k, KM.DIM), generator=g).float().cuda() * 2.0 ** -20
+    h, m, _ = KM.split_reference(x)
+    assert not torch.equal(h.float() + m.float(), x)     # the data really needs the third part
+    ws = KM.KMeansWorkspace(k, k, x.device)
+    sums, counts, assign = KM.step(x, x.clone(), ws, planes=planes)
+    assert torch.equal(assign.long().cpu(), torch.arange(k))
+    assert torch.equal(counts, torch.ones(k, dtype=torch.int64, device="cuda"))
+    assert torch.equal(sums, x.double())
+    perm = torch.randperm(k, generator=g)
+    sums, counts, assign = KM.step(x, x[perm.cuda()].clone(), ws, planes=planes)
+    inv = torch.argsort(perm)
+    assert torch.equal(assign.long().cpu(), inv)
+    assert torch.equal(sums, x[perm.cuda()].double())
+
+
+def test_kmeans_planes_iterations_track_f64_sums():
+    """Ten iterations on the split planes (assignments change, so xl moves between clusters):
+    every step's sums stay within f32 accumulation error of the f64 oracle's."""
+    from dryad_amd.ops import kmeans as KM
+    n, k = 300_000, 48
+    x = torch.empty((n, KM.DIM), dtype=torch.float32, device="cuda")
+    KM.generate(x, 0, blobs=32, seed=11)
+    x.add_(1000.0)                                      # constant offset: xl is far from zero-mean
+    c = x[:k].clone()
+    ws = KM.KMeansWorkspace(n, k, x.device)
+    for _ in range(10):
+        s, cnt, a = KM.step(x, c, ws)
+        rs, rc, ra, _d = KM.step_reference(x, c)
+        if torch.equal(a.long(), ra.long()):
+            assert torch.equal(cnt, rc)
+            torch.testing.assert_close(s, rs, rtol=2e-6, atol=0)
+        c = KM.update(c, s, cnt)
+
+
 def test_kmeans_generate_counter_based():
     from dryad_amd.ops import kmeans as KM
     a = torch.empty((1000, KM.DIM), dtype=torch.float32, device="cuda")

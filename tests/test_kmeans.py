@@ -53,3 +53,34 @@ def test_kmeans_do_while_matches_loop():
     loop = KMeansJob(_local_debug(), cfg, partitions=2).run()
     dw = KMeansJob(_local_debug(), cfg, partitions=2).run_do_while()
     np.testing.assert_allclose(dw, loop.centroids, atol=1e-6)
+
+
+def test_split_reference_is_exact_three_part():
+    """The k-means split planes' twin: x == (xh + xm) + xl for every f32 magnitude, and 24-bit
+    coordinates really need the third part."""
+    import torch
+    from dryad_amd.ops import kmeans as KM
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn((2000, KM.DIM), generator=g) * torch.logspace(-30, 30, 2000)[:, None]
+    h, m, lo = KM.split_reference(x)
+    assert torch.equal((h.float() + m.float()) + lo.float(), x)
+    xi = torch.randint(1 << 23, 1 << 24, (64, KM.DIM), generator=g).float()
+    h, m, lo = KM.split_reference(xi)
+    assert torch.equal((h.float() + m.float()) + lo.float(), xi)
+    assert not torch.equal(h.float() + m.float(), xi)
+
+
+def test_split_cache_follows_owner_and_version():
+    import gc
+    import torch
+    from dryad_amd.ops import kmeans as KM
+    x = torch.randn(300, KM.DIM)
+    a = KM.split_points(x)
+    assert KM.split_points(x[:]) is a                    # a new view of the same points hits
+    x.add_(1.0)
+    b = KM.split_points(x)
+    assert b is not a and torch.equal(b.planes[0], x.bfloat16())
+    n0 = len(KM._SPLITS)
+    del x, a, b
+    gc.collect()
+    assert len(KM._SPLITS) == n0 - 1                     # the entry dies with its owner

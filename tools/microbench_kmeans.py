@@ -33,11 +33,17 @@ def main():
     for k in ks:
         c = x[:k].clone()
         ws = KM.KMeansWorkspace(n, k, x.device)
-        ms = timeit(lambda: KM.step(x, c, ws))
         gb = n * KM.DIM * 4 / 1e9
-        res[f"mfma k={k} ms"] = round(ms, 3)
-        res[f"mfma k={k} GB/s"] = round(gb / ms * 1e3, 1)
-        res[f"mfma k={k} TFLOP/s"] = round(2 * n * k * KM.DIM / ms / 1e9, 1)
+        for tag, pl in (("planes", None), ("f32", False)) if k <= KM.PLANES_MAX_K else (("mfma", False),):
+            if tag == "planes":
+                t0 = time.perf_counter()
+                KM.split_points(x)
+                torch.cuda.synchronize()
+                res["split ms (once)"] = round((time.perf_counter() - t0) * 1e3, 3)
+            ms = timeit(lambda: KM.step(x, c, ws, planes=pl))
+            res[f"{tag} k={k} ms"] = round(ms, 3)
+            res[f"{tag} k={k} GB/s"] = round(gb / ms * 1e3, 1)
+            res[f"{tag} k={k} TFLOP/s"] = round(2 * n * k * KM.DIM / ms / 1e9, 1)
         if n <= 20_000_000 and os.environ.get("KM_TORCH") == "1":
             res[f"torch k={k} ms"] = round(timeit(lambda: KM.step_reference(x, c), 2), 3)
     print(json.dumps(res))
