@@ -7,7 +7,7 @@
 // nothing and the sort-based path pays 4 radix passes plus a random-row gather (45 ms of 32-byte
 // reads through the permutation, profiles/r2_kernels_gb.csv).  The reference's ParallelHashGroupBy
 // (DryadLinqVertex.cs:5342-6417) hashes every record into a per-thread dictionary; on MI355X the
-// dictionary becomes a 2^11-slot LDS table per workgroup, reached after two stable partition
+// dictionary becomes a 2^12-slot LDS table per workgroup, reached after two stable partition
 // passes over 16-byte rows:
 //
 //   row          key - kmin (kbits) | v0 - vmin0 | v1 - vmin1 | v2 - vmin2, bit-packed into 128 bits
@@ -15,20 +15,26 @@
 //   pass 1       columns -> rows, stable partition by key bits [tb, tb + d1)     (dg_scatter<true>)
 //   pass 2       rows -> rows, stable partition by key bits [tb + d1, kbits)    (dg_scatter<false>)
 //                => rows ordered by key >> tb: every run of equal key >> tb is one LDS table
-//   aggregate    one workgroup per (pass-2 bucket, piece of pass-1 digits): finds each run with a
-//                64-ary wave search, folds it into the table with LDS integer atomics (count,
-//                sum / min / max of the offsets), emits the occupied slots (global output cursor)
+//   aggregate    every workgroup streams an equal slice of the rows (ends moved to run starts by
+//                two 64-ary wave searches), folds each run into the table with LDS integer atomics
+//                (count, sum / min / max of the offsets) and emits the occupied slots when the run
+//                id changes (global output cursor)
 //
 // Each partition pass is count (per-workgroup histograms, bucket-major) + exclusive scan (host
-// side, torch) + scatter: a workgroup ranks a 2048-row tile by digit with wave64 ballot
+// side, torch) + scatter: a workgroup ranks a 4096-row tile by digit with wave64 ballot
 // multisplits, writes the rows into LDS in bucket order and stores every bucket's run contiguously.
 #include "common.h"
 
 namespace {
-constexpr int kDgTile = 2048;
-constexpr int kDgItems = kDgTile / kBlock;    // rows per thread per tile
+// Scatter and aggregate workgroups are 512 threads (8 waves), one per CU: a 4096-row tile puts
+// 8 rows (128 bytes, a full line) per bucket per tile at 512 buckets; scattered 16-byte rows
+// (2048-row tiles into 1024 buckets) measured 2.5-2.8x the written bytes at the memory side.
+constexpr int kDgThreads = 512;
+constexpr int kDgWaves = kDgThreads / 64;
+constexpr int kDgTile = 4096;
+constexpr int kDgItems = kDgTile / kDgThreads; // rows per thread per tile
 constexpr int kDgMaxDigit = 10;               // digit bits per pass (1024 buckets)
-constexpr int kDgTableBits = 11;              // LDS table slots per run: 2048
+constexpr int kDgTableBits = 12;              // LDS table slots per run: 4096
 constexpr int kDgSlots = 1 << kDgTableBits;
 constexpr int kDgMaxCols = 3;
 
@@ -44,17 +50,22 @@ struct DgPack {
   uint32_t ncols;
 };
 
-__device__ __forceinline__ u128 dg_pack_row(const DgPack& p, uint64_t i) {
-  u128 r = (u128)(uint64_t)(p.key[i] - p.kmin);
-  uint32_t off = p.kbits;
+// Exclusive scan across the 512-thread workgroup; scratch holds kDgWaves words of LDS.
+__device__ __forceinline__ uint32_t dg_block_scan(uint32_t v, uint32_t* scratch, uint32_t& total) {
+  const int w = wave_id(), l = lane_id();
+  const uint32_t inc = wave_inclusive_scan(v);
+  if (l == 63) scratch[w] = inc;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
 #pragma unroll
-  for (int j = 0; j < kDgMaxCols; ++j) {
-    if (j < (int)p.ncols) {
-      r |= (u128)(uint64_t)(p.col[j][i] - p.vmin[j]) << off;
-      off += p.vbits[j];
-    }
+  for (int k = 0; k < kDgWaves; ++k) {
+    const uint32_t x = scratch[k];
+    base += k < w ? x : 0u;
+    tot += x;
   }
-  return r;
+  total = tot;
+  __syncthreads();
+  return base + inc - v;
 }
 
 __device__ __forceinline__ uint64_t dg_field(u128 r, uint32_t off, uint32_t bits) {
@@ -92,50 +103,80 @@ __global__ __launch_bounds__(256) void dg_count_kernel(const int64_t* __restrict
 }
 
 // Stable partition of rows [beg, end) of each workgroup by digit; offsets[d * G + b] = first output
-// row of workgroup b's bucket d (exclusive prefix of the bucket-major counts).
-template <bool FROM_COLS>
-__global__ __launch_bounds__(256) void dg_scatter_kernel(DgPack pk, const uint4* __restrict__ in, uint64_t n,
-                                                         uint32_t shift, uint32_t dbits,
-                                                         const int64_t* __restrict__ offsets, uint32_t G,
+// row of workgroup b's bucket d (exclusive prefix of the bucket-major counts).  The next tile's
+// inputs are loaded while the current tile is ranked and written.
+template <bool FROM_COLS, int DB>
+__global__ __launch_bounds__(kDgThreads) void dg_scatter_kernel(DgPack pk, const uint4* __restrict__ in, uint64_t n,
+                                                         uint32_t shift, const int64_t* __restrict__ offsets, uint32_t G,
                                                          uint64_t per_block, uint4* __restrict__ out) {
+  constexpr uint32_t nb = 1u << DB, mask = nb - 1;
+  constexpr int kPer = (nb + kDgThreads - 1) / kDgThreads;   // buckets per thread in the scans
   __shared__ uint4 tile[kDgTile];
   __shared__ uint16_t dslot[kDgTile];
-  __shared__ uint32_t wcnt[4][1 << kDgMaxDigit];
-  __shared__ int64_t goff[1 << kDgMaxDigit];
-  __shared__ uint32_t bstart[1 << kDgMaxDigit];
-  __shared__ uint32_t sc[4];
+  __shared__ uint32_t wcnt[kDgWaves][nb];
+  __shared__ int64_t goff[nb];
+  __shared__ uint32_t bstart[nb];
+  __shared__ uint32_t sc[kDgWaves];
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
-  const uint32_t nb = 1u << dbits, mask = nb - 1;
-  constexpr int kPer = (1 << kDgMaxDigit) / kBlock;   // buckets per thread in the scans
   const uint64_t beg = (uint64_t)blockIdx.x * per_block;
   const uint64_t end = beg + per_block < n ? beg + per_block : n;
   if (beg >= end) return;                              // uniform: the whole workgroup leaves
   const uint64_t kmask = pk.kbits >= 64 ? ~0ull : ((1ull << pk.kbits) - 1);
-  for (uint32_t i = t; i < nb; i += kBlock) goff[i] = offsets[(uint64_t)i * G + blockIdx.x];
+  for (uint32_t i = t; i < nb; i += kDgThreads) goff[i] = offsets[(uint64_t)i * G + blockIdx.x];
+  // raw inputs of one tile: the key and value columns (FROM_COLS) or the packed rows
+  constexpr int kRaw = FROM_COLS ? 1 + kDgMaxCols : 1;
+  int64_t rawc[FROM_COLS ? kDgItems : 1][kRaw];
+  uint4 rawr[FROM_COLS ? 1 : kDgItems];
+  auto load_raw = [&](uint64_t tb) {
+#pragma unroll
+    for (int r = 0; r < kDgItems; ++r) {
+      const uint64_t i = tb + w * (kDgTile / kDgWaves) + r * 64 + l;
+      const bool ok = i < end;
+      if constexpr (FROM_COLS) {
+        rawc[r][0] = ok ? pk.key[i] : pk.kmin;
+#pragma unroll
+        for (int j = 0; j < kDgMaxCols; ++j)
+          rawc[r][1 + j] = (ok && j < (int)pk.ncols) ? pk.col[j][i] : pk.vmin[j];
+      } else {
+        rawr[r] = ok ? in[i] : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+  };
+  load_raw(beg);
   for (uint64_t base = beg; base < end; base += kDgTile) {
     const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kDgTile ? (end - base) : kDgTile);
-    for (uint32_t i = t; i < 4 * nb; i += kBlock) (&wcnt[0][0])[(i / nb) * (1 << kDgMaxDigit) + (i % nb)] = 0;
-    __syncthreads();
+    for (uint32_t i = t; i < kDgWaves * nb; i += kDgThreads) (&wcnt[0][0])[i] = 0;
     uint4 rv[kDgItems];
+#pragma unroll
+    for (int r = 0; r < kDgItems; ++r) {
+      if constexpr (FROM_COLS) {
+        u128 v = (u128)(uint64_t)(rawc[r][0] - pk.kmin);
+        uint32_t off = pk.kbits;
+#pragma unroll
+        for (int j = 0; j < kDgMaxCols; ++j) {
+          if (j < (int)pk.ncols) {
+            v |= (u128)(uint64_t)(rawc[r][1 + j] - pk.vmin[j]) << off;
+            off += pk.vbits[j];
+          }
+        }
+        rv[r] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96));
+      } else {
+        rv[r] = rawr[r];
+      }
+    }
+    if (base + kDgTile < end) load_raw(base + kDgTile);   // next tile in flight
+    __syncthreads();
     uint32_t rk[kDgItems], dg[kDgItems];
 #pragma unroll
     for (int r = 0; r < kDgItems; ++r) {
-      const uint32_t pos = w * (kDgTile / 4) + r * 64 + l;
+      const uint32_t pos = w * (kDgTile / kDgWaves) + r * 64 + l;
       const bool valid = pos < cnt;
-      uint4 row = make_uint4(0u, 0u, 0u, 0u);
-      if (valid) {
-        if constexpr (FROM_COLS) {
-          const u128 v = dg_pack_row(pk, base + pos);
-          row = make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96));
-        } else {
-          row = in[base + pos];
-        }
-      }
-      const uint64_t ko = (((uint64_t)row.y << 32) | row.x) & kmask;
+      const uint64_t ko = (((uint64_t)rv[r].y << 32) | rv[r].x) & kmask;
       const uint32_t d = valid ? (uint32_t)((ko >> shift) & mask) : 0u;
       // wave64 multisplit: the lanes holding the same digit, by one ballot per digit bit
       uint64_t peers = ballot64(valid);
-      for (uint32_t k = 0; k < dbits; ++k) {
+#pragma unroll
+      for (int k = 0; k < DB; ++k) {
         const bool bit = (d >> k) & 1u;
         const uint64_t b = ballot64(bit);
         peers &= bit ? b : ~b;
@@ -147,7 +188,6 @@ __global__ __launch_bounds__(256) void dg_scatter_kernel(DgPack pk, const uint4*
       __builtin_amdgcn_wave_barrier();
       rk[r] = prior + below;
       dg[r] = d;
-      rv[r] = row;
     }
     __syncthreads();
     // bucket totals, wave offsets inside each bucket, and the bucket starts inside the tile
@@ -157,14 +197,19 @@ __global__ __launch_bounds__(256) void dg_scatter_kernel(DgPack pk, const uint4*
       const uint32_t b = t * kPer + q;
       tot[q] = 0;
       if (b < nb) {
-        const uint32_t c0 = wcnt[0][b], c1 = wcnt[1][b], c2 = wcnt[2][b], c3 = wcnt[3][b];
-        tot[q] = c0 + c1 + c2 + c3;
-        wcnt[0][b] = 0; wcnt[1][b] = c0; wcnt[2][b] = c0 + c1; wcnt[3][b] = c0 + c1 + c2;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < kDgWaves; ++k) {
+          const uint32_t c = wcnt[k][b];
+          wcnt[k][b] = acc;
+          acc += c;
+        }
+        tot[q] = acc;
       }
       run += tot[q];
     }
     uint32_t all;
-    uint32_t pre = block_exclusive_scan256(run, sc, all);
+    uint32_t pre = dg_block_scan(run, sc, all);
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const uint32_t b = t * kPer + q;
@@ -174,7 +219,7 @@ __global__ __launch_bounds__(256) void dg_scatter_kernel(DgPack pk, const uint4*
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kDgItems; ++r) {
-      const uint32_t pos = w * (kDgTile / 4) + r * 64 + l;
+      const uint32_t pos = w * (kDgTile / kDgWaves) + r * 64 + l;
       if (pos < cnt) {
         const uint32_t slot = bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
         tile[slot] = rv[r];
@@ -183,7 +228,7 @@ __global__ __launch_bounds__(256) void dg_scatter_kernel(DgPack pk, const uint4*
     }
     __syncthreads();
     // consecutive slots of one bucket are consecutive output rows
-    for (uint32_t j = t; j < cnt; j += kBlock) {
+    for (uint32_t j = t; j < cnt; j += kDgThreads) {
       const uint32_t d = dslot[j];
       out[goff[d] + (int64_t)(j - bstart[d])] = tile[j];
     }
@@ -193,7 +238,6 @@ __global__ __launch_bounds__(256) void dg_scatter_kernel(DgPack pk, const uint4*
       const uint32_t b = t * kPer + q;
       if (b < nb) goff[b] += tot[q];
     }
-    __syncthreads();
   }
 }
 
@@ -237,10 +281,15 @@ __device__ __forceinline__ uint64_t dg_lower_bound(const uint4* __restrict__ row
   return lo + (uint64_t)(m ? __builtin_ctzll(m) : (int)(hi - lo));
 }
 
-// One workgroup per (bucket b of the last partition pass, piece q): rows [bstart[b], bstart[b+1])
-// are ordered by run id; the piece covers the runs b * runs_per_bucket + [q * rpp, (q + 1) * rpp).
-__global__ __launch_bounds__(256) void dg_agg_kernel(const uint4* __restrict__ rows, const int64_t* __restrict__ bstart,
-                                                     uint32_t nbuckets, uint32_t pieces, uint64_t runs_per_bucket,
+__device__ __forceinline__ uint64_t dg_run(const uint4& r, uint64_t kmask) {
+  return ((((uint64_t)r.y << 32) | r.x) & kmask) >> kDgTableBits;
+}
+
+// The rows are sorted by run id (key offset >> table bits).  Workgroup b owns the runs that start
+// in rows [b * per, (b + 1) * per): it moves both ends forward to run starts (two 64-ary searches),
+// then streams its rows 1024 at a time (the next 1024 in flight), folding each run into the LDS
+// table and emitting the table whenever the run id changes.
+__global__ __launch_bounds__(kDgThreads) void dg_agg_kernel(const uint4* __restrict__ rows, uint64_t n, uint64_t per,
                                                      uint32_t kbits, int64_t kmin, DgAgg ag,
                                                      unsigned long long* __restrict__ head, int64_t* __restrict__ okey,
                                                      int64_t* __restrict__ ocnt, int64_t* __restrict__ oacc0,
@@ -248,104 +297,114 @@ __global__ __launch_bounds__(256) void dg_agg_kernel(const uint4* __restrict__ r
   __shared__ uint32_t cnt[kDgSlots];
   __shared__ unsigned long long acc[kDgMaxCols][kDgSlots];
   __shared__ uint64_t bounds[2];
-  __shared__ uint32_t sc[4];
-  __shared__ unsigned long long obase;
+  __shared__ uint32_t sc[kDgWaves];
+  __shared__ unsigned long long obase, next_run;
   const int t = threadIdx.x, w = wave_id();
   const uint64_t kmask = kbits >= 64 ? ~0ull : ((1ull << kbits) - 1);
   int64_t* const oacc[3] = {oacc0, oacc1, oacc2};
-  constexpr int kSlotsPer = kDgSlots / kBlock;
-  auto reset = [&]() {
+  constexpr int kSlotsPer = kDgSlots / kDgThreads;
+  constexpr int kU = 4;                                 // rows per thread per step
+  for (int q = 0; q < kSlotsPer; ++q) {
+    const int sl = t * kSlotsPer + q;
+    cnt[sl] = 0;
+#pragma unroll
+    for (int a = 0; a < kDgMaxCols; ++a)
+      if (a < (int)ag.nacc) acc[a][sl] = ag.op[a] == 1 ? ~0ull : 0ull;
+  }
+  const uint64_t a0 = (uint64_t)blockIdx.x * per;
+  if (a0 >= n) return;                                  // uniform
+  const uint64_t b0 = a0 + per < n ? a0 + per : n;
+  if (w == 0) {
+    uint64_t s = a0, e = n;
+    if (a0 > 0) s = dg_lower_bound(rows, a0, n, kmask, dg_run(rows[a0 - 1], kmask) + 1);
+    if (b0 < n) e = dg_lower_bound(rows, b0, n, kmask, dg_run(rows[b0 - 1], kmask) + 1);
+    if (lane_id() == 0) { bounds[0] = s; bounds[1] = e; }
+  }
+  __syncthreads();
+  const uint64_t beg = bounds[0], end = bounds[1];
+  if (beg >= end) return;                               // uniform: no run starts here
+  uint64_t cur = dg_run(rows[beg], kmask);
+  // emit the occupied slots of run `run`: count, reserve a range of the output, write, reset
+  auto emit = [&](uint64_t run) {
+    uint32_t occ = 0;
+#pragma unroll
+    for (int q = 0; q < kSlotsPer; ++q) occ += cnt[t * kSlotsPer + q] != 0;
+    uint32_t total;
+    uint32_t pre = dg_block_scan(occ, sc, total);
+    if (t == 0) obase = atomicAdd(head, (unsigned long long)total);
+    __syncthreads();
+    const uint64_t o0 = obase;
 #pragma unroll
     for (int q = 0; q < kSlotsPer; ++q) {
-      const int s = t + q * kBlock;
-      cnt[s] = 0;
-#pragma unroll
-      for (int a = 0; a < kDgMaxCols; ++a)
-        if (a < (int)ag.nacc) acc[a][s] = ag.op[a] == 1 ? ~0ull : 0ull;
-    }
-  };
-  reset();
-  const uint64_t rpp = (runs_per_bucket + pieces - 1) / pieces;
-  for (uint64_t item = blockIdx.x; item < (uint64_t)nbuckets * pieces; item += gridDim.x) {
-    const uint32_t b = (uint32_t)(item / pieces), q = (uint32_t)(item % pieces);
-    const uint64_t blo = (uint64_t)bstart[b], bhi = (uint64_t)bstart[b + 1];
-    const uint64_t run0 = (uint64_t)b * runs_per_bucket + (uint64_t)q * rpp;
-    const uint64_t run1 = (uint64_t)b * runs_per_bucket + ((uint64_t)(q + 1) * rpp < runs_per_bucket
-                                                               ? (uint64_t)(q + 1) * rpp : runs_per_bucket);
-    if (blo == bhi || run0 >= run1) continue;          // uniform
-    // this piece's rows, then run by run
-    if (w == 0) {
-      const uint64_t s0 = dg_lower_bound(rows, blo, bhi, kmask, run0);
-      const uint64_t s1 = dg_lower_bound(rows, s0, bhi, kmask, run1);
-      if (lane_id() == 0) { bounds[0] = s0; bounds[1] = s1; }
-    }
-    __syncthreads();
-    uint64_t pos = bounds[0];
-    const uint64_t pend = bounds[1];
-    __syncthreads();
-    while (pos < pend) {
-      // the run of the row at pos: rows up to the first row of the next run
-      uint64_t run;
-      {
-        const uint4 r = rows[pos];
-        run = ((((uint64_t)r.y << 32) | r.x) & kmask) >> kDgTableBits;
-      }
-      if (w == 0) {
-        const uint64_t e = dg_lower_bound(rows, pos, pend, kmask, run + 1);
-        if (lane_id() == 0) bounds[1] = e;
-      }
-      __syncthreads();
-      const uint64_t rend = bounds[1];
-      for (uint64_t i = pos + t; i < rend; i += kBlock) {
-        const uint4 rr = rows[i];
-        const u128 v = (u128)rr.x | ((u128)rr.y << 32) | ((u128)rr.z << 64) | ((u128)rr.w << 96);
-        const uint32_t s = (uint32_t)((uint64_t)v & (kDgSlots - 1));
-        atomicAdd(&cnt[s], 1u);
+      const int sl = t * kSlotsPer + q;
+      const uint32_t c = cnt[sl];
+      if (c) {
+        const uint64_t o = o0 + pre++;
+        okey[o] = kmin + (int64_t)((run << kDgTableBits) | (uint64_t)sl);
+        ocnt[o] = c;
 #pragma unroll
         for (int a = 0; a < kDgMaxCols; ++a) {
           if (a < (int)ag.nacc) {
-            const unsigned long long f = dg_field(v, ag.field_off[a], ag.field_bits[a]);
-            if (ag.op[a] == 0) atomicAdd(&acc[a][s], f);
-            else if (ag.op[a] == 1) atomicMin(&acc[a][s], f);
-            else atomicMax(&acc[a][s], f);
+            const int64_t av = (int64_t)acc[a][sl];
+            oacc[a][o] = ag.op[a] == 0 ? av + (int64_t)c * ag.vmin[a] : av + ag.vmin[a];
           }
         }
+        cnt[sl] = 0;
+#pragma unroll
+        for (int a = 0; a < kDgMaxCols; ++a)
+          if (a < (int)ag.nacc) acc[a][sl] = ag.op[a] == 1 ? ~0ull : 0ull;
       }
-      __syncthreads();
-      // emit the occupied slots: count, reserve a range of the output, write, reset
-      uint32_t occ = 0;
+    }
+    __syncthreads();
+  };
+  uint4 buf[kU], nbuf[kU];
+  auto load = [&](uint64_t base, uint4* dst) {
 #pragma unroll
-      for (int q2 = 0; q2 < kSlotsPer; ++q2) occ += cnt[t * kSlotsPer + q2] != 0;
-      uint32_t total;
-      uint32_t pre = block_exclusive_scan256(occ, sc, total);
-      if (t == 0) obase = atomicAdd(head, (unsigned long long)total);
-      __syncthreads();
-      const uint64_t o0 = obase;
+    for (int u = 0; u < kU; ++u) {
+      const uint64_t i = base + (uint64_t)u * kDgThreads + t;
+      dst[u] = i < end ? rows[i] : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  load(beg, buf);
+  for (uint64_t base = beg; base < end; base += kU * kDgThreads) {
+    load(base + kU * kDgThreads, nbuf);                 // the next step in flight
 #pragma unroll
-      for (int q2 = 0; q2 < kSlotsPer; ++q2) {
-        const int s = t * kSlotsPer + q2;
-        const uint32_t c = cnt[s];
-        if (c) {
-          const uint64_t o = o0 + pre++;
-          okey[o] = kmin + (int64_t)((run << kDgTableBits) | (uint64_t)s);
-          ocnt[o] = c;
+    for (int u = 0; u < kU; ++u) {
+      const uint64_t i = base + (uint64_t)u * kDgThreads + t;
+      bool todo = i < end;
+      const uint4 rr = buf[u];
+      const uint64_t rid = dg_run(rr, kmask);
+      const u128 v = (u128)rr.x | ((u128)rr.y << 32) | ((u128)rr.z << 64) | ((u128)rr.w << 96);
+      // rows are sorted by run: those of the current run come first, later runs follow
+      while (true) {
+        if (todo && rid == cur) {
+          const uint32_t sl = (uint32_t)((uint64_t)v & (kDgSlots - 1));
+          atomicAdd(&cnt[sl], 1u);
 #pragma unroll
           for (int a = 0; a < kDgMaxCols; ++a) {
             if (a < (int)ag.nacc) {
-              const int64_t av = (int64_t)acc[a][s];
-              oacc[a][o] = ag.op[a] == 0 ? av + (int64_t)c * ag.vmin[a] : av + ag.vmin[a];
+              const unsigned long long f = dg_field(v, ag.field_off[a], ag.field_bits[a]);
+              if (ag.op[a] == 0) atomicAdd(&acc[a][sl], f);
+              else if (ag.op[a] == 1) atomicMin(&acc[a][sl], f);
+              else atomicMax(&acc[a][sl], f);
             }
           }
+          todo = false;
         }
-        cnt[s] = 0;
-#pragma unroll
-        for (int a = 0; a < kDgMaxCols; ++a)
-          if (a < (int)ag.nacc) acc[a][s] = ag.op[a] == 1 ? ~0ull : 0ull;
+        if (t == 0) next_run = ~0ull;
+        if (!__syncthreads_or(todo)) break;             // uniform
+        // a later run starts in this row slice: the current run is complete
+        atomicMin(&next_run, (unsigned long long)(todo ? rid : ~0ull));
+        __syncthreads();
+        const uint64_t nxt = next_run;
+        emit(cur);
+        cur = nxt;
       }
-      pos = rend;
-      __syncthreads();
     }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) buf[u] = nbuf[u];
   }
+  emit(cur);
 }
 }  // namespace
 
@@ -402,25 +461,35 @@ DR_API int dr_dg_scatter(const int64_t* key, const int64_t* const* cols, const i
   DgPack p;
   if (dg_pack_from(&p, key, cols, vmin, vbits, ncols, kmin, kbits)) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
-  if (in)
-    dg_scatter_kernel<false><<<G, 256, 0, s>>>(p, static_cast<const uint4*>(in), n, shift, dbits, offsets, G,
-                                                per_block, static_cast<uint4*>(out));
-  else
-    dg_scatter_kernel<true><<<G, 256, 0, s>>>(p, nullptr, n, shift, dbits, offsets, G, per_block,
-                                               static_cast<uint4*>(out));
+#define DG_SC(FC, DBV)                                                                                \
+  dg_scatter_kernel<FC, DBV><<<G, kDgThreads, 0, s>>>(p, static_cast<const uint4*>(in), n, shift, offsets, G, per_block, \
+                                               static_cast<uint4*>(out))
+#define DG_SC_ALL(FC)                                                                                 \
+  switch (dbits) {                                                                                    \
+    case 1: DG_SC(FC, 1); break; case 2: DG_SC(FC, 2); break; case 3: DG_SC(FC, 3); break;            \
+    case 4: DG_SC(FC, 4); break; case 5: DG_SC(FC, 5); break; case 6: DG_SC(FC, 6); break;            \
+    case 7: DG_SC(FC, 7); break; case 8: DG_SC(FC, 8); break; case 9: DG_SC(FC, 9); break;            \
+    default: DG_SC(FC, 10); break;                                                                    \
+  }
+  if (in) {
+    DG_SC_ALL(false);
+  } else {
+    DG_SC_ALL(true);
+  }
+#undef DG_SC_ALL
+#undef DG_SC
   DR_LAUNCH_CHECK();
   return 0;
 }
 
-// rows: n packed rows ordered by run id (key offset >> table bits) inside each of the nbuckets
-// ranges [bstart[b], bstart[b + 1]); bucket b holds the runs b * runs_per_bucket + [0, runs_per_bucket).
-// ops / off / bits / vmin: nacc accumulators over packed fields.  head (u64, zeroed) receives the
-// group count; outputs are sized by the caller (>= the number of groups).
-DR_API int dr_dg_aggregate(const void* rows, const int64_t* bstart, uint32_t nbuckets, uint64_t runs_per_bucket,
-                           uint32_t kbits, int64_t kmin, uint32_t nacc, const uint32_t* ops, const uint32_t* off,
-                           const uint32_t* bits, const int64_t* vmin, unsigned long long* head, int64_t* okey,
-                           int64_t* ocnt, int64_t* const* oacc, hipStream_t s) {
-  if (nacc > (uint32_t)kDgMaxCols || nbuckets == 0) return (int)hipErrorInvalidValue;
+// rows: n packed rows sorted by run id (key offset >> table bits).  ops / off / bits / vmin: nacc
+// accumulators over packed fields.  head (u64, zeroed) receives the group count; outputs are sized
+// by the caller (>= the number of groups).
+DR_API int dr_dg_aggregate(const void* rows, uint64_t n, uint32_t kbits, int64_t kmin, uint32_t nacc,
+                           const uint32_t* ops, const uint32_t* off, const uint32_t* bits, const int64_t* vmin,
+                           unsigned long long* head, int64_t* okey, int64_t* ocnt, int64_t* const* oacc,
+                           hipStream_t s) {
+  if (nacc > (uint32_t)kDgMaxCols) return (int)hipErrorInvalidValue;
   DgAgg ag;
   ag.nacc = nacc;
   for (uint32_t a = 0; a < (uint32_t)kDgMaxCols; ++a) {
@@ -431,14 +500,16 @@ DR_API int dr_dg_aggregate(const void* rows, const int64_t* bstart, uint32_t nbu
     if (a < nacc && (ag.op[a] > 2 || ag.field_bits[a] == 0 || ag.field_off[a] + ag.field_bits[a] > 128))
       return (int)hipErrorInvalidValue;
   }
-  // pieces: about 4 workgroups' worth of runs per resident workgroup
-  uint32_t pieces = 1;
-  while ((uint64_t)nbuckets * pieces < 2048 && pieces < runs_per_bucket) pieces <<= 1;
-  const uint64_t items = (uint64_t)nbuckets * pieces;
-  const unsigned grid = (unsigned)(items < 4096 ? items : 4096);
-  dg_agg_kernel<<<grid, 256, 0, s>>>(static_cast<const uint4*>(rows), bstart, nbuckets, pieces, runs_per_bucket, kbits,
-                                     kmin, ag, head, okey, ocnt, nacc > 0 ? oacc[0] : nullptr,
-                                     nacc > 1 ? oacc[1] : nullptr, nacc > 2 ? oacc[2] : nullptr);
+  if (n == 0) return 0;
+  // 1024 workgroups (4 rounds of one per CU) over equal row ranges; each handles the runs starting
+  // in its range
+  const uint64_t G = 1024;
+  uint64_t per = (n + G - 1) / G;
+  if (per < 4096) per = 4096;
+  const unsigned grid = (unsigned)((n + per - 1) / per);
+  dg_agg_kernel<<<grid, kDgThreads, 0, s>>>(static_cast<const uint4*>(rows), n, per, kbits, kmin, ag, head, okey, ocnt,
+                                     nacc > 0 ? oacc[0] : nullptr, nacc > 1 ? oacc[1] : nullptr,
+                                     nacc > 2 ? oacc[2] : nullptr);
   DR_LAUNCH_CHECK();
   return 0;
 }

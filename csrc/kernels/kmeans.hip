@@ -708,58 +708,39 @@ __global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __re
 }
 
 // ---------------------------------------------------------------------------------------------
-// K <= 64 on precomputed split planes (mode 3, default when the planes fit in HBM).
+// K <= 64 on a precomputed bf16 plane with incrementally maintained sums (mode 3, default when
+// the plane fits in HBM).
 //
-// Points are static across the iterations of a k-means job, so their exact three-part bf16 split
-// x = xh + xm + xl (each part a round-to-nearest bf16 of the remainder so far; 3 x 8 significand
-// bits cover f32's 24) is written ONCE (kmeans_split_kernel) into planes P[3][n][128] plus |x|
-// per point, and every iteration's kernel reads only the xh and xm planes: 512 B per point, the
-// bytes of the f32 row, with no conversion VALU left in the loop.
+// The points of a k-means job are static across its iterations, so two things are done once per
+// point table instead of once per iteration:
+//   * the bf16 rounding xh of every coordinate and |x| per point (kmeans_hi_kernel), 256 + 4 bytes
+//     per point: an iteration's assignment kernel reads half the bytes of the f32 rows and does
+//     no conversion work;
+//   * the per-cluster sums: S[c] = sum of x over the points assigned to c (f64) and the counts are
+//     kept with the table; after an iteration's final assignment, kmeans_movers_kernel moves the
+//     exact f32 row of every point whose cluster changed (all of them on the first iteration, a
+//     few percent after that) from its old cluster's sums to its new one's.
+// The step's result is therefore the exact sums of the f32 points of each cluster (f64
+// accumulation of f32 values), as a from-scratch pass would compute them.
 //
-//   distances  xh.ch + xh.cm + xm.ch as before, operands straight from the loaded registers
-//   sums       xh and xm: the block's 64 points are staged in two swizzled [point][dim] bf16 LDS
-//              images and read back transposed with ds_read_b64_tr_b16 (the sum MFMA reduces
-//              over points, the distance MFMA over dims)
-//   xl         the third part's per-cluster sums Sxl[c] = sum of xl over the points assigned to
-//              c are kept across steps: after the step's final assignment, kmeans_movers_kernel
-//              moves xl only for points whose assignment changed (all of them on the first step,
-//              a few after), and kmeans_add_kernel adds Sxl into the step's sums.
-// The sums are therefore those of the exact f32 points, up to the f32 accumulation of the
-// matrix-core accumulators (<= 128 steps, flushed to f64).
-__device__ __forceinline__ int km_img_off(int row, int ch) {
-  // byte offset of 16-byte chunk ch (0..15) of row `row` of a [64][128] bf16 image: 256-B rows
-  // with the chunk XOR-swizzled so the b128 row writes and the transposed reads spread over banks
-  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
-}
+//   assignment  each wave independently: 16-point tiles, xh.ch + xh.cm on 16x16x32 bf16 MFMAs
+//               (c = ch + cm split in LDS), argmin + runner-up merged over the 4 lanes of a point;
+//               |estimate - f32 distance| <= kKmTolH |x| max|c| (xh's rounding 2^-9 |x|, cm's
+//               residual 2^-17, f32 accumulation, doubled for d = |c|^2 - 2 x.c), so points whose
+//               best two estimates are closer than twice that are flagged and re-ranked exactly
+//               from the f32 row (kmeans_near_list + kmeans_rerank_kernel)
+constexpr float kKmTolH = 4.0e-3f;
 
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-__global__ __launch_bounds__(256) void kmeans_split_kernel(const float* __restrict__ X, uint64_t n,
-                                                           __bf16* __restrict__ P, float* __restrict__ xnorm) {
+__global__ __launch_bounds__(256) void kmeans_hi_kernel(const float* __restrict__ X, uint64_t n,
+                                                        __bf16* __restrict__ XH, float* __restrict__ xnorm) {
   // one wave per point, lane l: dims 2l, 2l + 1
   const int l = threadIdx.x & 63;
   const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   for (uint64_t p = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; p < n; p += nw) {
     const float2 v = reinterpret_cast<const float2*>(X + p * D)[l];
     float ss = fmaf(v.x, v.x, v.y * v.y);
-    __bf16 part[3][2];
-    const float vv[2] = {v.x, v.y};
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const __bf16 a0 = (__bf16)vv[e];
-      const float r1 = vv[e] - (float)a0;
-      const __bf16 a1 = (__bf16)r1;
-      part[0][e] = a0;
-      part[1][e] = a1;
-      part[2][e] = (__bf16)(r1 - (float)a1);
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      __bf16* dst = P + ((uint64_t)k * n + p) * D + 2 * l;
-      dst[0] = part[k][0];
-      dst[1] = part[k][1];
-    }
+    XH[p * D + 2 * l] = (__bf16)v.x;
+    XH[p * D + 2 * l + 1] = (__bf16)v.y;
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, 64);
     if (l == 0) xnorm[p] = sqrtf(ss);
@@ -767,20 +748,16 @@ __global__ __launch_bounds__(256) void kmeans_split_kernel(const float* __restri
 }
 
 template <int KT>
-__global__ __launch_bounds__(256, 2) void kmeans_planes_kernel(const __bf16* __restrict__ P,
-                                                               const float* __restrict__ xnorm, uint64_t n,
-                                                               const float* __restrict__ C,
-                                                               const float* __restrict__ cnorm, int K,
-                                                               int32_t* __restrict__ assign, double* __restrict__ gsum,
-                                                               unsigned long long* __restrict__ gcnt, int flush_steps) {
+__global__ __launch_bounds__(256) void kmeans_assign_kernel(const __bf16* __restrict__ XH,
+                                                            const float* __restrict__ xnorm, uint64_t n,
+                                                            const float* __restrict__ C,
+                                                            const float* __restrict__ cnorm, int K,
+                                                            int32_t* __restrict__ assign) {
   constexpr int KP = 16 * KT;
   __shared__ __attribute__((aligned(16))) __bf16 chi[KP * kCRow];
   __shared__ __attribute__((aligned(16))) __bf16 cmd[KP * kCRow];
   __shared__ float cn[KP];
   __shared__ float cmax_s;
-  __shared__ __attribute__((aligned(16))) __bf16 img[2][kM16Pts * D];   // xh, xm of the block's points
-  __shared__ __attribute__((aligned(16))) __bf16 ohs[KP * kM16Pts];
-  __shared__ unsigned int wcnt[KP];
   const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 15, g = l >> 4;
   for (int i = t; i < KP * D; i += 256) {
     const int c = i / D, d = i % D;
@@ -789,11 +766,7 @@ __global__ __launch_bounds__(256, 2) void kmeans_planes_kernel(const __bf16* __r
     chi[c * kCRow + d] = vh;
     cmd[c * kCRow + d] = (__bf16)(v - (float)vh);
   }
-  for (int i = t; i < KP * kM16Pts; i += 256) ohs[i] = (__bf16)0.f;
-  for (int c = t; c < KP; c += 256) {
-    cn[c] = c < K ? cnorm[c] : __builtin_inff();
-    wcnt[c] = 0u;
-  }
+  for (int c = t; c < KP; c += 256) cn[c] = c < K ? cnorm[c] : __builtin_inff();
   if (t == 0) {
     float m = 0.f;
     for (int c = 0; c < K; ++c) m = fmaxf(m, cnorm[c]);
@@ -801,83 +774,38 @@ __global__ __launch_bounds__(256, 2) void kmeans_planes_kernel(const __bf16* __r
   }
   __syncthreads();
   const float cmax = cmax_s;
-  const uint64_t steps = (n + kM16Pts - 1) / kM16Pts;
-  const __bf16* XH = P;
-  const __bf16* XM = P + n * D;
-  f32x4 S[KT][2];
+  const uint64_t tiles = (n + 15) / 16;
+  const uint64_t gw = (uint64_t)blockIdx.x * 4 + w, GW = (uint64_t)gridDim.x * 4;
+  // lane (r, g) holds dims 32 s + 8 g .. + 7 of point r of the tile, s < 4; clamped rows (a point
+  // past n re-reads point n - 1 and writes nothing), so the loads need no branch
+  bf16x8 xh[4];
+  float xn;
+  auto load = [&](uint64_t tile) {
+    const uint64_t p = min(tile * 16 + r, n - 1);
 #pragma unroll
-  for (int ct = 0; ct < KT; ++ct) {
-    S[ct][0] = f32x4{};
-    S[ct][1] = f32x4{};
-  }
-  // lane (r, g) holds dims 32 s + 8 g .. + 7 of its point, s < 4, of both planes
-  bf16x8 xh[4], xm[4];
-  float xn = 0.f, xn_next = 0.f;
-  // clamped, unconditional loads: a point past n re-reads point n - 1 (it sets no one-hot entry
-  // and writes no assignment), so no branch wraps them
-  auto row_of = [&](uint64_t step) { return min(step * kM16Pts + 16 * w + r, n - 1); };
-  {
-    const uint64_t p = row_of(blockIdx.x);
-#pragma unroll
-    for (int s_ = 0; s_ < 4; ++s_) {
-      xh[s_] = *reinterpret_cast<const bf16x8*>(XH + p * D + 32 * s_ + 8 * g);
-      xm[s_] = *reinterpret_cast<const bf16x8*>(XM + p * D + 32 * s_ + 8 * g);
-    }
+    for (int s_ = 0; s_ < 4; ++s_) xh[s_] = *reinterpret_cast<const bf16x8*>(XH + p * D + 32 * s_ + 8 * g);
     xn = xnorm[p];
-  }
-  auto flush = [&]() {
-#pragma unroll
-    for (int ct = 0; ct < KT; ++ct)
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int c = ct * 16 + 4 * g + q;
-          const float v = S[ct][dt][q];
-          if (c < K && v != 0.f) atomicAdd(gsum + (uint64_t)c * D + 32 * w + 16 * dt + r, (double)v);
-        }
-        S[ct][dt] = f32x4{};
-      }
   };
-  auto oh_at = [](int c, int pt) { return c * kM16Pts + 8 * ((pt >> 3) ^ ((c >> 1) & 7)) + (pt & 7); };
-  char* const imgb = reinterpret_cast<char*>(&img[0][0]);
-  // transposed-read addresses (T10): lane 4q + p of its 16-lane group reads row r0 + q, columns
-  // c0 + 4p .. + 3; it receives column c0 + (l & 15) of the 4 rows
-  const int tq = (l & 15) >> 2, tp = l & 3;
-  int since = 0, marked = -1;   // marked: the centroid whose one-hot entry this lane set last step
-  for (uint64_t step = blockIdx.x; step < steps; step += gridDim.x) {
-    const uint64_t p = step * kM16Pts + 16 * w + r;
-    const bool pvalid = p < n;
-    const int row = 16 * w + r;
-#pragma unroll
-    for (int s_ = 0; s_ < 4; ++s_) {
-      *reinterpret_cast<bf16x8*>(imgb + km_img_off(row, 4 * s_ + g)) = xh[s_];
-      *reinterpret_cast<bf16x8*>(imgb + kM16Pts * D * 2 + km_img_off(row, 4 * s_ + g)) = xm[s_];
-    }
+  if (gw < tiles) load(gw);
+  for (uint64_t tile = gw; tile < tiles; tile += GW) {
+    const uint64_t p = tile * 16 + r;
     f32x4 Dt[KT];
 #pragma unroll
     for (int ct = 0; ct < KT; ++ct) Dt[ct] = f32x4{};
-    const uint64_t pn = row_of(step + gridDim.x);
+    const bf16x8 b0 = xh[0], b1 = xh[1], b2 = xh[2], b3 = xh[3];
+    const float xnc = xn;
+    load(tile + GW < tiles ? tile + GW : tile);        // the next tile in flight under the MFMAs
+    const bf16x8 bx[4] = {b0, b1, b2, b3};
 #pragma unroll
     for (int s_ = 0; s_ < 4; ++s_) {
-      bf16x8 ah[KT], am[KT];
 #pragma unroll
       for (int ct = 0; ct < KT; ++ct) {
-        ah[ct] = *reinterpret_cast<const bf16x8*>(chi + (ct * 16 + r) * kCRow + 32 * s_ + 8 * g);
-        am[ct] = *reinterpret_cast<const bf16x8*>(cmd + (ct * 16 + r) * kCRow + 32 * s_ + 8 * g);
-      }
-      const bf16x8 bh = xh[s_], bm = xm[s_];
-      // the next step's dims of this k-step go in flight under the MFMAs, argmin and sums
-      xh[s_] = *reinterpret_cast<const bf16x8*>(XH + pn * D + 32 * s_ + 8 * g);
-      xm[s_] = *reinterpret_cast<const bf16x8*>(XM + pn * D + 32 * s_ + 8 * g);
-#pragma unroll
-      for (int ct = 0; ct < KT; ++ct) {
-        Dt[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[ct], bh, Dt[ct], 0, 0, 0);
-        Dt[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[ct], bm, Dt[ct], 0, 0, 0);
-        Dt[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[ct], bh, Dt[ct], 0, 0, 0);
+        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(chi + (ct * 16 + r) * kCRow + 32 * s_ + 8 * g);
+        const bf16x8 am = *reinterpret_cast<const bf16x8*>(cmd + (ct * 16 + r) * kCRow + 32 * s_ + 8 * g);
+        Dt[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bx[s_], Dt[ct], 0, 0, 0);
+        Dt[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bx[s_], Dt[ct], 0, 0, 0);
       }
     }
-    xn_next = xnorm[pn];
     float bd = __builtin_inff(), sd = __builtin_inff();
     int bj = 0;
 #pragma unroll
@@ -902,74 +830,25 @@ __global__ __launch_bounds__(256, 2) void kmeans_planes_kernel(const __bf16* __r
         sd = fminf(sd, obd);
       }
     }
-    const bool near = K > 1 && (sd - bd) <= 2.f * kKmTol * xn * cmax;
-    xn = xn_next;
-    if (g == 0) {
-      if (marked >= 0) ohs[oh_at(marked, row)] = (__bf16)0.f;
-      marked = pvalid ? bj : -1;
-      if (pvalid) {
-        ohs[oh_at(bj, row)] = (__bf16)1.f;
-        atomicAdd(&wcnt[bj], 1u);
-        assign[p] = near ? (int32_t)((uint32_t)bj | 0x80000000u) : bj;
-      }
-    }
-    __syncthreads();
-    // sums over the block's 64 points for this wave's dims 32 w .. 32 w + 31
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 oh[KT];
-#pragma unroll
-      for (int ct = 0; ct < KT; ++ct) oh[ct] = *reinterpret_cast<const bf16x8*>(ohs + oh_at(ct * 16 + r, 32 * ks + 8 * g));
-      bf16x8 bx[2][2];   // [dt][plane]: B[k = point 32 ks + 8 g + j][col = dim 32 w + 16 dt + (l & 15)]
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl) {
-          s16x4 lo4, hi4;
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            const int r0 = 32 * ks + 8 * g + 4 * hh;
-            const int c0 = 32 * w + 16 * dt;
-            const int off = pl * kM16Pts * D * 2 + km_img_off(r0 + tq, (c0 >> 3) + (tp >> 1)) + 8 * (tp & 1);
-            const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(imgb + off));
-            if (hh == 0) lo4 = v; else hi4 = v;
-          }
-          const short e[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
-#pragma unroll
-          for (int j = 0; j < 8; ++j) bx[dt][pl][j] = __builtin_bit_cast(__bf16, e[j]);
-        }
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int ct = 0; ct < KT; ++ct) {
-          S[ct][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oh[ct], bx[dt][0], S[ct][dt], 0, 0, 0);
-          S[ct][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oh[ct], bx[dt][1], S[ct][dt], 0, 0, 0);
-        }
-    }
-    __syncthreads();                          // images / ohs are rewritten by the next step
-    if (++since == flush_steps) {
-      since = 0;
-      flush();
-    }
+    const bool near = K > 1 && (sd - bd) <= 2.f * kKmTolH * xnc * cmax;
+    if (g == 0 && p < n) assign[p] = near ? (int32_t)((uint32_t)bj | 0x80000000u) : bj;
   }
-  flush();
-  __syncthreads();
-  for (int c = t; c < K; c += 256)
-    if (wcnt[c]) atomicAdd(gcnt + c, (unsigned long long)wcnt[c]);
 }
 
-// Moves the third split part of every point whose final assignment changed since the previous
-// step (prev < 0: never assigned) between the per-cluster sums Sxl, and records the assignment.
-// Centroid c's LDS row belongs to wave c & 3: plain read-modify-write, lanes = dim pairs; each wave
-// walks the block's 256-point batch by ballot and keeps 8 rows in flight.
-__global__ __launch_bounds__(256) void kmeans_movers_kernel(const __bf16* __restrict__ XL, uint64_t n,
+// Moves every point whose final assignment changed since the previous step (prev < 0: never
+// assigned) between the clusters' sums S (f64 [K][128]) and counts, and records the assignment.
+// Centroid c's LDS row belongs to wave c & 3: plain read-modify-write of f64, lanes = dims l and
+// 64 + l; each wave walks the block's 256-point batch by ballot and keeps 8 f32 rows in flight.
+__global__ __launch_bounds__(256) void kmeans_movers_kernel(const float* __restrict__ X, uint64_t n,
                                                             const int32_t* __restrict__ assign,
                                                             int32_t* __restrict__ prev, int K,
-                                                            double* __restrict__ sxl) {
-  __shared__ __attribute__((aligned(16))) float slab[64 * D];
+                                                            double* __restrict__ S, long long* __restrict__ cnt) {
+  __shared__ __attribute__((aligned(16))) double slab[64 * D];
+  __shared__ int dcnt[64];
   __shared__ int cur_s[256], old_s[256];
   const int t = threadIdx.x, w = t >> 6, l = t & 63;
-  for (int i = t; i < 64 * D; i += 256) slab[i] = 0.f;
+  for (int i = t; i < 64 * D; i += 256) slab[i] = 0.0;
+  if (t < 64) dcnt[t] = 0;
   for (uint64_t b = (uint64_t)blockIdx.x * 256; b < n; b += (uint64_t)gridDim.x * 256) {
     const uint64_t p = b + t;
     int a = -1, o = -1;
@@ -986,42 +865,42 @@ __global__ __launch_bounds__(256) void kmeans_movers_kernel(const __bf16* __rest
     for (int c = 0; c < 4; ++c) {
       const int ca = cur_s[64 * c + l], co = old_s[64 * c + l];
       const bool mv = ca != co;
-      // one list entry per (point, row this wave owns): +xl into row ca, -xl from row co
+      // one entry per (point, row this wave owns): +x into row ca, -x from row co
       uint64_t madd = ballot64(mv && ca >= 0 && (ca & 3) == w);
       uint64_t msub = ballot64(mv && co >= 0 && (co & 3) == w);
       while (madd | msub) {
         int idx[8], crow[8];
-        float sgn[8];
-        int cnt = 0;
+        double sgn[8];
+        int k8 = 0;
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          idx[u] = -1;
+          idx[u] = 0;
           crow[u] = 0;
-          sgn[u] = 0.f;
+          sgn[u] = 0.0;
           if (madd) {
             const int k = __builtin_ctzll(madd);
             madd &= madd - 1;
-            idx[u] = k; crow[u] = __builtin_amdgcn_readlane(ca, k); sgn[u] = 1.f; ++cnt;
+            idx[u] = k; crow[u] = __builtin_amdgcn_readlane(ca, k); sgn[u] = 1.0; ++k8;
           } else if (msub) {
             const int k = __builtin_ctzll(msub);
             msub &= msub - 1;
-            idx[u] = k; crow[u] = __builtin_amdgcn_readlane(co, k); sgn[u] = -1.f; ++cnt;
+            idx[u] = k; crow[u] = __builtin_amdgcn_readlane(co, k); sgn[u] = -1.0; ++k8;
           }
         }
-        uint32_t v[8];
+        float v0[8], v1[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const uint64_t pp = b + 64 * c + (idx[u] < 0 ? 0 : idx[u]);
-          v[u] = reinterpret_cast<const uint32_t*>(XL + pp * D)[l];
+          const float* xr = X + (b + 64 * c + idx[u]) * D;
+          v0[u] = xr[l];
+          v1[u] = xr[64 + l];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          if (u < cnt) {
-            float2* dst = reinterpret_cast<float2*>(slab + crow[u] * D) + l;
-            float2 s = *dst;
-            s.x += sgn[u] * __uint_as_float(v[u] << 16);
-            s.y += sgn[u] * __uint_as_float(v[u] & 0xFFFF0000u);
-            *dst = s;
+          if (u < k8) {
+            double* dst = slab + crow[u] * D;
+            dst[l] += sgn[u] * (double)v0[u];
+            dst[64 + l] += sgn[u] * (double)v1[u];
+            if (l == 0) dcnt[crow[u]] += sgn[u] > 0 ? 1 : -1;
           }
         }
       }
@@ -1029,13 +908,10 @@ __global__ __launch_bounds__(256) void kmeans_movers_kernel(const __bf16* __rest
   }
   __syncthreads();
   for (int i = t; i < K * D; i += 256) {
-    const float v = slab[i];
-    if (v != 0.f) atomicAdd(sxl + i, (double)v);
+    const double v = slab[i];
+    if (v != 0.0) atomicAdd(S + i, v);
   }
-}
-
-__global__ void kmeans_add_kernel(double* __restrict__ dst, const double* __restrict__ src, int m) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) dst[i] += src[i];
+  if (t < K && dcnt[t]) atomicAdd(reinterpret_cast<unsigned long long*>(cnt + t), (unsigned long long)(long long)dcnt[t]);
 }
 
 // Compaction of the near-tie flags (bit 31 of assign) into (point, estimate) pairs; clears the flag.
@@ -1074,13 +950,10 @@ __global__ __launch_bounds__(256) void kmeans_near_list(int32_t* __restrict__ as
 }
 
 // Exact f32 re-rank of the near-tie points listed by kmeans_near_list: one wave per point, lane
-// c computes the f32 distance to centroid c; if the estimate's choice was wrong the point's
-// contribution and count move to the right centroid.  The grid drains the device-side count.
-// PL: the points are split planes P[3][n][128] (x = xh + xm + xl exactly); the step kernel added
-// xh + xm, so that is what moves (the xl part follows the final assignment in kmeans_movers_kernel).
-template <bool PL>
-__global__ __launch_bounds__(64) void kmeans_rerank_kernel(const float* __restrict__ X, const __bf16* __restrict__ P,
-                                                           const float* __restrict__ C,
+// c computes the f32 distance to centroid c; if the estimate's choice was wrong the assignment is
+// corrected and, when the step kernel accumulated sums (gsum != null), the point's row and count
+// move to the right centroid.  The grid drains the device-side count.
+__global__ __launch_bounds__(64) void kmeans_rerank_kernel(const float* __restrict__ X, const float* __restrict__ C,
                                                            const float* __restrict__ cnorm, int K,
                                                            const uint32_t* __restrict__ near_cnt,
                                                            const uint32_t* __restrict__ near_list,
@@ -1088,22 +961,18 @@ __global__ __launch_bounds__(64) void kmeans_rerank_kernel(const float* __restri
                                                            unsigned long long* __restrict__ gcnt, uint64_t n) {
   const uint32_t total = (uint64_t)*near_cnt < n ? *near_cnt : (uint32_t)n;
   const int l = threadIdx.x;
-  auto xv = [&](uint64_t p, int d) -> float {
-    if constexpr (PL)
-      return ((float)P[p * D + d] + (float)P[(n + p) * D + d]) + (float)P[(2 * n + p) * D + d];
-    else
-      return X[p * D + d];
-  };
   for (uint32_t i = blockIdx.x; i < total; i += gridDim.x) {
     const uint64_t p = near_list[2 * (uint64_t)i];
     const int est = (int)near_list[2 * (uint64_t)i + 1];
+    const float4* xr = reinterpret_cast<const float4*>(X + p * D);
     float d = __builtin_inff();
     if (l < K) {
-      const float* cr = C + (uint64_t)l * D;
+      const float4* cr = reinterpret_cast<const float4*>(C + (uint64_t)l * D);
       float a0 = 0.f, a1 = 0.f;
-      for (int k = 0; k < D; k += 2) {
-        a0 = fmaf(xv(p, k), cr[k], a0);
-        a1 = fmaf(xv(p, k + 1), cr[k + 1], a1);
+      for (int k = 0; k < D / 4; k += 2) {
+        const float4 x0 = xr[k], x1 = xr[k + 1], c0 = cr[k], c1 = cr[k + 1];
+        a0 = fmaf(x0.x, c0.x, fmaf(x0.y, c0.y, fmaf(x0.z, c0.z, fmaf(x0.w, c0.w, a0))));
+        a1 = fmaf(x1.x, c1.x, fmaf(x1.y, c1.y, fmaf(x1.z, c1.z, fmaf(x1.w, c1.w, a1))));
       }
       d = cnorm[l] - 2.f * (a0 + a1);
     }
@@ -1114,25 +983,19 @@ __global__ __launch_bounds__(64) void kmeans_rerank_kernel(const float* __restri
       const int oj = __shfl_xor(bj, m, 64);
       if (od < d || (od == d && oj < bj)) { d = od; bj = oj; }
     }
-    if (bj != est) {
-      double v0, v1;
-      if constexpr (PL) {
-        v0 = (double)(float)P[p * D + l] + (double)(float)P[(n + p) * D + l];
-        v1 = (double)(float)P[p * D + 64 + l] + (double)(float)P[(n + p) * D + 64 + l];
-      } else {
-        v0 = X[p * D + l];
-        v1 = X[p * D + 64 + l];
-      }
-      atomicAdd(gsum + (uint64_t)est * D + l, -v0);
-      atomicAdd(gsum + (uint64_t)est * D + 64 + l, -v1);
-      atomicAdd(gsum + (uint64_t)bj * D + l, v0);
-      atomicAdd(gsum + (uint64_t)bj * D + 64 + l, v1);
+    if (bj == est) continue;
+    if (gsum) {
+      const float v0 = X[p * D + l], v1 = X[p * D + 64 + l];
+      atomicAdd(gsum + (uint64_t)est * D + l, -(double)v0);
+      atomicAdd(gsum + (uint64_t)est * D + 64 + l, -(double)v1);
+      atomicAdd(gsum + (uint64_t)bj * D + l, (double)v0);
+      atomicAdd(gsum + (uint64_t)bj * D + 64 + l, (double)v1);
       if (l == 0) {
         atomicAdd(gcnt + est, ~0ull);          // -1
         atomicAdd(gcnt + bj, 1ull);
-        assign[p] = bj;
       }
     }
+    if (l == 0) assign[p] = bj;
   }
 }
 
@@ -1224,7 +1087,7 @@ DR_API int dr_kmeans_step(const float* X, uint64_t n, int d, const float* C, int
     }
 #undef DR_KM3
     kmeans_near_list<<<grid_for(n, 256, 4096), 256, 0, s>>>(assign, n, near_cnt, near_list);
-    kmeans_rerank_kernel<false><<<1024, 64, 0, s>>>(X, nullptr, C, cnorm_ws, K, near_cnt, near_list, assign, gsum, gcnt, n);
+    kmeans_rerank_kernel<<<1024, 64, 0, s>>>(X, C, cnorm_ws, K, near_cnt, near_list, assign, gsum, gcnt, n);
     DR_LAUNCH_CHECK();
     if (dbg & 8) {
       uint32_t v = 0;
@@ -1267,40 +1130,41 @@ DR_API int dr_kmeans_step(const float* X, uint64_t n, int d, const float* C, int
   return 0;
 }
 
-// Split planes of n points (K <= 64 path): P = 3 * n * 128 bf16 (xh, xm, xl planes), xnorm = n f32.
-DR_API int dr_kmeans_split(const float* X, uint64_t n, __bf16* P, float* xnorm, hipStream_t s) {
+// bf16 plane of n points (K <= 64 path): XH = n * 128 bf16, xnorm = n f32 (|x|).
+DR_API int dr_kmeans_hi(const float* X, uint64_t n, __bf16* XH, float* xnorm, hipStream_t s) {
   if (n == 0) return 0;
-  kmeans_split_kernel<<<grid_for(n * 64, 256, 8192), 256, 0, s>>>(X, n, P, xnorm);
+  kmeans_hi_kernel<<<grid_for(n * 64, 256, 8192), 256, 0, s>>>(X, n, XH, xnorm);
   DR_LAUNCH_CHECK();
   return 0;
 }
 
-// One k-means step (K <= 64) on split planes.  gsum / gcnt accumulate (caller zeroes them); assign
-// (n) receives the final assignment; prev (n, -1 = none) and sxl (K * 128 f64) carry the xl part's
-// per-cluster sums across steps (zero sxl and fill prev with -1 whenever K or the points change).
-DR_API int dr_kmeans_step_planes(const __bf16* P, const float* xnorm, uint64_t n, const float* C, int K,
-                                 float* cnorm_ws, int32_t* assign, int32_t* prev, double* sxl, double* gsum,
-                                 unsigned long long* gcnt, void* near_ws, hipStream_t s) {
-  if (K < 1 || K > 64 || !assign || !prev || !sxl || !near_ws) return (int)hipErrorInvalidValue;
+// One k-means step (K <= 64) on the bf16 plane with sums kept across steps.  assign (n) receives
+// the final assignment; prev (n, -1 = none), S (K * 128 f64) and cnt (K i64) are the table's
+// running per-cluster state: zero S / cnt and fill prev with -1 whenever K or the points change.
+// After the call S / cnt hold the sums / counts of this step's assignment.
+DR_API int dr_kmeans_step_hi(const __bf16* XH, const float* xnorm, const float* X, uint64_t n, const float* C, int K,
+                             float* cnorm_ws, int32_t* assign, int32_t* prev, double* S, long long* cnt,
+                             void* near_ws, hipStream_t s) {
+  if (K < 1 || K > 64 || !assign || !prev || !S || !cnt || !near_ws) return (int)hipErrorInvalidValue;
   sq_norms_kernel<<<K, 64, 0, s>>>(C, K, cnorm_ws);
   if (n == 0) return 0;
   uint32_t* near_cnt = reinterpret_cast<uint32_t*>(near_ws);
   uint32_t* near_list = near_cnt + 4;
   kmeans_near_reset<<<1, 64, 0, s>>>(near_cnt);
-  const uint64_t st = (n + kM16Pts - 1) / kM16Pts;
-  const uint64_t cap = 2 * (uint64_t)num_cus();
-  const unsigned g16 = (unsigned)(st < cap ? st : cap);
-#define DR_KMP(KTV) kmeans_planes_kernel<KTV><<<g16, 256, 0, s>>>(P, xnorm, n, C, cnorm_ws, K, assign, gsum, gcnt, 128)
-  if (K <= 16) DR_KMP(1);
-  else if (K <= 32) DR_KMP(2);
-  else if (K <= 48) DR_KMP(3);
-  else DR_KMP(4);
-#undef DR_KMP
+  const uint64_t waves = (n + 15) / 16;
+  const uint64_t cap = 8 * (uint64_t)num_cus();
+  const unsigned ga = (unsigned)((waves + 3) / 4 < cap ? (waves + 3) / 4 : cap);
+#define DR_KMA(KTV) kmeans_assign_kernel<KTV><<<ga, 256, 0, s>>>(XH, xnorm, n, C, cnorm_ws, K, assign)
+  if (K <= 16) DR_KMA(1);
+  else if (K <= 32) DR_KMA(2);
+  else if (K <= 48) DR_KMA(3);
+  else DR_KMA(4);
+#undef DR_KMA
   kmeans_near_list<<<grid_for(n, 256, 4096), 256, 0, s>>>(assign, n, near_cnt, near_list);
-  kmeans_rerank_kernel<true><<<1024, 64, 0, s>>>(nullptr, P, C, cnorm_ws, K, near_cnt, near_list, assign, gsum, gcnt, n);
+  kmeans_rerank_kernel<<<1024, 64, 0, s>>>(X, C, cnorm_ws, K, near_cnt, near_list, assign, nullptr, nullptr, n);
   const uint64_t mb = (n + 255) / 256;
-  kmeans_movers_kernel<<<(unsigned)(mb < cap * 2 ? mb : cap * 2), 256, 0, s>>>(P + 2 * n * D, n, assign, prev, K, sxl);
-  kmeans_add_kernel<<<(K * D + 255) / 256, 256, 0, s>>>(gsum, sxl, K * D);
+  const uint64_t mcap = 4 * (uint64_t)num_cus();
+  kmeans_movers_kernel<<<(unsigned)(mb < mcap ? mb : mcap), 256, 0, s>>>(X, n, assign, prev, K, S, cnt);
   DR_LAUNCH_CHECK();
   return 0;
 }

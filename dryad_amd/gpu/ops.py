@@ -756,7 +756,7 @@ def _radix_groups(kcols, skeys, specs, n, nd=None):
 
 def _dense_groups(kcols, skeys, specs, n):
     """(keys, aggregate columns) through ops/densegroup.py (partition by key bits + LDS tables
-    addressed by the low key bits) for one plain integer key whose span needs 12..31 bits and
+    addressed by the low key bits) for one plain integer key whose span needs 13..32 bits and
     integer aggregates that pack with it into 16-byte rows, else None."""
     from ..ops import densegroup as DG
     if len(kcols) != 1 or skeys[0] is not None or kcols[0].dtype not in _INT_KEYS or n < DG.MIN_ROWS:
@@ -798,7 +798,7 @@ def op_group_partial(op, inputs, v):
                 for nm, r in zip(names, res):
                     out[nm] = r
                 return _partial_table(out, {}, d, 1, form)
-    # one integer key over a span of <= 2^31 values: partition by key bits, then LDS tables
+    # one integer key over a span of <= 2^32 values: partition by key bits, then LDS tables
     # addressed by the low key bits (no sort, no hash, no gather)
     got = _dense_groups(kcols, skeys, specs, t.n)
     if got is not None:

@@ -1,7 +1,7 @@
 """Dense-key GroupBy aggregation (csrc/kernels/densegroup.hip): two stable partition passes over
-bit-packed 16-byte rows by key bits, then one LDS table per run of 2^11 consecutive keys.
+bit-packed 16-byte rows by key bits, then one LDS table per run of 2^12 consecutive keys.
 
-Applies to one integer key whose value span needs 12..31 bits (2^11 < span <= 2^31: at most two
+Applies to one integer key whose value span needs 13..32 bits (2^12 < span <= 2^32: at most two
 partition passes of <= 10 bits) and <= 3 integer value columns whose spans, with the key's, pack
 into 128 bits; count / sum / min / max aggregates.  Reference: the partial / full hash GroupBy of
 DryadLinqVertex.cs:5342-6417 (ParallelHashGroupBy) -- here the hash table is an LDS table addressed
@@ -26,12 +26,11 @@ _lib.register_signatures({
     "dr_dg_count": (c_i32, [vp, vp, c_u64, c_i64, c_u32, c_u32, c_u32, vp, c_u32, c_u64, vp]),
     "dr_dg_scatter": (c_i32, [vp, ctypes.POINTER(vp), ctypes.POINTER(c_i64), ctypes.POINTER(c_u32), c_u32, c_i64,
                               c_u32, vp, c_u64, c_u32, c_u32, vp, c_u32, c_u64, vp, vp]),
-    "dr_dg_aggregate": (c_i32, [vp, vp, c_u32, c_u64, c_u32, c_i64, c_u32, ctypes.POINTER(c_u32),
-                                ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), ctypes.POINTER(c_i64), vp, vp, vp,
-                                ctypes.POINTER(vp), vp]),
+    "dr_dg_aggregate": (c_i32, [vp, c_u64, c_u32, c_i64, c_u32, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32),
+                                ctypes.POINTER(c_u32), ctypes.POINTER(c_i64), vp, vp, vp, ctypes.POINTER(vp), vp]),
 })
 
-TABLE_BITS = 11
+TABLE_BITS = 12
 MAX_DIGIT = 10
 MIN_ROWS = 1 << 20
 _INT = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8)
@@ -98,7 +97,7 @@ def _prepare(key: torch.Tensor, specs: list):
 
 
 def _partition(key64, cols64, vmin, vbits, kmin, kbits, src, n, shift, dbits, dev, st):
-    """One stable partition pass -> (rows, bucket totals int64 [2^dbits] on the device)."""
+    """One stable partition pass -> rows [n, 16 bytes]."""
     pb = c_u64(0)
     G = int(_lib.lib().dr_dg_grid(c_u64(n), ctypes.byref(pb)))
     nb = 1 << dbits
@@ -116,7 +115,7 @@ def _partition(key64, cols64, vmin, vbits, kmin, kbits, src, n, shift, dbits, de
     vbt = (c_u32 * 3)(*(list(vbits) + [0] * (3 - k)))
     _lib.call("dr_dg_scatter", ptr(key64), cp, vm, vbt, c_u32(k), c_i64(kmin), c_u32(kbits), ptr(src), c_u64(n),
               c_u32(shift), c_u32(dbits), ptr(offs), c_u32(G), pb, ptr(out), st)
-    return out, c64.view(nb, G).sum(1)
+    return out
 
 
 def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
@@ -134,17 +133,12 @@ def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
     key64 = key64.contiguous()
     cols64 = [(c if c.dtype == torch.int64 else c.to(torch.int64)).contiguous() for c in cols]
     # pass 1 packs the columns (low digit), pass 2 (if any) re-partitions the rows (high digit)
-    rows, tot = _partition(key64, cols64, vmin, vbits, kmin, kbits, None, n, TABLE_BITS, widths[0], dev, st)
-    runs_per_bucket = 1
+    # (LSD order: the rows end up sorted by run id = key offset >> TABLE_BITS)
+    rows = _partition(key64, cols64, vmin, vbits, kmin, kbits, None, n, TABLE_BITS, widths[0], dev, st)
     if len(widths) == 2:
-        nxt, tot = _partition(key64, cols64, vmin, vbits, kmin, kbits, rows, n, TABLE_BITS + widths[0], widths[1],
-                              dev, st)
+        nxt = _partition(key64, cols64, vmin, vbits, kmin, kbits, rows, n, TABLE_BITS + widths[0], widths[1], dev, st)
         del rows
         rows = nxt
-        runs_per_bucket = 1 << widths[0]
-    nb = tot.shape[0]
-    bstart = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(tot, 0, out=bstart[1:])
     # field offsets of the accumulated columns inside the packed row
     foff, o = [], kbits
     for b in vbits:
@@ -160,8 +154,8 @@ def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
     bts = (c_u32 * 3)(*([vbits[a[1]] for a in accs] + [0] * (3 - na)))
     vms = (c_i64 * 3)(*([vmin[a[1]] for a in accs] + [0] * (3 - na)))
     optr = (vp * 3)(*([t.data_ptr() for t in oacc] + [0] * (3 - na)))
-    _lib.call("dr_dg_aggregate", ptr(rows), ptr(bstart), c_u32(nb), c_u64(runs_per_bucket), c_u32(kbits),
-              c_i64(kmin), c_u32(na), ops, offs, bts, vms, ptr(head), ptr(okey), ptr(ocnt), optr, st)
+    _lib.call("dr_dg_aggregate", ptr(rows), c_u64(n), c_u32(kbits), c_i64(kmin), c_u32(na), ops, offs, bts, vms,
+              ptr(head), ptr(okey), ptr(ocnt), optr, st)
     del rows
     g = int(head.item())
     keys, cnt = okey[:g], ocnt[:g]

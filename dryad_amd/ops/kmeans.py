@@ -1,18 +1,11 @@
 """k-means step on MFMA (HIP kernels in csrc/kernels/kmeans.hip).
 
-K <= 64 (the benchmark's K = 64) runs on split planes: the static point table is split once into
-three exact bf16 parts (``SplitPoints``, cached per point tensor) and every iteration reads the
-xh/xm planes only (512 B per point, as many bytes as the f32 row, no conversion work in the loop);
-the third part's per-cluster sums follow the assignment incrementally (only points whose
-assignment changed move theirs).  Larger K, or planes that do not fit in free HBM, use the f32
-kernels.
-
-BASELINE config: "k-means on 1B x 128-dim points (Apply/Fork iterative DAG, MFMA reductions)".
-The reference runs k-means as a DoWhile over per-partition Apply bodies that compute nearest
-centroids and partial sums on the CPU, then a final aggregation stage (reference samples under
-DryadLinq/Samples and DryadLinqTests iterative jobs).  Here one kernel per partition does the
-assignment (f32 MFMA distance tiles + argmin) and the LDS-privatised partial sums; the cross-rank
-reduction is one RCCL all-reduce of K*(D+1) values.
+K <= 64 (the benchmark's K = 64) runs on a per-table state (``SplitPoints``, cached per point
+tensor): the bf16 rounding of every coordinate and |x| per point, written once, so an
+iteration's assignment kernel reads half the bytes of the f32 rows; and the per-cluster sums and
+counts, kept with the table and updated only for the points whose cluster changed (their exact
+f32 rows move from the old cluster's sums to the new one's).  Larger K, or a plane that does not
+fit in free HBM, use the f32 kernels.
 """
 from __future__ import annotations
 
@@ -30,8 +23,8 @@ _lib.register_signatures({
     "dr_kmeans_step": (c_i32, [vp, c_u64, c_i32, vp, c_i32, vp, vp, vp, vp, vp, vp]),
     "dr_kmeans_near_workspace": (c_u64, [c_u64]),
     "dr_kmeans_gen": (c_i32, [vp, c_u64, c_i32, c_u64, c_i32, c_u64, vp]),
-    "dr_kmeans_split": (c_i32, [vp, c_u64, vp, vp, vp]),
-    "dr_kmeans_step_planes": (c_i32, [vp, vp, c_u64, vp, c_i32, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "dr_kmeans_hi": (c_i32, [vp, c_u64, vp, vp, vp]),
+    "dr_kmeans_step_hi": (c_i32, [vp, vp, vp, c_u64, vp, c_i32, vp, vp, vp, vp, vp, vp, vp]),
 })
 
 PLANES_MAX_K = 64
@@ -54,31 +47,31 @@ class KMeansWorkspace:
 
 
 class SplitPoints:
-    """Exact three-part bf16 split of an [n, 128] f32 point table: planes [3, n, 128] (xh, xm, xl
-    with x = xh + xm + xl), |x| per point, and the state that carries the xl part's per-cluster
-    sums across steps (``prev``: last final assignment, -1 = none; ``sxl``: K x 128 f64)."""
+    """Per-point-table state of the K <= 64 path: ``xh`` [n, 128] bf16 (round-to-nearest of x),
+    ``xnorm`` |x| per point, and the running per-cluster state of the last step: ``prev`` (final
+    assignment, -1 = none), ``sums`` (K x 128 f64) and ``counts`` (K i64)."""
 
     def __init__(self, x: torch.Tensor):
         n = x.shape[0]
         self.n = n
         self.version = x._version
-        self.planes = torch.empty((3, n, DIM), dtype=torch.bfloat16, device=x.device)
+        self.xh = torch.empty((n, DIM), dtype=torch.bfloat16, device=x.device)
         self.xnorm = torch.empty(n, dtype=torch.float32, device=x.device)
         self.prev = torch.full((n,), -1, dtype=torch.int32, device=x.device)
-        self.sxl = None
+        self.sums = self.counts = None
         if x.is_cuda:
-            _lib.call("dr_kmeans_split", ptr(x), c_u64(n), ptr(self.planes), ptr(self.xnorm), stream_of(x))
+            _lib.call("dr_kmeans_hi", ptr(x), c_u64(n), ptr(self.xh), ptr(self.xnorm), stream_of(x))
         else:
-            h, m, lo = split_reference(x)
-            self.planes[0], self.planes[1], self.planes[2] = h, m, lo
+            self.xh.copy_(x.bfloat16())
             self.xnorm.copy_(x.double().norm(dim=1).float())
 
-    def state_for(self, k: int) -> torch.Tensor:
-        """The xl sums for ``k`` clusters; a new K restarts them (every point moves again)."""
-        if self.sxl is None or self.sxl.shape[0] != k:
-            self.sxl = torch.zeros((k, DIM), dtype=torch.float64, device=self.planes.device)
+    def state_for(self, k: int):
+        """The running sums / counts for ``k`` clusters; a new K restarts them (every point moves)."""
+        if self.sums is None or self.sums.shape[0] != k:
+            self.sums = torch.zeros((k, DIM), dtype=torch.float64, device=self.xh.device)
+            self.counts = torch.zeros(k, dtype=torch.int64, device=self.xh.device)
             self.prev.fill_(-1)
-        return self.sxl
+        return self.sums, self.counts
 
 
 # (device, data_ptr, n) -> SplitPoints.  The entry lives as long as the tensor that owns the
@@ -88,7 +81,7 @@ _SPLITS: dict = {}
 
 
 def split_bytes(n: int) -> int:
-    return n * (3 * DIM * 2 + 4 + 4)
+    return n * (DIM * 2 + 4 + 4)
 
 
 def split_points(x: torch.Tensor, create: bool = True) -> SplitPoints | None:
@@ -150,8 +143,8 @@ def step(points: torch.Tensor, centroids: torch.Tensor, ws: KMeansWorkspace | No
          planes: bool | None = None):
     """One assignment + partial-sum pass.  Returns (sums f64 [K,D], counts i64 [K], assign i32 [n]).
 
-    ``planes``: None = split planes when K <= 64 and they fit (the default), False = the f32
-    kernels, True = split planes or an error."""
+    ``planes``: None = the bf16-plane path with kept sums when K <= 64 and the plane fits (the
+    default), False = the f32 kernels, True = the plane path or an error."""
     _lib.require_gpu_tensor(points, "kmeans.step")
     _lib.require_gpu_tensor(centroids, "kmeans.step")
     assert points.dtype == torch.float32 and centroids.dtype == torch.float32
@@ -165,14 +158,16 @@ def step(points: torch.Tensor, centroids: torch.Tensor, ws: KMeansWorkspace | No
     if planes is not False and 1 <= k <= PLANES_MAX_K and n > 0:
         sp = split_points(points)
         if sp is None and planes:
-            raise MemoryError(f"kmeans.step: split planes of {n} points ({split_bytes(n) >> 20} MiB) do not fit")
+            raise MemoryError(f"kmeans.step: the bf16 plane of {n} points ({split_bytes(n) >> 20} MiB) does not fit")
     elif planes:
-        raise ValueError(f"kmeans.step: split planes need 1 <= K <= {PLANES_MAX_K} (K = {k})")
+        raise ValueError(f"kmeans.step: the plane path needs 1 <= K <= {PLANES_MAX_K} (K = {k})")
     if sp is not None:
-        sxl = sp.state_for(k)
-        _lib.call("dr_kmeans_step_planes", ptr(sp.planes), ptr(sp.xnorm), c_u64(n), ptr(centroids), k,
-                  ptr(ws.cnorm), ptr(ws.assign), ptr(sp.prev), ptr(sxl), ptr(ws.sums), ptr(ws.counts),
-                  ptr(ws.near), stream_of(points))
+        sums, counts = sp.state_for(k)
+        _lib.call("dr_kmeans_step_hi", ptr(sp.xh), ptr(sp.xnorm), ptr(points), c_u64(n), ptr(centroids), k,
+                  ptr(ws.cnorm), ptr(ws.assign), ptr(sp.prev), ptr(sums), ptr(counts), ptr(ws.near),
+                  stream_of(points))
+        ws.sums.copy_(sums)
+        ws.counts.copy_(counts)
         return ws.sums, ws.counts, ws.assign[:n]
     _lib.call("dr_kmeans_step", ptr(points), c_u64(n), DIM, ptr(centroids), k, ptr(ws.cnorm), ptr(ws.assign),
               ptr(ws.sums), ptr(ws.counts), ptr(ws.near), stream_of(points))

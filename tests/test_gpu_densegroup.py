@@ -32,7 +32,7 @@ def _check(key, specs):
         assert torch.equal(outs[i][order], ref[i]), specs[i][0]
 
 
-@pytest.mark.parametrize("span_bits,n", [(14, 100_000), (21, 2_000_000), (25, 3_000_000), (31, 1_500_000)])
+@pytest.mark.parametrize("span_bits,n", [(14, 100_000), (21, 2_000_000), (25, 3_000_000), (32, 1_500_000)])
 def test_dense_groupby_matches_torch(span_bits, n):
     g = torch.Generator(device="cuda").manual_seed(span_bits)
     kmin = -(1 << (span_bits - 2)) + 12345
@@ -41,7 +41,8 @@ def test_dense_groupby_matches_torch(span_bits, n):
     b = torch.randint(-(1 << 40), 1 << 40, (n,), generator=g, device="cuda")
     c = torch.randint(0, 7, (n,), generator=g, device="cuda", dtype=torch.int32)
     _check(key, [("count", None, torch.int64), ("sum", a, torch.int64), ("min", b, torch.int64),
-                 ("max", c, torch.int32), ("sum", b, torch.int64)])
+                 ("max", c, torch.int32)])
+    _check(key, [("sum", b, torch.int64), ("count", None, torch.int64), ("max", b, torch.int64)])
 
 
 def test_dense_groupby_skewed_and_int32_key():

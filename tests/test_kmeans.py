@@ -79,7 +79,7 @@ def test_split_cache_follows_owner_and_version():
     assert KM.split_points(x[:]) is a                    # a new view of the same points hits
     x.add_(1.0)
     b = KM.split_points(x)
-    assert b is not a and torch.equal(b.planes[0], x.bfloat16())
+    assert b is not a and torch.equal(b.xh, x.bfloat16())
     n0 = len(KM._SPLITS)
     del x, a, b
     gc.collect()
