@@ -75,19 +75,35 @@ __device__ __forceinline__ uint64_t dg_field(u128 r, uint32_t off, uint32_t bits
 
 // per-(bucket, workgroup) histogram of digit = (key offset >> shift) & (2^dbits - 1), either from
 // the int64 key column (ROWS = false) or from the packed rows (ROWS = true)
+// With ROWS and a non-null `joint`, also the size of every run (key offset >> table bits) of the
+// final order: the rows come from the first pass, sorted by its digit (the low bits of the run id),
+// so a workgroup's slice spans a few low-digit values: counted in an LDS window of kDgWin of them
+// (x the 2^dbits high digits), rows outside it straight into `joint` (global atomics).
+constexpr int kDgWin = 4;
+
 template <bool ROWS>
 __global__ __launch_bounds__(256) void dg_count_kernel(const int64_t* __restrict__ key, const uint4* __restrict__ rows,
                                                        uint64_t n, int64_t kmin, uint32_t kbits, uint32_t shift,
                                                        uint32_t dbits, uint32_t* __restrict__ counts, uint32_t G,
-                                                       uint64_t per_block) {
+                                                       uint64_t per_block, uint32_t* __restrict__ joint,
+                                                       uint32_t lo_bits) {
   __shared__ uint32_t hist[1 << kDgMaxDigit];
+  __shared__ uint32_t jw[ROWS ? kDgWin << kDgMaxDigit : 1];
   const int t = threadIdx.x;
   const uint32_t nb = 1u << dbits, mask = nb - 1;
+  const uint32_t lomask = (1u << lo_bits) - 1;
   for (uint32_t i = t; i < nb; i += kBlock) hist[i] = 0;
+  if (ROWS && joint)
+    for (uint32_t i = t; i < (uint32_t)kDgWin * nb; i += kBlock) jw[i] = 0;
   __syncthreads();
   const uint64_t beg = (uint64_t)blockIdx.x * per_block;
   const uint64_t end = beg + per_block < n ? beg + per_block : n;
   const uint64_t kmask = kbits >= 64 ? ~0ull : ((1ull << kbits) - 1);
+  uint32_t lo0 = 0;
+  if (ROWS && joint && beg < end) {
+    const uint4 r = rows[beg];
+    lo0 = (uint32_t)(((((uint64_t)r.y << 32) | r.x) & kmask) >> kDgTableBits) & lomask;
+  }
   for (uint64_t i = beg + t; i < end; i += kBlock) {
     uint64_t ko;
     if constexpr (ROWS) {
@@ -96,10 +112,22 @@ __global__ __launch_bounds__(256) void dg_count_kernel(const int64_t* __restrict
     } else {
       ko = (uint64_t)(key[i] - kmin);
     }
-    atomicAdd(&hist[(ko >> shift) & mask], 1u);
+    const uint32_t d = (uint32_t)((ko >> shift) & mask);
+    atomicAdd(&hist[d], 1u);
+    if (ROWS && joint) {
+      const uint32_t lo = (uint32_t)(ko >> kDgTableBits) & lomask;
+      if (lo - lo0 < (uint32_t)kDgWin) atomicAdd(&jw[d * kDgWin + (lo - lo0)], 1u);
+      else atomicAdd(&joint[((uint64_t)d << lo_bits) | lo], 1u);
+    }
   }
   __syncthreads();
   for (uint32_t i = t; i < nb; i += kBlock) counts[(uint64_t)i * G + blockIdx.x] = hist[i];
+  if (ROWS && joint)
+    for (uint32_t i = t; i < (uint32_t)kDgWin * nb; i += kBlock) {
+      const uint32_t v = jw[i];
+      const uint32_t lo = lo0 + i % kDgWin;
+      if (v && lo <= lomask) atomicAdd(&joint[((uint64_t)(i / kDgWin) << lo_bits) | lo], v);
+    }
 }
 
 // Stable partition of rows [beg, end) of each workgroup by digit; offsets[d * G + b] = first output
@@ -249,61 +277,26 @@ struct DgAgg {
   int64_t vmin[kDgMaxCols];
 };
 
-// First row in [lo, hi) whose run id (key offset >> kDgTableBits) is >= target; rows in [lo, hi)
-// are ordered by run id.  64-ary search by one wave: 3 steps cover 2^18 rows.
-__device__ __forceinline__ uint64_t dg_lower_bound(const uint4* __restrict__ rows, uint64_t lo, uint64_t hi,
-                                                   uint64_t kmask, uint64_t target) {
-  const int l = lane_id();
-  while (hi - lo > 64) {
-    const uint64_t step = (hi - lo + 63) / 64;
-    const uint64_t pos = lo + (uint64_t)l * step;
-    bool ge = true;
-    if (pos < hi) {
-      const uint4 r = rows[pos];
-      ge = (((((uint64_t)r.y << 32) | r.x) & kmask) >> kDgTableBits) >= target;
-    }
-    const uint64_t m = ballot64(ge);                  // lanes at and past the answer (monotone)
-    const int first = m ? __builtin_ctzll(m) : 64;
-    // the answer lies in (pos(first - 1), pos(first)]
-    const uint64_t nlo = first == 0 ? lo : lo + (uint64_t)(first - 1) * step + 1;
-    const uint64_t nhi = first == 64 ? hi : (lo + (uint64_t)first * step < hi ? lo + (uint64_t)first * step : hi);
-    lo = nlo;
-    hi = nhi;
-    if (first == 0) return lo;
-  }
-  const uint64_t pos = lo + l;
-  bool ge = true;
-  if (pos < hi) {
-    const uint4 r = rows[pos];
-    ge = (((((uint64_t)r.y << 32) | r.x) & kmask) >> kDgTableBits) >= target;
-  }
-  const uint64_t m = ballot64(ge || pos >= hi);
-  return lo + (uint64_t)(m ? __builtin_ctzll(m) : (int)(hi - lo));
-}
-
-__device__ __forceinline__ uint64_t dg_run(const uint4& r, uint64_t kmask) {
-  return ((((uint64_t)r.y << 32) | r.x) & kmask) >> kDgTableBits;
-}
-
-// The rows are sorted by run id (key offset >> table bits).  Workgroup b owns the runs that start
-// in rows [b * per, (b + 1) * per): it moves both ends forward to run starts (two 64-ary searches),
-// then streams its rows 1024 at a time (the next 1024 in flight), folding each run into the LDS
-// table and emitting the table whenever the run id changes.
-__global__ __launch_bounds__(kDgThreads) void dg_agg_kernel(const uint4* __restrict__ rows, uint64_t n, uint64_t per,
-                                                     uint32_t kbits, int64_t kmin, DgAgg ag,
-                                                     unsigned long long* __restrict__ head, int64_t* __restrict__ okey,
-                                                     int64_t* __restrict__ ocnt, int64_t* __restrict__ oacc0,
-                                                     int64_t* __restrict__ oacc1, int64_t* __restrict__ oacc2) {
+// The rows are sorted by run id (key offset >> table bits); rstart[r] .. rstart[r + 1] are run r's
+// rows.  Workgroup b folds the runs [wrun[b], wrun[b + 1]) (equal row shares) into its LDS table,
+// kU * 512 rows per step with the next step's rows (possibly of the next run) in flight, and
+// emits the table at the end of each run: no barrier inside a run.
+__global__ __launch_bounds__(kDgThreads) void dg_agg_kernel(const uint4* __restrict__ rows,
+                                                            const int64_t* __restrict__ rstart,
+                                                            const int64_t* __restrict__ wrun, uint32_t kbits,
+                                                            int64_t kmin, DgAgg ag, unsigned long long* __restrict__ head,
+                                                            int64_t* __restrict__ okey, int64_t* __restrict__ ocnt,
+                                                            int64_t* __restrict__ oacc0, int64_t* __restrict__ oacc1,
+                                                            int64_t* __restrict__ oacc2) {
   __shared__ uint32_t cnt[kDgSlots];
   __shared__ unsigned long long acc[kDgMaxCols][kDgSlots];
-  __shared__ uint64_t bounds[2];
   __shared__ uint32_t sc[kDgWaves];
-  __shared__ unsigned long long obase, next_run;
-  const int t = threadIdx.x, w = wave_id();
-  const uint64_t kmask = kbits >= 64 ? ~0ull : ((1ull << kbits) - 1);
+  __shared__ unsigned long long obase;
+  const int t = threadIdx.x;
   int64_t* const oacc[3] = {oacc0, oacc1, oacc2};
   constexpr int kSlotsPer = kDgSlots / kDgThreads;
   constexpr int kU = 4;                                 // rows per thread per step
+  constexpr uint64_t kStep = (uint64_t)kU * kDgThreads;
   for (int q = 0; q < kSlotsPer; ++q) {
     const int sl = t * kSlotsPer + q;
     cnt[sl] = 0;
@@ -311,19 +304,7 @@ __global__ __launch_bounds__(kDgThreads) void dg_agg_kernel(const uint4* __restr
     for (int a = 0; a < kDgMaxCols; ++a)
       if (a < (int)ag.nacc) acc[a][sl] = ag.op[a] == 1 ? ~0ull : 0ull;
   }
-  const uint64_t a0 = (uint64_t)blockIdx.x * per;
-  if (a0 >= n) return;                                  // uniform
-  const uint64_t b0 = a0 + per < n ? a0 + per : n;
-  if (w == 0) {
-    uint64_t s = a0, e = n;
-    if (a0 > 0) s = dg_lower_bound(rows, a0, n, kmask, dg_run(rows[a0 - 1], kmask) + 1);
-    if (b0 < n) e = dg_lower_bound(rows, b0, n, kmask, dg_run(rows[b0 - 1], kmask) + 1);
-    if (lane_id() == 0) { bounds[0] = s; bounds[1] = e; }
-  }
-  __syncthreads();
-  const uint64_t beg = bounds[0], end = bounds[1];
-  if (beg >= end) return;                               // uniform: no run starts here
-  uint64_t cur = dg_run(rows[beg], kmask);
+  const int64_t r1 = wrun[blockIdx.x + 1];
   // emit the occupied slots of run `run`: count, reserve a range of the output, write, reset
   auto emit = [&](uint64_t run) {
     uint32_t occ = 0;
@@ -357,54 +338,64 @@ __global__ __launch_bounds__(kDgThreads) void dg_agg_kernel(const uint4* __restr
     }
     __syncthreads();
   };
-  uint4 buf[kU], nbuf[kU];
-  auto load = [&](uint64_t base, uint4* dst) {
+  // the step after (run r, rows from b, run end e): the next kStep rows of r, else the first rows
+  // of the next non-empty run (false: none left)
+  auto advance = [&](int64_t& r, uint64_t& b, uint64_t& e) {
+    if (b + kStep < e) { b += kStep; return true; }
+    do {
+      if (++r >= r1) return false;
+      b = (uint64_t)rstart[r];
+      e = (uint64_t)rstart[r + 1];
+    } while (b == e);
+    return true;
+  };
+  auto load = [&](uint64_t b, uint64_t e, uint4* dst) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const uint64_t i = base + (uint64_t)u * kDgThreads + t;
-      dst[u] = i < end ? rows[i] : make_uint4(0u, 0u, 0u, 0u);
+      const uint64_t i = b + (uint64_t)u * kDgThreads + t;
+      dst[u] = i < e ? rows[i] : make_uint4(0u, 0u, 0u, 0u);
     }
   };
-  load(beg, buf);
-  for (uint64_t base = beg; base < end; base += kU * kDgThreads) {
-    load(base + kU * kDgThreads, nbuf);                 // the next step in flight
+  int64_t r = wrun[blockIdx.x] - 1;
+  uint64_t b = 0, e = 0;
+  if (!advance(r, b, e)) return;                         // uniform: no non-empty run here
+  uint4 buf[kU], nbuf[kU];
+  load(b, e, buf);
+  while (true) {
+    int64_t nr = r;
+    uint64_t nbg = b, ne = e;
+    const bool more = advance(nr, nbg, ne);
+    if (more) load(nbg, ne, nbuf);                       // the next step in flight
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const uint64_t i = base + (uint64_t)u * kDgThreads + t;
-      bool todo = i < end;
-      const uint4 rr = buf[u];
-      const uint64_t rid = dg_run(rr, kmask);
-      const u128 v = (u128)rr.x | ((u128)rr.y << 32) | ((u128)rr.z << 64) | ((u128)rr.w << 96);
-      // rows are sorted by run: those of the current run come first, later runs follow
-      while (true) {
-        if (todo && rid == cur) {
-          const uint32_t sl = (uint32_t)((uint64_t)v & (kDgSlots - 1));
-          atomicAdd(&cnt[sl], 1u);
+      const uint64_t i = b + (uint64_t)u * kDgThreads + t;
+      if (i < e) {
+        const uint4 rr = buf[u];
+        const u128 v = (u128)rr.x | ((u128)rr.y << 32) | ((u128)rr.z << 64) | ((u128)rr.w << 96);
+        const uint32_t sl = (uint32_t)((uint64_t)v & (kDgSlots - 1));
+        atomicAdd(&cnt[sl], 1u);
 #pragma unroll
-          for (int a = 0; a < kDgMaxCols; ++a) {
-            if (a < (int)ag.nacc) {
-              const unsigned long long f = dg_field(v, ag.field_off[a], ag.field_bits[a]);
-              if (ag.op[a] == 0) atomicAdd(&acc[a][sl], f);
-              else if (ag.op[a] == 1) atomicMin(&acc[a][sl], f);
-              else atomicMax(&acc[a][sl], f);
-            }
+        for (int a = 0; a < kDgMaxCols; ++a) {
+          if (a < (int)ag.nacc) {
+            const unsigned long long f = dg_field(v, ag.field_off[a], ag.field_bits[a]);
+            if (ag.op[a] == 0) atomicAdd(&acc[a][sl], f);
+            else if (ag.op[a] == 1) atomicMin(&acc[a][sl], f);
+            else atomicMax(&acc[a][sl], f);
           }
-          todo = false;
         }
-        if (t == 0) next_run = ~0ull;
-        if (!__syncthreads_or(todo)) break;             // uniform
-        // a later run starts in this row slice: the current run is complete
-        atomicMin(&next_run, (unsigned long long)(todo ? rid : ~0ull));
-        __syncthreads();
-        const uint64_t nxt = next_run;
-        emit(cur);
-        cur = nxt;
       }
     }
+    if (!more || nr != r) {                               // run r is complete
+      __syncthreads();
+      emit((uint64_t)r);
+    }
+    if (!more) break;
 #pragma unroll
     for (int u = 0; u < kU; ++u) buf[u] = nbuf[u];
+    r = nr;
+    b = nbg;
+    e = ne;
   }
-  emit(cur);
 }
 }  // namespace
 
@@ -439,15 +430,19 @@ static int dg_pack_from(DgPack* p, const int64_t* key, const int64_t* const* col
 }
 
 // rows == null: histogram of the key column; else of the packed rows.
+// joint (rows only, may be null): u32 [2^(dbits + lo_bits)] zeroed by the caller, receives the
+// size of every run id (digit << lo_bits | low digit) of the final order.
 DR_API int dr_dg_count(const int64_t* key, const void* rows, uint64_t n, int64_t kmin, uint32_t kbits, uint32_t shift,
-                       uint32_t dbits, uint32_t* counts, uint32_t G, uint64_t per_block, hipStream_t s) {
+                       uint32_t dbits, uint32_t* counts, uint32_t G, uint64_t per_block, uint32_t* joint,
+                       uint32_t lo_bits, hipStream_t s) {
   if (dbits == 0 || dbits > (uint32_t)kDgMaxDigit) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
   if (rows)
     dg_count_kernel<true><<<G, 256, 0, s>>>(nullptr, static_cast<const uint4*>(rows), n, kmin, kbits, shift, dbits,
-                                             counts, G, per_block);
+                                             counts, G, per_block, joint, lo_bits);
   else
-    dg_count_kernel<false><<<G, 256, 0, s>>>(key, nullptr, n, kmin, kbits, shift, dbits, counts, G, per_block);
+    dg_count_kernel<false><<<G, 256, 0, s>>>(key, nullptr, n, kmin, kbits, shift, dbits, counts, G, per_block,
+                                              nullptr, 0);
   DR_LAUNCH_CHECK();
   return 0;
 }
@@ -482,13 +477,14 @@ DR_API int dr_dg_scatter(const int64_t* key, const int64_t* const* cols, const i
   return 0;
 }
 
-// rows: n packed rows sorted by run id (key offset >> table bits).  ops / off / bits / vmin: nacc
-// accumulators over packed fields.  head (u64, zeroed) receives the group count; outputs are sized
-// by the caller (>= the number of groups).
-DR_API int dr_dg_aggregate(const void* rows, uint64_t n, uint32_t kbits, int64_t kmin, uint32_t nacc,
-                           const uint32_t* ops, const uint32_t* off, const uint32_t* bits, const int64_t* vmin,
-                           unsigned long long* head, int64_t* okey, int64_t* ocnt, int64_t* const* oacc,
-                           hipStream_t s) {
+// rows: packed rows sorted by run id (key offset >> table bits); rstart: int64 [runs + 1] row
+// offsets of the runs; wrun: int64 [G + 1] run ranges of the G workgroups.  ops / off / bits / vmin:
+// nacc accumulators over packed fields.  head (u64, zeroed) receives the group count; outputs are
+// sized by the caller (>= the number of groups).
+DR_API int dr_dg_aggregate(const void* rows, const int64_t* rstart, const int64_t* wrun, uint32_t G, uint32_t kbits,
+                           int64_t kmin, uint32_t nacc, const uint32_t* ops, const uint32_t* off, const uint32_t* bits,
+                           const int64_t* vmin, unsigned long long* head, int64_t* okey, int64_t* ocnt,
+                           int64_t* const* oacc, hipStream_t s) {
   if (nacc > (uint32_t)kDgMaxCols) return (int)hipErrorInvalidValue;
   DgAgg ag;
   ag.nacc = nacc;
@@ -500,16 +496,10 @@ DR_API int dr_dg_aggregate(const void* rows, uint64_t n, uint32_t kbits, int64_t
     if (a < nacc && (ag.op[a] > 2 || ag.field_bits[a] == 0 || ag.field_off[a] + ag.field_bits[a] > 128))
       return (int)hipErrorInvalidValue;
   }
-  if (n == 0) return 0;
-  // 1024 workgroups (4 rounds of one per CU) over equal row ranges; each handles the runs starting
-  // in its range
-  const uint64_t G = 1024;
-  uint64_t per = (n + G - 1) / G;
-  if (per < 4096) per = 4096;
-  const unsigned grid = (unsigned)((n + per - 1) / per);
-  dg_agg_kernel<<<grid, kDgThreads, 0, s>>>(static_cast<const uint4*>(rows), n, per, kbits, kmin, ag, head, okey, ocnt,
-                                     nacc > 0 ? oacc[0] : nullptr, nacc > 1 ? oacc[1] : nullptr,
-                                     nacc > 2 ? oacc[2] : nullptr);
+  if (G == 0) return 0;
+  dg_agg_kernel<<<G, kDgThreads, 0, s>>>(static_cast<const uint4*>(rows), rstart, wrun, kbits, kmin, ag, head, okey,
+                                         ocnt, nacc > 0 ? oacc[0] : nullptr, nacc > 1 ? oacc[1] : nullptr,
+                                         nacc > 2 ? oacc[2] : nullptr);
   DR_LAUNCH_CHECK();
   return 0;
 }

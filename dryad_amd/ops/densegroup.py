@@ -23,10 +23,10 @@ _lib.register_signatures({
     "dr_dg_table_bits": (c_u32, []),
     "dr_dg_max_digit": (c_u32, []),
     "dr_dg_grid": (c_u32, [c_u64, ctypes.POINTER(c_u64)]),
-    "dr_dg_count": (c_i32, [vp, vp, c_u64, c_i64, c_u32, c_u32, c_u32, vp, c_u32, c_u64, vp]),
+    "dr_dg_count": (c_i32, [vp, vp, c_u64, c_i64, c_u32, c_u32, c_u32, vp, c_u32, c_u64, vp, c_u32, vp]),
     "dr_dg_scatter": (c_i32, [vp, ctypes.POINTER(vp), ctypes.POINTER(c_i64), ctypes.POINTER(c_u32), c_u32, c_i64,
                               c_u32, vp, c_u64, c_u32, c_u32, vp, c_u32, c_u64, vp, vp]),
-    "dr_dg_aggregate": (c_i32, [vp, c_u64, c_u32, c_i64, c_u32, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32),
+    "dr_dg_aggregate": (c_i32, [vp, vp, vp, c_u32, c_u32, c_i64, c_u32, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32),
                                 ctypes.POINTER(c_u32), ctypes.POINTER(c_i64), vp, vp, vp, ctypes.POINTER(vp), vp]),
 })
 
@@ -96,14 +96,18 @@ def _prepare(key: torch.Tensor, specs: list):
     return cols, accs, where, kmin, kbits, [lo for lo, _ in vb], vbits, widths
 
 
-def _partition(key64, cols64, vmin, vbits, kmin, kbits, src, n, shift, dbits, dev, st):
-    """One stable partition pass -> rows [n, 16 bytes]."""
+def _partition(key64, cols64, vmin, vbits, kmin, kbits, src, n, shift, dbits, dev, st, lo_bits=0):
+    """One stable partition pass -> (rows [n, 16 bytes], run sizes int64 on the device).  Run sizes
+    (runs = key offset >> TABLE_BITS in the final order) come from the histogram itself on a single
+    pass, from the joint (digit, previous digit) count of a second pass (``lo_bits`` = the first
+    pass's digit bits)."""
     pb = c_u64(0)
     G = int(_lib.lib().dr_dg_grid(c_u64(n), ctypes.byref(pb)))
     nb = 1 << dbits
     counts = torch.empty(nb * G, dtype=torch.int32, device=dev)
+    joint = torch.zeros(nb << lo_bits, dtype=torch.int32, device=dev) if src is not None else None
     _lib.call("dr_dg_count", ptr(key64) if src is None else None, ptr(src), c_u64(n), c_i64(kmin), c_u32(kbits),
-              c_u32(shift), c_u32(dbits), ptr(counts), c_u32(G), pb, st)
+              c_u32(shift), c_u32(dbits), ptr(counts), c_u32(G), pb, ptr(joint), c_u32(lo_bits), st)
     c64 = counts.to(torch.int64)
     del counts
     offs = torch.cumsum(c64, 0)
@@ -115,7 +119,8 @@ def _partition(key64, cols64, vmin, vbits, kmin, kbits, src, n, shift, dbits, de
     vbt = (c_u32 * 3)(*(list(vbits) + [0] * (3 - k)))
     _lib.call("dr_dg_scatter", ptr(key64), cp, vm, vbt, c_u32(k), c_i64(kmin), c_u32(kbits), ptr(src), c_u64(n),
               c_u32(shift), c_u32(dbits), ptr(offs), c_u32(G), pb, ptr(out), st)
-    return out
+    runs = joint.to(torch.int64) if joint is not None else c64.view(nb, G).sum(1)
+    return out, runs
 
 
 def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
@@ -134,11 +139,18 @@ def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
     cols64 = [(c if c.dtype == torch.int64 else c.to(torch.int64)).contiguous() for c in cols]
     # pass 1 packs the columns (low digit), pass 2 (if any) re-partitions the rows (high digit)
     # (LSD order: the rows end up sorted by run id = key offset >> TABLE_BITS)
-    rows = _partition(key64, cols64, vmin, vbits, kmin, kbits, None, n, TABLE_BITS, widths[0], dev, st)
+    rows, runs = _partition(key64, cols64, vmin, vbits, kmin, kbits, None, n, TABLE_BITS, widths[0], dev, st)
     if len(widths) == 2:
-        nxt = _partition(key64, cols64, vmin, vbits, kmin, kbits, rows, n, TABLE_BITS + widths[0], widths[1], dev, st)
+        nxt, runs = _partition(key64, cols64, vmin, vbits, kmin, kbits, rows, n, TABLE_BITS + widths[0], widths[1],
+                               dev, st, lo_bits=widths[0])
         del rows
         rows = nxt
+    # run r's rows: rstart[r] .. rstart[r + 1]; workgroup g folds the runs starting in its share
+    rstart = torch.zeros(runs.shape[0] + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(runs, 0, out=rstart[1:])
+    G = max(1, min(1024, n // 4096))
+    targets = torch.arange(G + 1, dtype=torch.int64, device=dev) * ((n + G - 1) // G)
+    wrun = torch.searchsorted(rstart[:-1].contiguous(), targets)
     # field offsets of the accumulated columns inside the packed row
     foff, o = [], kbits
     for b in vbits:
@@ -154,8 +166,8 @@ def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
     bts = (c_u32 * 3)(*([vbits[a[1]] for a in accs] + [0] * (3 - na)))
     vms = (c_i64 * 3)(*([vmin[a[1]] for a in accs] + [0] * (3 - na)))
     optr = (vp * 3)(*([t.data_ptr() for t in oacc] + [0] * (3 - na)))
-    _lib.call("dr_dg_aggregate", ptr(rows), c_u64(n), c_u32(kbits), c_i64(kmin), c_u32(na), ops, offs, bts, vms,
-              ptr(head), ptr(okey), ptr(ocnt), optr, st)
+    _lib.call("dr_dg_aggregate", ptr(rows), ptr(rstart), ptr(wrun), c_u32(G), c_u32(kbits), c_i64(kmin), c_u32(na),
+              ops, offs, bts, vms, ptr(head), ptr(okey), ptr(ocnt), optr, st)
     del rows
     g = int(head.item())
     keys, cnt = okey[:g], ocnt[:g]
