@@ -14,6 +14,11 @@ One step = read the input table (synthetic generator store, materialised in HBM)
 range partition -> RCCL all-to-all-v over xGMI -> local LSD radix sort -> row gather into the
 output table.  Nothing is cached between steps; the output is validated valsort-style (global
 checksum, record count, in-rank order, cross-rank boundaries) after the timed region.
+
+``--total-bytes B`` sizes the job by its total input instead (B / N per GPU, e.g. 1e12 = the
+BASELINE's 1 TB).  A per-GPU share past what one GPU sorts in HBM (IN_HBM_MAX_BYTES) runs the
+out-of-core path (models/terasort.TeraSortOOCJob: hybrid external sort, buckets that fit the HBM
+budget stay resident, the rest spill to pinned host DRAM); the line then reports the PCIe bytes.
 """
 from __future__ import annotations
 
@@ -24,6 +29,7 @@ import sys
 import time
 
 BASELINE_GBPS = 3.1   # DryadLINQ TeraSort, 240 machines, ~1 TB in ~319 s
+IN_HBM_MAX_BYTES = 130e9   # per-GPU input the in-HBM sort holds (input + output + entries in 288 GB)
 METRIC = "GB/sec sorted (whole node), 1 TB TeraSort at 1/2/4/8 MI355X"
 
 
@@ -50,6 +56,10 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--records-per-gpu", type=int, default=1_250_000_000)
+    ap.add_argument("--total-bytes", type=float, default=None,
+                    help="total input bytes over all GPUs (overrides --records-per-gpu); past the in-HBM "
+                         "capacity per GPU the out-of-core path runs")
+    ap.add_argument("--hbm-budget-gb", type=float, default=None, help="out-of-core path: HBM budget per GPU")
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--direct", action="store_true",
                     help="run the sort pipeline directly instead of through the DryadLINQ query API")
@@ -60,14 +70,23 @@ def main():
 
     import torch
     from dryad_amd.parallel.comm import init_world, shutdown
-    from dryad_amd.models.terasort import TeraSortConfig, TeraSortJob, TeraSortQueryJob, run_steps
+    from dryad_amd.models.terasort import (TeraSortConfig, TeraSortJob, TeraSortOOCJob, TeraSortQueryJob, RECORD,
+                                           run_steps)
 
     world = init_world(device="cuda")
     if world.size != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world.size}", file=sys.stderr)
-    cfg = TeraSortConfig(records_per_rank=args.records_per_gpu)
+    records = args.records_per_gpu
+    if args.total_bytes is not None:
+        records = int(args.total_bytes / world.size) // RECORD
+    ooc = records * RECORD > IN_HBM_MAX_BYTES
+    cfg = TeraSortConfig(records_per_rank=records)
     t_alloc = time.perf_counter()
-    job = TeraSortJob(cfg, world) if args.direct else TeraSortQueryJob(cfg, world)
+    if ooc:
+        budget = None if args.hbm_budget_gb is None else int(args.hbm_budget_gb * 1e9)
+        job = TeraSortOOCJob(cfg, world, budget=budget)
+    else:
+        job = TeraSortJob(cfg, world) if args.direct else TeraSortQueryJob(cfg, world)
     if world.rank == 0:
         free, total = torch.cuda.mem_get_info(world.device)
         print(f"[bench] allocated working set in {time.perf_counter() - t_alloc:.1f}s; HBM free {free/1e9:.1f} "
@@ -114,7 +133,8 @@ def main():
                 "validated": None if val is None else val["ok"],
                 "env": env,
                 "rehearsal": bool(args.rehearsal),
-                "path": "direct" if args.direct else "DryadLINQ query -> GPU executor (fused OrderBy gang stage)",
+                "path": ("out-of-core hybrid external sort (HBM-resident buckets + pinned host DRAM)" if ooc else
+                         "direct" if args.direct else "DryadLINQ query -> GPU executor (fused OrderBy gang stage)"),
                 # the input read: every record is generated once per step; with one rank into the
                 # HBM input table the local sort gathers from, with several ranks straight into
                 # the all-to-all send buckets (the read stage fused with the range partition)
@@ -125,7 +145,10 @@ def main():
         }
         if val is not None and not val["ok"]:
             line["validation"] = val
-        if not args.direct:
+        if ooc:
+            line["config"]["out_of_core"] = job.report()
+            line["config"]["input"] = "gen://terasort, generated chunk by chunk in the timed step (count + partition passes)"
+        elif not args.direct:
             rep = job.executor_report()
             print(f"[bench] executor: {json.dumps(rep, default=str)[:2000]}", file=sys.stderr, flush=True)
         print(json.dumps(line), flush=True)

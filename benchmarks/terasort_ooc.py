@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-validate", action="store_true")
+    ap.add_argument("--no-hybrid", action="store_true", help="spill every bucket (no HBM-resident buckets)")
     a = ap.parse_args()
     w = world()
     import torch
@@ -43,9 +44,11 @@ def main():
     res = None
     for i in range(a.warmup + a.steps):
         st = EX.ExtSortStats()
-        dt, res = timed(w, lambda: EX.external_sort(src, 0, TS.KEY_BYTES, w, budget=budget, stats=st, out=out))
+        dt, res = timed(w, lambda: EX.external_sort(src, 0, TS.KEY_BYTES, w, budget=budget, stats=st, out=out,
+                                                    resident=not a.no_hybrid))
         print(f"[ooc] step {i}: {dt:.2f}s {st.seconds} buckets={st.buckets} chunks={st.chunks} "
-              f"h2d={st.bytes_h2d / 1e9:.0f}GB d2h={st.bytes_d2h / 1e9:.0f}GB", file=sys.stderr, flush=True)
+              f"h2d={st.bytes_h2d / 1e9:.0f}GB d2h={st.bytes_d2h / 1e9:.0f}GB resident={st.resident_rows / max(n, 1):.2f}",
+              file=sys.stderr, flush=True)
         if i >= a.warmup:
             stats = (stats or []) + [(dt, st)]
     ok = None
@@ -59,7 +62,7 @@ def main():
             TS.check(rows[: c1 - c0], acc)
         m64 = (1 << 64) - 1
         s64 = lambda v: (v & m64) - (1 << 64) if (v & m64) >= (1 << 63) else (v & m64)  # noqa: E731
-        tot = torch.tensor([int(acc[0].item()), s64(h), res.n, bad], dtype=torch.int64, device=w.device)
+        tot = torch.tensor([s64(int(acc[0].item())), s64(h), res.n, bad], dtype=torch.int64, device=w.device)
         shuffle.all_reduce_(tot, "sum", w)
         ok = int(tot[0]) == int(tot[1]) and int(tot[2]) == n * w.size and int(tot[3]) == 0
     secs = sorted(dt for dt, _ in stats)[len(stats) // 2]
@@ -71,6 +74,7 @@ def main():
                "data": "synthetic gensort-style 100-byte records (gen://terasort)", "validated": ok,
                "phases_s": {k: round(v, 3) for k, v in st.seconds.items()},
                "pcie_GB": {"h2d": round(st.bytes_h2d / 1e9, 1), "d2h": round(st.bytes_d2h / 1e9, 1)},
+               "resident_fraction": round(st.resident_rows / max(n, 1), 3), "hybrid": not a.no_hybrid,
                "config": {"records_per_gpu": n, "bytes_per_gpu": n * TS.RECORD_BYTES,
                           "hbm_budget_gb": a.hbm_budget_gb, "buckets_per_gpu": st.buckets, "chunks": st.chunks,
                           "parallelism": f"dp{w.size}"}})

@@ -111,3 +111,45 @@ class HostRows:
 
     def __len__(self):
         return self.n
+
+
+class TieredRows:
+    """A row table split across tiers in row order: ``segments`` = [rows tensor [k, stride]], each
+    a host tensor (pinned / mapped HostRows storage) or a device (HBM) tensor.  The hybrid
+    out-of-core sort (ops/extsort.py, ``resident=True``) returns one: the range buckets that fit the
+    HBM budget stay sorted in HBM, the rest sit in host DRAM, so only the overflow crosses PCIe."""
+
+    def __init__(self, segments: list, stride: int, key_off: int = 0, key_len: int | None = None, owners=()):
+        self.segments = [s for s in segments if s is not None and s.shape[0] > 0]
+        self.stride = int(stride)
+        self.key_off, self.key_len = key_off, key_len or stride
+        self.n = sum(int(s.shape[0]) for s in self.segments)
+        self._owners = list(owners)           # HostRows / device tensors keeping the storage alive
+
+    @property
+    def nbytes(self) -> int:
+        return self.n * self.stride
+
+    @property
+    def device_rows(self) -> int:
+        return sum(int(s.shape[0]) for s in self.segments if s.is_cuda)
+
+    @property
+    def host_rows(self) -> int:
+        return self.n - self.device_rows
+
+    def to_objects(self) -> list:
+        out = []
+        for s in self.segments:
+            a = s.cpu().numpy() if s.is_cuda else s.numpy()
+            out += [bytes(r) for r in a]
+        return out
+
+    def release(self):
+        for o in self._owners:
+            if hasattr(o, "release"):
+                o.release()
+        self._owners, self.segments, self.n = [], [], 0
+
+    def __len__(self):
+        return self.n

@@ -149,6 +149,93 @@ class TeraSortQueryJob:
     validate = TeraSortJob.validate
 
 
+class TeraSortOOCJob:
+    """TeraSort of a partition larger than one GPU sorts in HBM (the 1- and 2-GPU points of the
+    1 TB headline): ops/extsort.external_sort in hybrid mode over the generator source.
+    The phases work in a quarter of the HBM budget, the range buckets that fit the rest stay sorted
+    in HBM, the others go through pinned host DRAM (allocated once per job, like a job's spill
+    tier), so only the overflow crosses PCIe.  The output is a ``TieredRows`` table per rank."""
+
+    def __init__(self, cfg: TeraSortConfig, world: World | None = None, budget: int | None = None):
+        from ..io.hosttable import HostRows
+        from ..ops import extsort as EX
+        self.EX = EX
+        self.cfg = cfg
+        self.world = world or get_world()
+        self.n = cfg.records_per_rank
+        dev = self.world.device
+        free, _ = torch.cuda.mem_get_info(dev)
+        self.budget = int(budget or free * 0.92)
+        # host rows: at most n - (resident room) + one bucket (the suffix stops at a bucket edge)
+        W = self.world.size
+        work = min(self.budget, max(int(self.budget * EX.HYBRID_WORK_FRACTION), min(EX.HYBRID_MIN_WORK, self.budget // 2)))
+        _, cap, _ = EX.plan_geometry(self.n, self.n * W, RECORD, W, work)
+        room = self.budget - work - min(256 << 20, self.budget // 16)
+        host_rows = max(0, min(int(self.n * (1 + cfg.slack)) + 1024, int(self.n * (1 + cfg.slack)) - room // RECORD + cap))
+        self.host = HostRows(max(host_rows, 1), RECORD, 0, KEYLEN)
+        self.src = EX.GenTeraSortSource(self.world.rank * self.n, self.n, cfg.seed)
+        self.out = None
+        self.stats = None
+
+    @property
+    def bytes_per_rank(self) -> int:
+        return self.n * RECORD
+
+    def step(self):
+        st = self.EX.ExtSortStats()
+        self.out = self.EX.external_sort(self.src, 0, KEYLEN, self.world, budget=self.budget, stats=st,
+                                         out=self.host, resident=True)
+        self.stats = st
+        return self.out
+
+    def input_checksum(self) -> tuple[int, int]:
+        dev = self.world.device
+        rows = torch.empty((min(self.n, 1 << 26), RECORD), dtype=torch.uint8, device=dev)
+        acc = torch.zeros(2, dtype=torch.int64, device=dev)
+        for c0 in range(0, self.n, rows.shape[0]):
+            c1 = min(self.n, c0 + rows.shape[0])
+            TS.generate(rows[: c1 - c0], self.world.rank * self.n + c0, self.cfg.seed)
+            TS.check(rows[: c1 - c0], acc)
+        del rows
+        shuffle.all_reduce_(acc, "sum", self.world)
+        return int(acc[0].item()), self.n * self.world.size
+
+    def validate(self, expect_hash: int, expect_records: int) -> dict:
+        m64 = (1 << 64) - 1
+        h, bad, first, last = self.EX.check_terasort_host(self.out)
+        s64 = (h & m64) - (1 << 64) if (h & m64) >= (1 << 63) else (h & m64)
+        dev = self.world.device
+        tot = torch.tensor([s64, self.out.n, bad], dtype=torch.int64, device=dev)
+        shuffle.all_reduce_(tot, "sum", self.world)
+        ends = torch.zeros((1, 2 * KEYLEN + 1), dtype=torch.uint8, device=dev)
+        if self.out.n:
+            ends[0, 0] = 1
+            ends[0, 1:1 + KEYLEN] = torch.frombuffer(bytearray(first), dtype=torch.uint8)
+            ends[0, 1 + KEYLEN:] = torch.frombuffer(bytearray(last), dtype=torch.uint8)
+        allends = shuffle.all_gather_tensor(ends, self.world).cpu().numpy()
+        boundary_ok, prev_last = True, None
+        for row in allends:
+            if row[0] == 0:
+                continue
+            if prev_last is not None and prev_last > bytes(row[1:1 + KEYLEN]):
+                boundary_ok = False
+            prev_last = bytes(row[1 + KEYLEN:])
+        hv = int(tot[0]) & m64
+        ok = hv == (expect_hash & m64) and int(tot[2]) == 0 and int(tot[1]) == expect_records and boundary_ok
+        return dict(ok=bool(ok), hash_match=hv == (expect_hash & m64), violations=int(tot[2]),
+                    records=int(tot[1]), boundary_ok=boundary_ok)
+
+    def report(self) -> dict:
+        st = self.stats
+        if st is None:
+            return {}
+        return dict(phases_s={k: round(v, 3) for k, v in st.seconds.items()},
+                    pcie_GB={"h2d": round(st.bytes_h2d / 1e9, 1), "d2h": round(st.bytes_d2h / 1e9, 1)},
+                    resident_fraction=round(st.resident_rows / max(st.n_out, 1), 3),
+                    buckets=st.buckets, resident_buckets=st.resident_buckets, chunks=st.chunks,
+                    hbm_budget_gb=round(self.budget / 1e9, 1))
+
+
 def run_steps(job, steps: int) -> float:
     """Run ``steps`` steps bracketed by barrier+synchronize; returns max-over-ranks seconds."""
     w = job.world

@@ -25,6 +25,13 @@ Per rank (one process per GPU, W ranks):
                  place; the next bucket's upload and the previous bucket's download overlap the
                  sort (two copy streams, both PCIe directions busy)                     [HIP + DMA]
 
+Hybrid (``resident=True``): the phases work in a fraction of the HBM budget (smaller chunks and
+buckets) and the rest holds whole range buckets: after the count pass the largest suffix of this
+rank's buckets that fits stays in HBM -- their pieces are copied device to device in the partition
+pass, sorted in place in the sort pass, and returned in HBM (a ``TieredRows`` table: host buckets
+first, then the resident ones).  Only the overflow crosses PCIe: 2(1 - f) bytes per input byte for
+a resident fraction f instead of 3.
+
 Equal keys are split across buckets (and ranks) by a (rank, chunk, row) tie tag in the spare entry
 bits, so skewed keys still fit; the order is then the source order (rank 0's rows first, each rank
 in row order), i.e. the sort is stable.  With
@@ -39,7 +46,7 @@ from dataclasses import dataclass, field
 
 import torch
 
-from ..io.hosttable import HostRows, is_registered
+from ..io.hosttable import HostRows, TieredRows, is_registered
 from ..parallel import shuffle
 from ..parallel.comm import World, get_world
 from . import _lib
@@ -67,6 +74,8 @@ class ExtSortStats:
     bytes_h2d: int = 0
     bytes_d2h: int = 0
     tier: str = "dram"           # where the output rows live: "dram" (pinned) or "disk" (mapped file)
+    resident_rows: int = 0       # hybrid: rows of the buckets kept (sorted) in HBM
+    resident_buckets: int = 0
     seconds: dict = field(default_factory=dict)
 
 
@@ -248,17 +257,23 @@ def _separators(srt: torch.Tensor, W: int, P: int, tie_bits: bool, lo_key_mask: 
     return torch.cat(parts).contiguous() if parts else none
 
 
+HYBRID_WORK_FRACTION = 0.25    # of the HBM budget for the phases' buffers in hybrid mode
+HYBRID_MIN_WORK = 2 << 30
+
+
 def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | None = None,
                   budget: int | None = None, keep_ties: bool = False, sample_target: int = 1 << 20,
                   seed: int = 314159, stats: ExtSortStats | None = None,
-                  out: HostRows | None = None, out_factory=None) -> HostRows:
+                  out: HostRows | None = None, out_factory=None, resident: bool = False,
+                  work_fraction: float = HYBRID_WORK_FRACTION):
     """Globally sort the rows of ``src`` (this rank's partition) by the byte-string key
     [key_off, key_off + key_len) (memcmp order, key_len <= 12).  Rank r returns the r-th key range
     as a ``HostRows`` table in pinned host memory.  ``budget``: HBM bytes the sort may use
     (default 80% of free HBM).  ``out``: a preallocated host table to write into when it is large
     enough (the result is then a view of its first rows); ``out_factory(n_out)``: builds the
     output table once this rank's row count is known (e.g. a memory-mapped part file,
-    ``HostRows.mapped``, for outputs larger than host memory)."""
+    ``HostRows.mapped``, for outputs larger than host memory).  ``resident``: hybrid mode (module
+    docstring); returns a ``TieredRows`` table when some buckets stayed in HBM."""
     w = world or get_world()
     W, me = w.size, w.rank
     dev = w.device if w.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
@@ -268,19 +283,22 @@ def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | N
         raise ValueError("external_sort: key must be 1..12 bytes inside the row")
     t_all = time.perf_counter()
     budget = int(budget or default_budget(dev))
+    work = budget
+    if resident:
+        work = min(budget, max(int(budget * work_fraction), min(HYBRID_MIN_WORK, budget // 2)))
     tot = torch.tensor([n, n], dtype=torch.int64, device=dev if w.backend == "nccl" else "cpu")
     nmax = tot[:1].clone()
     shuffle.all_reduce_(tot[:1], "sum", w)
     shuffle.all_reduce_(nmax, "max", w)
     n_total, n_rank_max = int(tot[0]), int(nmax[0])
-    chunk_rows, bucket_cap, P = plan_geometry(n_rank_max, n_total, stride, W, budget)
+    chunk_rows, bucket_cap, P = plan_geometry(n_rank_max, n_total, stride, W, work)
     C = max(1, -(-n_rank_max // chunk_rows))
     C_local = -(-n // chunk_rows)
     _, _, lo_key_mask = RS.key_bits(key_len)
     split = key_len <= 10 and C * W < (1 << 16)
     part_mask = _M64 if split else lo_key_mask
     stats.n_in, stats.chunks, stats.chunk_rows, stats.buckets, stats.bucket_cap = n, C, chunk_rows, P, bucket_cap
-    arena = _Arena(budget, dev)
+    arena = _Arena(work, dev)
     comp = torch.cuda.current_stream(dev)
     h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     tag_of = lambda c: ((me * C + c) << 32)  # noqa: E731  (rank-major: the global source order)
@@ -345,17 +363,39 @@ def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | N
         raise RuntimeError(f"external sort: a range bucket holds {stats.max_bucket} rows > {bucket_cap} "
                            f"(key skew with keep_ties, or too small a sample); raise the HBM budget")
     n_out = int(rows_b.sum())
-    bucket_off = torch.cumsum(rows_b, 0) - rows_b
-    # host position of piece (s, c, b): bucket start + rows of earlier chunks + earlier sources
+    # hybrid: the largest suffix of buckets that fits next to the working arena stays in HBM
+    res_first = P
+    if resident:
+        room = budget - work - min(256 << 20, budget // 16)
+        acc = 0
+        for b in range(P - 1, -1, -1):
+            nb_ = int(rows_b[b]) * stride
+            if acc + nb_ > room:
+                break
+            acc += nb_
+            res_first = b
+    res_rows = int(rows_b[res_first:].sum())
+    n_host = n_out - res_rows
+    stats.resident_rows, stats.resident_buckets = res_rows, P - res_first
+    region = torch.empty((res_rows, stride), dtype=torch.uint8, device=dev) if res_rows else None
+    # bucket b's first row in its tier: host buckets [0, res_first), then the resident ones
+    base = torch.zeros(P, dtype=torch.int64)
+    if res_first > 0:
+        hb_ = rows_b[:res_first]
+        base[:res_first] = torch.cumsum(hb_, 0) - hb_
+    if res_first < P:
+        rb_ = rows_b[res_first:]
+        base[res_first:] = torch.cumsum(rb_, 0) - rb_
+    # position of piece (s, c, b) in its tier: bucket start + rows of earlier chunks + earlier sources
     flat = mine.permute(1, 0, 2).reshape(C * W, P)              # (chunk, src) major order
-    piece_pos = (torch.cumsum(flat, 0) - flat + bucket_off.unsqueeze(0)).view(C, W, P)
-    if out is not None and out.n >= n_out and out.stride == stride:
-        out = out.view(n_out)
+    piece_pos = (torch.cumsum(flat, 0) - flat + base.unsqueeze(0)).view(C, W, P)
+    if out is not None and out.n >= n_host and out.stride == stride:
+        out = out.view(n_host)
     elif out_factory is not None:
-        out = out_factory(n_out)
+        out = out_factory(n_host)
         stats.tier = "disk" if getattr(out, "path", None) else "dram"
     else:
-        out = HostRows(n_out, stride, key_off, key_len)
+        out = HostRows(n_host, stride, key_off, key_len)
     try:
         # ------------------------------------------------------------ 2. partition pass
         t0 = time.perf_counter()
@@ -423,8 +463,12 @@ def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | N
                     cnt = int(mine[s_, c, b])
                     if cnt:
                         p0 = int(piece_pos[c, s_, b])
-                        _copy(out.rows[p0:p0 + cnt], recv[k][a:a + cnt], d2h)
-                        stats.bytes_d2h += cnt * stride
+                        if b >= res_first:                 # resident bucket: stays in HBM
+                            with torch.cuda.stream(d2h):
+                                region[p0:p0 + cnt].copy_(recv[k][a:a + cnt], non_blocking=True)
+                        else:
+                            _copy(out.rows[p0:p0 + cnt], recv[k][a:a + cnt], d2h)
+                            stats.bytes_d2h += cnt * stride
                     a += cnt
             ev_d2h[k].record(d2h)
         torch.cuda.synchronize(dev)
@@ -438,68 +482,101 @@ def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | N
         bout = [arena.take((cap, stride)) for _ in range(2)]
         ea = arena.take((cap, 2), torch.int64)
         eb = arena.take((cap, 2), torch.int64)
-        ev_up = [None, None]
         ev_sorted = [torch.cuda.Event() for _ in range(2)]
         ev_down = [torch.cuda.Event() for _ in range(2)]
         for k in range(2):
             ev_sorted[k].record(comp)
             ev_down[k].record(d2h)
         sizes = [int(x) for x in rows_b.tolist()]
-        offs = [int(x) for x in bucket_off.tolist()]
+        offs = [int(x) for x in base.tolist()]
+        # processing order: host buckets (PCIe round trips) interleaved with resident ones (compute
+        # only), so the GPU sorts resident buckets while the copy engines move the others
+        nonres = [b for b in range(res_first) if sizes[b]]
+        resb = [b for b in range(res_first, P) if sizes[b]]
+        order = []
+        i_r = 0
+        for j, b in enumerate(nonres):
+            order.append(b)
+            want = ((j + 1) * len(resb)) // max(len(nonres), 1)
+            while i_r < want:
+                order.append(resb[i_r])
+                i_r += 1
+        order += resb[i_r:]
+        ev_up = {}
 
-        def upload(b):
-            if b >= P or sizes[b] == 0:
+        def upload(pos):
+            if pos >= len(order) or order[pos] >= res_first or pos in ev_up:
                 return
-            k = b % 2
-            h2d.wait_event(ev_sorted[k])
+            b = order[pos]
+            k = pos % 2
+            h2d.wait_event(ev_sorted[k])       # the slot's previous bucket has been sorted
             _copy(bin_[k][: sizes[b]], out.rows[offs[b]: offs[b] + sizes[b]], h2d)
             ev = torch.cuda.Event()
             ev.record(h2d)
-            ev_up[k] = ev
+            ev_up[pos] = ev
             stats.bytes_h2d += sizes[b] * stride
 
         upload(0)
-        for b in range(P):
-            k = b % 2
-            upload(b + 1)
+        upload(1)
+        for pos, b in enumerate(order):
+            k = pos % 2
             mb = sizes[b]
-            if mb == 0:
-                continue
-            comp.wait_event(ev_up[k])
             comp.wait_event(ev_down[k])
             hb = RS._range_hi_bounds(seps_hi, me * P + b)
-            res = RS.local_sort_rows(bin_[k][:mb], bout[k], ea, eb, key_off, key_len, hi_bounds=hb)
-            ev_sorted[k].record(comp)
-            d2h.wait_event(ev_sorted[k])
-            _copy(out.rows[offs[b]: offs[b] + mb], res[:mb], d2h)
-            ev_down[k].record(d2h)
-            stats.bytes_d2h += mb * stride
+            if b >= res_first:
+                rows_r = region[offs[b]: offs[b] + mb]
+                res = RS.local_sort_rows(rows_r, bout[k], ea, eb, key_off, key_len, hi_bounds=hb)
+                rows_r.copy_(res[:mb])
+                ev_sorted[k].record(comp)
+            else:
+                comp.wait_event(ev_up.pop(pos))
+                res = RS.local_sort_rows(bin_[k][:mb], bout[k], ea, eb, key_off, key_len, hi_bounds=hb)
+                ev_sorted[k].record(comp)
+                d2h.wait_event(ev_sorted[k])
+                _copy(out.rows[offs[b]: offs[b] + mb], res[:mb], d2h)
+                ev_down[k].record(d2h)
+                stats.bytes_d2h += mb * stride
+            upload(pos + 2)                    # slot k is free once this bucket is sorted
+            upload(pos + 1)
         torch.cuda.synchronize(dev)
         stats.seconds["sort"] = time.perf_counter() - t0
     finally:
         del arena
     stats.n_out = n_out
     stats.seconds["total"] = time.perf_counter() - t_all
+    if region is not None:
+        return TieredRows([out.rows[:n_host], region], stride, key_off, key_len, owners=[out])
     return out
 
 
-def check_terasort_host(out: HostRows, chunk_rows: int = 1 << 24) -> tuple[int, int, bytes, bytes]:
-    """valsort over a host TeraSort table: (hash sum mod 2^64, order violations incl. chunk
-    boundaries, first key, last key), streamed through HBM in chunks."""
+def check_terasort_host(out, chunk_rows: int = 1 << 24) -> tuple[int, int, bytes, bytes]:
+    """valsort over a host (``HostRows``) or tiered (``TieredRows``) TeraSort table: (hash sum mod
+    2^64, order violations incl. chunk and segment boundaries, first key, last key); host rows are
+    streamed through HBM in chunks, HBM-resident segments checked in place."""
     from . import terasort as TS
     dev = torch.device("cuda", torch.cuda.current_device())
     acc = torch.zeros(2, dtype=torch.int64, device=dev)
-    buf = torch.empty((min(max(out.n, 1), chunk_rows), out.stride), dtype=torch.uint8, device=dev)
-    prev, bad = None, 0
-    for a in range(0, out.n, chunk_rows):
-        b = min(out.n, a + chunk_rows)
-        _copy(buf[: b - a], out.rows[a:b], None)
-        TS.check(buf[: b - a], acc)
-        first = bytes(out.rows[a, :TS.KEY_BYTES].numpy())
-        if prev is not None and prev > first:
-            bad += 1
-        prev = bytes(out.rows[b - 1, :TS.KEY_BYTES].numpy())
+    segs = out.segments if isinstance(out, TieredRows) else ([out.rows[: out.n]] if out.n else [])
+    buf = None
+    prev, bad, first = None, 0, None
+    for seg in segs:
+        m = seg.shape[0]
+        for a in range(0, m, chunk_rows):
+            b = min(m, a + chunk_rows)
+            if seg.is_cuda:
+                rows = seg[a:b]
+            else:
+                if buf is None:
+                    buf = torch.empty((chunk_rows, seg.shape[1]), dtype=torch.uint8, device=dev)
+                _copy(buf[: b - a], seg[a:b], None)
+                rows = buf[: b - a]
+            TS.check(rows, acc)
+            k0 = bytes(seg[a, :TS.KEY_BYTES].cpu().numpy())
+            if first is None:
+                first = k0
+            if prev is not None and prev > k0:
+                bad += 1
+            prev = bytes(seg[b - 1, :TS.KEY_BYTES].cpu().numpy())
     torch.cuda.synchronize(dev)
     h, v = acc.tolist()
-    first = bytes(out.rows[0, :TS.KEY_BYTES].numpy()) if out.n else b""
-    return h & _M64, v + bad, first, prev or b""
+    return h & _M64, v + bad, first or b"", prev or b""

@@ -41,6 +41,41 @@ def test_extsort_generator_matches_in_hbm_sort(n, budget):
     assert bad == 0
 
 
+@pytest.mark.parametrize("n,budget", [(3_000_000, 160 << 20), (900_001, 64 << 20)])
+def test_extsort_hybrid_keeps_buckets_resident(n, budget):
+    """Hybrid mode: the buckets that fit next to the working arena stay sorted in HBM; the tiered
+    result equals the in-HBM sort and only the other buckets crossed PCIe."""
+    from dryad_amd.io.hosttable import TieredRows
+    from dryad_amd.ops import extsort as EX
+    st = EX.ExtSortStats()
+    out = EX.external_sort(EX.GenTeraSortSource(0, n, 11), 0, 10, budget=budget, stats=st, resident=True)
+    assert isinstance(out, TieredRows) and st.resident_buckets >= 1 and 0 < st.resident_rows < n
+    assert out.n == n and out.device_rows == st.resident_rows
+    assert [s.is_cuda for s in out.segments] == [False, True]
+    got = torch.cat([s.cpu() for s in out.segments])
+    assert torch.equal(got, _in_hbm_sorted(_gen_rows(n)))
+    host = n - st.resident_rows
+    assert st.bytes_d2h == 2 * host * 100 and st.bytes_h2d == host * 100
+    h, bad, _, _ = EX.check_terasort_host(out, chunk_rows=250_000)
+    assert bad == 0
+
+
+def test_extsort_hybrid_host_source_is_stable():
+    from dryad_amd.io.hosttable import HostRows
+    from dryad_amd.ops import extsort as EX
+    n, stride = 400_000, 32
+    g = np.random.default_rng(6)
+    a = g.integers(0, 256, size=(n, stride), dtype=np.uint8)
+    a[:, 4:14] = g.integers(0, 9, size=(n, 1), dtype=np.uint8)
+    a[:, 20:28] = np.arange(n, dtype=np.uint64).view(np.uint8).reshape(n, 8)
+    src = HostRows.from_tensor(torch.from_numpy(a), key_off=4, key_len=10)
+    st = EX.ExtSortStats()
+    out = EX.external_sort(EX.HostRowsSource(src), 4, 10, budget=12 << 20, stats=st, resident=True)
+    got = np.concatenate([s.cpu().numpy() for s in out.segments]) if hasattr(out, "segments") else out.rows.numpy()
+    assert st.resident_rows > 0
+    np.testing.assert_array_equal(got, _np_stable_sort(a, 4, 10))
+
+
 def test_extsort_host_source_duplicate_keys_is_stable():
     """Few distinct keys: runs of equal keys larger than a bucket are split by the tie tag and
     the result is the stable order."""
