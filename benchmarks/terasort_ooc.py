@@ -44,6 +44,7 @@ def main():
     res = None
     for i in range(a.warmup + a.steps):
         st = EX.ExtSortStats()
+        res = None                   # release the previous output's HBM-resident buckets first
         dt, res = timed(w, lambda: EX.external_sort(src, 0, TS.KEY_BYTES, w, budget=budget, stats=st, out=out,
                                                     resident=not a.no_hybrid))
         print(f"[ooc] step {i}: {dt:.2f}s {st.seconds} buckets={st.buckets} chunks={st.chunks} "

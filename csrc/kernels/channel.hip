@@ -163,14 +163,16 @@ __global__ __launch_bounds__(256) void pc_scatter_kernel(const E128* __restrict_
   }
 }
 
-// One wave per 64 consecutive rows: the wave's strings form one contiguous destination range of
-// T bytes; lane b copies bytes b, b+64, ... after a 6-step search of the row that holds it.
+// One wave per 64 consecutive rows: the wave's strings form one destination range of T bytes
+// (gaps between them allowed: bytes in a gap are not written); lane b copies bytes b, b+64, ...
+// after a 6-step search of the row that holds it.
 __global__ __launch_bounds__(256) void copy_segments_kernel(const uint8_t* __restrict__ src,
                                                             const int64_t* __restrict__ soff,
                                                             const int64_t* __restrict__ len,
                                                             const int64_t* __restrict__ doff, uint64_t n,
                                                             uint8_t* __restrict__ dst) {
   __shared__ int64_t ends[4][64];
+  __shared__ int64_t begs[4][64];
   __shared__ int64_t srcs[4][64];
   const int w = wave_id(), l = lane_id();
   const uint64_t nwaves = (uint64_t)gridDim.x * 4;
@@ -187,6 +189,7 @@ __global__ __launch_bounds__(256) void copy_segments_kernel(const uint8_t* __res
       st = e = doff[r0 + rows - 1] - base + len[r0 + rows - 1];
     }
     ends[w][l] = e;
+    begs[w][l] = st;
     srcs[w][l] = so;
     __builtin_amdgcn_wave_barrier();
     const int64_t T = __shfl(e, 63, 64);
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(256) void copy_segments_kernel(const uint8_t* __res
 #pragma unroll
       for (int step = 32; step >= 1; step >>= 1)
         if (lo + step <= 63 && ends[w][lo + step - 1] <= b) lo += step;
-      dst[base + b] = src[srcs[w][lo] + b];
+      if (b >= begs[w][lo]) dst[base + b] = src[srcs[w][lo] + b];   // gaps between strings stay
     }
     __builtin_amdgcn_wave_barrier();
   }

@@ -1,4 +1,6 @@
 // pybind11 module `_dryad_native`: the C++ runtime exposed to the Python planner/executors.
+#include <cstring>
+
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -6,6 +8,7 @@
 #include "codec.h"
 #include "fifo.h"
 #include "jobgraph.h"
+#include "partreader.h"
 #include "workqueue.h"
 
 namespace py = pybind11;
@@ -251,6 +254,47 @@ PYBIND11_MODULE(_dryad_native, m) {
   m.def("read_files_async", [](WorkQueue& q, const std::vector<std::string>& paths) {
     return PyReadBatch{read_files_async(q, paths)};
   });
+  m.def("scan_record_blocks", [](py::buffer buf, const std::vector<int>& schema_codes, size_t block) {
+    py::buffer_info bi = buf.request();
+    const auto schema = to_schema(schema_codes);
+    std::vector<int64_t> offs;
+    size_t n;
+    {
+      py::gil_scoped_release nogil;
+      n = scan_record_blocks(reinterpret_cast<const uint8_t*>(bi.ptr), (size_t)bi.size * bi.itemsize, schema, block,
+                             offs);
+    }
+    py::array_t<int64_t> a(offs.size());
+    if (!offs.empty()) std::memcpy(a.mutable_data(), offs.data(), offs.size() * sizeof(int64_t));
+    return py::make_tuple(n, a);
+  });
+  // ChunkReader: file -> ring of caller-owned (pinned) host buffers, several reader threads.
+  py::class_<ChunkReader>(m, "ChunkReader")
+      .def(py::init<const std::string&, int64_t, int64_t, int64_t, const std::vector<uint64_t>&, int>(),
+           py::arg("path"), py::arg("offset"), py::arg("length"), py::arg("chunk_bytes"), py::arg("buffers"),
+           py::arg("threads"))
+      .def("size", &ChunkReader::size)
+      .def("chunks", &ChunkReader::chunks)
+      .def("next", [](ChunkReader& r, int64_t timeout_ms) -> py::object {
+        ReadyChunk c;
+        bool more;
+        {
+          py::gil_scoped_release nogil;
+          more = r.next(&c, timeout_ms);
+        }
+        if (!more) {
+          const std::string e = r.error();
+          if (!e.empty()) throw std::runtime_error("ChunkReader: " + e);
+          return py::none();
+        }
+        return py::make_tuple(c.slot, c.chunk, c.bytes);
+      }, py::arg("timeout_ms") = -1)
+      .def("release", &ChunkReader::release)
+      .def("error", &ChunkReader::error)
+      .def("stop", [](ChunkReader& r) {
+        py::gil_scoped_release nogil;
+        r.stop();
+      });
   m.def("write_file_atomic", [](const std::string& path, py::buffer b) {
     py::buffer_info bi = b.request();
     py::gil_scoped_release nogil;

@@ -78,6 +78,49 @@ size_t decode_records(const uint8_t* buf, size_t len, const std::vector<FieldKin
   return n;
 }
 
+size_t scan_record_blocks(const uint8_t* buf, size_t len, const std::vector<FieldKind>& schema, size_t block,
+                          std::vector<int64_t>& offsets) {
+  if (block == 0) throw std::invalid_argument("scan_record_blocks: block size 0");
+  offsets.clear();
+  int fixed = 0;
+  bool var = false;
+  for (FieldKind k : schema) {
+    if (k == FieldKind::String) var = true;
+    else fixed += field_width(k);
+  }
+  if (!var) {             // fixed-width records: the offsets are arithmetic
+    if (fixed == 0 || len % (size_t)fixed) throw std::runtime_error("record stream length is not a multiple of the record width");
+    const size_t n = len / (size_t)fixed;
+    for (size_t r = 0; r < n; r += block) offsets.push_back((int64_t)(r * (size_t)fixed));
+    return n;
+  }
+  const uint8_t* p = buf;
+  const uint8_t* end = buf + len;
+  size_t n = 0;
+  while (p < end) {
+    if (n % block == 0) offsets.push_back((int64_t)(p - buf));
+    for (FieldKind k : schema) {
+      if (k == FieldKind::String) {
+        int32_t nchars = 0, nbytes = 0;
+        size_t c = read_compact(p, end, &nchars);
+        if (!c) throw std::runtime_error("truncated record stream (string length)");
+        p += c;
+        c = read_compact(p, end, &nbytes);
+        if (!c) throw std::runtime_error("truncated record stream (string bytes)");
+        p += c;
+        if (nbytes < 0 || p + nbytes > end) throw std::runtime_error("truncated record stream (string data)");
+        p += nbytes;
+      } else {
+        const int w = field_width(k);
+        if (p + w > end) throw std::runtime_error("truncated record stream (fixed field)");
+        p += w;
+      }
+    }
+    ++n;
+  }
+  return n;
+}
+
 std::vector<uint8_t> encode_records(size_t n, const std::vector<FieldKind>& schema,
                                     const std::vector<const uint8_t*>& fixed,
                                     const std::vector<const StringColumn*>& strings) {

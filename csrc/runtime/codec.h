@@ -54,6 +54,13 @@ std::vector<uint8_t> encode_records(size_t n, const std::vector<FieldKind>& sche
                                     const std::vector<const uint8_t*>& fixed,
                                     const std::vector<const StringColumn*>& strings);
 
+// Block index of a record stream: offsets[j] = byte offset of record j * block (j = 0, 1, ...),
+// found by skipping over fields (string bytes are not touched).  Returns the record count;
+// throws std::runtime_error on a truncated stream.  The device decoder (codec.hip) parses every
+// block in parallel from these offsets.
+size_t scan_record_blocks(const uint8_t* buf, size_t len, const std::vector<FieldKind>& schema, size_t block,
+                          std::vector<int64_t>& offsets);
+
 // Split text into lines on \n, \r and \r\n (DryadLinqTextReader.ReadLine semantics).
 void split_lines(const uint8_t* buf, size_t len, std::vector<int64_t>& starts, std::vector<int64_t>& ends);
 

@@ -260,24 +260,43 @@ def op_read(op, inputs, v):
         return t
     prov = provider_for(uri)
     if scheme in ("partfile", "file") and v.device.type == "cuda":
+        from ..io import reader as RD
         rp = prov.rows_part(uri, v.partition)
         if rp is not None:
-            # raw fixed-width rows (e.g. an out-of-core sort's output): one copy into pooled HBM
-            import numpy as np
+            # raw fixed-width rows (e.g. an out-of-core sort's output): chunked reader -> pooled HBM
             mm, ko, kl = rp
             rows = v.alloc_rows(mm.shape[0], mm.shape[1])
             if mm.shape[0]:
-                rows.copy_(torch.from_numpy(np.ascontiguousarray(mm)))
+                RD.read_to_device(mm.filename, v.device, offset=int(mm.offset), length=rows.numel(),
+                                  out=rows.view(-1))
             return DeviceTable(mm.shape[0], Shape("rows", key_off=ko, key_len=kl), rows=rows)
-        # binary part of fixed-width records: bytes -> HBM -> columns with the device codec
+        # binary part: bytes -> HBM by the chunked pinned reader -> columns with the device codec
+        # (fixed-width records: one thread per field; strings: parallel over the part's record
+        # blocks, the part's bytes becoming the string heap)
         from ..ops import codec as CD
         sch = prov.schema(uri) or {}
         dt = op.get("dtype") or sch.get("dtype")
-        if sch.get("format", "binary") == "binary" and dt is not None and CD.layout(dt) is not None:
-            data = prov.read_partition_bytes(uri, v.partition)
-            buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(v.device) if data else \
-                torch.zeros(0, dtype=torch.uint8, device=v.device)
-            t = CD.decode(buf, dt)
+        if sch.get("format", "binary") == "binary" and dt is not None and \
+                (CD.layout(dt) is not None or CD.var_layout(dt) is not None):
+            path = prov.part_file(uri, v.partition) if hasattr(prov, "part_file") else None
+            if path is not None:
+                buf = RD.read_to_device(path, v.device)
+            else:
+                data = prov.read_partition_bytes(uri, v.partition)
+                buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(v.device) if data else \
+                    torch.zeros(0, dtype=torch.uint8, device=v.device)
+            if CD.layout(dt) is not None:
+                t = CD.decode(buf, dt)
+            else:
+                from ..io import partfile as PF
+                idx = PF.read_index(path) if path is not None else None
+                if idx is not None:
+                    n, _nb, blk, offs = idx
+                else:            # no index sidecar: the native host scan finds the blocks
+                    host = buf.cpu().numpy()
+                    blk = CD.BLOCK
+                    n, offs = CD.block_index_host(host, dt, blk)
+                t = CD.decode_var(buf, dt, n, torch.from_numpy(offs).to(v.device), blk)
             if t is not None:
                 return t
     recs = prov.read_partition(uri, v.partition, op.get("dtype"))

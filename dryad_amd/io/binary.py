@@ -259,14 +259,28 @@ def decode_records(dtype, data) -> list:
     return out
 
 
-def write_records(path, dtype, records) -> int:
+INDEX_BLOCK = 64     # records per block of the part index sidecar (io/partfile.write_index)
+
+
+def write_records(path, dtype, records, index: bool = True) -> int:
+    """Write a part file; with ``index`` also its record block index sidecar (every
+    INDEX_BLOCK-th record's offset) when the records are not fixed-width."""
+    offs = [] if index and dtype is not None and dtype.fixed_width is None else None
+    n = 0
     with open(path, "wb") as f:
         w = BinaryWriter(f)
         for r in records:
+            if offs is not None and n % INDEX_BLOCK == 0:
+                offs.append(w.bytes_written + len(w._buf))
             dtype.encode(w, r)
             w.end_record()
+            n += 1
         w.close()
-        return w.bytes_written
+        nbytes = w.bytes_written
+    if offs is not None:
+        from . import partfile as PF
+        PF.write_index(path, n, nbytes, offs, INDEX_BLOCK)
+    return nbytes
 
 
 def read_records(path, dtype) -> list:

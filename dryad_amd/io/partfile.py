@@ -107,6 +107,10 @@ def commit_parts(meta_path: str, base: str, chosen: list[str], machine: str | No
         dst = f"{base}.{pos:08X}"
         if src != dst:
             os.replace(src, dst)
+            if os.path.exists(src + INDEX_SUFFIX):
+                os.replace(src + INDEX_SUFFIX, dst + INDEX_SUFFIX)
+            elif os.path.exists(dst + INDEX_SUFFIX):
+                os.remove(dst + INDEX_SUFFIX)      # a stale index of an earlier version
         parts.append(PartEntry(pos, os.path.getsize(dst), machine))
     meta = PartFileMeta(base, parts)
     write_meta(meta_path, meta)
@@ -140,6 +144,49 @@ def delete(meta_path: str):
         for p in meta.paths():
             if os.path.exists(p):
                 os.remove(p)
+            if os.path.exists(p + INDEX_SUFFIX):
+                os.remove(p + INDEX_SUFFIX)
     except Exception:
         pass
     os.remove(meta_path)
+
+
+# ------------------------------------------------------------------------------------------------
+# Record block index sidecar (``<part>.idx``): the byte offset of every B-th record of a part of
+# variable-length records, so the device decoder (ops/codec.decode_var) parses the blocks in
+# parallel without a sequential scan of the part.  Written next to the part by the writers that
+# know the record boundaries (io/binary.write_records, the device encoder); absent for parts
+# written elsewhere (the reader then scans the part on the host: codec.cpp scan_record_blocks).
+# Layout (little endian): b"DRIX", u32 version = 1, u32 B, u64 records, u64 part bytes,
+# u64 offsets[ceil(records / B)].
+INDEX_SUFFIX = ".idx"
+_INDEX_MAGIC = b"DRIX"
+
+
+def write_index(part_path: str, n: int, nbytes: int, offsets, block: int) -> None:
+    import struct
+    import numpy as np
+    offs = np.ascontiguousarray(np.asarray(offsets, dtype="<u8"))
+    with open(part_path + INDEX_SUFFIX, "wb") as f:
+        f.write(_INDEX_MAGIC + struct.pack("<IIQQ", 1, int(block), int(n), int(nbytes)))
+        f.write(offs.tobytes())
+
+
+def read_index(part_path: str):
+    """(records, part bytes, B, int64 offsets) of a part's index, or None when absent / stale."""
+    import struct
+    import numpy as np
+    p = part_path + INDEX_SUFFIX
+    if not os.path.exists(p):
+        return None
+    with open(p, "rb") as f:
+        head = f.read(28)
+        if len(head) != 28 or head[:4] != _INDEX_MAGIC:
+            return None
+        ver, block, n, nbytes = struct.unpack("<IIQQ", head[4:])
+        if ver != 1 or block == 0 or nbytes != os.path.getsize(part_path):
+            return None
+        offs = np.frombuffer(f.read(), dtype="<u8").astype(np.int64)
+    if offs.shape[0] != (n + block - 1) // block:
+        return None
+    return int(n), int(nbytes), int(block), offs

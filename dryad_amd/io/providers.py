@@ -139,6 +139,15 @@ class PartfileProvider(DataProvider):
             data = gzip.decompress(data)
         return B.decode_records(dtype, data)
 
+    def part_file(self, uri, i):
+        """Path of part i when its bytes are the record stream itself (not gzip-compressed), so a
+        reader can move them straight to HBM (io/reader.py); None otherwise."""
+        path = PF.read_meta(self._path(uri)).part_path(i)
+        with open(path, "rb") as f:
+            if f.read(2) == b"\x1f\x8b":
+                return None
+        return path
+
     def read_partition_bytes(self, uri, i) -> bytes:
         """The decoded record-stream bytes of part i (gzip-compressed parts are inflated)."""
         path = PF.read_meta(self._path(uri)).part_path(i)

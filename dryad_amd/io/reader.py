@@ -1,0 +1,99 @@
+"""File -> HBM: a part file read by the native ChunkReader (csrc/runtime/partreader.cpp: several
+reader threads pread() 64 MB chunks into a ring of page-locked host buffers) while every ready
+chunk is DMA'd to its place in the device buffer on a copy stream, so disk / page-cache reads,
+PCIe transfers and the readers' next chunks overlap.  Replaces read -> bytes -> pageable H2D
+(two host copies plus a bounce buffer).  Reference: the overlapped native channel reader,
+DryadVertex/VertexHost/system/channel/src/channelbuffernativereader.cpp.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from collections import deque
+
+import torch
+
+CHUNK = 64 << 20
+SLOTS = 8
+THREADS = 8
+
+_RING = None
+_RING_LOCK = threading.Lock()
+
+
+def _ring():
+    """The process's pinned staging ring (registered once; reused by every read)."""
+    global _RING
+    with _RING_LOCK:
+        if _RING is None:
+            from ..ops._lib import PinnedHostBuffer
+            _RING = [PinnedHostBuffer((CHUNK,)) for _ in range(SLOTS)]
+        return _RING
+
+
+class ReadStats:
+    def __init__(self):
+        self.bytes = 0
+        self.seconds = 0.0
+        self.chunks = 0
+
+
+def read_to_device(path: str, device, offset: int = 0, length: int = -1, out: torch.Tensor | None = None,
+                   stats: ReadStats | None = None) -> torch.Tensor:
+    """Bytes [offset, offset + length) of ``path`` (to the end when length < 0) into a device
+    uint8 tensor (``out`` when given).  Returns after the data is on the device (the copy stream
+    is joined to the current stream)."""
+    import time
+    from ..native import runtime
+    from ..ops import _lib
+    t0 = time.perf_counter()
+    size = os.path.getsize(path)
+    length = max(0, size - offset) if length < 0 else min(length, max(0, size - offset))
+    dev = torch.device(device)
+    if out is None:
+        out = torch.empty(length, dtype=torch.uint8, device=dev)
+    out = out.view(-1)
+    if out.numel() < length:
+        raise ValueError("read_to_device: output buffer too small")
+    if length == 0:
+        return out[:0]
+    ring = _ring()
+    with _RING_LOCK:           # one reader per process at a time owns the ring
+        rd = runtime().ChunkReader(path, int(offset), int(length), CHUNK, [b.tensor.data_ptr() for b in ring],
+                                   THREADS)
+        cur = torch.cuda.current_stream(dev)
+        cs = torch.cuda.Stream(dev)
+        cs.wait_stream(cur)
+        pending = deque()      # (slot, event) DMAs in flight
+        try:
+            while True:
+                while pending and pending[0][1].query():
+                    rd.release(pending.popleft()[0])
+                if len(pending) == len(ring):      # every slot is in a DMA: wait for the oldest
+                    s0, e0 = pending.popleft()
+                    e0.synchronize()
+                    rd.release(s0)
+                got = rd.next(-1)
+                if got is None:
+                    break
+                slot, chunk, nb = got
+                a = chunk * CHUNK
+                _lib.memcpy_async(out[a:a + nb], ring[slot].tensor[:nb], cs)
+                ev = torch.cuda.Event()
+                ev.record(cs)
+                pending.append((slot, ev))
+                if stats is not None:
+                    stats.chunks += 1
+            for s, e in pending:
+                e.synchronize()
+                rd.release(s)
+            pending.clear()
+        finally:
+            for s, e in pending:
+                e.synchronize()
+            rd.stop()
+        cur.wait_stream(cs)
+    if stats is not None:
+        stats.bytes += length
+        stats.seconds += time.perf_counter() - t0
+    return out[:length]

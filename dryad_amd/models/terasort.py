@@ -183,6 +183,7 @@ class TeraSortOOCJob:
 
     def step(self):
         st = self.EX.ExtSortStats()
+        self.out = None              # the previous output's HBM buckets are this step's to reuse
         self.out = self.EX.external_sort(self.src, 0, KEYLEN, self.world, budget=self.budget, stats=st,
                                          out=self.host, resident=True)
         self.stats = st

@@ -22,7 +22,11 @@ from ..gpu.table import DeviceTable
 
 
 def _compact_heap(t: DeviceTable) -> torch.Tensor:
-    """The selected lines of a text table as one '\\n'-separated heap."""
+    """The selected lines of a text table as one '\\n'-separated heap (e.g. the lines of a
+    decoded partfile part, whose heap is the record stream with length headers between lines)."""
+    if t.heap.is_cuda:
+        from ..ops import channel as CH
+        return CH.compact_heap(t.heap, t.cols["off"], t.cols["len"], sep=10)[0]
     ln1 = t.cols["len"] + 1
     tot = int(ln1.sum().item())
     starts = torch.cumsum(ln1, 0) - ln1

@@ -89,19 +89,26 @@ def scatter_columns(ent: torch.Tensor, n: int, cols: list, lut: torch.Tensor | N
     return outs, tot
 
 
-def compact_heap(heap: torch.Tensor, off: torch.Tensor, ln: torch.Tensor):
+def compact_heap(heap: torch.Tensor, off: torch.Tensor, ln: torch.Tensor, sep: int | None = None):
     """Bytes of strings (off[i], ln[i]) of ``heap`` laid out back to back in row order ->
-    (new heap, new int64 offsets)."""
+    (new heap, new int64 offsets).  ``sep``: one byte of that value after every string (e.g.
+    b'\\n' to turn selected lines into a tokenisable text heap)."""
     ln = ln.to(torch.int64)
-    doff = torch.cumsum(ln, 0) - ln
-    total = int(ln.sum()) if ln.numel() else 0
+    step = ln + 1 if sep is not None else ln
+    doff = torch.cumsum(step, 0) - step
+    total = int(step.sum()) if ln.numel() else 0
     out = torch.empty(total, dtype=torch.uint8, device=heap.device)
     if total == 0:
         return out, doff
     if not heap.is_cuda:
-        idx = torch.repeat_interleave(off.to(torch.int64) - doff, ln) + torch.arange(total)
-        return heap.index_select(0, idx), doff
-    off = off.to(torch.int64).contiguous()
-    _lib.call("dr_copy_segments", _lib.ptr(heap), _lib.ptr(off), _lib.ptr(ln.contiguous()), _lib.ptr(doff),
-              c_u64(off.shape[0]), _lib.ptr(out), _lib.stream_of(heap))
+        sel = torch.repeat_interleave(doff, ln) + torch.arange(int(ln.sum())) - \
+            torch.repeat_interleave(torch.cumsum(ln, 0) - ln, ln)
+        src = torch.repeat_interleave(off.to(torch.int64), ln) + sel - torch.repeat_interleave(doff, ln)
+        out[sel] = heap.index_select(0, src)
+    elif int(ln.sum()) > 0:
+        off = off.to(torch.int64).contiguous()
+        _lib.call("dr_copy_segments", _lib.ptr(heap), _lib.ptr(off), _lib.ptr(ln.contiguous()), _lib.ptr(doff),
+                  c_u64(off.shape[0]), _lib.ptr(out), _lib.stream_of(heap))
+    if sep is not None:
+        out[doff + ln] = sep
     return out, doff

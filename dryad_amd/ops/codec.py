@@ -77,3 +77,157 @@ def encode(table, dtype) -> torch.Tensor | None:
     _call(out, table.n, width, fields, cols, 1)
     return out
 
+
+
+# ------------------------------------------------------------------------------------------------
+# Variable-length records: strings (+ fixed-width primitives), csrc/kernels/codec.hip.
+_lib.register_signatures({
+    "dr_codec_var_decode": (c_i32, [vp, c_u64, vp, c_u64, c_u32, c_u64, c_i32, ctypes.POINTER(c_u32),
+                                    ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp]),
+    "dr_codec_var_sizes": (c_i32, [c_u64, c_i32, ctypes.POINTER(c_u32), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                   ctypes.POINTER(vp), vp, vp, vp]),
+    "dr_codec_var_encode": (c_i32, [vp, c_u64, c_i32, ctypes.POINTER(c_u32), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                    ctypes.POINTER(vp), vp, vp, vp]),
+})
+
+BLOCK = 64        # records per block of a block index (= io/binary.INDEX_BLOCK)
+
+# FieldKind codes of the native codec (csrc/runtime/codec.h)
+_KIND = {T.Byte: 0, T.SByte: 1, T.Bool: 2, T.Int16: 3, T.UInt16: 4, T.Int32: 5, T.UInt32: 6, T.Int64: 7,
+         T.UInt64: 8, T.Float32: 9, T.Float64: 10, T.String: 14}
+
+
+def var_layout(dtype):
+    """[(name, torch dtype | None for a string, bytes | 0)] of a record type of fixed-width
+    primitives and strings (no nullable fields, at least one string), or None."""
+    if dtype in (T.String, T.LineRecordT):
+        return [("v", None, 0)]
+    if isinstance(dtype, T.RecordT) and not dtype.nullable_fields:
+        out = []
+        for name, ft in dtype.fields:
+            if ft == T.String:
+                out.append((name, None, 0))
+            elif ft in _TORCH:
+                out.append((name, _TORCH[ft], ft.fixed_width))
+            else:
+                return None
+        return out if any(f[1] is None for f in out) and len(out) <= 32 else None
+    return None
+
+
+def schema_codes(dtype) -> list | None:
+    if dtype in (T.String, T.LineRecordT):
+        return [_KIND[T.String]]
+    if isinstance(dtype, T.RecordT) and not dtype.nullable_fields and all(ft in _KIND for _, ft in dtype.fields):
+        return [_KIND[ft] for _, ft in dtype.fields]
+    return None
+
+
+def block_index_host(data, dtype, block: int = BLOCK):
+    """(records, int64 offsets of every ``block``-th record) of a host record stream (native scan)."""
+    import numpy as np
+    from ..native import runtime
+    codes = schema_codes(dtype)
+    if codes is None:
+        raise ValueError(f"no native schema for {dtype}")
+    n, offs = runtime().scan_record_blocks(data, codes, int(block))
+    return int(n), np.asarray(offs, dtype=np.int64)
+
+
+class DecodeError(RuntimeError):
+    pass
+
+
+def decode_var(buf: torch.Tensor, dtype, n: int, block_off: torch.Tensor, block: int = BLOCK):
+    """HBM bytes of a part of variable-length records -> DeviceTable.  ``block_off``: int64
+    (device) byte offsets of records 0, block, 2 block, ...  String fields point into ``buf``
+    (the part's bytes become the string heap)."""
+    from ..gpu.table import DeviceTable, Shape, text_table
+    lay = var_layout(dtype)
+    if lay is None:
+        return None
+    dev = buf.device
+    cols, lens = [], []
+    for _, dt, sz in lay:
+        if dt is None:
+            cols.append(torch.empty(n, dtype=torch.int64, device=dev))
+            lens.append(torch.empty(n, dtype=torch.int64, device=dev))
+        else:
+            cols.append(torch.empty(n, dtype=dt, device=dev))
+            lens.append(None)
+    nf = len(lay)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    if n:
+        sizes = (c_u32 * nf)(*[sz for _, _, sz in lay])
+        cps = (vp * nf)(*[c.data_ptr() for c in cols])
+        lps = (vp * nf)(*[(x.data_ptr() if x is not None else 0) for x in lens])
+        bo = block_off.to(device=dev, dtype=torch.int64).contiguous()
+        _lib.call("dr_codec_var_decode", ptr(buf), c_u64(buf.numel()), ptr(bo), c_u64(bo.numel()), c_u32(block),
+                  c_u64(n), nf, sizes, cps, lps, ptr(err), stream_of(buf))
+        if int(err.item()):
+            raise DecodeError("record stream does not match its block index")
+    if dtype in (T.String, T.LineRecordT):
+        return text_table(buf, cols[0], lens[0], T.LineRecord if dtype == T.LineRecordT else str)
+    names = [f[0] for f in lay]
+    out, strs = {}, {}
+    for (name, dt, _), c, ln in zip(lay, cols, lens):
+        out[name] = c
+        if dt is None:
+            out[name + "#len"] = ln
+            strs[name] = buf
+    kind = "tuple" if dtype.pytype in (None, tuple) else "dataclass"
+    t = DeviceTable.from_columns(out, Shape(kind, names, None if kind == "tuple" else dtype.pytype))
+    t.strs = strs
+    return t
+
+
+def encode_var(table, dtype, block: int = BLOCK):
+    """Columnar DeviceTable with string fields -> (HBM record-stream bytes, int64 block index on
+    the device) in DryadLinqBinary layout, or None if not applicable."""
+    lay = var_layout(dtype)
+    if lay is None or table.rows is not None:
+        return None
+    n = table.n
+    dev = table.device
+    cols, lens, heaps = [], [], []
+    if dtype in (T.String, T.LineRecordT):
+        if table.heap is None:
+            return None
+        cols.append(table.cols["off"].to(torch.int64).contiguous())
+        lens.append(table.cols["len"].to(torch.int64).contiguous())
+        heaps.append(table.heap)
+    else:
+        if len(table.shape.fields) != len(lay):
+            return None
+        for (name, dt, _), fname in zip(lay, table.shape.fields):
+            if dt is None:
+                if fname not in table.strs:
+                    return None
+                cols.append(table.cols[fname].to(torch.int64).contiguous())
+                lens.append(table.cols[fname + "#len"].to(torch.int64).contiguous())
+                heaps.append(table.strs[fname])
+            else:
+                c = table.cols[fname]
+                if c.dtype != dt or c.dim() != 1:
+                    c = c.to(dt)
+                cols.append(c.contiguous())
+                lens.append(None)
+                heaps.append(None)
+    nf = len(lay)
+    nstr = sum(1 for f in lay if f[1] is None)
+    sizes = (c_u32 * nf)(*[sz for _, _, sz in lay])
+    cps = (vp * nf)(*[c.data_ptr() for c in cols])
+    lps = (vp * nf)(*[(x.data_ptr() if x is not None else 0) for x in lens])
+    hps = (vp * nf)(*[(h.data_ptr() if h is not None else 0) for h in heaps])
+    units = torch.empty(max(nstr * n, 1), dtype=torch.int32, device=dev)
+    rsz = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    st = stream_of(rsz)
+    if n:
+        _lib.call("dr_codec_var_sizes", c_u64(n), nf, sizes, cps, lps, hps, ptr(units), ptr(rsz), st)
+    offs = torch.cumsum(rsz[:n], 0)
+    total = int(offs[-1].item()) if n else 0
+    offs -= rsz[:n]
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    if n:
+        _lib.call("dr_codec_var_encode", ptr(out), c_u64(n), nf, sizes, cps, lps, hps, ptr(units), ptr(offs), st)
+    return out, offs[::block].contiguous()

@@ -1021,6 +1021,12 @@ def _commit_partfile_impl(runner, s, uri, path, local):
             mine[p] = tmp
             continue
         data = CD.encode(v, dt) if isinstance(v, DeviceTable) and v.device.type == "cuda" else None
+        index = None
+        if data is None and isinstance(v, DeviceTable) and v.device.type == "cuda":
+            enc = CD.encode_var(v, dt)              # strings: device encoder + block index
+            if enc is not None:
+                data, boffs = enc
+                index = (v.n, data.numel(), boffs.cpu().numpy(), CD.BLOCK)
         raw = data.cpu().numpy().tobytes() if data is not None else None
         if runner.ctx.OutputDataCompressionScheme.value != 0:
             import gzip
@@ -1030,6 +1036,8 @@ def _commit_partfile_impl(runner, s, uri, path, local):
         if raw is not None:
             with open(tmp, "wb") as f:
                 f.write(raw)
+            if index is not None and runner.ctx.OutputDataCompressionScheme.value == 0:
+                PF.write_index(tmp, index[0], index[1], index[2], index[3])
         else:
             B.write_records(tmp, dt, _to_objects(v) if not isinstance(v, list) else v)
         mine[p] = tmp
