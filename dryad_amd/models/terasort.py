@@ -168,7 +168,7 @@ class TeraSortOOCJob:
         self.budget = int(budget or free * 0.92)
         # host rows: at most n - (resident room) + one bucket (the suffix stops at a bucket edge)
         W = self.world.size
-        work = min(self.budget, max(int(self.budget * EX.HYBRID_WORK_FRACTION), min(EX.HYBRID_MIN_WORK, self.budget // 2)))
+        work = EX.hybrid_work(self.budget, self.n * RECORD)
         _, cap, _ = EX.plan_geometry(self.n, self.n * W, RECORD, W, work)
         room = self.budget - work - min(256 << 20, self.budget // 16)
         host_rows = max(0, min(int(self.n * (1 + cfg.slack)) + 1024, int(self.n * (1 + cfg.slack)) - room // RECORD + cap))
