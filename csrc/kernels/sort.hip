@@ -269,6 +269,91 @@ __global__ __launch_bounds__(256) void rs_scatter_v2(const T* __restrict__ in, T
   }
 }
 
+// v3: the v2 pass with the wave multisplit done through LDS lane masks instead of one ballot per
+// digit bit: every lane ORs its bit into the mask of its digit (ds_or_b64), reads the mask back
+// (= its peers), and the first peer clears it.  ~10 instructions per entry instead of ~45 for the
+// 8 ballots, which were half of the v2 pass's issue time (profiles/pmc_counters_r2.md).  LDS
+// instructions of one wave execute in order, so no barrier separates the OR, the read and the
+// clear.
+template <typename T, int ITEMS>
+__global__ __launch_bounds__(256) void rs_scatter_v3(const T* __restrict__ in, T* __restrict__ out,
+                                                     uint64_t n, int shift,
+                                                     const uint32_t* __restrict__ offsets, uint32_t G,
+                                                     uint64_t per_block) {
+  constexpr int kTile = kBlock * ITEMS;
+  __shared__ T stage[kTile];
+  __shared__ uint32_t wcnt[4][kBins];
+  __shared__ unsigned long long wmask[4][kBins];
+  __shared__ uint32_t goff[kBins];
+  __shared__ uint32_t bstart[kBins];
+  __shared__ uint32_t sc[4];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  goff[t] = offsets[(uint64_t)t * G + blockIdx.x];
+  wmask[0][t] = 0ull; wmask[1][t] = 0ull; wmask[2][t] = 0ull; wmask[3][t] = 0ull;
+  const uint64_t beg = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  T cur[ITEMS], nxt[ITEMS];
+  auto load_tile = [&](uint64_t base, T* dst) {
+    const uint32_t c = (uint32_t)((end - base) < (uint64_t)kTile ? (end - base) : kTile);
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+      if (pos < c) dst[r] = in[base + pos];
+    }
+  };
+  if (beg < end) load_tile(beg, cur);
+  const unsigned long long lanebit = 1ull << l;
+  for (uint64_t base = beg; base < end; base += kTile) {
+    const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kTile ? (end - base) : kTile);
+    if (base + kTile < end) load_tile(base + kTile, nxt);
+    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    __syncthreads();
+    uint32_t rk[ITEMS], dg[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+      const bool valid = pos < cnt;
+      const uint32_t d = valid ? digit_of(cur[r], shift) : 0u;
+      if (valid) atomicOr(&wmask[w][d], lanebit);
+      __builtin_amdgcn_wave_barrier();
+      const unsigned long long peers = valid ? wmask[w][d] : 0ull;
+      const uint32_t below = popc_below(peers);
+      const uint32_t prior = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) {
+        wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+        wmask[w][d] = 0ull;
+      }
+      __builtin_amdgcn_wave_barrier();
+      rk[r] = prior + below;
+      dg[r] = d;
+    }
+    __syncthreads();
+    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
+    uint32_t all;
+    bstart[t] = block_exclusive_scan256(tot, sc, all);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+      if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (uint32_t j = t; j < cnt; j += kBlock) {
+      const T v = stage[j];
+      const uint32_t d = digit_of(v, shift);
+      out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+    }
+    __syncthreads();
+    goff[t] += tot;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) cur[r] = nxt[r];
+  }
+}
+
 void scan_inplace(uint32_t* a, uint32_t M, uint32_t* partial, hipStream_t s) {
   const uint32_t S = (M + kScanChunk - 1) / kScanChunk;
   rs_scan_reduce<<<S, 256, 0, s>>>(a, M, partial);
@@ -1460,8 +1545,10 @@ DR_API int dr_extract_keys64(const uint8_t* rows, uint64_t n, uint32_t stride, u
 
 namespace {
 int g_items64 = 16;   // entries per thread per tile of the E64 scatter (8 / 16 / 32)
+int g_scatter64 = 3;  // E64 scatter variant: 2 = ballot multisplit, 3 = LDS lane-mask multisplit
 }
 DR_API void dr_sort64_set_items(int items) { g_items64 = (items == 8 || items == 32) ? items : 16; }
+DR_API void dr_sort64_set_variant(int v) { g_scatter64 = v == 2 ? 2 : 3; }
 
 // Stable LSD radix sort of E64 entries on bits [begin_bit, end_bit) (multiples of 8, < 64 = the
 // window); 16 entries per thread per tile (128 contiguous output bytes per digit run).
@@ -1485,7 +1572,14 @@ DR_API int dr_sort_u64(E64* keys, E64* tmp, uint64_t n, int begin_bit, int end_b
   for (int shift = begin_bit; shift < end_bit; shift += kRadixBits) {
     rs_count<<<G, 256, 0, s>>>(src, n, shift, counts, G, per_block);
     scan_inplace(counts, kBins * G, partial, s);
-    if (ITEMS == 32)
+    if (g_scatter64 == 3) {
+      if (ITEMS == 32)
+        rs_scatter_v3<E64, 32><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+      else if (ITEMS == 8)
+        rs_scatter_v3<E64, 8><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+      else
+        rs_scatter_v3<E64, 16><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+    } else if (ITEMS == 32)
       rs_scatter_v2<E64, 32><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
     else if (ITEMS == 8)
       rs_scatter_v2<E64, 8><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);

@@ -73,6 +73,10 @@ def init_world(device: str | None = None, backend: str | None = None, timeout_s:
             idx = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(idx)
         dev = torch.device("cuda", idx)
+        if os.environ.get("DRYAD_NUMA_BIND", "1") == "1":
+            # one rank per GPU: threads and pinned host buffers on the GPU's NUMA node
+            from .affinity import bind_to_gpu
+            bind_to_gpu(idx)
     else:
         dev = torch.device("cpu")
     if size > 1 and not dist.is_initialized():

@@ -62,3 +62,19 @@ def test_gpu_executor_fault_kinds_gloo(ranks):
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert f"FAULTS_OK {ranks}" in r.stdout
+
+
+def test_numa_affinity_helpers(tmp_path):
+    """GPU -> NUMA node -> CPU list from a fake sysfs tree (parallel/affinity.py)."""
+    from dryad_amd.parallel import affinity as A
+    dev = tmp_path / "bus" / "pci" / "devices" / "0000:c1:00.0"
+    dev.mkdir(parents=True)
+    (dev / "numa_node").write_text("1\n")
+    node = tmp_path / "devices" / "system" / "node" / "node1"
+    node.mkdir(parents=True)
+    (node / "cpulist").write_text("48-51,96,98-99\n")
+    assert A.parse_cpulist("0-2,5,7-8") == {0, 1, 2, 5, 7, 8}
+    assert A.gpu_numa_node("0000:C1:00.0", str(tmp_path)) == 1
+    assert A.node_cpus(1, str(tmp_path)) == {48, 49, 50, 51, 96, 98, 99}
+    (dev / "numa_node").write_text("-1\n")
+    assert A.gpu_numa_node("0000:c1:00.0", str(tmp_path)) is None

@@ -37,9 +37,13 @@ def main():
     lib = _lib.lib()
     lib.dr_sort64_set_items.argtypes = [_lib.c_i32]
     lib.dr_sort64_set_items.restype = None
+    lib.dr_sort64_set_variant.argtypes = [_lib.c_i32]
+    lib.dr_sort64_set_variant.restype = None
+    ref = None
     for rnd in range(2):
-        for items in (8, 16, 32):
+        for items, var in ((16, 2), (16, 3), (8, 3), (32, 3)):
             lib.dr_sort64_set_items(items)
+            lib.dr_sort64_set_variant(var)
 
             def srt():
                 ent.copy_(base)
@@ -49,8 +53,16 @@ def main():
                 ent.copy_(base)
             med, best = timeit(srt)
             cmed, _ = timeit(cp)
-            print(f"round {rnd} items={items}: sort64 4 passes {med - cmed:.2f} ms (median {med:.2f}, copy {cmed:.2f})",
-                  flush=True)
+            srt()
+            torch.cuda.synchronize()
+            res = ent.clone()
+            if ref is None:
+                ref = res
+            same = bool(torch.equal(res, ref))
+            print(f"round {rnd} items={items} variant={var}: sort64 4 passes {med - cmed:.2f} ms (median {med:.2f}, "
+                  f"copy {cmed:.2f}) same_as_first={same}", flush=True)
+    lib.dr_sort64_set_items(16)
+    lib.dr_sort64_set_variant(3)
 
 
 if __name__ == "__main__":
