@@ -457,35 +457,31 @@ class GpuJobRunner:
     # ------------------------------------------------------------------ channel transport
     def _transport(self, s, si, sends, recv_ids):
         """Move port values between ranks: ``sends[r]`` = values for rank r (in ``recv_ids`` order on
-        the receiving side).  Device tables of one schema go through parallel/exchange (RCCL
-        all-to-all-v per column, string heaps included); anything else (host records left by a
-        fallback, structurally different tables) through the object transport, recorded in
-        ``self.transports``.  Returns, per source rank, {source partition: value}."""
+        the receiving side), through the first transport of the channel registry
+        (parallel/channels.py) every rank can use: device tables of one schema as RCCL
+        all-to-all-v per column (string heaps included), anything else as host objects, recorded
+        in ``self.transports``.  Returns, per source rank, {source partition: value}."""
+        from ..parallel import channels as CHN
         from ..parallel import exchange as EXC
         W = self.world.size
-        dev_ok = all(isinstance(x, DeviceTable) for lst in sends for x in lst)
-        votes = [None] * W
-        dist.all_gather_object(votes, dev_ok)
-        if all(votes):
+        why = None
+        for tr in CHN.transports():
+            ok = tr.usable(sends)
+            votes = [None] * W
+            dist.all_gather_object(votes, ok)
+            if not all(votes):
+                why = why or ("host records on the channel" if tr.name == "device" else f"{tr.name} not usable")
+                continue
             try:
-                st = EXC.ExchangeStats()
-                got = EXC.exchange(self.world, sends, st)
-                self.transports.append((s.name, si.kind, "device", st.bytes_sent))
-                return [dict(zip(recv_ids[r], got[r])) for r in range(W)]
+                got, kind, detail = tr.move(self, sends)
             except EXC.SchemaMismatch as e:
                 why = str(e)
-        else:
-            why = "host records on the channel"
-        gathered = [None] * W
-        payload = [[self._ship(x) for x in lst] for lst in sends]
-        dist.all_gather_object(gathered, payload)
-        # one host value per partition (aggregate partials: the reference's final-aggregate
-        # vertex input) is control-plane sized; anything bigger is a data-plane object transfer
-        scalar = all(isinstance(x, list) and len(x) <= 1 for lst in sends for x in lst)
-        self.transports.append((s.name, si.kind, "scalar" if scalar and not why.startswith("ranks") else "object",
-                                why))
-        me = self.world.rank
-        return [dict(zip(recv_ids[r], [self._unship(x) for x in gathered[r][me]])) for r in range(W)]
+                continue
+            if kind == "scalar" and why and why.startswith("ranks"):
+                kind = "object"          # the ranks' tables disagree: not a control-plane partial
+            self.transports.append((s.name, si.kind, kind, detail if kind == "device" or why is None else why))
+            return [dict(zip(recv_ids[r], got[r])) for r in range(W)]
+        raise RuntimeError("no channel transport could move the values")
 
     @staticmethod
     def _ship(x):

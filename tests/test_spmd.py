@@ -78,3 +78,22 @@ def test_numa_affinity_helpers(tmp_path):
     assert A.node_cpus(1, str(tmp_path)) == {48, 49, 50, 51, 96, 98, 99}
     (dev / "numa_node").write_text("-1\n")
     assert A.gpu_numa_node("0000:c1:00.0", str(tmp_path)) is None
+
+
+def test_channel_registry_order_and_registration():
+    from dryad_amd.parallel import channels as CHN
+    names = [t.name for t in CHN.transports()]
+    assert names[:1] == ["device"] and names[-1] == "object"
+
+    class Probe(CHN.Transport):
+        name = "probe"
+
+        def usable(self, sends):
+            return False
+
+    CHN.register_transport(Probe())
+    try:
+        assert [t.name for t in CHN.transports()][0] == "probe"
+    finally:
+        CHN.unregister_transport("probe")
+    assert "probe" not in [t.name for t in CHN.transports()]
