@@ -54,6 +54,15 @@ def node_cpus(node: int, sysfs: str = SYSFS) -> set:
     return parse_cpulist(_read(os.path.join(sysfs, "devices", "system", "node", f"node{node}", "cpulist")) or "")
 
 
+def pci_address(props) -> str:
+    """'dddd:bb:dd.0' of a torch device-properties object (domain / bus / device ids are ints)."""
+    bus = getattr(props, "pci_bus_id", None)
+    if isinstance(bus, str):
+        return bus
+    return f"{int(getattr(props, 'pci_domain_id', 0) or 0):04x}:{int(bus or 0):02x}:" \
+           f"{int(getattr(props, 'pci_device_id', 0) or 0):02x}.0"
+
+
 def bind_to_gpu(device_index: int, sysfs: str = SYSFS, apply: bool = True) -> dict:
     """Restrict this process to the CPUs of GPU ``device_index``'s NUMA node.  Returns what was
     decided ({"node", "cpus", "applied"}); never raises (placement is an optimisation)."""
@@ -61,11 +70,7 @@ def bind_to_gpu(device_index: int, sysfs: str = SYSFS, apply: bool = True) -> di
     try:
         import torch
         props = torch.cuda.get_device_properties(device_index)
-        bus = getattr(props, "pci_bus_id", None)
-        if bus is None:
-            dom = getattr(props, "pci_domain_id", 0)
-            bus = f"{dom:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}.0"
-        node = gpu_numa_node(str(bus), sysfs)
+        node = gpu_numa_node(pci_address(props), sysfs)
     except Exception:  # noqa: BLE001
         return info
     info["node"] = node

@@ -97,3 +97,10 @@ def test_channel_registry_order_and_registration():
     finally:
         CHN.unregister_transport("probe")
     assert "probe" not in [t.name for t in CHN.transports()]
+
+
+def test_numa_pci_address_format():
+    from types import SimpleNamespace
+    from dryad_amd.parallel import affinity as A
+    assert A.pci_address(SimpleNamespace(pci_bus_id=0xc1, pci_device_id=0, pci_domain_id=0)) == "0000:c1:00.0"
+    assert A.pci_address(SimpleNamespace(pci_bus_id="0000:05:00.0")) == "0000:05:00.0"
