@@ -1,3 +1,5 @@
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch, os, json
 from dryad_amd.parallel import affinity as A
 p = torch.cuda.get_device_properties(0)
