@@ -7,15 +7,22 @@ import tempfile
 import dryad_amd as D
 
 _CTX = {}
+# "cpu": the process executor (vertex hosts); "gpu": the SPMD GPU executor, n partitions on this
+# process's GPU (tests/test_gpu_oracle_suites.py reruns the oracle suites that way)
+MODE = "cpu"
 
 
 def cluster_ctx(n=3, pool="thread"):
-    key = (n, pool)
+    key = (MODE, n, pool)
     c = _CTX.get(key)
     if c is None:
-        c = D.DryadLinqContext(n)
-        c._props["PoolKind"] = pool
-        c._props["OutlierThresholdSeconds"] = None
+        if MODE == "gpu":
+            c = D.DryadLinqContext(platform="gpu")
+            c.PartitionCount = n
+        else:
+            c = D.DryadLinqContext(n)
+            c._props["PoolKind"] = pool
+            c._props["OutlierThresholdSeconds"] = None
         _CTX[key] = c
     return c
 
