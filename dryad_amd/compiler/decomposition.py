@@ -339,6 +339,9 @@ def decompose(result_selector, element_selector=None) -> Decomposition | None:
     """Try to decompose ``result_selector(key, group)``; None if not decomposable."""
     if result_selector is None:
         return None
+    from ..gpu.trace import uses_identity
+    if uses_identity(result_selector) or (element_selector is not None and uses_identity(element_selector)):
+        return None             # `is` on a symbolic key / group cannot be decided per group
     aggs: list = []
     g = GroupProxy(aggs)
     try:

@@ -237,10 +237,37 @@ def proxy(table: DeviceTable):
     return RecProxy(table)
 
 
+_IDENTITY_CACHE: dict = {}
+
+
+def _code_uses_identity(code) -> bool:
+    import dis
+    import types
+    for ins in dis.get_instructions(code):
+        if ins.opname == "IS_OP":
+            return True
+    return any(_code_uses_identity(c) for c in code.co_consts if isinstance(c, types.CodeType))
+
+
+def uses_identity(fn) -> bool:
+    """Does fn (or a function nested in it) compare with ``is`` / ``is not``?  Identity cannot be
+    overloaded, so a traced field would compare as one Python object: ``b is True`` would turn
+    into a constant instead of a per-record test (reference MiscBugFixTests Bug15159)."""
+    code = getattr(fn, "__code__", None)
+    if code is None:
+        return False
+    r = _IDENTITY_CACHE.get(code)
+    if r is None:
+        r = _IDENTITY_CACHE[code] = _code_uses_identity(code)
+    return r
+
+
 def call(fn, table: DeviceTable, index_base: int | None = None):
     """Evaluate fn over the table's records; returns the raw traced result."""
     if table.n == 0:
         raise NotTraceable("empty partition (evaluated on host)")
+    if uses_identity(fn):
+        raise NotTraceable("identity comparison (`is`) on a record")
     args = [proxy(table)]
     if index_base is not None:
         args.append(Col(torch.arange(index_base, index_base + table.n, device=table.device, dtype=torch.int64)))
