@@ -41,7 +41,7 @@ def main():
     lib.dr_sort64_set_variant.restype = None
     ref = None
     for rnd in range(2):
-        for items, var in ((16, 2), (16, 3), (8, 3), (32, 3)):
+        for items, var in ((16, 3), (16, 4)):
             lib.dr_sort64_set_items(items)
             lib.dr_sort64_set_variant(var)
 
@@ -63,6 +63,19 @@ def main():
                   f"copy {cmed:.2f}) same_as_first={same}", flush=True)
     lib.dr_sort64_set_items(16)
     lib.dr_sort64_set_variant(3)
+    # gather: plain vs nontemporal output stores
+    lib.dr_gather_fixup_set_nt.argtypes = [_lib.c_i32]
+    lib.dr_gather_fixup_set_nt.restype = None
+    ent.copy_(base)
+    srt_e = S.sort_entries64(ent, tmp, 32)
+    out = torch.empty_like(rows)
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    for rnd in range(2):
+        for nt in (0, 1):
+            lib.dr_gather_fixup_set_nt(nt)
+            med, best = timeit(lambda: S.gather_fixup(rows, srt_e, out, 0, 10, 32, flag))
+            print(f"round {rnd} gather nt={nt}: {med:.2f} ms (best {best:.2f})", flush=True)
+    lib.dr_gather_fixup_set_nt(0)
 
 
 if __name__ == "__main__":
