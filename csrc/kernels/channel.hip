@@ -203,6 +203,28 @@ __global__ __launch_bounds__(256) void copy_segments_kernel(const uint8_t* __res
     __builtin_amdgcn_wave_barrier();
   }
 }
+// Bulk copy by the CUs (16-byte vector loads / stores, 4 in flight per lane, grid-stride).  Either
+// side may be page-locked host memory mapped into the device address space: the CUs then move the
+// bytes over PCIe themselves, without a DMA engine (a second path next to the copy engines when
+// both directions stream at once).
+__global__ __launch_bounds__(256) void copy_wide_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                        uint64_t n16) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = src[i + k * stride];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[i + k * stride] = v[k];
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+__global__ void copy_tail_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint32_t n) {
+  const uint32_t i = threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
 }  // namespace
 
 // Geometry shared by the count and scatter launches (the caller sizes `counts` as 256 * G).
@@ -248,6 +270,25 @@ DR_API int dr_copy_segments(const uint8_t* src, const int64_t* soff, const int64
                             uint64_t n, uint8_t* dst, hipStream_t s) {
   if (n == 0) return 0;
   copy_segments_kernel<<<grid_for((n + 63) / 64, 4, 8192), 256, 0, s>>>(src, soff, len, doff, n, dst);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// dst/src: device pointers (HBM, or page-locked host memory through its device mapping).
+// grid: workgroups (0 = 1024).  Bytes past the last 16-byte block are copied by a second launch.
+DR_API int dr_copy_wide(void* dst, const void* src, uint64_t nbytes, uint32_t grid, hipStream_t s) {
+  if (nbytes == 0) return 0;
+  if (((uintptr_t)dst | (uintptr_t)src) & 15) return (int)hipErrorInvalidValue;
+  const uint64_t n16 = nbytes / 16;
+  if (n16) {
+    const uint64_t want = (n16 + 255) / 256;
+    const uint32_t g = (uint32_t)(want < (grid ? grid : 1024u) ? want : (grid ? grid : 1024u));
+    copy_wide_kernel<<<g, 256, 0, s>>>(static_cast<const uint4*>(src), static_cast<uint4*>(dst), n16);
+  }
+  const uint32_t tail = (uint32_t)(nbytes - n16 * 16);
+  if (tail)
+    copy_tail_kernel<<<1, 64, 0, s>>>(static_cast<const uint8_t*>(src) + n16 * 16, static_cast<uint8_t*>(dst) + n16 * 16,
+                                      tail);
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -143,7 +143,20 @@ def hip_runtime():
         _HIP.hipHostUnregister.argtypes = [vp]
         _HIP.hipMemcpyAsync.restype = c_i32
         _HIP.hipMemcpyAsync.argtypes = [vp, vp, ctypes.c_size_t, c_i32, vp]
+        _HIP.hipHostGetDevicePointer.restype = c_i32
+        _HIP.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(vp), vp, ctypes.c_uint]
     return _HIP
+
+
+def device_address(t: torch.Tensor) -> int:
+    """Address of ``t``'s first element as the GPU sees it: HBM tensors as they are, page-locked
+    host memory (torch-pinned or hipHostRegister'ed) through its device mapping."""
+    if t.is_cuda:
+        return t.data_ptr()
+    out = vp()
+    check(hip_runtime().hipHostGetDevicePointer(ctypes.byref(out), ctypes.c_void_p(t.data_ptr()), 0),
+          "hipHostGetDevicePointer")
+    return int(out.value or 0)
 
 
 HIP_MEMCPY_H2D, HIP_MEMCPY_D2H = 1, 2

@@ -20,6 +20,7 @@ _lib.register_signatures({
     "dr_pc_scatter": (ctypes.c_int, [vp, c_u64, vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(c_u32),
                                      c_u32, vp, c_u32, c_u64, vp]),
     "dr_copy_segments": (ctypes.c_int, [vp, vp, vp, vp, c_u64, vp, vp]),
+    "dr_copy_wide": (ctypes.c_int, [vp, vp, c_u64, c_u32, vp]),
 })
 
 MAX_COLS = 16
@@ -112,3 +113,22 @@ def compact_heap(heap: torch.Tensor, off: torch.Tensor, ln: torch.Tensor, sep: i
     if sep is not None:
         out[doff + ln] = sep
     return out, doff
+
+
+def copy_wide(dst: torch.Tensor, src: torch.Tensor, stream=None, grid: int = 0) -> None:
+    """dst <- src by a CU copy kernel on ``stream``.  One side may be page-locked host memory: the
+    CUs then read or write it over PCIe through its device mapping, leaving the DMA engines to the
+    other direction (dr_copy_wide).  Both tensors contiguous, same byte size, 16-byte aligned."""
+    n = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() != n:
+        raise ValueError("copy_wide: size mismatch")
+    if n == 0:
+        return
+    if not (dst.is_contiguous() and src.is_contiguous()):
+        raise ValueError("copy_wide: contiguous tensors only")
+    dev = dst.device if dst.is_cuda else src.device
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    with torch.cuda.device(dev):
+        _lib.call("dr_copy_wide", ctypes.c_void_p(_lib.device_address(dst)), ctypes.c_void_p(_lib.device_address(src)),
+                  c_u64(n), c_u32(grid), ctypes.c_void_p(stream.cuda_stream))

@@ -70,3 +70,24 @@ def test_compact_heap_matches_python(n):
     assert torch.equal(out.cpu(), exp)
     cpu_out, cpu_doff = CH.compact_heap(h, off.cpu(), ln.cpu())
     assert torch.equal(cpu_out, exp) and torch.equal(cpu_doff, doff.cpu())
+
+
+@pytest.mark.parametrize("nbytes", [1, 15, 16, 4097, (3 << 20) + 5])
+def test_copy_wide_between_hbm_and_pinned_host(nbytes):
+    """CU copy kernel: HBM -> HBM, page-locked host -> HBM and HBM -> page-locked host (through
+    the host buffer's device mapping), tails that are not a multiple of 16 bytes included."""
+    from dryad_amd.ops import _lib
+    g = torch.Generator().manual_seed(nbytes)
+    src_h = _lib.PinnedHostBuffer((nbytes,))
+    src_h.tensor.copy_(torch.randint(0, 256, (nbytes,), dtype=torch.uint8, generator=g))
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    CH.copy_wide(d, src_h.tensor)
+    d2 = torch.empty_like(d)
+    CH.copy_wide(d2, d, grid=7)
+    back = _lib.PinnedHostBuffer((nbytes,))
+    CH.copy_wide(back.tensor, d2)
+    torch.cuda.synchronize()
+    assert torch.equal(d.cpu(), src_h.tensor)
+    assert torch.equal(back.tensor, src_h.tensor)
+    with pytest.raises(ValueError):
+        CH.copy_wide(d[:nbytes - 1] if nbytes > 1 else d[:0], src_h.tensor)
