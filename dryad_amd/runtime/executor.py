@@ -63,8 +63,16 @@ class _BaseExecutor:
             except Exception:
                 pass
 
+    def _enter_job_thread(self):
+        """Per-thread setup of a job thread (the GPU executor binds it to its rank's device)."""
+
     def submit(self, outs, handle):
         def body():
+            try:
+                self._enter_job_thread()
+            except BaseException as e:  # noqa: BLE001
+                handle.finish(False, e)
+                return
             handle.set_running()
             try:
                 r = self.run_job(outs, handle)

@@ -1076,7 +1076,17 @@ class GpuExecutor(_BaseExecutor):
         from ..gpu.pool import HbmPool
         self.pool = HbmPool(w.device) if w.device.type == "cuda" else None
 
+    def _enter_job_thread(self):
+        """Jobs run on a thread of their own, and the HIP current device is per thread (a new one
+        starts on device 0): bind it to this rank's GPU, or the library's launches on the default
+        (null) stream and its device queries would go to GPU 0 on every rank."""
+        if self.world.device.type == "cuda" and self.world.device.index is not None:
+            torch.cuda.set_device(self.world.device)
+
     def run_job(self, outs, handle):
+        dev = self.world.device
+        if dev.type == "cuda" and dev.index is not None and torch.cuda.current_device() != dev.index:
+            torch.cuda.set_device(dev)
         plan = compile_queries(self.ctx, outs)
         faults = self.ctx._props.get("FaultInjection") or []
         for st in plan.stages:      # CheckExistence(deleteIfExists) at submission
