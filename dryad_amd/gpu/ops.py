@@ -251,9 +251,16 @@ def op_read(op, inputs, v):
         from ..ops import text as TX
         from .table import text_table
         from .. import types as T
-        data = provider_for(uri).read_partition_bytes(uri, v.partition)
-        heap = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(v.device) if data else \
-            torch.zeros(0, dtype=torch.uint8, device=v.device)
+        prov = provider_for(uri)
+        if v.device.type == "cuda" and hasattr(prov, "ranges"):
+            # the partition's byte range through the native chunked reader (pinned ring -> HBM)
+            from ..io import reader as RD
+            f, a, b = prov.ranges(uri)[v.partition]
+            heap = RD.read_to_device(f, v.device, offset=a, length=b - a)
+        else:
+            data = prov.read_partition_bytes(uri, v.partition)
+            heap = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(v.device) if data else \
+                torch.zeros(0, dtype=torch.uint8, device=v.device)
         off, ln = TX.lines(heap)
         t = text_table(heap, off, ln, T.LineRecord)
         t.whole_heap = True           # every line of the heap, in order (tokenise the heap directly)

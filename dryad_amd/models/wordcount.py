@@ -45,7 +45,8 @@ def word_counts(lines: DeviceTable) -> list:
     if lines.heap is not None and lines.heap.is_cuda:
         from ..ops import text as TX
         heap = lines.heap if getattr(lines, "whole_heap", False) else _compact_heap(lines)
-        return TX.word_count(heap)
+        t = TX.word_count_table(heap)        # (word, count) groups stay in HBM
+        return t if t is not None else TX.word_count(heap)
     c = Counter()
     for ln in lines.to_objects():
         c.update((ln.Line if hasattr(ln, "Line") else ln).split())

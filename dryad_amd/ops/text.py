@@ -102,12 +102,14 @@ def gather_strings(buf: torch.Tensor, off: torch.Tensor, ln: torch.Tensor) -> li
     return out
 
 
-def word_count(buf: torch.Tensor) -> list:
-    """[(word, count)] of the whitespace tokens in ``buf`` (device hash-group + exact check)."""
+def _word_groups(buf: torch.Tensor):
+    """Token groups of ``buf``: (token offsets, lengths, sorted representative token per group,
+    group start positions in the sorted order, token count), or None on a 64-bit hash collision
+    between different words."""
     off, ln = tokens(buf)
     nt = off.shape[0]
     if nt == 0:
-        return []
+        return off, ln, None, None, 0
     h = token_hash(buf, off, ln)
     e = torch.empty((nt, 2), dtype=torch.int64, device=buf.device)
     e[:, 1] = h
@@ -121,12 +123,44 @@ def word_count(buf: torch.Tensor) -> list:
     bad = torch.zeros(1, dtype=torch.int32, device=buf.device)
     _lib.call("dr_token_verify", ptr(buf), ptr(off), ptr(ln), ptr(rep), c_u64(nt), ptr(bad), stream_of(buf))
     if int(bad.item()):
+        return None
+    return off, ln, order.index_select(0, starts), starts, nt
+
+
+def word_count(buf: torch.Tensor) -> list:
+    """[(word, count)] of the whitespace tokens in ``buf`` (device hash-group + exact check)."""
+    g = _word_groups(buf)
+    if g is None:
         # 64-bit hash collision between different words: exact host path (never seen in practice)
         from collections import Counter
-        words = gather_strings(buf, off, ln)
-        return list(Counter(words).items())
+        off, ln = tokens(buf)
+        return list(Counter(gather_strings(buf, off, ln)).items())
+    off, ln, reps, starts, nt = g
+    if nt == 0:
+        return []
     ends = torch.cat([starts[1:], torch.tensor([nt], dtype=torch.int64, device=buf.device)])
     counts = (ends - starts).cpu().tolist()
-    reps = order.index_select(0, starts)
     words = gather_strings(buf, off.index_select(0, reps), ln.index_select(0, reps))
     return list(zip(words, counts))
+
+
+def word_count_table(buf: torch.Tensor):
+    """The (word, count) groups of ``buf`` as an HBM table of (String, Int32) tuples -- the words
+    compacted into a string heap on the device, no host round trip -- or None when the exact
+    check found a hash collision (the caller then takes the host path)."""
+    from ..gpu.table import DeviceTable, Shape
+    from . import channel as CH
+    g = _word_groups(buf)
+    if g is None:
+        return None
+    off, ln, reps, starts, nt = g
+    if nt == 0:
+        return None
+    ends = torch.cat([starts[1:], torch.tensor([nt], dtype=torch.int64, device=buf.device)])
+    counts = ends - starts
+    wl = ln.index_select(0, reps)
+    heap, woff = CH.compact_heap(buf, off.index_select(0, reps), wl)
+    cnt = counts.to(torch.int32) if nt < (1 << 31) else counts
+    t = DeviceTable.from_columns({"Item1": woff, "Item1#len": wl, "Item2": cnt}, Shape("tuple", ["Item1", "Item2"]))
+    t.strs = {"Item1": heap}
+    return t

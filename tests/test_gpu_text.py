@@ -35,6 +35,19 @@ def test_word_count_matches_counter(tmp_path):
     assert got == dict(Counter(data.decode().split()))
 
 
+def test_word_count_table_matches_counter(tmp_path):
+    """(word, count) groups built as an HBM table (device-compacted word heap, Int32 counts)."""
+    from dryad_amd.models.wordcount import synthetic_corpus
+    from dryad_amd.ops import text as TX
+    p = synthetic_corpus(str(tmp_path / "c.txt"), 20000, vocab=3000)
+    data = open(p, "rb").read()
+    t = TX.word_count_table(_heap(data))
+    assert t is not None and t.strs["Item1"].is_cuda and t.cols["Item2"].dtype == torch.int32
+    got = dict(t.to_objects())
+    assert got == dict(Counter(data.decode().split()))
+    assert TX.word_count_table(_heap(b"   \n")) is None
+
+
 def test_wordcount_query_on_gpu_executor(tmp_path):
     import dryad_amd as D
     from dryad_amd.models.wordcount import synthetic_corpus, word_count_query
