@@ -28,6 +28,9 @@ def newest_job(home: str | None = None) -> str | None:
 
 
 def load(job_dir: str) -> dict:
+    import sys
+    if "dryad_amd.runtime.gpu_executor" in sys.modules:      # in-process: queued GPU job-dir writes
+        sys.modules["dryad_amd.runtime.gpu_executor"].flush_job_dirs()
     j = {"dir": job_dir, "events": [], "stats": {}, "explain": "", "error": None}
     ev = os.path.join(job_dir, "log", "events.jsonl")
     if os.path.exists(ev):
