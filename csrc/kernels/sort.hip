@@ -1432,17 +1432,45 @@ __global__ __launch_bounds__(256) void extract_keys64_kernel(const uint8_t* __re
   }
 }
 
+// ent[i] := (key bits [P, P + 32) of row (ent[i] & 0xFFFFFFFF)) << 32 | row: the next, more
+// significant window of an LSD chain of compact sorts over a key longer than one window.
+__global__ __launch_bounds__(256) void rekey64_kernel(const uint8_t* __restrict__ rows, uint32_t pitch,
+                                                      uint32_t key_off, uint32_t key_len, uint32_t P,
+                                                      E64* __restrict__ ent, uint64_t n) {
+  const bool aligned = ((pitch | key_off) & 3) == 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t idx = (uint32_t)ent[i].v;
+    uint64_t k0, k1;
+    load_key128(rows + (uint64_t)idx * pitch + key_off, key_len, aligned, k0, k1);
+    E64 e;
+    e.v = ((uint64_t)key_window(k0, k1, P) << 32) | idx;
+    ent[i] = e;
+  }
+}
+
+// ent[i] := i << 32 | row: every entry its own run (the gather copies without a fix-up).
+__global__ __launch_bounds__(256) void e64_position_window_kernel(E64* __restrict__ ent, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    E64 e;
+    e.v = (i << 32) | (uint32_t)ent[i].v;
+    ent[i] = e;
+  }
+}
+
 constexpr int kGfCore = 256, kGfExt = 64, kGfWin = kGfCore + kGfExt;
 
 // One workgroup per 256 output positions (grid-stride): owns the runs that START in its core and
 // finishes them up to 64 positions past it; positions of a run started by the previous workgroup
 // are left to that workgroup.  Rows are copied dword-wise, output-coalesced (gather_rows_kernel).
-template <int WC, bool NT = false>
+// WIC: input words per row when the input rows are stored at a wider pitch than the output's
+// (0: same as the output).
+template <int WC, bool NT = false, int WIC = 0>
 __global__ __launch_bounds__(256) void gather_fixup_kernel(const uint32_t* __restrict__ rows, uint32_t* __restrict__ out,
                                                            const E64* __restrict__ ent, uint64_t n, uint32_t Wdyn,
                                                            uint32_t key_off, uint32_t key_len, int run_shift,
                                                            uint32_t* __restrict__ overflow) {
   const uint32_t W = WC > 0 ? (uint32_t)WC : Wdyn;
+  const uint32_t Win = WIC > 0 ? (uint32_t)WIC : W;
   __shared__ uint32_t rid[kGfWin + 1];     // rid[p + 1] = run id of window position p; rid[0] = position -1
   __shared__ uint32_t idx[kGfWin];
   __shared__ uint32_t sidx[kGfWin];
@@ -1450,7 +1478,7 @@ __global__ __launch_bounds__(256) void gather_fixup_kernel(const uint32_t* __res
   __shared__ uint32_t own[2];
   const int t = threadIdx.x;
   const uint8_t* rbytes = reinterpret_cast<const uint8_t*>(rows);
-  const bool aligned = (((W * 4) | key_off) & 3) == 0;
+  const bool aligned = (((Win * 4) | key_off) & 3) == 0;
   for (uint64_t c0 = (uint64_t)blockIdx.x * kGfCore; c0 < n; c0 += (uint64_t)gridDim.x * kGfCore) {
     const uint32_t L = (uint32_t)((n - c0) < (uint64_t)kGfWin ? (n - c0) : kGfWin);
     const uint32_t core = L < (uint32_t)kGfCore ? L : (uint32_t)kGfCore;
@@ -1487,7 +1515,7 @@ __global__ __launch_bounds__(256) void gather_fixup_kernel(const uint32_t* __res
       const bool multi = (p > ob && rid[p + 1] == rid[p]) || (p + 1 < oe && rid[p + 2] == rid[p + 1]);
       if (multi) {
         uint64_t k0, k1;
-        load_key128(rbytes + (uint64_t)idx[p] * (W * 4) + key_off, key_len, aligned, k0, k1);
+        load_key128(rbytes + (uint64_t)idx[p] * (Win * 4) + key_off, key_len, aligned, k0, k1);
         kk0[p] = k0;
         kk1[p] = k1;
       } else {
@@ -1521,7 +1549,7 @@ __global__ __launch_bounds__(256) void gather_fixup_kernel(const uint32_t* __res
       for (int k = 0; k < 4; ++k) {
         const uint32_t jj = j + k * kBlock;
         const uint32_t r = jj / W, c = jj - r * W;
-        v[k] = rows[(uint64_t)sidx[r] * W + c];
+        v[k] = rows[(uint64_t)sidx[r] * Win + c];
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -1531,7 +1559,7 @@ __global__ __launch_bounds__(256) void gather_fixup_kernel(const uint32_t* __res
     }
     for (; j < words; j += kBlock) {
       const uint32_t r = j / W, c = j - r * W;
-      o[j] = rows[(uint64_t)sidx[r] * W + c];
+      o[j] = rows[(uint64_t)sidx[r] * Win + c];
     }
     __syncthreads();
   }
@@ -1659,6 +1687,40 @@ DR_API int dr_gather_fixup(const uint8_t* rows, uint8_t* out, const E64* ent, ui
     gather_fixup_kernel<25><<<g, 256, 0, s>>>(in, o, ent, n, W, key_off, key_len, run_shift, overflow);
   else
     gather_fixup_kernel<0><<<g, 256, 0, s>>>(in, o, ent, n, W, key_off, key_len, run_shift, overflow);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// dr_gather_fixup from input rows stored at a 128-byte pitch (in: n x 128 bytes, the first
+// `stride` bytes of each row are the record) into back-to-back rows of `stride` bytes.
+DR_API int dr_gather_fixup_pitch128(const uint8_t* rows, uint8_t* out, const E64* ent, uint64_t n, uint32_t stride,
+                                    uint32_t key_off, uint32_t key_len, int run_shift, uint32_t* overflow,
+                                    hipStream_t s) {
+  if (stride != 100 || key_len == 0 || key_len > 16 || key_off + key_len > stride) return (int)hipErrorInvalidValue;
+  if (run_shift < 32 || run_shift > 63) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  const unsigned g = grid_for(n, kGfCore, 16384);
+  gather_fixup_kernel<25, true, 32><<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows),
+                                                      reinterpret_cast<uint32_t*>(out), ent, n, 25, key_off, key_len,
+                                                      run_shift, overflow);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// Rows are `pitch` bytes apart (100 back to back, or 128 for the line-aligned layout).
+DR_API int dr_rekey64(const uint8_t* rows, uint32_t pitch, uint32_t key_off, uint32_t key_len, uint32_t P, E64* ent,
+                      uint64_t n, hipStream_t s) {
+  if (key_len == 0 || key_len > 16 || key_off + key_len > pitch || n >= (1ull << 32)) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  rekey64_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(rows, pitch, key_off, key_len, P, ent, n);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+DR_API int dr_e64_position_window(E64* ent, uint64_t n, hipStream_t s) {
+  if (n >= (1ull << 32)) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  e64_position_window_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(ent, n);
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -26,7 +26,9 @@ using dr_ts::ts_record;
 // that consumes the generated table skips its key-extraction pass (one 100-byte row read each).
 // KEYS: 0 = rows only, 1 = E128 entries (full 80-bit key), 2 = E64 entries of the compact row
 // sort (key bits 0..31 in the high word: the window for a zero common prefix).
-template <int KEYS, bool ROWS = true>
+// PITCH: 32-bit words per stored row: 25 (100-byte rows back to back) or 32 (one row per aligned
+// 128-byte line, bytes 100..127 zero: the HBM line a random row read fetches holds exactly that row).
+template <int KEYS, bool ROWS = true, int PITCH = 25>
 __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out, uint64_t n, uint64_t first,
                                                      uint64_t seed, void* __restrict__ keys, uint32_t idx_base,
                                                      unsigned long long* __restrict__ hi_range) {
@@ -58,6 +60,21 @@ __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out,
     }
     if (!ROWS) continue;                       // keys only: no record image to store
     __syncthreads();
+    if constexpr (PITCH == 32) {
+      uint4* dst = reinterpret_cast<uint4*>(out + row0 * 32);
+      for (uint32_t j = threadIdx.x; j < rows * 8; j += 256) {
+        const uint32_t r = j >> 3, q = (j & 7) * 4;
+        const uint32_t* src = img + r * 25 + q;
+        uint4 v;
+        v.x = q < 25 ? src[0] : 0u;
+        v.y = q + 1 < 25 ? src[1] : 0u;
+        v.z = q + 2 < 25 ? src[2] : 0u;
+        v.w = q + 3 < 25 ? src[3] : 0u;
+        dst[j] = v;
+      }
+      __syncthreads();
+      continue;
+    }
     uint32_t* o = out + row0 * 25;
     const uint32_t words = rows * 25;
     if (rows == 256) {
@@ -149,6 +166,19 @@ DR_API int dr_terasort_gen_keys64(uint8_t* out, uint64_t n, uint64_t first_index
   ts_gen_kernel<2><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index,
                                                            seed, keys, idx_base,
                                                            reinterpret_cast<unsigned long long*>(hi_range));
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// Same with the records at a 128-byte pitch (out: n x 128 bytes, bytes 100..127 of each row zero).
+DR_API int dr_terasort_gen_keys64_pitch128(uint8_t* out, uint64_t n, uint64_t first_index, uint64_t seed, E64* keys,
+                                           uint32_t idx_base, uint64_t* hi_range, hipStream_t s) {
+  if (n == 0) return 0;
+  if (n + idx_base > (1ull << 32)) return (int)hipErrorInvalidValue;
+  if (reinterpret_cast<uintptr_t>(out) & 15) return (int)hipErrorInvalidValue;
+  ts_gen_kernel<2, true, 32><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index,
+                                                                     seed, keys, idx_base,
+                                                                     reinterpret_cast<unsigned long long*>(hi_range));
   DR_LAUNCH_CHECK();
   return 0;
 }

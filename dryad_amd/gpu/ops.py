@@ -180,6 +180,17 @@ def op_read(op, inputs, v):
         lo, hi = GenProvider().bounds(uri, v.partition)
         if kind == "terasort":
             from ..ops import terasort as TSK
+            if v.world.size == 1 and v.stage.id in getattr(v.runner, "pitch_gen_stages", ()):
+                # only the one-rank fused OrderBy reads this table: records at a 128-byte pitch
+                rows = v.alloc_rows(hi - lo, 100, layout="pitch128")
+                if rows is not None:
+                    t = DeviceTable(hi - lo, Shape("rows", key_off=0, key_len=10), rows=rows)
+                    bs = _pooled_set(t, v)
+                    rng = torch.tensor([-1, 0], dtype=torch.int64, device=rows.device)
+                    TSK.generate_with_keys64_pitch128(bs.bufs.rows_in[: hi - lo], lo, int(q.get("seed", 0)),
+                                                      bs.bufs.ent_a, rng)
+                    bs.keys_ready = (rows.data_ptr(), hi - lo, 0, 10, rng, "e64")
+                    return t
             rows = v.alloc_rows(hi - lo, 100)
             t = DeviceTable(hi - lo, Shape("rows", key_off=0, key_len=10), rows=rows)
             bs = _pooled_set(t, v)
@@ -410,6 +421,18 @@ def op_sort(op, inputs, v):
     if t.n <= 1:
         return t
     bs = _pooled_set(t, v)
+    if bs is not None and bs.layout == "pitch128":
+        # records at a 128-byte pitch (op_read of a one-rank gen://terasort -> OrderBy stage)
+        kind, spec = TR.key_columns(TR.call(op["key"], t), t)
+        if op.get("comparer") is None and not op.get("descending", False) and kind == "bytes" and spec.length <= 16:
+            kr = bs.take_keys(t.rows, spec.off, spec.length)
+            info = {}
+            out = S.sort_rows_pitch128(bs.bufs.rows_in[: t.n], bs.bufs.rows_out, bs.bufs.ent_a, spec.off,
+                                       spec.length, keys_ready=kr is not None and kr[2] == "e64", stats=info)
+            if v.runner is not None:
+                v.runner.last_sort_path = info.get("path")
+            return DeviceTable(out.shape[0], t.shape, rows=out)
+        bs = None                                   # any other sort of such a table: generic path
     if bs is not None and op.get("comparer") is None:
         # in-place key-pointer sort of pooled rows: rows_in -> rows_out, entries in the pool
         kind, spec = TR.key_columns(TR.call(op["key"], t), t)

@@ -17,9 +17,14 @@ from ..ops import recordsort as RS
 
 
 class BufferSet:
-    def __init__(self, bufs: RS.SortBuffers, stride: int):
+    def __init__(self, bufs: RS.SortBuffers, stride: int, layout: str = "plain"):
         self.bufs = bufs
         self.stride = stride
+        # "plain": rows_in [cap, stride], rows_out [cap, stride], two E128 entry arrays.
+        # "pitch128": rows_in [cap, 128] (records of `stride` <= 128 bytes, one aligned HBM line
+        # each), rows_out [cap, stride], ent_a [cap] int64 compact entries, no ent_b (the radix
+        # sort ping-pongs through rows_out: ops/sort.sort_rows_pitch128)
+        self.layout = layout
         self.pins = 0
         self.in_use = False
         # set by a producer that also wrote rows_in's sort entries into bufs.ent_a:
@@ -62,12 +67,26 @@ class BufferSet:
 RESERVE_BYTES = 2 << 30
 
 
-def working_set_bytes(capacity: int, stride: int) -> int:
+def working_set_bytes(capacity: int, stride: int, layout: str = "plain") -> int:
     cap = int(capacity) + 1024
+    if layout == "pitch128":
+        return cap * (128 + stride + 8)
     return cap * (2 * stride + 32)
 
 
-def check_fits(capacity: int, stride: int, device) -> None:
+def allocate(capacity: int, stride: int, device, layout: str = "plain") -> RS.SortBuffers:
+    if layout == "plain":
+        return RS.SortBuffers.allocate(capacity, stride, device)
+    if layout != "pitch128" or stride > 128:
+        raise ValueError(f"HbmPool: unknown layout {layout!r} for {stride}-byte rows")
+    cap = int(capacity) + 1024
+    return RS.SortBuffers(rows_in=torch.empty((cap, 128), dtype=torch.uint8, device=device),
+                          rows_out=torch.empty((cap, stride), dtype=torch.uint8, device=device),
+                          ent_a=torch.empty(cap, dtype=torch.int64, device=device),
+                          ent_b=torch.empty(0, dtype=torch.int64, device=device))
+
+
+def check_fits(capacity: int, stride: int, device, layout: str = "plain") -> None:
     """Refuse, with a clear error, an in-HBM sort working set (rows in + rows out + two entry
     arrays) that cannot fit this GPU; e.g. 1.25e9 TeraSort rows per GPU need 293 GB of the 309 GB.
     Larger partitions go through the out-of-core OrderBy (ops/extsort.py: ``ExternalSort=True``
@@ -75,7 +94,7 @@ def check_fits(capacity: int, stride: int, device) -> None:
     if device.type != "cuda":
         return
     free, total = torch.cuda.mem_get_info(device)
-    need = working_set_bytes(capacity, stride)
+    need = working_set_bytes(capacity, stride, layout)
     if need + RESERVE_BYTES > free:
         from ..errors import DryadLinqException, ErrorCode
         raise DryadLinqException(
@@ -91,10 +110,11 @@ class HbmPool:
         self.sets: list = []
         self.lock = threading.Lock()
 
-    def acquire(self, capacity: int, stride: int) -> BufferSet:
+    def acquire(self, capacity: int, stride: int, layout: str = "plain") -> BufferSet:
         with self.lock:
             for s in self.sets:
-                if not s.in_use and s.pins == 0 and s.stride == stride and s.capacity >= capacity:
+                if not s.in_use and s.pins == 0 and s.stride == stride and s.layout == layout \
+                        and s.capacity >= capacity:
                     s.in_use = True
                     s.keys_ready = None
                     return s
@@ -102,8 +122,8 @@ class HbmPool:
             keep = [s for s in self.sets if s.in_use or s.pins > 0]
             self.sets = keep
             torch.cuda.empty_cache() if self.device.type == "cuda" else None
-            check_fits(capacity, stride, self.device)
-            s = BufferSet(RS.SortBuffers.allocate(capacity, stride, self.device), stride)
+            check_fits(capacity, stride, self.device, layout)
+            s = BufferSet(allocate(capacity, stride, self.device, layout), stride, layout)
             s.in_use = True
             self.sets.append(s)
             return s

@@ -281,6 +281,10 @@ _lib.register_signatures({
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "dr_gather_fixup": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_u64, c_u32, c_u32, c_u32,
                                        ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "dr_gather_fixup_pitch128": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_u64, c_u32, c_u32,
+                                                c_u32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "dr_rekey64": (ctypes.c_int, [ctypes.c_void_p, c_u32, c_u32, c_u32, c_u32, ctypes.c_void_p, c_u64, ctypes.c_void_p]),
+    "dr_e64_position_window": (ctypes.c_int, [ctypes.c_void_p, c_u64, ctypes.c_void_p]),
 })
 # expected entries per run the compact sort sizes its window for (window = smallest multiple of 8
 # bits, at most 32, with n <= RUN_TARGET64 * 2^window)
@@ -371,3 +375,86 @@ def _hi_range64(e: torch.Tensor) -> tuple[int, int]:
     w = (e >> 32) & 0xFFFFFFFF                 # unsigned window (>> is arithmetic on int64)
     mn, mx = int(w.min().item()), int(w.max().item())
     return mn << 32, mx << 32
+
+
+# ------------------------------------------------------------------------------------------------
+# Rows at a 128-byte pitch.  A table whose 100-byte records each start an aligned 128-byte line
+# (bytes 100..127 padding) costs 28% more bytes to write, but every random row read of the sort's
+# gather is then ONE HBM line instead of ~1.78 (the fetch unit is the whole 128-byte line): at
+# 1e9 rows the gather drops from 57.9 to 43.6 ms and the generator grows from 15.4 to 19.1 ms
+# (profiles/r3/pitch128_ab.log).  Used for gen://terasort tables that only a one-rank OrderBy reads.
+PITCH = 128
+
+
+def gather_fixup_pitch128(rows_p: torch.Tensor, srt: torch.Tensor, out: torch.Tensor, key_off: int, key_len: int,
+                          win: int, flag: torch.Tensor):
+    """gather_fixup from ``rows_p`` ([n, 128] uint8: the first 100 bytes of each row are the record)
+    into ``out`` ([n, 100], back to back)."""
+    n = rows_p.shape[0]
+    if rows_p.shape[1] != PITCH or out.shape[1] != 100 or not rows_p.is_contiguous():
+        raise ValueError("gather_fixup_pitch128: [n, 128] input rows and [n, 100] output rows")
+    _lib.call("dr_gather_fixup_pitch128", ptr(rows_p), ptr(out), ptr(srt), c_u64(n), c_u32(100), c_u32(key_off),
+              c_u32(key_len), 64 - win, ptr(flag), stream_of(rows_p))
+
+
+def rekey64(rows: torch.Tensor, ent: torch.Tensor, key_off: int, key_len: int, P: int) -> torch.Tensor:
+    """ent[i] := key bits [P, P + 32) of row (ent[i] & 0xFFFFFFFF) << 32 | row (rows [m, pitch])."""
+    _lib.require_gpu_tensor(rows, "rekey64")
+    _lib.call("dr_rekey64", ptr(rows), c_u32(rows.shape[1]), c_u32(key_off), c_u32(key_len), c_u32(P), ptr(ent),
+              c_u64(ent.shape[0]), stream_of(rows))
+    return ent
+
+
+def _sort64_into(e: torch.Tensor, tmp: torch.Tensor, win: int) -> torch.Tensor:
+    """sort_entries64 whose result always ends in ``e`` (``tmp`` may alias the gather's output)."""
+    srt = sort_entries64(e, tmp, win)
+    if srt.data_ptr() != e.data_ptr():
+        e.copy_(srt)
+    return e
+
+
+def sort_rows_pitch128(rows_p: torch.Tensor, out: torch.Tensor, keys: torch.Tensor, key_off: int, key_len: int,
+                       keys_ready: bool = True, stats: dict | None = None) -> torch.Tensor:
+    """Stable sort of the records in ``rows_p`` ([n, 128], 100-byte records) by their byte-string
+    key into ``out[:n]`` ([>= n, 100]).  ``keys[:n]``: the rows' compact entries for prefix 0
+    (written by the generator) when ``keys_ready``, else the key is read from the rows.  The radix
+    sort's ping-pong buffer is ``out`` itself (free until the gather), so the working set is rows
+    + output + 8 bytes per row.
+
+    A run of equal 32-bit windows too long for the gather's fix-up (heavily duplicated keys) is
+    resolved exactly without more memory: an LSD chain of compact sorts over every 32-bit window
+    of the key, from the least significant, each window re-read from the rows (``rekey64``),
+    then a gather without fix-up."""
+    n = rows_p.shape[0]
+    if n == 0:
+        return out[:0]
+    if n >= (1 << 32) or key_len > 16 or key_off + key_len > 100:
+        raise ValueError("sort_rows_pitch128: < 2^32 rows, key inside the 100-byte record, <= 16 bytes")
+    tmp = out.view(-1)[: n * 8].view(torch.int64)
+    e = keys[:n]
+    flag = torch.zeros(1, dtype=torch.int32, device=rows_p.device)
+    path = "compact pitch128"
+    if keys_ready and key_off == 0:
+        win = min(window_bits64(n), max(8, ((8 * key_len + 7) // 8) * 8), 32)
+        _sort64_into(e, tmp, win)
+        gather_fixup_pitch128(rows_p, e, out[:n], key_off, key_len, win, flag)
+        path += f" win={win}"
+        chain = int(flag.item()) != 0
+    else:
+        torch.arange(n, out=e)                  # entries = row index; windows come from the rows
+        chain = True
+    if chain:
+        bits = 8 * key_len
+        windows = list(range(max(0, bits - 32), -1, -32))
+        if windows[-1] != 0:
+            windows.append(0)
+        for P in windows:                       # least significant window first
+            rekey64(rows_p, e, key_off, key_len, P)
+            _sort64_into(e, tmp, 32)
+        _lib.call("dr_e64_position_window", ptr(e), c_u64(n), stream_of(e))
+        flag.zero_()
+        gather_fixup_pitch128(rows_p, e, out[:n], key_off, key_len, 32, flag)
+        path += f" + full-key LSD chain over windows {windows}"
+    if stats is not None:
+        stats["path"] = path
+    return out[:n]

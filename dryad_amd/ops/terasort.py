@@ -57,6 +57,18 @@ def generate_with_keys64(out: torch.Tensor, first_index: int, seed: int, keys: t
     return out
 
 
+def generate_with_keys64_pitch128(out: torch.Tensor, first_index: int, seed: int, keys: torch.Tensor,
+                                  hi_range: torch.Tensor | None = None) -> torch.Tensor:
+    """``generate_with_keys64`` with the records at a 128-byte pitch (``out`` [n, 128] uint8, bytes
+    100..127 of each row zero): one aligned HBM line per record (ops/sort.sort_rows_pitch128)."""
+    _lib.require_gpu_tensor(out, "terasort.generate_with_keys64_pitch128")
+    n = out.shape[0]
+    assert out.shape[1] == 128 and keys.numel() >= n and keys.dtype == torch.int64 and keys.is_contiguous()
+    _lib.call("dr_terasort_gen_keys64_pitch128", ptr(out), c_u64(n), c_u64(first_index), c_u64(seed & (2**64 - 1)),
+              ptr(keys), c_u32(0), ptr(hi_range), stream_of(out))
+    return out
+
+
 def check(rows: torch.Tensor, acc: torch.Tensor | None = None) -> torch.Tensor:
     """Accumulate [sum of record hashes mod 2^64, #adjacent order violations] into ``acc``."""
     _lib.require_gpu_tensor(rows, "terasort.check")

@@ -70,15 +70,19 @@ class GpuVertexContext(V.VertexContext):
         """Plain device allocation for a vertex's own (non-row) tables."""
         return torch.empty(shape, dtype=dtype, device=self.device)
 
-    def alloc_rows(self, n, stride):
-        """Large row tables come from the executor's HBM pool (reused across jobs)."""
+    def alloc_rows(self, n, stride, layout="plain"):
+        """Large row tables come from the executor's HBM pool (reused across jobs).  ``layout``
+        "pitch128": the rows live at a 128-byte pitch (a [n, stride] view of [n, 128] rows; only
+        for tables that the one-rank fused OrderBy alone reads, see _pitch_gen_reads)."""
         r = self.runner
         if r is None or r.pool is None or self.device.type != "cuda" or n * stride < (64 << 20):
+            if layout != "plain":
+                return None
             return torch.empty((n, stride), dtype=torch.uint8, device=self.device)
         slack = r.ctx._props.get("ShuffleSlack", 0.01) if self.world.size > 1 else 0.0
-        bs = r.pool.acquire(int(n * (1 + slack)) + 1024, stride)
+        bs = r.pool.acquire(int(n * (1 + slack)) + 1024, stride, layout)
         r.row_sets[(self.stage.id, self.partition)] = bs
-        return bs.bufs.rows_in[:n]
+        return bs.bufs.rows_in[:n] if layout == "plain" else bs.bufs.rows_in[:n, :stride]
 
 
 def _to_objects(x):
@@ -218,6 +222,33 @@ class GpuJobRunner:
                 out.add(x.id)
         return out
 
+    def _pitch_gen_reads(self) -> set:
+        """One rank: stages ``read(gen://terasort) -> sort(ascending byte-string key of <= 16
+        bytes) -> ...`` (the one-rank OrderBy plan).  Their op_read stores the records at a
+        128-byte pitch (one aligned HBM line per record) and op_sort sorts them with
+        ops/sort.sort_rows_pitch128: the sort's random row reads fetch one line per record
+        instead of ~1.78.  ``LineAlignedSortInput=False`` (context property) turns it off."""
+        out = set()
+        if self.world.size != 1 or not self.gpu_ok or not self.ctx._props.get("LineAlignedSortInput", True):
+            return out
+        from ..gpu import trace as TR
+        from ..gpu.table import Shape
+        for x in self.plan.stages:
+            if not (not x.inputs and len(x.ops) >= 2 and x.ops[0]["op"] == "read" and x.ops[1]["op"] == "sort"
+                    and parse_uri(x.ops[0]["uri"])[0] == "gen"
+                    and parse_uri(x.ops[0]["uri"])[1].strip("/") == "terasort"
+                    and x.ops[1].get("comparer") is None and not x.ops[1].get("descending", False)):
+                continue
+            rows = torch.zeros((2, 100), dtype=torch.uint8, device=self.dev)
+            t = DeviceTable(2, Shape("rows", key_off=0, key_len=10), rows=rows)
+            try:
+                kind, spec = TR.key_columns(TR.call(x.ops[1]["key"], t), t)
+            except Exception:  # noqa: BLE001
+                continue
+            if kind == "bytes" and 1 <= spec.length <= 16 and spec.off + spec.length <= 100:
+                out.add(x.id)
+        return out
+
     def _materialize(self, sid: int):
         """Write the records of lazy gen reads of stage sid (its consumers are not fused after all)."""
         for p in range(self.plan.stages[sid].partitions):
@@ -225,6 +256,7 @@ class GpuJobRunner:
             t = self.channels.get((sid, p))
             if bs is not None and bs.lazy_gen is not None and isinstance(t, DeviceTable):
                 bs.materialize(t.n)
+
 
     def _run_fused(self, m, f):
         from ..ops import recordsort as RS
@@ -650,6 +682,7 @@ class GpuJobRunner:
             self.fused.pop(sid, None)
             self.skipped.update(e["skip"])
         self.lazy_gen_stages = self._lazy_gen_reads()
+        self.pitch_gen_stages = self._pitch_gen_reads()
         fused_first = {f["stages"][0]: mid for mid, f in self.fused.items()}
         active_fused = {}
         self.fused_joins = FJ.find(self.plan) if self.gpu_ok else {}
@@ -1190,6 +1223,7 @@ class GpuExecutor(_BaseExecutor):
         self.last_job_dir = job_dir
         self.last_result = res
         self.last_plan = plan
+        self.last_sort_path = getattr(runner, "last_sort_path", None)
         if handle is not None:
             handle.events.extend(res["events"])
         return res
