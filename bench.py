@@ -134,13 +134,16 @@ def main():
                 "env": env,
                 "rehearsal": bool(args.rehearsal),
                 "path": ("out-of-core hybrid external sort (HBM-resident buckets + pinned host DRAM)" if ooc else
-                         "direct" if args.direct else "DryadLINQ query -> GPU executor (fused OrderBy gang stage)"),
+                         "direct" if args.direct else
+                         "DryadLINQ query -> GPU executor (fused OrderBy gang stage)" if world.size > 1 else
+                         "DryadLINQ query -> GPU executor (one stage: read -> compact radix sort + gather -> output)"),
                 # the input read: every record is generated once per step; with one rank into the
                 # HBM input table the local sort gathers from, with several ranks straight into
                 # the all-to-all send buckets (the read stage fused with the range partition)
                 "input": "gen://terasort, generated in the timed step" + (
                     " into the send buckets (read fused with the range partition)" if world.size > 1 and not args.direct
-                    else " into the HBM input table"),
+                    else " into the HBM input table" + ("" if args.direct else
+                                                         " (records at a 128-byte pitch: one aligned HBM line each)")),
             },
         }
         if val is not None and not val["ok"]:
