@@ -1665,6 +1665,231 @@ DR_API int dr_sort_u64_expand(E64* keys, E64* tmp, E128* out, uint64_t n, int be
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Single-histogram LSD sort of E64 entries with decoupled look-back ("onesweep").
+//
+// dr_sort_u64 reads the entries twice per pass: rs_count builds the per-workgroup digit counts of
+// the pass, then rs_scatter_v3 moves them.  A digit's count over the whole array does not depend
+// on the order, so here ONE read (os_hist_kernel) builds the histograms of every pass, and each
+// scatter pass finds a tile's per-digit output offset from the tiles before it instead of from a
+// count matrix:
+//   * tiles (4096 entries) are claimed in order from a per-pass ticket counter, so every tile a
+//     workgroup waits for belongs to a workgroup that is already running;
+//   * a tile publishes its 256 digit counts as 8-byte {tag, value} granules (one agent-scope
+//     atomic store each: the granule is its own flag), first tagged "aggregate of this tile", then,
+//     once its prefix is known, "inclusive prefix up to this tile";
+//   * digit d's thread walks back over the predecessors' granules, adding aggregates, until it
+//     meets an inclusive prefix (tile 0 publishes its inclusive prefix at once).
+// Tags are 2 * (pass + 1) + {0 aggregate, 1 inclusive}; the granules and tickets are zeroed by one
+// memset per call, so a granule left by an earlier pass or call is never taken for this pass's.
+// The ranking inside a tile and the LDS reorder are rs_scatter_v3's.  A spin that outlives
+// kOsSpinLimit polls sets the error word and gives up (the prefix it has summed is a lower bound,
+// so every store stays inside the output); the caller checks that word.
+namespace {
+
+constexpr int kOsItems = 16;
+constexpr int kOsTile = kBlock * kOsItems;
+constexpr int kOsMaxPasses = 8;
+constexpr uint32_t kOsHistGrid = 1024;
+constexpr uint32_t kOsSpinLimit = 1u << 22;
+constexpr uint64_t kOsHeader = 256;            // tickets[8] at 0, error word at 64
+typedef __attribute__((address_space(1))) unsigned long long os_gu64;
+typedef __attribute__((address_space(1))) unsigned int os_gu32;
+
+inline uint64_t os_tiles(uint64_t n) { return (n + kOsTile - 1) / kOsTile; }
+
+// workspace: [header | granules: tiles x 256 u64 | gbase: 8 x 256 u32 | partial hists] (bytes)
+inline uint64_t os_granule_bytes(uint64_t n) { return os_tiles(n) * kBins * 8; }
+inline uint64_t os_workspace_bytes(uint64_t n) {
+  return kOsHeader + os_granule_bytes(n) + (uint64_t)kOsMaxPasses * kBins * 4 +
+         (uint64_t)kOsHistGrid * kOsMaxPasses * kBins * 4;
+}
+
+// partial[g][p][d] = count of digit d of pass p (bits begin_bit + 8p ..) in workgroup g's slice
+__global__ __launch_bounds__(256) void os_hist_kernel(const uint64_t* __restrict__ in, uint64_t n, int begin_bit,
+                                                      int P, uint32_t* __restrict__ partial) {
+  __shared__ uint32_t hist[4][kOsMaxPasses][kBins];
+  const int t = threadIdx.x, w = wave_id();
+  for (int i = t; i < 4 * kOsMaxPasses * kBins; i += kBlock) (&hist[0][0][0])[i] = 0;
+  __syncthreads();
+  const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const uint64_t beg = (uint64_t)blockIdx.x * per;
+  const uint64_t end = beg + per < n ? beg + per : n;
+  uint64_t i = beg + t;
+  for (; i + 7 * kBlock < end; i += 8 * kBlock) {
+    uint64_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = in[i + k * kBlock];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint64_t x = v[k] >> begin_bit;
+      for (int p = 0; p < P; ++p) atomicAdd(&hist[w][p][(x >> (8 * p)) & 0xFF], 1u);
+    }
+  }
+  for (; i < end; i += kBlock) {
+    const uint64_t x = in[i] >> begin_bit;
+    for (int p = 0; p < P; ++p) atomicAdd(&hist[w][p][(x >> (8 * p)) & 0xFF], 1u);
+  }
+  __syncthreads();
+  for (int p = 0; p < P; ++p)
+    partial[((uint64_t)blockIdx.x * kOsMaxPasses + p) * kBins + t] =
+        hist[0][p][t] + hist[1][p][t] + hist[2][p][t] + hist[3][p][t];
+}
+
+// gbase[p][d] = exclusive prefix over digits of pass p's histogram (one workgroup per pass)
+__global__ __launch_bounds__(256) void os_hist_scan_kernel(const uint32_t* __restrict__ partial, uint32_t G,
+                                                           uint32_t* __restrict__ gbase) {
+  __shared__ uint32_t sc[4];
+  const int t = threadIdx.x, p = blockIdx.x;
+  uint32_t s = 0;
+  for (uint32_t g = 0; g < G; ++g) s += partial[((uint64_t)g * kOsMaxPasses + p) * kBins + t];
+  uint32_t total;
+  gbase[p * kBins + t] = block_exclusive_scan256(s, sc, total);
+}
+
+template <int ITEMS>
+__global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__ in, E64* __restrict__ out,
+                                                         uint64_t n, int shift, const uint32_t* __restrict__ gbase,
+                                                         unsigned long long* granules, uint32_t* ticket,
+                                                         uint32_t* err, uint32_t tag_agg) {
+  constexpr int kTile = kBlock * ITEMS;
+  __shared__ E64 stage[kTile];
+  __shared__ uint32_t wcnt[4][kBins];
+  __shared__ unsigned long long wmask[4][kBins];
+  __shared__ uint32_t bstart[kBins];
+  __shared__ uint32_t goff[kBins];
+  __shared__ uint32_t sc[4];
+  __shared__ uint32_t tile_sh;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  if (t == 0) tile_sh = __hip_atomic_fetch_add((os_gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  wmask[0][t] = 0ull; wmask[1][t] = 0ull; wmask[2][t] = 0ull; wmask[3][t] = 0ull;
+  wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+  __syncthreads();
+  const uint32_t tile = tile_sh;                 // the grid has exactly one workgroup per tile
+  const uint64_t base = (uint64_t)tile * kTile;
+  const uint32_t cnt = (uint32_t)((n - base) < (uint64_t)kTile ? (n - base) : kTile);
+  E64 cur[ITEMS];
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+    if (pos < cnt) cur[r] = in[base + pos];
+  }
+  const unsigned long long lanebit = 1ull << l;
+  uint32_t rk[ITEMS], dg[ITEMS];
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+    const bool valid = pos < cnt;
+    const uint32_t d = valid ? digit_of(cur[r], shift) : 0u;
+    if (valid) atomicOr(&wmask[w][d], lanebit);
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long peers = valid ? wmask[w][d] : 0ull;
+    const uint32_t below = popc_below(peers);
+    const uint32_t prior = wcnt[w][d];
+    __builtin_amdgcn_wave_barrier();
+    if (valid && below == 0) {
+      wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      wmask[w][d] = 0ull;
+    }
+    __builtin_amdgcn_wave_barrier();
+    rk[r] = prior + below;
+    dg[r] = d;
+  }
+  __syncthreads();
+  const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+  const uint32_t tot = c0 + c1 + c2 + c3;
+  // publish this tile's count of digit t before anything else, so successors can move past it
+  os_gu64* mine = (os_gu64*)(granules + (uint64_t)tile * kBins + t);
+  const unsigned long long tag_inc = tag_agg + 1u;
+  __hip_atomic_store(mine, ((tile == 0 ? tag_inc : (unsigned long long)tag_agg) << 32) | tot, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
+  uint32_t all;
+  bstart[t] = block_exclusive_scan256(tot, sc, all);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+    if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
+  }
+  // look-back for digit t
+  uint32_t excl = 0;
+  if (tile > 0) {
+    uint64_t j = tile - 1;
+    uint32_t spins = 0;
+    for (;;) {
+      const unsigned long long g = __hip_atomic_load((os_gu64*)(granules + j * kBins + t), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t tag = (uint32_t)(g >> 32);
+      if (tag == (uint32_t)tag_inc) {
+        excl += (uint32_t)g;
+        break;
+      }
+      if (tag == tag_agg) {
+        excl += (uint32_t)g;
+        --j;                                     // tile 0 always publishes an inclusive prefix
+        continue;
+      }
+      if (++spins > kOsSpinLimit) {
+        __hip_atomic_fetch_or((os_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __hip_atomic_store(mine, (tag_inc << 32) | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  goff[t] = gbase[t] + excl;
+  __syncthreads();
+#pragma unroll 4
+  for (uint32_t j = t; j < cnt; j += kBlock) {
+    const E64 v = stage[j];
+    const uint32_t d = digit_of(v, shift);
+    out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+  }
+}
+
+}  // namespace
+
+DR_API uint64_t dr_sort_u64_onesweep_workspace(uint64_t n) { return os_workspace_bytes(n > 0 ? n : 1); }
+
+// Stable LSD sort of E64 entries on bits [begin_bit, end_bit) (multiples of 8, <= 64 bits, at most
+// 8 passes) through one histogram read and one look-back scatter per pass.  `ws` holds
+// dr_sort_u64_onesweep_workspace(n) bytes; its word at byte 64 is non-zero after the call when a
+// look-back gave up (the result is then not sorted; the caller raises).
+DR_API int dr_sort_u64_onesweep(E64* keys, E64* tmp, uint64_t n, int begin_bit, int end_bit, void* ws,
+                                uint64_t ws_bytes, hipStream_t s, int* result_in_tmp) {
+  *result_in_tmp = 0;
+  if (n == 0 || begin_bit >= end_bit) return 0;
+  if (end_bit > 64 || begin_bit < 0 || (begin_bit & 7) || (end_bit & 7)) return (int)hipErrorInvalidValue;
+  if (n >= (1ull << 32) || ws_bytes < os_workspace_bytes(n)) return (int)hipErrorInvalidValue;
+  const int P = (end_bit - begin_bit) / 8;
+  const uint64_t tiles = os_tiles(n);
+  if (tiles >= (1ull << 31)) return (int)hipErrorInvalidValue;
+  uint8_t* w8 = reinterpret_cast<uint8_t*>(ws);
+  uint32_t* tickets = reinterpret_cast<uint32_t*>(w8);
+  uint32_t* err = reinterpret_cast<uint32_t*>(w8 + 64);
+  unsigned long long* granules = reinterpret_cast<unsigned long long*>(w8 + kOsHeader);
+  uint32_t* gbase = reinterpret_cast<uint32_t*>(w8 + kOsHeader + os_granule_bytes(n));
+  uint32_t* partial = gbase + kOsMaxPasses * kBins;
+  hipError_t e = hipMemsetAsync(w8, 0, kOsHeader + os_granule_bytes(n), s);
+  if (e != hipSuccess) return (int)e;
+  const uint32_t G = (uint32_t)(tiles < kOsHistGrid ? tiles : kOsHistGrid);
+  os_hist_kernel<<<G, 256, 0, s>>>(reinterpret_cast<const uint64_t*>(keys), n, begin_bit, P, partial);
+  os_hist_scan_kernel<<<P, 256, 0, s>>>(partial, G, gbase);
+  E64* src = keys;
+  E64* dst = tmp;
+  int flips = 0;
+  for (int p = 0; p < P; ++p) {
+    os_scatter_kernel<kOsItems><<<(unsigned)tiles, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
+                                                                granules, tickets + p, err, 2u * (p + 1));
+    E64* x = src; src = dst; dst = x;
+    flips ^= 1;
+  }
+  DR_LAUNCH_CHECK();
+  *result_in_tmp = flips;
+  return 0;
+}
+
 namespace {
 int g_gather_nt = 1;   // nontemporal output stores (A/B: -1.2% gather time at 1e9 rows, dr_gather_fixup_set_nt)
 }

@@ -302,6 +302,7 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
         pending = keep
     if fixups:
         flags = torch.cat([f for _, _, f in fixups]).tolist()
+        S.onesweep_check(out.device)
         for (a2, z2, _), bad in zip(fixups, flags):
             if bad:     # a run of equal windows too long for the fix-up: full-key sort of the range
                 srt = _sort_keys(bufs.rows_in[a2:z2], bufs.ent_a[a2:z2], bufs.ent_b[a2:z2], key_off, key_len,

@@ -285,6 +285,9 @@ _lib.register_signatures({
                                                 c_u32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "dr_rekey64": (ctypes.c_int, [ctypes.c_void_p, c_u32, c_u32, c_u32, c_u32, ctypes.c_void_p, c_u64, ctypes.c_void_p]),
     "dr_e64_position_window": (ctypes.c_int, [ctypes.c_void_p, c_u64, ctypes.c_void_p]),
+    "dr_sort_u64_onesweep_workspace": (c_u64, [c_u64]),
+    "dr_sort_u64_onesweep": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u64, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_void_p, c_u64, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
 })
 # expected entries per run the compact sort sizes its window for (window = smallest multiple of 8
 # bits, at most 32, with n <= RUN_TARGET64 * 2^window)
@@ -314,12 +317,43 @@ def window_bits64(n: int) -> int:
     return win
 
 
+# E64 sorts of at least this many entries take the single-histogram look-back sort
+# (dr_sort_u64_onesweep: one histogram read for all passes instead of a count read per pass)
+ONESWEEP_MIN = 1 << 62                 # off until measured on the GPU
+_OS_CACHE: dict = {}
+
+
+def _onesweep_workspace(n: int, device) -> torch.Tensor:
+    """Workspace of the look-back sort (granules: 2 KB per 4096-entry tile, ~625 MB at 1.25e9),
+    kept per device and grown on demand."""
+    nbytes = int(_lib.lib().dr_sort_u64_onesweep_workspace(c_u64(max(n, 1))))
+    ws = _OS_CACHE.get(device)
+    if ws is None or ws.numel() < nbytes:
+        _OS_CACHE.pop(device, None)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _OS_CACHE[device] = ws
+    return ws
+
+
+def onesweep_check(device) -> None:
+    """Raise if a look-back of the last single-histogram sort on ``device`` gave up (its error word
+    at byte 64 of the workspace); synchronises with the stream."""
+    ws = _OS_CACHE.get(device)
+    if ws is not None and int(ws[64:68].view(torch.int32).item()) != 0:
+        raise RuntimeError("dr_sort_u64_onesweep: a look-back spin gave up; the sort result is invalid")
+
+
 def sort_entries64(e: torch.Tensor, tmp: torch.Tensor, win: int) -> torch.Tensor:
     """Stable LSD sort of E64 entries on their top ``win`` window bits."""
     n = e.shape[0]
-    ws = _workspace(n, e.device)
     flag = ctypes.c_int(0)
-    _lib.call("dr_sort_u64", ptr(e), ptr(tmp), c_u64(n), 64 - win, 64, ptr(ws), stream_of(e), ctypes.byref(flag))
+    if n >= ONESWEEP_MIN:
+        ws = _onesweep_workspace(n, e.device)
+        _lib.call("dr_sort_u64_onesweep", ptr(e), ptr(tmp), c_u64(n), 64 - win, 64, ptr(ws), c_u64(ws.numel()),
+                  stream_of(e), ctypes.byref(flag))
+    else:
+        ws = _workspace(n, e.device)
+        _lib.call("dr_sort_u64", ptr(e), ptr(tmp), c_u64(n), 64 - win, 64, ptr(ws), stream_of(e), ctypes.byref(flag))
     return tmp[:n] if flag.value else e
 
 
@@ -363,7 +397,9 @@ def sort_rows_compact(rows: torch.Tensor, out: torch.Tensor, ent: torch.Tensor, 
     gather_fixup(rows, srt, out, key_off, key_len, win, flag)
     if stats is not None:
         stats["path"] = f"compact win={win} prefix={P}"
-    if int(flag.item()) != 0:
+    overflow = int(flag.item()) != 0
+    onesweep_check(rows.device)
+    if overflow:
         if stats is not None:
             stats["path"] += " overflow"
         return None
@@ -440,6 +476,7 @@ def sort_rows_pitch128(rows_p: torch.Tensor, out: torch.Tensor, keys: torch.Tens
         gather_fixup_pitch128(rows_p, e, out[:n], key_off, key_len, win, flag)
         path += f" win={win}"
         chain = int(flag.item()) != 0
+        onesweep_check(rows_p.device)
     else:
         torch.arange(n, out=e)                  # entries = row index; windows come from the rows
         chain = True
@@ -454,6 +491,7 @@ def sort_rows_pitch128(rows_p: torch.Tensor, out: torch.Tensor, keys: torch.Tens
         _lib.call("dr_e64_position_window", ptr(e), c_u64(n), stream_of(e))
         flag.zero_()
         gather_fixup_pitch128(rows_p, e, out[:n], key_off, key_len, 32, flag)
+        onesweep_check(rows_p.device)
         path += f" + full-key LSD chain over windows {windows}"
     if stats is not None:
         stats["path"] = path
