@@ -1698,16 +1698,15 @@ typedef __attribute__((address_space(1))) unsigned int os_gu32;
 
 inline uint64_t os_tiles(uint64_t n) { return (n + kOsTile - 1) / kOsTile; }
 
-// workspace: [header | granules: tiles x 256 u64 | gbase: 8 x 256 u32 | partial hists] (bytes)
+// workspace: [header | digit counts: 8 x 256 u32 | granules: tiles x 256 u64] (bytes), all zeroed
+// per call
+constexpr uint64_t kOsCounts = (uint64_t)kOsMaxPasses * kBins * 4;
 inline uint64_t os_granule_bytes(uint64_t n) { return os_tiles(n) * kBins * 8; }
-inline uint64_t os_workspace_bytes(uint64_t n) {
-  return kOsHeader + os_granule_bytes(n) + (uint64_t)kOsMaxPasses * kBins * 4 +
-         (uint64_t)kOsHistGrid * kOsMaxPasses * kBins * 4;
-}
+inline uint64_t os_workspace_bytes(uint64_t n) { return kOsHeader + kOsCounts + os_granule_bytes(n); }
 
-// partial[g][p][d] = count of digit d of pass p (bits begin_bit + 8p ..) in workgroup g's slice
+// counts[p][d] += count of digit d of pass p (bits begin_bit + 8p ..) in this workgroup's slice
 __global__ __launch_bounds__(256) void os_hist_kernel(const uint64_t* __restrict__ in, uint64_t n, int begin_bit,
-                                                      int P, uint32_t* __restrict__ partial) {
+                                                      int P, uint32_t* counts) {
   __shared__ uint32_t hist[4][kOsMaxPasses][kBins];
   const int t = threadIdx.x, w = wave_id();
   for (int i = t; i < 4 * kOsMaxPasses * kBins; i += kBlock) (&hist[0][0][0])[i] = 0;
@@ -1731,27 +1730,44 @@ __global__ __launch_bounds__(256) void os_hist_kernel(const uint64_t* __restrict
     for (int p = 0; p < P; ++p) atomicAdd(&hist[w][p][(x >> (8 * p)) & 0xFF], 1u);
   }
   __syncthreads();
-  for (int p = 0; p < P; ++p)
-    partial[((uint64_t)blockIdx.x * kOsMaxPasses + p) * kBins + t] =
-        hist[0][p][t] + hist[1][p][t] + hist[2][p][t] + hist[3][p][t];
+  for (int p = 0; p < P; ++p) {
+    const uint32_t c = hist[0][p][t] + hist[1][p][t] + hist[2][p][t] + hist[3][p][t];
+    if (c) __hip_atomic_fetch_add((os_gu32*)(counts + p * kBins + t), c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
-// gbase[p][d] = exclusive prefix over digits of pass p's histogram (one workgroup per pass)
-__global__ __launch_bounds__(256) void os_hist_scan_kernel(const uint32_t* __restrict__ partial, uint32_t G,
-                                                           uint32_t* __restrict__ gbase) {
+// counts[p][d] += sum over a range of producer partials part[k][first + p][d] (k < parts; the
+// partials cover the 4 digits of bits [32, 64), the sort the P = 4 - first digits from first)
+__global__ __launch_bounds__(256) void os_hist_parts_kernel(const uint32_t* __restrict__ part, uint32_t parts,
+                                                            int first, uint32_t* counts) {
+  const int t = threadIdx.x;
+  const uint32_t per = (parts + gridDim.x - 1) / gridDim.x;
+  const uint32_t k0 = blockIdx.x * per, k1 = k0 + per < parts ? k0 + per : parts;
+  uint32_t s[4] = {0, 0, 0, 0};
+  for (uint32_t k = k0; k < k1; ++k) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) s[p] += p >= first ? part[((uint64_t)k * 4 + p) * kBins + t] : 0u;
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+    if (p >= first && s[p]) __hip_atomic_fetch_add((os_gu32*)(counts + (p - first) * kBins + t), s[p], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// counts[p][d] := exclusive prefix over the digits of pass p (one workgroup per pass)
+__global__ __launch_bounds__(256) void os_hist_scan_kernel(uint32_t* __restrict__ counts) {
   __shared__ uint32_t sc[4];
   const int t = threadIdx.x, p = blockIdx.x;
-  uint32_t s = 0;
-  for (uint32_t g = 0; g < G; ++g) s += partial[((uint64_t)g * kOsMaxPasses + p) * kBins + t];
   uint32_t total;
-  gbase[p * kBins + t] = block_exclusive_scan256(s, sc, total);
+  const uint32_t ex = block_exclusive_scan256(counts[p * kBins + t], sc, total);
+  counts[p * kBins + t] = ex;
 }
 
-template <int ITEMS>
+template <int ITEMS, int LB>
 __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__ in, E64* __restrict__ out,
                                                          uint64_t n, int shift, const uint32_t* __restrict__ gbase,
                                                          unsigned long long* granules, uint32_t* ticket,
-                                                         uint32_t* err, uint32_t tag_agg) {
+                                                         uint32_t* err, uint32_t tag_agg, uint32_t tiles) {
   constexpr int kTile = kBlock * ITEMS;
   __shared__ E64 stage[kTile];
   __shared__ uint32_t wcnt[4][kBins];
@@ -1761,11 +1777,13 @@ __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__
   __shared__ uint32_t sc[4];
   __shared__ uint32_t tile_sh;
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const unsigned long long tag_inc = tag_agg + 1u;
   if (t == 0) tile_sh = __hip_atomic_fetch_add((os_gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   wmask[0][t] = 0ull; wmask[1][t] = 0ull; wmask[2][t] = 0ull; wmask[3][t] = 0ull;
   wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
   __syncthreads();
   const uint32_t tile = tile_sh;                 // the grid has exactly one workgroup per tile
+  if (tile >= tiles) return;
   const uint64_t base = (uint64_t)tile * kTile;
   const uint32_t cnt = (uint32_t)((n - base) < (uint64_t)kTile ? (n - base) : kTile);
   E64 cur[ITEMS];
@@ -1775,80 +1793,101 @@ __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__
     if (pos < cnt) cur[r] = in[base + pos];
   }
   const unsigned long long lanebit = 1ull << l;
-  uint32_t rk[ITEMS], dg[ITEMS];
+  {
+    uint32_t rk[ITEMS], dg[ITEMS];
 #pragma unroll
-  for (int r = 0; r < ITEMS; ++r) {
-    const uint32_t pos = w * (kTile / 4) + r * 64 + l;
-    const bool valid = pos < cnt;
-    const uint32_t d = valid ? digit_of(cur[r], shift) : 0u;
-    if (valid) atomicOr(&wmask[w][d], lanebit);
-    __builtin_amdgcn_wave_barrier();
-    const unsigned long long peers = valid ? wmask[w][d] : 0ull;
-    const uint32_t below = popc_below(peers);
-    const uint32_t prior = wcnt[w][d];
-    __builtin_amdgcn_wave_barrier();
-    if (valid && below == 0) {
-      wcnt[w][d] = prior + (uint32_t)__popcll(peers);
-      wmask[w][d] = 0ull;
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+      const bool valid = pos < cnt;
+      const uint32_t d = valid ? digit_of(cur[r], shift) : 0u;
+      if (valid) atomicOr(&wmask[w][d], lanebit);
+      __builtin_amdgcn_wave_barrier();
+      const unsigned long long peers = valid ? wmask[w][d] : 0ull;
+      const uint32_t below = popc_below(peers);
+      const uint32_t prior = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) {
+        wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+        wmask[w][d] = 0ull;
+      }
+      __builtin_amdgcn_wave_barrier();
+      rk[r] = prior + below;
+      dg[r] = d;
     }
-    __builtin_amdgcn_wave_barrier();
-    rk[r] = prior + below;
-    dg[r] = d;
-  }
-  __syncthreads();
-  const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
-  const uint32_t tot = c0 + c1 + c2 + c3;
-  // publish this tile's count of digit t before anything else, so successors can move past it
-  os_gu64* mine = (os_gu64*)(granules + (uint64_t)tile * kBins + t);
-  const unsigned long long tag_inc = tag_agg + 1u;
-  __hip_atomic_store(mine, ((tile == 0 ? tag_inc : (unsigned long long)tag_agg) << 32) | tot, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-  wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
-  uint32_t all;
-  bstart[t] = block_exclusive_scan256(tot, sc, all);
-  __syncthreads();
+    __syncthreads();
+    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    // publish this tile's count of digit t before anything else, so successors can move past it
+    os_gu64* mine = (os_gu64*)(granules + (uint64_t)tile * kBins + t);
+    __hip_atomic_store(mine, ((tile == 0 ? tag_inc : (unsigned long long)tag_agg) << 32) | tot, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
+    uint32_t all;
+    bstart[t] = block_exclusive_scan256(tot, sc, all);
+    __syncthreads();
 #pragma unroll
-  for (int r = 0; r < ITEMS; ++r) {
-    const uint32_t pos = w * (kTile / 4) + r * 64 + l;
-    if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
-  }
-  // look-back for digit t
-  uint32_t excl = 0;
-  if (tile > 0) {
-    uint64_t j = tile - 1;
-    uint32_t spins = 0;
-    for (;;) {
-      const unsigned long long g = __hip_atomic_load((os_gu64*)(granules + j * kBins + t), __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t tag = (uint32_t)(g >> 32);
-      if (tag == (uint32_t)tag_inc) {
-        excl += (uint32_t)g;
-        break;
-      }
-      if (tag == tag_agg) {
-        excl += (uint32_t)g;
-        --j;                                     // tile 0 always publishes an inclusive prefix
-        continue;
-      }
-      if (++spins > kOsSpinLimit) {
-        __hip_atomic_fetch_or((os_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+      if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
     }
-    __hip_atomic_store(mine, (tag_inc << 32) | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  goff[t] = gbase[t] + excl;
-  __syncthreads();
+    // look-back for digit t: LB predecessors per round trip, nearest first; aggregates
+    // are summed up to the first inclusive prefix, or up to the first granule not yet published
+    // (then that one is polled again)
+    uint32_t excl = 0;
+    if (tile > 0) {
+      uint64_t j = tile;                         // granules of tiles < j are still to be summed
+      uint32_t spins = 0;
+      for (;;) {
+        unsigned long long g[LB];
+#pragma unroll
+        for (int k = 0; k < LB; ++k)
+          g[k] = j >= (uint64_t)k + 1
+                     ? __hip_atomic_load((os_gu64*)(granules + (j - 1 - k) * kBins + t), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT)
+                     : 0ull;
+        bool done = false;
+        int used = 0;
+#pragma unroll
+        for (int k = 0; k < LB; ++k) {
+          if (done || used < k) continue;        // stopped at an earlier granule
+          const uint32_t tag = (uint32_t)(g[k] >> 32);
+          if (tag == (uint32_t)tag_inc) {
+            excl += (uint32_t)g[k];
+            done = true;
+          } else if (tag == tag_agg) {
+            excl += (uint32_t)g[k];
+            used = k + 1;
+          }
+        }
+        if (done) break;
+        j -= (uint64_t)used;                     // tile 0 always publishes an inclusive prefix
+        if (used == 0) {
+          if (++spins > kOsSpinLimit) {
+            __hip_atomic_fetch_or((os_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __hip_atomic_store(mine, (tag_inc << 32) | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    goff[t] = gbase[t] + excl;
+    __syncthreads();
 #pragma unroll 4
-  for (uint32_t j = t; j < cnt; j += kBlock) {
-    const E64 v = stage[j];
-    const uint32_t d = digit_of(v, shift);
-    out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+    for (uint32_t j = t; j < cnt; j += kBlock) {
+      const E64 v = stage[j];
+      const uint32_t d = digit_of(v, shift);
+      out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+    }
   }
 }
 
 }  // namespace
+
+namespace {
+int g_os_lookback = 4;   // predecessor granules per look-back round trip (4; 8 for the A/B: slower)
+}
+DR_API void dr_sort64_onesweep_set_lookback(int lb) { g_os_lookback = lb == 8 ? 8 : 4; }
 
 DR_API uint64_t dr_sort_u64_onesweep_workspace(uint64_t n) { return os_workspace_bytes(n > 0 ? n : 1); }
 
@@ -1856,8 +1895,12 @@ DR_API uint64_t dr_sort_u64_onesweep_workspace(uint64_t n) { return os_workspace
 // 8 passes) through one histogram read and one look-back scatter per pass.  `ws` holds
 // dr_sort_u64_onesweep_workspace(n) bytes; its word at byte 64 is non-zero after the call when a
 // look-back gave up (the result is then not sorted; the caller raises).
+// hist_part (nullable; sorts of bits [32 + 8k, 64) only): `parts` per-workgroup [4][256]
+// histograms of the digits of bits [32, 64) the producer of the entries wrote
+// (dr_terasort_gen_keys64_pitch128), used instead of the histogram read.
 DR_API int dr_sort_u64_onesweep(E64* keys, E64* tmp, uint64_t n, int begin_bit, int end_bit, void* ws,
-                                uint64_t ws_bytes, hipStream_t s, int* result_in_tmp) {
+                                uint64_t ws_bytes, const uint32_t* hist_part, uint32_t parts, hipStream_t s,
+                                int* result_in_tmp) {
   *result_in_tmp = 0;
   if (n == 0 || begin_bit >= end_bit) return 0;
   if (end_bit > 64 || begin_bit < 0 || (begin_bit & 7) || (end_bit & 7)) return (int)hipErrorInvalidValue;
@@ -1868,20 +1911,30 @@ DR_API int dr_sort_u64_onesweep(E64* keys, E64* tmp, uint64_t n, int begin_bit, 
   uint8_t* w8 = reinterpret_cast<uint8_t*>(ws);
   uint32_t* tickets = reinterpret_cast<uint32_t*>(w8);
   uint32_t* err = reinterpret_cast<uint32_t*>(w8 + 64);
-  unsigned long long* granules = reinterpret_cast<unsigned long long*>(w8 + kOsHeader);
-  uint32_t* gbase = reinterpret_cast<uint32_t*>(w8 + kOsHeader + os_granule_bytes(n));
-  uint32_t* partial = gbase + kOsMaxPasses * kBins;
-  hipError_t e = hipMemsetAsync(w8, 0, kOsHeader + os_granule_bytes(n), s);
+  uint32_t* gbase = reinterpret_cast<uint32_t*>(w8 + kOsHeader);
+  unsigned long long* granules = reinterpret_cast<unsigned long long*>(w8 + kOsHeader + kOsCounts);
+  hipError_t e = hipMemsetAsync(w8, 0, os_workspace_bytes(n), s);
   if (e != hipSuccess) return (int)e;
-  const uint32_t G = (uint32_t)(tiles < kOsHistGrid ? tiles : kOsHistGrid);
-  os_hist_kernel<<<G, 256, 0, s>>>(reinterpret_cast<const uint64_t*>(keys), n, begin_bit, P, partial);
-  os_hist_scan_kernel<<<P, 256, 0, s>>>(partial, G, gbase);
+  if (hist_part) {
+    if (begin_bit < 32 || end_bit != 64 || parts == 0) return (int)hipErrorInvalidValue;
+    os_hist_parts_kernel<<<parts < 256 ? parts : 256, 256, 0, s>>>(hist_part, parts, (begin_bit - 32) / 8, gbase);
+  } else {
+    const uint32_t G = (uint32_t)(tiles < kOsHistGrid ? tiles : kOsHistGrid);
+    os_hist_kernel<<<G, 256, 0, s>>>(reinterpret_cast<const uint64_t*>(keys), n, begin_bit, P, gbase);
+  }
+  os_hist_scan_kernel<<<P, 256, 0, s>>>(gbase);
   E64* src = keys;
   E64* dst = tmp;
   int flips = 0;
   for (int p = 0; p < P; ++p) {
-    os_scatter_kernel<kOsItems><<<(unsigned)tiles, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
-                                                                granules, tickets + p, err, 2u * (p + 1));
+    if (g_os_lookback == 8)
+      os_scatter_kernel<kOsItems, 8><<<(unsigned)tiles, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
+                                                                    granules, tickets + p, err, 2u * (p + 1),
+                                                                    (uint32_t)tiles);
+    else
+      os_scatter_kernel<kOsItems, 4><<<(unsigned)tiles, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
+                                                                    granules, tickets + p, err, 2u * (p + 1),
+                                                                    (uint32_t)tiles);
     E64* x = src; src = dst; dst = x;
     flips ^= 1;
   }

@@ -28,11 +28,21 @@ using dr_ts::ts_record;
 // sort (key bits 0..31 in the high word: the window for a zero common prefix).
 // PITCH: 32-bit words per stored row: 25 (100-byte rows back to back) or 32 (one row per aligned
 // 128-byte line, bytes 100..127 zero: the HBM line a random row read fetches holds exactly that row).
-template <int KEYS, bool ROWS = true, int PITCH = 25>
+// HIST (KEYS == 2): also the histograms of the four window bytes (the digits of the compact sort's
+// four LSD passes), one [4][256] partial per workgroup in hist_part, so that sort needs no
+// histogram read of its own (dr_sort_u64_onesweep with hist_part).
+template <int KEYS, bool ROWS = true, int PITCH = 25, bool HIST = false>
 __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out, uint64_t n, uint64_t first,
                                                      uint64_t seed, void* __restrict__ keys, uint32_t idx_base,
-                                                     unsigned long long* __restrict__ hi_range) {
+                                                     unsigned long long* __restrict__ hi_range,
+                                                     uint32_t* __restrict__ hist_part = nullptr) {
   __shared__ __attribute__((aligned(16))) uint32_t img[256 * 25];
+  __shared__ uint32_t hist[HIST ? 4 : 1][256];
+  if constexpr (HIST) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) hist[p][threadIdx.x] = 0;
+    __syncthreads();
+  }
   uint64_t mn = ~0ull, mx = 0;
   for (uint64_t row0 = (uint64_t)blockIdx.x * 256; row0 < n; row0 += (uint64_t)gridDim.x * 256) {
     const uint32_t rows = (uint32_t)((n - row0) < 256 ? (n - row0) : 256);
@@ -53,6 +63,10 @@ __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out,
           static_cast<E128*>(keys)[row0 + threadIdx.x] = e;
         } else {
           static_cast<uint64_t*>(keys)[row0 + threadIdx.x] = (hi & 0xFFFFFFFF00000000ull) | idx;
+          if constexpr (HIST) {
+#pragma unroll
+            for (int p = 0; p < 4; ++p) atomicAdd(&hist[p][(uint32_t)(hi >> (32 + 8 * p)) & 0xFF], 1u);
+          }
         }
         mn = hi < mn ? hi : mn;
         mx = hi > mx ? hi : mx;
@@ -85,6 +99,11 @@ __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out,
       for (uint32_t j = threadIdx.x; j < words; j += 256) o[j] = img[j];
     }
     __syncthreads();
+  }
+  if constexpr (HIST) {
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 4; ++p) hist_part[((uint64_t)blockIdx.x * 4 + p) * 256 + threadIdx.x] = hist[p][threadIdx.x];
   }
   if (KEYS && hi_range) {
 #pragma unroll
@@ -171,14 +190,23 @@ DR_API int dr_terasort_gen_keys64(uint8_t* out, uint64_t n, uint64_t first_index
 }
 
 // Same with the records at a 128-byte pitch (out: n x 128 bytes, bytes 100..127 of each row zero).
+// hist_part (nullable): [dr_terasort_gen_hist_parts(n)][4][256] uint32 per-workgroup histograms of
+// the four window bytes of the entries.
+DR_API uint32_t dr_terasort_gen_hist_parts(uint64_t n) { return grid_for(n, 256, 16384); }
+
 DR_API int dr_terasort_gen_keys64_pitch128(uint8_t* out, uint64_t n, uint64_t first_index, uint64_t seed, E64* keys,
-                                           uint32_t idx_base, uint64_t* hi_range, hipStream_t s) {
+                                           uint32_t idx_base, uint64_t* hi_range, uint32_t* hist_part, hipStream_t s) {
   if (n == 0) return 0;
   if (n + idx_base > (1ull << 32)) return (int)hipErrorInvalidValue;
   if (reinterpret_cast<uintptr_t>(out) & 15) return (int)hipErrorInvalidValue;
-  ts_gen_kernel<2, true, 32><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index,
-                                                                     seed, keys, idx_base,
-                                                                     reinterpret_cast<unsigned long long*>(hi_range));
+  const unsigned g = grid_for(n, 256, 16384);
+  if (hist_part)
+    ts_gen_kernel<2, true, 32, true><<<g, 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index, seed, keys,
+                                                       idx_base, reinterpret_cast<unsigned long long*>(hi_range),
+                                                       hist_part);
+  else
+    ts_gen_kernel<2, true, 32><<<g, 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index, seed, keys,
+                                                 idx_base, reinterpret_cast<unsigned long long*>(hi_range));
   DR_LAUNCH_CHECK();
   return 0;
 }

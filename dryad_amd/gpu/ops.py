@@ -188,7 +188,7 @@ def op_read(op, inputs, v):
                     bs = _pooled_set(t, v)
                     rng = torch.tensor([-1, 0], dtype=torch.int64, device=rows.device)
                     TSK.generate_with_keys64_pitch128(bs.bufs.rows_in[: hi - lo], lo, int(q.get("seed", 0)),
-                                                      bs.bufs.ent_a, rng)
+                                                      bs.bufs.ent_a, rng, hist=True)
                     bs.keys_ready = (rows.data_ptr(), hi - lo, 0, 10, rng, "e64")
                     return t
             rows = v.alloc_rows(hi - lo, 100)

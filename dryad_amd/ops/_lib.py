@@ -42,7 +42,8 @@ _SIGS = {
     "dr_terasort_check": (c_i32, [vp, c_u64, vp, vp]),
     "dr_terasort_gen_keys": (c_i32, [vp, c_u64, c_u64, c_u64, vp, c_u32, vp, vp]),
     "dr_terasort_gen_keys64": (c_i32, [vp, c_u64, c_u64, c_u64, vp, c_u32, vp, vp]),
-    "dr_terasort_gen_keys64_pitch128": (c_i32, [vp, c_u64, c_u64, c_u64, vp, c_u32, vp, vp]),
+    "dr_terasort_gen_keys64_pitch128": (c_i32, [vp, c_u64, c_u64, c_u64, vp, c_u32, vp, vp, vp]),
+    "dr_terasort_gen_hist_parts": (c_u32, [c_u64]),
     "dr_terasort_gen_keys_only": (c_i32, [c_u64, c_u64, c_u64, vp, c_u32, vp, vp]),
     "dr_tie_fixup": (c_i32, [vp, c_u64, c_u32, vp, vp]),
     "dr_sort_set_items": (None, [c_i32]),

@@ -287,7 +287,8 @@ _lib.register_signatures({
     "dr_e64_position_window": (ctypes.c_int, [ctypes.c_void_p, c_u64, ctypes.c_void_p]),
     "dr_sort_u64_onesweep_workspace": (c_u64, [c_u64]),
     "dr_sort_u64_onesweep": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u64, ctypes.c_int, ctypes.c_int,
-                                            ctypes.c_void_p, c_u64, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
+                                            ctypes.c_void_p, c_u64, ctypes.c_void_p, c_u32, ctypes.c_void_p,
+                                            ctypes.POINTER(ctypes.c_int)]),
 })
 # expected entries per run the compact sort sizes its window for (window = smallest multiple of 8
 # bits, at most 32, with n <= RUN_TARGET64 * 2^window)
@@ -319,7 +320,7 @@ def window_bits64(n: int) -> int:
 
 # E64 sorts of at least this many entries take the single-histogram look-back sort
 # (dr_sort_u64_onesweep: one histogram read for all passes instead of a count read per pass)
-ONESWEEP_MIN = 1 << 62                 # off until measured on the GPU
+ONESWEEP_MIN = 1 << 20
 _OS_CACHE: dict = {}
 
 
@@ -343,14 +344,44 @@ def onesweep_check(device) -> None:
         raise RuntimeError("dr_sort_u64_onesweep: a look-back spin gave up; the sort result is invalid")
 
 
-def sort_entries64(e: torch.Tensor, tmp: torch.Tensor, win: int) -> torch.Tensor:
-    """Stable LSD sort of E64 entries on their top ``win`` window bits."""
+_GEN_HIST: dict = {}
+
+
+def gen_hist_buffer(parts: int, device) -> torch.Tensor:
+    """Per-workgroup [4][256] window-digit histograms a producer of E64 entries writes (uint32)."""
+    buf = _OS_CACHE.get(("gen_hist", device))
+    if buf is None or buf.numel() < parts * 1024:
+        buf = torch.empty(parts * 1024, dtype=torch.int32, device=device)
+        _OS_CACHE[("gen_hist", device)] = buf
+    return buf[: parts * 1024]
+
+
+def note_gen_hist(keys: torch.Tensor, n: int, part: torch.Tensor | None) -> None:
+    """Record that ``part`` holds the window histograms of ``keys[:n]`` (None: forget any)."""
+    if part is None:
+        _GEN_HIST.pop(keys.device, None)
+    else:
+        _GEN_HIST[keys.device] = (keys.data_ptr(), n, part)
+
+
+def take_gen_hist(e: torch.Tensor):
+    """The producer histograms of the entries ``e`` if they are still the generated ones (one use)."""
+    h = _GEN_HIST.pop(e.device, None)
+    if h is not None and h[0] == e.data_ptr() and h[1] == e.shape[0]:
+        return h[2]
+    return None
+
+
+def sort_entries64(e: torch.Tensor, tmp: torch.Tensor, win: int, gen_hist: torch.Tensor | None = None) -> torch.Tensor:
+    """Stable LSD sort of E64 entries on their top ``win`` window bits.  ``gen_hist``: the window
+    digit histograms of ``e``'s 32-bit key window written by its producer (take_gen_hist)."""
     n = e.shape[0]
     flag = ctypes.c_int(0)
     if n >= ONESWEEP_MIN:
         ws = _onesweep_workspace(n, e.device)
+        parts = 0 if gen_hist is None else gen_hist.numel() // 1024
         _lib.call("dr_sort_u64_onesweep", ptr(e), ptr(tmp), c_u64(n), 64 - win, 64, ptr(ws), c_u64(ws.numel()),
-                  stream_of(e), ctypes.byref(flag))
+                  ptr(gen_hist), c_u32(parts), stream_of(e), ctypes.byref(flag))
     else:
         ws = _workspace(n, e.device)
         _lib.call("dr_sort_u64", ptr(e), ptr(tmp), c_u64(n), 64 - win, 64, ptr(ws), stream_of(e), ctypes.byref(flag))
@@ -441,9 +472,9 @@ def rekey64(rows: torch.Tensor, ent: torch.Tensor, key_off: int, key_len: int, P
     return ent
 
 
-def _sort64_into(e: torch.Tensor, tmp: torch.Tensor, win: int) -> torch.Tensor:
+def _sort64_into(e: torch.Tensor, tmp: torch.Tensor, win: int, gen_hist=None) -> torch.Tensor:
     """sort_entries64 whose result always ends in ``e`` (``tmp`` may alias the gather's output)."""
-    srt = sort_entries64(e, tmp, win)
+    srt = sort_entries64(e, tmp, win, gen_hist)
     if srt.data_ptr() != e.data_ptr():
         e.copy_(srt)
     return e
@@ -468,11 +499,14 @@ def sort_rows_pitch128(rows_p: torch.Tensor, out: torch.Tensor, keys: torch.Tens
         raise ValueError("sort_rows_pitch128: < 2^32 rows, key inside the 100-byte record, <= 16 bytes")
     tmp = out.view(-1)[: n * 8].view(torch.int64)
     e = keys[:n]
+    gen_hist = take_gen_hist(e) if keys_ready else None
     flag = torch.zeros(1, dtype=torch.int32, device=rows_p.device)
     path = "compact pitch128"
     if keys_ready and key_off == 0:
         win = min(window_bits64(n), max(8, ((8 * key_len + 7) // 8) * 8), 32)
-        _sort64_into(e, tmp, win)
+        _sort64_into(e, tmp, win, gen_hist)
+        if gen_hist is not None and n >= ONESWEEP_MIN:
+            path += " gen-hist"
         gather_fixup_pitch128(rows_p, e, out[:n], key_off, key_len, win, flag)
         path += f" win={win}"
         chain = int(flag.item()) != 0

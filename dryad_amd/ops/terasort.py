@@ -58,14 +58,22 @@ def generate_with_keys64(out: torch.Tensor, first_index: int, seed: int, keys: t
 
 
 def generate_with_keys64_pitch128(out: torch.Tensor, first_index: int, seed: int, keys: torch.Tensor,
-                                  hi_range: torch.Tensor | None = None) -> torch.Tensor:
+                                  hi_range: torch.Tensor | None = None, hist: bool = False) -> torch.Tensor:
     """``generate_with_keys64`` with the records at a 128-byte pitch (``out`` [n, 128] uint8, bytes
-    100..127 of each row zero): one aligned HBM line per record (ops/sort.sort_rows_pitch128)."""
+    100..127 of each row zero): one aligned HBM line per record (ops/sort.sort_rows_pitch128).
+    ``hist``: the generator also writes the digit histograms of the entries' key window, handed to
+    the sort of ``keys[:n]`` (ops/sort.take_gen_hist) so that it skips its histogram read."""
+    from . import sort as S
     _lib.require_gpu_tensor(out, "terasort.generate_with_keys64_pitch128")
     n = out.shape[0]
     assert out.shape[1] == 128 and keys.numel() >= n and keys.dtype == torch.int64 and keys.is_contiguous()
+    part = None
+    if hist and n >= S.ONESWEEP_MIN:
+        parts = int(_lib.lib().dr_terasort_gen_hist_parts(c_u64(n)))
+        part = S.gen_hist_buffer(parts, out.device)
     _lib.call("dr_terasort_gen_keys64_pitch128", ptr(out), c_u64(n), c_u64(first_index), c_u64(seed & (2**64 - 1)),
-              ptr(keys), c_u32(0), ptr(hi_range), stream_of(out))
+              ptr(keys), c_u32(0), ptr(hi_range), ptr(part), stream_of(out))
+    S.note_gen_hist(keys, n, part)
     return out
 
 

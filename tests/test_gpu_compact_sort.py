@@ -113,7 +113,7 @@ def _sort64_both(ent: torch.Tensor, win: int):
     ws = S._onesweep_workspace(n, ent.device)
     from dryad_amd.ops import _lib
     _lib.call("dr_sort_u64_onesweep", S.ptr(a), S.ptr(ta), S.c_u64(n), 64 - win, 64, S.ptr(ws), S.c_u64(ws.numel()),
-              S.stream_of(a), __import__("ctypes").byref(flag))
+              None, S.c_u32(0), S.stream_of(a), __import__("ctypes").byref(flag))
     ra = ta if flag.value else a
     b, tb = ent.clone(), torch.empty_like(ent)
     wsb = S._workspace(n, ent.device)
@@ -144,3 +144,42 @@ def test_onesweep_sort64_matches_stable_reference(n, win, kind):
     ref = ent.cpu()[order]
     assert torch.equal(ra.cpu(), ref)
     assert torch.equal(rb.cpu(), ref)
+
+
+def test_onesweep_lookback8_variant_matches():
+    """The 8-granule look-back of the single-histogram sort (A/B only) sorts identically."""
+    from dryad_amd.ops import _lib
+    lib = _lib.lib()
+    lib.dr_sort64_onesweep_set_lookback.argtypes = [__import__("ctypes").c_int]
+    lib.dr_sort64_onesweep_set_lookback.restype = None
+    n = (1 << 21) + 77
+    g = torch.Generator().manual_seed(3)
+    w = torch.randint(0, 1 << 32, (n,), generator=g, dtype=torch.int64)
+    ent = ((w << 32) | torch.arange(n, dtype=torch.int64)).to(DEV)
+    lib.dr_sort64_onesweep_set_lookback(8)
+    try:
+        ra, rb = _sort64_both(ent, 32)
+    finally:
+        lib.dr_sort64_onesweep_set_lookback(4)
+    assert torch.equal(ra, rb)
+
+
+def test_pitch128_sort_with_generator_histograms():
+    """gen://terasort rows at a 128-byte pitch whose generator also wrote the window histograms:
+    the sort uses them (no histogram read) and orders exactly like the plain path."""
+    n = (1 << 20) + 4097
+    rows = torch.empty((n, 128), dtype=torch.uint8, device=DEV)
+    keys = torch.empty(n, dtype=torch.int64, device=DEV)
+    out_a = torch.empty((n, 100), dtype=torch.uint8, device=DEV)
+    out_b = torch.empty((n, 100), dtype=torch.uint8, device=DEV)
+    TS.generate_with_keys64_pitch128(rows, 0, 99, keys, hist=True)
+    st = {}
+    S.sort_rows_pitch128(rows, out_a, keys, 0, 10, keys_ready=True, stats=st)
+    assert "gen-hist" in st["path"], st
+    TS.generate_with_keys64_pitch128(rows, 0, 99, keys, hist=False)
+    st2 = {}
+    S.sort_rows_pitch128(rows, out_b, keys, 0, 10, keys_ready=True, stats=st2)
+    assert "gen-hist" not in st2["path"], st2
+    assert torch.equal(out_a, out_b)
+    chk = TS.check(out_a)
+    assert int(chk[1]) == 0

@@ -49,13 +49,24 @@ def main():
         _lib.call("dr_sort_u64", S.ptr(ent), S.ptr(tmp), S.c_u64(n), 32, 64, S.ptr(ws_old), S.stream_of(ent),
                   ctypes.byref(flag))
 
+    lib = _lib.lib()
+    lib.dr_sort64_onesweep_set_lookback.argtypes = [ctypes.c_int]
+    lib.dr_sort64_onesweep_set_lookback.restype = None
+
     def new():
+        lib.dr_sort64_onesweep_set_lookback(4)
         _lib.call("dr_sort_u64_onesweep", S.ptr(ent), S.ptr(tmp), S.c_u64(n), 32, 64, S.ptr(ws_os),
-                  S.c_u64(ws_os.numel()), S.stream_of(ent), ctypes.byref(flag))
+                  S.c_u64(ws_os.numel()), None, S.c_u32(0), S.stream_of(ent), ctypes.byref(flag))
+
+    def new_lb8():
+        lib.dr_sort64_onesweep_set_lookback(8)
+        _lib.call("dr_sort_u64_onesweep", S.ptr(ent), S.ptr(tmp), S.c_u64(n), 32, 64, S.ptr(ws_os),
+                  S.c_u64(ws_os.numel()), None, S.c_u32(0), S.stream_of(ent), ctypes.byref(flag))
+        lib.dr_sort64_onesweep_set_lookback(4)
 
     results = {}
     for rnd in range(2):
-        for name, fn in (("count+scatter", old), ("onesweep", new)):
+        for name, fn in (("count+scatter", old), ("onesweep", new), ("onesweep-lb8", new_lb8)):
             def run():
                 ent.copy_(base)
                 fn()
@@ -69,7 +80,8 @@ def main():
                   f"copy {cmed:.2f})", flush=True)
             del res
     S.onesweep_check(base.device)
-    same = torch.equal(results["count+scatter"], results["onesweep"])
+    same = torch.equal(results["count+scatter"], results["onesweep"]) and \
+        torch.equal(results["count+scatter"], results["onesweep-lb8"])
     w = (results["onesweep"] >> 32) & 0xFFFFFFFF
     ordered = bool((w[1:] >= w[:-1]).all())
     print(f"n={n} identical={same} ordered={ordered}", flush=True)

@@ -35,7 +35,7 @@ def main():
     lib = _lib.lib()
     lib.dr_terasort_gen_keys64_pitch128.restype = ctypes.c_int
     lib.dr_terasort_gen_keys64_pitch128.argtypes = [ctypes.c_void_p, c_u64, c_u64, c_u64, ctypes.c_void_p, c_u32,
-                                                   ctypes.c_void_p, ctypes.c_void_p]
+                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.dr_gather_fixup_pitch128.restype = ctypes.c_int
     lib.dr_gather_fixup_pitch128.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_u64, c_u32, c_u32,
                                             c_u32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
@@ -46,7 +46,7 @@ def main():
         # (workgroup b of the 16384-workgroup grid-stride gather runs on XCD b % 8, chunk c on b = c % 16384)
         rows_p = buf.view(n, 128)
         _lib.check(lib.dr_terasort_gen_keys64_pitch128(ptr(rows_p), c_u64(n), c_u64(0), c_u64(7), ptr(keys), c_u32(0),
-                                                       None, stream_of(buf)), "gen pitch128")
+                                                       None, None, stream_of(buf)), "gen pitch128")
         pos = out.view(-1)[: n * 8].view(torch.int64)          # scratch (the gather overwrites it)
         blk = n // 8
         for mode in ("random", "xcd-local", "random", "xcd-local"):
@@ -79,7 +79,7 @@ def main():
                 continue
             rows_m = buf[: m * 128].view(m, 128)
             _lib.check(lib.dr_terasort_gen_keys64_pitch128(ptr(rows_m), c_u64(m), c_u64(0), c_u64(7), ptr(keys),
-                                                           c_u32(0), None, stream_of(buf)), "gen pitch128")
+                                                           c_u32(0), None, None, stream_of(buf)), "gen pitch128")
             srt = S.sort_entries64(keys[:m], tmp[:m], 32)
             best = None
             for _ in range(3):
@@ -104,7 +104,7 @@ def main():
         else:
             rows = buf.view(n, 128)
             _lib.check(lib.dr_terasort_gen_keys64_pitch128(ptr(buf), c_u64(n), c_u64(0), c_u64(7), ptr(keys), c_u32(0),
-                                                           None, stream_of(buf)), "gen pitch128")
+                                                           None, None, stream_of(buf)), "gen pitch128")
         ev[1].record()
         srt = S.sort_entries64(keys, tmp, 32)
         ev[2].record()
