@@ -183,3 +183,4 @@ def test_pitch128_sort_with_generator_histograms():
     assert torch.equal(out_a, out_b)
     chk = TS.check(out_a)
     assert int(chk[1]) == 0
+
