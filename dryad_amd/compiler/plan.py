@@ -34,6 +34,8 @@ class StageInput:
     offset: int = 0
     merge_sort: dict | None = None      # k-way merge of sorted source ports: {key, comparer, descending}
     group: int = 0                      # kind "group": partition j reads source partitions [j*g, (j+1)*g)
+    dynamic: bool = False               # kind "group": regroup by the sources' output sizes at run time
+                                        # (runtime/aggmanager.py; the static groups are the fallback)
 
     def to_json(self):
         d = {"UniqueId": self.src, "ConnectionOperator": {"pointwise": "Pointwise", "cross": "CrossProduct",
@@ -46,6 +48,8 @@ class StageInput:
             d["MergeSort"] = True
         if self.group:
             d["GroupSize"] = self.group
+        if self.dynamic:
+            d["DynamicManager"] = "PartialAggregator"
         return d
 
 

@@ -565,14 +565,17 @@ class Planner:
         """Aggregation tree (reference DrDynamicAggregateManager, GraphBuilder.cs:633-703;
         DryadLinqApplication.cs:173-175: at most 150 inputs per aggregation vertex, groups of
         32): while more partials than the fan-in limit would meet in one merge vertex, insert a
-        level of combine vertices, each folding one group of partials into one partial."""
+        level of combine vertices, each folding one group of partials into one partial.  The
+        groups are dynamic: the process executor regroups the partials by their actual output sizes
+        against ``AggregateThreshold`` once they exist (runtime/aggmanager.py); the static groups
+        of ``AggregationTreeGroup`` bound the number of combine vertices."""
         max_in = int(self.ctx._props.get("AggregationTreeMaxInputs") or 150)
         group = int(self.ctx._props.get("AggregationTreeGroup") or 32)
         level = 0
         while partial.partitions > max_in and group > 1:
             level += 1
             n = -(-partial.partitions // group)
-            partial = self._new(f"{kind}Combine", n, [StageInput(partial, "group", group=group)],
+            partial = self._new(f"{kind}Combine", n, [StageInput(partial, "group", group=group, dynamic=True)],
                                 [dict(op="agg_combine", spec=spec, explain=f"{kind} (combine, tree level {level})")],
                                 DataSetInfo(PartitionInfo.random(n)))
         return partial
@@ -762,7 +765,7 @@ class Planner:
             n.id = k
         stages = []
         for n in order:
-            ins = [StageInput(i.src.id, i.kind, i.port, i.offset, i.merge_sort, i.group) for i in n.inputs]
+            ins = [StageInput(i.src.id, i.kind, i.port, i.offset, i.merge_sort, i.group, getattr(i, "dynamic", False)) for i in n.inputs]
             ops = n.ops if n.ops else [dict(op="identity", explain="merge")]
             st = Stage(n.id, n.name, n.partitions, ins, ops, n.out_ports, n.dtype, n.info,
                        dict(n.output) if n.output else None, n.dynamic_manager, explain=list(n.explain), gang=n.gang)

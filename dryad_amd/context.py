@@ -97,6 +97,8 @@ _DEFAULTS = dict(
     DynamicOptLevel=0x1,               # broadcast only (DryadLinqGlobals.cs:43-52)
     AggregationTreeMaxInputs=150,      # aggregation tree: max inputs per vertex (DryadLinqApplication.cs:173-175)
     AggregationTreeGroup=32,           # ... and partials folded per interior vertex
+    AggregateThreshold=1 << 30,        # dynamic aggregation: bytes per combine vertex (the GM's
+                                       # at/aggregatethreshold, DryadLinqApplication.cs:143-175; "512MB" ok)
     HeadNode="localhost",
     DryadHomeDirectory=None,
     PartitionUncPath=None,

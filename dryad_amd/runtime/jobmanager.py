@@ -44,6 +44,8 @@ class JobRunner:
             p.default_outlier_threshold = float(thr)
             p.min_outlier_threshold = min(p.min_outlier_threshold, float(thr))
         self.g = R.JobGraph(p)
+        self.out_bytes: dict = {}     # vid -> bytes written by its accepted version
+        self.dyn_groups: dict = {}    # (stage id, input index) -> source partitions per combine vertex
         self.vids: list[list[int]] = []
         self.inputs_of: dict = {}    # vid -> [[(src_vid, src_port, edge_id), ...] per stage input]
         self.events = []
@@ -75,6 +77,10 @@ class JobRunner:
                     elif si.kind == "offset":
                         q = p - si.offset
                         pairs = [(self.vids[si.src][q], si.port)] if 0 <= q < src_stage.partitions else []
+                    elif si.kind == "group" and getattr(si, "dynamic", False):
+                        # dynamic aggregation: every combine vertex waits for all the partials; which
+                        # of them it reads is decided from their sizes when it is scheduled
+                        pairs = [(v, si.port) for v in self.vids[si.src]]
                     elif si.kind == "group":
                         pairs = [(self.vids[si.src][q], si.port)
                                  for q in range(p * si.group, min(src_stage.partitions, (p + 1) * si.group))]
@@ -103,13 +109,35 @@ class JobRunner:
             return PF.tmp_part_path(base, partition, vid, 0, version)
         return os.path.join(self.job_dir, "out", f"s{stage.id}.p{partition}.v{version}")
 
+    def _dynamic_group(self, stage, ii, part):
+        """Source partitions the combine vertex ``part`` of ``stage`` folds (runtime/aggmanager):
+        decided once per stage input from the partials' sizes, then kept for re-executions."""
+        key = (stage.id, ii)
+        if key not in self.dyn_groups:
+            from .aggmanager import assign_groups, parse_size
+            si = stage.inputs[ii]
+            sizes = [int(self.out_bytes.get(v, 0)) for v in self.vids[si.src]]
+            props = getattr(self.ctx, "_props", {})
+            thr = parse_size(props.get("AggregateThreshold") or (1 << 30))
+            max_in = int(props.get("AggregationTreeMaxInputs") or 150)
+            groups = assign_groups(sizes, stage.partitions, max_in, thr)
+            self.dyn_groups[key] = groups
+            self._event(dict(event="dynamic_aggregate", stage=f"{stage.id}:{stage.name}", threshold=thr,
+                             partials=len(sizes), partial_bytes=sum(sizes),
+                             groups=[len(x) for x in groups if x]))
+        return set(self.dyn_groups[key][part])
+
     def command(self, vid, version):
         g = self.g
         sid = g.vertex_stage(vid)
         part = g.vertex_partition(vid)
         stage = self.plan.stages[sid]
         inputs = []
-        for lst in self.inputs_of[vid]:
+        for ii, lst in enumerate(self.inputs_of[vid]):
+            si = stage.inputs[ii]
+            if si.kind == "group" and getattr(si, "dynamic", False):
+                chosen = self._dynamic_group(stage, ii, part)
+                lst = [(src, port, e) for src, port, e in lst if g.vertex_partition(src) in chosen]
             inputs.append([(self.chan_path(src, g.completed_version(src), port), e) for src, port, e in lst])
         cmd = dict(job=self.job_dir, stage=sid, partition=part, vertex=vid, version=version, inputs=inputs,
                    outputs=[self.chan_path(vid, version, k) for k in range(stage.out_ports)],
@@ -208,6 +236,7 @@ class JobRunner:
             accepted, cancel = g.on_completed(v, ver, now(), int(res["bytes_read"]), int(res["bytes_written"]))
             if accepted:
                 results[v] = res
+                self.out_bytes[v] = int(res["bytes_written"])
             for cv, cver in cancel:
                 slot = running.pop((cv, cver), None)
                 if slot is not None:
