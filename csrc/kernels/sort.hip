@@ -1687,8 +1687,9 @@ DR_API int dr_sort_u64_expand(E64* keys, E64* tmp, E128* out, uint64_t n, int be
 // so every store stays inside the output); the caller checks that word.
 namespace {
 
-constexpr int kOsItems = 16;
-constexpr int kOsTile = kBlock * kOsItems;
+constexpr int kOsItems = 32;                   // 8192-entry tiles: 78 KB of LDS, 2 workgroups per CU
+                                               // (A/B at 1.25e9: 16 items 33.9 ms / 4 passes, 20: 32.7,
+                                               //  24: 29.3, 32: 25.1, 40: 34.6, 48: 32.9, 64: 30.2)
 constexpr int kOsMaxPasses = 8;
 constexpr uint32_t kOsHistGrid = 1024;
 constexpr uint32_t kOsSpinLimit = 1u << 22;
@@ -1696,7 +1697,11 @@ constexpr uint64_t kOsHeader = 256;            // tickets[8] at 0, error word at
 typedef __attribute__((address_space(1))) unsigned long long os_gu64;
 typedef __attribute__((address_space(1))) unsigned int os_gu32;
 
-inline uint64_t os_tiles(uint64_t n) { return (n + kOsTile - 1) / kOsTile; }
+constexpr int kOsMinItems = 16;                // smallest tile size selectable (sizes the workspace)
+inline uint64_t os_tiles(uint64_t n, int items = kOsMinItems) {
+  const uint64_t tile = (uint64_t)kBlock * items;
+  return (n + tile - 1) / tile;
+}
 
 // workspace: [header | digit counts: 8 x 256 u32 | granules: tiles x 256 u64] (bytes), all zeroed
 // per call
@@ -1885,9 +1890,9 @@ __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__
 }  // namespace
 
 namespace {
-int g_os_lookback = 4;   // predecessor granules per look-back round trip (4; 8 for the A/B: slower)
+int g_os_items = kOsItems;   // entries per thread of a look-back tile (32; 16 for the A/B)
 }
-DR_API void dr_sort64_onesweep_set_lookback(int lb) { g_os_lookback = lb == 8 ? 8 : 4; }
+DR_API void dr_sort64_onesweep_set_items(int items) { g_os_items = items == 16 ? 16 : kOsItems; }
 
 DR_API uint64_t dr_sort_u64_onesweep_workspace(uint64_t n) { return os_workspace_bytes(n > 0 ? n : 1); }
 
@@ -1913,7 +1918,7 @@ DR_API int dr_sort_u64_onesweep(E64* keys, E64* tmp, uint64_t n, int begin_bit, 
   uint32_t* err = reinterpret_cast<uint32_t*>(w8 + 64);
   uint32_t* gbase = reinterpret_cast<uint32_t*>(w8 + kOsHeader);
   unsigned long long* granules = reinterpret_cast<unsigned long long*>(w8 + kOsHeader + kOsCounts);
-  hipError_t e = hipMemsetAsync(w8, 0, os_workspace_bytes(n), s);
+  hipError_t e = hipMemsetAsync(w8, 0, kOsHeader + kOsCounts + os_tiles(n, g_os_items) * kBins * 8, s);
   if (e != hipSuccess) return (int)e;
   if (hist_part) {
     if (begin_bit < 32 || end_bit != 64 || parts == 0) return (int)hipErrorInvalidValue;
@@ -1927,14 +1932,14 @@ DR_API int dr_sort_u64_onesweep(E64* keys, E64* tmp, uint64_t n, int begin_bit, 
   E64* dst = tmp;
   int flips = 0;
   for (int p = 0; p < P; ++p) {
-    if (g_os_lookback == 8)
-      os_scatter_kernel<kOsItems, 8><<<(unsigned)tiles, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
-                                                                    granules, tickets + p, err, 2u * (p + 1),
-                                                                    (uint32_t)tiles);
+    const uint64_t tl = os_tiles(n, g_os_items);
+    if (g_os_items == 16)
+      os_scatter_kernel<16, 4><<<(unsigned)tl, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins, granules,
+                                                            tickets + p, err, 2u * (p + 1), (uint32_t)tl);
     else
-      os_scatter_kernel<kOsItems, 4><<<(unsigned)tiles, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
-                                                                    granules, tickets + p, err, 2u * (p + 1),
-                                                                    (uint32_t)tiles);
+      os_scatter_kernel<kOsItems, 4><<<(unsigned)tl, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
+                                                                  granules, tickets + p, err, 2u * (p + 1),
+                                                                  (uint32_t)tl);
     E64* x = src; src = dst; dst = x;
     flips ^= 1;
   }

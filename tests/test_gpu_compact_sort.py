@@ -146,21 +146,22 @@ def test_onesweep_sort64_matches_stable_reference(n, win, kind):
     assert torch.equal(rb.cpu(), ref)
 
 
-def test_onesweep_lookback8_variant_matches():
-    """The 8-granule look-back of the single-histogram sort (A/B only) sorts identically."""
+@pytest.mark.parametrize("items", [16])
+def test_onesweep_tile_size_variants_match(items):
+    """The 4096-entry look-back tiles (A/B only) sort identically."""
     from dryad_amd.ops import _lib
     lib = _lib.lib()
-    lib.dr_sort64_onesweep_set_lookback.argtypes = [__import__("ctypes").c_int]
-    lib.dr_sort64_onesweep_set_lookback.restype = None
+    lib.dr_sort64_onesweep_set_items.argtypes = [__import__("ctypes").c_int]
+    lib.dr_sort64_onesweep_set_items.restype = None
     n = (1 << 21) + 77
     g = torch.Generator().manual_seed(3)
     w = torch.randint(0, 1 << 32, (n,), generator=g, dtype=torch.int64)
     ent = ((w << 32) | torch.arange(n, dtype=torch.int64)).to(DEV)
-    lib.dr_sort64_onesweep_set_lookback(8)
+    lib.dr_sort64_onesweep_set_items(items)
     try:
         ra, rb = _sort64_both(ent, 32)
     finally:
-        lib.dr_sort64_onesweep_set_lookback(4)
+        lib.dr_sort64_onesweep_set_items(32)
     assert torch.equal(ra, rb)
 
 

@@ -50,23 +50,19 @@ def main():
                   ctypes.byref(flag))
 
     lib = _lib.lib()
-    lib.dr_sort64_onesweep_set_lookback.argtypes = [ctypes.c_int]
-    lib.dr_sort64_onesweep_set_lookback.restype = None
+    lib.dr_sort64_onesweep_set_items.argtypes = [ctypes.c_int]
+    lib.dr_sort64_onesweep_set_items.restype = None
 
-    def new():
-        lib.dr_sort64_onesweep_set_lookback(4)
+    def new_items(items):
+        lib.dr_sort64_onesweep_set_items(items)
         _lib.call("dr_sort_u64_onesweep", S.ptr(ent), S.ptr(tmp), S.c_u64(n), 32, 64, S.ptr(ws_os),
                   S.c_u64(ws_os.numel()), None, S.c_u32(0), S.stream_of(ent), ctypes.byref(flag))
-
-    def new_lb8():
-        lib.dr_sort64_onesweep_set_lookback(8)
-        _lib.call("dr_sort_u64_onesweep", S.ptr(ent), S.ptr(tmp), S.c_u64(n), 32, 64, S.ptr(ws_os),
-                  S.c_u64(ws_os.numel()), None, S.c_u32(0), S.stream_of(ent), ctypes.byref(flag))
-        lib.dr_sort64_onesweep_set_lookback(4)
+        lib.dr_sort64_onesweep_set_items(32)
 
     results = {}
     for rnd in range(2):
-        for name, fn in (("count+scatter", old), ("onesweep", new), ("onesweep-lb8", new_lb8)):
+        for name, fn in (("count+scatter", old), ("onesweep-items32", lambda: new_items(32)),
+                         ("onesweep-items16", lambda: new_items(16))):
             def run():
                 ent.copy_(base)
                 fn()
@@ -80,9 +76,8 @@ def main():
                   f"copy {cmed:.2f})", flush=True)
             del res
     S.onesweep_check(base.device)
-    same = torch.equal(results["count+scatter"], results["onesweep"]) and \
-        torch.equal(results["count+scatter"], results["onesweep-lb8"])
-    w = (results["onesweep"] >> 32) & 0xFFFFFFFF
+    same = all(torch.equal(results["count+scatter"], results[f"onesweep-items{i}"]) for i in (32, 16))
+    w = (results["onesweep-items32"] >> 32) & 0xFFFFFFFF
     ordered = bool((w[1:] >= w[:-1]).all())
     print(f"n={n} identical={same} ordered={ordered}", flush=True)
 
