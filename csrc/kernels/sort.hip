@@ -1565,6 +1565,122 @@ __global__ __launch_bounds__(256) void gather_fixup_kernel(const uint32_t* __res
   }
 }
 
+// gather_fixup_kernel<25, true, 32> with 16-byte row loads: 8 lanes per 128-byte input line
+// (7 loads of it hold the 100-byte record), every row of the window requested before any is
+// stored, staged through LDS at the output's 100-byte pitch, then written out as contiguous
+// dwords.  The dword-per-lane copy keeps ~3 lines per load instruction in flight; this one 8.
+__global__ __launch_bounds__(256) void gather_fixup_p128w_kernel(const uint32_t* __restrict__ rows,
+                                                                 uint32_t* __restrict__ out,
+                                                                 const E64* __restrict__ ent, uint64_t n,
+                                                                 uint32_t key_off, uint32_t key_len, int run_shift,
+                                                                 uint32_t* __restrict__ overflow) {
+  constexpr uint32_t W = 25, Win = 32;
+  __shared__ uint32_t rid[kGfWin + 1];     // rid[p + 1] = run id of window position p; rid[0] = position -1
+  __shared__ uint32_t idx[kGfWin];
+  __shared__ uint32_t sidx[kGfWin];
+  // the run keys (phases A, B) and the row staging (phase C) share one buffer
+  __shared__ __attribute__((aligned(16))) uint32_t sbuf[kGfWin * 25 > kGfWin * 4 ? kGfWin * 25 : kGfWin * 4];
+  uint64_t* kk0 = reinterpret_cast<uint64_t*>(sbuf);
+  uint64_t* kk1 = kk0 + kGfWin;
+  __shared__ uint32_t own[2];
+  const int t = threadIdx.x;
+  const uint8_t* rbytes = reinterpret_cast<const uint8_t*>(rows);
+  const bool aligned = (((Win * 4) | key_off) & 3) == 0;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * kGfCore; c0 < n; c0 += (uint64_t)gridDim.x * kGfCore) {
+    const uint32_t L = (uint32_t)((n - c0) < (uint64_t)kGfWin ? (n - c0) : kGfWin);
+    const uint32_t core = L < (uint32_t)kGfCore ? L : (uint32_t)kGfCore;
+    for (uint32_t p = t; p < L; p += kBlock) {
+      const uint64_t v = ent[c0 + p].v;
+      rid[p + 1] = (uint32_t)(v >> run_shift);
+      idx[p] = (uint32_t)v;
+    }
+    if (t == 0) {
+      rid[0] = c0 > 0 ? (uint32_t)(ent[c0 - 1].v >> run_shift) : 0u;
+      own[0] = 0xFFFFFFFFu;
+      own[1] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    for (uint32_t p = t; p < L; p += kBlock) {
+      const bool start = (c0 + p == 0) || rid[p + 1] != rid[p];
+      if (start) atomicMin(&own[p < core ? 0 : 1], p);
+    }
+    __syncthreads();
+    const uint32_t ob = own[0];
+    uint32_t oe = own[1];
+    if (oe == 0xFFFFFFFFu && c0 + L == n) oe = L;
+    if (ob == 0xFFFFFFFFu) {           // the whole core continues a run owned by a previous workgroup
+      __syncthreads();
+      continue;
+    }
+    if (oe == 0xFFFFFFFFu) {           // a run owned here does not end inside the window
+      if (t == 0) atomicOr(overflow, 1u);
+      __syncthreads();
+      continue;
+    }
+    // phase A: keys of the rows in multi-entry runs
+    for (uint32_t p = ob + t; p < oe; p += kBlock) {
+      const bool multi = (p > ob && rid[p + 1] == rid[p]) || (p + 1 < oe && rid[p + 2] == rid[p + 1]);
+      if (multi) {
+        uint64_t k0, k1;
+        load_key128(rbytes + (uint64_t)idx[p] * (Win * 4) + key_off, key_len, aligned, k0, k1);
+        kk0[p] = k0;
+        kk1[p] = k1;
+      } else {
+        sidx[p - ob] = idx[p];
+      }
+    }
+    __syncthreads();
+    // phase B: rank inside each run: (key, position) order = stable
+    for (uint32_t p = ob + t; p < oe; p += kBlock) {
+      const uint32_t r = rid[p + 1];
+      const bool multi = (p > ob && rid[p] == r) || (p + 1 < oe && rid[p + 2] == r);
+      if (!multi) continue;
+      uint32_t rs = p, re = p + 1;
+      while (rs > ob && rid[rs] == r) --rs;
+      while (re < oe && rid[re + 1] == r) ++re;
+      const uint64_t a0 = kk0[p], a1 = kk1[p];
+      uint32_t cnt = 0;
+      for (uint32_t q = rs; q < re; ++q) {
+        const uint64_t b0 = kk0[q], b1 = kk1[q];
+        cnt += (b0 < a0 || (b0 == a0 && (b1 < a1 || (b1 == a1 && q < p)))) ? 1u : 0u;
+      }
+      sidx[rs + cnt - ob] = idx[p];
+    }
+    __syncthreads();
+    const uint32_t nrows = oe - ob;
+    {
+      constexpr int kRounds = kGfWin / 32;         // 32 rows per round (8 lanes each)
+      const uint32_t g = t >> 3, sub = t & 7;
+      const uint8_t* rb = reinterpret_cast<const uint8_t*>(rows);
+      uint4 buf[kRounds];
+#pragma unroll
+      for (int k = 0; k < kRounds; ++k) {
+        const uint32_t r = g + 32 * k;
+        if (r < nrows && sub < 7) buf[k] = *reinterpret_cast<const uint4*>(rb + (uint64_t)sidx[r] * 128 + sub * 16);
+      }
+      __syncthreads();                             // kk0 / kk1 are dead: sbuf becomes the staging
+#pragma unroll
+      for (int k = 0; k < kRounds; ++k) {
+        const uint32_t r = g + 32 * k;
+        if (r < nrows && sub < 7) {
+          uint32_t* d = sbuf + r * W + sub * 4;
+          d[0] = buf[k].x;
+          if (sub < 6) {
+            d[1] = buf[k].y;
+            d[2] = buf[k].z;
+            d[3] = buf[k].w;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t words = nrows * W;
+    uint32_t* o = out + (c0 + ob) * W;
+    for (uint32_t j = t; j < words; j += kBlock) __builtin_nontemporal_store(sbuf[j], o + j);
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 DR_API int dr_extract_keys64(const uint8_t* rows, uint64_t n, uint32_t stride, uint32_t key_off, uint32_t key_len,
@@ -1952,6 +2068,10 @@ namespace {
 int g_gather_nt = 1;   // nontemporal output stores (A/B: -1.2% gather time at 1e9 rows, dr_gather_fixup_set_nt)
 }
 DR_API void dr_gather_fixup_set_nt(int on) { g_gather_nt = on ? 1 : 0; }
+namespace {
+int g_gather_wide = 1;   // 16-byte row loads staged through LDS (pitch-128 input; A/B: 0 = dword copy)
+}
+DR_API void dr_gather_fixup_set_wide(int on) { g_gather_wide = on ? 1 : 0; }
 
 // Row gather + run fix-up of the compact sort: out = rows in (window, full key, position) order.
 // run_shift = 64 - (window bits the LSD sort covered).  stride % 4 == 0, key_len <= 16.
@@ -1983,6 +2103,12 @@ DR_API int dr_gather_fixup_pitch128(const uint8_t* rows, uint8_t* out, const E64
   if (run_shift < 32 || run_shift > 63) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
   const unsigned g = grid_for(n, kGfCore, 16384);
+  if (g_gather_wide) {
+    gather_fixup_p128w_kernel<<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows), reinterpret_cast<uint32_t*>(out),
+                                                ent, n, key_off, key_len, run_shift, overflow);
+    DR_LAUNCH_CHECK();
+    return 0;
+  }
   gather_fixup_kernel<25, true, 32><<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows),
                                                       reinterpret_cast<uint32_t*>(out), ent, n, 25, key_off, key_len,
                                                       run_shift, overflow);

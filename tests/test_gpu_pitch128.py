@@ -103,3 +103,32 @@ def test_one_rank_terasort_query_uses_the_line_aligned_input():
     assert runner_path is not None and "pitch128" in runner_path
     assert ex.last_result["fallbacks"] == []
     provider_for("hbm://ts_pitch").delete("hbm://ts_pitch")
+
+
+@pytest.mark.parametrize("wide", [1, 0])
+def test_pitch128_gather_fixup_runs_wide_and_dword_copy(wide):
+    """Short runs of equal 32-bit windows (about 4 rows each, resolved by the gather's in-LDS
+    fix-up) copied by the 16-byte-load gather (default) and by the dword copy (A/B): numpy order."""
+    import ctypes
+    from dryad_amd.ops import _lib
+    from dryad_amd.ops import sort as S
+    lib = _lib.lib()
+    lib.dr_gather_fixup_set_wide.argtypes = [ctypes.c_int]
+    lib.dr_gather_fixup_set_wide.restype = None
+    n = 200_003
+    g = np.random.default_rng(5)
+    rows = g.integers(0, 256, size=(n, 100), dtype=np.uint8)
+    win = (g.integers(0, 50_000, size=n, dtype=np.uint64) * 85_899).astype(np.uint32)   # spread: top 24 bits differ
+    rows[:, 0:4] = win.astype(">u4").view(np.uint8).reshape(n, 4)
+    padded = torch.zeros((n, 128), dtype=torch.uint8, device="cuda")
+    padded[:, :100] = torch.from_numpy(rows).cuda()
+    keys = ((torch.from_numpy(win.astype(np.int64)) << 32) | torch.arange(n, dtype=torch.int64)).cuda()
+    out = torch.empty((n, 100), dtype=torch.uint8, device="cuda")
+    info = {}
+    lib.dr_gather_fixup_set_wide(wide)
+    try:
+        got = S.sort_rows_pitch128(padded, out, keys, 0, 10, keys_ready=True, stats=info)
+    finally:
+        lib.dr_gather_fixup_set_wide(1)
+    assert "LSD chain" not in info["path"], info
+    np.testing.assert_array_equal(got.cpu().numpy(), rows[_reference_order(rows, 0, 10)])
