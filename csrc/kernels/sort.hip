@@ -1569,6 +1569,7 @@ __global__ __launch_bounds__(256) void gather_fixup_kernel(const uint32_t* __res
 // (7 loads of it hold the 100-byte record), every row of the window requested before any is
 // stored, staged through LDS at the output's 100-byte pitch, then written out as contiguous
 // dwords.  The dword-per-lane copy keeps ~3 lines per load instruction in flight; this one 8.
+template <bool NTL>
 __global__ __launch_bounds__(256) void gather_fixup_p128w_kernel(const uint32_t* __restrict__ rows,
                                                                  uint32_t* __restrict__ out,
                                                                  const E64* __restrict__ ent, uint64_t n,
@@ -1656,7 +1657,17 @@ __global__ __launch_bounds__(256) void gather_fixup_p128w_kernel(const uint32_t*
 #pragma unroll
       for (int k = 0; k < kRounds; ++k) {
         const uint32_t r = g + 32 * k;
-        if (r < nrows && sub < 7) buf[k] = *reinterpret_cast<const uint4*>(rb + (uint64_t)sidx[r] * 128 + sub * 16);
+        if (r < nrows && sub < 7) {
+          const uint4* src = reinterpret_cast<const uint4*>(rb + (uint64_t)sidx[r] * 128 + sub * 16);
+          if constexpr (NTL) {
+            buf[k].x = __builtin_nontemporal_load(&src->x);
+            buf[k].y = __builtin_nontemporal_load(&src->y);
+            buf[k].z = __builtin_nontemporal_load(&src->z);
+            buf[k].w = __builtin_nontemporal_load(&src->w);
+          } else {
+            buf[k] = *src;
+          }
+        }
       }
       __syncthreads();                             // kk0 / kk1 are dead: sbuf becomes the staging
 #pragma unroll
@@ -1884,7 +1895,7 @@ __global__ __launch_bounds__(256) void os_hist_scan_kernel(uint32_t* __restrict_
   counts[p * kBins + t] = ex;
 }
 
-template <int ITEMS, int LB>
+template <int ITEMS, int LB, int NT = 0>   // NT bit 0: nontemporal entry loads, bit 1: stores
 __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__ in, E64* __restrict__ out,
                                                          uint64_t n, int shift, const uint32_t* __restrict__ gbase,
                                                          unsigned long long* granules, uint32_t* ticket,
@@ -1911,7 +1922,10 @@ __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
     const uint32_t pos = w * (kTile / 4) + r * 64 + l;
-    if (pos < cnt) cur[r] = in[base + pos];
+    if (pos < cnt) {
+      if constexpr ((NT & 1) != 0) cur[r].v = __builtin_nontemporal_load(&in[base + pos].v);
+      else cur[r] = in[base + pos];
+    }
   }
   const unsigned long long lanebit = 1ull << l;
   {
@@ -1998,7 +2012,8 @@ __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__
     for (uint32_t j = t; j < cnt; j += kBlock) {
       const E64 v = stage[j];
       const uint32_t d = digit_of(v, shift);
-      out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+      if constexpr ((NT & 2) != 0) __builtin_nontemporal_store(v.v, &out[(uint64_t)goff[d] + (j - bstart[d])].v);
+      else out[(uint64_t)goff[d] + (j - bstart[d])] = v;
     }
   }
 }
@@ -2009,6 +2024,10 @@ namespace {
 int g_os_items = kOsItems;   // entries per thread of a look-back tile (32; 16 for the A/B)
 }
 DR_API void dr_sort64_onesweep_set_items(int items) { g_os_items = items == 16 ? 16 : kOsItems; }
+namespace {
+int g_os_nt = 0;             // A/B: nontemporal entry loads (1) / stores (2) of the look-back scatter
+}
+DR_API void dr_sort64_onesweep_set_nt(int mask) { g_os_nt = mask & 3; }
 
 DR_API uint64_t dr_sort_u64_onesweep_workspace(uint64_t n) { return os_workspace_bytes(n > 0 ? n : 1); }
 
@@ -2052,6 +2071,18 @@ DR_API int dr_sort_u64_onesweep(E64* keys, E64* tmp, uint64_t n, int begin_bit, 
     if (g_os_items == 16)
       os_scatter_kernel<16, 4><<<(unsigned)tl, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins, granules,
                                                             tickets + p, err, 2u * (p + 1), (uint32_t)tl);
+    else if (g_os_nt == 1)
+      os_scatter_kernel<kOsItems, 4, 1><<<(unsigned)tl, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
+                                                                     granules, tickets + p, err, 2u * (p + 1),
+                                                                     (uint32_t)tl);
+    else if (g_os_nt == 2)
+      os_scatter_kernel<kOsItems, 4, 2><<<(unsigned)tl, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
+                                                                     granules, tickets + p, err, 2u * (p + 1),
+                                                                     (uint32_t)tl);
+    else if (g_os_nt == 3)
+      os_scatter_kernel<kOsItems, 4, 3><<<(unsigned)tl, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
+                                                                     granules, tickets + p, err, 2u * (p + 1),
+                                                                     (uint32_t)tl);
     else
       os_scatter_kernel<kOsItems, 4><<<(unsigned)tl, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
                                                                   granules, tickets + p, err, 2u * (p + 1),
@@ -2069,9 +2100,10 @@ int g_gather_nt = 1;   // nontemporal output stores (A/B: -1.2% gather time at 1
 }
 DR_API void dr_gather_fixup_set_nt(int on) { g_gather_nt = on ? 1 : 0; }
 namespace {
-int g_gather_wide = 1;   // 16-byte row loads staged through LDS (pitch-128 input; A/B: 0 = dword copy)
+int g_gather_wide = 2;   // 16-byte nontemporal row loads staged through LDS (pitch-128 input; A/B:
+                         // 0 = dword copy, 1 = cached 16-byte loads; profiles/r3/ab_gather_wide_p128.log)
 }
-DR_API void dr_gather_fixup_set_wide(int on) { g_gather_wide = on ? 1 : 0; }
+DR_API void dr_gather_fixup_set_wide(int on) { g_gather_wide = (on == 2) ? 2 : (on ? 1 : 0); }
 
 // Row gather + run fix-up of the compact sort: out = rows in (window, full key, position) order.
 // run_shift = 64 - (window bits the LSD sort covered).  stride % 4 == 0, key_len <= 16.
@@ -2103,8 +2135,15 @@ DR_API int dr_gather_fixup_pitch128(const uint8_t* rows, uint8_t* out, const E64
   if (run_shift < 32 || run_shift > 63) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
   const unsigned g = grid_for(n, kGfCore, 16384);
+  if (g_gather_wide == 2) {
+    gather_fixup_p128w_kernel<true><<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows),
+                                                      reinterpret_cast<uint32_t*>(out), ent, n, key_off, key_len,
+                                                      run_shift, overflow);
+    DR_LAUNCH_CHECK();
+    return 0;
+  }
   if (g_gather_wide) {
-    gather_fixup_p128w_kernel<<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows), reinterpret_cast<uint32_t*>(out),
+    gather_fixup_p128w_kernel<false><<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows), reinterpret_cast<uint32_t*>(out),
                                                 ent, n, key_off, key_len, run_shift, overflow);
     DR_LAUNCH_CHECK();
     return 0;

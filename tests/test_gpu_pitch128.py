@@ -105,10 +105,11 @@ def test_one_rank_terasort_query_uses_the_line_aligned_input():
     provider_for("hbm://ts_pitch").delete("hbm://ts_pitch")
 
 
-@pytest.mark.parametrize("wide", [1, 0])
+@pytest.mark.parametrize("wide", [2, 1, 0])
 def test_pitch128_gather_fixup_runs_wide_and_dword_copy(wide):
     """Short runs of equal 32-bit windows (about 4 rows each, resolved by the gather's in-LDS
-    fix-up) copied by the 16-byte-load gather (default) and by the dword copy (A/B): numpy order."""
+    fix-up) copied by the 16-byte nontemporal-load gather (default), the cached 16-byte loads and
+    the dword copy (A/B): numpy order."""
     import ctypes
     from dryad_amd.ops import _lib
     from dryad_amd.ops import sort as S
@@ -129,6 +130,6 @@ def test_pitch128_gather_fixup_runs_wide_and_dword_copy(wide):
     try:
         got = S.sort_rows_pitch128(padded, out, keys, 0, 10, keys_ready=True, stats=info)
     finally:
-        lib.dr_gather_fixup_set_wide(1)
+        lib.dr_gather_fixup_set_wide(2)
     assert "LSD chain" not in info["path"], info
     np.testing.assert_array_equal(got.cpu().numpy(), rows[_reference_order(rows, 0, 10)])

@@ -27,7 +27,7 @@ def main():
     for _ in range(2):
         job.step()
     for r in range(rounds):
-        for name, wide in (("dword copy", 0), ("16-byte loads + LDS", 1)):
+        for name, wide in (("dword copy", 0), ("16-byte loads + LDS", 1), ("16-byte nontemporal loads + LDS", 2)):
             lib.dr_gather_fixup_set_wide(wide)
             job.step()
             secs = run_steps(job, steps)
