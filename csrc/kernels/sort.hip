@@ -1895,7 +1895,7 @@ __global__ __launch_bounds__(256) void os_hist_scan_kernel(uint32_t* __restrict_
   counts[p * kBins + t] = ex;
 }
 
-template <int ITEMS, int LB, int NT = 0>   // NT bit 0: nontemporal entry loads, bit 1: stores
+template <int ITEMS, int LB>
 __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__ in, E64* __restrict__ out,
                                                          uint64_t n, int shift, const uint32_t* __restrict__ gbase,
                                                          unsigned long long* granules, uint32_t* ticket,
@@ -1922,10 +1922,7 @@ __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
     const uint32_t pos = w * (kTile / 4) + r * 64 + l;
-    if (pos < cnt) {
-      if constexpr ((NT & 1) != 0) cur[r].v = __builtin_nontemporal_load(&in[base + pos].v);
-      else cur[r] = in[base + pos];
-    }
+    if (pos < cnt) cur[r] = in[base + pos];
   }
   const unsigned long long lanebit = 1ull << l;
   {
@@ -2012,8 +2009,7 @@ __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__
     for (uint32_t j = t; j < cnt; j += kBlock) {
       const E64 v = stage[j];
       const uint32_t d = digit_of(v, shift);
-      if constexpr ((NT & 2) != 0) __builtin_nontemporal_store(v.v, &out[(uint64_t)goff[d] + (j - bstart[d])].v);
-      else out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+      out[(uint64_t)goff[d] + (j - bstart[d])] = v;    // plain stores (nontemporal: slower, onesweep_nt_ab.log)
     }
   }
 }
@@ -2024,10 +2020,7 @@ namespace {
 int g_os_items = kOsItems;   // entries per thread of a look-back tile (32; 16 for the A/B)
 }
 DR_API void dr_sort64_onesweep_set_items(int items) { g_os_items = items == 16 ? 16 : kOsItems; }
-namespace {
-int g_os_nt = 0;             // A/B: nontemporal entry loads (1) / stores (2) of the look-back scatter
-}
-DR_API void dr_sort64_onesweep_set_nt(int mask) { g_os_nt = mask & 3; }
+
 
 DR_API uint64_t dr_sort_u64_onesweep_workspace(uint64_t n) { return os_workspace_bytes(n > 0 ? n : 1); }
 
@@ -2071,18 +2064,6 @@ DR_API int dr_sort_u64_onesweep(E64* keys, E64* tmp, uint64_t n, int begin_bit, 
     if (g_os_items == 16)
       os_scatter_kernel<16, 4><<<(unsigned)tl, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins, granules,
                                                             tickets + p, err, 2u * (p + 1), (uint32_t)tl);
-    else if (g_os_nt == 1)
-      os_scatter_kernel<kOsItems, 4, 1><<<(unsigned)tl, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
-                                                                     granules, tickets + p, err, 2u * (p + 1),
-                                                                     (uint32_t)tl);
-    else if (g_os_nt == 2)
-      os_scatter_kernel<kOsItems, 4, 2><<<(unsigned)tl, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
-                                                                     granules, tickets + p, err, 2u * (p + 1),
-                                                                     (uint32_t)tl);
-    else if (g_os_nt == 3)
-      os_scatter_kernel<kOsItems, 4, 3><<<(unsigned)tl, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
-                                                                     granules, tickets + p, err, 2u * (p + 1),
-                                                                     (uint32_t)tl);
     else
       os_scatter_kernel<kOsItems, 4><<<(unsigned)tl, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
                                                                   granules, tickets + p, err, 2u * (p + 1),

@@ -59,19 +59,10 @@ def main():
                   S.c_u64(ws_os.numel()), None, S.c_u32(0), S.stream_of(ent), ctypes.byref(flag))
         lib.dr_sort64_onesweep_set_items(32)
 
-    lib.dr_sort64_onesweep_set_nt.argtypes = [ctypes.c_int]
-    lib.dr_sort64_onesweep_set_nt.restype = None
-
-    def new_nt(mask):
-        lib.dr_sort64_onesweep_set_nt(mask)
-        new_items(32)
-        lib.dr_sort64_onesweep_set_nt(0)
-
     results = {}
     for rnd in range(2):
         for name, fn in (("count+scatter", old), ("onesweep-items32", lambda: new_items(32)),
-                         ("onesweep-nt-loads", lambda: new_nt(1)), ("onesweep-nt-stores", lambda: new_nt(2)),
-                         ("onesweep-nt-both", lambda: new_nt(3))):
+                         ("onesweep-items16", lambda: new_items(16))):
             def run():
                 ent.copy_(base)
                 fn()
@@ -85,7 +76,7 @@ def main():
                   f"copy {cmed:.2f})", flush=True)
             del res
     S.onesweep_check(base.device)
-    same = all(torch.equal(results["count+scatter"], results[f"onesweep-{i}"]) for i in ("items32", "nt-loads", "nt-stores", "nt-both"))
+    same = all(torch.equal(results["count+scatter"], results[f"onesweep-{i}"]) for i in ("items32", "items16"))
     w = (results["onesweep-items32"] >> 32) & 0xFFFFFFFF
     ordered = bool((w[1:] >= w[:-1]).all())
     print(f"n={n} identical={same} ordered={ordered}", flush=True)
