@@ -31,7 +31,7 @@ using dr_ts::ts_record;
 // HIST (KEYS == 2): also the histograms of the four window bytes (the digits of the compact sort's
 // four LSD passes), one [4][256] partial per workgroup in hist_part, so that sort needs no
 // histogram read of its own (dr_sort_u64_onesweep with hist_part).
-template <int KEYS, bool ROWS = true, int PITCH = 25, bool HIST = false>
+template <int KEYS, bool ROWS = true, int PITCH = 25, bool HIST = false, bool NTS = false, bool NTK = false>
 __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out, uint64_t n, uint64_t first,
                                                      uint64_t seed, void* __restrict__ keys, uint32_t idx_base,
                                                      unsigned long long* __restrict__ hi_range,
@@ -62,7 +62,10 @@ __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out,
           e.lo = ((uint64_t)(bswap32(w[2]) & 0xFFFF0000u) << 32) | idx;
           static_cast<E128*>(keys)[row0 + threadIdx.x] = e;
         } else {
-          static_cast<uint64_t*>(keys)[row0 + threadIdx.x] = (hi & 0xFFFFFFFF00000000ull) | idx;
+          if constexpr (NTK)   // A/B value 2: the entries too
+            __builtin_nontemporal_store((hi & 0xFFFFFFFF00000000ull) | idx, static_cast<uint64_t*>(keys) + row0 + threadIdx.x);
+          else
+            static_cast<uint64_t*>(keys)[row0 + threadIdx.x] = (hi & 0xFFFFFFFF00000000ull) | idx;
           if constexpr (HIST) {
 #pragma unroll
             for (int p = 0; p < 4; ++p) atomicAdd(&hist[p][(uint32_t)(hi >> (32 + 8 * p)) & 0xFF], 1u);
@@ -84,7 +87,15 @@ __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out,
         v.y = q + 1 < 25 ? src[1] : 0u;
         v.z = q + 2 < 25 ? src[2] : 0u;
         v.w = q + 3 < 25 ? src[3] : 0u;
-        dst[j] = v;
+        if constexpr (NTS) {
+          uint32_t* d = reinterpret_cast<uint32_t*>(dst + j);
+          __builtin_nontemporal_store(v.x, d);
+          __builtin_nontemporal_store(v.y, d + 1);
+          __builtin_nontemporal_store(v.z, d + 2);
+          __builtin_nontemporal_store(v.w, d + 3);
+        } else {
+          dst[j] = v;
+        }
       }
       __syncthreads();
       continue;
@@ -194,13 +205,29 @@ DR_API int dr_terasort_gen_keys64(uint8_t* out, uint64_t n, uint64_t first_index
 // the four window bytes of the entries.
 DR_API uint32_t dr_terasort_gen_hist_parts(uint64_t n) { return grid_for(n, 256, 16384); }
 
+namespace {
+int g_gen_nt = 1;   // nontemporal row stores of the pitch-128 generator (A/B: 0 plain, 2 entries too;
+                    // profiles/r3/ab_gen_nt.log: 105.8-106.2 -> 103.7-104.0 ms per step)
+}
+DR_API void dr_terasort_gen_set_nt(int v) { g_gen_nt = (v == 0 || v == 2) ? v : 1; }
+
 DR_API int dr_terasort_gen_keys64_pitch128(uint8_t* out, uint64_t n, uint64_t first_index, uint64_t seed, E64* keys,
                                            uint32_t idx_base, uint64_t* hi_range, uint32_t* hist_part, hipStream_t s) {
   if (n == 0) return 0;
   if (n + idx_base > (1ull << 32)) return (int)hipErrorInvalidValue;
   if (reinterpret_cast<uintptr_t>(out) & 15) return (int)hipErrorInvalidValue;
   const unsigned g = grid_for(n, 256, 16384);
-  if (hist_part)
+  if (hist_part && g_gen_nt == 2)
+    ts_gen_kernel<2, true, 32, true, true, true><<<g, 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index,
+                                                                   seed, keys, idx_base,
+                                                                   reinterpret_cast<unsigned long long*>(hi_range),
+                                                                   hist_part);
+  else if (hist_part && g_gen_nt)
+    ts_gen_kernel<2, true, 32, true, true><<<g, 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index, seed,
+                                                             keys, idx_base,
+                                                             reinterpret_cast<unsigned long long*>(hi_range),
+                                                             hist_part);
+  else if (hist_part)
     ts_gen_kernel<2, true, 32, true><<<g, 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index, seed, keys,
                                                        idx_base, reinterpret_cast<unsigned long long*>(hi_range),
                                                        hist_part);
