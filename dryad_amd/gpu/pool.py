@@ -80,8 +80,10 @@ def allocate(capacity: int, stride: int, device, layout: str = "plain") -> RS.So
     if layout != "pitch128" or stride > 128:
         raise ValueError(f"HbmPool: unknown layout {layout!r} for {stride}-byte rows")
     cap = int(capacity) + 1024
-    return RS.SortBuffers(rows_in=torch.empty((cap, 128), dtype=torch.uint8, device=device),
-                          rows_out=torch.empty((cap, stride), dtype=torch.uint8, device=device),
+    # the output table is allocated before the 128-byte-pitch input (A/B: profiles/r3/alloc_order_ab.log)
+    rows_out = torch.empty((cap, stride), dtype=torch.uint8, device=device)
+    rows_in = torch.empty((cap, 128), dtype=torch.uint8, device=device)
+    return RS.SortBuffers(rows_in=rows_in, rows_out=rows_out,
                           ent_a=torch.empty(cap, dtype=torch.int64, device=device),
                           ent_b=torch.empty(0, dtype=torch.int64, device=device))
 
