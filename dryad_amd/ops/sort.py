@@ -437,10 +437,16 @@ def sort_rows_compact(rows: torch.Tensor, out: torch.Tensor, ent: torch.Tensor, 
     return out[:n]
 
 
-def _hi_range64(e: torch.Tensor) -> tuple[int, int]:
-    """(min, max) of the E64 window words, as hi-word bounds (window bits in the top 32)."""
-    w = (e >> 32) & 0xFFFFFFFF                 # unsigned window (>> is arithmetic on int64)
-    mn, mx = int(w.min().item()), int(w.max().item())
+def _hi_range64(e: torch.Tensor, chunk: int = 1 << 26) -> tuple[int, int]:
+    """(min, max) of the E64 window words, as hi-word bounds (window bits in the top 32).  Chunked,
+    so the temporaries stay at 2 x 512 MB however large ``e`` is (a 1.25e9-entry table next to a
+    290 GB sort working set has no room for a full-size copy)."""
+    mins, maxs = [], []
+    for a in range(0, e.shape[0], chunk):
+        w = (e[a:a + chunk] >> 32) & 0xFFFFFFFF          # unsigned window (>> is arithmetic on int64)
+        mins.append(w.min())
+        maxs.append(w.max())
+    mn, mx = int(torch.stack(mins).min().item()), int(torch.stack(maxs).max().item())
     return mn << 32, mx << 32
 
 
