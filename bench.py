@@ -65,8 +65,14 @@ def main():
                     help="run the sort pipeline directly instead of through the DryadLINQ query API")
     ap.add_argument("--rehearsal", action="store_true",
                     help="shared-GPU gloo rehearsal of the multi-rank path (admits DRYAD_DIST_BACKEND)")
+    ap.add_argument("--loopback-ranks", type=int, default=0,
+                    help="run the per-rank program of a W-rank job on this one GPU, the all-to-all-v replaced by "
+                         "generating the exact bytes this rank would receive (not timed); reports per-rank ms")
+    ap.add_argument("--loopback-rank", type=int, default=0, help="which rank of the --loopback-ranks job to run")
     args = ap.parse_args()
     env = check_env(args.rehearsal)
+    if args.loopback_ranks:
+        return loopback(args, env)
 
     import torch
     from dryad_amd.parallel.comm import init_world, shutdown
@@ -156,6 +162,46 @@ def main():
             print(f"[bench] executor: {json.dumps(rep, default=str)[:2000]}", file=sys.stderr, flush=True)
         print(json.dumps(line), flush=True)
     shutdown()
+    if val is not None and not val["ok"]:
+        sys.exit(3)
+
+
+def loopback(args, env):
+    """``--loopback-ranks W``: one rank's share of a W-GPU job, timed phase by phase on one GPU."""
+    import torch
+    from dryad_amd.models.terasort import TeraSortConfig, TeraSortLoopbackJob
+    W, r = args.loopback_ranks, args.loopback_rank
+    if W < 2 or not 0 <= r < W:
+        print("[bench] --loopback-ranks needs W >= 2 and 0 <= --loopback-rank < W", file=sys.stderr)
+        sys.exit(2)
+    job = TeraSortLoopbackJob(TeraSortConfig(records_per_rank=args.records_per_gpu), W, r)
+    for i in range(args.warmup):
+        job.step()
+        print(f"[bench] warmup {i}: {job.ms:.2f} ms {job.phases}", file=sys.stderr, flush=True)
+    ms, walls, phases = [], [], []
+    for i in range(args.steps):
+        t0 = time.perf_counter()
+        job.step()
+        walls.append(time.perf_counter() - t0)
+        ms.append(job.ms)
+        phases.append(job.phases)
+        print(f"[bench] step {i}: {job.ms:.2f} ms {job.phases}", file=sys.stderr, flush=True)
+    val = None if args.no_validate else job.validate()
+    mean = sum(ms) / len(ms)
+    line = {
+        "metric": f"TeraSort per-rank step of a {W}-rank job (loopback on one GPU: all-to-all-v replaced)",
+        "value": round(mean, 3), "unit": "ms", "higher_is_better": False, "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(mean, 3), "dtype": "uint8",
+        "data": "synthetic (gensort-style counter-generated 100-byte records, 10-byte random keys)",
+        "config": {"model": "TeraSort 100-byte records / 10-byte key", "records_per_rank": job.n,
+                   "bytes_per_rank": job.bytes_per_rank, "ranks": W, "rank": r, "rounds": job.B,
+                   "received_rows": int(job.out.shape[0]),
+                   "phases_ms": {k: round(sum(p[k] for p in phases) / len(phases), 3) for k in phases[0]},
+                   "per_rank_GBps": round(job.bytes_per_rank / 1e6 / mean, 1),
+                   "wall_s_per_step_incl_simulated_exchange": round(sum(walls) / len(walls), 3),
+                   "validated": None if val is None else val["ok"], "validation": val, "env": env},
+    }
+    print(json.dumps(line), flush=True)
     if val is not None and not val["ok"]:
         sys.exit(3)
 

@@ -96,9 +96,10 @@ __global__ __launch_bounds__(256) void codec_var_decode(const uint8_t* __restric
   for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nblocks;
        b += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t pos = (uint64_t)block_off[b];
-    const uint64_t end = b + 1 < nblocks ? (uint64_t)block_off[b + 1] : nbytes;
+    uint64_t end = b + 1 < nblocks ? (uint64_t)block_off[b + 1] : nbytes;
+    end = end < nbytes ? end : nbytes;             // a stale / corrupt index never reads past the part
     const uint64_t r0 = b * B, r1 = r0 + B < n ? r0 + B : n;
-    bool bad = false;
+    bool bad = pos > end;
     for (uint64_t r = r0; r < r1 && !bad; ++r) {
       for (int f = 0; f < nf; ++f) {
         const uint32_t sz = m.size[f];

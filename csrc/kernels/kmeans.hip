@@ -278,220 +278,10 @@ constexpr int kXRow = 132;   // floats per point row of the LDS tile
 // accumulation over 384 products (2.3e-5), both relative to sum |x_i c_i| <= |x| |c|, doubled.
 constexpr float kKmTol = 1.5e-4f;
 
-// DBG (profiling builds only): bit0 skips the sum MFMAs, bit1 the distance MFMAs, bit2 the
-// near-tie listing.
-template <int KT, int DBG>
-__global__ __launch_bounds__(256) void kmeans_mfma_kernel(const float* __restrict__ X, uint64_t n,
-                                                          const float* __restrict__ C, const float* __restrict__ cnorm,
-                                                          int K, int32_t* __restrict__ assign,
-                                                          double* __restrict__ gsum, unsigned long long* __restrict__ gcnt,
-                                                          int flush_tiles) {
-  constexpr int KP = 32 * KT;
-  __shared__ __attribute__((aligned(16))) __bf16 chi[KP * kCRow];
-  __shared__ __attribute__((aligned(16))) __bf16 cmd[KP * kCRow];
-  __shared__ float cn[KP];
-  __shared__ float cmax_s;
-  __shared__ __attribute__((aligned(16))) float xs[4][32 * kXRow];
-  __shared__ __attribute__((aligned(16))) int bjs[4][32];
-  __shared__ unsigned int wcnt[4][KP];
-  const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
-  for (int i = t; i < KP * D; i += 256) {
-    const int c = i / D, d = i % D;
-    const float v = c < K ? C[(uint64_t)c * D + d] : 0.f;
-    const __bf16 vh = (__bf16)v;
-    chi[c * kCRow + d] = vh;
-    cmd[c * kCRow + d] = (__bf16)(v - (float)vh);
-  }
-  for (int c = t; c < KP; c += 256) cn[c] = c < K ? cnorm[c] : __builtin_inff();
-  for (int i = t; i < 4 * KP; i += 256) (&wcnt[0][0])[i] = 0u;
-  if (t == 0) {
-    float m = 0.f;
-    for (int c = 0; c < K; ++c) m = fmaxf(m, cnorm[c]);
-    cmax_s = sqrtf(m);
-  }
-  __syncthreads();
-  const float cmax = cmax_s;
-  float* xw = xs[w];
-  const uint64_t tiles = (n + 31) / 32;
-  const uint64_t gw = (uint64_t)blockIdx.x * 4 + w, GW = (uint64_t)gridDim.x * 4;
-  f32x16 S[KT][4];
-#pragma unroll
-  for (int ct = 0; ct < KT; ++ct)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) S[ct][q] = f32x16{};
-  float xr[64];
-  // the 8 dims 16 s + 8 h .. + 7 of point r of `tile` into dst[8 s .. 8 s + 7]
-  auto load_part = [&](uint64_t tile, int s, float* dst) {
-    const uint64_t p = tile * 32 + r;
-    const bool ok = p < n;
-    const float4* src = reinterpret_cast<const float4*>(X + (ok ? p : 0) * D + 8 * h);
-    const float4 a = ok ? src[4 * s] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 b = ok ? src[4 * s + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
-    dst[8 * s + 0] = a.x; dst[8 * s + 1] = a.y; dst[8 * s + 2] = a.z; dst[8 * s + 3] = a.w;
-    dst[8 * s + 4] = b.x; dst[8 * s + 5] = b.y; dst[8 * s + 6] = b.z; dst[8 * s + 7] = b.w;
-  };
-  auto load = [&](uint64_t tile, float* dst) {
-#pragma unroll
-    for (int s = 0; s < 8; ++s) load_part(tile, s, dst);
-  };
-  // flush: one centroid tile at a time through the wave's LDS tile area (32 x 128 floats), then
-  // f64 atomics on consecutive addresses (128 distinct addresses computed in registers would be
-  // hoisted out of the loop and pin 256 VGPRs)
-  auto flush = [&]() {
-#pragma unroll
-    for (int ct = 0; ct < KT; ++ct) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-#pragma unroll
-        for (int g = 0; g < 16; ++g) xw[((g & 3) + 8 * (g >> 2) + 4 * h) * D + 32 * q + r] = S[ct][q][g];
-        S[ct][q] = f32x16{};
-      }
-      double* gs = gsum + (uint64_t)ct * 32 * D;
-      const int rows = K - ct * 32 < 32 ? K - ct * 32 : 32;
-      for (int i = l; i < rows * D; i += 64) {
-        const float v = xw[i];
-        if (v != 0.f) atomicAdd(gs + i, (double)v);
-      }
-    }
-    for (int c = l; c < KP; c += 64) {
-      const unsigned int v = wcnt[w][c];
-      if (v) {
-        atomicAdd(gcnt + c, (unsigned long long)v);
-        wcnt[w][c] = 0u;
-      }
-    }
-  };
-  int since = 0;
-  if (gw < tiles) load(gw, xr);
-  for (uint64_t tile = gw; tile < tiles; tile += GW) {
-    // the centroid fragments are re-read from LDS every tile: hoisted out of the loop they would
-    // pin 128 VGPRs and push the sum accumulators into scratch
-    asm volatile("" ::: "memory");
-    const uint64_t p = tile * 32 + r;
-    const bool pvalid = p < n;
-    // stage the tile for the point-major reads of the sum MFMA (a wave's LDS ops run in order)
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      *reinterpret_cast<float4*>(xw + r * kXRow + 16 * s + 8 * h) = make_float4(xr[8 * s], xr[8 * s + 1], xr[8 * s + 2], xr[8 * s + 3]);
-      *reinterpret_cast<float4*>(xw + r * kXRow + 16 * s + 8 * h + 4) =
-          make_float4(xr[8 * s + 4], xr[8 * s + 5], xr[8 * s + 6], xr[8 * s + 7]);
-    }
-    // distances: Dt[c][p] = c . x_p over 8 k-steps of 16 dims
-    f32x16 Dt[KT];
-#pragma unroll
-    for (int ct = 0; ct < KT; ++ct) Dt[ct] = f32x16{};
-    float xx = 0.f;
-    const bool more = tile + GW < tiles;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      bf16x8 xh, xm;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float v = xr[8 * s + j];
-        xx = fmaf(v, v, xx);
-        xh[j] = (__bf16)v;
-        xm[j] = (__bf16)(v - (float)xh[j]);
-      }
-      // these 8 registers are dead now: the next tile's dims of this k-step go in flight under
-      // the distance MFMAs, the argmin and the sum MFMAs (the re-rank reads the LDS copy)
-      if (more) load_part(tile + GW, s, xr);
-#pragma unroll
-      for (int ct = 0; ct < KT; ++ct) {
-        if constexpr ((DBG & 2) != 0) continue;
-        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(chi + (ct * 32 + r) * kCRow + 16 * s + 8 * h);
-        const bf16x8 am = *reinterpret_cast<const bf16x8*>(cmd + (ct * 32 + r) * kCRow + 16 * s + 8 * h);
-        Dt[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xh, Dt[ct], 0, 0, 0);
-        Dt[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xm, Dt[ct], 0, 0, 0);
-        Dt[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, xh, Dt[ct], 0, 0, 0);
-      }
-    }
-    // argmin with the runner-up, merged across the two lane halves
-    float bd = __builtin_inff(), sd = __builtin_inff();
-    int bj = 0;
-#pragma unroll
-    for (int ct = 0; ct < KT; ++ct)
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int c = ct * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
-        const float d = fmaf(-2.f, Dt[ct][g], cn[c]);
-        // c increases along the loop, so a strict < keeps the lowest index of equal values
-        sd = fminf(sd, fmaxf(bd, d));
-        bj = d < bd ? c : bj;
-        bd = fminf(bd, d);
-      }
-    {
-      const float obd = __shfl_xor(bd, 32, 64), osd = __shfl_xor(sd, 32, 64);
-      const int obj = __shfl_xor(bj, 32, 64);
-      xx += __shfl_xor(xx, 32, 64);
-      if (obd < bd || (obd == bd && obj < bj)) {
-        sd = fminf(bd, osd);
-        bd = obd;
-        bj = obj;
-      } else {
-        sd = fminf(sd, obd);
-      }
-    }
-    // near ties (estimates of the best and the runner-up closer than the error bound): flagged in
-    // bit 31 of the point's assignment; kmeans_near_list + kmeans_rerank_kernel re-rank them with
-    // exact f32 distances afterwards and move the point's contribution if the estimate was wrong
-    // (no atomics or ballots in this loop).
-    const bool near = (DBG & 4) == 0 && K > 1 && (sd - bd) <= 2.f * kKmTol * sqrtf(xx) * cmax;
-    if (!pvalid) bj = -1;
-    if (h == 0) {
-      bjs[w][r] = bj;
-      if (pvalid) {
-        atomicAdd(&wcnt[w][bj], 1u);
-        assign[p] = near ? (int32_t)((uint32_t)bj | 0x80000000u) : bj;
-      }
-    }
-    // sums: S[ct][q] += onehot^T (centroids x 16 points) . X (16 points x 32 dims), x in 3 exact parts
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int4 b0 = *reinterpret_cast<const int4*>(&bjs[w][16 * s + 8 * h]);
-      const int4 b1 = *reinterpret_cast<const int4*>(&bjs[w][16 * s + 8 * h + 4]);
-      const int bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-      bf16x8 oh[KT];
-#pragma unroll
-      for (int ct = 0; ct < KT; ++ct)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) oh[ct][j] = (bv[j] == ct * 32 + r) ? (__bf16)1.0f : (__bf16)0.0f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        bf16x8 ph, pm, pl;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float v = xw[(16 * s + 8 * h + j) * kXRow + 32 * q + r];
-          const __bf16 a0 = (__bf16)v;
-          const float r1 = v - (float)a0;
-          const __bf16 a1 = (__bf16)r1;
-          ph[j] = a0;
-          pm[j] = a1;
-          pl[j] = (__bf16)(r1 - (float)a1);
-        }
-#pragma unroll
-        for (int ct = 0; ct < KT; ++ct) {
-          if constexpr ((DBG & 1) != 0) continue;
-          S[ct][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oh[ct], ph, S[ct][q], 0, 0, 0);
-          S[ct][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oh[ct], pm, S[ct][q], 0, 0, 0);
-          S[ct][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oh[ct], pl, S[ct][q], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);   // one dim tile's operands live at a time
-      }
-    }
-    if (++since == flush_tiles) {
-      since = 0;
-      flush();
-    }
-  }
-  flush();
-}
-
-
 // K <= 64 on 16x16x32 bf16 MFMA, two workgroups per CU (mode 3, default).
 //
-// The 32x32 kernel above holds a wave's whole K x 128 sum tile in registers (496 VGPR+AGPR) and a
-// 32-point LDS tile per wave, so a CU runs one wave per SIMD and the wave's MFMA, VALU and HBM
-// waits serialise.  Here a workgroup steps over 64 points (16 per wave):
+// (A 32x32x16 kernel that held a wave's whole K x 128 sum tile in registers, 496 VGPR+AGPR, and
+// a 32-point LDS tile per wave ran one wave per SIMD, so its MFMA, VALU and HBM waits serialised.)  Here a workgroup steps over 64 points (16 per wave):
 //   distances  each wave: its 16 points x 16-centroid tiles, 3 split-bf16 MFMAs per 32 dims, the
 //              next step's loads issued per k-step as their registers free up; argmin + runner-up
 //              merged over the 4 lanes that share a point; near ties flagged as before
@@ -1026,16 +816,8 @@ void set_smem(F kern, uint32_t bytes) {
 // Mode chosen for K (exposed for tests/benchmarks): 0 = centroids + slab resident,
 // 1 = streamed centroid tiles + slab, 2 = assignment pass + sliced accumulation,
 // 3 = K <= 64 on bf16 MFMA (split-precision distances with exact re-rank, MFMA one-hot sums).
-int g_km_f32 = 0;    // dr_kmeans_set_variant: keep the exact-f32 MFMA distance path for every K
-int g_km_mfma16 = 1;  // dr_kmeans_set_variant: 0 = the 32x32 one-workgroup-per-CU kernel (tests)
-
-DR_API void dr_kmeans_set_variant(int f32_only, int mfma16) {
-  g_km_f32 = f32_only ? 1 : 0;
-  g_km_mfma16 = mfma16 ? 1 : 0;
-}
-
 DR_API int dr_kmeans_mode(int K) {
-  if (K <= 64 && !g_km_f32) return 3;
+  if (K <= 64) return 3;
   if (step_smem(K, true, true) <= kLdsBudget) return 0;
   if (step_smem(K, false, true) <= kLdsBudget) return 1;
   return 2;
@@ -1063,8 +845,7 @@ DR_API int dr_kmeans_step(const float* X, uint64_t n, int d, const float* C, int
     uint32_t* near_cnt = reinterpret_cast<uint32_t*>(near_ws);
     uint32_t* near_list = near_cnt + 4;
     kmeans_near_reset<<<1, 64, 0, s>>>(near_cnt);
-#define DR_KM3(KTV, DB) kmeans_mfma_kernel<KTV, DB><<<g3, 256, 0, s>>>(X, n, C, cnorm_ws, K, assign, gsum, gcnt, 256)
-    if (g_km_mfma16) {
+    {
       const uint64_t st = (n + kM16Pts - 1) / kM16Pts;
       const uint64_t cap = 2 * (uint64_t)num_cus();
       const unsigned g16 = (unsigned)(st < cap ? st : cap);
@@ -1074,18 +855,7 @@ DR_API int dr_kmeans_step(const float* X, uint64_t n, int d, const float* C, int
       else if (K <= 48) DR_KM16(3);
       else DR_KM16(4);
 #undef DR_KM16
-    } else if (K <= 32) {
-      DR_KM3(1, 0);
-    } else {
-      switch (dbg & 7) {
-        case 1: DR_KM3(2, 1); break;
-        case 4: DR_KM3(2, 4); break;
-        case 6: DR_KM3(2, 6); break;
-        case 7: DR_KM3(2, 7); break;
-        default: DR_KM3(2, 0); break;
-      }
     }
-#undef DR_KM3
     kmeans_near_list<<<grid_for(n, 256, 4096), 256, 0, s>>>(assign, n, near_cnt, near_list);
     kmeans_rerank_kernel<<<1024, 64, 0, s>>>(X, C, cnorm_ws, K, near_cnt, near_list, assign, gsum, gcnt, n);
     DR_LAUNCH_CHECK();

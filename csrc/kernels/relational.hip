@@ -214,49 +214,6 @@ __device__ __forceinline__ void m_atomic(uint64_t* p, uint64_t v, int op) {
   }
 }
 
-__global__ __launch_bounds__(256) void seg_reduce_multi_kernel(const E128* __restrict__ ent,
-                                                               const int64_t* __restrict__ seg, uint64_t n,
-                                                               int nagg, AggSpecs sp) {
-  const int lane = lane_id();
-  const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  const uint64_t w0 = (((uint64_t)blockIdx.x * blockDim.x) + threadIdx.x) >> 6;
-  for (uint64_t base = w0 * 64; base < n; base += waves * 64) {
-    const uint64_t i = base + lane;
-    const bool valid = i < n;
-    const int64_t s = valid ? seg[i] : -1 - (int64_t)lane;
-    const uint32_t row = valid ? (ent ? (uint32_t)ent[i].lo : (uint32_t)i) : 0u;
-    // same-segment predicates of the 6 scan steps, shared by every aggregate
-    uint32_t same = 0;
-#pragma unroll
-    for (int k = 0, d = 1; d < 64; d <<= 1, ++k) {
-      const int64_t os = __shfl_up(s, d, 64);
-      if (lane >= d && os == s) same |= 1u << k;
-    }
-    const int64_t prev = __shfl_up(s, 1, 64), next = __shfl_down(s, 1, 64);
-    bool head = lane > 0 ? prev != s : (i == 0 || !valid || seg[i - 1] != s);
-    bool end = lane < 63 ? next != s : true;
-    if (lane == 63 && valid && i + 1 < n) end = seg[i + 1] != s;
-    if (valid && i + 1 >= n) end = true;
-    const int64_t s0 = __shfl(s, 0, 64);
-    const bool h0 = __shfl(head, 0, 64);
-    const bool tail = valid && (lane == 63 || i + 1 >= n || next != s);
-    const bool plain = tail && end && (s != s0 || h0);
-    for (int a = 0; a < nagg; ++a) {
-      const int op = sp.op[a];
-      uint64_t v = 0;
-      if (valid) v = (op == M_COUNT) ? 1ull : sp.vals[a][(uint64_t)row * sp.stride[a]];
-#pragma unroll
-      for (int k = 0, d = 1; d < 64; d <<= 1, ++k) {
-        const uint64_t o = __shfl_up(v, d, 64);
-        if (same & (1u << k)) v = m_combine(v, o, op);
-      }
-      if (tail) {
-        if (plain) sp.out[a][s] = v;
-        else m_atomic(sp.out[a] + s, v, op);
-      }
-    }
-  }
-}
 
 // Thread-serial variant: each lane reduces PER consecutive sorted elements on its own (segments
 // that start and end inside the lane are written directly), and only the per-lane tail partials
@@ -625,14 +582,7 @@ DR_API int dr_seg_reduce(const void* vals, const E128* ent, const int64_t* seg, 
   return 0;
 }
 
-// seg_reduce_multi_serial (one thread walks each chunk of rows) is the default; the variant that
-// reduces each segment across a wave is kept for tests (dr_seg_reduce_set_serial(0)).
-namespace {
-int g_segred_serial = 1;
-}
-DR_API void dr_seg_reduce_set_serial(int on) { g_segred_serial = on ? 1 : 0; }
-
-// Fused multi-aggregate segmented reduce (see seg_reduce_multi_kernel).  ops/vals/outs: host
+// Fused multi-aggregate segmented reduce (seg_reduce_multi_serial: one thread walks each chunk of rows).  ops/vals/outs: host
 // arrays of nagg (<= 8) entries; outputs must be pre-filled with each op's identity.
 // strides: host array of nagg element strides (nullptr = all 1); with ent == nullptr the values
 // are already in sorted order (row = position).
@@ -671,7 +621,7 @@ DR_API int dr_seg_reduce_multi(const E128* ent, const int64_t* seg, uint64_t n, 
     }
     if (packed) sp.rows = reinterpret_cast<const uint64_t*>(base);
   }
-  if (g_segred_serial) {
+  {
     const unsigned g = grid_for(n, 256 * 8, 8192);
 #define DR_SEGRED_CASE(N)                                                             \
       case N:                                                                          \
@@ -685,8 +635,6 @@ DR_API int dr_seg_reduce_multi(const E128* ent, const int64_t* seg, uint64_t n, 
     }
 #undef DR_SEGRED_CASE
   }
-  else
-    seg_reduce_multi_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(ent, seg, n, nagg, sp);
   DR_LAUNCH_CHECK();
   return 0;
 }

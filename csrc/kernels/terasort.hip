@@ -31,7 +31,7 @@ using dr_ts::ts_record;
 // HIST (KEYS == 2): also the histograms of the four window bytes (the digits of the compact sort's
 // four LSD passes), one [4][256] partial per workgroup in hist_part, so that sort needs no
 // histogram read of its own (dr_sort_u64_onesweep with hist_part).
-template <int KEYS, bool ROWS = true, int PITCH = 25, bool HIST = false, bool NTS = false, bool NTK = false>
+template <int KEYS, bool ROWS = true, int PITCH = 25, bool HIST = false, bool NTS = false>
 __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out, uint64_t n, uint64_t first,
                                                      uint64_t seed, void* __restrict__ keys, uint32_t idx_base,
                                                      unsigned long long* __restrict__ hi_range,
@@ -62,10 +62,7 @@ __global__ __launch_bounds__(256) void ts_gen_kernel(uint32_t* __restrict__ out,
           e.lo = ((uint64_t)(bswap32(w[2]) & 0xFFFF0000u) << 32) | idx;
           static_cast<E128*>(keys)[row0 + threadIdx.x] = e;
         } else {
-          if constexpr (NTK)   // A/B value 2: the entries too
-            __builtin_nontemporal_store((hi & 0xFFFFFFFF00000000ull) | idx, static_cast<uint64_t*>(keys) + row0 + threadIdx.x);
-          else
-            static_cast<uint64_t*>(keys)[row0 + threadIdx.x] = (hi & 0xFFFFFFFF00000000ull) | idx;
+          static_cast<uint64_t*>(keys)[row0 + threadIdx.x] = (hi & 0xFFFFFFFF00000000ull) | idx;
           if constexpr (HIST) {
 #pragma unroll
             for (int p = 0; p < 4; ++p) atomicAdd(&hist[p][(uint32_t)(hi >> (32 + 8 * p)) & 0xFF], 1u);
@@ -165,6 +162,44 @@ __global__ __launch_bounds__(256) void ts_check_kernel(const uint32_t* __restric
   }
 }
 
+
+// Records first + idx[p] generated into rows p of `out` (100-byte rows back to back, 4-byte
+// aligned): the send-buffer pack of a distributed sort over gen://terasort (ops/recordsort.py),
+// idx being the bucket-ordered record offsets of dr_ts_dest_partition.  Each workgroup builds 256
+// records in LDS and streams them out with 16-byte nontemporal stores from the first 16-byte
+// boundary on (dword stores for the few words before it and after the last full chunk).
+__global__ __launch_bounds__(256) void ts_gen_gather_kernel(uint32_t* __restrict__ out, const uint32_t* __restrict__ idx,
+                                                            uint64_t n, uint64_t first, uint64_t seed) {
+  __shared__ __attribute__((aligned(16))) uint32_t img[256 * 25];
+  const uint32_t t = threadIdx.x;
+  for (uint64_t row0 = (uint64_t)blockIdx.x * 256; row0 < n; row0 += (uint64_t)gridDim.x * 256) {
+    const uint32_t rows = (uint32_t)((n - row0) < 256 ? (n - row0) : 256);
+    if (t < rows) {
+      uint32_t w[25];
+      ts_record(seed, first + idx[row0 + t], w);
+#pragma unroll
+      for (int k = 0; k < 25; ++k) img[t * 25 + k] = w[k];
+    }
+    __syncthreads();
+    uint32_t* o = out + row0 * 25;
+    const uint32_t words = rows * 25;
+    uint32_t head = (4u - (uint32_t)((reinterpret_cast<uintptr_t>(o) >> 2) & 3u)) & 3u;
+    head = head < words ? head : words;
+    if (t < head) o[t] = img[t];
+    const uint32_t nch = (words - head) >> 2;
+    for (uint32_t c = t; c < nch; c += 256) {
+      const uint32_t q = head + 4 * c;
+      uint32_t* d = o + q;
+      __builtin_nontemporal_store(img[q], d);
+      __builtin_nontemporal_store(img[q + 1], d + 1);
+      __builtin_nontemporal_store(img[q + 2], d + 2);
+      __builtin_nontemporal_store(img[q + 3], d + 3);
+    }
+    for (uint32_t q = head + 4 * nch + t; q < words; q += 256) o[q] = img[q];
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 DR_API int dr_terasort_gen(uint8_t* out, uint64_t n, uint64_t first_index, uint64_t seed, hipStream_t s) {
@@ -205,47 +240,34 @@ DR_API int dr_terasort_gen_keys64(uint8_t* out, uint64_t n, uint64_t first_index
 // the four window bytes of the entries.
 DR_API uint32_t dr_terasort_gen_hist_parts(uint64_t n) { return grid_for(n, 256, 16384); }
 
-namespace {
-int g_gen_nt = 1;   // nontemporal row stores of the pitch-128 generator (A/B: 0 plain, 2 entries too;
-                    // profiles/r3/ab_gen_nt.log: 105.8-106.2 -> 103.7-104.0 ms per step)
-}
-DR_API void dr_terasort_gen_set_nt(int v) { g_gen_nt = (v == 0 || v == 2) ? v : 1; }
-
 DR_API int dr_terasort_gen_keys64_pitch128(uint8_t* out, uint64_t n, uint64_t first_index, uint64_t seed, E64* keys,
                                            uint32_t idx_base, uint64_t* hi_range, uint32_t* hist_part, hipStream_t s) {
   if (n == 0) return 0;
   if (n + idx_base > (1ull << 32)) return (int)hipErrorInvalidValue;
   if (reinterpret_cast<uintptr_t>(out) & 15) return (int)hipErrorInvalidValue;
   const unsigned g = grid_for(n, 256, 16384);
-  if (hist_part && g_gen_nt == 2)
-    ts_gen_kernel<2, true, 32, true, true, true><<<g, 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index,
-                                                                   seed, keys, idx_base,
-                                                                   reinterpret_cast<unsigned long long*>(hi_range),
-                                                                   hist_part);
-  else if (hist_part && g_gen_nt)
+  // nontemporal row stores (profiles/r3/ab_gen_nt.log: 105.8-106.2 -> 103.7-104.0 ms per step)
+  if (hist_part)
     ts_gen_kernel<2, true, 32, true, true><<<g, 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index, seed,
                                                              keys, idx_base,
                                                              reinterpret_cast<unsigned long long*>(hi_range),
                                                              hist_part);
-  else if (hist_part)
-    ts_gen_kernel<2, true, 32, true><<<g, 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index, seed, keys,
-                                                       idx_base, reinterpret_cast<unsigned long long*>(hi_range),
-                                                       hist_part);
   else
-    ts_gen_kernel<2, true, 32><<<g, 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index, seed, keys,
-                                                 idx_base, reinterpret_cast<unsigned long long*>(hi_range));
+    ts_gen_kernel<2, true, 32, false, true><<<g, 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), n, first_index, seed,
+                                                              keys, idx_base,
+                                                              reinterpret_cast<unsigned long long*>(hi_range));
   DR_LAUNCH_CHECK();
   return 0;
 }
 
-// Entries only (the E128 layout of dr_terasort_gen_keys), no records: the distributed sort's
-// send side generates the records straight into their buckets (dr_bucket_scatter_gen_terasort).
-DR_API int dr_terasort_gen_keys_only(uint64_t n, uint64_t first_index, uint64_t seed, E128* keys, uint32_t idx_base,
-                                     uint64_t* hi_range, hipStream_t s) {
+
+// Send rows of a generated input: out row p = record first + idx[p] (see ts_gen_gather_kernel).
+DR_API int dr_terasort_gen_gather(uint8_t* out, const uint32_t* idx, uint64_t n, uint64_t first, uint64_t seed,
+                                  hipStream_t s) {
   if (n == 0) return 0;
-  if (n + idx_base > (1ull << 32)) return (int)hipErrorInvalidValue;
-  ts_gen_kernel<1, false><<<grid_for(n, 256, 16384), 256, 0, s>>>(nullptr, n, first_index, seed, keys, idx_base,
-                                                                  reinterpret_cast<unsigned long long*>(hi_range));
+  if (reinterpret_cast<uintptr_t>(out) & 3) return (int)hipErrorInvalidValue;
+  ts_gen_gather_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), idx, n, first,
+                                                               seed);
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -17,10 +17,17 @@ __device__ __forceinline__ uint32_t hex_word(uint64_t g, uint32_t k) {
   return w;
 }
 
+// The two hash words behind record g's 10-byte key: key bytes 0..7 = kA (big-endian), bytes 8..9 =
+// the top 16 bits of kB.
+__device__ __forceinline__ void ts_key_words(uint64_t seed, uint64_t g, uint64_t& kA, uint64_t& kB) {
+  kA = mix64(seed ^ mix64(g));
+  kB = mix64(kA ^ 0xD1B54A32D192ED03ull);
+}
+
 // The 25 little-endian dwords of record g, computed directly (one hash triple per record).
 __device__ __forceinline__ void ts_record(uint64_t seed, uint64_t g, uint32_t* w) {
-  const uint64_t kA = mix64(seed ^ mix64(g));
-  const uint64_t kB = mix64(kA ^ 0xD1B54A32D192ED03ull);
+  uint64_t kA, kB;
+  ts_key_words(seed, g, kA, kB);
   const uint64_t fil = mix64(g ^ (seed * 0x2545F4914F6CDD1Dull) ^ 0xF00DF00DF00DF00Dull);
   w[0] = bswap32((uint32_t)(kA >> 32));
   w[1] = bswap32((uint32_t)kA);

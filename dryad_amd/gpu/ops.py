@@ -24,6 +24,9 @@ from ..ops import sort as S
 from . import trace as TR
 from .table import DeviceTable, PartialMeta, Ported, PortTables, Shape, from_objects
 from .trace import NotTraceable
+from ..utils.log import get_logger
+
+log = get_logger("gpu.ops")
 
 E_SHAPE = Shape("tuple", ["lo", "hi"])
 
@@ -198,10 +201,11 @@ def op_read(op, inputs, v):
                 # producer-side key extraction: a following OrderBy(key bytes 0..9) starts sorting
                 rng = torch.tensor([-1, 0], dtype=torch.int64, device=rows.device)
                 if v.world.size > 1 and v.stage.id in getattr(v.runner, "lazy_gen_stages", ()):
-                    # only a fused distributed OrderBy reads this table: entries now, records
-                    # generated straight into the send buckets (or materialised if it is not fused)
-                    TSK.generate_keys_only(hi - lo, lo, int(q.get("seed", 0)), bs.bufs.ent_a, rng)
-                    bs.keys_ready = (rows.data_ptr(), hi - lo, 0, 10, rng, "e128")
+                    # only a fused distributed OrderBy reads this table: nothing is written now;
+                    # the sort's send side generates the sample keys, the range partition and the
+                    # records (into the send buckets) itself (ops/recordsort.pack_gen), any other
+                    # consumer materialises the records first
+                    bs.keys_ready = (rows.data_ptr(), hi - lo, 0, 10, None, "gen")
                     bs.lazy_gen = (lo, int(q.get("seed", 0)))
                     return t
                 if v.world.size == 1 and S.compact_sort_ok(rows, 10):
@@ -308,13 +312,17 @@ def op_read(op, inputs, v):
             else:
                 from ..io import partfile as PF
                 idx = PF.read_index(path) if path is not None else None
+                t = None
                 if idx is not None:
                     n, _nb, blk, offs = idx
-                else:            # no index sidecar: the native host scan finds the blocks
-                    host = buf.cpu().numpy()
-                    blk = CD.BLOCK
-                    n, offs = CD.block_index_host(host, dt, blk)
-                t = CD.decode_var(buf, dt, n, torch.from_numpy(offs).to(v.device), blk)
+                    try:
+                        t = CD.decode_var(buf, dt, n, torch.from_numpy(offs).to(v.device), blk)
+                    except CD.DecodeError as e:     # a sidecar that does not match the part: rebuilt
+                        log.warning("%s: %s; the block index is rebuilt from the part", path, e)
+                        idx = None
+                if idx is None:
+                    n, offs, blk = CD.block_index(buf, dt)
+                    t = CD.decode_var(buf, dt, n, offs, blk)
             if t is not None:
                 return t
     recs = prov.read_partition(uri, v.partition, op.get("dtype"))

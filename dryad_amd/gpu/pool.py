@@ -29,11 +29,12 @@ class BufferSet:
         self.in_use = False
         # set by a producer that also wrote rows_in's sort entries into bufs.ent_a:
         # (rows_in data_ptr, n, key_off, key_len, hi_range device tensor, entry format "e64" |
-        # "e128"); consumed by one sort
+        # "e128"), or the format "gen" (no entries: a lazy gen://terasort read, see lazy_gen);
+        # consumed by one sort
         self.keys_ready = None
-        # (first record, seed): rows_in holds gen://terasort records first.. that were NOT written
-        # (only their sort entries were); the distributed sort generates them straight into its
-        # send buckets, any other consumer must call materialize() first
+        # (first record, seed): rows_in holds gen://terasort records first.. that were NOT written;
+        # the distributed sort generates them straight into its send buckets, any other consumer
+        # must call materialize() first
         self.lazy_gen = None
 
     def materialize(self, n: int):
@@ -43,6 +44,8 @@ class BufferSet:
             first, seed = self.lazy_gen
             TS.generate(self.bufs.rows_in[:n], first, seed)
             self.lazy_gen = None
+            if self.keys_ready is not None and self.keys_ready[5] == "gen":
+                self.keys_ready = None
 
     def take_keys(self, rows, key_off: int, key_len: int):
         """(hi min, hi max, entry format) of the entries in ent_a for exactly these rows and key,
@@ -53,6 +56,8 @@ class BufferSet:
         ptr_, n, off, ln, rng, fmt = kr
         if ptr_ != rows.data_ptr() or n != rows.shape[0] or off != key_off or ln != key_len:
             return None
+        if rng is None:                  # "gen": no entries, the bounds are the whole key space
+            return 0, (1 << 64) - 1, fmt
         mn, mx = (int(x) & ((1 << 64) - 1) for x in rng.cpu().tolist())
         return mn, mx, fmt
 

@@ -189,4 +189,7 @@ def read_index(part_path: str):
         offs = np.frombuffer(f.read(), dtype="<u8").astype(np.int64)
     if offs.shape[0] != (n + block - 1) // block:
         return None
+    # offsets a block-parallel decoder may trust: from 0, never decreasing, inside the part
+    if offs.shape[0] and (offs[0] != 0 or (offs[1:] < offs[:-1]).any() or offs[-1] > nbytes or offs[-1] < 0):
+        return None
     return int(n), int(nbytes), int(block), offs

@@ -19,6 +19,7 @@ from dataclasses import dataclass
 import torch
 
 from ..ops import recordsort as RS
+from ..ops import sort as S
 from ..ops import terasort as TS
 from ..parallel import shuffle
 from ..parallel.comm import World, get_world
@@ -235,6 +236,120 @@ class TeraSortOOCJob:
                     resident_fraction=round(st.resident_rows / max(st.n_out, 1), 3),
                     buckets=st.buckets, resident_buckets=st.resident_buckets, chunks=st.chunks,
                     hbm_budget_gb=round(self.budget / 1e9, 1))
+
+
+class TeraSortLoopbackJob:
+    """The per-rank program of a W-rank TeraSort, run on one GPU (``bench.py --loopback-ranks W``).
+
+    Rank ``rank`` of W ranks owns records [rank * n, (rank + 1) * n) of gen://terasort and does
+    exactly what ``distributed_sort_rows`` does on a node: its sample, the separators of the W * B
+    key ranges, the send-side pack (bucket order from the generator's keys, every round's records
+    generated into the send buffer), then, per received round, the E64 extraction, the look-back
+    radix sort and the row gather with run fix-up into the output table.  The all-to-all-v is the
+    only part replaced: the bytes this rank would receive (round b = the records of EVERY source
+    rank whose key falls in this rank's b-th range, in source order) are generated into the receive
+    buffer by the same partition + generator kernels, outside the timed segments.  The other
+    ranks' samples (what the sample all-gather returns) are generated outside them too.
+
+    Timed with HIP events: (own sample) + (separators + pack) + (receive-side sorts); the phases
+    are reported separately.  Validated: the output is in order, holds exactly the received
+    records (hash sum and count), and its keys lie inside this rank's separator bounds."""
+
+    def __init__(self, cfg: TeraSortConfig, W: int, rank: int = 0, device=None):
+        self.cfg, self.W, self.rank = cfg, W, rank
+        self.n = cfg.records_per_rank
+        self.dev = torch.device(device or "cuda")
+        self.bufs = RS.SortBuffers.allocate(int(self.n * (1 + cfg.slack)), RECORD, self.dev)
+        self.B = RS.pipeline_subs(self.n * RECORD, W)
+        self.out = None
+        self.phases = {}
+        self.recv_hash = None
+        self.bounds = None
+
+    @property
+    def bytes_per_rank(self) -> int:
+        return self.n * RECORD
+
+    def _events(self):
+        return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def _receive(self, seps):
+        """The exchange, simulated: every source's pieces for this rank, generated in place."""
+        n, W, B, me, seed = self.n, self.W, self.B, self.rank, self.cfg.seed
+        idx = self.bufs.ent_b.view(-1).view(torch.int32)[:n]
+        M64 = (1 << 64) - 1
+        starts = [S.dest_partition_gen(s * n, seed, n, seps, s << 32, M64, B, W, idx).tolist() for s in range(W)]
+        cnt = [[starts[s][b * W + me + 1] - starts[s][b * W + me] for s in range(W)] for b in range(B)]
+        off = [0]
+        for b in range(B):
+            off.append(off[-1] + sum(cnt[b]))
+        if off[-1] > self.bufs.capacity:
+            raise RuntimeError(f"range partition skew: {off[-1]} rows > capacity {self.bufs.capacity}")
+        for s in range(W):
+            st = S.dest_partition_gen(s * n, seed, n, seps, s << 32, M64, B, W, idx).tolist()
+            pos = [off[b] + sum(cnt[b][:s]) for b in range(B)]
+            for b in range(B):
+                a, z = st[b * W + me], st[b * W + me + 1]
+                if z > a:
+                    TS.gen_gather(self.bufs.rows_in[pos[b]: pos[b] + z - a], idx[a:z], s * n, seed)
+        return off
+
+    def step(self):
+        n, W, B, me = self.n, self.W, self.B, self.rank
+        seed, M64 = self.cfg.seed, (1 << 64) - 1
+        dev = self.dev
+        tgt, sseed = self.cfg.sample_target, 314159
+        e = [self._events() for _ in range(3)]
+        e[0][0].record()
+        mine = RS.gen_samples((me * n, seed), n, me, me << 32, M64, tgt, sseed, dev)
+        e[0][1].record()
+        others = [RS.gen_samples((s * n, seed), n, s, s << 32, M64, tgt, sseed, dev) for s in range(W) if s != me]
+        allsamp = torch.cat(others[:me] + [mine] + others[me:])
+        e[1][0].record()
+        seps = RS.separators_from_samples(allsamp, W * B)
+        seps_hi = [int(x) & M64 for x in seps[:, 1].tolist()]
+        st, pack = RS.pack_gen(self.bufs, (me * n, seed), n, seps, me << 32, M64, B, W)
+        for b in range(B):
+            pack(b)
+        e[1][1].record()
+        off = self._receive(seps)                      # the all-to-all-v (not timed)
+        acc = TS.check(self.bufs.rows_in[: off[-1]])
+        e[2][0].record()
+        out = RS.sort_received_rounds(self.bufs, off, [off[-1]] * B, 0, seps_hi, B, me, 0, KEYLEN)
+        e[2][1].record()
+        torch.cuda.synchronize(dev)
+        self.out, self.recv_hash = out, acc
+        lo = seps[me * B - 1] if me > 0 else None
+        hi = seps[(me + 1) * B - 1] if me < W - 1 else None
+        self.bounds = (lo, hi)
+        self.phases = {"sample_ms": e[0][0].elapsed_time(e[0][1]), "separators_pack_ms": e[1][0].elapsed_time(e[1][1]),
+                       "receive_sort_ms": e[2][0].elapsed_time(e[2][1])}
+        self.sent_rows = st[-1]
+        return out
+
+    @property
+    def ms(self) -> float:
+        return sum(self.phases.values())
+
+    def validate(self) -> dict:
+        out = self.out
+        acc = TS.check(out)
+        h_in, h_out = int(self.recv_hash[0].item()), int(acc[0].item())
+        viol = int(acc[1].item())
+        ok_lo = ok_hi = True
+        if out.shape[0]:
+            first = bytes(out[0, :KEYLEN].cpu().tolist())
+            last = bytes(out[-1, :KEYLEN].cpu().tolist())
+            lo, hi = self.bounds
+
+            def sep_key(sep):
+                h, lw = (int(x) & ((1 << 64) - 1) for x in sep.tolist()[::-1])
+                return h.to_bytes(8, "big") + (lw >> 48).to_bytes(2, "big")
+            ok_lo = lo is None or first >= sep_key(lo)
+            ok_hi = hi is None or last <= sep_key(hi)
+        ok = h_in == h_out and viol == 0 and ok_lo and ok_hi
+        return dict(ok=bool(ok), hash_match=h_in == h_out, violations=viol, records=int(out.shape[0]),
+                    in_bounds=bool(ok_lo and ok_hi))
 
 
 def run_steps(job, steps: int) -> float:

@@ -37,18 +37,13 @@ _SIGS = {
     "dr_gather_rows": (c_i32, [vp, vp, vp, vp, c_u64, c_u32, vp]),
     "dr_range_dest_u128": (c_i32, [vp, vp, c_u64, vp, c_u32, c_u64, c_i32, c_u32, c_u32, vp]),
     "dr_bucket_scatter_rows": (c_i32, [vp, vp, vp, c_u64, c_u32, vp, vp, vp]),
-    "dr_bucket_scatter_gen_terasort": (c_i32, [vp, c_u64, c_u64, vp, c_u64, vp, vp, vp]),
     "dr_terasort_gen": (c_i32, [vp, c_u64, c_u64, c_u64, vp]),
     "dr_terasort_check": (c_i32, [vp, c_u64, vp, vp]),
     "dr_terasort_gen_keys": (c_i32, [vp, c_u64, c_u64, c_u64, vp, c_u32, vp, vp]),
     "dr_terasort_gen_keys64": (c_i32, [vp, c_u64, c_u64, c_u64, vp, c_u32, vp, vp]),
     "dr_terasort_gen_keys64_pitch128": (c_i32, [vp, c_u64, c_u64, c_u64, vp, c_u32, vp, vp, vp]),
     "dr_terasort_gen_hist_parts": (c_u32, [c_u64]),
-    "dr_terasort_gen_keys_only": (c_i32, [c_u64, c_u64, c_u64, vp, c_u32, vp, vp]),
     "dr_tie_fixup": (c_i32, [vp, c_u64, c_u32, vp, vp]),
-    "dr_sort_set_items": (None, [c_i32]),
-    "dr_gather_set_v4": (None, [c_i32]),
-    "dr_sort_set_scatter_v2": (None, [c_i32]),
     "dr_seg_sort_runs": (c_i32, [vp, c_u64, c_i32, c_u64, c_u64, vp, vp]),
     "dr_hi_range": (c_i32, [vp, c_u64, vp, vp]),
 }
@@ -119,6 +114,18 @@ def call(name: str, *args):
     rc = getattr(lib(), name)(*args)
     check(rc, name)
     return rc
+
+
+def written(*tensors) -> None:
+    """Record that a kernel wrote these existing tensors in place (through raw pointers, which
+    torch does not see): bumps their version counters, so caches keyed on a tensor's version
+    (column bounds in gpu/stats.py, the k-means split planes and kept sums) drop stale entries."""
+    from torch.autograd.graph import increment_version
+    for t in tensors:
+        if t is not None:
+            increment_version(t if t._base is None else t._base)
+            if t._base is not None:
+                increment_version(t)
 
 
 def require_gpu_tensor(t: torch.Tensor, what: str):

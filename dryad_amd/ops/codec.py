@@ -134,6 +134,14 @@ def block_index_host(data, dtype, block: int = BLOCK):
     return int(n), np.asarray(offs, dtype=np.int64)
 
 
+def block_index(buf: torch.Tensor, dtype, block: int = BLOCK):
+    """(records, int64 device offsets of every ``block``-th record, block) of a part of
+    variable-length records in HBM, for a part without a (valid) index sidecar."""
+    import numpy as np
+    n, offs = block_index_host(buf.cpu().numpy(), dtype, block)
+    return n, torch.from_numpy(np.ascontiguousarray(offs)).to(buf.device), block
+
+
 class DecodeError(RuntimeError):
     pass
 

@@ -136,6 +136,7 @@ def generate(points: torch.Tensor, first: int = 0, blobs: int = 64, seed: int = 
     assert points.dtype == torch.float32 and points.dim() == 2 and points.shape[1] == DIM
     _lib.call("dr_kmeans_gen", ptr(points), c_u64(points.shape[0]), DIM, c_u64(first), int(blobs),
               c_u64(seed), stream_of(points))
+    _lib.written(points)
     return points
 
 

@@ -29,6 +29,7 @@ import torch
 from ..parallel.comm import World, get_world
 from ..parallel import shuffle
 from . import sort as S
+from . import terasort as TSG
 import os as _os
 
 # local sort algorithm: "hybrid" (top-window LSD + in-LDS run sort, default), "prefix"
@@ -127,25 +128,50 @@ def local_sort_rows(rows: torch.Tensor, out: torch.Tensor, ent_a: torch.Tensor, 
     return S.gather_rows(rows, entries=srt, out=out[:n])
 
 
+def sample_count(n: int, sample_target: int) -> tuple[int, int]:
+    """(m, stride) of a rank's sample: ~0.001 of its n keys, at least min(n, 16), at most
+    sample_target (reference DryadLinqSampler.cs:38-106)."""
+    m = max(1, min(n, max(16, min(sample_target, n // 1000 if n >= 16000 else n))))
+    return m, max(1, n // m)
+
+
+def sample_offset(seed: int, rank: int, stride: int) -> int:
+    """First sampled position of a rank: deterministic given (seed, rank), so a re-executed
+    vertex draws the same sample (the reference seeds its sampler with the vertex id)."""
+    return (seed + rank * 7919) % stride if stride > 1 else 0
+
+
+def separators_from_samples(allsamp: torch.Tensor, parts: int) -> torch.Tensor:
+    """Sort every rank's sample on the GPU and pick ``parts`` - 1 evenly spaced separators."""
+    total = allsamp.shape[0]
+    scratch = torch.empty_like(allsamp)
+    srt = S.sort_entries(allsamp.contiguous(), 0, 128, tmp=scratch)
+    pos = torch.tensor([(j * total) // parts for j in range(1, parts)], dtype=torch.int64, device=srt.device)
+    return srt.index_select(0, pos).contiguous()
+
+
 def choose_separators(entries: torch.Tensor, n: int, world: World, lo_mask: int, sample_target: int,
                       seed: int, tmp: torch.Tensor, parts: int | None = None) -> torch.Tensor:
     """Sampler (reference DryadLinqSampler.cs:38-246): per-rank stride sample at ~0.001 (at least
     min(n, 16) keys, at most sample_target), all-gathered, sorted on the GPU, ``parts``-1
     (default world-1) separators at evenly spaced ranks.  Deterministic given (rank, n, seed)."""
     parts = parts or world.size
-    m = max(1, min(n, max(16, min(sample_target, n // 1000 if n >= 16000 else n))))
-    stride = max(1, n // m)
-    off = (seed + world.rank * 7919) % stride if stride > 1 else 0
+    m, stride = sample_count(n, sample_target)
+    off = sample_offset(seed, world.rank, stride)
     samp = entries[off: off + stride * m: stride][:m].clone()
     # keep only key bits in lo
     samp[:, 0] = samp[:, 0] & _as_i64(lo_mask)
-    allsamp = shuffle.all_gather_varlen(samp, world)
-    total = allsamp.shape[0]
-    scratch = torch.empty_like(allsamp)
-    srt = S.sort_entries(allsamp.contiguous(), 0, 128, tmp=scratch)
-    pos = torch.tensor([(j * total) // parts for j in range(1, parts)], dtype=torch.int64,
-                       device=srt.device)
-    return srt.index_select(0, pos).contiguous()
+    return separators_from_samples(shuffle.all_gather_varlen(samp, world), parts)
+
+
+def gen_samples(gen: tuple[int, int], n: int, rank: int, lo_or: int, lo_mask: int, sample_target: int,
+                seed: int, device) -> torch.Tensor:
+    """``choose_separators``' sample of one rank over gen://terasort records gen[0] .. gen[0] + n - 1,
+    generated at the sampled positions (the same entries as sampling a generated entry table)."""
+    m, stride = sample_count(n, sample_target)
+    samp = TSG.sample_keys(gen[0], gen[1], sample_offset(seed, rank, stride), stride, m, lo_or, device)
+    samp[:, 0] = samp[:, 0] & _as_i64(lo_mask)
+    return samp
 
 
 def rank_hi_bounds(seps: torch.Tensor, rank: int) -> tuple[int, int]:
@@ -205,24 +231,27 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     ``split_ties``: runs of equal keys may be split over ranks (skew); keeps the global order but
     not the co-location of equal keys, so the planner turns it off (keep_ties) when a consumer
     relies on the output being partitioned by the key.  ``gen = (first, seed)``: ``rows_in`` was
-    never written; row i is gen://terasort record first + i (``keys_ready`` E128 entries required),
-    generated by the send-buffer pack itself.
+    never written; row i is gen://terasort record first + i, and the send side works from the
+    generator alone (``keys_fmt`` "gen": no entries either; see ``pack_gen``).
 
     With several ranks the exchange is pipelined with the local sort.  The sampled separators cut
-    the key space into ``W * B`` ranges, B consecutive ones per destination rank.  One bucket
-    scatter packs the rows round-major (round b = every rank's b-th range), and the B rounds are
-    queued as RCCL all-to-all-v collectives up front.  Rank r receives round b as one contiguous
-    block holding ALL rows of its key range b, so it extracts + radix-sorts range b while rounds
-    b+1.. are still on the wire, and gathers the sorted rows into ``rows_out`` as soon as the
-    send region under them has gone out.  Only the last range's sort is exposed after the
-    exchange (reference: the sampler + RangePartition + MergeSort stages of
-    DryadLinqQueryGen.cs:2362-2474, CrossProduct channels GraphBuilder.cs:481-504)."""
+    the key space into ``W * B`` ranges, B consecutive ones per destination rank, and the send
+    buffer is packed round-major (round b = every rank's b-th range), each round queued as an RCCL
+    all-to-all-v as soon as its rows are packed.  Rank r receives round b as one contiguous block
+    holding ALL rows of its key range b, so it sorts range b while rounds b+1.. are still on the
+    wire, and gathers the sorted rows into ``rows_out`` as soon as the send region under them has
+    gone out (``sort_received_rounds``).  Only the last range's sort is exposed after the exchange
+    (reference: the sampler + RangePartition + MergeSort stages of DryadLinqQueryGen.cs:2362-2474,
+    CrossProduct channels GraphBuilder.cs:481-504)."""
     w = world or get_world()
     rows = bufs.rows_in[:n]
-    if gen is not None and (w.size == 1 or not keys_ready or keys_fmt != "e128"):
-        from . import terasort as TS
-        TS.generate(rows, gen[0], gen[1])       # the fused pack needs the E128 entries of a real exchange
+    gen_path = gen is not None and w.size > 1 and key_off == 0 and key_len == TSG.KEY_BYTES \
+        and rows.shape[1] == TSG.RECORD_BYTES and n < (1 << 31)
+    if gen is not None and not gen_path:
+        TSG.generate(rows, gen[0], gen[1])       # the records are needed after all
         gen = None
+        if keys_fmt == "gen":
+            keys_ready = False
     if w.size == 1:
         out = local_sort_rows(rows, bufs.rows_out, bufs.ent_a, bufs.ent_b, key_off, key_len,
                               hi_bounds=hi_bounds, keys_ready=keys_ready, keys_fmt=keys_fmt)
@@ -230,28 +259,33 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
             stats.n_in = stats.n_out = n
         return out
     W, stride = w.size, rows.shape[1]
-    if keys_fmt != "e128":
-        keys_ready = False
-    ent = bufs.ent_a[:n] if keys_ready else S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
     _, _, lo_mask = key_bits(key_len)
-    part_mask = lo_mask
-    if split_ties and key_len <= 10 and W < (1 << 16):
-        # skew: equal keys must not all land on one rank.  Bits 47..32 of lo are free for keys of
-        # <= 10 bytes; with the rank there (and the row index below it) every entry is unique, so
-        # the sampled separators split runs of equal keys across ranks while the global order
-        # (key, rank, row) stays a valid OrderBy order.
-        ent[:, 0].bitwise_or_(w.rank << 32)
-        part_mask = (1 << 64) - 1
+    split = split_ties and key_len <= 10 and W < (1 << 16)
+    # skew: equal keys must not all land on one rank.  Bits 47..32 of lo are free for keys of
+    # <= 10 bytes; with the rank there (and the row index below it) every entry is unique, so the
+    # sampled separators split runs of equal keys across ranks while the global order (key, rank,
+    # row) stays a valid OrderBy order.
+    part_mask = _M64 if split else lo_mask
+    lo_or = (w.rank << 32) if split else 0
     nmax = torch.tensor([n], dtype=torch.int64, device=w.device)
     shuffle.all_reduce_(nmax, "max", w)
     B = pipeline_subs(int(nmax.item()) * stride, W)
-    seps = choose_separators(ent, n, w, part_mask, sample_target, seed, bufs.ent_b, parts=W * B)
-    seps_hi = [int(x) & _M64 for x in seps[:, 1].tolist()]
-    S.range_dest(ent, seps, part_mask, subs=B, ranks=W)                  # ent.hi := b * W + rank
-    if gen is not None:                                                  # send buffer, round-major
-        st = S.bucket_scatter_gen_terasort(ent, n, gen[0], gen[1], bufs.rows_out)
+    pack = None
+    if gen_path:
+        seps = separators_from_samples(
+            shuffle.all_gather_varlen(gen_samples(gen, n, w.rank, lo_or, part_mask, sample_target, seed, w.device), w),
+            W * B)
+        st, pack = pack_gen(bufs, gen, n, seps, lo_or, part_mask, B, W)
     else:
-        st = S.bucket_scatter_rows(ent, rows, bufs.rows_out)
+        if keys_fmt != "e128":
+            keys_ready = False
+        ent = bufs.ent_a[:n] if keys_ready else S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
+        if split:
+            ent[:, 0].bitwise_or_(lo_or)
+        seps = choose_separators(ent, n, w, part_mask, sample_target, seed, bufs.ent_b, parts=W * B)
+        S.range_dest(ent, seps, part_mask, subs=B, ranks=W)                  # ent.hi := b * W + rank
+        st = S.bucket_scatter_rows(ent, rows, bufs.rows_out)                # send buffer, round-major
+    seps_hi = [int(x) & _M64 for x in seps[:, 1].tolist()]
     send = [[st[b * W + r + 1] - st[b * W + r] for r in range(W)] for b in range(B)]
     sc = torch.tensor([[send[b][r] for b in range(B)] for r in range(W)], dtype=torch.int64)
     rc = shuffle.exchange_counts(sc.flatten(), w).view(W, B).tolist()    # rc[src][b]
@@ -262,54 +296,92 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     if n_recv > bufs.capacity:
         raise RuntimeError(f"range partition skew: rank {w.rank} receives {n_recv} rows > capacity {bufs.capacity}")
     send_flat, recv_flat = bufs.rows_out.view(-1), bufs.rows_in.view(-1)
-    handles = [shuffle.alltoallv_bytes_async(
-        send_flat[st[b * W] * stride: st[(b + 1) * W] * stride], [c * stride for c in send[b]],
-        recv_flat[off[b] * stride: off[b + 1] * stride], [rc[s][b] * stride for s in range(W)], w)
-        for b in range(B)]
-    out = bufs.rows_out
-    pending, fixups = [], []
-    e64a, e64b = bufs.ent_a.view(-1), bufs.ent_b.view(-1)
-    compact = S.compact_sort_ok(bufs.rows_in[:2], key_len)
+    handles = []
     for b in range(B):
-        shuffle.wait(handles[b])
-        a, z = off[b], off[b + 1]
-        if z > a:
-            hb = _range_hi_bounds(seps_hi, w.rank * B + b)
-            if compact and z - a >= 2:
-                # compact sort of this key range; its gather (with the run fix-up) is deferred
-                # like the full-key path's
-                r = bufs.rows_in[a:z]
-                P = min(S.common_prefix_bits(*hb), 8 * key_len)
-                e = S.extract_keys64(r, key_off, key_len, P, e64a[a:z])
-                win = min(S.window_bits64(z - a), max(8, ((8 * key_len - P + 7) // 8) * 8), 32)
-                pending.append((a, z, ("e64", S.sort_entries64(e, e64b[a:z], win), win)))
-            else:
-                srt = _sort_keys(bufs.rows_in[a:z], bufs.ent_a[a:z], bufs.ent_b[a:z], key_off, key_len, hb)
-                pending.append((a, z, ("e128", srt, 0)))
-        # rows_out[:sent] has been sent (rounds <= b are complete); rows_out[n:] never held data
-        sent = st[(b + 1) * W]
-        keep = []
-        for a2, z2, (fmt, s2, win) in pending:
-            if b == B - 1 or z2 <= sent or a2 >= n:
-                if fmt == "e64":
-                    flag = torch.zeros(1, dtype=torch.int32, device=out.device)
-                    S.gather_fixup(bufs.rows_in[a2:z2], s2, out[a2:z2], key_off, key_len, win, flag)
-                    fixups.append((a2, z2, flag))
-                else:
-                    S.gather_rows(bufs.rows_in[a2:z2], entries=s2, out=out[a2:z2])
-            else:
-                keep.append((a2, z2, (fmt, s2, win)))
-        pending = keep
-    if fixups:
-        flags = torch.cat([f for _, _, f in fixups]).tolist()
-        S.onesweep_check(out.device)
-        for (a2, z2, _), bad in zip(fixups, flags):
-            if bad:     # a run of equal windows too long for the fix-up: full-key sort of the range
-                srt = _sort_keys(bufs.rows_in[a2:z2], bufs.ent_a[a2:z2], bufs.ent_b[a2:z2], key_off, key_len,
-                                 None)
-                S.gather_rows(bufs.rows_in[a2:z2], entries=srt, out=out[a2:z2])
+        if pack is not None:
+            pack(b)                    # round b's rows packed (compute stream) before it is queued
+        handles.append(shuffle.alltoallv_bytes_async(
+            send_flat[st[b * W] * stride: st[(b + 1) * W] * stride], [c * stride for c in send[b]],
+            recv_flat[off[b] * stride: off[b + 1] * stride], [rc[s][b] * stride for s in range(W)], w))
+    out = sort_received_rounds(bufs, off, [st[(b + 1) * W] for b in range(B)], n, seps_hi, B, w.rank, key_off,
+                               key_len, wait=lambda b: shuffle.wait(handles[b]))
     if stats is not None:
         stats.n_in, stats.n_out, stats.rounds = n, n_recv, B
         stats.send_counts = [sum(send[b][r] for b in range(B)) for r in range(W)]
         stats.recv_counts = [sum(rc[s]) for s in range(W)]
     return out[:n_recv]
+
+
+def pack_gen(bufs: SortBuffers, gen: tuple[int, int], n: int, seps: torch.Tensor, lo_or: int, lo_mask: int,
+             B: int, W: int):
+    """Send side over gen://terasort records gen[0] .. gen[0] + n - 1: the records' bucket order
+    from the generator's keys (``dest_partition_gen``: 32-bit offsets into the first 4n bytes of
+    ``bufs.ent_a``), then a packer generating round b's records into their send rows.  Returns
+    (bucket starts as a host list, pack(b)).  The offsets are dead once every round is packed, so
+    the receive side may reuse ``ent_a`` after the last pack (stream order)."""
+    idx = bufs.ent_a.view(-1).view(torch.int32)[:n]
+    st = S.dest_partition_gen(gen[0], gen[1], n, seps, lo_or, lo_mask, B, W, idx).tolist()
+
+    def pack(b: int):
+        a, z = st[b * W], st[(b + 1) * W]
+        if z > a:
+            TSG.gen_gather(bufs.rows_out[a:z], idx[a:z], gen[0], gen[1])
+    return st, pack
+
+
+def sort_received_rounds(bufs: SortBuffers, off: list, sent_after: list, n_sent: int, seps_hi: list, B: int,
+                         rank: int, key_off: int, key_len: int, wait=None) -> torch.Tensor:
+    """Receive side of the pipelined range shuffle: round b's block ``rows_in[off[b]:off[b+1]]``
+    holds all rows of this rank's key range b.  Each is sorted as it arrives (``wait(b)``): E64
+    entries of the rows read through LDS with the look-back sort's histograms fused in, the
+    look-back radix sort, then the row gather with the run fix-up into ``rows_out[off[b]:...]``,
+    deferred until the send rows under it have gone out (``sent_after[b]`` = send rows complete
+    after round b; rows past ``n_sent`` never held data).  A look-back failure or a run too long
+    for the fix-up is redone after the last round (count + scatter sort, or the full-key sort)."""
+    out = bufs.rows_out
+    e64a, e64b = bufs.ent_a.view(-1), bufs.ent_b.view(-1)
+    compact = S.compact_sort_ok(bufs.rows_in[:2], key_len)
+    flags = torch.zeros((B, 2), dtype=torch.int32, device=out.device)     # [gather overflow, look-back error]
+    pending, compact_rounds = [], []
+    for b in range(B):
+        if wait is not None:
+            wait(b)
+        a, z = off[b], off[b + 1]
+        if z > a:
+            hb = _range_hi_bounds(seps_hi, rank * B + b)
+            if compact and z - a >= 2:
+                r = bufs.rows_in[a:z]
+                P = min(S.common_prefix_bits(*hb), 8 * key_len)
+                win = min(S.window_bits64(z - a), max(8, ((8 * key_len - P + 7) // 8) * 8), 32)
+                e, hist = S.extract_keys64_tile(r, key_off, key_len, P, e64a[a:z], hist=True)
+                srt = S.sort_entries64(e, e64b[a:z], win, gen_hist=hist, err=flags[b, 1:])
+                pending.append((a, z, b, ("e64", srt, win)))
+                compact_rounds.append((a, z, b, P, win))
+            else:
+                srt = _sort_keys(bufs.rows_in[a:z], bufs.ent_a[a:z], bufs.ent_b[a:z], key_off, key_len, hb)
+                pending.append((a, z, b, ("e128", srt, 0)))
+        keep = []
+        for a2, z2, b2, (fmt, s2, win) in pending:
+            if b == B - 1 or z2 <= sent_after[b] or a2 >= n_sent:
+                if fmt == "e64":
+                    S.gather_fixup(bufs.rows_in[a2:z2], s2, out[a2:z2], key_off, key_len, win, flags[b2, :1])
+                else:
+                    S.gather_rows(bufs.rows_in[a2:z2], entries=s2, out=out[a2:z2])
+            else:
+                keep.append((a2, z2, b2, (fmt, s2, win)))
+        pending = keep
+    if compact_rounds:
+        fl = flags.tolist()
+        for a2, z2, b2, P, win in compact_rounds:
+            overflow, failed = fl[b2][0] != 0, fl[b2][1] != 0
+            r = bufs.rows_in[a2:z2]
+            if failed:        # the look-back sort failed: the entries again, count + scatter passes
+                e = S.extract_keys64(r, key_off, key_len, P, e64a[a2:z2])
+                srt = S.sort_entries64(e, e64b[a2:z2], win, lookback=False)
+                flag = torch.zeros(1, dtype=torch.int32, device=out.device)
+                S.gather_fixup(r, srt, out[a2:z2], key_off, key_len, win, flag)
+                overflow = int(flag.item()) != 0
+            if overflow:      # a run of equal windows too long for the fix-up: full-key sort of the range
+                srt = _sort_keys(r, bufs.ent_a[a2:z2], bufs.ent_b[a2:z2], key_off, key_len, None)
+                S.gather_rows(r, entries=srt, out=out[a2:z2])
+    return out[: off[-1]]

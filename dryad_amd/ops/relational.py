@@ -205,6 +205,7 @@ def gen_records64_rows(out: torch.Tensor, first: int, nkeys: int, seed: int, dim
     assert out.dtype == torch.int64 and out.dim() == 2
     _lib.call("dr_gen_records64_rows", ptr(out), out.shape[1], c_u64(out.shape[0]), c_u64(first), c_u64(nkeys),
               c_u64(seed & (2**64 - 1)), c_u64(dim_mult), stream_of(out))
+    _lib.written(out)
     return out
 
 
@@ -218,6 +219,7 @@ def gen_records64(cols: list, first: int, nkeys: int, seed: int, dim_mult: int =
     ptrs = torch.tensor([c.data_ptr() for c in cols], dtype=torch.int64, device=cols[0].device)
     _lib.call("dr_gen_records64", ptr(ptrs), len(cols), c_u64(n), c_u64(first), c_u64(nkeys),
               c_u64(seed & (2**64 - 1)), c_u64(dim_mult), stream_of(cols[0]))
+    _lib.written(*cols)
     return cols
 
 

@@ -8,6 +8,7 @@ of ``lo`` (key-pointer sort).  Fixed-width record tables are ``uint8`` tensors `
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import torch
 
@@ -154,18 +155,6 @@ def sort_entries_hybrid(entries: torch.Tensor, begin_bit: int, end_bit: int = 12
     return sort_entries(srt, begin_bit, 128, other[:n])
 
 
-def set_sort_items(items: int):
-    _lib.lib().dr_sort_set_items(int(items))
-
-
-def set_scatter_v2(on: bool):
-    _lib.lib().dr_sort_set_scatter_v2(int(bool(on)))
-
-
-def set_gather_v4(on: bool):
-    _lib.lib().dr_gather_set_v4(int(bool(on)))
-
-
 def partition_pass(entries: torch.Tensor, shift: int, out: torch.Tensor | None = None):
     """One stable counting-sort pass on the byte digit at ``shift``.
 
@@ -247,20 +236,6 @@ def bucket_scatter_rows(entries: torch.Tensor, rows: torch.Tensor, out: torch.Te
     return starts.tolist() if sync else starts
 
 
-def bucket_scatter_gen_terasort(entries: torch.Tensor, n: int, first: int, seed: int, out: torch.Tensor,
-                                sync: bool = True):
-    """``bucket_scatter_rows`` for a gen://terasort input whose records were never stored: entry i
-    (row order) stands for record ``first + i``, which the kernel generates straight into its
-    bucket of ``out`` (dr_bucket_scatter_gen_terasort)."""
-    _lib.require_gpu_tensor(out, "bucket_scatter_gen_terasort")
-    assert out.dtype == torch.uint8 and out.shape[1] == 100 and out.shape[0] >= n and entries.shape[0] >= n
-    starts = torch.empty(257, dtype=torch.int64, device=out.device)
-    ws = _workspace(n, out.device)
-    _lib.call("dr_bucket_scatter_gen_terasort", ptr(entries), c_u64(first), c_u64(seed & (2**64 - 1)), ptr(out),
-              c_u64(n), ptr(ws), ptr(starts), stream_of(out))
-    return starts.tolist() if sync else starts
-
-
 def entries_to_key_int(entries: torch.Tensor, lo_keep_bits: int = 64):
     """Host helper for tests: composite keys as Python ints (hi<<64 | lo masked)."""
     e = entries.cpu().numpy()
@@ -288,7 +263,7 @@ _lib.register_signatures({
     "dr_sort_u64_onesweep_workspace": (c_u64, [c_u64]),
     "dr_sort_u64_onesweep": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u64, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_void_p, c_u64, ctypes.c_void_p, c_u32, ctypes.c_void_p,
-                                            ctypes.POINTER(ctypes.c_int)]),
+                                            ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
 })
 # expected entries per run the compact sort sizes its window for (window = smallest multiple of 8
 # bits, at most 32, with n <= RUN_TARGET64 * 2^window)
@@ -336,52 +311,62 @@ def _onesweep_workspace(n: int, device) -> torch.Tensor:
     return ws
 
 
-def onesweep_check(device) -> None:
-    """Raise if a look-back of the last single-histogram sort on ``device`` gave up (its error word
-    at byte 64 of the workspace); synchronises with the stream."""
-    ws = _OS_CACHE.get(device)
-    if ws is not None and int(ws[64:68].view(torch.int32).item()) != 0:
-        raise RuntimeError("dr_sort_u64_onesweep: a look-back spin gave up; the sort result is invalid")
+def lookback_error() -> torch.Tensor:
+    """A fresh device flag for ``sort_entries64(err=...)`` (int32 [1], zero)."""
+    return torch.zeros(1, dtype=torch.int32, device=torch.cuda.current_device())
 
 
 _GEN_HIST: dict = {}
+_GEN_HIST_LOCK = threading.Lock()
 
 
 def gen_hist_buffer(parts: int, device) -> torch.Tensor:
-    """Per-workgroup [4][256] window-digit histograms a producer of E64 entries writes (uint32)."""
-    buf = _OS_CACHE.get(("gen_hist", device))
-    if buf is None or buf.numel() < parts * 1024:
-        buf = torch.empty(parts * 1024, dtype=torch.int32, device=device)
-        _OS_CACHE[("gen_hist", device)] = buf
-    return buf[: parts * 1024]
+    """Per-workgroup [4][256] window-digit histograms a producer of E64 entries writes (int32).
+    A buffer of its own per producer call: two jobs on one device never share one."""
+    return torch.empty(parts * 1024, dtype=torch.int32, device=device)
 
 
 def note_gen_hist(keys: torch.Tensor, n: int, part: torch.Tensor | None) -> None:
-    """Record that ``part`` holds the window histograms of ``keys[:n]`` (None: forget any)."""
-    if part is None:
-        _GEN_HIST.pop(keys.device, None)
-    else:
-        _GEN_HIST[keys.device] = (keys.data_ptr(), n, part)
+    """Record that ``part`` holds the window histograms of ``keys[:n]`` (None: forget them).  The
+    record keeps ``keys`` alive, so its address cannot be reused by other entries meanwhile."""
+    k = (keys.device, keys.data_ptr())
+    with _GEN_HIST_LOCK:
+        if part is None:
+            _GEN_HIST.pop(k, None)
+            return
+        _GEN_HIST[k] = (keys, n, part)
+        while len(_GEN_HIST) > 8:                 # producers whose sort never came: drop the oldest
+            _GEN_HIST.pop(next(iter(_GEN_HIST)))
 
 
 def take_gen_hist(e: torch.Tensor):
     """The producer histograms of the entries ``e`` if they are still the generated ones (one use)."""
-    h = _GEN_HIST.pop(e.device, None)
-    if h is not None and h[0] == e.data_ptr() and h[1] == e.shape[0]:
+    with _GEN_HIST_LOCK:
+        h = _GEN_HIST.pop((e.device, e.data_ptr()), None)
+    if h is not None and h[1] == e.shape[0]:
         return h[2]
     return None
 
 
-def sort_entries64(e: torch.Tensor, tmp: torch.Tensor, win: int, gen_hist: torch.Tensor | None = None) -> torch.Tensor:
+def sort_entries64(e: torch.Tensor, tmp: torch.Tensor, win: int, gen_hist: torch.Tensor | None = None,
+                   err: torch.Tensor | None = None, lookback: bool = True) -> torch.Tensor:
     """Stable LSD sort of E64 entries on their top ``win`` window bits.  ``gen_hist``: the window
-    digit histograms of ``e``'s 32-bit key window written by its producer (take_gen_hist)."""
+    digit histograms of ``e``'s 32-bit key window written by its producer (take_gen_hist).
+
+    At least ONESWEEP_MIN entries take the look-back sort unless ``lookback`` is False (then, like
+    smaller sorts, the count + scatter passes).  A look-back sort can fail (a spin gave up, or the
+    histograms do not count the entries): it then ORs a non-zero code into ``err`` (a device int32
+    flag, see lookback_error; required for look-back sorts) and leaves the entries unsorted and
+    reordered, so the caller rebuilds them from the rows and sorts again with ``lookback=False``."""
     n = e.shape[0]
     flag = ctypes.c_int(0)
-    if n >= ONESWEEP_MIN:
+    if lookback and n >= ONESWEEP_MIN:
+        if err is None:
+            raise ValueError("sort_entries64: a look-back sort needs an error flag (err=lookback_error())")
         ws = _onesweep_workspace(n, e.device)
         parts = 0 if gen_hist is None else gen_hist.numel() // 1024
         _lib.call("dr_sort_u64_onesweep", ptr(e), ptr(tmp), c_u64(n), 64 - win, 64, ptr(ws), c_u64(ws.numel()),
-                  ptr(gen_hist), c_u32(parts), stream_of(e), ctypes.byref(flag))
+                  ptr(gen_hist), c_u32(parts), ptr(err), stream_of(e), ctypes.byref(flag))
     else:
         ws = _workspace(n, e.device)
         _lib.call("dr_sort_u64", ptr(e), ptr(tmp), c_u64(n), 64 - win, 64, ptr(ws), stream_of(e), ctypes.byref(flag))
@@ -423,13 +408,20 @@ def sort_rows_compact(rows: torch.Tensor, out: torch.Tensor, ent: torch.Tensor, 
         else:
             e = extract_keys64(rows, key_off, key_len, P, ent)
     win = min(window_bits64(n), max(8, ((8 * key_len - P + 7) // 8) * 8), 32)
-    srt = sort_entries64(e, tmp, win)
-    flag = torch.zeros(1, dtype=torch.int32, device=rows.device)
-    gather_fixup(rows, srt, out, key_off, key_len, win, flag)
+    flags = torch.zeros(2, dtype=torch.int32, device=rows.device)        # [gather overflow, look-back error]
+    srt = sort_entries64(e, tmp, win, err=flags[1:])
+    gather_fixup(rows, srt, out, key_off, key_len, win, flags[:1])
     if stats is not None:
         stats["path"] = f"compact win={win} prefix={P}"
-    overflow = int(flag.item()) != 0
-    onesweep_check(rows.device)
+    overflow, failed = (int(x) != 0 for x in flags.tolist())
+    if failed:              # the look-back sort failed: the entries again, count + scatter passes
+        e = extract_keys64(rows, key_off, key_len, P, ent)
+        srt = sort_entries64(e, tmp, win, lookback=False)
+        flags.zero_()
+        gather_fixup(rows, srt, out, key_off, key_len, win, flags[:1])
+        overflow = int(flags[0].item()) != 0
+        if stats is not None:
+            stats["path"] += " look-back failed: count+scatter"
     if overflow:
         if stats is not None:
             stats["path"] += " overflow"
@@ -448,6 +440,52 @@ def _hi_range64(e: torch.Tensor, chunk: int = 1 << 26) -> tuple[int, int]:
         maxs.append(w.max())
     mn, mx = int(torch.stack(mins).min().item()), int(torch.stack(maxs).max().item())
     return mn << 32, mx << 32
+
+
+_lib.register_signatures({
+    "dr_ts_dest_workspace": (c_u64, [c_u64]),
+    "dr_ts_dest_partition": (ctypes.c_int, [c_u64, c_u64, c_u64, ctypes.c_void_p, c_u32, c_u64, c_u64, c_u32, c_u32,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "dr_extract_keys64_tile_parts": (c_u32, [c_u64]),
+    "dr_extract_keys64_tile": (ctypes.c_int, [ctypes.c_void_p, c_u64, c_u32, c_u32, c_u32, c_u32, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p]),
+})
+
+
+def dest_partition_gen(first: int, seed: int, n: int, seps: torch.Tensor, lo_or: int, lo_mask: int, subs: int,
+                       ranks: int, idx: torch.Tensor) -> torch.Tensor:
+    """Range partition of gen://terasort records ``first .. first + n - 1`` without entries
+    (dr_ts_dest_partition): ``idx[:n]`` (int32) receives the slice offsets in bucket order, stable;
+    returns the 257 bucket starts (device int64).  Buckets as ``range_dest``: the count of
+    ``seps`` below the key {hi, (lo | lo_or) & lo_mask}, renumbered round-major with ``subs``."""
+    assert idx.dtype == torch.int32 and idx.numel() >= n and seps.dtype == torch.int64
+    starts = torch.empty(257, dtype=torch.int64, device=idx.device)
+    ws = _dest_workspace(n, idx.device)
+    seps = seps.contiguous()
+    _lib.call("dr_ts_dest_partition", c_u64(first), c_u64(seed & _M64), c_u64(n), ptr(seps), c_u32(seps.shape[0]),
+              c_u64(lo_or & _M64), c_u64(lo_mask & _M64), c_u32(subs), c_u32(ranks), ptr(ws), ptr(idx), ptr(starts),
+              stream_of(idx))
+    return starts
+
+
+def _dest_workspace(n: int, device) -> torch.Tensor:
+    nbytes = int(_lib.lib().dr_ts_dest_workspace(c_u64(max(n, 1))))
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+
+
+def extract_keys64_tile(rows: torch.Tensor, key_off: int, key_len: int, prefix_bits: int, out: torch.Tensor,
+                        hist: bool = False):
+    """``extract_keys64`` reading whole rows through LDS (dr_extract_keys64_tile); ``hist``: also
+    the window-digit histograms a following look-back sort takes instead of its histogram read.
+    Returns (entries, histograms or None)."""
+    _lib.require_gpu_tensor(rows, "extract_keys64_tile")
+    n, stride = rows.shape
+    part = None
+    if hist and n >= ONESWEEP_MIN:
+        part = gen_hist_buffer(int(_lib.lib().dr_extract_keys64_tile_parts(c_u64(n))), rows.device)
+    _lib.call("dr_extract_keys64_tile", ptr(rows), c_u64(n), c_u32(stride), c_u32(key_off), c_u32(key_len),
+              c_u32(prefix_bits), ptr(out), ptr(part), stream_of(rows))
+    return out[:n], part
 
 
 # ------------------------------------------------------------------------------------------------
@@ -478,9 +516,10 @@ def rekey64(rows: torch.Tensor, ent: torch.Tensor, key_off: int, key_len: int, P
     return ent
 
 
-def _sort64_into(e: torch.Tensor, tmp: torch.Tensor, win: int, gen_hist=None) -> torch.Tensor:
+def _sort64_into(e: torch.Tensor, tmp: torch.Tensor, win: int, gen_hist=None, err=None,
+                 lookback: bool = True) -> torch.Tensor:
     """sort_entries64 whose result always ends in ``e`` (``tmp`` may alias the gather's output)."""
-    srt = sort_entries64(e, tmp, win, gen_hist)
+    srt = sort_entries64(e, tmp, win, gen_hist, err=err, lookback=lookback)
     if srt.data_ptr() != e.data_ptr():
         e.copy_(srt)
     return e
@@ -506,17 +545,22 @@ def sort_rows_pitch128(rows_p: torch.Tensor, out: torch.Tensor, keys: torch.Tens
     tmp = out.view(-1)[: n * 8].view(torch.int64)
     e = keys[:n]
     gen_hist = take_gen_hist(e) if keys_ready else None
-    flag = torch.zeros(1, dtype=torch.int32, device=rows_p.device)
+    flags = torch.zeros(2, dtype=torch.int32, device=rows_p.device)      # [gather overflow, look-back error]
+    flag = flags[:1]
     path = "compact pitch128"
+    lookback = True
     if keys_ready and key_off == 0:
         win = min(window_bits64(n), max(8, ((8 * key_len + 7) // 8) * 8), 32)
-        _sort64_into(e, tmp, win, gen_hist)
+        _sort64_into(e, tmp, win, gen_hist, err=flags[1:])
         if gen_hist is not None and n >= ONESWEEP_MIN:
             path += " gen-hist"
         gather_fixup_pitch128(rows_p, e, out[:n], key_off, key_len, win, flag)
         path += f" win={win}"
-        chain = int(flag.item()) != 0
-        onesweep_check(rows_p.device)
+        overflow, failed = (int(x) != 0 for x in flags.tolist())
+        chain = overflow or failed
+        if failed:          # the entries are lost: rebuilt from the rows by the chain below
+            lookback = False
+            path += " look-back failed"
     else:
         torch.arange(n, out=e)                  # entries = row index; windows come from the rows
         chain = True
@@ -525,13 +569,22 @@ def sort_rows_pitch128(rows_p: torch.Tensor, out: torch.Tensor, keys: torch.Tens
         windows = list(range(max(0, bits - 32), -1, -32))
         if windows[-1] != 0:
             windows.append(0)
+        if not lookback:
+            torch.arange(n, out=e)
+        flags.zero_()
         for P in windows:                       # least significant window first
             rekey64(rows_p, e, key_off, key_len, P)
-            _sort64_into(e, tmp, 32)
+            _sort64_into(e, tmp, 32, err=flags[1:], lookback=lookback)
         _lib.call("dr_e64_position_window", ptr(e), c_u64(n), stream_of(e))
-        flag.zero_()
         gather_fixup_pitch128(rows_p, e, out[:n], key_off, key_len, 32, flag)
-        onesweep_check(rows_p.device)
+        if int(flags[1].item()) != 0:           # a look-back pass of the chain failed: once more without
+            torch.arange(n, out=e)
+            for P in windows:
+                rekey64(rows_p, e, key_off, key_len, P)
+                _sort64_into(e, tmp, 32, lookback=False)
+            _lib.call("dr_e64_position_window", ptr(e), c_u64(n), stream_of(e))
+            gather_fixup_pitch128(rows_p, e, out[:n], key_off, key_len, 32, flag)
+            path += " (look-back failed: count+scatter)"
         path += f" + full-key LSD chain over windows {windows}"
     if stats is not None:
         stats["path"] = path

@@ -1,10 +1,17 @@
 """TeraSort record store kernels: synthetic generator + valsort-style checker (csrc/kernels/terasort.hip)."""
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
 from ._lib import c_u32, c_u64, ptr, stream_of
+
+_lib.register_signatures({
+    "dr_ts_sample_keys": (ctypes.c_int, [c_u64, c_u64, c_u64, c_u64, c_u64, c_u64, ctypes.c_void_p, ctypes.c_void_p]),
+    "dr_terasort_gen_gather": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u64, c_u64, c_u64, ctypes.c_void_p]),
+})
 
 RECORD_BYTES = 100
 KEY_BYTES = 10
@@ -18,6 +25,7 @@ def generate(out: torch.Tensor, first_index: int, seed: int) -> torch.Tensor:
     assert out.dtype == torch.uint8 and out.dim() == 2 and out.shape[1] == RECORD_BYTES
     _lib.call("dr_terasort_gen", ptr(out), c_u64(out.shape[0]), c_u64(first_index), c_u64(seed & (2**64 - 1)),
               stream_of(out))
+    _lib.written(out)
     return out
 
 
@@ -32,17 +40,6 @@ def generate_with_keys(out: torch.Tensor, first_index: int, seed: int, keys: tor
     _lib.call("dr_terasort_gen_keys", ptr(out), c_u64(n), c_u64(first_index), c_u64(seed & (2**64 - 1)),
               ptr(keys), c_u32(0), ptr(hi_range), stream_of(out))
     return out
-
-
-def generate_keys_only(n: int, first_index: int, seed: int, keys: torch.Tensor,
-                       hi_range: torch.Tensor | None = None) -> torch.Tensor:
-    """The sort entries of ``generate_with_keys`` without the records themselves (a distributed
-    sort then generates each record straight into its send bucket: sort.bucket_scatter_gen_terasort)."""
-    _lib.require_gpu_tensor(keys, "terasort.generate_keys_only")
-    assert keys.shape[0] >= n and keys.dtype == torch.int64 and keys.is_contiguous()
-    _lib.call("dr_terasort_gen_keys_only", c_u64(n), c_u64(first_index), c_u64(seed & (2**64 - 1)), ptr(keys),
-              c_u32(0), ptr(hi_range), stream_of(keys))
-    return keys
 
 
 def generate_with_keys64(out: torch.Tensor, first_index: int, seed: int, keys: torch.Tensor,
@@ -84,3 +81,26 @@ def check(rows: torch.Tensor, acc: torch.Tensor | None = None) -> torch.Tensor:
         acc = torch.zeros(2, dtype=torch.int64, device=rows.device)
     _lib.call("dr_terasort_check", ptr(rows), c_u64(rows.shape[0]), ptr(acc), stream_of(rows))
     return acc
+
+
+def sample_keys(first: int, seed: int, off: int, stride: int, m: int, lo_or: int, device) -> torch.Tensor:
+    """Sort entries ([m, 2] int64, the ``generate_keys_only`` layout with ``lo_or`` OR-ed into lo)
+    of records ``first + off + k * stride`` (k < m), generated at those positions only: the
+    sampler of a distributed sort over gen://terasort draws them without a full entry table."""
+    out = torch.empty((max(m, 0), 2), dtype=torch.int64, device=device)
+    if m > 0:
+        _lib.call("dr_ts_sample_keys", c_u64(first), c_u64(seed & (2**64 - 1)), c_u64(off), c_u64(stride), c_u64(m),
+                  c_u64(lo_or & (2**64 - 1)), ptr(out), stream_of(out))
+    return out
+
+
+def gen_gather(out: torch.Tensor, idx: torch.Tensor, first: int, seed: int) -> torch.Tensor:
+    """``out[p]`` := record ``first + idx[p]`` (``out`` [m, 100] uint8 rows back to back, ``idx``
+    int32 [m] slice offsets): the send-buffer pack of a distributed sort over gen://terasort."""
+    _lib.require_gpu_tensor(out, "terasort.gen_gather")
+    m = idx.shape[0]
+    assert out.dtype == torch.uint8 and out.shape[0] >= m and out.shape[1] == RECORD_BYTES and out.is_contiguous()
+    assert idx.dtype == torch.int32 and idx.is_contiguous()
+    _lib.call("dr_terasort_gen_gather", ptr(out), ptr(idx), c_u64(m), c_u64(first), c_u64(seed & (2**64 - 1)),
+              stream_of(out))
+    return out[:m]

@@ -16,6 +16,7 @@ Mapping of the Dryad runtime onto a node of GPUs:
 from __future__ import annotations
 
 import atexit
+import collections
 import json
 import os
 import pickle
@@ -120,6 +121,7 @@ class GpuJobRunner:
         self.faults = faults or []
         self.channels: dict = {}          # (stage, partition) -> DeviceTable | Ported | list | list-of-lists
         self.fallbacks: list = []
+        self.op_counts = collections.Counter()   # (operator, "device" | "host") -> executions
         self.transports: list = []      # (stage, edge kind, "device" | "object", bytes / reason)
         self.timings: dict = {}
         R = native_runtime()
@@ -265,8 +267,10 @@ class GpuJobRunner:
         bs = self.row_sets[(f["x"], me)]
         off, ln = f["spec"]
         stats = RS.SortStats()
+        f["consumed"] = (bs.lazy_gen, bs.keys_ready)      # what a retry restores (gen inputs)
         kr = bs.take_keys(t.rows, off, ln)
         gen, bs.lazy_gen = bs.lazy_gen, None
+        f["clobbered"] = True                             # rows_in becomes the receive buffer
         if gen is not None and kr is None:         # entries were not claimed: records are needed
             bs.lazy_gen = gen
             bs.materialize(t.n)
@@ -284,6 +288,99 @@ class GpuJobRunner:
         for op in m.ops[1:]:
             data = self._run_op(op, [data], vctx, m)
         return data
+
+    # ------------------------------------------------------------------ fused gang stages
+    def _run_gang(self, s, body, ready, refresh, now, restore=None):
+        """Run a fused stage (distributed or out-of-core OrderBy) as versioned attempts of its
+        vertices, the reference's gang re-execution (DrGang::EnsurePendingVersion, DrCohort.cpp:852;
+        DrActiveVertex::ReactToFailedVertex, DrVertex.cpp:1042-1171; DrGraph::ReportFailure,
+        DrGraph.cpp:392-456).  One attempt = ``body()`` on every rank (it holds collectives).
+
+        Decisions are voted so no rank enters a collective alone: injected faults are agreed
+        before the body (fail, read_error, slow) and after it (crash: the attempt's output is
+        discarded), and each rank's outcome after it.  A failed attempt fails the vertex of its
+        rank's partition, and every member restarts at its next version (gang) after ``restore()``
+        rebuilt what the attempt consumed; a read error re-reads the input from lineage first.
+        MaxVertexFailures failures abort the job.  An exception raised inside the collective body
+        on one rank only leaves its peers in the exchange: the communicator's error handling then
+        ends the job (parallel/comm.py), as a lost process would."""
+        g, W, me = self.g, self.world.size, self.world.rank
+        mine = [p for p in range(s.partitions) if self.owner(p) == me]
+        while True:
+            refresh()
+            vers = {}
+            for p in range(s.partitions):
+                vid = self.vids[s.id][p]
+                vers[p] = ready.pop(vid)
+                g.on_running(vid, vers[p], self.owner(p), now())
+            faults = {p: self._fault(s, p, vers[p]) for p in mine}
+            pre = next(((p, k) for p, k in faults.items() if k in ("fail", "read_error")), None)
+            for k in faults.values():
+                if k and k.startswith("slow"):
+                    time.sleep(float(k.split(":")[1]) if ":" in k else 1.0)
+            outcome = self._vote(None if pre is None else (pre[0], pre[1], f"injected {pre[1]} of {s.name}[{pre[0]}]"))
+            out = None
+            if outcome is None:
+                err = None
+                try:
+                    out = body()
+                    crash = next((p for p, k in faults.items() if k == "crash"), None)
+                    if crash is not None:
+                        err = (crash, "crash", f"injected crash of {s.name}[{crash}] (output discarded)")
+                except Exception as e:  # noqa: BLE001
+                    self._last_exc = e
+                    err = (mine[0] if mine else 0, "fail", f"{type(e).__name__}: {e}")
+                outcome = self._vote(err)
+            if outcome is None:
+                for p in range(s.partitions):
+                    g.on_completed(self.vids[s.id][p], vers[p], now(), 0, _object_bytes(out) if p in mine else 0)
+                return out
+            failed = {}
+            for r, (p, kind, msg) in outcome:
+                failed[p] = (kind, msg)
+                self._dump_restart(s, p, vers[p], [], msg) if r == me else None
+                log.warning("fused stage %s[%d] v%d failed (%s): %s", s.name, p, vers[p], kind, msg)
+            for p in sorted(failed):                # the first failure restarts the whole gang
+                g.on_failed(self.vids[s.id][p], vers[p], now(), -1, failed[p][1])
+                self.recovery.append(("upstream" if failed[p][0] == "read_error" else "gang_restart", s.name, p))
+            if g.failed():
+                raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed, g.failure(),
+                                            inner=getattr(self, "_last_exc", None))
+            if restore is not None:
+                restore(any(k == "read_error" for k, _ in failed.values()))
+
+    def _vote(self, err):
+        """All-gather of each rank's attempt outcome: None (ok) or (partition, kind, message).
+        Returns None when every rank succeeded, else [(rank, outcome)] of the failures."""
+        W = self.world.size
+        got = [err]
+        if W > 1:
+            got = [None] * W
+            dist.all_gather_object(got, err)
+        bad = [(r, e) for r, e in enumerate(got) if e is not None]
+        return bad or None
+
+    def _restore_fused_input(self, f, reread: bool = False):
+        """Before a retry of a fused distributed OrderBy: its input table again.  A gen://terasort
+        input that was never written only needs its generator parameters back; a table the
+        failed attempt clobbered (rows_in became the receive buffer), or one whose read failed
+        (``reread``), is rebuilt from lineage.  Collective (every rank decides alike: the
+        outcome was voted)."""
+        me = self.world.rank
+        clobbered = f.pop("clobbered", False)
+        bs = self.row_sets.get((f["x"], me))
+        gen, keys = f.pop("consumed", (None, None)) if clobbered else (bs.lazy_gen if bs else None, None)
+        if bs is not None and gen is not None:
+            if clobbered:
+                bs.lazy_gen, bs.keys_ready = gen, keys
+            return
+        if not clobbered and not reread:
+            return
+        if bs is not None and self.pool is not None:
+            self.pool.release(bs)               # the rebuilt table reuses the same HBM
+        for key in [k for k in self.channels if k[0] == f["x"]]:
+            del self.channels[key]
+        self._rematerialize(f["x"])
 
     # ------------------------------------------------------------------ out-of-core OrderBy
     def _plan_external(self):
@@ -626,13 +723,16 @@ class GpuJobRunner:
         device_apply = name == "apply" and is_device_function(op["fn"])
         if fn is not None and (device_apply or all(a is None or isinstance(a, DeviceTable) for a in args)):
             try:
-                return fn(op, [a for a in args] if args else [], vctx)
+                out = fn(op, [a for a in args] if args else [], vctx)
+                self.op_counts[(name, "device")] += 1
+                return out
             except NotTraceable as e:
                 self._fallback(s, name, str(e), args)
         elif fn is None or not self.gpu_ok:
-            self._fallback(s, name, "host op", args)
+            self._fallback(s, name, "host op" if fn is None or not self.gpu_ok else "host records in", args)
         objs = [(_to_objects(a) if not isinstance(a, list) else a) if a is not None else [] for a in args]
         out = V.OPS[name](op, objs, vctx)
+        self.op_counts[(name, "host")] += 1
         return self._maybe_device(out, s, name)
 
     def _fallback(self, s, name, why, args):
@@ -681,6 +781,10 @@ class GpuJobRunner:
         for sid, e in self.external.items():
             self.fused.pop(sid, None)
             self.skipped.update(e["skip"])
+        for sid in list(self.external) + list(self.fused):
+            if self.plan.stages[sid].partitions > 1 and sid not in self.gang_stages:
+                self.g.set_gang(self.vids[sid])      # one collective program: its vertices restart together
+                self.gang_stages.add(sid)
         self.lazy_gen_stages = self._lazy_gen_reads()
         self.pitch_gen_stages = self._pitch_gen_reads()
         fused_first = {f["stages"][0]: mid for mid, f in self.fused.items()}
@@ -729,36 +833,17 @@ class GpuJobRunner:
                 self.timings[f"{s.id}:{s.name}(fused)"] = 0.0
                 continue
             if s.id in self.external:
-                refresh()
-                vid = self.vids[s.id][me]
-                ver = ready.pop(vid)
-                g.on_running(vid, ver, me, now())
-                out = self._run_external(s, self.external[s.id])
+                e = self.external[s.id]
+                out = self._run_gang(s, lambda: self._run_external(s, e), ready, refresh, now)
                 self.channels[(s.id, me)] = out
-                g.on_completed(vid, ver, now(), 0, out.nbytes)
-                for p in range(s.partitions):
-                    if p != me:
-                        v2 = self.vids[s.id][p]
-                        ver2 = ready.pop(v2)
-                        g.on_running(v2, ver2, self.owner(p), now())
-                        g.on_completed(v2, ver2, now(), 0, 0)
                 self._release(s)
                 self.timings[f"{s.id}:{s.name}(out-of-core OrderBy)"] = time.time() - t0
                 continue
             if s.id in active_fused:
-                refresh()
-                vid = self.vids[s.id][me]
-                ver = ready.pop(vid)
-                g.on_running(vid, ver, me, now())
-                out = self._run_fused(s, active_fused[s.id])
+                f = active_fused[s.id]
+                out = self._run_gang(s, lambda: self._run_fused(s, f), ready, refresh, now,
+                                     restore=lambda reread: self._restore_fused_input(f, reread))
                 self.channels[(s.id, me)] = out
-                g.on_completed(vid, ver, now(), 0, _object_bytes(out))
-                for p in range(s.partitions):
-                    if p != me:
-                        v2 = self.vids[s.id][p]
-                        ver2 = ready.pop(v2)
-                        g.on_running(v2, ver2, self.owner(p), now())
-                        g.on_completed(v2, ver2, now(), 0, 0)
                 self._release(s)
                 if self.gpu_ok:
                     torch.cuda.synchronize(self.dev)
@@ -774,6 +859,7 @@ class GpuJobRunner:
             for b in set(self.row_sets.values()):
                 self.pool.release(b)
         return dict(committed=committed, fallbacks=self.fallbacks, timings=self.timings, transports=self.transports,
+                    op_counts={f"{k[0]}:{k[1]}": v for k, v in self.op_counts.items()},
                     statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()],
                     external_sort=getattr(self, "extsort_stats", None), join=getattr(self, "join_stats", None),
                     recovery=self.recovery)
@@ -916,21 +1002,50 @@ class GpuJobRunner:
 
     def _try_fused_join(self, desc):
         """Run a Join + aggregate idiom as one fused grace join stage (runtime/fused_join.py) when
-        every rank can; None (the plan's stages run as compiled) otherwise."""
+        every rank can; None (the plan's stages run as compiled) otherwise.
+
+        Attempts are voted like a gang stage's (``_run_gang``): injected faults on the join stage's
+        partitions are agreed before the body (fail, read_error) or after it (crash), and a failed
+        attempt is re-run from its inputs (generated or HBM-resident, so re-readable) until
+        MaxVertexFailures.  An exception raised on EVERY rank (e.g. an allocation the budget check
+        let through) means every rank left the body together: the compiled stages run instead.
+        One raised on some ranks only leaves the others in a collective; the communicator's error
+        handling then ends the job (parallel/comm.py)."""
         lay = FJ.vote(desc, self)
         if lay is None:
             return None
-        out, err = None, None
-        try:
-            out = FJ.run(desc, self, lay)
-        except Exception as e:  # noqa: BLE001
-            err = e
-            log.warning("fused grace join failed, running the compiled stages: %s", e)
-        ok = [err is None]
-        if self.world.size > 1:
-            ok = [None] * self.world.size
-            dist.all_gather_object(ok, err is None)
-        return out if all(ok) else None
+        st = self.plan.stages[desc["join"]]
+        me = self.world.rank
+        mine = [p for p in range(st.partitions) if self.owner(p) == me]
+        limit = int(getattr(self.ctx, "MaxVertexFailures", 6) or 6)
+        for version in range(limit):
+            faults = {p: self._fault(st, p, version) for p in mine}
+            pre = next(((p, k) for p, k in faults.items() if k in ("fail", "read_error")), None)
+            outcome = self._vote(None if pre is None else (pre[0], pre[1], f"injected {pre[1]} of {st.name}[{pre[0]}]"))
+            out = None
+            real = False
+            if outcome is None:
+                err = None
+                try:
+                    out = FJ.run(desc, self, lay)
+                    crash = next((p for p, k in faults.items() if k == "crash"), None)
+                    if crash is not None:
+                        err = (crash, "crash", f"injected crash of {st.name}[{crash}] (output discarded)")
+                except Exception as e:  # noqa: BLE001
+                    err = (mine[0] if mine else 0, "exception", f"{type(e).__name__}: {e}")
+                    log.warning("fused grace join attempt %d failed: %s", version, e)
+                outcome = self._vote(err)
+                real = outcome is not None and len(outcome) == self.world.size and \
+                    all(e[1] == "exception" for _, e in outcome)
+            if outcome is None:
+                return out
+            if real:
+                self.recovery.append(("fused_join_declined", st.name, outcome[0][1][2]))
+                return None
+            for _, (p, kind, _msg) in outcome:
+                self.recovery.append(("upstream" if kind == "read_error" else "gang_restart", st.name, p))
+        raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed,
+                                    f"fused grace join {st.name} failed {limit} times: {outcome[0][1][2]}")
 
     def _release(self, s):
         later = {i.src for st in self.plan.stages if st.id > s.id for i in st.inputs}
@@ -1170,6 +1285,8 @@ class GpuExecutor(_BaseExecutor):
             w = World(0, 1, 0, torch.device("cuda", torch.cuda.current_device()), None)
         self.world = w
         self.last_result = None
+        # per job (the last 1000): host fallbacks and device / host operator counts
+        self.job_log = collections.deque(maxlen=1000)
         from ..gpu.pool import HbmPool
         self.pool = HbmPool(w.device) if w.device.type == "cuda" else None
 
@@ -1222,6 +1339,7 @@ class GpuExecutor(_BaseExecutor):
             _JOB_DIR_WRITER.submit(_write_json, os.path.join(job_dir, "statistics.json"), st)
         self.last_job_dir = job_dir
         self.last_result = res
+        self.job_log.append(dict(fallbacks=list(res["fallbacks"]), op_counts=dict(res["op_counts"])))
         self.last_plan = plan
         self.last_sort_path = getattr(runner, "last_sort_path", None)
         if handle is not None:

@@ -48,6 +48,8 @@ def main():
                 print(f"[faults] {kind} {name}: {'ok' if ok else 'MISMATCH'} recovery={sorted(kinds)}", flush=True)
             if not ok:
                 bad.append((kind, name, sorted(kinds)))
+    if w.device.type == "cuda":
+        bad += fused_stage_faults(w, loc)
     import torch.distributed as dist
     allbad = [bad]
     if W > 1:
@@ -57,6 +59,63 @@ def main():
         flat = [x for b in allbad for x in b]
         assert not flat, flat
         print("FAULTS_OK", W, flush=True)
+
+
+def fused_stage_faults(w, loc):
+    """The same fault kinds in the fused stages (GPU ranks): the distributed OrderBy gang stage (one
+    stage per rank at W = 1), the out-of-core OrderBy (host:// output) and the fused grace join;
+    outputs checked exactly (order and records) and the recovery kinds as above."""
+    import torch
+    from dryad_amd.io.providers import provider_for
+    from dryad_amd.ops import extsort as EX
+    W = w.size
+    bad = []
+    ts = "gen://terasort?records=300000&partitions=%d&seed=5" % W
+    key = lambda r: r[0:10]  # noqa: E731
+    exp_sorted = list(loc.FromStore(ts).OrderBy(key))
+    R = "gen://records64?count=60000&partitions=%d&keys=60000&seed=3&mode=dim" % W
+    S = "gen://records64?count=60000&partitions=%d&keys=60000&seed=4" % W
+
+    def join(c):
+        return c.FromStore(R).Join(c.FromStore(S), lambda r: r[0], lambda s: s[0], lambda r, s: r[1] + s[1]).Sum()
+    exp_join = join(loc)
+    for kind in ("fail", "read_error", "crash"):
+        want = {"fail": {"retry", "gang_restart"}, "crash": {"retry", "gang_restart"}, "read_error": {"upstream"}}[kind]
+        for name in ("fused_orderby", "external_orderby", "fused_join"):
+            g = D.DryadLinqContext(platform="gpu")
+            g.PartitionCount = W
+            g.FaultInjection = [dict(stage=None, partition=0, version=0, kind=kind)]
+            if name == "fused_orderby":
+                ok = list(g.FromStore(ts).OrderBy(key)) == exp_sorted
+            elif name == "external_orderby":
+                g.ExternalSort = True
+                g.HbmBudgetBytes = 16 << 20
+                uri = "host://faults_ext"
+                g.FromStore(ts).OrderBy(key).ToStore(uri, delete_if_exists=True).SubmitAndWait()
+                ent = provider_for(uri).get(uri)
+                h, viol, first, last = EX.check_terasort_host(ent["local"][w.rank])
+                rows = ent["local"][w.rank]
+                mine = [bytes(x) for x in rows.rows[: rows.n].numpy()]
+                allrows = [None] * W
+                if W > 1:
+                    import torch.distributed as dist
+                    dist.all_gather_object(allrows, mine)
+                else:
+                    allrows = [mine]
+                ok = [x for part in allrows for x in part] == exp_sorted and viol == 0
+                provider_for(uri).delete(uri)
+            else:
+                ok = join(g) == exp_join
+            rec = g._get_executor().last_result.get("recovery") or []
+            kinds = {r[0] for r in rec}
+            if not (kinds & want):
+                ok = False
+            if w.rank == 0:
+                print(f"[faults] {kind} {name}: {'ok' if ok else 'MISMATCH'} recovery={sorted(kinds)}", flush=True)
+            if not ok:
+                bad.append((kind, name, sorted(kinds)))
+    torch.cuda.synchronize()
+    return bad
 
 
 if __name__ == "__main__":

@@ -113,3 +113,26 @@ def test_wordcount_on_partfile_line_records(tmp_path):
     res = dict(word_count_query(c, uri))
     assert res == dict(Counter(" ".join(lines).split()))
     assert not c._get_executor().last_result["fallbacks"]
+
+
+def test_tampered_index_sidecar_is_rebuilt(tmp_path):
+    """A sidecar whose offsets are in bounds but wrong (one block start moved by a byte) decodes
+    to a DecodeError, which the read turns into a rebuilt index: the query result is exact."""
+    import dryad_amd as D
+    from dryad_amd.io import partfile as PF
+    from dryad_amd.io.providers import provider_for
+    dt = _dtype()
+    recs = _records(9000, seed=4)
+    uri = "partfile://" + str(tmp_path / "tam.pt")
+    provider_for(uri).write_table(uri, [recs], dt)
+    part = PF.read_meta(str(tmp_path / "tam.pt")).part_path(0)
+    n, nb, blk, offs = PF.read_index(part)
+    assert offs.shape[0] >= 3
+    offs = offs.copy()
+    offs[1] += 1
+    PF.write_index(part, n, nb, offs, blk)
+    assert PF.read_index(part) is not None          # plausible on its face
+    c = D.DryadLinqContext(platform="gpu")
+    c.PartitionCount = 1
+    got = list(c.FromStore(uri, dtype=dt).Select(lambda r: (r[0], r[1])))
+    assert got == [(r[0], r[1]) for r in recs]

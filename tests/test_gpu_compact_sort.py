@@ -111,16 +111,17 @@ def _sort64_both(ent: torch.Tensor, win: int):
     a, ta = ent.clone(), torch.empty_like(ent)
     flag = __import__("ctypes").c_int(0)
     ws = S._onesweep_workspace(n, ent.device)
+    err = S.lookback_error()
     from dryad_amd.ops import _lib
     _lib.call("dr_sort_u64_onesweep", S.ptr(a), S.ptr(ta), S.c_u64(n), 64 - win, 64, S.ptr(ws), S.c_u64(ws.numel()),
-              None, S.c_u32(0), S.stream_of(a), __import__("ctypes").byref(flag))
+              None, S.c_u32(0), S.ptr(err), S.stream_of(a), __import__("ctypes").byref(flag))
     ra = ta if flag.value else a
     b, tb = ent.clone(), torch.empty_like(ent)
     wsb = S._workspace(n, ent.device)
     _lib.call("dr_sort_u64", S.ptr(b), S.ptr(tb), S.c_u64(n), 64 - win, 64, S.ptr(wsb), S.stream_of(b),
               __import__("ctypes").byref(flag))
     rb = tb if flag.value else b
-    S.onesweep_check(ent.device)
+    assert int(err.item()) == 0, "look-back sort failed"
     return ra, rb
 
 
@@ -146,25 +147,6 @@ def test_onesweep_sort64_matches_stable_reference(n, win, kind):
     assert torch.equal(rb.cpu(), ref)
 
 
-@pytest.mark.parametrize("items", [16])
-def test_onesweep_tile_size_variants_match(items):
-    """The 4096-entry look-back tiles (A/B only) sort identically."""
-    from dryad_amd.ops import _lib
-    lib = _lib.lib()
-    lib.dr_sort64_onesweep_set_items.argtypes = [__import__("ctypes").c_int]
-    lib.dr_sort64_onesweep_set_items.restype = None
-    n = (1 << 21) + 77
-    g = torch.Generator().manual_seed(3)
-    w = torch.randint(0, 1 << 32, (n,), generator=g, dtype=torch.int64)
-    ent = ((w << 32) | torch.arange(n, dtype=torch.int64)).to(DEV)
-    lib.dr_sort64_onesweep_set_items(items)
-    try:
-        ra, rb = _sort64_both(ent, 32)
-    finally:
-        lib.dr_sort64_onesweep_set_items(32)
-    assert torch.equal(ra, rb)
-
-
 def test_pitch128_sort_with_generator_histograms():
     """gen://terasort rows at a 128-byte pitch whose generator also wrote the window histograms:
     the sort uses them (no histogram read) and orders exactly like the plain path."""
@@ -185,3 +167,46 @@ def test_pitch128_sort_with_generator_histograms():
     chk = TS.check(out_a)
     assert int(chk[1]) == 0
 
+
+
+def test_onesweep_refuses_foreign_histograms():
+    """Producer histograms that do not count the entries (another producer's) are refused before
+    any entry moves: the error flag is set and the caller's fallback sorts correctly."""
+    n = (1 << 20) + 999
+    g = torch.Generator().manual_seed(11)
+    w = torch.randint(0, 1 << 32, (n,), generator=g, dtype=torch.int64)
+    ent = ((w << 32) | torch.arange(n, dtype=torch.int64)).to(DEV)
+    foreign = torch.zeros(4 * 1024, dtype=torch.int32, device=DEV)    # 4 parts, all-zero counts
+    e, tmp = ent.clone(), torch.empty_like(ent)
+    err = S.lookback_error()
+    S.sort_entries64(e, tmp, 32, gen_hist=foreign, err=err)
+    assert int(err.item()) & 2
+    assert torch.equal(e, ent)                   # nothing moved
+    srt = S.sort_entries64(e, tmp, 32, lookback=False)
+    assert torch.equal((srt & 0xFFFFFFFF).cpu(), torch.sort(w, stable=True).indices)
+
+
+def test_sort_rows_compact_recovers_from_failed_lookback(monkeypatch):
+    """A failed look-back sort inside the compact row sort is redone with count + scatter passes."""
+    from dryad_amd.ops import terasort as TS
+    n = (1 << 20) + 4321
+    rows = torch.empty((n, 100), dtype=torch.uint8, device=DEV)
+    TS.generate(rows, 0, 3)
+    real = S.sort_entries64
+    calls = []
+
+    def failing(e, tmp, win, gen_hist=None, err=None, lookback=True):
+        calls.append(lookback)
+        if lookback and err is not None:
+            err.fill_(1)                      # as if a spin had given up (entries scrambled)
+            e.copy_(e.flip(0))
+            return e
+        return real(e, tmp, win, gen_hist, err=err, lookback=lookback)
+    monkeypatch.setattr(S, "sort_entries64", failing)
+    out = torch.empty_like(rows)
+    info = {}
+    got = S.sort_rows_compact(rows, out, torch.empty(n, dtype=torch.int64, device=DEV),
+                              torch.empty(n, dtype=torch.int64, device=DEV), 0, 10, stats=info)
+    assert calls == [True, False] and "look-back failed" in info["path"]
+    acc = TS.check(got)
+    assert int(acc[1].item()) == 0 and int(acc[0].item()) == int(TS.check(rows)[0].item())

@@ -4,7 +4,9 @@ MiscBugFixTests / TypesInQueryTests / ApplyAndForkTests scenarios) runs again wi
 "cluster" side being the SPMD GPU executor (3 partitions on this GPU) and the LocalDebug oracle
 on the other side.  Scenarios that assert properties of the CPU process executor itself (vertex
 host processes, its plan shape or its fault injection) are listed in CPU_ONLY with the reason."""
+import collections
 import inspect
+import os
 
 import pytest
 
@@ -29,6 +31,20 @@ def _cases():
     return out
 
 
+# Host fallbacks a scenario may take on the GPU executor, each with the reason its operator cannot
+# run on the device.  Any other fallback fails the scenario: passing the oracle comparison on a
+# silent host path would not show that the device path works.
+ALLOWED_FALLBACKS = {
+}
+
+_COVERAGE = collections.Counter()      # (operator, "device" | "host") over every scenario
+
+
+def _gpu_jobs():
+    ctxs = [c for (mode, *_), c in helpers._CTX.items() if mode == "gpu"]
+    return [j for c in ctxs for j in c._get_executor().job_log]
+
+
 @pytest.mark.parametrize("mod,name", _cases())
 def test_oracle_scenario_on_gpu_executor(mod, name, tmp_path, monkeypatch):
     monkeypatch.setattr(helpers, "MODE", "gpu")
@@ -39,4 +55,26 @@ def test_oracle_scenario_on_gpu_executor(mod, name, tmp_path, monkeypatch):
         kwargs["tmp_path"] = tmp_path
     if any(p not in ("tmp_path",) for p in params):
         pytest.skip(f"needs fixtures {list(params)}")
+    for c in [c for (mode, *_), c in helpers._CTX.items() if mode == "gpu"]:
+        c._get_executor().job_log.clear()
     fn(**kwargs)
+    jobs = _gpu_jobs()
+    allowed = ALLOWED_FALLBACKS.get(name, {})
+    for j in jobs:
+        for k, v in j["op_counts"].items():
+            op, where = k.rsplit(":", 1)
+            _COVERAGE[(op, where)] += v
+    unexplained = sorted({(stage, op, why) for j in jobs for stage, op, why in j["fallbacks"] if op not in allowed})
+    assert not unexplained, f"{name}: host fallbacks not in ALLOWED_FALLBACKS: {unexplained}"
+
+
+def test_zz_print_device_coverage():
+    """Per-operator executions on the device vs on the host over the scenarios above."""
+    ops = sorted({op for op, _ in _COVERAGE})
+    lines = [f"{op:24s} device {_COVERAGE[(op, 'device')]:5d}   host {_COVERAGE[(op, 'host')]:5d}" for op in ops]
+    text = "[oracle suites on the GPU executor: operator executions]\n" + "\n".join(lines) + "\n"
+    print("\n" + text)
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    if os.path.isdir(out):
+        with open(os.path.join(out, "oracle_device_coverage.txt"), "w") as f:
+            f.write(text)

@@ -105,17 +105,10 @@ def test_one_rank_terasort_query_uses_the_line_aligned_input():
     provider_for("hbm://ts_pitch").delete("hbm://ts_pitch")
 
 
-@pytest.mark.parametrize("wide", [2, 1, 0])
-def test_pitch128_gather_fixup_runs_wide_and_dword_copy(wide):
+def test_pitch128_gather_fixup_short_runs():
     """Short runs of equal 32-bit windows (about 4 rows each, resolved by the gather's in-LDS
-    fix-up) copied by the 16-byte nontemporal-load gather (default), the cached 16-byte loads and
-    the dword copy (A/B): numpy order."""
-    import ctypes
-    from dryad_amd.ops import _lib
+    fix-up) copied by the 16-byte nontemporal-load gather: numpy order."""
     from dryad_amd.ops import sort as S
-    lib = _lib.lib()
-    lib.dr_gather_fixup_set_wide.argtypes = [ctypes.c_int]
-    lib.dr_gather_fixup_set_wide.restype = None
     n = 200_003
     g = np.random.default_rng(5)
     rows = g.integers(0, 256, size=(n, 100), dtype=np.uint8)
@@ -126,10 +119,6 @@ def test_pitch128_gather_fixup_runs_wide_and_dword_copy(wide):
     keys = ((torch.from_numpy(win.astype(np.int64)) << 32) | torch.arange(n, dtype=torch.int64)).cuda()
     out = torch.empty((n, 100), dtype=torch.uint8, device="cuda")
     info = {}
-    lib.dr_gather_fixup_set_wide(wide)
-    try:
-        got = S.sort_rows_pitch128(padded, out, keys, 0, 10, keys_ready=True, stats=info)
-    finally:
-        lib.dr_gather_fixup_set_wide(2)
+    got = S.sort_rows_pitch128(padded, out, keys, 0, 10, keys_ready=True, stats=info)
     assert "LSD chain" not in info["path"], info
     np.testing.assert_array_equal(got.cpu().numpy(), rows[_reference_order(rows, 0, 10)])

@@ -189,35 +189,20 @@ def test_prefix_sort_with_tie_fixup_matches_full_sort(dup):
     np.testing.assert_array_equal(pre, full)
 
 
-def test_sort_tile16_and_gather_v4_variants():
+def test_gather_rows_matches_index_select():
     from dryad_amd.ops import sort as S
     n = 300_001
-    e = torch.randint(-2**63, 2**63 - 1, (n, 2), dtype=torch.int64, device="cuda")
-    ref = S.sort_entries(e.clone(), 0, 128).cpu().numpy()
-    S.set_sort_items(16)
-    try:
-        np.testing.assert_array_equal(S.sort_entries(e.clone(), 0, 128).cpu().numpy(), ref)
-    finally:
-        S.set_sort_items(8)
-    rows = torch.randint(0, 256, (n, 100), dtype=torch.uint8, device="cuda")
-    perm = torch.randperm(n, device="cuda")
-    S.set_gather_v4(True)
-    a = S.gather_rows(rows, index=perm)
-    S.set_gather_v4(False)
-    b = S.gather_rows(rows, index=perm)
-    S.set_gather_v4(True)
-    assert torch.equal(a, rows[perm]) and torch.equal(a, b)
+    for stride in (100, 64):              # 16-byte vector gather (100) and the dword gather
+        rows = torch.randint(0, 256, (n, stride), dtype=torch.uint8, device="cuda")
+        perm = torch.randperm(n, device="cuda")
+        assert torch.equal(S.gather_rows(rows, index=perm), rows[perm])
 
 
-def test_scatter_v1_v2_agree():
+def test_sort_entries_matches_reference():
     from dryad_amd.ops import sort as S
     n = 250_003
     e = torch.randint(-2**63, 2**63 - 1, (n, 2), dtype=torch.int64, device="cuda")
-    S.set_scatter_v2(False)
     a = S.sort_entries(e.clone(), 0, 128).cpu().numpy()
-    S.set_scatter_v2(True)
-    b = S.sort_entries(e.clone(), 0, 128).cpu().numpy()
-    np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(a, e.cpu().numpy()[_ref_order(e)])
 
 
@@ -296,48 +281,82 @@ def test_seg_reduce_multi_matches_torch(nkeys):
     assert torch.equal(mxf, torch.full((uk.numel(),), -1e300, dtype=torch.float64, device="cuda").scatter_reduce(0, inv, vf, "amax"))
 
 
-@pytest.mark.parametrize("serial", ["0", "1"])
-def test_seg_reduce_multi_variants_agree(serial, monkeypatch):
-    import subprocess, sys, os
-    code = (
-        "import torch\n"
-        "from dryad_amd.ops import relational as R, _lib\n"
-        f"_lib.lib().dr_seg_reduce_set_serial({int(serial)})\n"
-        "torch.manual_seed(1)\n"
-        "for n, nk in ((1, 1), (511, 3), (513, 600), (4097, 2), (1_000_003, 50), (2_000_000, 1_500_000)):\n"
-        "    k = torch.sort(torch.randint(0, nk, (n,), device='cuda'))[0]\n"
-        "    flags = torch.ones(n, dtype=torch.int64, device='cuda'); flags[1:] = (k[1:] != k[:-1]).long()\n"
-        "    seg = torch.cumsum(flags, 0) - 1; nseg = int(seg[-1]) + 1\n"
-        "    vi = torch.randint(-10**6, 10**6, (n,), device='cuda'); vf = torch.randn(n, device='cuda', dtype=torch.float64)\n"
-        "    c, s, mn, mxf = R.seg_reduce_multi(None, seg, nseg, [('count', None, torch.int64), ('sum', vi, torch.int64),\n"
-        "                                        ('min', vi, torch.int64), ('max', vf, torch.float64)])\n"
-        "    assert torch.equal(c, torch.bincount(seg, minlength=nseg))\n"
-        "    assert torch.equal(s, torch.zeros(nseg, dtype=torch.int64, device='cuda').index_add_(0, seg, vi))\n"
-        "    assert torch.equal(mn, torch.full((nseg,), 2**62, device='cuda').scatter_reduce(0, seg, vi, 'amin'))\n"
-        "    assert torch.equal(mxf, torch.full((nseg,), -1e300, dtype=torch.float64, device='cuda').scatter_reduce(0, seg, vf, 'amax'))\n"
-        "print('OK')\n")
-    env = dict(os.environ)
-    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300,
-                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    assert out.returncode == 0 and "OK" in out.stdout, out.stderr[-3000:]
+def test_seg_reduce_multi_matches_torch():
+    from dryad_amd.ops import relational as R
+    torch.manual_seed(1)
+    for n, nk in ((1, 1), (511, 3), (513, 600), (4097, 2), (1_000_003, 50), (2_000_000, 1_500_000)):
+        k = torch.sort(torch.randint(0, nk, (n,), device="cuda"))[0]
+        flags = torch.ones(n, dtype=torch.int64, device="cuda")
+        flags[1:] = (k[1:] != k[:-1]).long()
+        seg = torch.cumsum(flags, 0) - 1
+        nseg = int(seg[-1]) + 1
+        vi = torch.randint(-10**6, 10**6, (n,), device="cuda")
+        vf = torch.randn(n, device="cuda", dtype=torch.float64)
+        c, sm, mn, mxf = R.seg_reduce_multi(None, seg, nseg, [("count", None, torch.int64), ("sum", vi, torch.int64),
+                                                              ("min", vi, torch.int64), ("max", vf, torch.float64)])
+        assert torch.equal(c, torch.bincount(seg, minlength=nseg))
+        assert torch.equal(sm, torch.zeros(nseg, dtype=torch.int64, device="cuda").index_add_(0, seg, vi))
+        assert torch.equal(mn, torch.full((nseg,), 2**62, device="cuda").scatter_reduce(0, seg, vi, "amin"))
+        assert torch.equal(mxf, torch.full((nseg,), -1e300, dtype=torch.float64, device="cuda").scatter_reduce(
+            0, seg, vf, "amax"))
 
 
-@pytest.mark.parametrize("n,nb", [(1, 4), (5000, 3), (300_001, 200)])
-def test_bucket_scatter_gen_terasort_matches_stored_rows(n, nb):
-    """Records generated straight into their buckets == the bucket scatter of the stored records."""
+@pytest.mark.parametrize("n,W,B,split", [(1, 2, 2, True), (5000, 2, 4, False), (300_001, 4, 8, True),
+                                         (2_000_003, 8, 16, True)])
+def test_gen_pack_matches_stored_rows_bucket_scatter(n, W, B, split):
+    """The send side over gen://terasort from the generator alone (sample keys, bucket order of the
+    record offsets, records generated into their send rows) == sampling the stored records'
+    entries, range destination and the bucket scatter of the stored rows."""
+    from dryad_amd.ops import recordsort as RS
     from dryad_amd.ops import sort as S
     from dryad_amd.ops import terasort as TS
-    first, seed = 12345, 99
+    first, seed, rank = 12345, 99, 1
+    M64 = (1 << 64) - 1
+    mask = M64 if split else TS.LO_KEY_MASK_10
+    lo_or = (rank << 32) if split else 0
     rows = torch.empty((n, 100), dtype=torch.uint8, device="cuda")
-    keys = torch.empty((n, 2), dtype=torch.int64, device="cuda")
-    TS.generate_with_keys(rows, first, seed, keys)
-    k2 = torch.empty_like(keys)
-    TS.generate_keys_only(n, first, seed, k2)
-    assert torch.equal(keys, k2)
-    g = torch.Generator(device="cuda").manual_seed(n)
-    keys[:, 1] = torch.randint(0, nb, (n,), device="cuda", generator=g)
-    a, b = torch.empty_like(rows), torch.empty_like(rows)
-    sa = S.bucket_scatter_rows(keys, rows, a)
-    sb = S.bucket_scatter_gen_terasort(keys, n, first, seed, b)
-    assert sa == sb
-    assert torch.equal(a, b)
+    ent = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    TS.generate_with_keys(rows, first, seed, ent)
+    ent[:, 0].bitwise_or_(lo_or)
+    m, stride = RS.sample_count(n, 1 << 20)
+    off = RS.sample_offset(314159, rank, stride)
+    ref_s = ent[off: off + stride * m: stride][:m].clone()
+    ref_s[:, 0] &= RS._as_i64(mask)
+    samp = RS.gen_samples((first, seed), n, rank, lo_or, mask, 1 << 20, 314159, rows.device)
+    assert torch.equal(samp, ref_s)
+    seps = RS.separators_from_samples(samp, W * B)
+    S.range_dest(ent, seps, mask, subs=B, ranks=W)
+    ref = torch.empty_like(rows)
+    st_ref = S.bucket_scatter_rows(ent, rows, ref)
+    idx = torch.empty(n, dtype=torch.int32, device="cuda")
+    st = S.dest_partition_gen(first, seed, n, seps, lo_or, mask, B, W, idx).tolist()
+    assert st == st_ref
+    got = torch.empty_like(rows)
+    for b in range(B):                        # one exchange round at a time, like the packer
+        a, z = st[b * W], st[(b + 1) * W]
+        if z > a:
+            TS.gen_gather(got[a:z], idx[a:z], first, seed)
+    assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("n,start", [(1, 0), (255, 3), (70_001, 1), (1_300_000, 5)])
+def test_extract_keys64_tile_matches_row_extract(n, start):
+    """Entries read through LDS tiles (any 4-byte alignment of the first row) == extract_keys64,
+    and the fused histograms == the digit counts of the windows."""
+    from dryad_amd.ops import sort as S
+    from dryad_amd.ops import terasort as TS
+    buf = torch.empty((n + start, 100), dtype=torch.uint8, device="cuda")
+    TS.generate(buf, 777, 5)
+    rows = buf[start:]
+    for P in (0, 7, 40):
+        ref = S.extract_keys64(rows, 0, 10, P, torch.empty(n, dtype=torch.int64, device="cuda"))
+        got, hist = S.extract_keys64_tile(rows, 0, 10, P, torch.empty(n, dtype=torch.int64, device="cuda"), hist=True)
+        assert torch.equal(got, ref)
+        if hist is not None:
+            h = hist.view(-1, 4, 256).sum(0).cpu()
+            win = ((ref >> 32) & 0xFFFFFFFF).cpu()
+            for p in range(4):
+                assert torch.equal(h[p].long(), torch.bincount((win >> (8 * p)) & 0xFF, minlength=256))
+    ref = S.extract_keys64(rows, 3, 7, 0, torch.empty(n, dtype=torch.int64, device="cuda"))    # unaligned key
+    got, _ = S.extract_keys64_tile(rows, 3, 7, 0, torch.empty(n, dtype=torch.int64, device="cuda"))
+    assert torch.equal(got, ref)

@@ -111,3 +111,19 @@ def test_gpu_runner_fallback_guard_without_gpu():
     r2 = SimpleNamespace(fallbacks=[], gpu_ok=True, ctx=ctx2)
     GpuJobRunner._fallback(r2, st, "aggregate_seq", "not traceable", [t])
     assert r2.fallbacks == [("s0", "aggregate_seq", "not traceable")]
+
+
+def test_index_sidecar_validation(tmp_path):
+    """read_index refuses offsets a block-parallel decoder must not trust: not starting at 0,
+    decreasing, or past the part's end."""
+    import numpy as np
+    from dryad_amd.io import partfile as PF
+    part = str(tmp_path / "p.00000000")
+    with open(part, "wb") as f:
+        f.write(b"\0" * 1000)
+    good = np.array([0, 100, 250, 900], dtype=np.int64)
+    PF.write_index(part, 16, 1000, good, 4)
+    assert PF.read_index(part) is not None
+    for bad in ([5, 100, 250, 900], [0, 300, 250, 900], [0, 100, 250, 1001]):
+        PF.write_index(part, 16, 1000, np.array(bad, dtype=np.int64), 4)
+        assert PF.read_index(part) is None, bad

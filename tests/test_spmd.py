@@ -51,6 +51,19 @@ def test_exchange_gloo(ranks):
     assert f"EXCHANGE_OK {ranks}" in r.stdout
 
 
+@pytest.mark.parametrize("ranks", [2, 4, 8])
+def test_chunked_alltoallv_gloo(ranks):
+    """The chunked batch_isend_irecv rounds of shuffle.alltoallv_bytes (pairs above the chunk
+    size) and the count exchange, byte-exact, over 2, 4 and 8 gloo ranks."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tests", "dist", "chunked_alltoall_ranks.py")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert f"CHUNKED_OK {ranks}" in r.stdout
+
+
 @pytest.mark.parametrize("ranks", [1, 2])
 def test_gpu_executor_fault_kinds_gloo(ranks):
     """Every fault kind (fail, read_error, crash, slow) on the SPMD GPU executor's stage machinery

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_kmeans.py tests/test_gpu_hipgraph.py -m gpu -x -q --timeout 120 \
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kmeans.py -m gpu -x -q --timeout 120 \
   --timeout-method thread > gpurun_out/km_tests.log 2>&1 || { tail -40 gpurun_out/km_tests.log; exit 1; }
 tail -2 gpurun_out/km_tests.log
 timeout -k 10 300 python -u benchmarks/kmeans.py > gpurun_out/km_bench.log 2>&1 || { tail -30 gpurun_out/km_bench.log; exit 1; }

@@ -2,13 +2,13 @@
 TeraSort), ms and GB/s moved (rows read + written), for the kernel chosen by
 DRYAD_BUCKET_SCATTER_V2 (1: 16-byte pieces + register prefetch, 0: dword loads).
 
-    python tools/microbench_bucket_scatter.py [rows=3e8] [buckets=8]
+    python tools/micro/microbench_bucket_scatter.py [rows=3e8] [buckets=8]
 """
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import torch  # noqa: E402
 

@@ -4,7 +4,7 @@ import sys
 import time
 
 import os
-sys_path = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys_path = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, sys_path)
 
 import torch  # noqa: E402

@@ -2,7 +2,7 @@
 
 Times the same in-HBM sort (RS.local_sort_rows: compact radix sort + fused gather) on rows in
 generator order and on the same rows stably partitioned by their top key byte (256 buckets), so the
-gather of each output range reads one bucket.  python tools/microbench_mall.py [rows]"""
+gather of each output range reads one bucket.  python tools/micro/microbench_mall.py [rows]"""
 import sys
 import time
 

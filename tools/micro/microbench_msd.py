@@ -3,14 +3,14 @@ remaining LSD passes bucket by bucket while each bucket (n/256 entries, ~80 MB i
 1.25e9 entries) stays resident in the 256 MB Infinity Cache — against the plain 4-pass LSD of the
 same 32-bit window.  Interleaved in one process, results checked equal.
 
-    python tools/microbench_msd.py [entries]
+    python tools/micro/microbench_msd.py [entries]
 """
 import ctypes
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import torch  # noqa: E402
 

@@ -1,13 +1,13 @@
 """Microbenchmarks of the whole-partition aggregate kernel (reduce.hip) and the device hash join
 (hashjoin.hip) against torch reductions and the sort-merge join, interleaved in one process.
 
-    python tools/microbench_ops.py [rows]
+    python tools/micro/microbench_ops.py [rows]
 """
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import torch  # noqa: E402
 

@@ -2,7 +2,7 @@
 (hipMemcpyAsync in 512 MB pieces, as ops/extsort._copy issues them) and by a CU copy kernel that
 reads or writes the page-locked host buffer through its device mapping (ops/channel.copy_wide).
 
-    python tools/microbench_pcie.py [GB per direction] [--grids 256,1024]
+    python tools/micro/microbench_pcie.py [GB per direction] [--grids 256,1024]
 
 The out-of-core sort's bucket phase streams one direction up and the other down at the same
 time; this measures which engine mix moves the most bytes per second.
@@ -11,7 +11,7 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import torch  # noqa: E402
 

@@ -1,7 +1,7 @@
 """TeraSort in HBM with the input rows at a 100-byte vs a 128-byte pitch: generator (+ E64 keys),
 compact radix sort, row gather with the run fix-up -- timed phase by phase, outputs compared.
 
-    python tools/microbench_pitch.py [rows] [--span r1,r2,...] [--xcd]
+    python tools/micro/microbench_pitch.py [rows] [--span r1,r2,...] [--xcd]
 
 ``--span``: only the 128-byte-pitch gather, for several row counts inside one allocation (ns per
 row against the span of the random reads).
@@ -14,7 +14,7 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import torch  # noqa: E402
 
@@ -80,7 +80,7 @@ def main():
             rows_m = buf[: m * 128].view(m, 128)
             _lib.check(lib.dr_terasort_gen_keys64_pitch128(ptr(rows_m), c_u64(m), c_u64(0), c_u64(7), ptr(keys),
                                                            c_u32(0), None, None, stream_of(buf)), "gen pitch128")
-            srt = S.sort_entries64(keys[:m], tmp[:m], 32)
+            srt = S.sort_entries64(keys[:m], tmp[:m], 32, err=S.lookback_error())
             best = None
             for _ in range(3):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -106,7 +106,7 @@ def main():
             _lib.check(lib.dr_terasort_gen_keys64_pitch128(ptr(buf), c_u64(n), c_u64(0), c_u64(7), ptr(keys), c_u32(0),
                                                            None, None, stream_of(buf)), "gen pitch128")
         ev[1].record()
-        srt = S.sort_entries64(keys, tmp, 32)
+        srt = S.sort_entries64(keys, tmp, 32, err=S.lookback_error())
         ev[2].record()
         flag.zero_()
         if pitch == 100:

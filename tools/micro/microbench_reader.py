@@ -1,14 +1,14 @@
 """Page cache -> HBM bandwidth of the chunked pinned reader (io/reader.py) vs the old
 read() -> bytearray -> pageable H2D path.  The file is written first (so it sits in the page cache).
 
-    python tools/microbench_reader.py [GB]
+    python tools/micro/microbench_reader.py [GB]
 """
 import json
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

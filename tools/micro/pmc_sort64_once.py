@@ -1,9 +1,9 @@
 """One compact (E64) radix sort of n generated TeraSort keys, for rocprofv3 PMC passes over the
-count / scatter kernels.   python tools/pmc_sort64_once.py [n]"""
+count / scatter kernels.   python tools/micro/pmc_sort64_once.py [n]"""
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import torch  # noqa: E402
 
@@ -18,7 +18,7 @@ def main():
     tmp = torch.empty(n, dtype=torch.int64, device="cuda")
     TS.generate_with_keys64(rows, 0, 7, ent)
     del rows
-    S.sort_entries64(ent, tmp, 32)
+    S.sort_entries64(ent, tmp, 32, err=S.lookback_error())
     torch.cuda.synchronize()
     print("sorted", n, flush=True)
 
