@@ -9,6 +9,7 @@
 #include "fifo.h"
 #include "jobgraph.h"
 #include "partreader.h"
+#include "partwriter.h"
 #include "workqueue.h"
 
 namespace py = pybind11;
@@ -294,6 +295,29 @@ PYBIND11_MODULE(_dryad_native, m) {
       .def("stop", [](ChunkReader& r) {
         py::gil_scoped_release nogil;
         r.stop();
+      });
+  // ChunkWriter: ring of caller-owned (pinned) host buffers -> file, several writer threads.
+  py::class_<ChunkWriter>(m, "ChunkWriter")
+      .def(py::init<const std::string&, const std::vector<uint64_t>&, int, int64_t>(), py::arg("path"),
+           py::arg("buffers"), py::arg("threads"), py::arg("extend_bytes") = (int64_t)(256ll << 20))
+      .def("acquire", [](ChunkWriter& w) {
+        int s;
+        {
+          py::gil_scoped_release nogil;
+          s = w.acquire();
+        }
+        if (s < 0) throw std::runtime_error("ChunkWriter: " + w.error());
+        return s;
+      })
+      .def("submit", &ChunkWriter::submit)
+      .def("finish", [](ChunkWriter& w, int64_t size) {
+        py::gil_scoped_release nogil;
+        return w.finish(size);
+      })
+      .def("error", &ChunkWriter::error)
+      .def("abort", [](ChunkWriter& w) {
+        py::gil_scoped_release nogil;
+        w.abort();
       });
   m.def("write_file_atomic", [](const std::string& path, py::buffer b) {
     py::buffer_info bi = b.request();

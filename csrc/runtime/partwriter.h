@@ -1,0 +1,54 @@
+// ChunkWriter: a part file written from a ring of caller-owned (page-locked) host buffers by a
+// pool of writer threads, so the caller can DMA the next chunk out of HBM while earlier ones are
+// written.  The native side of the HBM -> partfile path (reference: the overlapped channel writer
+// DryadVertex/VertexHost/system/channel/src/channelbuffernativewriter.cpp, which extends its file
+// in 256 MB steps, s_fileExtendChunk at :35, and keeps several writes in flight).  The HIP copies
+// stay on the Python side (io/writer.py): the writer only drains host buffers.
+//
+//   acquire()                 a free buffer slot (blocks while every slot is queued / writing)
+//   submit(slot, off, bytes)  write the slot's first `bytes` bytes at file offset `off`; the file
+//                             is pre-extended ahead of the writes in `extend` steps
+//   finish(size)              wait for every write, cut the file to `size`, close it
+#pragma once
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace dryad {
+
+class ChunkWriter {
+ public:
+  ChunkWriter(const std::string& path, const std::vector<uint64_t>& buf_ptrs, int threads, int64_t extend_bytes);
+  ~ChunkWriter();
+  int acquire();                                   // -1 on error (see error())
+  void submit(int slot, int64_t offset, int64_t bytes);
+  int64_t finish(int64_t final_size);              // bytes written; throws on error
+  std::string error();
+  void abort();                                    // stop the threads, close (the file stays)
+
+ private:
+  struct Job {
+    int slot;
+    int64_t off, bytes;
+  };
+  void run();
+  void extend_to(int64_t end);
+  int fd_ = -1;
+  std::string path_;
+  int64_t extend_ = 0, allocated_ = 0, written_ = 0;
+  std::vector<uint8_t*> bufs_;
+  std::vector<std::thread> pool_;
+  std::mutex mu_, ext_mu_;
+  std::condition_variable cv_job_, cv_free_, cv_idle_;
+  std::deque<int> free_;
+  std::deque<Job> jobs_;
+  int active_ = 0;
+  bool stop_ = false;
+  std::string err_;
+};
+
+}  // namespace dryad

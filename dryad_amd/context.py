@@ -115,6 +115,8 @@ _DEFAULTS = dict(
     RerunInputsMaxBytes=1 << 30,  # inputs a failed GPU vertex's restart record may persist
     ExternalSortToDisk=None,      # its partfile:// output written through a memory-mapped part file
     #                               (None: when the output exceeds half of the available host memory)
+    GraceJoin=None,               # a Join as the partitioned grace join stage (runtime/grace_stage.py;
+    #                               None: when its inputs would crowd the HBM budget; False: never)
 )
 
 _READONLY_AFTER_USE = set(_DEFAULTS) - {"LocalDebug"}

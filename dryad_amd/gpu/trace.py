@@ -84,22 +84,39 @@ class Col:
                              rounding_mode="floor"))
 
     def __mod__(self, o):
-        return Col(torch.remainder(self.t, _t(o)))
+        return Col(torch.remainder(*_promote(self.t, _t(o))))
 
     def __rmod__(self, o):
         return Col(torch.remainder(torch.full_like(self.t, o), self.t))
 
 
-def _bin(name, fn, rfn=None):
+def _bin(name, fn, rfn=None, arith=False):
+    if arith:
+        setattr(Col, f"__{name}__", lambda a, b: Col(fn(*_promote(a.t, _t(b)))))
+        if rfn is not None:
+            setattr(Col, f"__r{name}__", lambda a, b: Col(rfn(*_promote(a.t, _t(b)))))
+        return
     setattr(Col, f"__{name}__", lambda a, b: Col(fn(a.t, _t(b))))
     if rfn is not None:
         setattr(Col, f"__r{name}__", lambda a, b: Col(rfn(a.t, _t(b))))
 
 
-_bin("add", lambda a, b: a + b, lambda a, b: b + a)
-_bin("sub", lambda a, b: a - b, lambda a, b: b - a)
-_bin("mul", lambda a, b: a * b, lambda a, b: b * a)
-_bin("pow", lambda a, b: a ** b, lambda a, b: b ** a)
+def _promote(a, b):
+    """Arithmetic with a floating operand runs in float64, as the LocalDebug oracle's Python
+    floats (and C#'s long * double) do: torch alone would compute int64 column * 1.5 in float32."""
+    fb = isinstance(b, float) or isinstance(b, torch.Tensor) and b.is_floating_point()
+    if a.is_floating_point() or fb:
+        if a.dtype != torch.float64:
+            a = a.to(torch.float64)
+        if isinstance(b, torch.Tensor) and b.dtype != torch.float64:
+            b = b.to(torch.float64)
+    return a, b
+
+
+_bin("add", lambda a, b: a + b, lambda a, b: b + a, arith=True)
+_bin("sub", lambda a, b: a - b, lambda a, b: b - a, arith=True)
+_bin("mul", lambda a, b: a * b, lambda a, b: b * a, arith=True)
+_bin("pow", lambda a, b: a ** b, lambda a, b: b ** a, arith=True)
 _bin("and", lambda a, b: a & b, lambda a, b: b & a)
 _bin("or", lambda a, b: a | b, lambda a, b: b | a)
 _bin("xor", lambda a, b: a ^ b, lambda a, b: b ^ a)

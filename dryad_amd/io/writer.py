@@ -1,0 +1,163 @@
+"""HBM -> file: a part file written by the native ChunkWriter (csrc/runtime/partwriter.cpp:
+writer threads pwrite() 64 MB chunks out of a ring of page-locked host buffers, pre-extending the
+file in 256 MB steps) while the next chunks are DMA'd out of HBM on a copy stream, so PCIe
+transfers and the page-cache / disk writes overlap.  Replaces device -> pageable ``cpu()`` ->
+``tobytes()`` -> Python ``write`` (a full host copy of the partition and a serial write).
+Reference: the overlapped native channel writer,
+DryadVertex/VertexHost/system/channel/src/channelbuffernativewriter.cpp (256 MB extends at :35).
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+import time
+from collections import deque
+
+import torch
+
+CHUNK = 64 << 20
+SLOTS = 8
+THREADS = 4
+
+_RING = None
+_RING_LOCK = threading.Lock()
+
+
+def _ring():
+    """The process's pinned staging ring for writes (registered once; reused by every writer)."""
+    global _RING
+    with _RING_LOCK:
+        if _RING is None:
+            if torch.cuda.is_available():
+                from ..ops._lib import PinnedHostBuffer
+                _RING = [PinnedHostBuffer((CHUNK,)) for _ in range(SLOTS)]
+            else:                    # no GPU: plain host buffers (host sources only)
+                _RING = [_HostBuffer(CHUNK) for _ in range(SLOTS)]
+        return _RING
+
+
+class _HostBuffer:
+    def __init__(self, n):
+        self.tensor = torch.empty(n, dtype=torch.uint8)
+
+
+class WriteStats:
+    def __init__(self):
+        self.bytes = 0
+        self.seconds = 0.0
+
+    @property
+    def gbps(self) -> float:
+        return self.bytes / 1e9 / self.seconds if self.seconds else 0.0
+
+
+class PartWriter:
+    """Append device (or host) byte tensors to a new file; ``close()`` returns the byte count.
+    One writer per process at a time owns the ring (``with PartWriter(...) as w``)."""
+
+    def __init__(self, path: str, device=None, stats: WriteStats | None = None):
+        from ..native import runtime
+        self.path = path
+        self.stats = stats
+        self.t0 = time.perf_counter()
+        self.ring = _ring()
+        _RING_LOCK.acquire()
+        try:
+            self.w = runtime().ChunkWriter(path, [b.tensor.data_ptr() for b in self.ring], THREADS)
+        except Exception:
+            _RING_LOCK.release()
+            raise
+        self.dev = torch.device(device) if device is not None else None
+        self.cs = torch.cuda.Stream(self.dev) if self.dev is not None and self.dev.type == "cuda" else None
+        self.off = 0
+        self.pending = deque()           # (slot, event, file offset, bytes): D2H copies in flight
+        self.closed = False
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, et, e, tb):
+        if et is None:
+            self.close()
+        else:
+            self.abort()
+
+    def _submit_done(self, block: bool):
+        while self.pending and (block or self.pending[0][1] is None or self.pending[0][1].query()):
+            slot, ev, off, n = self.pending.popleft()
+            if ev is not None:
+                ev.synchronize()
+            self.w.submit(slot, off, n)
+
+    def write(self, data) -> None:
+        """Append ``data``: a contiguous device or host tensor (its bytes), or a bytes-like object."""
+        from ..ops import _lib
+        if not isinstance(data, torch.Tensor):
+            data = torch.frombuffer(bytearray(data), dtype=torch.uint8) if len(data) else torch.empty(0, dtype=torch.uint8)
+        flat = data.reshape(-1).view(torch.uint8)
+        n = flat.numel()
+        if n == 0:
+            return
+        dev_src = flat.is_cuda
+        if dev_src:
+            if self.cs is None:
+                self.dev = flat.device
+                self.cs = torch.cuda.Stream(self.dev)
+            self.cs.wait_stream(torch.cuda.current_stream(flat.device))
+        piece = min(CHUNK, self.ring[0].tensor.numel())        # the ring may predate a CHUNK change
+        for a in range(0, n, piece):
+            m = min(piece, n - a)
+            self._submit_done(block=False)
+            while len(self.pending) > SLOTS - 2:        # keep slots on the native side: acquire returns
+                self._submit_oldest()
+            slot = self.w.acquire()
+            dst = self.ring[slot].tensor[:m]
+            if dev_src:
+                _lib.memcpy_async(dst, flat[a:a + m], self.cs)
+                ev = torch.cuda.Event()
+                ev.record(self.cs)
+            else:
+                ctypes.memmove(dst.data_ptr(), flat[a:a + m].data_ptr(), m)
+                ev = None
+            self.pending.append((slot, ev, self.off, m))
+            self.off += m
+
+    def _submit_oldest(self):
+        slot, ev, off, n = self.pending.popleft()
+        if ev is not None:
+            ev.synchronize()
+        self.w.submit(slot, off, n)
+
+    def close(self) -> int:
+        if self.closed:
+            return self.off
+        try:
+            self._submit_done(block=True)
+            self.w.finish(self.off)
+        finally:
+            self.closed = True
+            _RING_LOCK.release()
+        if self.stats is not None:
+            self.stats.bytes += self.off
+            self.stats.seconds += time.perf_counter() - self.t0
+        return self.off
+
+    def abort(self):
+        if self.closed:
+            return
+        try:
+            for _, ev, _, _ in self.pending:
+                if ev is not None:
+                    ev.synchronize()
+            self.pending.clear()
+            self.w.abort()
+        finally:
+            self.closed = True
+            _RING_LOCK.release()
+
+
+def write_device(path: str, data: torch.Tensor, stats: WriteStats | None = None) -> int:
+    """Write one device (or host) tensor's bytes to a new file at ``path``."""
+    with PartWriter(path, data.device if isinstance(data, torch.Tensor) else None, stats) as w:
+        w.write(data)
+    return w.off

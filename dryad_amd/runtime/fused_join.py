@@ -389,6 +389,16 @@ def run(desc, runner, lay) -> dict:
         stats = grace.stats
     finally:
         grace.release()
+    # the device sums are int64: exact only while matches x max |value| < 2^63 per side (the
+    # reference's checked Sum throws on overflow).  Decided collectively, so every rank declines
+    # together and the compiled stages (whose Sum detects overflow) take over.
+    big = torch.tensor([0], dtype=torch.int64, device=dev)
+    for side, f in ((0, lay["vo"]), (1, lay["vi"])):
+        if f is not None and cnt * max((_max_abs(x, f, dev) for x in srcs[side]), default=0) >= (1 << 63):
+            big.fill_(1)
+    shuffle.all_reduce_(big, "max", w)
+    if int(big.item()):
+        raise OverflowError("fused join: int64 sums could overflow for these values")
     s_o, s_i = (s_build, s_probe) if build == 0 else (s_probe, s_build)
     total = lay["co"] * s_o + lay["ci"] * s_i + lay["const"] * cnt
     runner.join_stats = dict(spilled_bytes=stats.spilled_bytes, buckets=stats.buckets, resident=stats.resident,
@@ -404,6 +414,16 @@ def run(desc, runner, lay) -> dict:
     else:
         res = [[total]] + [[0]] * (len(parts) - 1)
     return dict(zip(parts, res))
+
+
+def _max_abs(src, f, dev) -> int:
+    """Bound on |value| of field f of a row source: the generator's value contract (keys below
+    ``keys``, payloads 31-bit), or a device min/max pass over a resident column."""
+    if isinstance(src, _GenRows):
+        return max(src.nk, 1 << 31)
+    from ..gpu import stats
+    lo, hi = stats.bounds([src.t.cols[src.fields[f]]])[0]
+    return max(abs(lo), abs(hi))
 
 
 def vote(desc, runner):

@@ -42,6 +42,7 @@ from ..parallel.comm import World, get_world, init_world
 from ..utils import trace as TRC
 from ..utils.log import get_logger
 from . import fused_join as FJ
+from . import grace_stage as GS
 from . import vertex_ops as V
 from .executor import _BaseExecutor
 
@@ -122,6 +123,8 @@ class GpuJobRunner:
         self.channels: dict = {}          # (stage, partition) -> DeviceTable | Ported | list | list-of-lists
         self.fallbacks: list = []
         self.op_counts = collections.Counter()   # (operator, "device" | "host") -> executions
+        from ..io.writer import WriteStats
+        self.write_stats = WriteStats()          # partfile parts written by this job
         self.transports: list = []      # (stage, edge kind, "device" | "object", bytes / reason)
         self.timings: dict = {}
         R = native_runtime()
@@ -790,21 +793,32 @@ class GpuJobRunner:
         fused_first = {f["stages"][0]: mid for mid, f in self.fused.items()}
         active_fused = {}
         self.fused_joins = FJ.find(self.plan) if self.gpu_ok else {}
-        join_first = {min(d["stages"]): jid for jid, d in self.fused_joins.items()}
+        self.grace_joins = GS.find(self.plan) if self.gpu_ok else {}
+        join_first = {min(d["stages"]): jid for jid, d in list(self.fused_joins.items()) + list(self.grace_joins.items())}
         precomputed = {}
         for s in self.plan.stages:
             t0 = time.time()
             status, err = 0, ""
             if s.id in join_first:
-                out = self._try_fused_join(self.fused_joins[join_first[s.id]])
+                jid = join_first[s.id]
+                out, rest, how = None, [], ""
+                if jid in self.fused_joins:
+                    out, rest, how = self._try_fused_join(self.fused_joins[jid]), self.fused_joins[jid]["rest"], \
+                        "fused grace join"
+                if out is None and jid in self.grace_joins:
+                    desc = self.grace_joins[jid]
+                    lay = GS.vote(desc, self)
+                    if lay is not None:
+                        out, rest, how = self._attempt_stage(self.plan.stages[jid], lambda: GS.run(desc, self, lay)), \
+                            [], "grace join stage"
                 if out is not None:
-                    precomputed[join_first[s.id]] = out
-                    self.skipped.update(self.fused_joins[join_first[s.id]]["stages"])
-                    self.timings[f"{join_first[s.id]}:Join(fused grace join)"] = time.time() - t0
+                    precomputed[jid] = (out, rest)
+                    self.skipped.update((self.fused_joins.get(jid) or self.grace_joins[jid])["stages"])
+                    self.timings[f"{jid}:Join({how})"] = time.time() - t0
             if s.id in precomputed:
                 refresh()
-                rest = self.fused_joins[s.id]["rest"]
-                for p, v in precomputed.pop(s.id).items():
+                outs, rest = precomputed.pop(s.id)
+                for p, v in outs.items():
                     vctx = GpuVertexContext(p, s.partitions, self.vids[s.id][p], 0, s, self.dev, self.world, self)
                     for op in rest:                 # the join stage's program after the aggregate
                         v = self._run_op(op, [v], vctx, s)
@@ -860,6 +874,7 @@ class GpuJobRunner:
                 self.pool.release(b)
         return dict(committed=committed, fallbacks=self.fallbacks, timings=self.timings, transports=self.transports,
                     op_counts={f"{k[0]}:{k[1]}": v for k, v in self.op_counts.items()},
+                    write=dict(bytes=self.write_stats.bytes, seconds=round(self.write_stats.seconds, 4)),
                     statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()],
                     external_sort=getattr(self, "extsort_stats", None), join=getattr(self, "join_stats", None),
                     recovery=self.recovery)
@@ -1002,22 +1017,25 @@ class GpuJobRunner:
 
     def _try_fused_join(self, desc):
         """Run a Join + aggregate idiom as one fused grace join stage (runtime/fused_join.py) when
-        every rank can; None (the plan's stages run as compiled) otherwise.
-
-        Attempts are voted like a gang stage's (``_run_gang``): injected faults on the join stage's
-        partitions are agreed before the body (fail, read_error) or after it (crash), and a failed
-        attempt is re-run from its inputs (generated or HBM-resident, so re-readable) until
-        MaxVertexFailures.  An exception raised on EVERY rank (e.g. an allocation the budget check
-        let through) means every rank left the body together: the compiled stages run instead.
-        One raised on some ranks only leaves the others in a collective; the communicator's error
-        handling then ends the job (parallel/comm.py)."""
+        every rank can; None (the plan's stages run as compiled) otherwise."""
         lay = FJ.vote(desc, self)
         if lay is None:
             return None
-        st = self.plan.stages[desc["join"]]
+        return self._attempt_stage(self.plan.stages[desc["join"]], lambda: FJ.run(desc, self, lay))
+
+    def _attempt_stage(self, st, body):
+        """Versioned, voted attempts of a precomputed (fused) join stage, whose vertices the main
+        loop completes later.  Attempts are voted like a gang stage's (``_run_gang``): injected
+        faults on the stage's partitions are agreed before the body (fail, read_error) or after it
+        (crash), and a failed attempt is re-run from its inputs (generated, HBM-resident or stored,
+        so re-readable) until MaxVertexFailures.  An exception raised on EVERY rank (e.g. an
+        allocation the budget check let through) means every rank left the body together: None,
+        the compiled stages run instead.  One raised on some ranks only leaves the others in a
+        collective; the communicator's error handling then ends the job (parallel/comm.py)."""
         me = self.world.rank
         mine = [p for p in range(st.partitions) if self.owner(p) == me]
         limit = int(getattr(self.ctx, "MaxVertexFailures", 6) or 6)
+        outcome = None
         for version in range(limit):
             faults = {p: self._fault(st, p, version) for p in mine}
             pre = next(((p, k) for p, k in faults.items() if k in ("fail", "read_error")), None)
@@ -1027,25 +1045,28 @@ class GpuJobRunner:
             if outcome is None:
                 err = None
                 try:
-                    out = FJ.run(desc, self, lay)
+                    out = body()
                     crash = next((p for p, k in faults.items() if k == "crash"), None)
                     if crash is not None:
                         err = (crash, "crash", f"injected crash of {st.name}[{crash}] (output discarded)")
                 except Exception as e:  # noqa: BLE001
                     err = (mine[0] if mine else 0, "exception", f"{type(e).__name__}: {e}")
-                    log.warning("fused grace join attempt %d failed: %s", version, e)
+                    log.warning("%s attempt %d failed: %s", st.name, version, e)
                 outcome = self._vote(err)
                 real = outcome is not None and len(outcome) == self.world.size and \
                     all(e[1] == "exception" for _, e in outcome)
             if outcome is None:
                 return out
             if real:
-                self.recovery.append(("fused_join_declined", st.name, outcome[0][1][2]))
+                self.recovery.append(("fused_stage_declined", st.name, outcome[0][1][2]))
                 return None
             for _, (p, kind, _msg) in outcome:
                 self.recovery.append(("upstream" if kind == "read_error" else "gang_restart", st.name, p))
         raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed,
-                                    f"fused grace join {st.name} failed {limit} times: {outcome[0][1][2]}")
+                                    f"{st.name} failed {limit} times: {outcome[0][1][2]}")
+
+    def _vertex_ctx(self, s, p, version=0):
+        return GpuVertexContext(p, s.partitions, self.vids[s.id][p], version, s, self.dev, self.world, self)
 
     def _release(self, s):
         later = {i.src for st in self.plan.stages if st.id > s.id for i in st.inputs}
@@ -1130,11 +1151,21 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     from .. import types as T
     from ..io import binary as B
     from ..io import partfile as PF
+    from ..io import writer as WR
     from ..ops import codec as CD
     from .jobmanager import write_schema
     W, me = runner.world.size, runner.world.rank
     dt = s.dtype
     rows_fmt = any(isinstance(v, HostRows) for v in local.values())
+    streamed = [v for v in local.values() if isinstance(v, GS.StreamedPart)]
+    if streamed and (dt is None or dt == T.Pickle):
+        dt = streamed[0].dtype
+    if W > 1 and (dt is None or dt == T.Pickle):
+        # the record type one rank learnt from its streamed part (ranks without rows have none)
+        allts = [None] * W
+        dist.all_gather_object(allts, None if dt is None or dt == T.Pickle else T.dtype_to_json(dt))
+        got = next((x for x in allts if x is not None), None)
+        dt = T.dtype_from_json(got) if got is not None else dt
     if not rows_fmt and (dt is None or dt == T.Pickle):
         return False
     prov = provider_for(uri)
@@ -1150,10 +1181,17 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     mine, fmt_extra = {}, None
     for p, v in local.items():
         tmp = PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, 0)
+        if isinstance(v, GS.StreamedPart):          # written bucket by bucket by its stage
+            os.replace(v.path, tmp)
+            mine[p] = tmp
+            continue
         if rows_fmt:
-            # raw fixed-width rows straight from the pinned host tier (out-of-core sort output)
-            if not isinstance(v, HostRows):
-                v = HostRows.from_tensor(v.rows, v.shape.key_off, v.shape.key_len, pinned=False)
+            # raw fixed-width rows: device rows or the pinned host tier (out-of-core sort output)
+            if isinstance(v, DeviceTable):
+                WR.write_device(tmp, v.rows[: v.n], stats=runner.write_stats)
+                fmt_extra = dict(stride=v.rows.shape[1], key_off=v.shape.key_off, key_len=v.shape.key_len)
+                mine[p] = tmp
+                continue
             if getattr(v, "path", None) and os.path.exists(v.path):
                 # disk tier: the rows already are a file; flush it and rename it into place
                 v.flush()
@@ -1161,9 +1199,7 @@ def _commit_partfile_impl(runner, s, uri, path, local):
                     os.truncate(v.path, v.n * v.stride)
                 os.replace(v.path, tmp)
             else:
-                with open(tmp, "wb") as f:
-                    if v.n:
-                        f.write(memoryview(v.rows.numpy()).cast("B"))
+                WR.write_device(tmp, v.rows[: v.n], stats=runner.write_stats)
             fmt_extra = dict(stride=v.stride, key_off=v.key_off, key_len=v.key_len)
             mine[p] = tmp
             continue
@@ -1174,16 +1210,16 @@ def _commit_partfile_impl(runner, s, uri, path, local):
             if enc is not None:
                 data, boffs = enc
                 index = (v.n, data.numel(), boffs.cpu().numpy(), CD.BLOCK)
-        raw = data.cpu().numpy().tobytes() if data is not None else None
         if runner.ctx.OutputDataCompressionScheme.value != 0:
             import gzip
-            if raw is None:
-                raw = B.encode_records(dt, _to_objects(v) if not isinstance(v, list) else v)
-            raw = gzip.compress(raw, compresslevel=6)
-        if raw is not None:
+            raw = data.cpu().numpy().tobytes() if data is not None else \
+                B.encode_records(dt, _to_objects(v) if not isinstance(v, list) else v)
             with open(tmp, "wb") as f:
-                f.write(raw)
-            if index is not None and runner.ctx.OutputDataCompressionScheme.value == 0:
+                f.write(gzip.compress(raw, compresslevel=6))
+        elif data is not None:
+            # device-encoded records: HBM -> pinned ring -> native writer threads
+            WR.write_device(tmp, data, stats=runner.write_stats)
+            if index is not None:
                 PF.write_index(tmp, index[0], index[1], index[2], index[3])
         else:
             B.write_records(tmp, dt, _to_objects(v) if not isinstance(v, list) else v)
