@@ -4,8 +4,9 @@
 // serialises as the little-endian fields back to back (reference DryadLinqBinaryWriter.cs
 // WriteRawBytes of each primitive; DryadLinqCodeGen.cs:1041-1096 field order), so a partfile
 // part of such records is an [n, width] byte matrix.  Decoding = scattering each field's bytes
-// into its column (AoS -> SoA), encoding = the reverse; one thread per (record, field).  Bytes
-// are moved with byte loads/stores because fields need not be aligned inside the record.
+// into its column (AoS -> SoA), encoding = the reverse: records of <= 128 bytes through LDS tiles
+// (codec_tile_kernel), wider ones one thread per (record, field) with byte loads / stores
+// (fields need not be aligned inside the record).
 #include "common.h"
 
 namespace {
@@ -34,6 +35,78 @@ __global__ __launch_bounds__(256) void codec_kernel(uint8_t* __restrict__ rows, 
     }
   }
 }
+
+// Tiled variant (records of <= 128 bytes): a 256-record tile moves between HBM and LDS as whole
+// 16-byte chunks (coalesced, from the first 16-byte boundary of the tile on), and between LDS and
+// the columns one element per thread (coalesced column access).  The per-(record, field) kernel
+// above issues one byte load and one byte store per byte at a record stride.  Encode writes the
+// tile's partial first / last chunks byte by byte (their other bytes belong to the neighbouring
+// tiles).
+__device__ __forceinline__ uint64_t lds_bytes(const uint8_t* p, uint32_t sz) {
+  uint64_t v = 0;
+  for (uint32_t b = 0; b < sz; ++b) v |= (uint64_t)p[b] << (8 * b);
+  return v;
+}
+
+template <bool DECODE>
+__global__ __launch_bounds__(256) void codec_tile_kernel(uint8_t* __restrict__ rows, uint64_t n, uint32_t width, int nf,
+                                                         FieldMap m) {
+  __shared__ uint4 img[(256 * 128 + 32) / 16];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(img);
+  const uint32_t t = threadIdx.x;
+  for (uint64_t row0 = (uint64_t)blockIdx.x * 256; row0 < n; row0 += (uint64_t)gridDim.x * 256) {
+    const uint32_t nr = (uint32_t)((n - row0) < 256 ? (n - row0) : 256);
+    uint8_t* a = rows + row0 * width;
+    const uint32_t shift = (uint32_t)(reinterpret_cast<uintptr_t>(a) & 15);
+    uint4* base = reinterpret_cast<uint4*>(a - shift);
+    const uint32_t bytes = nr * width;
+    const uint32_t chunks = (bytes + shift + 15) / 16;
+    __syncthreads();                               // the previous tile is done with the LDS image
+    if (DECODE) {
+      for (uint32_t c = t; c < chunks; c += 256) img[c] = base[c];
+      __syncthreads();
+      for (int f = 0; f < nf; ++f) {
+        const uint32_t sz = m.size[f];
+        if (t < nr) {
+          const uint8_t* src = lds + shift + t * width + m.off[f];
+          uint8_t* dst = m.col[f] + (row0 + t) * sz;
+          if (sz == 8) *reinterpret_cast<uint64_t*>(dst) = lds_bytes(src, 8);
+          else if (sz == 4) *reinterpret_cast<uint32_t*>(dst) = (uint32_t)lds_bytes(src, 4);
+          else if (sz == 2) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)lds_bytes(src, 2);
+          else for (uint32_t b = 0; b < sz; ++b) dst[b] = src[b];
+        }
+      }
+    } else {
+      for (int f = 0; f < nf; ++f) {
+        const uint32_t sz = m.size[f];
+        if (t < nr) {
+          uint8_t* dst = lds + shift + t * width + m.off[f];
+          const uint8_t* src = m.col[f] + (row0 + t) * sz;
+          uint64_t v = 0;
+          if (sz == 8) v = *reinterpret_cast<const uint64_t*>(src);
+          else if (sz == 4) v = *reinterpret_cast<const uint32_t*>(src);
+          else if (sz == 2) v = *reinterpret_cast<const uint16_t*>(src);
+          if (sz == 8 || sz == 4 || sz == 2) {
+            for (uint32_t b = 0; b < sz; ++b) dst[b] = (uint8_t)(v >> (8 * b));
+          } else {
+            for (uint32_t b = 0; b < sz; ++b) dst[b] = src[b];
+          }
+        }
+      }
+      __syncthreads();
+      for (uint32_t c = t; c < chunks; c += 256) {
+        const uint32_t c0 = c * 16;                 // chunk bytes [c0, c0 + 16) of the image
+        if (c0 >= shift && c0 + 16 <= shift + bytes) {
+          base[c] = img[c];
+        } else {
+          uint8_t* d = reinterpret_cast<uint8_t*>(base + c);
+          for (uint32_t b = 0; b < 16; ++b)
+            if (c0 + b >= shift && c0 + b < shift + bytes) d[b] = lds[c0 + b];
+        }
+      }
+    }
+  }
+}
 }  // namespace
 
 // direction 0: rows -> columns (decode), 1: columns -> rows (encode).  offs/sizes/cols are host
@@ -48,6 +121,18 @@ DR_API int dr_codec_fixed(uint8_t* rows, uint64_t n, uint32_t width, int nf, con
     m.size[f] = sizes[f];
     m.col[f] = cols[f];
     if (offs[f] + sizes[f] > width) return (int)hipErrorInvalidValue;
+  }
+  bool aligned_cols = true;                    // column element stores need natural alignment
+  for (int f = 0; f < nf; ++f)
+    if (reinterpret_cast<uintptr_t>(cols[f]) % (sizes[f] <= 8 ? sizes[f] : 1)) aligned_cols = false;
+  if (width <= 128 && aligned_cols) {
+    const unsigned g = grid_for(n, 256, 16384);
+    if (direction == 0)
+      codec_tile_kernel<true><<<g, 256, 0, s>>>(rows, n, width, nf, m);
+    else
+      codec_tile_kernel<false><<<g, 256, 0, s>>>(rows, n, width, nf, m);
+    DR_LAUNCH_CHECK();
+    return 0;
   }
   const unsigned g = grid_for(n * (uint64_t)nf, 256, 16384);
   if (direction == 0)

@@ -271,6 +271,7 @@ __global__ __launch_bounds__(kDgThreads) void dg_scatter_kernel(DgPack pk, const
 
 struct DgAgg {
   uint32_t nacc;
+  uint32_t pack;                 // PACK: the Sum accumulator that carries the count
   uint32_t op[kDgMaxCols];       // 0 = sum, 1 = min, 2 = max (of the column's offsets)
   uint32_t field_off[kDgMaxCols];
   uint32_t field_bits[kDgMaxCols];
@@ -281,65 +282,75 @@ struct DgAgg {
 // rows.  Workgroup b folds the runs [wrun[b], wrun[b + 1]) (equal row shares) into its LDS table,
 // kU * 512 rows per step with the next step's rows (possibly of the next run) in flight, and
 // emits the table at the end of each run: no barrier inside a run.
-__global__ __launch_bounds__(kDgThreads) void dg_agg_kernel(const uint4* __restrict__ rows,
-                                                            const int64_t* __restrict__ rstart,
-                                                            const int64_t* __restrict__ wrun, uint32_t kbits,
-                                                            int64_t kmin, DgAgg ag, unsigned long long* __restrict__ head,
-                                                            int64_t* __restrict__ okey, int64_t* __restrict__ ocnt,
-                                                            int64_t* __restrict__ oacc0, int64_t* __restrict__ oacc1,
-                                                            int64_t* __restrict__ oacc2) {
-  __shared__ uint32_t cnt[kDgSlots];
-  __shared__ unsigned long long acc[kDgMaxCols][kDgSlots];
-  __shared__ uint32_t sc[kDgWaves];
-  __shared__ unsigned long long obase;
-  const int t = threadIdx.x;
-  int64_t* const oacc[3] = {oacc0, oacc1, oacc2};
-  constexpr int kSlotsPer = kDgSlots / kDgThreads;
+//
+// PACK (a Sum aggregate ag.pack of a field of <= 32 bits, runs of < 2^16 rows): the count rides
+// in the top 16 bits of that sum's 64-bit slot, one LDS atomic per row fewer.
+//
+// Emission: slot q * 512 + t is thread t's in round q.  Each wave compacts its occupied slots of a
+// round with a ballot, so every wave store writes one contiguous range of each output column (the
+// slot-major assignment wrote 8 scattered elements per thread and cost ~2.5x the bytes written).
+template <bool PACK>
+__device__ __forceinline__ void dg_agg_body(const uint4* __restrict__ rows, const int64_t* __restrict__ rstart,
+                                            const int64_t* __restrict__ wrun, int64_t kmin, const DgAgg& ag,
+                                            unsigned long long* __restrict__ head, int64_t* __restrict__ okey,
+                                            int64_t* __restrict__ ocnt, int64_t* const* oacc, uint32_t* cnt,
+                                            unsigned long long (*acc)[kDgSlots], uint32_t* wtot,
+                                            unsigned long long* obase) {
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  constexpr int kRounds = kDgSlots / kDgThreads;
   constexpr int kU = 4;                                 // rows per thread per step
   constexpr uint64_t kStep = (uint64_t)kU * kDgThreads;
-  for (int q = 0; q < kSlotsPer; ++q) {
-    const int sl = t * kSlotsPer + q;
-    cnt[sl] = 0;
+  constexpr unsigned long long kOne = 1ull << 48, kLow = kOne - 1;
+  const int64_t r1 = wrun[blockIdx.x + 1];
+  auto reset = [&](int sl) {
+    if (!PACK) cnt[sl] = 0;
 #pragma unroll
     for (int a = 0; a < kDgMaxCols; ++a)
       if (a < (int)ag.nacc) acc[a][sl] = ag.op[a] == 1 ? ~0ull : 0ull;
-  }
-  const int64_t r1 = wrun[blockIdx.x + 1];
-  // emit the occupied slots of run `run`: count, reserve a range of the output, write, reset
+  };
+  for (int q = 0; q < kRounds; ++q) reset(q * kDgThreads + t);
   auto emit = [&](uint64_t run) {
-    uint32_t occ = 0;
+    uint32_t pos[kRounds];
+    uint32_t mine = 0;
 #pragma unroll
-    for (int q = 0; q < kSlotsPer; ++q) occ += cnt[t * kSlotsPer + q] != 0;
-    uint32_t total;
-    uint32_t pre = dg_block_scan(occ, sc, total);
-    if (t == 0) obase = atomicAdd(head, (unsigned long long)total);
+    for (int q = 0; q < kRounds; ++q) {
+      const int sl = q * kDgThreads + t;
+      const bool occ = PACK ? acc[ag.pack][sl] != 0ull : cnt[sl] != 0u;
+      const uint64_t bal = ballot64(occ);
+      pos[q] = popc_below(bal);
+      mine |= (uint32_t)occ << q;
+      if (l == 0) wtot[q * kDgWaves + w] = (uint32_t)__popcll(bal);
+    }
     __syncthreads();
-    const uint64_t o0 = obase;
+    if (t == 0) {
+      uint32_t total = 0;
+      for (int k = 0; k < kRounds * kDgWaves; ++k) total += wtot[k];
+      *obase = atomicAdd(head, (unsigned long long)total);
+    }
+    __syncthreads();
+    uint64_t o = *obase;
 #pragma unroll
-    for (int q = 0; q < kSlotsPer; ++q) {
-      const int sl = t * kSlotsPer + q;
-      const uint32_t c = cnt[sl];
-      if (c) {
-        const uint64_t o = o0 + pre++;
-        okey[o] = kmin + (int64_t)((run << kDgTableBits) | (uint64_t)sl);
-        ocnt[o] = c;
+    for (int q = 0; q < kRounds; ++q) {
+      uint32_t before = 0;
+      for (int k = 0; k < q * kDgWaves + w; ++k) before += wtot[k];
+      if ((mine >> q) & 1u) {
+        const int sl = q * kDgThreads + t;
+        const uint64_t oo = o + before + pos[q];
+        const uint32_t c = PACK ? (uint32_t)(acc[ag.pack][sl] >> 48) : cnt[sl];
+        okey[oo] = kmin + (int64_t)((run << kDgTableBits) | (uint64_t)sl);
+        ocnt[oo] = c;
 #pragma unroll
         for (int a = 0; a < kDgMaxCols; ++a) {
           if (a < (int)ag.nacc) {
-            const int64_t av = (int64_t)acc[a][sl];
-            oacc[a][o] = ag.op[a] == 0 ? av + (int64_t)c * ag.vmin[a] : av + ag.vmin[a];
+            const int64_t av = PACK && a == (int)ag.pack ? (int64_t)(acc[a][sl] & kLow) : (int64_t)acc[a][sl];
+            oacc[a][oo] = ag.op[a] == 0 ? av + (int64_t)c * ag.vmin[a] : av + ag.vmin[a];
           }
         }
-        cnt[sl] = 0;
-#pragma unroll
-        for (int a = 0; a < kDgMaxCols; ++a)
-          if (a < (int)ag.nacc) acc[a][sl] = ag.op[a] == 1 ? ~0ull : 0ull;
+        reset(sl);
       }
     }
     __syncthreads();
   };
-  // the step after (run r, rows from b, run end e): the next kStep rows of r, else the first rows
-  // of the next non-empty run (false: none left)
   auto advance = [&](int64_t& r, uint64_t& b, uint64_t& e) {
     if (b + kStep < e) { b += kStep; return true; }
     do {
@@ -373,12 +384,12 @@ __global__ __launch_bounds__(kDgThreads) void dg_agg_kernel(const uint4* __restr
         const uint4 rr = buf[u];
         const u128 v = (u128)rr.x | ((u128)rr.y << 32) | ((u128)rr.z << 64) | ((u128)rr.w << 96);
         const uint32_t sl = (uint32_t)((uint64_t)v & (kDgSlots - 1));
-        atomicAdd(&cnt[sl], 1u);
+        if (!PACK) atomicAdd(&cnt[sl], 1u);
 #pragma unroll
         for (int a = 0; a < kDgMaxCols; ++a) {
           if (a < (int)ag.nacc) {
             const unsigned long long f = dg_field(v, ag.field_off[a], ag.field_bits[a]);
-            if (ag.op[a] == 0) atomicAdd(&acc[a][sl], f);
+            if (ag.op[a] == 0) atomicAdd(&acc[a][sl], PACK && a == (int)ag.pack ? (kOne | f) : f);
             else if (ag.op[a] == 1) atomicMin(&acc[a][sl], f);
             else atomicMax(&acc[a][sl], f);
           }
@@ -396,6 +407,24 @@ __global__ __launch_bounds__(kDgThreads) void dg_agg_kernel(const uint4* __restr
     b = nbg;
     e = ne;
   }
+}
+
+__global__ __launch_bounds__(kDgThreads) void dg_agg_kernel(const uint4* __restrict__ rows,
+                                                            const int64_t* __restrict__ rstart,
+                                                            const int64_t* __restrict__ wrun, uint32_t kbits,
+                                                            int64_t kmin, DgAgg ag, unsigned long long* __restrict__ head,
+                                                            int64_t* __restrict__ okey, int64_t* __restrict__ ocnt,
+                                                            int64_t* __restrict__ oacc0, int64_t* __restrict__ oacc1,
+                                                            int64_t* __restrict__ oacc2, int pack) {
+  __shared__ uint32_t cnt[kDgSlots];
+  __shared__ unsigned long long acc[kDgMaxCols][kDgSlots];
+  __shared__ uint32_t wtot[(kDgSlots / kDgThreads) * kDgWaves];
+  __shared__ unsigned long long obase;
+  int64_t* const oacc[3] = {oacc0, oacc1, oacc2};
+  if (pack)
+    dg_agg_body<true>(rows, rstart, wrun, kmin, ag, head, okey, ocnt, oacc, cnt, acc, wtot, &obase);
+  else
+    dg_agg_body<false>(rows, rstart, wrun, kmin, ag, head, okey, ocnt, oacc, cnt, acc, wtot, &obase);
 }
 }  // namespace
 
@@ -480,11 +509,13 @@ DR_API int dr_dg_scatter(const int64_t* key, const int64_t* const* cols, const i
 // rows: packed rows sorted by run id (key offset >> table bits); rstart: int64 [runs + 1] row
 // offsets of the runs; wrun: int64 [G + 1] run ranges of the G workgroups.  ops / off / bits / vmin:
 // nacc accumulators over packed fields.  head (u64, zeroed) receives the group count; outputs are
-// sized by the caller (>= the number of groups).
+// sized by the caller (>= the number of groups).  pack: 1 + the index of a Sum accumulator over a
+// field of <= 32 bits when every run is shorter than 2^16 rows (the count then shares its LDS
+// slot), else 0.
 DR_API int dr_dg_aggregate(const void* rows, const int64_t* rstart, const int64_t* wrun, uint32_t G, uint32_t kbits,
                            int64_t kmin, uint32_t nacc, const uint32_t* ops, const uint32_t* off, const uint32_t* bits,
                            const int64_t* vmin, unsigned long long* head, int64_t* okey, int64_t* ocnt,
-                           int64_t* const* oacc, hipStream_t s) {
+                           int64_t* const* oacc, int pack, hipStream_t s) {
   if (nacc > (uint32_t)kDgMaxCols) return (int)hipErrorInvalidValue;
   DgAgg ag;
   ag.nacc = nacc;
@@ -496,10 +527,12 @@ DR_API int dr_dg_aggregate(const void* rows, const int64_t* rstart, const int64_
     if (a < nacc && (ag.op[a] > 2 || ag.field_bits[a] == 0 || ag.field_off[a] + ag.field_bits[a] > 128))
       return (int)hipErrorInvalidValue;
   }
+  ag.pack = pack > 0 ? (uint32_t)(pack - 1) : 0;
+  if (pack && (ag.pack >= nacc || ag.op[ag.pack] != 0 || ag.field_bits[ag.pack] > 32)) return (int)hipErrorInvalidValue;
   if (G == 0) return 0;
   dg_agg_kernel<<<G, kDgThreads, 0, s>>>(static_cast<const uint4*>(rows), rstart, wrun, kbits, kmin, ag, head, okey,
                                          ocnt, nacc > 0 ? oacc[0] : nullptr, nacc > 1 ? oacc[1] : nullptr,
-                                         nacc > 2 ? oacc[2] : nullptr);
+                                         nacc > 2 ? oacc[2] : nullptr, pack);
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -27,7 +27,7 @@ _lib.register_signatures({
     "dr_dg_scatter": (c_i32, [vp, ctypes.POINTER(vp), ctypes.POINTER(c_i64), ctypes.POINTER(c_u32), c_u32, c_i64,
                               c_u32, vp, c_u64, c_u32, c_u32, vp, c_u32, c_u64, vp, vp]),
     "dr_dg_aggregate": (c_i32, [vp, vp, vp, c_u32, c_u32, c_i64, c_u32, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32),
-                                ctypes.POINTER(c_u32), ctypes.POINTER(c_i64), vp, vp, vp, ctypes.POINTER(vp), vp]),
+                                ctypes.POINTER(c_u32), ctypes.POINTER(c_i64), vp, vp, vp, ctypes.POINTER(vp), c_i32, vp]),
 })
 
 TABLE_BITS = 12
@@ -166,8 +166,12 @@ def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
     bts = (c_u32 * 3)(*([vbits[a[1]] for a in accs] + [0] * (3 - na)))
     vms = (c_i64 * 3)(*([vmin[a[1]] for a in accs] + [0] * (3 - na)))
     optr = (vp * 3)(*([t.data_ptr() for t in oacc] + [0] * (3 - na)))
+    # a Sum of a field of <= 32 bits carries the count in its slot's top 16 bits (needs runs of
+    # fewer than 2^16 rows, so no slot's count can reach that field)
+    ps = next((j for j, a in enumerate(accs) if a[0] == 0 and vbits[a[1]] <= 32), None)
+    pack = 0 if ps is None or int(runs.max().item()) >= (1 << 16) else ps + 1
     _lib.call("dr_dg_aggregate", ptr(rows), ptr(rstart), ptr(wrun), c_u32(G), c_u32(kbits), c_i64(kmin), c_u32(na),
-              ops, offs, bts, vms, ptr(head), ptr(okey), ptr(ocnt), optr, st)
+              ops, offs, bts, vms, ptr(head), ptr(okey), ptr(ocnt), optr, pack, st)
     del rows
     g = int(head.item())
     keys, cnt = okey[:g], ocnt[:g]

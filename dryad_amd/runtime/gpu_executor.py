@@ -153,6 +153,7 @@ class GpuJobRunner:
                 self.g.set_gang(self.vids[s.id])
                 self.gang_stages.add(s.id)
         self.recovery: list = []         # recovery actions taken (tests / statistics)
+        self.precomputed_bodies: dict = {}   # fused join stage id -> (attempt body, program after it)
 
     def owner(self, p: int) -> int:
         return p % self.world.size
@@ -813,6 +814,9 @@ class GpuJobRunner:
                             [], "grace join stage"
                 if out is not None:
                     precomputed[jid] = (out, rest)
+                    body = (lambda d=self.fused_joins[jid]: FJ.run(d, self, FJ.vote(d, self))) \
+                        if how == "fused grace join" else (lambda d=desc, ly=lay: GS.run(d, self, ly))
+                    self.precomputed_bodies[jid] = (body, rest)
                     self.skipped.update((self.fused_joins.get(jid) or self.grace_joins[jid])["stages"])
                     self.timings[f"{jid}:Join({how})"] = time.time() - t0
             if s.id in precomputed:
@@ -983,6 +987,25 @@ class GpuJobRunner:
         its inputs delivered again (and rebuilt from lineage where they were released)."""
         st, p = self.plan.stages[self.stage_of[vid]], self.part_of[vid]
         me = self.world.rank
+        if st.id in self.precomputed_bodies:
+            # a fused stage's partitions come from one computation (its own key routing), so one
+            # of them is rebuilt by running the whole fused stage again (every rank takes part)
+            body, rest = self.precomputed_bodies[st.id]
+            refresh()
+            ver = ready.pop(vid)
+            self.g.on_running(vid, ver, self.owner(p), now())
+            outs = self._attempt_stage(st, body, first_version=ver)
+            if outs is None:
+                raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed,
+                                            f"re-execution of the fused stage {st.name} was declined")
+            for q, v in outs.items():
+                vctx = self._vertex_ctx(st, q, ver)
+                for op in rest:
+                    v = self._run_op(op, [v], vctx, st)
+                self.channels[(st.id, q)] = v
+            self.g.on_completed(vid, ver, now(), 0, 0)
+            self.recovery.append(("rerun_fused", st.name, p))
+            return
         raw = self._gather_inputs(st, only=[p], recover=True)
         refresh()
         ver = ready.pop(vid)
@@ -1023,7 +1046,7 @@ class GpuJobRunner:
             return None
         return self._attempt_stage(self.plan.stages[desc["join"]], lambda: FJ.run(desc, self, lay))
 
-    def _attempt_stage(self, st, body):
+    def _attempt_stage(self, st, body, first_version: int = 0):
         """Versioned, voted attempts of a precomputed (fused) join stage, whose vertices the main
         loop completes later.  Attempts are voted like a gang stage's (``_run_gang``): injected
         faults on the stage's partitions are agreed before the body (fail, read_error) or after it
@@ -1036,7 +1059,7 @@ class GpuJobRunner:
         mine = [p for p in range(st.partitions) if self.owner(p) == me]
         limit = int(getattr(self.ctx, "MaxVertexFailures", 6) or 6)
         outcome = None
-        for version in range(limit):
+        for version in range(first_version, first_version + limit):
             faults = {p: self._fault(st, p, version) for p in mine}
             pre = next(((p, k) for p, k in faults.items() if k in ("fail", "read_error")), None)
             outcome = self._vote(None if pre is None else (pre[0], pre[1], f"injected {pre[1]} of {st.name}[{pre[0]}]"))

@@ -37,3 +37,27 @@ def test_partfile_roundtrip_on_gpu_executor(tmp_path):
     # the files are ordinary DryadLinqBinary partfiles: the CPU executor reads them too
     c = D.DryadLinqContext(2)
     assert sorted(c.FromStore(uri)) == sorted((a * 2, b + 1.0) for a, b in data)
+
+
+@pytest.mark.parametrize("n,start,wide", [(1, 0, False), (255, 3, False), (70_001, 5, False), (3000, 1, True)])
+def test_tiled_codec_any_alignment_and_width(n, start, wide):
+    """LDS-tiled decode / encode (records of <= 128 bytes; wider ones take the per-field kernel)
+    of a part starting at any byte offset, against the host codec."""
+    import numpy as np
+    from dryad_amd.io import binary as B
+    from dryad_amd.ops import codec as CD
+    fields = [("a", T.Int16), ("b", T.Int64), ("c", T.Byte), ("d", T.Float64), ("e", T.Int32)]
+    if wide:
+        fields += [(f"w{i}", T.Int64) for i in range(16)]
+    dt = T.RecordT(fields, tuple)
+    rng = np.random.default_rng(n)
+    recs = [tuple(int(rng.integers(-3000, 3000)) if ft in (T.Int16, T.Int32, T.Int64) else
+                  int(rng.integers(0, 256)) if ft is T.Byte else float(rng.standard_normal())
+                  for _, ft in fields) for _ in range(n)]
+    host = B.encode_records(dt, recs)
+    buf = torch.zeros(len(host) + start + 16, dtype=torch.uint8, device="cuda")
+    buf[start:start + len(host)] = torch.frombuffer(bytearray(host), dtype=torch.uint8).cuda()
+    t = CD.decode(buf[start:start + len(host)], dt)
+    assert t.to_objects() == recs
+    enc = CD.encode(t, dt)
+    assert enc.cpu().numpy().tobytes() == host
