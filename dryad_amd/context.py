@@ -87,6 +87,8 @@ _DEFAULTS = dict(
     ThreadsPerWorker=None,
     JobRuntimeLimit=None,
     EnableSpeculativeDuplication=True,
+    OutlierThresholdSeconds=None,      # a vertex running past it gets a duplicate (None: the stage's
+    #                                    non-parametric estimate, >= 10 s; DrStageStatistics.cpp:93-111)
     LocalDebug=False,
     DebugBreak=False,
     RuntimeLoggingLevel=QueryLoggingLevel.Error,

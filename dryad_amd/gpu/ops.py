@@ -515,12 +515,14 @@ def hash_partition_perm(table: DeviceTable, key_fn, n: int):
     return _perm(e), st.tolist()
 
 
-def _port_order(n: int, world_size: int):
+def _port_order(n: int, world_size: int, place=None):
     """Bucket order of a partition vertex's ports: rank-major for a multi-rank job (port p lives
-    on rank p % W), so each destination rank's rows are one contiguous slice -> (order, LUT)."""
+    on rank ``place[p]``, p % W without a placement), so each destination rank's rows are one
+    contiguous slice -> (order, LUT)."""
     if world_size <= 1 or n <= 1:
         return None, None
-    order = sorted(range(n), key=lambda p: (p % world_size, p))
+    rank = (lambda p: place[p]) if place is not None and len(place) >= n else (lambda p: p % world_size)
+    order = sorted(range(n), key=lambda p: (rank(p), p))
     if order == list(range(n)):
         return None, None
     lut = [0] * 256
@@ -529,7 +531,12 @@ def _port_order(n: int, world_size: int):
     return order, lut
 
 
-def partition_by_entries(t: DeviceTable, e: torch.Tensor, n: int, world_size: int = 1):
+def _dest_place(v):
+    r = getattr(v, "runner", None)
+    return getattr(r, "place", None)
+
+
+def partition_by_entries(t: DeviceTable, e: torch.Tensor, n: int, world_size: int = 1, place=None):
     """Port-grouped copy of ``t``: row i goes to port ``e[i, 1]`` (< n <= 256), stable within a
     port, every column moved in one pass (ops/channel.scatter_columns, csrc/kernels/channel.hip).
     None when the table's columns do not fit that kernel."""
@@ -539,7 +546,7 @@ def partition_by_entries(t: DeviceTable, e: torch.Tensor, n: int, world_size: in
     cols = [t.rows] if t.rows is not None else list(t.cols.values())
     if not cols or not CH.kernel_ok(cols):
         return None
-    order, lut = _port_order(n, world_size)
+    order, lut = _port_order(n, world_size, place)
     lut_t = torch.tensor(lut, dtype=torch.uint8, device=t.device) if lut is not None else None
     outs, cnt = CH.scatter_columns(e, t.n, cols, lut_t)
     offs = [0]
@@ -562,7 +569,7 @@ def op_hash_partition(op, inputs, v):
     if n <= 256 and t.n < (1 << 32):
         keys, tup = hash_keys(t, op["key"])
         e, _ = R.stable_hash_dest(keys, t.n, n, tup, t.device)
-        out = partition_by_entries(t, e, n, v.world.size)
+        out = partition_by_entries(t, e, n, v.world.size, _dest_place(v))
         if out is not None:
             return out
     perm, st = hash_partition_perm(t, op["key"], n)
@@ -638,7 +645,7 @@ def op_range_partition(op, inputs, v):
     if op.get("separators") is not None:
         seps = _separator_entries(t, op["key"], list(op["separators"]))
         S.range_dest(e, seps, lo_mask, descending=op.get("descending", False))
-        out = partition_by_entries(t, e, n, v.world.size)
+        out = partition_by_entries(t, e, n, v.world.size, _dest_place(v))
         if out is not None:
             return out
         part, starts = S.partition_pass(e, 64)
@@ -648,7 +655,7 @@ def op_range_partition(op, inputs, v):
     seps_t = _entries_table(seps_t)
     seps = torch.stack([seps_t.cols["lo"], seps_t.cols["hi"]], 1).contiguous()
     S.range_dest(e, seps, lo_mask, descending=op.get("descending", False))
-    out = partition_by_entries(t, e, n, v.world.size)
+    out = partition_by_entries(t, e, n, v.world.size, _dest_place(v))
     if out is not None:
         return out
     part, starts = S.partition_pass(e, 64)

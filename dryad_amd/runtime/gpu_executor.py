@@ -61,6 +61,10 @@ class VertexCrash(RuntimeError):
     """A vertex attempt died (its output is discarded and it is re-executed)."""
 
 
+class VertexCancelled(Exception):
+    """A losing speculative attempt stopped at an operator boundary (its duplicate won)."""
+
+
 class GpuVertexContext(V.VertexContext):
     def __init__(self, partition, partitions, vertex_id, version, stage, device, world, runner=None):
         super().__init__(partition, partitions, vertex_id, version, stage)
@@ -110,11 +114,31 @@ def _device_bytes(x) -> int:
     return 0
 
 
+def _read_sizes(uri, P):
+    """Bytes (or rows) of each of the P partitions of a store, known without reading it: the
+    partfile metadata's part sizes, or the generator's row ranges (None otherwise)."""
+    scheme = parse_uri(uri)[0]
+    try:
+        if scheme in ("partfile", "file"):
+            from ..io import partfile as PF
+            m = PF.read_meta(parse_uri(uri)[1])
+            return [e.size for e in m.parts] if m.count == P else None
+        if scheme == "gen":
+            from ..io.providers import GenProvider
+            b = [GenProvider().bounds(uri, p) for p in range(P)]
+            return [hi - lo for lo, hi in b]
+    except Exception:  # noqa: BLE001
+        return None
+    return None
+
+
 class GpuJobRunner:
     def __init__(self, ctx, plan, world: World, faults=None, pool=None):
         self.ctx, self.plan, self.world = ctx, plan, world
         self.pool = pool
         self.row_sets: dict = {}          # (stage, partition) -> pooled BufferSet holding its rows
+        self.moved: dict = {}             # (stage, partition) -> rank whose duplicate attempt won
+        self.place = None                 # partition -> rank (None: p % W)
         self.fused: dict = {}             # merge stage id -> fused distributed-OrderBy descriptor
         self.skipped: set = set()
         self.dev = world.device
@@ -130,12 +154,19 @@ class GpuJobRunner:
         R = native_runtime()
         p = R.Params()
         p.max_failures = int(getattr(ctx, "MaxVertexFailures", 6) or 6)
-        p.speculative = False            # collectives: no duplicates (a straggler holds the gang anyway)
+        # speculative duplicates (DrDefaultManager::CheckForDuplicates) only for leaf stages outside
+        # gangs: a duplicate re-reads the vertex's source on an idle rank (no collective inside)
+        p.speculative = bool(getattr(ctx, "EnableSpeculativeDuplication", True)) and world.size > 1
+        thr = ctx._props.get("OutlierThresholdSeconds")
+        if thr is not None:
+            p.default_outlier_threshold = float(thr)
+            p.min_outlier_threshold = min(p.min_outlier_threshold, float(thr))
         self.g = R.JobGraph(p)
+        self.g_speculative = p.speculative
         self.vids = []
         self.part_of, self.stage_of = {}, {}
         for s in plan.stages:
-            self.g.add_stage(f"{s.id}:{s.name}", s.partitions, False, s.is_output)
+            self.g.add_stage(f"{s.id}:{s.name}", s.partitions, p.speculative and self._duplicable(s, plan), s.is_output)
             self.vids.append([self.g.add_vertex(s.id, q) for q in range(s.partitions)])
             for q, v in enumerate(self.vids[-1]):
                 self.part_of[v], self.stage_of[v] = q, s.id
@@ -155,8 +186,53 @@ class GpuJobRunner:
         self.recovery: list = []         # recovery actions taken (tests / statistics)
         self.precomputed_bodies: dict = {}   # fused join stage id -> (attempt body, program after it)
 
-    def owner(self, p: int) -> int:
+    @staticmethod
+    def _duplicable(s, plan) -> bool:
+        """A stage whose vertices a duplicate can run anywhere: no input channels (it reads its
+        source itself, re-readable: the reference's inputs are immutable files too)."""
+        if s.inputs or not s.ops:
+            return False
+        o = s.ops[0]
+        return o["op"] == "enumerable" or (o["op"] == "read" and parse_uri(o["uri"])[0] in ("gen", "partfile", "file"))
+
+    def owner(self, p: int, sid: int | None = None) -> int:
+        """Rank of partition p (of stage ``sid``): a speculative duplicate that won moved that one
+        vertex's output (``moved``); otherwise the job's placement (``place``, by input size when
+        there are more partitions than ranks), else p % W."""
+        if sid is not None and self.moved and (sid, p) in self.moved:
+            return self.moved[(sid, p)]
+        if self.place is not None and p < len(self.place):
+            return self.place[p]
         return p % self.world.size
+
+    # ------------------------------------------------------------------ placement
+    def _placement(self):
+        """Partition -> rank when the job has more partitions than ranks.  The reference places each
+        vertex by its inputs' location and size (LocalScheduler.ScheduleProcessInternal,
+        LocalScheduler.cs:132-268; the GM passes input size hints, DrVertex.cpp:356-429); here the
+        partitions of the job's largest leaf read (sizes from the partfile metadata or the
+        generator's ranges, the same on every rank) go largest first to the least-loaded rank, and
+        every stage keeps that map, so pointwise channels stay local.  None (p % W) when the job
+        has no more partitions than ranks or the sizes are unknown / equal."""
+        W = self.world.size
+        P = max((st.partitions for st in self.plan.stages), default=1)
+        if W == 1 or P <= W:
+            return None
+        best = None
+        for st in self.plan.stages:
+            if st.inputs or st.partitions != P or not st.ops or st.ops[0]["op"] != "read":
+                continue
+            sizes = _read_sizes(st.ops[0]["uri"], P)
+            if sizes is not None and (best is None or sum(sizes) > sum(best)):
+                best = sizes
+        if best is None or len(set(best)) == 1:
+            return None
+        load, place = [0] * W, [0] * P
+        for p in sorted(range(P), key=lambda q: (-best[q], q)):
+            r = min(range(W), key=lambda k: (load[k], k))
+            place[p] = r
+            load[r] += best[p]
+        return place
 
     # ------------------------------------------------------------------ fused distributed OrderBy
     def _find_fused_orderby(self):
@@ -309,14 +385,14 @@ class GpuJobRunner:
         on one rank only leaves its peers in the exchange: the communicator's error handling then
         ends the job (parallel/comm.py), as a lost process would."""
         g, W, me = self.g, self.world.size, self.world.rank
-        mine = [p for p in range(s.partitions) if self.owner(p) == me]
+        mine = [p for p in range(s.partitions) if self.owner(p, s.id) == me]
         while True:
             refresh()
             vers = {}
             for p in range(s.partitions):
                 vid = self.vids[s.id][p]
                 vers[p] = ready.pop(vid)
-                g.on_running(vid, vers[p], self.owner(p), now())
+                g.on_running(vid, vers[p], self.owner(p, s.id), now())
             faults = {p: self._fault(s, p, vers[p]) for p in mine}
             pre = next(((p, k) for p, k in faults.items() if k in ("fail", "read_error")), None)
             for k in faults.values():
@@ -536,12 +612,14 @@ class GpuJobRunner:
         ``only``: just these partitions (re-execution).  Source channels released after an earlier
         delivery are rebuilt from lineage first (all ranks release in lockstep)."""
         W, me = self.world.size, self.world.rank
-        local = [p for p in range(s.partitions) if self.owner(p) == me and (only is None or p in only)]
+        local = [p for p in range(s.partitions) if self.owner(p, s.id) == me and (only is None or p in only)]
         inputs = {p: [[] for _ in s.inputs] for p in local}
         for ii, si in enumerate(s.inputs):
             src_stage = self.plan.stages[si.src]
+            so = lambda q, _s=si.src: self.owner(q, _s)  # noqa: E731  (source partition -> its rank)
+            do = lambda p, _s=s.id: self.owner(p, _s)    # noqa: E731
             if recover:      # (collective vote: a rank that owns no source partition still takes part)
-                mine = [q for q in range(src_stage.partitions) if self.owner(q) == me]
+                mine = [q for q in range(src_stage.partitions) if so(q) == me]
                 miss = [any((si.src, q) not in self.channels for q in mine)]
                 if W > 1:
                     miss = [None] * W
@@ -558,7 +636,7 @@ class GpuJobRunner:
             need_remote = False
             for p in dst_parts:
                 for q in self._sources(si, p):
-                    if self.owner(q) != self.owner(p):
+                    if so(q) != do(p):
                         need_remote = True
             if not need_remote:
                 for p in local:
@@ -568,25 +646,25 @@ class GpuJobRunner:
                     and s.ops and s.ops[0]["op"] == "agg_final":
                 # dynamic aggregation level 1 (DrDynamicAggregateManager machine grouping): each rank
                 # folds the partials of its own source partitions into one before the final vertex
-                mine = [q for q in range(src_stage.partitions) if self.owner(q) == me]
-                got = self._transport(s, si, [[self._combine_local(s, si, mine)] if self.owner(0) == r else []
+                mine = [q for q in range(src_stage.partitions) if so(q) == me]
+                got = self._transport(s, si, [[self._combine_local(s, si, mine)] if do(0) == r else []
                                               for r in range(W)],
-                                      [[("rank", r)] if self.owner(0) == me else [] for r in range(W)])
+                                      [[("rank", r)] if do(0) == me else [] for r in range(W)])
                 for p in local:
                     inputs[p][ii] = [x for r in range(W) for x in got[r].values()]
                 self.recovery.append(("dynamic_aggregate", s.name, len(mine)))
                 continue
             # merge / broadcast / remote pointwise edges: every rank sends each port value another
             # rank needs once (a q feeding several of its partitions travels once)
-            need = [sorted({q for p in dst_parts if self.owner(p) == r for q in self._sources(si, p)
-                            if self.owner(q) != r}) for r in range(W)]
+            need = [sorted({q for p in dst_parts if do(p) == r for q in self._sources(si, p)
+                            if so(q) != r}) for r in range(W)]
             mine = {q: self._port_of(si, self.channels[(si.src, q)], None) for r in range(W) for q in need[r]
-                    if self.owner(q) == me}
-            sends = [[mine[q] for q in need[r] if self.owner(q) == me] for r in range(W)]
-            got = self._transport(s, si, sends, [[q for q in need[me] if self.owner(q) == r] for r in range(W)])
+                    if so(q) == me}
+            sends = [[mine[q] for q in need[r] if so(q) == me] for r in range(W)]
+            got = self._transport(s, si, sends, [[q for q in need[me] if so(q) == r] for r in range(W)])
             recv = {q: x for r in range(W) for q, x in got[r].items()}
             for p in local:
-                inputs[p][ii] = [self._port_of(si, self.channels[(si.src, q)], p) if self.owner(q) == me
+                inputs[p][ii] = [self._port_of(si, self.channels[(si.src, q)], p) if so(q) == me
                                  else recv[q] for q in self._sources(si, p)]
         return inputs
 
@@ -645,19 +723,19 @@ class GpuJobRunner:
         and the pieces a partition receives arrive adjacent, so neither side copies."""
         W, me = self.world.size, self.world.rank
         P_src, P_dst = src_stage.partitions, dst_stage.partitions
-        local_src = [q for q in range(P_src) if self.owner(q) == me]
-        local_dst = [p for p in range(P_dst) if self.owner(p) == me]
+        local_src = [q for q in range(P_src) if self.owner(q, si.src) == me]
+        local_dst = [p for p in range(P_dst) if self.owner(p, dst_stage.id) == me]
         sends, ids = [], []
         for r in range(W):
             lst = []
             for q in local_src:
                 v = self.channels[(si.src, q)]
                 for p in range(P_dst):
-                    if self.owner(p) == r:
+                    if self.owner(p, dst_stage.id) == r:
                         lst.append(self._port_of(si, v, p))
             sends.append(lst)
         for r in range(W):
-            ids.append([(q, p) for q in range(P_src) if self.owner(q) == r for p in local_dst])
+            ids.append([(q, p) for q in range(P_src) if self.owner(q, si.src) == r for p in local_dst])
         got = self._transport(dst_stage, si, sends, ids)
         out = {p: [None] * P_src for p in local_dst}
         for r in range(W):
@@ -698,12 +776,16 @@ class GpuJobRunner:
         objs = [x if isinstance(x, list) else _to_objects(x) for x in streams]
         return [y for o in objs for y in o]
 
-    def run_vertex(self, s, p, version, raw_inputs, inject=True):
+    def run_vertex(self, s, p, version, raw_inputs, inject=True, cancel=None):
         fault = self._fault(s, p, version) if inject else None
         if fault == "fail":
             raise RuntimeError(f"injected vertex failure {s.name}[{p}] v{version}")
         if fault and fault.startswith("slow"):
-            time.sleep(float(fault.split(":")[1]) if ":" in fault else 1.0)
+            t = float(fault.split(":")[1]) if ":" in fault else 1.0
+            if cancel is not None:
+                cancel.wait(t)
+            else:
+                time.sleep(t)
         if fault == "read_error" and s.inputs:
             q = next(iter(self._sources(s.inputs[0], p)), None)
             if q is not None:
@@ -714,6 +796,8 @@ class GpuJobRunner:
         data = None
         with TRC.range(f"vertex {s.id}:{s.name}[{p}] v{version}"):
             for i, op in enumerate(s.ops):
+                if cancel is not None and cancel.is_set():
+                    raise VertexCancelled(f"{s.name}[{p}] v{version}")
                 args = inputs if i == 0 else [data]
                 with TRC.range(op["op"]):
                     data = self._run_op(op, args, vctx, s)
@@ -780,6 +864,7 @@ class GpuJobRunner:
             for it in g.take_ready(1 << 30, now()):
                 ready[it.vertex] = it.version
 
+        self.place = self._placement()
         self.fused = self._find_fused_orderby()
         self.external = self._plan_external()
         for sid, e in self.external.items():
@@ -830,7 +915,7 @@ class GpuJobRunner:
                 for p in range(s.partitions):
                     vid = self.vids[s.id][p]
                     ver = ready.pop(vid)
-                    g.on_running(vid, ver, self.owner(p), now())
+                    g.on_running(vid, ver, self.owner(p, s.id), now())
                     g.on_completed(vid, ver, now(), 0, 0)
                 self._release(s)
                 continue
@@ -846,7 +931,7 @@ class GpuJobRunner:
                 for p in range(s.partitions):
                     vid = self.vids[s.id][p]
                     ver = ready.pop(vid)
-                    g.on_running(vid, ver, self.owner(p), now())
+                    g.on_running(vid, ver, self.owner(p, s.id), now())
                     g.on_completed(vid, ver, now(), 0, 0)
                 self.timings[f"{s.id}:{s.name}(fused)"] = 0.0
                 continue
@@ -867,7 +952,10 @@ class GpuJobRunner:
                     torch.cuda.synchronize(self.dev)
                 self.timings[f"{s.id}:{s.name}(fused OrderBy)"] = time.time() - t0
                 continue
-            self._run_stage(s, ready, refresh, now)
+            if self.world.size > 1 and self._speculate(s):
+                self._run_stage_speculative(s, ready, refresh, now)
+            else:
+                self._run_stage(s, ready, refresh, now)
             self._release(s)
             if self.gpu_ok:
                 torch.cuda.synchronize(self.dev)
@@ -878,6 +966,7 @@ class GpuJobRunner:
                 self.pool.release(b)
         return dict(committed=committed, fallbacks=self.fallbacks, timings=self.timings, transports=self.transports,
                     op_counts={f"{k[0]}:{k[1]}": v for k, v in self.op_counts.items()},
+                    placement=self.place, moved={f"{k[0]}:{k[1]}": v for k, v in self.moved.items()},
                     write=dict(bytes=self.write_stats.bytes, seconds=round(self.write_stats.seconds, 4)),
                     statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()],
                     external_sort=getattr(self, "extsort_stats", None), join=getattr(self, "join_stats", None),
@@ -898,7 +987,7 @@ class GpuJobRunner:
             lineage), then the channel is delivered again.
         """
         g, W, me = self.g, self.world.size, self.world.rank
-        local = [p for p in range(s.partitions) if self.owner(p) == me]
+        local = [p for p in range(s.partitions) if self.owner(p, s.id) == me]
         raw, need_gather = None, True
         while True:
             if need_gather:
@@ -963,6 +1052,147 @@ class GpuJobRunner:
             if all(g.completed_version(v) >= 0 for v in self.vids[s.id]):
                 return
 
+    def _speculate(self, s) -> bool:
+        return self.g_speculative and s.id not in self.gang_stages and s.id not in self.skipped and \
+            self._duplicable(s, self.plan)
+
+    def _run_stage_speculative(self, s, ready, refresh, now):
+        """A leaf stage with speculative duplication (DrManagerBase::CheckForDuplicates,
+        DrDefaultManager.cpp:664-714; outlier threshold DrStageStatistics.cpp:93-111).  Each rank runs
+        its vertices on a worker thread; every SPEC_POLL seconds the ranks all-gather what started
+        and finished and replay it on their JobGraphs in rank order (identical decisions everywhere,
+        the latest rank clock as the common time).  A vertex running past the stage's outlier
+        threshold gets a duplicate version on an idle rank (it re-reads its source); the first
+        completion wins, its output stays on the winner's rank (``moved``) and later stages fetch
+        it from there.  The losing attempt is cancelled at its next operator boundary (the
+        reference kills the losing process), so every rank's worker drains before the stage ends
+        and nothing runs on the device behind the next stage's collectives."""
+        g, W, me = self.g, self.world.size, self.world.rank
+        jobs, done = queue.Queue(), queue.Queue()
+        dev = self.dev
+        cancels = {}                                       # (p, version) -> Event of my live attempts
+
+        def worker():
+            if dev.type == "cuda":
+                torch.cuda.set_device(dev)
+            while True:
+                item = jobs.get()
+                if item is None:
+                    return
+                p, ver, dup = item
+                try:
+                    out = self.run_vertex(s, p, ver, [[] for _ in s.inputs], cancel=cancels[(p, ver)])
+                    if dev.type == "cuda":
+                        torch.cuda.synchronize(dev)
+                    done.put((p, ver, dup, "ok", out, ""))
+                except VertexCancelled:
+                    done.put((p, ver, dup, "cancelled", None, ""))
+                except Exception as e:  # noqa: BLE001
+                    done.put((p, ver, dup, "fail", None, f"{type(e).__name__}: {e}"))
+
+        th = threading.Thread(target=worker, daemon=True, name=f"dryad-vertex-{s.id}")
+        th.start()
+        pending, started, outs = 0, [], {}
+
+        def launch(p, ver, dup):
+            nonlocal pending
+            cancels[(p, ver)] = threading.Event()
+            jobs.put((p, ver, dup))
+            started.append((self.vids[s.id][p], ver, dup))
+            pending += 1
+
+        def take_ready():
+            refresh()
+            for p in range(s.partitions):
+                vid = self.vids[s.id][p]
+                if vid in ready:
+                    ver = ready.pop(vid)
+                    if g.completed_version(vid) < 0 and self.owner(p, s.id) == me:
+                        launch(p, ver, False)
+        try:
+            take_ready()
+            while True:
+                finished, got = [], []
+                try:                                           # wake at a local completion or a poll tick
+                    got.append(done.get(timeout=self.SPEC_POLL))
+                except queue.Empty:
+                    pass
+                while not done.empty():
+                    got.append(done.get())
+                for p, ver, dup, kind, out, err in got:
+                    pending -= 1
+                    cancels.pop((p, ver), None)
+                    finished.append((self.vids[s.id][p], ver, dup, kind, err))
+                    if kind == "ok":
+                        outs[(p, ver)] = out
+                rep = dict(t=now(), started=started, finished=finished, idle=pending == 0)
+                started = []
+                reps = [rep]
+                if W > 1:
+                    reps = [None] * W
+                    dist.all_gather_object(reps, rep)
+                T = max(r["t"] for r in reps)
+                for r, x in enumerate(reps):
+                    for vid, ver, dup in x["started"]:
+                        g.on_running(vid, ver, r, T)
+                for r, x in enumerate(reps):
+                    for vid, ver, dup, kind, err in x["finished"]:
+                        p = self.part_of[vid]
+                        if kind == "cancelled":
+                            g.on_cancelled(vid, ver, T)
+                        elif kind == "ok":
+                            accepted, losers = g.on_completed(vid, ver, T, 0, 0)
+                            if r == me:
+                                out = outs.pop((p, ver))
+                                if accepted:
+                                    self.channels[(s.id, p)] = out if out is not None else []
+                            if accepted:
+                                if r != self.owner(p, s.id):
+                                    self.moved[(s.id, p)] = r
+                                if dup:
+                                    self.recovery.append(("duplicate_won", s.name, p, r))
+                                for lv, lver in losers:        # stop the losing attempt where it runs
+                                    ev = cancels.get((self.part_of[lv], lver))
+                                    if ev is not None:
+                                        ev.set()
+                        else:
+                            g.on_failed(vid, ver, T, -1, err)
+                            if g.completed_version(vid) < 0:
+                                self.recovery.append(("retry", s.name, p))
+                            log.warning("vertex %s[%d] v%d failed: %s", s.name, p, ver, err)
+                if g.failed():
+                    raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed, g.failure())
+                if all(g.completed_version(v) >= 0 for v in self.vids[s.id]) and \
+                        not any(x["started"] for x in reps) and all(x["idle"] for x in reps):
+                    return
+                take_ready()                                   # retries of failed attempts
+                idle = [r for r, x in enumerate(reps) if x["idle"]]
+                if not idle:
+                    continue
+                dups = g.check_duplicates(T)
+                refresh()                                      # the duplicates are placed here, not by owner
+                for it in dups:
+                    if ready.get(it.vertex) == it.version:
+                        ready.pop(it.vertex)
+                    p = self.part_of[it.vertex]
+                    cand = [r for r in idle if r != self.owner(p, s.id)]
+                    if not cand:
+                        g.on_cancelled(it.vertex, it.version, T)
+                        continue
+                    r = cand[0]
+                    idle.remove(r)
+                    self.recovery.append(("duplicate", s.name, p, r))
+                    log.info("duplicate of %s[%d] v%d on rank %d", s.name, p, it.version, r)
+                    if r == me:
+                        launch(p, it.version, True)
+        finally:
+            for ev in cancels.values():
+                ev.set()
+            jobs.put(None)
+            th.join()
+
+    SPEC_POLL = 0.02
+
     def _dump_restart(self, s, p, ver, streams, error):
         """Restart record of a failed GPU vertex attempt (DumpRestartCommand, dvertexpncontrol.cpp:
         348-736): its delivered inputs persisted under ``log/rerun/vertex-V.v/`` (device tables as
@@ -993,7 +1223,7 @@ class GpuJobRunner:
             body, rest = self.precomputed_bodies[st.id]
             refresh()
             ver = ready.pop(vid)
-            self.g.on_running(vid, ver, self.owner(p), now())
+            self.g.on_running(vid, ver, self.owner(p, st.id), now())
             outs = self._attempt_stage(st, body, first_version=ver)
             if outs is None:
                 raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed,
@@ -1009,9 +1239,9 @@ class GpuJobRunner:
         raw = self._gather_inputs(st, only=[p], recover=True)
         refresh()
         ver = ready.pop(vid)
-        self.g.on_running(vid, ver, self.owner(p), now())
+        self.g.on_running(vid, ver, self.owner(p, st.id), now())
         ok, err = True, ""
-        if self.owner(p) == me:
+        if self.owner(p, st.id) == me:
             try:
                 out = self.run_vertex(st, p, ver, raw[p])
                 self.channels[(st.id, p)] = out if out is not None else []
@@ -1056,7 +1286,7 @@ class GpuJobRunner:
         the compiled stages run instead.  One raised on some ranks only leaves the others in a
         collective; the communicator's error handling then ends the job (parallel/comm.py)."""
         me = self.world.rank
-        mine = [p for p in range(st.partitions) if self.owner(p) == me]
+        mine = [p for p in range(st.partitions) if self.owner(p, st.id) == me]
         limit = int(getattr(self.ctx, "MaxVertexFailures", 6) or 6)
         outcome = None
         for version in range(first_version, first_version + limit):
@@ -1107,14 +1337,14 @@ class GpuJobRunner:
                 continue
             uri = s.output["uri"]
             scheme, path, _ = parse_uri(uri)
-            local = {p: self.channels[(s.id, p)] for p in range(s.partitions) if self.owner(p) == me}
+            local = {p: self.channels[(s.id, p)] for p in range(s.partitions) if self.owner(p, s.id) == me}
             if scheme == "hbm":
                 tabs = {p: (v if isinstance(v, DeviceTable) else v) for p, v in local.items()}
                 pins = [self.row_sets[(s.id, p)] for p in local if (s.id, p) in self.row_sets]
                 for b in pins:
                     self.pool.pin(b)
                 provider_for(uri).put(uri, {"dtype": s.dtype, "partitions": s.partitions, "local": tabs,
-                                            "owner_of": {p: self.owner(p) for p in range(s.partitions)},
+                                            "owner_of": {p: self.owner(p, s.id) for p in range(s.partitions)},
                                             "bytes": sum(_object_bytes(v) for v in tabs.values()),
                                             "pins": pins, "pool": self.pool})
                 committed[uri] = s.partitions
@@ -1128,7 +1358,7 @@ class GpuJobRunner:
                     else:
                         tabs[p] = _to_objects(v) if not isinstance(v, list) else v
                 provider_for(uri).put(uri, {"dtype": s.dtype, "partitions": s.partitions, "local": tabs,
-                                            "owner_of": {p: self.owner(p) for p in range(s.partitions)}})
+                                            "owner_of": {p: self.owner(p, s.id) for p in range(s.partitions)}})
                 committed[uri] = s.partitions
             elif scheme in ("partfile", "file") and self._commit_partfile(s, uri, path, local):
                 committed[uri] = s.partitions

@@ -48,6 +48,8 @@ def main():
                 print(f"[faults] {kind} {name}: {'ok' if ok else 'MISMATCH'} recovery={sorted(kinds)}", flush=True)
             if not ok:
                 bad.append((kind, name, sorted(kinds)))
+    if W > 1:
+        bad += straggler(w, loc)
     if w.device.type == "cuda":
         bad += fused_stage_faults(w, loc)
     import torch.distributed as dist
@@ -59,6 +61,35 @@ def main():
         flat = [x for b in allbad for x in b]
         assert not flat, flat
         print("FAULTS_OK", W, flush=True)
+
+
+def straggler(w, loc):
+    """A leaf-stage vertex stalls (slow:4 at version 0): past the outlier threshold a duplicate runs
+    on an idle rank, wins, and later stages read its output from there (the reference's
+    CheckForDuplicates).  The job must finish well before the straggler would have."""
+    import time
+    bad = []
+    for name, q in queries().items():
+        g = D.DryadLinqContext(platform="gpu")
+        g.PartitionCount = 2 * w.size
+        g.OutlierThresholdSeconds = 0.3
+        g.FaultInjection = [dict(stage=0, partition=1, version=0, kind="slow:4")]   # the leaf stage
+        t = time.time()
+        got = q(g)
+        got = got if isinstance(got, list) else list(got)
+        dt = time.time() - t
+        exp = q(loc)
+        exp = exp if isinstance(exp, list) else list(exp)
+        res = g._get_executor().last_result
+        kinds = {r[0] for r in res.get("recovery") or []}
+        ok = sorted(got, key=repr) == sorted(exp, key=repr) and "duplicate_won" in kinds and dt < 3.5 \
+            and res.get("moved")
+        if w.rank == 0:
+            print(f"[faults] straggler {name}: {'ok' if ok else 'MISMATCH'} {dt:.2f}s recovery={sorted(kinds)} "
+                  f"moved={res.get('moved')}", flush=True)
+        if not ok:
+            bad.append(("straggler", name, sorted(kinds), round(dt, 2)))
+    return bad
 
 
 def fused_stage_faults(w, loc):

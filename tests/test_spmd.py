@@ -117,3 +117,17 @@ def test_numa_pci_address_format():
     from dryad_amd.parallel import affinity as A
     assert A.pci_address(SimpleNamespace(pci_bus_id=0xc1, pci_device_id=0, pci_domain_id=0)) == "0000:c1:00.0"
     assert A.pci_address(SimpleNamespace(pci_bus_id="0000:05:00.0")) == "0000:05:00.0"
+
+
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_size_aware_placement_gloo(ranks, tmp_path):
+    """More partitions than ranks over a skewed partfile: partitions are placed by part size
+    (largest first on the least-loaded rank) and the results still equal the oracle."""
+    env = dict(os.environ, SPMD_DEVICE="cpu", DRYAD_DIST_BACKEND="gloo", PYTHONPATH=ROOT,
+               PLACEMENT_DIR=str(tmp_path))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tests", "dist", "placement_ranks.py")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert f"PLACEMENT_OK {ranks}" in r.stdout
