@@ -69,6 +69,10 @@ def main():
                     help="run the per-rank program of a W-rank job on this one GPU, the all-to-all-v replaced by "
                          "generating the exact bytes this rank would receive (not timed); reports per-rank ms")
     ap.add_argument("--loopback-rank", type=int, default=0, help="which rank of the --loopback-ranks job to run")
+    ap.add_argument("--input", default=None,
+                    help="stored-data TeraSort: read this partfile:// table of raw 100-byte rows (written from the "
+                         "generator first, untimed, if absent) and write the sorted table to --output")
+    ap.add_argument("--output", default=None, help="with --input: the output partfile:// table")
     args = ap.parse_args()
     env = check_env(args.rehearsal)
     if args.loopback_ranks:
@@ -76,8 +80,8 @@ def main():
 
     import torch
     from dryad_amd.parallel.comm import init_world, shutdown
-    from dryad_amd.models.terasort import (TeraSortConfig, TeraSortJob, TeraSortOOCJob, TeraSortQueryJob, RECORD,
-                                           run_steps)
+    from dryad_amd.models.terasort import (TeraSortConfig, TeraSortJob, TeraSortOOCJob, TeraSortQueryJob,
+                                           TeraSortStoredJob, RECORD, run_steps)
 
     world = init_world(device="cuda")
     if world.size != args.gpus:
@@ -88,7 +92,16 @@ def main():
     ooc = records * RECORD > IN_HBM_MAX_BYTES
     cfg = TeraSortConfig(records_per_rank=records)
     t_alloc = time.perf_counter()
-    if ooc:
+    stored = args.input is not None
+    if stored:
+        if ooc or not args.input.startswith("partfile://"):
+            print("[bench] --input takes a partfile:// table that fits the in-HBM sort", file=sys.stderr)
+            sys.exit(2)
+        job = TeraSortStoredJob(cfg, world, args.input, args.output or args.input.rstrip("/") + "_sorted")
+        prep = job.prepare()
+        if world.rank == 0:
+            print(f"[bench] input table: {prep}", file=sys.stderr, flush=True)
+    elif ooc:
         budget = None if args.hbm_budget_gb is None else int(args.hbm_budget_gb * 1e9)
         job = TeraSortOOCJob(cfg, world, budget=budget)
     else:
@@ -154,10 +167,17 @@ def main():
         }
         if val is not None and not val["ok"]:
             line["validation"] = val
-        if ooc:
+        if stored:
+            line["metric"] = METRIC + " [stored-data variant: partfile in -> sort -> partfile out]"
+            line["vs_baseline"] = round(gbps / BASELINE_GBPS, 3)
+            line["config"]["path"] = "DryadLINQ query -> GPU executor: partfile read -> in-HBM sort -> partfile write"
+            line["config"]["input"] = f"{args.input} (raw 100-byte rows, read in the timed step)"
+            line["config"]["output"] = job.dst
+            line["config"]["stored"] = job.report()
+        elif ooc:
             line["config"]["out_of_core"] = job.report()
             line["config"]["input"] = "gen://terasort, generated chunk by chunk in the timed step (count + partition passes)"
-        elif not args.direct:
+        elif not args.direct and not stored:
             rep = job.executor_report()
             print(f"[bench] executor: {json.dumps(rep, default=str)[:2000]}", file=sys.stderr, flush=True)
         print(json.dumps(line), flush=True)

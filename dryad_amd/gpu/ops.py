@@ -287,10 +287,27 @@ def op_read(op, inputs, v):
         if rp is not None:
             # raw fixed-width rows (e.g. an out-of-core sort's output): chunked reader -> pooled HBM
             mm, ko, kl = rp
+            stats = getattr(v.runner, "read_stats", None)
+            spec = getattr(v.runner, "pitch_gen_stages", {}).get(v.stage.id) if v.world.size == 1 else None
+            if spec is not None and mm.shape[1] == 100 and 0 < mm.shape[0] < (1 << 32):
+                # only the one-rank OrderBy reads these 100-byte rows: stored at a 128-byte pitch
+                # (one aligned HBM line per record) and the sort's compact entries + window
+                # histograms extracted from them right after the read, as the generator does
+                rows = v.alloc_rows(mm.shape[0], 100, layout="pitch128")
+                if rows is not None:
+                    n = mm.shape[0]
+                    t = DeviceTable(n, Shape("rows", key_off=ko, key_len=kl), rows=rows)
+                    RD.read_rows_to_device(mm.filename, v.device, int(mm.offset), n, 100, rows, stats=stats)
+                    bs = _pooled_set(t, v)
+                    if bs is not None and spec[0] == 0:
+                        _, part = S.extract_keys64_tile(bs.bufs.rows_in[:n], 0, spec[1], 0, bs.bufs.ent_a, hist=True)
+                        S.note_gen_hist(bs.bufs.ent_a[:n], n, part)
+                        bs.keys_ready = (rows.data_ptr(), n, 0, spec[1], None, "e64")
+                    return t
             rows = v.alloc_rows(mm.shape[0], mm.shape[1])
             if mm.shape[0]:
                 RD.read_to_device(mm.filename, v.device, offset=int(mm.offset), length=rows.numel(),
-                                  out=rows.view(-1))
+                                  out=rows.view(-1), stats=stats)
             return DeviceTable(mm.shape[0], Shape("rows", key_off=ko, key_len=kl), rows=rows)
         # binary part: bytes -> HBM by the chunked pinned reader -> columns with the device codec
         # (fixed-width records: one thread per field; strings: parallel over the part's record

@@ -97,3 +97,72 @@ def read_to_device(path: str, device, offset: int = 0, length: int = -1, out: to
         stats.bytes += length
         stats.seconds += time.perf_counter() - t0
     return out[:length]
+
+
+def read_rows_to_device(path: str, device, offset: int, n: int, stride: int, out: torch.Tensor,
+                        stats: ReadStats | None = None) -> torch.Tensor:
+    """``n`` fixed-width rows of ``stride`` bytes at ``offset`` of ``path`` into ``out``, an
+    [n, stride] uint8 device view whose rows may sit at a wider pitch (e.g. the 128-byte-pitch
+    sort input, ops/sort.sort_rows_pitch128).  A contiguous ``out`` is one read_to_device; a
+    pitched one goes chunk by chunk (whole rows per chunk) through a device staging buffer and
+    one strided copy per chunk, on the copy stream, behind the chunk's DMA."""
+    import time
+    from ..native import runtime
+    from ..ops import _lib
+    if out.shape[0] < n or out.shape[1] != stride:
+        raise ValueError("read_rows_to_device: output view too small")
+    if n == 0:
+        return out[:0]
+    if out[:n].is_contiguous():
+        read_to_device(path, device, offset=offset, length=n * stride, out=out[:n].view(-1), stats=stats)
+        return out[:n]
+    t0 = time.perf_counter()
+    dev = torch.device(device)
+    cb = (CHUNK // stride) * stride
+    length = n * stride
+    if os.path.getsize(path) < offset + length:
+        raise ValueError(f"read_rows_to_device: {path} holds fewer than {n} rows of {stride} bytes")
+    stage = torch.empty(cb, dtype=torch.uint8, device=dev)
+    ring = _ring()
+    with _RING_LOCK:
+        rd = runtime().ChunkReader(path, int(offset), int(length), cb, [b.tensor.data_ptr() for b in ring], THREADS)
+        cur = torch.cuda.current_stream(dev)
+        cs = torch.cuda.Stream(dev)
+        cs.wait_stream(cur)
+        pending = deque()
+        try:
+            with torch.cuda.stream(cs):
+                while True:
+                    while pending and pending[0][1].query():
+                        rd.release(pending.popleft()[0])
+                    if len(pending) == len(ring):
+                        s0, e0 = pending.popleft()
+                        e0.synchronize()
+                        rd.release(s0)
+                    got = rd.next(-1)
+                    if got is None:
+                        break
+                    slot, chunk, nb = got
+                    r0, nr = chunk * (cb // stride), nb // stride
+                    _lib.memcpy_async(stage[:nb], ring[slot].tensor[:nb], cs)
+                    ev = torch.cuda.Event()
+                    ev.record(cs)
+                    pending.append((slot, ev))
+                    out[r0:r0 + nr].copy_(stage[:nb].view(nr, stride))   # same stream: after the DMA,
+                    if stats is not None:                                   # before the next one
+                        stats.chunks += 1
+            for s_, e_ in pending:
+                e_.synchronize()
+                rd.release(s_)
+            pending.clear()
+        finally:
+            for s_, e_ in pending:
+                e_.synchronize()
+            rd.stop()
+        cur.wait_stream(cs)
+        stage.record_stream(cur)
+    if stats is not None:
+        stats.bytes += length
+        stats.seconds += time.perf_counter() - t0
+    return out[:n]
+

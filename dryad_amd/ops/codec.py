@@ -13,6 +13,9 @@ import torch
 from .. import types as T
 from . import _lib
 from ._lib import c_i32, c_u32, c_u64, ptr, stream_of, vp
+from ..utils.log import get_logger
+
+log = get_logger("codec")
 
 _lib.register_signatures({"dr_codec_fixed": (c_i32, [vp, c_u64, c_u32, c_i32, vp, vp, vp, c_i32, vp])})
 
@@ -82,6 +85,9 @@ def encode(table, dtype) -> torch.Tensor | None:
 # ------------------------------------------------------------------------------------------------
 # Variable-length records: strings (+ fixed-width primitives), csrc/kernels/codec.hip.
 _lib.register_signatures({
+    "dr_varscan_chains": (c_i32, [vp, c_u64, c_u32, c_i32, ctypes.POINTER(c_u32), vp, vp, vp, c_u32, vp]),
+    "dr_varscan_fix": (c_i32, [vp, c_u64, c_u32, c_i32, ctypes.POINTER(c_u32), vp, vp, vp, vp, vp, vp, vp]),
+    "dr_varscan_select": (c_i32, [c_u64, c_u32, vp, vp, c_u32, vp, vp]),
     "dr_codec_var_decode": (c_i32, [vp, c_u64, vp, c_u64, c_u32, c_u64, c_i32, ctypes.POINTER(c_u32),
                                     ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp]),
     "dr_codec_var_sizes": (c_i32, [c_u64, c_i32, ctypes.POINTER(c_u32), ctypes.POINTER(vp), ctypes.POINTER(vp),
@@ -134,10 +140,88 @@ def block_index_host(data, dtype, block: int = BLOCK):
     return int(n), np.asarray(offs, dtype=np.int64)
 
 
+VARSCAN_CHUNK = 4096          # bytes per speculative chain (csrc/kernels/varscan.hip)
+VARSCAN_MAX_WALK = 1 << 16    # records a chain's exit walk may take before giving up
+
+
+def block_index_device(buf: torch.Tensor, dtype, block: int = BLOCK, chunk: int = VARSCAN_CHUNK):
+    """(records, int64 device offsets of every ``block``-th record) of a part in HBM, found on
+    the device by speculative per-chunk parses stitched at their sync points
+    (csrc/kernels/varscan.hip), or None when the stream is irregular there (a walk that never
+    re-synchronises, a record the plausibility checks reject): the caller then scans on the host.
+    Two host syncs (the stitch check and the record count); the pointer chase over chunk sync
+    points runs on the host only when some walk did not sync in the very next chunk."""
+    import numpy as np
+    lay = var_layout(dtype)
+    if lay is None or not buf.is_cuda or chunk % 32:
+        return None
+    n = buf.numel()
+    dev = buf.device
+    if n == 0:
+        return 0, torch.empty(0, dtype=torch.int64, device=dev)
+    nf = len(lay)
+    sizes = (c_u32 * nf)(*[sz for _, _, sz in lay])
+    C = int(chunk)
+    nch = (n + C - 1) // C
+    bits = torch.empty((n + 31) // 32, dtype=torch.int32, device=dev)
+    exitp = torch.empty(nch, dtype=torch.int64, device=dev)
+    sync = torch.empty(nch, dtype=torch.int64, device=dev)
+    st = stream_of(buf)
+    _lib.call("dr_varscan_chains", ptr(buf), c_u64(n), c_u32(C), nf, sizes, ptr(bits), ptr(exitp), ptr(sync),
+              c_u32(VARSCAN_MAX_WALK), st)
+    ok = (exitp >= 0).all() & (exitp[-1] == n)
+    if nch > 1:
+        y = sync[:-1]
+        ok = ok & ((y >= 0) & (y < n) & (torch.div(y, C, rounding_mode="floor") ==
+                                         torch.arange(1, nch, device=dev))).all()
+    if bool(ok.item()):
+        entry = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), sync[:-1]])
+        on_path = torch.ones(nch, dtype=torch.uint8, device=dev)
+    else:
+        ex, sy = exitp.cpu().numpy(), sync.cpu().numpy()
+        ent = np.full(nch, -1, dtype=np.int64)
+        on = np.zeros(nch, dtype=np.uint8)
+        c, ent[0] = 0, 0
+        while True:
+            on[c] = 1
+            if ex[c] < 0:
+                return None
+            if c == nch - 1:
+                if ex[c] != n:
+                    return None
+                break
+            y = int(sy[c])
+            if y < 0:
+                return None
+            if y == n:
+                break
+            k = y // C
+            ent[k], c = y, k
+        entry = torch.from_numpy(ent).to(dev)
+        on_path = torch.from_numpy(on).to(dev)
+    cnt = torch.zeros(nch, dtype=torch.int64, device=dev)
+    _lib.call("dr_varscan_fix", ptr(buf), c_u64(n), c_u32(C), nf, sizes, ptr(entry), ptr(on_path), ptr(exitp),
+              ptr(sync), ptr(bits), ptr(cnt), st)
+    incl = torch.cumsum(cnt, 0)
+    total = int(incl[-1].item())
+    base = incl - cnt
+    offs = torch.empty((total + block - 1) // block, dtype=torch.int64, device=dev)
+    if total:
+        _lib.call("dr_varscan_select", c_u64(n), c_u32(C), ptr(bits), ptr(base), c_u32(block), ptr(offs), st)
+    return total, offs
+
+
 def block_index(buf: torch.Tensor, dtype, block: int = BLOCK):
     """(records, int64 device offsets of every ``block``-th record, block) of a part of
-    variable-length records in HBM, for a part without a (valid) index sidecar."""
+    variable-length records in HBM, for a part without a (valid) index sidecar: found on the
+    device (block_index_device), the host scan (codec.cpp scan_record_blocks) only when the
+    device parse reports the stream irregular."""
     import numpy as np
+    got = block_index_device(buf, dtype, block) if buf.is_cuda else None
+    if got is not None:
+        return got[0], got[1], block
+    if buf.is_cuda:
+        log.info("variable-length part: device boundary scan declined, scanning %d bytes on the host", buf.numel())
     n, offs = block_index_host(buf.cpu().numpy(), dtype, block)
     return n, torch.from_numpy(np.ascontiguousarray(offs)).to(buf.device), block
 

@@ -114,6 +114,20 @@ def _device_bytes(x) -> int:
     return 0
 
 
+def _rows100_source(uri) -> bool:
+    """gen://terasort, or a stored table of raw 100-byte rows (partfile ``format: rows``)."""
+    scheme, path, _ = parse_uri(uri)
+    if scheme == "gen":
+        return path.strip("/") == "terasort"
+    if scheme in ("partfile", "file"):
+        try:
+            sch = provider_for(uri).schema(uri) or {}
+        except Exception:  # noqa: BLE001
+            return False
+        return sch.get("format") == "rows" and int(sch.get("stride", 0)) == 100
+    return False
+
+
 def _read_sizes(uri, P):
     """Bytes (or rows) of each of the P partitions of a store, known without reading it: the
     partfile metadata's part sizes, or the generator's row ranges (None otherwise)."""
@@ -149,6 +163,8 @@ class GpuJobRunner:
         self.op_counts = collections.Counter()   # (operator, "device" | "host") -> executions
         from ..io.writer import WriteStats
         self.write_stats = WriteStats()          # partfile parts written by this job
+        from ..io.reader import ReadStats
+        self.read_stats = ReadStats()            # part files read into HBM by this job
         self.transports: list = []      # (stage, edge kind, "device" | "object", bytes / reason)
         self.timings: dict = {}
         R = native_runtime()
@@ -304,21 +320,22 @@ class GpuJobRunner:
                 out.add(x.id)
         return out
 
-    def _pitch_gen_reads(self) -> set:
-        """One rank: stages ``read(gen://terasort) -> sort(ascending byte-string key of <= 16
-        bytes) -> ...`` (the one-rank OrderBy plan).  Their op_read stores the records at a
-        128-byte pitch (one aligned HBM line per record) and op_sort sorts them with
+    def _pitch_gen_reads(self) -> dict:
+        """One rank: stages ``read(100-byte records) -> sort(ascending byte-string key of <= 16
+        bytes) -> ...`` (the one-rank OrderBy plan) over gen://terasort or a stored table of raw
+        100-byte rows (partfile ``format: rows``).  Their op_read stores the records at a 128-byte
+        pitch (one aligned HBM line per record) and op_sort sorts them with
         ops/sort.sort_rows_pitch128: the sort's random row reads fetch one line per record
-        instead of ~1.78.  ``LineAlignedSortInput=False`` (context property) turns it off."""
-        out = set()
+        instead of ~1.78.  ``LineAlignedSortInput=False`` (context property) turns it off.
+        Returns {stage id: (key offset, key length)}."""
+        out = {}
         if self.world.size != 1 or not self.gpu_ok or not self.ctx._props.get("LineAlignedSortInput", True):
             return out
         from ..gpu import trace as TR
         from ..gpu.table import Shape
         for x in self.plan.stages:
             if not (not x.inputs and len(x.ops) >= 2 and x.ops[0]["op"] == "read" and x.ops[1]["op"] == "sort"
-                    and parse_uri(x.ops[0]["uri"])[0] == "gen"
-                    and parse_uri(x.ops[0]["uri"])[1].strip("/") == "terasort"
+                    and _rows100_source(x.ops[0]["uri"])
                     and x.ops[1].get("comparer") is None and not x.ops[1].get("descending", False)):
                 continue
             rows = torch.zeros((2, 100), dtype=torch.uint8, device=self.dev)
@@ -328,7 +345,7 @@ class GpuJobRunner:
             except Exception:  # noqa: BLE001
                 continue
             if kind == "bytes" and 1 <= spec.length <= 16 and spec.off + spec.length <= 100:
-                out.add(x.id)
+                out[x.id] = (spec.off, spec.length)
         return out
 
     def _materialize(self, sid: int):
@@ -968,6 +985,8 @@ class GpuJobRunner:
                     op_counts={f"{k[0]}:{k[1]}": v for k, v in self.op_counts.items()},
                     placement=self.place, moved={f"{k[0]}:{k[1]}": v for k, v in self.moved.items()},
                     write=dict(bytes=self.write_stats.bytes, seconds=round(self.write_stats.seconds, 4)),
+                    read=dict(bytes=self.read_stats.bytes, seconds=round(self.read_stats.seconds, 4)),
+                    sort_path=getattr(self, "last_sort_path", None),
                     statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()],
                     external_sort=getattr(self, "extsort_stats", None), join=getattr(self, "join_stats", None),
                     recovery=self.recovery)
@@ -1409,7 +1428,9 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     from .jobmanager import write_schema
     W, me = runner.world.size, runner.world.rank
     dt = s.dtype
-    rows_fmt = any(isinstance(v, HostRows) for v in local.values())
+    rows_fmt = any(isinstance(v, HostRows) or (isinstance(v, DeviceTable) and v.rows is not None and
+                                               v.shape.kind == "rows" and v.device.type == "cuda")
+                   for v in local.values())
     streamed = [v for v in local.values() if isinstance(v, GS.StreamedPart)]
     if streamed and (dt is None or dt == T.Pickle):
         dt = streamed[0].dtype

@@ -3,8 +3,9 @@
     python tools/micro/codec_bw.py [GB]
 
 * fixed-width records (8 x Int64 = 64 bytes): decode (rows -> columns) and encode;
-* variable-length records (Int64 key, a 12..40-character string, a Float64) with the part's
-  block index: decode.
+* variable-length records (Int64 key, a 12..40-character string, a Float64): record-boundary
+  discovery without a sidecar (device speculative chains, csrc/kernels/varscan.hip, vs the host
+  scan) and decode with the found block index.
 GB/s = part bytes / kernel time (best of 3, HIP events)."""
 import os
 import sys
@@ -52,9 +53,17 @@ def main():
     blob = B.encode_records(vdt, recs)
     reps = max(1, int(gb * 1e9) // len(blob))
     part = np.tile(np.frombuffer(blob, dtype=np.uint8), reps)
+    import time
+    t0 = time.time()
     n_idx, offs = CD.block_index_host(part, vdt)
+    th = time.time() - t0
     dbuf = torch.from_numpy(part).cuda()
-    doffs = torch.from_numpy(offs).cuda()
+    got = CD.block_index_device(dbuf, vdt)
+    assert got is not None and got[0] == n_idx and torch.equal(got[1].cpu(), torch.from_numpy(offs)), "boundary mismatch"
+    ms = timed(lambda: CD.block_index_device(dbuf, vdt))
+    print(f"string boundaries (device, no sidecar): {part.size / 1e9:.1f} GB in {ms:.2f} ms = "
+          f"{part.size / 1e6 / ms:.0f} GB/s (host scan {th * 1e3:.0f} ms = {part.size / 1e9 / th:.1f} GB/s)", flush=True)
+    doffs = got[1]
     ms = timed(lambda: CD.decode_var(dbuf, vdt, n_idx, doffs))
     print(f"string decode: {part.size / 1e9:.1f} GB ({n_idx} records) in {ms:.2f} ms = {part.size / 1e6 / ms:.0f} GB/s",
           flush=True)
