@@ -117,6 +117,9 @@ _DEFAULTS = dict(
     RerunInputsMaxBytes=1 << 30,  # inputs a failed GPU vertex's restart record may persist
     ExternalSortToDisk=None,      # its partfile:// output written through a memory-mapped part file
     #                               (None: when the output exceeds half of the available host memory)
+    StreamStages=None,            # read -> record-wise ops -> partfile stages chunk-streamed (runtime/
+    #                               streaming.py; None: when a source partition exceeds StreamChunkBytes)
+    StreamChunkBytes=4 << 30,     # ... and their chunk size
     GraceJoin=None,               # a Join as the partitioned grace join stage (runtime/grace_stage.py;
     #                               None: when its inputs would crowd the HBM budget; False: never)
 )

@@ -235,10 +235,12 @@ def op_read(op, inputs, v):
             R.gen_records64(cols, lo, nk, int(q.get("seed", 0)), dim_multiplier(nk) if q.get("mode") == "dim" else 0)
             # the generator's value contract (models/records_cpu.py): keys in [0, nk), payloads
             # mix64(..) >> 33, i.e. 31-bit -- column statistics for operators that pack by width
+            # (``bounds=0`` withholds them, as a stored table would: operators then measure them)
             from . import stats
-            stats.set_bounds(cols[0], 0, nk - 1)
-            for c in cols[1:]:
-                stats.set_bounds(c, 0, (1 << 31) - 1)
+            if str(q.get("bounds", "1")) != "0":
+                stats.set_bounds(cols[0], 0, nk - 1)
+                for c in cols[1:]:
+                    stats.set_bounds(c, 0, (1 << 31) - 1)
             names = FIELDS[:ncols]
             return DeviceTable.from_columns(dict(zip(names, cols)), Shape("tuple", names))
         if kind == "range":

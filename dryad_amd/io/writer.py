@@ -104,6 +104,7 @@ class PartWriter:
                 self.dev = flat.device
                 self.cs = torch.cuda.Stream(self.dev)
             self.cs.wait_stream(torch.cuda.current_stream(flat.device))
+            flat.record_stream(self.cs)          # the caller may drop it while its DMAs are in flight
         piece = min(CHUNK, self.ring[0].tensor.numel())        # the ring may predate a CHUNK change
         for a in range(0, n, piece):
             m = min(piece, n - a)

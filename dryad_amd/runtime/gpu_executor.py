@@ -43,6 +43,7 @@ from ..utils import trace as TRC
 from ..utils.log import get_logger
 from . import fused_join as FJ
 from . import grace_stage as GS
+from . import streaming as ST
 from . import vertex_ops as V
 from .executor import _BaseExecutor
 
@@ -152,6 +153,8 @@ class GpuJobRunner:
         self.pool = pool
         self.row_sets: dict = {}          # (stage, partition) -> pooled BufferSet holding its rows
         self.moved: dict = {}             # (stage, partition) -> rank whose duplicate attempt won
+        self.stream_plans: dict = {}      # stage -> chunk plan of a streamed stage (None: not streamed)
+        self.stream_stats: dict = {}      # (stage, partition) -> chunks / records / bytes streamed
         self.place = None                 # partition -> rank (None: p % W)
         self.fused: dict = {}             # merge stage id -> fused distributed-OrderBy descriptor
         self.skipped: set = set()
@@ -809,6 +812,16 @@ class GpuJobRunner:
                 raise ChannelReadError(self.edge_ids[(self.vids[s.inputs[0].src][q], self.vids[s.id][p], 0)],
                                        f"injected read error on the channel {s.inputs[0].src}[{q}] -> {s.id}[{p}]")
         vctx = GpuVertexContext(p, s.partitions, self.vids[s.id][p], version, s, self.dev, self.world, self)
+        if s.id not in self.stream_plans:
+            self.stream_plans[s.id] = ST.streamable(self, s)
+        if self.stream_plans[s.id] is not None:
+            # read -> record-wise ops -> write, chunk by chunk in bounded HBM (runtime/streaming.py)
+            with TRC.range(f"vertex {s.id}:{s.name}[{p}] v{version} (streamed)"):
+                out = ST.run(self, s, p, version, vctx, self.stream_plans[s.id], cancel)
+            if fault == "crash":
+                os.remove(out.path)
+                raise VertexCrash(f"injected crash of {s.name}[{p}] v{version} (output discarded)")
+            return out
         inputs = [self._merge_streams(si, streams) for si, streams in zip(s.inputs, raw_inputs)]
         data = None
         with TRC.range(f"vertex {s.id}:{s.name}[{p}] v{version}"):
@@ -987,6 +1000,7 @@ class GpuJobRunner:
                     write=dict(bytes=self.write_stats.bytes, seconds=round(self.write_stats.seconds, 4)),
                     read=dict(bytes=self.read_stats.bytes, seconds=round(self.read_stats.seconds, 4)),
                     sort_path=getattr(self, "last_sort_path", None),
+                    streamed={f"{k[0]}:{k[1]}": v for k, v in self.stream_stats.items()},
                     statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()],
                     external_sort=getattr(self, "extsort_stats", None), join=getattr(self, "join_stats", None),
                     recovery=self.recovery)
@@ -1430,6 +1444,7 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     dt = s.dtype
     rows_fmt = any(isinstance(v, HostRows) or (isinstance(v, DeviceTable) and v.rows is not None and
                                                v.shape.kind == "rows" and v.device.type == "cuda")
+                   or (isinstance(v, GS.StreamedPart) and v.rows is not None)
                    for v in local.values())
     streamed = [v for v in local.values() if isinstance(v, GS.StreamedPart)]
     if streamed and (dt is None or dt == T.Pickle):
@@ -1455,8 +1470,10 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     mine, fmt_extra = {}, None
     for p, v in local.items():
         tmp = PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, 0)
-        if isinstance(v, GS.StreamedPart):          # written bucket by bucket by its stage
+        if isinstance(v, GS.StreamedPart):          # written bucket / chunk by chunk by its stage
             os.replace(v.path, tmp)
+            if v.rows is not None:
+                fmt_extra = dict(v.rows)
             mine[p] = tmp
             continue
         if rows_fmt:

@@ -57,8 +57,9 @@ class StreamedPart:
     """A partition already written to ``path`` (a tmp part file) by a streaming stage; the output
     commit renames it into place (runtime/gpu_executor._commit_partfile_impl)."""
 
-    def __init__(self, path: str, n: int, nbytes: int, dtype):
+    def __init__(self, path: str, n: int, nbytes: int, dtype, rows: dict | None = None):
         self.path, self.n, self.nbytes, self.dtype = path, n, nbytes, dtype
+        self.rows = rows                  # raw fixed-width rows: {stride, key_off, key_len}
 
 
 # ------------------------------------------------------------------------------------------------
