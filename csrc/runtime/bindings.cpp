@@ -10,6 +10,7 @@
 #include "jobgraph.h"
 #include "partreader.h"
 #include "partwriter.h"
+#include "pump.h"
 #include "workqueue.h"
 
 namespace py = pybind11;
@@ -355,4 +356,24 @@ PYBIND11_MODULE(_dryad_native, m) {
       .def("blocks_written", &BlockFifo::blocks_written)
       .def("capacity", &BlockFifo::capacity)
       .def("closed", &BlockFifo::closed);
+
+  // Job manager event pump (G-10): wait() releases the GIL until a message or a timer is due.
+  py::class_<MessagePump>(m, "MessagePump")
+      .def(py::init<>())
+      .def("post", &MessagePump::post, py::arg("kind"), py::arg("payload") = 0)
+      .def("post_after", &MessagePump::post_after, py::arg("delay_ms"), py::arg("kind"), py::arg("payload") = 0)
+      .def("wait", [](MessagePump& p, int64_t timeout_ms) {
+            std::vector<MessagePump::Message> got;
+            {
+              py::gil_scoped_release nogil;
+              got = p.wait(timeout_ms);
+            }
+            py::list out;
+            for (auto& x : got) out.append(py::make_tuple(x.kind, x.payload));
+            return out;
+          }, py::arg("timeout_ms") = -1)
+      .def("close", &MessagePump::close)
+      .def("pending", &MessagePump::pending)
+      .def("posted", &MessagePump::posted)
+      .def("delivered", &MessagePump::delivered);
 }

@@ -16,6 +16,7 @@
 
 #include "../codec.h"
 #include "../jobgraph.h"
+#include "../pump.h"
 #include "../workqueue.h"
 
 using namespace dryad;
@@ -148,11 +149,44 @@ static int test_workqueue(const std::string& dir) {
   return 0;
 }
 
+// the job manager pump under concurrent posters (run under TSan by tests/test_sanitizers.py)
+static int test_pump() {
+  dryad::MessagePump p;
+  constexpr int kThreads = 4, kEach = 2000;
+  std::vector<std::thread> th;
+  for (int t = 0; t < kThreads; ++t)
+    th.emplace_back([&p, t] {
+      for (int i = 0; i < kEach; ++i) {
+        if (i % 100 == 0) p.post_after(1, 2, t);
+        p.post(1, (int64_t)t * kEach + i);
+      }
+    });
+  int64_t got = 0, timers = 0, sum = 0;
+  while (got < kThreads * kEach || timers < kThreads * (kEach / 100)) {
+    for (auto& m : p.wait(-1)) {
+      if (m.kind == 1) {
+        ++got;
+        sum += m.payload;
+      } else {
+        ++timers;
+      }
+    }
+  }
+  for (auto& x : th) x.join();
+  const int64_t n = (int64_t)kThreads * kEach;
+  CHECK(sum == n * (n - 1) / 2);
+  CHECK(p.wait(0).empty());
+  p.close();
+  CHECK(p.wait(-1).empty());
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const std::string dir = argc > 1 ? argv[1] : "/tmp";
   if (int r = test_jobgraph()) return r;
   if (int r = test_codec()) return r;
   if (int r = test_workqueue(dir)) return r;
+  if (int r = test_pump()) return r;
   std::printf("SELFTEST_OK\n");
   return 0;
 }

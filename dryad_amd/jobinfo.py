@@ -48,10 +48,16 @@ class JobHandle:
 
     def cancel(self):
         self._cancel.set()
+        pump = getattr(self, "pump", None)          # wake the job manager blocked in its pump
+        if pump is not None:
+            pump.post(MSG_CANCEL, 0)
 
     @property
     def cancelled(self) -> bool:
         return self._cancel.is_set()
+
+
+MSG_RESULT, MSG_DUPLICATES, MSG_CANCEL = 1, 2, 3     # job manager pump message kinds
 
 
 class DryadLinqJobInfo:

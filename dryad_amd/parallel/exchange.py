@@ -129,10 +129,13 @@ def exchange(world: World, sends: list, stats: ExchangeStats | None = None) -> l
     assert len(sends) == W
     proto = next((p for lst in sends for p in lst if p is not None), None)
     sig = signature(proto) if proto is not None else None
+    # string bytes per piece: every length column summed on the device, one host read for all
+    sums = [p.cols[lc][:p.n].sum().to(torch.int64) for lst in sends for p in lst if p.n
+            for _, lc, _ in _string_specs(p)]
+    vals = iter(torch.stack(sums).tolist() if sums else [])
     manifest = []
     for lst in sends:
-        manifest.append([(p.n, [int(p.cols[lc][:p.n].sum()) if p.n else 0 for _, lc, _ in _string_specs(p)])
-                         for p in lst])
+        manifest.append([(p.n, [next(vals) if p.n else 0 for _ in _string_specs(p)]) for p in lst])
     gathered = [None] * W
     dist.all_gather_object(gathered, (sig, manifest))
     sigs = [g[0] for g in gathered if g[0] is not None]

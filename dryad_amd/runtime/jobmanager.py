@@ -28,6 +28,8 @@ log = get_logger("jobmanager")
 class JobRunner:
     """Builds the vertex graph of one plan and drives it to completion."""
 
+    DUPLICATE_CHECK_MS = 500      # period of the straggler check (a pump timer, not a poll)
+
     def __init__(self, ctx, plan, pool, job_dir: str, handle=None, faults=None):
         self.ctx = ctx
         self.plan = plan
@@ -175,7 +177,15 @@ class JobRunner:
         running = {}          # (vid, version) -> slot
         pending = []          # ReadyItems waiting for a slot
         results = {}          # vid -> result of the winning version
-        last_dup = 0.0
+        # event pump (DrMessagePump): results, the duplicate-check timer and a user cancel are
+        # messages; the loop blocks in pump.wait() (GIL released) until one is due
+        from ..jobinfo import MSG_CANCEL, MSG_DUPLICATES, MSG_RESULT
+        pump = native_runtime().MessagePump()
+        self.pump = pump
+        self.pool.attach(pump, MSG_RESULT)
+        if self.handle is not None:
+            self.handle.pump = pump
+        pump.post_after(int(self.DUPLICATE_CHECK_MS), MSG_DUPLICATES)
         try:
             while not g.done():
                 if g.failed():
@@ -204,15 +214,17 @@ class JobRunner:
                         g.abort("deadlock: nothing runnable")
                         break
                     continue
-                for slot, res in self.pool.poll(0.2 if running else 0.0):
+                for kind, _ in pump.wait(-1 if running else 0):
+                    if kind == MSG_DUPLICATES:
+                        # duplicates are queued inside the JobGraph; take_ready hands them out
+                        g.check_duplicates(now())
+                        pump.post_after(int(self.DUPLICATE_CHECK_MS), MSG_DUPLICATES)
+                for slot, res in self.pool.poll(0):
                     key = (res["vertex"], res["version"])
                     running.pop(key, None)
                     self.pool.release(slot)
                     self._handle_result(res, running, results, now)
-                if now() - last_dup > 0.5:
-                    last_dup = now()
-                    # duplicates are queued inside the JobGraph; take_ready hands them out
-                    g.check_duplicates(now())
+                self.pool.rearm()
                 self._drain_events()
             self._drain_events()
             if g.failed():
@@ -226,6 +238,11 @@ class JobRunner:
         finally:
             for key, slot in list(running.items()):
                 self.pool.kill(slot)
+            self.pool.attach(None, MSG_RESULT)
+            if self.handle is not None:
+                self.handle.pump = None
+            self.pump_stats = dict(posted=pump.posted(), delivered=pump.delivered())
+            pump.close()
 
     def _handle_result(self, res, running, results, now):
         g = self.g

@@ -41,6 +41,56 @@ class ProcessPool:
             self._launch(i)
         for i in range(self.n):
             self._accept(i)
+        self._pump = None
+        self._watcher = None
+        self._armed = threading.Event()
+        self._wake_r, self._wake_w = mp.Pipe(duplex=False)
+        self._closed = False
+
+    # ---- event-driven results: a watcher thread posts a pump message when a host has something
+    # to say; the job manager then collects it with poll(0) on its own thread and re-arms
+    def attach(self, pump, kind: int):
+        self._pump, self._kind = pump, kind
+        if self._watcher is None:
+            self._watcher = threading.Thread(target=self._watch, daemon=True, name="dryad-vh-watch")
+            self._watcher.start()
+        self._armed.set()
+
+    def rearm(self):
+        self._armed.set()
+
+    def _conns_changed(self):
+        if self._watcher is not None:
+            try:
+                self._wake_w.send_bytes(b"x")
+            except OSError:
+                pass
+
+    def _watch(self):
+        while not self._closed:
+            self._armed.wait()
+            if self._closed:
+                return
+            conns = [c for c in list(self._conns) if c is not None]
+            try:
+                ready = mp_wait(conns + [self._wake_r])
+            except (OSError, ValueError):            # a connection closed under us: let poll() see
+                ready = conns
+            if self._wake_r in ready:
+                try:
+                    while self._wake_r.poll():
+                        self._wake_r.recv_bytes()
+                except (OSError, EOFError):
+                    return
+                ready = [r for r in ready if r is not self._wake_r]
+                if not ready:
+                    continue                         # refresh the connection list
+            if self._closed:
+                return
+            self._armed.clear()
+            pump = self._pump
+            if pump is not None:
+                pump.post(self._kind, 0)
 
     def _launch(self, i):
         import sys
@@ -77,11 +127,18 @@ class ProcessPool:
 
     def poll(self, timeout):
         out = []
-        live = {c: i for i, c in enumerate(self._conns) if self._current[i] is not None}
+        conns = {c: i for i, c in enumerate(self._conns) if c is not None}
+        live = {c for c, i in conns.items() if self._current[i] is not None}
         if not live:
-            return out
-        for r in mp_wait(list(live), timeout):
-            i = live[r]
+            timeout = 0                              # only idle hosts to look at
+        for r in mp_wait(list(conns), timeout):
+            i = conns[r]
+            if r not in live:                        # an idle host: died (EOF) -> restarted
+                try:
+                    r.recv()
+                except (EOFError, OSError):
+                    self._restart(i)
+                continue
             try:
                 res = r.recv()
             except (EOFError, OSError):
@@ -107,6 +164,7 @@ class ProcessPool:
             p.wait(5)
         self._launch(i)
         self._accept(i)
+        self._conns_changed()
 
     def kill(self, slot):
         """Cancel the vertex running on a slot by killing its host (restarted immediately)."""
@@ -115,6 +173,9 @@ class ProcessPool:
         self.sched.release(slot)
 
     def close(self):
+        self._closed = True
+        self._armed.set()
+        self._conns_changed()
         for c in self._conns:
             try:
                 c.send(None)
@@ -154,6 +215,7 @@ class ThreadPool:
         self._cancelled = set()
         self._plans = {}
         self._threads = []
+        self._pump = None
         for i in range(self.n):
             t = threading.Thread(target=self._loop, args=(i,), daemon=True, name=f"dryad-vertex-{i}")
             t.start()
@@ -170,6 +232,15 @@ class ThreadPool:
                 return
             res = execute_vertex(cmd, self._plans.get(cmd["job"]))
             self._q.put((i, res))
+            pump = self._pump
+            if pump is not None:
+                pump.post(self._kind, 0)
+
+    def attach(self, pump, kind: int):
+        self._pump, self._kind = pump, kind
+
+    def rearm(self):
+        pass
 
     def acquire(self, preferred=(), waited=1e9):
         w = self.sched.place(list(preferred), waited)
