@@ -816,8 +816,13 @@ class GpuJobRunner:
             self.stream_plans[s.id] = ST.streamable(self, s)
         if self.stream_plans[s.id] is not None:
             # read -> record-wise ops -> write, chunk by chunk in bounded HBM (runtime/streaming.py)
-            with TRC.range(f"vertex {s.id}:{s.name}[{p}] v{version} (streamed)"):
-                out = ST.run(self, s, p, version, vctx, self.stream_plans[s.id], cancel)
+            try:
+                with TRC.range(f"vertex {s.id}:{s.name}[{p}] v{version} (streamed)"):
+                    out = ST.run(self, s, p, version, vctx, self.stream_plans[s.id], cancel)
+            except ST.NotStreamable as e:
+                log.info("%s: streamed execution declined (%s)", s.name, e)
+                self.stream_plans[s.id] = None
+                return self.run_vertex(s, p, version, raw_inputs, inject=False, cancel=cancel)
             if fault == "crash":
                 os.remove(out.path)
                 raise VertexCrash(f"injected crash of {s.name}[{p}] v{version} (output discarded)")
@@ -1086,8 +1091,23 @@ class GpuJobRunner:
                 return
 
     def _speculate(self, s) -> bool:
-        return self.g_speculative and s.id not in self.gang_stages and s.id not in self.skipped and \
-            self._duplicable(s, self.plan)
+        """Duplicates only where a vertex's output may live on any rank: a leaf stage outside
+        gangs whose consumers all fetch their inputs through owner() (the fused OrderBy / join /
+        grace / out-of-core stages and the lazy or pitched reads feeding them assume partition p
+        on its home rank, so they and their inputs are excluded)."""
+        if not self.g_speculative or not self._duplicable(s, self.plan) or s.id in self.gang_stages:
+            return False
+        # (a gang consumer is fine: its exchange gathers every source partition from owner())
+        special = set(self.skipped) | set(getattr(self, "lazy_gen_stages", ())) \
+            | set(getattr(self, "pitch_gen_stages", ()))
+        if self.gpu_ok:                  # (the fused OrderBy only runs on GPU ranks)
+            for f in self.fused.values():
+                special |= {f["x"], *f["stages"]}
+        for d in (*self.fused_joins.values(), *self.grace_joins.values()):
+            special |= set(d["stages"])
+        for e in self.external.values():
+            special |= set(e.get("skip", ()))
+        return s.id not in special and not any(c in special for c in self.plan.consumers(s.id))
 
     def _run_stage_speculative(self, s, ready, refresh, now):
         """A leaf stage with speculative duplication (DrManagerBase::CheckForDuplicates,

@@ -89,10 +89,14 @@ def streamable(runner, s):
     big = max((_partition_bytes(src[0], src[1], p) for p in range(s.partitions)), default=0)
     if not force and big <= chunk:
         return None
-    dt = s.dtype
-    if src[0] != "rows" and (dt is None or dt == T.Pickle):
+    if s.dtype == T.Pickle:
         return None
     return dict(kind=src[0], info=src[1], chunk=chunk)
+
+
+class NotStreamable(Exception):
+    """The first chunk's output has no fixed record layout the part writer could encode (the
+    vertex then runs unstreamed)."""
 
 
 def _chunks(plan, p, device, vctx):
@@ -191,7 +195,8 @@ def run(runner, s, p, version, vctx, plan, cancel=None):
     base = PF.default_base(path)
     os.makedirs(os.path.dirname(base) or ".", exist_ok=True)
     tmp = f"{PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, version)}.stream"
-    n, rows_fmt, chunks = 0, None, 0
+    from .grace_stage import _table_dtype
+    n, rows_fmt, chunks, dtype = 0, None, 0, s.dtype
     with WR.PartWriter(tmp, vctx.device, runner.write_stats) as w:
         for t in _chunks(plan, p, vctx.device, vctx):
             if cancel is not None and cancel.is_set():
@@ -200,10 +205,16 @@ def run(runner, s, p, version, vctx, plan, cancel=None):
             for op in s.ops[1:-1]:
                 data = runner._run_op(op, [data], vctx, s)
             data = runner._run_op(s.ops[-1], [data], vctx, s)
-            b, rf = _encode(data, s.dtype)
+            is_rows = isinstance(data, DeviceTable) and data.rows is not None and data.shape.kind == "rows"
+            if dtype is None and not is_rows:
+                # the plan does not know the record type: the first chunk's columns decide it
+                dtype = _table_dtype(data) if isinstance(data, DeviceTable) else None
+                if dtype is None:
+                    raise NotStreamable(f"{s.name}: no fixed record layout to stream")
+            b, rf = _encode(data, dtype)
             rows_fmt = rows_fmt or rf
             w.write(b)
             n += data.n if isinstance(data, DeviceTable) else len(data)
             chunks += 1
     runner.stream_stats[(s.id, p)] = dict(chunks=chunks, records=n, bytes=w.off)
-    return StreamedPart(tmp, n, w.off, s.dtype, rows=rows_fmt)
+    return StreamedPart(tmp, n, w.off, dtype, rows=rows_fmt)

@@ -1,0 +1,238 @@
+// A/B of the look-back radix scatter pass (csrc/kernels/sort.hip os_scatter_kernel) on 1.25e9
+// E64 entries: one 8-bit digit pass, the production tile geometry, two ways of ranking a wave's
+// entries by digit:
+//   lds     per item: LDS atomicOr of the lane bit into a per-(wave, digit) mask, read the mask
+//           back (the digit's peers), leader updates the wave's digit counter (production);
+//   ballot  per item: the peers mask from 8 ballots of the digit bits (no LDS atomics, no mask
+//           reset), leader updates the counter.
+// Reports ms per pass and the logical TB/s (8 B read + 8 B written per entry); checks that both
+// variants produce the same permutation.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc/kernels tools/micro/scatter_ab.hip -o build/scatter_ab
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+constexpr int kBins = 256;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+
+__device__ __forceinline__ uint32_t dig(const E64& e, int shift) { return (uint32_t)((e.v >> shift) & 0xFF); }
+
+__global__ void fill(E64* x, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    x[i].v = (mix64(i * 0x9E37ull + 11) & ~0xFFFFFFFFull) | (uint32_t)i;
+}
+
+__global__ void hist(const E64* x, uint64_t n, int shift, uint32_t* counts) {
+  __shared__ uint32_t h[kBins];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    atomicAdd(&h[dig(x[i], shift)], 1u);
+  __syncthreads();
+  atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ void excl(uint32_t* c) {
+  __shared__ uint32_t sc[4];
+  uint32_t tot;
+  c[threadIdx.x] = block_exclusive_scan256(c[threadIdx.x], sc, tot);
+}
+
+template <int ITEMS, bool BALLOT>
+__global__ __launch_bounds__(256) void scatter(const E64* __restrict__ in, E64* __restrict__ out, uint64_t n, int shift,
+                                               const uint32_t* __restrict__ gbase, unsigned long long* granules,
+                                               uint32_t* ticket, uint32_t tiles) {
+  constexpr int kTile = kBlock * ITEMS;
+  constexpr uint32_t tag_agg = 2, tag_inc = 3;
+  __shared__ E64 stage[kTile];
+  __shared__ uint32_t wcnt[4][kBins];
+  __shared__ unsigned long long wmask[BALLOT ? 1 : 4][kBins];
+  __shared__ uint32_t bstart[kBins];
+  __shared__ uint32_t goff[kBins];
+  __shared__ uint32_t sc[4];
+  __shared__ uint32_t tile_sh;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  if (t == 0) tile_sh = __hip_atomic_fetch_add((gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (!BALLOT) {
+    wmask[0][t] = 0ull; wmask[1][t] = 0ull; wmask[2][t] = 0ull; wmask[3][t] = 0ull;
+  }
+  wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+  __syncthreads();
+  const uint32_t tile = tile_sh;
+  if (tile >= tiles) return;
+  const uint64_t base = (uint64_t)tile * kTile;
+  const uint32_t cnt = (uint32_t)((n - base) < (uint64_t)kTile ? (n - base) : kTile);
+  E64 cur[ITEMS];
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+    if (pos < cnt) cur[r] = in[base + pos];
+  }
+  uint32_t rk[ITEMS], dg[ITEMS];
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+    const bool valid = pos < cnt;
+    const uint32_t d = valid ? dig(cur[r], shift) : 0u;
+    unsigned long long peers;
+    if constexpr (BALLOT) {
+      peers = __ballot(valid);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const unsigned long long m = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? m : ~m;
+      }
+      if (!valid) peers = 0ull;
+    } else {
+      if (valid) atomicOr(&wmask[w][d], 1ull << l);
+      __builtin_amdgcn_wave_barrier();
+      peers = valid ? wmask[w][d] : 0ull;
+    }
+    const uint32_t below = popc_below(peers);
+    const uint32_t prior = wcnt[w][d];
+    __builtin_amdgcn_wave_barrier();
+    if (valid && below == 0) {
+      wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      if constexpr (!BALLOT) wmask[w][d] = 0ull;
+    }
+    __builtin_amdgcn_wave_barrier();
+    rk[r] = prior + below;
+    dg[r] = d;
+  }
+  __syncthreads();
+  const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+  const uint32_t tot = c0 + c1 + c2 + c3;
+  gu64* mine = (gu64*)(granules + (uint64_t)tile * kBins + t);
+  __hip_atomic_store(mine, ((unsigned long long)(tile == 0 ? tag_inc : tag_agg) << 32) | tot, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
+  uint32_t all;
+  bstart[t] = block_exclusive_scan256(tot, sc, all);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+    if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
+  }
+  uint32_t ex = 0;
+  if (tile > 0) {
+    uint64_t j = tile;
+    for (;;) {
+      unsigned long long g[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        g[k] = j >= (uint64_t)k + 1 ? __hip_atomic_load((gu64*)(granules + (j - 1 - k) * kBins + t), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT)
+                                    : 0ull;
+      bool done = false;
+      int used = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (done || used < k) continue;
+        const uint32_t tag = (uint32_t)(g[k] >> 32);
+        if (tag == tag_inc) {
+          ex += (uint32_t)g[k];
+          done = true;
+        } else if (tag == tag_agg) {
+          ex += (uint32_t)g[k];
+          used = k + 1;
+        }
+      }
+      if (done) break;
+      j -= (uint64_t)used;
+      if (used == 0) __builtin_amdgcn_s_sleep(1);
+    }
+    __hip_atomic_store(mine, ((unsigned long long)tag_inc << 32) | (ex + tot), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  goff[t] = gbase[t] + ex;
+  __syncthreads();
+#pragma unroll 4
+  for (uint32_t j = t; j < cnt; j += kBlock) {
+    const E64 v = stage[j];
+    const uint32_t d = dig(v, shift);
+    out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+  }
+}
+
+__global__ void diff(const E64* a, const E64* b, uint64_t n, unsigned long long* bad) {
+  uint32_t k = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    k += a[i].v != b[i].v;
+  if (k) atomicAdd(bad, (unsigned long long)k);
+}
+}  // namespace
+
+#define HC(x)                                                              \
+  do {                                                                     \
+    hipError_t e_ = (x);                                                   \
+    if (e_ != hipSuccess) {                                                \
+      std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));         \
+      std::exit(1);                                                        \
+    }                                                                      \
+  } while (0)
+
+template <int ITEMS, bool BALLOT>
+static float run(const E64* in, E64* out, uint64_t n, int shift, const uint32_t* gbase, void* ws, size_t ws_bytes) {
+  const uint64_t tile = 256ull * ITEMS, tiles = (n + tile - 1) / tile;
+  float best = 1e9f;
+  hipEvent_t a, b;
+  HC(hipEventCreate(&a));
+  HC(hipEventCreate(&b));
+  for (int it = 0; it < 4; ++it) {
+    HC(hipMemset(ws, 0, ws_bytes));
+    HC(hipEventRecord(a));
+    scatter<ITEMS, BALLOT><<<(unsigned)tiles, 256>>>(in, out, n, shift, gbase,
+                                                     reinterpret_cast<unsigned long long*>((char*)ws + 256),
+                                                     reinterpret_cast<uint32_t*>(ws), (uint32_t)tiles);
+    HC(hipEventRecord(b));
+    HC(hipEventSynchronize(b));
+    float ms;
+    HC(hipEventElapsedTime(&ms, a, b));
+    if (it > 0 && ms < best) best = ms;
+  }
+  return best;
+}
+
+int main(int argc, char** argv) {
+  const uint64_t n = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1250000000ull;
+  const int shift = 32;
+  E64 *in, *o1, *o2;
+  uint32_t* gbase;
+  unsigned long long* bad;
+  HC(hipMalloc(&in, n * 8));
+  HC(hipMalloc(&o1, n * 8));
+  HC(hipMalloc(&o2, n * 8));
+  HC(hipMalloc(&gbase, kBins * 4));
+  HC(hipMalloc(&bad, 8));
+  const size_t ws_bytes = 256 + ((n + 4095) / 4096 + 1) * kBins * 8;
+  void* ws;
+  HC(hipMalloc(&ws, ws_bytes));
+  fill<<<8192, 256>>>(in, n);
+  HC(hipMemset(gbase, 0, kBins * 4));
+  hist<<<4096, 256>>>(in, n, shift, gbase);
+  excl<<<1, 256>>>(gbase);
+  HC(hipDeviceSynchronize());
+  const double gb = n * 16.0 / 1e9;
+  float ms = run<32, false>(in, o1, n, shift, gbase, ws, ws_bytes);
+  std::printf("lds    items=32: %.3f ms  %.2f TB/s\n", ms, gb / ms);
+  ms = run<32, true>(in, o2, n, shift, gbase, ws, ws_bytes);
+  std::printf("ballot items=32: %.3f ms  %.2f TB/s\n", ms, gb / ms);
+  HC(hipMemset(bad, 0, 8));
+  diff<<<4096, 256>>>(o1, o2, n, bad);
+  unsigned long long hb = 0;
+  HC(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
+  std::printf("mismatches lds vs ballot: %llu\n", hb);
+  ms = run<24, true>(in, o2, n, shift, gbase, ws, ws_bytes);
+  std::printf("ballot items=24: %.3f ms  %.2f TB/s\n", ms, gb / ms);
+  ms = run<16, true>(in, o2, n, shift, gbase, ws, ws_bytes);
+  std::printf("ballot items=16: %.3f ms  %.2f TB/s\n", ms, gb / ms);
+  std::fflush(stdout);
+  return hb != 0;
+}
