@@ -70,7 +70,6 @@ def _partition_bytes(kind, info, p) -> int:
 
 def streamable(runner, s):
     """The stage's chunk plan (source kind, info, chunk bytes) if it can stream, else None."""
-    from .. import types as T
     if not runner.gpu_ok or s.inputs or len(s.ops) < 2 or s.ops[-1]["op"] != "output" or not s.is_output:
         return None
     if any(o["op"] not in STREAM_OPS for o in s.ops[1:-1]):
@@ -88,8 +87,6 @@ def streamable(runner, s):
     force = bool(props.get("StreamStages"))
     big = max((_partition_bytes(src[0], src[1], p) for p in range(s.partitions)), default=0)
     if not force and big <= chunk:
-        return None
-    if s.dtype == T.Pickle:
         return None
     return dict(kind=src[0], info=src[1], chunk=chunk)
 
@@ -196,7 +193,9 @@ def run(runner, s, p, version, vctx, plan, cancel=None):
     os.makedirs(os.path.dirname(base) or ".", exist_ok=True)
     tmp = f"{PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, version)}.stream"
     from .grace_stage import _table_dtype
-    n, rows_fmt, chunks, dtype = 0, None, 0, s.dtype
+    from .. import types as T
+    n, rows_fmt, chunks = 0, None, 0
+    dtype = None if s.dtype in (None, T.Pickle) else s.dtype    # unknown: the first chunk decides
     with WR.PartWriter(tmp, vctx.device, runner.write_stats) as w:
         for t in _chunks(plan, p, vctx.device, vctx):
             if cancel is not None and cancel.is_set():
