@@ -4,9 +4,10 @@
 // without an index sidecar.  A length-prefixed stream is only parseable from a known boundary,
 // so the part is cut into C-byte chunks and parsed speculatively:
 //
-//   1. vs_chain   one lane per chunk parses from the chunk start as if it were a boundary and
-//                 sets a bit for every position it visits (the chunk's speculative chain), plus
-//                 the first position it reaches past the chunk (its exit).
+//   1. vs_chain   one lane per chunk parses from the chunk start as if it were a boundary
+//                 (restarting a byte later until kLock records in a row parse) and sets a bit
+//                 for every position it visits (the chunk's speculative chain), plus the first
+//                 position it reaches past the chunk (its exit).
 //   2. vs_walk    lane c walks on from its exit until it lands on a position some later chain
 //                 visited (the sync point).  From there on the two parses coincide (the parse
 //                 is a function of the position), so if chain c is right at its exit, the walk
@@ -73,28 +74,59 @@ __device__ __forceinline__ bool vs_bit(const uint32_t* __restrict__ bits, uint64
   return (bits[p >> 5] >> (p & 31)) & 1u;
 }
 
+// A chain locks onto the stream once kLock records in a row parse; until then a failed parse
+// restarts it one byte after the previous start (and forgets the positions of that attempt), so
+// a chunk whose start is not a boundary still finds one and follows the stream from there (the
+// exit walks of the previous chunk then meet it within the chunk).  A locked chain that fails
+// stops: it was not on the stream.
+constexpr int kLock = 4;
+
 __global__ __launch_bounds__(256) void vs_chain(const uint8_t* __restrict__ b, uint64_t n, uint32_t C, uint64_t nch,
                                                 VSchema s, uint32_t* __restrict__ bits, int64_t* __restrict__ exitp) {
   for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nch; c += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t s0 = c * C, s1 = s0 + C < n ? s0 + C : n;
     const uint64_t wend = (s1 + 31) >> 5;
-    uint64_t cw = s0 >> 5, p = s0;
+    uint64_t cw = s0 >> 5, p = s0, start = s0;
     uint32_t acc = 0;
-    while (p < s1) {
-      const uint64_t w = p >> 5;
+    uint64_t tent[kLock];
+    int run = 0;
+    bool locked = c == 0;                             // offset 0 is a boundary: chain 0 never restarts
+    auto mark = [&](uint64_t q) {                     // positions arrive in increasing order
+      const uint64_t w = q >> 5;
       while (cw < w) {
         bits[cw++] = acc;
         acc = 0;
       }
-      acc |= 1u << (p & 31);
-      p = vs_step(b, p, n, s);
-      if (p == kBad) break;
+      acc |= 1u << (q & 31);
+    };
+    while (p < s1) {
+      const uint64_t q = vs_step(b, p, n, s);
+      if (q == kBad) {
+        if (locked) break;
+        run = 0;                                      // not a boundary after all: next start
+        p = ++start;
+        continue;
+      }
+      if (locked) {
+        mark(p);
+      } else {
+        tent[run++] = p;
+        if (run == kLock) {
+          locked = true;
+          for (int k = 0; k < kLock; ++k) mark(tent[k]);
+        }
+      }
+      p = q;
+    }
+    if (!locked && run > 0 && p >= s1) {               // a short run that reached the chunk end
+      for (int k = 0; k < run; ++k) mark(tent[k]);
+      locked = true;
     }
     while (cw < wend) {
       bits[cw++] = acc;
       acc = 0;
     }
-    exitp[c] = (int64_t)p;                            // -1 = the chain failed
+    exitp[c] = locked && p >= s1 ? (int64_t)p : -1;   // -1 = no run reached the chunk end
   }
 }
 

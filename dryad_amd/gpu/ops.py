@@ -419,6 +419,40 @@ def _scalar_table(vals, dtype, device):
     return DeviceTable.from_columns({"v": torch.tensor(vals, dtype=dtype, device=device)}, Shape("scalar", ["v"]))
 
 
+def op_sequence_equal(op, inputs, v):
+    """SequenceEqual of the two merged inputs (reference SequenceEqual: same length and pairwise
+    Equals in order) on the device: the lengths, then every field compared elementwise after
+    dtype promotion (NaN != NaN, as Python's ==).  Tables with string heaps or different record
+    shapes, and a custom comparer, stay on the host."""
+    if op.get("comparer") is not None or len(inputs) != 2:
+        raise NotTraceable("SequenceEqual with a comparer")
+    a, b = _check(inputs[0]), _check(inputs[1])
+    if a.heap is not None or b.heap is not None or a.strs or b.strs:
+        raise NotTraceable("SequenceEqual over strings")
+    if a.n != b.n:
+        return _scalar_table([False], torch.bool, v.device)
+    if a.n == 0:
+        return _scalar_table([True], torch.bool, v.device)
+    if (a.rows is None) != (b.rows is None):
+        raise NotTraceable("SequenceEqual of differently laid out tables")
+    if a.rows is not None:
+        if a.rows.shape[1] != b.rows.shape[1]:
+            return _scalar_table([False], torch.bool, v.device)
+        eq = torch.equal(a.rows[: a.n], b.rows[: b.n])
+        return _scalar_table([bool(eq)], torch.bool, v.device)
+    fa, fb = list(a.shape.fields), list(b.shape.fields)
+    if a.shape.kind != b.shape.kind or len(fa) != len(fb):
+        raise NotTraceable("SequenceEqual of different record shapes")
+    ok = torch.ones((), dtype=torch.bool, device=v.device)
+    for x, y in zip(fa, fb):
+        cx, cy = a.cols[x][: a.n], b.cols[y][: b.n]
+        if cx.shape[1:] != cy.shape[1:]:
+            return _scalar_table([False], torch.bool, v.device)
+        dt = torch.promote_types(cx.dtype, cy.dtype)
+        ok = ok & (cx.to(dt) == cy.to(dt)).all()
+    return _scalar_table([bool(ok.item())], torch.bool, v.device)
+
+
 def op_count(op, inputs, v):
     t = _check(_one(inputs))
     return _scalar_table([t.n], torch.int64, v.device)

@@ -141,6 +141,7 @@ def block_index_host(data, dtype, block: int = BLOCK):
 
 
 VARSCAN_CHUNK = 4096          # bytes per speculative chain (csrc/kernels/varscan.hip)
+LAST_SCAN: dict = {}          # chunks and whether the last device scan stitched on the device alone
 VARSCAN_MAX_WALK = 1 << 16    # records a chain's exit walk may take before giving up
 
 
@@ -174,7 +175,9 @@ def block_index_device(buf: torch.Tensor, dtype, block: int = BLOCK, chunk: int 
         y = sync[:-1]
         ok = ok & ((y >= 0) & (y < n) & (torch.div(y, C, rounding_mode="floor") ==
                                          torch.arange(1, nch, device=dev))).all()
-    if bool(ok.item()):
+    fast = bool(ok.item())
+    LAST_SCAN.update(chunks=nch, fast=fast)
+    if fast:
         entry = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), sync[:-1]])
         on_path = torch.ones(nch, dtype=torch.uint8, device=dev)
     else:

@@ -62,7 +62,8 @@ def main():
     assert got is not None and got[0] == n_idx and torch.equal(got[1].cpu(), torch.from_numpy(offs)), "boundary mismatch"
     ms = timed(lambda: CD.block_index_device(dbuf, vdt))
     print(f"string boundaries (device, no sidecar): {part.size / 1e9:.1f} GB in {ms:.2f} ms = "
-          f"{part.size / 1e6 / ms:.0f} GB/s (host scan {th * 1e3:.0f} ms = {part.size / 1e9 / th:.1f} GB/s)", flush=True)
+          f"{part.size / 1e6 / ms:.0f} GB/s (host scan {th * 1e3:.0f} ms = {part.size / 1e9 / th:.1f} GB/s) "
+          f"{CD.LAST_SCAN}", flush=True)
     doffs = got[1]
     ms = timed(lambda: CD.decode_var(dbuf, vdt, n_idx, doffs))
     print(f"string decode: {part.size / 1e9:.1f} GB ({n_idx} records) in {ms:.2f} ms = {part.size / 1e6 / ms:.0f} GB/s",

@@ -5,7 +5,7 @@
 //   aligned16 8 lanes per row load the 16-byte-aligned pieces that cover the row (7 or 8 loads,
 //             every piece of the window requested before any is used), the row is shifted into
 //             place in LDS at the output's 100-byte pitch, then stored as contiguous 16-byte words.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc/kernels tools/micro/gather100_ab.hip -o build/gather100_ab
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc/kernels tools/micro/gather100_ab.hip -o tools/micro/bin/gather100_ab
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

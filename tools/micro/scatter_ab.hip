@@ -7,7 +7,7 @@
 //           reset), leader updates the counter.
 // Reports ms per pass and the logical TB/s (8 B read + 8 B written per entry); checks that both
 // variants produce the same permutation.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc/kernels tools/micro/scatter_ab.hip -o build/scatter_ab
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc/kernels tools/micro/scatter_ab.hip -o tools/micro/bin/scatter_ab
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
