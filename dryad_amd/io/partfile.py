@@ -135,9 +135,36 @@ def exists(meta_path: str) -> bool:
     return os.path.exists(meta_path)
 
 
-def delete(meta_path: str):
-    """Delete the table: every partition then the metadata (CheckExistence(deleteIfExists))."""
+def delete(meta_path: str, background: bool = False):
+    """Delete the table: every partition then the metadata (CheckExistence(deleteIfExists)).
+    ``background``: the files are renamed out of the way at once (the table is gone and its
+    names are free for a new one) and unlinked by a daemon thread: unlinking tens of GB of
+    page-cached parts takes seconds the job does not have to wait for."""
     if not os.path.exists(meta_path):
+        return
+    if background:
+        tag = ".deleting-" + uuid.uuid4().hex[:8]
+        moved = []
+        try:
+            meta = read_meta(meta_path)
+            for p in meta.paths():
+                for q in (p, p + INDEX_SUFFIX):
+                    if os.path.exists(q):
+                        os.replace(q, q + tag)
+                        moved.append(q + tag)
+        except Exception:
+            pass
+        os.replace(meta_path, meta_path + tag)
+        moved.append(meta_path + tag)
+
+        def unlink_all():
+            for q in moved:
+                try:
+                    os.remove(q)
+                except OSError:
+                    pass
+        import threading
+        threading.Thread(target=unlink_all, daemon=True, name="dryad-partfile-delete").start()
         return
     try:
         meta = read_meta(meta_path)

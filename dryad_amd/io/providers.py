@@ -96,9 +96,9 @@ class PartfileProvider(DataProvider):
     def exists(self, uri):
         return os.path.exists(self._path(uri))
 
-    def delete(self, uri):
+    def delete(self, uri, background: bool = False):
         path = self._path(uri)
-        PF.delete(path)
+        PF.delete(path, background=background)
         if os.path.exists(path + ".dryadtype"):
             os.remove(path + ".dryadtype")
 

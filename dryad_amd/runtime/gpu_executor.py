@@ -1480,7 +1480,10 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     prov = provider_for(uri)
     if me == 0 and prov.exists(uri):
         if s.output.get("delete_if_exists") or s.output.get("temp"):
-            prov.delete(uri)
+            try:                    # the old parts move aside now and are unlinked in the background
+                prov.delete(uri, background=True)
+            except TypeError:
+                prov.delete(uri)
         else:
             raise DryadLinqException(ErrorCode.JobToCreateTableFailed, f"output {uri} exists")
     if W > 1:
