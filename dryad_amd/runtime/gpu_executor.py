@@ -115,6 +115,19 @@ def _device_bytes(x) -> int:
     return 0
 
 
+def _records(x) -> int:
+    """Records held by an operator argument (a device table, a record list, a ported table)."""
+    if x is None:
+        return 0
+    if isinstance(x, DeviceTable):
+        return x.n
+    if isinstance(x, Ported):
+        return x.table.n
+    if isinstance(x, list):
+        return sum(_records(y) for y in x) if x and isinstance(x[0], (list, DeviceTable)) else len(x)
+    return 1
+
+
 def _rows100_source(uri) -> bool:
     """gen://terasort, or a stored table of raw 100-byte rows (partfile ``format: rows``)."""
     scheme, path, _ = parse_uri(uri)
@@ -154,6 +167,7 @@ class GpuJobRunner:
         self.row_sets: dict = {}          # (stage, partition) -> pooled BufferSet holding its rows
         self.moved: dict = {}             # (stage, partition) -> rank whose duplicate attempt won
         self.stream_plans: dict = {}      # stage -> chunk plan of a streamed stage (None: not streamed)
+        self.empty_host_ops: list = []    # host operators that ran over empty inputs only
         self.stream_stats: dict = {}      # (stage, partition) -> chunks / records / bytes streamed
         self.place = None                 # partition -> rank (None: p % W)
         self.fused: dict = {}             # merge stage id -> fused distributed-OrderBy descriptor
@@ -855,14 +869,19 @@ class GpuJobRunner:
             self._fallback(s, name, "host op" if fn is None or not self.gpu_ok else "host records in", args)
         objs = [(_to_objects(a) if not isinstance(a, list) else a) if a is not None else [] for a in args]
         out = V.OPS[name](op, objs, vctx)
-        self.op_counts[(name, "host")] += 1
+        self.op_counts[(name, "host" if any(_records(a) for a in args) else "host-empty")] += 1
         return self._maybe_device(out, s, name)
 
     def _fallback(self, s, name, why, args):
         """Record a host fallback; refuse one that would pull more than HostFallbackMaxBytes of
         device data into Python objects (a silent cliff on a 100 GB partition) unless the context
-        allows it (AllowHostFallback)."""
+        allows it (AllowHostFallback).  An operator over empty inputs only (no record to process,
+        e.g. a partition a shuffle left empty, whose output type a kernel cannot infer) is noted
+        apart: it moves no data."""
         nb = sum(_device_bytes(a) for a in args)
+        if all(_records(a) == 0 for a in args):
+            self.empty_host_ops.append((s.name, name, why))
+            return
         self.fallbacks.append((s.name, name, why))
         props = self.ctx._props
         if self.gpu_ok and nb > int(props.get("HostFallbackMaxBytes") or 0) and not props.get("AllowHostFallback"):
@@ -1001,6 +1020,7 @@ class GpuJobRunner:
                 self.pool.release(b)
         return dict(committed=committed, fallbacks=self.fallbacks, timings=self.timings, transports=self.transports,
                     op_counts={f"{k[0]}:{k[1]}": v for k, v in self.op_counts.items()},
+                    empty_host_ops=self.empty_host_ops,
                     placement=self.place, moved={f"{k[0]}:{k[1]}": v for k, v in self.moved.items()},
                     write=dict(bytes=self.write_stats.bytes, seconds=round(self.write_stats.seconds, 4)),
                     read=dict(bytes=self.read_stats.bytes, seconds=round(self.read_stats.seconds, 4)),

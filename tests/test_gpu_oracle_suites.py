@@ -34,7 +34,51 @@ def _cases():
 # Host fallbacks a scenario may take on the GPU executor, each with the reason its operator cannot
 # run on the device.  Any other fallback fails the scenario: passing the oracle comparison on a
 # silent host path would not show that the device path works.
+_GROUPING = "a GroupBy without an aggregating result selector yields Grouping objects (the group " \
+            "as a Python sequence), or its selector builds a Python object from the group"
+_USER_AGG = "the aggregate is user Python code (a decomposable class's Seed / Accumulate / " \
+            "RecursiveAccumulate)"
+_TEXT = "the lambda calls Python str methods on the record (indexing, upper(), split())"
+_APPLY = "Apply / ApplyWithPartitionIndex bodies are arbitrary Python over the partition's sequence " \
+         "(only @device_function bodies run on HBM tables)"
+_OBJECTS = "the records are Python objects with nullable / None / nested fields: no column layout"
+_DICT = "the result selector builds a dict / list / nested tuple per record"
+
 ALLOWED_FALLBACKS = {
+    "test_empty_inputs": {"group_by": _GROUPING},
+    "test_user_types_in_query": {"group_by": _GROUPING},
+    "test_DistributiveResultSelector_and_Select": {"group_by": _GROUPING},
+    "test_GroupByReduceWithCustomDecomposableFunction_NonDistributableCombiner": {"group_by": _GROUPING},
+    "test_GroupByReduce_BitwiseNegationOperator": {"group_by": _GROUPING},
+    "test_GroupByWithAnonymousTypes_Pipeline_and_Nested": {"group_by": _GROUPING, "group_partial": _DICT,
+                                                          "select": _DICT},
+    "test_groupby_decomposable_aggregates": {"group_final": _DICT},
+    "test_groupby_with_comparer": {"group_partial": "GroupBy with a user IEqualityComparer (Python Equals)"},
+    "test_user_decomposable": {"group_partial": _USER_AGG},
+    "test_GroupByReduceWithCustomDecomposableFunction_DistributableCombiner_DifferingTypes_NoFinalizer":
+        {"group_partial": _USER_AGG},
+    "test_GroupByReduce_BuiltIn_First": {"group_partial": "First depends on the record order inside a group, "
+                                                          "which the device grouping kernels do not keep"},
+    "test_GroupByReduce_ResultSelector_ComplexNewExpression_and_ListInitializer": {"group_partial": _USER_AGG},
+    "test_GroupByReduce_UseAllInternalDecomposables_and_SameDecomposableUsedTwice": {"group_partial": _USER_AGG},
+    "test_Aggregate_WithCombiner": {"agg_partial": "Aggregate with a user accumulator / combiner function"},
+    "test_groupby_variants": {"group_partial": _TEXT, "hash_partition": _TEXT},
+    "test_GroupByReduce_ProgrammingManualExample": {"group_partial": _TEXT},
+    "test_selectmany_result_selector": {"select_many": _TEXT},
+    "test_hash_partition_overloads": {"apply_index": _APPLY},
+    "test_Bug14192_MultiApplySubExpressionReuse": {"apply": _APPLY},
+    "test_FullHomomorphicBinaryApply_IdenticalDataSets": {"apply": _APPLY},
+    "test_indexed_select_where_selectmany": {"select_many_idx": "indexed SelectMany returning a variable-length Python list"},
+    "test_Bug11638_LongMethods": {"select_many_idx": "indexed SelectMany returning a variable-length Python list"},
+    "test_Bug13529_and_Bug13593_IndexedOperatorCompilation":
+        {"select_many_idx": "indexed SelectMany returning a variable-length Python list"},
+    "test_join_and_groupjoin": {"hash_group_join": "GroupJoin result selector iterates the Python group (len(os))"},
+    "test_Bug15159_NotOperatorForNullableBool": {"enumerable": _OBJECTS,
+                                                 "where": "Python identity comparison (`is None`) on a record"},
+    "test_Bug15570_GetHashCodeAndEqualsForNullableFieldsOfAnonymousTypes": {"enumerable": _OBJECTS},
+    "test_NonSealedTypeRecords_and_DerivedTypeRecords": {"enumerable": _OBJECTS, "group_partial": _OBJECTS,
+                                                         "select": _OBJECTS},
+    "test_ObjectRecords": {"enumerable": _OBJECTS},
 }
 
 _COVERAGE = collections.Counter()      # (operator, "device" | "host") over every scenario
