@@ -170,38 +170,42 @@ def block_index_device(buf: torch.Tensor, dtype, block: int = BLOCK, chunk: int 
     st = stream_of(buf)
     _lib.call("dr_varscan_chains", ptr(buf), c_u64(n), c_u32(C), nf, sizes, ptr(bits), ptr(exitp), ptr(sync),
               c_u32(VARSCAN_MAX_WALK), st)
-    ok = (exitp >= 0).all() & (exitp[-1] == n)
+    # a chunk is "regular" when its chain reached its end and its exit walk met the next chunk's
+    # chain inside that chunk: then the next chunk's true entry is that sync point.  Only the
+    # irregular chunks (normally none) go to the host, which resolves the path around them.
+    good = exitp >= 0
     if nch > 1:
         y = sync[:-1]
-        ok = ok & ((y >= 0) & (y < n) & (torch.div(y, C, rounding_mode="floor") ==
-                                         torch.arange(1, nch, device=dev))).all()
-    fast = bool(ok.item())
-    LAST_SCAN.update(chunks=nch, fast=fast)
-    if fast:
-        entry = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), sync[:-1]])
-        on_path = torch.ones(nch, dtype=torch.uint8, device=dev)
-    else:
-        ex, sy = exitp.cpu().numpy(), sync.cpu().numpy()
-        ent = np.full(nch, -1, dtype=np.int64)
-        on = np.zeros(nch, dtype=np.uint8)
-        c, ent[0] = 0, 0
-        while True:
-            on[c] = 1
-            if ex[c] < 0:
+        good[:-1] &= (y >= 0) & (y < n) & (torch.div(y, C, rounding_mode="floor") ==
+                                           torch.arange(1, nch, device=dev))
+    good[-1:] &= exitp[-1:] == n
+    bad = torch.nonzero(~good).flatten()
+    entry = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), sync[:-1]])
+    on_path = torch.ones(nch, dtype=torch.uint8, device=dev)
+    nbad = int(bad.numel())
+    LAST_SCAN.update(chunks=nch, irregular=nbad, fast=nbad == 0)
+    if nbad:
+        bl = bad.tolist()
+        exb, syb = exitp[bad].tolist(), sync[bad].tolist()
+        covered = 0                                  # chunks below this one are settled
+        for c, e, y in zip(bl, exb, syb):
+            if c < covered:
+                continue                             # off the path: inside an earlier walk
+            if e < 0:                                # the stream is irregular on the path
                 return None
             if c == nch - 1:
-                if ex[c] != n:
+                if e != n:
                     return None
-                break
-            y = int(sy[c])
+                continue
             if y < 0:
                 return None
-            if y == n:
-                break
-            k = y // C
-            ent[k], c = y, k
-        entry = torch.from_numpy(ent).to(dev)
-        on_path = torch.from_numpy(on).to(dev)
+            k = nch if y == n else y // C            # the walk ran to chunk k (or to the end)
+            if k > c + 1:
+                entry[c + 1:k] = -1
+                on_path[c + 1:k] = 0
+            if k < nch:
+                entry[k] = y
+            covered = k
     cnt = torch.zeros(nch, dtype=torch.int64, device=dev)
     _lib.call("dr_varscan_fix", ptr(buf), c_u64(n), c_u32(C), nf, sizes, ptr(entry), ptr(on_path), ptr(exitp),
               ptr(sync), ptr(bits), ptr(cnt), st)
