@@ -145,7 +145,8 @@ LAST_SCAN: dict = {}          # chunks and whether the last device scan stitched
 VARSCAN_MAX_WALK = 1 << 16    # records a chain's exit walk may take before giving up
 
 
-def block_index_device(buf: torch.Tensor, dtype, block: int = BLOCK, chunk: int = VARSCAN_CHUNK):
+def block_index_device(buf: torch.Tensor, dtype, block: int = BLOCK, chunk: int = VARSCAN_CHUNK,
+                       debug: dict | None = None):
     """(records, int64 device offsets of every ``block``-th record) of a part in HBM, found on
     the device by speculative per-chunk parses stitched at their sync points
     (csrc/kernels/varscan.hip), or None when the stream is irregular there (a walk that never
@@ -180,15 +181,18 @@ def block_index_device(buf: torch.Tensor, dtype, block: int = BLOCK, chunk: int 
                                            torch.arange(1, nch, device=dev))
     good[-1:] &= exitp[-1:] == n
     bad = torch.nonzero(~good).flatten()
+    if debug is not None:
+        debug.update(exitp=exitp.clone(), sync=sync.clone(), bits=bits.clone(), good=good.clone())
     entry = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), sync[:-1]])
     on_path = torch.ones(nch, dtype=torch.uint8, device=dev)
     nbad = int(bad.numel())
     LAST_SCAN.update(chunks=nch, irregular=nbad, fast=nbad == 0)
     if nbad:
-        bl = bad.tolist()
-        exb, syb = exitp[bad].tolist(), sync[bad].tolist()
+        bl = bad.cpu().numpy()
+        exb, syb = exitp[bad].cpu().numpy(), sync[bad].cpu().numpy()
         covered = 0                                  # chunks below this one are settled
-        for c, e, y in zip(bl, exb, syb):
+        off, ek, ev = [], [], []                     # off-path chunk ranges, entry overrides
+        for c, e, y in zip(bl.tolist(), exb.tolist(), syb.tolist()):
             if c < covered:
                 continue                             # off the path: inside an earlier walk
             if e < 0:                                # the stream is irregular on the path
@@ -201,11 +205,17 @@ def block_index_device(buf: torch.Tensor, dtype, block: int = BLOCK, chunk: int 
                 return None
             k = nch if y == n else y // C            # the walk ran to chunk k (or to the end)
             if k > c + 1:
-                entry[c + 1:k] = -1
-                on_path[c + 1:k] = 0
+                off.append(np.arange(c + 1, k, dtype=np.int64))
             if k < nch:
-                entry[k] = y
+                ek.append(k)
+                ev.append(y)
             covered = k
+        if off:
+            oi = torch.from_numpy(np.concatenate(off)).to(dev)
+            entry[oi] = -1
+            on_path[oi] = 0
+        if ek:
+            entry[torch.tensor(ek, device=dev)] = torch.tensor(ev, dtype=torch.int64, device=dev)
     cnt = torch.zeros(nch, dtype=torch.int64, device=dev)
     _lib.call("dr_varscan_fix", ptr(buf), c_u64(n), c_u32(C), nf, sizes, ptr(entry), ptr(on_path), ptr(exitp),
               ptr(sync), ptr(bits), ptr(cnt), st)
