@@ -44,13 +44,13 @@ __global__ void excl(uint32_t* c) {
   c[threadIdx.x] = block_exclusive_scan256(c[threadIdx.x], sc, tot);
 }
 
-template <int ITEMS, bool BALLOT>
+template <int ITEMS, bool BALLOT, bool DIRECT = false>
 __global__ __launch_bounds__(256) void scatter(const E64* __restrict__ in, E64* __restrict__ out, uint64_t n, int shift,
                                                const uint32_t* __restrict__ gbase, unsigned long long* granules,
                                                uint32_t* ticket, uint32_t tiles) {
   constexpr int kTile = kBlock * ITEMS;
   constexpr uint32_t tag_agg = 2, tag_inc = 3;
-  __shared__ E64 stage[kTile];
+  __shared__ E64 stage[DIRECT ? 1 : kTile];
   __shared__ uint32_t wcnt[4][kBins];
   __shared__ unsigned long long wmask[BALLOT ? 1 : 4][kBins];
   __shared__ uint32_t bstart[kBins];
@@ -115,10 +115,12 @@ __global__ __launch_bounds__(256) void scatter(const E64* __restrict__ in, E64* 
   uint32_t all;
   bstart[t] = block_exclusive_scan256(tot, sc, all);
   __syncthreads();
+  if constexpr (!DIRECT) {
 #pragma unroll
-  for (int r = 0; r < ITEMS; ++r) {
-    const uint32_t pos = w * (kTile / 4) + r * 64 + l;
-    if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+      if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
+    }
   }
   uint32_t ex = 0;
   if (tile > 0) {
@@ -153,11 +155,20 @@ __global__ __launch_bounds__(256) void scatter(const E64* __restrict__ in, E64* 
   }
   goff[t] = gbase[t] + ex;
   __syncthreads();
+  if constexpr (DIRECT) {
+    // no LDS reorder: every entry stored from its register to its final place
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+      if (pos < cnt) out[(uint64_t)goff[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
+    }
+  } else {
 #pragma unroll 4
-  for (uint32_t j = t; j < cnt; j += kBlock) {
-    const E64 v = stage[j];
-    const uint32_t d = dig(v, shift);
-    out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+    for (uint32_t j = t; j < cnt; j += kBlock) {
+      const E64 v = stage[j];
+      const uint32_t d = dig(v, shift);
+      out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+    }
   }
 }
 
@@ -178,7 +189,7 @@ __global__ void diff(const E64* a, const E64* b, uint64_t n, unsigned long long*
     }                                                                      \
   } while (0)
 
-template <int ITEMS, bool BALLOT>
+template <int ITEMS, bool BALLOT, bool DIRECT = false>
 static float run(const E64* in, E64* out, uint64_t n, int shift, const uint32_t* gbase, void* ws, size_t ws_bytes) {
   const uint64_t tile = 256ull * ITEMS, tiles = (n + tile - 1) / tile;
   float best = 1e9f;
@@ -188,7 +199,7 @@ static float run(const E64* in, E64* out, uint64_t n, int shift, const uint32_t*
   for (int it = 0; it < 4; ++it) {
     HC(hipMemset(ws, 0, ws_bytes));
     HC(hipEventRecord(a));
-    scatter<ITEMS, BALLOT><<<(unsigned)tiles, 256>>>(in, out, n, shift, gbase,
+    scatter<ITEMS, BALLOT, DIRECT><<<(unsigned)tiles, 256>>>(in, out, n, shift, gbase,
                                                      reinterpret_cast<unsigned long long*>((char*)ws + 256),
                                                      reinterpret_cast<uint32_t*>(ws), (uint32_t)tiles);
     HC(hipEventRecord(b));
@@ -229,6 +240,14 @@ int main(int argc, char** argv) {
   unsigned long long hb = 0;
   HC(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
   std::printf("mismatches lds vs ballot: %llu\n", hb);
+  ms = run<32, false, true>(in, o2, n, shift, gbase, ws, ws_bytes);
+  std::printf("direct items=32 (no LDS reorder): %.3f ms  %.2f TB/s\n", ms, gb / ms);
+  HC(hipMemset(bad, 0, 8));
+  diff<<<4096, 256>>>(o1, o2, n, bad);
+  HC(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
+  std::printf("mismatches lds vs direct: %llu\n", hb);
+  ms = run<16, false, true>(in, o2, n, shift, gbase, ws, ws_bytes);
+  std::printf("direct items=16: %.3f ms  %.2f TB/s\n", ms, gb / ms);
   ms = run<24, true>(in, o2, n, shift, gbase, ws, ws_bytes);
   std::printf("ballot items=24: %.3f ms  %.2f TB/s\n", ms, gb / ms);
   ms = run<16, true>(in, o2, n, shift, gbase, ws, ws_bytes);

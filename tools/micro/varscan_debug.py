@@ -23,19 +23,19 @@ def step(b, p, n, sizes):
             continue
         if p >= n:
             return BAD
-        u = b[p]
+        u = int(b[p])
         if u < 0x80:
             p += 1
         else:
             if p + 4 > n:
                 return BAD
-            u = ((u & 0x7f) << 24) | (b[p + 1] << 16) | (b[p + 2] << 8) | b[p + 3]
+            u = ((u & 0x7f) << 24) | (int(b[p + 1]) << 16) | (int(b[p + 2]) << 8) | int(b[p + 3])
             if u < 0x80:
                 return BAD
             p += 4
         if p >= n:
             return BAD
-        nb = b[p]
+        nb = int(b[p])
         wide = (u + 1) * 3 >= 0x80
         if nb < 0x80:
             if wide:
@@ -44,7 +44,7 @@ def step(b, p, n, sizes):
         else:
             if not wide or p + 4 > n:
                 return BAD
-            nb = ((nb & 0x7f) << 24) | (b[p + 1] << 16) | (b[p + 2] << 8) | b[p + 3]
+            nb = ((nb & 0x7f) << 24) | (int(b[p + 1]) << 16) | (int(b[p + 2]) << 8) | int(b[p + 3])
             p += 4
         if nb < u or nb > 3 * u:
             return BAD
@@ -85,7 +85,8 @@ def main():
     recs = [(i, "".join(alpha[j] for j in rng.integers(0, 26, size=int(rng.integers(12, 41)))), i * 0.5)
             for i in range(200_000)]
     blob = np.frombuffer(B.encode_records(vdt, recs), dtype=np.uint8)
-    part = np.tile(blob, 4)
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    part = np.tile(blob, reps)
     buf = torch.from_numpy(part).cuda()
     dbg = {}
     got = CD.block_index_device(buf, vdt, debug=dbg)
@@ -94,13 +95,20 @@ def main():
     sy = dbg["sync"].cpu().numpy()
     bits = dbg["bits"].cpu().numpy().view(np.uint32)
     good = dbg["good"].cpu().numpy()
-    b = part.tolist()
-    n = len(b)
+    n = len(part)
+    b = part                                             # numpy indexing: no list of 10e9 ints
     C = CD.VARSCAN_CHUNK
     bad_idx = np.nonzero(~good)[0]
     print("irregular chunks:", len(bad_idx), "first:", bad_idx[:20].tolist())
+    if len(bad_idx):
+        exb, syb = ex[bad_idx], sy[bad_idx]
+        far = (syb >= 0) & (syb // C != bad_idx + 1)
+        print("  exit < 0:", int((exb < 0).sum()), " sync < 0:", int(((exb >= 0) & (syb < 0)).sum()),
+              " sync past the next chunk:", int(far.sum()))
+        print("  irregular chunk positions (bytes):", (bad_idx[:10] * C).tolist())
     mism = 0
     for c in list(range(0, 40)) + bad_idx[:10].tolist():
+        c = int(c)
         e, pos = chain(b, n, c, C, [8, 0, 8])
         w0, w1 = (c * C) >> 5, (min(c * C + C, n) + 31) >> 5
         dev = [((w << 5) + k) for w in range(w0, w1) for k in range(32) if (bits[w] >> k) & 1]
