@@ -74,12 +74,14 @@ __device__ __forceinline__ bool vs_bit(const uint32_t* __restrict__ bits, uint64
   return (bits[p >> 5] >> (p & 31)) & 1u;
 }
 
-// A chain locks onto the stream once kLock records in a row parse; until then a failed parse
-// restarts it one byte after the previous start (and forgets the positions of that attempt), so
-// a chunk whose start is not a boundary still finds one and follows the stream from there (the
-// exit walks of the previous chunk then meet it within the chunk).  A locked chain that fails
-// stops: it was not on the stream.
-constexpr int kLock = 4;
+// A chain locks onto the stream once kLock records in a row parse, each shorter than the chunk;
+// until then a failed (or implausibly long) parse restarts it one byte after the previous start
+// (and forgets the positions of that attempt), so a chunk whose start is not a boundary still
+// finds one and follows the stream from there (the exit walks of the previous chunk then meet it
+// within the chunk).  The length bound matters in large parts: a misaligned 4-byte length there
+// can land gigabytes ahead and still inside the part.  A locked chain that fails stops: it was
+// not on the stream.  (A false lock only costs speed: the walks step over it.)
+constexpr int kLock = 6;
 
 __global__ __launch_bounds__(256) void vs_chain(const uint8_t* __restrict__ b, uint64_t n, uint32_t C, uint64_t nch,
                                                 VSchema s, uint32_t* __restrict__ bits, int64_t* __restrict__ exitp) {
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(256) void vs_chain(const uint8_t* __restrict__ b, u
     };
     while (p < s1) {
       const uint64_t q = vs_step(b, p, n, s);
-      if (q == kBad) {
+      if (q == kBad || (!locked && q - p > C)) {
         if (locked) break;
         run = 0;                                      // not a boundary after all: next start
         p = ++start;

@@ -13,7 +13,7 @@ from dryad_amd.io import binary as B  # noqa: E402
 from dryad_amd.ops import codec as CD  # noqa: E402
 
 BAD = -1
-K = 4
+K = 6
 
 
 def step(b, p, n, sizes):
@@ -58,7 +58,7 @@ def chain(b, n, c, C, sizes):
     pos = []
     while p < s1:
         q = step(b, p, n, sizes)
-        if q == BAD:
+        if q == BAD or (not locked and q - p > C):
             if locked:
                 break
             run, start = [], start + 1
@@ -118,6 +118,23 @@ def main():
             print(f"chunk {c}: cpu exit {e} dev exit {ex[c]} sync {sy[c]}; cpu {len(pos)} positions {pos[:6]}, "
                   f"dev {len(dev)} positions {dev[:6]}")
     print("mismatching chunks:", mism)
+    # the exit walks of the first irregular chunks, redone on the host over the device's bits
+    for c in bad_idx[:8].tolist():
+        p, k, y = int(ex[c]), 0, BAD
+        while p != BAD:
+            if p >= n:
+                y = n if p == n else BAD
+                break
+            if (int(bits[p >> 5]) >> (p & 31)) & 1:
+                y = p
+                break
+            k += 1
+            if k > 70000:
+                y = -2
+                break
+            p = step(b, p, n, [8, 0, 8])
+        print(f"walk of chunk {c}: host sync {y} (chunk {y // C if y >= 0 else None}, {k} steps), device sync {sy[c]}, "
+              f"exit {ex[c]}")
 
 
 if __name__ == "__main__":
