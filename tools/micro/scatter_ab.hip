@@ -44,10 +44,10 @@ __global__ void excl(uint32_t* c) {
   c[threadIdx.x] = block_exclusive_scan256(c[threadIdx.x], sc, tot);
 }
 
-template <int ITEMS, bool BALLOT, bool DIRECT = false>
+template <int ITEMS, bool BALLOT, bool DIRECT = false, int MODE = 0>
 __global__ __launch_bounds__(256) void scatter(const E64* __restrict__ in, E64* __restrict__ out, uint64_t n, int shift,
                                                const uint32_t* __restrict__ gbase, unsigned long long* granules,
-                                               uint32_t* ticket, uint32_t tiles) {
+                                               uint32_t* ticket, uint32_t tiles, const uint32_t* toff = nullptr) {
   constexpr int kTile = kBlock * ITEMS;
   constexpr uint32_t tag_agg = 2, tag_inc = 3;
   __shared__ E64 stage[DIRECT ? 1 : kTile];
@@ -81,6 +81,11 @@ __global__ __launch_bounds__(256) void scatter(const E64* __restrict__ in, E64* 
     const bool valid = pos < cnt;
     const uint32_t d = valid ? dig(cur[r], shift) : 0u;
     unsigned long long peers;
+    if constexpr (MODE == 1) {      // timing only: one returning LDS atomic per item (unstable order)
+      rk[r] = valid ? atomicAdd(&wcnt[w][d], 1u) : 0u;
+      dg[r] = d;
+      continue;
+    }
     if constexpr (BALLOT) {
       peers = __ballot(valid);
 #pragma unroll
@@ -123,7 +128,9 @@ __global__ __launch_bounds__(256) void scatter(const E64* __restrict__ in, E64* 
     }
   }
   uint32_t ex = 0;
-  if (tile > 0) {
+  if (MODE == 2) {
+    ex = toff[(uint64_t)tile * kBins + t];        // offsets computed beforehand: no look-back
+  } else if (tile > 0) {
     uint64_t j = tile;
     for (;;) {
       unsigned long long g[4];
@@ -307,6 +314,26 @@ __global__ __launch_bounds__(256) void scatter_dual(const E64* __restrict__ in, 
   }
 }
 
+// per-tile digit counts (8192-entry tiles) and their exclusive prefix over tiles, per digit
+__global__ void tile_hist(const E64* x, uint64_t n, int shift, uint32_t* th) {
+  __shared__ uint32_t h[kBins];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t b0 = (uint64_t)blockIdx.x * 8192, b1 = b0 + 8192 < n ? b0 + 8192 : n;
+  for (uint64_t i = b0 + threadIdx.x; i < b1; i += 256) atomicAdd(&h[dig(x[i], shift)], 1u);
+  __syncthreads();
+  th[(uint64_t)blockIdx.x * kBins + threadIdx.x] = h[threadIdx.x];
+}
+
+__global__ void tile_scan(uint32_t* th, uint64_t tiles) {       // one thread per digit
+  uint32_t acc = 0;
+  for (uint64_t t = 0; t < tiles; ++t) {
+    const uint32_t v = th[t * kBins + threadIdx.x];
+    th[t * kBins + threadIdx.x] = acc;
+    acc += v;
+  }
+}
+
 __global__ void diff(const E64* a, const E64* b, uint64_t n, unsigned long long* bad) {
   uint32_t k = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
@@ -398,6 +425,43 @@ int main(int argc, char** argv) {
     diff<<<4096, 256>>>(o1, o2, n, bad);
     HC(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
     std::printf("mismatches lds vs dual: %llu\n", hb);
+  }
+  {
+    const uint64_t tl = 256ull * 32, tiles = (n + tl - 1) / tl;
+    uint32_t* toff;
+    HC(hipMalloc(&toff, tiles * kBins * 4));
+    tile_hist<<<(unsigned)tiles, 256>>>(in, n, shift, toff);
+    tile_scan<<<1, 256>>>(toff, tiles);
+    HC(hipDeviceSynchronize());
+    hipEvent_t a, b;
+    HC(hipEventCreate(&a));
+    HC(hipEventCreate(&b));
+    for (int mode = 1; mode <= 2; ++mode) {
+      float best = 1e9f;
+      for (int it = 0; it < 4; ++it) {
+        HC(hipMemset(ws, 0, ws_bytes));
+        HC(hipEventRecord(a));
+        auto* g = reinterpret_cast<unsigned long long*>((char*)ws + 256);
+        auto* tk = reinterpret_cast<uint32_t*>(ws);
+        if (mode == 1)
+          scatter<32, false, false, 1><<<(unsigned)tiles, 256>>>(in, o2, n, shift, gbase, g, tk, (uint32_t)tiles, toff);
+        else
+          scatter<32, false, false, 2><<<(unsigned)tiles, 256>>>(in, o2, n, shift, gbase, g, tk, (uint32_t)tiles, toff);
+        HC(hipEventRecord(b));
+        HC(hipEventSynchronize(b));
+        float t_;
+        HC(hipEventElapsedTime(&t_, a, b));
+        if (it > 0 && t_ < best) best = t_;
+      }
+      std::printf("%s: %.3f ms  %.2f TB/s\n", mode == 1 ? "atomic ranks, unstable (timing only)" : "offsets precomputed (no look-back)",
+                  best, gb / best);
+      if (mode == 2) {
+        HC(hipMemset(bad, 0, 8));
+        diff<<<4096, 256>>>(o1, o2, n, bad);
+        HC(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
+        std::printf("mismatches lds vs precomputed: %llu\n", hb);
+      }
+    }
   }
   ms = run<24, true>(in, o2, n, shift, gbase, ws, ws_bytes);
   std::printf("ballot items=24: %.3f ms  %.2f TB/s\n", ms, gb / ms);
