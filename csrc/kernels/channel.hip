@@ -29,7 +29,16 @@ struct PcCols {
   uint32_t ncols;
 };
 
-__global__ __launch_bounds__(256) void pc_count_kernel(const E128* __restrict__ ent, uint64_t n,
+// A row's bucket: the low byte of its E128 entry's hi word, or its byte of a uint8 port array
+// (PORT8: the hash partitioner's compact form, 1 byte per row instead of 16).
+template <bool PORT8>
+__device__ __forceinline__ uint32_t pc_port(const void* __restrict__ ent, uint64_t i) {
+  if constexpr (PORT8) return static_cast<const uint8_t*>(ent)[i];
+  else return (uint32_t)(static_cast<const E128*>(ent)[i].hi & 0xFF);
+}
+
+template <bool PORT8>
+__global__ __launch_bounds__(256) void pc_count_kernel(const void* __restrict__ ent, uint64_t n,
                                                        const uint8_t* __restrict__ lut, uint32_t* __restrict__ counts,
                                                        uint32_t G, uint64_t per_block) {
   __shared__ uint32_t hist[256];
@@ -40,7 +49,7 @@ __global__ __launch_bounds__(256) void pc_count_kernel(const E128* __restrict__ 
   __syncthreads();
   const uint64_t beg = (uint64_t)blockIdx.x * per_block;
   const uint64_t end = beg + per_block < n ? beg + per_block : n;
-  for (uint64_t i = beg + t; i < end; i += kBlock) atomicAdd(&hist[slut[ent[i].hi & 0xFF]], 1u);
+  for (uint64_t i = beg + t; i < end; i += kBlock) atomicAdd(&hist[slut[pc_port<PORT8>(ent, i)]], 1u);
   __syncthreads();
   counts[(uint64_t)t * G + blockIdx.x] = hist[t];
 }
@@ -54,7 +63,8 @@ __device__ __forceinline__ void pc_store_narrow(uint8_t* p, uint64_t row, uint32
   else reinterpret_cast<uint16_t*>(p)[row] = (uint16_t)v;
 }
 
-__global__ __launch_bounds__(256) void pc_scatter_kernel(const E128* __restrict__ ent, uint64_t n,
+template <bool PORT8>
+__global__ __launch_bounds__(256) void pc_scatter_kernel(const void* __restrict__ ent, uint64_t n,
                                                          const uint8_t* __restrict__ lut, PcCols cols,
                                                          const int64_t* __restrict__ offsets, uint32_t G,
                                                          uint64_t per_block) {
@@ -82,7 +92,7 @@ __global__ __launch_bounds__(256) void pc_scatter_kernel(const E128* __restrict_
     for (int r = 0; r < kPcItems; ++r) {
       const uint32_t pos = w * (kPcTile / 4) + r * 64 + l;
       const bool valid = pos < cnt;
-      const uint32_t d = valid ? (uint32_t)slut[ent[base + pos].hi & 0xFF] : 0u;
+      const uint32_t d = valid ? (uint32_t)slut[pc_port<PORT8>(ent, base + pos)] : 0u;
       uint64_t peers = ballot64(valid);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -237,19 +247,23 @@ DR_API uint32_t dr_pc_grid(uint64_t n, uint64_t* per_block) {
   return (uint32_t)G;
 }
 
-DR_API int dr_pc_count(const E128* ent, uint64_t n, const uint8_t* lut, uint32_t* counts, uint32_t G,
-                       uint64_t per_block, hipStream_t s) {
+// ent: E128 entries (port8 = 0) or a uint8 port per row (port8 = 1).
+DR_API int dr_pc_count(const void* ent, uint64_t n, const uint8_t* lut, uint32_t* counts, uint32_t G,
+                       uint64_t per_block, int port8, hipStream_t s) {
   if (n == 0) return 0;
-  pc_count_kernel<<<G, 256, 0, s>>>(ent, n, lut, counts, G, per_block);
+  if (port8)
+    pc_count_kernel<true><<<G, 256, 0, s>>>(ent, n, lut, counts, G, per_block);
+  else
+    pc_count_kernel<false><<<G, 256, 0, s>>>(ent, n, lut, counts, G, per_block);
   DR_LAUNCH_CHECK();
   return 0;
 }
 
 // offsets: int64 [256 * G], exclusive prefix of the bucket-major counts (destination row of each
 // workgroup's first row of each bucket).  in/out/width: ncols (<= 16) device columns.
-DR_API int dr_pc_scatter(const E128* ent, uint64_t n, const uint8_t* lut, const void* const* in, void* const* out,
+DR_API int dr_pc_scatter(const void* ent, uint64_t n, const uint8_t* lut, const void* const* in, void* const* out,
                          const uint32_t* width, uint32_t ncols, const int64_t* offsets, uint32_t G, uint64_t per_block,
-                         hipStream_t s) {
+                         int port8, hipStream_t s) {
   if (ncols > (uint32_t)kPcMaxCols || n >= (1ull << 40)) return (int)hipErrorInvalidValue;
   if (n == 0 || ncols == 0) return 0;
   PcCols c;
@@ -261,7 +275,10 @@ DR_API int dr_pc_scatter(const E128* ent, uint64_t n, const uint8_t* lut, const 
     c.width[k] = wb;
   }
   c.ncols = ncols;
-  pc_scatter_kernel<<<G, 256, 0, s>>>(ent, n, lut, c, offsets, G, per_block);
+  if (port8)
+    pc_scatter_kernel<true><<<G, 256, 0, s>>>(ent, n, lut, c, offsets, G, per_block);
+  else
+    pc_scatter_kernel<false><<<G, 256, 0, s>>>(ent, n, lut, c, offsets, G, per_block);
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -88,7 +88,8 @@ __device__ __forceinline__ uint64_t hash_one(const HashCol& c, uint64_t i) {
 }
 
 __global__ __launch_bounds__(256) void stable_hash_dest_kernel(HashSpec spec, uint64_t n, uint32_t nparts,
-                                                               E128* __restrict__ out, int64_t* __restrict__ hout) {
+                                                               E128* __restrict__ out, int64_t* __restrict__ hout,
+                                                               uint8_t* __restrict__ pout) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t h;
     if (spec.tuple_form) {
@@ -104,17 +105,20 @@ __global__ __launch_bounds__(256) void stable_hash_dest_kernel(HashSpec spec, ui
       e.hi = (nparts ? (h & 0x7FFFFFFFull) % nparts : 0);
       out[i] = e;
     }
+    if (pout) pout[i] = (uint8_t)(nparts ? (h & 0x7FFFFFFFull) % nparts : 0);
   }
 }
 
 }  // namespace
 
 // kinds/ptrs describe up to 8 key columns (see HashCol); nparts = 0 only returns the hashes.
+// out: E128 {row, port} entries; pout (nparts <= 256): one port byte per row; either may be null.
 DR_API int dr_stable_hash_dest(const int* kinds, const void* const* ptrs, const int64_t* const* offs,
                                const int64_t* const* lens, const uint32_t* strides, const uint32_t* boffs,
                                const uint32_t* blens, int ncols, int tuple_form, uint64_t n, uint32_t nparts,
-                               E128* out, int64_t* hout, hipStream_t s) {
+                               E128* out, int64_t* hout, uint8_t* pout, hipStream_t s) {
   if (ncols < 1 || ncols > kMaxHashCols || (!tuple_form && ncols != 1)) return (int)hipErrorInvalidValue;
+  if (pout && (nparts == 0 || nparts > 256)) return (int)hipErrorInvalidValue;
   if (nparts > 0x7FFFFFFFu) return (int)hipErrorInvalidValue;
   HashSpec spec{};
   for (int c = 0; c < ncols; ++c) {
@@ -132,7 +136,7 @@ DR_API int dr_stable_hash_dest(const int* kinds, const void* const* ptrs, const 
   spec.ncols = ncols;
   spec.tuple_form = tuple_form;
   if (n == 0) return 0;
-  stable_hash_dest_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(spec, n, nparts, out, hout);
+  stable_hash_dest_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(spec, n, nparts, out, hout, pout);
   DR_LAUNCH_CHECK();
   return 0;
 }

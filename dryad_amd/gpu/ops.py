@@ -621,7 +621,9 @@ def op_hash_partition(op, inputs, v):
         return Ported(t, [0] * (n + 1))
     if n <= 256 and t.n < (1 << 32):
         keys, tup = hash_keys(t, op["key"])
-        e, _ = R.stable_hash_dest(keys, t.n, n, tup, t.device)
+        # one port byte per row (not 16-byte entries): the partition pass reads 1 B/row of
+        # destinations and the temporaries of a shuffle shrink by 15 B/row
+        e, _ = R.stable_hash_dest(keys, t.n, n, tup, t.device, ports=t.device.type == "cuda")
         out = partition_by_entries(t, e, n, v.world.size, _dest_place(v))
         if out is not None:
             return out

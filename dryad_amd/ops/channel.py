@@ -16,9 +16,9 @@ from ._lib import c_u32, c_u64, vp
 
 _lib.register_signatures({
     "dr_pc_grid": (c_u32, [c_u64, ctypes.POINTER(c_u64)]),
-    "dr_pc_count": (ctypes.c_int, [vp, c_u64, vp, vp, c_u32, c_u64, vp]),
+    "dr_pc_count": (ctypes.c_int, [vp, c_u64, vp, vp, c_u32, c_u64, ctypes.c_int, vp]),
     "dr_pc_scatter": (ctypes.c_int, [vp, c_u64, vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(c_u32),
-                                     c_u32, vp, c_u32, c_u64, vp]),
+                                     c_u32, vp, c_u32, c_u64, ctypes.c_int, vp]),
     "dr_copy_segments": (ctypes.c_int, [vp, vp, vp, vp, c_u64, vp, vp]),
     "dr_copy_wide": (ctypes.c_int, [vp, vp, c_u64, c_u32, vp]),
 })
@@ -44,11 +44,18 @@ def kernel_ok(cols: list) -> bool:
     return True
 
 
+def _ports(ent: torch.Tensor, n: int) -> torch.Tensor:
+    """Bucket of each row: ``ent`` is E128 entries ([n, 2] int64, port in the low byte of [:, 1])
+    or one uint8 port per row (the hash partitioner's compact form)."""
+    return ent[:n].to(torch.int64) if ent.dtype == torch.uint8 else ent[:n, 1] & 0xFF
+
+
 def bucket_counts(ent: torch.Tensor, n: int, lut: torch.Tensor | None):
-    """Rows per bucket (256 buckets: low byte of ent[:, 1] mapped through ``lut``) -> int64 [256] on
-    the host, plus the device-side workgroup offsets the scatter needs."""
+    """Rows per bucket (256 buckets: the row's port mapped through ``lut``) -> int64 [256] on the
+    host, plus the device-side workgroup offsets the scatter needs.  ``ent``: E128 entries or
+    uint8 ports."""
     if not ent.is_cuda:
-        d = ent[:n, 1] & 0xFF
+        d = _ports(ent, n)
         if lut is not None:
             d = lut.to(torch.int64)[d]
         return torch.bincount(d, minlength=256)[:256], None
@@ -57,7 +64,7 @@ def bucket_counts(ent: torch.Tensor, n: int, lut: torch.Tensor | None):
     counts = torch.zeros(256 * G, dtype=torch.int32, device=ent.device)
     st = _lib.stream_of(ent)
     _lib.call("dr_pc_count", _lib.ptr(ent), c_u64(n), _lib.ptr(lut) if lut is not None else None, _lib.ptr(counts),
-              c_u32(G), pb, st)
+              c_u32(G), pb, int(ent.dtype == torch.uint8), st)
     c64 = counts.to(torch.int64)
     del counts
     offs = torch.cumsum(c64, 0)
@@ -67,12 +74,13 @@ def bucket_counts(ent: torch.Tensor, n: int, lut: torch.Tensor | None):
 
 def scatter_columns(ent: torch.Tensor, n: int, cols: list, lut: torch.Tensor | None = None):
     """Stable partition of the first ``n`` rows of ``cols`` by bucket -> (new columns, int64 [256]
-    rows per bucket).  Bucket of row i = lut[ent[i, 1] & 0xFF] (identity without a LUT)."""
+    rows per bucket).  Bucket of row i = lut[port of row i] (identity without a LUT); ``ent``:
+    E128 entries (port = ent[i, 1] & 0xFF) or uint8 ports."""
     outs = [torch.empty_like(c[:n]) for c in cols]
     if n == 0:
         return outs, torch.zeros(256, dtype=torch.int64)
     if not ent.is_cuda:
-        d = ent[:n, 1] & 0xFF
+        d = _ports(ent, n)
         if lut is not None:
             d = lut.to(torch.int64)[d]
         order = torch.sort(d, stable=True).indices
@@ -86,7 +94,7 @@ def scatter_columns(ent: torch.Tensor, n: int, cols: list, lut: torch.Tensor | N
     ous = (vp * k)(*[o.data_ptr() for o in outs])
     ws = (c_u32 * k)(*[col_width(c) for c in cols])
     _lib.call("dr_pc_scatter", _lib.ptr(ent), c_u64(n), _lib.ptr(lut) if lut is not None else None, ins, ous, ws,
-              c_u32(k), _lib.ptr(offs), c_u32(G), c_u64(pb), _lib.stream_of(ent))
+              c_u32(k), _lib.ptr(offs), c_u32(G), c_u64(pb), int(ent.dtype == torch.uint8), _lib.stream_of(ent))
     return outs, tot
 
 

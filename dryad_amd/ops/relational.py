@@ -475,7 +475,7 @@ def hash_aggregate(key: torch.Tensor, specs: list, capacity: int | None = None):
 _lib.register_signatures({
     "dr_stable_hash_dest": (c_i32, [ctypes.POINTER(c_i32), ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
                                     ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), c_i32, c_i32,
-                                    c_u64, c_u32, vp, vp, vp]),
+                                    c_u64, c_u32, vp, vp, vp, vp]),
 })
 
 H_BYTES, H_STR = 20, 21
@@ -511,10 +511,11 @@ class HashKey:
 
 
 def stable_hash_dest(keys: list, n: int, nparts: int, tuple_form: bool, device,
-                     want_hash: bool = False):
+                     want_hash: bool = False, ports: bool = False):
     """Destination partition of every record under the host partitioner hash
     (runtime/vertex_ops.stable_hash): -> (E128 entries {lo = row, hi = port} or None,
-    int64 hashes or None).  ``tuple_form``: the key is a tuple/record of ``keys``."""
+    int64 hashes or None).  ``tuple_form``: the key is a tuple/record of ``keys``.  ``ports``
+    (nparts <= 256): one uint8 port per row instead of the 16-byte entries."""
     if not keys or len(keys) > MAX_HASH_COLS or (not tuple_form and len(keys) != 1):
         raise ValueError("stable_hash_dest: 1..8 key fields (exactly 1 unless tuple_form)")
     if n >= (1 << 32):
@@ -527,12 +528,15 @@ def stable_hash_dest(keys: list, n: int, nparts: int, tuple_form: bool, device,
     strides = (c_u32 * k)(*[x.stride for x in keys])
     boffs = (c_u32 * k)(*[x.boff for x in keys])
     blens = (c_u32 * k)(*[x.blen for x in keys])
-    ent = torch.empty((n, 2), dtype=torch.int64, device=device) if nparts else None
+    if ports and not 0 < nparts <= 256:
+        raise ValueError("stable_hash_dest: uint8 ports need 1..256 partitions")
+    ent = torch.empty((n, 2), dtype=torch.int64, device=device) if nparts and not ports else None
+    pt = torch.empty(n, dtype=torch.uint8, device=device) if ports else None
     hs = torch.empty(n, dtype=torch.int64, device=device) if want_hash else None
     _lib.call("dr_stable_hash_dest", kinds, ptrs, offs, lens, strides, boffs, blens, k, int(bool(tuple_form)),
               c_u64(n), c_u32(nparts), ptr(ent) if ent is not None else None,
-              ptr(hs) if hs is not None else None, stream_of(keys[0].t))
-    return ent, hs
+              ptr(hs) if hs is not None else None, ptr(pt) if pt is not None else None, stream_of(keys[0].t))
+    return (pt if ports else ent), hs
 
 
 # ---------------------------------------------------------------------------------------------

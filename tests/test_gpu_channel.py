@@ -45,6 +45,33 @@ def test_scatter_columns_matches_stable_argsort(n, nb):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("n,nb", [(1, 3), (513, 7), (2_000_003, 256), (777_777, 37)])
+def test_uint8_ports_match_e128_entries(n, nb):
+    """The hash partitioner's compact form (one uint8 port per row) moves every column exactly as
+    the 16-byte entries do, with or without a port LUT."""
+    g = torch.Generator(device="cuda").manual_seed(7 * n + nb)
+    ports = torch.randint(0, nb, (n,), device="cuda", generator=g)
+    ent = torch.stack([torch.arange(n, device="cuda"), ports], 1)
+    cols = [torch.randint(-2**62, 2**62, (n,), device="cuda", generator=g),
+            torch.randint(0, 255, (n, 100), device="cuda", generator=g, dtype=torch.uint8)]
+    for lut in (None, torch.randperm(256, device="cuda", generator=g).to(torch.uint8)):
+        a, ca = CH.scatter_columns(ent, n, cols, lut)
+        b, cb = CH.scatter_columns(ports.to(torch.uint8), n, cols, lut)
+        assert torch.equal(ca, cb)
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+
+
+def test_stable_hash_ports_match_entries():
+    from dryad_amd.ops import relational as R
+    n = 300_001
+    k = torch.randint(-2**40, 2**40, (n,), device="cuda")
+    keys = [R.HashKey.column(k)]
+    e, _ = R.stable_hash_dest(keys, n, 37, False, k.device)
+    p, _ = R.stable_hash_dest(keys, n, 37, False, k.device, ports=True)
+    assert p.dtype == torch.uint8 and torch.equal(p.to(torch.int64), e[:, 1])
+
+
 def test_scatter_columns_cpu_path_matches_gpu():
     n = 50_000
     ent = torch.zeros((n, 2), dtype=torch.int64)
