@@ -578,10 +578,6 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(const __bf16* __rest
   };
   if (gw < tiles) load(gw);
   for (uint64_t tile = gw; tile < tiles; tile += GW) {
-    // the centroid tiles are re-read from LDS every step instead of being hoisted into 128
-    // registers: that keeps the kernel at ~80 VGPRs, so four waves per SIMD (not two) keep their
-    // next point tiles in flight (the loop reads HBM; LDS has bandwidth to spare)
-    asm volatile("" ::: "memory");
     const uint64_t p = tile * 16 + r;
     f32x4 Dt[KT];
 #pragma unroll
@@ -926,7 +922,7 @@ DR_API int dr_kmeans_step_hi(const __bf16* XH, const float* xnorm, const float* 
   uint32_t* near_list = near_cnt + 4;
   kmeans_near_reset<<<1, 64, 0, s>>>(near_cnt);
   const uint64_t waves = (n + 15) / 16;
-  const uint64_t cap = 4 * (uint64_t)num_cus();      // four resident workgroups per CU (LDS-bound)
+  const uint64_t cap = 8 * (uint64_t)num_cus();
   const unsigned ga = (unsigned)((waves + 3) / 4 < cap ? (waves + 3) / 4 : cap);
 #define DR_KMA(KTV) kmeans_assign_kernel<KTV><<<ga, 256, 0, s>>>(XH, xnorm, n, C, cnorm_ws, K, assign)
   if (K <= 16) DR_KMA(1);
