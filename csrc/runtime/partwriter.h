@@ -9,6 +9,8 @@
 //   submit(slot, off, bytes)  write the slot's first `bytes` bytes at file offset `off`; the file
 //                             is pre-extended ahead of the writes in `extend` steps
 //   finish(size)              wait for every write, cut the file to `size`, close it
+// `mapped`: the threads copy into shared mappings of the file instead of pwrite()ing, so they
+// fill the page cache in parallel (partwriter.cpp, write_mapped).
 #pragma once
 #include <condition_variable>
 #include <cstdint>
@@ -22,7 +24,8 @@ namespace dryad {
 
 class ChunkWriter {
  public:
-  ChunkWriter(const std::string& path, const std::vector<uint64_t>& buf_ptrs, int threads, int64_t extend_bytes);
+  ChunkWriter(const std::string& path, const std::vector<uint64_t>& buf_ptrs, int threads, int64_t extend_bytes,
+              bool mapped = false);
   ~ChunkWriter();
   int acquire();                                   // -1 on error (see error())
   void submit(int slot, int64_t offset, int64_t bytes);
@@ -36,7 +39,8 @@ class ChunkWriter {
     int64_t off, bytes;
   };
   void run();
-  void extend_to(int64_t end);
+  bool extend_to(int64_t end);
+  bool write_mapped(const Job& j);
   int fd_ = -1;
   std::string path_;
   int64_t extend_ = 0, allocated_ = 0, written_ = 0;
@@ -47,7 +51,7 @@ class ChunkWriter {
   std::deque<int> free_;
   std::deque<Job> jobs_;
   int active_ = 0;
-  bool stop_ = false;
+  bool stop_ = false, mapped_ = false;
   std::string err_;
 };
 

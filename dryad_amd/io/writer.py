@@ -19,6 +19,9 @@ CHUNK = 64 << 20
 SLOTS = 16         # 1 GB of pinned ring: enough chunks in flight for every writer thread
 THREADS = 12       # page-cache copies run at ~3-4 GB/s per pwrite thread (4 threads: 12.3 GB/s,
 #                    profiles/r4/stored.log)
+MAPPED = True      # threads copy into shared mappings of the file: buffered pwrite()s to one file
+#                    serialise on its inode lock (4 or 12 threads: ~11.5-12.3 GB/s), page faults on
+#                    distinct pages do not (tools/micro/filewrite_ab.cpp)
 
 _RING = None
 _RING_LOCK = threading.Lock()
@@ -64,7 +67,7 @@ class PartWriter:
         self.ring = _ring()
         _RING_LOCK.acquire()
         try:
-            self.w = runtime().ChunkWriter(path, [b.tensor.data_ptr() for b in self.ring], THREADS)
+            self.w = runtime().ChunkWriter(path, [b.tensor.data_ptr() for b in self.ring], THREADS, mapped=MAPPED)
         except Exception:
             _RING_LOCK.release()
             raise

@@ -3,13 +3,16 @@ device path is covered by tests/test_gpu_writer.py)."""
 import os
 
 import numpy as np
+import pytest
 import torch
 
 from dryad_amd.io import writer as WR
 
 
-def test_part_writer_host_chunks(tmp_path, monkeypatch):
+@pytest.mark.parametrize("mapped", [False, True])
+def test_part_writer_host_chunks(tmp_path, monkeypatch, mapped):
     monkeypatch.setattr(WR, "CHUNK", 1 << 16)           # many chunks through a small ring
+    monkeypatch.setattr(WR, "MAPPED", mapped)           # pwrite() and shared-mapping writers
     p = str(tmp_path / "part.bin")
     rng = np.random.default_rng(2)
     pieces = [rng.integers(0, 256, size=n, dtype=np.uint8) for n in (0, 1, 65535, 65536, 300_001, 7)]

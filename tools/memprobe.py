@@ -18,16 +18,18 @@ def main():
     n = 2_000_000
     orig_op, orig_gather = GE.GpuJobRunner._run_op, GE.GpuJobRunner._gather_inputs
 
-    def run_op(self, op, args, vctx, s):
-        out = orig_op(self, op, args, vctx, s)
+    def run_op(self, *a, **k):
+        out = orig_op(self, *a, **k)
+        s = a[3] if len(a) > 3 else k["s"]
+        op = a[0]
         torch.cuda.synchronize()
         if w.rank == 0:
             print(f"[mem] {s.name}:{op['op']}: alloc {torch.cuda.memory_allocated() / 1e6:.1f} MB, "
                   f"peak {torch.cuda.max_memory_allocated() / 1e6:.1f} MB", flush=True)
         return out
 
-    def gather(self, s):
-        out = orig_gather(self, s)
+    def gather(self, s, *a, **k):
+        out = orig_gather(self, s, *a, **k)
         torch.cuda.synchronize()
         if w.rank == 0:
             print(f"[mem] {s.name}:gather: alloc {torch.cuda.memory_allocated() / 1e6:.1f} MB, "

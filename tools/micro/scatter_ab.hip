@@ -116,6 +116,14 @@ __global__ __launch_bounds__(256) void scatter(const E64* __restrict__ in, E64* 
   gu64* mine = (gu64*)(granules + (uint64_t)tile * kBins + t);
   __hip_atomic_store(mine, ((unsigned long long)(tile == 0 ? tag_inc : tag_agg) << 32) | tot, __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long pre[4] = {0ull, 0ull, 0ull, 0ull};
+  if constexpr (MODE == 3) {                      // first look-back window in flight under the stage fill
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (tile >= (uint32_t)k + 1)
+        pre[k] = __hip_atomic_load((gu64*)(granules + (uint64_t)(tile - 1 - k) * kBins + t), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  }
   wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
   uint32_t all;
   bstart[t] = block_exclusive_scan256(tot, sc, all);
@@ -132,13 +140,16 @@ __global__ __launch_bounds__(256) void scatter(const E64* __restrict__ in, E64* 
     ex = toff[(uint64_t)tile * kBins + t];        // offsets computed beforehand: no look-back
   } else if (tile > 0) {
     uint64_t j = tile;
+    bool first = MODE == 3;
     for (;;) {
       unsigned long long g[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        g[k] = j >= (uint64_t)k + 1 ? __hip_atomic_load((gu64*)(granules + (j - 1 - k) * kBins + t), __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT)
-                                    : 0ull;
+        g[k] = first ? pre[k]
+                     : j >= (uint64_t)k + 1 ? __hip_atomic_load((gu64*)(granules + (j - 1 - k) * kBins + t),
+                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                            : 0ull;
+      first = false;
       bool done = false;
       int used = 0;
 #pragma unroll
@@ -436,7 +447,7 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     HC(hipEventCreate(&a));
     HC(hipEventCreate(&b));
-    for (int mode = 1; mode <= 2; ++mode) {
+    for (int mode = 1; mode <= 3; ++mode) {
       float best = 1e9f;
       for (int it = 0; it < 4; ++it) {
         HC(hipMemset(ws, 0, ws_bytes));
@@ -445,17 +456,20 @@ int main(int argc, char** argv) {
         auto* tk = reinterpret_cast<uint32_t*>(ws);
         if (mode == 1)
           scatter<32, false, false, 1><<<(unsigned)tiles, 256>>>(in, o2, n, shift, gbase, g, tk, (uint32_t)tiles, toff);
-        else
+        else if (mode == 2)
           scatter<32, false, false, 2><<<(unsigned)tiles, 256>>>(in, o2, n, shift, gbase, g, tk, (uint32_t)tiles, toff);
+        else
+          scatter<32, false, false, 3><<<(unsigned)tiles, 256>>>(in, o2, n, shift, gbase, g, tk, (uint32_t)tiles, toff);
         HC(hipEventRecord(b));
         HC(hipEventSynchronize(b));
         float t_;
         HC(hipEventElapsedTime(&t_, a, b));
         if (it > 0 && t_ < best) best = t_;
       }
-      std::printf("%s: %.3f ms  %.2f TB/s\n", mode == 1 ? "atomic ranks, unstable (timing only)" : "offsets precomputed (no look-back)",
+      std::printf("%s: %.3f ms  %.2f TB/s\n", mode == 1 ? "atomic ranks, unstable (timing only)" :
+                  mode == 2 ? "offsets precomputed (no look-back)" : "look-back window prefetched under the stage fill",
                   best, gb / best);
-      if (mode == 2) {
+      if (mode >= 2) {
         HC(hipMemset(bad, 0, 8));
         diff<<<4096, 256>>>(o1, o2, n, bad);
         HC(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
