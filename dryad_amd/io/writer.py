@@ -19,9 +19,9 @@ CHUNK = 64 << 20
 SLOTS = 16         # 1 GB of pinned ring: enough chunks in flight for every writer thread
 THREADS = 12       # page-cache copies run at ~3-4 GB/s per pwrite thread (4 threads: 12.3 GB/s,
 #                    profiles/r4/stored.log)
-MAPPED = True      # threads copy into shared mappings of the file: buffered pwrite()s to one file
-#                    serialise on its inode lock (4 or 12 threads: ~11.5-12.3 GB/s), page faults on
-#                    distinct pages do not (tools/micro/filewrite_ab.cpp)
+MAPPED = False     # True: threads copy into shared mappings of the file instead of pwrite().  On
+#                    the MI355X box that fills the page cache at 3.5-6.3 GB/s against pwrite's
+#                    11.5-12.6 GB/s (profiles/r4/filewrite_ab.log), so pwrite stays the default
 
 _RING = None
 _RING_LOCK = threading.Lock()

@@ -1,9 +1,14 @@
 // Page-cache write ceiling for one part file: N threads pwrite() 64 MB chunks into one file
 // (buffered writes to one inode serialise on its lock) against N threads copying the same chunks
 // into a shared MAP_SHARED mapping of the pre-sized file (page faults on distinct pages run in
-// parallel), with and without MADV_POPULATE_WRITE pre-faulting each chunk.
+// parallel), with and without MADV_POPULATE_WRITE pre-faulting each chunk; then the same bytes
+// pwrite()n into one file per thread (is the ceiling per inode or global?) and O_DIRECT pwrite()s
+// into one preallocated file (no page cache).
 // Build: g++ -O3 -std=c++17 -pthread tools/micro/filewrite_ab.cpp -o tools/micro/bin/filewrite_ab
 // Run:   filewrite_ab <dir> <GB> <threads...>
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE
+#endif
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <unistd.h>
@@ -57,15 +62,36 @@ int main(int argc, char** argv) {
   const std::string path = dir + "/filewrite_ab.bin";
   for (int a = 3; a < argc; ++a) {
     const int nt = std::atoi(argv[a]);
-    for (int mode = 0; mode < 3; ++mode) {
+    for (int mode = 0; mode < 5; ++mode) {
       ::unlink(path.c_str());
-      const int fd = ::open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0644);
+      if (mode == 3) {                       // one file per thread
+        std::vector<int> fds(nt);
+        for (int i = 0; i < nt; ++i) {
+          fds[i] = ::open((path + "." + std::to_string(i)).c_str(), O_RDWR | O_CREAT | O_TRUNC, 0644);
+          if (fds[i] < 0) { std::perror("open"); return 1; }
+        }
+        const double t0 = now();
+        std::vector<std::thread> ts;
+        for (int i = 0; i < nt; ++i)
+          ts.emplace_back([&, i] {
+            for (size_t c = i, k = 0; c < chunks; c += nt, ++k)
+              if (::pwrite(fds[i], src[c % 16], kChunk, (off_t)(k * kChunk)) != (ssize_t)kChunk) std::abort();
+          });
+        for (auto& t : ts) t.join();
+        const double t1 = now();
+        for (int i = 0; i < nt; ++i) { ::close(fds[i]); ::unlink((path + "." + std::to_string(i)).c_str()); }
+        std::printf("%-28s threads %2d  %.2f GB in %.3f s = %.2f GB/s\n", "pwrite (one file per thread)", nt,
+                    bytes / 1e9, t1 - t0, bytes / 1e9 / (t1 - t0));
+        std::fflush(stdout);
+        continue;
+      }
+      const int fd = ::open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC | (mode == 4 ? O_DIRECT : 0), 0644);
       if (fd < 0) {
         std::perror("open");
         return 1;
       }
       const double t0 = now();
-      if (mode == 0) {
+      if (mode == 0 || mode == 4) {
         ::posix_fallocate(fd, 0, (off_t)bytes);
         run_threads(nt, chunks, [&](size_t c) {
           size_t done = 0;
@@ -93,7 +119,8 @@ int main(int argc, char** argv) {
       const double t1 = now();
       ::close(fd);
       std::printf("%-28s threads %2d  %.2f GB in %.3f s = %.2f GB/s\n",
-                  mode == 0 ? "pwrite (one file)" : mode == 1 ? "mmap memcpy" : "mmap populate+memcpy", nt,
+                  mode == 0 ? "pwrite (one file)" : mode == 1 ? "mmap memcpy" : mode == 2 ? "mmap populate+memcpy"
+                                                                                       : "O_DIRECT pwrite (one file)", nt,
                   bytes / 1e9, t1 - t0, bytes / 1e9 / (t1 - t0));
       std::fflush(stdout);
     }
