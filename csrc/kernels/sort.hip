@@ -1270,27 +1270,28 @@ __global__ __launch_bounds__(256) void gather_fixup_kernel(const uint32_t* __res
   }
 }
 
-// gather_fixup_kernel<25, true, 32> with 16-byte row loads: 8 lanes per 128-byte input line
-// (7 loads of it hold the 100-byte record), every row of the window requested before any is
-// stored, staged through LDS at the output's 100-byte pitch, then written out as contiguous
-// dwords.  The dword-per-lane copy keeps ~3 lines per load instruction in flight; this one 8.
-__global__ __launch_bounds__(256) void gather_fixup_p128w_kernel(const uint32_t* __restrict__ rows,
-                                                                 uint32_t* __restrict__ out,
-                                                                 const E64* __restrict__ ent, uint64_t n,
-                                                                 uint32_t key_off, uint32_t key_len, int run_shift,
-                                                                 uint32_t* __restrict__ overflow) {
-  constexpr uint32_t W = 25, Win = 32;
+// Row gather + run fix-up for 100-byte records stored at a 128-byte pitch, rows fetched FIRST:
+// the window's rows [ob, oe) are requested in position order (8 lanes per aligned 128-byte line,
+// 7 16-byte nontemporal loads hold the record, every load of the window in flight before any is
+// used) and staged in LDS at the output's 100-byte pitch; runs of equal windows are then ranked
+// from the staged keys (no second, dependent round trip to HBM for the keys of multi-entry
+// runs), and the output is written from LDS in rank order as contiguous dwords.
+// (1-GPU TeraSort step 103.5 -> 101.4 ms; the same staging of 100-byte-pitch rows with dword
+// loads was slower than gather_fixup_kernel<25>: 84 -> 99-101 ms over 1.25e9 received rows.)
+__global__ __launch_bounds__(256) void gather_fixup_staged_kernel(const uint32_t* __restrict__ rows,
+                                                                  uint32_t* __restrict__ out,
+                                                                  const E64* __restrict__ ent, uint64_t n,
+                                                                  uint32_t key_off, uint32_t key_len, int run_shift,
+                                                                  uint32_t* __restrict__ overflow) {
+  constexpr uint32_t W = 25;
   __shared__ uint32_t rid[kGfWin + 1];     // rid[p + 1] = run id of window position p; rid[0] = position -1
   __shared__ uint32_t idx[kGfWin];
-  __shared__ uint32_t sidx[kGfWin];
-  // the run keys (phases A, B) and the row staging (phase C) share one buffer
-  __shared__ __attribute__((aligned(16))) uint32_t sbuf[kGfWin * 25 > kGfWin * 4 ? kGfWin * 25 : kGfWin * 4];
-  uint64_t* kk0 = reinterpret_cast<uint64_t*>(sbuf);
-  uint64_t* kk1 = kk0 + kGfWin;
+  __shared__ uint16_t slot[kGfWin];        // output position - ob -> staged row
+  __shared__ __attribute__((aligned(16))) uint32_t stage[kGfWin * W];
   __shared__ uint32_t own[2];
   const int t = threadIdx.x;
-  const uint8_t* rbytes = reinterpret_cast<const uint8_t*>(rows);
-  const bool aligned = (((Win * 4) | key_off) & 3) == 0;
+  const uint8_t* sbytes = reinterpret_cast<const uint8_t*>(stage);
+  const bool aligned = (key_off & 3) == 0;
   for (uint64_t c0 = (uint64_t)blockIdx.x * kGfCore; c0 < n; c0 += (uint64_t)gridDim.x * kGfCore) {
     const uint32_t L = (uint32_t)((n - c0) < (uint64_t)kGfWin ? (n - c0) : kGfWin);
     const uint32_t core = L < (uint32_t)kGfCore ? L : (uint32_t)kGfCore;
@@ -1322,37 +1323,8 @@ __global__ __launch_bounds__(256) void gather_fixup_p128w_kernel(const uint32_t*
       __syncthreads();
       continue;
     }
-    // phase A: keys of the rows in multi-entry runs
-    for (uint32_t p = ob + t; p < oe; p += kBlock) {
-      const bool multi = (p > ob && rid[p + 1] == rid[p]) || (p + 1 < oe && rid[p + 2] == rid[p + 1]);
-      if (multi) {
-        uint64_t k0, k1;
-        load_key128(rbytes + (uint64_t)idx[p] * (Win * 4) + key_off, key_len, aligned, k0, k1);
-        kk0[p] = k0;
-        kk1[p] = k1;
-      } else {
-        sidx[p - ob] = idx[p];
-      }
-    }
-    __syncthreads();
-    // phase B: rank inside each run: (key, position) order = stable
-    for (uint32_t p = ob + t; p < oe; p += kBlock) {
-      const uint32_t r = rid[p + 1];
-      const bool multi = (p > ob && rid[p] == r) || (p + 1 < oe && rid[p + 2] == r);
-      if (!multi) continue;
-      uint32_t rs = p, re = p + 1;
-      while (rs > ob && rid[rs] == r) --rs;
-      while (re < oe && rid[re + 1] == r) ++re;
-      const uint64_t a0 = kk0[p], a1 = kk1[p];
-      uint32_t cnt = 0;
-      for (uint32_t q = rs; q < re; ++q) {
-        const uint64_t b0 = kk0[q], b1 = kk1[q];
-        cnt += (b0 < a0 || (b0 == a0 && (b1 < a1 || (b1 == a1 && q < p)))) ? 1u : 0u;
-      }
-      sidx[rs + cnt - ob] = idx[p];
-    }
-    __syncthreads();
     const uint32_t nrows = oe - ob;
+    // phase 1: fetch the rows in position order into the stage
     {
       constexpr int kRounds = kGfWin / 32;         // 32 rows per round (8 lanes each)
       const uint32_t g = t >> 3, sub = t & 7;
@@ -1362,19 +1334,18 @@ __global__ __launch_bounds__(256) void gather_fixup_p128w_kernel(const uint32_t*
       for (int k = 0; k < kRounds; ++k) {
         const uint32_t r = g + 32 * k;
         if (r < nrows && sub < 7) {
-          const uint4* src = reinterpret_cast<const uint4*>(rb + (uint64_t)sidx[r] * 128 + sub * 16);
+          const uint4* src = reinterpret_cast<const uint4*>(rb + (uint64_t)idx[ob + r] * 128 + sub * 16);
           buf[k].x = __builtin_nontemporal_load(&src->x);
           buf[k].y = __builtin_nontemporal_load(&src->y);
           buf[k].z = __builtin_nontemporal_load(&src->z);
           buf[k].w = __builtin_nontemporal_load(&src->w);
         }
       }
-      __syncthreads();                             // kk0 / kk1 are dead: sbuf becomes the staging
 #pragma unroll
       for (int k = 0; k < kRounds; ++k) {
         const uint32_t r = g + 32 * k;
         if (r < nrows && sub < 7) {
-          uint32_t* d = sbuf + r * W + sub * 4;
+          uint32_t* d = stage + r * W + sub * 4;
           d[0] = buf[k].x;
           if (sub < 6) {
             d[1] = buf[k].y;
@@ -1385,9 +1356,35 @@ __global__ __launch_bounds__(256) void gather_fixup_p128w_kernel(const uint32_t*
       }
     }
     __syncthreads();
+    // phase 2: rank inside each run of equal windows, (key, position) order = stable
+    for (uint32_t p = ob + t; p < oe; p += kBlock) {
+      const uint32_t r = rid[p + 1];
+      const bool multi = (p > ob && rid[p] == r) || (p + 1 < oe && rid[p + 2] == r);
+      if (!multi) {
+        slot[p - ob] = (uint16_t)(p - ob);
+        continue;
+      }
+      uint32_t rs = p, re = p + 1;
+      while (rs > ob && rid[rs] == r) --rs;
+      while (re < oe && rid[re + 1] == r) ++re;
+      uint64_t a0, a1;
+      load_key128(sbytes + (p - ob) * (W * 4) + key_off, key_len, aligned, a0, a1);
+      uint32_t cnt = 0;
+      for (uint32_t q = rs; q < re; ++q) {
+        uint64_t b0, b1;
+        load_key128(sbytes + (q - ob) * (W * 4) + key_off, key_len, aligned, b0, b1);
+        cnt += (b0 < a0 || (b0 == a0 && (b1 < a1 || (b1 == a1 && q < p)))) ? 1u : 0u;
+      }
+      slot[rs + cnt - ob] = (uint16_t)(p - ob);
+    }
+    __syncthreads();
+    // phase 3: the output rows from the stage in rank order
     const uint32_t words = nrows * W;
     uint32_t* o = out + (c0 + ob) * W;
-    for (uint32_t j = t; j < words; j += kBlock) __builtin_nontemporal_store(sbuf[j], o + j);
+    for (uint32_t j = t; j < words; j += kBlock) {
+      const uint32_t r = j / W, c = j - r * W;
+      __builtin_nontemporal_store(stage[(uint32_t)slot[r] * W + c], o + j);
+    }
     __syncthreads();
   }
 }
@@ -1780,8 +1777,9 @@ DR_API int dr_gather_fixup_pitch128(const uint8_t* rows, uint8_t* out, const E64
   if (run_shift < 32 || run_shift > 63) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
   const unsigned g = grid_for(n, kGfCore, 16384);
-  gather_fixup_p128w_kernel<<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows), reinterpret_cast<uint32_t*>(out),
-                                              ent, n, key_off, key_len, run_shift, overflow);
+  gather_fixup_staged_kernel<<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows),
+                                                   reinterpret_cast<uint32_t*>(out), ent, n, key_off, key_len,
+                                                   run_shift, overflow);
   DR_LAUNCH_CHECK();
   return 0;
 }
