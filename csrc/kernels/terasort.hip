@@ -168,6 +168,8 @@ __global__ __launch_bounds__(256) void ts_check_kernel(const uint32_t* __restric
 // idx being the bucket-ordered record offsets of dr_ts_dest_partition.  Each workgroup builds 256
 // records in LDS and streams them out with 16-byte nontemporal stores from the first 16-byte
 // boundary on (dword stores for the few words before it and after the last full chunk).
+// IS = idx stride in 32-bit words: 1 (int32 offsets) or 2 (the low words of sorted E64 entries).
+template <int IS>
 __global__ __launch_bounds__(256) void ts_gen_gather_kernel(uint32_t* __restrict__ out, const uint32_t* __restrict__ idx,
                                                             uint64_t n, uint64_t first, uint64_t seed) {
   __shared__ __attribute__((aligned(16))) uint32_t img[256 * 25];
@@ -176,7 +178,7 @@ __global__ __launch_bounds__(256) void ts_gen_gather_kernel(uint32_t* __restrict
     const uint32_t rows = (uint32_t)((n - row0) < 256 ? (n - row0) : 256);
     if (t < rows) {
       uint32_t w[25];
-      ts_record(seed, first + idx[row0 + t], w);
+      ts_record(seed, first + idx[(row0 + t) * IS], w);
 #pragma unroll
       for (int k = 0; k < 25; ++k) img[t * 25 + k] = w[k];
     }
@@ -266,8 +268,38 @@ DR_API int dr_terasort_gen_gather(uint8_t* out, const uint32_t* idx, uint64_t n,
                                   hipStream_t s) {
   if (n == 0) return 0;
   if (reinterpret_cast<uintptr_t>(out) & 3) return (int)hipErrorInvalidValue;
-  ts_gen_gather_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), idx, n, first,
-                                                               seed);
+  ts_gen_gather_kernel<1><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out), idx, n, first,
+                                                                  seed);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// Send rows of a generated input in the order of sorted E64 entries: out row p = record
+// first + (uint32)ent[p] (the fine-bucket send side of the multi-rank TeraSort, ops/recordsort.py).
+DR_API int dr_terasort_gen_gather64(uint8_t* out, const E64* ent, uint64_t n, uint64_t first, uint64_t seed,
+                                    hipStream_t s) {
+  if (n == 0) return 0;
+  if (reinterpret_cast<uintptr_t>(out) & 3) return (int)hipErrorInvalidValue;
+  ts_gen_gather_kernel<2><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out),
+                                                                  reinterpret_cast<const uint32_t*>(ent), n, first,
+                                                                  seed);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// E64 entries only (key bytes 0..3 << 32 | idx_base + i), no records: the send side of the
+// multi-rank TeraSort sorts these before any record exists.  hist_part as in
+// dr_terasort_gen_keys64_pitch128 ([dr_terasort_gen_hist_parts(n)][4][256], nullable).
+DR_API int dr_terasort_gen_entries64(E64* keys, uint64_t n, uint64_t first_index, uint64_t seed, uint32_t idx_base,
+                                     uint32_t* hist_part, hipStream_t s) {
+  if (n == 0) return 0;
+  if (n + idx_base > (1ull << 32)) return (int)hipErrorInvalidValue;
+  const unsigned g = grid_for(n, 256, 16384);
+  if (hist_part)
+    ts_gen_kernel<2, false, 25, true><<<g, 256, 0, s>>>(nullptr, n, first_index, seed, keys, idx_base, nullptr,
+                                                        hist_part);
+  else
+    ts_gen_kernel<2, false><<<g, 256, 0, s>>>(nullptr, n, first_index, seed, keys, idx_base, nullptr);
   DR_LAUNCH_CHECK();
   return 0;
 }

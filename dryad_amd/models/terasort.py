@@ -355,13 +355,14 @@ class TeraSortLoopbackJob:
 
     Rank ``rank`` of W ranks owns records [rank * n, (rank + 1) * n) of gen://terasort and does
     exactly what ``distributed_sort_rows`` does on a node: its sample, the separators of the W * B
-    key ranges, the send-side pack (bucket order from the generator's keys, every round's records
-    generated into the send buffer), then, per received round, the E64 extraction, the look-back
-    radix sort and the row gather with run fix-up into the output table.  The all-to-all-v is the
-    only part replaced: the bytes this rank would receive (round b = the records of EVERY source
-    rank whose key falls in this rank's b-th range, in source order) are generated into the receive
-    buffer by the same partition + generator kernels, outside the timed segments.  The other
-    ranks' samples (what the sample all-gather returns) are generated outside them too.
+    key ranges (cut to fine-bucket edges), the send side (E64 entries from the generator, one
+    look-back sort, the fine-bucket starts, every round's records generated into the send buffer in
+    key order), then, per received round, the per-bucket LDS merge (ts_tile_merge) into the output
+    table.  The all-to-all-v is the only part replaced: the bytes this rank would receive (round b
+    = the records of EVERY source rank whose key falls in this rank's b-th range, in source order,
+    and every source's per-bucket counts) are produced by running each source's send side, outside
+    the timed segments.  The other ranks' samples (what the sample all-gather returns) are
+    generated outside them too.
 
     Timed with HIP events: (own sample) + (separators + pack) + (receive-side sorts); the phases
     are reported separately.  Validated: the output is in order, holds exactly the received
@@ -385,26 +386,37 @@ class TeraSortLoopbackJob:
     def _events(self):
         return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
-    def _receive(self, seps):
-        """The exchange, simulated: every source's pieces for this rank, generated in place."""
+    def _receive(self, seps_hi, L, fb):
+        """The exchange, simulated: every source's send side run for it (entries, look-back sort,
+        fine-bucket starts), its pieces for this rank generated in place, its per-bucket counts
+        of this rank's key ranges stacked.  Returns (round offsets, fine counts [W, K])."""
         n, W, B, me, seed = self.n, self.W, self.B, self.rank, self.cfg.seed
-        idx = self.bufs.ent_b.view(-1).view(torch.int32)[:n]
-        M64 = (1 << 64) - 1
-        starts = [S.dest_partition_gen(s * n, seed, n, seps, s << 32, M64, B, W, idx).tolist() for s in range(W)]
-        cnt = [[starts[s][b * W + me + 1] - starts[s][b * W + me] for s in range(W)] for b in range(B)]
+        e, tmp = self.bufs.ent_a.view(-1)[:n], self.bufs.ent_b.view(-1)[:n]
+        Lt = torch.tensor(L, dtype=torch.int64, device=self.dev)
+
+        def send_side(s):
+            TS.gen_entries64(e, s * n, seed, hist=False)
+            srt = S.sort_entries64(e, tmp, 32, lookback=False)
+            starts = TS.fine_starts(srt, fb)
+            return srt, starts, starts.index_select(0, Lt).tolist()
+        sizes, fine = [], []
+        for s in range(W):
+            _, starts, Sg = send_side(s)
+            sizes.append([Sg[me * B + b + 1] - Sg[me * B + b] for b in range(B)])
+            fine.append((starts[L[me * B] + 1: L[(me + 1) * B] + 1] - starts[L[me * B]: L[(me + 1) * B]]).clone())
         off = [0]
         for b in range(B):
-            off.append(off[-1] + sum(cnt[b]))
+            off.append(off[-1] + sum(sizes[s][b] for s in range(W)))
         if off[-1] > self.bufs.capacity:
             raise RuntimeError(f"range partition skew: {off[-1]} rows > capacity {self.bufs.capacity}")
         for s in range(W):
-            st = S.dest_partition_gen(s * n, seed, n, seps, s << 32, M64, B, W, idx).tolist()
-            pos = [off[b] + sum(cnt[b][:s]) for b in range(B)]
+            srt, _, Sg = send_side(s)
             for b in range(B):
-                a, z = st[b * W + me], st[b * W + me + 1]
-                if z > a:
-                    TS.gen_gather(self.bufs.rows_in[pos[b]: pos[b] + z - a], idx[a:z], s * n, seed)
-        return off
+                pos = off[b] + sum(sizes[s2][b] for s2 in range(s))
+                g = me * B + b
+                if Sg[g + 1] > Sg[g]:
+                    TS.gen_gather64(self.bufs.rows_in[pos: pos + Sg[g + 1] - Sg[g]], srt[Sg[g]: Sg[g + 1]], s * n, seed)
+        return off, torch.stack(fine)
 
     def step(self):
         n, W, B, me = self.n, self.W, self.B, self.rank
@@ -420,20 +432,19 @@ class TeraSortLoopbackJob:
         e[1][0].record()
         seps = RS.separators_from_samples(allsamp, W * B)
         seps_hi = [int(x) & M64 for x in seps[:, 1].tolist()]
-        st, pack = RS.pack_gen(self.bufs, (me * n, seed), n, seps, me << 32, M64, B, W)
+        fb = RS.fine_bits(n * W)
+        st, pack, counts, L = RS.pack_gen_fine(self.bufs, (me * n, seed), n, seps_hi, B, W, fb)
         for b in range(B):
             pack(b)
         e[1][1].record()
-        off = self._receive(seps)                      # the all-to-all-v (not timed)
+        off, fine = self._receive(seps_hi, L, fb)            # the all-to-all-v (not timed)
         acc = TS.check(self.bufs.rows_in[: off[-1]])
         e[2][0].record()
-        out = RS.sort_received_rounds(self.bufs, off, [off[-1]] * B, 0, seps_hi, B, me, 0, KEYLEN)
+        out = RS.merge_received_rounds(self.bufs, off, fine, L, fb, B, me, [off[-1]] * B, 0)
         e[2][1].record()
         torch.cuda.synchronize(dev)
         self.out, self.recv_hash = out, acc
-        lo = seps[me * B - 1] if me > 0 else None
-        hi = seps[(me + 1) * B - 1] if me < W - 1 else None
-        self.bounds = (lo, hi)
+        self.bounds = RS.fine_hi_bounds([L[me * B], L[(me + 1) * B]], fb, 0)
         self.phases = {"sample_ms": e[0][0].elapsed_time(e[0][1]), "separators_pack_ms": e[1][0].elapsed_time(e[1][1]),
                        "receive_sort_ms": e[2][0].elapsed_time(e[2][1])}
         self.sent_rows = st[-1]
@@ -450,15 +461,10 @@ class TeraSortLoopbackJob:
         viol = int(acc[1].item())
         ok_lo = ok_hi = True
         if out.shape[0]:
-            first = bytes(out[0, :KEYLEN].cpu().tolist())
-            last = bytes(out[-1, :KEYLEN].cpu().tolist())
-            lo, hi = self.bounds
-
-            def sep_key(sep):
-                h, lw = (int(x) & ((1 << 64) - 1) for x in sep.tolist()[::-1])
-                return h.to_bytes(8, "big") + (lw >> 48).to_bytes(2, "big")
-            ok_lo = lo is None or first >= sep_key(lo)
-            ok_hi = hi is None or last <= sep_key(hi)
+            first = int.from_bytes(bytes(out[0, :8].cpu().tolist()), "big")
+            last = int.from_bytes(bytes(out[-1, :8].cpu().tolist()), "big")
+            lo, hi = self.bounds            # hi words of this rank's key ranges (fine-bucket edges)
+            ok_lo, ok_hi = first >= lo, last <= hi
         ok = h_in == h_out and viol == 0 and ok_lo and ok_hi
         return dict(ok=bool(ok), hash_match=h_in == h_out, violations=viol, records=int(out.shape[0]),
                     in_bounds=bool(ok_lo and ok_hi))

@@ -232,7 +232,8 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     not the co-location of equal keys, so the planner turns it off (keep_ties) when a consumer
     relies on the output being partitioned by the key.  ``gen = (first, seed)``: ``rows_in`` was
     never written; row i is gen://terasort record first + i, and the send side works from the
-    generator alone (``keys_fmt`` "gen": no entries either; see ``pack_gen``).
+    generator alone (``keys_fmt`` "gen": no entries either): the fine-bucket exchange of
+    ``pack_gen_fine`` / ``merge_received_rounds``.
 
     With several ranks the exchange is pipelined with the local sort.  The sampled separators cut
     the key space into ``W * B`` ranges, B consecutive ones per destination rank, and the send
@@ -271,11 +272,14 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     shuffle.all_reduce_(nmax, "max", w)
     B = pipeline_subs(int(nmax.item()) * stride, W)
     pack = None
+    fine = None
     if gen_path:
         seps = separators_from_samples(
             shuffle.all_gather_varlen(gen_samples(gen, n, w.rank, lo_or, part_mask, sample_target, seed, w.device), w),
             W * B)
-        st, pack = pack_gen(bufs, gen, n, seps, lo_or, part_mask, B, W)
+        fb = fine_bits(int(nmax.item()) * W)
+        st, pack, counts, L = pack_gen_fine(bufs, gen, n, [int(x) & _M64 for x in seps[:, 1].tolist()], B, W, fb)
+        fine = exchange_fine_counts(counts, L, B, W, w)
     else:
         if keys_fmt != "e128":
             keys_ready = False
@@ -303,13 +307,138 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
         handles.append(shuffle.alltoallv_bytes_async(
             send_flat[st[b * W] * stride: st[(b + 1) * W] * stride], [c * stride for c in send[b]],
             recv_flat[off[b] * stride: off[b + 1] * stride], [rc[s][b] * stride for s in range(W)], w))
-    out = sort_received_rounds(bufs, off, [st[(b + 1) * W] for b in range(B)], n, seps_hi, B, w.rank, key_off,
-                               key_len, wait=lambda b: shuffle.wait(handles[b]))
+    sent_after = [st[(b + 1) * W] for b in range(B)]
+    if fine is not None:
+        out = merge_received_rounds(bufs, off, fine, L, fb, B, w.rank, sent_after, n,
+                                    wait=lambda b: shuffle.wait(handles[b]))
+    else:
+        out = sort_received_rounds(bufs, off, sent_after, n, seps_hi, B, w.rank, key_off, key_len,
+                                   wait=lambda b: shuffle.wait(handles[b]))
     if stats is not None:
         stats.n_in, stats.n_out, stats.rounds = n, n_recv, B
         stats.send_counts = [sum(send[b][r] for b in range(B)) for r in range(W)]
         stats.recv_counts = [sum(rc[s]) for s in range(W)]
     return out[:n_recv]
+
+
+# Fine buckets of the gen:// exchange: the top ``fb`` key bits, about FINE_ROWS rows of the whole
+# job each (at most tile_cap() = 512 are ordered in LDS), fb >= 25 so that a bucket's remaining
+# key bits and its 9-bit tile index fit one 64-bit LDS sort key.
+FINE_MIN_BITS, FINE_MAX_BITS, FINE_ROWS = 25, 28, 300
+
+
+def fine_bits(total_rows: int) -> int:
+    fb = FINE_MIN_BITS
+    while fb < FINE_MAX_BITS and total_rows > FINE_ROWS * (1 << fb):
+        fb += 1
+    return fb
+
+
+def fine_bounds(seps_hi: list, fb: int) -> list:
+    """L[g] = first fine bucket of key range g (g = 0 .. len(seps_hi) + 1): each separator cut
+    down to a bucket edge, so a key range is a union of whole fine buckets."""
+    return [0] + [int(x) >> (64 - fb) for x in seps_hi] + [1 << fb]
+
+
+def fine_hi_bounds(L: list, fb: int, g: int) -> tuple[int, int]:
+    """(min, max) of the key ``hi`` words key range ``g`` of fine bounds ``L`` holds."""
+    return L[g] << (64 - fb), min((L[g + 1] << (64 - fb)) - 1, _M64)
+
+
+def pack_gen_fine(bufs: SortBuffers, gen: tuple[int, int], n: int, seps_hi: list, B: int, W: int, fb: int):
+    """Send side over gen://terasort records gen[0] .. gen[0] + n - 1 for the fine-bucket exchange:
+    E64 entries from the generator (key bytes 0..3 as the window, with the look-back sort's digit
+    histograms), one look-back sort of them (stable), the fine-bucket starts of the sorted order.
+    Key range g = fine buckets [L[g], L[g + 1]) is then the contiguous run of sorted entries
+    [S[L[g]], S[L[g + 1]]), and the send buffer (``bufs.rows_out``) is packed round-major (round b
+    = range r * B + b for every destination r), each range's records generated in key order
+    (bucket order; unsorted within a bucket).  Returns (send-row starts st[b * W + r] as a host
+    list, pack(b), the per-bucket row counts (device int32 [2^fb]), L).  The sorted entries live in
+    ``bufs.ent_a`` / ``ent_b`` until the last pack."""
+    e, tmp = bufs.ent_a.view(-1)[:n], bufs.ent_b.view(-1)[:n]
+    hist = TSG.gen_entries64(e, gen[0], gen[1])
+    err = S.lookback_error()
+    srt = S.sort_entries64(e, tmp, 32, gen_hist=hist, err=err)
+    starts = TSG.fine_starts(srt, fb)
+    L = fine_bounds(seps_hi, fb)
+    Lt = torch.tensor(L, dtype=torch.int64, device=e.device)
+    host = torch.cat([starts.index_select(0, Lt).to(torch.int64), err.to(torch.int64)]).tolist()
+    Sg = host[:-1]
+    if host[-1]:                 # the look-back sort gave up: entries again, count + scatter passes
+        TSG.gen_entries64(e, gen[0], gen[1], hist=False)
+        srt = S.sort_entries64(e, tmp, 32, lookback=False)
+        starts = TSG.fine_starts(srt, fb)
+        Sg = starts.index_select(0, Lt).tolist()
+    counts = starts[1:] - starts[:-1]
+    size = [[Sg[r * B + b + 1] - Sg[r * B + b] for r in range(W)] for b in range(B)]
+    st, acc = [], 0
+    for b in range(B):
+        for r in range(W):
+            st.append(acc)
+            acc += size[b][r]
+    st.append(acc)
+
+    def pack(b: int):
+        for r in range(W):
+            g, m = r * B + b, size[b][r]
+            if m:
+                TSG.gen_gather64(bufs.rows_out[st[b * W + r]: st[b * W + r] + m], srt[Sg[g]: Sg[g + 1]], gen[0], gen[1])
+    return st, pack, counts, L
+
+
+def exchange_fine_counts(counts: torch.Tensor, L: list, B: int, W: int, world: World) -> torch.Tensor:
+    """Every source's per-bucket row counts of this rank's key ranges: int32 [W, K] (K = buckets
+    of ranges rank * B .. rank * B + B - 1, which are contiguous in every source's counts)."""
+    me = world.rank
+    K = L[(me + 1) * B] - L[me * B]
+    recv = torch.empty(W * K, dtype=torch.int32, device=counts.device)
+    shuffle.alltoallv_bytes(counts.contiguous().view(torch.uint8), [(L[(r + 1) * B] - L[r * B]) * 4 for r in range(W)],
+                            recv.view(torch.uint8), [K * 4] * W, world)
+    return recv.view(W, K)
+
+
+def merge_received_rounds(bufs: SortBuffers, off: list, fine: torch.Tensor, L: list, fb: int, B: int, rank: int,
+                          sent_after: list, n_sent: int, wait=None, key_len: int = 10) -> torch.Tensor:
+    """Receive side of the fine-bucket exchange: round b's block ``rows_in[off[b]:off[b+1]]`` holds
+    key range g = rank * B + b as W source pieces (source order), each in bucket order, and
+    ``fine[s, k]`` = rows of bucket L[rank * B] + k from source s.  Per round (``wait(b)``) the
+    slices of every bucket are located on the device (prefix sums of ``fine``) and ts_tile_merge
+    orders each bucket in LDS into ``rows_out[off[b]:...]``, deferred until the send rows under it
+    have gone out (``sent_after``, as in sort_received_rounds).  A bucket too large for LDS (heavy
+    key skew) flags its round, which is then sorted after the last round with local_sort_rows."""
+    out = bufs.rows_out
+    W = fine.shape[0]
+    flags = torch.zeros(B, dtype=torch.int32, device=out.device)
+    base = L[rank * B]
+    pending = []
+    for b in range(B):
+        if wait is not None:
+            wait(b)
+        a, z = off[b], off[b + 1]
+        if z > a:
+            g = rank * B + b
+            cnt = fine[:, L[g] - base: L[g + 1] - base].contiguous()
+            rows_per_src = cnt.sum(1, dtype=torch.int64)
+            pre = (torch.cumsum(cnt, 1, dtype=torch.int64) - cnt
+                   + (torch.cumsum(rows_per_src, 0) - rows_per_src + a).view(W, 1)).contiguous()
+            col = cnt.sum(0, dtype=torch.int64)
+            outoff = (torch.cumsum(col, 0) - col + a).contiguous()
+            pending.append((a, z, b, pre, cnt, outoff))
+        keep = []
+        for item in pending:
+            a2, z2, b2, pre, cnt, outoff = item
+            if b == B - 1 or z2 <= sent_after[b] or a2 >= n_sent:
+                TSG.tile_merge(bufs.rows_in, out, pre, cnt, outoff, fb, flags[b2:b2 + 1])
+            else:
+                keep.append(item)
+        pending = keep
+    fl = flags.tolist()
+    for b in range(B):
+        if fl[b]:
+            a, z = off[b], off[b + 1]
+            local_sort_rows(bufs.rows_in[a:z], out[a:z], bufs.ent_a[a:z], bufs.ent_b[a:z], 0, key_len,
+                            hi_bounds=fine_hi_bounds(L, fb, rank * B + b))
+    return out[: off[-1]]
 
 
 def pack_gen(bufs: SortBuffers, gen: tuple[int, int], n: int, seps: torch.Tensor, lo_or: int, lo_mask: int,

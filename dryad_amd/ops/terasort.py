@@ -104,3 +104,69 @@ def gen_gather(out: torch.Tensor, idx: torch.Tensor, first: int, seed: int) -> t
     _lib.call("dr_terasort_gen_gather", ptr(out), ptr(idx), c_u64(m), c_u64(first), c_u64(seed & (2**64 - 1)),
               stream_of(out))
     return out[:m]
+
+
+_lib.register_signatures({
+    "dr_terasort_gen_gather64": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u64, c_u64, c_u64, ctypes.c_void_p]),
+    "dr_terasort_gen_entries64": (ctypes.c_int, [ctypes.c_void_p, c_u64, c_u64, c_u64, c_u32, ctypes.c_void_p,
+                                                 ctypes.c_void_p]),
+    "dr_ts_fine_starts": (ctypes.c_int, [ctypes.c_void_p, c_u64, c_u32, ctypes.c_void_p, ctypes.c_void_p]),
+    "dr_ts_tile_merge": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, c_u32, c_u32, c_u32, ctypes.c_void_p, ctypes.c_void_p]),
+    "dr_ts_tile_cap": (ctypes.c_uint32, []),
+})
+
+
+def gen_entries64(keys: torch.Tensor, first: int, seed: int, hist: bool = True):
+    """E64 sort entries of records ``first .. first + n - 1`` (``keys`` int64 [n]: key bytes 0..3
+    << 32 | i), no records; with ``hist`` also the window-digit histograms a following look-back
+    sort of ``keys`` takes (ops/sort.sort_entries64 gen_hist).  Returns the histograms or None."""
+    from . import sort as S
+    _lib.require_gpu_tensor(keys, "terasort.gen_entries64")
+    n = keys.shape[0]
+    assert keys.dtype == torch.int64 and keys.dim() == 1 and n < (1 << 32)
+    part = None
+    if hist and n >= S.ONESWEEP_MIN:
+        part = S.gen_hist_buffer(int(_lib.lib().dr_terasort_gen_hist_parts(c_u64(n))), keys.device)
+    _lib.call("dr_terasort_gen_entries64", ptr(keys), c_u64(n), c_u64(first), c_u64(seed & (2**64 - 1)), c_u32(0),
+              ptr(part), stream_of(keys))
+    return part
+
+
+def gen_gather64(out: torch.Tensor, ent: torch.Tensor, first: int, seed: int) -> torch.Tensor:
+    """``out[p]`` := record ``first + (ent[p] & 0xFFFFFFFF)`` (``ent`` int64 [m] sorted E64 entries)."""
+    _lib.require_gpu_tensor(out, "terasort.gen_gather64")
+    m = ent.shape[0]
+    assert out.dtype == torch.uint8 and out.shape[0] >= m and out.shape[1] == RECORD_BYTES and out.is_contiguous()
+    assert ent.dtype == torch.int64 and ent.is_contiguous()
+    _lib.call("dr_terasort_gen_gather64", ptr(out), ptr(ent), c_u64(m), c_u64(first), c_u64(seed & (2**64 - 1)),
+              stream_of(out))
+    return out[:m]
+
+
+def fine_starts(ent: torch.Tensor, fb: int) -> torch.Tensor:
+    """int32 [2^fb + 1]: for each fine bucket k (the top ``fb`` key bits) the first position of the
+    window-sorted entries ``ent`` in bucket >= k."""
+    _lib.require_gpu_tensor(ent, "terasort.fine_starts")
+    starts = torch.empty((1 << fb) + 1, dtype=torch.int32, device=ent.device)
+    _lib.call("dr_ts_fine_starts", ptr(ent), c_u64(ent.shape[0]), c_u32(fb), ptr(starts), stream_of(ent))
+    return starts
+
+
+def tile_cap() -> int:
+    """Rows of one fine bucket the receive side orders in LDS (ts_tile_merge)."""
+    return int(_lib.lib().dr_ts_tile_cap())
+
+
+def tile_merge(rows: torch.Tensor, out: torch.Tensor, pre: torch.Tensor, cnt: torch.Tensor, outoff: torch.Tensor,
+               fb: int, overflow: torch.Tensor) -> None:
+    """Order the received fine buckets: bucket k's rows are the W slices ``rows[pre[s, k] :
+    pre[s, k] + cnt[s, k]]`` (all sharing their top ``fb`` key bits), written in key order (ties by
+    source, then slice position) to ``out[outoff[k]:]``.  A bucket past tile_cap() rows is left
+    out and flags ``overflow``."""
+    W, K = cnt.shape
+    assert pre.shape == (W, K) and pre.dtype == torch.int64 and cnt.dtype == torch.int32 and outoff.shape == (K,)
+    assert rows.shape[1] == RECORD_BYTES and out.shape[1] == RECORD_BYTES
+    _lib.call("dr_ts_tile_merge", ptr(rows), ptr(out), ptr(pre.contiguous()), ptr(cnt.contiguous()),
+              ptr(outoff.contiguous()), c_u32(W), c_u32(K), c_u32(fb), ptr(overflow), stream_of(rows))
+    _lib.written(out)
