@@ -169,16 +169,32 @@ __global__ __launch_bounds__(256) void ts_check_kernel(const uint32_t* __restric
 // records in LDS and streams them out with 16-byte nontemporal stores from the first 16-byte
 // boundary on (dword stores for the few words before it and after the last full chunk).
 // IS = idx stride in 32-bit words: 1 (int32 offsets) or 2 (the low words of sorted E64 entries).
+// seg (nullable): nseg segments {out row, idx position}, ascending in out row, seg[0].out = 0:
+// out row p takes idx position seg[s].idx + p - seg[s].out of the last segment starting at or
+// before p (one launch packs a whole exchange round: one segment per destination).
 template <int IS>
 __global__ __launch_bounds__(256) void ts_gen_gather_kernel(uint32_t* __restrict__ out, const uint32_t* __restrict__ idx,
-                                                            uint64_t n, uint64_t first, uint64_t seed) {
+                                                            uint64_t n, uint64_t first, uint64_t seed,
+                                                            const int64_t* __restrict__ seg = nullptr,
+                                                            uint32_t nseg = 0) {
   __shared__ __attribute__((aligned(16))) uint32_t img[256 * 25];
+  __shared__ int64_t sseg[64][2];
   const uint32_t t = threadIdx.x;
+  if (nseg) {
+    if (t < 2 * nseg) sseg[t >> 1][t & 1] = seg[t];
+    __syncthreads();
+  }
   for (uint64_t row0 = (uint64_t)blockIdx.x * 256; row0 < n; row0 += (uint64_t)gridDim.x * 256) {
     const uint32_t rows = (uint32_t)((n - row0) < 256 ? (n - row0) : 256);
     if (t < rows) {
       uint32_t w[25];
-      ts_record(seed, first + idx[(row0 + t) * IS], w);
+      uint64_t p = row0 + t;
+      if (nseg) {
+        uint32_t s = 0;
+        while (s + 1 < nseg && (uint64_t)sseg[s + 1][0] <= p) ++s;
+        p = (uint64_t)sseg[s][1] + (p - (uint64_t)sseg[s][0]);
+      }
+      ts_record(seed, first + idx[p * IS], w);
 #pragma unroll
       for (int k = 0; k < 25; ++k) img[t * 25 + k] = w[k];
     }
@@ -275,14 +291,17 @@ DR_API int dr_terasort_gen_gather(uint8_t* out, const uint32_t* idx, uint64_t n,
 }
 
 // Send rows of a generated input in the order of sorted E64 entries: out row p = record
-// first + (uint32)ent[p] (the fine-bucket send side of the multi-rank TeraSort, ops/recordsort.py).
+// first + (uint32)ent[q(p)] (the fine-bucket send side of the multi-rank TeraSort,
+// ops/recordsort.py), q(p) = p, or through nseg <= 64 segments {out row, entry} (device int64
+// [nseg][2], see ts_gen_gather_kernel): one launch per exchange round.
 DR_API int dr_terasort_gen_gather64(uint8_t* out, const E64* ent, uint64_t n, uint64_t first, uint64_t seed,
-                                    hipStream_t s) {
+                                    const int64_t* seg, uint32_t nseg, hipStream_t s) {
   if (n == 0) return 0;
   if (reinterpret_cast<uintptr_t>(out) & 3) return (int)hipErrorInvalidValue;
+  if (nseg > 64 || (nseg > 0 && seg == nullptr)) return (int)hipErrorInvalidValue;
   ts_gen_gather_kernel<2><<<grid_for(n, 256, 16384), 256, 0, s>>>(reinterpret_cast<uint32_t*>(out),
                                                                   reinterpret_cast<const uint32_t*>(ent), n, first,
-                                                                  seed);
+                                                                  seed, seg, nseg);
   DR_LAUNCH_CHECK();
   return 0;
 }

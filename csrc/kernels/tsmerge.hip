@@ -1,27 +1,29 @@
 // Fine-bucket exchange of the multi-rank TeraSort (ops/recordsort.py, gen:// inputs).
 //
-// The send side sorts its records' E64 entries (key bytes 0..3 as the window) on the window, so
-// its rows leave in key order, and the key ranges of the exchange are unions of FINE BUCKETS (the
-// top `fb` key bits, fb >= 25: ~300 rows of the whole job per bucket).  Every source sends, next
+// The send side sorts its records' E64 entries (key bytes 0..3 as the window) on the top bits of
+// the window, so its rows leave in bucket order, and the key ranges of the exchange are unions of
+// FINE BUCKETS (the top `fb` key bits, 16 <= fb <= 24: ~600 rows of the whole job per bucket).  Every source sends, next
 // to its rows, its row count per fine bucket.  A received key range is then, per fine bucket, W
 // contiguous slices (one per source) of rows that all share their top fb key bits, and the
-// receive side orders each bucket on its own in LDS (ts_tile_merge): no entry extraction, no
-// radix passes and no random row gather over the received block, one sequential read and one
-// sequential write of the rows.
+// receive side orders each bucket on its own (ts_tile_merge): no entry extraction, no radix
+// passes and no random row gather over the received block, one read and one write of the rows.
 //   ts_fine_starts   starts[k] = first sorted entry with bucket >= k (k = 0 .. 2^fb)
-//   ts_tile_merge    one workgroup per fine bucket: its slices staged in LDS at the 100-byte
-//                    pitch, keys (bits fb..79 + tile index) bitonic-sorted in LDS, rows written
-//                    back in key order
+//   ts_tile_merge    one workgroup per fine bucket: its rows held in registers (two per lane),
+//                    their keys ranked by an LDS counting sort, the rows stored to their slots
 // Reference: the sampler + RangePartition + MergeSort stages of CreateRangePartition
 // (LinqToDryad/DryadLinqQueryGen.cs:2362-2474); its merge of the sorted inputs becomes a
-// per-bucket LDS sort because the buckets are small enough to hold.
+// per-bucket sort because the buckets are small enough to hold in one workgroup.
 #include "common.h"
 
 namespace {
 
-constexpr uint32_t kTmCap = 512;                   // rows of one bucket held in LDS (9 index bits)
+constexpr uint32_t kTmCap = 1024;                  // rows of one bucket a workgroup orders
 constexpr uint32_t kTmMaxW = 64;                   // sources
 constexpr uint32_t kTmWords = 25;                  // 100-byte rows
+constexpr uint32_t kTmThreads = 512;
+constexpr uint32_t kTmRows = kTmCap / kTmThreads;  // rows per lane, held in registers (2 x 25 dwords)
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(4)));   // 16-byte access, 4-byte aligned
+constexpr uint32_t kTmBins = 1024;                 // LDS counting-sort bins (next 10 key bits)
 
 __global__ __launch_bounds__(256) void ts_fine_starts_kernel(const E64* __restrict__ ent, uint64_t n, uint32_t fb,
                                                              uint32_t* __restrict__ starts) {
@@ -42,18 +44,28 @@ __global__ __launch_bounds__(256) void ts_fine_starts_kernel(const E64* __restri
 }
 
 // pre[s * K + k] = row (of `rows`) where bucket k's slice from source s starts, cnt[s * K + k] its
-// rows; bucket k's output rows start at out row outoff[k].  A bucket of more than kTmCap rows is
-// skipped and flagged (*overflow); the caller orders that key range another way.
-__global__ __launch_bounds__(256) void ts_tile_merge_kernel(const uint32_t* __restrict__ rows, uint32_t* __restrict__ out,
-                                                            const int64_t* __restrict__ pre,
-                                                            const int32_t* __restrict__ cnt,
-                                                            const int64_t* __restrict__ outoff, uint32_t W, uint32_t K,
-                                                            uint32_t fb, uint32_t* __restrict__ overflow) {
-  __shared__ __attribute__((aligned(16))) uint32_t stage[kTmCap * kTmWords];
+// rows; bucket k's output rows start at out row outoff[k].  Per bucket: lane t holds tile rows t
+// and t + 512 in registers, loaded at once as 6 x 16 + 4 bytes each (the slices are contiguous:
+// the wave's loads cover whole lines between them, one round trip); the rows' remaining key bits
+// [fb, 80) go to LDS, an LDS counting sort on their next 10 bits places each row (ties inside a
+// bin ranked by (key, tile index): source-major = stable), and every lane stores its rows to
+// their output slots.  A bucket of more than kTmCap rows is skipped and flagged (*overflow); the
+// caller orders that key range another way.
+__global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4))) void ts_tile_merge_kernel(const uint32_t* __restrict__ rows,
+                                                                   uint32_t* __restrict__ out,
+                                                                   const int64_t* __restrict__ pre,
+                                                                   const int32_t* __restrict__ cnt,
+                                                                   const int64_t* __restrict__ outoff, uint32_t W,
+                                                                   uint32_t K, uint32_t fb,
+                                                                   uint32_t* __restrict__ overflow) {
   __shared__ uint64_t key[kTmCap];
-  __shared__ uint64_t srow[kTmCap];
+  __shared__ uint16_t member[kTmCap];
+  __shared__ uint16_t rnk[kTmCap];
+  __shared__ uint32_t bcnt[kTmBins];
+  __shared__ uint32_t bcur[kTmBins];
   __shared__ int64_t sbase[kTmMaxW];
   __shared__ uint32_t spre[kTmMaxW + 1];
+  __shared__ uint32_t wtot[kTmThreads / 64];
   const uint32_t t = threadIdx.x;
   for (uint32_t k = blockIdx.x; k < K; k += gridDim.x) {
     if (t < W) sbase[t] = pre[(uint64_t)t * K + k];
@@ -65,6 +77,8 @@ __global__ __launch_bounds__(256) void ts_tile_merge_kernel(const uint32_t* __re
       }
       spre[W] = acc;
     }
+    bcnt[t] = 0;
+    bcnt[t + kTmThreads] = 0;
     __syncthreads();
     const uint32_t nt = spre[W];
     if (nt == 0 || nt > kTmCap) {
@@ -72,65 +86,70 @@ __global__ __launch_bounds__(256) void ts_tile_merge_kernel(const uint32_t* __re
       __syncthreads();
       continue;
     }
-    for (uint32_t i = t; i < nt; i += kBlock) {     // source row of each tile row (source-major = stable)
-      uint32_t s = 0;
-      while (spre[s + 1] <= i) ++s;
-      srow[i] = (uint64_t)(sbase[s] + (int64_t)(i - spre[s]));
-    }
-    __syncthreads();
-    // the bucket's rows into LDS: W contiguous slices, every load of a batch in flight at once
-    const uint32_t words = nt * kTmWords;
-    for (uint32_t j0 = t; j0 < words; j0 += kBlock * 10) {
-      uint32_t v[10];
+    u32x4u v[kTmRows][6];
+    uint32_t tail[kTmRows];
 #pragma unroll
-      for (int q = 0; q < 10; ++q) {
-        const uint32_t j = j0 + q * kBlock;
-        if (j < words) {
-          const uint32_t r = j / kTmWords, c = j - r * kTmWords;
-          v[q] = rows[srow[r] * kTmWords + c];
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 10; ++q) {
-        const uint32_t j = j0 + q * kBlock;
-        if (j < words) stage[j] = v[q];
-      }
-    }
-    __syncthreads();
-    // sort keys: key bits [fb, 80) left-aligned (the top fb bits are the bucket), tile index below
-    uint32_t P = 1;
-    while (P < nt) P <<= 1;
-    for (uint32_t i = t; i < P; i += kBlock) {
-      uint64_t kv = ~0ull;
+    for (uint32_t h = 0; h < kTmRows; ++h) {
+      const uint32_t i = t + h * kTmThreads;        // tile row: source-major = stable
       if (i < nt) {
-        const uint32_t* w = stage + i * kTmWords;
-        const uint64_t k0 = ((uint64_t)bswap32(w[0]) << 32) | bswap32(w[1]);
-        const uint64_t k1 = (uint64_t)(bswap32(w[2]) >> 16);          // key bytes 8, 9
-        const uint64_t hi = (k0 << fb) | ((k1 << 48) >> (64 - fb));
-        kv = (hi & ~(uint64_t)(kTmCap - 1)) | i;
+        uint32_t s = 0;
+        while (spre[s + 1] <= i) ++s;
+        const uint32_t* src = rows + (uint64_t)(sbase[s] + (int64_t)(i - spre[s])) * kTmWords;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) v[h][q] = *reinterpret_cast<const u32x4u*>(src + 4 * q);
+        tail[h] = src[24];
       }
-      key[i] = kv;
+    }
+#pragma unroll
+    for (uint32_t h = 0; h < kTmRows; ++h) {
+      const uint32_t i = t + h * kTmThreads;
+      if (i < nt) {
+        // key bits [fb, 80) left-aligned (fb >= 16: they fit 64 bits); the top 10 pick the bin
+        const uint64_t k0 = ((uint64_t)bswap32(v[h][0].x) << 32) | bswap32(v[h][0].y);
+        const uint64_t k1 = (uint64_t)(bswap32(v[h][0].z) >> 16);          // key bytes 8, 9
+        const uint64_t kv = (k0 << fb) | ((k1 << 48) >> (64 - fb));
+        key[i] = kv;
+        atomicAdd(&bcnt[(uint32_t)(kv >> 54)], 1u);
+      }
     }
     __syncthreads();
-    for (uint32_t size = 2; size <= P; size <<= 1) {
-      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-        for (uint32_t i = t; i < (P >> 1); i += kBlock) {
-          const uint32_t lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
-          const bool asc = (lo & size) == 0;
-          const uint64_t a = key[lo], b = key[hi];
-          if ((a > b) == asc) {
-            key[lo] = b;
-            key[hi] = a;
-          }
-        }
-        __syncthreads();
-      }
+    {                                               // exclusive scan of the 1024 bins, 2 per lane
+      const uint32_t c0 = bcnt[2 * t], c1 = bcnt[2 * t + 1];
+      const uint32_t inc = wave_inclusive_scan(c0 + c1);
+      if (lane_id() == 63) wtot[wave_id()] = inc;
+      __syncthreads();
+      uint32_t run = inc - c0 - c1;
+      for (int w = 0; w < wave_id(); ++w) run += wtot[w];
+      bcur[2 * t] = run;
+      bcur[2 * t + 1] = run + c0;
     }
+    __syncthreads();
+    for (uint32_t i = t; i < nt; i += kTmThreads) member[atomicAdd(&bcur[(uint32_t)(key[i] >> 54)], 1u)] = (uint16_t)i;
+    __syncthreads();
+    for (uint32_t i = t; i < nt; i += kTmThreads) {   // rank = bin start + smaller (key, index) in the bin
+      const uint64_t a = key[i];
+      const uint32_t d = (uint32_t)(a >> 54), end = bcur[d], beg = end - bcnt[d];
+      uint32_t r = beg;
+      for (uint32_t m = beg; m < end; ++m) {
+        const uint32_t x = member[m];
+        const uint64_t b = key[x];
+        r += (b < a || (b == a && x < i)) ? 1u : 0u;
+      }
+      rnk[i] = (uint16_t)r;
+    }
+    __syncthreads();
     uint32_t* o = out + (uint64_t)outoff[k] * kTmWords;
-    for (uint32_t j = t; j < words; j += kBlock) {
-      const uint32_t r = j / kTmWords, c = j - r * kTmWords;
-      const uint32_t i = (uint32_t)(key[r] & (kTmCap - 1));
-      __builtin_nontemporal_store(stage[i * kTmWords + c], o + j);
+#pragma unroll
+    for (uint32_t h = 0; h < kTmRows; ++h) {
+      const uint32_t i = t + h * kTmThreads;
+      if (i < nt) {
+        uint32_t* dst = o + (uint32_t)rnk[i] * kTmWords;
+        // plain stores: a row is a partial line, completed in L2 by its neighbours (nontemporal
+        // stores write the partial lines through: 61 -> 397 ms per 125 GB received)
+#pragma unroll
+        for (int q = 0; q < 6; ++q) *reinterpret_cast<u32x4u*>(dst + 4 * q) = v[h][q];
+        dst[24] = tail[h];
+      }
     }
     __syncthreads();
   }
@@ -150,16 +169,16 @@ DR_API int dr_ts_fine_starts(const E64* ent, uint64_t n, uint32_t fb, uint32_t* 
 
 DR_API uint32_t dr_ts_tile_cap() { return kTmCap; }
 
-// rows / out: 100-byte rows (4-byte aligned); pre, cnt: [W][K]; outoff: [K]; 25 <= fb <= 32.
+// rows / out: 100-byte rows (4-byte aligned); pre, cnt: [W][K]; outoff: [K]; 16 <= fb <= 32.
 DR_API int dr_ts_tile_merge(const uint8_t* rows, uint8_t* out, const int64_t* pre, const int32_t* cnt,
                             const int64_t* outoff, uint32_t W, uint32_t K, uint32_t fb, uint32_t* overflow,
                             hipStream_t s) {
-  if (W == 0 || W > kTmMaxW || fb < 25 || fb > 32) return (int)hipErrorInvalidValue;
+  if (W == 0 || W > kTmMaxW || fb < 16 || fb > 32) return (int)hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(out)) & 3) return (int)hipErrorInvalidValue;
   if (K == 0) return 0;
   const unsigned g = K < 65536u ? K : 65536u;
-  ts_tile_merge_kernel<<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows), reinterpret_cast<uint32_t*>(out),
-                                         pre, cnt, outoff, W, K, fb, overflow);
+  ts_tile_merge_kernel<<<g, kTmThreads, 0, s>>>(reinterpret_cast<const uint32_t*>(rows),
+                                                reinterpret_cast<uint32_t*>(out), pre, cnt, outoff, W, K, fb, overflow);
   DR_LAUNCH_CHECK();
   return 0;
 }

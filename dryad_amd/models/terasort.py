@@ -396,7 +396,7 @@ class TeraSortLoopbackJob:
 
         def send_side(s):
             TS.gen_entries64(e, s * n, seed, hist=False)
-            srt = S.sort_entries64(e, tmp, 32, lookback=False)
+            srt = S.sort_entries64(e, tmp, 8 * ((fb + 7) // 8), lookback=False)
             starts = TS.fine_starts(srt, fb)
             return srt, starts, starts.index_select(0, Lt).tolist()
         sizes, fine = [], []

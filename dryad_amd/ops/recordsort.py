@@ -322,9 +322,10 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
 
 
 # Fine buckets of the gen:// exchange: the top ``fb`` key bits, about FINE_ROWS rows of the whole
-# job each (at most tile_cap() = 512 are ordered in LDS), fb >= 25 so that a bucket's remaining
-# key bits and its 9-bit tile index fit one 64-bit LDS sort key.
-FINE_MIN_BITS, FINE_MAX_BITS, FINE_ROWS = 25, 28, 300
+# job each (at most tile_cap() = 1024 are ordered by one workgroup); 16 <= fb <= 24, so the send
+# side's sort needs at most three 8-bit look-back passes and a bucket's remaining key bits fit
+# one 64-bit word.
+FINE_MIN_BITS, FINE_MAX_BITS, FINE_ROWS = 16, 24, 600
 
 
 def fine_bits(total_rows: int) -> int:
@@ -348,7 +349,8 @@ def fine_hi_bounds(L: list, fb: int, g: int) -> tuple[int, int]:
 def pack_gen_fine(bufs: SortBuffers, gen: tuple[int, int], n: int, seps_hi: list, B: int, W: int, fb: int):
     """Send side over gen://terasort records gen[0] .. gen[0] + n - 1 for the fine-bucket exchange:
     E64 entries from the generator (key bytes 0..3 as the window, with the look-back sort's digit
-    histograms), one look-back sort of them (stable), the fine-bucket starts of the sorted order.
+    histograms), one look-back sort of them on the top 8 * ceil(fb / 8) key bits (stable), the
+    fine-bucket starts of the sorted order.
     Key range g = fine buckets [L[g], L[g + 1]) is then the contiguous run of sorted entries
     [S[L[g]], S[L[g + 1]]), and the send buffer (``bufs.rows_out``) is packed round-major (round b
     = range r * B + b for every destination r), each range's records generated in key order
@@ -358,7 +360,8 @@ def pack_gen_fine(bufs: SortBuffers, gen: tuple[int, int], n: int, seps_hi: list
     e, tmp = bufs.ent_a.view(-1)[:n], bufs.ent_b.view(-1)[:n]
     hist = TSG.gen_entries64(e, gen[0], gen[1])
     err = S.lookback_error()
-    srt = S.sort_entries64(e, tmp, 32, gen_hist=hist, err=err)
+    win = 8 * ((fb + 7) // 8)
+    srt = S.sort_entries64(e, tmp, win, gen_hist=hist, err=err)
     starts = TSG.fine_starts(srt, fb)
     L = fine_bounds(seps_hi, fb)
     Lt = torch.tensor(L, dtype=torch.int64, device=e.device)
@@ -366,7 +369,7 @@ def pack_gen_fine(bufs: SortBuffers, gen: tuple[int, int], n: int, seps_hi: list
     Sg = host[:-1]
     if host[-1]:                 # the look-back sort gave up: entries again, count + scatter passes
         TSG.gen_entries64(e, gen[0], gen[1], hist=False)
-        srt = S.sort_entries64(e, tmp, 32, lookback=False)
+        srt = S.sort_entries64(e, tmp, win, lookback=False)
         starts = TSG.fine_starts(srt, fb)
         Sg = starts.index_select(0, Lt).tolist()
     counts = starts[1:] - starts[:-1]
@@ -378,11 +381,14 @@ def pack_gen_fine(bufs: SortBuffers, gen: tuple[int, int], n: int, seps_hi: list
             acc += size[b][r]
     st.append(acc)
 
+    # one generator launch per round: segment r = {send row - round start, first sorted entry}
+    segs = torch.tensor([[[st[b * W + r] - st[b * W], Sg[r * B + b]] for r in range(W)] for b in range(B)],
+                        dtype=torch.int64).to(e.device)
+
     def pack(b: int):
-        for r in range(W):
-            g, m = r * B + b, size[b][r]
-            if m:
-                TSG.gen_gather64(bufs.rows_out[st[b * W + r]: st[b * W + r] + m], srt[Sg[g]: Sg[g + 1]], gen[0], gen[1])
+        a, z = st[b * W], st[(b + 1) * W]
+        if z > a:
+            TSG.gen_gather64(bufs.rows_out[a:z], srt, gen[0], gen[1], seg=segs[b], n=z - a)
     return st, pack, counts, L
 
 
@@ -407,9 +413,16 @@ def merge_received_rounds(bufs: SortBuffers, off: list, fine: torch.Tensor, L: l
     have gone out (``sent_after``, as in sort_received_rounds).  A bucket too large for LDS (heavy
     key skew) flags its round, which is then sorted after the last round with local_sort_rows."""
     out = bufs.rows_out
-    W = fine.shape[0]
+    W, Kme = fine.shape
     flags = torch.zeros(B, dtype=torch.int32, device=out.device)
     base = L[rank * B]
+    # slice starts of every bucket from one flat scan of all sources' counts (a 1-D device scan;
+    # per round only elementwise differences): ex[s, k] = rows of source s before bucket k
+    fine = fine.contiguous()
+    ex = (torch.cumsum(fine.view(-1), 0, dtype=torch.int64).view(W, Kme) - fine)
+    ex = ex - ex[:, :1]
+    col = fine.sum(0, dtype=torch.int64)
+    cex = torch.cumsum(col, 0) - col
     pending = []
     for b in range(B):
         if wait is not None:
@@ -417,13 +430,13 @@ def merge_received_rounds(bufs: SortBuffers, off: list, fine: torch.Tensor, L: l
         a, z = off[b], off[b + 1]
         if z > a:
             g = rank * B + b
-            cnt = fine[:, L[g] - base: L[g + 1] - base].contiguous()
-            rows_per_src = cnt.sum(1, dtype=torch.int64)
-            pre = (torch.cumsum(cnt, 1, dtype=torch.int64) - cnt
-                   + (torch.cumsum(rows_per_src, 0) - rows_per_src + a).view(W, 1)).contiguous()
-            col = cnt.sum(0, dtype=torch.int64)
-            outoff = (torch.cumsum(col, 0) - col + a).contiguous()
-            pending.append((a, z, b, pre, cnt, outoff))
+            k0, k1 = L[g] - base, L[g + 1] - base
+            cnt = fine[:, k0:k1]
+            exr = ex[:, k0:k1] - ex[:, k0:k0 + 1]                       # within the range
+            rows_per_src = (ex[:, k1:k1 + 1] if k1 < Kme else (ex[:, -1:] + fine[:, -1:])) - ex[:, k0:k0 + 1]
+            pre = (exr + (torch.cumsum(rows_per_src, 0) - rows_per_src) + a).contiguous()
+            outoff = (cex[k0:k1] - cex[k0] + a).contiguous()
+            pending.append((a, z, b, pre, cnt.contiguous(), outoff))
         keep = []
         for item in pending:
             a2, z2, b2, pre, cnt, outoff = item

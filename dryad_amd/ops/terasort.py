@@ -107,7 +107,8 @@ def gen_gather(out: torch.Tensor, idx: torch.Tensor, first: int, seed: int) -> t
 
 
 _lib.register_signatures({
-    "dr_terasort_gen_gather64": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u64, c_u64, c_u64, ctypes.c_void_p]),
+    "dr_terasort_gen_gather64": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u64, c_u64, c_u64, ctypes.c_void_p,
+                                                c_u32, ctypes.c_void_p]),
     "dr_terasort_gen_entries64": (ctypes.c_int, [ctypes.c_void_p, c_u64, c_u64, c_u64, c_u32, ctypes.c_void_p,
                                                  ctypes.c_void_p]),
     "dr_ts_fine_starts": (ctypes.c_int, [ctypes.c_void_p, c_u64, c_u32, ctypes.c_void_p, ctypes.c_void_p]),
@@ -133,14 +134,22 @@ def gen_entries64(keys: torch.Tensor, first: int, seed: int, hist: bool = True):
     return part
 
 
-def gen_gather64(out: torch.Tensor, ent: torch.Tensor, first: int, seed: int) -> torch.Tensor:
-    """``out[p]`` := record ``first + (ent[p] & 0xFFFFFFFF)`` (``ent`` int64 [m] sorted E64 entries)."""
+def gen_gather64(out: torch.Tensor, ent: torch.Tensor, first: int, seed: int, seg: torch.Tensor | None = None,
+                 n: int | None = None) -> torch.Tensor:
+    """``out[p]`` := record ``first + (ent[q] & 0xFFFFFFFF)`` (``ent`` int64 sorted E64 entries),
+    q = p, or with ``seg`` (device int64 [nseg, 2] of {out row, entry}, ascending, seg[0, 0] = 0,
+    nseg <= 64) q = seg[s, 1] + p - seg[s, 0] for the last segment starting at or before p; ``n``
+    rows (default ``ent``'s length)."""
     _lib.require_gpu_tensor(out, "terasort.gen_gather64")
-    m = ent.shape[0]
+    m = ent.shape[0] if n is None else n
     assert out.dtype == torch.uint8 and out.shape[0] >= m and out.shape[1] == RECORD_BYTES and out.is_contiguous()
     assert ent.dtype == torch.int64 and ent.is_contiguous()
+    nseg = 0
+    if seg is not None:
+        assert seg.dtype == torch.int64 and seg.is_contiguous() and seg.dim() == 2 and seg.shape[1] == 2
+        nseg = seg.shape[0]
     _lib.call("dr_terasort_gen_gather64", ptr(out), ptr(ent), c_u64(m), c_u64(first), c_u64(seed & (2**64 - 1)),
-              stream_of(out))
+              ptr(seg), c_u32(nseg), stream_of(out))
     return out[:m]
 
 

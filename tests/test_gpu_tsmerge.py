@@ -52,7 +52,7 @@ def test_tile_merge_orders_buckets_and_flags_overflow():
     g = np.random.default_rng(3)
     W, K, fb = 3, 40, 25
     cnt = g.integers(0, 120, size=(W, K)).astype(np.int32)
-    cnt[1, 7] = 600                               # a bucket past the LDS capacity
+    cnt[1, 7] = 1100                              # a bucket past one workgroup's capacity
     total = int(cnt.sum())
     rows = g.integers(0, 256, size=(total, 100), dtype=np.uint8)
     # rows of bucket k share their top fb key bits: bucket id in the first 25 bits, random below
@@ -86,6 +86,14 @@ def test_tile_merge_orders_buckets_and_flags_overflow():
             assert not seg.any()                  # left out for the caller's fallback
         else:
             assert np.array_equal(seg, exp), k
+
+
+def test_fine_bits_keep_buckets_small():
+    assert RS.fine_bits(10_000_000_000) == 24          # 8 ranks x 1.25e9: ~600 rows per bucket
+    assert RS.fine_bits(1000) == 16
+    for total in (2_500_000_000, 5_000_000_000, 10_000_000_000):
+        assert total / (1 << RS.fine_bits(total)) <= 1.01 * RS.FINE_ROWS
+    assert TS.tile_cap() >= 1.5 * RS.FINE_ROWS
 
 
 @pytest.mark.parametrize("W,rank", [(4, 1), (2, 0)])
