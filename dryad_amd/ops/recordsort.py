@@ -454,23 +454,6 @@ def merge_received_rounds(bufs: SortBuffers, off: list, fine: torch.Tensor, L: l
     return out[: off[-1]]
 
 
-def pack_gen(bufs: SortBuffers, gen: tuple[int, int], n: int, seps: torch.Tensor, lo_or: int, lo_mask: int,
-             B: int, W: int):
-    """Send side over gen://terasort records gen[0] .. gen[0] + n - 1: the records' bucket order
-    from the generator's keys (``dest_partition_gen``: 32-bit offsets into the first 4n bytes of
-    ``bufs.ent_a``), then a packer generating round b's records into their send rows.  Returns
-    (bucket starts as a host list, pack(b)).  The offsets are dead once every round is packed, so
-    the receive side may reuse ``ent_a`` after the last pack (stream order)."""
-    idx = bufs.ent_a.view(-1).view(torch.int32)[:n]
-    st = S.dest_partition_gen(gen[0], gen[1], n, seps, lo_or, lo_mask, B, W, idx).tolist()
-
-    def pack(b: int):
-        a, z = st[b * W], st[(b + 1) * W]
-        if z > a:
-            TSG.gen_gather(bufs.rows_out[a:z], idx[a:z], gen[0], gen[1])
-    return st, pack
-
-
 def sort_received_rounds(bufs: SortBuffers, off: list, sent_after: list, n_sent: int, seps_hi: list, B: int,
                          rank: int, key_off: int, key_len: int, wait=None) -> torch.Tensor:
     """Receive side of the pipelined range shuffle: round b's block ``rows_in[off[b]:off[b+1]]``

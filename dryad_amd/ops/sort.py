@@ -443,34 +443,10 @@ def _hi_range64(e: torch.Tensor, chunk: int = 1 << 26) -> tuple[int, int]:
 
 
 _lib.register_signatures({
-    "dr_ts_dest_workspace": (c_u64, [c_u64]),
-    "dr_ts_dest_partition": (ctypes.c_int, [c_u64, c_u64, c_u64, ctypes.c_void_p, c_u32, c_u64, c_u64, c_u32, c_u32,
-                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "dr_extract_keys64_tile_parts": (c_u32, [c_u64]),
     "dr_extract_keys64_tile": (ctypes.c_int, [ctypes.c_void_p, c_u64, c_u32, c_u32, c_u32, c_u32, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p]),
 })
-
-
-def dest_partition_gen(first: int, seed: int, n: int, seps: torch.Tensor, lo_or: int, lo_mask: int, subs: int,
-                       ranks: int, idx: torch.Tensor) -> torch.Tensor:
-    """Range partition of gen://terasort records ``first .. first + n - 1`` without entries
-    (dr_ts_dest_partition): ``idx[:n]`` (int32) receives the slice offsets in bucket order, stable;
-    returns the 257 bucket starts (device int64).  Buckets as ``range_dest``: the count of
-    ``seps`` below the key {hi, (lo | lo_or) & lo_mask}, renumbered round-major with ``subs``."""
-    assert idx.dtype == torch.int32 and idx.numel() >= n and seps.dtype == torch.int64
-    starts = torch.empty(257, dtype=torch.int64, device=idx.device)
-    ws = _dest_workspace(n, idx.device)
-    seps = seps.contiguous()
-    _lib.call("dr_ts_dest_partition", c_u64(first), c_u64(seed & _M64), c_u64(n), ptr(seps), c_u32(seps.shape[0]),
-              c_u64(lo_or & _M64), c_u64(lo_mask & _M64), c_u32(subs), c_u32(ranks), ptr(ws), ptr(idx), ptr(starts),
-              stream_of(idx))
-    return starts
-
-
-def _dest_workspace(n: int, device) -> torch.Tensor:
-    nbytes = int(_lib.lib().dr_ts_dest_workspace(c_u64(max(n, 1))))
-    return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
 
 def extract_keys64_tile(rows: torch.Tensor, key_off: int, key_len: int, prefix_bits: int, out: torch.Tensor,

@@ -2,9 +2,8 @@
 
     python tools/micro/ts_rank_phases.py [rows]
 
-* sender: bucket order of the record offsets from the generator's keys over 128 ranges (W=8 x
-  B=16), the records generated into their send rows (100-byte pitch);
-* receiver: E64 key extraction from 100-byte rows (row per lane / LDS tiles with the histograms),
+* (the send side of generated inputs: tools/micro/ts_send_ab.py)
+* receiver of stored-row inputs: E64 key extraction from 100-byte rows (row per lane / LDS tiles with the histograms),
   look-back radix sort, row gather + fix-up;
 * ``--locality``: the row gather again with sources confined to windows of 2^k rows (how much of
   the random 100-byte row reads a locality-clustered layout would turn into cache hits).
@@ -41,18 +40,6 @@ def main():
     ent = torch.empty((n, 2), dtype=torch.int64, device=dev)        # E128 (sender) / 2 x E64 (receiver)
     seed = 7
     print(f"rows {n:.3g} ({n * 100 / 1e9:.0f} GB)", flush=True)
-
-    # ---- sender (generated input): bucket order from the generator's keys, records into the send rows
-    W, B = 8, 16
-    M64 = (1 << 64) - 1
-    from dryad_amd.ops import recordsort as RS
-    samp = RS.gen_samples((0, seed), n, 0, 0, M64, 1 << 20, 314159, dev)
-    seps = RS.separators_from_samples(samp, W * B)
-    idx = ent.view(-1).view(torch.int32)[:n]
-    t = timed(lambda: S.dest_partition_gen(0, seed, n, seps, 0, M64, B, W, idx), reps=2)
-    print(f"dest partition (gen keys)  {t:8.2f} ms", flush=True)
-    t = timed(lambda: TS.gen_gather(out, idx, 0, seed), reps=2)
-    print(f"gen gather (send rows)     {t:8.2f} ms", flush=True)
 
     # ---- receiver (one range block of n rows)
     TS.generate(rows, 0, seed)
