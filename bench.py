@@ -160,7 +160,8 @@ def main():
                 # HBM input table the local sort gathers from, with several ranks straight into
                 # the all-to-all send buckets (the read stage fused with the range partition)
                 "input": "gen://terasort, generated in the timed step" + (
-                    " into the send buckets (read fused with the range partition)" if world.size > 1 and not args.direct
+                    ": sort entries first, then the records into the send rows in key order (the read fused with "
+                    "the range partition)" if world.size > 1 and not args.direct
                     else " into the HBM input table" + ("" if args.direct else
                                                          " (records at a 128-byte pitch: one aligned HBM line each)")),
             },
