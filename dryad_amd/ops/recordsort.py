@@ -246,8 +246,8 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     CrossProduct channels GraphBuilder.cs:481-504)."""
     w = world or get_world()
     rows = bufs.rows_in[:n]
-    gen_path = gen is not None and w.size > 1 and key_off == 0 and key_len == TSG.KEY_BYTES \
-        and rows.shape[1] == TSG.RECORD_BYTES and n < (1 << 31)
+    gen_path = gen is not None and 1 < w.size <= 64 and key_off == 0 and key_len == TSG.KEY_BYTES \
+        and rows.shape[1] == TSG.RECORD_BYTES and n < (1 << 31)       # (64: sources per merged bucket)
     if gen is not None and not gen_path:
         TSG.generate(rows, gen[0], gen[1])       # the records are needed after all
         gen = None
