@@ -302,6 +302,8 @@ PYBIND11_MODULE(_dryad_native, m) {
       .def(py::init<const std::string&, const std::vector<uint64_t>&, int, int64_t, bool>(), py::arg("path"),
            py::arg("buffers"), py::arg("threads"), py::arg("extend_bytes") = (int64_t)(256ll << 20),
            py::arg("mapped") = false)
+      .def(py::init<const std::vector<std::string>&, const std::vector<uint64_t>&, int, int64_t>(),
+           py::arg("paths"), py::arg("buffers"), py::arg("threads"), py::arg("extend_bytes") = (int64_t)(256ll << 20))
       .def("acquire", [](ChunkWriter& w) {
         int s;
         {
@@ -311,10 +313,14 @@ PYBIND11_MODULE(_dryad_native, m) {
         if (s < 0) throw std::runtime_error("ChunkWriter: " + w.error());
         return s;
       })
-      .def("submit", &ChunkWriter::submit)
+      .def("submit", &ChunkWriter::submit, py::arg("slot"), py::arg("offset"), py::arg("bytes"), py::arg("file") = 0)
       .def("finish", [](ChunkWriter& w, int64_t size) {
         py::gil_scoped_release nogil;
         return w.finish(size);
+      })
+      .def("finish_all", [](ChunkWriter& w, const std::vector<int64_t>& sizes) {
+        py::gil_scoped_release nogil;
+        return w.finish_all(sizes);
       })
       .def("error", &ChunkWriter::error)
       .def("abort", [](ChunkWriter& w) {

@@ -122,6 +122,9 @@ _DEFAULTS = dict(
     StreamChunkBytes=4 << 30,     # ... and their chunk size
     GraceJoin=None,               # a Join as the partitioned grace join stage (runtime/grace_stage.py;
     #                               None: when its inputs would crowd the HBM budget; False: never)
+    PartFileSplitBytes=0,         # GPU executor: a fixed-width partfile:// output partition of at least
+    #                               this many bytes is written as several part files at once (0: one
+    #                               part file per partition, as the reference; io/writer.split_count)
 )
 
 _READONLY_AFTER_USE = set(_DEFAULTS) - {"LocalDebug"}

@@ -166,3 +166,79 @@ def write_device(path: str, data: torch.Tensor, stats: WriteStats | None = None)
     with PartWriter(path, data.device if isinstance(data, torch.Tensor) else None, stats) as w:
         w.write(data)
     return w.off
+
+
+# A large partition may be written as several part files at once (context PartFileSplitBytes, at
+# most SPLIT_MAX files): page-cache writes to one file serialise on its inode lock (~12 GB/s on the
+# MI355X box), to distinct files they do not (40-93 GB/s, profiles/r4/filewrite_ab2.log).
+SPLIT_MAX = 8
+
+
+def write_device_pieces(paths: list, data: torch.Tensor, bounds: list, stats: WriteStats | None = None) -> list:
+    """Write byte ranges [bounds[i], bounds[i + 1]) of ``data`` (a contiguous device or host tensor)
+    to ``paths[i]``, every file at once: the chunks go out round-robin over the files, so the
+    writer threads work on distinct inodes.  Returns the file sizes."""
+    from ..native import runtime
+    from ..ops import _lib
+    k = len(paths)
+    assert len(bounds) == k + 1 and bounds[0] == 0
+    flat = data.reshape(-1).view(torch.uint8)
+    assert bounds[-1] <= flat.numel()
+    t0 = time.perf_counter()
+    ring = _ring()
+    with _RING_LOCK:
+        w = runtime().ChunkWriter(list(paths), [b.tensor.data_ptr() for b in ring], THREADS)
+        dev_src = flat.is_cuda
+        cs = None
+        if dev_src:
+            cs = torch.cuda.Stream(flat.device)
+            cs.wait_stream(torch.cuda.current_stream(flat.device))
+            flat.record_stream(cs)
+        piece = min(CHUNK, ring[0].tensor.numel())
+        pending = deque()
+        done = False
+        try:
+            offs = [0] * k
+            while any(bounds[i] + offs[i] < bounds[i + 1] for i in range(k)):
+                for i in range(k):
+                    a = bounds[i] + offs[i]
+                    m = min(piece, bounds[i + 1] - a)
+                    if m <= 0:
+                        continue
+                    while pending and (pending[0][1] is None or pending[0][1].query()):
+                        slot, ev, f, off, n = pending.popleft()
+                        w.submit(slot, off, n, f)
+                    while len(pending) > SLOTS - 2:
+                        slot, ev, f, off, n = pending.popleft()
+                        if ev is not None:
+                            ev.synchronize()
+                        w.submit(slot, off, n, f)
+                    slot = w.acquire()
+                    dst = ring[slot].tensor[:m]
+                    if dev_src:
+                        _lib.memcpy_async(dst, flat[a:a + m], cs)
+                        ev = torch.cuda.Event()
+                        ev.record(cs)
+                    else:
+                        ctypes.memmove(dst.data_ptr(), flat[a:a + m].data_ptr(), m)
+                        ev = None
+                    pending.append((slot, ev, i, offs[i], m))
+                    offs[i] += m
+            while pending:
+                slot, ev, f, off, n = pending.popleft()
+                if ev is not None:
+                    ev.synchronize()
+                w.submit(slot, off, n, f)
+            sizes = [bounds[i + 1] - bounds[i] for i in range(k)]
+            w.finish_all(sizes)
+            done = True
+        finally:
+            if not done:
+                for _, ev, _, _, _ in pending:
+                    if ev is not None:
+                        ev.synchronize()
+                w.abort()
+    if stats is not None:
+        stats.bytes += bounds[-1]
+        stats.seconds += time.perf_counter() - t0
+    return sizes

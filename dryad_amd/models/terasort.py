@@ -171,6 +171,11 @@ class TeraSortStoredJob:
         self.ctx = D.DryadLinqContext(platform="gpu")
         self.ctx.PartitionCount = W
         self.ctx._props["ShuffleSlack"] = cfg.slack
+        # the sorted output: each rank's partition as several part files written at once (one
+        # file's page-cache writes serialise on its inode lock, profiles/r4/filewrite_ab2.log)
+        self.ctx.PartFileSplitBytes = 2 << 30
+        self.prep_ctx = D.DryadLinqContext(platform="gpu")
+        self.prep_ctx.PartitionCount = W
         self.src, self.dst = src, dst
         self.gen = f"gen://terasort?records={self.n * W}&partitions={W}&seed={cfg.seed}"
         self.res = None
@@ -191,8 +196,8 @@ class TeraSortStoredJob:
                 self.prepared = dict(reused=True)
                 return self.prepared
         t0 = time.perf_counter()
-        self.ctx.FromStore(self.gen).ToStore(self.src, delete_if_exists=True).SubmitAndWait()
-        r = self.ctx._get_executor().last_result or {}
+        self.prep_ctx.FromStore(self.gen).ToStore(self.src, delete_if_exists=True).SubmitAndWait()
+        r = self.prep_ctx._get_executor().last_result or {}
         w = r.get("write") or {}
         self.prepared = dict(reused=False, seconds=round(time.perf_counter() - t0, 2),
                              write_GBps=round(w.get("bytes", 0) / 1e9 / max(w.get("seconds", 0), 1e-9), 2))
@@ -219,38 +224,44 @@ class TeraSortStoredJob:
     input_checksum = TeraSortQueryJob.input_checksum
 
     def validate(self, expect_hash: int, expect_records: int) -> dict:
-        """valsort over this rank's output part, streamed back through the chunked reader."""
+        """valsort over the output table streamed back through the chunked reader: rank r checks
+        the part files i with i % W == r (hash sum, count, in-part order), the first / last key of
+        every part are all-gathered to check the order across parts."""
         from ..io import partfile as PF
         from ..io import reader as RD
         from ..io.providers import parse_uri
-        dev = self.world.device
+        dev, W, me = self.world.device, self.world.size, self.world.rank
         meta = PF.read_meta(parse_uri(self.dst)[1])
-        path = meta.part_path(self.world.rank)
-        n = meta.parts[self.world.rank].size // RECORD
         acc = torch.zeros(2, dtype=torch.int64, device=dev)
-        step = min(max(n, 1), 1 << 26)
-        buf = torch.empty((step, RECORD), dtype=torch.uint8, device=dev)
-        bad_edges, prev, first = 0, None, None
-        for c0 in range(0, n, step):
-            c1 = min(n, c0 + step)
-            rows = RD.read_rows_to_device(path, dev, c0 * RECORD, c1 - c0, RECORD, buf)
-            TS.check(rows, acc)
-            a, b = bytes(rows[0, :KEYLEN].cpu().numpy()), bytes(rows[-1, :KEYLEN].cpu().numpy())
-            first = a if first is None else first
-            if prev is not None and prev > a:
-                bad_edges += 1
-            prev = b
+        ends = torch.zeros((meta.count, 2 * KEYLEN + 1), dtype=torch.uint8, device=dev)
+        n_mine, bad_edges = 0, 0
+        buf = None
+        for i in range(me, meta.count, W):
+            path = meta.part_path(i)
+            n = meta.parts[i].size // RECORD
+            n_mine += n
+            step = min(max(n, 1), 1 << 26)
+            if buf is None or buf.shape[0] < step:
+                buf = torch.empty((step, RECORD), dtype=torch.uint8, device=dev)
+            prev = None
+            for c0 in range(0, n, step):
+                c1 = min(n, c0 + step)
+                rows = RD.read_rows_to_device(path, dev, c0 * RECORD, c1 - c0, RECORD, buf)
+                TS.check(rows, acc)
+                a, b = bytes(rows[0, :KEYLEN].cpu().numpy()), bytes(rows[-1, :KEYLEN].cpu().numpy())
+                if c0 == 0:
+                    ends[i, 0] = 1
+                    ends[i, 1:1 + KEYLEN] = rows[0, :KEYLEN]
+                if prev is not None and prev > a:
+                    bad_edges += 1
+                prev = b
+                ends[i, 1 + KEYLEN:] = rows[-1, :KEYLEN]
         del buf
-        tot = torch.tensor([int(acc[0].item()), n, int(acc[1].item()) + bad_edges], dtype=torch.int64, device=dev)
+        tot = torch.tensor([int(acc[0].item()), n_mine, int(acc[1].item()) + bad_edges], dtype=torch.int64, device=dev)
         shuffle.all_reduce_(tot, "sum", self.world)
-        ends = torch.zeros((1, 2 * KEYLEN + 1), dtype=torch.uint8, device=dev)
-        if n:
-            ends[0, 0] = 1
-            ends[0, 1:1 + KEYLEN] = torch.frombuffer(bytearray(first), dtype=torch.uint8)
-            ends[0, 1 + KEYLEN:] = torch.frombuffer(bytearray(prev), dtype=torch.uint8)
-        allends = shuffle.all_gather_tensor(ends, self.world).cpu().numpy()
+        shuffle.all_reduce_(ends, "sum", self.world)          # every part's row comes from one rank
         boundary_ok, last = True, None
-        for row in allends:
+        for row in ends.cpu().numpy():
             if row[0] == 0:
                 continue
             if last is not None and last > bytes(row[1:1 + KEYLEN]):
@@ -259,7 +270,7 @@ class TeraSortStoredJob:
         h = int(tot[0].item())
         ok = h == expect_hash and int(tot[2].item()) == 0 and int(tot[1].item()) == expect_records and boundary_ok
         return dict(ok=bool(ok), hash_match=h == expect_hash, violations=int(tot[2].item()),
-                    records=int(tot[1].item()), boundary_ok=boundary_ok)
+                    records=int(tot[1].item()), boundary_ok=boundary_ok, parts=meta.count)
 
 
 class TeraSortOOCJob:

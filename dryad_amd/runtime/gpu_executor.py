@@ -1522,9 +1522,8 @@ def _commit_partfile_impl(runner, s, uri, path, local):
         if rows_fmt:
             # raw fixed-width rows: device rows or the pinned host tier (out-of-core sort output)
             if isinstance(v, DeviceTable):
-                WR.write_device(tmp, v.rows[: v.n], stats=runner.write_stats)
+                mine[p] = _write_split(runner, tmp, v.rows[: v.n], v.n, v.rows.shape[1])
                 fmt_extra = dict(stride=v.rows.shape[1], key_off=v.shape.key_off, key_len=v.shape.key_len)
-                mine[p] = tmp
                 continue
             if getattr(v, "path", None) and os.path.exists(v.path):
                 # disk tier: the rows already are a file; flush it and rename it into place
@@ -1552,6 +1551,9 @@ def _commit_partfile_impl(runner, s, uri, path, local):
                 f.write(gzip.compress(raw, compresslevel=6))
         elif data is not None:
             # device-encoded records: HBM -> pinned ring -> native writer threads
+            if index is None and v.n and data.numel() % v.n == 0:      # fixed-width records
+                mine[p] = _write_split(runner, tmp, data, v.n, data.numel() // v.n)
+                continue
             WR.write_device(tmp, data, stats=runner.write_stats)
             if index is not None:
                 PF.write_index(tmp, index[0], index[1], index[2], index[3])
@@ -1569,7 +1571,10 @@ def _commit_partfile_impl(runner, s, uri, path, local):
         parts = {}
         for d in gathered:
             parts.update(d)
-        PF.commit_parts(path, base, [parts[p] for p in range(s.partitions)])
+        chosen = []                 # a split partition contributes its part files in order
+        for p in range(s.partitions):
+            chosen.extend(parts[p] if isinstance(parts[p], list) else [parts[p]])
+        PF.commit_parts(path, base, chosen)
         if rows_fmt:
             extras = [x for x in gathered_fmt if x] if W > 1 else [fmt_extra]
             write_schema(path, dt, "rows", **(extras[0] if extras and extras[0] else {}))
@@ -1578,6 +1583,24 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     if W > 1:
         runner.world.barrier()
     return True
+
+
+def _write_split(runner, tmp: str, data, n: int, rec: int):
+    """Write ``n`` fixed-width records of ``rec`` bytes (``data``) to the part file ``tmp``, or, with
+    ``PartFileSplitBytes`` set and at least that many bytes, to several part files at once split at
+    record boundaries (io/writer.write_device_pieces).  Returns the tmp path or the list of them."""
+    from ..io import writer as WR
+    split = int(runner.ctx.PartFileSplitBytes or 0)
+    nbytes = n * rec
+    k = min(WR.SPLIT_MAX, nbytes // split) if split > 0 else 1
+    if k <= 1:
+        WR.write_device(tmp, data, stats=runner.write_stats)
+        return tmp
+    per = -(-n // k)
+    bounds = [min(n, j * per) * rec for j in range(k + 1)]
+    paths = [f"{tmp}.{j}" for j in range(k)]
+    WR.write_device_pieces(paths, data, bounds, stats=runner.write_stats)
+    return paths
 
 
 GpuJobRunner._commit_partfile = lambda self, s, uri, path, local: _commit_partfile_impl(self, s, uri, path, local)
