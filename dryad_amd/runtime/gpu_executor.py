@@ -936,8 +936,13 @@ class GpuJobRunner:
         self.grace_joins = GS.find(self.plan) if self.gpu_ok else {}
         join_first = {min(d["stages"]): jid for jid, d in list(self.fused_joins.items()) + list(self.grace_joins.items())}
         precomputed = {}
+        stage_events = []          # (timing key, host seconds, start event, end event)
         for s in self.plan.stages:
             t0 = time.time()
+            ev0 = None
+            if self.gpu_ok:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record(torch.cuda.current_stream(self.dev))
             status, err = 0, ""
             if s.id in join_first:
                 jid = join_first[s.id]
@@ -1011,9 +1016,19 @@ class GpuJobRunner:
             else:
                 self._run_stage(s, ready, refresh, now)
             self._release(s)
-            if self.gpu_ok:
-                torch.cuda.synchronize(self.dev)
-            self.timings[f"{s.id}:{s.name}"] = time.time() - t0
+            # no synchronize between stages: the next stage's launches queue behind this one's
+            # (a k-means iteration's four stages left the GPU idle while the host set up the
+            # next); the stage time is its GPU span (events) or its host time, if longer
+            if ev0 is not None:
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record(torch.cuda.current_stream(self.dev))
+                stage_events.append((f"{s.id}:{s.name}", time.time() - t0, ev0, ev1))
+            else:
+                self.timings[f"{s.id}:{s.name}"] = time.time() - t0
+        if stage_events:
+            stage_events[-1][3].synchronize()
+            for key, host_s, ev0, ev1 in stage_events:
+                self.timings[key] = max(host_s, ev0.elapsed_time(ev1) / 1e3)
         committed = self._commit()
         if self.pool is not None:
             for b in set(self.row_sets.values()):

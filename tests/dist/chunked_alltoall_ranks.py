@@ -50,3 +50,7 @@ def main():
 
 if __name__ == "__main__":
     main()
+    # tear the process group down before the interpreter exits: gloo's threads torn down during
+    # finalisation abort the process now and then ("terminate called without an active exception")
+    from dryad_amd.parallel.comm import shutdown
+    shutdown()

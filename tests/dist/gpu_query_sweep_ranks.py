@@ -208,3 +208,7 @@ def memory_check(g, w):
 
 if __name__ == "__main__":
     main()
+    # tear the process group down before the interpreter exits: gloo's threads torn down during
+    # finalisation abort the process now and then ("terminate called without an active exception")
+    from dryad_amd.parallel.comm import shutdown
+    shutdown()
