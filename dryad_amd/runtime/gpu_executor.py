@@ -1664,6 +1664,7 @@ def flush_job_dirs():
 
 
 def _write_plan_files(d, plan):
+    os.makedirs(os.path.join(d, "log"), exist_ok=True)
     with open(os.path.join(d, "plan.json"), "w") as f:
         f.write(plan.dumps())
     with open(os.path.join(d, "QueryPlan.xml"), "w") as f:   # the reference job directory's plan
@@ -1732,6 +1733,7 @@ class GpuExecutor(_BaseExecutor):
             res = runner.run()
         except BaseException as e:
             if job_dir:
+                os.makedirs(os.path.join(job_dir, "log"), exist_ok=True)
                 with open(os.path.join(job_dir, "log", "error.txt"), "w") as f:
                     f.write(str(e))
             raise
@@ -1775,8 +1777,7 @@ class GpuExecutor(_BaseExecutor):
         from .executor import dryad_home
         GpuExecutor._seq += 1
         d = os.path.join(dryad_home(self.ctx), "LocalJobs", f"gpu-{os.getpid()}-{int(time.time() * 1000) % 10**9}-{GpuExecutor._seq}")
-        os.makedirs(os.path.join(d, "log"), exist_ok=True)
-        _JOB_DIR_WRITER.submit(_write_plan_files, d, plan)
+        _JOB_DIR_WRITER.submit(_write_plan_files, d, plan)      # creates the directory first
         return d
 
     def _rank_job_dir(self, plan):
