@@ -117,3 +117,47 @@ def test_loopback_rank_output_is_exact(W, rank):
     got = job.out.cpu().numpy()
     assert got.shape == exp.shape
     assert np.array_equal(got, exp)
+
+
+def test_merge_received_rounds_falls_back_on_a_skewed_bucket():
+    """A fine bucket past one workgroup's capacity (heavy key skew) flags its round, which is then
+    sorted by the stored-row radix sort: the output is still the exact stable order."""
+    g = np.random.default_rng(11)
+    W, B, fb = 2, 2, 16
+    n_src = [30_000, 25_000]
+    L = [0, 1 << 15, 1 << 16]                     # range 0 = buckets [0, 2^15), range 1 = the rest
+    pieces, fine_rows = [], []
+    for s in range(W):
+        n = n_src[s]
+        hi = g.integers(0, 1 << 64, size=n, dtype=np.uint64)
+        hot = g.random(n) < 0.05                   # ~2750 rows of the job in bucket 777 (range 0)
+        hi[hot] = (np.uint64(777) << np.uint64(48)) | (hi[hot] & np.uint64((1 << 48) - 1))
+        rows = g.integers(0, 256, size=(n, 100), dtype=np.uint8)
+        rows[:, :8] = hi.astype(">u8").view(np.uint8).reshape(n, 8)
+        rows[::13, 8:10] = 7
+        b = (hi >> np.uint64(64 - fb)).astype(np.int64)
+        order = np.argsort(b, kind="stable")      # the send side's bucket order
+        rows, b = rows[order], b[order]
+        pieces.append((rows, b))
+    # receive layout: round r = range r, source-major pieces
+    blocks, off, fine = [], [0], np.zeros((W, 1 << fb), dtype=np.int32)
+    for r in range(B):
+        for s in range(W):
+            rows, b = pieces[s]
+            sel = (b >= L[r]) & (b < L[r + 1])
+            blocks.append(rows[sel])
+        off.append(off[-1] + sum(len(x) for x in blocks[-W:]))
+    for s in range(W):
+        fine[s] = np.bincount(pieces[s][1], minlength=1 << fb)
+    recv = np.concatenate(blocks)
+    N = recv.shape[0]
+    bufs = RS.SortBuffers.allocate(N, 100, "cuda")
+    bufs.rows_in[:N] = torch.from_numpy(recv).cuda()
+    out = RS.merge_received_rounds(bufs, off, torch.from_numpy(fine).cuda(), L, fb, B, 0, [N] * B, 0)
+    got = out.cpu().numpy()
+    exp = []
+    for r in range(B):
+        blk = recv[off[r]: off[r + 1]]
+        key = [bytes(x[:10]) for x in blk]
+        exp.append(blk[sorted(range(len(blk)), key=lambda i: (key[i], i))])
+    assert np.array_equal(got, np.concatenate(exp))
