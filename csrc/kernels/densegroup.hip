@@ -322,17 +322,18 @@ __device__ __forceinline__ void dg_agg_body(const uint4* __restrict__ rows, cons
       if (l == 0) wtot[q * kDgWaves + w] = (uint32_t)__popcll(bal);
     }
     __syncthreads();
-    if (t == 0) {
-      uint32_t total = 0;
-      for (int k = 0; k < kRounds * kDgWaves; ++k) total += wtot[k];
-      *obase = atomicAdd(head, (unsigned long long)total);
+    static_assert(kRounds * kDgWaves <= 64, "one wave scans the per-(round, wave) counts");
+    if (w == 0) {                        // exclusive scan of the (round, wave) counts, one lane each
+      const uint32_t c = l < kRounds * kDgWaves ? wtot[l] : 0u;
+      const uint32_t inc = wave_inclusive_scan(c);
+      if (l < kRounds * kDgWaves) wtot[l] = inc - c;
+      if (l == 63) *obase = atomicAdd(head, (unsigned long long)inc);
     }
     __syncthreads();
     uint64_t o = *obase;
 #pragma unroll
     for (int q = 0; q < kRounds; ++q) {
-      uint32_t before = 0;
-      for (int k = 0; k < q * kDgWaves + w; ++k) before += wtot[k];
+      const uint32_t before = wtot[q * kDgWaves + w];
       if ((mine >> q) & 1u) {
         const int sl = q * kDgThreads + t;
         const uint64_t oo = o + before + pos[q];
