@@ -96,7 +96,7 @@ def _prepare(key: torch.Tensor, specs: list):
     return cols, accs, where, kmin, kbits, [lo for lo, _ in vb], vbits, widths
 
 
-def _partition(key64, cols64, vmin, vbits, kmin, kbits, src, n, shift, dbits, dev, st, lo_bits=0):
+def _partition(key64, cols64, vmin, vbits, kmin, kbits, src, n, shift, dbits, dev, st, lo_bits=0, need_runs=True):
     """One stable partition pass -> (rows [n, 16 bytes], run sizes int64 on the device).  Run sizes
     (runs = key offset >> TABLE_BITS in the final order) come from the histogram itself on a single
     pass, from the joint (digit, previous digit) count of a second pass (``lo_bits`` = the first
@@ -119,7 +119,10 @@ def _partition(key64, cols64, vmin, vbits, kmin, kbits, src, n, shift, dbits, de
     vbt = (c_u32 * 3)(*(list(vbits) + [0] * (3 - k)))
     _lib.call("dr_dg_scatter", ptr(key64), cp, vm, vbt, c_u32(k), c_i64(kmin), c_u32(kbits), ptr(src), c_u64(n),
               c_u32(shift), c_u32(dbits), ptr(offs), c_u32(G), pb, ptr(out), st)
-    runs = joint.to(torch.int64) if joint is not None else c64.view(nb, G).sum(1)
+    if joint is not None:
+        runs = joint.to(torch.int64)
+    else:
+        runs = c64.view(nb, G).sum(1) if need_runs else None
     return out, runs
 
 
@@ -139,7 +142,8 @@ def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
     cols64 = [(c if c.dtype == torch.int64 else c.to(torch.int64)).contiguous() for c in cols]
     # pass 1 packs the columns (low digit), pass 2 (if any) re-partitions the rows (high digit)
     # (LSD order: the rows end up sorted by run id = key offset >> TABLE_BITS)
-    rows, runs = _partition(key64, cols64, vmin, vbits, kmin, kbits, None, n, TABLE_BITS, widths[0], dev, st)
+    rows, runs = _partition(key64, cols64, vmin, vbits, kmin, kbits, None, n, TABLE_BITS, widths[0], dev, st,
+                            need_runs=len(widths) == 1)
     if len(widths) == 2:
         nxt, runs = _partition(key64, cols64, vmin, vbits, kmin, kbits, rows, n, TABLE_BITS + widths[0], widths[1],
                                dev, st, lo_bits=widths[0])
