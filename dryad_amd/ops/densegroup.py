@@ -57,6 +57,13 @@ def applicable(key: torch.Tensor, specs: list) -> bool:
     return _prepare(key, specs) is not None
 
 
+def _same_column(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """The same column even when the traced lambdas produced distinct tensor objects (e.g.
+    Sum / Min / Max of r[1]): one packed field and one column read serve all of them."""
+    return a is b or (a.dtype == b.dtype and a.shape == b.shape and a.stride() == b.stride()
+                      and a.device == b.device and a.data_ptr() == b.data_ptr())
+
+
 def _prepare(key: torch.Tensor, specs: list):
     from ..gpu import stats
     n = key.shape[0]
@@ -69,7 +76,7 @@ def _prepare(key: torch.Tensor, specs: list):
             continue
         if op not in _OP or vals is None or vals.dtype not in _INT or dtype not in _INT:
             return None
-        j = next((j for j, c in enumerate(cols) if c is vals), None)
+        j = next((j for j, c in enumerate(cols) if _same_column(c, vals)), None)
         if j is None:
             if len(cols) == 3:
                 return None
