@@ -381,14 +381,32 @@ def pack_gen_fine(bufs: SortBuffers, gen: tuple[int, int], n: int, seps_hi: list
             acc += size[b][r]
     st.append(acc)
 
-    # one generator launch per round: segment r = {send row - round start, first sorted entry}
-    segs = torch.tensor([[[st[b * W + r] - st[b * W], Sg[r * B + b]] for r in range(W)] for b in range(B)],
-                        dtype=torch.int64).to(e.device)
+    # generator launches over groups of rounds 1, 1, 2, 4, ... (at most 64 // W rounds, the segment
+    # limit): round 0 goes out after 1/B of the pack, and the pack is a handful of launches (16
+    # per-round launches cost 27.1 ms against 21.3 ms for one, profiles/r4/send_ab2.log).
+    # Segment = {send row - group start, first sorted entry} per (round, destination).
+    groups, b0, size_g = [], 0, 1
+    while b0 < B:
+        g1 = min(B, b0 + size_g, b0 + max(1, 64 // W))
+        groups.append((b0, g1))
+        if b0 > 0:
+            size_g *= 2
+        b0 = g1
+    segs = torch.tensor([[st[b * W + r] - st[g0 * W], Sg[r * B + b]] for g0, g1 in groups for b in range(g0, g1)
+                         for r in range(W)], dtype=torch.int64).to(e.device)
+    first_seg = {}
+    k = 0
+    for g0, g1 in groups:
+        first_seg[g0] = (g1, k)
+        k += (g1 - g0) * W
 
     def pack(b: int):
-        a, z = st[b * W], st[(b + 1) * W]
+        if b not in first_seg:
+            return                   # packed with the first round of its group
+        g1, k0 = first_seg[b]
+        a, z = st[b * W], st[g1 * W]
         if z > a:
-            TSG.gen_gather64(bufs.rows_out[a:z], srt, gen[0], gen[1], seg=segs[b], n=z - a)
+            TSG.gen_gather64(bufs.rows_out[a:z], srt, gen[0], gen[1], seg=segs[k0: k0 + (g1 - b) * W], n=z - a)
     return st, pack, counts, L
 
 

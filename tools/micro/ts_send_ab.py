@@ -67,6 +67,34 @@ def main():
             TS.gen_gather64(out[cuts[j]: cuts[j + 1]], s[cuts[j]: cuts[j + 1]], 0, seed)
     t = timed(per_range)
     print(f"gen_gather64, {W * B} launches  {t:8.2f} ms", flush=True)
+    R = 16
+    cut16 = [(n * j) // R for j in range(R + 1)]
+
+    def per_round_plain():
+        for j in range(R):
+            TS.gen_gather64(out[cut16[j]: cut16[j + 1]], s[cut16[j]: cut16[j + 1]], 0, seed)
+    t = timed(per_round_plain)
+    print(f"gen_gather64, {R} launches, no segments  {t:8.2f} ms", flush=True)
+    # the pack's layout: round b = W segments (ranges r * B + b) of the key-ordered entries
+    W8 = W
+    segs = []
+    for b in range(R):
+        rows_b, seg = 0, []
+        for r in range(W8):
+            g = r * R + b
+            a0, a1 = (n * g) // (W8 * R), (n * (g + 1)) // (W8 * R)
+            seg.append([rows_b, a0])
+            rows_b += a1 - a0
+        segs.append((rows_b, torch.tensor(seg, dtype=torch.int64, device=dev)))
+    starts = [0]
+    for rows_b, _ in segs:
+        starts.append(starts[-1] + rows_b)
+
+    def per_round_segs():
+        for b in range(R):
+            TS.gen_gather64(out[starts[b]: starts[b + 1]], s, 0, seed, seg=segs[b][1], n=segs[b][0])
+    t = timed(per_round_segs)
+    print(f"gen_gather64, {R} launches x {W8} segments  {t:8.2f} ms", flush=True)
     idx = tmp.view(torch.int32)[:n]
     idx.copy_((s & 0xFFFFFFFF).to(torch.int32))
     t = timed(lambda: TS.gen_gather(out, idx, 0, seed))
