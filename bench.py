@@ -69,9 +69,13 @@ def main():
                     help="run the per-rank program of a W-rank job on this one GPU, the all-to-all-v replaced by "
                          "generating the exact bytes this rank would receive (not timed); reports per-rank ms")
     ap.add_argument("--loopback-rank", type=int, default=0, help="which rank of the --loopback-ranks job to run")
+    ap.add_argument("--gen-fused", action="store_true",
+                    help="N > 1 (and --loopback-ranks): no input table; the records are generated straight into "
+                         "the exchange's send rows in key order (GenFusedShuffle; labelled in config.input)")
     ap.add_argument("--input", default=None,
                     help="stored-data TeraSort: read this partfile:// table of raw 100-byte rows (written from the "
-                         "generator first, untimed, if absent) and write the sorted table to --output")
+                         "generator first, untimed, if absent) and write the sorted table to --output; with "
+                         "--loopback-ranks: the rank's input table is read from it (one part, written if absent)")
     ap.add_argument("--output", default=None, help="with --input: the output partfile:// table")
     args = ap.parse_args()
     env = check_env(args.rehearsal)
@@ -105,7 +109,7 @@ def main():
         budget = None if args.hbm_budget_gb is None else int(args.hbm_budget_gb * 1e9)
         job = TeraSortOOCJob(cfg, world, budget=budget)
     else:
-        job = TeraSortJob(cfg, world) if args.direct else TeraSortQueryJob(cfg, world)
+        job = TeraSortJob(cfg, world) if args.direct else TeraSortQueryJob(cfg, world, gen_fused=args.gen_fused)
     if world.rank == 0:
         free, total = torch.cuda.mem_get_info(world.device)
         print(f"[bench] allocated working set in {time.perf_counter() - t_alloc:.1f}s; HBM free {free/1e9:.1f} "
@@ -160,10 +164,13 @@ def main():
                 # HBM input table the local sort gathers from, with several ranks straight into
                 # the all-to-all send buckets (the read stage fused with the range partition)
                 "input": "gen://terasort, generated in the timed step" + (
-                    ": sort entries first, then the records into the send rows in key order (the read fused with "
-                    "the range partition)" if world.size > 1 and not args.direct
+                    ": [GenFusedShuffle variant, no input table] sort entries first, then the records into the "
+                    "send rows in key order (the read fused with the range partition)"
+                    if world.size > 1 and args.gen_fused and not args.direct
                     else " into the HBM input table" + ("" if args.direct else
-                                                         " (records at a 128-byte pitch: one aligned HBM line each)")),
+                                                         " (records at a 128-byte pitch: one aligned HBM line each)")
+                    + (", then the fine-bucket exchange's send side reads it (entry sort + one row gather into "
+                       "the send rows)" if world.size > 1 and not args.direct else "")),
             },
         }
         if val is not None and not val["ok"]:
@@ -181,6 +188,9 @@ def main():
         elif not args.direct and not stored:
             rep = job.executor_report()
             print(f"[bench] executor: {json.dumps(rep, default=str)[:2000]}", file=sys.stderr, flush=True)
+            if rep.get("exchange"):
+                # per-round exchange bytes and arrival times of the last step (rank 0's view)
+                line["config"]["exchange"] = rep["exchange"]
         print(json.dumps(line), flush=True)
     shutdown()
     if val is not None and not val["ok"]:
@@ -195,7 +205,9 @@ def loopback(args, env):
     if W < 2 or not 0 <= r < W:
         print("[bench] --loopback-ranks needs W >= 2 and 0 <= --loopback-rank < W", file=sys.stderr)
         sys.exit(2)
-    job = TeraSortLoopbackJob(TeraSortConfig(records_per_rank=args.records_per_gpu), W, r)
+    mode = "gen-fused" if args.gen_fused else "table"
+    job = TeraSortLoopbackJob(TeraSortConfig(records_per_rank=args.records_per_gpu), W, r, mode=mode,
+                              input_uri=args.input)
     for i in range(args.warmup):
         job.step()
         print(f"[bench] warmup {i}: {job.ms:.2f} ms {job.phases}", file=sys.stderr, flush=True)
@@ -219,6 +231,10 @@ def loopback(args, env):
                    "received_rows": int(job.out.shape[0]),
                    "phases_ms": {k: round(sum(p[k] for p in phases) / len(phases), 3) for k in phases[0]},
                    "per_rank_GBps": round(job.bytes_per_rank / 1e6 / mean, 1),
+                   "input": (f"{args.input} (read through the chunked reader at a 128-byte pitch, timed)" if args.input
+                             else "[GenFusedShuffle variant, no input table] records generated into the send rows"
+                             if mode == "gen-fused" else
+                             "gen://terasort generated into the rank's HBM table (128-byte pitch), timed"),
                    "wall_s_per_step_incl_simulated_exchange": round(sum(walls) / len(walls), 3),
                    "validated": None if val is None else val["ok"], "validation": val, "env": env},
     }

@@ -30,7 +30,16 @@ def main():
     ap.add_argument("--no-bounds", action="store_true",
                     help="withhold the generator's column bounds (as for a stored table): the dense "
                          "GroupBy path then measures the key range itself, inside the timed step")
+    ap.add_argument("--loopback-ranks", type=int, default=0,
+                    help="run the per-rank program of a W-rank job on this one GPU (runtime/loopback.py): the "
+                         "all-to-all-v replaced by running every other source's stage untimed; reports per-rank ms")
+    ap.add_argument("--loopback-rank", type=int, default=0)
+    ap.add_argument("--raw-shuffle", action="store_true",
+                    help="with --loopback-ranks: shuffle the pruned raw rows (Select -> HashPartition -> GroupBy) "
+                         "instead of partial aggregation before the shuffle")
     a = ap.parse_args()
+    if a.loopback_ranks:
+        return loopback(a)
     w = world()
     import torch
     import dryad_amd as D
@@ -83,6 +92,82 @@ def main():
         "config": {"model": "GroupBy(Key) -> Count/Sum/Min/Max (decomposable, hash shuffle)",
                    "records": n, "record_bytes": 64, "keys": int(a.keys), "parallelism": f"dp{w.size}",
                    "column_bounds": "measured in the step" if a.no_bounds else "declared by the generator"}})
+
+
+def loopback(a):
+    """Rank ``--loopback-rank`` of a ``--loopback-ranks``-rank GroupBy on one GPU: stage A (read ->
+    partial GroupBy -> hash partition) and stage B (final GroupBy) timed, the exchange simulated.
+    Validated: every group of this rank's hash range is complete (count and V1 sum of its groups
+    against the rank's share of the input, computed by a host-side pass over the same generator)."""
+    import json
+    import torch
+    import dryad_amd as D
+    from dryad_amd.compiler.planner import compile_queries
+    from dryad_amd.runtime.loopback import LoopbackRank
+    W, r = a.loopback_ranks, a.loopback_rank
+    n = int(a.records_per_gpu) * W
+    src = f"gen://records64?count={n}&partitions={W}&keys={int(a.keys)}&seed=4242" + ("&bounds=0" if a.no_bounds else "")
+    ctx = D.DryadLinqContext(platform="gpu")
+    ctx.PartitionCount = W
+    res = lambda k, g: (k, g.Count(), g.Sum(lambda x: x[1]), g.Min(lambda x: x[2]), g.Max(lambda x: x[3]))  # noqa: E731
+    q = ctx.FromStore(src)
+    if a.raw_shuffle:
+        q = q.Select(lambda x: (x[0], x[1], x[2], x[3])).HashPartition(lambda x: x[0], W).GroupBy(lambda x: x[0], res)
+    else:
+        q = q.GroupBy(lambda x: x[0], res)
+    plan = compile_queries(ctx, [q.ToStore("hbm://groupby_lb", delete_if_exists=True)])
+    job = LoopbackRank(plan, W, r)
+    ms, ph = [], []
+    for i in range(a.warmup + a.steps):
+        p = job.step()
+        print(f"[groupby-lb] {'warmup' if i < a.warmup else 'step'} {i}: {job.ms:.2f} ms {p} {job.bytes}",
+              flush=True)
+        if i >= a.warmup:
+            ms.append(job.ms)
+            ph.append(p)
+    valid = None
+    if not a.no_validate:
+        out = job.out
+        cnt, s1, groups = int(out.col(1).sum()), int(out.col(2).sum()), out.n
+        # the input rows hashed to rank r, from every source partition: count and V1 sum
+        from dryad_amd.ops import relational as R
+        exp_cnt = exp_s1 = 0
+        for s_ in range(W):
+            lo, hi = (n * s_) // W, (n * (s_ + 1)) // W
+            for c0 in range(lo, hi, 1 << 27):
+                c1 = min(hi, c0 + (1 << 27))
+                cols = [torch.empty(c1 - c0, dtype=torch.int64, device="cuda") for _ in range(2)]
+                R.gen_records64(cols, c0, int(a.keys), 4242)
+                dest = _dest_of(cols[0], W)
+                m = dest == r
+                exp_cnt += int(m.sum())
+                exp_s1 += int(cols[1][m].sum())
+        valid = dict(ok=cnt == exp_cnt and s1 == exp_s1, records=cnt, expected_records=exp_cnt, groups=groups)
+    mean = sum(ms) / len(ms)
+    print(json.dumps({
+        "metric": f"GroupBy-Aggregate per-rank step of a {W}-rank job (loopback on one GPU: all-to-all-v replaced)",
+        "value": round(mean, 3), "unit": "ms", "higher_is_better": False, "n_gpus": 1, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(mean, 3), "dtype": "int64",
+        "data": "synthetic gen://records64 (uniform keys)",
+        "config": {"model": "GroupBy(Key) -> Count/Sum/Min/Max", "records_per_rank": int(a.records_per_gpu),
+                   "keys": int(a.keys), "ranks": W, "rank": r,
+                   "plan": "Select(4 cols) -> HashPartition -> GroupBy (raw rows shuffled)" if a.raw_shuffle else
+                   "partial GroupBy -> HashPartition -> final GroupBy",
+                   "phases_ms": {k: round(sum(p[k] for p in ph) / len(ph), 3) for k in ph[0]},
+                   "exchange": {k: v for k, v in job.bytes.items()},
+                   "per_rank_input_GBps": round(int(a.records_per_gpu) * 64 / 1e6 / mean, 1),
+                   "validated": valid}}), flush=True)
+
+
+def _dest_of(keys, W):
+    """Destination rank of int64 keys under the executor's hash partition (gpu/ops.op_hash_partition)."""
+    from dryad_amd.ops import relational as R
+    from dryad_amd.gpu import ops as G
+    from dryad_amd.gpu.table import DeviceTable, Shape
+    t = DeviceTable.from_columns({"k": keys}, Shape("scalar", ["k"]))
+    k, tup = G.hash_keys(t, lambda x: x)
+    e, _ = R.stable_hash_dest(k, t.n, W, tup, keys.device, ports=False)
+    return e[:, 1] if e.dim() == 2 else e
 
 
 if __name__ == "__main__":

@@ -1173,7 +1173,9 @@ template <int WC, bool NT = false>
 __global__ __launch_bounds__(256) void gather_fixup_kernel(const uint32_t* __restrict__ rows, uint32_t* __restrict__ out,
                                                            const E64* __restrict__ ent, uint64_t n, uint32_t Wdyn,
                                                            uint32_t key_off, uint32_t key_len, int run_shift,
-                                                           uint32_t* __restrict__ overflow) {
+                                                           uint32_t* __restrict__ overflow,
+                                                           const int32_t* __restrict__ err) {
+  if (err != nullptr && *err != 0) return;     // the look-back sort failed: the entries are no permutation
   const uint32_t W = WC > 0 ? (uint32_t)WC : Wdyn;
   const uint32_t Win = W;
   __shared__ uint32_t rid[kGfWin + 1];     // rid[p + 1] = run id of window position p; rid[0] = position -1
@@ -1190,7 +1192,12 @@ __global__ __launch_bounds__(256) void gather_fixup_kernel(const uint32_t* __res
     for (uint32_t p = t; p < L; p += kBlock) {
       const uint64_t v = ent[c0 + p].v;
       rid[p + 1] = (uint32_t)(v >> run_shift);
-      idx[p] = (uint32_t)v;
+      uint32_t i = (uint32_t)v;
+      if (i >= n) {                    // corrupt entries: never read past the rows (flag 2: redo)
+        atomicOr(overflow, 2u);
+        i = 0;
+      }
+      idx[p] = i;
     }
     if (t == 0) {
       rid[0] = c0 > 0 ? (uint32_t)(ent[c0 - 1].v >> run_shift) : 0u;
@@ -1282,7 +1289,9 @@ __global__ __launch_bounds__(256) void gather_fixup_staged_kernel(const uint32_t
                                                                   uint32_t* __restrict__ out,
                                                                   const E64* __restrict__ ent, uint64_t n,
                                                                   uint32_t key_off, uint32_t key_len, int run_shift,
-                                                                  uint32_t* __restrict__ overflow) {
+                                                                  uint32_t* __restrict__ overflow,
+                                                                  const int32_t* __restrict__ err) {
+  if (err != nullptr && *err != 0) return;     // the look-back sort failed: the entries are no permutation
   constexpr uint32_t W = 25;
   __shared__ uint32_t rid[kGfWin + 1];     // rid[p + 1] = run id of window position p; rid[0] = position -1
   __shared__ uint32_t idx[kGfWin];
@@ -1298,7 +1307,12 @@ __global__ __launch_bounds__(256) void gather_fixup_staged_kernel(const uint32_t
     for (uint32_t p = t; p < L; p += kBlock) {
       const uint64_t v = ent[c0 + p].v;
       rid[p + 1] = (uint32_t)(v >> run_shift);
-      idx[p] = (uint32_t)v;
+      uint32_t i = (uint32_t)v;
+      if (i >= n) {                    // corrupt entries: never read past the rows (flag 2: redo)
+        atomicOr(overflow, 2u);
+        i = 0;
+      }
+      idx[p] = i;
     }
     if (t == 0) {
       rid[0] = c0 > 0 ? (uint32_t)(ent[c0 - 1].v >> run_shift) : 0u;
@@ -1751,8 +1765,11 @@ DR_API int dr_sort_u64_onesweep(E64* keys, E64* tmp, uint64_t n, int begin_bit, 
 
 // Row gather + run fix-up of the compact sort: out = rows in (window, full key, position) order.
 // run_shift = 64 - (window bits the LSD sort covered).  stride % 4 == 0, key_len <= 16.
+// err (nullable): the look-back sort's error word; when set nothing is read or written.  An entry
+// naming a row >= n sets bit 1 of *overflow (the caller redoes the sort) instead of being read.
 DR_API int dr_gather_fixup(const uint8_t* rows, uint8_t* out, const E64* ent, uint64_t n, uint32_t stride,
-                           uint32_t key_off, uint32_t key_len, int run_shift, uint32_t* overflow, hipStream_t s) {
+                           uint32_t key_off, uint32_t key_len, int run_shift, uint32_t* overflow, const int32_t* err,
+                           hipStream_t s) {
   if (stride == 0 || (stride & 3) || key_len == 0 || key_len > 16 || key_off + key_len > stride) return (int)hipErrorInvalidValue;
   if (run_shift < 32 || run_shift > 63) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
@@ -1761,9 +1778,9 @@ DR_API int dr_gather_fixup(const uint8_t* rows, uint8_t* out, const E64* ent, ui
   const uint32_t* in = reinterpret_cast<const uint32_t*>(rows);
   uint32_t* o = reinterpret_cast<uint32_t*>(out);
   if (W == 25)   // nontemporal output stores (-1.2% gather time at 1e9 rows)
-    gather_fixup_kernel<25, true><<<g, 256, 0, s>>>(in, o, ent, n, W, key_off, key_len, run_shift, overflow);
+    gather_fixup_kernel<25, true><<<g, 256, 0, s>>>(in, o, ent, n, W, key_off, key_len, run_shift, overflow, err);
   else
-    gather_fixup_kernel<0><<<g, 256, 0, s>>>(in, o, ent, n, W, key_off, key_len, run_shift, overflow);
+    gather_fixup_kernel<0><<<g, 256, 0, s>>>(in, o, ent, n, W, key_off, key_len, run_shift, overflow, err);
   DR_LAUNCH_CHECK();
   return 0;
 }
@@ -1772,14 +1789,14 @@ DR_API int dr_gather_fixup(const uint8_t* rows, uint8_t* out, const E64* ent, ui
 // `stride` bytes of each row are the record) into back-to-back rows of `stride` bytes.
 DR_API int dr_gather_fixup_pitch128(const uint8_t* rows, uint8_t* out, const E64* ent, uint64_t n, uint32_t stride,
                                     uint32_t key_off, uint32_t key_len, int run_shift, uint32_t* overflow,
-                                    hipStream_t s) {
+                                    const int32_t* err, hipStream_t s) {
   if (stride != 100 || key_len == 0 || key_len > 16 || key_off + key_len > stride) return (int)hipErrorInvalidValue;
   if (run_shift < 32 || run_shift > 63) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
   const unsigned g = grid_for(n, kGfCore, 16384);
   gather_fixup_staged_kernel<<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows),
                                                    reinterpret_cast<uint32_t*>(out), ent, n, key_off, key_len,
-                                                   run_shift, overflow);
+                                                   run_shift, overflow, err);
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -155,12 +155,136 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
   }
 }
 
+// Send side of the fine-bucket exchange over a MATERIALISED table (hbm:// / partfile:// rows or
+// the generator's table): out row p (100-byte rows back to back) := input row (uint32)ent[q(p)],
+// q(p) = seg[s].ent + p - seg[s].out for the last segment s starting at or before p (one segment
+// per (round, destination): the send buffer is round-major, every piece in fine-bucket order).
+// PW = input pitch in dwords: 32 (one aligned 128-byte line per row: every random row read is one
+// HBM line) or 25 (rows back to back, 4-byte aligned).  One workgroup moves 256 rows per tile:
+// their entry indices to LDS, then 8 lanes per row issue the row's 16-byte loads (7 per row, all
+// 8 rows of a lane in flight before any is used) into an LDS stage at the output pitch, and the
+// tile leaves as contiguous 16-byte nontemporal stores.  ``err`` (nullable): the look-back sort's
+// error word; non-zero means the entries are not a permutation, and nothing is read.  An index
+// past n_in (a broken caller) is not dereferenced: the row is zero-filled and *bad is set.
+template <int PW>
+__global__ __launch_bounds__(256) void ts_pack_rows_kernel(const uint32_t* __restrict__ rows, uint64_t n_in,
+                                                           const E64* __restrict__ ent, uint64_t n,
+                                                           const int64_t* __restrict__ seg, uint32_t nseg,
+                                                           uint32_t* __restrict__ out, const int32_t* __restrict__ err,
+                                                           uint32_t* __restrict__ bad) {
+  __shared__ __attribute__((aligned(16))) uint32_t stage[256 * kTmWords];
+  __shared__ uint32_t sidx[256];
+  __shared__ int64_t sseg[256][2];
+  const uint32_t t = threadIdx.x;
+  if (err != nullptr && *err != 0) return;
+  for (uint32_t k = t; k < 2 * nseg; k += 256) sseg[k >> 1][k & 1] = seg[k];
+  __syncthreads();
+  for (uint64_t row0 = (uint64_t)blockIdx.x * 256; row0 < n; row0 += (uint64_t)gridDim.x * 256) {
+    const uint32_t rows_here = (uint32_t)((n - row0) < 256 ? (n - row0) : 256);
+    if (t < rows_here) {
+      const uint64_t p = row0 + t;
+      uint32_t lo = 0, hi = nseg;                  // last segment with out <= p
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((uint64_t)sseg[mid][0] <= p) lo = mid; else hi = mid;
+      }
+      const uint64_t q = nseg ? (uint64_t)sseg[lo][1] + (p - (uint64_t)sseg[lo][0]) : p;
+      uint32_t i = (uint32_t)ent[q].v;
+      if (i >= n_in) {
+        atomicOr(bad, 1u);
+        i = 0xFFFFFFFFu;
+      }
+      sidx[t] = i;
+    }
+    __syncthreads();
+    {
+      const uint32_t g = t >> 3, sub = t & 7;
+      u32x4u buf[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t r = g + 32 * k;
+        buf[k] = u32x4u{0u, 0u, 0u, 0u};
+        if (r < rows_here && sub < 7 && sidx[r] != 0xFFFFFFFFu) {
+          const uint32_t* src = rows + (uint64_t)sidx[r] * PW + sub * 4;
+          if (PW == 32) {
+            const uint4* s4 = reinterpret_cast<const uint4*>(src);
+            buf[k].x = __builtin_nontemporal_load(&s4->x);
+            buf[k].y = __builtin_nontemporal_load(&s4->y);
+            buf[k].z = __builtin_nontemporal_load(&s4->z);
+            buf[k].w = __builtin_nontemporal_load(&s4->w);
+          } else if (sub < 6) {
+            buf[k] = *reinterpret_cast<const u32x4u*>(src);
+          } else {
+            buf[k].x = src[0];                 // word 24: never read past the row
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t r = g + 32 * k;
+        if (r < rows_here && sub < 7) {
+          uint32_t* d = stage + r * kTmWords + sub * 4;
+          d[0] = buf[k].x;
+          if (sub < 6) {
+            d[1] = buf[k].y;
+            d[2] = buf[k].z;
+            d[3] = buf[k].w;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    uint32_t* o = out + row0 * kTmWords;
+    const uint32_t words = rows_here * kTmWords;
+    uint32_t head = (4u - (uint32_t)((reinterpret_cast<uintptr_t>(o) >> 2) & 3u)) & 3u;
+    head = head < words ? head : words;
+    if (t < head) o[t] = stage[t];
+    const uint32_t nch = (words - head) >> 2;
+    for (uint32_t c = t; c < nch; c += 256) {
+      const uint32_t q = head + 4 * c;
+      uint32_t* d = o + q;
+      __builtin_nontemporal_store(stage[q], d);
+      __builtin_nontemporal_store(stage[q + 1], d + 1);
+      __builtin_nontemporal_store(stage[q + 2], d + 2);
+      __builtin_nontemporal_store(stage[q + 3], d + 3);
+    }
+    for (uint32_t q = head + 4 * nch + t; q < words; q += 256) o[q] = stage[q];
+    __syncthreads();
+  }
+}
+
 }  // namespace
+
+// Send rows of a materialised table in the order of window-sorted E64 entries (see
+// ts_pack_rows_kernel).  rows: n_in input rows at `pitch` bytes (100 or 128; 128 needs 16-byte
+// alignment); out: n rows of 100 bytes; seg: nseg <= 256 segments {out row, entry} (device int64
+// [nseg][2], seg[0].out = 0, ascending), or nseg = 0 for q(p) = p; err: look-back error word
+// (nullable); bad: set when an entry's row index is out of range.
+DR_API int dr_ts_pack_rows(const uint8_t* rows, uint64_t n_in, uint32_t pitch, const E64* ent, uint64_t n,
+                           const int64_t* seg, uint32_t nseg, uint8_t* out, const int32_t* err, uint32_t* bad,
+                           hipStream_t s) {
+  if (n == 0) return 0;
+  if (nseg > 256 || (nseg > 0 && seg == nullptr) || bad == nullptr) return (int)hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(rows)) & 3) return (int)hipErrorInvalidValue;
+  const unsigned g = grid_for(n, 256, 32768);
+  if (pitch == 128) {
+    if (reinterpret_cast<uintptr_t>(rows) & 15) return (int)hipErrorInvalidValue;
+    ts_pack_rows_kernel<32><<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows), n_in, ent, n, seg, nseg,
+                                              reinterpret_cast<uint32_t*>(out), err, bad);
+  } else if (pitch == 100) {
+    ts_pack_rows_kernel<25><<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows), n_in, ent, n, seg, nseg,
+                                              reinterpret_cast<uint32_t*>(out), err, bad);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  DR_LAUNCH_CHECK();
+  return 0;
+}
 
 // starts: (1 << fb) + 1 uint32 = for each fine bucket k the first position of `ent` (sorted on
 // at least the top fb window bits) whose bucket is >= k; starts[1 << fb] = n.
 DR_API int dr_ts_fine_starts(const E64* ent, uint64_t n, uint32_t fb, uint32_t* starts, hipStream_t s) {
-  if (fb == 0 || fb > 28 || n >= (1ull << 32)) return (int)hipErrorInvalidValue;
+  if (fb < 16 || fb > 24 || n >= (1ull << 32)) return (int)hipErrorInvalidValue;   // FINE_MIN/MAX_BITS
   if (n == 0) return (int)hipMemsetAsync(starts, 0, ((size_t(1) << fb) + 1) * sizeof(uint32_t), s);
   ts_fine_starts_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(ent, n, fb, starts);
   DR_LAUNCH_CHECK();
@@ -169,11 +293,12 @@ DR_API int dr_ts_fine_starts(const E64* ent, uint64_t n, uint32_t fb, uint32_t* 
 
 DR_API uint32_t dr_ts_tile_cap() { return kTmCap; }
 
-// rows / out: 100-byte rows (4-byte aligned); pre, cnt: [W][K]; outoff: [K]; 16 <= fb <= 32.
+// rows / out: 100-byte rows (4-byte aligned); pre, cnt: [W][K]; outoff: [K]; 16 <= fb <= 24 (the
+// caller's FINE_MIN_BITS..FINE_MAX_BITS).  A bucket past kTmCap rows is flagged, never ordered.
 DR_API int dr_ts_tile_merge(const uint8_t* rows, uint8_t* out, const int64_t* pre, const int32_t* cnt,
                             const int64_t* outoff, uint32_t W, uint32_t K, uint32_t fb, uint32_t* overflow,
                             hipStream_t s) {
-  if (W == 0 || W > kTmMaxW || fb < 16 || fb > 32) return (int)hipErrorInvalidValue;
+  if (W == 0 || W > kTmMaxW || fb < 16 || fb > 24) return (int)hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(out)) & 3) return (int)hipErrorInvalidValue;
   if (K == 0) return 0;
   const unsigned g = K < 65536u ? K : 65536u;

@@ -122,6 +122,11 @@ _DEFAULTS = dict(
     StreamChunkBytes=4 << 30,     # ... and their chunk size
     GraceJoin=None,               # a Join as the partitioned grace join stage (runtime/grace_stage.py;
     #                               None: when its inputs would crowd the HBM budget; False: never)
+    LineAlignedSortInput=True,    # GPU executor: a table of 100-byte rows that only an OrderBy reads is
+    #                               stored at a 128-byte pitch (one HBM line per record gather)
+    GenFusedShuffle=False,        # multi-rank OrderBy over gen://terasort: generate the records straight
+    #                               into the exchange's send rows (no input table; a benchmark variant)
+    ShuffleSlack=0.01,            # receive-buffer headroom of a range-partitioned exchange
     PartFileSplitBytes=0,         # GPU executor: a fixed-width partfile:// output partition of at least
     #                               this many bytes is written as several part files at once (0: one
     #                               part file per partition, as the reference; io/writer.split_count)

@@ -249,5 +249,18 @@ class DryadLinqVertexException(DryadLinqException):
         self.version = version
 
 
+class GangAgreementError(DryadLinqVertexException):
+    """A collective (gang) stage stopped before its payload exchange because some rank could not
+    go on: every rank raises it alike after one small all-gather of the ranks' status, so no rank
+    is left blocked inside a collective its peers never enter.  ``retryable`` is False when the
+    cause is deterministic (a key range past a rank's receive capacity): a re-execution would fail
+    the same way, so the gang aborts at once instead of spending MaxVertexFailures attempts."""
+
+    def __init__(self, message: str, retryable: bool = True, ranks=()):
+        super().__init__(ErrorCode.FailureInSort, message)
+        self.retryable = retryable
+        self.ranks = tuple(ranks)
+
+
 def raise_not_supported(op: str):
     raise DryadLinqCodeGenException(ErrorCode.OperatorNotSupported, f"operator {op} is not supported")

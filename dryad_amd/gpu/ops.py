@@ -173,6 +173,15 @@ def op_enumerable(op, inputs, v):
     return t
 
 
+def _entries_home(bs, n: int, v):
+    """Where a producer writes the E64 sort entries of a pitch-128 table: ent_a for the one-rank
+    sort; with several ranks the send buffer's first n * 8 bytes ("e64@out": the fine-bucket
+    exchange's entry sort then ends in ent_a, away from the rows its pack writes)."""
+    if v.world.size > 1:
+        return bs.bufs.rows_out.view(-1)[: n * 8].view(torch.int64), "e64@out"
+    return bs.bufs.ent_a, "e64"
+
+
 def op_read(op, inputs, v):
     from ..io.providers import parse_uri, provider_for
     uri = op["uri"]
@@ -183,16 +192,19 @@ def op_read(op, inputs, v):
         lo, hi = GenProvider().bounds(uri, v.partition)
         if kind == "terasort":
             from ..ops import terasort as TSK
-            if v.world.size == 1 and v.stage.id in getattr(v.runner, "pitch_gen_stages", ()):
-                # only the one-rank fused OrderBy reads this table: records at a 128-byte pitch
+            if v.stage.id in getattr(v.runner, "pitch_gen_stages", ()):
+                # only the fused OrderBy reads this table: records at a 128-byte pitch, the sort's
+                # E64 entries + window histograms written with them (several ranks: into the send
+                # buffer's memory, free until the exchange's pack, see SortBuffers.entry_pair)
                 rows = v.alloc_rows(hi - lo, 100, layout="pitch128")
                 if rows is not None:
                     t = DeviceTable(hi - lo, Shape("rows", key_off=0, key_len=10), rows=rows)
                     bs = _pooled_set(t, v)
                     rng = torch.tensor([-1, 0], dtype=torch.int64, device=rows.device)
+                    ent, fmt = _entries_home(bs, hi - lo, v)
                     TSK.generate_with_keys64_pitch128(bs.bufs.rows_in[: hi - lo], lo, int(q.get("seed", 0)),
-                                                      bs.bufs.ent_a, rng, hist=True)
-                    bs.keys_ready = (rows.data_ptr(), hi - lo, 0, 10, rng, "e64")
+                                                      ent, rng, hist=True)
+                    bs.keys_ready = (rows.data_ptr(), hi - lo, 0, 10, rng, fmt)
                     return t
             rows = v.alloc_rows(hi - lo, 100)
             t = DeviceTable(hi - lo, Shape("rows", key_off=0, key_len=10), rows=rows)
@@ -290,7 +302,7 @@ def op_read(op, inputs, v):
             # raw fixed-width rows (e.g. an out-of-core sort's output): chunked reader -> pooled HBM
             mm, ko, kl = rp
             stats = getattr(v.runner, "read_stats", None)
-            spec = getattr(v.runner, "pitch_gen_stages", {}).get(v.stage.id) if v.world.size == 1 else None
+            spec = getattr(v.runner, "pitch_gen_stages", {}).get(v.stage.id)
             if spec is not None and mm.shape[1] == 100 and 0 < mm.shape[0] < (1 << 32):
                 # only the one-rank OrderBy reads these 100-byte rows: stored at a 128-byte pitch
                 # (one aligned HBM line per record) and the sort's compact entries + window
@@ -302,9 +314,10 @@ def op_read(op, inputs, v):
                     RD.read_rows_to_device(mm.filename, v.device, int(mm.offset), n, 100, rows, stats=stats)
                     bs = _pooled_set(t, v)
                     if bs is not None and spec[0] == 0:
-                        _, part = S.extract_keys64_tile(bs.bufs.rows_in[:n], 0, spec[1], 0, bs.bufs.ent_a, hist=True)
-                        S.note_gen_hist(bs.bufs.ent_a[:n], n, part)
-                        bs.keys_ready = (rows.data_ptr(), n, 0, spec[1], None, "e64")
+                        ent, fmt = _entries_home(bs, n, v)
+                        _, part = S.extract_keys64_tile(bs.bufs.rows_in[:n], 0, spec[1], 0, ent, hist=True)
+                        S.note_gen_hist(ent[:n], n, part)
+                        bs.keys_ready = (rows.data_ptr(), n, 0, spec[1], None, fmt)
                     return t
             rows = v.alloc_rows(mm.shape[0], mm.shape[1])
             if mm.shape[0]:

@@ -106,7 +106,7 @@ class TeraSortQueryJob:
 
     OUT = "hbm://terasort_out"
 
-    def __init__(self, cfg: TeraSortConfig, world: World | None = None):
+    def __init__(self, cfg: TeraSortConfig, world: World | None = None, gen_fused: bool = False):
         import dryad_amd as D
         self.cfg = cfg
         self.world = world or get_world()
@@ -114,7 +114,10 @@ class TeraSortQueryJob:
         W = self.world.size
         self.ctx = D.DryadLinqContext(platform="gpu")
         self.ctx.PartitionCount = W
-        self.ctx._props["ShuffleSlack"] = cfg.slack
+        self.ctx.ShuffleSlack = cfg.slack
+        # default: the input table is materialised (128-byte pitch, as on one GPU) and the
+        # fine-bucket exchange reads it; GenFusedShuffle generates the records into the send rows
+        self.ctx.GenFusedShuffle = bool(gen_fused)
         self.src = f"gen://terasort?records={self.n * W}&partitions={W}&seed={cfg.seed}"
         self.out = None
 
@@ -137,7 +140,7 @@ class TeraSortQueryJob:
     def executor_report(self) -> dict:
         ex = self.ctx._get_executor()
         r = ex.last_result or {}
-        return dict(fallbacks=r.get("fallbacks"), timings=r.get("timings"))
+        return dict(fallbacks=r.get("fallbacks"), timings=r.get("timings"), exchange=r.get("exchange"))
 
     def input_checksum(self) -> tuple[int, int]:
         rows = torch.empty((self.n, RECORD), dtype=torch.uint8, device=self.world.device)
@@ -170,7 +173,7 @@ class TeraSortStoredJob:
         W = self.world.size
         self.ctx = D.DryadLinqContext(platform="gpu")
         self.ctx.PartitionCount = W
-        self.ctx._props["ShuffleSlack"] = cfg.slack
+        self.ctx.ShuffleSlack = cfg.slack
         # the sorted output: each rank's partition as several part files written at once (one
         # file's page-cache writes serialise on its inode lock, profiles/r4/filewrite_ab2.log)
         self.ctx.PartFileSplitBytes = 2 << 30
@@ -365,26 +368,38 @@ class TeraSortLoopbackJob:
     """The per-rank program of a W-rank TeraSort, run on one GPU (``bench.py --loopback-ranks W``).
 
     Rank ``rank`` of W ranks owns records [rank * n, (rank + 1) * n) of gen://terasort and does
-    exactly what ``distributed_sort_rows`` does on a node: its sample, the separators of the W * B
-    key ranges (cut to fine-bucket edges), the send side (E64 entries from the generator, one
-    look-back sort, the fine-bucket starts, every round's records generated into the send buffer in
-    key order), then, per received round, the per-bucket LDS merge (ts_tile_merge) into the output
-    table.  The all-to-all-v is the only part replaced: the bytes this rank would receive (round b
-    = the records of EVERY source rank whose key falls in this rank's b-th range, in source order,
-    and every source's per-bucket counts) are produced by running each source's send side, outside
+    exactly what the fused distributed OrderBy does on a node.  By default (``mode`` "table") the
+    input is a MATERIALISED table, as the 1-GPU step has it: the generator (or, with ``input_uri``,
+    the chunked reader from a partfile://) writes the rank's 125 GB of records at a 128-byte pitch
+    with their E64 entries and window histograms, then the fine-bucket send side
+    (ops/recordsort.send_fine_rows): the rank's sample, the separators of the W * B key ranges (cut
+    to fine-bucket edges), one look-back sort of the entries on the top key bits, the fine-bucket
+    starts, ONE gather of the rows into the round-major send buffer.  ``mode`` "gen-fused" runs the
+    GenFusedShuffle variant instead (no input table: the records are generated straight into the
+    send rows in key order, ``pack_gen_fine``).  Then, per received round, the per-bucket LDS
+    merge (ts_tile_merge) into the output table.
+
+    The all-to-all-v is the only part replaced: the bytes this rank would receive (round b = the
+    records of EVERY source rank whose key falls in this rank's b-th range, in source order, and
+    every source's per-bucket counts) are produced by running each source's send side, outside
     the timed segments.  The other ranks' samples (what the sample all-gather returns) are
     generated outside them too.
 
-    Timed with HIP events: (own sample) + (separators + pack) + (receive-side sorts); the phases
-    are reported separately.  Validated: the output is in order, holds exactly the received
-    records (hash sum and count), and its keys lie inside this rank's separator bounds."""
+    Timed with HIP events: (input) + (sample) + (separators + send side) + (receive-side merge);
+    the phases are reported separately.  Validated: the output is in order, holds exactly the
+    received records (hash sum and count), and its keys lie inside this rank's separator bounds."""
 
-    def __init__(self, cfg: TeraSortConfig, W: int, rank: int = 0, device=None):
+    def __init__(self, cfg: TeraSortConfig, W: int, rank: int = 0, device=None, mode: str = "table",
+                 input_uri: str | None = None):
         self.cfg, self.W, self.rank = cfg, W, rank
         self.n = cfg.records_per_rank
         self.dev = torch.device(device or "cuda")
-        self.bufs = RS.SortBuffers.allocate(int(self.n * (1 + cfg.slack)), RECORD, self.dev)
+        self.mode = mode
+        cap = int(self.n * (1 + cfg.slack))
+        self.bufs = RS.SortBuffers.allocate(cap, RECORD, self.dev) if mode == "gen-fused" else \
+            RS.SortBuffers.allocate_pitch128(cap, RECORD, self.dev)
         self.B = RS.pipeline_subs(self.n * RECORD, W)
+        self.input = None if input_uri is None else self._prepare_input(input_uri)
         self.out = None
         self.phases = {}
         self.recv_hash = None
@@ -394,6 +409,34 @@ class TeraSortLoopbackJob:
     def bytes_per_rank(self) -> int:
         return self.n * RECORD
 
+    def _prepare_input(self, uri: str) -> str:
+        """partfile:// table of this rank's raw 100-byte rows (one part), written from the
+        generator (not timed) unless a part of that size is there.  Returns the part's path."""
+        import os
+        from ..io import partfile as PF
+        from ..io.providers import parse_uri
+        from ..io.writer import PartWriter
+        scheme, path, _ = parse_uri(uri)
+        if scheme not in ("partfile", "file"):
+            raise ValueError("--input takes a partfile:// table")
+        if PF.exists(path):
+            m = PF.read_meta(path)
+            if m.count == 1 and m.parts[0].size == self.n * RECORD:
+                return m.part_path(0)
+        base = PF.default_base(path)
+        os.makedirs(os.path.dirname(base), exist_ok=True)
+        part = f"{base}.{0:08X}"
+        chunk = min(self.n, 1 << 26)
+        tmp = torch.empty((chunk, RECORD), dtype=torch.uint8, device=self.dev)
+        with PartWriter(part, self.dev) as wr:
+            for c0 in range(0, self.n, chunk):
+                c1 = min(self.n, c0 + chunk)
+                TS.generate(tmp[: c1 - c0], self.rank * self.n + c0, self.cfg.seed)
+                wr.write(tmp[: c1 - c0])
+        del tmp
+        PF.write_meta(path, PF.PartFileMeta(base, [PF.PartEntry(0, self.n * RECORD)]))
+        return part
+
     def _events(self):
         return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
@@ -402,7 +445,11 @@ class TeraSortLoopbackJob:
         fine-bucket starts), its pieces for this rank generated in place, its per-bucket counts
         of this rank's key ranges stacked.  Returns (round offsets, fine counts [W, K])."""
         n, W, B, me, seed = self.n, self.W, self.B, self.rank, self.cfg.seed
-        e, tmp = self.bufs.ent_a.view(-1)[:n], self.bufs.ent_b.view(-1)[:n]
+        bufs = self.bufs
+        # scratch: the entry arrays, or (pitch-128 set) ent_a + the send rows, dead by now
+        e = bufs.ent_a.view(-1)[:n]
+        tmp = bufs.ent_b.view(-1)[:n] if bufs.ent_b.numel() >= n else bufs.rows_out.view(-1)[: n * 8].view(torch.int64)
+        recv = bufs.recv_rows()
         Lt = torch.tensor(L, dtype=torch.int64, device=self.dev)
 
         def send_side(s):
@@ -418,46 +465,83 @@ class TeraSortLoopbackJob:
         off = [0]
         for b in range(B):
             off.append(off[-1] + sum(sizes[s][b] for s in range(W)))
-        if off[-1] > self.bufs.capacity:
-            raise RuntimeError(f"range partition skew: {off[-1]} rows > capacity {self.bufs.capacity}")
+        if off[-1] > bufs.capacity:
+            raise RuntimeError(f"range partition skew: {off[-1]} rows > capacity {bufs.capacity}")
         for s in range(W):
             srt, _, Sg = send_side(s)
             for b in range(B):
                 pos = off[b] + sum(sizes[s2][b] for s2 in range(s))
                 g = me * B + b
                 if Sg[g + 1] > Sg[g]:
-                    TS.gen_gather64(self.bufs.rows_in[pos: pos + Sg[g + 1] - Sg[g]], srt[Sg[g]: Sg[g + 1]], s * n, seed)
+                    TS.gen_gather64(recv[pos: pos + Sg[g + 1] - Sg[g]], srt[Sg[g]: Sg[g + 1]], s * n, seed)
         return off, torch.stack(fine)
+
+    def _samples(self, mine):
+        """Every rank's sample as the sample all-gather returns it (others generated, untimed)."""
+        n, W, me, seed = self.n, self.W, self.rank, self.cfg.seed
+        tgt, sseed, M64 = self.cfg.sample_target, 314159, (1 << 64) - 1
+        if self.mode == "gen-fused":
+            others = [RS.gen_samples((s * n, seed), n, s, s << 32, M64, tgt, sseed, self.dev) for s in range(W) if s != me]
+        else:
+            others = []
+            for s in range(W):
+                if s != me:
+                    x = RS.gen_samples((s * n, seed), n, s, 0, M64, tgt, sseed, self.dev)
+                    x[:, 1] &= RS._as_i64(0xFFFFFFFF00000000)
+                    x[:, 0] = 0
+                    others.append(x)
+        return torch.cat(others[:me] + [mine] + others[me:])
 
     def step(self):
         n, W, B, me = self.n, self.W, self.B, self.rank
         seed, M64 = self.cfg.seed, (1 << 64) - 1
-        dev = self.dev
+        dev, bufs = self.dev, self.bufs
         tgt, sseed = self.cfg.sample_target, 314159
-        e = [self._events() for _ in range(3)]
-        e[0][0].record()
-        mine = RS.gen_samples((me * n, seed), n, me, me << 32, M64, tgt, sseed, dev)
-        e[0][1].record()
-        others = [RS.gen_samples((s * n, seed), n, s, s << 32, M64, tgt, sseed, dev) for s in range(W) if s != me]
-        allsamp = torch.cat(others[:me] + [mine] + others[me:])
-        e[1][0].record()
+        ev = [self._events() for _ in range(4)]
+        fb = RS.fine_bits(n * W)
+        ev[0][0].record()
+        if self.mode == "gen-fused":
+            ev[0][1].record()
+            mine = RS.gen_samples((me * n, seed), n, me, me << 32, M64, tgt, sseed, dev)
+        else:
+            e, tmp = bufs.entry_pair(n, in_out=True)
+            rows = bufs.rows_in[:n, :RECORD]
+            if self.input is None:
+                TS.generate_with_keys64_pitch128(bufs.rows_in[:n], me * n, seed, e, None, hist=True)
+                hist = S.take_gen_hist(e)
+            else:
+                from ..io import reader as RD
+                RD.read_rows_to_device(self.input, dev, 0, n, RECORD, rows)
+                e, hist = S.extract_keys64_tile(bufs.rows_in[:n], 0, KEYLEN, 0, e, hist=True)
+            ev[0][1].record()
+            mine = RS.e64_samples(e, n, me, tgt, sseed)
+        ev[1][0].record()
+        ev[1][1].record()
+        allsamp = self._samples(mine)
+        ev[2][0].record()
         seps = RS.separators_from_samples(allsamp, W * B)
         seps_hi = [int(x) & M64 for x in seps[:, 1].tolist()]
-        fb = RS.fine_bits(n * W)
-        st, pack, counts, L = RS.pack_gen_fine(self.bufs, (me * n, seed), n, seps_hi, B, W, fb)
-        for b in range(B):
-            pack(b)
-        e[1][1].record()
+        if self.mode == "gen-fused":
+            st, pack, counts, L = RS.pack_gen_fine(bufs, (me * n, seed), n, seps_hi, B, W, fb)
+            for b in range(B):
+                pack(b)
+        else:
+            st, counts, L, bad = RS.send_fine_rows(bufs, rows, e, tmp, hist, n, seps_hi, B, W, fb)
+        ev[2][1].record()
         off, fine = self._receive(seps_hi, L, fb)            # the all-to-all-v (not timed)
-        acc = TS.check(self.bufs.rows_in[: off[-1]])
-        e[2][0].record()
-        out = RS.merge_received_rounds(self.bufs, off, fine, L, fb, B, me, [off[-1]] * B, 0)
-        e[2][1].record()
+        acc = TS.check(bufs.recv_rows()[: off[-1]])
+        ev[3][0].record()
+        out = RS.merge_received_rounds(bufs, off, fine, L, fb, B, me, [off[-1]] * B, 0)
+        ev[3][1].record()
         torch.cuda.synchronize(dev)
+        if self.mode != "gen-fused" and int(bad.item()):
+            raise RuntimeError("send-side pack: an entry named a row past the table")
         self.out, self.recv_hash = out, acc
         self.bounds = RS.fine_hi_bounds([L[me * B], L[(me + 1) * B]], fb, 0)
-        self.phases = {"sample_ms": e[0][0].elapsed_time(e[0][1]), "separators_pack_ms": e[1][0].elapsed_time(e[1][1]),
-                       "receive_sort_ms": e[2][0].elapsed_time(e[2][1])}
+        self.phases = {"input_ms": ev[0][0].elapsed_time(ev[0][1]),
+                       "sample_ms": ev[0][1].elapsed_time(ev[1][0]),
+                       "separators_pack_ms": ev[2][0].elapsed_time(ev[2][1]),
+                       "receive_sort_ms": ev[3][0].elapsed_time(ev[3][1])}
         self.sent_rows = st[-1]
         return out
 

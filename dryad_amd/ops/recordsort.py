@@ -71,9 +71,46 @@ class SortBuffers:
             ent_b=torch.empty((cap, 2), dtype=torch.int64, device=device),
         )
 
+    @staticmethod
+    def allocate_pitch128(capacity: int, rec: int, device) -> "SortBuffers":
+        """The fine-bucket exchange's working set over a table stored at a 128-byte pitch: rows_in
+        [cap, 128] (the input, one aligned HBM line per record; after the send-side pack, the
+        receive buffer at the record width), rows_out [cap, rec] (send rows, then the output),
+        ent_a [cap] int64 (E64 entries).  The entry sort's ping-pong half lives in rows_out,
+        free until the pack.  ~1.25e9 TeraSort rows: 298 GB."""
+        cap = int(capacity) + 1024
+        rows_out = torch.empty((cap, rec), dtype=torch.uint8, device=device)
+        rows_in = torch.empty((cap, 128), dtype=torch.uint8, device=device)
+        return SortBuffers(rows_in=rows_in, rows_out=rows_out, ent_a=torch.empty(cap, dtype=torch.int64, device=device),
+                           ent_b=torch.empty(0, dtype=torch.int64, device=device))
+
     @property
     def capacity(self) -> int:
-        return self.rows_in.shape[0]
+        """Rows a rank can receive: the output's rows, and what rows_in holds at the record width."""
+        rec = self.rows_out.shape[1]
+        return min(self.rows_out.shape[0], self.rows_in.numel() // rec)
+
+    @property
+    def pitch(self) -> int:
+        return self.rows_in.shape[1]
+
+    def recv_rows(self) -> torch.Tensor:
+        """rows_in as the receive buffer: [capacity, record width] over its flat bytes."""
+        rec = self.rows_out.shape[1]
+        if self.rows_in.shape[1] == rec:
+            return self.rows_in
+        cap = self.rows_in.numel() // rec
+        return self.rows_in.view(-1)[: cap * rec].view(cap, rec)
+
+    def entry_pair(self, n: int, in_out: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
+        """(entries, ping-pong scratch) of n E64 entries.  ``in_out``: the producer wrote the
+        entries into rows_out's first n * 8 bytes (pitch-128 sets, multi-rank: the sort's odd
+        pass count then ends in ent_a, away from the rows the pack writes)."""
+        e64 = self.ent_a.view(-1)
+        if self.ent_b.numel() >= n:
+            return e64[:n], self.ent_b.view(-1)[:n]
+        t = self.rows_out.view(-1)[: n * 8].view(torch.int64)
+        return (t, e64[:n]) if in_out else (e64[:n], t)
 
 
 @dataclass
@@ -83,6 +120,34 @@ class SortStats:
     rounds: int = 1
     send_counts: list = field(default_factory=list)
     recv_counts: list = field(default_factory=list)
+    path: str = ""
+    round_send_bytes: list = field(default_factory=list)
+    round_recv_bytes: list = field(default_factory=list)
+    # HIP events on the compute stream: before the first payload collective is queued, after
+    # round b's wait (its rows usable), after the receive side's last kernel
+    events: dict = field(default_factory=dict)
+
+    def exchange_report(self) -> dict:
+        """Per-round exchange bytes and arrival times (ms after the first payload round was queued:
+        when the compute stream could use round b's rows), and the receive tail after the last
+        arrival.  Call after the step has synchronised."""
+        ev = self.events
+        out = dict(path=self.path, rounds=self.rounds, send_GB=round(sum(self.round_send_bytes) / 1e9, 3),
+                   recv_GB=round(sum(self.round_recv_bytes) / 1e9, 3),
+                   round_send_MB=[round(b / 1e6, 1) for b in self.round_send_bytes],
+                   round_recv_MB=[round(b / 1e6, 1) for b in self.round_recv_bytes])
+        if "start" in ev and ev.get("arrive"):
+            try:
+                ev["done"].synchronize()
+                arr = [ev["start"].elapsed_time(e) for e in ev["arrive"]]
+                out["round_arrival_ms"] = [round(a, 3) for a in arr]
+                out["round_wait_ms"] = [round(b - a, 3) for a, b in zip([0.0] + arr[:-1], arr)]
+                if "done" in ev:
+                    out["receive_tail_ms"] = round(ev["arrive"][-1].elapsed_time(ev["done"]), 3)
+                    out["exchange_to_done_ms"] = round(ev["start"].elapsed_time(ev["done"]), 3)
+            except RuntimeError:          # events not recorded (gloo rehearsal on CPU tensors)
+                pass
+        return out
 
 
 def local_sort_rows(rows: torch.Tensor, out: torch.Tensor, ent_a: torch.Tensor, ent_b: torch.Tensor,
@@ -218,78 +283,184 @@ def _sort_keys(rows: torch.Tensor, ent: torch.Tensor, tmp: torch.Tensor, key_off
     return S.sort_entries(e, b0, b1, tmp=tmp)
 
 
+def _agree(err: BaseException | None, w: World, what: str, value: int = 0):
+    """Gang agreement before a payload collective: every rank's status in one all-gather; if any
+    rank failed, every rank raises GangAgreementError alike (the failing one chaining its own
+    error), so no rank is left inside a collective its peers never enter.  Returns the ranks'
+    values (e.g. their row counts)."""
+    st = shuffle.gang_status(err is None, value, w)
+    bad = [r for r, (ok, _) in enumerate(st) if not ok]
+    if bad:
+        from ..errors import GangAgreementError
+        msg = f"{what}: rank(s) {bad} failed before the exchange"
+        if err is not None:
+            raise GangAgreementError(f"{msg} (rank {w.rank}: {type(err).__name__}: {err})", ranks=bad) from err
+        raise GangAgreementError(msg, ranks=bad)
+    return [v for _, v in st]
+
+
+def _check_capacity(n_recv: int, cap: int, w: World):
+    """Voted capacity check: every rank learns whether any key range overflows its receive
+    buffer BEFORE the payload collectives start; all raise the same non-retryable error (the
+    split is deterministic: a re-execution would overflow again)."""
+    st = shuffle.gang_status(n_recv <= cap, n_recv - cap, w)
+    over = [(r, v) for r, (ok, v) in enumerate(st) if not ok]
+    if over:
+        from ..errors import GangAgreementError
+        raise GangAgreementError(
+            "range partition skew: " + ", ".join(f"rank {r} receives {v} rows past its capacity" for r, v in over)
+            + " (a run of equal keys larger than one rank's buffer, or ShuffleSlack too small)",
+            retryable=False, ranks=[r for r, _ in over])
+
+
+def fine_rows_ok(rec: int, pitch: int, key_off: int, key_len: int, W: int, n: int) -> bool:
+    """The fine-bucket exchange applies: 100-byte records keyed by bytes 0..9 (TeraSort rows),
+    stored at a 100- or 128-byte pitch, 2..64 ranks (sources per merged bucket)."""
+    return (1 < W <= 64 and key_off == 0 and key_len == TSG.KEY_BYTES and rec == TSG.RECORD_BYTES
+            and pitch in (TSG.RECORD_BYTES, 128) and n < (1 << 31))
+
+
 def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int, world: World | None = None,
                           sample_target: int = 1 << 20, seed: int = 314159,
                           stats: SortStats | None = None, keys_ready: bool = False,
                           hi_bounds: tuple[int, int] | None = None, split_ties: bool = True,
-                          keys_fmt: str = "e128", gen: tuple[int, int] | None = None) -> torch.Tensor:
-    """Globally sort the first ``n`` rows of ``bufs.rows_in`` across all ranks.
+                          keys_fmt: str = "e128", gen: tuple[int, int] | None = None,
+                          src: torch.Tensor | None = None) -> torch.Tensor:
+    """Globally sort the first ``n`` rows of ``bufs.rows_in`` (or of ``src``, a table read in
+    place and left intact) across all ranks.
 
     On return rank r holds, in ``bufs.rows_out[:n_r]``, the r-th key range in ascending order.
-    ``bufs.rows_in`` is clobbered (it becomes the receive buffer).  ``keys_ready``: ``bufs.ent_a[:n]``
-    already holds the rows' sort entries; ``hi_bounds``: known hi range of the local keys.
+    ``bufs.rows_in`` is clobbered (it becomes the receive buffer).  ``keys_ready``: the rows'
+    sort entries are already there (``keys_fmt`` "e128": ``bufs.ent_a[:n]``; "e64": E64 entries
+    with the producer's window histograms in ``ent_a``, "e64@out": in rows_out's first n * 8
+    bytes, see SortBuffers.entry_pair); ``hi_bounds``: known hi range of the local keys.
     ``split_ties``: runs of equal keys may be split over ranks (skew); keeps the global order but
     not the co-location of equal keys, so the planner turns it off (keep_ties) when a consumer
-    relies on the output being partitioned by the key.  ``gen = (first, seed)``: ``rows_in`` was
-    never written; row i is gen://terasort record first + i, and the send side works from the
-    generator alone (``keys_fmt`` "gen": no entries either): the fine-bucket exchange of
-    ``pack_gen_fine`` / ``merge_received_rounds``.
+    relies on the output being partitioned by the key.
 
-    With several ranks the exchange is pipelined with the local sort.  The sampled separators cut
-    the key space into ``W * B`` ranges, B consecutive ones per destination rank, and the send
-    buffer is packed round-major (round b = every rank's b-th range), each round queued as an RCCL
-    all-to-all-v as soon as its rows are packed.  Rank r receives round b as one contiguous block
-    holding ALL rows of its key range b, so it sorts range b while rounds b+1.. are still on the
-    wire, and gathers the sorted rows into ``rows_out`` as soon as the send region under them has
-    gone out (``sort_received_rounds``).  Only the last range's sort is exposed after the exchange
-    (reference: the sampler + RangePartition + MergeSort stages of DryadLinqQueryGen.cs:2362-2474,
-    CrossProduct channels GraphBuilder.cs:481-504)."""
+    Three send sides:
+      * fine-bucket exchange over the materialised table (TeraSort rows, the default for such
+        tables, ``send_fine_rows``): E64 entries sorted on the top ``fb`` key bits, the rows
+        packed into the round-major send buffer in fine-bucket order by one gather from the
+        table; the receive side orders each fine bucket in LDS (``merge_received_rounds``).
+      * ``gen = (first, seed)``: ``rows_in`` was never written; row i is gen://terasort record
+        first + i and the send side generates the records into the send rows in bucket order
+        (``pack_gen_fine``; the GenFusedShuffle context property: the read fused with the
+        exchange, no input table).
+      * any other fixed-width table: E128 entries, range destination, stable LDS bucket scatter of
+        the rows, and per received round extract + radix sort + gather (``sort_received_rounds``).
+
+    The sampled separators cut the key space into ``W * B`` ranges, B consecutive ones per
+    destination rank; the send buffer is round-major (round b = every rank's b-th range), each
+    round one RCCL all-to-all-v, all queued up front.  Rank r receives round b as one contiguous
+    block holding ALL rows of its key range b and orders it while rounds b+1.. are in flight,
+    writing into the send region under it once that has gone out.  Before any payload collective
+    the ranks agree (``_agree``, ``_check_capacity``): a rank whose send side failed, or whose
+    key ranges overflow its buffers, stops every rank alike instead of leaving its peers in the
+    exchange (reference: the sampler + RangePartition + MergeSort stages of
+    DryadLinqQueryGen.cs:2362-2474, CrossProduct channels GraphBuilder.cs:481-504)."""
     w = world or get_world()
-    rows = bufs.rows_in[:n]
-    gen_path = gen is not None and 1 < w.size <= 64 and key_off == 0 and key_len == TSG.KEY_BYTES \
-        and rows.shape[1] == TSG.RECORD_BYTES and n < (1 << 31)       # (64: sources per merged bucket)
+    W = w.size
+    rec = bufs.rows_out.shape[1]
+    pitch = bufs.pitch
+    rows = bufs.rows_in[:n, :rec] if src is None else src[:n]
+    if src is not None:
+        assert src.shape[1] == rec and gen is None and not keys_ready, "src: [n, record width] rows, no producer keys"
+        pitch = rec
+    gen_path = gen is not None and fine_rows_ok(rec, pitch, key_off, key_len, W, n) and pitch == rec
     if gen is not None and not gen_path:
-        TSG.generate(rows, gen[0], gen[1])       # the records are needed after all
+        TSG.generate(bufs.rows_in[:n], gen[0], gen[1])       # the records are needed after all
         gen = None
         if keys_fmt == "gen":
             keys_ready = False
-    if w.size == 1:
-        out = local_sort_rows(rows, bufs.rows_out, bufs.ent_a, bufs.ent_b, key_off, key_len,
-                              hi_bounds=hi_bounds, keys_ready=keys_ready, keys_fmt=keys_fmt)
+    if W == 1:
+        if src is not None:
+            bufs.rows_in[:n].copy_(src[:n])
+            rows = bufs.rows_in[:n]
+        if pitch != rec:
+            out = S.sort_rows_pitch128(bufs.rows_in[:n], bufs.rows_out, bufs.ent_a, key_off, key_len,
+                                       keys_ready=keys_ready and keys_fmt == "e64")
+        else:
+            out = local_sort_rows(rows, bufs.rows_out, bufs.ent_a, bufs.ent_b, key_off, key_len,
+                                  hi_bounds=hi_bounds, keys_ready=keys_ready, keys_fmt=keys_fmt)
         if stats is not None:
             stats.n_in = stats.n_out = n
+            stats.path = "local"
         return out
-    W, stride = w.size, rows.shape[1]
+    fine_rows = gen is None and fine_rows_ok(rec, pitch, key_off, key_len, W, n)
+    if pitch != bufs.pitch and not fine_rows:
+        raise ValueError("distributed_sort_rows: a src table needs a buffer set at its record width")
+    if pitch != rec and not fine_rows:
+        raise ValueError(f"distributed_sort_rows: a {pitch}-byte-pitch table needs the fine-bucket exchange")
     _, _, lo_mask = key_bits(key_len)
     split = split_ties and key_len <= 10 and W < (1 << 16)
     # skew: equal keys must not all land on one rank.  Bits 47..32 of lo are free for keys of
     # <= 10 bytes; with the rank there (and the row index below it) every entry is unique, so the
     # sampled separators split runs of equal keys across ranks while the global order (key, rank,
-    # row) stays a valid OrderBy order.
+    # row) stays a valid OrderBy order.  (The fine-bucket paths cut separators to bucket edges:
+    # equal keys stay on one rank there.)
     part_mask = _M64 if split else lo_mask
     lo_or = (w.rank << 32) if split else 0
-    nmax = torch.tensor([n], dtype=torch.int64, device=w.device)
-    shuffle.all_reduce_(nmax, "max", w)
-    B = pipeline_subs(int(nmax.item()) * stride, W)
+    err = None
+    samp = None
+    try:
+        if gen_path:
+            samp = gen_samples(gen, n, w.rank, lo_or, part_mask, sample_target, seed, w.device)
+        elif fine_rows:
+            in_out = keys_ready and keys_fmt == "e64@out"
+            e, tmp = bufs.entry_pair(n, in_out=in_out)
+            hist = S.take_gen_hist(e) if keys_ready and keys_fmt in ("e64", "e64@out") else None
+            if hist is None and not (keys_ready and keys_fmt in ("e64", "e64@out")):
+                e, hist = S.extract_keys64_tile(rows, key_off, key_len, 0, e, hist=True)
+            samp = e64_samples(e, n, w.rank, sample_target, seed)
+        else:
+            if keys_fmt != "e128":
+                keys_ready = False
+            ent = bufs.ent_a[:n] if keys_ready else S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
+            if split:
+                ent[:, 0].bitwise_or_(lo_or)
+    except Exception as ex:  # noqa: BLE001
+        err = ex
+    nmax = max(_agree(err, w, "distributed OrderBy (entries)", n))
+    B = pipeline_subs(nmax * rec, W)
     pack = None
     fine = None
-    if gen_path:
-        seps = separators_from_samples(
-            shuffle.all_gather_varlen(gen_samples(gen, n, w.rank, lo_or, part_mask, sample_target, seed, w.device), w),
-            W * B)
-        fb = fine_bits(int(nmax.item()) * W)
-        st, pack, counts, L = pack_gen_fine(bufs, gen, n, [int(x) & _M64 for x in seps[:, 1].tolist()], B, W, fb)
-        fine = exchange_fine_counts(counts, L, B, W, w)
+    try:
+        if gen_path or fine_rows:
+            seps = separators_from_samples(shuffle.all_gather_varlen(samp, w), W * B)
+            fb = fine_bits(nmax * W)
+            seps_hi = [int(x) & _M64 for x in seps[:, 1].tolist()]
+            if fine_rows and split and _fine_collapsed(seps_hi, fb) and bufs.ent_b.numel() >= 2 * n:
+                # heavy duplication: two separators inside one fine bucket.  The fine cut would give
+                # the whole bucket to one rank; the E128 path splits runs of equal keys (key, rank,
+                # row) instead.  The separators are global, so every rank switches alike.
+                fine_rows = False
+                ent = S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
+                ent[:, 0].bitwise_or_(lo_or)
+                seps = choose_separators(ent, n, w, part_mask, sample_target, seed, bufs.ent_b, parts=W * B)
+                seps_hi = [int(x) & _M64 for x in seps[:, 1].tolist()]
+            elif gen_path:
+                st, pack, counts, L = pack_gen_fine(bufs, gen, n, seps_hi, B, W, fb)
+            if fine_rows:
+                st, counts, L, bad = send_fine_rows(bufs, rows, e, tmp, hist, n, seps_hi, B, W, fb,
+                                                    rebuild=lambda: S.extract_keys64_tile(rows, key_off, key_len, 0, e)[0])
+        else:
+            seps = choose_separators(ent, n, w, part_mask, sample_target, seed, bufs.ent_b, parts=W * B)
+            seps_hi = [int(x) & _M64 for x in seps[:, 1].tolist()]
+    except Exception as ex:  # noqa: BLE001
+        err = ex
     else:
-        if keys_fmt != "e128":
-            keys_ready = False
-        ent = bufs.ent_a[:n] if keys_ready else S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
-        if split:
-            ent[:, 0].bitwise_or_(lo_or)
-        seps = choose_separators(ent, n, w, part_mask, sample_target, seed, bufs.ent_b, parts=W * B)
-        S.range_dest(ent, seps, part_mask, subs=B, ranks=W)                  # ent.hi := b * W + rank
-        st = S.bucket_scatter_rows(ent, rows, bufs.rows_out)                # send buffer, round-major
-    seps_hi = [int(x) & _M64 for x in seps[:, 1].tolist()]
+        err = None
+    if err is None and not (gen_path or fine_rows):
+        # (choose_separators holds a collective: the agreement after it covers range_dest + scatter)
+        try:
+            S.range_dest(ent, seps, part_mask, subs=B, ranks=W)                  # ent.hi := b * W + rank
+            st = S.bucket_scatter_rows(ent, rows, bufs.rows_out)                # send buffer, round-major
+        except Exception as ex:  # noqa: BLE001
+            err = ex
+    _agree(err, w, "distributed OrderBy (send side)")
+    if gen_path or fine_rows:
+        fine = exchange_fine_counts(counts, L, B, W, w)
     send = [[st[b * W + r + 1] - st[b * W + r] for r in range(W)] for b in range(B)]
     sc = torch.tensor([[send[b][r] for b in range(B)] for r in range(W)], dtype=torch.int64)
     rc = shuffle.exchange_counts(sc.flatten(), w).view(W, B).tolist()    # rc[src][b]
@@ -297,28 +468,111 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     for b in range(B):
         off.append(off[-1] + sum(rc[s][b] for s in range(W)))
     n_recv = off[-1]
-    if n_recv > bufs.capacity:
-        raise RuntimeError(f"range partition skew: rank {w.rank} receives {n_recv} rows > capacity {bufs.capacity}")
-    send_flat, recv_flat = bufs.rows_out.view(-1), bufs.rows_in.view(-1)
+    _check_capacity(n_recv, bufs.capacity, w)
+    recv_rows = bufs.recv_rows()
+    send_flat, recv_flat = bufs.rows_out.view(-1), recv_rows.view(-1)
+    ev = {}
+    if stats is not None and bufs.rows_out.is_cuda:
+        ev = dict(start=torch.cuda.Event(enable_timing=True), done=torch.cuda.Event(enable_timing=True),
+                  arrive=[torch.cuda.Event(enable_timing=True) for _ in range(B)])
+        ev["start"].record()
     handles = []
     for b in range(B):
         if pack is not None:
             pack(b)                    # round b's rows packed (compute stream) before it is queued
         handles.append(shuffle.alltoallv_bytes_async(
-            send_flat[st[b * W] * stride: st[(b + 1) * W] * stride], [c * stride for c in send[b]],
-            recv_flat[off[b] * stride: off[b + 1] * stride], [rc[s][b] * stride for s in range(W)], w))
+            send_flat[st[b * W] * rec: st[(b + 1) * W] * rec], [c * rec for c in send[b]],
+            recv_flat[off[b] * rec: off[b + 1] * rec], [rc[s][b] * rec for s in range(W)], w))
+
+    def wait(b):
+        shuffle.wait(handles[b])
+        if ev:
+            ev["arrive"][b].record()
     sent_after = [st[(b + 1) * W] for b in range(B)]
     if fine is not None:
-        out = merge_received_rounds(bufs, off, fine, L, fb, B, w.rank, sent_after, n,
-                                    wait=lambda b: shuffle.wait(handles[b]))
+        out = merge_received_rounds(bufs, off, fine, L, fb, B, w.rank, sent_after, n, wait=wait)
     else:
-        out = sort_received_rounds(bufs, off, sent_after, n, seps_hi, B, w.rank, key_off, key_len,
-                                   wait=lambda b: shuffle.wait(handles[b]))
+        out = sort_received_rounds(bufs, off, sent_after, n, seps_hi, B, w.rank, key_off, key_len, wait=wait)
+    if ev:
+        ev["done"].record()
+    if fine_rows and int(bad.item()):
+        raise RuntimeError("fine-bucket send side: an entry named a row past the table (corrupt entries)")
     if stats is not None:
         stats.n_in, stats.n_out, stats.rounds = n, n_recv, B
         stats.send_counts = [sum(send[b][r] for b in range(B)) for r in range(W)]
         stats.recv_counts = [sum(rc[s]) for s in range(W)]
+        stats.path = ("fine-bucket exchange, records generated into the send rows" if gen_path else
+                      f"fine-bucket exchange over the table (pitch {pitch})" if fine_rows else
+                      "E128 range partition + per-round radix sort")
+        stats.round_send_bytes = [(st[(b + 1) * W] - st[b * W] - send[b][w.rank]) * rec for b in range(B)]
+        stats.round_recv_bytes = [(off[b + 1] - off[b] - rc[w.rank][b]) * rec for b in range(B)]
+        stats.events = ev
     return out[:n_recv]
+
+
+def _fine_collapsed(seps_hi: list, fb: int) -> bool:
+    """Two separators fall into one fine bucket (some key range would be empty and one bucket
+    would carry a whole range's share of rows): heavily duplicated keys."""
+    L = fine_bounds(seps_hi, fb)
+    return any(L[g] == L[g + 1] for g in range(1, len(L) - 2))
+
+
+def e64_samples(e: torch.Tensor, n: int, rank: int, sample_target: int, seed: int) -> torch.Tensor:
+    """``choose_separators``' sample of one rank taken from its E64 entries (key bytes 0..3 in the
+    high word): [m, 2] int64 sample entries whose hi word holds those key bits.  The fine-bucket
+    exchange cuts separators to the top fb <= 24 key bits, which the window holds."""
+    m, stride = sample_count(n, sample_target)
+    off = sample_offset(seed, rank, stride)
+    w = e[off: off + stride * m: stride][:m]
+    samp = torch.zeros((w.shape[0], 2), dtype=torch.int64, device=e.device)
+    samp[:, 1] = w & _as_i64(0xFFFFFFFF00000000)
+    return samp
+
+
+def send_fine_rows(bufs: SortBuffers, rows: torch.Tensor, e: torch.Tensor, tmp: torch.Tensor, hist, n: int,
+                   seps_hi: list, B: int, W: int, fb: int, rebuild=None):
+    """Send side of the fine-bucket exchange over a materialised table (``rows``: [n, 100] at a
+    100- or 128-byte pitch): one look-back sort of the rows' E64 entries ``e`` (window = key bytes
+    0..3, with the producer's / extraction's histograms ``hist``) on the top 8 * ceil(fb / 8) key
+    bits, the fine-bucket starts of the sorted order, then ONE gather of the rows into the
+    round-major send buffer ``bufs.rows_out`` (round b = key range r * B + b for every
+    destination r, each piece in fine-bucket order; ts_pack_rows: 16-byte loads, one HBM line per
+    row at pitch 128).  The pack runs to completion before the exchange: the receive buffer is
+    the table's own memory.  A failed look-back sort (``err``) keeps the pack from reading and
+    is redone with count + scatter passes over ``rebuild()``'s entries.  Returns (send-row starts
+    st[b * W + r], per-bucket row counts (device int32 [2^fb]), fine bounds L)."""
+    err = S.lookback_error()
+    win = 8 * ((fb + 7) // 8)
+    srt = S.sort_entries64(e, tmp, win, gen_hist=hist, err=err)
+    starts = TSG.fine_starts(srt, fb)
+    L = fine_bounds(seps_hi, fb)
+    Lt = torch.tensor(L, dtype=torch.int64, device=e.device)
+    host = torch.cat([starts.index_select(0, Lt).to(torch.int64), err.to(torch.int64)]).tolist()
+    Sg = host[:-1]
+    if host[-1]:                  # the look-back sort gave up: entries again, count + scatter passes
+        e2 = rebuild() if rebuild is not None else e
+        srt = S.sort_entries64(e2, tmp if e2.data_ptr() == e.data_ptr() else e, win, lookback=False)
+        starts = TSG.fine_starts(srt, fb)
+        Sg = starts.index_select(0, Lt).tolist()
+        err = None
+    counts = starts[1:] - starts[:-1]
+    st, acc = [], 0
+    for b in range(B):
+        for r in range(W):
+            st.append(acc)
+            acc += Sg[r * B + b + 1] - Sg[r * B + b]
+    st.append(acc)
+    if srt.data_ptr() == bufs.rows_out.data_ptr():
+        # (an even pass count left the entries in rows_out, which the pack writes: move them)
+        e64 = bufs.ent_a.view(-1)[:n] if bufs.ent_a.data_ptr() != srt.data_ptr() else None
+        if e64 is None or e64.numel() < n:
+            raise RuntimeError("send_fine_rows: no room for the sorted entries outside the send buffer")
+        e64.copy_(srt)
+        srt = e64
+    segs = torch.tensor([[st[b * W + r], Sg[r * B + b]] for b in range(B) for r in range(W)],
+                        dtype=torch.int64).to(e.device)
+    bad = TSG.pack_rows(bufs.rows_out, rows, srt, acc, seg=segs, err=err)
+    return st, counts, L, bad
 
 
 # Fine buckets of the gen:// exchange: the top ``fb`` key bits, about FINE_ROWS rows of the whole
@@ -431,6 +685,7 @@ def merge_received_rounds(bufs: SortBuffers, off: list, fine: torch.Tensor, L: l
     have gone out (``sent_after``, as in sort_received_rounds).  A bucket too large for LDS (heavy
     key skew) flags its round, which is then sorted after the last round with local_sort_rows."""
     out = bufs.rows_out
+    recv = bufs.recv_rows()
     W, Kme = fine.shape
     flags = torch.zeros(B, dtype=torch.int32, device=out.device)
     base = L[rank * B]
@@ -459,7 +714,7 @@ def merge_received_rounds(bufs: SortBuffers, off: list, fine: torch.Tensor, L: l
         for item in pending:
             a2, z2, b2, pre, cnt, outoff = item
             if b == B - 1 or z2 <= sent_after[b] or a2 >= n_sent:
-                TSG.tile_merge(bufs.rows_in, out, pre, cnt, outoff, fb, flags[b2:b2 + 1])
+                TSG.tile_merge(recv, out, pre, cnt, outoff, fb, flags[b2:b2 + 1])
             else:
                 keep.append(item)
         pending = keep
@@ -467,9 +722,26 @@ def merge_received_rounds(bufs: SortBuffers, off: list, fine: torch.Tensor, L: l
     for b in range(B):
         if fl[b]:
             a, z = off[b], off[b + 1]
-            local_sort_rows(bufs.rows_in[a:z], out[a:z], bufs.ent_a[a:z], bufs.ent_b[a:z], 0, key_len,
-                            hi_bounds=fine_hi_bounds(L, fb, rank * B + b))
+            ea, eb = _round_scratch(bufs, off[-1], a, z)
+            local_sort_rows(recv[a:z], out[a:z], ea, eb, 0, key_len, hi_bounds=fine_hi_bounds(L, fb, rank * B + b))
     return out[: off[-1]]
+
+
+def _round_scratch(bufs: SortBuffers, n_recv: int, a: int, z: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """Two [z - a, 2] int64 entry arrays for re-sorting received rows a..z after the exchange: the
+    buffer set's entry arrays when it has 16-byte ones, else the free tail of rows_in past the
+    received rows (a pitch-128 set: ~28 bytes per row), else fresh memory."""
+    m = z - a
+    if bufs.ent_b.numel() >= 2 * z and bufs.ent_a.numel() >= 2 * z:
+        return bufs.ent_a.view(-1, 2)[a:z], bufs.ent_b.view(-1, 2)[a:z]
+    rec = bufs.rows_out.shape[1]
+    flat = bufs.rows_in.view(-1)
+    lo = (n_recv * rec + 255) // 256 * 256
+    if flat.numel() - lo >= 32 * m:
+        t = flat[lo: lo + 32 * m].view(torch.int64).view(2, m, 2)
+        return t[0], t[1]
+    return (torch.empty((m, 2), dtype=torch.int64, device=flat.device),
+            torch.empty((m, 2), dtype=torch.int64, device=flat.device))
 
 
 def sort_received_rounds(bufs: SortBuffers, off: list, sent_after: list, n_sent: int, seps_hi: list, B: int,
@@ -507,7 +779,8 @@ def sort_received_rounds(bufs: SortBuffers, off: list, sent_after: list, n_sent:
         for a2, z2, b2, (fmt, s2, win) in pending:
             if b == B - 1 or z2 <= sent_after[b] or a2 >= n_sent:
                 if fmt == "e64":
-                    S.gather_fixup(bufs.rows_in[a2:z2], s2, out[a2:z2], key_off, key_len, win, flags[b2, :1])
+                    S.gather_fixup(bufs.rows_in[a2:z2], s2, out[a2:z2], key_off, key_len, win, flags[b2, :1],
+                                   err=flags[b2, 1:])
                 else:
                     S.gather_rows(bufs.rows_in[a2:z2], entries=s2, out=out[a2:z2])
             else:

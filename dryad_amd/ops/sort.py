@@ -255,9 +255,9 @@ _lib.register_signatures({
     "dr_sort_u64": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_u64, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "dr_gather_fixup": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_u64, c_u32, c_u32, c_u32,
-                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "dr_gather_fixup_pitch128": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_u64, c_u32, c_u32,
-                                                c_u32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+                                                c_u32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "dr_rekey64": (ctypes.c_int, [ctypes.c_void_p, c_u32, c_u32, c_u32, c_u32, ctypes.c_void_p, c_u64, ctypes.c_void_p]),
     "dr_e64_position_window": (ctypes.c_int, [ctypes.c_void_p, c_u64, ctypes.c_void_p]),
     "dr_sort_u64_onesweep_workspace": (c_u64, [c_u64]),
@@ -374,10 +374,13 @@ def sort_entries64(e: torch.Tensor, tmp: torch.Tensor, win: int, gen_hist: torch
 
 
 def gather_fixup(rows: torch.Tensor, srt: torch.Tensor, out: torch.Tensor, key_off: int, key_len: int,
-                 win: int, flag: torch.Tensor):
+                 win: int, flag: torch.Tensor, err: torch.Tensor | None = None):
+    """Row gather through window-sorted E64 entries with the run fix-up.  ``flag`` (int32) gets
+    bit 0 when a run outgrows the window, bit 1 when an entry names a row past ``rows`` (never
+    read); ``err``: the look-back sort's error word, when set the kernel reads nothing."""
     n, stride = rows.shape
     _lib.call("dr_gather_fixup", ptr(rows), ptr(out), ptr(srt), c_u64(n), c_u32(stride), c_u32(key_off),
-              c_u32(key_len), 64 - win, ptr(flag), stream_of(rows))
+              c_u32(key_len), 64 - win, ptr(flag), ptr(err), stream_of(rows))
 
 
 def compact_sort_ok(rows: torch.Tensor, key_len: int) -> bool:
@@ -410,7 +413,7 @@ def sort_rows_compact(rows: torch.Tensor, out: torch.Tensor, ent: torch.Tensor, 
     win = min(window_bits64(n), max(8, ((8 * key_len - P + 7) // 8) * 8), 32)
     flags = torch.zeros(2, dtype=torch.int32, device=rows.device)        # [gather overflow, look-back error]
     srt = sort_entries64(e, tmp, win, err=flags[1:])
-    gather_fixup(rows, srt, out, key_off, key_len, win, flags[:1])
+    gather_fixup(rows, srt, out, key_off, key_len, win, flags[:1], err=flags[1:])
     if stats is not None:
         stats["path"] = f"compact win={win} prefix={P}"
     overflow, failed = (int(x) != 0 for x in flags.tolist())
@@ -474,14 +477,14 @@ PITCH = 128
 
 
 def gather_fixup_pitch128(rows_p: torch.Tensor, srt: torch.Tensor, out: torch.Tensor, key_off: int, key_len: int,
-                          win: int, flag: torch.Tensor):
+                          win: int, flag: torch.Tensor, err: torch.Tensor | None = None):
     """gather_fixup from ``rows_p`` ([n, 128] uint8: the first 100 bytes of each row are the record)
     into ``out`` ([n, 100], back to back)."""
     n = rows_p.shape[0]
     if rows_p.shape[1] != PITCH or out.shape[1] != 100 or not rows_p.is_contiguous():
         raise ValueError("gather_fixup_pitch128: [n, 128] input rows and [n, 100] output rows")
     _lib.call("dr_gather_fixup_pitch128", ptr(rows_p), ptr(out), ptr(srt), c_u64(n), c_u32(100), c_u32(key_off),
-              c_u32(key_len), 64 - win, ptr(flag), stream_of(rows_p))
+              c_u32(key_len), 64 - win, ptr(flag), ptr(err), stream_of(rows_p))
 
 
 def rekey64(rows: torch.Tensor, ent: torch.Tensor, key_off: int, key_len: int, P: int) -> torch.Tensor:
@@ -530,7 +533,7 @@ def sort_rows_pitch128(rows_p: torch.Tensor, out: torch.Tensor, keys: torch.Tens
         _sort64_into(e, tmp, win, gen_hist, err=flags[1:])
         if gen_hist is not None and n >= ONESWEEP_MIN:
             path += " gen-hist"
-        gather_fixup_pitch128(rows_p, e, out[:n], key_off, key_len, win, flag)
+        gather_fixup_pitch128(rows_p, e, out[:n], key_off, key_len, win, flag, err=flags[1:])
         path += f" win={win}"
         overflow, failed = (int(x) != 0 for x in flags.tolist())
         chain = overflow or failed
@@ -552,7 +555,7 @@ def sort_rows_pitch128(rows_p: torch.Tensor, out: torch.Tensor, keys: torch.Tens
             rekey64(rows_p, e, key_off, key_len, P)
             _sort64_into(e, tmp, 32, err=flags[1:], lookback=lookback)
         _lib.call("dr_e64_position_window", ptr(e), c_u64(n), stream_of(e))
-        gather_fixup_pitch128(rows_p, e, out[:n], key_off, key_len, 32, flag)
+        gather_fixup_pitch128(rows_p, e, out[:n], key_off, key_len, 32, flag, err=flags[1:])
         if int(flags[1].item()) != 0:           # a look-back pass of the chain failed: once more without
             torch.arange(n, out=e)
             for P in windows:

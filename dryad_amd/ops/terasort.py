@@ -179,3 +179,36 @@ def tile_merge(rows: torch.Tensor, out: torch.Tensor, pre: torch.Tensor, cnt: to
     _lib.call("dr_ts_tile_merge", ptr(rows), ptr(out), ptr(pre.contiguous()), ptr(cnt.contiguous()),
               ptr(outoff.contiguous()), c_u32(W), c_u32(K), c_u32(fb), ptr(overflow), stream_of(rows))
     _lib.written(out)
+
+
+_lib.register_signatures({
+    "dr_ts_pack_rows": (ctypes.c_int, [ctypes.c_void_p, c_u64, c_u32, ctypes.c_void_p, c_u64, ctypes.c_void_p, c_u32,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+})
+
+
+def pack_rows(out: torch.Tensor, rows: torch.Tensor, ent: torch.Tensor, n: int, seg: torch.Tensor | None = None,
+              err: torch.Tensor | None = None, bad: torch.Tensor | None = None) -> torch.Tensor:
+    """Send rows of a materialised table: ``out[p]`` := ``rows[ent[q(p)] & 0xFFFFFFFF]`` for p < n
+    (``rows`` [n_in, 100] or [n_in, 128] uint8 holding 100-byte records, ``out`` [>= n, 100]);
+    q(p) = p, or through ``seg`` (device int64 [nseg <= 256, 2] of {out row, entry}, ascending,
+    seg[0, 0] = 0).  ``err``: the look-back sort's error word (nothing is read when it is set);
+    ``bad`` (int32 [1]) is set when an entry names a row past n_in.  Returns ``bad``."""
+    _lib.require_gpu_tensor(out, "terasort.pack_rows")
+    pitch = rows.stride(0)
+    assert rows.dtype == torch.uint8 and pitch in (100, 128) and rows.stride(1) == 1
+    assert out.dtype == torch.uint8 and out.shape[1] == RECORD_BYTES and out.is_contiguous() and out.shape[0] >= n
+    assert ent.dtype == torch.int64 and ent.is_contiguous()
+    nseg = 0
+    if seg is not None:
+        assert seg.dtype == torch.int64 and seg.is_contiguous() and seg.dim() == 2 and seg.shape[1] == 2
+        nseg = seg.shape[0]
+        assert nseg <= 256
+    else:
+        assert ent.shape[0] >= n
+    if bad is None:
+        bad = torch.zeros(1, dtype=torch.int32, device=out.device)
+    _lib.call("dr_ts_pack_rows", ptr(rows), c_u64(rows.shape[0]), c_u32(pitch), ptr(ent), c_u64(n), ptr(seg),
+              c_u32(nseg), ptr(out), ptr(err), ptr(bad), stream_of(out))
+    _lib.written(out)
+    return bad

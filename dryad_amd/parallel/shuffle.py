@@ -38,6 +38,14 @@ def exchange_counts(send_counts: torch.Tensor, world: World | None = None) -> to
     return r.to(send_counts.device)
 
 
+def _native(w: World, *tensors) -> bool:
+    """The tensors live where the backend moves data itself: HBM under RCCL, host memory under
+    gloo.  These transfers take the collective branches (async handles, split sizes, chunked P2P
+    rounds); a gloo CPU run exercises exactly the code an RCCL run executes."""
+    want_cuda = w.backend == "nccl"
+    return all(t.is_cuda == want_cuda for t in tensors)
+
+
 def alltoallv_bytes(send: torch.Tensor, send_counts: list[int], recv: torch.Tensor, recv_counts: list[int],
                     world: World | None = None):
     """All-to-all-v over flat uint8 views: ``send`` is grouped by destination with
@@ -52,7 +60,7 @@ def alltoallv_bytes(send: torch.Tensor, send_counts: list[int], recv: torch.Tens
     assert len(send_counts) == w.size and len(recv_counts) == w.size
     total_s, total_r = sum(send_counts), sum(recv_counts)
     assert send.numel() >= total_s and recv.numel() >= total_r
-    if w.backend != "nccl" and (send.is_cuda or recv.is_cuda):
+    if not _native(w, send, recv):
         # gloo transport for device buffers (tests / shared-GPU ranks): stage through host memory
         s_cpu = send[:total_s].cpu()
         r_cpu = torch.empty(total_r, dtype=torch.uint8)
@@ -111,7 +119,7 @@ def alltoallv_bytes_async(send: torch.Tensor, send_counts: list[int], recv: torc
     on the wire).  Other transports (gloo staging through the host, rounds chunked past
     CHUNK_BYTES per peer) complete before returning and give ``None``."""
     w = world or get_world()
-    if (w.size > 1 and w.backend == "nccl" and send.is_cuda and recv.is_cuda
+    if (w.size > 1 and _native(w, send, recv)
             and max(max(send_counts), max(recv_counts)) <= CHUNK_BYTES):
         ts, tr = sum(send_counts), sum(recv_counts)
         return dist.all_to_all_single(recv[:tr], send[:ts], output_split_sizes=list(recv_counts),
@@ -124,6 +132,18 @@ def wait(handle) -> None:
     """Make the current stream wait for an ``alltoallv_bytes_async`` handle."""
     if handle is not None:
         handle.wait()
+
+
+def gang_status(ok: bool, value: int = 0, world: World | None = None) -> list[tuple[bool, int]]:
+    """Every rank's (ok, value) from one small all-gather: the agreement a gang stage reaches
+    before it enters a payload collective (ops/recordsort: a rank whose pre-exchange work failed,
+    or whose key range overflows its receive buffer, says so here and every rank stops alike)."""
+    w = world or get_world()
+    if w.size == 1:
+        return [(bool(ok), int(value))]
+    dev = w.device if w.backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([[1 if ok else 0, int(value)]], dtype=torch.int64, device=dev)
+    return [(bool(a), int(b)) for a, b in all_gather_tensor(t, w).tolist()]
 
 
 def all_gather_tensor(t: torch.Tensor, world: World | None = None) -> torch.Tensor:

@@ -188,9 +188,14 @@ class GpuJobRunner:
         p = R.Params()
         p.max_failures = int(getattr(ctx, "MaxVertexFailures", 6) or 6)
         # speculative duplicates (DrDefaultManager::CheckForDuplicates) only for leaf stages outside
-        # gangs: a duplicate re-reads the vertex's source on an idle rank (no collective inside)
-        p.speculative = bool(getattr(ctx, "EnableSpeculativeDuplication", True)) and world.size > 1
+        # gangs: a duplicate re-reads the vertex's source on an idle rank (no collective inside).
+        # On one node of identical GPUs the reference's adaptive threshold (>= 10 s,
+        # DrStageStatistics.cpp:93-111) almost never fires, while the speculative stage loop polls
+        # a collective every SPEC_POLL behind the vertices' kernels: the GPU executor speculates
+        # only under an explicit straggler policy (OutlierThresholdSeconds set).
         thr = ctx._props.get("OutlierThresholdSeconds")
+        p.speculative = bool(getattr(ctx, "EnableSpeculativeDuplication", True)) and world.size > 1 \
+            and thr is not None
         if thr is not None:
             p.default_outlier_threshold = float(thr)
             p.min_outlier_threshold = min(p.min_outlier_threshold, float(thr))
@@ -305,7 +310,10 @@ class GpuJobRunner:
         spec = None
         if ok:
             t = self.channels.get((f["x"], self.world.rank))
-            ok = isinstance(t, DeviceTable) and t.rows is not None and (f["x"], self.world.rank) in self.row_sets
+            # a table in a pooled buffer set is sorted in place; any other row table (an hbm://
+            # input, a previous job's output) is read where it is, into a set of its own
+            ok = isinstance(t, DeviceTable) and t.rows is not None and (
+                (f["x"], self.world.rank) in self.row_sets or (self.pool is not None and t.rows.is_contiguous()))
             if ok:
                 try:
                     kind, spec = TR.key_columns(TR.call(f["key"], t), t)
@@ -327,7 +335,7 @@ class GpuJobRunner:
         op_read writes just the sort entries (ops/gpu: lazy_gen) and the records are generated
         straight into the exchange's send buckets."""
         st, out = self.plan.stages, set()
-        if self.world.size < 2 or not self.gpu_ok:
+        if self.world.size < 2 or not self.gpu_ok or not self.ctx._props.get("GenFusedShuffle", False):
             return out
         for f in self.fused.values():
             x = st[f["x"]]
@@ -346,10 +354,12 @@ class GpuJobRunner:
         instead of ~1.78.  ``LineAlignedSortInput=False`` (context property) turns it off.
         Returns {stage id: (key offset, key length)}."""
         out = {}
-        if self.world.size != 1 or not self.gpu_ok or not self.ctx._props.get("LineAlignedSortInput", True):
+        if not self.gpu_ok or not self.ctx._props.get("LineAlignedSortInput", True):
             return out
         from ..gpu import trace as TR
         from ..gpu.table import Shape
+        if self.world.size > 1:
+            return self._pitch_fused_reads()
         for x in self.plan.stages:
             if not (not x.inputs and len(x.ops) >= 2 and x.ops[0]["op"] == "read" and x.ops[1]["op"] == "sort"
                     and _rows100_source(x.ops[0]["uri"])
@@ -365,6 +375,35 @@ class GpuJobRunner:
                 out[x.id] = (spec.off, spec.length)
         return out
 
+    def _pitch_fused_reads(self) -> dict:
+        """Several ranks: read stages of 100-byte rows (gen://terasort or a stored ``format: rows``
+        table) that only a fused distributed OrderBy on key bytes 0..9 consumes.  Their op_read
+        stores the records at a 128-byte pitch with the E64 entries (+ window histograms) in the
+        send buffer's memory, and the fused stage runs the fine-bucket exchange over that table
+        (ops/recordsort.send_fine_rows: the send-side row gather reads one HBM line per record).
+        ``GenFusedShuffle`` keeps gen:// reads lazy instead (records generated into the send rows)."""
+        from ..gpu import trace as TR
+        from ..gpu.table import Shape
+        from ..ops import recordsort as RS
+        st, out = self.plan.stages, {}
+        lazy = self._lazy_gen_reads()
+        for f in self.fused.values():
+            x = st[f["x"]]
+            if (x.id in lazy or x.inputs or len(x.ops) != 1 or x.ops[0]["op"] != "read"
+                    or not _rows100_source(x.ops[0]["uri"]) or f["comparer"] is not None or f["desc"]
+                    or set(self.plan.consumers(x.id)) != {f["stages"][0], f["stages"][2]}
+                    or not RS.fine_rows_ok(100, 128, 0, 10, self.world.size, 1)):
+                continue
+            rows = torch.zeros((2, 100), dtype=torch.uint8, device=self.dev)
+            t = DeviceTable(2, Shape("rows", key_off=0, key_len=10), rows=rows)
+            try:
+                kind, spec = TR.key_columns(TR.call(f["key"], t), t)
+            except Exception:  # noqa: BLE001
+                continue
+            if kind == "bytes" and spec.off == 0 and spec.length == 10:
+                out[x.id] = (0, 10)
+        return out
+
     def _materialize(self, sid: int):
         """Write the records of lazy gen reads of stage sid (its consumers are not fused after all)."""
         for p in range(self.plan.stages[sid].partitions):
@@ -378,21 +417,30 @@ class GpuJobRunner:
         from ..ops import recordsort as RS
         me = self.world.rank
         t = self.channels[(f["x"], me)]
-        bs = self.row_sets[(f["x"], me)]
+        bs = self.row_sets.get((f["x"], me))
         off, ln = f["spec"]
         stats = RS.SortStats()
-        f["consumed"] = (bs.lazy_gen, bs.keys_ready)      # what a retry restores (gen inputs)
-        kr = bs.take_keys(t.rows, off, ln)
-        gen, bs.lazy_gen = bs.lazy_gen, None
-        f["clobbered"] = True                             # rows_in becomes the receive buffer
-        if gen is not None and kr is None:         # entries were not claimed: records are needed
-            bs.lazy_gen = gen
-            bs.materialize(t.n)
-            gen = None
+        src = None
+        if bs is None:
+            # the input table is not ours to clobber: its rows are read in place (entries, the
+            # send-side pack) and the exchange works in a buffer set of its own
+            slack = self.ctx._props.get("ShuffleSlack", 0.01)
+            bs = self.pool.acquire(int(t.n * (1 + slack)) + 1024, t.rows.shape[1])
+            src = t.rows
+            kr, gen = None, None
+        else:
+            f["consumed"] = (bs.lazy_gen, bs.keys_ready)      # what a retry restores (gen inputs)
+            kr = bs.take_keys(t.rows, off, ln)
+            gen, bs.lazy_gen = bs.lazy_gen, None
+            f["clobbered"] = True                             # rows_in becomes the receive buffer
+            if gen is not None and kr is None:         # entries were not claimed: records are needed
+                bs.lazy_gen = gen
+                bs.materialize(t.n)
+                gen = None
         out = RS.distributed_sort_rows(bs.bufs, t.n, off, ln, self.world, stats=stats,
                                        keys_ready=kr is not None, hi_bounds=None if kr is None else kr[:2],
                                        split_ties=not f.get("keep_ties", False),
-                                       keys_fmt="e128" if kr is None else kr[2], gen=gen)
+                                       keys_fmt="e128" if kr is None else kr[2], gen=gen, src=src)
         self.row_sets[(m.id, me)] = bs
         self.last_sort_stats = stats
         table = DeviceTable(out.shape[0], t.shape, rows=out)
@@ -443,7 +491,10 @@ class GpuJobRunner:
                         err = (crash, "crash", f"injected crash of {s.name}[{crash}] (output discarded)")
                 except Exception as e:  # noqa: BLE001
                     self._last_exc = e
-                    err = (mine[0] if mine else 0, "fail", f"{type(e).__name__}: {e}")
+                    # a deterministic failure every rank agreed on before the exchange (range
+                    # skew past capacity): re-executing would fail alike, so the job ends now
+                    kind = "fatal" if getattr(e, "retryable", True) is False else "fail"
+                    err = (mine[0] if mine else 0, kind, f"{type(e).__name__}: {e}")
                 outcome = self._vote(err)
             if outcome is None:
                 for p in range(s.partitions):
@@ -457,6 +508,10 @@ class GpuJobRunner:
             for p in sorted(failed):                # the first failure restarts the whole gang
                 g.on_failed(self.vids[s.id][p], vers[p], now(), -1, failed[p][1])
                 self.recovery.append(("upstream" if failed[p][0] == "read_error" else "gang_restart", s.name, p))
+            fatal = [msg for kind, msg in failed.values() if kind == "fatal"]
+            if fatal:
+                raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed, f"{s.name}: {fatal[0]}",
+                                            inner=getattr(self, "_last_exc", None))
             if g.failed():
                 raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed, g.failure(),
                                             inner=getattr(self, "_last_exc", None))
@@ -1040,6 +1095,8 @@ class GpuJobRunner:
                     write=dict(bytes=self.write_stats.bytes, seconds=round(self.write_stats.seconds, 4)),
                     read=dict(bytes=self.read_stats.bytes, seconds=round(self.read_stats.seconds, 4)),
                     sort_path=getattr(self, "last_sort_path", None),
+                    exchange=(self.last_sort_stats.exchange_report() if getattr(self, "last_sort_stats", None)
+                              is not None and self.last_sort_stats.rounds > 1 else None),
                     streamed={f"{k[0]}:{k[1]}": v for k, v in self.stream_stats.items()},
                     statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()],
                     external_sort=getattr(self, "extsort_stats", None), join=getattr(self, "join_stats", None),
@@ -1174,6 +1231,7 @@ class GpuJobRunner:
                         torch.cuda.synchronize(dev)
                     done.put((p, ver, dup, "ok", out, ""))
                 except VertexCancelled:
+                    self._drop_attempt(s, p, ver)
                     done.put((p, ver, dup, "cancelled", None, ""))
                 except Exception as e:  # noqa: BLE001
                     done.put((p, ver, dup, "fail", None, f"{type(e).__name__}: {e}"))
@@ -1234,6 +1292,8 @@ class GpuJobRunner:
                                 out = outs.pop((p, ver))
                                 if accepted:
                                     self.channels[(s.id, p)] = out if out is not None else []
+                                elif (s.id, p) not in self.channels:
+                                    self._drop_attempt(s, p, ver)     # a losing completion: free its HBM
                             if accepted:
                                 if r != self.owner(p, s.id):
                                     self.moved[(s.id, p)] = r
@@ -1280,6 +1340,26 @@ class GpuJobRunner:
             th.join()
 
     SPEC_POLL = 0.02
+
+    def _drop_attempt(self, s, p, ver):
+        """A speculative attempt (s, p, ver) that lost or was cancelled on this rank: its pooled
+        rows go back to the pool and its streamed part file (``<tmp part>.stream``) is removed."""
+        bs = self.row_sets.get((s.id, p))
+        if bs is not None and (s.id, p) not in self.channels and self.pool is not None:
+            self.row_sets.pop((s.id, p), None)
+            self.pool.release(bs)
+        if s.is_output and getattr(s, "output", None):
+            try:
+                scheme, path, _ = parse_uri(s.output["uri"])
+            except Exception:  # noqa: BLE001
+                return
+            if scheme in ("partfile", "file"):
+                from ..io import partfile as PF
+                f = PF.tmp_part_path(PF.default_base(path), p, self.vids[s.id][p], 0, ver) + ".stream"
+                try:
+                    os.remove(f)
+                except OSError:
+                    pass
 
     def _dump_restart(self, s, p, ver, streams, error):
         """Restart record of a failed GPU vertex attempt (DumpRestartCommand, dvertexpncontrol.cpp:

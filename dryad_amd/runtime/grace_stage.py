@@ -444,6 +444,11 @@ def run(desc, runner, lay) -> dict:
             sink.add(data)
         t2 = time.perf_counter()
         stats = grace.stats
+    except BaseException:
+        # the sink's part writer holds the process-wide writer ring: give it back (and drop the
+        # partial part file) before the retry or the fallback stages open a writer of their own
+        sink.abort()
+        raise
     finally:
         grace.release()
     out = sink.finish(V)
@@ -494,6 +499,20 @@ class _Sink:
         if self.writer is not None:
             raise RuntimeError("grace join stage: a bucket result could not be encoded like the others")
         self.chunks.append(data)
+
+    def abort(self):
+        """An attempt failed mid-stream: stop the writer (its threads, the ring lock) and remove
+        the partial part file."""
+        w, self.writer = self.writer, None
+        if w is not None:
+            try:
+                w.abort()
+            finally:
+                try:
+                    os.remove(self.tmp)
+                except OSError:
+                    pass
+        self.chunks, self.partials = [], []
 
     def finish(self, V):
         runner, parts = self.runner, self.parts

@@ -1,0 +1,127 @@
+"""Multi-rank OrderBy over MATERIALISED tables through the fine-bucket exchange, on GPU ranks that
+share one GPU (gloo transport; run by tests/test_gpu_multirank.py):
+
+  * gen://terasort read into a 128-byte-pitch table (the bench default) and the GenFusedShuffle
+    variant, through the query API, validated valsort-style;
+  * an hbm:// input table (read in place, sorted into a buffer set of its own) and a partfile://
+    table of raw rows, both validated;
+  * skew: all keys equal with the ties kept (OrderBy(k).GroupBy(k)), so one rank's key range
+    overflows its buffer: every rank stops at the voted capacity check within seconds, instead of
+    blocking in the exchange until the collective timeout;
+  * heavy duplication with ties split: the fine cut would overflow, the E128 path splits the run.
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+import torch  # noqa: E402
+
+import dryad_amd as D  # noqa: E402
+from dryad_amd.models.terasort import TeraSortConfig, TeraSortQueryJob, TeraSortStoredJob  # noqa: E402
+from dryad_amd.ops import recordsort as RS  # noqa: E402
+from dryad_amd.ops import terasort as TS  # noqa: E402
+from dryad_amd.parallel import shuffle  # noqa: E402
+from dryad_amd.parallel.comm import init_world, shutdown  # noqa: E402
+
+
+def _valsort(rows, w, expect_hash, expect_n):
+    acc = TS.check(rows)
+    cnt = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
+    shuffle.all_reduce_(acc, "sum", w)
+    shuffle.all_reduce_(cnt, "sum", w)
+    ends = torch.zeros((1, 21), dtype=torch.uint8, device=rows.device)
+    if rows.shape[0]:
+        ends[0, 0] = 1
+        ends[0, 1:11], ends[0, 11:] = rows[0, :10], rows[-1, :10]
+    prev = None
+    for r in shuffle.all_gather_tensor(ends, w).cpu().numpy():
+        if r[0]:
+            assert prev is None or prev <= bytes(r[1:11]), "rank boundary out of order"
+            prev = bytes(r[11:])
+    assert int(acc[0]) == expect_hash and int(acc[1]) == 0 and int(cnt) == expect_n, (acc.tolist(), int(cnt))
+
+
+def main():
+    w = init_world(device="cuda")
+    n = int(os.environ.get("TS_RECORDS", "1500000"))
+    cfg = TeraSortConfig(records_per_rank=n)
+    # 1. the bench's default: the generated table at a 128-byte pitch, fine-bucket exchange over it
+    for gen_fused in (False, True):
+        job = TeraSortQueryJob(cfg, w, gen_fused=gen_fused)
+        expect = job.input_checksum()
+        for _ in range(2):
+            job.step()
+            v = job.validate(*expect)
+            assert v["ok"], (w.rank, gen_fused, v)
+        ex = job.executor_report()["exchange"]
+        want = "records generated into the send rows" if gen_fused else "over the table (pitch 128)"
+        assert ex is not None and want in ex["path"], ex
+        assert ex["rounds"] == len(ex["round_send_MB"]) and ex["send_GB"] > 0, ex
+    # 2. an hbm:// table (a previous job's output) read in place, and a stored partfile of rows
+    g = D.DryadLinqContext(platform="gpu")
+    g.PartitionCount = w.size
+    src = f"gen://terasort?records={n * w.size}&partitions={w.size}&seed={cfg.seed}"
+    g.FromStore(src).ToStore("hbm://fine_in", delete_if_exists=True).SubmitAndWait()
+    from dryad_amd.io.providers import provider_for
+    g.FromStore("hbm://fine_in").OrderBy(lambda r: r[0:10]).ToStore("hbm://fine_out", delete_if_exists=True) \
+        .SubmitAndWait()
+    res = g._get_executor().last_result
+    assert not {op for _, op, _ in res["fallbacks"]} & {"sample", "separators", "range_partition", "sort"}, \
+        res["fallbacks"]
+    assert res["exchange"] is not None and "pitch 100" in res["exchange"]["path"], res["exchange"]
+    out = provider_for("hbm://fine_out").get("hbm://fine_out")["local"][w.rank].rows
+    _valsort(out, w, expect[0], n * w.size)
+    kept = provider_for("hbm://fine_in").get("hbm://fine_in")["local"][w.rank].rows   # the input is intact
+    assert int(TS.check(kept)[0]) != 0 and kept.shape[0] == n
+    base = os.environ.get("FINE_TMP", "/tmp/dryad_fine_rows")
+    st = TeraSortStoredJob(cfg, w, f"partfile://{base}/in", f"partfile://{base}/out")
+    st.prepare(force=True)
+    st.step()
+    v = st.validate(*expect)
+    assert v["ok"], (w.rank, v)
+    assert "pitch 128" in (st.ctx._get_executor().last_result["exchange"] or {}).get("path", ""), \
+        st.ctx._get_executor().last_result["exchange"]
+    # 3. skew past capacity with the ties kept: a voted, non-retryable stop within seconds
+    ts = f"gen://terasort?records={200_000 * w.size}&partitions={w.size}&seed=5"
+    bufs = RS.SortBuffers.allocate(200_000, 100, w.device, slack=0.01)
+    TS.generate(bufs.rows_in[:200_000], w.rank * 200_000, 5)
+    bufs.rows_in[:200_000, :10] = 42
+    t0 = time.perf_counter()
+    try:
+        RS.distributed_sort_rows(bufs, 200_000, 0, 10, w, split_ties=False)
+        raise AssertionError("an overflowing key range must stop the sort")
+    except D.errors.GangAgreementError as e:
+        assert not e.retryable and "range partition skew" in str(e), e
+    assert time.perf_counter() - t0 < 10, time.perf_counter() - t0
+    # ... and through the query API: OrderBy(k).GroupBy(k) keeps ties (the GroupBy elides its
+    # shuffle); bytes 10..13 of every gen://terasort record are equal (00 11 '0' '0'), so one rank
+    # would receive every row: the job fails cleanly on every rank at the vote
+    qctx = D.DryadLinqContext(platform="gpu")
+    qctx.PartitionCount = w.size
+    k = lambda r: r[10:14]  # noqa: E731
+    t0 = time.perf_counter()
+    try:
+        list(qctx.FromStore(ts).OrderBy(k).GroupBy(k, lambda kk, gr: (kk, gr.Count())))
+        raise AssertionError("the skewed job must fail")
+    except D.errors.DryadLinqJobException as e:
+        assert "range partition skew" in str(e) + str(getattr(e, "inner", "")), e
+    dt = time.perf_counter() - t0
+    assert dt < 10, dt
+    # 4. every key equal with ties split: the E128 path spreads the run over the ranks
+    TS.generate(bufs.rows_in[:200_000], w.rank * 200_000, 5)
+    bufs.rows_in[:200_000, :10] = 42
+    stt = RS.SortStats()
+    out = RS.distributed_sort_rows(bufs, 200_000, 0, 10, w, stats=stt)
+    assert "E128" in stt.path and abs(stt.n_out - 200_000) <= 2_000, (stt.path, stt.n_out)
+    assert torch.equal(out[:, :10], torch.full_like(out[:, :10], 42))
+    w.barrier()
+    if w.rank == 0:
+        print("FINE_ROWS_OK", w.size, flush=True)
+    torch.cuda.synchronize()
+    shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -98,3 +98,30 @@ def test_join_partfile_and_hbm_inputs(tmp_path):
     exp = sorted(_loc().FromStore(R.format(P=2)).Join(_loc().FromStore(S.format(P=2)).Select(
         lambda s: (s[0], s[1])), lambda r: r[0], lambda s: s[0], lambda r, s: (r[1], s[1])))
     _same(got, exp)
+
+
+def test_join_to_partfile_recovers_from_a_bucket_failure(tmp_path, monkeypatch):
+    """A bucket that fails after earlier buckets were streamed into the output part file: the
+    stage's writer is aborted (the process-wide writer ring released, the partial part removed),
+    so the compiled stages that take over (the failure hit every rank) open their own writer and
+    the job completes oracle-equal."""
+    from dryad_amd.ops import grace as GR
+    real = GR.hash_join_pairs
+    calls = {"n": 0}
+
+    def flaky(*a, **k):
+        calls["n"] += 1
+        if calls["n"] == 3:                  # the third bucket of the first attempt
+            raise RuntimeError("injected bucket failure")
+        return real(*a, **k)
+    monkeypatch.setattr(GR, "hash_join_pairs", flaky)
+    g = _ctx()
+    uri = "partfile://" + str(tmp_path / "jf.pt")
+    q = lambda c: c.FromStore(R.format(P=2)).Join(c.FromStore(S.format(P=2)), lambda r: r[0], lambda s: s[0],  # noqa
+                                                   lambda r, s: (r[0], r[1], s[2]))
+    q(g).ToStore(uri, delete_if_exists=True).SubmitAndWait()      # (hung in PartWriter before the fix)
+    assert calls["n"] >= 3
+    import os
+    parts_dir = str(tmp_path / "jf.pt.parts")
+    assert not [f for f in os.listdir(parts_dir) if f.endswith(".tmp")], os.listdir(parts_dir)
+    _same(sorted(g.FromStore(uri)), sorted(q(_loc())))

@@ -57,7 +57,7 @@ def main():
 
     def gather(e: torch.Tensor):
         _lib.call("dr_gather_fixup", ptr(rows), ptr(out), ptr(e), ctypes.c_uint64(e.shape[0]), ctypes.c_uint32(100),
-                  ctypes.c_uint32(0), ctypes.c_uint32(10), 32, ptr(flag), stream_of(rows))
+                  ctypes.c_uint32(0), ctypes.c_uint32(10), 32, ptr(flag), ptr(None), stream_of(rows))
 
     print(f"rows {n:.3g} ({n * 100 / 1e9:.0f} GB), one range = {m} rows ({m * 100 / 1e9:.2f} GB)", flush=True)
     b = 3

@@ -38,7 +38,7 @@ def main():
                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.dr_gather_fixup_pitch128.restype = ctypes.c_int
     lib.dr_gather_fixup_pitch128.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_u64, c_u32, c_u32,
-                                            c_u32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+                                            c_u32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 
     if "--xcd" in sys.argv:
         # gather timing with synthetic entries (window = position: no fix-up runs): sources random
@@ -66,7 +66,7 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 _lib.check(lib.dr_gather_fixup_pitch128(ptr(rows_p), ptr(out), ptr(keys), c_u64(n), c_u32(100),
-                                                        c_u32(0), c_u32(10), 32, ptr(flag), stream_of(buf)), "gather")
+                                                        c_u32(0), c_u32(10), 32, ptr(flag), ptr(None), stream_of(buf)), "gather")
                 e1.record()
                 torch.cuda.synchronize()
                 best = e0.elapsed_time(e1) if best is None else min(best, e0.elapsed_time(e1))
@@ -86,7 +86,7 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 _lib.check(lib.dr_gather_fixup_pitch128(ptr(rows_m), ptr(out), ptr(srt), c_u64(m), c_u32(100),
-                                                        c_u32(0), c_u32(10), 32, ptr(flag), stream_of(buf)), "gather")
+                                                        c_u32(0), c_u32(10), 32, ptr(flag), ptr(None), stream_of(buf)), "gather")
                 e1.record()
                 torch.cuda.synchronize()
                 t = e0.elapsed_time(e1)
@@ -113,7 +113,7 @@ def main():
             S.gather_fixup(rows, srt, out, 0, 10, 32, flag)
         else:
             _lib.check(lib.dr_gather_fixup_pitch128(ptr(buf), ptr(out), ptr(srt), c_u64(n), c_u32(100), c_u32(0),
-                                                    c_u32(10), 32, ptr(flag), stream_of(buf)), "gather pitch128")
+                                                    c_u32(10), 32, ptr(flag), ptr(None), stream_of(buf)), "gather pitch128")
         ev[3].record()
         torch.cuda.synchronize()
         return [ev[i].elapsed_time(ev[i + 1]) for i in range(3)], int(flag.item())
