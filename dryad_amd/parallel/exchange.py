@@ -5,10 +5,11 @@ The reference moves every cross-vertex channel as a file served over HTTP
 shuffle is N x M such files (``GraphBuilder.cs:481-504``).  Here a channel between GPUs is a slice
 of an HBM table, and one stage's worth of channels is ONE exchange:
 
-  * a manifest all-gather (piece row counts, string-heap bytes, the table schema: a few hundred
-    bytes per rank) so every rank sizes its receive buffers and agrees on column types
-    (partitions whose inferred widths differ, e.g. Int32 vs Int64 columns, are promoted);
-  * one all-to-all-v per column over xGMI (RCCL ``all_to_all_single``; the send side is a view of
+  * a manifest as two small tensor collectives (header all-gather: structure digest and column
+    dtypes; all-to-all of piece row counts and string-heap bytes) so every rank sizes its receive
+    buffers and agrees on column types (partitions whose inferred widths differ, e.g. Int32 vs
+    Int64 columns, are promoted);
+  * one asynchronous all-to-all-v per column over xGMI, all queued back to back (RCCL ``all_to_all_single``; the send side is a view of
     the producer's port-grouped columns whenever the pieces for consecutive ranks are adjacent,
     which is what the rank-major partition order of ``gpu/ops`` guarantees, so nothing is packed);
   * one more all-to-all-v per string field: the pieces' string bytes compacted in row order
@@ -121,44 +122,107 @@ class ExchangeStats:
         self.collectives = 0
 
 
-def exchange(world: World, sends: list, stats: ExchangeStats | None = None) -> list:
-    """``sends[r]``: DeviceTables (pieces) for rank r, in order.  Returns ``recv[s]``: the pieces
-    rank s sent to this rank, in its order.  Collective: every rank calls it with W send lists.
-    Raises SchemaMismatch (on every rank) when the ranks' tables are structurally different."""
-    W, me = world.size, world.rank
-    assert len(sends) == W
-    proto = next((p for lst in sends for p in lst if p is not None), None)
+# dtype codes of the tensor manifest (index in this list)
+_DTYPES = [torch.bool, torch.uint8, torch.int8, torch.int16, torch.int32, torch.int64, torch.float16,
+           torch.bfloat16, torch.float32, torch.float64]
+_MAXC = 64                     # columns a manifest header carries
+
+
+def _struct_hash(struct) -> int:
+    """A 63-bit digest of a table structure (identical structures on every rank hash alike)."""
+    import hashlib
+    return int.from_bytes(hashlib.blake2b(repr(struct).encode(), digest_size=8).digest(), "little") >> 1
+
+
+def _manifest(world: World, sends: list, proto):
+    """The exchange's control plane as two small tensor collectives instead of pickled objects:
+    an all-gather of each rank's header (has a piece, structure digest, column dtypes, string
+    fields, pieces per destination) and an all-to-all of per-destination piece sizes (rows and
+    string bytes per piece).  Returns (headers [W][...], pieces[s] = [(rows, [string bytes])] that
+    rank s sends here, in order)."""
+    W = world.size
+    dev = world.device if world.backend == "nccl" else torch.device("cpu")
     sig = signature(proto) if proto is not None else None
+    nstr = len(_string_specs(proto)) if proto is not None else 0
+    if sig is not None and len(sig[1]) > _MAXC:
+        raise SchemaMismatch(f"tables of more than {_MAXC} columns travel as objects")
     # string bytes per piece: every length column summed on the device, one host read for all
     sums = [p.cols[lc][:p.n].sum().to(torch.int64) for lst in sends for p in lst if p.n
             for _, lc, _ in _string_specs(p)]
     vals = iter(torch.stack(sums).tolist() if sums else [])
-    manifest = []
-    for lst in sends:
-        manifest.append([(p.n, [next(vals) if p.n else 0 for _ in _string_specs(p)]) for p in lst])
-    gathered = [None] * W
-    dist.all_gather_object(gathered, (sig, manifest))
-    sigs = [g[0] for g in gathered if g[0] is not None]
-    if not sigs:                      # nobody holds a piece
+    per_dest = [[(p.n, [next(vals) if p.n else 0 for _ in range(nstr)]) for p in lst] for lst in sends]
+    maxp = max((len(x) for x in per_dest), default=0)
+    hdr = torch.zeros(5 + _MAXC, dtype=torch.int64)
+    if sig is not None:
+        hdr[0], hdr[1], hdr[2], hdr[3] = 1, _struct_hash(sig[0]), len(sig[1]), nstr
+        for j, d in enumerate(sig[1]):
+            if _dtype(d) not in _DTYPES:
+                raise SchemaMismatch(f"column dtype {d} has no manifest code")
+            hdr[5 + j] = _DTYPES.index(_dtype(d))
+    hdr[4] = maxp
+    heads = shuffle.all_gather_tensor(hdr.view(1, -1).to(dev), world).cpu().tolist()
+    M = max(h[4] for h in heads)
+    S = max(h[3] for h in heads)
+    rec = 1 + M * (1 + S)
+    out = torch.zeros((W, rec), dtype=torch.int64)
+    for r, lst in enumerate(per_dest):
+        out[r, 0] = len(lst)
+        for i, (n, sb) in enumerate(lst):
+            out[r, 1 + i * (1 + S)] = n
+            for j, b in enumerate(sb):
+                out[r, 2 + i * (1 + S) + j] = b
+    got = out.clone()
+    if W > 1:
+        send_t, recv_t = out.to(dev).view(-1), torch.empty(W * rec, dtype=torch.int64, device=dev)
+        dist.all_to_all_single(recv_t, send_t)
+        got = recv_t.view(W, rec).cpu()
+    g = got.tolist()
+    pieces = [[(g[s][1 + i * (1 + S)], g[s][2 + i * (1 + S): 2 + i * (1 + S) + S]) for i in range(g[s][0])]
+              for s in range(W)]
+    return heads, pieces
+
+
+def exchange(world: World, sends: list, stats: ExchangeStats | None = None) -> list:
+    """``sends[r]``: DeviceTables (pieces) for rank r, in order.  Returns ``recv[s]``: the pieces
+    rank s sent to this rank, in its order.  Collective: every rank calls it with W send lists.
+    Raises SchemaMismatch (on every rank) when the ranks' tables are structurally different.
+
+    The manifest is two tensor collectives (``_manifest``); the payload columns are queued as
+    asynchronous all-to-all-v collectives back to back (RCCL runs them in order on its stream
+    while the host prepares the next) and waited for together; a partition's received pieces are
+    adjacent slices of one buffer per column (DeviceTable.concat takes them as one view)."""
+    W, me = world.size, world.rank
+    assert len(sends) == W
+    proto = next((p for lst in sends for p in lst if p is not None), None)
+    heads, recv_pieces = _manifest(world, sends, proto)
+    have = [h for h in heads if h[0]]
+    if not have:                      # nobody holds a piece
         return [[] for _ in range(W)]
-    structs = {s[0] for s in sigs}
-    if len(structs) != 1:
-        raise SchemaMismatch(f"ranks hold different table structures: {structs}")
-    struct = sigs[0][0]
+    if len({h[1] for h in have}) != 1 or len({h[2] for h in have}) != 1:
+        raise SchemaMismatch("ranks hold different table structures")
+    if len(have) < W:
+        # a rank without source pieces learns the structure from the others (rare: fewer source
+        # partitions than ranks); every rank sees the same headers, so all take this branch
+        objs = [None] * W
+        dist.all_gather_object(objs, signature(proto)[0] if proto is not None else None)
+        struct = next(o for o in objs if o is not None)
+    else:
+        struct = signature(proto)[0]
     kind, fields, pytype, key_off, key_len, colspecs, strspecs = struct
     dtypes = []
     for j in range(len(colspecs)):
-        dt = _dtype(sigs[0][1][j])
-        for s in sigs[1:]:
-            dt = torch.promote_types(dt, _dtype(s[1][j]))
+        dt = _DTYPES[have[0][5 + j]]
+        for h in have[1:]:
+            dt = torch.promote_types(dt, _DTYPES[h[5 + j]])
         dtypes.append(dt)
     shape = Shape(kind, list(fields), pytype, key_off, key_len)
     dev = world.device if world.device.type == "cuda" else (proto.device if proto is not None else torch.device("cpu"))
-    recv_rows = [sum(n for n, _ in gathered[s][1][me]) for s in range(W)]
+    recv_rows = [sum(n for n, _ in recv_pieces[s]) for s in range(W)]
     send_rows = [sum(p.n for p in sends[r]) for r in range(W)]
     total_r = sum(recv_rows)
     out_cols = {name: None for name, _ in colspecs}
     offset_cols = {oc for oc, _, _ in strspecs}        # rebuilt from the lengths on arrival
+    handles = []
     for (name, tail), dt in zip(colspecs, dtypes):
         if name in offset_cols:
             out_cols[name] = dt
@@ -171,12 +235,15 @@ def exchange(world: World, sends: list, stats: ExchangeStats | None = None) -> l
         like = torch.empty((0,) + tuple(tail), dtype=dt, device=dev)
         send = _bytes(_cat(pieces, like)) if pieces else torch.empty(0, dtype=torch.uint8, device=dev)
         recv = torch.empty(total_r * per, dtype=torch.uint8, device=dev)
-        shuffle.alltoallv_bytes(send, [c * per for c in send_rows], recv, [c * per for c in recv_rows], world)
+        handles.append(shuffle.alltoallv_bytes_async(send, [c * per for c in send_rows], recv,
+                                                     [c * per for c in recv_rows], world))
         out_cols[name] = recv.view(dt).view((total_r,) + tuple(tail))
         if stats is not None:
             stats.bytes_sent += sum(send_rows) * per
             stats.bytes_received += total_r * per
             stats.collectives += 1
+    for h in handles:
+        shuffle.wait(h)
     heaps = {}
     for j, (oc, lc, hk) in enumerate(strspecs):
         parts, send_b = [], []
@@ -190,7 +257,7 @@ def exchange(world: World, sends: list, stats: ExchangeStats | None = None) -> l
                 parts.append(h)
                 nb += h.numel()
             send_b.append(nb)
-        recv_b = [sum(m[1][j] for m in gathered[s][1][me]) for s in range(W)]
+        recv_b = [sum(sb[j] for _, sb in recv_pieces[s]) for s in range(W)]
         send = torch.cat(parts) if len(parts) > 1 else (parts[0] if parts else torch.empty(0, dtype=torch.uint8,
                                                                                                 device=dev))
         recv = torch.empty(sum(recv_b), dtype=torch.uint8, device=dev)
@@ -210,7 +277,7 @@ def exchange(world: World, sends: list, stats: ExchangeStats | None = None) -> l
     res, a = [], 0
     for s in range(W):
         lst = []
-        for n, _ in gathered[s][1][me]:
+        for n, _ in recv_pieces[s]:
             lst.append(big.slice(a, a + n))
             a += n
         res.append(lst)

@@ -521,13 +521,26 @@ class GpuJobRunner:
     def _vote(self, err):
         """All-gather of each rank's attempt outcome: None (ok) or (partition, kind, message).
         Returns None when every rank succeeded, else [(rank, outcome)] of the failures."""
-        W = self.world.size
-        got = [err]
-        if W > 1:
-            got = [None] * W
-            dist.all_gather_object(got, err)
+        got = self._gather_if_any(err) if self.world.size > 1 else ([err] if err is not None else None)
+        if got is None:
+            return None
         bad = [(r, e) for r, e in enumerate(got) if e is not None]
         return bad or None
+
+    def _gather_if_any(self, obj):
+        """None when every rank passes None (one tensor all-gather of a flag, no pickling: the
+        per-stage votes of an iterative job stay off the host's object path), else every rank's
+        object (all_gather_object, only when some rank has something to say)."""
+        from ..parallel import shuffle
+        st = shuffle.gang_status(obj is None, 0, self.world)
+        if all(ok for ok, _ in st):
+            return None
+        return self._gather_objects(obj)
+
+    def _gather_objects(self, obj):
+        got = [None] * self.world.size
+        dist.all_gather_object(got, obj)
+        return got
 
     def _restore_fused_input(self, f, reread: bool = False):
         """Before a retry of a fused distributed OrderBy: its input table again.  A gen://terasort
@@ -770,9 +783,8 @@ class GpuJobRunner:
         why = None
         for tr in CHN.transports():
             ok = tr.usable(sends)
-            votes = [None] * W
-            dist.all_gather_object(votes, ok)
-            if not all(votes):
+            from ..parallel import shuffle as SH
+            if not all(v for v, _ in SH.gang_status(bool(ok), 0, self.world)):
                 why = why or ("host records on the channel" if tr.name == "device" else f"{tr.name} not usable")
                 continue
             try:
@@ -1143,8 +1155,18 @@ class GpuJobRunner:
                     self._dump_restart(s, p, ver, raw[p], f"{type(e).__name__}: {e}")
             reports = [report]
             if W > 1:
-                reports = [None] * W
-                dist.all_gather_object(reports, report)
+                # common case (every attempt succeeded): one small tensor all-gather; every rank
+                # rebuilds the others' reports from the replicated ready set.  Only a failure
+                # somewhere pays for the pickled reports with their messages.
+                bad = self._gather_if_any(report if any(x[2] != "ok" for x in report) else None)
+                if bad is None:
+                    reports = [[(self.vids[s.id][p], ready[self.vids[s.id][p]], "ok", -1, "", True)
+                                for p in range(s.partitions) if self.owner(p, s.id) == r
+                                and g.completed_version(self.vids[s.id][p]) < 0 and self.vids[s.id][p] in ready]
+                               for r in range(W)]
+                    assert reports[me] == report, (reports[me], report)
+                else:
+                    reports = self._gather_objects(report)
             fatal, blamed = None, []
             for r in range(W):
                 for vid, ver, kind, edge, err, retriable in reports[r]:

@@ -43,6 +43,39 @@ def main():
             assert torch.equal(recv[off: off + rc[s]], payload(s, me, rc[s])), (me, s, case)
             off += rc[s]
         assert torch.equal(recv[off:], torch.full((5,), 0xEE, dtype=torch.uint8)), "wrote past the receive counts"
+    # the branch an RCCL run takes below the chunk size: tensors where the backend moves them (host
+    # memory under gloo, HBM under RCCL) -> one asynchronous all_to_all_single with split sizes,
+    # a real work handle that the caller waits for later (recordsort's pipelined rounds)
+    shuffle.CHUNK_BYTES = 1 << 30
+    for case in range(2):
+        sc = [count(me, d, case) for d in range(W)]
+        rc = [count(s, me, case) for s in range(W)]
+        send = torch.cat([payload(me, d, sc[d]) for d in range(W)])
+        recv = torch.full((sum(rc),), 0xEE, dtype=torch.uint8)
+        h = shuffle.alltoallv_bytes_async(send, sc, recv, rc, w)
+        assert (h is not None) == (W > 1), h
+        shuffle.wait(h)
+        off = 0
+        for s in range(W):
+            assert torch.equal(recv[off: off + rc[s]], payload(s, me, rc[s])), (me, s, "async", case)
+            off += rc[s]
+    # the gang agreement before a payload collective: a rank past its capacity stops every rank
+    from dryad_amd.errors import GangAgreementError
+    from dryad_amd.ops import recordsort as RS
+    st = shuffle.gang_status(me != W - 1, me * 10, w)
+    assert st == [(r != W - 1, r * 10) for r in range(W)], st
+    try:
+        RS._check_capacity(100 if me == W - 1 else 10, 50, w)
+        raise AssertionError("the over-capacity rank must stop every rank")
+    except GangAgreementError as e:
+        assert not e.retryable and e.ranks == (W - 1,) and f"rank {W - 1} receives 50 rows past" in str(e), e
+    try:
+        RS._agree(RuntimeError("boom") if me == 0 else None, w, "test stage")
+        raise AssertionError("a failed rank must stop every rank")
+    except GangAgreementError as e:
+        assert e.retryable and e.ranks == (0,), e
+        assert ("boom" in str(e)) == (me == 0), e
+    assert RS._agree(None, w, "ok", value=me + 1) == list(range(1, W + 1))
     w.barrier()
     if me == 0:
         print(f"CHUNKED_OK {W}", flush=True)
