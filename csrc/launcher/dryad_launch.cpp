@@ -2,19 +2,32 @@
 // submission / H-3 ProcessService: LocalJobSubmission.cs starts the graph manager and a vertex
 // host per computer; here every rank is a peer SPMD process over RCCL).
 //
-//   dryad-launch --gpus N [--master-port P] [--log-dir DIR] [--grace-seconds S] -- prog args...
+//   dryad-launch --gpus N [--master-port P] [--log-dir DIR] [--grace-seconds S]
+//                [--max-restarts K] [--checkpoint-dir DIR] -- prog args...
 //
 // Each child gets RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
 // MASTER_PORT (the torch.distributed env:// contract) and runs in its own process group.  The
 // launcher waits for all ranks; the first rank that fails (non-zero exit or signal) makes it
 // SIGTERM the others (SIGKILL after the grace period) so a dead rank never leaves the rest hung
-// in a collective — the gang-failure rule of DrGang/DrCohort.  Exit status = first failure's.
+// in a collective — the gang-failure rule of DrGang/DrCohort.
+//
+// Gang relaunch (--max-restarts K > 0): when the first failure is a LOST process (a rank killed by
+// a signal, or one that exits with EX_TEMPFAIL = 75 to ask for it), the whole gang is stopped and
+// a fresh gang of NEW child processes is started, up to K times: epoch e gets DRYAD_GANG_EPOCH=e,
+// DRYAD_GANG_RESTARTS=K, DRYAD_CHECKPOINT_DIR (the persisted stage outputs it resumes from,
+// runtime/checkpoint.py) and MASTER_PORT = P + e (a fresh rendezvous).  Nothing is ever re-exec'd
+// in place: a process that initialised the GPU only exits.  A rank that fails with an ordinary
+// error code (a deterministic job failure) ends the job as before.  The reference re-executes a
+// failed vertex process from its persisted inputs the same way (DrVertex.cpp:1042-1171,
+// DrGraph.cpp:392-456).  Every relaunch is one JSON line in <log-dir>/launcher.jsonl.
+// Exit status = the last gang's first failure (0 when a gang completed).
 #include <csignal>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
 #include <fcntl.h>
+#include <ftw.h>
 #include <string>
 #include <sys/stat.h>
 #include <sys/types.h>
@@ -26,6 +39,7 @@ namespace {
 
 std::vector<pid_t> g_children;
 volatile sig_atomic_t g_stop = 0;
+constexpr int kTempFail = 75;          // EX_TEMPFAIL: "relaunch me"
 
 void on_signal(int sig) {
   g_stop = sig;
@@ -38,42 +52,37 @@ void kill_all(int sig) {
 
 int usage() {
   std::fprintf(stderr,
-               "usage: dryad-launch --gpus N [--master-port P] [--log-dir DIR] [--grace-seconds S] -- prog args...\n");
+               "usage: dryad-launch --gpus N [--master-port P] [--log-dir DIR] [--grace-seconds S] "
+               "[--max-restarts K] [--checkpoint-dir DIR] -- prog args...\n");
   return 2;
 }
 
-}  // namespace
+struct GangResult {
+  int code = 0;          // first failure's status (128 + signal for a signal death)
+  int rank = -1;
+  bool lost = false;     // the first failure was a lost process (signal, or EX_TEMPFAIL)
+};
 
-int main(int argc, char** argv) {
-  int n = 1, port = 29511, grace = 10;
-  std::string log_dir;
-  int i = 1;
-  for (; i < argc; ++i) {
-    std::string a = argv[i];
-    if (a == "--") { ++i; break; }
-    if (a == "--gpus" && i + 1 < argc) n = std::atoi(argv[++i]);
-    else if (a == "--master-port" && i + 1 < argc) port = std::atoi(argv[++i]);
-    else if (a == "--log-dir" && i + 1 < argc) log_dir = argv[++i];
-    else if (a == "--grace-seconds" && i + 1 < argc) grace = std::atoi(argv[++i]);
-    else return usage();
-  }
-  if (i >= argc || n < 1 || n > 64) return usage();
-  if (!log_dir.empty()) mkdir(log_dir.c_str(), 0755);
-  struct sigaction sa {};
-  sa.sa_handler = on_signal;
-  sigaction(SIGINT, &sa, nullptr);
-  sigaction(SIGTERM, &sa, nullptr);
+struct Options {
+  int n = 1, port = 29511, grace = 10, max_restarts = 0;
+  std::string log_dir, ckpt_dir;
+  char** prog = nullptr;
+};
 
-  for (int r = 0; r < n; ++r) {
+GangResult run_gang(const Options& o, int epoch, const std::string& reason) {
+  g_children.assign(o.n, -1);
+  for (int r = 0; r < o.n; ++r) {
     pid_t pid = fork();
     if (pid < 0) {
       std::perror("fork");
       kill_all(SIGTERM);
-      return 1;
+      GangResult g;
+      g.code = 1;
+      return g;
     }
     if (pid == 0) {
       setpgid(0, 0);
-      const std::string rs = std::to_string(r), ns = std::to_string(n), ps = std::to_string(port);
+      const std::string rs = std::to_string(r), ns = std::to_string(o.n), ps = std::to_string(o.port + epoch);
       setenv("RANK", rs.c_str(), 1);
       setenv("LOCAL_RANK", rs.c_str(), 1);
       setenv("WORLD_SIZE", ns.c_str(), 1);
@@ -81,9 +90,13 @@ int main(int argc, char** argv) {
       setenv("GROUP_RANK", "0", 1);
       setenv("MASTER_ADDR", "127.0.0.1", 1);
       setenv("MASTER_PORT", ps.c_str(), 1);
+      setenv("DRYAD_GANG_EPOCH", std::to_string(epoch).c_str(), 1);
+      setenv("DRYAD_GANG_RESTARTS", std::to_string(o.max_restarts).c_str(), 1);
+      if (!reason.empty()) setenv("DRYAD_GANG_RELAUNCH_REASON", reason.c_str(), 1);
+      if (!o.ckpt_dir.empty()) setenv("DRYAD_CHECKPOINT_DIR", o.ckpt_dir.c_str(), 1);
       if (!getenv("HSA_ENABLE_IPC_MODE_LEGACY")) setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0", 1);
-      if (!log_dir.empty()) {
-        const std::string path = log_dir + "/rank" + rs + ".log";
+      if (!o.log_dir.empty()) {
+        const std::string path = o.log_dir + "/rank" + rs + (epoch ? ".e" + std::to_string(epoch) : "") + ".log";
         int fd = open(path.c_str(), O_CREAT | O_WRONLY | O_TRUNC, 0644);
         if (fd >= 0) {
           dup2(fd, 1);
@@ -91,15 +104,16 @@ int main(int argc, char** argv) {
           close(fd);
         }
       }
-      execvp(argv[i], argv + i);
+      execvp(o.prog[0], o.prog);
       std::perror("execvp");
       _exit(127);
     }
     setpgid(pid, pid);
-    g_children.push_back(pid);
+    g_children[r] = pid;
   }
 
-  int first_fail = 0, first_rank = -1, alive = n;
+  GangResult res;
+  int alive = o.n;
   time_t kill_deadline = 0;
   while (alive > 0) {
     int status = 0;
@@ -108,32 +122,109 @@ int main(int argc, char** argv) {
       if (g_stop) {
         kill_all(SIGTERM);
         g_stop = 0;
-        if (!kill_deadline) kill_deadline = time(nullptr) + grace;
+        if (!kill_deadline) kill_deadline = time(nullptr) + o.grace;
+        if (res.rank < 0) {       // the launcher itself was stopped: no relaunch
+          res.code = 128 + SIGTERM;
+          res.rank = o.n;
+        }
         continue;
       }
       if (kill_deadline && time(nullptr) > kill_deadline) kill_all(SIGKILL);
       continue;
     }
     int rank = -1;
-    for (int r = 0; r < n; ++r)
+    for (int r = 0; r < o.n; ++r)
       if (g_children[r] == pid) rank = r;
-    if (rank < 0) continue;
+    if (rank < 0) {
+      if (kill_deadline && time(nullptr) > kill_deadline) kill_all(SIGKILL);
+      continue;               // the grace-period timer (below)
+    }
     g_children[rank] = -1;
     --alive;
+    const bool signaled = WIFSIGNALED(status);
     const int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + WTERMSIG(status);
-    std::fprintf(stderr, "[dryad-launch] rank %d exited with %d\n", rank, code);
-    if (code != 0 && first_rank < 0) {
-      first_fail = code;
-      first_rank = rank;
+    std::fprintf(stderr, "[dryad-launch] epoch %d: rank %d exited with %d%s\n", epoch, rank, code,
+                 signaled ? " (signal)" : "");
+    if (code != 0 && res.rank < 0) {
+      res.code = code;
+      res.rank = rank;
+      res.lost = signaled || code == kTempFail;
       kill_all(SIGTERM);                       // gang failure: stop the peers
-      kill_deadline = time(nullptr) + grace;
+      kill_deadline = time(nullptr) + o.grace;
       if (fork() == 0) {                       // escalate to SIGKILL after the grace period
-        sleep((unsigned)grace);
+        sleep((unsigned)o.grace);
         _exit(0);
       }
     }
     if (kill_deadline && time(nullptr) > kill_deadline) kill_all(SIGKILL);
   }
-  if (first_rank >= 0) std::fprintf(stderr, "[dryad-launch] job failed: rank %d status %d\n", first_rank, first_fail);
-  return first_fail;
+  return res;
+}
+
+int rm_entry(const char* path, const struct stat*, int, struct FTW*) {
+  return remove(path) == 0 ? 0 : 0;
+}
+
+// Empty the checkpoint directory (its contents, not the directory): before the first gang, so a
+// new launch never resumes a previous launch's stage outputs, and after the job completed.
+void wipe_checkpoints(const Options& o) {
+  if (o.ckpt_dir.empty()) return;
+  struct stat st {};
+  if (stat(o.ckpt_dir.c_str(), &st) != 0) return;
+  nftw(o.ckpt_dir.c_str(), rm_entry, 16, FTW_DEPTH | FTW_PHYS);
+  mkdir(o.ckpt_dir.c_str(), 0755);
+}
+
+void log_event(const Options& o, const std::string& json) {
+  std::fprintf(stderr, "[dryad-launch] %s\n", json.c_str());
+  if (o.log_dir.empty()) return;
+  const std::string path = o.log_dir + "/launcher.jsonl";
+  if (FILE* f = std::fopen(path.c_str(), "a")) {
+    std::fprintf(f, "%s\n", json.c_str());
+    std::fclose(f);
+  }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Options o;
+  int i = 1;
+  for (; i < argc; ++i) {
+    std::string a = argv[i];
+    if (a == "--") { ++i; break; }
+    if (a == "--gpus" && i + 1 < argc) o.n = std::atoi(argv[++i]);
+    else if (a == "--master-port" && i + 1 < argc) o.port = std::atoi(argv[++i]);
+    else if (a == "--log-dir" && i + 1 < argc) o.log_dir = argv[++i];
+    else if (a == "--grace-seconds" && i + 1 < argc) o.grace = std::atoi(argv[++i]);
+    else if (a == "--max-restarts" && i + 1 < argc) o.max_restarts = std::atoi(argv[++i]);
+    else if (a == "--checkpoint-dir" && i + 1 < argc) o.ckpt_dir = argv[++i];
+    else return usage();
+  }
+  if (i >= argc || o.n < 1 || o.n > 64 || o.max_restarts < 0) return usage();
+  o.prog = argv + i;
+  if (!o.log_dir.empty()) mkdir(o.log_dir.c_str(), 0755);
+  wipe_checkpoints(o);
+  if (!o.ckpt_dir.empty()) mkdir(o.ckpt_dir.c_str(), 0755);
+  struct sigaction sa {};
+  sa.sa_handler = on_signal;
+  sigaction(SIGINT, &sa, nullptr);
+  sigaction(SIGTERM, &sa, nullptr);
+
+  std::string reason;
+  for (int epoch = 0;; ++epoch) {
+    const GangResult r = run_gang(o, epoch, reason);
+    if (r.rank < 0) {
+      if (epoch > 0) log_event(o, "{\"ev\":\"job_complete\",\"epoch\":" + std::to_string(epoch) + "}");
+      wipe_checkpoints(o);
+      return 0;
+    }
+    if (!r.lost || epoch >= o.max_restarts || r.rank >= o.n) {
+      std::fprintf(stderr, "[dryad-launch] job failed: rank %d status %d\n", r.rank, r.code);
+      return r.code;
+    }
+    reason = "rank " + std::to_string(r.rank) + " lost (status " + std::to_string(r.code) + ")";
+    log_event(o, "{\"ev\":\"gang_relaunch\",\"epoch\":" + std::to_string(epoch + 1) + ",\"rank\":" +
+                     std::to_string(r.rank) + ",\"status\":" + std::to_string(r.code) + ",\"reason\":\"" + reason + "\"}");
+  }
 }

@@ -200,6 +200,7 @@ PYBIND11_MODULE(_dryad_native, m) {
       .def("preferred_workers", [](const JobGraph& g, int v) { return g.vertex(v).preferred_workers; })
       .def("outlier_threshold", &JobGraph::outlier_threshold)
       .def("drain_events", &JobGraph::drain_events)
+      .def("event", &JobGraph::event, "append a JSON event line (executor-side events: gang relaunch, resume)")
       .def("topology_json", &JobGraph::topology_json)
       .def("statistics_json", &JobGraph::statistics_json);
 

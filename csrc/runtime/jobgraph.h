@@ -138,13 +138,14 @@ class JobGraph {
   std::vector<std::string> drain_events();
   std::string topology_json() const;
   std::string statistics_json() const;
+  // Append one JSON event line (the executor's own events: gang relaunch, resumed stages).
+  void event(const std::string& json);
 
  private:
   void enqueue(int v, double now, bool duplicate);
   void mark_completed_downstream(int v, double now);
   void invalidate(int v, double now);
   void reestimate(Stage& s);
-  void event(const std::string& json);
 
   Params p_;
   std::vector<Stage> stages_;

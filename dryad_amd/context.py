@@ -127,6 +127,9 @@ _DEFAULTS = dict(
     GenFusedShuffle=False,        # multi-rank OrderBy over gen://terasort: generate the records straight
     #                               into the exchange's send rows (no input table; a benchmark variant)
     ShuffleSlack=0.01,            # receive-buffer headroom of a range-partitioned exchange
+    PersistStageOutputs=None,     # GPU executor: copy completed stage outputs to a checkpoint store so a
+    #                               relaunched gang resumes there (None: under a relaunching launcher;
+    #                               a directory or True: always; False: never; runtime/checkpoint.py)
     PartFileSplitBytes=0,         # GPU executor: a fixed-width partfile:// output partition of at least
     #                               this many bytes is written as several part files at once (0: one
     #                               part file per partition, as the reference; io/writer.split_count)

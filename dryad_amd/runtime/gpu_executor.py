@@ -36,6 +36,7 @@ from ..gpu.trace import NotTraceable
 from ..io.hosttable import HostRows
 from ..ops import extsort as EX
 from ..io.providers import parse_uri, provider_for
+from . import checkpoint as CK
 from ..native import runtime as native_runtime
 from ..parallel import shuffle
 from ..parallel.comm import World, get_world, init_world
@@ -222,6 +223,8 @@ class GpuJobRunner:
                 self.g.set_gang(self.vids[s.id])
                 self.gang_stages.add(s.id)
         self.recovery: list = []         # recovery actions taken (tests / statistics)
+        self.ckpt = None                 # runtime/checkpoint.StageCheckpoint of a resumable job
+        self.persist_seconds = 0.0
         self.precomputed_bodies: dict = {}   # fused join stage id -> (attempt body, program after it)
 
     @staticmethod
@@ -879,6 +882,12 @@ class GpuJobRunner:
 
     def run_vertex(self, s, p, version, raw_inputs, inject=True, cancel=None):
         fault = self._fault(s, p, version) if inject else None
+        if fault == "kill" and CK.gang_epoch() == 0:
+            # a LOST rank process (not a simulated one): the launcher relaunches the gang, which
+            # resumes from the persisted stage outputs (first start only, or it would die again)
+            log.warning("injected kill of rank %d in %s[%d]", self.world.rank, s.name, p)
+            import signal
+            os.kill(os.getpid(), signal.SIGKILL)
         if fault == "fail":
             raise RuntimeError(f"injected vertex failure {s.name}[{p}] v{version}")
         if fault and fault.startswith("slow"):
@@ -972,6 +981,41 @@ class GpuJobRunner:
             t = None
         return t if t is not None else out
 
+    # ------------------------------------------------------------------ gang relaunch / resume
+    def _persist_stage(self, s):
+        """Copy this rank's outputs of a completed stage to the checkpoint store (persist policy
+        of a job run under a relaunching launcher, runtime/checkpoint.py)."""
+        me = self.world.rank
+        t0 = time.time()
+        saved = 0
+        for p in range(s.partitions):
+            if self.owner(p, s.id) == me and (s.id, p) in self.channels:
+                saved += int(self.ckpt.save(s.id, p, self.channels[(s.id, p)]))
+        self.persist_seconds += time.time() - t0
+
+    def _resume_stage(self, s, ready, refresh, now) -> bool:
+        """A relaunched gang: when EVERY rank holds the persisted outputs of all its partitions of
+        stage s (one vote), load them instead of running the stage again."""
+        me = self.world.rank
+        mine = [p for p in range(s.partitions) if self.owner(p, s.id) == me]
+        have = all(self.ckpt.has(s.id, p) for p in mine)
+        from ..parallel import shuffle as SH
+        if not all(ok for ok, _ in SH.gang_status(have, 0, self.world)):
+            return False
+        dev = self.dev if self.gpu_ok else torch.device("cpu")
+        for p in mine:
+            self.channels[(s.id, p)] = self.ckpt.load(s.id, p, dev)
+        refresh()
+        for p in range(s.partitions):
+            vid = self.vids[s.id][p]
+            ver = ready.pop(vid)
+            self.g.on_running(vid, ver, self.owner(p, s.id), now())
+            self.g.on_completed(vid, ver, now(), 0, 0)
+        self.recovery.append(("resumed", s.name))
+        self.g.event(json.dumps({"ev": "stage_resumed", "t": now(), "stage": s.name, "partitions": s.partitions,
+                                 "epoch": CK.gang_epoch()}))
+        return True
+
     # ------------------------------------------------------------------ main loop
     def run(self):
         g = self.g
@@ -979,6 +1023,16 @@ class GpuJobRunner:
         t_start = time.time()
         now = lambda: time.time() - t_start  # noqa: E731
         g.start(now())
+        if self.ckpt is not None and CK.gang_epoch() == 0:
+            # a first start never resumes: drop what an earlier run left under this job's key
+            for st in self.plan.stages:
+                for p in range(st.partitions):
+                    if self.owner(p, st.id) == me:
+                        self.ckpt.drop(st.id, p)
+        if CK.gang_epoch() > 0:
+            g.event(json.dumps({"ev": "gang_relaunch", "t": now(), "epoch": CK.gang_epoch(),
+                                "reason": os.environ.get("DRYAD_GANG_RELAUNCH_REASON", ""),
+                                "checkpoint": self.ckpt.dir if self.ckpt is not None else None}))
         ready = {}
 
         def refresh():
@@ -1078,10 +1132,16 @@ class GpuJobRunner:
                     torch.cuda.synchronize(self.dev)
                 self.timings[f"{s.id}:{s.name}(fused OrderBy)"] = time.time() - t0
                 continue
+            if self.ckpt is not None and self._resume_stage(s, ready, refresh, now):
+                self._release(s)
+                self.timings[f"{s.id}:{s.name}(resumed)"] = time.time() - t0
+                continue
             if self.world.size > 1 and self._speculate(s):
                 self._run_stage_speculative(s, ready, refresh, now)
             else:
                 self._run_stage(s, ready, refresh, now)
+            if self.ckpt is not None:
+                self._persist_stage(s)
             self._release(s)
             # no synchronize between stages: the next stage's launches queue behind this one's
             # (a k-means iteration's four stages left the GPU idle while the host set up the
@@ -1112,7 +1172,7 @@ class GpuJobRunner:
                     streamed={f"{k[0]}:{k[1]}": v for k, v in self.stream_stats.items()},
                     statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()],
                     external_sort=getattr(self, "extsort_stats", None), join=getattr(self, "join_stats", None),
-                    recovery=self.recovery)
+                    recovery=self.recovery, persist_seconds=round(self.persist_seconds, 4))
 
     # ------------------------------------------------------------------ fault-tolerant stage execution
     def _run_stage(self, s, ready, refresh, now):
@@ -1824,6 +1884,10 @@ class GpuExecutor(_BaseExecutor):
                         raise DryadLinqException(ErrorCode.JobToCreateTableFailed,
                                                  f"output {st.output['uri']} already exists")
         runner = GpuJobRunner(self.ctx, plan, self.world, faults, self.pool)
+        root = CK.from_env(self.ctx)
+        if root is not None:
+            GpuExecutor._ckpt_seq += 1
+            runner.ckpt = CK.StageCheckpoint(root, CK.job_key(GpuExecutor._ckpt_seq, plan))
         job_dir = self._job_dir(plan) if self.world.rank == 0 else None
         runner.job_dir = job_dir
         self.last_job_dir = job_dir
@@ -1859,6 +1923,7 @@ class GpuExecutor(_BaseExecutor):
         return res
 
     _seq = 0
+    _ckpt_seq = 0              # jobs run by this process (the checkpoint key: same order after a relaunch)
     _last_job_dir = None
 
     @property

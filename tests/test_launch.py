@@ -46,3 +46,41 @@ def test_spmd_query_job_through_launcher(tmp_path):
                          capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "SPMD_OK 2" in out.stdout
+
+
+@pytest.mark.timeout(300)
+def test_gang_relaunch_resumes_after_a_lost_rank(tmp_path):
+    """Rank 1 is SIGKILLed mid-stage (a real lost process): dryad-launch stops the gang, starts a
+    fresh one (new processes, new rendezvous port), and the job resumes from the persisted stage
+    outputs: oracle-equal result, a gang_relaunch event in the job's events.jsonl, stage 0 not run
+    again (a stage_resumed event) and the relaunch in the launcher's own log."""
+    import json
+    env = dict(os.environ, SPMD_DEVICE="cpu", PYTHONPATH=ROOT, DRYAD_HOME=str(tmp_path / "home"))
+    logs = tmp_path / "logs"
+    out = subprocess.run([_launcher(), "--gpus", "2", "--master-port", "29641", "--grace-seconds", "3",
+                          "--max-restarts", "2", "--checkpoint-dir", str(tmp_path / "ckpt"), "--log-dir", str(logs),
+                          "--", sys.executable, os.path.join(ROOT, "tests", "dist", "gang_relaunch_job.py")],
+                         capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:] + open(logs / "rank0.log").read()[-2000:]
+    rank0 = open(logs / "rank0.e1.log").read()
+    line = next(ln for ln in rank0.splitlines() if ln.startswith("{"))
+    rep = json.loads(line)
+    assert rep["ok"] and rep["n"] > 0 and rep["epoch"] == 1, rep
+    assert ["resumed", rep["stages"][0]] in rep["recovery"], rep["recovery"]
+    evs = [json.loads(x) for x in open(os.path.join(rep["job_dir"], "log", "events.jsonl"))]
+    kinds = [e.get("ev") for e in evs]
+    assert "gang_relaunch" in kinds and "stage_resumed" in kinds, kinds
+    relaunch = next(e for e in evs if e.get("ev") == "gang_relaunch")
+    assert relaunch["epoch"] == 1 and "rank 1 lost" in relaunch["reason"], relaunch
+    launcher = [json.loads(x) for x in open(logs / "launcher.jsonl")]
+    assert launcher[0]["ev"] == "gang_relaunch" and launcher[0]["rank"] == 1 and launcher[0]["status"] == 128 + 9
+    assert launcher[-1]["ev"] == "job_complete"
+    assert "(signal)" in out.stderr
+
+
+def test_launcher_does_not_relaunch_a_deterministic_failure(tmp_path):
+    script = tmp_path / "fail.py"
+    script.write_text("import os, sys\nsys.exit(3 if os.environ['RANK'] == '0' else 0)\n")
+    out = subprocess.run([_launcher(), "--gpus", "2", "--max-restarts", "3", "--", sys.executable, str(script)],
+                         capture_output=True, text=True, timeout=40)
+    assert out.returncode == 3 and "epoch 1" not in out.stderr, out.stderr
