@@ -34,6 +34,9 @@ def main():
                     help="run the per-rank program of a W-rank job on this one GPU (runtime/loopback.py): the "
                          "all-to-all-v replaced by running every other source's stage untimed; reports per-rank ms")
     ap.add_argument("--loopback-rank", type=int, default=0)
+    ap.add_argument("--hbm-budget-gb", type=float, default=None,
+                    help="HbmBudgetBytes: a partition past it is aggregated chunk by chunk (runtime/stream_agg.py), "
+                         "e.g. --records-per-gpu 6.25e9 (400 GB) --hbm-budget-gb 60")
     ap.add_argument("--raw-shuffle", action="store_true",
                     help="with --loopback-ranks: shuffle the pruned raw rows (Select -> HashPartition -> GroupBy) "
                          "instead of partial aggregation before the shuffle")
@@ -46,6 +49,8 @@ def main():
     from dryad_amd.io.providers import provider_for
     ctx = D.DryadLinqContext(platform="gpu")
     ctx.PartitionCount = w.size
+    if a.hbm_budget_gb:
+        ctx.HbmBudgetBytes = int(a.hbm_budget_gb * 1e9)
     n = int(a.records_per_gpu) * w.size
     src = f"gen://records64?count={n}&partitions={w.size}&keys={int(a.keys)}&seed=4242" + \
         ("&bounds=0" if a.no_bounds else "")
@@ -82,6 +87,7 @@ def main():
         cnt, s1, s_in, groups = tot.tolist()
         valid = cnt == n and s1 == s_in
     med = sorted(times)[len(times) // 2]
+    streamed = [v for v in (ex.last_result.get("streamed") or {}).values() if v.get("kind") == "streamed aggregation"]
     report(w, {
         "metric": "GroupBy-Aggregate GB/s of input (10B x 64-byte records at 8 GPUs)",
         "value": round(n * 64 / med / 1e9, 3), "unit": "GB/s", "n_gpus": w.size, "steps": a.steps,
@@ -91,7 +97,9 @@ def main():
         "all_step_ms": [round(t * 1e3, 2) for t in times],
         "config": {"model": "GroupBy(Key) -> Count/Sum/Min/Max (decomposable, hash shuffle)",
                    "records": n, "record_bytes": 64, "keys": int(a.keys), "parallelism": f"dp{w.size}",
-                   "column_bounds": "measured in the step" if a.no_bounds else "declared by the generator"}})
+                   "column_bounds": "measured in the step" if a.no_bounds else "declared by the generator",
+                   "hbm_budget_bytes": ctx.HbmBudgetBytes,
+                   "streamed_aggregation": streamed[0] if streamed else None}})
 
 
 def loopback(a):

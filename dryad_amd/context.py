@@ -120,6 +120,8 @@ _DEFAULTS = dict(
     StreamStages=None,            # read -> record-wise ops -> partfile stages chunk-streamed (runtime/
     #                               streaming.py; None: when a source partition exceeds StreamChunkBytes)
     StreamChunkBytes=4 << 30,     # ... and their chunk size
+    StreamAggregate=None,         # read -> GroupBy / Distinct stages folded chunk by chunk in bounded HBM
+    #                               (runtime/stream_agg.py; None: when a partition exceeds HbmBudgetBytes)
     GraceJoin=None,               # a Join as the partitioned grace join stage (runtime/grace_stage.py;
     #                               None: when its inputs would crowd the HBM budget; False: never)
     LineAlignedSortInput=True,    # GPU executor: a table of 100-byte rows that only an OrderBy reads is

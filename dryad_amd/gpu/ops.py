@@ -968,13 +968,9 @@ def op_group_partial(op, inputs, v):
     return _partial_table(out, strs, d, len(kcols), form)
 
 
-def op_group_final(op, inputs, v):
-    t = _check(_one(inputs))
-    d = op["decomp"]
-    if t.n == 0:
-        raise NotTraceable("empty partition")
-    if t.shape.kind != "partial":
-        raise NotTraceable("group_final input is not a device partial table")
+def _accumulate_partials(t, d):
+    """RecursiveAccumulate over a device partial table: (key values, groups, iterator over the
+    per-spec accumulator columns) with one group per distinct key."""
     nkeys = t.shape.pytype.nkeys
     kcols, skeys = TR.eq_key_columns(tuple(TR.Col(v) if isinstance(v, torch.Tensor) else v
                                            for v in _key_values(t, nkeys)), t)
@@ -995,12 +991,51 @@ def op_group_final(op, inputs, v):
     if got is None:
         got = _payload_groups(kcols, skeys, specs, t.n)
     if got is not None:
-        keys, nseg, res = [got[0]], got[0].shape[0], iter(got[1])
-    else:
-        srt, seg, nseg, rows_at_start, starts = _group_keys(kcols, skeys)
-        kout, kstrs = _key_outputs(kcols, skeys, rows_at_start, srt, starts)
-        keys = _key_values(DeviceTable(nseg, Shape("tuple", list(kout)), kout, strs=kstrs), nkeys)
-        res = iter(R.seg_reduce_multi(srt, seg, nseg, specs))
+        return [got[0]], got[0].shape[0], iter(got[1])
+    srt, seg, nseg, rows_at_start, starts = _group_keys(kcols, skeys)
+    kout, kstrs = _key_outputs(kcols, skeys, rows_at_start, srt, starts)
+    keys = _key_values(DeviceTable(nseg, Shape("tuple", list(kout)), kout, strs=kstrs), nkeys)
+    return keys, nseg, iter(R.seg_reduce_multi(srt, seg, nseg, specs))
+
+
+def combine_partials(t, d):
+    """Partial tables (concatenated in ``t``) folded into one partial row per distinct key, in the
+    same partial layout: the combine step of a streamed GroupBy (runtime/stream_agg.py), whose
+    running state stays a partial table until the final reduce."""
+    if t.shape.kind != "partial":
+        raise NotTraceable("combine_partials: not a device partial table")
+    if t.strs:
+        raise NotTraceable("combine_partials: string keys")
+    if t.n == 0:
+        return t
+    keys, nseg, res = _accumulate_partials(t, d)
+    out = {f"k{i}": k for i, k in enumerate(keys)}
+    for j, a in enumerate(d.aggs):
+        out[f"a{j}"] = next(res)
+        if a.kind == "avg":
+            out[f"c{j}"] = next(res)
+    meta = t.shape.pytype
+    for j, a in enumerate(d.aggs):         # min / max / any / all keep the partial table's dtypes
+        col = t.cols[f"a{j}"]                # (sums and counts stay widened: no overflow on the way)
+        if out[f"a{j}"].dtype != col.dtype and a.kind in ("min", "max", "any", "all"):
+            out[f"a{j}"] = out[f"a{j}"].to(col.dtype)
+    tb = DeviceTable.from_columns(out, Shape("partial", list(out), meta))
+    return tb
+
+
+def op_group_final(op, inputs, v):
+    t = _check(_one(inputs))
+    d = op["decomp"]
+    if t.n == 0:
+        raise NotTraceable("empty partition")
+    if t.shape.kind != "partial":
+        raise NotTraceable("group_final input is not a device partial table")
+    return final_reduce(t, d)
+
+
+def final_reduce(t, d):
+    """RecursiveAccumulate + FinalReduce of a partial table -> the GroupBy's result table."""
+    keys, nseg, res = _accumulate_partials(t, d)
     vals = []
     for j, a in enumerate(d.aggs):
         col = t.cols[f"a{j}"]

@@ -37,6 +37,7 @@ from ..io.hosttable import HostRows
 from ..ops import extsort as EX
 from ..io.providers import parse_uri, provider_for
 from . import checkpoint as CK
+from . import stream_agg as SA
 from ..native import runtime as native_runtime
 from ..parallel import shuffle
 from ..parallel.comm import World, get_world, init_world
@@ -168,6 +169,7 @@ class GpuJobRunner:
         self.row_sets: dict = {}          # (stage, partition) -> pooled BufferSet holding its rows
         self.moved: dict = {}             # (stage, partition) -> rank whose duplicate attempt won
         self.stream_plans: dict = {}      # stage -> chunk plan of a streamed stage (None: not streamed)
+        self.agg_plans: dict = {}         # stage -> plan of a streamed (out-of-core) GroupBy / Distinct
         self.empty_host_ops: list = []    # host operators that ran over empty inputs only
         self.stream_stats: dict = {}      # (stage, partition) -> chunks / records / bytes streamed
         self.place = None                 # partition -> rank (None: p % W)
@@ -902,6 +904,16 @@ class GpuJobRunner:
                 raise ChannelReadError(self.edge_ids[(self.vids[s.inputs[0].src][q], self.vids[s.id][p], 0)],
                                        f"injected read error on the channel {s.inputs[0].src}[{q}] -> {s.id}[{p}]")
         vctx = GpuVertexContext(p, s.partitions, self.vids[s.id][p], version, s, self.dev, self.world, self)
+        if s.id not in self.agg_plans:
+            self.agg_plans[s.id] = SA.plan(self, s)
+        if self.agg_plans[s.id] is not None:
+            # read -> ... -> GroupBy / Distinct over a partition past the HBM budget: chunks folded
+            # into hash-bucketed running states, spilled to pinned host memory when they outgrow it
+            with TRC.range(f"vertex {s.id}:{s.name}[{p}] v{version} (streamed aggregation)"):
+                out = SA.run(self, s, p, version, vctx, self.agg_plans[s.id])
+            if fault == "crash":
+                raise VertexCrash(f"injected crash of {s.name}[{p}] v{version} (output discarded)")
+            return out
         if s.id not in self.stream_plans:
             self.stream_plans[s.id] = ST.streamable(self, s)
         if self.stream_plans[s.id] is not None:

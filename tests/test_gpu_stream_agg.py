@@ -1,0 +1,73 @@
+"""Streamed, out-of-core GroupBy / Distinct (runtime/stream_agg.py): a partition far past the HBM
+budget aggregated chunk by chunk into hash-bucketed running states, the largest states spilled to
+pinned host memory; results against the LocalDebug oracle, no host fallbacks."""
+import pytest
+
+import dryad_amd as D
+
+pytestmark = pytest.mark.gpu
+
+SRC = "gen://records64?count={n}&partitions={P}&keys={k}&seed=11"
+
+
+def _ctx(P=1, budget=24 << 20, chunk=2 << 20):
+    c = D.DryadLinqContext(platform="gpu")
+    c.PartitionCount = P
+    c.HbmBudgetBytes = budget
+    c.StreamChunkBytes = chunk
+    return c
+
+
+def _loc():
+    c = D.DryadLinqContext(1)
+    c.LocalDebug = True
+    return c
+
+
+def _stats(c):
+    r = c._get_executor().last_result
+    st = [v for v in (r.get("streamed") or {}).values() if v.get("kind") == "streamed aggregation"]
+    return r, st
+
+
+@pytest.mark.parametrize("keys", [3000, 400_000])
+def test_streamed_groupby_matches_oracle(keys):
+    src = SRC.format(n=600_000, P=1, k=keys)
+    q = lambda c: c.FromStore(src).Where(lambda r: r[3] % 7 != 0).GroupBy(  # noqa: E731
+        lambda r: r[0], lambda k, g: (k, g.Count(), g.Sum(lambda r: r[1]), g.Min(lambda r: r[2]),
+                                      g.Max(lambda r: r[4]), g.Average(lambda r: r[5])))
+    g = _ctx()
+    got = sorted(q(g))
+    res, st = _stats(g)
+    assert st and st[0]["chunks"] > 4 and st[0]["combines"] > 0, st
+    if keys > 100_000:
+        assert st[0]["spilled_bytes"] > 0, st          # the states outgrow the 24 MB budget
+    assert res["fallbacks"] == [], res["fallbacks"]
+    exp = sorted(q(_loc()))
+    assert len(got) == len(exp)
+    for a, b in zip(got, exp):
+        assert a[:5] == b[:5] and abs(a[5] - b[5]) <= 1e-9 * max(1.0, abs(b[5])), (a, b)
+
+
+def test_streamed_distinct_matches_oracle():
+    src = SRC.format(n=500_000, P=1, k=1 << 20)
+    q = lambda c: c.FromStore(src).Select(lambda r: r[0] % 150_001).Distinct()  # noqa: E731
+    g = _ctx()
+    got = sorted(q(g))
+    res, st = _stats(g)
+    assert st and st[0]["chunks"] > 4, st
+    assert res["fallbacks"] == [], res["fallbacks"]
+    assert got == sorted(q(_loc()))
+
+
+def test_streamed_partial_side_of_a_two_partition_groupby():
+    """Two partitions on one rank: the partial side (read -> group_partial -> hash_partition)
+    streams, the folded partials go through the exchange and the final GroupBy."""
+    src = SRC.format(n=400_000, P=2, k=50_000)
+    q = lambda c: c.FromStore(src).GroupBy(lambda r: r[0], lambda k, g: (k, g.Count(), g.Sum(lambda r: r[1])))  # noqa
+    g = _ctx(P=2)
+    got = sorted(q(g))
+    res, st = _stats(g)
+    assert len(st) == 2 and all(x["chunks"] > 4 for x in st), st
+    assert res["fallbacks"] == [], res["fallbacks"]
+    assert got == sorted(q(_loc()))
