@@ -112,3 +112,41 @@ DR_API int dr_token_verify(const uint8_t* buf, const int64_t* off, const int64_t
   DR_LAUNCH_CHECK();
   return 0;
 }
+
+namespace {
+
+// Strings laid inline into fixed-width rows (the grace join's packed rows, runtime/grace_stage.py):
+// one wave per 64 rows, each lane copying one row's string byte by byte (strings are short: the
+// caller caps them at max_len); the destination bytes past a string stay as they were (zero).
+__global__ __launch_bounds__(256) void scatter_strings_kernel(const uint8_t* __restrict__ heap,
+                                                              const int64_t* __restrict__ off,
+                                                              const int64_t* __restrict__ len, uint64_t n,
+                                                              uint8_t* __restrict__ dst, uint64_t stride,
+                                                              uint32_t dst_off, uint32_t max_len,
+                                                              uint32_t* __restrict__ overflow) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    int64_t L = len[i];
+    if (L < 0 || L > (int64_t)max_len) {
+      atomicOr(overflow, 1u);
+      L = L < 0 ? 0 : (int64_t)max_len;
+    }
+    const uint8_t* s = heap + off[i];
+    uint8_t* d = dst + i * stride + dst_off;
+    for (int64_t k = 0; k < L; ++k) d[k] = s[k];
+  }
+}
+
+}  // namespace
+
+// dst row i (stride bytes apart) gets string i's bytes at dst_off; lengths past max_len are cut
+// and flag *overflow (the caller refuses the layout).
+DR_API int dr_scatter_strings(const uint8_t* heap, const int64_t* off, const int64_t* len, uint64_t n, uint8_t* dst,
+                              uint64_t stride, uint32_t dst_off, uint32_t max_len, uint32_t* overflow,
+                              hipStream_t s) {
+  if (n == 0) return 0;
+  if (dst_off + max_len > stride || overflow == nullptr) return (int)hipErrorInvalidValue;
+  scatter_strings_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(heap, off, len, n, dst, stride, dst_off, max_len,
+                                                                  overflow);
+  DR_LAUNCH_CHECK();
+  return 0;
+}

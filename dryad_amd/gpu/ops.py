@@ -255,6 +255,12 @@ def op_read(op, inputs, v):
                     stats.set_bounds(c, 0, (1 << 31) - 1)
             names = FIELDS[:ncols]
             return DeviceTable.from_columns(dict(zip(names, cols)), Shape("tuple", names))
+        if kind == "names":
+            from ..models import names as NM
+            from ..models.records_cpu import dim_multiplier
+            nk = int(q.get("keys", 1 << 20))
+            return NM.device_table(lo, hi - lo, nk, int(q.get("seed", 0)),
+                                   dim_multiplier(nk) if q.get("mode") == "dim" else 0, v.device)
         if kind == "range":
             start = int(q.get("start", 0))
             a = torch.arange(start + lo, start + hi, dtype=torch.int32 if start + hi < 2**31 else torch.int64,

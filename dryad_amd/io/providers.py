@@ -352,7 +352,9 @@ class GenProvider(DataProvider):
     (tuples on the object path, one [n, 128] HBM tensor on the GPU executor);
     ``gen://records64?count=N&partitions=P&keys=K&seed=S[&cols=C]`` yields 64-byte records of 8
     int64 fields (Key uniform in [0, K), V1..V7 31-bit values), columnar in HBM; ``&mode=dim``
-    makes it a dimension table (keys a bijection of [0, K), payload a function of the key)."""
+    makes it a dimension table (keys a bijection of [0, K), payload a function of the key);
+    ``gen://names?count=N&partitions=P&keys=K&seed=S[&mode=dim]`` yields (Name, V1, V2) records with
+    a string key "u<decimal>" (models/names.py)."""
     scheme = "gen"
 
     def _args(self, uri):
@@ -368,6 +370,8 @@ class GenProvider(DataProvider):
             return p, int(q.get("count", 0)) * 4 * 128
         if kind == "records64":
             return p, int(q.get("count", 0)) * 8 * int(q.get("cols", 8))
+        if kind == "names":
+            return p, int(q.get("count", 0)) * 32
         return p, int(q.get("count", 0)) * 4
 
     def exists(self, uri):
@@ -381,6 +385,9 @@ class GenProvider(DataProvider):
             from ..models.records_cpu import FIELDS
             ncols = int(self._args(uri)[1].get("cols", 8))
             dt = T.RecordT([(f, T.Int64) for f in FIELDS[:ncols]], tuple)
+        if kind == "names":
+            from ..models import names as NM
+            dt = NM.dtype()
         return {"dtype": dt}
 
     def delete(self, uri):
@@ -410,6 +417,12 @@ class GenProvider(DataProvider):
             nk = int(q.get("keys", 1 << 20))
             return gen_records(lo, hi - lo, nk, int(q.get("seed", 0)), int(q.get("cols", 8)),
                                dim_multiplier(nk) if q.get("mode") == "dim" else 0)
+        if kind == "names":
+            from ..models import names as NM
+            from ..models.records_cpu import dim_multiplier
+            nk = int(q.get("keys", 1 << 20))
+            return NM.host_records(lo, hi - lo, nk, int(q.get("seed", 0)),
+                                   dim_multiplier(nk) if q.get("mode") == "dim" else 0)
         raise DryadLinqException(ErrorCode.UnrecognizedDataSource, f"unknown generator {kind}")
 
     def temp_uri(self, name):

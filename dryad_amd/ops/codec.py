@@ -290,9 +290,11 @@ def decode_var(buf: torch.Tensor, dtype, n: int, block_off: torch.Tensor, block:
     return t
 
 
-def encode_var(table, dtype, block: int = BLOCK):
+def encode_var(table, dtype, block: int = BLOCK, full_offsets: bool = False):
     """Columnar DeviceTable with string fields -> (HBM record-stream bytes, int64 block index on
-    the device) in DryadLinqBinary layout, or None if not applicable."""
+    the device) in DryadLinqBinary layout, or None if not applicable.  ``full_offsets``: the
+    second value is every record's byte offset (a streamed writer builds the block index of the
+    concatenated stream from them)."""
     lay = var_layout(dtype)
     if lay is None or table.rows is not None:
         return None
@@ -339,4 +341,4 @@ def encode_var(table, dtype, block: int = BLOCK):
     out = torch.empty(total, dtype=torch.uint8, device=dev)
     if n:
         _lib.call("dr_codec_var_encode", ptr(out), c_u64(n), nf, sizes, cps, lps, hps, ptr(units), ptr(offs), st)
-    return out, offs[::block].contiguous()
+    return out, (offs if full_offsets else offs[::block].contiguous())

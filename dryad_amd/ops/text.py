@@ -164,3 +164,24 @@ def word_count_table(buf: torch.Tensor):
     t = DeviceTable.from_columns({"Item1": woff, "Item1#len": wl, "Item2": cnt}, Shape("tuple", ["Item1", "Item2"]))
     t.strs = {"Item1": heap}
     return t
+
+
+_lib.register_signatures({
+    "dr_scatter_strings": (c_i32, [vp, vp, vp, c_u64, vp, c_u64, ctypes.c_uint32, ctypes.c_uint32, vp, vp]),
+})
+
+
+def scatter_strings(heap: torch.Tensor, off: torch.Tensor, ln: torch.Tensor, dst: torch.Tensor, dst_off: int,
+                    max_len: int | None = None) -> bool:
+    """Copy string i (``heap[off[i]: off[i] + ln[i]]``) into row i of ``dst`` ([n, stride] uint8)
+    at byte ``dst_off``.  Returns False when a string is longer than ``max_len`` (default: the
+    room up to the row's end), which is then cut."""
+    n, stride = dst.shape
+    ml = stride - dst_off if max_len is None else max_len
+    flag = torch.zeros(1, dtype=torch.int32, device=dst.device)
+    if heap.numel() == 0:
+        heap = torch.zeros(8, dtype=torch.uint8, device=dst.device)
+    _lib.call("dr_scatter_strings", ptr(heap), ptr(off.to(torch.int64).contiguous()), ptr(ln.to(torch.int64).contiguous()),
+              c_u64(n), ptr(dst), c_u64(stride), ctypes.c_uint32(dst_off), ctypes.c_uint32(ml), ptr(flag),
+              stream_of(dst))
+    return int(flag.item()) == 0

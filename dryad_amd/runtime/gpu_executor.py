@@ -1704,6 +1704,8 @@ def _commit_partfile_impl(runner, s, uri, path, local):
         tmp = PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, 0)
         if isinstance(v, GS.StreamedPart):          # written bucket / chunk by chunk by its stage
             os.replace(v.path, tmp)
+            if os.path.exists(v.path + PF.INDEX_SUFFIX):         # the block index of string records
+                os.replace(v.path + PF.INDEX_SUFFIX, tmp + PF.INDEX_SUFFIX)
             if v.rows is not None:
                 fmt_extra = dict(v.rows)
             mine[p] = tmp

@@ -63,30 +63,52 @@ class StreamedPart:
 
 
 # ------------------------------------------------------------------------------------------------
-# input sides: rows of int64 words (floats by bit pattern, narrower ints widened)
+# input sides: device tables chunk by chunk; packed into rows of int64 words for the grace
+# partitioner: word 0 = the join key word, then every field the result selector reads (a fixed-
+# width field is one word, floats by bit pattern; a string field is a length word and its bytes
+# inline, zero-padded, up to GraceJoinStringBytes).
 class _Side:
     fields: list
-    dtypes: list                          # torch dtype per field
-    shape: Shape
+    dtypes: list                          # torch dtype per field, None for a string field
     n: int
+    shape: Shape | None = None
 
-    def chunk(self, a: int, b: int, dev) -> torch.Tensor:          # int64 [b - a, len(fields)]
+    def chunk_table(self, a: int, b: int, dev) -> DeviceTable:
         raise NotImplementedError
 
-    def table(self, words: torch.Tensor, cols: list) -> DeviceTable:
-        """DeviceTable of this side from int64 words [m, 1 + len(cols)] (column 0 = key) holding
-        the fields ``cols``; fields the selector never reads are absent."""
-        out = {}
-        for j, f in enumerate(cols):
-            w = words[:, 1 + j]
-            dt = self.dtypes[f]
+    def field_words(self, f: int, S: int) -> int:
+        return 1 + S if self.dtypes[f] is None else 1
+
+    def table(self, words: torch.Tensor, cols: list, S: int) -> DeviceTable:
+        """DeviceTable of this side from packed rows ``words`` [m, width] (word 0 = key word)
+        holding the fields ``cols`` in order; fields the selector never reads are absent.  String
+        fields point into the rows' own bytes (the gathered pair rows are the string heap)."""
+        out, strs = {}, {}
+        m, width = words.shape
+        pos = 1
+        heap = None
+        for f in cols:
+            name, dt = self.fields[f], self.dtypes[f]
+            if dt is None:
+                if heap is None:
+                    heap = words.contiguous().view(torch.uint8).view(-1)
+                base = torch.arange(m, dtype=_I64, device=words.device) * (8 * width)
+                out[name] = base + 8 * (pos + 1)
+                out[name + "#len"] = words[:, pos].contiguous()
+                strs[name] = heap
+                pos += 1 + S
+                continue
+            w = words[:, pos]
             if dt.itemsize == 8:
-                out[self.fields[f]] = w.view(dt)
+                out[name] = w.view(dt)
             elif dt.is_floating_point:              # stored as the float64 bit pattern
-                out[self.fields[f]] = w.view(torch.float64).to(dt)
+                out[name] = w.view(torch.float64).to(dt)
             else:
-                out[self.fields[f]] = w.to(dt)
-        return DeviceTable(words.shape[0], self.shape, out)
+                out[name] = w.to(dt)
+            pos += 1
+        t = DeviceTable(m, self.shape if self.shape is not None else Shape("tuple", list(self.fields)), out)
+        t.strs = strs
+        return t
 
 
 def _as_words(cols: list) -> torch.Tensor:
@@ -101,6 +123,14 @@ def _as_words(cols: list) -> torch.Tensor:
     return torch.stack(ws, 1)
 
 
+def _word(c: torch.Tensor) -> torch.Tensor:
+    if c.dtype.itemsize == 8:
+        return c.view(_I64)
+    if c.dtype.is_floating_point:
+        return c.double().view(_I64)
+    return c.to(_I64)
+
+
 class _GenSide(_Side):
     def __init__(self, uri, part):
         self.g = FJ._GenRows(uri, part)
@@ -108,19 +138,39 @@ class _GenSide(_Side):
         self.dtypes = [_I64] * len(self.fields)
         self.shape = Shape("tuple", self.fields)
 
-    def chunk(self, a, b, dev):
-        return self.g.chunk(a, b, dev)
+    def chunk_table(self, a, b, dev):
+        w = self.g.chunk(a, b, dev)
+        return DeviceTable(b - a, self.shape, {f: w[:, j] for j, f in enumerate(self.fields)})
+
+
+class _NamesSide(_Side):
+    """gen://names: (Name string, V1, V2), generated on the device chunk by chunk."""
+
+    def __init__(self, uri, part):
+        from ..models import names as NM
+        from ..models.records_cpu import dim_multiplier
+        _, _, q = parse_uri(uri)
+        self.lo, hi = GenProvider().bounds(uri, part)
+        self.n = hi - self.lo
+        self.nk, self.seed = int(q.get("keys", 1 << 20)), int(q.get("seed", 0))
+        self.dim = dim_multiplier(self.nk) if q.get("mode") == "dim" else 0
+        self.fields, self.dtypes = list(NM.FIELDS), [None, _I64, _I64]
+        self.shape = Shape("tuple", self.fields)
+
+    def chunk_table(self, a, b, dev):
+        from ..models import names as NM
+        return NM.device_table(self.lo + a, b - a, self.nk, self.seed, self.dim, dev)
 
 
 class _TableSide(_Side):
     def __init__(self, t: DeviceTable):
         self.t, self.n = t, t.n
         self.fields = list(t.shape.fields)
-        self.dtypes = [t.cols[f].dtype for f in self.fields]
+        self.dtypes = [None if f in t.strs else t.cols[f].dtype for f in self.fields]
         self.shape = t.shape
 
-    def chunk(self, a, b, dev):
-        return _as_words([self.t.cols[f][a:b] for f in self.fields])
+    def chunk_table(self, a, b, dev):
+        return self.t.slice(a, b)
 
 
 class _PartfileSide(_Side):
@@ -134,50 +184,207 @@ class _PartfileSide(_Side):
         self.dtypes = [f[1] for f in lay]
         self.shape = None
 
-    def chunk(self, a, b, dev):
+    def chunk_table(self, a, b, dev):
         from ..io import reader as RD
         from ..ops import codec as CD
         if b <= a:
-            return torch.empty((0, len(self.fields)), dtype=_I64, device=dev)
+            return DeviceTable(0, self.shape or Shape("tuple", self.fields),
+                               {f: torch.empty(0, dtype=d, device=dev) for f, d in zip(self.fields, self.dtypes)})
         buf = RD.read_to_device(self.path, dev, offset=a * self.width, length=(b - a) * self.width)
         t = CD.decode(buf, self.dt)
         if self.shape is None:
             self.shape = t.shape
-        return _as_words([t.cols[f] for f in self.fields])
+        return t
 
-    def table(self, words, cols):
+
+class _VarPartfileSide(_Side):
+    """A partfile:// table of records with string fields: whole index blocks of records read by
+    the chunked reader and decoded on the device (ops/codec.decode_var over the part's
+    ``.idx`` block index), the part bytes of the chunk being the strings' heap."""
+
+    def __init__(self, path, dtype, vlay, idx):
+        self.path, self.dt = path, dtype
+        self.n, self.nbytes, self.block, self.offs = idx
+        self.fields = [f[0] for f in vlay]
+        self.dtypes = [f[1] for f in vlay]
+        self.shape = None
+
+    def align(self, rows: int) -> int:
+        return max(self.block, rows // self.block * self.block)
+
+    def chunk_table(self, a, b, dev):
+        from ..io import reader as RD
+        from ..ops import codec as CD
+        B = self.block
+        if b <= a:
+            t = CD.decode_var(torch.empty(0, dtype=torch.uint8, device=dev), self.dt, 0,
+                              torch.zeros(0, dtype=_I64, device=dev), B)
+            return t
+        assert a % B == 0 and (b % B == 0 or b == self.n), (a, b, B)
+        lo = int(self.offs[a // B])
+        hi = int(self.offs[b // B]) if b < self.n else self.nbytes
+        buf = RD.read_to_device(self.path, dev, offset=lo, length=hi - lo)
+        bo = torch.from_numpy(self.offs[a // B: -(-b // B)] - lo).to(dev)
+        t = CD.decode_var(buf, self.dt, b - a, bo, B)
         if self.shape is None:
-            self.chunk(0, min(self.n, 1), words.device)
-        return _Side.table(self, words, cols)
+            self.shape = t.shape
+        return t
 
 
 def _side(read_op, part):
     scheme, path, q = parse_uri(read_op["uri"])
     if scheme == "gen" and path.strip("/") == "records64":
         return _GenSide(read_op["uri"], part)
+    if scheme == "gen" and path.strip("/") == "names":
+        return _NamesSide(read_op["uri"], part)
     if scheme == "hbm":
         ent = provider_for(read_op["uri"]).get(read_op["uri"])
         t = ent["local"].get(part)
-        if isinstance(t, DeviceTable) and t.rows is None and not t.strs and t.heap is None and t.cols and \
-                all(t.cols[f].dim() == 1 and t.cols[f].dtype in _WORD for f in t.shape.fields):
+        if isinstance(t, DeviceTable) and t.rows is None and t.heap is None and t.cols and \
+                all(f in t.strs or (t.cols[f].dim() == 1 and t.cols[f].dtype in _WORD) for f in t.shape.fields):
             return _TableSide(t)
         return None
     if scheme in ("partfile", "file"):
         from ..ops import codec as CD
+        from ..io import partfile as PF
         prov = provider_for(read_op["uri"])
         if not prov.exists(read_op["uri"]):
             return None
         sch = prov.schema(read_op["uri"]) or {}
         dt = read_op.get("dtype") or sch.get("dtype")
-        lay = CD.layout(dt) if dt is not None and sch.get("format", "binary") == "binary" else None
-        pf = prov.part_file(read_op["uri"], part) if hasattr(prov, "part_file") else None
-        if lay is None or pf is None or any(f[1] not in _WORD for f in lay[0]):
+        if dt is None or sch.get("format", "binary") != "binary":
             return None
-        return _PartfileSide(pf, dt, lay[0], lay[1])
+        pf = prov.part_file(read_op["uri"], part) if hasattr(prov, "part_file") else None
+        if pf is None:
+            return None
+        lay = CD.layout(dt)
+        if lay is not None:
+            if any(f[1] not in _WORD for f in lay[0]):
+                return None
+            return _PartfileSide(pf, dt, lay[0], lay[1])
+        vlay = CD.var_layout(dt)
+        idx = PF.read_index(pf) if vlay is not None and dt not in ("String",) else None
+        if vlay is None or idx is None or any(f[1] is not None and f[1] not in _WORD for f in vlay):
+            return None
+        if len(vlay) == 1:                  # a bare String table (text_table layout): not a record
+            return None
+        return _VarPartfileSide(pf, dt, [(f[0], f[1]) for f in vlay], idx)
     return None
 
 
 _WORD = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool, torch.float64, torch.float32)
+
+
+# ------------------------------------------------------------------------------------------------
+# join keys: a field or a tuple of fields of each side
+class _FieldRef:
+    __slots__ = ("i",)
+
+    def __init__(self, i):
+        self.i = i
+
+
+class _KRec:
+    def __init__(self, fields):
+        self._fields = list(fields)
+
+    def __getitem__(self, i):
+        if isinstance(i, int) and -len(self._fields) <= i < len(self._fields):
+            return _FieldRef(i % len(self._fields))
+        raise KeyError(i)
+
+    def __getattr__(self, name):
+        if name.startswith("_") or name not in self._fields:
+            raise AttributeError(name)
+        return _FieldRef(self._fields.index(name))
+
+
+def _key_spec(fn, fields):
+    """Field indices of a key selector that returns a field or a tuple of fields, else None."""
+    try:
+        k = fn(_KRec(fields))
+    except Exception:  # noqa: BLE001
+        return None
+    if isinstance(k, _FieldRef):
+        return [k.i]
+    if isinstance(k, tuple) and k and all(isinstance(x, _FieldRef) for x in k):
+        return [x.i for x in k]
+    return None
+
+
+def _key_kinds(side, spec):
+    return tuple("str" if side.dtypes[f] is None else "float" if side.dtypes[f].is_floating_point else "int"
+                 for f in spec)
+
+
+def _canon_float(c: torch.Tensor) -> torch.Tensor:
+    """float64 with -0.0 -> 0.0 and one NaN (LINQ's Double.Equals: NaN equals NaN, 0.0 == -0.0)."""
+    x = c.double() + 0.0
+    return torch.where(torch.isnan(x), torch.full_like(x, float("nan")), x)
+
+
+def _key_word(t: DeviceTable, side, spec, exact: bool) -> torch.Tensor:
+    """The join key word of every row of chunk ``t``: the integer key itself or the canonical
+    float bits (``exact``), else a 64-bit hash of the key fields (strings by their bytes) whose
+    matches are verified field by field after the probe."""
+    from ..ops import relational as R
+    if exact:
+        c = t.cols[side.fields[spec[0]]]
+        return _canon_float(c).view(_I64) if c.is_floating_point() else c.to(_I64)
+    keys = []
+    for f in spec:
+        name = side.fields[f]
+        if side.dtypes[f] is None:
+            keys.append(R.HashKey.string(t.strs[name], t.cols[name], t.cols[name + "#len"]))
+        else:
+            c = t.cols[name]
+            keys.append(R.HashKey.column(_canon_float(c) if c.is_floating_point() else c.to(_I64)))
+    _, hs = R.stable_hash_dest(keys, t.n, 0, len(keys) > 1, t.device, want_hash=True)
+    return hs
+
+
+def _pack(t: DeviceTable, side, cols: list, width: int, S: int, kw: torch.Tensor):
+    """Rows [m, width] int64: word 0 = kw, then the fields ``cols`` (strings: length + bytes).
+    Returns (rows, ok): ok False when a string is longer than S words."""
+    m = t.n
+    rows = torch.zeros((m, width), dtype=_I64, device=kw.device)
+    if m == 0:
+        return rows, True
+    rows[:, 0] = kw
+    pos = 1
+    ok = True
+    for f in cols:
+        name = side.fields[f]
+        if side.dtypes[f] is None:
+            from ..ops import text as TX
+            off, ln = t.cols[name].to(_I64), t.cols[name + "#len"].to(_I64)
+            rows[:, pos] = ln
+            rb = rows.view(torch.uint8).view(m, 8 * width)
+            ok = TX.scatter_strings(t.strs[name], off, ln, rb, 8 * (pos + 1), max_len=8 * S) and ok
+            pos += 1 + S
+            continue
+        rows[:, pos] = _word(t.cols[name])
+        pos += 1
+    return rows, ok
+
+
+def _verify(orows, irows, oi, ii, lay, S):
+    """Pairs whose key fields are equal (hash-keyed joins): each component compared word by word
+    (strings: length and inline bytes; floats: as canonical values)."""
+    keep = None
+    for (of, opos, kind), (inf, ipos, _) in zip(lay["kpos"][0], lay["kpos"][1]):
+        if kind == "str":
+            a = orows.index_select(0, oi)[:, opos: opos + 1 + S]
+            b = irows.index_select(0, ii)[:, ipos: ipos + 1 + S]
+            eq = (a == b).all(1)
+        elif kind == "float":
+            a = orows[:, opos].index_select(0, oi).view(torch.float64)
+            b = irows[:, ipos].index_select(0, ii).view(torch.float64)
+            eq = (a == b) | (torch.isnan(a) & torch.isnan(b))
+        else:
+            eq = orows[:, opos].index_select(0, oi) == irows[:, ipos].index_select(0, ii)
+        keep = eq if keep is None else keep & eq
+    return keep
 
 
 # ------------------------------------------------------------------------------------------------
@@ -340,17 +547,21 @@ def plan_local(desc, runner):
         return None
     fo, fi = sides[0][0].fields, sides[1][0].fields
     op = desc["op"]
-    try:
-        ko = FJ._key_field(op["outer_key"], 0, fo)
-        ki = FJ._key_field(op["inner_key"], 1, fi)
-    except FJ.NotLinear as e:
-        log.info("join %s: no grace stage (%s)", desc["join"], e)
+    ko, ki = _key_spec(op["outer_key"], fo), _key_spec(op["inner_key"], fi)
+    if ko is None or ki is None or len(ko) != len(ki):
+        log.info("join %s: no grace stage (keys are not fields / tuples of fields)", desc["join"])
         return None
-    if sides[0][0].dtypes[ko].is_floating_point or sides[1][0].dtypes[ki].is_floating_point:
+    kinds = _key_kinds(sides[0][0], ko)
+    if kinds != _key_kinds(sides[1][0], ki):
         return None
+    exact = len(ko) == 1 and kinds[0] != "str"
     used = _used_fields(op["result"], fo, fi) or (list(range(len(fo))), list(range(len(fi))))
+    uo, ui = list(used[0]), list(used[1])
+    if not exact:                         # the key fields travel too: matches are verified
+        uo = sorted(set(uo) | set(ko))
+        ui = sorted(set(ui) | set(ki))
     rows = [sum(x.n for x in sd) for sd in sides]
-    return dict(ko=ko, ki=ki, uo=used[0], ui=used[1], rows=rows,
+    return dict(ko=ko, ki=ki, uo=uo, ui=ui, rows=rows, exact=exact, kinds=list(kinds),
                 bytes=rows[0] * 8 * len(fo) + rows[1] * 8 * len(fi))
 
 
@@ -366,9 +577,9 @@ def vote(desc, runner):
     if W > 1:
         votes = [None] * W
         dist.all_gather_object(votes, lay)
-    if any(v is None for v in votes) or any((v["ko"], v["ki"], v["uo"], v["ui"]) !=
-                                            (votes[0]["ko"], votes[0]["ki"], votes[0]["uo"], votes[0]["ui"])
-                                            for v in votes):
+    if any(v is None for v in votes) or any((v["ko"], v["ki"], v["uo"], v["ui"], v["exact"]) !=
+                                            (votes[0]["ko"], votes[0]["ki"], votes[0]["uo"], votes[0]["ui"],
+                                             votes[0]["exact"]) for v in votes):
         return None
     if force is not True:
         from ..ops.extsort import default_budget
@@ -391,7 +602,19 @@ def run(desc, runner, lay) -> dict:
     parts = [p for p in range(stage.partitions) if runner.owner(p) == me]
     sides = [[_side(r, p) for p in parts] for r in desc["reads"]]
     keys, used = (lay["ko"], lay["ki"]), (lay["uo"], lay["ui"])
-    width = 1 + max(len(used[0]), len(used[1]))              # [key, fields..] padded to one stride
+    S = -(-int(runner.ctx._props.get("GraceJoinStringBytes") or 64) // 8)      # inline string words
+    proto = [sides[0][0], sides[1][0]]
+    nwords = [1 + sum(proto[k].field_words(f, S) for f in used[k]) for k in (0, 1)]
+    width = max(nwords)                                      # [key word, fields..] padded to one stride
+    # where each key field sits in the packed rows (for the verification of hash-keyed matches)
+    kpos = []
+    for k in (0, 1):
+        pos, at = 1, {}
+        for f in used[k]:
+            at[f] = pos
+            pos += proto[k].field_words(f, S)
+        kpos.append([(f, at.get(f, -1), kind) for f, kind in zip(keys[k], lay["kinds"])])
+    vlay = dict(kpos=kpos)
     n_loc = torch.tensor([sum(x.n for x in sd) for sd in sides], dtype=_I64, device=dev)
     n_tot, n_max = n_loc.clone(), n_loc.clone()
     shuffle.all_reduce_(n_tot, "sum", w)
@@ -402,29 +625,35 @@ def run(desc, runner, lay) -> dict:
     chunk_rows = max(1, min(CHUNK_ROWS, max(n_max)))
     sched = []
     for s_ in (0, 1):                     # the same number of (collective) add_chunk calls everywhere
-        lst = [(x, a, min(x.n, a + chunk_rows)) for x in sides[s_] for a in range(0, x.n, chunk_rows)]
+        step = sides[s_][0].align(chunk_rows) if hasattr(sides[s_][0], "align") else chunk_rows
+        lst = [(x, a, min(x.n, a + step)) for x in sides[s_] for a in range(0, x.n, step)]
         cnt = torch.tensor([len(lst)], dtype=_I64, device=dev)
         shuffle.all_reduce_(cnt, "max", w)
         lst += [(sides[s_][0], 0, 0)] * (int(cnt.item()) - len(lst))
         sched.append(lst)
-    grace = GR.GraceHashJoin(w, 8 * width, 0, 8, {"O": -(-n_tot[0] // W), "I": -(-n_tot[1] // W)}, chunk_rows,
+    grace = GR.GraceHashJoin(w, 8 * width, 0, 8, {"O": -(-n_tot[0] // W), "I": -(-n_tot[1] // W)},
+                             max(b - a for lst in sched for _, a, b in lst) or 1,
                              hbm_budget=runner.ctx._props.get("HbmBudgetBytes"), build=names[build])
     t0 = time.perf_counter()
     sink = _Sink(runner, stage, parts, desc)
     matches = 0
+    strings = any(d is None for k in (0, 1) for d in proto[k].dtypes)
     try:
         for s_ in (0, 1):
-            sel = [keys[s_]] + list(used[s_])
             for src, a, b in sched[s_]:
-                words = src.chunk(a, b, dev)
-                rows = torch.zeros((b - a, width), dtype=_I64, device=dev)
-                if b > a:
-                    rows[:, : len(sel)] = words[:, sel]
+                t = src.chunk_table(a, b, dev)
+                kw = _key_word(t, src, keys[s_], lay["exact"]) if t.n else torch.empty(0, dtype=_I64, device=dev)
+                rows, ok = _pack(t, src, used[s_], width, S, kw)
+                if strings and not all(o for o, _ in shuffle.gang_status(ok, 0, w)):
+                    # a string past GraceJoinStringBytes on some rank: every rank leaves together
+                    from ..errors import GangAgreementError
+                    raise GangAgreementError(f"grace join: a string field longer than {8 * S} bytes "
+                                             "(GraceJoinStringBytes)")
+                del t
                 grace.add_chunk(names[s_], rows.view(torch.uint8).reshape(b - a, 8 * width))
         grace.finish_partitioning()
         t1 = time.perf_counter()
         bname, pname = names[build], names[1 - build]
-        proto = [sides[0][0], sides[1][0]]
         vctx = runner._vertex_ctx(stage, parts[0])
         for b, brows, prows in grace.buckets(bname, pname):
             if brows.shape[0] == 0 or prows.shape[0] == 0:
@@ -432,12 +661,18 @@ def run(desc, runner, lay) -> dict:
             po, bo = GR.hash_join_pairs(brows, prows, 0, 8)
             if po.numel() == 0:
                 continue
-            matches += po.numel()
             oi, ii = (bo, po) if build == 0 else (po, bo)
             orows = (brows if build == 0 else prows).view(_I64).view(-1, width)
             irows = (prows if build == 0 else brows).view(_I64).view(-1, width)
-            a_ = proto[0].table(orows.index_select(0, oi), used[0])
-            b_ = proto[1].table(irows.index_select(0, ii), used[1])
+            if not lay["exact"]:           # hash-keyed: keep the pairs whose key fields are equal
+                keep = _verify(orows, irows, oi, ii, vlay, S)
+                if not bool(keep.all()):
+                    oi, ii = oi[keep], ii[keep]
+                if oi.numel() == 0:
+                    continue
+            matches += oi.numel()
+            a_ = proto[0].table(orows.index_select(0, oi), used[0], S)
+            b_ = proto[1].table(irows.index_select(0, ii), used[1], S)
             data = G._result_table(G._traced(desc["op"]["result"], TR.proxy(a_), TR.proxy(b_)), a_)
             for op in desc["per_bucket"]:
                 data = runner._run_op(op, [data], vctx, stage)
@@ -453,7 +688,9 @@ def run(desc, runner, lay) -> dict:
         grace.release()
     out = sink.finish(V)
     runner.join_stats = dict(spilled_bytes=stats.spilled_bytes, buckets=stats.buckets, resident=stats.resident,
-                             in_hbm=stats.in_hbm, build=names[build], layout=f"{width} x 8-byte words (pruned)",
+                             in_hbm=stats.in_hbm, build=names[build],
+                             layout=f"{width} x 8-byte words (pruned{', strings inline' if strings else ''})",
+                             key="exact" if lay["exact"] else "hashed + verified",
                              matches=matches, partition_s=round(t1 - t0, 4), join_s=round(t2 - t1, 4),
                              written_bytes=sink.written, kind="grace join stage")
     return out
@@ -468,6 +705,7 @@ class _Sink:
         self.agg = desc["agg"]
         self.chunks, self.partials = [], []
         self.writer, self.dtype, self.n, self.written = None, None, 0, 0
+        self.written_bytes, self.index = 0, []          # (string records) block index of the stream
         self.stream = False
         if stage.is_output and not self.agg and not desc["after"]:
             scheme, path, _ = parse_uri(stage.output["uri"])
@@ -487,12 +725,22 @@ class _Sink:
             if self.dtype is None:
                 self.dtype = _table_dtype(data)
             enc = CD.encode(data, self.dtype) if self.dtype is not None else None
+            if enc is None and self.dtype is not None and CD.var_layout(self.dtype) is not None:
+                got = CD.encode_var(data, self.dtype, full_offsets=True)
+                if got is not None:
+                    enc, offs = got
+                    # block index of the concatenated stream: records n, n + B, ... of it
+                    B = CD.BLOCK
+                    j0 = (-self.n) % B
+                    if data.n > j0:
+                        self.index.append(offs[j0::B] + self.written_bytes)
             if enc is not None:
                 if self.writer is None:
                     from ..io.writer import PartWriter
                     self.writer = PartWriter(self.tmp, data.device, self.runner.write_stats)
                 self.writer.write(enc)
                 self.n += data.n
+                self.written_bytes += enc.numel()
                 return
             if self.writer is None:
                 self.stream = False
@@ -538,6 +786,10 @@ class _Sink:
             return out
         if self.writer is not None:
             self.written = self.writer.close()
+            if self.index:
+                from ..io import partfile as PF
+                from ..ops import codec as CD
+                PF.write_index(self.tmp, self.n, self.written, torch.cat(self.index).cpu().numpy(), CD.BLOCK)
             out[parts[0]] = StreamedPart(self.tmp, self.n, self.written, self.dtype)
             self.writer = None
         else:
@@ -568,17 +820,24 @@ class _Sink:
 
 
 def _table_dtype(t: DeviceTable):
-    """Record type of a columnar device table of fixed-width numeric fields (None otherwise)."""
+    """Record type of a columnar device table of fixed-width numeric fields and strings (None
+    otherwise)."""
     from .. import types as T
     m = {torch.int64: T.Int64, torch.int32: T.Int32, torch.int16: T.Int16, torch.uint8: T.Byte, torch.int8: T.SByte,
          torch.bool: T.Bool, torch.float64: T.Float64, torch.float32: T.Float32}
-    if t.rows is not None or t.heap is not None or t.strs:
+    if t.rows is not None or t.heap is not None:
         return None
     fields = list(t.shape.fields)
-    if any(f not in t.cols or t.cols[f].dim() != 1 or t.cols[f].dtype not in m for f in fields):
+
+    def ft(f):
+        if f in t.strs:
+            return T.String
+        return m.get(t.cols[f].dtype) if f in t.cols and t.cols[f].dim() == 1 else None
+    types = [ft(f) for f in fields]
+    if any(x is None for x in types):
         return None
     if t.shape.kind == "scalar" and len(fields) == 1:
-        return m[t.cols[fields[0]].dtype]
+        return types[0]
     if t.shape.kind == "tuple":
-        return T.RecordT([(f"Item{i + 1}", m[t.cols[f].dtype]) for i, f in enumerate(fields)], tuple)
+        return T.RecordT([(f"Item{i + 1}", x) for i, x in enumerate(types)], tuple)
     return None

@@ -42,7 +42,7 @@ def _source(runner, s):
     scheme, path, q = parse_uri(uri)
     if scheme == "gen":
         kind = path.strip("/")
-        if kind in ("terasort", "records64", "range"):
+        if kind in ("terasort", "records64", "range", "names"):
             return kind, dict(q=q, uri=uri)
         return None
     if scheme in ("partfile", "file"):
@@ -64,7 +64,7 @@ def _partition_bytes(kind, info, p) -> int:
         return m.parts[p].size if p < m.count else 0
     from ..io.providers import GenProvider
     lo, hi = GenProvider().bounds(info["uri"], p)
-    per = {"terasort": 100, "records64": 8 * int(info["q"].get("cols", 8)), "range": 8}[kind]
+    per = {"terasort": 100, "records64": 8 * int(info["q"].get("cols", 8)), "range": 8, "names": 32}[kind]
     return (hi - lo) * per
 
 
@@ -150,6 +150,16 @@ def _chunks(plan, p, device, vctx):
             R.gen_records64(cols, a, nk, int(q.get("seed", 0)), dim_multiplier(nk) if q.get("mode") == "dim" else 0)
             names = FIELDS[:ncols]
             yield DeviceTable.from_columns(dict(zip(names, cols)), Shape("tuple", names))
+        return
+    if kind == "names":
+        from ..models import names as NM
+        from ..models.records_cpu import dim_multiplier
+        nk = int(q.get("keys", 1 << 20))
+        per = max(1, chunk // 32)
+        for a in range(lo, hi, per):
+            m = min(per, hi - a)
+            yield NM.device_table(a, m, nk, int(q.get("seed", 0)), dim_multiplier(nk) if q.get("mode") == "dim" else 0,
+                                  device)
         return
     if kind == "range":
         start = int(q.get("start", 0))

@@ -125,3 +125,63 @@ def test_join_to_partfile_recovers_from_a_bucket_failure(tmp_path, monkeypatch):
     parts_dir = str(tmp_path / "jf.pt.parts")
     assert not [f for f in os.listdir(parts_dir) if f.endswith(".tmp")], os.listdir(parts_dir)
     _same(sorted(g.FromStore(uri)), sorted(q(_loc())))
+
+
+NAMES_R = "gen://names?count=200000&partitions={P}&keys=150000&seed=3&mode=dim"
+NAMES_S = "gen://names?count=300000&partitions={P}&keys=150000&seed=4"
+
+
+@pytest.mark.parametrize("stored", [False, True])
+def test_string_key_join_spills_and_streams_to_partfile(tmp_path, stored):
+    """Join on a string key (the device hash of the key bytes, every match verified byte by byte)
+    with the rows spilled past a small budget and string results streamed into the output part
+    file with its block index; the inputs either generated or string-bearing partfile tables
+    decoded on the device."""
+    g = _ctx(budget=6 << 20)
+    r_src, s_src = NAMES_R.format(P=2), NAMES_S.format(P=2)
+    if stored:
+        w = _ctx()
+        r_src, s_src = "partfile://" + str(tmp_path / "r.pt"), "partfile://" + str(tmp_path / "s.pt")
+        w.FromStore(NAMES_R.format(P=2)).ToStore(r_src, delete_if_exists=True).SubmitAndWait()
+        w.FromStore(NAMES_S.format(P=2)).ToStore(s_src, delete_if_exists=True).SubmitAndWait()
+    uri = "partfile://" + str(tmp_path / "js.pt")
+    q = lambda c, a, b: c.FromStore(a).Join(c.FromStore(b), lambda r: r[0], lambda s: s[0],  # noqa: E731
+                                            lambda r, s: (r[0], r[1], s[2]))
+    q(g, r_src, s_src).ToStore(uri, delete_if_exists=True).SubmitAndWait()
+    res, js = _stats(g)
+    assert js.get("kind") == "grace join stage" and js.get("key") == "hashed + verified", js
+    assert js["spilled_bytes"] > 0 and "strings inline" in js["layout"], js
+    assert res["fallbacks"] == [], res["fallbacks"]
+    got = sorted(g.FromStore(uri))
+    exp = sorted(q(_loc(), NAMES_R.format(P=2), NAMES_S.format(P=2)))
+    _same(got, exp)
+    assert len(got) == 300000 and isinstance(got[0][0], str)
+
+
+def test_composite_and_float_key_joins():
+    g = _ctx()
+    R2 = "gen://records64?count=50000&partitions=2&keys=3000&seed=7&cols=3"
+    S2 = "gen://records64?count=70000&partitions=2&keys=3000&seed=8&cols=3"
+    q = lambda c: c.FromStore(R2).Join(c.FromStore(S2), lambda r: (r[0], r[0]), lambda s: (s[0], s[0]),  # noqa
+                                       lambda r, s: (r[0], r[2], s[1]))
+    got = sorted(q(g))
+    res, js = _stats(g)
+    assert js.get("key") == "hashed + verified" and res["fallbacks"] == [], (js, res["fallbacks"])
+    _same(got, sorted(q(_loc())))
+
+
+def test_float_key_join_from_stored_tables(tmp_path):
+    g = _ctx()
+    a, b = "partfile://" + str(tmp_path / "fa.pt"), "partfile://" + str(tmp_path / "fb.pt")
+    g.FromStore("gen://records64?count=40000&partitions=2&keys=500&seed=9&cols=2") \
+        .Select(lambda r: (r[0] * 0.5, r[1])).ToStore(a, delete_if_exists=True).SubmitAndWait()
+    g.FromStore("gen://records64?count=30000&partitions=2&keys=500&seed=10&cols=2") \
+        .Select(lambda r: (r[0] * 0.5, r[1])).ToStore(b, delete_if_exists=True).SubmitAndWait()
+    q = lambda c: c.FromStore(a).Join(c.FromStore(b), lambda r: r[0], lambda s: s[0],  # noqa: E731
+                                      lambda r, s: (r[0], r[1] + s[1]))
+    got = sorted(q(g))
+    res, js = _stats(g)
+    assert js.get("kind") == "grace join stage" and js.get("key") == "exact", js
+    assert res["fallbacks"] == [], res["fallbacks"]
+    loc = _loc()
+    _same(got, sorted(q(loc)))
