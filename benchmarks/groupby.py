@@ -34,6 +34,8 @@ def main():
                     help="run the per-rank program of a W-rank job on this one GPU (runtime/loopback.py): the "
                          "all-to-all-v replaced by running every other source's stage untimed; reports per-rank ms")
     ap.add_argument("--loopback-rank", type=int, default=0)
+    ap.add_argument("--aggregation", choices=("auto", "radix", "sort"), default="auto",
+                    help="GroupByAggregation context property (single integer key strategy)")
     ap.add_argument("--hbm-budget-gb", type=float, default=None,
                     help="HbmBudgetBytes: a partition past it is aggregated chunk by chunk (runtime/stream_agg.py), "
                          "e.g. --records-per-gpu 6.25e9 (400 GB) --hbm-budget-gb 60")
@@ -51,6 +53,7 @@ def main():
     ctx.PartitionCount = w.size
     if a.hbm_budget_gb:
         ctx.HbmBudgetBytes = int(a.hbm_budget_gb * 1e9)
+    ctx.GroupByAggregation = a.aggregation
     n = int(a.records_per_gpu) * w.size
     src = f"gen://records64?count={n}&partitions={w.size}&keys={int(a.keys)}&seed=4242" + \
         ("&bounds=0" if a.no_bounds else "")
@@ -98,7 +101,7 @@ def main():
         "config": {"model": "GroupBy(Key) -> Count/Sum/Min/Max (decomposable, hash shuffle)",
                    "records": n, "record_bytes": 64, "keys": int(a.keys), "parallelism": f"dp{w.size}",
                    "column_bounds": "measured in the step" if a.no_bounds else "declared by the generator",
-                   "hbm_budget_bytes": ctx.HbmBudgetBytes,
+                   "hbm_budget_bytes": ctx.HbmBudgetBytes, "aggregation": a.aggregation,
                    "streamed_aggregation": streamed[0] if streamed else None}})
 
 

@@ -128,6 +128,8 @@ _DEFAULTS = dict(
     #                               stored at a 128-byte pitch (one HBM line per record gather)
     GenFusedShuffle=False,        # multi-rank OrderBy over gen://terasort: generate the records straight
     #                               into the exchange's send rows (no input table; a benchmark variant)
+    GroupByAggregation="auto",    # single-integer-key GroupBy: "auto" (radix aggregation for keys spanning
+    #                               >= 2^32 values), "radix" or "sort" (ops/tuning.py)
     ShuffleSlack=0.01,            # receive-buffer headroom of a range-partitioned exchange
     PersistStageOutputs=None,     # GPU executor: copy completed stage outputs to a checkpoint store so a
     #                               relaunched gang resumes there (None: under a relaunching launcher;

@@ -24,7 +24,6 @@ atomics in arbitrary order.
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 
@@ -41,13 +40,12 @@ _lib.register_signatures({
                              vp]),
 })
 
-# "auto": only for integer keys whose value span is 2^32 or more (there the sort-based GroupBy needs
-# 16-byte entries and is the slower one; measured on MI355X, profiles/README.md); "1": every
-# large single-integer-key GroupBy; "0": never
-MODE = os.environ.get("DRYAD_RADIX_AGG", "auto")
-ENABLED = MODE != "0"
+# When it runs is the job's GroupByAggregation (ops/tuning.py): "auto" only for integer keys whose
+# value span is 2^32 or more (there the sort-based GroupBy needs 16-byte entries and is the slower
+# one; measured on MI355X, profiles/README.md), "radix" for every large single-integer-key
+# GroupBy, "sort" never.
 MIN_ROWS = 1 << 22                 # below this the sort-based path is as fast
-KEYS_PER_PART = int(os.environ.get("DRYAD_RADIX_AGG_KPP", "300"))   # target distinct keys per final
+KEYS_PER_PART = 300                # target distinct keys per final
 #                                  partition (LDS table: up to 1024 slots, 3 per row)
 MIN_BITS = 11                      # >= 2048 partitions: enough workgroups to fill the chip
 MAX_BITS = 24
@@ -160,10 +158,12 @@ def wide_key(key: torch.Tensor) -> bool:
 
 
 def wanted(key: torch.Tensor) -> bool:
-    """Whether the GroupBy operators route this key through radix_aggregate (see MODE)."""
-    if not ENABLED or key.shape[0] < MIN_ROWS or key.dtype not in _INT:
+    """Whether the GroupBy operators route this key through radix_aggregate (GroupByAggregation)."""
+    from .tuning import current
+    mode = current().groupby_aggregation
+    if mode == "sort" or key.shape[0] < MIN_ROWS or key.dtype not in _INT:
         return False
-    return MODE == "1" or wide_key(key)
+    return mode == "radix" or wide_key(key)
 
 
 def radix_aggregate(key: torch.Tensor, specs: list, nd_est: int | None = None, force: bool = False):
@@ -174,7 +174,8 @@ def radix_aggregate(key: torch.Tensor, specs: list, nd_est: int | None = None, f
     n = key.shape[0]
     if key.dim() != 1 or key.dtype not in _INT or n < 2 or n >= (1 << 32):
         return None
-    if not force and (not ENABLED or n < MIN_ROWS):
+    from .tuning import current
+    if not force and (current().groupby_aggregation == "sort" or n < MIN_ROWS):
         return None
     dev = key.device
     k64 = key.to(torch.int64).contiguous()

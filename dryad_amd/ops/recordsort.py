@@ -30,15 +30,14 @@ from ..parallel.comm import World, get_world
 from ..parallel import shuffle
 from . import sort as S
 from . import terasort as TSG
-import os as _os
 
-# local sort algorithm: "hybrid" (top-window LSD + in-LDS run sort, default), "prefix"
-# (64-bit LSD + tie fix-up) or "lsd" (full-width LSD)
-SORT_ALGO = _os.environ.get("DRYAD_SORT_ALGO", "hybrid")
+# local sort algorithm of 16-byte entries: "hybrid" (top-window LSD + in-LDS run sort); the
+# "prefix" (64-bit LSD + tie fix-up) and full-width "lsd" variants remain for tests
+SORT_ALGO = "hybrid"
 # pipelined exchange of the multi-rank sort: key sub-ranges per destination rank (0 = from the
-# data size) and the target bytes per (source, destination) pair and round
-PIPE_SUBS = int(_os.environ.get("DRYAD_SHUFFLE_SUBS", "0"))
-PIPE_ROUND_BYTES = int(_os.environ.get("DRYAD_SHUFFLE_ROUND_BYTES", str(1 << 30)))
+# data size; tests set it) and the target bytes per (source, destination) pair and round
+PIPE_SUBS = 0
+PIPE_ROUND_BYTES = 1 << 30
 _M64 = (1 << 64) - 1
 
 

@@ -233,10 +233,10 @@ _MOPS = {("sum", 0): 0, ("min", 0): 1, ("max", 0): 2, ("count", 0): 3, ("sum", 1
 # into 32- / 40-byte rows (dr_pack_wide) so each sorted entry costs one sector-aligned random read
 # instead of one cache line per column: GroupBy of 1.25e9 rows x 3 columns 249.4 -> 238.7 ms per
 # step (the torch.stack packing tried first cost 47 ms and lost; profiles/README.md)
-AOS_MIN_ROWS = int(os.environ.get("DRYAD_SEGRED_AOS_MIN_ROWS", str(1 << 24)))
+AOS_MIN_ROWS = 1 << 24
 
 
-FUSED_GROUP_KEYS = os.environ.get("DRYAD_FUSED_GROUP_KEYS", "1") == "1"
+FUSED_GROUP_KEYS = True
 
 
 def group_reduce_sorted(srt: torch.Tensor, specs: list, key_xor: int):
@@ -343,7 +343,7 @@ _lib.register_signatures({
 # GroupBy benchmark it measured 260.6 ms against 251.2 ms for the key-pointer sort — the E256
 # scatter passes (26 ms each vs 12 for E128) and their count passes cost more than the random
 # gathers they remove (profiles/README.md)
-PAYLOAD_SORT_MIN_ROWS = int(os.environ.get("DRYAD_PAYLOAD_SORT_MIN_ROWS", str(1 << 62)))
+PAYLOAD_SORT_MIN_ROWS = 1 << 62
 PAYLOAD_SORT_MAX_PASSES = 4
 _PAYLOAD_WORDS = (0, 2, 3, 4)      # payload words of an E256 / E320 entry: lo, p0, p1, p2 (hi = key)
 
@@ -548,7 +548,7 @@ _lib.register_signatures({
 _INT_BITS = {torch.uint8: 8, torch.int8: 8, torch.bool: 8, torch.int16: 16, torch.uint16: 16, torch.int32: 32,
              torch.uint32: 32, torch.int64: 64, torch.uint64: 64}
 _SIGNED = {torch.int8, torch.int16, torch.int32, torch.int64}
-INT_KEY_SORT = os.environ.get("DRYAD_INT_KEY_SORT", "1") == "1"
+INT_KEY_SORT = True
 
 
 def _norm_int(v: int, dtype) -> int:

@@ -92,8 +92,7 @@ def hi_range(entries: torch.Tensor) -> tuple[int, int]:
 _M64 = (1 << 64) - 1
 # expected run length the segmented phase is sized for (window = smallest multiple of 8 bits with
 # n / 2^window <= RUN_TARGET); overridable for tuning
-import os as _os  # noqa: E402
-RUN_TARGET = int(_os.environ.get("DRYAD_SORT_RUN_TARGET", "16"))
+RUN_TARGET = 16
 
 
 def _mask_words(begin_bit: int, end_bit: int) -> tuple[int, int]:
@@ -267,8 +266,8 @@ _lib.register_signatures({
 })
 # expected entries per run the compact sort sizes its window for (window = smallest multiple of 8
 # bits, at most 32, with n <= RUN_TARGET64 * 2^window)
-RUN_TARGET64 = float(_os.environ.get("DRYAD_SORT64_RUN_TARGET", "1"))
-COMPACT_SORT = _os.environ.get("DRYAD_COMPACT_SORT", "1") == "1"
+RUN_TARGET64 = 1.0
+COMPACT_SORT = True
 
 
 def common_prefix_bits(mn: int, mx: int) -> int:

@@ -10,20 +10,18 @@ Reference mapping:
   * R4 aggregation trees -> all-reduce (dense) or all-to-all + local combine (sparse keys).
   * R5 sampler gather -> all-gather of the samples.
 
-Large exchanges are issued in chunks (``DRYAD_SHUFFLE_CHUNK_BYTES``, default 4 GiB per peer per
-round) so that RCCL's internal staging and the int32 limits of some code paths are never hit and
+Large exchanges are issued in chunks (``CHUNK_BYTES``, 4 GiB per peer per round) so that RCCL's internal staging and the int32 limits of some code paths are never hit and
 so a later version can overlap the next chunk's pack kernel with the current transfer.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.distributed as dist
 
 from .comm import World, get_world
 
-CHUNK_BYTES = int(os.environ.get("DRYAD_SHUFFLE_CHUNK_BYTES", str(4 << 30)))
+CHUNK_BYTES = 4 << 30         # per (source, destination) pair and round (tests shrink it)
 
 
 def exchange_counts(send_counts: torch.Tensor, world: World | None = None) -> torch.Tensor:

@@ -1909,8 +1909,10 @@ class GpuExecutor(_BaseExecutor):
             runner.job_dir_factory = lambda: self._rank_job_dir(plan)    # restart records of rank > 0
         t0 = time.time()
         res = None
+        from ..ops import tuning
         try:
-            res = runner.run()
+            with tuning.scope(self.ctx):          # the job's operator strategies (context properties)
+                res = runner.run()
         except BaseException as e:
             if job_dir:
                 os.makedirs(os.path.join(job_dir, "log"), exist_ok=True)

@@ -65,7 +65,7 @@ def test_streamed_partial_side_of_a_two_partition_groupby():
     streams, the folded partials go through the exchange and the final GroupBy."""
     src = SRC.format(n=400_000, P=2, k=50_000)
     q = lambda c: c.FromStore(src).GroupBy(lambda r: r[0], lambda k, g: (k, g.Count(), g.Sum(lambda r: r[1])))  # noqa
-    g = _ctx(P=2)
+    g = _ctx(P=2, budget=8 << 20)             # each partition (12.8 MB) past the budget
     got = sorted(q(g))
     res, st = _stats(g)
     assert len(st) == 2 and all(x["chunks"] > 4 for x in st), st
