@@ -57,24 +57,30 @@ class WriteStats:
 
 class PartWriter:
     """Append device (or host) byte tensors to a new file; ``close()`` returns the byte count.
-    One writer per process at a time owns the ring (``with PartWriter(...) as w``)."""
+    One writer per process at a time owns the ring (``with PartWriter(...) as w``).  ``path`` may
+    be a list of paths: ``write(data, file=i)`` then appends to file i (a streamed partitioning
+    stage writes every output partition at once; ``close()`` returns the byte counts)."""
 
-    def __init__(self, path: str, device=None, stats: WriteStats | None = None):
+    def __init__(self, path, device=None, stats: WriteStats | None = None):
         from ..native import runtime
+        self.multi = isinstance(path, (list, tuple))
         self.path = path
         self.stats = stats
         self.t0 = time.perf_counter()
         self.ring = _ring()
         _RING_LOCK.acquire()
         try:
-            self.w = runtime().ChunkWriter(path, [b.tensor.data_ptr() for b in self.ring], THREADS, mapped=MAPPED)
+            ptrs = [b.tensor.data_ptr() for b in self.ring]
+            self.w = runtime().ChunkWriter(list(path), ptrs, THREADS) if self.multi else \
+                runtime().ChunkWriter(path, ptrs, THREADS, mapped=MAPPED)
         except Exception:
             _RING_LOCK.release()
             raise
         self.dev = torch.device(device) if device is not None else None
         self.cs = torch.cuda.Stream(self.dev) if self.dev is not None and self.dev.type == "cuda" else None
         self.off = 0
-        self.pending = deque()           # (slot, event, file offset, bytes): D2H copies in flight
+        self.offs = [0] * (len(path) if self.multi else 1)
+        self.pending = deque()           # (slot, event, file offset, bytes, file): D2H copies in flight
         self.closed = False
 
     def __enter__(self):
@@ -88,13 +94,14 @@ class PartWriter:
 
     def _submit_done(self, block: bool):
         while self.pending and (block or self.pending[0][1] is None or self.pending[0][1].query()):
-            slot, ev, off, n = self.pending.popleft()
+            slot, ev, off, n, f = self.pending.popleft()
             if ev is not None:
                 ev.synchronize()
-            self.w.submit(slot, off, n)
+            self.w.submit(slot, off, n, f)
 
-    def write(self, data) -> None:
-        """Append ``data``: a contiguous device or host tensor (its bytes), or a bytes-like object."""
+    def write(self, data, file: int = 0) -> None:
+        """Append ``data`` (to file ``file`` of a multi-file writer): a contiguous device or host
+        tensor (its bytes), or a bytes-like object."""
         from ..ops import _lib
         if not isinstance(data, torch.Tensor):
             data = torch.frombuffer(bytearray(data), dtype=torch.uint8) if len(data) else torch.empty(0, dtype=torch.uint8)
@@ -124,34 +131,38 @@ class PartWriter:
             else:
                 ctypes.memmove(dst.data_ptr(), flat[a:a + m].data_ptr(), m)
                 ev = None
-            self.pending.append((slot, ev, self.off, m))
+            self.pending.append((slot, ev, self.offs[file], m, file))
+            self.offs[file] += m
             self.off += m
 
     def _submit_oldest(self):
-        slot, ev, off, n = self.pending.popleft()
+        slot, ev, off, n, f = self.pending.popleft()
         if ev is not None:
             ev.synchronize()
-        self.w.submit(slot, off, n)
+        self.w.submit(slot, off, n, f)
 
-    def close(self) -> int:
+    def close(self):
         if self.closed:
-            return self.off
+            return list(self.offs) if self.multi else self.off
         try:
             self._submit_done(block=True)
-            self.w.finish(self.off)
+            if self.multi:
+                self.w.finish_all(list(self.offs))
+            else:
+                self.w.finish(self.off)
         finally:
             self.closed = True
             _RING_LOCK.release()
         if self.stats is not None:
             self.stats.bytes += self.off
             self.stats.seconds += time.perf_counter() - self.t0
-        return self.off
+        return list(self.offs) if self.multi else self.off
 
     def abort(self):
         if self.closed:
             return
         try:
-            for _, ev, _, _ in self.pending:
+            for _, ev, _, _, _ in self.pending:
                 if ev is not None:
                     ev.synchronize()
             self.pending.clear()

@@ -170,6 +170,7 @@ class GpuJobRunner:
         self.moved: dict = {}             # (stage, partition) -> rank whose duplicate attempt won
         self.stream_plans: dict = {}      # stage -> chunk plan of a streamed stage (None: not streamed)
         self.agg_plans: dict = {}         # stage -> plan of a streamed (out-of-core) GroupBy / Distinct
+        self.part_stream_plans: dict = {}  # stage -> plan of a streamed HashPartition -> ToStore
         self.empty_host_ops: list = []    # host operators that ran over empty inputs only
         self.stream_stats: dict = {}      # (stage, partition) -> chunks / records / bytes streamed
         self.place = None                 # partition -> rank (None: p % W)
@@ -877,6 +878,8 @@ class GpuJobRunner:
     def _merge_streams(self, si, streams):
         if not streams:
             return None
+        if len(streams) == 1 and isinstance(streams[0], GS.StreamedPart):
+            return streams[0]            # a part file a streamed producer already wrote
         if all(isinstance(x, DeviceTable) for x in streams):
             return DeviceTable.concat(streams)
         objs = [x if isinstance(x, list) else _to_objects(x) for x in streams]
@@ -904,6 +907,17 @@ class GpuJobRunner:
                 raise ChannelReadError(self.edge_ids[(self.vids[s.inputs[0].src][q], self.vids[s.id][p], 0)],
                                        f"injected read error on the channel {s.inputs[0].src}[{q}] -> {s.id}[{p}]")
         vctx = GpuVertexContext(p, s.partitions, self.vids[s.id][p], version, s, self.dev, self.world, self)
+        if s.id not in self.part_stream_plans:
+            self.part_stream_plans[s.id] = ST.partition_plan(self, s)
+        if self.part_stream_plans[s.id] is not None:
+            # read -> record-wise ops -> HashPartition -> ToStore(partfile) on one rank: every chunk's
+            # ports appended to the output partitions' part files (runtime/streaming.py)
+            try:
+                with TRC.range(f"vertex {s.id}:{s.name}[{p}] v{version} (streamed partition)"):
+                    return ST.run_partitioned(self, s, p, version, vctx, self.part_stream_plans[s.id])
+            except ST.NotStreamable as e:
+                log.info("%s: streamed partitioning declined (%s)", s.name, e)
+                self.part_stream_plans[s.id] = None
         if s.id not in self.agg_plans:
             self.agg_plans[s.id] = SA.plan(self, s)
         if self.agg_plans[s.id] is not None:
@@ -930,6 +944,8 @@ class GpuJobRunner:
                 raise VertexCrash(f"injected crash of {s.name}[{p}] v{version} (output discarded)")
             return out
         inputs = [self._merge_streams(si, streams) for si, streams in zip(s.inputs, raw_inputs)]
+        if len(s.ops) == 1 and s.ops[0]["op"] == "output" and len(inputs) == 1 and isinstance(inputs[0], GS.StreamedPart):
+            return inputs[0]             # the output stage of a streamed partitioning: committed by rename
         data = None
         with TRC.range(f"vertex {s.id}:{s.name}[{p}] v{version}"):
             for i, op in enumerate(s.ops):

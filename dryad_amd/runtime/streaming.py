@@ -227,3 +227,80 @@ def run(runner, s, p, version, vctx, plan, cancel=None):
             chunks += 1
     runner.stream_stats[(s.id, p)] = dict(chunks=chunks, records=n, bytes=w.off)
     return StreamedPart(tmp, n, w.off, dtype, rows=rows_fmt)
+
+
+def partition_plan(runner, s):
+    """``read -> (Select | Where)* -> HashPartition -(cross)-> ToStore(partfile)`` over one source
+    partition on one rank: the chunks' ports stream straight into the output's part files (one
+    multi-file writer), so the partition never has to fit in HBM.  None when not applicable."""
+    if not runner.gpu_ok or runner.world.size != 1 or s.inputs or s.partitions != 1 or len(s.ops) < 2:
+        return None
+    if s.ops[-1]["op"] != "hash_partition" or any(o["op"] not in STREAM_OPS for o in s.ops[1:-1]):
+        return None
+    if s.id in runner.skipped or s.id in runner.gang_stages:
+        return None
+    cons = runner.plan.consumers(s.id)
+    if len(cons) != 1:
+        return None
+    B = runner.plan.stages[cons[0]]
+    if [o["op"] for o in B.ops] != ["output"] or not B.is_output or len(B.inputs) != 1 or B.inputs[0].kind != "cross":
+        return None
+    if parse_uri(B.output["uri"])[0] not in ("partfile", "file") or runner.ctx.OutputDataCompressionScheme.value != 0:
+        return None
+    src = _source(runner, s)
+    if src is None:
+        return None
+    props = runner.ctx._props
+    chunk = int(props.get("StreamChunkBytes") or DEFAULT_CHUNK_BYTES)
+    if not props.get("StreamStages") and _partition_bytes(src[0], src[1], 0) <= chunk:
+        return None
+    return dict(kind=src[0], info=src[1], chunk=chunk, out_stage=B)
+
+
+def run_partitioned(runner, s, p, version, vctx, plan):
+    """Stream partition p of stage s through its HashPartition into the output stage's part
+    files -> [StreamedPart per output partition] (the cross edge hands port k to partition k)."""
+    from ..io import partfile as PF
+    from ..io import writer as WR
+    from .grace_stage import StreamedPart, _table_dtype
+    from .. import types as T
+    B = plan["out_stage"]
+    nparts = B.partitions
+    _, path, _ = parse_uri(B.output["uri"])
+    base = PF.default_base(path)
+    os.makedirs(os.path.dirname(base) or ".", exist_ok=True)
+    paths = [f"{PF.tmp_part_path(base, k, runner.vids[B.id][k], 0, version)}.stream" for k in range(nparts)]
+    dtype = None if B.dtype in (None, T.Pickle) else B.dtype
+    counts, rows_fmt, chunks = [0] * nparts, None, 0
+    w = WR.PartWriter(paths, vctx.device, runner.write_stats)
+    try:
+        for t in _chunks(plan, p, vctx.device, vctx):
+            data = t
+            for op in s.ops[1:]:
+                data = runner._run_op(op, [data], vctx, s)
+            for k in range(nparts):
+                piece = data.port(k)
+                if piece is None or (hasattr(piece, "n") and piece.n == 0):
+                    continue
+                is_rows = isinstance(piece, DeviceTable) and piece.rows is not None and piece.shape.kind == "rows"
+                if dtype is None and not is_rows:
+                    dtype = _table_dtype(piece) if isinstance(piece, DeviceTable) else None
+                    if dtype is None:
+                        raise NotStreamable(f"{s.name}: no fixed record layout to stream")
+                b, rf = _encode(piece, dtype)
+                rows_fmt = rows_fmt or rf
+                w.write(b, file=k)
+                counts[k] += piece.n if isinstance(piece, DeviceTable) else len(piece)
+            chunks += 1
+        sizes = w.close()
+    except BaseException:
+        w.abort()
+        for f in paths:
+            try:
+                os.remove(f)
+            except OSError:
+                pass
+        raise
+    runner.stream_stats[(s.id, p)] = dict(chunks=chunks, records=sum(counts), bytes=sum(sizes), ports=nparts,
+                                          kind="streamed partition to store")
+    return [StreamedPart(paths[k], counts[k], sizes[k], dtype, rows=rows_fmt) for k in range(nparts)]

@@ -71,3 +71,29 @@ def test_streamed_partial_side_of_a_two_partition_groupby():
     assert len(st) == 2 and all(x["chunks"] > 4 for x in st), st
     assert res["fallbacks"] == [], res["fallbacks"]
     assert got == sorted(q(_loc()))
+
+
+def test_streamed_hash_partition_to_store(tmp_path):
+    """One source partition far past the chunk size, HashPartition(4) -> ToStore(partfile): every
+    chunk's ports appended to the four output part files at once (one multi-file writer), each
+    output partition holding exactly the records the host partitioner sends there."""
+    from dryad_amd.io.providers import provider_for
+    src = SRC.format(n=300_000, P=1, k=10_000)
+    uri = "partfile://" + str(tmp_path / "hp.pt")
+    g = _ctx()
+    g.FromStore(src).Where(lambda r: r[2] % 3 != 0).HashPartition(lambda r: r[0], 4) \
+        .ToStore(uri, delete_if_exists=True).SubmitAndWait()
+    res = g._get_executor().last_result
+    st = [v for v in (res.get("streamed") or {}).values() if v.get("kind") == "streamed partition to store"]
+    assert st and st[0]["chunks"] > 4 and st[0]["ports"] == 4, res.get("streamed")
+    assert res["fallbacks"] == [], res["fallbacks"]
+    loc = _loc()
+    exp_uri = "partfile://" + str(tmp_path / "hp_exp.pt")
+    loc.FromStore(src).Where(lambda r: r[2] % 3 != 0).HashPartition(lambda r: r[0], 4) \
+        .ToStore(exp_uri, delete_if_exists=True).SubmitAndWait()
+    prov = provider_for(uri)
+    dt = (prov.schema(uri) or {}).get("dtype")
+    for k in range(4):
+        got = sorted(prov.read_partition(uri, k, dt))
+        exp = sorted(prov.read_partition(exp_uri, k, dt))
+        assert got == exp and got, (k, len(got), len(exp))
