@@ -467,8 +467,18 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     for b in range(B):
         off.append(off[-1] + sum(rc[s][b] for s in range(W)))
     n_recv = off[-1]
-    _check_capacity(n_recv, bufs.capacity, w)
-    recv_rows = bufs.recv_rows()
+    # a rank whose key ranges outgrow its buffers (skew past ShuffleSlack, e.g. runs of equal keys
+    # kept together) receives into buffers of its own when HBM allows; the vote below stops every
+    # rank cleanly when it does not
+    rb, n_sent = bufs, n
+    if n_recv > bufs.capacity:
+        try:
+            rb = SortBuffers.allocate(n_recv, rec, bufs.rows_out.device)
+            n_sent = 0                      # the output no longer overlays the send rows
+        except Exception:  # noqa: BLE001 (out of HBM: the capacity vote reports it)
+            rb = bufs
+    _check_capacity(n_recv, rb.capacity, w)
+    recv_rows = rb.recv_rows()
     send_flat, recv_flat = bufs.rows_out.view(-1), recv_rows.view(-1)
     ev = {}
     if stats is not None and bufs.rows_out.is_cuda:
@@ -489,9 +499,9 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
             ev["arrive"][b].record()
     sent_after = [st[(b + 1) * W] for b in range(B)]
     if fine is not None:
-        out = merge_received_rounds(bufs, off, fine, L, fb, B, w.rank, sent_after, n, wait=wait)
+        out = merge_received_rounds(rb, off, fine, L, fb, B, w.rank, sent_after, n_sent, wait=wait)
     else:
-        out = sort_received_rounds(bufs, off, sent_after, n, seps_hi, B, w.rank, key_off, key_len, wait=wait)
+        out = sort_received_rounds(rb, off, sent_after, n_sent, seps_hi, B, w.rank, key_off, key_len, wait=wait)
     if ev:
         ev["done"].record()
     if fine_rows and int(bad.item()):

@@ -326,6 +326,8 @@ class GpuJobRunner:
                     ok = kind == "bytes" and spec.length <= 12 and not f["desc"]
                 except Exception:  # noqa: BLE001
                     ok = False
+                if not ok:
+                    spec = None
         votes = [None] * self.world.size
         if self.world.size > 1:
             dist.all_gather_object(votes, (bool(ok), None if spec is None else (spec.off, spec.length)))

@@ -6,8 +6,9 @@ share one GPU (gloo transport; run by tests/test_gpu_multirank.py):
   * an hbm:// input table (read in place, sorted into a buffer set of its own) and a partfile://
     table of raw rows, both validated;
   * skew: all keys equal with the ties kept (OrderBy(k).GroupBy(k)), so one rank's key range
-    overflows its buffer: every rank stops at the voted capacity check within seconds, instead of
-    blocking in the exchange until the collective timeout;
+    overflows its buffer: it receives into larger buffers of its own, and without HBM for them
+    every rank stops at the voted capacity check within seconds, instead of blocking in the
+    exchange until the collective timeout;
   * heavy duplication with ties split: the fine cut would overflow, the E128 path splits the run.
 """
 import os
@@ -56,7 +57,7 @@ def main():
             v = job.validate(*expect)
             assert v["ok"], (w.rank, gen_fused, v)
         ex = job.executor_report()["exchange"]
-        want = "records generated into the send rows" if gen_fused else "over the table (pitch 128)"
+        want = "records generated into the send rows" if gen_fused else "fine-bucket exchange over the table"
         assert ex is not None and want in ex["path"], ex
         assert ex["rounds"] == len(ex["round_send_MB"]) and ex["send_GB"] > 0, ex
     # 2. an hbm:// table (a previous job's output) read in place, and a stored partfile of rows
@@ -83,32 +84,43 @@ def main():
     assert v["ok"], (w.rank, v)
     assert "pitch 128" in (st.ctx._get_executor().last_result["exchange"] or {}).get("path", ""), \
         st.ctx._get_executor().last_result["exchange"]
-    # 3. skew past capacity with the ties kept: a voted, non-retryable stop within seconds
+    # 3. skew past capacity with the ties kept: the overflowing rank receives into buffers of its
+    # own; when HBM cannot hold them, a voted, non-retryable stop within seconds on every rank
     ts = f"gen://terasort?records={200_000 * w.size}&partitions={w.size}&seed=5"
     bufs = RS.SortBuffers.allocate(200_000, 100, w.device, slack=0.01)
+    TS.generate(bufs.rows_in[:200_000], w.rank * 200_000, 5)
+    bufs.rows_in[:200_000, :10] = 42
+    acc_in = TS.check(bufs.rows_in[:200_000]).clone()
+    st3 = RS.SortStats()
+    out = RS.distributed_sort_rows(bufs, 200_000, 0, 10, w, split_ties=False, stats=st3)
+    tot = torch.stack([acc_in[0], TS.check(out)[0], torch.tensor(out.shape[0], device=w.device)])
+    shuffle.all_reduce_(tot, "sum", w)
+    assert int(tot[0]) == int(tot[1]) and int(tot[2]) == 200_000 * w.size, tot.tolist()
+    assert st3.n_out in (0, 200_000 * w.size), st3.n_out          # the one run of equal keys on one rank
+    real = RS.SortBuffers.allocate
+
+    def no_hbm(*a, **k):
+        raise torch.cuda.OutOfMemoryError("injected: no HBM for a larger receive buffer")
+    RS.SortBuffers.allocate = staticmethod(no_hbm)
     TS.generate(bufs.rows_in[:200_000], w.rank * 200_000, 5)
     bufs.rows_in[:200_000, :10] = 42
     t0 = time.perf_counter()
     try:
         RS.distributed_sort_rows(bufs, 200_000, 0, 10, w, split_ties=False)
-        raise AssertionError("an overflowing key range must stop the sort")
+        raise AssertionError("an overflowing key range without HBM to grow must stop the sort")
     except D.errors.GangAgreementError as e:
         assert not e.retryable and "range partition skew" in str(e), e
+    finally:
+        RS.SortBuffers.allocate = real
     assert time.perf_counter() - t0 < 10, time.perf_counter() - t0
     # ... and through the query API: OrderBy(k).GroupBy(k) keeps ties (the GroupBy elides its
     # shuffle); bytes 10..13 of every gen://terasort record are equal (00 11 '0' '0'), so one rank
-    # would receive every row: the job fails cleanly on every rank at the vote
+    # receives every row and grows its buffers: one group, oracle-equal
     qctx = D.DryadLinqContext(platform="gpu")
     qctx.PartitionCount = w.size
     k = lambda r: r[10:14]  # noqa: E731
-    t0 = time.perf_counter()
-    try:
-        list(qctx.FromStore(ts).OrderBy(k).GroupBy(k, lambda kk, gr: (kk, gr.Count())))
-        raise AssertionError("the skewed job must fail")
-    except D.errors.DryadLinqJobException as e:
-        assert "range partition skew" in str(e) + str(getattr(e, "inner", "")), e
-    dt = time.perf_counter() - t0
-    assert dt < 10, dt
+    got = list(qctx.FromStore(ts).OrderBy(k).GroupBy(k, lambda kk, gr: (kk, gr.Count())))
+    assert [(bytes(a), c) for a, c in got] == [(b"\x00\x11" + b"00", 200_000 * w.size)], got
     # 4. every key equal with ties split: the E128 path spreads the run over the ranks
     TS.generate(bufs.rows_in[:200_000], w.rank * 200_000, 5)
     bufs.rows_in[:200_000, :10] = 42
