@@ -928,6 +928,11 @@ def op_group_partial(op, inputs, v):
         nd, m = R.estimate_distinct(kcols[0])
         from ..ops.radixagg import distinct_upper_estimate
         nd_est = distinct_upper_estimate(nd, m, t.n)
+        if v.partitions > 1 and op.get("adaptive", True) and nd_est >= RAW_PARTIAL_FRACTION * t.n:
+            # almost every key distinct: folding would barely shrink the rows the shuffle moves
+            # but cost a full aggregation pass (8-rank GroupBy, 2^30 keys per 1.25e9 rows: 173 vs
+            # 104 ms per rank, profiles/r5/gb_lb8_*.log): the rows go out as a raw partial table
+            return _raw_partial(d, t, kcols[0], form)
         if nd <= R.HASH_AGG_MAX_KEYS and nd * 8 < m:
             got = R.hash_aggregate(kcols[0], specs)
             if got is not None:
@@ -982,13 +987,21 @@ def _accumulate_partials(t, d):
                                            for v in _key_values(t, nkeys)), t)
     specs = []
     for j, a in enumerate(d.aggs):
-        col = t.cols[f"a{j}"]
-        if a.kind in ("count", "sum"):
+        col = t.cols.get(f"a{j}")
+        if a.kind == "count":
+            # int8 counts are the ones of a raw partial (_raw_partial; a folded partial's counts are
+            # int64, and a mix of both arrives promoted): count the rows instead of summing them,
+            # one value column less for the packed aggregation rows
+            implicit = col is None or col.dtype == torch.int8
+            specs.append(("count", None, torch.int64) if implicit else ("sum", col, torch.int64))
+        elif a.kind == "sum":
             specs.append(("sum", col, col.dtype))
         elif a.kind in ("min", "max"):
             specs.append((a.kind, col, col.dtype))
         elif a.kind == "avg":
-            specs += [("sum", col, torch.float64), ("sum", t.cols[f"c{j}"], torch.int64)]
+            c = t.cols.get(f"c{j}")
+            specs += [("sum", col, torch.float64),
+                      ("count", None, torch.int64) if c is None or c.dtype == torch.int8 else ("sum", c, torch.int64)]
         elif a.kind in ("any", "all"):
             specs.append(("max" if a.kind == "any" else "min", col, torch.int64))
     got = _dense_groups(kcols, skeys, specs, t.n)
@@ -1020,13 +1033,41 @@ def combine_partials(t, d):
         out[f"a{j}"] = next(res)
         if a.kind == "avg":
             out[f"c{j}"] = next(res)
-    meta = t.shape.pytype
+    m = t.shape.pytype
+    meta = PartialMeta(m.nkeys, m.kinds, m.key_form)      # folded: the standard (not raw) layout
     for j, a in enumerate(d.aggs):         # min / max / any / all keep the partial table's dtypes
-        col = t.cols[f"a{j}"]                # (sums and counts stay widened: no overflow on the way)
-        if out[f"a{j}"].dtype != col.dtype and a.kind in ("min", "max", "any", "all"):
+        col = t.cols.get(f"a{j}")            # (sums and counts stay widened: no overflow on the way)
+        if col is not None and out[f"a{j}"].dtype != col.dtype and a.kind in ("min", "max", "any", "all"):
             out[f"a{j}"] = out[f"a{j}"].to(col.dtype)
     tb = DeviceTable.from_columns(out, Shape("partial", list(out), meta))
     return tb
+
+
+# estimated distinct keys / rows above which a multi-partition GroupBy's partial step ships raw rows
+RAW_PARTIAL_FRACTION = 0.5
+
+
+def _raw_partial(d, t, key, form):
+    """A partial table of one row per record, in the standard partial layout: the key column and
+    each aggregate's value column as they are, counts as int8 ones (the final step sums them
+    into int64; a rank whose partial did fold sends int64 counts and the exchange promotes).
+    Ranks may decide differently, so the layout must not differ from a folded partial."""
+    out = {"k0": key}
+    ones = None
+    for j, a in enumerate(d.aggs):
+        val = _agg_value(a, t)
+        if a.kind in ("count", "avg") and (val is None or a.kind == "avg"):
+            if ones is None:
+                ones = torch.ones(t.n, dtype=torch.int8, device=t.device)
+        if a.kind == "count":
+            out[f"a{j}"] = ones if val is None else val
+        elif a.kind == "avg":
+            out[f"a{j}"] = val.to(torch.float64)
+            out[f"c{j}"] = ones
+        else:
+            out[f"a{j}"] = val
+    meta = PartialMeta(1, tuple(a.kind for a in d.aggs), form)
+    return DeviceTable.from_columns(out, Shape("partial", list(out), meta))
 
 
 def op_group_final(op, inputs, v):
@@ -1044,9 +1085,11 @@ def final_reduce(t, d):
     keys, nseg, res = _accumulate_partials(t, d)
     vals = []
     for j, a in enumerate(d.aggs):
-        col = t.cols[f"a{j}"]
+        col = t.cols.get(f"a{j}")
         r = next(res)
-        if a.kind in ("count", "sum", "min", "max"):
+        if col is None:                      # a raw partial's implicit count
+            vals.append(r)
+        elif a.kind in ("count", "sum", "min", "max"):
             vals.append(r if col.dtype in (torch.int64, torch.float64) else r.to(col.dtype))
         elif a.kind == "avg":
             vals.append(r / next(res).to(torch.float64))

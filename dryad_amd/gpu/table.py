@@ -47,10 +47,13 @@ class PartialMeta:
     """Layout of a device GroupBy partial-aggregate table: key columns k0..k{nkeys-1} then the
     accumulator columns of each aggregate (a{j}, plus c{j} for averages).  Only plain data, so
     the shape pickles across ranks.  ``key_form`` = "single" | "tuple" (how the host path
-    represents the group key)."""
+    represents the group key).  ``raw``: one row per input record, not aggregated (the partial
+    step found almost every key distinct and skipped the fold, gpu/ops.op_group_partial): a count
+    without a predicate and an average's count are implicit (1 per row) and have no column."""
     nkeys: int
     kinds: tuple
     key_form: str = "single"
+    raw: bool = False
 
 
 class DeviceTable:
@@ -261,10 +264,11 @@ def _partial_objects(meta: PartialMeta, arrs: dict) -> list:
     keys = [arrs[f"k{i}"].tolist() for i in range(meta.nkeys)]
     kv = keys[0] if meta.nkeys == 1 and meta.key_form == "single" else list(zip(*keys))
     accs = []
+    n = len(keys[0]) if keys else 0
     for j, kind in enumerate(meta.kinds):
-        a = arrs[f"a{j}"].tolist()
+        a = arrs[f"a{j}"].tolist() if f"a{j}" in arrs else [1] * n            # raw: implicit count
         if kind == "avg":
-            accs.append(list(zip(a, arrs[f"c{j}"].tolist())))
+            accs.append(list(zip(a, arrs[f"c{j}"].tolist() if f"c{j}" in arrs else [1] * n)))
         elif kind in ("any", "all"):
             accs.append([bool(x) for x in a])
         else:

@@ -25,7 +25,7 @@ def _shape_json(sh):
     from ..gpu.table import PartialMeta
     py = sh.pytype
     if isinstance(py, PartialMeta):
-        pyj = {"partial": [py.nkeys, list(py.kinds), py.key_form]}
+        pyj = {"partial": [py.nkeys, list(py.kinds), py.key_form, bool(getattr(py, "raw", False))]}
     elif py is None:
         pyj = None
     elif isinstance(py, type):
@@ -42,7 +42,8 @@ def _shape_from(d):
     pj = d.get("pytype")
     py = None
     if pj and "partial" in pj:
-        py = PartialMeta(pj["partial"][0], tuple(pj["partial"][1]), pj["partial"][2])
+        py = PartialMeta(pj["partial"][0], tuple(pj["partial"][1]), pj["partial"][2],
+                         bool(pj["partial"][3]) if len(pj["partial"]) > 3 else False)
     elif pj and "class" in pj:
         py = T._lookup_class(pj["class"])
         if py is None and pj["class"] in ("builtins:str",):

@@ -102,3 +102,21 @@ def test_streamed_hash_partition_to_store(tmp_path):
             where = {x: j for j, e in enumerate(exps) for x in e}
             moved = [(x, where.get(x)) for x in gots[k][:5]]
             raise AssertionError(f"partition {k}: {len(gots[k])} vs {len(exps[k])} records; e.g. {moved}")
+
+
+@pytest.mark.parametrize("keys", [10_000_000, 5_000])
+def test_groupby_partial_step_ships_raw_rows_when_keys_are_distinct(keys):
+    """A multi-partition GroupBy whose partial step finds almost every key distinct ships the rows
+    as a raw partial table (no fold, counts as int8 ones) and the final step aggregates them;
+    with few keys it folds as before.  Oracle-equal either way, no host fallbacks."""
+    src = SRC.format(n=400_000, P=2, k=keys)
+    q = lambda c: c.FromStore(src).GroupBy(lambda r: r[0], lambda k, g: (  # noqa: E731
+        k, g.Count(), g.Sum(lambda r: r[1]), g.Min(lambda r: r[2]), g.Max(lambda r: r[3]), g.Average(lambda r: r[4])))
+    g = D.DryadLinqContext(platform="gpu")
+    g.PartitionCount = 2
+    got = sorted(q(g))
+    assert g._get_executor().last_result["fallbacks"] == []
+    exp = sorted(q(_loc()))
+    assert len(got) == len(exp)
+    for a, b in zip(got, exp):
+        assert a[:5] == b[:5] and abs(a[5] - b[5]) <= 1e-9 * max(1.0, abs(b[5])), (a, b)
