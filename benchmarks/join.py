@@ -33,6 +33,12 @@ def main():
     ap.add_argument("--to-store", default=None,
                     help="partfile:// output: time R.Join(S, ..., (r, s) => (r.Key, r.V1, s.V1)).ToStore(uri) instead "
                          "of the Sum (the general grace join stage, pairs streamed bucket by bucket to the part files)")
+    ap.add_argument("--names", action="store_true",
+                    help="string keys: both tables are gen://names (Name = \"u\" + decimal(Key), V1, V2 from the same "
+                         "generator), joined on Name; with --to-store the result is (r.V2, r.V1, s.V1), so the "
+                         "validation of the integer-key join applies unchanged")
+    ap.add_argument("--string-bytes", type=int, default=24,
+                    help="GraceJoinStringBytes: inline bytes per string field in the packed bucket rows")
     a = ap.parse_args()
     w = world()
     import dryad_amd as D
@@ -45,8 +51,14 @@ def main():
     ctx.PartitionCount = w.size
     if budget is not None:
         ctx.HbmBudgetBytes = budget
-    R = f"gen://records64?count={rows}&partitions={w.size}&keys={rows}&seed={SEED_R}&mode=dim"
-    S = f"gen://records64?count={rows}&partitions={w.size}&keys={rows}&seed={SEED_S}"
+    if a.to_store:
+        ctx.PartFileSplitBytes = 1 << 30      # a rank's output partition over 8 part files at once
+    gen = "names" if a.names else "records64"
+    R = f"gen://{gen}?count={rows}&partitions={w.size}&keys={rows}&seed={SEED_R}&mode=dim"
+    S = f"gen://{gen}?count={rows}&partitions={w.size}&keys={rows}&seed={SEED_S}"
+    if a.names:
+        ctx.GraceJoin = True
+        ctx.GraceJoinStringBytes = a.string_bytes
 
     def api_step():
         total = ctx.FromStore(R).Join(ctx.FromStore(S), lambda r: r[0], lambda s: s[0],
@@ -54,7 +66,8 @@ def main():
         return [ctx._get_executor().last_result["join"]["matches"], total]
 
     def store_step():
-        ctx.FromStore(R).Join(ctx.FromStore(S), lambda r: r[0], lambda s: s[0], lambda r, s: (r[0], r[1], s[1])) \
+        sel = (lambda r, s: (r[2], r[1], s[1])) if a.names else (lambda r, s: (r[0], r[1], s[1]))
+        ctx.FromStore(R).Join(ctx.FromStore(S), lambda r: r[0], lambda s: s[0], sel) \
             .ToStore(a.to_store, delete_if_exists=True).SubmitAndWait()
         return None
 
@@ -100,7 +113,12 @@ def main():
             res = store_check()
         ok = res[0] == exp[0] and res[1] == exp[1]
     med = sorted(times)[len(times) // 2]
-    total = 2 * rows * 64
+    if a.names:                 # Name bytes ("u" + decimal key, keys < rows) + V1 + V2 per record
+        lo = lambda d: 10 ** (d - 1) if d > 1 else 0  # noqa: E731  (first key with d digits)
+        ndig = sum(d * (min(rows, 10 ** d) - lo(d)) for d in range(1, 20) if lo(d) < rows)
+        total = 2 * (rows * 17 + ndig)
+    else:
+        total = 2 * rows * 64
     if a.direct:
         js = dict(job.last)
         fallbacks = []
@@ -115,15 +133,20 @@ def main():
         "metric": "Hash-join GB/s of input (two 100 GB tables, spill HBM -> host DRAM)",
         "value": round(total / med / 1e9, 3), "unit": "GB/s", "n_gpus": w.size, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(med * 1e3, 2), "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "int64", "data": "synthetic gen://records64 row tables (dimension x fact)",
+        "vs_baseline": None, "dtype": "int64",
+        "data": ("synthetic gen://names tables (string key, dimension x fact; input bytes = Name + 2 x int64)"
+                 if a.names else "synthetic gen://records64 row tables (dimension x fact)"),
         "validated": ok, "matches": res[0] if res else None, "all_step_ms": [round(t * 1e3, 1) for t in times],
         "path": "direct (models/hashjoin.py)" if a.direct else (
             f"DryadLINQ query -> grace join stage -> {a.to_store}" if a.to_store else
             "DryadLINQ query -> fused grace join stage"),
         "fallbacks": fallbacks, "join": js,
-        "config": {"model": ("R.Join(S, Key, (r, s) => (r.Key, r.V1, s.V1)).ToStore(partfile)" if a.to_store else
+        "config": {"model": ("R.Join(S, Name, (r, s) => (r.V2, r.V1, s.V1)).ToStore(partfile)" if a.names and a.to_store
+                             else "R.Join(S, Name).Select(r.V1 + s.V1).Sum()" if a.names
+                             else "R.Join(S, Key, (r, s) => (r.Key, r.V1, s.V1)).ToStore(partfile)" if a.to_store else
                              "R.Join(S, Key).Select(r.V1 + s.V1).Sum()") + " (grace hash join)", "rows_per_table": rows,
-                   "row_bytes": 64, "hbm_budget_gb": a.hbm_budget_gb, "parallelism": f"dp{w.size}"}})
+                   "row_bytes": None if a.names else 64, "input_GB": round(total / 1e9, 2),
+                   "hbm_budget_gb": a.hbm_budget_gb, "parallelism": f"dp{w.size}"}})
 
 
 if __name__ == "__main__":

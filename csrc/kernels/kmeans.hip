@@ -520,6 +520,17 @@ __global__ __launch_bounds__(256, 2) void kmeans_mfma16_kernel(const float* __re
 //               best two estimates are closer than twice that are flagged and re-ranked exactly
 //               from the f32 row (kmeans_near_list + kmeans_rerank_kernel)
 constexpr float kKmTolH = 4.0e-3f;
+#ifndef DR_KM_DEPTH
+#define DR_KM_DEPTH 2                               // (a build-time constant; tools/micro/km_depth_ab.py)
+#endif
+constexpr int kKmDepth = DR_KM_DEPTH;               // 16-point tiles in flight per wave
+#ifndef DR_KM_WAVES
+#define DR_KM_WAVES 8                               // waves per workgroup (they share the LDS fragments)
+#endif
+constexpr int kKmWaves = DR_KM_WAVES;
+#ifndef DR_KM_CH_REGS
+#define DR_KM_CH_REGS 0                             // ch fragments kept in registers (0: LDS per tile)
+#endif
 
 __global__ __launch_bounds__(256) void kmeans_hi_kernel(const float* __restrict__ X, uint64_t n,
                                                         __bf16* __restrict__ XH, float* __restrict__ xnorm) {
@@ -537,8 +548,13 @@ __global__ __launch_bounds__(256) void kmeans_hi_kernel(const float* __restrict_
   }
 }
 
-template <int KT>
-__global__ __launch_bounds__(256) void kmeans_assign_kernel(const __bf16* __restrict__ XH,
+// The points stream through registers, KD 16-point tiles ahead of the one being assigned (the
+// 32 GB plane is read once; only deep prefetch keeps enough bytes in flight per CU at two waves
+// per SIMD).  The ch fragments (KT x 4 x 16 bytes per lane) are read from LDS once per wave and stay
+// in registers, the cm fragments are read from LDS per tile (16 KB of LDS per tile and wave at
+// KT = 4: a quarter of the fragment traffic of reading both per tile).
+template <int KT, int KD>
+__global__ __launch_bounds__(64 * kKmWaves) void kmeans_assign_kernel(const __bf16* __restrict__ XH,
                                                             const float* __restrict__ xnorm, uint64_t n,
                                                             const float* __restrict__ C,
                                                             const float* __restrict__ cnorm, int K,
@@ -549,14 +565,14 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(const __bf16* __rest
   __shared__ float cn[KP];
   __shared__ float cmax_s;
   const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 15, g = l >> 4;
-  for (int i = t; i < KP * D; i += 256) {
+  for (int i = t; i < KP * D; i += 64 * kKmWaves) {
     const int c = i / D, d = i % D;
     const float v = c < K ? C[(uint64_t)c * D + d] : 0.f;
     const __bf16 vh = (__bf16)v;
     chi[c * kCRow + d] = vh;
     cmd[c * kCRow + d] = (__bf16)(v - (float)vh);
   }
-  for (int c = t; c < KP; c += 256) cn[c] = c < K ? cnorm[c] : __builtin_inff();
+  for (int c = t; c < KP; c += 64 * kKmWaves) cn[c] = c < K ? cnorm[c] : __builtin_inff();
   if (t == 0) {
     float m = 0.f;
     for (int c = 0; c < K; ++c) m = fmaxf(m, cnorm[c]);
@@ -564,36 +580,57 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(const __bf16* __rest
   }
   __syncthreads();
   const float cmax = cmax_s;
+#if DR_KM_CH_REGS
+  bf16x8 ch[KT][4];
+#pragma unroll
+  for (int ct = 0; ct < KT; ++ct)
+#pragma unroll
+    for (int s_ = 0; s_ < 4; ++s_)
+      ch[ct][s_] = *reinterpret_cast<const bf16x8*>(chi + (ct * 16 + r) * kCRow + 32 * s_ + 8 * g);
+#endif
   const uint64_t tiles = (n + 15) / 16;
-  const uint64_t gw = (uint64_t)blockIdx.x * 4 + w, GW = (uint64_t)gridDim.x * 4;
+  const uint64_t gw = (uint64_t)blockIdx.x * kKmWaves + w, GW = (uint64_t)gridDim.x * kKmWaves;
   // lane (r, g) holds dims 32 s + 8 g .. + 7 of point r of the tile, s < 4; clamped rows (a point
   // past n re-reads point n - 1 and writes nothing), so the loads need no branch
-  bf16x8 xh[4];
-  float xn;
-  auto load = [&](uint64_t tile) {
+  struct Pts {
+    bf16x8 x[4];
+    float xn;
+  };
+  auto load = [&](uint64_t tile, Pts& d) {
     const uint64_t p = min(tile * 16 + r, n - 1);
 #pragma unroll
-    for (int s_ = 0; s_ < 4; ++s_) xh[s_] = *reinterpret_cast<const bf16x8*>(XH + p * D + 32 * s_ + 8 * g);
-    xn = xnorm[p];
+    for (int s_ = 0; s_ < 4; ++s_) d.x[s_] = *reinterpret_cast<const bf16x8*>(XH + p * D + 32 * s_ + 8 * g);
+    d.xn = xnorm[p];
   };
-  if (gw < tiles) load(gw);
+  Pts ring[KD];
+#pragma unroll
+  for (int j = 0; j < KD; ++j)
+    if (gw + j * GW < tiles) load(gw + j * GW, ring[j]);
   for (uint64_t tile = gw; tile < tiles; tile += GW) {
+    // compiler barrier: keeps the cm fragment reads below inside the loop (hoisted, they would
+    // take 16 x KT more registers per lane than the prefetch ring they displace)
+    asm volatile("" ::: "memory");
     const uint64_t p = tile * 16 + r;
     f32x4 Dt[KT];
 #pragma unroll
     for (int ct = 0; ct < KT; ++ct) Dt[ct] = f32x4{};
-    const bf16x8 b0 = xh[0], b1 = xh[1], b2 = xh[2], b3 = xh[3];
-    const float xnc = xn;
-    load(tile + GW < tiles ? tile + GW : tile);        // the next tile in flight under the MFMAs
-    const bf16x8 bx[4] = {b0, b1, b2, b3};
+    const Pts cur = ring[0];
+#pragma unroll
+    for (int j = 0; j + 1 < KD; ++j) ring[j] = ring[j + 1];
+    const uint64_t nx = tile + KD * GW;
+    load(nx < tiles ? nx : tile, ring[KD - 1]);       // KD tiles in flight under the MFMAs
 #pragma unroll
     for (int s_ = 0; s_ < 4; ++s_) {
 #pragma unroll
       for (int ct = 0; ct < KT; ++ct) {
-        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(chi + (ct * 16 + r) * kCRow + 32 * s_ + 8 * g);
         const bf16x8 am = *reinterpret_cast<const bf16x8*>(cmd + (ct * 16 + r) * kCRow + 32 * s_ + 8 * g);
-        Dt[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bx[s_], Dt[ct], 0, 0, 0);
-        Dt[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bx[s_], Dt[ct], 0, 0, 0);
+#if DR_KM_CH_REGS
+        const bf16x8 ah = ch[ct][s_];
+#else
+        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(chi + (ct * 16 + r) * kCRow + 32 * s_ + 8 * g);
+#endif
+        Dt[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, cur.x[s_], Dt[ct], 0, 0, 0);
+        Dt[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, cur.x[s_], Dt[ct], 0, 0, 0);
       }
     }
     float bd = __builtin_inff(), sd = __builtin_inff();
@@ -620,7 +657,7 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(const __bf16* __rest
         sd = fminf(sd, obd);
       }
     }
-    const bool near = K > 1 && (sd - bd) <= 2.f * kKmTolH * xnc * cmax;
+    const bool near = K > 1 && (sd - bd) <= 2.f * kKmTolH * cur.xn * cmax;
     if (g == 0 && p < n) assign[p] = near ? (int32_t)((uint32_t)bj | 0x80000000u) : bj;
   }
 }
@@ -922,9 +959,10 @@ DR_API int dr_kmeans_step_hi(const __bf16* XH, const float* xnorm, const float* 
   uint32_t* near_list = near_cnt + 4;
   kmeans_near_reset<<<1, 64, 0, s>>>(near_cnt);
   const uint64_t waves = (n + 15) / 16;
-  const uint64_t cap = 8 * (uint64_t)num_cus();
-  const unsigned ga = (unsigned)((waves + 3) / 4 < cap ? (waves + 3) / 4 : cap);
-#define DR_KMA(KTV) kmeans_assign_kernel<KTV><<<ga, 256, 0, s>>>(XH, xnorm, n, C, cnorm_ws, K, assign)
+  const uint64_t cap = 32 / kKmWaves * (uint64_t)num_cus();
+  const uint64_t wg = (waves + kKmWaves - 1) / kKmWaves;
+  const unsigned ga = (unsigned)(wg < cap ? wg : cap);
+#define DR_KMA(KTV) kmeans_assign_kernel<KTV, kKmDepth><<<ga, 64 * kKmWaves, 0, s>>>(XH, xnorm, n, C, cnorm_ws, K, assign)
   if (K <= 16) DR_KMA(1);
   else if (K <= 32) DR_KMA(2);
   else if (K <= 48) DR_KMA(3);

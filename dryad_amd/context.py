@@ -124,7 +124,9 @@ _DEFAULTS = dict(
     #                               (runtime/stream_agg.py; None: when a partition exceeds HbmBudgetBytes)
     GraceJoin=None,               # a Join as the partitioned grace join stage (runtime/grace_stage.py;
     #                               None: when its inputs would crowd the HBM budget; False: never)
-    LineAlignedSortInput=True,    # GPU executor: a table of 100-byte rows that only an OrderBy reads is
+    GraceJoinStringBytes=64,      # ... inline bytes per string field in its packed bucket rows (longer
+    #                               strings: a voted GangAgreementError)
+    LineAlignedSortInput=True,   # GPU executor: a table of 100-byte rows that only an OrderBy reads is
     #                               stored at a 128-byte pitch (one HBM line per record gather)
     GenFusedShuffle=False,        # multi-rank OrderBy over gen://terasort: generate the records straight
     #                               into the exchange's send rows (no input table; a benchmark variant)

@@ -15,6 +15,8 @@ Elementwise projections/predicates are traced user lambdas executed as PyTorch-R
 """
 from __future__ import annotations
 
+import functools
+
 import torch
 
 from ..compiler.decomposition import Sym, substitute
@@ -1669,9 +1671,12 @@ def _interleave(tabs):
     for t in tabs[1:]:
         if t.rows is not None or t.shape.kind != t0.shape.kind or t.shape.fields != t0.shape.fields or \
                 t.shape.pytype is not t0.shape.pytype or \
-                any(t.cols[k].dtype != c.dtype or t.cols[k].shape[1:] != c.shape[1:] for k, c in t0.cols.items()):
+                any(t.cols[k].shape[1:] != c.shape[1:] or t.cols[k].is_floating_point() != c.is_floating_point()
+                    for k, c in t0.cols.items()):
             raise NotTraceable("SelectMany elements of different layouts")
-    cols = {k: torch.stack([t.cols[k] for t in tabs], 1).reshape((t0.n * L,) + tuple(c.shape[1:]))
+    # [x, x + 1]: an Int32 field and its int64 arithmetic share the wider type (Python ints)
+    wide = {k: functools.reduce(torch.promote_types, [t.cols[k].dtype for t in tabs]) for k in t0.cols}
+    cols = {k: torch.stack([t.cols[k].to(wide[k]) for t in tabs], 1).reshape((t0.n * L,) + tuple(c.shape[1:]))
             for k, c in t0.cols.items()}
     return DeviceTable(t0.n * L, t0.shape, cols)
 

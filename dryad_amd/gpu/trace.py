@@ -103,13 +103,15 @@ def _bin(name, fn, rfn=None, arith=False):
 
 def _promote(a, b):
     """Arithmetic with a floating operand runs in float64, as the LocalDebug oracle's Python
-    floats (and C#'s long * double) do: torch alone would compute int64 column * 1.5 in float32."""
+    floats (and C#'s long * double) do: torch alone would compute int64 column * 1.5 in float32.
+    Integer arithmetic runs in int64: narrower columns (an Int32 field of a stored table) would
+    wrap where the oracle's Python ints do not."""
     fb = isinstance(b, float) or isinstance(b, torch.Tensor) and b.is_floating_point()
-    if a.is_floating_point() or fb:
-        if a.dtype != torch.float64:
-            a = a.to(torch.float64)
-        if isinstance(b, torch.Tensor) and b.dtype != torch.float64:
-            b = b.to(torch.float64)
+    wide = torch.float64 if a.is_floating_point() or fb else torch.int64
+    if a.dtype != wide:
+        a = a.to(wide)
+    if isinstance(b, torch.Tensor) and b.dtype != wide:
+        b = b.to(wide)
     return a, b
 
 

@@ -1720,6 +1720,12 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     mine, fmt_extra = {}, None
     for p, v in local.items():
         tmp = PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, 0)
+        if isinstance(v, GS.StreamedPart) and isinstance(v.path, list):    # split over part files
+            mine[p] = []
+            for j, f in enumerate(v.path):
+                os.replace(f, f"{tmp}.{j}")
+                mine[p].append(f"{tmp}.{j}")
+            continue
         if isinstance(v, GS.StreamedPart):          # written bucket / chunk by chunk by its stage
             os.replace(v.path, tmp)
             if os.path.exists(v.path + PF.INDEX_SUFFIX):         # the block index of string records

@@ -54,8 +54,9 @@ _I64 = torch.int64
 
 
 class StreamedPart:
-    """A partition already written to ``path`` (a tmp part file) by a streaming stage; the output
-    commit renames it into place (runtime/gpu_executor._commit_partfile_impl)."""
+    """A partition already written to ``path`` (a tmp part file, or a list of them: a partition
+    split over several part files) by a streaming stage; the output commit renames it into place
+    (runtime/gpu_executor._commit_partfile_impl)."""
 
     def __init__(self, path: str, n: int, nbytes: int, dtype, rows: dict | None = None):
         self.path, self.n, self.nbytes, self.dtype = path, n, nbytes, dtype
@@ -707,6 +708,8 @@ class _Sink:
         self.writer, self.dtype, self.n, self.written = None, None, 0, 0
         self.written_bytes, self.index = 0, []          # (string records) block index of the stream
         self.stream = False
+        self.paths, self.fbytes = None, None            # a split output: its part files and their sizes
+        self.split = int(runner.ctx.PartFileSplitBytes or 0) > 0
         if stage.is_output and not self.agg and not desc["after"]:
             scheme, path, _ = parse_uri(stage.output["uri"])
             self.stream = scheme in ("partfile", "file") and runner.ctx.OutputDataCompressionScheme.value == 0
@@ -725,6 +728,7 @@ class _Sink:
             if self.dtype is None:
                 self.dtype = _table_dtype(data)
             enc = CD.encode(data, self.dtype) if self.dtype is not None else None
+            fixed = enc is not None
             if enc is None and self.dtype is not None and CD.var_layout(self.dtype) is not None:
                 got = CD.encode_var(data, self.dtype, full_offsets=True)
                 if got is not None:
@@ -736,9 +740,21 @@ class _Sink:
                         self.index.append(offs[j0::B] + self.written_bytes)
             if enc is not None:
                 if self.writer is None:
-                    from ..io.writer import PartWriter
-                    self.writer = PartWriter(self.tmp, data.device, self.runner.write_stats)
-                self.writer.write(enc)
+                    from ..io.writer import SPLIT_MAX, PartWriter
+                    if self.split and fixed:
+                        # fixed-width records with PartFileSplitBytes: the buckets' results go to
+                        # SPLIT_MAX part files at once (page-cache writes serialise per inode)
+                        self.paths = [f"{self.tmp}.{j}" for j in range(SPLIT_MAX)]
+                        self.fbytes = [0] * SPLIT_MAX
+                        self.writer = PartWriter(self.paths, data.device, self.runner.write_stats)
+                    else:
+                        self.writer = PartWriter(self.tmp, data.device, self.runner.write_stats)
+                if self.paths is not None:
+                    j = min(range(len(self.fbytes)), key=self.fbytes.__getitem__)
+                    self.writer.write(enc, file=j)
+                    self.fbytes[j] += enc.numel()
+                else:
+                    self.writer.write(enc)
                 self.n += data.n
                 self.written_bytes += enc.numel()
                 return
@@ -756,10 +772,11 @@ class _Sink:
             try:
                 w.abort()
             finally:
-                try:
-                    os.remove(self.tmp)
-                except OSError:
-                    pass
+                for f in self.paths or [self.tmp]:
+                    try:
+                        os.remove(f)
+                    except OSError:
+                        pass
         self.chunks, self.partials = [], []
 
     def finish(self, V):
@@ -784,7 +801,18 @@ class _Sink:
             for p in parts[1:]:
                 out[p] = empty
             return out
-        if self.writer is not None:
+        if self.writer is not None and self.paths is not None:
+            sizes = self.writer.close()
+            self.written = sum(sizes)
+            keep = []
+            for f, b in zip(self.paths, sizes):
+                if b:
+                    keep.append(f)
+                else:
+                    os.remove(f)
+            out[parts[0]] = StreamedPart(keep or self.paths[:1], self.n, self.written, self.dtype)
+            self.writer = None
+        elif self.writer is not None:
             self.written = self.writer.close()
             if self.index:
                 from ..io import partfile as PF

@@ -289,8 +289,10 @@ def test_payload_sort_rejects_wide_key_span():
 
 @pytest.mark.parametrize("parts", [1, 3])
 def test_groupby_payload_path_matches_localdebug(parts, monkeypatch):
+    from dryad_amd.gpu import ops as G
     from dryad_amd.ops import relational as R
     monkeypatch.setattr(R, "PAYLOAD_SORT_MIN_ROWS", 0)
+    monkeypatch.setattr(G, "_fused_int64_groups", lambda *a: None)   # (the int64 key would take it first)
     calls = []
     orig = R.payload_groups
     monkeypatch.setattr(R, "payload_groups", lambda *a: calls.append(1) or orig(*a))

@@ -60,6 +60,23 @@ def test_join_select_to_partfile_streams_buckets(tmp_path, budget):
     assert len(got) == 300000
 
 
+def test_join_to_partfile_split_over_part_files(tmp_path):
+    """With PartFileSplitBytes the streamed bucket results go to several part files of the one
+    output partition at once (page-cache writes serialise per inode); the table reads back whole."""
+    from dryad_amd.io import partfile as PF
+    g = _ctx(budget=6 << 20)
+    g.PartFileSplitBytes = 1
+    uri = "partfile://" + str(tmp_path / "js.pt")
+    q = lambda c: c.FromStore(R.format(P=2)).Join(c.FromStore(S.format(P=2)), lambda r: r[0], lambda s: s[0],  # noqa
+                                                   lambda r, s: (r[0], r[1], s[2]))
+    q(g).ToStore(uri, delete_if_exists=True).SubmitAndWait()
+    res, js = _stats(g)
+    assert js.get("kind") == "grace join stage" and res["fallbacks"] == [], (js, res["fallbacks"])
+    meta = PF.read_meta(str(tmp_path / "js.pt"))
+    assert meta.count > 2, meta.count                  # 2 partitions, at least one split
+    _same(sorted(g.FromStore(uri)), sorted(q(_loc())))
+
+
 def test_join_float_sum_and_groupby_after_join():
     g = _ctx(budget=6 << 20)
     q = lambda c: c.FromStore(R.format(P=2)).Join(c.FromStore(S.format(P=2)), lambda r: r[0], lambda s: s[0],  # noqa
@@ -115,7 +132,7 @@ def test_join_to_partfile_recovers_from_a_bucket_failure(tmp_path, monkeypatch):
             raise RuntimeError("injected bucket failure")
         return real(*a, **k)
     monkeypatch.setattr(GR, "hash_join_pairs", flaky)
-    g = _ctx()
+    g = _ctx(budget=6 << 20)                  # several buckets (the pruned rows fit one otherwise)
     uri = "partfile://" + str(tmp_path / "jf.pt")
     q = lambda c: c.FromStore(R.format(P=2)).Join(c.FromStore(S.format(P=2)), lambda r: r[0], lambda s: s[0],  # noqa
                                                    lambda r, s: (r[0], r[1], s[2]))
@@ -155,7 +172,7 @@ def test_string_key_join_spills_and_streams_to_partfile(tmp_path, stored):
     got = sorted(g.FromStore(uri))
     exp = sorted(q(_loc(), NAMES_R.format(P=2), NAMES_S.format(P=2)))
     _same(got, exp)
-    assert len(got) == 300000 and isinstance(got[0][0], str)
+    assert len(got) > 300000 and isinstance(got[0][0], str)     # R repeats some of its 150000 keys
 
 
 def test_composite_and_float_key_joins():

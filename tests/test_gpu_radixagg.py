@@ -104,8 +104,6 @@ def test_group_by_query_uses_radix_path(monkeypatch, parts):
     import dryad_amd as D
     from dryad_amd.ops import radixagg as RA
     monkeypatch.setattr(RA, "MIN_ROWS", 1 << 12)
-    monkeypatch.setattr(RA, "MODE", "1")
-    monkeypatch.setattr(RA, "ENABLED", True)
     calls = []
     orig = RA.radix_aggregate
     monkeypatch.setattr(RA, "radix_aggregate", lambda *a, **kw: calls.append(1) or orig(*a, **kw))
@@ -118,6 +116,7 @@ def test_group_by_query_uses_radix_path(monkeypatch, parts):
                                           g.Max(lambda r: r[3])))
     gpu = D.DryadLinqContext(platform="gpu")
     gpu.PartitionCount = parts
+    gpu.GroupByAggregation = "radix"              # every large integer key (ops/tuning.py)
     local = D.DryadLinqContext(1)
     local.LocalDebug = True
     assert sorted(q(gpu)) == sorted(q(local))
@@ -127,8 +126,12 @@ def test_group_by_query_uses_radix_path(monkeypatch, parts):
 
 def test_auto_route_takes_only_wide_keys(monkeypatch):
     from dryad_amd.ops import radixagg as RA
+    from dryad_amd.ops import tuning
     monkeypatch.setattr(RA, "MIN_ROWS", 16)
-    monkeypatch.setattr(RA, "MODE", "auto")
-    monkeypatch.setattr(RA, "ENABLED", True)
     narrow = torch.arange(100_000, device="cuda")
-    assert not RA.wanted(narrow) and RA.wanted(narrow << 40) and RA.wanted(-(narrow << 20))
+    with tuning.scope(groupby_aggregation="auto"):
+        assert not RA.wanted(narrow) and RA.wanted(narrow << 40) and RA.wanted(-(narrow << 20))
+    with tuning.scope(groupby_aggregation="radix"):
+        assert RA.wanted(narrow)
+    with tuning.scope(groupby_aggregation="sort"):
+        assert not RA.wanted(narrow << 40)
