@@ -43,14 +43,32 @@ __global__ __launch_bounds__(256) void ts_fine_starts_kernel(const E64* __restri
   }
 }
 
+// Key bits [fb, 80) of a 100-byte row (fb >= 16: they fit 64 bits), left-aligned.
+__device__ __forceinline__ uint64_t tm_key(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t fb) {
+  const uint64_t k0 = ((uint64_t)bswap32(w0) << 32) | bswap32(w1);
+  const uint64_t k1 = (uint64_t)(bswap32(w2) >> 16);                  // key bytes 8, 9
+  return (k0 << fb) | ((k1 << 48) >> (64 - fb));
+}
+
+// Rows of one bucket staged in LDS at the record pitch (two workgroups per CU: 79.4 KB each).
+constexpr uint32_t kTsStage = 736;
+constexpr uint32_t kTsBins = 256;                  // staged path: next 8 key bits
+constexpr uint32_t kTsPasses = (kTsStage + 63) / 64;
+constexpr uint32_t kTsHalf = (kTsPasses + 1) / 2;   // row loads a lane group keeps in flight
+constexpr uint32_t kTsPoolWords = kTsStage * kTmWords + kTsStage + 2 * kTsBins;
+
 // pre[s * K + k] = row (of `rows`) where bucket k's slice from source s starts, cnt[s * K + k] its
-// rows; bucket k's output rows start at out row outoff[k].  Per bucket: lane t holds tile rows t
-// and t + 512 in registers, loaded at once as 6 x 16 + 4 bytes each (the slices are contiguous:
-// the wave's loads cover whole lines between them, one round trip); the rows' remaining key bits
-// [fb, 80) go to LDS, an LDS counting sort on their next 10 bits places each row (ties inside a
-// bin ranked by (key, tile index): source-major = stable), and every lane stores its rows to
-// their output slots.  A bucket of more than kTmCap rows is skipped and flagged (*overflow); the
-// caller orders that key range another way.
+// rows; bucket k's output rows start at out row outoff[k].  Per bucket (a bucket averages ~600
+// rows; FINE_ROWS):
+//   * nt <= kTsStage rows (staged path): the W source slices are copied into an LDS stage at the
+//     100-byte pitch (8 lanes per row, 16-byte loads; a wave reads 8 consecutive rows of a slice,
+//     800 contiguous bytes), an LDS counting sort on the next 8 key bits plus an in-bin rank by
+//     (key, tile index) gives each output slot its tile row (source-major tile index = stable),
+//     and the bucket leaves in OUTPUT order: a wave stores 8 consecutive output rows, 800
+//     contiguous bytes, every row read back from the stage.  Both HBM streams are contiguous.
+//   * kTsStage < nt <= kTmCap (a rare large bucket): left to ts_tile_merge_big_kernel.
+// A bucket of more than kTmCap rows is skipped and flagged (*overflow); the caller orders that
+// key range another way.
 __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4))) void ts_tile_merge_kernel(const uint32_t* __restrict__ rows,
                                                                    uint32_t* __restrict__ out,
                                                                    const int64_t* __restrict__ pre,
@@ -58,11 +76,7 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
                                                                    const int64_t* __restrict__ outoff, uint32_t W,
                                                                    uint32_t K, uint32_t fb,
                                                                    uint32_t* __restrict__ overflow) {
-  __shared__ uint64_t key[kTmCap];
-  __shared__ uint16_t member[kTmCap];
-  __shared__ uint16_t rnk[kTmCap];
-  __shared__ uint32_t bcnt[kTmBins];
-  __shared__ uint32_t bcur[kTmBins];
+  __shared__ __attribute__((aligned(16))) uint32_t pool[kTsPoolWords];
   __shared__ int64_t sbase[kTmMaxW];
   __shared__ uint32_t spre[kTmMaxW + 1];
   __shared__ uint32_t wtot[kTmThreads / 64];
@@ -77,8 +91,6 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
       }
       spre[W] = acc;
     }
-    bcnt[t] = 0;
-    bcnt[t + kTmThreads] = 0;
     __syncthreads();
     const uint32_t nt = spre[W];
     if (nt == 0 || nt > kTmCap) {
@@ -86,6 +98,145 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
       __syncthreads();
       continue;
     }
+    uint32_t* o = out + (uint64_t)outoff[k] * kTmWords;
+    if (nt <= kTsStage) {
+      uint32_t* stage = pool;
+      uint16_t* member = reinterpret_cast<uint16_t*>(pool + kTsStage * kTmWords);
+      uint16_t* perm = member + kTsStage;
+      uint32_t* bcnt = pool + kTsStage * kTmWords + kTsStage;
+      uint32_t* bcur = bcnt + kTsBins;
+      if (t < kTsBins) bcnt[t] = 0;
+      const uint32_t g = t >> 3, sub = t & 7;
+      uint32_t s = 0;
+      for (uint32_t p0 = 0; p0 < kTsPasses && g + 64 * p0 < nt; p0 += kTsHalf) {   // loads in flight: kTsHalf rows per lane group
+        u32x4u v[kTsHalf];
+#pragma unroll
+        for (uint32_t p = 0; p < kTsHalf; ++p) {
+          const uint32_t i = g + 64 * (p0 + p);
+          if (i < nt && sub < 7) {
+            while (spre[s + 1] <= i) ++s;
+            const uint32_t* src = rows + (uint64_t)(sbase[s] + (int64_t)(i - spre[s])) * kTmWords + sub * 4;
+            if (sub < 6) v[p] = *reinterpret_cast<const u32x4u*>(src);
+            else v[p].x = src[0];
+          }
+        }
+#pragma unroll
+        for (uint32_t p = 0; p < kTsHalf; ++p) {
+          const uint32_t i = g + 64 * (p0 + p);
+          if (i < nt && sub < 7) {
+            uint32_t* d = stage + i * kTmWords + sub * 4;
+            d[0] = v[p].x;
+            if (sub < 6) {
+              d[1] = v[p].y;
+              d[2] = v[p].z;
+              d[3] = v[p].w;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      for (uint32_t i = t; i < nt; i += kTmThreads) {
+        const uint32_t* r = stage + i * kTmWords;
+        atomicAdd(&bcnt[(uint32_t)(tm_key(r[0], r[1], r[2], fb) >> 56)], 1u);
+      }
+      __syncthreads();
+      uint32_t c = 0, inc = 0;
+      if (t < kTsBins) {                          // exclusive scan of the 256 bins: waves 0..3
+        c = bcnt[t];
+        inc = wave_inclusive_scan(c);
+        if (lane_id() == 63) wtot[wave_id()] = inc;
+      }
+      __syncthreads();
+      if (t < kTsBins) {
+        uint32_t run = inc - c;
+        for (int w = 0; w < wave_id(); ++w) run += wtot[w];
+        bcur[t] = run;
+      }
+      __syncthreads();
+      for (uint32_t i = t; i < nt; i += kTmThreads) {
+        const uint32_t* r = stage + i * kTmWords;
+        member[atomicAdd(&bcur[(uint32_t)(tm_key(r[0], r[1], r[2], fb) >> 56)], 1u)] = (uint16_t)i;
+      }
+      __syncthreads();
+      for (uint32_t i = t; i < nt; i += kTmThreads) {   // slot = bin start + smaller (key, index) in the bin
+        const uint32_t* r = stage + i * kTmWords;
+        const uint64_t a = tm_key(r[0], r[1], r[2], fb);
+        const uint32_t d = (uint32_t)(a >> 56), end = bcur[d], beg = end - bcnt[d];
+        uint32_t slot = beg;
+        for (uint32_t m = beg; m < end; ++m) {
+          const uint32_t x = member[m];
+          const uint32_t* q = stage + x * kTmWords;
+          const uint64_t b = tm_key(q[0], q[1], q[2], fb);
+          slot += (b < a || (b == a && x < i)) ? 1u : 0u;
+        }
+        perm[slot] = (uint16_t)i;
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (uint32_t p = 0; p < kTsPasses; ++p) {
+        const uint32_t j = g + 64 * p;
+        if (j < nt && sub < 7) {
+          const uint32_t* sr = stage + (uint32_t)perm[j] * kTmWords + sub * 4;
+          uint32_t* dst = o + j * kTmWords + sub * 4;
+          // plain stores: the bucket's first and last lines are partial, completed in L2 by the
+          // neighbouring buckets (nontemporal stores write partial lines through)
+          if (sub < 6) *reinterpret_cast<u32x4u*>(dst) = u32x4u{sr[0], sr[1], sr[2], sr[3]};
+          else dst[0] = sr[0];
+        }
+      }
+      __syncthreads();
+      continue;
+    }
+    __syncthreads();               // kTsStage < nt <= kTmCap: ts_tile_merge_big_kernel
+  }
+}
+
+// The buckets of kTsStage < nt <= kTmCap rows (rare: > 5 sigma above the ~600-row mean at
+// FINE_ROWS) that ts_tile_merge_kernel leaves: each workgroup scans 512 buckets' sizes, lists the
+// large ones in LDS and orders them with the register path -- lane t holds tile rows t and t + 512
+// (6 x 16 + 4 bytes each), ranks by the next 10 key bits, rows stored to their slots.
+__global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4))) void ts_tile_merge_big_kernel(
+    const uint32_t* __restrict__ rows, uint32_t* __restrict__ out, const int64_t* __restrict__ pre,
+    const int32_t* __restrict__ cnt, const int64_t* __restrict__ outoff, uint32_t W, uint32_t K, uint32_t fb) {
+  __shared__ uint64_t key[kTmCap];
+  __shared__ uint16_t member[kTmCap];
+  __shared__ uint16_t rnk[kTmCap];
+  __shared__ uint32_t bcnt[kTmBins];
+  __shared__ uint32_t bcur[kTmBins];
+  __shared__ int64_t sbase[kTmMaxW];
+  __shared__ uint32_t spre[kTmMaxW + 1];
+  __shared__ uint32_t wtot[kTmThreads / 64];
+  __shared__ uint32_t list[kTmThreads];
+  __shared__ uint32_t nlist;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) nlist = 0;
+  __syncthreads();
+  {
+    const uint64_t kk = (uint64_t)blockIdx.x * kTmThreads + t;
+    if (kk < K) {
+      uint32_t nt = 0;
+      for (uint32_t s = 0; s < W; ++s) nt += (uint32_t)cnt[(uint64_t)s * K + kk];
+      if (nt > kTsStage && nt <= kTmCap) list[atomicAdd(&nlist, 1u)] = (uint32_t)kk;
+    }
+  }
+  __syncthreads();
+  const uint32_t nl = nlist;
+  for (uint32_t li = 0; li < nl; ++li) {
+    const uint32_t k = list[li];
+    if (t < W) sbase[t] = pre[(uint64_t)t * K + k];
+    if (t == 0) {
+      uint32_t acc = 0;
+      for (uint32_t s = 0; s < W; ++s) {
+        spre[s] = acc;
+        acc += (uint32_t)cnt[(uint64_t)s * K + k];
+      }
+      spre[W] = acc;
+    }
+    __syncthreads();
+    const uint32_t nt = spre[W];
+    uint32_t* o = out + (uint64_t)outoff[k] * kTmWords;
+    bcnt[t] = 0;
+    bcnt[t + kTmThreads] = 0;
     u32x4u v[kTmRows][6];
     uint32_t tail[kTmRows];
 #pragma unroll
@@ -100,14 +251,12 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
         tail[h] = src[24];
       }
     }
+    __syncthreads();
 #pragma unroll
     for (uint32_t h = 0; h < kTmRows; ++h) {
       const uint32_t i = t + h * kTmThreads;
       if (i < nt) {
-        // key bits [fb, 80) left-aligned (fb >= 16: they fit 64 bits); the top 10 pick the bin
-        const uint64_t k0 = ((uint64_t)bswap32(v[h][0].x) << 32) | bswap32(v[h][0].y);
-        const uint64_t k1 = (uint64_t)(bswap32(v[h][0].z) >> 16);          // key bytes 8, 9
-        const uint64_t kv = (k0 << fb) | ((k1 << 48) >> (64 - fb));
+        const uint64_t kv = tm_key(v[h][0].x, v[h][0].y, v[h][0].z, fb);   // the top 10 bits pick the bin
         key[i] = kv;
         atomicAdd(&bcnt[(uint32_t)(kv >> 54)], 1u);
       }
@@ -138,14 +287,11 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
       rnk[i] = (uint16_t)r;
     }
     __syncthreads();
-    uint32_t* o = out + (uint64_t)outoff[k] * kTmWords;
 #pragma unroll
     for (uint32_t h = 0; h < kTmRows; ++h) {
       const uint32_t i = t + h * kTmThreads;
       if (i < nt) {
         uint32_t* dst = o + (uint32_t)rnk[i] * kTmWords;
-        // plain stores: a row is a partial line, completed in L2 by its neighbours (nontemporal
-        // stores write the partial lines through: 61 -> 397 ms per 125 GB received)
 #pragma unroll
         for (int q = 0; q < 6; ++q) *reinterpret_cast<u32x4u*>(dst + 4 * q) = v[h][q];
         dst[24] = tail[h];
@@ -304,6 +450,9 @@ DR_API int dr_ts_tile_merge(const uint8_t* rows, uint8_t* out, const int64_t* pr
   const unsigned g = K < 65536u ? K : 65536u;
   ts_tile_merge_kernel<<<g, kTmThreads, 0, s>>>(reinterpret_cast<const uint32_t*>(rows),
                                                 reinterpret_cast<uint32_t*>(out), pre, cnt, outoff, W, K, fb, overflow);
+  DR_LAUNCH_CHECK();
+  ts_tile_merge_big_kernel<<<(K + kTmThreads - 1) / kTmThreads, kTmThreads, 0, s>>>(
+      reinterpret_cast<const uint32_t*>(rows), reinterpret_cast<uint32_t*>(out), pre, cnt, outoff, W, K, fb);
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -303,8 +303,9 @@ PYBIND11_MODULE(_dryad_native, m) {
       .def(py::init<const std::string&, const std::vector<uint64_t>&, int, int64_t, bool>(), py::arg("path"),
            py::arg("buffers"), py::arg("threads"), py::arg("extend_bytes") = (int64_t)(256ll << 20),
            py::arg("mapped") = false)
-      .def(py::init<const std::vector<std::string>&, const std::vector<uint64_t>&, int, int64_t>(),
-           py::arg("paths"), py::arg("buffers"), py::arg("threads"), py::arg("extend_bytes") = (int64_t)(256ll << 20))
+      .def(py::init<const std::vector<std::string>&, const std::vector<uint64_t>&, int, int64_t, bool>(),
+           py::arg("paths"), py::arg("buffers"), py::arg("threads"), py::arg("extend_bytes") = (int64_t)(256ll << 20),
+           py::arg("reuse") = false)
       .def("acquire", [](ChunkWriter& w) {
         int s;
         {

@@ -2,6 +2,7 @@
 
 #include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -24,8 +25,8 @@ ChunkWriter::ChunkWriter(const std::string& path, const std::vector<uint64_t>& b
 }
 
 ChunkWriter::ChunkWriter(const std::vector<std::string>& paths, const std::vector<uint64_t>& buf_ptrs, int threads,
-                         int64_t extend_bytes)
-    : extend_(extend_bytes > 0 ? extend_bytes : (256ll << 20)) {
+                         int64_t extend_bytes, bool reuse)
+    : extend_(extend_bytes > 0 ? extend_bytes : (256ll << 20)), reuse_(reuse) {
   if (buf_ptrs.empty()) throw std::invalid_argument("ChunkWriter: no buffers");
   if (paths.empty()) throw std::invalid_argument("ChunkWriter: no files");
   paths_ = paths;
@@ -35,7 +36,9 @@ ChunkWriter::ChunkWriter(const std::vector<std::string>& paths, const std::vecto
 
 void ChunkWriter::start(int threads) {
   for (const auto& p : paths_) {
-    const int fd = ::open(p.c_str(), O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    // reuse_: an existing file (a recycled part of a replaced table) is overwritten in place, its
+    // blocks and page-cache pages kept; finish() cuts it to the new size
+    const int fd = ::open(p.c_str(), O_RDWR | O_CREAT | (reuse_ ? 0 : O_TRUNC) | O_CLOEXEC, 0644);
     if (fd < 0) {
       const std::string e = std::strerror(errno);
       for (int f : fds_) ::close(f);
@@ -43,7 +46,12 @@ void ChunkWriter::start(int threads) {
       throw std::runtime_error("ChunkWriter: cannot create " + p + ": " + e);
     }
     fds_.push_back(fd);
-    allocated_.push_back(0);
+    off_t have = 0;
+    if (reuse_) {
+      struct stat st;
+      if (::fstat(fd, &st) == 0) have = st.st_size;
+    }
+    allocated_.push_back((int64_t)have);
   }
   for (size_t i = 0; i < bufs_.size(); ++i) free_.push_back((int)i);
   const int nt = threads < 1 ? 1 : threads;

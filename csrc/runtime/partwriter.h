@@ -14,6 +14,9 @@
 // file serialise on its inode lock (~12 GB/s on the MI355X box), writes to distinct files do not
 // (40-93 GB/s with 4-12 threads, profiles/r4/filewrite_ab2.log), so the caller interleaves the
 // chunks of the files.
+// `reuse` (several files): existing files are overwritten in place instead of truncated (the
+// parts of a replaced table recycled as the new table's part files: no page-cache pages freed and
+// allocated again, io/partfile.py recycle pool).
 // `mapped`: the threads copy into shared mappings of the file instead of pwrite()ing, so they
 // fill the page cache in parallel (partwriter.cpp, write_mapped).
 #pragma once
@@ -32,7 +35,7 @@ class ChunkWriter {
   ChunkWriter(const std::string& path, const std::vector<uint64_t>& buf_ptrs, int threads, int64_t extend_bytes,
               bool mapped = false);
   ChunkWriter(const std::vector<std::string>& paths, const std::vector<uint64_t>& buf_ptrs, int threads,
-              int64_t extend_bytes);
+              int64_t extend_bytes, bool reuse = false);
   ~ChunkWriter();
   int acquire();                                   // -1 on error (see error())
   void submit(int slot, int64_t offset, int64_t bytes, int file = 0);
@@ -62,7 +65,7 @@ class ChunkWriter {
   std::deque<int> free_;
   std::deque<Job> jobs_;
   int active_ = 0;
-  bool stop_ = false, mapped_ = false;
+  bool stop_ = false, mapped_ = false, reuse_ = false;
   std::string err_;
 };
 

@@ -135,23 +135,101 @@ def exists(meta_path: str) -> bool:
     return os.path.exists(meta_path)
 
 
-def delete(meta_path: str, background: bool = False):
+# Replaced tables recycle their part files.  A table replaced by ToStore(delete_if_exists=True)
+# usually has a successor of about the same size written into the same directory; its parts are
+# renamed into ``<parts dir>/.recycle/`` instead of being unlinked, and the writer of a new part
+# claims one (atomic rename, so ranks sharing the directory never claim the same file) and
+# overwrites it in place (io/writer.write_device_pieces(reuse=True)).  Unlinking a page-cached part
+# frees its pages, and writing a fresh one allocates them again: 15 GB written into fresh files
+# while the previous 15 GB are unlinked runs at a fraction of the writer's rate
+# (tools/micro/writeback_probe2.py).  Files nobody claims within RECYCLE_TTL seconds are unlinked
+# by a daemon thread (and by the next delete's sweep, after a restart).
+RECYCLE_DIR = ".recycle"
+RECYCLE_TTL = 60.0
+
+
+def _recycle_dir(path: str) -> str:
+    return os.path.join(os.path.dirname(path), RECYCLE_DIR)
+
+
+def _sweep(d: str, older_than: float):
+    import time
+    now = time.time()
+    try:
+        names = os.listdir(d)
+    except OSError:
+        return
+    for fn in names:
+        try:
+            stamp = int(fn.split("-")[1]) / 1e3
+        except (IndexError, ValueError):
+            continue
+        if now - stamp >= older_than:
+            try:
+                os.remove(os.path.join(d, fn))
+            except OSError:
+                pass
+
+
+def claim_recycled(paths: list) -> int:
+    """Rename recycled part files (the largest first) onto ``paths`` (new part files of one
+    directory that do not exist yet); returns how many were claimed.  The writer then overwrites
+    them in place and cuts them to size."""
+    if not paths:
+        return 0
+    d = _recycle_dir(paths[0])
+    try:
+        cands = sorted(((os.path.getsize(os.path.join(d, fn)), fn) for fn in os.listdir(d)
+                        if fn.startswith("r-")), reverse=True)
+    except OSError:
+        return 0
+    got = 0
+    it = iter(cands)
+    for p in paths:
+        if os.path.exists(p):
+            continue
+        for _, fn in it:
+            try:
+                os.rename(os.path.join(d, fn), p)
+            except OSError:          # claimed by another rank meanwhile
+                continue
+            got += 1
+            break
+        else:
+            break
+    return got
+
+
+def delete(meta_path: str, background: bool = False, recycle: bool = True):
     """Delete the table: every partition then the metadata (CheckExistence(deleteIfExists)).
     ``background``: the files are renamed out of the way at once (the table is gone and its
-    names are free for a new one) and unlinked by a daemon thread: unlinking tens of GB of
-    page-cached parts takes seconds the job does not have to wait for."""
+    names are free for a new one); with ``recycle`` the part files go to the recycle directory of
+    their parts directory (see RECYCLE_DIR), everything else is unlinked by a daemon thread:
+    unlinking tens of GB of page-cached parts takes seconds the job does not have to wait for."""
     if not os.path.exists(meta_path):
         return
     if background:
+        import threading
+        import time
         tag = ".deleting-" + uuid.uuid4().hex[:8]
-        moved = []
+        stamp = int(time.time() * 1e3)
+        moved, recycled = [], []
+        rdir = None
         try:
             meta = read_meta(meta_path)
-            for p in meta.paths():
-                for q in (p, p + INDEX_SUFFIX):
-                    if os.path.exists(q):
-                        os.replace(q, q + tag)
-                        moved.append(q + tag)
+            for i, p in enumerate(meta.paths()):
+                if recycle and os.path.exists(p):
+                    rdir = _recycle_dir(p)
+                    os.makedirs(rdir, exist_ok=True)
+                    q = os.path.join(rdir, f"r-{stamp}-{uuid.uuid4().hex[:8]}-{i}")
+                    os.replace(p, q)
+                    recycled.append(q)
+                elif os.path.exists(p):
+                    os.replace(p, p + tag)
+                    moved.append(p + tag)
+                if os.path.exists(p + INDEX_SUFFIX):
+                    os.replace(p + INDEX_SUFFIX, p + INDEX_SUFFIX + tag)
+                    moved.append(p + INDEX_SUFFIX + tag)
         except Exception:
             pass
         os.replace(meta_path, meta_path + tag)
@@ -163,7 +241,14 @@ def delete(meta_path: str, background: bool = False):
                     os.remove(q)
                 except OSError:
                     pass
-        import threading
+            if rdir is not None:
+                _sweep(rdir, 10 * RECYCLE_TTL)      # leftovers of an earlier process
+                time.sleep(RECYCLE_TTL)
+                for q in recycled:                  # not claimed by a successor
+                    try:
+                        os.remove(q)
+                    except OSError:
+                        pass
         threading.Thread(target=unlink_all, daemon=True, name="dryad-partfile-delete").start()
         return
     try:

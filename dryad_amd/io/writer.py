@@ -185,10 +185,13 @@ def write_device(path: str, data: torch.Tensor, stats: WriteStats | None = None)
 SPLIT_MAX = 8
 
 
-def write_device_pieces(paths: list, data: torch.Tensor, bounds: list, stats: WriteStats | None = None) -> list:
+def write_device_pieces(paths: list, data: torch.Tensor, bounds: list, stats: WriteStats | None = None,
+                        reuse: bool = False) -> list:
     """Write byte ranges [bounds[i], bounds[i + 1]) of ``data`` (a contiguous device or host tensor)
     to ``paths[i]``, every file at once: the chunks go out round-robin over the files, so the
-    writer threads work on distinct inodes.  Returns the file sizes."""
+    writer threads work on distinct inodes.  ``reuse``: files already at ``paths`` (recycled parts
+    of a replaced table) are overwritten in place and cut to size, not truncated first.  Returns
+    the file sizes."""
     from ..native import runtime
     from ..ops import _lib
     k = len(paths)
@@ -198,7 +201,7 @@ def write_device_pieces(paths: list, data: torch.Tensor, bounds: list, stats: Wr
     t0 = time.perf_counter()
     ring = _ring()
     with _RING_LOCK:
-        w = runtime().ChunkWriter(list(paths), [b.tensor.data_ptr() for b in ring], THREADS)
+        w = runtime().ChunkWriter(list(paths), [b.tensor.data_ptr() for b in ring], THREADS, reuse=reuse)
         dev_src = flat.is_cuda
         cs = None
         if dev_src:

@@ -220,6 +220,8 @@ class TeraSortStoredJob:
                     read_GBps=round(rd.get("bytes", 0) / 1e9 / max(rd.get("seconds") or 0, 1e-9), 2),
                     write_GB=round(wr.get("bytes", 0) / 1e9, 2), write_s=wr.get("seconds"),
                     write_GBps=round(wr.get("bytes", 0) / 1e9 / max(wr.get("seconds") or 0, 1e-9), 2),
+                    # output parts written over the recycled parts of the table the step replaced
+                    write_recycled_parts=wr.get("recycled_parts", 0),
                     sort_stage_s_excl_read=round(max(0.0, stage - (rd.get("seconds") or 0)), 3),
                     sort_path=r.get("sort_path"), timings=tm, fallbacks=r.get("fallbacks"),
                     prepare=self.prepared)

@@ -184,6 +184,7 @@ class GpuJobRunner:
         self.op_counts = collections.Counter()   # (operator, "device" | "host") -> executions
         from ..io.writer import WriteStats
         self.write_stats = WriteStats()          # partfile parts written by this job
+        self.recycled_parts = 0                  # of them, recycled parts of a replaced table
         from ..io.reader import ReadStats
         self.read_stats = ReadStats()            # part files read into HBM by this job
         self.transports: list = []      # (stage, edge kind, "device" | "object", bytes / reason)
@@ -1194,7 +1195,8 @@ class GpuJobRunner:
                     op_counts={f"{k[0]}:{k[1]}": v for k, v in self.op_counts.items()},
                     empty_host_ops=self.empty_host_ops,
                     placement=self.place, moved={f"{k[0]}:{k[1]}": v for k, v in self.moved.items()},
-                    write=dict(bytes=self.write_stats.bytes, seconds=round(self.write_stats.seconds, 4)),
+                    write=dict(bytes=self.write_stats.bytes, seconds=round(self.write_stats.seconds, 4),
+                               recycled_parts=self.recycled_parts),
                     read=dict(bytes=self.read_stats.bytes, seconds=round(self.read_stats.seconds, 4)),
                     sort_path=getattr(self, "last_sort_path", None),
                     exchange=(self.last_sort_stats.exchange_report() if getattr(self, "last_sort_stats", None)
@@ -1804,6 +1806,7 @@ def _write_split(runner, tmp: str, data, n: int, rec: int):
     """Write ``n`` fixed-width records of ``rec`` bytes (``data``) to the part file ``tmp``, or, with
     ``PartFileSplitBytes`` set and at least that many bytes, to several part files at once split at
     record boundaries (io/writer.write_device_pieces).  Returns the tmp path or the list of them."""
+    from ..io import partfile as PF
     from ..io import writer as WR
     split = int(runner.ctx.PartFileSplitBytes or 0)
     nbytes = n * rec
@@ -1814,7 +1817,10 @@ def _write_split(runner, tmp: str, data, n: int, rec: int):
     per = -(-n // k)
     bounds = [min(n, j * per) * rec for j in range(k + 1)]
     paths = [f"{tmp}.{j}" for j in range(k)]
-    WR.write_device_pieces(paths, data, bounds, stats=runner.write_stats)
+    # parts of a table this job replaced are overwritten in place (io/partfile.py RECYCLE_DIR)
+    got = PF.claim_recycled(paths)
+    runner.recycled_parts += got
+    WR.write_device_pieces(paths, data, bounds, stats=runner.write_stats, reuse=got > 0)
     return paths
 
 

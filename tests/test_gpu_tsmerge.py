@@ -53,6 +53,9 @@ def test_tile_merge_orders_buckets_and_flags_overflow():
     W, K, fb = 3, 40, 24
     cnt = g.integers(0, 120, size=(W, K)).astype(np.int32)
     cnt[1, 7] = 1100                              # a bucket past one workgroup's capacity
+    cnt[:, 11] = [300, 300, 300]                  # past the LDS stage: the register-path kernel
+    cnt[:, 13] = [300, 300, 136]                  # exactly the LDS stage (736 rows)
+    cnt[:, 17] = [0, 1024, 0]                     # exactly the capacity, one source
     total = int(cnt.sum())
     rows = g.integers(0, 256, size=(total, 100), dtype=np.uint8)
     # rows of bucket k share their top fb key bits: bucket id in the first 24 bits, random below
