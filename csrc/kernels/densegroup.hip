@@ -131,19 +131,19 @@ __global__ __launch_bounds__(256) void dg_count_kernel(const int64_t* __restrict
 }
 
 // Stable partition of rows [beg, end) of each workgroup by digit; offsets[d * G + b] = first output
-// row of workgroup b's bucket d (exclusive prefix of the bucket-major counts).  The next tile's
-// inputs are loaded while the current tile is ranked and written.
+// row of workgroup b's bucket d (exclusive prefix of the bucket-major counts).
 template <bool FROM_COLS, int DB>
-__global__ __launch_bounds__(kDgThreads) void dg_scatter_kernel(DgPack pk, const uint4* __restrict__ in, uint64_t n,
+__global__ __launch_bounds__(kDgThreads) __attribute__((amdgpu_waves_per_eu(4))) void dg_scatter_kernel(DgPack pk, const uint4* __restrict__ in, uint64_t n,
                                                          uint32_t shift, const int64_t* __restrict__ offsets, uint32_t G,
                                                          uint64_t per_block, uint4* __restrict__ out) {
   constexpr uint32_t nb = 1u << DB, mask = nb - 1;
   constexpr int kPer = (nb + kDgThreads - 1) / kDgThreads;   // buckets per thread in the scans
+  // 16-bit wave counts and bucket starts (<= kDgTile) and no per-slot digit array (recomputed from
+  // the staged row): 77 KB of LDS at DB = 9, two workgroups per CU
   __shared__ uint4 tile[kDgTile];
-  __shared__ uint16_t dslot[kDgTile];
-  __shared__ uint32_t wcnt[kDgWaves][nb];
+  __shared__ uint16_t wcnt[kDgWaves][nb];
   __shared__ int64_t goff[nb];
-  __shared__ uint32_t bstart[nb];
+  __shared__ uint16_t bstart[nb];
   __shared__ uint32_t sc[kDgWaves];
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   const uint64_t beg = (uint64_t)blockIdx.x * per_block;
@@ -170,9 +170,11 @@ __global__ __launch_bounds__(kDgThreads) void dg_scatter_kernel(DgPack pk, const
       }
     }
   };
-  load_raw(beg);
   for (uint64_t base = beg; base < end; base += kDgTile) {
     const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kDgTile ? (end - base) : kDgTile);
+    // two workgroups per CU: the other one's tile overlaps this one's loads (a register prefetch
+    // of the next tile would need ~150-180 VGPRs, one workgroup per CU)
+    load_raw(base);
     for (uint32_t i = t; i < kDgWaves * nb; i += kDgThreads) (&wcnt[0][0])[i] = 0;
     uint4 rv[kDgItems];
 #pragma unroll
@@ -192,7 +194,6 @@ __global__ __launch_bounds__(kDgThreads) void dg_scatter_kernel(DgPack pk, const
         rv[r] = rawr[r];
       }
     }
-    if (base + kDgTile < end) load_raw(base + kDgTile);   // next tile in flight
     __syncthreads();
     uint32_t rk[kDgItems], dg[kDgItems];
 #pragma unroll
@@ -212,7 +213,7 @@ __global__ __launch_bounds__(kDgThreads) void dg_scatter_kernel(DgPack pk, const
       const uint32_t below = popc_below(peers);
       const uint32_t prior = wcnt[w][d];
       __builtin_amdgcn_wave_barrier();
-      if (valid && below == 0) wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      if (valid && below == 0) wcnt[w][d] = (uint16_t)(prior + (uint32_t)__popcll(peers));
       __builtin_amdgcn_wave_barrier();
       rk[r] = prior + below;
       dg[r] = d;
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(kDgThreads) void dg_scatter_kernel(DgPack pk, const
 #pragma unroll
         for (int k = 0; k < kDgWaves; ++k) {
           const uint32_t c = wcnt[k][b];
-          wcnt[k][b] = acc;
+          wcnt[k][b] = (uint16_t)acc;
           acc += c;
         }
         tot[q] = acc;
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(kDgThreads) void dg_scatter_kernel(DgPack pk, const
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const uint32_t b = t * kPer + q;
-      if (b < nb) bstart[b] = pre;
+      if (b < nb) bstart[b] = (uint16_t)pre;
       pre += tot[q];
     }
     __syncthreads();
@@ -249,16 +250,17 @@ __global__ __launch_bounds__(kDgThreads) void dg_scatter_kernel(DgPack pk, const
     for (int r = 0; r < kDgItems; ++r) {
       const uint32_t pos = w * (kDgTile / kDgWaves) + r * 64 + l;
       if (pos < cnt) {
-        const uint32_t slot = bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
+        const uint32_t slot = (uint32_t)bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
         tile[slot] = rv[r];
-        dslot[slot] = (uint16_t)dg[r];
       }
     }
     __syncthreads();
     // consecutive slots of one bucket are consecutive output rows
+#pragma unroll 4
     for (uint32_t j = t; j < cnt; j += kDgThreads) {
-      const uint32_t d = dslot[j];
-      out[goff[d] + (int64_t)(j - bstart[d])] = tile[j];
+      const uint4 v = tile[j];
+      const uint32_t d = (uint32_t)((((((uint64_t)v.y << 32) | v.x) & kmask) >> shift) & mask);
+      out[goff[d] + (int64_t)(j - bstart[d])] = v;
     }
     __syncthreads();
 #pragma unroll

@@ -272,7 +272,13 @@ __global__ void sq_norms_kernel(const float* __restrict__ C, int K, float* __res
 // Lane map (32x32x16 bf16): A[row r][k = 8h + j], B[k = 8h + j][col r], C col = l & 31,
 // row = (g & 3) + 8 (g >> 2) + 4 h.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-constexpr int kCRow = 136;   // bf16 per centroid row in LDS (272 B: b128 reads spread over banks)
+#ifndef DR_KM_CROW
+#define DR_KM_CROW 144
+#endif
+// bf16 per centroid row in LDS: 288 B = 72 dwords, so the 16-byte fragment reads (lane (r, g) at
+// row r, dims 32 s + 8 g) of every ds_read_b128 lane group hit 16 distinct 4-bank sets (136, the
+// previous pitch: 2-way conflicts in each group, ~1e9 conflict cycles per assignment call)
+constexpr int kCRow = DR_KM_CROW;
 constexpr int kXRow = 132;   // floats per point row of the LDS tile
 // |estimate - f32 distance| <= kKmTol |x| max|c|: bf16 split residuals 3 * 2^-16 plus f32
 // accumulation over 384 products (2.3e-5), both relative to sum |x_i c_i| <= |x| |c|, doubled.

@@ -207,9 +207,12 @@ class TeraSortStoredJob:
         return self.prepared
 
     def step(self):
-        self.ctx.FromStore(self.src).OrderBy(lambda r: r[0:10]).ToStore(self.dst, delete_if_exists=True) \
-            .SubmitAndWait()
-        self.res = self.ctx._get_executor().last_result or {}
+        t0 = time.perf_counter()
+        q = self.ctx.FromStore(self.src).OrderBy(lambda r: r[0:10]).ToStore(self.dst, delete_if_exists=True)
+        t1 = time.perf_counter()
+        q.SubmitAndWait()
+        self.res = dict(self.ctx._get_executor().last_result or {})
+        self.res["submit_s"] = dict(build_query=round(t1 - t0, 4), submit_and_wait=round(time.perf_counter() - t1, 4))
 
     def report(self) -> dict:
         r = self.res or {}
@@ -224,6 +227,7 @@ class TeraSortStoredJob:
                     write_recycled_parts=wr.get("recycled_parts", 0),
                     sort_stage_s_excl_read=round(max(0.0, stage - (rd.get("seconds") or 0)), 3),
                     sort_path=r.get("sort_path"), timings=tm, fallbacks=r.get("fallbacks"),
+                    job_phases_s=r.get("phases"), submit_and_wait_s=r.get("submit_s"),
                     prepare=self.prepared)
 
     input_checksum = TeraSortQueryJob.input_checksum

@@ -149,6 +149,16 @@ class SortStats:
         return out
 
 
+def invert_keys(e: torch.Tensor, key_len: int) -> torch.Tensor:
+    """Invert the key bits (not the row index / tie bits) of E128 entries in place, so that an
+    ascending radix sort of them orders the keys descending (OrderByDescending)."""
+    _, _, lo_mask = key_bits(key_len)
+    e[:, 1].bitwise_not_()
+    if lo_mask:
+        e[:, 0].bitwise_xor_(torch.tensor(_as_i64(lo_mask), dtype=torch.int64, device=e.device))
+    return e
+
+
 def local_sort_rows(rows: torch.Tensor, out: torch.Tensor, ent_a: torch.Tensor, ent_b: torch.Tensor,
                     key_off: int, key_len: int, descending: bool = False,
                     hi_bounds: tuple[int, int] | None = None, keys_ready: bool = False,
@@ -176,12 +186,7 @@ def local_sort_rows(rows: torch.Tensor, out: torch.Tensor, ent_a: torch.Tensor, 
         keys_ready = False
     e = ent_a[:n] if keys_ready else S.extract_keys(rows, key_off, key_len, 0, out=ent_a[:n])
     if descending:
-        # invert the key bits (not the row index) so an ascending radix sort yields descending keys
-        b0, _, lo_mask = key_bits(key_len)
-        e[:, 1].bitwise_not_()
-        if lo_mask:
-            e[:, 0].bitwise_xor_(torch.tensor(lo_mask - (1 << 64) if lo_mask >= (1 << 63) else lo_mask,
-                                              dtype=torch.int64, device=e.device))
+        invert_keys(e, key_len)
     b0, b1, _ = key_bits(key_len)
     if SORT_ALGO == "hybrid":
         srt = S.sort_entries_hybrid(e, b0, b1, tmp=ent_b[:n], hi_bounds=None if descending else hi_bounds)
@@ -270,10 +275,13 @@ def _range_hi_bounds(seps_hi: list, g: int) -> tuple[int, int]:
 
 
 def _sort_keys(rows: torch.Tensor, ent: torch.Tensor, tmp: torch.Tensor, key_off: int, key_len: int,
-               hi_bounds) -> torch.Tensor:
+               hi_bounds, descending: bool = False) -> torch.Tensor:
     """Extract + sort the entries of ``rows`` (row indices relative to ``rows``); returns the
     tensor holding the sorted entries (``ent`` or ``tmp``)."""
     e = S.extract_keys(rows, key_off, key_len, 0, out=ent)
+    if descending:
+        invert_keys(e, key_len)
+        hi_bounds = None
     b0, b1, _ = key_bits(key_len)
     if SORT_ALGO == "hybrid":
         return S.sort_entries_hybrid(e, b0, b1, tmp=tmp, hi_bounds=hi_bounds)
@@ -324,7 +332,7 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
                           stats: SortStats | None = None, keys_ready: bool = False,
                           hi_bounds: tuple[int, int] | None = None, split_ties: bool = True,
                           keys_fmt: str = "e128", gen: tuple[int, int] | None = None,
-                          src: torch.Tensor | None = None) -> torch.Tensor:
+                          src: torch.Tensor | None = None, descending: bool = False) -> torch.Tensor:
     """Globally sort the first ``n`` rows of ``bufs.rows_in`` (or of ``src``, a table read in
     place and left intact) across all ranks.
 
@@ -335,7 +343,9 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     bytes, see SortBuffers.entry_pair); ``hi_bounds``: known hi range of the local keys.
     ``split_ties``: runs of equal keys may be split over ranks (skew); keeps the global order but
     not the co-location of equal keys, so the planner turns it off (keep_ties) when a consumer
-    relies on the output being partitioned by the key.
+    relies on the output being partitioned by the key.  ``descending`` (OrderByDescending): the
+    E128 path with the key bits of the entries inverted (rank 0 receives the largest keys; ties
+    stay in (rank, row) order), every received round sorted by its inverted keys.
 
     Three send sides:
       * fine-bucket exchange over the materialised table (TeraSort rows, the default for such
@@ -366,7 +376,9 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     if src is not None:
         assert src.shape[1] == rec and gen is None and not keys_ready, "src: [n, record width] rows, no producer keys"
         pitch = rec
-    gen_path = gen is not None and fine_rows_ok(rec, pitch, key_off, key_len, W, n) and pitch == rec
+    if descending:
+        hi_bounds = None              # bounds of the ascending keys
+    gen_path = gen is not None and fine_rows_ok(rec, pitch, key_off, key_len, W, n) and pitch == rec and not descending
     if gen is not None and not gen_path:
         TSG.generate(bufs.rows_in[:n], gen[0], gen[1])       # the records are needed after all
         gen = None
@@ -377,16 +389,19 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
             bufs.rows_in[:n].copy_(src[:n])
             rows = bufs.rows_in[:n]
         if pitch != rec:
+            if descending:
+                raise ValueError("distributed_sort_rows: a 128-byte-pitch table sorts ascending only")
             out = S.sort_rows_pitch128(bufs.rows_in[:n], bufs.rows_out, bufs.ent_a, key_off, key_len,
                                        keys_ready=keys_ready and keys_fmt == "e64")
         else:
             out = local_sort_rows(rows, bufs.rows_out, bufs.ent_a, bufs.ent_b, key_off, key_len,
-                                  hi_bounds=hi_bounds, keys_ready=keys_ready, keys_fmt=keys_fmt)
+                                  descending=descending, hi_bounds=hi_bounds, keys_ready=keys_ready,
+                                  keys_fmt=keys_fmt)
         if stats is not None:
             stats.n_in = stats.n_out = n
             stats.path = "local"
         return out
-    fine_rows = gen is None and fine_rows_ok(rec, pitch, key_off, key_len, W, n)
+    fine_rows = gen is None and fine_rows_ok(rec, pitch, key_off, key_len, W, n) and not descending
     if pitch != bufs.pitch and not fine_rows:
         raise ValueError("distributed_sort_rows: a src table needs a buffer set at its record width")
     if pitch != rec and not fine_rows:
@@ -416,6 +431,8 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
             if keys_fmt != "e128":
                 keys_ready = False
             ent = bufs.ent_a[:n] if keys_ready else S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
+            if descending:
+                invert_keys(ent, key_len)
             if split:
                 ent[:, 0].bitwise_or_(lo_or)
     except Exception as ex:  # noqa: BLE001
@@ -501,7 +518,8 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     if fine is not None:
         out = merge_received_rounds(rb, off, fine, L, fb, B, w.rank, sent_after, n_sent, wait=wait)
     else:
-        out = sort_received_rounds(rb, off, sent_after, n_sent, seps_hi, B, w.rank, key_off, key_len, wait=wait)
+        out = sort_received_rounds(rb, off, sent_after, n_sent, seps_hi, B, w.rank, key_off, key_len, wait=wait,
+                                   descending=descending)
     if ev:
         ev["done"].record()
     if fine_rows and int(bad.item()):
@@ -754,7 +772,7 @@ def _round_scratch(bufs: SortBuffers, n_recv: int, a: int, z: int) -> tuple[torc
 
 
 def sort_received_rounds(bufs: SortBuffers, off: list, sent_after: list, n_sent: int, seps_hi: list, B: int,
-                         rank: int, key_off: int, key_len: int, wait=None) -> torch.Tensor:
+                         rank: int, key_off: int, key_len: int, wait=None, descending: bool = False) -> torch.Tensor:
     """Receive side of the pipelined range shuffle: round b's block ``rows_in[off[b]:off[b+1]]``
     holds all rows of this rank's key range b.  Each is sorted as it arrives (``wait(b)``): E64
     entries of the rows read through LDS with the look-back sort's histograms fused in, the
@@ -764,7 +782,7 @@ def sort_received_rounds(bufs: SortBuffers, off: list, sent_after: list, n_sent:
     for the fix-up is redone after the last round (count + scatter sort, or the full-key sort)."""
     out = bufs.rows_out
     e64a, e64b = bufs.ent_a.view(-1), bufs.ent_b.view(-1)
-    compact = S.compact_sort_ok(bufs.rows_in[:2], key_len)
+    compact = S.compact_sort_ok(bufs.rows_in[:2], key_len) and not descending
     flags = torch.zeros((B, 2), dtype=torch.int32, device=out.device)     # [gather overflow, look-back error]
     pending, compact_rounds = [], []
     for b in range(B):
@@ -782,7 +800,8 @@ def sort_received_rounds(bufs: SortBuffers, off: list, sent_after: list, n_sent:
                 pending.append((a, z, b, ("e64", srt, win)))
                 compact_rounds.append((a, z, b, P, win))
             else:
-                srt = _sort_keys(bufs.rows_in[a:z], bufs.ent_a[a:z], bufs.ent_b[a:z], key_off, key_len, hb)
+                srt = _sort_keys(bufs.rows_in[a:z], bufs.ent_a[a:z], bufs.ent_b[a:z], key_off, key_len, hb,
+                                 descending=descending)
                 pending.append((a, z, b, ("e128", srt, 0)))
         keep = []
         for a2, z2, b2, (fmt, s2, win) in pending:

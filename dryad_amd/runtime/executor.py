@@ -67,6 +67,8 @@ class _BaseExecutor:
         """Per-thread setup of a job thread (the GPU executor binds it to its rank's device)."""
 
     def submit(self, outs, handle):
+        handle.t_submit = time.perf_counter()
+
         def body():
             try:
                 self._enter_job_thread()

@@ -185,6 +185,7 @@ class GpuJobRunner:
         from ..io.writer import WriteStats
         self.write_stats = WriteStats()          # partfile parts written by this job
         self.recycled_parts = 0                  # of them, recycled parts of a replaced table
+        self.phases: dict = {}                   # host seconds: setup / stages / commit (run_job: compile, total)
         from ..io.reader import ReadStats
         self.read_stats = ReadStats()            # part files read into HBM by this job
         self.transports: list = []      # (stage, edge kind, "device" | "object", bytes / reason)
@@ -324,7 +325,7 @@ class GpuJobRunner:
             if ok:
                 try:
                     kind, spec = TR.key_columns(TR.call(f["key"], t), t)
-                    ok = kind == "bytes" and spec.length <= 12 and not f["desc"]
+                    ok = kind == "bytes" and spec.length <= 12
                 except Exception:  # noqa: BLE001
                     ok = False
                 if not ok:
@@ -449,7 +450,8 @@ class GpuJobRunner:
         out = RS.distributed_sort_rows(bs.bufs, t.n, off, ln, self.world, stats=stats,
                                        keys_ready=kr is not None, hi_bounds=None if kr is None else kr[:2],
                                        split_ties=not f.get("keep_ties", False),
-                                       keys_fmt="e128" if kr is None else kr[2], gen=gen, src=src)
+                                       keys_fmt="e128" if kr is None else kr[2], gen=gen, src=src,
+                                       descending=bool(f.get("desc", False)))
         self.row_sets[(m.id, me)] = bs
         self.last_sort_stats = stats
         table = DeviceTable(out.shape[0], t.shape, rows=out)
@@ -1089,6 +1091,8 @@ class GpuJobRunner:
         join_first = {min(d["stages"]): jid for jid, d in list(self.fused_joins.items()) + list(self.grace_joins.items())}
         precomputed = {}
         stage_events = []          # (timing key, host seconds, start event, end event)
+        t_stages = time.time()
+        self.phases["setup"] = t_stages - t_start
         for s in self.plan.stages:
             t0 = time.time()
             ev0 = None
@@ -1187,16 +1191,20 @@ class GpuJobRunner:
             stage_events[-1][3].synchronize()
             for key, host_s, ev0, ev1 in stage_events:
                 self.timings[key] = max(host_s, ev0.elapsed_time(ev1) / 1e3)
+        t_commit = time.time()
+        self.phases["stages"] = t_commit - t_stages
         committed = self._commit()
         if self.pool is not None:
             for b in set(self.row_sets.values()):
                 self.pool.release(b)
+        self.phases["commit"] = time.time() - t_commit
         return dict(committed=committed, fallbacks=self.fallbacks, timings=self.timings, transports=self.transports,
                     op_counts={f"{k[0]}:{k[1]}": v for k, v in self.op_counts.items()},
                     empty_host_ops=self.empty_host_ops,
                     placement=self.place, moved={f"{k[0]}:{k[1]}": v for k, v in self.moved.items()},
                     write=dict(bytes=self.write_stats.bytes, seconds=round(self.write_stats.seconds, 4),
                                recycled_parts=self.recycled_parts),
+                    phases={k: round(v, 4) for k, v in self.phases.items()},
                     read=dict(bytes=self.read_stats.bytes, seconds=round(self.read_stats.seconds, 4)),
                     sort_path=getattr(self, "last_sort_path", None),
                     exchange=(self.last_sort_stats.exchange_report() if getattr(self, "last_sort_stats", None)
@@ -1916,7 +1924,9 @@ class GpuExecutor(_BaseExecutor):
         dev = self.world.device
         if dev.type == "cuda" and dev.index is not None and torch.cuda.current_device() != dev.index:
             torch.cuda.set_device(dev)
+        t_job = time.perf_counter()
         plan = compile_queries(self.ctx, outs)
+        t_compiled = time.perf_counter()
         faults = self.ctx._props.get("FaultInjection") or []
         for st in plan.stages:      # CheckExistence(deleteIfExists) at submission
             if st.is_output and st.output["uri"].startswith(("hbm://", "host://")):
@@ -1960,6 +1970,10 @@ class GpuExecutor(_BaseExecutor):
                       transports=res.get("transports"), recovery=res.get("recovery"))
             _JOB_DIR_WRITER.submit(_write_json, os.path.join(job_dir, "statistics.json"), st)
         self.last_job_dir = job_dir
+        t_sub = getattr(handle, "t_submit", None)
+        res.setdefault("phases", {}).update(compile=round(t_compiled - t_job, 4),
+                                            job=round(time.perf_counter() - t_job, 4),
+                                            queued=None if t_sub is None else round(t_job - t_sub, 4))
         self.last_result = res
         self.job_log.append(dict(fallbacks=list(res["fallbacks"]), op_counts=dict(res["op_counts"])))
         self.last_plan = plan

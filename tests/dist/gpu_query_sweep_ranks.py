@@ -55,6 +55,11 @@ def queries():
                       True),
         "terasort_bytes": (lambda c, W: c.FromStore(ts % W).OrderBy(lambda r: r[0:10]).Select(lambda r: r[0:10]),
                            True),
+        # the fused distributed OrderBy, descending: inverted E128 keys, ties in (partition, row) order
+        "terasort_bytes_desc": (lambda c, W: c.FromStore(ts % W).OrderByDescending(lambda r: r[0:10]).Select(
+            lambda r: r[0:10]), True),
+        "terasort_desc_ties": (lambda c, W: c.FromStore(ts % W).OrderByDescending(lambda r: r[0:1]).Select(
+            lambda r: r[0:10]), True),
         "terasort_where_take": (lambda c, W: c.FromStore(ts % W).Where(lambda r: r[0] < 16).Select(lambda r: r[0:4]),
                                 False),
         "hash_partition": (lambda c, W: c.FromEnumerable(DATA).HashPartition(lambda x: x % 37, 4), False),

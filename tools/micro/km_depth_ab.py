@@ -29,7 +29,9 @@ def main():
     sp = KM.split_points(x)
     ws = KM.KMeansWorkspace(n, k, dev)
     here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_km_ab")
-    libs = sorted(f for f in os.listdir(here) if f.endswith(".so"))
+    libs = sorted(f for f in os.listdir(here) if f.endswith(".so")) if os.path.isdir(here) else []
+    if os.environ.get("KM_AB_ONLY_IN_TREE"):
+        libs = []
     ref = None
     for name in ["in-tree"] + libs:
         if name == "in-tree":
