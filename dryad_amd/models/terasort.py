@@ -183,6 +183,7 @@ class TeraSortStoredJob:
         self.gen = f"gen://terasort?records={self.n * W}&partitions={W}&seed={cfg.seed}"
         self.res = None
         self.prepared = None
+        self.step_log = []             # per step: seconds, read / write / stage / commit split
 
     @property
     def bytes_per_rank(self) -> int:
@@ -213,6 +214,10 @@ class TeraSortStoredJob:
         q.SubmitAndWait()
         self.res = dict(self.ctx._get_executor().last_result or {})
         self.res["submit_s"] = dict(build_query=round(t1 - t0, 4), submit_and_wait=round(time.perf_counter() - t1, 4))
+        ph = self.res.get("phases") or {}
+        self.step_log.append(dict(step_s=round(time.perf_counter() - t0, 4), read_s=(self.res.get("read") or {}).get("seconds"),
+                                  write_s=(self.res.get("write") or {}).get("seconds"), stages_s=ph.get("stages"),
+                                  commit_s=ph.get("commit")))
 
     def report(self) -> dict:
         r = self.res or {}
@@ -227,7 +232,7 @@ class TeraSortStoredJob:
                     write_recycled_parts=wr.get("recycled_parts", 0),
                     sort_stage_s_excl_read=round(max(0.0, stage - (rd.get("seconds") or 0)), 3),
                     sort_path=r.get("sort_path"), timings=tm, fallbacks=r.get("fallbacks"),
-                    job_phases_s=r.get("phases"), submit_and_wait_s=r.get("submit_s"),
+                    job_phases_s=r.get("phases"), submit_and_wait_s=r.get("submit_s"), steps=self.step_log,
                     prepare=self.prepared)
 
     input_checksum = TeraSortQueryJob.input_checksum
