@@ -200,6 +200,16 @@ def claim_recycled(paths: list) -> int:
     return got
 
 
+def drop_recycled(base: str):
+    """Unlink (on a daemon thread) the recycled files of ``base``'s parts directory that the table
+    just written there did not claim: they would only hold disk space until their TTL."""
+    d = _recycle_dir(base)
+    if not os.path.isdir(d):
+        return
+    import threading
+    threading.Thread(target=_sweep, args=(d, 0.0), daemon=True, name="dryad-recycle-drop").start()
+
+
 def delete(meta_path: str, background: bool = False, recycle: bool = True):
     """Delete the table: every partition then the metadata (CheckExistence(deleteIfExists)).
     ``background``: the files are renamed out of the way at once (the table is gone and its

@@ -1807,6 +1807,8 @@ def _commit_partfile_impl(runner, s, uri, path, local):
             write_schema(path, dt, "binary")
     if W > 1:
         runner.world.barrier()
+    if me == 0:
+        PF.drop_recycled(base)          # every rank has claimed what it overwrote
     return True
 
 

@@ -63,3 +63,16 @@ def test_sweep_removes_stale_recycled_files(tmp_path):
     fresh.write_bytes(b"y")
     PF._sweep(str(d), 600)
     assert not old.exists() and fresh.exists()
+
+
+def test_drop_recycled_unlinks_unclaimed(tmp_path):
+    meta, base = _table(tmp_path, "v", [100, 200])
+    PF.delete(meta, background=True)
+    rdir = os.path.join(os.path.dirname(base), PF.RECYCLE_DIR)
+    assert len(os.listdir(rdir)) == 2
+    PF.drop_recycled(base)
+    for _ in range(100):
+        if not os.listdir(rdir):
+            break
+        time.sleep(0.02)
+    assert os.listdir(rdir) == []
