@@ -320,10 +320,11 @@ def _check_capacity(n_recv: int, cap: int, w: World):
             retryable=False, ranks=[r for r, _ in over])
 
 
-def fine_rows_ok(rec: int, pitch: int, key_off: int, key_len: int, W: int, n: int) -> bool:
+def fine_rows_ok(rec: int, pitch: int, key_off: int, key_len: int, W: int, n: int, one_rank: bool = False) -> bool:
     """The fine-bucket exchange applies: 100-byte records keyed by bytes 0..9 (TeraSort rows),
-    stored at a 100- or 128-byte pitch, 2..64 ranks (sources per merged bucket)."""
-    return (1 < W <= 64 and key_off == 0 and key_len == TSG.KEY_BYTES and rec == TSG.RECORD_BYTES
+    stored at a 100- or 128-byte pitch, 2..64 ranks (sources per merged bucket; ``one_rank``: a
+    one-rank world that still exchanges through its communicator)."""
+    return ((1 < W or (one_rank and W == 1)) and W <= 64 and key_off == 0 and key_len == TSG.KEY_BYTES and rec == TSG.RECORD_BYTES
             and pitch in (TSG.RECORD_BYTES, 128) and n < (1 << 31))
 
 
@@ -378,13 +379,14 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
         pitch = rec
     if descending:
         hi_bounds = None              # bounds of the ascending keys
-    gen_path = gen is not None and fine_rows_ok(rec, pitch, key_off, key_len, W, n) and pitch == rec and not descending
+    gen_path = gen is not None and fine_rows_ok(rec, pitch, key_off, key_len, W, n, w.force_collectives) \
+        and pitch == rec and not descending
     if gen is not None and not gen_path:
         TSG.generate(bufs.rows_in[:n], gen[0], gen[1])       # the records are needed after all
         gen = None
         if keys_fmt == "gen":
             keys_ready = False
-    if W == 1:
+    if not w.collective:
         if src is not None:
             bufs.rows_in[:n].copy_(src[:n])
             rows = bufs.rows_in[:n]
@@ -401,7 +403,8 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
             stats.n_in = stats.n_out = n
             stats.path = "local"
         return out
-    fine_rows = gen is None and fine_rows_ok(rec, pitch, key_off, key_len, W, n) and not descending
+    fine_rows = gen is None and fine_rows_ok(rec, pitch, key_off, key_len, W, n, w.force_collectives) \
+        and not descending
     if pitch != bufs.pitch and not fine_rows:
         raise ValueError("distributed_sort_rows: a src table needs a buffer set at its record width")
     if pitch != rec and not fine_rows:

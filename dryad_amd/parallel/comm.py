@@ -23,6 +23,14 @@ class World:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: str | None = None
+    # a one-rank world whose exchanges still go through the collectives (a one-rank RCCL
+    # communicator: tests run the multi-rank code paths against real RCCL on a one-GPU box)
+    force_collectives: bool = False
+
+    @property
+    def collective(self) -> bool:
+        """Data movement goes through the process group (several ranks, or force_collectives)."""
+        return self.size > 1 or self.force_collectives
 
     @property
     def distributed(self) -> bool:

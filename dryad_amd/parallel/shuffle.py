@@ -27,7 +27,7 @@ CHUNK_BYTES = 4 << 30         # per (source, destination) pair and round (tests 
 def exchange_counts(send_counts: torch.Tensor, world: World | None = None) -> torch.Tensor:
     """All-to-all of per-destination counts (int64 [world]).  Returns the receive counts."""
     w = world or get_world()
-    if w.size == 1:
+    if not w.collective:
         return send_counts.clone()
     dev = w.device if w.backend == "nccl" else torch.device("cpu")
     s = send_counts.to(dev, torch.int64).contiguous()
@@ -51,7 +51,7 @@ def alltoallv_bytes(send: torch.Tensor, send_counts: list[int], recv: torch.Tens
     in source-rank order."""
     w = world or get_world()
     assert send.dtype == torch.uint8 and recv.dtype == torch.uint8
-    if w.size == 1:
+    if not w.collective:
         n = send_counts[0]
         recv[:n].copy_(send[:n])
         return recv
@@ -117,7 +117,7 @@ def alltoallv_bytes_async(send: torch.Tensor, send_counts: list[int], recv: torc
     on the wire).  Other transports (gloo staging through the host, rounds chunked past
     CHUNK_BYTES per peer) complete before returning and give ``None``."""
     w = world or get_world()
-    if (w.size > 1 and _native(w, send, recv)
+    if (w.collective and _native(w, send, recv)
             and max(max(send_counts), max(recv_counts)) <= CHUNK_BYTES):
         ts, tr = sum(send_counts), sum(recv_counts)
         return dist.all_to_all_single(recv[:tr], send[:ts], output_split_sizes=list(recv_counts),
@@ -137,7 +137,7 @@ def gang_status(ok: bool, value: int = 0, world: World | None = None) -> list[tu
     before it enters a payload collective (ops/recordsort: a rank whose pre-exchange work failed,
     or whose key range overflows its receive buffer, says so here and every rank stops alike)."""
     w = world or get_world()
-    if w.size == 1:
+    if not w.collective:
         return [(bool(ok), int(value))]
     dev = w.device if w.backend == "nccl" else torch.device("cpu")
     t = torch.tensor([[1 if ok else 0, int(value)]], dtype=torch.int64, device=dev)
@@ -147,7 +147,7 @@ def gang_status(ok: bool, value: int = 0, world: World | None = None) -> list[tu
 def all_gather_tensor(t: torch.Tensor, world: World | None = None) -> torch.Tensor:
     """All-gather equally shaped tensors along dim 0 (R5: sampler gather, R3 broadcast of small data)."""
     w = world or get_world()
-    if w.size == 1:
+    if not w.collective:
         return t.clone()
     dev_ok = (w.backend == "nccl") == t.is_cuda
     src = t if dev_ok else (t.to(w.device) if w.backend == "nccl" else t.cpu())
@@ -159,7 +159,7 @@ def all_gather_tensor(t: torch.Tensor, world: World | None = None) -> torch.Tens
 def all_gather_varlen(t: torch.Tensor, world: World | None = None) -> torch.Tensor:
     """All-gather tensors whose dim 0 differs per rank."""
     w = world or get_world()
-    if w.size == 1:
+    if not w.collective:
         return t.clone()
     n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
     ns = all_gather_tensor(n, w).tolist()
@@ -173,7 +173,7 @@ def all_gather_varlen(t: torch.Tensor, world: World | None = None) -> torch.Tens
 
 def all_reduce_(t: torch.Tensor, op: str = "sum", world: World | None = None) -> torch.Tensor:
     w = world or get_world()
-    if w.size == 1:
+    if not w.collective:
         return t
     rop = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op]
     if (w.backend == "nccl") != t.is_cuda:
@@ -187,7 +187,7 @@ def all_reduce_(t: torch.Tensor, op: str = "sum", world: World | None = None) ->
 
 def broadcast_(t: torch.Tensor, src: int = 0, world: World | None = None) -> torch.Tensor:
     w = world or get_world()
-    if w.size == 1:
+    if not w.collective:
         return t
     if (w.backend == "nccl") != t.is_cuda:
         tmp = t.to(w.device) if w.backend == "nccl" else t.cpu()

@@ -100,3 +100,16 @@ def test_fine_rows_ranks_share_one_gpu(ranks, tmp_path):
     _dump(os.path.basename(out.args[-1]) + str(ranks), out)
     assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
     assert f"FINE_ROWS_OK {ranks}" in out.stdout
+
+
+@pytest.mark.timeout(300)
+def test_rccl_one_rank_runs_the_collective_paths():
+    """A one-rank RCCL communicator with force_collectives: the RCCL branches of the shuffle
+    primitives and of the fine-bucket / E128 distributed OrderBy, against real RCCL."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("DRYAD_DIST_BACKEND", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "dist", "rccl_one_rank.py")],
+                         capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    _dump("rccl_one_rank", out)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
+    assert "RCCL_ONE_RANK_OK" in out.stdout
