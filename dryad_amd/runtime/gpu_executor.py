@@ -1727,64 +1727,83 @@ def _commit_partfile_impl(runner, s, uri, path, local):
         runner.world.barrier()
     base = PF.default_base(path)
     os.makedirs(os.path.dirname(base) or ".", exist_ok=True)
-    mine, fmt_extra = {}, None
-    for p, v in local.items():
-        tmp = PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, 0)
-        if isinstance(v, GS.StreamedPart) and isinstance(v.path, list):    # split over part files
-            mine[p] = []
-            for j, f in enumerate(v.path):
-                os.replace(f, f"{tmp}.{j}")
-                mine[p].append(f"{tmp}.{j}")
-            continue
-        if isinstance(v, GS.StreamedPart):          # written bucket / chunk by chunk by its stage
-            os.replace(v.path, tmp)
-            if os.path.exists(v.path + PF.INDEX_SUFFIX):         # the block index of string records
-                os.replace(v.path + PF.INDEX_SUFFIX, tmp + PF.INDEX_SUFFIX)
-            if v.rows is not None:
-                fmt_extra = dict(v.rows)
-            mine[p] = tmp
-            continue
-        if rows_fmt:
-            # raw fixed-width rows: device rows or the pinned host tier (out-of-core sort output)
-            if isinstance(v, DeviceTable):
-                mine[p] = _write_split(runner, tmp, v.rows[: v.n], v.n, v.rows.shape[1])
-                fmt_extra = dict(stride=v.rows.shape[1], key_off=v.shape.key_off, key_len=v.shape.key_len)
+    mine = {}
+    state = dict(fmt_extra=None)
+
+    def write_parts():
+        for p, v in local.items():
+            tmp = PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, 0)
+            if isinstance(v, GS.StreamedPart) and isinstance(v.path, list):    # split over part files
+                mine[p] = []
+                for j, f in enumerate(v.path):
+                    os.replace(f, f"{tmp}.{j}")
+                    mine[p].append(f"{tmp}.{j}")
                 continue
-            if getattr(v, "path", None) and os.path.exists(v.path):
-                # disk tier: the rows already are a file; flush it and rename it into place
-                v.flush()
-                if v.n * v.stride != os.path.getsize(v.path):
-                    os.truncate(v.path, v.n * v.stride)
+            if isinstance(v, GS.StreamedPart):          # written bucket / chunk by chunk by its stage
                 os.replace(v.path, tmp)
-            else:
-                WR.write_device(tmp, v.rows[: v.n], stats=runner.write_stats)
-            fmt_extra = dict(stride=v.stride, key_off=v.key_off, key_len=v.key_len)
-            mine[p] = tmp
-            continue
-        data = CD.encode(v, dt) if isinstance(v, DeviceTable) and v.device.type == "cuda" else None
-        index = None
-        if data is None and isinstance(v, DeviceTable) and v.device.type == "cuda":
-            enc = CD.encode_var(v, dt)              # strings: device encoder + block index
-            if enc is not None:
-                data, boffs = enc
-                index = (v.n, data.numel(), boffs.cpu().numpy(), CD.BLOCK)
-        if runner.ctx.OutputDataCompressionScheme.value != 0:
-            import gzip
-            raw = data.cpu().numpy().tobytes() if data is not None else \
-                B.encode_records(dt, _to_objects(v) if not isinstance(v, list) else v)
-            with open(tmp, "wb") as f:
-                f.write(gzip.compress(raw, compresslevel=6))
-        elif data is not None:
-            # device-encoded records: HBM -> pinned ring -> native writer threads
-            if index is None and v.n and data.numel() % v.n == 0:      # fixed-width records
-                mine[p] = _write_split(runner, tmp, data, v.n, data.numel() // v.n)
+                if os.path.exists(v.path + PF.INDEX_SUFFIX):         # the block index of string records
+                    os.replace(v.path + PF.INDEX_SUFFIX, tmp + PF.INDEX_SUFFIX)
+                if v.rows is not None:
+                    state["fmt_extra"] = dict(v.rows)
+                mine[p] = tmp
                 continue
-            WR.write_device(tmp, data, stats=runner.write_stats)
-            if index is not None:
-                PF.write_index(tmp, index[0], index[1], index[2], index[3])
-        else:
-            B.write_records(tmp, dt, _to_objects(v) if not isinstance(v, list) else v)
-        mine[p] = tmp
+            if rows_fmt:
+                # raw fixed-width rows: device rows or the pinned host tier (out-of-core sort output)
+                if isinstance(v, DeviceTable):
+                    mine[p] = _write_split(runner, tmp, v.rows[: v.n], v.n, v.rows.shape[1])
+                    state["fmt_extra"] = dict(stride=v.rows.shape[1], key_off=v.shape.key_off, key_len=v.shape.key_len)
+                    continue
+                if getattr(v, "path", None) and os.path.exists(v.path):
+                    # disk tier: the rows already are a file; flush it and rename it into place
+                    v.flush()
+                    if v.n * v.stride != os.path.getsize(v.path):
+                        os.truncate(v.path, v.n * v.stride)
+                    os.replace(v.path, tmp)
+                else:
+                    WR.write_device(tmp, v.rows[: v.n], stats=runner.write_stats)
+                state["fmt_extra"] = dict(stride=v.stride, key_off=v.key_off, key_len=v.key_len)
+                mine[p] = tmp
+                continue
+            data = CD.encode(v, dt) if isinstance(v, DeviceTable) and v.device.type == "cuda" else None
+            index = None
+            if data is None and isinstance(v, DeviceTable) and v.device.type == "cuda":
+                enc = CD.encode_var(v, dt)              # strings: device encoder + block index
+                if enc is not None:
+                    data, boffs = enc
+                    index = (v.n, data.numel(), boffs.cpu().numpy(), CD.BLOCK)
+            if runner.ctx.OutputDataCompressionScheme.value != 0:
+                import gzip
+                raw = data.cpu().numpy().tobytes() if data is not None else \
+                    B.encode_records(dt, _to_objects(v) if not isinstance(v, list) else v)
+                with open(tmp, "wb") as f:
+                    f.write(gzip.compress(raw, compresslevel=6))
+            elif data is not None:
+                # device-encoded records: HBM -> pinned ring -> native writer threads
+                if index is None and v.n and data.numel() % v.n == 0:      # fixed-width records
+                    mine[p] = _write_split(runner, tmp, data, v.n, data.numel() // v.n)
+                    continue
+                WR.write_device(tmp, data, stats=runner.write_stats)
+                if index is not None:
+                    PF.write_index(tmp, index[0], index[1], index[2], index[3])
+            else:
+                B.write_records(tmp, dt, _to_objects(v) if not isinstance(v, list) else v)
+            mine[p] = tmp
+
+    try:
+        write_parts()
+    except BaseException:
+        # this rank's uncommitted part files (tmp, split pieces, block indexes) go with the failure
+        prefixes = [PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, 0) for p in local]
+        d = os.path.dirname(base) or "."
+        for fn in os.listdir(d):
+            q = os.path.join(d, fn)
+            if any(q.startswith(x) for x in prefixes):
+                try:
+                    os.remove(q)
+                except OSError:
+                    pass
+        raise
+    fmt_extra = state["fmt_extra"]
     gathered = [None] * W
     gathered_fmt = [None] * W
     if W > 1:
