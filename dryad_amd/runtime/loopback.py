@@ -80,9 +80,12 @@ class LoopbackRank:
     def step(self) -> dict:
         W, me, A, B = self.W, self.rank, self.A, self.B
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        torch.cuda.reset_peak_memory_stats(self.dev)
+        base = torch.cuda.memory_allocated(self.dev)
         ev[0].record()
         mine = self._run(A, me, None, A.ops)                 # read -> ... -> partition: this rank's work
         ev[1].record()
+        peak_a = torch.cuda.max_memory_allocated(self.dev) - base
         if not isinstance(mine, Ported):
             raise ValueError("loopback: stage A does not end in a partitioning operator")
         sent = sum(_nbytes(mine.port(p)) for p in range(mine.nports) if p % W != me)
@@ -99,12 +102,18 @@ class LoopbackRank:
         recv_bytes = _nbytes(recv)
         ops = [o for o in B.ops if o["op"] != "output"]
         torch.cuda.synchronize(self.dev)
+        torch.cuda.reset_peak_memory_stats(self.dev)
+        base_b = torch.cuda.memory_allocated(self.dev)
         ev[2].record()
         self.out = self._run(B, me, recv, ops)
         ev[3].record()
         torch.cuda.synchronize(self.dev)
+        peak_b = torch.cuda.max_memory_allocated(self.dev) - base_b + recv_bytes
         self.phases = {"stage_a_ms": ev[0].elapsed_time(ev[1]), "stage_b_ms": ev[2].elapsed_time(ev[3])}
-        self.bytes = {"sent_bytes": sent, "received_bytes": recv_bytes, "received_rows": recv.n}
+        # HBM working set of each timed stage (caching-allocator peaks above what was live before
+        # it; stage B counts the received table it consumes)
+        self.bytes = {"sent_bytes": sent, "received_bytes": recv_bytes, "received_rows": recv.n,
+                      "hbm_stage_a_GB": round(peak_a / 1e9, 2), "hbm_stage_b_GB": round(peak_b / 1e9, 2)}
         return self.phases
 
     @property
