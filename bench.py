@@ -77,6 +77,10 @@ def main():
                          "generator first, untimed, if absent) and write the sorted table to --output; with "
                          "--loopback-ranks: the rank's input table is read from it (one part, written if absent)")
     ap.add_argument("--output", default=None, help="with --input: the output partfile:// table")
+    ap.add_argument("--rccl-one-rank", action="store_true",
+                    help="rehearsal: one rank over a one-rank RCCL communicator that still runs the multi-rank "
+                         "program (sampled range shuffle, fine-bucket exchange through RCCL all-to-all-v, votes) "
+                         "at the full per-GPU size: the HBM working set and the RCCL path of an N-GPU run")
     args = ap.parse_args()
     env = check_env(args.rehearsal)
     if args.loopback_ranks:
@@ -87,7 +91,14 @@ def main():
     from dryad_amd.models.terasort import (TeraSortConfig, TeraSortJob, TeraSortOOCJob, TeraSortQueryJob,
                                            TeraSortStoredJob, RECORD, run_steps)
 
-    world = init_world(device="cuda")
+    if args.rccl_one_rank:
+        if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+            print("[bench] --rccl-one-rank runs without torchrun (one rank)", file=sys.stderr)
+            sys.exit(2)
+        from dryad_amd.parallel.comm import init_one_rank_rccl
+        world = init_one_rank_rccl()
+    else:
+        world = init_world(device="cuda")
     if world.size != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world.size}", file=sys.stderr)
     records = args.records_per_gpu
@@ -155,7 +166,7 @@ def main():
                 "total_bytes": total_bytes,
                 "validated": None if val is None else val["ok"],
                 "env": env,
-                "rehearsal": bool(args.rehearsal),
+                "rehearsal": bool(args.rehearsal or args.rccl_one_rank),
                 "path": ("out-of-core hybrid external sort (HBM-resident buckets + pinned host DRAM)" if ooc else
                          "direct" if args.direct else
                          "DryadLINQ query -> GPU executor (fused OrderBy gang stage)" if world.size > 1 else
@@ -175,6 +186,13 @@ def main():
         }
         if val is not None and not val["ok"]:
             line["validation"] = val
+        if args.rccl_one_rank:
+            line["metric"] = METRIC + " [one-rank RCCL rehearsal of the multi-rank program]"
+            line["config"]["path"] = ("DryadLINQ query -> GPU executor (fused OrderBy gang stage) over a one-rank RCCL "
+                                      "communicator: sampler, fine-bucket send side, RCCL all-to-all-v rounds to "
+                                      "itself, tile merge")
+            line["config"]["hbm_free_after_step_GB"] = round(torch.cuda.mem_get_info(world.device)[0] / 1e9, 2)
+            line["config"]["hbm_peak_allocated_GB"] = round(torch.cuda.max_memory_allocated(world.device) / 1e9, 2)
         if stored:
             line["metric"] = METRIC + " [stored-data variant: partfile in -> sort -> partfile out]"
             line["vs_baseline"] = round(gbps / BASELINE_GBPS, 3)

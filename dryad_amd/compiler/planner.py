@@ -296,7 +296,7 @@ class Planner:
         if src.info.order is not None and src.info.order.is_ordered_by(key, cmp, desc) and (
                 src.partitions == 1 or src.info.partition.kind == PartitionType.RANGE and src.info.partition.is_partitioned_by(key)):
             return src
-        if src.partitions == 1:
+        if src.partitions == 1 and not self.ctx._props.get("ExchangeOneRank", False):
             info = DataSetInfo(PartitionInfo.random(1), OrderInfo(key, cmp, desc), src.info.distinct)
             return self.pointwise(src, "OrderBy", [sort_op], info, dtype=src.dtype)
         if src.info.partition.kind == PartitionType.RANGE and src.info.partition.is_partitioned_by(key, cmp) \

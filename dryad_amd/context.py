@@ -133,6 +133,8 @@ _DEFAULTS = dict(
     GroupByAggregation="auto",    # single-integer-key GroupBy: "auto" (radix aggregation for keys spanning
     #                               >= 2^32 values), "radix" or "sort" (ops/tuning.py)
     ShuffleSlack=0.01,            # receive-buffer headroom of a range-partitioned exchange
+    ExchangeOneRank=False,        # plan a one-partition OrderBy as the sampled range shuffle, so a one-rank
+    #                               RCCL communicator (World.force_collectives) runs the multi-rank program
     PersistStageOutputs=None,     # GPU executor: copy completed stage outputs to a checkpoint store so a
     #                               relaunched gang resumes there (None: under a relaunching launcher;
     #                               a directory or True: always; False: never; runtime/checkpoint.py)

@@ -118,6 +118,9 @@ class TeraSortQueryJob:
         # default: the input table is materialised (128-byte pitch, as on one GPU) and the
         # fine-bucket exchange reads it; GenFusedShuffle generates the records into the send rows
         self.ctx.GenFusedShuffle = bool(gen_fused)
+        # a one-rank RCCL communicator that still exchanges (bench.py --rccl-one-rank): the one
+        # partition's OrderBy is planned as the sampled range shuffle of a multi-rank job
+        self.ctx.ExchangeOneRank = bool(self.world.force_collectives)
         self.src = f"gen://terasort?records={self.n * W}&partitions={W}&seed={cfg.seed}"
         self.out = None
 

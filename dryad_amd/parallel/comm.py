@@ -95,7 +95,41 @@ def init_world(device: str | None = None, backend: str | None = None, timeout_s:
             kwargs["device_id"] = dev
             os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         dist.init_process_group(**kwargs)
+        if be == "nccl":
+            warm_collectives(dev, size)
     _WORLD = World(rank=rank, size=size, local_rank=local_rank, device=dev, backend=be if size > 1 else None)
+    return _WORLD
+
+
+def warm_collectives(dev: torch.device, size: int):
+    """One small all-to-all, all-gather and all-reduce right after the communicator is created:
+    RCCL connects its point-to-point channels (and allocates their buffers) on a peer's first
+    send / receive, so this happens before a job fills HBM with its working set, not inside the
+    first 100 GB exchange with a few GB left."""
+    x = torch.arange(size, dtype=torch.int32, device=dev)
+    y = torch.empty_like(x)
+    dist.all_to_all_single(y, x)
+    g = torch.empty(size, dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(g, x[:1].contiguous())
+    dist.all_reduce(y)
+    torch.cuda.synchronize(dev)
+
+
+def init_one_rank_rccl(device_index: int = 0, timeout_s: int = COLLECTIVE_TIMEOUT_S) -> World:
+    """A one-rank RCCL communicator whose World still exchanges through it (force_collectives):
+    the multi-rank program (sampler all-gather, count and payload all-to-all-v, votes) runs
+    against real RCCL on a one-GPU box (RCCL refuses two ranks on one device)."""
+    global _WORLD
+    dev = torch.device("cuda", device_index)
+    torch.cuda.set_device(dev)
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        dist.init_process_group(backend="nccl", rank=0, world_size=1,
+                                timeout=datetime.timedelta(seconds=timeout_s), device_id=dev)
+        warm_collectives(dev, 1)
+    _WORLD = World(rank=0, size=1, local_rank=0, device=dev, backend="nccl", force_collectives=True)
     return _WORLD
 
 

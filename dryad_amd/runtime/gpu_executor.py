@@ -88,7 +88,7 @@ class GpuVertexContext(V.VertexContext):
             if layout != "plain":
                 return None
             return torch.empty((n, stride), dtype=torch.uint8, device=self.device)
-        slack = r.ctx._props.get("ShuffleSlack", 0.01) if self.world.size > 1 else 0.0
+        slack = r.ctx._props.get("ShuffleSlack", 0.01) if self.world.collective else 0.0
         bs = r.pool.acquire(int(n * (1 + slack)) + 1024, stride, layout)
         r.row_sets[(self.stage.id, self.partition)] = bs
         return bs.bufs.rows_in[:n] if layout == "plain" else bs.bufs.rows_in[:n, :stride]
@@ -331,7 +331,7 @@ class GpuJobRunner:
                 if not ok:
                     spec = None
         votes = [None] * self.world.size
-        if self.world.size > 1:
+        if self.world.collective:
             dist.all_gather_object(votes, (bool(ok), None if spec is None else (spec.off, spec.length)))
         else:
             votes = [(bool(ok), None if spec is None else (spec.off, spec.length))]
@@ -345,7 +345,7 @@ class GpuJobRunner:
         op_read writes just the sort entries (ops/gpu: lazy_gen) and the records are generated
         straight into the exchange's send buckets."""
         st, out = self.plan.stages, set()
-        if self.world.size < 2 or not self.gpu_ok or not self.ctx._props.get("GenFusedShuffle", False):
+        if not self.world.collective or not self.gpu_ok or not self.ctx._props.get("GenFusedShuffle", False):
             return out
         for f in self.fused.values():
             x = st[f["x"]]
@@ -368,7 +368,7 @@ class GpuJobRunner:
             return out
         from ..gpu import trace as TR
         from ..gpu.table import Shape
-        if self.world.size > 1:
+        if self.world.collective:
             return self._pitch_fused_reads()
         for x in self.plan.stages:
             if not (not x.inputs and len(x.ops) >= 2 and x.ops[0]["op"] == "read" and x.ops[1]["op"] == "sort"
@@ -402,7 +402,7 @@ class GpuJobRunner:
             if (x.id in lazy or x.inputs or len(x.ops) != 1 or x.ops[0]["op"] != "read"
                     or not _rows100_source(x.ops[0]["uri"]) or f["comparer"] is not None or f["desc"]
                     or set(self.plan.consumers(x.id)) != {f["stages"][0], f["stages"][2]}
-                    or not RS.fine_rows_ok(100, 128, 0, 10, self.world.size, 1)):
+                    or not RS.fine_rows_ok(100, 128, 0, 10, self.world.size, 1, self.world.force_collectives)):
                 continue
             rows = torch.zeros((2, 100), dtype=torch.uint8, device=self.dev)
             t = DeviceTable(2, Shape("rows", key_off=0, key_len=10), rows=rows)

@@ -83,7 +83,23 @@ def main():
         torch.cuda.synchronize()
         assert st2.path.startswith("E128"), st2.path
         assert out2.shape[0] == n and int(acc2[1]) == 0 and int(acc2[0]) == int(acc_in[0]), acc2.tolist()
-        print(f"RCCL_ONE_RANK_OK fine={rep['round_arrival_ms']} desc={st2.path}", flush=True)
+        del bufs, src, out, out2
+        torch.cuda.empty_cache()
+        # 4. the bench's N > 1 program: the DryadLINQ query through the executor's fused OrderBy gang
+        #    stage (ExchangeOneRank plans the sampled range shuffle for the one partition), validated
+        from dryad_amd.models.terasort import TeraSortConfig, TeraSortQueryJob
+        from dryad_amd.parallel.comm import set_world
+        set_world(w)
+        job = TeraSortQueryJob(TeraSortConfig(records_per_rank=n), w)
+        expect = job.input_checksum()
+        job.step()
+        val = job.validate(*expect)
+        q = job.executor_report()
+        assert val["ok"], val
+        assert q["exchange"] and q["exchange"]["path"].startswith("fine-bucket exchange over the table"), q
+        assert not q["fallbacks"], q
+        print(f"RCCL_ONE_RANK_OK fine={rep['round_arrival_ms']} desc={st2.path} query={q['exchange']['path']}",
+              flush=True)
     finally:
         dist.destroy_process_group()
 

@@ -127,3 +127,20 @@ def test_expensive_associative_aggregate_gets_full_aggregator():
     assert "<Type>FullAggregator</Type>" in p.to_xml()
     assert all(list(c2.FromEnumerable(DATA).Aggregate(0, add) for c2 in [_ctx(k)])[0] == sum(DATA)
                for k in ("local", "proc", "spmd"))
+
+
+def test_exchange_one_rank_plans_the_range_shuffle():
+    """ExchangeOneRank (the one-rank RCCL rehearsal, bench.py --rccl-one-rank): a one-partition
+    OrderBy is planned as Sample -> Separators -> RangePartition -(cross)-> Merge+sort, and the
+    query still gives the oracle's order on one CPU rank."""
+    c = D.DryadLinqContext(platform="gpu")
+    c.PartitionCount = 1
+    c.ExchangeOneRank = True
+    q = c.FromEnumerable(DATA).OrderBy(lambda x: x)
+    p, ops = _ops(q, c)
+    assert {"sample", "separators", "range_partition", "sort"} <= set(ops), ops
+    assert list(q) == sorted(DATA)
+    c1 = D.DryadLinqContext(platform="gpu")
+    c1.PartitionCount = 1
+    _, ops1 = _ops(c1.FromEnumerable(DATA).OrderBy(lambda x: x), c1)
+    assert "range_partition" not in ops1, ops1
