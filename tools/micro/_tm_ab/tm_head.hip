@@ -54,25 +54,21 @@ __device__ __forceinline__ uint64_t tm_key(uint32_t w0, uint32_t w1, uint32_t w2
 constexpr uint32_t kTsStage = 736;
 constexpr uint32_t kTsBins = 256;                  // staged path: next 8 key bits
 constexpr uint32_t kTsPasses = (kTsStage + 63) / 64;
+constexpr uint32_t kTsHalf = (kTsPasses + 1) / 2;   // row loads a lane group keeps in flight
 constexpr uint32_t kTsPoolWords = kTsStage * kTmWords + kTsStage + 2 * kTsBins;
 
 // pre[s * K + k] = row (of `rows`) where bucket k's slice from source s starts, cnt[s * K + k] its
-// rows; bucket k's output rows start at out row outoff[k].  A workgroup orders buckets
-// blockIdx.x, + gridDim.x, ... (a bucket averages ~600 rows; FINE_ROWS), two in flight: while it
-// ranks and stores bucket j from the LDS stage, the rows of bucket j + 1 are already loading into
-// registers (12 x 16 bytes per lane, issued right after bucket j was staged), and wave 0 holds
-// the slice metadata of bucket j + 2 (the barriers wait on LDS traffic only, so the row loads stay
-// in flight across them).  Per bucket of nt <= kTsStage rows:
-//   * its W source slices, already in registers (8 lanes per row, 16-byte loads; a wave reads 8
-//     consecutive rows of a slice, 800 contiguous bytes), are written to the stage at the 100-byte
-//     pitch;
-//   * an LDS counting sort on the next 8 key bits plus an in-bin rank by (key, tile index) gives
-//     each output slot its tile row (source-major tile index = stable);
-//   * the bucket leaves in OUTPUT order: a wave stores 8 consecutive output rows, 800 contiguous
-//     bytes, every row read back from the stage.  Both HBM streams are contiguous.
-// kTsStage < nt <= kTmCap (a rare large bucket): left to ts_tile_merge_big_kernel.  A bucket of
-// more than kTmCap rows is skipped and flagged (*overflow); the caller orders that key range
-// another way.
+// rows; bucket k's output rows start at out row outoff[k].  Per bucket (a bucket averages ~600
+// rows; FINE_ROWS):
+//   * nt <= kTsStage rows (staged path): the W source slices are copied into an LDS stage at the
+//     100-byte pitch (8 lanes per row, 16-byte loads; a wave reads 8 consecutive rows of a slice,
+//     800 contiguous bytes), an LDS counting sort on the next 8 key bits plus an in-bin rank by
+//     (key, tile index) gives each output slot its tile row (source-major tile index = stable),
+//     and the bucket leaves in OUTPUT order: a wave stores 8 consecutive output rows, 800
+//     contiguous bytes, every row read back from the stage.  Both HBM streams are contiguous.
+//   * kTsStage < nt <= kTmCap (a rare large bucket): left to ts_tile_merge_big_kernel.
+// A bucket of more than kTmCap rows is skipped and flagged (*overflow); the caller orders that
+// key range another way.
 __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4))) void ts_tile_merge_kernel(const uint32_t* __restrict__ rows,
                                                                    uint32_t* __restrict__ out,
                                                                    const int64_t* __restrict__ pre,
@@ -81,94 +77,64 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
                                                                    uint32_t K, uint32_t fb,
                                                                    uint32_t* __restrict__ overflow) {
   __shared__ __attribute__((aligned(16))) uint32_t pool[kTsPoolWords];
-  __shared__ int64_t sbase[2][kTmMaxW];
-  __shared__ uint32_t spre[2][kTmMaxW + 1];
-  __shared__ int64_t sout[2];
+  __shared__ int64_t sbase[kTmMaxW];
+  __shared__ uint32_t spre[kTmMaxW + 1];
   __shared__ uint32_t wtot[kTmThreads / 64];
   const uint32_t t = threadIdx.x;
-  const uint32_t G = gridDim.x;
-  uint32_t* stage = pool;
-  uint16_t* member = reinterpret_cast<uint16_t*>(pool + kTsStage * kTmWords);
-  uint16_t* perm = member + kTsStage;
-  uint32_t* bcnt = pool + kTsStage * kTmWords + kTsStage;
-  uint32_t* bcur = bcnt + kTsBins;
-  const uint32_t g = t >> 3, sub = t & 7;
-
-  // wave 0, lane s < W: source s's (slice start, rows) of a bucket; lane 0 also its output row
-  int64_t nx_pre = 0, nx_out = 0;
-  uint32_t nx_cnt = 0;
-  auto meta_load = [&](uint32_t k) {
-    nx_cnt = 0;
-    if (t < W && k < K) {
-      nx_pre = pre[(uint64_t)t * K + k];
-      nx_cnt = (uint32_t)cnt[(uint64_t)t * K + k];
-      if (t == 0) nx_out = outoff[k];
-    }
-  };
-  auto meta_store = [&](uint32_t buf) {           // wave 0: slice starts within the tile, by scan
-    const uint32_t c = t < W ? nx_cnt : 0u;
-    const uint32_t inc = wave_inclusive_scan(c);
-    if (t < W) {
-      sbase[buf][t] = nx_pre;
-      spre[buf][t] = inc - c;
-    }
-    if (t == 63) spre[buf][W] = inc;
-    if (t == 0) sout[buf] = nx_out;
-  };
-  u32x4u v[kTsPasses];
-  auto rows_load = [&](uint32_t buf, uint32_t nt) {
-    uint32_t s = 0;
-#pragma unroll
-    for (uint32_t p = 0; p < kTsPasses; ++p) {
-      const uint32_t i = g + 64 * p;
-      if (i < nt && sub < 7) {
-        while (spre[buf][s + 1] <= i) ++s;
-        const uint32_t* src = rows + (uint64_t)(sbase[buf][s] + (int64_t)(i - spre[buf][s])) * kTmWords + sub * 4;
-        if (sub < 6) v[p] = *reinterpret_cast<const u32x4u*>(src);
-        else v[p].x = src[0];
+  for (uint32_t k = blockIdx.x; k < K; k += gridDim.x) {
+    if (t < W) sbase[t] = pre[(uint64_t)t * K + k];
+    if (t == 0) {
+      uint32_t acc = 0;
+      for (uint32_t s = 0; s < W; ++s) {
+        spre[s] = acc;
+        acc += (uint32_t)cnt[(uint64_t)s * K + k];
       }
+      spre[W] = acc;
     }
-  };
-
-  uint32_t k = blockIdx.x;
-  if (t < 64) {
-    meta_load(k);
-    meta_store(0);
-    meta_load(k + G);
-  }
-  __syncthreads();
-  uint32_t nt = spre[0][W];
-  if (k < K && nt <= kTsStage) rows_load(0, nt);
-  for (uint32_t j = 0; k < K; ++j, k += G) {
-    const uint32_t b = j & 1;
-    const int64_t ob = sout[b];
-    if (t < 64) {
-      meta_store(b ^ 1);                            // bucket k + G
-      meta_load(k + 2 * G);
+    __syncthreads();
+    const uint32_t nt = spre[W];
+    if (nt == 0 || nt > kTmCap) {
+      if (nt > kTmCap && t == 0) atomicOr(overflow, 1u);
+      __syncthreads();
+      continue;
     }
-    if (t < kTsBins) bcnt[t] = 0;
-    const bool staged = nt > 0 && nt <= kTsStage;
-    if (staged) {
+    uint32_t* o = out + (uint64_t)outoff[k] * kTmWords;
+    if (nt <= kTsStage) {
+      uint32_t* stage = pool;
+      uint16_t* member = reinterpret_cast<uint16_t*>(pool + kTsStage * kTmWords);
+      uint16_t* perm = member + kTsStage;
+      uint32_t* bcnt = pool + kTsStage * kTmWords + kTsStage;
+      uint32_t* bcur = bcnt + kTsBins;
+      if (t < kTsBins) bcnt[t] = 0;
+      const uint32_t g = t >> 3, sub = t & 7;
+      uint32_t s = 0;
+      for (uint32_t p0 = 0; p0 < kTsPasses && g + 64 * p0 < nt; p0 += kTsHalf) {   // loads in flight: kTsHalf rows per lane group
+        u32x4u v[kTsHalf];
 #pragma unroll
-      for (uint32_t p = 0; p < kTsPasses; ++p) {
-        const uint32_t i = g + 64 * p;
-        if (i < nt && sub < 7) {
-          uint32_t* d = stage + i * kTmWords + sub * 4;
-          d[0] = v[p].x;
-          if (sub < 6) {
-            d[1] = v[p].y;
-            d[2] = v[p].z;
-            d[3] = v[p].w;
+        for (uint32_t p = 0; p < kTsHalf; ++p) {
+          const uint32_t i = g + 64 * (p0 + p);
+          if (i < nt && sub < 7) {
+            while (spre[s + 1] <= i) ++s;
+            const uint32_t* src = rows + (uint64_t)(sbase[s] + (int64_t)(i - spre[s])) * kTmWords + sub * 4;
+            if (sub < 6) v[p] = *reinterpret_cast<const u32x4u*>(src);
+            else v[p].x = src[0];
+          }
+        }
+#pragma unroll
+        for (uint32_t p = 0; p < kTsHalf; ++p) {
+          const uint32_t i = g + 64 * (p0 + p);
+          if (i < nt && sub < 7) {
+            uint32_t* d = stage + i * kTmWords + sub * 4;
+            d[0] = v[p].x;
+            if (sub < 6) {
+              d[1] = v[p].y;
+              d[2] = v[p].z;
+              d[3] = v[p].w;
+            }
           }
         }
       }
-    }
-    __syncthreads();
-    const uint32_t nt2 = spre[b ^ 1][W];
-    if (k + G < K && nt2 <= kTsStage) rows_load(b ^ 1, nt2);     // in flight while bucket k is ordered
-    if (nt > kTmCap && t == 0) atomicOr(overflow, 1u);
-    if (staged) {
-      uint32_t* o = out + (uint64_t)ob * kTmWords;
+      __syncthreads();
       for (uint32_t i = t; i < nt; i += kTmThreads) {
         const uint32_t* r = stage + i * kTmWords;
         atomicAdd(&bcnt[(uint32_t)(tm_key(r[0], r[1], r[2], fb) >> 56)], 1u);
@@ -200,27 +166,28 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
         for (uint32_t m = beg; m < end; ++m) {
           const uint32_t x = member[m];
           const uint32_t* q = stage + x * kTmWords;
-          const uint64_t bb = tm_key(q[0], q[1], q[2], fb);
-          slot += (bb < a || (bb == a && x < i)) ? 1u : 0u;
+          const uint64_t b = tm_key(q[0], q[1], q[2], fb);
+          slot += (b < a || (b == a && x < i)) ? 1u : 0u;
         }
         perm[slot] = (uint16_t)i;
       }
       __syncthreads();
 #pragma unroll 4
       for (uint32_t p = 0; p < kTsPasses; ++p) {
-        const uint32_t jj = g + 64 * p;
-        if (jj < nt && sub < 7) {
-          const uint32_t* sr = stage + (uint32_t)perm[jj] * kTmWords + sub * 4;
-          uint32_t* dst = o + jj * kTmWords + sub * 4;
+        const uint32_t j = g + 64 * p;
+        if (j < nt && sub < 7) {
+          const uint32_t* sr = stage + (uint32_t)perm[j] * kTmWords + sub * 4;
+          uint32_t* dst = o + j * kTmWords + sub * 4;
           // plain stores: the bucket's first and last lines are partial, completed in L2 by the
           // neighbouring buckets (nontemporal stores write partial lines through)
           if (sub < 6) *reinterpret_cast<u32x4u*>(dst) = u32x4u{sr[0], sr[1], sr[2], sr[3]};
           else dst[0] = sr[0];
         }
       }
+      __syncthreads();
+      continue;
     }
-    __syncthreads();
-    nt = nt2;
+    __syncthreads();               // kTsStage < nt <= kTmCap: ts_tile_merge_big_kernel
   }
 }
 
