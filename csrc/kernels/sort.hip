@@ -1403,6 +1403,235 @@ __global__ __launch_bounds__(256) void gather_fixup_staged_kernel(const uint32_t
   }
 }
 
+// Row gather + BUCKET sort for 100-byte records at a 128-byte pitch whose E64 entries are sorted
+// on the top `win` window bits only (win = 64 - run_shift, e.g. 24 of the 32: one look-back radix
+// pass fewer), so a run of equal run ids -- a key bucket -- averages tens of rows (~75 for 1.25e9
+// rows at 24 bits) and is ordered here, in LDS, by the rest of its key (then by position: stable).
+// A workgroup owns the runs that START in its kBkCore-position core and finishes them up to kBkExt
+// positions past it (a longer run flags overflow bit 0 and the caller re-sorts).  Two windows in
+// flight: while window j is ranked and stored from the LDS stage, the rows of window j + 1 are
+// loading into registers (8 lanes per aligned 128-byte line) and the entries of window j + 2 too
+// (the barriers wait on LDS traffic only).  Per window: the staged rows' 64 key bits after the run
+// id become their sub-keys; an LDS counting sort on bin = ((run id - first) << 8 | next 8 key bits)
+// >> bsh (bins ordered like the keys) places every row but the few sharing a bin, ranked by (run
+// id, sub-key, full key, position); the window leaves in rank order as 16-byte stores.
+constexpr uint32_t kBkCore = 352, kBkExt = 192, kBkWin = kBkCore + kBkExt, kBkThreads = 512;
+constexpr uint32_t kBkBins = kBkThreads;
+constexpr int kBkRounds = (kBkWin + 63) / 64;          // row-load rounds: 64 rows (8 lanes each) per round
+static_assert(kBkWin <= 2 * kBkThreads, "two entries per thread");
+
+__global__ __launch_bounds__(kBkThreads) __attribute__((amdgpu_waves_per_eu(4))) void gather_bucket_staged_kernel(
+    const uint32_t* __restrict__ rows, uint32_t* __restrict__ out, const E64* __restrict__ ent, uint64_t n,
+    uint32_t key_off, uint32_t key_len, int run_shift, uint32_t* __restrict__ overflow,
+    const int32_t* __restrict__ err) {
+  if (err != nullptr && *err != 0) return;     // the look-back sort failed: the entries are no permutation
+  constexpr uint32_t W = 25;
+  typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+  __shared__ uint32_t rid[2][kBkWin + 1];  // rid[b][p + 1] = run id of window position p; [b][0] = position -1
+  __shared__ uint32_t idx[2][kBkWin];
+  __shared__ uint64_t sk[kBkWin];          // staged row -> key bits [win, win + 64)
+  __shared__ uint16_t slot[kBkWin];        // output position - ob -> staged row
+  __shared__ uint16_t member[kBkWin];      // rows of bin b: member[bin start .. bin end)
+  __shared__ uint32_t bcnt[kBkBins];
+  __shared__ uint32_t bcur[kBkBins];
+  __shared__ uint32_t wsum[kBkThreads / 64];
+  __shared__ uint32_t own[2][2];
+  __shared__ __attribute__((aligned(16))) uint32_t stage[kBkWin * W];
+  const uint32_t t = threadIdx.x;
+  const uint8_t* sbytes = reinterpret_cast<const uint8_t*>(stage);
+  const uint8_t* rb8 = reinterpret_cast<const uint8_t*>(rows);
+  const bool aligned = (key_off & 3) == 0;
+  const int win = 64 - run_shift;
+  const uint64_t step = (uint64_t)gridDim.x * kBkCore;
+  const uint32_t g = t >> 3, sub = t & 7;
+
+  uint64_t ev0 = 0, ev1 = 0, evp = 0;      // entries of the next window to publish (positions t, t + 512, -1)
+  auto ent_load = [&](uint64_t c0) {
+    if (c0 >= n) return;
+    const uint64_t L = (n - c0) < (uint64_t)kBkWin ? (n - c0) : kBkWin;
+    if (t < L) ev0 = ent[c0 + t].v;
+    if (t + kBkThreads < L) ev1 = ent[c0 + t + kBkThreads].v;
+    if (t == 0 && c0 > 0) evp = ent[c0 - 1].v;
+  };
+  // publish the loaded entries of the window at c0 into buffer b and find its owned range
+  auto publish = [&](uint32_t b, uint64_t c0) {
+    const uint32_t L = (uint32_t)((n - c0) < (uint64_t)kBkWin ? (n - c0) : kBkWin);
+    if (t < L) {
+      rid[b][t + 1] = (uint32_t)(ev0 >> run_shift);
+      uint32_t i = (uint32_t)ev0;
+      if (i >= n) {                    // corrupt entries: never read past the rows (flag 2: redo)
+        atomicOr(overflow, 2u);
+        i = 0;
+      }
+      idx[b][t] = i;
+    }
+    if (t + kBkThreads < L) {
+      rid[b][t + kBkThreads + 1] = (uint32_t)(ev1 >> run_shift);
+      uint32_t i = (uint32_t)ev1;
+      if (i >= n) {
+        atomicOr(overflow, 2u);
+        i = 0;
+      }
+      idx[b][t + kBkThreads] = i;
+    }
+    if (t == 0) {
+      rid[b][0] = c0 > 0 ? (uint32_t)(evp >> run_shift) : 0u;
+      own[b][0] = 0xFFFFFFFFu;
+      own[b][1] = 0xFFFFFFFFu;
+    }
+  };
+  auto find_owned = [&](uint32_t b, uint64_t c0) {
+    const uint32_t L = (uint32_t)((n - c0) < (uint64_t)kBkWin ? (n - c0) : kBkWin);
+    const uint32_t core = L < kBkCore ? L : kBkCore;
+    for (uint32_t p = t; p < L; p += kBkThreads) {
+      const bool start = (c0 + p == 0) || rid[b][p + 1] != rid[b][p];
+      if (start) atomicMin(&own[b][p < core ? 0 : 1], p);
+    }
+  };
+  // owned range [ob, oe) of the published window (oe = ob: nothing to do; overflow flagged)
+  auto owned = [&](uint32_t b, uint64_t c0, uint32_t& ob, uint32_t& oe) {
+    const uint32_t L = (uint32_t)((n - c0) < (uint64_t)kBkWin ? (n - c0) : kBkWin);
+    ob = own[b][0];
+    oe = own[b][1];
+    if (oe == 0xFFFFFFFFu && c0 + L == n) oe = L;
+    if (ob == 0xFFFFFFFFu) {           // the whole core continues a run owned by a previous workgroup
+      ob = oe = 0;
+    } else if (oe == 0xFFFFFFFFu) {    // a run owned here does not end inside the window
+      if (t == 0) atomicOr(overflow, 1u);
+      ob = oe = 0;
+    }
+  };
+  uint4 buf[kBkRounds];
+  // every lane loads (rows past nrows re-read the last row's line, a cache hit): no branch around
+  // the loads, so the compiler never has to wait for one load before issuing the next
+  auto rows_load = [&](uint32_t b, uint32_t ob, uint32_t nrows) {
+    const uint32_t last = nrows ? nrows - 1 : 0;
+#pragma unroll
+    for (int k = 0; k < kBkRounds; ++k) {
+      const uint32_t r = g + 64 * k;
+      const uint32_t i = idx[b][ob + (r < nrows ? r : last)];
+      const uint4* src = reinterpret_cast<const uint4*>(rb8 + (uint64_t)i * 128 + sub * 16);
+      buf[k].x = __builtin_nontemporal_load(&src->x);
+      buf[k].y = __builtin_nontemporal_load(&src->y);
+      buf[k].z = __builtin_nontemporal_load(&src->z);
+      buf[k].w = __builtin_nontemporal_load(&src->w);
+    }
+  };
+
+  // prologue: window 0 published and its rows loading, the entries of window 1 loading
+  uint64_t c0 = (uint64_t)blockIdx.x * kBkCore;
+  if (c0 >= n) return;
+  ent_load(c0);
+  publish(0, c0);
+  __syncthreads();
+  find_owned(0, c0);
+  __syncthreads();
+  uint32_t ob, oe;
+  owned(0, c0, ob, oe);
+  rows_load(0, ob, oe - ob);
+  ent_load(c0 + step);
+  for (uint32_t j = 0; c0 < n; ++j, c0 += step) {
+    const uint32_t b = j & 1;
+    const uint32_t nrows = oe - ob;
+    const uint64_t c1 = c0 + step;
+    // (1) this window's rows to the stage; the next window's entries published
+#pragma unroll
+    for (int k = 0; k < kBkRounds; ++k) {
+      const uint32_t r = g + 64 * k;
+      if (r < nrows && sub < 7) {
+        uint32_t* d = stage + r * W + sub * 4;
+        d[0] = buf[k].x;
+        if (sub < 6) {
+          d[1] = buf[k].y;
+          d[2] = buf[k].z;
+          d[3] = buf[k].w;
+        }
+      }
+    }
+    if (c1 < n) publish(b ^ 1, c1);
+    bcnt[t] = 0;
+    __syncthreads();
+    // (2) sub-keys of the staged rows; the next window's owned range
+    for (uint32_t r = t; r < nrows; r += kBkThreads) {
+      uint64_t k0, k1;
+      load_key128(sbytes + r * (W * 4) + key_off, key_len, aligned, k0, k1);
+      sk[r] = (k0 << win) | (k1 >> (64 - win));
+    }
+    if (c1 < n) find_owned(b ^ 1, c1);
+    __syncthreads();
+    // (3) the next window's rows and the entries after it start loading
+    uint32_t ob1 = 0, oe1 = 0;
+    if (c1 < n) {
+      owned(b ^ 1, c1, ob1, oe1);
+      rows_load(b ^ 1, ob1, oe1 - ob1);
+      ent_load(c1 + step);
+    }
+    // (4) this window: counting sort, in-bin rank, stores in rank order
+    if (nrows > 0) {
+      const uint32_t rid0 = rid[b][ob + 1];
+      const uint64_t span = ((uint64_t)(rid[b][oe] - rid0) + 1) << 8;
+      uint32_t bsh = 0;
+      while ((span >> bsh) > kBkBins) ++bsh;
+      auto bin_of = [&](uint32_t p) -> uint32_t {
+        return (uint32_t)(((((uint64_t)(rid[b][p + 1] - rid0)) << 8) | (sk[p - ob] >> 56)) >> bsh);
+      };
+      for (uint32_t p = ob + t; p < oe; p += kBkThreads) atomicAdd(&bcnt[bin_of(p)], 1u);
+      __syncthreads();
+      {                                // exclusive scan of the kBkBins bins, one per lane
+        const uint32_t c = bcnt[t];
+        const uint32_t inc = wave_inclusive_scan(c);
+        if (lane_id() == 63) wsum[wave_id()] = inc;
+        __syncthreads();
+        uint32_t run = inc - c;
+        for (int w = 0; w < wave_id(); ++w) run += wsum[w];
+        bcur[t] = run;
+      }
+      __syncthreads();
+      for (uint32_t p = ob + t; p < oe; p += kBkThreads) member[atomicAdd(&bcur[bin_of(p)], 1u)] = (uint16_t)(p - ob);
+      __syncthreads();
+      for (uint32_t p = ob + t; p < oe; p += kBkThreads) {
+        const uint32_t bn = bin_of(p), end = bcur[bn], beg = end - bcnt[bn];
+        const uint32_t me = p - ob, ra = rid[b][p + 1];
+        const uint64_t a = sk[me];
+        uint32_t r = beg;
+        bool full = false;
+        uint64_t a0 = 0, a1 = 0;
+        for (uint32_t m = beg; m < end; ++m) {
+          const uint32_t x = member[m];
+          if (x == me) continue;
+          const uint32_t rbx = rid[b][x + ob + 1];
+          const uint64_t bk = sk[x];
+          if (rbx != ra || bk != a) {
+            r += (rbx < ra || (rbx == ra && bk < a)) ? 1u : 0u;
+            continue;
+          }
+          if (!full) {                 // equal sub-keys: the full key, then the position
+            load_key128(sbytes + me * (W * 4) + key_off, key_len, aligned, a0, a1);
+            full = true;
+          }
+          uint64_t b0, b1;
+          load_key128(sbytes + x * (W * 4) + key_off, key_len, aligned, b0, b1);
+          r += (b0 < a0 || (b0 == a0 && (b1 < a1 || (b1 == a1 && x < me)))) ? 1u : 0u;
+        }
+        slot[r] = (uint16_t)me;
+      }
+      __syncthreads();
+      uint32_t* o = out + (c0 + ob) * W;
+      for (uint32_t jj = g; jj < nrows; jj += kBkThreads / 8) {
+        if (sub < 7) {
+          const uint32_t* sr = stage + (uint32_t)slot[jj] * W + sub * 4;
+          uint32_t* dst = o + jj * W + sub * 4;
+          if (sub < 6) *reinterpret_cast<u32x4a*>(dst) = u32x4a{sr[0], sr[1], sr[2], sr[3]};
+          else dst[0] = sr[0];
+        }
+      }
+    }
+    __syncthreads();
+    ob = ob1;
+    oe = oe1;
+  }
+}
+
 }  // namespace
 
 DR_API int dr_extract_keys64(const uint8_t* rows, uint64_t n, uint32_t stride, uint32_t key_off, uint32_t key_len,
@@ -1797,6 +2026,22 @@ DR_API int dr_gather_fixup_pitch128(const uint8_t* rows, uint8_t* out, const E64
   gather_fixup_staged_kernel<<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows),
                                                    reinterpret_cast<uint32_t*>(out), ent, n, key_off, key_len,
                                                    run_shift, overflow, err);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// gather_bucket_staged_kernel: entries sorted on their top 64 - run_shift window bits (16..31 of
+// them), key at most 16 bytes.  Overflow bit 0: a run longer than the kernel's window extension.
+DR_API int dr_gather_bucket_pitch128(const uint8_t* rows, uint8_t* out, const E64* ent, uint64_t n, uint32_t key_off,
+                                     uint32_t key_len, int run_shift, uint32_t* overflow, const int32_t* err,
+                                     hipStream_t s) {
+  if (key_len == 0 || key_len > 16 || key_off + key_len > 100) return (int)hipErrorInvalidValue;
+  if (run_shift < 33 || run_shift > 48 || n >= (1ull << 32)) return (int)hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(rows) & 15) || (reinterpret_cast<uintptr_t>(out) & 3)) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  gather_bucket_staged_kernel<<<grid_for(n, kBkCore, 16384), kBkThreads, 0, s>>>(
+      reinterpret_cast<const uint32_t*>(rows), reinterpret_cast<uint32_t*>(out), ent, n, key_off, key_len, run_shift,
+      overflow, err);
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -179,7 +179,8 @@ def _entries_home(bs, n: int, v):
     """Where a producer writes the E64 sort entries of a pitch-128 table: ent_a for the one-rank
     sort; with several ranks the send buffer's first n * 8 bytes ("e64@out": the fine-bucket
     exchange's entry sort then ends in ent_a, away from the rows its pack writes)."""
-    if v.world.size > 1:
+    if v.world.collective or S.bucket_sort_ok(n, 10):
+        # (one rank, bucket sort: its three look-back passes end in ent_a, away from the output)
         return bs.bufs.rows_out.view(-1)[: n * 8].view(torch.int64), "e64@out"
     return bs.bufs.ent_a, "e64"
 
@@ -510,7 +511,8 @@ def op_sort(op, inputs, v):
             kr = bs.take_keys(t.rows, spec.off, spec.length)
             info = {}
             out = S.sort_rows_pitch128(bs.bufs.rows_in[: t.n], bs.bufs.rows_out, bs.bufs.ent_a, spec.off,
-                                       spec.length, keys_ready=kr is not None and kr[2] == "e64", stats=info)
+                                       spec.length, keys_ready=kr is not None and kr[2] in ("e64", "e64@out"),
+                                       stats=info, keys_fmt="e64" if kr is None else kr[2])
             if v.runner is not None:
                 v.runner.last_sort_path = info.get("path")
             return DeviceTable(out.shape[0], t.shape, rows=out)

@@ -58,8 +58,9 @@ def read_to_device(path: str, device, offset: int = 0, length: int = -1, out: to
     if length == 0:
         return out[:0]
     ring = _ring()
+    chunk = min(CHUNK, ring[0].tensor.numel())      # the ring may predate a CHUNK change
     with _RING_LOCK:           # one reader per process at a time owns the ring
-        rd = runtime().ChunkReader(path, int(offset), int(length), CHUNK, [b.tensor.data_ptr() for b in ring],
+        rd = runtime().ChunkReader(path, int(offset), int(length), chunk, [b.tensor.data_ptr() for b in ring],
                                    THREADS)
         cur = torch.cuda.current_stream(dev)
         cs = torch.cuda.Stream(dev)
@@ -76,8 +77,8 @@ def read_to_device(path: str, device, offset: int = 0, length: int = -1, out: to
                 got = rd.next(-1)
                 if got is None:
                     break
-                slot, chunk, nb = got
-                a = chunk * CHUNK
+                slot, ci, nb = got
+                a = ci * chunk
                 _lib.memcpy_async(out[a:a + nb], ring[slot].tensor[:nb], cs)
                 ev = torch.cuda.Event()
                 ev.record(cs)
@@ -118,12 +119,16 @@ def read_rows_to_device(path: str, device, offset: int, n: int, stride: int, out
         return out[:n]
     t0 = time.perf_counter()
     dev = torch.device(device)
-    cb = (CHUNK // stride) * stride
     length = n * stride
     if os.path.getsize(path) < offset + length:
         raise ValueError(f"read_rows_to_device: {path} holds fewer than {n} rows of {stride} bytes")
-    stage = torch.empty(cb, dtype=torch.uint8, device=dev)
     ring = _ring()
+    # whole rows per chunk, at most a ring buffer (the ring may predate a CHUNK change: a reader
+    # told a chunk larger than its buffers would write past them)
+    cb = (min(CHUNK, ring[0].tensor.numel()) // stride) * stride
+    if cb == 0:
+        raise ValueError(f"read_rows_to_device: {stride}-byte rows exceed the {ring[0].tensor.numel()}-byte ring buffers")
+    stage = torch.empty(cb, dtype=torch.uint8, device=dev)
     with _RING_LOCK:
         rd = runtime().ChunkReader(path, int(offset), int(length), cb, [b.tensor.data_ptr() for b in ring], THREADS)
         cur = torch.cuda.current_stream(dev)
@@ -142,8 +147,8 @@ def read_rows_to_device(path: str, device, offset: int, n: int, stride: int, out
                     got = rd.next(-1)
                     if got is None:
                         break
-                    slot, chunk, nb = got
-                    r0, nr = chunk * (cb // stride), nb // stride
+                    slot, ci, nb = got
+                    r0, nr = ci * (cb // stride), nb // stride
                     _lib.memcpy_async(stage[:nb], ring[slot].tensor[:nb], cs)
                     ev = torch.cuda.Event()
                     ev.record(cs)

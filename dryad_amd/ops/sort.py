@@ -503,8 +503,22 @@ def _sort64_into(e: torch.Tensor, tmp: torch.Tensor, win: int, gen_hist=None, er
     return e
 
 
+# One-rank sorts of pitch-128 tables: the entries sorted on their top BUCKET_BITS window bits only
+# (three look-back passes instead of four) and every run of equal 24-bit prefixes -- a key bucket
+# of ~n / 2^24 rows -- ordered by the row gather itself (dr_gather_bucket_pitch128), when the
+# buckets average BUCKET_MIN_ROWS .. BUCKET_MAX_ROWS rows (the gather's window holds runs of up
+# to 192 rows; a longer one is flagged and the full-key chain below takes over)
+BUCKET_BITS = 24
+BUCKET_MIN_ROWS, BUCKET_MAX_ROWS = 16, 96
+
+
+def bucket_sort_ok(n: int, key_len: int) -> bool:
+    return 8 * key_len > BUCKET_BITS and key_len <= 16 and \
+        (BUCKET_MIN_ROWS << BUCKET_BITS) <= n <= min(BUCKET_MAX_ROWS << BUCKET_BITS, (1 << 32) - 1)
+
+
 def sort_rows_pitch128(rows_p: torch.Tensor, out: torch.Tensor, keys: torch.Tensor, key_off: int, key_len: int,
-                       keys_ready: bool = True, stats: dict | None = None) -> torch.Tensor:
+                       keys_ready: bool = True, stats: dict | None = None, keys_fmt: str = "e64") -> torch.Tensor:
     """Stable sort of the records in ``rows_p`` ([n, 128], 100-byte records) by their byte-string
     key into ``out[:n]`` ([>= n, 100]).  ``keys[:n]``: the rows' compact entries for prefix 0
     (written by the generator) when ``keys_ready``, else the key is read from the rows.  The radix
@@ -514,7 +528,10 @@ def sort_rows_pitch128(rows_p: torch.Tensor, out: torch.Tensor, keys: torch.Tens
     A run of equal 32-bit windows too long for the gather's fix-up (heavily duplicated keys) is
     resolved exactly without more memory: an LSD chain of compact sorts over every 32-bit window
     of the key, from the least significant, each window re-read from the rows (``rekey64``),
-    then a gather without fix-up."""
+    then a gather without fix-up.
+
+    ``keys_fmt`` "e64@out": the producer wrote the entries into ``out``'s first n * 8 bytes (the
+    bucket sort's home for them: its odd pass count then ends in ``keys``, see bucket_sort_ok)."""
     n = rows_p.shape[0]
     if n == 0:
         return out[:0]
@@ -522,12 +539,30 @@ def sort_rows_pitch128(rows_p: torch.Tensor, out: torch.Tensor, keys: torch.Tens
         raise ValueError("sort_rows_pitch128: < 2^32 rows, key inside the 100-byte record, <= 16 bytes")
     tmp = out.view(-1)[: n * 8].view(torch.int64)
     e = keys[:n]
-    gen_hist = take_gen_hist(e) if keys_ready else None
+    in_out = keys_ready and keys_fmt == "e64@out"
+    gen_hist = take_gen_hist(tmp if in_out else e) if keys_ready else None
     flags = torch.zeros(2, dtype=torch.int32, device=rows_p.device)      # [gather overflow, look-back error]
     flag = flags[:1]
     path = "compact pitch128"
     lookback = True
-    if keys_ready and key_off == 0:
+    bucket = keys_ready and key_off == 0 and bucket_sort_ok(n, key_len)
+    if in_out and not bucket:
+        e.copy_(tmp)                            # the entries where the four-pass path wants them
+    if bucket:
+        src, dst = (tmp, e) if in_out else (e, tmp)
+        srt = sort_entries64(src, dst, BUCKET_BITS, gen_hist, err=flags[1:])
+        if srt.data_ptr() != e.data_ptr():
+            e.copy_(srt)                        # the entries must not lie under the output
+        _lib.call("dr_gather_bucket_pitch128", ptr(rows_p), ptr(out), ptr(e), c_u64(n), c_u32(key_off),
+                  c_u32(key_len), 64 - BUCKET_BITS, ptr(flag), ptr(flags[1:]), stream_of(rows_p))
+        path += (" gen-hist" if gen_hist is not None and n >= ONESWEEP_MIN else "") + \
+            f" bucket sort: win={BUCKET_BITS} + in-LDS bucket order"
+        overflow, failed = (int(x) != 0 for x in flags.tolist())
+        chain = overflow or failed
+        if failed:
+            lookback = False
+            path += " look-back failed"
+    elif keys_ready and key_off == 0:
         win = min(window_bits64(n), max(8, ((8 * key_len + 7) // 8) * 8), 32)
         _sort64_into(e, tmp, win, gen_hist, err=flags[1:])
         if gen_hist is not None and n >= ONESWEEP_MIN:

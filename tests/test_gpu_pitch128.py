@@ -122,3 +122,75 @@ def test_pitch128_gather_fixup_short_runs():
     got = S.sort_rows_pitch128(padded, out, keys, 0, 10, keys_ready=True, stats=info)
     assert "LSD chain" not in info["path"], info
     np.testing.assert_array_equal(got.cpu().numpy(), rows[_reference_order(rows, 0, 10)])
+
+
+def _bucket_gather(padded, e_sorted, key_off, key_len, win):
+    from dryad_amd.ops import _lib
+    from dryad_amd.ops._lib import c_u32, c_u64, ptr, stream_of
+    n = padded.shape[0]
+    out = torch.zeros((n, 100), dtype=torch.uint8, device="cuda")
+    flags = torch.zeros(2, dtype=torch.int32, device="cuda")
+    _lib.call("dr_gather_bucket_pitch128", ptr(padded), ptr(out), ptr(e_sorted), c_u64(n), c_u32(key_off),
+              c_u32(key_len), 64 - win, ptr(flags[:1]), ptr(flags[1:]), stream_of(padded))
+    return out, int(flags[0].item())
+
+
+@pytest.mark.parametrize("case", ["random", "ties", "key_off"])
+def test_bucket_gather_orders_each_run_by_the_full_key(case):
+    """dr_gather_bucket_pitch128: entries sorted on their top 16 window bits only (runs of ~40
+    rows), every run ordered in LDS by the rest of the key, ties by position -- numpy's stable
+    lexsort of the key bytes."""
+    from dryad_amd.ops import sort as S
+    n = 40 << 16
+    key_off, key_len = (5, 12) if case == "key_off" else (0, 10)
+    g = np.random.default_rng({"random": 1, "ties": 2, "key_off": 3}[case])
+    rows = g.integers(0, 256, size=(n, 100), dtype=np.uint8)
+    if case == "ties":          # few distinct sub-keys per run: the full-key / position tie path
+        rows[:, key_off + 2:key_off + key_len] = g.integers(0, 2, size=(n, 1), dtype=np.uint8)
+        rows[:, key_off + key_len - 1] = g.integers(0, 3, size=n)
+    padded = torch.zeros((n, 128), dtype=torch.uint8, device="cuda")
+    padded[:, :100] = torch.from_numpy(rows).cuda()
+    e = S.extract_keys64(padded, key_off, key_len, 0, torch.empty(n, dtype=torch.int64, device="cuda"))
+    tmp = torch.empty_like(e)
+    srt = S.sort_entries64(e, tmp, 16, lookback=False)
+    out, ovf = _bucket_gather(padded, srt, key_off, key_len, 16)
+    assert ovf == 0
+    np.testing.assert_array_equal(out.cpu().numpy(), rows[_reference_order(rows, key_off, key_len)])
+
+
+def test_bucket_gather_flags_a_run_past_its_window():
+    from dryad_amd.ops import sort as S
+    n = 1 << 16
+    rows = np.random.default_rng(5).integers(0, 256, size=(n, 100), dtype=np.uint8)
+    rows[: n // 2, 0:2] = 7                      # one run of 32768 rows on the top 16 bits
+    padded = torch.zeros((n, 128), dtype=torch.uint8, device="cuda")
+    padded[:, :100] = torch.from_numpy(rows).cuda()
+    e = S.extract_keys64(padded, 0, 10, 0, torch.empty(n, dtype=torch.int64, device="cuda"))
+    srt = S.sort_entries64(e, torch.empty_like(e), 16, lookback=False)
+    _, ovf = _bucket_gather(padded, srt, 0, 10, 16)
+    assert ovf & 1
+
+
+@pytest.mark.parametrize("fmt", ["e64", "e64@out"])
+def test_pitch128_bucket_sort_path_matches_the_compact_sort(fmt, monkeypatch):
+    """sort_rows_pitch128's bucket path (three look-back passes on 24 bits + the bucket gather),
+    entries from the generator in ent_a or in the output's memory, against the plain compact sort."""
+    from dryad_amd.ops import sort as S
+    from dryad_amd.ops import terasort as TS
+    monkeypatch.setattr(S, "BUCKET_MIN_ROWS", 1)
+    n = 3 << 24
+    plain, kp, padded, kq = _gen(n, seed=11)
+    ref = S.sort_rows_compact(plain, torch.empty((n, 100), dtype=torch.uint8, device="cuda"), kp,
+                              torch.empty(n, dtype=torch.int64, device="cuda"), 0, 10,
+                              hi_bounds=(0, (1 << 64) - 1), keys_ready=True).clone()
+    del plain, kp
+    out = torch.empty((n, 100), dtype=torch.uint8, device="cuda")
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    home = keys if fmt == "e64" else out.view(-1)[: n * 8].view(torch.int64)
+    TS.generate_with_keys64_pitch128(padded, 0, 11, home, torch.tensor([-1, 0], dtype=torch.int64, device="cuda"),
+                                     hist=True)
+    info = {}
+    got = S.sort_rows_pitch128(padded, out, keys, 0, 10, keys_ready=True, stats=info, keys_fmt=fmt)
+    assert "bucket sort" in info["path"] and "chain" not in info["path"], info
+    assert "gen-hist" in info["path"], info
+    assert torch.equal(got, ref)

@@ -29,6 +29,30 @@ def test_read_rows_pitched_matches_contiguous(tmp_path):
     assert int(big[:, w:].sum().item()) == 0
 
 
+def test_reads_after_a_chunk_change_stay_inside_the_ring(tmp_path):
+    """The pinned ring is created once, at the CHUNK of its first use; a later, larger CHUNK must
+    not make the native reader write past its buffers (it did: a segfault in the next job)."""
+    from dryad_amd.io import reader as RD
+    old, old_ring = RD.CHUNK, RD._RING
+    try:
+        RD._RING = None
+        RD.CHUNK = 1 << 20
+        RD._ring()                               # the ring at 1 MB buffers
+        RD.CHUNK = old
+        n, w = 40_000, 100                       # 4 MB: several 1 MB chunks
+        data = torch.randint(0, 256, (n, w), dtype=torch.uint8)
+        p = tmp_path / "rows.bin"
+        p.write_bytes(data.numpy().tobytes())
+        flat = RD.read_to_device(str(p), "cuda")
+        assert torch.equal(flat.cpu(), data.view(-1))
+        big = torch.zeros((n, 128), dtype=torch.uint8, device="cuda")
+        RD.read_rows_to_device(str(p), "cuda", 0, n, w, big[:, :w])
+        assert torch.equal(big[:, :w].cpu(), data)
+    finally:
+        RD.CHUNK = old
+        RD._RING = old_ring
+
+
 def test_stored_terasort_end_to_end(tmp_path):
     from dryad_amd.models.terasort import TeraSortConfig, TeraSortStoredJob
     from dryad_amd.parallel.comm import init_world
