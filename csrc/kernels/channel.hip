@@ -12,6 +12,7 @@
 //   pc_scatter_kernel  stable multi-column bucket scatter: each 512-row tile is ranked by bucket
 //                      with wave64 ballot multisplits, then every column is staged through LDS
 //                      (coalesced loads) and written as one contiguous run per bucket
+//                      (pc_scatter_rows_kernel: <= 32 bytes of dword columns per row staged whole)
 //   copy_segments      variable-length string bytes into a compact heap in row order (the string
 //                      heap of the rows sent to each rank, sent by a second all-to-all-v)
 #include "common.h"
@@ -173,6 +174,157 @@ __global__ __launch_bounds__(256) void pc_scatter_kernel(const void* __restrict_
   }
 }
 
+// pc_scatter_kernel for tables whose 4k-byte columns hold at most kPcChunk dwords per row in total
+// (e.g. a key and three int64 values, plus any 1- or 2-byte columns, moved one pass each after
+// them): every dword of the tile's rows, over all those columns, is loaded at once (kPcRowItems independent loads per lane, no branch around them: the
+// lanes past the tile re-read its first row) and staged in LDS as whole rows, then stored slot by
+// slot into every column.  Item i of lane t is dword c = i / 2 of tile row t + 256 (i % 2): the
+// column of every load and store is a compile-time dword index, its pointer a scalar.  The
+// per-column passes above keep one column's 4 KB per workgroup in flight between barriers (2.4 TB/s
+// in the 8-rank GroupBy's hash partition).
+constexpr int kPcRowItems = kPcTile * kPcChunk / kBlock;
+
+// global (not flat) accesses through a generic pointer of global memory: flat loads and stores
+// also count on the LDS wait counter, so every LDS wait would wait for them too
+__device__ __forceinline__ uint32_t gload(const uint32_t* p, uint64_t i) {
+  return reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(reinterpret_cast<uintptr_t>(p))[i];
+}
+__device__ __forceinline__ void gstore(uint32_t* p, uint64_t i, uint32_t v) {
+  reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(reinterpret_cast<uintptr_t>(p))[i] = v;
+}
+static_assert(kPcRowItems == 2 * kPcChunk && kPcTile == 2 * kBlock, "item i: dword i / 2, row half i % 2");
+
+template <bool PORT8>
+__global__ __launch_bounds__(256) void pc_scatter_rows_kernel(const void* __restrict__ ent, uint64_t n,
+                                                              const uint8_t* __restrict__ lut, PcCols cols,
+                                                              const int64_t* __restrict__ offsets, uint32_t G,
+                                                              uint64_t per_block) {
+  __shared__ uint32_t buf[kPcTile * kPcChunk];
+  __shared__ uint16_t perm[kPcTile];
+  __shared__ uint8_t dslot[kPcTile];
+  __shared__ uint32_t wcnt[4][256];
+  __shared__ int64_t goff[256];
+  __shared__ uint32_t bstart[256];
+  __shared__ uint32_t sc[4];
+  __shared__ uint8_t slut[256];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const uint64_t beg = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  if (beg >= end) return;                                    // uniform: the whole workgroup leaves
+  slut[t] = lut ? lut[t] : (uint8_t)t;
+  goff[t] = offsets[(uint64_t)t * G + blockIdx.x];
+  // row dword c -> its column's words, words per row and word index (all scalars)
+  const uint32_t* cin[kPcChunk];
+  uint32_t* cout[kPcChunk];
+  uint32_t cwpr[kPcChunk], cwd[kPcChunk];
+  uint32_t WT = 0;
+#pragma unroll
+  for (int c = 0; c < kPcChunk; ++c) {
+    cin[c] = nullptr;
+    cout[c] = nullptr;
+    cwpr[c] = 1;
+    cwd[c] = 0;
+    uint32_t start = 0;
+#pragma unroll
+    for (int k = 0; k < kPcMaxCols; ++k) {
+      const uint32_t wk = (uint32_t)k < cols.ncols && cols.width[k] >= 4 ? cols.width[k] >> 2 : 0u;
+      if ((uint32_t)c >= start && (uint32_t)c < start + wk) {
+        cin[c] = reinterpret_cast<const uint32_t*>(cols.in[k]);
+        cout[c] = reinterpret_cast<uint32_t*>(cols.out[k]);
+        cwpr[c] = wk;
+        cwd[c] = (uint32_t)c - start;
+      }
+      start += wk;
+    }
+    if (c == kPcChunk - 1) WT = start;
+  }
+  __syncthreads();
+  for (uint64_t base = beg; base < end; base += kPcTile) {
+    const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kPcTile ? (end - base) : kPcTile);
+    // the tile's rows, every column, all loads in flight
+    uint32_t v[kPcRowItems];
+#pragma unroll
+    for (int i = 0; i < kPcRowItems; ++i) {
+      const int c = i >> 1;
+      const uint32_t r = (uint32_t)t + (uint32_t)(i & 1) * kBlock;
+      v[i] = 0;
+      if ((uint32_t)c < WT) v[i] = gload(cin[c], (base + (r < cnt ? r : 0u)) * cwpr[c] + cwd[c]);
+    }
+    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    __syncthreads();
+    uint32_t rk[kPcItems], dg[kPcItems];
+#pragma unroll
+    for (int r = 0; r < kPcItems; ++r) {
+      const uint32_t pos = w * (kPcTile / 4) + r * 64 + l;
+      const bool valid = pos < cnt;
+      const uint32_t d = valid ? (uint32_t)slut[pc_port<PORT8>(ent, base + pos)] : 0u;
+      uint64_t peers = ballot64(valid);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool bit = (d >> k) & 1u;
+        const uint64_t b = ballot64(bit);
+        peers &= bit ? b : ~b;
+      }
+      const uint32_t below = popc_below(peers);
+      const uint32_t prior = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      rk[r] = prior + below;
+      dg[r] = d;
+    }
+#pragma unroll
+    for (int i = 0; i < kPcRowItems; ++i) {
+      const int c = i >> 1;
+      const uint32_t r = (uint32_t)t + (uint32_t)(i & 1) * kBlock;
+      if ((uint32_t)c < WT && r < cnt) buf[r * WT + c] = v[i];
+    }
+    __syncthreads();
+    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
+    uint32_t all;
+    bstart[t] = block_exclusive_scan256(tot, sc, all);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kPcItems; ++r) {
+      const uint32_t pos = w * (kPcTile / 4) + r * 64 + l;
+      if (pos < cnt) {
+        const uint32_t slot = bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
+        perm[slot] = (uint16_t)pos;
+        dslot[slot] = (uint8_t)dg[r];
+      }
+    }
+    __syncthreads();
+    // slot-major stores: consecutive slots of one bucket are consecutive output rows of a column
+#pragma unroll
+    for (int i = 0; i < kPcRowItems; ++i) {
+      const int c = i >> 1;
+      const uint32_t j = (uint32_t)t + (uint32_t)(i & 1) * kBlock;
+      if ((uint32_t)c < WT && j < cnt) {
+        const uint32_t d = dslot[j];
+        const uint64_t row = (uint64_t)(goff[d] + (int64_t)(j - bstart[d]));
+        gstore(cout[c], row * cwpr[c] + cwd[c], buf[(uint32_t)perm[j] * WT + c]);
+      }
+    }
+    __syncthreads();                   // every store has read buf
+    // 1- and 2-byte columns (e.g. a count column of int8 ones): one pass each through buf
+    for (uint32_t k = 0; k < cols.ncols; ++k) {
+      const uint32_t wb = cols.width[k];
+      if (wb >= 4) continue;
+      for (uint32_t j = t; j < cnt; j += kBlock) buf[j] = pc_load_narrow(cols.in[k], base + j, wb);
+      __syncthreads();
+      for (uint32_t j = t; j < cnt; j += kBlock) {
+        const uint32_t d = dslot[j];
+        pc_store_narrow(cols.out[k], (uint64_t)(goff[d] + (int64_t)(j - bstart[d])), wb, buf[perm[j]]);
+      }
+      __syncthreads();
+    }
+    goff[t] += tot;
+    __syncthreads();
+  }
+}
+
 // One wave per 64 consecutive rows: the wave's strings form one destination range of T bytes
 // (gaps between them allowed: bytes in a gap are not written); lane b copies bytes b, b+64, ...
 // after a 6-step search of the row that holds it.
@@ -275,7 +427,14 @@ DR_API int dr_pc_scatter(const void* ent, uint64_t n, const uint8_t* lut, const 
     c.width[k] = wb;
   }
   c.ncols = ncols;
-  if (port8)
+  uint32_t wt = 0;
+  for (uint32_t k = 0; k < ncols; ++k) wt += width[k] >= 4 ? width[k] >> 2 : 0u;
+  if (wt > 0 && wt <= (uint32_t)kPcChunk) {    // the dword columns' rows staged at once
+    if (port8)
+      pc_scatter_rows_kernel<true><<<G, 256, 0, s>>>(ent, n, lut, c, offsets, G, per_block);
+    else
+      pc_scatter_rows_kernel<false><<<G, 256, 0, s>>>(ent, n, lut, c, offsets, G, per_block);
+  } else if (port8)
     pc_scatter_kernel<true><<<G, 256, 0, s>>>(ent, n, lut, c, offsets, G, per_block);
   else
     pc_scatter_kernel<false><<<G, 256, 0, s>>>(ent, n, lut, c, offsets, G, per_block);

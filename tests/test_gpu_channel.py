@@ -45,6 +45,30 @@ def test_scatter_columns_matches_stable_argsort(n, nb):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("n,nb", [(1, 3), (511, 2), (100_000, 8), (2_000_003, 256)])
+@pytest.mark.parametrize("kind", ["4xint64", "3xint32", "int64+int32+f32", "8xint32", "int64+int8+3xint64+int16"])
+def test_scatter_whole_rows_matches_stable_argsort(n, nb, kind):
+    """Dword columns of <= 32 bytes per row in total take pc_scatter_rows_kernel (every dword of a
+    tile's rows loaded at once): the same stable order as the per-column kernel."""
+    g = torch.Generator(device="cuda").manual_seed(7 * n + nb)
+    ent = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    ent[:, 1] = torch.randint(0, nb, (n,), device="cuda", generator=g)
+    i64 = lambda: torch.randint(-2**62, 2**62, (n,), device="cuda", generator=g)          # noqa: E731
+    i32 = lambda: torch.randint(-2**31, 2**31 - 1, (n,), device="cuda", generator=g, dtype=torch.int32)  # noqa: E731
+    cols = {"4xint64": lambda: [i64() for _ in range(4)],
+            "3xint32": lambda: [i32() for _ in range(3)],
+            "int64+int32+f32": lambda: [i64(), i32(), torch.randn(n, device="cuda", generator=g)],
+            "8xint32": lambda: [i32() for _ in range(8)],
+            "int64+int8+3xint64+int16": lambda: [
+                i64(), torch.randint(-128, 127, (n,), device="cuda", generator=g, dtype=torch.int8), i64(), i64(),
+                i64(), torch.randint(-30000, 30000, (n,), device="cuda", generator=g, dtype=torch.int16)]}[kind]()
+    got, cnt = CH.scatter_columns(ent, n, cols, None)
+    exp, ecnt = _ref_scatter(ent, cols, None)
+    assert torch.equal(cnt, ecnt)
+    for a, b in zip(got, exp):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("n,nb", [(1, 3), (513, 7), (2_000_003, 256), (777_777, 37)])
 def test_uint8_ports_match_e128_entries(n, nb):
     """The hash partitioner's compact form (one uint8 port per row) moves every column exactly as
