@@ -175,8 +175,8 @@ __global__ __launch_bounds__(256) void pc_scatter_kernel(const void* __restrict_
 }
 
 // pc_scatter_kernel for tables whose 4k-byte columns hold at most kPcChunk dwords per row in total
-// (e.g. a key and three int64 values, plus any 1- or 2-byte columns, moved one pass each after
-// them): every dword of the tile's rows, over all those columns, is loaded at once (kPcRowItems independent loads per lane, no branch around them: the
+// (e.g. a key and three int64 values) plus at most kPcNarrow 1- or 2-byte columns (e.g. a count of
+// int8 ones): every dword and narrow value of the tile's rows, over all columns, is loaded at once (kPcRowItems independent loads per lane, no branch around them: the
 // lanes past the tile re-read its first row) and staged in LDS as whole rows, then stored slot by
 // slot into every column.  Item i of lane t is dword c = i / 2 of tile row t + 256 (i % 2): the
 // column of every load and store is a compile-time dword index, its pointer a scalar.  The
@@ -192,6 +192,17 @@ __device__ __forceinline__ uint32_t gload(const uint32_t* p, uint64_t i) {
 __device__ __forceinline__ void gstore(uint32_t* p, uint64_t i, uint32_t v) {
   reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(reinterpret_cast<uintptr_t>(p))[i] = v;
 }
+__device__ __forceinline__ uint32_t gload_narrow(const uint8_t* p, uint64_t row, uint32_t w) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  return w == 1 ? (uint32_t)reinterpret_cast<const __attribute__((address_space(1))) uint8_t*>(a)[row]
+                : (uint32_t)reinterpret_cast<const __attribute__((address_space(1))) uint16_t*>(a)[row];
+}
+__device__ __forceinline__ void gstore_narrow(uint8_t* p, uint64_t row, uint32_t w, uint32_t v) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  if (w == 1) reinterpret_cast<__attribute__((address_space(1))) uint8_t*>(a)[row] = (uint8_t)v;
+  else reinterpret_cast<__attribute__((address_space(1))) uint16_t*>(a)[row] = (uint16_t)v;
+}
+constexpr int kPcNarrow = 2;             // 1- / 2-byte columns the row kernel carries
 static_assert(kPcRowItems == 2 * kPcChunk && kPcTile == 2 * kBlock, "item i: dword i / 2, row half i % 2");
 
 template <bool PORT8>
@@ -200,6 +211,7 @@ __global__ __launch_bounds__(256) void pc_scatter_rows_kernel(const void* __rest
                                                               const int64_t* __restrict__ offsets, uint32_t G,
                                                               uint64_t per_block) {
   __shared__ uint32_t buf[kPcTile * kPcChunk];
+  __shared__ uint16_t nbuf[kPcNarrow][kPcTile];
   __shared__ uint16_t perm[kPcTile];
   __shared__ uint8_t dslot[kPcTile];
   __shared__ uint32_t wcnt[4][256];
@@ -238,6 +250,27 @@ __global__ __launch_bounds__(256) void pc_scatter_rows_kernel(const void* __rest
     }
     if (c == kPcChunk - 1) WT = start;
   }
+  // the 1- and 2-byte columns (at most kPcNarrow: the caller checks), loaded with the dwords
+  const uint8_t* nin[kPcNarrow];
+  uint8_t* nout[kPcNarrow];
+  uint32_t nw[kPcNarrow];
+#pragma unroll
+  for (int m = 0; m < kPcNarrow; ++m) {
+    nin[m] = nullptr;
+    nout[m] = nullptr;
+    nw[m] = 0;
+    uint32_t seen = 0;
+#pragma unroll
+    for (int k = 0; k < kPcMaxCols; ++k) {
+      const bool narrow = (uint32_t)k < cols.ncols && cols.width[k] < 4;
+      if (narrow && seen == (uint32_t)m) {
+        nin[m] = cols.in[k];
+        nout[m] = cols.out[k];
+        nw[m] = cols.width[k];
+      }
+      seen += narrow ? 1u : 0u;
+    }
+  }
   __syncthreads();
   for (uint64_t base = beg; base < end; base += kPcTile) {
     const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kPcTile ? (end - base) : kPcTile);
@@ -250,6 +283,14 @@ __global__ __launch_bounds__(256) void pc_scatter_rows_kernel(const void* __rest
       v[i] = 0;
       if ((uint32_t)c < WT) v[i] = gload(cin[c], (base + (r < cnt ? r : 0u)) * cwpr[c] + cwd[c]);
     }
+    uint32_t nv[kPcNarrow][2];
+#pragma unroll
+    for (int m = 0; m < kPcNarrow; ++m)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t r = (uint32_t)t + (uint32_t)h * kBlock;
+        nv[m][h] = nw[m] ? gload_narrow(nin[m], base + (r < cnt ? r : 0u), nw[m]) : 0u;
+      }
     wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
     __syncthreads();
     uint32_t rk[kPcItems], dg[kPcItems];
@@ -279,6 +320,13 @@ __global__ __launch_bounds__(256) void pc_scatter_rows_kernel(const void* __rest
       const uint32_t r = (uint32_t)t + (uint32_t)(i & 1) * kBlock;
       if ((uint32_t)c < WT && r < cnt) buf[r * WT + c] = v[i];
     }
+#pragma unroll
+    for (int m = 0; m < kPcNarrow; ++m)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t r = (uint32_t)t + (uint32_t)h * kBlock;
+        if (nw[m] && r < cnt) nbuf[m][r] = (uint16_t)nv[m][h];
+      }
     __syncthreads();
     const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
     const uint32_t tot = c0 + c1 + c2 + c3;
@@ -307,19 +355,17 @@ __global__ __launch_bounds__(256) void pc_scatter_rows_kernel(const void* __rest
         gstore(cout[c], row * cwpr[c] + cwd[c], buf[(uint32_t)perm[j] * WT + c]);
       }
     }
-    __syncthreads();                   // every store has read buf
-    // 1- and 2-byte columns (e.g. a count column of int8 ones): one pass each through buf
-    for (uint32_t k = 0; k < cols.ncols; ++k) {
-      const uint32_t wb = cols.width[k];
-      if (wb >= 4) continue;
-      for (uint32_t j = t; j < cnt; j += kBlock) buf[j] = pc_load_narrow(cols.in[k], base + j, wb);
-      __syncthreads();
-      for (uint32_t j = t; j < cnt; j += kBlock) {
-        const uint32_t d = dslot[j];
-        pc_store_narrow(cols.out[k], (uint64_t)(goff[d] + (int64_t)(j - bstart[d])), wb, buf[perm[j]]);
+#pragma unroll
+    for (int m = 0; m < kPcNarrow; ++m)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t j = (uint32_t)t + (uint32_t)h * kBlock;
+        if (nw[m] && j < cnt) {
+          const uint32_t d = dslot[j];
+          gstore_narrow(nout[m], (uint64_t)(goff[d] + (int64_t)(j - bstart[d])), nw[m], nbuf[m][perm[j]]);
+        }
       }
-      __syncthreads();
-    }
+    __syncthreads();                   // every store has read goff / bstart
     goff[t] += tot;
     __syncthreads();
   }
@@ -427,9 +473,12 @@ DR_API int dr_pc_scatter(const void* ent, uint64_t n, const uint8_t* lut, const 
     c.width[k] = wb;
   }
   c.ncols = ncols;
-  uint32_t wt = 0;
-  for (uint32_t k = 0; k < ncols; ++k) wt += width[k] >= 4 ? width[k] >> 2 : 0u;
-  if (wt > 0 && wt <= (uint32_t)kPcChunk) {    // the dword columns' rows staged at once
+  uint32_t wt = 0, narrow = 0;
+  for (uint32_t k = 0; k < ncols; ++k) {
+    wt += width[k] >= 4 ? width[k] >> 2 : 0u;
+    narrow += width[k] < 4 ? 1u : 0u;
+  }
+  if (wt > 0 && wt <= (uint32_t)kPcChunk && narrow <= (uint32_t)kPcNarrow) {   // whole rows staged at once
     if (port8)
       pc_scatter_rows_kernel<true><<<G, 256, 0, s>>>(ent, n, lut, c, offsets, G, per_block);
     else

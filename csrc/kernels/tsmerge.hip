@@ -419,13 +419,21 @@ __global__ __launch_bounds__(256) void ts_pack_rows_kernel(const uint32_t* __res
     head = head < words ? head : words;
     if (t < head) o[t] = stage[t];
     const uint32_t nch = (words - head) >> 2;
-    for (uint32_t c = t; c < nch; c += 256) {
-      const uint32_t q = head + 4 * c;
-      uint32_t* d = o + q;
-      __builtin_nontemporal_store(stage[q], d);
-      __builtin_nontemporal_store(stage[q + 1], d + 1);
-      __builtin_nontemporal_store(stage[q + 2], d + 2);
-      __builtin_nontemporal_store(stage[q + 3], d + 3);
+    if (head == 0) {                 // (a tile starts at a multiple of 256 rows: always, for an aligned out)
+      typedef uint32_t u32x4n __attribute__((ext_vector_type(4)));
+      for (uint32_t c = t; c < nch; c += 256) {  // one 16-byte nontemporal store per lane and chunk
+        const u32x4n v = *reinterpret_cast<const u32x4n*>(stage + 4 * c);
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4n*>(o + 4 * c));
+      }
+    } else {
+      for (uint32_t c = t; c < nch; c += 256) {
+        const uint32_t q = head + 4 * c;
+        uint32_t* d = o + q;
+        __builtin_nontemporal_store(stage[q], d);
+        __builtin_nontemporal_store(stage[q + 1], d + 1);
+        __builtin_nontemporal_store(stage[q + 2], d + 2);
+        __builtin_nontemporal_store(stage[q + 3], d + 3);
+      }
     }
     for (uint32_t q = head + 4 * nch + t; q < words; q += 256) o[q] = stage[q];
     __syncthreads();
