@@ -8,6 +8,6 @@ tail -1 gpurun_out/r5c_pc2_tests.log
 timeout -k 10 300 python -u bench.py --loopback-ranks 8 --steps 3 --warmup 1 > gpurun_out/r5c_pc2_lb8.log 2>&1 || { tail -20 gpurun_out/r5c_pc2_lb8.log; exit 1; }
 grep "step 2" gpurun_out/r5c_pc2_lb8.log | cut -c1-250; tail -1 gpurun_out/r5c_pc2_lb8.log | grep -o '"validated": [a-z]*'
 cd benchmarks
-timeout -k 10 500 rocprofv3 --kernel-trace --stats -d ../gpurun_out/prof_r5c_gblb3 -o run --output-format csv -- \
-  python3 -u groupby.py --loopback-ranks 8 --steps 2 --warmup 1 > ../gpurun_out/r5c_gblb3.log 2>&1 || { tail -20 ../gpurun_out/r5c_gblb3.log; exit 1; }
-grep '"metric"' ../gpurun_out/r5c_gblb3.log | cut -c1-450
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d ../gpurun_out/prof_r5c_gblb4 -o run --output-format csv -- \
+  python3 -u groupby.py --loopback-ranks 8 --steps 2 --warmup 1 > ../gpurun_out/r5c_gblb4.log 2>&1 || { tail -20 ../gpurun_out/r5c_gblb4.log; exit 1; }
+grep '"metric"' ../gpurun_out/r5c_gblb4.log | cut -c1-450
