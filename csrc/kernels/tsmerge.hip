@@ -25,20 +25,45 @@ constexpr uint32_t kTmRows = kTmCap / kTmThreads;  // rows per lane, held in reg
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(4)));   // 16-byte access, 4-byte aligned
 constexpr uint32_t kTmBins = 1024;                 // LDS counting-sort bins (next 10 key bits)
 
+// Four entries per lane per step (two 16-byte loads; the entry before them comes from the lane
+// below, or one cached load for lane 0 of a wave), every bucket boundary between consecutive
+// entries written once.
+template <bool PAIRS>
 __global__ __launch_bounds__(256) void ts_fine_starts_kernel(const E64* __restrict__ ent, uint64_t n, uint32_t fb,
                                                              uint32_t* __restrict__ starts) {
   const uint32_t nb = 1u << fb;
   const int sh = 64 - (int)fb;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t b = (uint32_t)(ent[i].v >> sh);
-    if (i == 0) {
-      for (uint32_t k = 0; k <= b; ++k) starts[k] = 0;
+  const uint64_t groups = (n + 3) / 4;
+  const uint64_t* e = reinterpret_cast<const uint64_t*>(ent);
+  for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x; g0 < groups; g0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t g = g0 + threadIdx.x;
+    const uint64_t i0 = 4 * g;
+    uint32_t b[4] = {0, 0, 0, 0};
+    if (PAIRS && i0 + 3 < n) {
+      const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(e + i0);
+      const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(e + i0 + 2);
+      b[0] = (uint32_t)(a.x >> sh); b[1] = (uint32_t)(a.y >> sh); b[2] = (uint32_t)(c.x >> sh); b[3] = (uint32_t)(c.y >> sh);
     } else {
-      const uint32_t pb = (uint32_t)(ent[i - 1].v >> sh);
-      for (uint32_t k = pb + 1; k <= b; ++k) starts[k] = (uint32_t)i;
+      for (int k = 0; k < 4; ++k) b[k] = i0 + k < n ? (uint32_t)(e[i0 + k] >> sh) : 0u;
     }
-    if (i == n - 1) {
-      for (uint32_t k = b + 1; k <= nb; ++k) starts[k] = (uint32_t)n;
+    // the bucket of entry i0 - 1: the lane below's last, or a load at a wave's first lane
+    uint32_t prev = __shfl_up(b[3], 1, 64);
+    if (lane_id() == 0 && i0 > 0 && i0 - 1 < n) prev = (uint32_t)(e[i0 - 1] >> sh);
+    if (i0 < n) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t i = i0 + k;
+        if (i >= n) break;
+        const uint32_t pb = k == 0 ? prev : b[k - 1];
+        if (i == 0) {
+          for (uint32_t q = 0; q <= b[k]; ++q) starts[q] = 0;
+        } else {
+          for (uint32_t q = pb + 1; q <= b[k]; ++q) starts[q] = (uint32_t)i;
+        }
+        if (i == n - 1) {
+          for (uint32_t q = b[k] + 1; q <= nb; ++q) starts[q] = (uint32_t)n;
+        }
+      }
     }
   }
 }
@@ -473,7 +498,10 @@ DR_API int dr_ts_pack_rows(const uint8_t* rows, uint64_t n_in, uint32_t pitch, c
 DR_API int dr_ts_fine_starts(const E64* ent, uint64_t n, uint32_t fb, uint32_t* starts, hipStream_t s) {
   if (fb < 16 || fb > 24 || n >= (1ull << 32)) return (int)hipErrorInvalidValue;   // FINE_MIN/MAX_BITS
   if (n == 0) return (int)hipMemsetAsync(starts, 0, ((size_t(1) << fb) + 1) * sizeof(uint32_t), s);
-  ts_fine_starts_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(ent, n, fb, starts);
+  if (reinterpret_cast<uintptr_t>(ent) & 15)       // 16-byte pair loads need 16-byte aligned entries
+    ts_fine_starts_kernel<false><<<grid_for((n + 3) / 4, 256, 16384), 256, 0, s>>>(ent, n, fb, starts);
+  else
+    ts_fine_starts_kernel<true><<<grid_for((n + 3) / 4, 256, 16384), 256, 0, s>>>(ent, n, fb, starts);
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -25,12 +25,17 @@ def test_gen_entries64_match_generated_rows():
 
 
 @pytest.mark.parametrize("fb", [16, 24])
-def test_fine_starts(fb):
-    g = np.random.default_rng(fb)
-    n = 200_000
+@pytest.mark.parametrize("n,skew", [(200_000, 0), (200_003, 0), (1, 0), (7, 1), (100_001, 1)])
+def test_fine_starts(fb, n, skew):
+    """Bucket starts of window-sorted entries; four entries per lane with 16-byte loads, or 8-byte
+    loads when the entries are not 16-byte aligned (``skew``: a slice one entry in)."""
+    g = np.random.default_rng(fb + n)
     win = np.sort(g.integers(0, 1 << 32, size=n, dtype=np.uint64))
-    win[:5000] = win[5000]                       # a long run of one bucket
-    e = torch.from_numpy(((win << np.uint64(32)) | np.arange(n, dtype=np.uint64)).view(np.int64)).cuda()
+    win[:min(n, 5000)] = win[min(n - 1, 5000)]   # a long run of one bucket
+    full = torch.from_numpy(((win << np.uint64(32)) | np.arange(n, dtype=np.uint64)).view(np.int64)).cuda()
+    e = full
+    if skew:
+        e = torch.cat([full[:1], full]).contiguous()[1:]
     starts = TS.fine_starts(e, fb).cpu().numpy().astype(np.int64)
     b = (win >> np.uint64(32 - fb)).astype(np.int64)
     exp = np.searchsorted(b, np.arange((1 << fb) + 1), side="left")
