@@ -122,6 +122,8 @@ _DEFAULTS = dict(
     StreamChunkBytes=4 << 30,     # ... and their chunk size
     StreamAggregate=None,         # read -> GroupBy / Distinct stages folded chunk by chunk in bounded HBM
     #                               (runtime/stream_agg.py; None: when a partition exceeds HbmBudgetBytes)
+    StreamDenseState=True,        # ... a streamed GroupBy of one integer key keeps its running state
+    #                               directly addressed by key while the keys' range fits the budget
     GraceJoin=None,               # a Join as the partitioned grace join stage (runtime/grace_stage.py;
     #                               None: when its inputs would crowd the HBM budget; False: never)
     GraceJoinStringBytes=64,      # ... inline bytes per string field in its packed bucket rows (longer

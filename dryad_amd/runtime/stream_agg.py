@@ -145,6 +145,141 @@ def _buckets(t: DeviceTable, K: int, agg_kind: str) -> list:
     return [nt.slice(off[k], off[k + 1]) if off[k + 1] > off[k] else None for k in range(K)]
 
 
+class DenseState:
+    """Running GroupBy state of ONE integer key addressed directly by key - lo: one slot per key
+    of the keys' range, per accumulator column (sums and counts added, min / max reduced into
+    their slots by the device scatter kernels) and an occupancy byte.  Used while the range times
+    the slot bytes fits DENSE_FRACTION of the budget (e.g. 2^30 keys x 33 bytes = 35 GB of a 60 GB
+    budget): a chunk's partial rows then fold into the state in place, with no hash buckets,
+    pending pieces, combines or spills.  The range grows (coarsely aligned) as chunks reach past it;
+    when it no longer fits, the state becomes one partial piece of the hash-bucket path."""
+
+    DENSE_FRACTION = 0.75
+
+    def __init__(self, d, budget: int):
+        self.d, self.cap = d, int(budget * self.DENSE_FRACTION)
+        self.lo = self.hi = None
+        self.specs = None            # [(state name, op, source column name or None, dtype)]
+        self.state: dict = {}
+        self.seen = None
+        self.meta = None
+        self.kdtype = None
+        self.outdt: dict = {}
+
+    @staticmethod
+    def eligible(part: DeviceTable) -> bool:
+        m = part.shape.pytype
+        k = part.cols.get("k0") if part.rows is None else None
+        return (part.shape.kind == "partial" and not part.strs and getattr(m, "nkeys", 0) == 1 and k is not None
+                and k.dtype in (torch.int8, torch.int16, torch.int32, torch.int64))
+
+    def _plan(self, part: DeviceTable):
+        specs = []
+        for j, a in enumerate(self.d.aggs):
+            col = part.cols.get(f"a{j}")
+            if a.kind == "count":
+                implicit = col is None or col.dtype == torch.int8
+                specs.append((f"a{j}", "count" if implicit else "sum", None if implicit else f"a{j}", torch.int64))
+                self.outdt[f"a{j}"] = torch.int64
+            elif a.kind == "sum":
+                dt = torch.float64 if col.dtype.is_floating_point else torch.int64
+                specs.append((f"a{j}", "sum", f"a{j}", dt))
+                self.outdt[f"a{j}"] = dt
+            elif a.kind in ("min", "max"):
+                specs.append((f"a{j}", a.kind, f"a{j}", col.dtype))
+                self.outdt[f"a{j}"] = col.dtype
+            elif a.kind == "avg":
+                c = part.cols.get(f"c{j}")
+                specs.append((f"a{j}", "sum", f"a{j}", torch.float64))
+                specs.append((f"c{j}", "count" if c is None or c.dtype == torch.int8 else "sum",
+                              None if c is None or c.dtype == torch.int8 else f"c{j}", torch.int64))
+                self.outdt[f"a{j}"], self.outdt[f"c{j}"] = torch.float64, torch.int64
+            else:
+                return None              # any / all / user aggregates: the bucket path
+        return specs
+
+    def _slot_bytes(self) -> int:
+        return 1 + sum(torch.empty(0, dtype=dt).element_size() for _, _, _, dt in self.specs)
+
+    def _alloc(self, lo: int, hi: int, dev):
+        R = hi - lo + 1
+        st = {}
+        for name, op, _, dt in self.specs:
+            if op == "min":
+                fill = torch.iinfo(dt).max if not dt.is_floating_point else float("inf")
+            elif op == "max":
+                fill = torch.iinfo(dt).min if not dt.is_floating_point else float("-inf")
+            else:
+                fill = 0
+            st[name] = torch.full((R,), fill, dtype=dt, device=dev)
+        seen = torch.zeros(R, dtype=torch.int8, device=dev)
+        if self.lo is not None:          # the old range moves into the grown one
+            a, b = self.lo - lo, self.hi - lo + 1
+            for name in st:
+                st[name][a:b].copy_(self.state[name])
+            seen[a:b].copy_(self.seen)
+        self.state, self.seen, self.lo, self.hi = st, seen, lo, hi
+
+    def add(self, part: DeviceTable) -> bool:
+        """Fold a chunk's partial rows in; False when its keys' range would not fit (the caller
+        moves to the hash buckets)."""
+        n = part.n
+        if n == 0:
+            return True
+        if self.specs is None:
+            self.specs = self._plan(part)
+            self.meta = part.shape.pytype
+            self.kdtype = part.cols["k0"].dtype
+            if self.specs is None:
+                return False
+        k = part.cols["k0"][:n]
+        mn, mx = (int(x) for x in torch.aminmax(k))
+        lo, hi = (mn, mx) if self.lo is None else (min(mn, self.lo), max(mx, self.hi))
+        if self.lo is None or lo < self.lo or hi > self.hi:
+            span = hi - lo + 1
+            g = 1 << max(0, span.bit_length() - 4)        # coarse alignment: few regrowths
+            alo, ahi = (lo // g) * g, -(-(hi + 1) // g) * g - 1
+            if (ahi - alo + 1) * self._slot_bytes() <= self.cap:
+                lo, hi = alo, ahi
+            if (hi - lo + 1) * self._slot_bytes() > self.cap:
+                return False
+            self._alloc(lo, hi, k.device)
+        idx = (k - self.lo).to(torch.int64)
+        self.seen.index_fill_(0, idx, 1)
+        for name, op, src, dt in self.specs:
+            st = self.state[name]
+            if op == "count":
+                st.index_add_(0, idx, torch.ones(1, dtype=dt, device=st.device).expand(n))
+                continue
+            v = part.cols[src][:n]
+            v = v if v.dtype == dt else v.to(dt)
+            if op == "sum":
+                st.index_add_(0, idx, v)
+            else:
+                st.scatter_reduce_(0, idx, v, reduce="amin" if op == "min" else "amax", include_self=True)
+        return True
+
+    def nbytes(self) -> int:
+        return 0 if self.lo is None else (self.hi - self.lo + 1) * self._slot_bytes()
+
+    def to_partial(self) -> DeviceTable | None:
+        """The occupied slots as a partial table in the folded (standard) layout."""
+        if self.lo is None:
+            return None
+        occ = torch.nonzero(self.seen).squeeze(1)
+        out = {"k0": (occ + self.lo).to(self.kdtype)}
+        for name, _, _, _ in self.specs:
+            out[name] = self.state[name].index_select(0, occ)
+        for j, a in enumerate(self.d.aggs):      # min / max keep their dtype (as combine_partials)
+            if a.kind in ("min", "max") and out[f"a{j}"].dtype != self.outdt[f"a{j}"]:
+                out[f"a{j}"] = out[f"a{j}"].to(self.outdt[f"a{j}"])
+        self.state, self.seen = {}, None
+        from ..gpu.table import PartialMeta
+        m = self.meta
+        meta = PartialMeta(m.nkeys, m.kinds, m.key_form)
+        return DeviceTable.from_columns(out, Shape("partial", list(out), meta))
+
+
 class StreamAggregator:
     """Bounded-HBM GroupBy / Distinct over a stream of chunks (see the module docstring)."""
 
@@ -159,6 +294,9 @@ class StreamAggregator:
         self.pending: list = []        # per bucket: [DeviceTable | HostPiece]
         self.spilled: set = set()
         self.stats = dict(chunks=0, records_in=0, combines=0, spilled_bytes=0, spill_events=0)
+        # GroupBy of one integer key: the directly addressed running state while it fits
+        use = runner.ctx._props.get("StreamDenseState", True) and self.kind == "group"
+        self.dense = DenseState(self.d, self.budget) if use else None
 
     # ------------------------------------------------------------------ per chunk
     def _partial(self, t: DeviceTable) -> DeviceTable:
@@ -223,15 +361,29 @@ class StreamAggregator:
     def add_chunk(self, t: DeviceTable):
         self.stats["chunks"] += 1
         self.stats["records_in"] += t.n
+        if "chunk_bytes_first" not in self.p:
+            self.p["chunk_bytes_first"] = _nbytes(t)
         data = t
         for op in self.p["pre"]:
             data = self.runner._run_op(op, [data], self.v, self.s)
         if data is None or data.n == 0:
             return
         part = self._partial(data)
+        if self.dense is not None:
+            if DenseState.eligible(part) and self.dense.add(part):
+                self.stats["dense_state_GB"] = round(self.dense.nbytes() / 1e9, 2)
+                return
+            # the keys outgrew the dense state: it becomes one piece of the hash-bucket path
+            prior, self.dense = self.dense.to_partial(), None
+            self.stats["dense_fallback"] = True
+            if prior is not None and prior.n:
+                self._add_partial(prior, rows_in=t.n)
+        self._add_partial(part, rows_in=t.n)
+
+    def _add_partial(self, part: DeviceTable, rows_in: int):
         if self.K is None:
-            self.p["chunk_bytes_first"] = _nbytes(t)
-            self._choose_buckets(part, t.n)
+            self.p["chunk_bytes_first"] = self.p.get("chunk_bytes_first") or _nbytes(part)
+            self._choose_buckets(part, rows_in)
         for k, piece in enumerate(_buckets(part, self.K, self.kind)):
             if piece is None:
                 continue
@@ -249,6 +401,12 @@ class StreamAggregator:
     # ------------------------------------------------------------------ end of stream
     def bucket_results(self, final: bool):
         """Yield each bucket's folded state (``final``: reduced to the GroupBy's result)."""
+        if self.dense is not None:
+            t = self.dense.to_partial()
+            self.dense = None
+            if t is not None and t.n:
+                yield G.final_reduce(t, self.d) if final else t
+            return
         for k in range(self.K or 0):
             t = self._fold([self.state[k]] + self.pending[k])
             self.state[k], self.pending[k] = None, []

@@ -30,23 +30,49 @@ def _stats(c):
     return r, st
 
 
-@pytest.mark.parametrize("keys", [3000, 400_000])
-def test_streamed_groupby_matches_oracle(keys):
+@pytest.mark.parametrize("keys,dense", [(3000, False), (400_000, False), (3000, True), (400_000, True),
+                                        (4_000_000, True)])
+def test_streamed_groupby_matches_oracle(keys, dense):
+    """Hash-bucketed running states (StreamDenseState=False), and the directly addressed dense state
+    of the integer key: it holds 3000 and 400k keys (32 MB budget); 4M keys never fit (24 MB),
+    so the stream goes to the hash buckets from its first chunk."""
     src = SRC.format(n=600_000, P=1, k=keys)
     q = lambda c: c.FromStore(src).Where(lambda r: r[3] % 7 != 0).GroupBy(  # noqa: E731
         lambda r: r[0], lambda k, g: (k, g.Count(), g.Sum(lambda r: r[1]), g.Min(lambda r: r[2]),
                                       g.Max(lambda r: r[4]), g.Average(lambda r: r[5])))
-    g = _ctx()
+    g = _ctx(budget=(32 << 20) if dense and keys < 1_000_000 else (24 << 20))
+    g.StreamDenseState = dense
     got = sorted(q(g))
     res, st = _stats(g)
-    assert st and st[0]["chunks"] > 4 and st[0]["combines"] > 0, st
-    if keys > 100_000:
-        assert st[0]["spilled_bytes"] > 0, st          # the states outgrow the 24 MB budget
+    assert st and st[0]["chunks"] > 4, st
+    if not dense:
+        assert st[0]["combines"] > 0, st
+        if keys > 100_000:
+            assert st[0]["spilled_bytes"] > 0, st      # the states outgrow the 24 MB budget
+    elif keys < 1_000_000:
+        assert st[0].get("dense_state_GB") is not None and not st[0].get("dense_fallback"), st
+        assert st[0]["combines"] == 0 and st[0]["spilled_bytes"] == 0, st
+    else:
+        assert st[0].get("dense_fallback"), st
     assert res["fallbacks"] == [], res["fallbacks"]
     exp = sorted(q(_loc()))
     assert len(got) == len(exp)
     for a, b in zip(got, exp):
         assert a[:5] == b[:5] and abs(a[5] - b[5]) <= 1e-9 * max(1.0, abs(b[5])), (a, b)
+
+
+def test_dense_state_that_outgrows_the_budget_becomes_a_bucket_piece():
+    """Keys that grow with the stream (gen://range): the dense state regrows until its range no
+    longer fits, then its occupied slots join the hash-bucket path as one partial piece."""
+    src = "gen://range?count=4000000&partitions=1"
+    q = lambda c: c.FromStore(src).GroupBy(  # noqa: E731
+        lambda x: x // 4, lambda k, g: (k, g.Count(), g.Sum(lambda x: x), g.Max(lambda x: x)))
+    g = _ctx(budget=24 << 20, chunk=1 << 20)
+    got = sorted(q(g))
+    res, st = _stats(g)
+    assert st and st[0].get("dense_fallback") and st[0]["chunks"] > 8, st
+    assert res["fallbacks"] == [], res["fallbacks"]
+    assert got == sorted(q(_loc()))
 
 
 def test_streamed_distinct_matches_oracle():
