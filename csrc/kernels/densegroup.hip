@@ -539,3 +539,91 @@ DR_API int dr_dg_aggregate(const void* rows, const int64_t* rstart, const int64_
   DR_LAUNCH_CHECK();
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Dense running state of a streamed GroupBy (runtime/stream_agg.DenseState): one slot per key of
+// the range [lo, lo + R), one array per accumulator.  A chunk's (partial) rows fold into it in ONE
+// pass: per row the slot index, the occupancy byte, and every accumulator's atomic (count / add /
+// min / max), instead of one library scatter kernel per accumulator re-reading the keys.
+namespace {
+constexpr int kDsMaxSpecs = 8;
+
+struct DsSpecs {
+  void* state[kDsMaxSpecs];
+  const void* val[kDsMaxSpecs];
+  uint32_t op[kDsMaxSpecs];      // 0 count (+1), 1 add, 2 min, 3 max
+  uint32_t sdt[kDsMaxSpecs];     // state dtype: 0 int64, 1 float64 (add only)
+  uint32_t vdt[kDsMaxSpecs];     // value dtype: 0 int64, 1 float64, 2 int32, 3 int8, 4 float32, 5 int16
+  uint32_t nspec;
+};
+
+__device__ __forceinline__ int64_t ds_load_i(const void* p, uint32_t dt, uint64_t i) {
+  switch (dt) {
+    case 0: return static_cast<const int64_t*>(p)[i];
+    case 2: return static_cast<const int32_t*>(p)[i];
+    case 3: return static_cast<const int8_t*>(p)[i];
+    case 5: return static_cast<const int16_t*>(p)[i];
+    case 1: return (int64_t) static_cast<const double*>(p)[i];
+    default: return (int64_t) static_cast<const float*>(p)[i];
+  }
+}
+
+__device__ __forceinline__ double ds_load_f(const void* p, uint32_t dt, uint64_t i) {
+  if (dt == 1) return static_cast<const double*>(p)[i];
+  if (dt == 4) return (double)static_cast<const float*>(p)[i];
+  return (double)ds_load_i(p, dt, i);
+}
+
+__global__ __launch_bounds__(256) void dense_state_update_kernel(const void* __restrict__ key, uint32_t kdt, uint64_t n,
+                                                                 int64_t lo, uint64_t range, uint8_t* __restrict__ seen,
+                                                                 DsSpecs sp, uint32_t* __restrict__ bad) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t idx = (uint64_t)(ds_load_i(key, kdt, i) - lo);
+    if (idx >= range) {                  // a key outside the state (a broken caller): not stored
+      atomicOr(bad, 1u);
+      continue;
+    }
+    seen[idx] = 1;
+    for (uint32_t s = 0; s < sp.nspec; ++s) {
+      const uint32_t op = sp.op[s];
+      if (sp.sdt[s] == 1) {
+        atomicAdd(static_cast<double*>(sp.state[s]) + idx, ds_load_f(sp.val[s], sp.vdt[s], i));
+        continue;
+      }
+      long long* st = static_cast<long long*>(sp.state[s]) + idx;
+      if (op == 0) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(st), 1ull);
+      } else {
+        const long long v = (long long)ds_load_i(sp.val[s], sp.vdt[s], i);
+        if (op == 1) atomicAdd(reinterpret_cast<unsigned long long*>(st), (unsigned long long)v);
+        else if (op == 2) atomicMin(st, v);
+        else atomicMax(st, v);
+      }
+    }
+  }
+}
+}  // namespace
+
+// key: n keys of dtype kdt (0 int64, 2 int32, 5 int16, 3 int8); seen: `range` bytes; state / val /
+// op / sdt / vdt: nspec accumulators (see DsSpecs; val ignored for count).  bad: set when a key
+// falls outside [lo, lo + range).
+DR_API int dr_dense_state_update(const void* key, uint32_t kdt, uint64_t n, int64_t lo, uint64_t range, uint8_t* seen,
+                                 void* const* state, const void* const* val, const uint32_t* op, const uint32_t* sdt,
+                                 const uint32_t* vdt, uint32_t nspec, uint32_t* bad, hipStream_t s) {
+  if (nspec > (uint32_t)kDsMaxSpecs || (kdt != 0 && kdt != 2 && kdt != 3 && kdt != 5)) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  DsSpecs sp;
+  for (uint32_t k = 0; k < nspec; ++k) {
+    if (op[k] > 3 || sdt[k] > 1 || vdt[k] > 5 || (sdt[k] == 1 && op[k] != 1) || (op[k] != 0 && val[k] == nullptr))
+      return (int)hipErrorInvalidValue;
+    sp.state[k] = state[k];
+    sp.val[k] = val[k];
+    sp.op[k] = op[k];
+    sp.sdt[k] = sdt[k];
+    sp.vdt[k] = vdt[k];
+  }
+  sp.nspec = nspec;
+  dense_state_update_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(key, kdt, n, lo, range, seen, sp, bad);
+  DR_LAUNCH_CHECK();
+  return 0;
+}

@@ -932,10 +932,11 @@ def op_group_partial(op, inputs, v):
         nd, m = R.estimate_distinct(kcols[0])
         from ..ops.radixagg import distinct_upper_estimate
         nd_est = distinct_upper_estimate(nd, m, t.n)
-        if v.partitions > 1 and op.get("adaptive", True) and nd_est >= RAW_PARTIAL_FRACTION * t.n:
+        if (v.partitions > 1 or op.get("raw_ok")) and op.get("adaptive", True) and nd_est >= RAW_PARTIAL_FRACTION * t.n:
             # almost every key distinct: folding would barely shrink the rows the shuffle moves
             # but cost a full aggregation pass (8-rank GroupBy, 2^30 keys per 1.25e9 rows: 173 vs
             # 104 ms per rank, profiles/r5/gb_lb8_*.log): the rows go out as a raw partial table
+            # (``raw_ok``: a streamed GroupBy whose dense running state folds the rows itself)
             return _raw_partial(d, t, kcols[0], form)
         if nd <= R.HASH_AGG_MAX_KEYS and nd * 8 < m:
             got = R.hash_aggregate(kcols[0], specs)

@@ -192,3 +192,44 @@ def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
     if key.dtype != torch.int64:
         keys = keys.to(key.dtype)
     return keys, outs
+
+
+_lib.register_signatures({
+    "dr_dense_state_update": (c_i32, [vp, c_u32, c_u64, c_i64, c_u64, vp, ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                      ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), c_u32, vp, vp]),
+})
+_DS_KEY = {torch.int64: 0, torch.int32: 2, torch.int8: 3, torch.int16: 5}
+_DS_VAL = {torch.int64: 0, torch.float64: 1, torch.int32: 2, torch.int8: 3, torch.float32: 4, torch.int16: 5}
+_DS_OP = {"count": 0, "sum": 1, "min": 2, "max": 3}
+
+
+def dense_state_ok(specs: list, key: torch.Tensor) -> bool:
+    """Can dense_state_update fold these accumulators?  specs: [(state, op, value or None)]: int64
+    states with any op, float64 states with sums, values of the listed dtypes."""
+    if key.dtype not in _DS_KEY or len(specs) > 8:
+        return False
+    for st, op, v in specs:
+        if st.dtype == torch.int64:
+            pass
+        elif not (st.dtype == torch.float64 and op == "sum"):
+            return False
+        if op != "count" and (v is None or v.dtype not in _DS_VAL or not v.is_contiguous()):
+            return False
+    return key.is_contiguous()
+
+
+def dense_state_update(key: torch.Tensor, lo: int, seen: torch.Tensor, specs: list) -> None:
+    """One pass over the rows: seen[key - lo] = 1 and every accumulator's atomic into its slot
+    (runtime/stream_agg.DenseState).  Raises if a key falls outside the state."""
+    _lib.require_gpu_tensor(key, "dense_state_update")
+    n, k = key.shape[0], len(specs)
+    states = (vp * k)(*[st.data_ptr() for st, _, _ in specs])
+    vals = (vp * k)(*[(v.data_ptr() if v is not None else None) for _, _, v in specs])
+    ops = (c_u32 * k)(*[_DS_OP[op] for _, op, _ in specs])
+    sdt = (c_u32 * k)(*[0 if st.dtype == torch.int64 else 1 for st, _, _ in specs])
+    vdt = (c_u32 * k)(*[_DS_VAL[v.dtype] if v is not None else 0 for _, _, v in specs])
+    bad = torch.zeros(1, dtype=torch.int32, device=key.device)
+    _lib.call("dr_dense_state_update", ptr(key), c_u32(_DS_KEY[key.dtype]), c_u64(n), c_i64(lo), c_u64(seen.numel()),
+              ptr(seen), states, vals, ops, sdt, vdt, c_u32(k), ptr(bad), stream_of(key))
+    if int(bad.item()):
+        raise RuntimeError("dense_state_update: a key outside the state's range")

@@ -150,7 +150,8 @@ class DenseState:
     of the keys' range, per accumulator column (sums and counts added, min / max reduced into
     their slots by the device scatter kernels) and an occupancy byte.  Used while the range times
     the slot bytes fits DENSE_FRACTION of the budget (e.g. 2^30 keys x 33 bytes = 35 GB of a 60 GB
-    budget): a chunk's partial rows then fold into the state in place, with no hash buckets,
+    budget): a chunk's partial rows then fold into the state in place (ops/densegroup
+    .dense_state_update: one pass of atomics per row), with no hash buckets,
     pending pieces, combines or spills.  The range grows (coarsely aligned) as chunks reach past it;
     when it no longer fits, the state becomes one partial piece of the hash-bucket path."""
 
@@ -244,6 +245,12 @@ class DenseState:
             if (hi - lo + 1) * self._slot_bytes() > self.cap:
                 return False
             self._alloc(lo, hi, k.device)
+        from ..ops import densegroup as DG
+        fused = [(self.state[name], op, part.cols[src][:n] if src is not None else None)
+                 for name, op, src, _ in self.specs]
+        if DG.dense_state_ok(fused, k):
+            DG.dense_state_update(k, self.lo, self.seen, fused)      # one pass, every accumulator
+            return True
         idx = (k - self.lo).to(torch.int64)
         self.seen.index_fill_(0, idx, 1)
         for name, op, src, dt in self.specs:
@@ -303,6 +310,8 @@ class StreamAggregator:
         if self.kind == "distinct":
             return G.op_distinct(self.agg, [t], self.v)
         op = dict(self.agg, op="group_partial")
+        if self.dense is not None:
+            op["raw_ok"] = True      # mostly distinct keys: the dense state folds the raw rows itself
         return G.op_group_partial(op, [t], self.v)
 
     def _fold(self, pieces: list) -> DeviceTable:

@@ -102,3 +102,31 @@ def test_groupby_query_takes_dense_path():
     assert [k for k, _, _ in got] == uk.tolist()
     assert [c for _, c, _ in got] == cnt.tolist()
     assert np.array_equal(np.array([s for _, _, s in got], dtype=np.float64), s1)
+
+
+def test_dense_state_update_matches_torch_scatter():
+    """ops/densegroup.dense_state_update (one pass of atomics per row) == the library scatter
+    reductions it replaces: occupancy, count, int64 sum of int32 values, min / max of int64 values,
+    float64 sum; keys repeat within the batch."""
+    from dryad_amd.ops import densegroup as DG
+    g = torch.Generator(device="cuda").manual_seed(3)
+    n, lo, R = 2_000_003, -5000, 300_000
+    key = torch.randint(lo, lo + R, (n,), device="cuda", generator=g)
+    v32 = torch.randint(-2**31, 2**31 - 1, (n,), device="cuda", generator=g, dtype=torch.int32)
+    v64 = torch.randint(-2**62, 2**62, (n,), device="cuda", generator=g)
+    vf = torch.randn(n, device="cuda", generator=g, dtype=torch.float64)
+    mk = lambda fill, dt=torch.int64: torch.full((R,), fill, dtype=dt, device="cuda")  # noqa: E731
+    cnt, sm, mn, mx, fs = mk(0), mk(0), mk(2**63 - 1), mk(-2**63), mk(0.0, torch.float64)
+    seen = torch.zeros(R, dtype=torch.int8, device="cuda")
+    specs = [(cnt, "count", None), (sm, "sum", v32), (mn, "min", v64), (mx, "max", v64), (fs, "sum", vf)]
+    assert DG.dense_state_ok(specs, key)
+    DG.dense_state_update(key, lo, seen, specs)
+    idx = key - lo
+    assert torch.equal(seen, torch.zeros_like(seen).index_fill_(0, idx, 1))
+    assert torch.equal(cnt, mk(0).index_add_(0, idx, torch.ones_like(idx)))
+    assert torch.equal(sm, mk(0).index_add_(0, idx, v32.to(torch.int64)))
+    assert torch.equal(mn, mk(2**63 - 1).scatter_reduce_(0, idx, v64, "amin"))
+    assert torch.equal(mx, mk(-2**63).scatter_reduce_(0, idx, v64, "amax"))
+    assert torch.allclose(fs, mk(0.0, torch.float64).index_add_(0, idx, vf), rtol=1e-9, atol=1e-9)
+    with pytest.raises(RuntimeError):
+        DG.dense_state_update(key[:10] + R, lo, seen, specs)
