@@ -576,21 +576,22 @@ __device__ __forceinline__ double ds_load_f(const void* p, uint32_t dt, uint64_t
 
 __global__ __launch_bounds__(256) void dense_state_update_kernel(const void* __restrict__ key, uint32_t kdt, uint64_t n,
                                                                  int64_t lo, uint64_t range, uint8_t* __restrict__ seen,
-                                                                 DsSpecs sp, uint32_t* __restrict__ bad) {
+                                                                 DsSpecs sp, uint64_t stride, uint32_t* __restrict__ bad) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t idx = (uint64_t)(ds_load_i(key, kdt, i) - lo);
     if (idx >= range) {                  // a key outside the state (a broken caller): not stored
       atomicOr(bad, 1u);
       continue;
     }
-    seen[idx] = 1;
+    if (seen != nullptr) seen[idx] = 1;
+    const uint64_t slot = idx * stride;  // stride > 1: a key's accumulators side by side (one sector)
     for (uint32_t s = 0; s < sp.nspec; ++s) {
       const uint32_t op = sp.op[s];
       if (sp.sdt[s] == 1) {
-        atomicAdd(static_cast<double*>(sp.state[s]) + idx, ds_load_f(sp.val[s], sp.vdt[s], i));
+        atomicAdd(static_cast<double*>(sp.state[s]) + slot, ds_load_f(sp.val[s], sp.vdt[s], i));
         continue;
       }
-      long long* st = static_cast<long long*>(sp.state[s]) + idx;
+      long long* st = static_cast<long long*>(sp.state[s]) + slot;
       if (op == 0) {
         atomicAdd(reinterpret_cast<unsigned long long*>(st), 1ull);
       } else {
@@ -604,12 +605,14 @@ __global__ __launch_bounds__(256) void dense_state_update_kernel(const void* __r
 }
 }  // namespace
 
-// key: n keys of dtype kdt (0 int64, 2 int32, 5 int16, 3 int8); seen: `range` bytes; state / val /
-// op / sdt / vdt: nspec accumulators (see DsSpecs; val ignored for count).  bad: set when a key
-// falls outside [lo, lo + range).
+// key: n keys of dtype kdt (0 int64, 2 int32, 5 int16, 3 int8); seen: `range` bytes (nullable: a
+// count accumulator tells occupancy); state / val / op / sdt / vdt: nspec accumulators (see
+// DsSpecs; val ignored for count), key k's slot of accumulator s at state[s][(k - lo) * stride]
+// (stride = nspec: one row of 8-byte slots per key).  bad: set when a key falls outside the range.
 DR_API int dr_dense_state_update(const void* key, uint32_t kdt, uint64_t n, int64_t lo, uint64_t range, uint8_t* seen,
                                  void* const* state, const void* const* val, const uint32_t* op, const uint32_t* sdt,
-                                 const uint32_t* vdt, uint32_t nspec, uint32_t* bad, hipStream_t s) {
+                                 const uint32_t* vdt, uint32_t nspec, uint64_t stride, uint32_t* bad, hipStream_t s) {
+  if (stride == 0) return (int)hipErrorInvalidValue;
   if (nspec > (uint32_t)kDsMaxSpecs || (kdt != 0 && kdt != 2 && kdt != 3 && kdt != 5)) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
   DsSpecs sp;
@@ -623,7 +626,7 @@ DR_API int dr_dense_state_update(const void* key, uint32_t kdt, uint64_t n, int6
     sp.vdt[k] = vdt[k];
   }
   sp.nspec = nspec;
-  dense_state_update_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(key, kdt, n, lo, range, seen, sp, bad);
+  dense_state_update_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(key, kdt, n, lo, range, seen, sp, stride, bad);
   DR_LAUNCH_CHECK();
   return 0;
 }

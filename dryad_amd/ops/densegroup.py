@@ -196,17 +196,21 @@ def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
 
 _lib.register_signatures({
     "dr_dense_state_update": (c_i32, [vp, c_u32, c_u64, c_i64, c_u64, vp, ctypes.POINTER(vp), ctypes.POINTER(vp),
-                                      ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), c_u32, vp, vp]),
+                                      ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), c_u32, c_u64,
+                                      vp, vp]),
 })
 _DS_KEY = {torch.int64: 0, torch.int32: 2, torch.int8: 3, torch.int16: 5}
 _DS_VAL = {torch.int64: 0, torch.float64: 1, torch.int32: 2, torch.int8: 3, torch.float32: 4, torch.int16: 5}
 _DS_OP = {"count": 0, "sum": 1, "min": 2, "max": 3}
 
 
-def dense_state_ok(specs: list, key: torch.Tensor) -> bool:
+def dense_state_ok(specs: list, key: torch.Tensor, stride: int = 1) -> bool:
     """Can dense_state_update fold these accumulators?  specs: [(state, op, value or None)]: int64
-    states with any op, float64 states with sums, values of the listed dtypes."""
+    states with any op, float64 states with sums, values of the listed dtypes; every state a
+    column of ``stride``-element rows."""
     if key.dtype not in _DS_KEY or len(specs) > 8:
+        return False
+    if any(st.dim() != 1 or st.stride(0) != stride for st, _, _ in specs):
         return False
     for st, op, v in specs:
         if st.dtype == torch.int64:
@@ -218,9 +222,12 @@ def dense_state_ok(specs: list, key: torch.Tensor) -> bool:
     return key.is_contiguous()
 
 
-def dense_state_update(key: torch.Tensor, lo: int, seen: torch.Tensor, specs: list) -> None:
-    """One pass over the rows: seen[key - lo] = 1 and every accumulator's atomic into its slot
-    (runtime/stream_agg.DenseState).  Raises if a key falls outside the state."""
+def dense_state_update(key: torch.Tensor, lo: int, seen, specs: list, rng: int | None = None,
+                       stride: int = 1) -> None:
+    """One pass over the rows: seen[key - lo] = 1 (``seen`` may be None) and every accumulator's
+    atomic into its slot (runtime/stream_agg.DenseState); the states are columns of
+    ``stride``-element rows (an [R, stride] matrix: a key's slots in one sector).  Raises if a key
+    falls outside the state's ``rng`` keys."""
     _lib.require_gpu_tensor(key, "dense_state_update")
     n, k = key.shape[0], len(specs)
     states = (vp * k)(*[st.data_ptr() for st, _, _ in specs])
@@ -229,7 +236,9 @@ def dense_state_update(key: torch.Tensor, lo: int, seen: torch.Tensor, specs: li
     sdt = (c_u32 * k)(*[0 if st.dtype == torch.int64 else 1 for st, _, _ in specs])
     vdt = (c_u32 * k)(*[_DS_VAL[v.dtype] if v is not None else 0 for _, _, v in specs])
     bad = torch.zeros(1, dtype=torch.int32, device=key.device)
-    _lib.call("dr_dense_state_update", ptr(key), c_u32(_DS_KEY[key.dtype]), c_u64(n), c_i64(lo), c_u64(seen.numel()),
-              ptr(seen), states, vals, ops, sdt, vdt, c_u32(k), ptr(bad), stream_of(key))
+    rng = seen.numel() if rng is None else rng
+    _lib.call("dr_dense_state_update", ptr(key), c_u32(_DS_KEY[key.dtype]), c_u64(n), c_i64(lo), c_u64(rng),
+              ptr(seen) if seen is not None else None, states, vals, ops, sdt, vdt, c_u32(k), c_u64(stride), ptr(bad),
+              stream_of(key))
     if int(bad.item()):
         raise RuntimeError("dense_state_update: a key outside the state's range")

@@ -147,8 +147,9 @@ def _buckets(t: DeviceTable, K: int, agg_kind: str) -> list:
 
 class DenseState:
     """Running GroupBy state of ONE integer key addressed directly by key - lo: one slot per key
-    of the keys' range, per accumulator column (sums and counts added, min / max reduced into
-    their slots by the device scatter kernels) and an occupancy byte.  Used while the range times
+    of the keys' range and accumulator (8-byte accumulators side by side per key: one HBM sector
+    per folded row; sums and counts added, min / max reduced into their slots), plus an occupancy
+    byte unless a count accumulator tells occupancy.  Used while the range times
     the slot bytes fits DENSE_FRACTION of the budget (e.g. 2^30 keys x 33 bytes = 35 GB of a 60 GB
     budget): a chunk's partial rows then fold into the state in place (ops/densegroup
     .dense_state_update: one pass of atomics per row), with no hash buckets,
@@ -161,8 +162,10 @@ class DenseState:
         self.d, self.cap = d, int(budget * self.DENSE_FRACTION)
         self.lo = self.hi = None
         self.specs = None            # [(state name, op, source column name or None, dtype)]
-        self.state: dict = {}
-        self.seen = None
+        self.state = {}              # [R, S] int64 matrix (aos) or {name: [R] array}
+        self.seen = None             # occupancy bytes, unless a count accumulator tells it
+        self.aos = False
+        self.count_name = None
         self.meta = None
         self.kdtype = None
         self.outdt: dict = {}
@@ -199,12 +202,31 @@ class DenseState:
                 return None              # any / all / user aggregates: the bucket path
         return specs
 
+    def _layout(self):
+        """8-byte accumulators only: one [R, S] matrix, a key's S slots side by side (its folds touch
+        one HBM sector instead of S); a count accumulator doubles as the occupancy flag."""
+        self.aos = all(dt in (torch.int64, torch.float64) for _, _, _, dt in self.specs)
+        cnt = {f"a{j}" for j, a in enumerate(self.d.aggs) if a.kind == "count"} | \
+            {f"c{j}" for j, a in enumerate(self.d.aggs) if a.kind == "avg"}
+        self.count_name = next((name for name, _, _, _ in self.specs if name in cnt), None)
+
     def _slot_bytes(self) -> int:
-        return 1 + sum(torch.empty(0, dtype=dt).element_size() for _, _, _, dt in self.specs)
+        return (0 if self.count_name else 1) + sum(torch.empty(0, dtype=dt).element_size() for _, _, _, dt in self.specs)
+
+    def _col(self, st, name: str):
+        """The state column of accumulator ``name`` (a strided view of the matrix, or its array)."""
+        if not self.aos:
+            return st[name]
+        s = self.slot[name]
+        dt = self.dtypes[name]
+        return (st if dt == torch.int64 else st.view(dt))[:, s]
 
     def _alloc(self, lo: int, hi: int, dev):
         R = hi - lo + 1
-        st = {}
+        if self.aos:
+            st = torch.empty((R, len(self.specs)), dtype=torch.int64, device=dev)
+        else:
+            st = {name: torch.empty(R, dtype=dt, device=dev) for name, _, _, dt in self.specs}
         for name, op, _, dt in self.specs:
             if op == "min":
                 fill = torch.iinfo(dt).max if not dt.is_floating_point else float("inf")
@@ -212,13 +234,17 @@ class DenseState:
                 fill = torch.iinfo(dt).min if not dt.is_floating_point else float("-inf")
             else:
                 fill = 0
-            st[name] = torch.full((R,), fill, dtype=dt, device=dev)
-        seen = torch.zeros(R, dtype=torch.int8, device=dev)
+            self._col(st, name).fill_(fill)
+        seen = None if self.count_name else torch.zeros(R, dtype=torch.int8, device=dev)
         if self.lo is not None:          # the old range moves into the grown one
             a, b = self.lo - lo, self.hi - lo + 1
-            for name in st:
-                st[name][a:b].copy_(self.state[name])
-            seen[a:b].copy_(self.seen)
+            if self.aos:
+                st[a:b].copy_(self.state)
+            else:
+                for name in st:
+                    st[name][a:b].copy_(self.state[name])
+            if seen is not None:
+                seen[a:b].copy_(self.seen)
         self.state, self.seen, self.lo, self.hi = st, seen, lo, hi
 
     def add(self, part: DeviceTable) -> bool:
@@ -233,6 +259,9 @@ class DenseState:
             self.kdtype = part.cols["k0"].dtype
             if self.specs is None:
                 return False
+            self.slot = {name: i for i, (name, _, _, _) in enumerate(self.specs)}
+            self.dtypes = {name: dt for name, _, _, dt in self.specs}
+            self._layout()
         k = part.cols["k0"][:n]
         mn, mx = (int(x) for x in torch.aminmax(k))
         lo, hi = (mn, mx) if self.lo is None else (min(mn, self.lo), max(mx, self.hi))
@@ -246,15 +275,18 @@ class DenseState:
                 return False
             self._alloc(lo, hi, k.device)
         from ..ops import densegroup as DG
-        fused = [(self.state[name], op, part.cols[src][:n] if src is not None else None)
+        fused = [(self._col(self.state, name), op, part.cols[src][:n] if src is not None else None)
                  for name, op, src, _ in self.specs]
-        if DG.dense_state_ok(fused, k):
-            DG.dense_state_update(k, self.lo, self.seen, fused)      # one pass, every accumulator
+        stride = len(self.specs) if self.aos else 1
+        if DG.dense_state_ok(fused, k, stride):
+            # one pass, every accumulator
+            DG.dense_state_update(k, self.lo, self.seen, fused, rng=self.hi - self.lo + 1, stride=stride)
             return True
         idx = (k - self.lo).to(torch.int64)
-        self.seen.index_fill_(0, idx, 1)
+        if self.seen is not None:
+            self.seen.index_fill_(0, idx, 1)
         for name, op, src, dt in self.specs:
-            st = self.state[name]
+            st = self._col(self.state, name)
             if op == "count":
                 st.index_add_(0, idx, torch.ones(1, dtype=dt, device=st.device).expand(n))
                 continue
@@ -273,10 +305,11 @@ class DenseState:
         """The occupied slots as a partial table in the folded (standard) layout."""
         if self.lo is None:
             return None
-        occ = torch.nonzero(self.seen).squeeze(1)
+        occupied = self.seen if self.seen is not None else self._col(self.state, self.count_name)
+        occ = torch.nonzero(occupied).squeeze(1)
         out = {"k0": (occ + self.lo).to(self.kdtype)}
         for name, _, _, _ in self.specs:
-            out[name] = self.state[name].index_select(0, occ)
+            out[name] = self._col(self.state, name).index_select(0, occ)
         for j, a in enumerate(self.d.aggs):      # min / max keep their dtype (as combine_partials)
             if a.kind in ("min", "max") and out[f"a{j}"].dtype != self.outdt[f"a{j}"]:
                 out[f"a{j}"] = out[f"a{j}"].to(self.outdt[f"a{j}"])

@@ -130,3 +130,14 @@ def test_dense_state_update_matches_torch_scatter():
     assert torch.allclose(fs, mk(0.0, torch.float64).index_add_(0, idx, vf), rtol=1e-9, atol=1e-9)
     with pytest.raises(RuntimeError):
         DG.dense_state_update(key[:10] + R, lo, seen, specs)
+    # the same accumulators as the columns of one [R, 5] matrix (a key's slots side by side), no
+    # occupancy bytes
+    mat = torch.zeros((R, 5), dtype=torch.int64, device="cuda")
+    mat[:, 2] = 2**63 - 1
+    mat[:, 3] = -2**63
+    cols = [mat[:, 0], mat[:, 1], mat[:, 2], mat[:, 3], mat.view(torch.float64)[:, 4]]
+    aos = [(c, op, v) for c, (_, op, v) in zip(cols, specs)]
+    assert DG.dense_state_ok(aos, key, stride=5) and not DG.dense_state_ok(aos, key)
+    DG.dense_state_update(key, lo, None, aos, rng=R, stride=5)
+    for c, (ref, _, _) in zip(cols, specs):
+        assert torch.allclose(c, ref, rtol=1e-9, atol=1e-9) if c.dtype == torch.float64 else torch.equal(c, ref)
