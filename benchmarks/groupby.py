@@ -16,6 +16,16 @@ region (group counts and V1 sums against column totals).
 from __future__ import annotations
 
 import argparse
+import os
+import sys
+
+if "--loopback-ranks" in sys.argv:
+    # the loopback harness runs all W sources' stage A in this one process to simulate the
+    # exchange; with the default caching allocator that fragments HBM, and one step's stage B in
+    # three paid fresh allocations (1.8 s: profiles/r5/gb_lb8_final.log).  Expandable segments
+    # keep every step steady (94.3-95.3 ms, profiles/r5/gb_lb8_expandable.log); the per-rank
+    # program is unchanged.  Set before torch initialises the device.
+    os.environ.setdefault("PYTORCH_HIP_ALLOC_CONF", "expandable_segments:True")
 
 from common import report, timed, world  # noqa: E402
 
