@@ -272,25 +272,40 @@ __global__ __launch_bounds__(256) void pc_scatter_rows_kernel(const void* __rest
     }
   }
   __syncthreads();
-  for (uint64_t base = beg; base < end; base += kPcTile) {
-    const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kPcTile ? (end - base) : kPcTile);
-    // the tile's rows, every column, all loads in flight
-    uint32_t v[kPcRowItems];
+  // a tile's rows (every column) and ports, loaded at once with clamped rows (no branch around a
+  // load); the next tile's loads are issued as soon as this tile is staged, so they are in flight
+  // while it is ranked and stored
+  uint32_t v[kPcRowItems];
+  uint32_t nv[kPcNarrow][2];
+  uint32_t pd[kPcItems];
+  auto load_tile = [&](uint64_t b0, uint32_t cn) {
 #pragma unroll
     for (int i = 0; i < kPcRowItems; ++i) {
       const int c = i >> 1;
       const uint32_t r = (uint32_t)t + (uint32_t)(i & 1) * kBlock;
-      v[i] = 0;
-      if ((uint32_t)c < WT) v[i] = gload(cin[c], (base + (r < cnt ? r : 0u)) * cwpr[c] + cwd[c]);
+      const bool use = (uint32_t)c < WT;
+      v[i] = gload(use ? cin[c] : cin[0], (b0 + (r < cn ? r : 0u)) * (use ? cwpr[c] : 1u) + (use ? cwd[c] : 0u));
     }
-    uint32_t nv[kPcNarrow][2];
 #pragma unroll
     for (int m = 0; m < kPcNarrow; ++m)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const uint32_t r = (uint32_t)t + (uint32_t)h * kBlock;
-        nv[m][h] = nw[m] ? gload_narrow(nin[m], base + (r < cnt ? r : 0u), nw[m]) : 0u;
+        nv[m][h] = gload_narrow(nw[m] ? nin[m] : reinterpret_cast<const uint8_t*>(cin[0]), b0 + (r < cn ? r : 0u),
+                                nw[m] ? nw[m] : 1u);
       }
+#pragma unroll
+    for (int r = 0; r < kPcItems; ++r) {
+      const uint32_t pos = w * (kPcTile / 4) + r * 64 + l;
+      pd[r] = pc_port<PORT8>(ent, b0 + (pos < cn ? pos : 0u));
+    }
+  };
+  auto tile_rows = [&](uint64_t b0) -> uint32_t {
+    return (uint32_t)((end - b0) < (uint64_t)kPcTile ? (end - b0) : kPcTile);
+  };
+  load_tile(beg, tile_rows(beg));
+  for (uint64_t base = beg; base < end; base += kPcTile) {
+    const uint32_t cnt = tile_rows(base);
     wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
     __syncthreads();
     uint32_t rk[kPcItems], dg[kPcItems];
@@ -298,7 +313,7 @@ __global__ __launch_bounds__(256) void pc_scatter_rows_kernel(const void* __rest
     for (int r = 0; r < kPcItems; ++r) {
       const uint32_t pos = w * (kPcTile / 4) + r * 64 + l;
       const bool valid = pos < cnt;
-      const uint32_t d = valid ? (uint32_t)slut[pc_port<PORT8>(ent, base + pos)] : 0u;
+      const uint32_t d = valid ? (uint32_t)slut[pd[r]] : 0u;
       uint64_t peers = ballot64(valid);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -327,6 +342,7 @@ __global__ __launch_bounds__(256) void pc_scatter_rows_kernel(const void* __rest
         const uint32_t r = (uint32_t)t + (uint32_t)h * kBlock;
         if (nw[m] && r < cnt) nbuf[m][r] = (uint16_t)nv[m][h];
       }
+    if (base + kPcTile < end) load_tile(base + kPcTile, tile_rows(base + kPcTile));
     __syncthreads();
     const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
     const uint32_t tot = c0 + c1 + c2 + c3;
