@@ -31,7 +31,16 @@ namespace {
 // (2048-row tiles into 1024 buckets) measured 2.5-2.8x the written bytes at the memory side.
 constexpr int kDgThreads = 512;
 constexpr int kDgWaves = kDgThreads / 64;
-constexpr int kDgTile = 4096;
+#ifndef DR_DG_TILE
+#define DR_DG_TILE 4096
+#endif
+#ifndef DR_DG_WPE
+#define DR_DG_WPE 4
+#endif
+#ifndef DR_DG_GMAX
+#define DR_DG_GMAX 1536
+#endif
+constexpr int kDgTile = DR_DG_TILE;   // build-time constants: tools/micro/dg_tile_ab.sh measures variants
 constexpr int kDgItems = kDgTile / kDgThreads; // rows per thread per tile
 constexpr int kDgMaxDigit = 10;               // digit bits per pass (1024 buckets)
 constexpr int kDgTableBits = 12;              // LDS table slots per run: 4096
@@ -133,7 +142,7 @@ __global__ __launch_bounds__(256) void dg_count_kernel(const int64_t* __restrict
 // Stable partition of rows [beg, end) of each workgroup by digit; offsets[d * G + b] = first output
 // row of workgroup b's bucket d (exclusive prefix of the bucket-major counts).
 template <bool FROM_COLS, int DB>
-__global__ __launch_bounds__(kDgThreads) __attribute__((amdgpu_waves_per_eu(4))) void dg_scatter_kernel(DgPack pk, const uint4* __restrict__ in, uint64_t n,
+__global__ __launch_bounds__(kDgThreads) __attribute__((amdgpu_waves_per_eu(DR_DG_WPE))) void dg_scatter_kernel(DgPack pk, const uint4* __restrict__ in, uint64_t n,
                                                          uint32_t shift, const int64_t* __restrict__ offsets, uint32_t G,
                                                          uint64_t per_block, uint4* __restrict__ out) {
   constexpr uint32_t nb = 1u << DB, mask = nb - 1;
@@ -438,7 +447,7 @@ DR_API uint32_t dr_dg_max_digit() { return kDgMaxDigit; }
 DR_API uint32_t dr_dg_grid(uint64_t n, uint64_t* per_block) {
   uint64_t tiles = (n + kDgTile - 1) / kDgTile;
   if (tiles < 1) tiles = 1;
-  const uint64_t G = tiles < 1024 ? tiles : 1024;
+  const uint64_t G = tiles < DR_DG_GMAX ? tiles : DR_DG_GMAX;
   *per_block = ((tiles + G - 1) / G) * kDgTile;
   return (uint32_t)G;
 }
