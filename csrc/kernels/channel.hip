@@ -452,11 +452,16 @@ __global__ void copy_tail_kernel(const uint8_t* __restrict__ src, uint8_t* __res
 }  // namespace
 
 // Geometry shared by the count and scatter launches (the caller sizes `counts` as 256 * G).
+#ifndef DR_PC_GMAX
+#define DR_PC_GMAX 16384
+#endif
 DR_API uint32_t dr_pc_grid(uint64_t n, uint64_t* per_block) {
   uint64_t tiles = (n + kPcTile - 1) / kPcTile;
   if (tiles < 1) tiles = 1;
-  // 1024 workgroups x 4 waves fill the 256 CUs; more only grows the [256][G] offset matrix
-  const uint64_t G = tiles < 1024 ? tiles : 1024;
+  // up to DR_PC_GMAX workgroups of 4 waves: at 1024 (16 waves per CU, many tiles each) the row
+  // scatter waited on memory; a few tiles per workgroup keeps more of them in flight
+  // (tools/gpurun/r5c_pc_ab.sh, profiles/r5/pc_grid_ab.txt)
+  const uint64_t G = tiles < DR_PC_GMAX ? tiles : DR_PC_GMAX;
   *per_block = ((tiles + G - 1) / G) * kPcTile;
   return (uint32_t)G;
 }
