@@ -23,6 +23,7 @@ from ..compiler.decomposition import Sym, substitute
 from ..ops import recordsort as RS
 from ..ops import relational as R
 from ..ops import sort as S
+from . import stats
 from . import trace as TR
 from .table import DeviceTable, PartialMeta, Ported, PortTables, Shape, from_objects
 from .trace import NotTraceable
@@ -632,6 +633,8 @@ def partition_by_entries(t: DeviceTable, e: torch.Tensor, n: int, world_size: in
         nt = DeviceTable(t.n, t.shape, rows=outs[0])
     else:
         nt = DeviceTable(t.n, t.shape, dict(zip(t.cols.keys(), outs)), heap=t.heap, strs=t.strs)
+        for k, o in nt.cols.items():           # a permutation of the rows keeps the column bounds
+            stats.inherit(o, t.cols[k])
     return Ported(nt, offs, order)
 
 
@@ -1064,6 +1067,7 @@ def _raw_partial(d, t, key, form):
         if a.kind in ("count", "avg") and (val is None or a.kind == "avg"):
             if ones is None:
                 ones = torch.ones(t.n, dtype=torch.int8, device=t.device)
+                stats.set_bounds(ones, 1, 1)
         if a.kind == "count":
             out[f"a{j}"] = ones if val is None else val
         elif a.kind == "avg":

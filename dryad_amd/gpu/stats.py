@@ -27,6 +27,20 @@ def known(col: torch.Tensor):
     return e[0], e[1]
 
 
+def inherit(dst: torch.Tensor, src: torch.Tensor) -> None:
+    """``dst`` holds a subset (or a copy) of ``src``'s values: it keeps src's bounds."""
+    b = known(src)
+    if b is not None:
+        set_bounds(dst, *b)
+
+
+def union(dst: torch.Tensor, srcs: list) -> None:
+    """``dst`` holds the values of ``srcs`` (concatenated): bounds when every source has them."""
+    bs = [known(x) for x in srcs]
+    if bs and all(b is not None for b in bs):
+        set_bounds(dst, min(b[0] for b in bs), max(b[1] for b in bs))
+
+
 def bounds(cols: list) -> list:
     """[(lo, hi)] for integer columns (one device pass over those without registered bounds)."""
     out = [known(c) for c in cols]

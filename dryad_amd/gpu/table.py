@@ -24,6 +24,7 @@ import numpy as np
 import torch
 
 from .. import types as T
+from . import stats as _stats
 
 
 @dataclass
@@ -114,8 +115,11 @@ class DeviceTable:
     def slice(self, a: int, b: int) -> "DeviceTable":
         if self.rows is not None:
             return DeviceTable(b - a, self.shape, rows=self.rows[a:b])
-        return DeviceTable(b - a, self.shape, {k: v[a:b] for k, v in self.cols.items()}, heap=self.heap,
-                           strs=self.strs)
+        cols = {}
+        for k, v in self.cols.items():
+            cols[k] = v[a:b]
+            _stats.inherit(cols[k], v)
+        return DeviceTable(b - a, self.shape, cols, heap=self.heap, strs=self.strs)
 
     def take(self, idx: torch.Tensor) -> "DeviceTable":
         """Gather rows by an int64 index tensor (HIP row gather for row tables)."""
@@ -132,6 +136,15 @@ class DeviceTable:
     @staticmethod
     def concat(tables: list) -> "DeviceTable":
         tables = [t for t in tables if t is not None]
+        out = DeviceTable._concat(tables)
+        if out is not None and out.rows is None and out.heap is None and len(tables) > 1:
+            for k, v in out.cols.items():             # column bounds of the pieces (gpu/stats.py);
+                if k not in out.strs and all(k in t.cols for t in tables):   # not rebased offsets
+                    _stats.union(v, [t.cols[k] for t in tables])
+        return out
+
+    @staticmethod
+    def _concat(tables: list) -> "DeviceTable":
         if not tables:
             return None
         t0 = tables[0]

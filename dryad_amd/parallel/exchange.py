@@ -134,6 +134,29 @@ def _struct_hash(struct) -> int:
     return int.from_bytes(hashlib.blake2b(repr(struct).encode(), digest_size=8).digest(), "little") >> 1
 
 
+_BOUNDS_AT = 5 + _MAXC         # header slots of the per-column bounds
+_I64_MIN, _I64_MAX = -(1 << 63), (1 << 63) - 1
+
+
+def _sent_bounds(sends: list, name: str):
+    """(lo, hi) over every piece this rank sends of integer column ``name`` when all of them have
+    registered bounds ((I64_MAX, I64_MIN) when it sends no rows), else None."""
+    from ..gpu import stats as ST
+    lo, hi = _I64_MAX, _I64_MIN
+    for lst in sends:
+        for p in lst:
+            if p is None or p.n == 0:
+                continue
+            c = _columns(p).get(name)
+            if c is None or c.dtype in (torch.bool,) or c.is_floating_point() or c.is_complex():
+                return None
+            b = ST.known(c)
+            if b is None:
+                return None
+            lo, hi = min(lo, b[0]), max(hi, b[1])
+    return lo, hi
+
+
 def _manifest(world: World, sends: list, proto):
     """The exchange's control plane as two small tensor collectives instead of pickled objects:
     an all-gather of each rank's header (has a piece, structure digest, column dtypes, string
@@ -152,13 +175,18 @@ def _manifest(world: World, sends: list, proto):
     vals = iter(torch.stack(sums).tolist() if sums else [])
     per_dest = [[(p.n, [next(vals) if p.n else 0 for _ in range(nstr)]) for p in lst] for lst in sends]
     maxp = max((len(x) for x in per_dest), default=0)
-    hdr = torch.zeros(5 + _MAXC, dtype=torch.int64)
+    hdr = torch.zeros(_BOUNDS_AT + 3 * _MAXC, dtype=torch.int64)
     if sig is not None:
         hdr[0], hdr[1], hdr[2], hdr[3] = 1, _struct_hash(sig[0]), len(sig[1]), nstr
         for j, d in enumerate(sig[1]):
             if _dtype(d) not in _DTYPES:
                 raise SchemaMismatch(f"column dtype {d} has no manifest code")
             hdr[5 + j] = _DTYPES.index(_dtype(d))
+        # the column bounds this rank's pieces carry (gpu/stats.py): known, lo, hi per column
+        for j, name in enumerate(_columns(proto)):
+            b = _sent_bounds(sends, name)
+            if b is not None:
+                hdr[_BOUNDS_AT + 3 * j: _BOUNDS_AT + 3 * j + 3] = torch.tensor([1, b[0], b[1]], dtype=torch.int64)
     hdr[4] = maxp
     heads = shuffle.all_gather_tensor(hdr.view(1, -1).to(dev), world).cpu().tolist()
     M = max(h[4] for h in heads)
@@ -180,6 +208,23 @@ def _manifest(world: World, sends: list, proto):
     pieces = [[(g[s][1 + i * (1 + S)], g[s][2 + i * (1 + S): 2 + i * (1 + S) + S]) for i in range(g[s][0])]
               for s in range(W)]
     return heads, pieces
+
+
+def _set_received_bounds(have: list, colspecs, out_cols: dict, offset_cols: set) -> None:
+    """A received integer column holds the union of what the senders held: it keeps their bounds
+    when every sender knew them (its consumer then skips a min/max pass, gpu/stats.py)."""
+    from ..gpu import stats as ST
+    for j, (name, _) in enumerate(colspecs):
+        col = out_cols.get(name)
+        if name in offset_cols or name == "__rows__" or not isinstance(col, torch.Tensor) \
+                or col.is_floating_point() or col.dtype == torch.bool or j >= _MAXC:
+            continue
+        at = _BOUNDS_AT + 3 * j
+        if not all(h[at] == 1 for h in have):
+            continue
+        lo, hi = min(h[at + 1] for h in have), max(h[at + 2] for h in have)
+        if lo <= hi:
+            ST.set_bounds(col, lo, hi)
 
 
 def exchange(world: World, sends: list, stats: ExchangeStats | None = None) -> list:
@@ -269,6 +314,7 @@ def exchange(world: World, sends: list, stats: ExchangeStats | None = None) -> l
             stats.bytes_sent += sum(send_b)
             stats.bytes_received += recv.numel()
             stats.collectives += 1
+    _set_received_bounds(have, colspecs, out_cols, offset_cols)
     if "__rows__" in out_cols:
         big = DeviceTable(total_r, shape, rows=out_cols["__rows__"])
     else:

@@ -20,6 +20,7 @@ from __future__ import annotations
 import torch
 
 from ..gpu import ops as G
+from ..gpu import stats
 from ..gpu.table import DeviceTable, Ported
 from ..parallel.comm import World
 from .gpu_executor import GpuVertexContext
@@ -41,7 +42,11 @@ def _copy_table(t: DeviceTable) -> DeviceTable:
         return DeviceTable(t.n, t.shape, rows=t.rows.clone())
     if t.heap is not None or t.strs:
         raise ValueError("loopback: string-bearing shuffles are not simulated")
-    return DeviceTable(t.n, t.shape, {k: v[: t.n].clone() for k, v in t.cols.items()})
+    cols = {}
+    for k, v in t.cols.items():
+        cols[k] = v[: t.n].clone()
+        stats.inherit(cols[k], v)           # as parallel/exchange.py delivers them: bounds kept
+    return DeviceTable(t.n, t.shape, cols)
 
 
 def _nbytes(t: DeviceTable) -> int:
@@ -97,7 +102,11 @@ class LoopbackRank:
             del src
         recv = DeviceTable.concat(pieces)
         if recv.rows is None:
-            recv = DeviceTable(recv.n, recv.shape, {k: v.contiguous() for k, v in recv.cols.items()})
+            cols = {}
+            for k, v in recv.cols.items():
+                cols[k] = v.contiguous()
+                stats.inherit(cols[k], v)
+            recv = DeviceTable(recv.n, recv.shape, cols)
         del pieces, mine
         recv_bytes = _nbytes(recv)
         ops = [o for o in B.ops if o["op"] != "output"]

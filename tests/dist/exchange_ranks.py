@@ -111,6 +111,23 @@ def main():
             e = ent_table(s_, n)
             if [x.to_objects() for x in got[s_]] != [e.slice(0, 1).to_objects(), e.slice(1, n).to_objects()]:
                 bad.append(("strided", n, s_))
+    # column bounds travel with the pieces (gpu/stats.py): the receiver's concatenation knows the
+    # union of the senders' registered bounds; one sender without bounds leaves it unmeasured
+    from dryad_amd.gpu import stats as ST
+    for unknown_rank in (None, W - 1):
+        n = 0 if me == 1 else 50 + me
+        col = torch.arange(n, dtype=torch.int64, device=dev) + 100 * me
+        if me != unknown_rank:
+            ST.set_bounds(col, 100 * me - 5, 100 * me + 60)
+        t = DeviceTable.from_columns({"v": col}, Shape("scalar", ["v"]))
+        per = (n + W - 1) // W
+        got = EXC.exchange(w, [[t.slice(min(r * per, n), min((r + 1) * per, n))] for r in range(W)])
+        merged = DeviceTable.concat([x for lst in got for x in lst])
+        senders = [r for r in range(W) if r != 1]
+        want = None if unknown_rank is not None and unknown_rank != 1 else \
+            (min(100 * r - 5 for r in senders), max(100 * r + 60 for r in senders))
+        if ST.known(merged.cols["v"]) != want:
+            bad.append(("bounds", unknown_rank, ST.known(merged.cols["v"]), want))
     w.barrier()
     assert not bad, (me, bad[:5])
     if me == 0:
