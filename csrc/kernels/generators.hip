@@ -34,6 +34,58 @@ __global__ __launch_bounds__(256) void gen_records64_kernel(int64_t* const* __re
   }
 }
 
+// Columns, two rows per lane (uniform-key mode): the column pointers are read once into
+// registers, the field loop is unrolled (NC a template argument) and each lane writes one 16-byte
+// nontemporal store per column (the one-row kernel above re-reads the pointer array and issues
+// 8-byte stores in a runtime loop: ~3 TB/s on the GroupBy config's 40 GB).  Columns that are not
+// 16-byte aligned take the one-row path (a uniform branch).
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) u64x2 gu64x2;   // global (not flat) stores
+template <int NC>
+__global__ __launch_bounds__(256) void gen_records64_pair_kernel(int64_t* const* __restrict__ cols, uint64_t n,
+                                                                 uint64_t first, uint64_t nkeys, uint64_t mkeys,
+                                                                 uint64_t seed) {
+  int64_t* c[NC];
+  bool aligned = true;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    c[j] = cols[j];
+    aligned = aligned && ((((uintptr_t)c[j]) & 15) == 0);
+  }
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (!aligned) {
+    for (uint64_t r = t0; r < n; r += stride) {
+      const uint64_t i = first + r;
+      c[0][r] = (int64_t)fast_mod64(mix64(seed ^ (i * kG)), nkeys, mkeys);
+#pragma unroll
+      for (int j = 1; j < NC; ++j) c[j][r] = (int64_t)(mix64((seed + (uint64_t)j * kH) ^ i) >> 33);
+    }
+    return;
+  }
+  const uint64_t pairs = n >> 1;
+  for (uint64_t q = t0; q < pairs; q += stride) {
+    const uint64_t i = first + 2 * q;
+    u64x2 v;
+    v.x = fast_mod64(mix64(seed ^ (i * kG)), nkeys, mkeys);
+    v.y = fast_mod64(mix64(seed ^ ((i + 1) * kG)), nkeys, mkeys);
+    __builtin_nontemporal_store(v, (gu64x2*)(c[0]) + q);
+#pragma unroll
+    for (int j = 1; j < NC; ++j) {
+      const uint64_t h = seed + (uint64_t)j * kH;
+      v.x = mix64(h ^ i) >> 33;
+      v.y = mix64(h ^ (i + 1)) >> 33;
+      __builtin_nontemporal_store(v, (gu64x2*)(c[j]) + q);
+    }
+  }
+  if ((n & 1) && t0 == 0) {                         // the last row of an odd count
+    const uint64_t r = n - 1, i = first + r;
+    c[0][r] = (int64_t)fast_mod64(mix64(seed ^ (i * kG)), nkeys, mkeys);
+#pragma unroll
+    for (int j = 1; j < NC; ++j) c[j][r] = (int64_t)(mix64((seed + (uint64_t)j * kH) ^ i) >> 33);
+  }
+}
+
 // Row-major twin: out[r * ncols + j] (a 64-byte row store when ncols = 8).  One lane per field,
 // so a wave writes 8 consecutive 64-byte rows with coalesced 8-byte stores; the key modulo is a
 // multiply-high reduction (fast_mod64) instead of a 64- or 128-bit software division.  WIDE: the
@@ -105,6 +157,18 @@ DR_API int dr_gen_records64(int64_t* const* cols, int ncols, uint64_t n, uint64_
                             uint64_t seed, uint64_t dim_mult, hipStream_t s) {
   if (ncols < 1 || ncols > 8 || nkeys == 0) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
+  if (!dim_mult) {
+    const unsigned g = grid_for((n + 1) / 2, 256, 16384);
+    switch (ncols) {
+#define DR_GEN_PAIR(NCV) \
+  case NCV: gen_records64_pair_kernel<NCV><<<g, 256, 0, s>>>(cols, n, first, nkeys, ~0ull / nkeys, seed); break;
+      DR_GEN_PAIR(1) DR_GEN_PAIR(2) DR_GEN_PAIR(3) DR_GEN_PAIR(4)
+      DR_GEN_PAIR(5) DR_GEN_PAIR(6) DR_GEN_PAIR(7) DR_GEN_PAIR(8)
+#undef DR_GEN_PAIR
+    }
+    DR_LAUNCH_CHECK();
+    return 0;
+  }
   const unsigned __int128 top = (unsigned __int128)(first + n) * dim_mult + seed;
   gen_records64_kernel<<<grid_for(n, 256, 16384), 256, 0, s>>>(cols, ncols, n, first, nkeys, ~0ull / nkeys, seed,
                                                                dim_mult, dim_mult && (top >> 64) != 0);

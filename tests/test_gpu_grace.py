@@ -61,6 +61,27 @@ def test_records64_rows_generator_matches_numpy_twin(ncols, dim):
         np.testing.assert_array_equal(rows[:, j].cpu().numpy(), ref[j])
 
 
+@pytest.mark.parametrize("ncols,dim,n,skew", [(4, False, 20_011, 0), (1, False, 4096, 0), (8, False, 777, 1),
+                                              (3, True, 5_003, 0), (5, False, 1, 0)])
+def test_records64_columns_generator_matches_numpy_twin(ncols, dim, n, skew):
+    """dr_gen_records64 (column stores: two rows per lane with 16-byte stores, the one-row path for
+    columns that are not 16-byte aligned (``skew``) and odd counts) against the numpy twin."""
+    import numpy as np
+    from dryad_amd.models.records_cpu import dim_multiplier, gen_columns
+    from dryad_amd.ops import relational as R
+    nkeys = 1_000_003 if dim else 977
+    dm = dim_multiplier(nkeys) if dim else 0
+    first = 500_000 if dim else 123
+    base = [torch.full((n + skew,), -7, dtype=torch.int64, device="cuda") for _ in range(ncols)]
+    cols = [b[skew:] for b in base]
+    R.gen_records64(cols, first, nkeys, 11, dm)
+    ref = gen_columns(first, n, nkeys, 11, ncols=ncols, dim_mult=dm)
+    for j in range(ncols):
+        np.testing.assert_array_equal(cols[j].cpu().numpy(), ref[j])
+        if skew:
+            assert int(base[j][0]) == -7
+
+
 def _rows(keys, stride=64, key_len=8):
     n = len(keys)
     r = torch.zeros((n, stride // 8), dtype=torch.int64)
