@@ -84,6 +84,9 @@ class LoopbackRank:
 
     def step(self) -> dict:
         W, me, A, B = self.W, self.rank, self.A, self.B
+        # the previous step's output is not kept through this one (a real rank hands it on): held,
+        # it crowded stage B's allocations into fresh segments (a 1.8 s stage B, one step in four)
+        self.out = None
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         torch.cuda.reset_peak_memory_stats(self.dev)
         base = torch.cuda.memory_allocated(self.dev)
