@@ -31,6 +31,8 @@ _lib.register_signatures({
 })
 
 TABLE_BITS = 12
+# aggregation workgroups (one per CU by LDS: 1024 = four rounds over the 256 CUs)
+AGG_GRID = 1024
 MAX_DIGIT = 10
 MIN_ROWS = 1 << 20
 _INT = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8)
@@ -159,7 +161,7 @@ def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
     # run r's rows: rstart[r] .. rstart[r + 1]; workgroup g folds the runs starting in its share
     rstart = torch.zeros(runs.shape[0] + 1, dtype=torch.int64, device=dev)
     torch.cumsum(runs, 0, out=rstart[1:])
-    G = max(1, min(1024, n // 4096))
+    G = max(1, min(AGG_GRID, n // 4096))
     targets = torch.arange(G + 1, dtype=torch.int64, device=dev) * ((n + G - 1) // G)
     wrun = torch.searchsorted(rstart[:-1].contiguous(), targets)
     # field offsets of the accumulated columns inside the packed row
