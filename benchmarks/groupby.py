@@ -52,12 +52,7 @@ def main():
     ap.add_argument("--raw-shuffle", action="store_true",
                     help="with --loopback-ranks: shuffle the pruned raw rows (Select -> HashPartition -> GroupBy) "
                          "instead of partial aggregation before the shuffle")
-    ap.add_argument("--dg-agg-grid", type=int, default=0,
-                    help="A/B only: workgroups of the dense aggregation kernel (ops/densegroup.AGG_GRID)")
     a = ap.parse_args()
-    if a.dg_agg_grid:
-        from dryad_amd.ops import densegroup as _DG
-        _DG.AGG_GRID = a.dg_agg_grid
     if a.loopback_ranks:
         return loopback(a)
     w = world()

@@ -15,7 +15,9 @@
 // a signal, or one that exits with EX_TEMPFAIL = 75 to ask for it), the whole gang is stopped and
 // a fresh gang of NEW child processes is started, up to K times: epoch e gets DRYAD_GANG_EPOCH=e,
 // DRYAD_GANG_RESTARTS=K, DRYAD_CHECKPOINT_DIR (the persisted stage outputs it resumes from,
-// runtime/checkpoint.py) and MASTER_PORT = P + e (a fresh rendezvous).  Nothing is ever re-exec'd
+// runtime/checkpoint.py) and MASTER_PORT = P + e (a fresh rendezvous).  The checkpoint directory
+// is launcher-owned: <--checkpoint-dir>/dryad-ckpt-<launcher pid>, created at start and removed
+// when the launcher exits; nothing else under --checkpoint-dir is ever touched.  Nothing is ever re-exec'd
 // in place: a process that initialised the GPU only exits.  A rank that fails with an ordinary
 // error code (a deterministic job failure) ends the job as before.  The reference re-executes a
 // failed vertex process from its persisted inputs the same way (DrVertex.cpp:1042-1171,
@@ -65,7 +67,7 @@ struct GangResult {
 
 struct Options {
   int n = 1, port = 29511, grace = 10, max_restarts = 0;
-  std::string log_dir, ckpt_dir;
+  std::string log_dir, ckpt_dir;     // ckpt_dir: the launcher-owned subdirectory (see above)
   char** prog = nullptr;
 };
 
@@ -165,14 +167,13 @@ int rm_entry(const char* path, const struct stat*, int, struct FTW*) {
   return remove(path) == 0 ? 0 : 0;
 }
 
-// Empty the checkpoint directory (its contents, not the directory): before the first gang, so a
-// new launch never resumes a previous launch's stage outputs, and after the job completed.
-void wipe_checkpoints(const Options& o) {
+// Remove this launch's own checkpoint subdirectory (never the user's --checkpoint-dir itself):
+// a new launch has a new subdirectory, so it never resumes a previous launch's stage outputs.
+void remove_checkpoints(const Options& o) {
   if (o.ckpt_dir.empty()) return;
   struct stat st {};
-  if (stat(o.ckpt_dir.c_str(), &st) != 0) return;
+  if (lstat(o.ckpt_dir.c_str(), &st) != 0 || !S_ISDIR(st.st_mode)) return;
   nftw(o.ckpt_dir.c_str(), rm_entry, 16, FTW_DEPTH | FTW_PHYS);
-  mkdir(o.ckpt_dir.c_str(), 0755);
 }
 
 void log_event(const Options& o, const std::string& json) {
@@ -204,8 +205,18 @@ int main(int argc, char** argv) {
   if (i >= argc || o.n < 1 || o.n > 64 || o.max_restarts < 0) return usage();
   o.prog = argv + i;
   if (!o.log_dir.empty()) mkdir(o.log_dir.c_str(), 0755);
-  wipe_checkpoints(o);
-  if (!o.ckpt_dir.empty()) mkdir(o.ckpt_dir.c_str(), 0755);
+  if (!o.ckpt_dir.empty()) {
+    struct stat st {};
+    if (stat(o.ckpt_dir.c_str(), &st) != 0) {
+      if (mkdir(o.ckpt_dir.c_str(), 0755) != 0) { std::perror("--checkpoint-dir"); return 2; }
+    } else if (!S_ISDIR(st.st_mode)) {
+      std::fprintf(stderr, "[dryad-launch] --checkpoint-dir %s is not a directory\n", o.ckpt_dir.c_str());
+      return 2;
+    }
+    o.ckpt_dir += "/dryad-ckpt-" + std::to_string(getpid());
+    remove_checkpoints(o);                     // a stale one of a recycled pid
+    if (mkdir(o.ckpt_dir.c_str(), 0700) != 0) { std::perror("checkpoint subdirectory"); return 2; }
+  }
   struct sigaction sa {};
   sa.sa_handler = on_signal;
   sigaction(SIGINT, &sa, nullptr);
@@ -216,11 +227,12 @@ int main(int argc, char** argv) {
     const GangResult r = run_gang(o, epoch, reason);
     if (r.rank < 0) {
       if (epoch > 0) log_event(o, "{\"ev\":\"job_complete\",\"epoch\":" + std::to_string(epoch) + "}");
-      wipe_checkpoints(o);
+      remove_checkpoints(o);
       return 0;
     }
     if (!r.lost || epoch >= o.max_restarts || r.rank >= o.n) {
       std::fprintf(stderr, "[dryad-launch] job failed: rank %d status %d\n", r.rank, r.code);
+      remove_checkpoints(o);
       return r.code;
     }
     reason = "rank " + std::to_string(r.rank) + " lost (status " + std::to_string(r.code) + ")";

@@ -273,7 +273,8 @@ PYBIND11_MODULE(_dryad_native, m) {
   });
   // ChunkReader: file -> ring of caller-owned (pinned) host buffers, several reader threads.
   py::class_<ChunkReader>(m, "ChunkReader")
-      .def(py::init<const std::string&, int64_t, int64_t, int64_t, const std::vector<uint64_t>&, int>(),
+      .def(py::init<const std::string&, int64_t, int64_t, int64_t, const std::vector<std::pair<uint64_t, int64_t>>&,
+                    int>(),
            py::arg("path"), py::arg("offset"), py::arg("length"), py::arg("chunk_bytes"), py::arg("buffers"),
            py::arg("threads"))
       .def("size", &ChunkReader::size)

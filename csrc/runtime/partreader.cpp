@@ -12,8 +12,13 @@
 namespace dryad {
 
 ChunkReader::ChunkReader(const std::string& path, int64_t offset, int64_t length, int64_t chunk_bytes,
-                         const std::vector<uint64_t>& buf_ptrs, int threads) {
-  if (chunk_bytes <= 0 || buf_ptrs.empty()) throw std::invalid_argument("ChunkReader: chunk size / buffers");
+                         const std::vector<std::pair<uint64_t, int64_t>>& bufs, int threads) {
+  if (chunk_bytes <= 0 || bufs.empty()) throw std::invalid_argument("ChunkReader: chunk size / buffers");
+  for (size_t i = 0; i < bufs.size(); ++i)
+    if (bufs[i].first == 0 || bufs[i].second < chunk_bytes)
+      throw std::invalid_argument("ChunkReader: buffer " + std::to_string(i) + " holds " +
+                                  std::to_string(bufs[i].second) + " bytes, less than a " +
+                                  std::to_string(chunk_bytes) + "-byte chunk");
   fd_ = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
   if (fd_ < 0) throw std::runtime_error("ChunkReader: cannot open " + path + ": " + std::strerror(errno));
   struct stat st;
@@ -29,8 +34,8 @@ ChunkReader::ChunkReader(const std::string& path, int64_t offset, int64_t length
 #ifdef POSIX_FADV_SEQUENTIAL
   ::posix_fadvise(fd_, offset_, length_, POSIX_FADV_SEQUENTIAL);
 #endif
-  for (size_t i = 0; i < buf_ptrs.size(); ++i) {
-    bufs_.push_back(reinterpret_cast<uint8_t*>(buf_ptrs[i]));
+  for (size_t i = 0; i < bufs.size(); ++i) {
+    bufs_.push_back(reinterpret_cast<uint8_t*>(bufs[i].first));
     free_.push_back((int)i);
   }
   const int nt = threads < 1 ? 1 : threads;

@@ -21,6 +21,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 namespace dryad {
@@ -34,9 +35,11 @@ struct ReadyChunk {
 class ChunkReader {
  public:
   // [offset, offset + length) of `path` (length < 0: to the end) in chunks of chunk_bytes, into
-  // the buffers buf_ptrs[i] (each >= chunk_bytes), with `threads` reader threads.
+  // the buffers bufs[i] = (address, size in bytes), with `threads` reader threads.  Every buffer
+  // must hold a whole chunk: a buffer smaller than chunk_bytes (or a null one) is refused with
+  // std::invalid_argument before any thread starts, so no read can run past a buffer.
   ChunkReader(const std::string& path, int64_t offset, int64_t length, int64_t chunk_bytes,
-              const std::vector<uint64_t>& buf_ptrs, int threads);
+              const std::vector<std::pair<uint64_t, int64_t>>& bufs, int threads);
   ~ChunkReader();
   int64_t size() const { return length_; }
   int64_t chunks() const { return nchunks_; }

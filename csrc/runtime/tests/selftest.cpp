@@ -16,6 +16,7 @@
 
 #include "../codec.h"
 #include "../jobgraph.h"
+#include "../partreader.h"
 #include "../pump.h"
 #include "../workqueue.h"
 
@@ -181,12 +182,60 @@ static int test_pump() {
   return 0;
 }
 
+// ChunkReader: buffers are (address, size) pairs; one smaller than a chunk is refused before any
+// reader thread starts; a read through a ring smaller than the file returns every byte in order.
+static int test_chunk_reader(const std::string& dir) {
+  const std::string path = dir + "/chunkreader.bin";
+  std::vector<uint8_t> data(1000003);
+  for (size_t i = 0; i < data.size(); ++i) data[i] = (uint8_t)(i * 2654435761u >> 13);
+  {
+    std::ofstream f(path, std::ios::binary);
+    f.write(reinterpret_cast<const char*>(data.data()), (std::streamsize)data.size());
+  }
+  const int64_t chunk = 65536;
+  std::vector<std::vector<uint8_t>> ring(3, std::vector<uint8_t>(chunk));
+  std::vector<uint8_t> small(chunk - 1);
+  bool refused = false;
+  try {
+    ChunkReader bad(path, 0, -1, chunk, {{(uint64_t)ring[0].data(), chunk}, {(uint64_t)small.data(), chunk - 1}}, 2);
+  } catch (const std::invalid_argument&) {
+    refused = true;
+  }
+  CHECK(refused);
+  refused = false;
+  try {
+    ChunkReader bad(path, 0, -1, chunk, {{0, chunk}}, 1);
+  } catch (const std::invalid_argument&) {
+    refused = true;
+  }
+  CHECK(refused);
+  std::vector<std::pair<uint64_t, int64_t>> bufs;
+  for (auto& b : ring) bufs.emplace_back((uint64_t)b.data(), (int64_t)b.size());
+  ChunkReader rd(path, 17, -1, chunk, bufs, 3);
+  CHECK(rd.size() == (int64_t)data.size() - 17);
+  std::vector<uint8_t> got(rd.size());
+  ReadyChunk c;
+  int64_t seen = 0;
+  while (rd.next(&c, -1)) {
+    CHECK(c.slot >= 0 && c.bytes <= chunk);
+    std::memcpy(got.data() + c.chunk * chunk, ring[c.slot].data(), (size_t)c.bytes);
+    seen += c.bytes;
+    rd.release(c.slot);
+  }
+  CHECK(rd.error().empty());
+  CHECK(seen == rd.size());
+  CHECK(std::memcmp(got.data(), data.data() + 17, got.size()) == 0);
+  std::remove(path.c_str());
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const std::string dir = argc > 1 ? argv[1] : "/tmp";
   if (int r = test_jobgraph()) return r;
   if (int r = test_codec()) return r;
   if (int r = test_workqueue(dir)) return r;
   if (int r = test_pump()) return r;
+  if (int r = test_chunk_reader(dir)) return r;
   std::printf("SELFTEST_OK\n");
   return 0;
 }

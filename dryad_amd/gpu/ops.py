@@ -264,7 +264,7 @@ def op_read(op, inputs, v):
             from ..models.records_cpu import dim_multiplier
             nk = int(q.get("keys", 1 << 20))
             return NM.device_table(lo, hi - lo, nk, int(q.get("seed", 0)),
-                                   dim_multiplier(nk) if q.get("mode") == "dim" else 0, v.device)
+                                   dim_multiplier(nk) if q.get("mode") == "dim" else 0, v.device, NM.namelen(q))
         if kind == "range":
             start = int(q.get("start", 0))
             a = torch.arange(start + lo, start + hi, dtype=torch.int32 if start + hi < 2**31 else torch.int64,

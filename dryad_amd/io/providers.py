@@ -371,7 +371,8 @@ class GenProvider(DataProvider):
         if kind == "records64":
             return p, int(q.get("count", 0)) * 8 * int(q.get("cols", 8))
         if kind == "names":
-            return p, int(q.get("count", 0)) * 32
+            from ..models import names as NM
+            return p, int(q.get("count", 0)) * (16 + max(16, NM.namelen(q)))
         return p, int(q.get("count", 0)) * 4
 
     def exists(self, uri):
@@ -422,7 +423,7 @@ class GenProvider(DataProvider):
             from ..models.records_cpu import dim_multiplier
             nk = int(q.get("keys", 1 << 20))
             return NM.host_records(lo, hi - lo, nk, int(q.get("seed", 0)),
-                                   dim_multiplier(nk) if q.get("mode") == "dim" else 0)
+                                   dim_multiplier(nk) if q.get("mode") == "dim" else 0, NM.namelen(q))
         raise DryadLinqException(ErrorCode.UnrecognizedDataSource, f"unknown generator {kind}")
 
     def temp_uri(self, name):

@@ -38,6 +38,11 @@ class ReadStats:
         self.chunks = 0
 
 
+def _sized(ring) -> list:
+    """The ring as (address, bytes) pairs: the native reader refuses a chunk larger than a buffer."""
+    return [(b.tensor.data_ptr(), b.tensor.numel() * b.tensor.element_size()) for b in ring]
+
+
 def read_to_device(path: str, device, offset: int = 0, length: int = -1, out: torch.Tensor | None = None,
                    stats: ReadStats | None = None) -> torch.Tensor:
     """Bytes [offset, offset + length) of ``path`` (to the end when length < 0) into a device
@@ -60,8 +65,7 @@ def read_to_device(path: str, device, offset: int = 0, length: int = -1, out: to
     ring = _ring()
     chunk = min(CHUNK, ring[0].tensor.numel())      # the ring may predate a CHUNK change
     with _RING_LOCK:           # one reader per process at a time owns the ring
-        rd = runtime().ChunkReader(path, int(offset), int(length), chunk, [b.tensor.data_ptr() for b in ring],
-                                   THREADS)
+        rd = runtime().ChunkReader(path, int(offset), int(length), chunk, _sized(ring), THREADS)
         cur = torch.cuda.current_stream(dev)
         cs = torch.cuda.Stream(dev)
         cs.wait_stream(cur)
@@ -130,7 +134,7 @@ def read_rows_to_device(path: str, device, offset: int, n: int, stride: int, out
         raise ValueError(f"read_rows_to_device: {stride}-byte rows exceed the {ring[0].tensor.numel()}-byte ring buffers")
     stage = torch.empty(cb, dtype=torch.uint8, device=dev)
     with _RING_LOCK:
-        rd = runtime().ChunkReader(path, int(offset), int(length), cb, [b.tensor.data_ptr() for b in ring], THREADS)
+        rd = runtime().ChunkReader(path, int(offset), int(length), cb, _sized(ring), THREADS)
         cur = torch.cuda.current_stream(dev)
         cs = torch.cuda.Stream(dev)
         cs.wait_stream(cur)

@@ -135,8 +135,9 @@ def _partition(key64, cols64, vmin, vbits, kmin, kbits, src, n, shift, dbits, de
     return out, runs
 
 
-def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
-    """GroupBy on one integer key column through the dense-key path; see the module docstring."""
+def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False, agg_grid: int = AGG_GRID):
+    """GroupBy on one integer key column through the dense-key path; see the module docstring.
+    ``agg_grid``: workgroups of the aggregation kernel (an argument, for A/B tools only)."""
     n = key.shape[0]
     if not key.is_cuda or (not force and n < MIN_ROWS):
         return None
@@ -161,7 +162,7 @@ def dense_aggregate(key: torch.Tensor, specs: list, force: bool = False):
     # run r's rows: rstart[r] .. rstart[r + 1]; workgroup g folds the runs starting in its share
     rstart = torch.zeros(runs.shape[0] + 1, dtype=torch.int64, device=dev)
     torch.cumsum(runs, 0, out=rstart[1:])
-    G = max(1, min(AGG_GRID, n // 4096))
+    G = max(1, min(int(agg_grid), n // 4096))
     targets = torch.arange(G + 1, dtype=torch.int64, device=dev) * ((n + G - 1) // G)
     wrun = torch.searchsorted(rstart[:-1].contiguous(), targets)
     # field offsets of the accumulated columns inside the packed row
@@ -210,7 +211,7 @@ def dense_state_ok(specs: list, key: torch.Tensor, stride: int = 1) -> bool:
     """Can dense_state_update fold these accumulators?  specs: [(state, op, value or None)]: int64
     states with any op, float64 states with sums, values of the listed dtypes; every state a
     column of ``stride``-element rows."""
-    if key.dtype not in _DS_KEY or len(specs) > 8:
+    if not key.is_cuda or key.dtype not in _DS_KEY or len(specs) > 8:
         return False
     if any(st.dim() != 1 or st.stride(0) != stride for st, _, _ in specs):
         return False

@@ -31,9 +31,6 @@ from ..parallel import shuffle
 from . import sort as S
 from . import terasort as TSG
 
-# local sort algorithm of 16-byte entries: "hybrid" (top-window LSD + in-LDS run sort); the
-# "prefix" (64-bit LSD + tie fix-up) and full-width "lsd" variants remain for tests
-SORT_ALGO = "hybrid"
 # pipelined exchange of the multi-rank sort: key sub-ranges per destination rank (0 = from the
 # data size; tests set it) and the target bytes per (source, destination) pair and round
 PIPE_SUBS = 0
@@ -188,12 +185,8 @@ def local_sort_rows(rows: torch.Tensor, out: torch.Tensor, ent_a: torch.Tensor, 
     if descending:
         invert_keys(e, key_len)
     b0, b1, _ = key_bits(key_len)
-    if SORT_ALGO == "hybrid":
-        srt = S.sort_entries_hybrid(e, b0, b1, tmp=ent_b[:n], hi_bounds=None if descending else hi_bounds)
-    elif SORT_ALGO == "prefix" and b0 < 64:
-        srt = S.sort_entries_prefix(e, b0, tmp=ent_b[:n])
-    else:
-        srt = S.sort_entries(e, b0, b1, tmp=ent_b[:n])
+    # 16-byte entries: the hybrid sort (top-window LSD passes + in-LDS run sort)
+    srt = S.sort_entries_hybrid(e, b0, b1, tmp=ent_b[:n], hi_bounds=None if descending else hi_bounds)
     return S.gather_rows(rows, entries=srt, out=out[:n])
 
 
@@ -283,11 +276,7 @@ def _sort_keys(rows: torch.Tensor, ent: torch.Tensor, tmp: torch.Tensor, key_off
         invert_keys(e, key_len)
         hi_bounds = None
     b0, b1, _ = key_bits(key_len)
-    if SORT_ALGO == "hybrid":
-        return S.sort_entries_hybrid(e, b0, b1, tmp=tmp, hi_bounds=hi_bounds)
-    if SORT_ALGO == "prefix" and b0 < 64:
-        return S.sort_entries_prefix(e, b0, tmp=tmp)
-    return S.sort_entries(e, b0, b1, tmp=tmp)
+    return S.sort_entries_hybrid(e, b0, b1, tmp=tmp, hi_bounds=hi_bounds)
 
 
 def _agree(err: BaseException | None, w: World, what: str, value: int = 0):

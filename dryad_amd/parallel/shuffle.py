@@ -144,6 +144,32 @@ def gang_status(ok: bool, value: int = 0, world: World | None = None) -> list[tu
     return [(bool(a), int(b)) for a, b in all_gather_tensor(t, w).tolist()]
 
 
+def digest(obj) -> int:
+    """A 63-bit digest of a plain-data value (its repr): what ranks compare in a planning vote
+    instead of pickling the value to every peer."""
+    import hashlib
+    return int.from_bytes(hashlib.blake2b(repr(obj).encode(), digest_size=8).digest(), "little") >> 1
+
+
+def gather_ints(values: list, world: World | None = None) -> list:
+    """Every rank's list of int64 ``values`` (same length everywhere) from one small tensor
+    all-gather: [[rank 0's values], [rank 1's], ...]."""
+    w = world or get_world()
+    if not w.collective:
+        return [list(values)]
+    dev = w.device if w.backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([list(values)], dtype=torch.int64, device=dev)
+    return all_gather_tensor(t, w).tolist()
+
+
+def vote(ok: bool, key=None, world: World | None = None, values: tuple = ()) -> tuple[bool, list]:
+    """A planning vote as one tensor all-gather: (every rank ok and every rank's ``key`` equal,
+    every rank's ``values``).  Replaces pickled all_gather_object votes on the per-job path."""
+    got = gather_ints([1 if ok else 0, digest(key)] + [int(v) for v in values], world)
+    agree = all(g[0] for g in got) and len({g[1] for g in got}) == 1
+    return agree, [g[2:] for g in got]
+
+
 def all_gather_tensor(t: torch.Tensor, world: World | None = None) -> torch.Tensor:
     """All-gather equally shaped tensors along dim 0 (R5: sampler gather, R3 broadcast of small data)."""
     w = world or get_world()

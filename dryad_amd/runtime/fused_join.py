@@ -28,7 +28,6 @@ final aggregate vertex is unchanged.  Sums are 64-bit integer sums of int64 fiel
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
 
 from ..gpu.table import DeviceTable
 from ..io.providers import GenProvider, parse_uri, provider_for
@@ -429,11 +428,6 @@ def _max_abs(src, f, dev) -> int:
 def vote(desc, runner):
     """Collective: every rank's layout; fused iff all ranks can and agree."""
     lay = plan_local(desc, runner)
-    W = runner.world.size
-    votes = [lay]
-    if W > 1:
-        votes = [None] * W
-        dist.all_gather_object(votes, lay)
-    if all(v is not None for v in votes) and all(v == votes[0] for v in votes):
-        return votes[0]
-    return None
+    # one tensor all-gather of (ok, digest of the layout): every rank fused alike, no pickles
+    agree, _ = shuffle.vote(lay is not None, sorted(lay.items()) if lay is not None else None, runner.world)
+    return lay if agree else None

@@ -330,13 +330,10 @@ class GpuJobRunner:
                     ok = False
                 if not ok:
                     spec = None
-        votes = [None] * self.world.size
-        if self.world.collective:
-            dist.all_gather_object(votes, (bool(ok), None if spec is None else (spec.off, spec.length)))
-        else:
-            votes = [(bool(ok), None if spec is None else (spec.off, spec.length))]
-        if all(v[0] for v in votes) and len({v[1] for v in votes}) == 1:
-            f["spec"] = votes[0][1]
+        mine = None if spec is None else (spec.off, spec.length)
+        agree, _ = shuffle.vote(bool(ok), mine, self.world)      # one tensor all-gather, no pickles
+        if agree:
+            f["spec"] = mine
             return True
         return False
 
@@ -614,11 +611,8 @@ class GpuJobRunner:
                 ok = spec is not None and (force is True or need > int(budget or EX.default_budget(self.dev)))
             else:
                 ok = False
-            votes = [(ok, spec)]
-            if W > 1:
-                votes = [None] * W
-                dist.all_gather_object(votes, (ok, spec))
-            if all(v[0] for v in votes) and len({v[1] for v in votes}) == 1:
+            agree, _ = shuffle.vote(bool(ok), spec, self.world)
+            if agree:
                 out[sid] = dict(c, source=src, spec=spec)
         return out
 
@@ -733,10 +727,8 @@ class GpuJobRunner:
             do = lambda p, _s=s.id: self.owner(p, _s)    # noqa: E731
             if recover:      # (collective vote: a rank that owns no source partition still takes part)
                 mine = [q for q in range(src_stage.partitions) if so(q) == me]
-                miss = [any((si.src, q) not in self.channels for q in mine)]
-                if W > 1:
-                    miss = [None] * W
-                    dist.all_gather_object(miss, any((si.src, q) not in self.channels for q in mine))
+                lost = any((si.src, q) not in self.channels for q in mine)
+                miss = [not ok for ok, _ in shuffle.gang_status(not lost, 0, self.world)] if W > 1 else [lost]
                 if any(miss):
                     self._rematerialize(si.src)
             if si.kind == "cross" and W > 1:
@@ -1737,6 +1729,8 @@ def _commit_partfile_impl(runner, s, uri, path, local):
                 mine[p] = []
                 for j, f in enumerate(v.path):
                     os.replace(f, f"{tmp}.{j}")
+                    if os.path.exists(f + PF.INDEX_SUFFIX):          # the piece's block index
+                        os.replace(f + PF.INDEX_SUFFIX, f"{tmp}.{j}" + PF.INDEX_SUFFIX)
                     mine[p].append(f"{tmp}.{j}")
                 continue
             if isinstance(v, GS.StreamedPart):          # written bucket / chunk by chunk by its stage

@@ -39,7 +39,6 @@ import os
 import time
 
 import torch
-import torch.distributed as dist
 
 from ..gpu.table import DeviceTable, Shape
 from ..io.providers import GenProvider, parse_uri, provider_for
@@ -51,6 +50,8 @@ log = get_logger("grace_stage")
 
 CHUNK_ROWS = 1 << 26
 _I64 = torch.int64
+# longest string a packed join row carries inline (a longer one fails the stage, non-retryable)
+MAX_INLINE_STRING_BYTES = 1 << 16
 
 
 class StreamedPart:
@@ -67,7 +68,10 @@ class StreamedPart:
 # input sides: device tables chunk by chunk; packed into rows of int64 words for the grace
 # partitioner: word 0 = the join key word, then every field the result selector reads (a fixed-
 # width field is one word, floats by bit pattern; a string field is a length word and its bytes
-# inline, zero-padded, up to GraceJoinStringBytes).
+# inline, zero-padded, in S words).  S covers the longest string the ranks voted (a side that
+# knows its strings' lengths says so before the stage starts) and at least GraceJoinStringBytes;
+# a longer string met while partitioning restarts pass A, on every rank alike, with S widened to
+# it (run: no string length aborts the join).
 class _Side:
     fields: list
     dtypes: list                          # torch dtype per field, None for a string field
@@ -79,6 +83,11 @@ class _Side:
 
     def field_words(self, f: int, S: int) -> int:
         return 1 + S if self.dtypes[f] is None else 1
+
+    def max_string_bytes(self, fields) -> int:
+        """Longest string among ``fields`` of this side (0: none of them is a string; -1: not
+        known before the data is read)."""
+        return 0 if all(self.dtypes[f] is not None for f in fields) else -1
 
     def table(self, words: torch.Tensor, cols: list, S: int) -> DeviceTable:
         """DeviceTable of this side from packed rows ``words`` [m, width] (word 0 = key word)
@@ -155,12 +164,17 @@ class _NamesSide(_Side):
         self.n = hi - self.lo
         self.nk, self.seed = int(q.get("keys", 1 << 20)), int(q.get("seed", 0))
         self.dim = dim_multiplier(self.nk) if q.get("mode") == "dim" else 0
+        self.name_len = NM.namelen(q)
         self.fields, self.dtypes = list(NM.FIELDS), [None, _I64, _I64]
         self.shape = Shape("tuple", self.fields)
 
+    def max_string_bytes(self, fields) -> int:
+        from ..models import names as NM
+        return NM.max_name_bytes(self.name_len) if 0 in fields else 0
+
     def chunk_table(self, a, b, dev):
         from ..models import names as NM
-        return NM.device_table(self.lo + a, b - a, self.nk, self.seed, self.dim, dev)
+        return NM.device_table(self.lo + a, b - a, self.nk, self.seed, self.dim, dev, self.name_len)
 
 
 class _TableSide(_Side):
@@ -172,6 +186,13 @@ class _TableSide(_Side):
 
     def chunk_table(self, a, b, dev):
         return self.t.slice(a, b)
+
+    def max_string_bytes(self, fields) -> int:
+        m = 0
+        for f in fields:
+            if self.dtypes[f] is None and self.t.n:
+                m = max(m, int(self.t.cols[self.fields[f] + "#len"][: self.t.n].max()))
+        return m
 
 
 class _PartfileSide(_Side):
@@ -346,14 +367,16 @@ def _key_word(t: DeviceTable, side, spec, exact: bool) -> torch.Tensor:
 
 def _pack(t: DeviceTable, side, cols: list, width: int, S: int, kw: torch.Tensor):
     """Rows [m, width] int64: word 0 = kw, then the fields ``cols`` (strings: length + bytes).
-    Returns (rows, ok): ok False when a string is longer than S words."""
+    Returns (rows, ok, longest): ok False when a string is longer than S words, and then
+    ``longest`` = the chunk's longest string in bytes (0 otherwise)."""
     m = t.n
     rows = torch.zeros((m, width), dtype=_I64, device=kw.device)
     if m == 0:
-        return rows, True
+        return rows, True, 0
     rows[:, 0] = kw
     pos = 1
     ok = True
+    lens = []
     for f in cols:
         name = side.fields[f]
         if side.dtypes[f] is None:
@@ -362,11 +385,12 @@ def _pack(t: DeviceTable, side, cols: list, width: int, S: int, kw: torch.Tensor
             rows[:, pos] = ln
             rb = rows.view(torch.uint8).view(m, 8 * width)
             ok = TX.scatter_strings(t.strs[name], off, ln, rb, 8 * (pos + 1), max_len=8 * S) and ok
+            lens.append(ln)
             pos += 1 + S
             continue
         rows[:, pos] = _word(t.cols[name])
         pos += 1
-    return rows, ok
+    return rows, ok, (0 if ok else max(int(x.max()) for x in lens))
 
 
 def _verify(orows, irows, oi, ii, lay, S):
@@ -562,8 +586,10 @@ def plan_local(desc, runner):
         uo = sorted(set(uo) | set(ko))
         ui = sorted(set(ui) | set(ki))
     rows = [sum(x.n for x in sd) for sd in sides]
+    lens = [x.max_string_bytes(u) for sd, u in zip(sides, (uo, ui)) for x in sd]
     return dict(ko=ko, ki=ki, uo=uo, ui=ui, rows=rows, exact=exact, kinds=list(kinds),
-                bytes=rows[0] * 8 * len(fo) + rows[1] * 8 * len(fi))
+                bytes=rows[0] * 8 * len(fo) + rows[1] * 8 * len(fi),
+                max_str=-1 if any(x < 0 for x in lens) else max(lens, default=0))
 
 
 def vote(desc, runner):
@@ -573,21 +599,19 @@ def vote(desc, runner):
     shuffled copies and the gathered pairs)."""
     force = runner.ctx._props.get("GraceJoin")
     lay = None if force is False else plan_local(desc, runner)
-    W = runner.world.size
-    votes = [lay]
-    if W > 1:
-        votes = [None] * W
-        dist.all_gather_object(votes, lay)
-    if any(v is None for v in votes) or any((v["ko"], v["ki"], v["uo"], v["ui"], v["exact"]) !=
-                                            (votes[0]["ko"], votes[0]["ki"], votes[0]["uo"], votes[0]["ui"],
-                                             votes[0]["exact"]) for v in votes):
+    key = None if lay is None else (lay["ko"], lay["ki"], lay["uo"], lay["ui"], lay["exact"])
+    # one tensor all-gather: (ok, digest of the layout, input bytes) of every rank
+    agree, vals = shuffle.vote(lay is not None, key, runner.world,
+                               values=(0 if lay is None else lay["bytes"], 0 if lay is None else lay["max_str"]))
+    if not agree:
         return None
     if force is not True:
         from ..ops.extsort import default_budget
         budget = int(runner.ctx._props.get("HbmBudgetBytes") or default_budget(runner.dev))
-        if 3 * max(v["bytes"] for v in votes) <= budget:
+        if 3 * max(v[0] for v in vals) <= budget:
             return None
-    return votes[0]
+    lens = [v[1] for v in vals]
+    return dict(lay, max_str=-1 if min(lens) < 0 else max(lens))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -603,19 +627,21 @@ def run(desc, runner, lay) -> dict:
     parts = [p for p in range(stage.partitions) if runner.owner(p) == me]
     sides = [[_side(r, p) for p in parts] for r in desc["reads"]]
     keys, used = (lay["ko"], lay["ki"]), (lay["uo"], lay["ui"])
-    S = -(-int(runner.ctx._props.get("GraceJoinStringBytes") or 64) // 8)      # inline string words
     proto = [sides[0][0], sides[1][0]]
-    nwords = [1 + sum(proto[k].field_words(f, S) for f in used[k]) for k in (0, 1)]
-    width = max(nwords)                                      # [key word, fields..] padded to one stride
-    # where each key field sits in the packed rows (for the verification of hash-keyed matches)
-    kpos = []
-    for k in (0, 1):
-        pos, at = 1, {}
-        for f in used[k]:
-            at[f] = pos
-            pos += proto[k].field_words(f, S)
-        kpos.append([(f, at.get(f, -1), kind) for f, kind in zip(keys[k], lay["kinds"])])
-    vlay = dict(kpos=kpos)
+    # inline string bytes: GraceJoinStringBytes, or the longest string the ranks voted
+    s_bytes = max(int(runner.ctx._props.get("GraceJoinStringBytes") or 64), int(lay.get("max_str") or 0))
+
+    def layout(S):
+        """(row width in words, verification layout) for S inline string words."""
+        nwords = [1 + sum(proto[k].field_words(f, S) for f in used[k]) for k in (0, 1)]
+        kpos = []        # where each key field sits in the packed rows (verification of hashed matches)
+        for k in (0, 1):
+            pos, at = 1, {}
+            for f in used[k]:
+                at[f] = pos
+                pos += proto[k].field_words(f, S)
+            kpos.append([(f, at.get(f, -1), kind) for f, kind in zip(keys[k], lay["kinds"])])
+        return max(nwords), dict(kpos=kpos)            # [key word, fields..] padded to one stride
     n_loc = torch.tensor([sum(x.n for x in sd) for sd in sides], dtype=_I64, device=dev)
     n_tot, n_max = n_loc.clone(), n_loc.clone()
     shuffle.all_reduce_(n_tot, "sum", w)
@@ -632,26 +658,51 @@ def run(desc, runner, lay) -> dict:
         shuffle.all_reduce_(cnt, "max", w)
         lst += [(sides[s_][0], 0, 0)] * (int(cnt.item()) - len(lst))
         sched.append(lst)
-    grace = GR.GraceHashJoin(w, 8 * width, 0, 8, {"O": -(-n_tot[0] // W), "I": -(-n_tot[1] // W)},
-                             max(b - a for lst in sched for _, a, b in lst) or 1,
-                             hbm_budget=runner.ctx._props.get("HbmBudgetBytes"), build=names[build])
     t0 = time.perf_counter()
     sink = _Sink(runner, stage, parts, desc)
     matches = 0
     strings = any(d is None for k in (0, 1) for d in proto[k].dtypes)
+    # string lengths unknown before the data is read: every chunk's fit is agreed (a host sync);
+    # lengths the ranks voted are covered by S, so no per-chunk agreement is needed
+    check = strings and int(lay.get("max_str", -1)) < 0
+    widened = 0
+    grace = None
     try:
-        for s_ in (0, 1):
-            for src, a, b in sched[s_]:
-                t = src.chunk_table(a, b, dev)
-                kw = _key_word(t, src, keys[s_], lay["exact"]) if t.n else torch.empty(0, dtype=_I64, device=dev)
-                rows, ok = _pack(t, src, used[s_], width, S, kw)
-                if strings and not all(o for o, _ in shuffle.gang_status(ok, 0, w)):
-                    # a string past GraceJoinStringBytes on some rank: every rank leaves together
-                    from ..errors import GangAgreementError
-                    raise GangAgreementError(f"grace join: a string field longer than {8 * S} bytes "
-                                             "(GraceJoinStringBytes)")
-                del t
-                grace.add_chunk(names[s_], rows.view(torch.uint8).reshape(b - a, 8 * width))
+        while True:                       # pass A; again with wider rows if a string did not fit
+            S = -(-s_bytes // 8)                                    # inline string words
+            width, vlay = layout(S)
+            grace = GR.GraceHashJoin(w, 8 * width, 0, 8, {"O": -(-n_tot[0] // W), "I": -(-n_tot[1] // W)},
+                                     max(b - a for lst in sched for _, a, b in lst) or 1,
+                                     hbm_budget=runner.ctx._props.get("HbmBudgetBytes"), build=names[build])
+            need = 0
+            for s_ in (0, 1):
+                for src, a, b in sched[s_]:
+                    t = src.chunk_table(a, b, dev)
+                    kw = _key_word(t, src, keys[s_], lay["exact"]) if t.n else torch.empty(0, dtype=_I64, device=dev)
+                    rows, ok, longest = _pack(t, src, used[s_], width, S, kw)
+                    del t
+                    if not ok and not check:
+                        raise RuntimeError("grace join: a string longer than the voted maximum (internal)")
+                    if check:
+                        st = shuffle.gang_status(ok, longest, w)
+                        if not all(o for o, _ in st):
+                            # a string longer than S words on some rank: every rank widens alike
+                            need = max(v for _, v in st)
+                            break
+                    grace.add_chunk(names[s_], rows.view(torch.uint8).reshape(b - a, 8 * width))
+                if need:
+                    break
+            if not need:
+                break
+            grace.release()
+            grace = None
+            if need > MAX_INLINE_STRING_BYTES:
+                from ..errors import GangAgreementError
+                raise GangAgreementError(f"grace join: a {need}-byte string field is longer than the "
+                                         f"{MAX_INLINE_STRING_BYTES}-byte row limit", retryable=False)
+            s_bytes = -(-need // 64) * 64
+            widened += 1
+            log.info("grace join %s: string of %d bytes, pass A again with %d inline bytes", desc["join"], need, s_bytes)
         grace.finish_partitioning()
         t1 = time.perf_counter()
         bname, pname = names[build], names[1 - build]
@@ -686,11 +737,13 @@ def run(desc, runner, lay) -> dict:
         sink.abort()
         raise
     finally:
-        grace.release()
+        if grace is not None:
+            grace.release()
     out = sink.finish(V)
     runner.join_stats = dict(spilled_bytes=stats.spilled_bytes, buckets=stats.buckets, resident=stats.resident,
                              in_hbm=stats.in_hbm, build=names[build],
                              layout=f"{width} x 8-byte words (pruned{', strings inline' if strings else ''})",
+                             string_bytes=8 * S if strings else 0, widened=widened,
                              key="exact" if lay["exact"] else "hashed + verified",
                              matches=matches, partition_s=round(t1 - t0, 4), join_s=round(t2 - t1, 4),
                              written_bytes=sink.written, kind="grace join stage")
@@ -709,6 +762,7 @@ class _Sink:
         self.written_bytes, self.index = 0, []          # (string records) block index of the stream
         self.stream = False
         self.paths, self.fbytes = None, None            # a split output: its part files and their sizes
+        self.frecs, self.findex = None, None            # ... their record counts and block indexes
         self.split = int(runner.ctx.PartFileSplitBytes or 0) > 0
         if stage.is_output and not self.agg and not desc["after"]:
             scheme, path, _ = parse_uri(stage.output["uri"])
@@ -728,32 +782,39 @@ class _Sink:
             if self.dtype is None:
                 self.dtype = _table_dtype(data)
             enc = CD.encode(data, self.dtype) if self.dtype is not None else None
-            fixed = enc is not None
+            offs = None
             if enc is None and self.dtype is not None and CD.var_layout(self.dtype) is not None:
                 got = CD.encode_var(data, self.dtype, full_offsets=True)
                 if got is not None:
                     enc, offs = got
-                    # block index of the concatenated stream: records n, n + B, ... of it
-                    B = CD.BLOCK
-                    j0 = (-self.n) % B
-                    if data.n > j0:
-                        self.index.append(offs[j0::B] + self.written_bytes)
             if enc is not None:
+                B = CD.BLOCK
                 if self.writer is None:
                     from ..io.writer import SPLIT_MAX, PartWriter
-                    if self.split and fixed:
-                        # fixed-width records with PartFileSplitBytes: the buckets' results go to
-                        # SPLIT_MAX part files at once (page-cache writes serialise per inode)
+                    if self.split:
+                        # PartFileSplitBytes: the buckets' results go to SPLIT_MAX part files at
+                        # once (page-cache writes serialise per inode); string records keep one
+                        # block index per file
                         self.paths = [f"{self.tmp}.{j}" for j in range(SPLIT_MAX)]
-                        self.fbytes = [0] * SPLIT_MAX
+                        self.fbytes, self.frecs = [0] * SPLIT_MAX, [0] * SPLIT_MAX
+                        self.findex = [[] for _ in range(SPLIT_MAX)]
                         self.writer = PartWriter(self.paths, data.device, self.runner.write_stats)
                     else:
                         self.writer = PartWriter(self.tmp, data.device, self.runner.write_stats)
                 if self.paths is not None:
                     j = min(range(len(self.fbytes)), key=self.fbytes.__getitem__)
+                    if offs is not None:          # block index of file j: its records n, n + B, ...
+                        j0 = (-self.frecs[j]) % B
+                        if data.n > j0:
+                            self.findex[j].append(offs[j0::B] + self.fbytes[j])
                     self.writer.write(enc, file=j)
                     self.fbytes[j] += enc.numel()
+                    self.frecs[j] += data.n
                 else:
+                    if offs is not None:          # block index of the stream: records n, n + B, ...
+                        j0 = (-self.n) % B
+                        if data.n > j0:
+                            self.index.append(offs[j0::B] + self.written_bytes)
                     self.writer.write(enc)
                 self.n += data.n
                 self.written_bytes += enc.numel()
@@ -805,9 +866,13 @@ class _Sink:
             sizes = self.writer.close()
             self.written = sum(sizes)
             keep = []
-            for f, b in zip(self.paths, sizes):
+            from ..io import partfile as PF
+            from ..ops import codec as CD
+            for j, (f, b) in enumerate(zip(self.paths, sizes)):
                 if b:
                     keep.append(f)
+                    if self.findex[j]:
+                        PF.write_index(f, self.frecs[j], b, torch.cat(self.findex[j]).cpu().numpy(), CD.BLOCK)
                 else:
                     os.remove(f)
             out[parts[0]] = StreamedPart(keep or self.paths[:1], self.n, self.written, self.dtype)

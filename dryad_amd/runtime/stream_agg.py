@@ -178,12 +178,15 @@ class DenseState:
                 and k.dtype in (torch.int8, torch.int16, torch.int32, torch.int64))
 
     def _plan(self, part: DeviceTable):
+        """Accumulator layout, fixed by the first chunk.  Count accumulators are recorded as
+        "count" here; whether a chunk's count column is implicit (a raw partial: int8 ones) or a
+        folded count to be summed is decided per chunk (``_chunk_specs``), because the partial step
+        may emit raw rows for one chunk and folded rows for the next."""
         specs = []
         for j, a in enumerate(self.d.aggs):
             col = part.cols.get(f"a{j}")
             if a.kind == "count":
-                implicit = col is None or col.dtype == torch.int8
-                specs.append((f"a{j}", "count" if implicit else "sum", None if implicit else f"a{j}", torch.int64))
+                specs.append((f"a{j}", "count", None, torch.int64))
                 self.outdt[f"a{j}"] = torch.int64
             elif a.kind == "sum":
                 dt = torch.float64 if col.dtype.is_floating_point else torch.int64
@@ -195,12 +198,24 @@ class DenseState:
             elif a.kind == "avg":
                 c = part.cols.get(f"c{j}")
                 specs.append((f"a{j}", "sum", f"a{j}", torch.float64))
-                specs.append((f"c{j}", "count" if c is None or c.dtype == torch.int8 else "sum",
-                              None if c is None or c.dtype == torch.int8 else f"c{j}", torch.int64))
+                specs.append((f"c{j}", "count", None, torch.int64))
                 self.outdt[f"a{j}"], self.outdt[f"c{j}"] = torch.float64, torch.int64
             else:
                 return None              # any / all / user aggregates: the bucket path
         return specs
+
+    def _chunk_specs(self, part: DeviceTable):
+        """The specs for one chunk: a count accumulator sums the chunk's count column when it is a
+        folded count (wider than int8), and adds one per row when the column is absent or holds
+        the raw partial's int8 ones."""
+        out = []
+        for name, op, src, dt in self.specs:
+            if op == "count":
+                col = part.cols.get(name)
+                if col is not None and col.dtype != torch.int8:
+                    op, src = "sum", name
+            out.append((name, op, src, dt))
+        return out
 
     def _layout(self):
         """8-byte accumulators only: one [R, S] matrix, a key's S slots side by side (its folds touch
@@ -275,8 +290,9 @@ class DenseState:
                 return False
             self._alloc(lo, hi, k.device)
         from ..ops import densegroup as DG
+        specs = self._chunk_specs(part)
         fused = [(self._col(self.state, name), op, part.cols[src][:n] if src is not None else None)
-                 for name, op, src, _ in self.specs]
+                 for name, op, src, _ in specs]
         stride = len(self.specs) if self.aos else 1
         if DG.dense_state_ok(fused, k, stride):
             # one pass, every accumulator
@@ -285,7 +301,7 @@ class DenseState:
         idx = (k - self.lo).to(torch.int64)
         if self.seen is not None:
             self.seen.index_fill_(0, idx, 1)
-        for name, op, src, dt in self.specs:
+        for name, op, src, dt in specs:
             st = self._col(self.state, name)
             if op == "count":
                 st.index_add_(0, idx, torch.ones(1, dtype=dt, device=st.device).expand(n))

@@ -159,7 +159,7 @@ def _chunks(plan, p, device, vctx):
         for a in range(lo, hi, per):
             m = min(per, hi - a)
             yield NM.device_table(a, m, nk, int(q.get("seed", 0)), dim_multiplier(nk) if q.get("mode") == "dim" else 0,
-                                  device)
+                                  device, NM.namelen(q))
         return
     if kind == "range":
         start = int(q.get("start", 0))

@@ -202,3 +202,37 @@ def test_float_key_join_from_stored_tables(tmp_path):
     assert res["fallbacks"] == [], res["fallbacks"]
     loc = _loc()
     _same(got, sorted(q(loc)))
+
+
+@pytest.mark.parametrize("stored", [False, True])
+def test_long_string_keys_widen_and_split_output(tmp_path, stored):
+    """200-byte string keys (gen://names&namelen=200) past the 64-byte GraceJoinStringBytes: the
+    generator's declared length widens the packed rows up front; from stored tables the length is
+    unknown, the first chunk that does not fit restarts pass A with wider rows on every rank (no
+    abort).  The string records stream into several part files at once (PartFileSplitBytes), each
+    with its own block index, and read back oracle-equal."""
+    from dryad_amd.io import partfile as PF
+    nr = "gen://names?count=60000&partitions=2&keys=50000&seed=3&mode=dim&namelen=200"
+    ns = "gen://names?count=90000&partitions=2&keys=50000&seed=4&namelen=200"
+    g = _ctx(budget=16 << 20)
+    g.PartFileSplitBytes = 1
+    r_src, s_src = nr, ns
+    if stored:
+        w = _ctx()
+        r_src, s_src = "partfile://" + str(tmp_path / "r.pt"), "partfile://" + str(tmp_path / "s.pt")
+        w.FromStore(nr).ToStore(r_src, delete_if_exists=True).SubmitAndWait()
+        w.FromStore(ns).ToStore(s_src, delete_if_exists=True).SubmitAndWait()
+    uri = "partfile://" + str(tmp_path / "jl.pt")
+    q = lambda c, a, b: c.FromStore(a).Join(c.FromStore(b), lambda r: r[0], lambda s: s[0],  # noqa: E731
+                                            lambda r, s: (r[0], r[1], s[2]))
+    q(g, r_src, s_src).ToStore(uri, delete_if_exists=True).SubmitAndWait()
+    res, js = _stats(g)
+    assert js.get("kind") == "grace join stage" and res["fallbacks"] == [], (js, res["fallbacks"])
+    assert js["string_bytes"] >= 200, js
+    assert (js["widened"] > 0) == stored, js
+    meta = PF.read_meta(str(tmp_path / "jl.pt"))
+    assert meta.count > 2, meta.count
+    got = sorted(g.FromStore(uri))
+    exp = sorted(q(_loc(), nr, ns))
+    _same(got, exp)
+    assert len(got[0][0]) == 200

@@ -84,3 +84,23 @@ def test_launcher_does_not_relaunch_a_deterministic_failure(tmp_path):
     out = subprocess.run([_launcher(), "--gpus", "2", "--max-restarts", "3", "--", sys.executable, str(script)],
                          capture_output=True, text=True, timeout=40)
     assert out.returncode == 3 and "epoch 1" not in out.stderr, out.stderr
+
+
+def test_launcher_checkpoint_dir_is_launcher_owned(tmp_path):
+    """--checkpoint-dir names a PARENT: the ranks get <dir>/dryad-ckpt-<launcher pid>, which the
+    launcher removes when it exits; the user's own files under <dir> are never touched."""
+    d = tmp_path / "data"
+    d.mkdir()
+    (d / "keep.txt").write_text("user data")
+    script = tmp_path / "ck.py"
+    script.write_text("import os\nc = os.environ['DRYAD_CHECKPOINT_DIR']\nassert os.path.isdir(c), c\n"
+                      "open(os.path.join(c, 'x' + os.environ['RANK']), 'w').write('1')\nprint(c)\n")
+    out = subprocess.run([_launcher(), "--gpus", "2", "--checkpoint-dir", str(d), "--log-dir", str(tmp_path / "logs"),
+                          "--", sys.executable, str(script)], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    owned = open(tmp_path / "logs" / "rank0.log").read().strip()
+    assert os.path.dirname(owned) == str(d) and os.path.basename(owned).startswith("dryad-ckpt-"), owned
+    assert sorted(os.listdir(d)) == ["keep.txt"] and (d / "keep.txt").read_text() == "user data"
+    bad = subprocess.run([_launcher(), "--gpus", "1", "--checkpoint-dir", str(d / "keep.txt"), "--", sys.executable,
+                          "-c", "pass"], capture_output=True, text=True, timeout=60)
+    assert bad.returncode == 2 and (d / "keep.txt").exists()

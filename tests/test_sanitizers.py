@@ -1,5 +1,5 @@
 """Host-side sanitizer runs of the native runtime: the job graph, codec, text
-splitting and WorkQueue self-test built with -fsanitize=address,undefined and with
+splitting, WorkQueue and ChunkReader self-test built with -fsanitize=address,undefined and with
 -fsanitize=thread.  (GPU sanitizers are not available on this pool; kernels are covered by the
 numerics tests.)"""
 import os
@@ -9,7 +9,7 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = [os.path.join(ROOT, "csrc", "runtime", f) for f in ("jobgraph.cpp", "codec.cpp", "workqueue.cpp")]
+SRC = [os.path.join(ROOT, "csrc", "runtime", f) for f in ("jobgraph.cpp", "codec.cpp", "workqueue.cpp", "partreader.cpp")]
 TEST = os.path.join(ROOT, "csrc", "runtime", "tests", "selftest.cpp")
 
 

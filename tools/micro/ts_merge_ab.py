@@ -6,6 +6,11 @@ previous revision of tsmerge.hip) are timed against the in-tree library and thei
 compared with it.
 
     python tools/micro/ts_merge_ab.py [variant ...]      # default: in-tree + every _tm_ab/*.so
+
+A baseline variant is built from a previous revision, not kept as a source snapshot:
+
+    mkdir -p tools/micro/_tm_ab && git show HEAD~1:csrc/kernels/tsmerge.hip > /tmp/tm_base.hip && \
+    hipcc --offload-arch=gfx950 -O3 -shared -fPIC -Icsrc/kernels /tmp/tm_base.hip -o tools/micro/_tm_ab/libtm_base.so
 """
 import ctypes
 import os
@@ -18,7 +23,8 @@ import torch  # noqa: E402
 
 def main():
     here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_tm_ab")
-    want = sys.argv[1:] or ["in-tree"] + sorted(f for f in os.listdir(here) if f.endswith(".so"))
+    have = sorted(f for f in os.listdir(here) if f.endswith(".so")) if os.path.isdir(here) else []
+    want = sys.argv[1:] or ["in-tree"] + have
     W, K, fb = 8, 131072, 24
     dev = torch.device("cuda")
     g = torch.Generator(device=dev)
