@@ -69,6 +69,10 @@ def main():
                     help="run the per-rank program of a W-rank job on this one GPU, the all-to-all-v replaced by "
                          "generating the exact bytes this rank would receive (not timed); reports per-rank ms")
     ap.add_argument("--loopback-rank", type=int, default=0, help="which rank of the --loopback-ranks job to run")
+    ap.add_argument("--model-link-GBps", type=float, nargs="*", default=[300.0, 450.0],
+                    help="with --loopback-ranks: MODELLED per-rank step with the all-to-all-v on a link of this many "
+                         "GB/s per GPU (measured per-round pack / merge times replayed in the exchange's queue order; "
+                         "labelled modelled)")
     ap.add_argument("--gen-fused", action="store_true",
                     help="N > 1 (and --loopback-ranks): no input table; the records are generated straight into "
                          "the exchange's send rows in key order (GenFusedShuffle; labelled in config.input)")
@@ -254,6 +258,12 @@ def loopback(args, env):
                              if mode == "gen-fused" else
                              "gen://terasort generated into the rank's HBM table (128-byte pitch), timed"),
                    "wall_s_per_step_incl_simulated_exchange": round(sum(walls) / len(walls), 3),
+                   # the exchange is not run here: these steps are MODELLED from the measured per-round
+                   # pack / merge kernel times of the last step and an assumed per-GPU link rate
+                   "modelled_exchange": ([job.model(x) for x in args.model_link_GBps]
+                                         if mode == "table" and args.model_link_GBps else None),
+                   "round_pack_ms": [round(x, 3) for x in job.rounds["pack_ms"]] if mode == "table" else None,
+                   "round_merge_ms": [round(x, 3) for x in job.rounds["merge_ms"]],
                    "validated": None if val is None else val["ok"], "validation": val, "env": env},
     }
     print(json.dumps(line), flush=True)

@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void gp_offsets_kernel(uint32_t* __restrict__ 
 // ATOMIC (every destination appends at its fill counter, row order inside a destination free):
 // no count pass; each tile reserves its rows per destination with one atomicAdd on the fill
 // counter (a join's buckets do not need the input order).  Rows past cap are dropped and flagged.
-template <int ITEMS, int WC, int OWC, bool VEC, bool STAGE_PROJ = false, bool ATOMIC = false>
+template <int ITEMS, int WC, int OWC, bool VEC, bool STAGE_PROJ = false, bool ATOMIC = false, int LDSW = 16384>
 __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restrict__ rows, uint64_t n, uint32_t Wdyn,
                                                          uint32_t kw, int key_len, uint64_t seed, int shift, uint32_t nb,
                                                          const uint32_t* __restrict__ prefix,
@@ -187,7 +187,10 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
                                                          int64_t* __restrict__ fill = nullptr,
                                                          uint32_t* __restrict__ overflow = nullptr) {
   constexpr int TILE = kBlock * ITEMS;
-  constexpr int LDS_DW = STAGE_PROJ ? 8192 : 16384;  // projected tiles: 32 KiB, three workgroups per CU
+  // projected tiles: 32 KiB, three workgroups per CU; rows of 129..512 bytes: one row per thread
+  // in a 128 KiB tile (one workgroup per CU)
+  constexpr int LDS_DW = STAGE_PROJ ? 8192 : LDSW;
+  static_assert(STAGE_PROJ || LDS_DW >= kBlock * ITEMS, "tile");
   static_assert(!STAGE_PROJ || OWC == 4, "staged projections are one 16-byte piece per row");
   const uint32_t W = WC > 0 ? (uint32_t)WC : Wdyn;
   const uint32_t OW = OWC > 0 ? (uint32_t)OWC : OWdyn;
@@ -449,14 +452,18 @@ bool key_ok(uint32_t stride, uint32_t key_off, uint32_t key_len) {
 
 }  // namespace
 
+// Rows up to this many bytes are partitioned (wide rows: one per thread, kWideLdsDw dwords of LDS).
+constexpr uint32_t kMaxStride = 512;
+constexpr int kWideLdsDw = 256 * (kMaxStride / 4);
+
 // Workspace (bytes) of dr_grace_partition for n rows of `stride` bytes into nb destinations.
 DR_API uint64_t dr_grace_workspace(uint64_t n, uint32_t stride, uint32_t nb) {
   uint32_t G; uint64_t per_block;
-  geometry(n, stride <= 64 ? 1024 : 512, G, per_block);     // the most workgroups any tile size gives
+  geometry(n, stride <= 64 ? 1024 : stride <= 128 ? 512 : 256, G, per_block);   // the most workgroups any tile gives
   return (uint64_t)nb * G * 4 + (uint64_t)nb * 8 * 2 + 256;
 }
 
-// Partition `n` rows (stride % 4 == 0, <= 128 bytes) by dest = fastrange(32 bits of hash(key) at
+// Partition `n` rows (stride % 4 == 0, <= kMaxStride bytes) by dest = fastrange(32 bits of hash(key) at
 // `shift`, nb) into per-destination runs at dst_ptr[d] (device array of nb row pointers).  The
 // destination rows are bytes [proj_off, proj_off + out_stride) of the input rows (out_stride =
 // stride, proj_off = 0: whole rows).
@@ -469,7 +476,7 @@ DR_API int dr_grace_partition(const uint8_t* rows, uint64_t n, uint32_t stride, 
                               const int64_t* cap, uint32_t contig_from, int64_t* chunk_counts, int64_t* bases,
                               uint32_t* overflow, void* ws, uint32_t out_stride, uint32_t proj_off, int unordered,
                               hipStream_t s) {
-  if (!key_ok(stride, key_off, key_len) || stride > 128 || nb < 1 || nb > kMaxBuckets || n >= (1ull << 32) ||
+  if (!key_ok(stride, key_off, key_len) || stride > kMaxStride || nb < 1 || nb > kMaxBuckets || n >= (1ull << 32) ||
       (shift != 0 && shift != 32))
     return (int)hipErrorInvalidValue;
   if (out_stride == 0 || (out_stride & 3) || (proj_off & 3) || proj_off + out_stride > stride)
@@ -478,14 +485,14 @@ DR_API int dr_grace_partition(const uint8_t* rows, uint64_t n, uint32_t stride, 
     hipMemsetAsync(chunk_counts, 0, sizeof(int64_t) * nb, s);
     return 0;
   }
-  const bool small = stride <= 64;
+  const bool small = stride <= 64, wide = stride > 128;
   const bool vec0 = (stride & 15) == 0 && (out_stride & 15) == 0 && (proj_off & 15) == 0 &&
                     (((uintptr_t)rows) & 15) == 0;
   // 16-byte projection holding the key: stage only the projected slice (4096-row tiles)
   const bool stage_proj = vec0 && out_stride == 16 && stride > 16 && key_off >= proj_off &&
                           key_off + key_len <= proj_off + out_stride;
   uint32_t G; uint64_t per_block;
-  geometry(n, stage_proj ? 2048 : (small ? 1024 : 512), G, per_block);
+  geometry(n, stage_proj ? 2048 : (small ? 1024 : wide ? 256 : 512), G, per_block);
   uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
   uint64_t* totals = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(ws) + (((uint64_t)nb * G * 4 + 15) & ~15ull));
   const uint32_t W = stride / 4, kw = key_off / 4;
@@ -510,6 +517,13 @@ DR_API int dr_grace_partition(const uint8_t* rows, uint64_t n, uint32_t stride, 
   if (stage_proj) {
     gp_scatter_kernel<8, 0, 4, true, true><<<G, 256, 0, s>>>(in, n, W, kw, (int)key_len, seed, shift, nb, counts,
                                                              bases, dst_ptr, cap, contig_from, G, per_block, OW, PO);
+  } else if (wide) {
+    if (vec)
+      gp_scatter_kernel<1, 0, 0, true, false, false, kWideLdsDw><<<G, 256, 0, s>>>(
+          in, n, W, kw, (int)key_len, seed, shift, nb, counts, bases, dst_ptr, cap, contig_from, G, per_block, OW, PO);
+    else
+      gp_scatter_kernel<1, 0, 0, false, false, false, kWideLdsDw><<<G, 256, 0, s>>>(
+          in, n, W, kw, (int)key_len, seed, shift, nb, counts, bases, dst_ptr, cap, contig_from, G, per_block, OW, PO);
   } else if (small) {
     if (stride == 64 && out_stride == 64 && vec) DR_GP_SCATTER(4, 16, 16, true);
     else if (vec) DR_GP_SCATTER(4, 0, 0, true);

@@ -412,7 +412,7 @@ class TeraSortLoopbackJob:
         cap = int(self.n * (1 + cfg.slack))
         self.bufs = RS.SortBuffers.allocate(cap, RECORD, self.dev) if mode == "gen-fused" else \
             RS.SortBuffers.allocate_pitch128(cap, RECORD, self.dev)
-        self.B = RS.pipeline_subs(self.n * RECORD, W)
+        self.B = RS.pipeline_subs(self.n * RECORD, W) if mode == "gen-fused" else RS.fine_subs(self.n * RECORD, W)
         self.input = None if input_uri is None else self._prepare_input(input_uri)
         self.out = None
         self.phases = {}
@@ -488,6 +488,7 @@ class TeraSortLoopbackJob:
                 g = me * B + b
                 if Sg[g + 1] > Sg[g]:
                     TS.gen_gather64(recv[pos: pos + Sg[g + 1] - Sg[g]], srt[Sg[g]: Sg[g + 1]], s * n, seed)
+        self.recv_sizes = sizes
         return off, torch.stack(fine)
 
     def _samples(self, mine):
@@ -535,18 +536,43 @@ class TeraSortLoopbackJob:
         ev[2][0].record()
         seps = RS.separators_from_samples(allsamp, W * B)
         seps_hi = [int(x) & M64 for x in seps[:, 1].tolist()]
+        ev_plan = torch.cuda.Event(enable_timing=True)
+        pack_ev = [torch.cuda.Event(enable_timing=True) for _ in range(B)]
         if self.mode == "gen-fused":
             st, pack, counts, L = RS.pack_gen_fine(bufs, (me * n, seed), n, seps_hi, B, W, fb)
+            ev_plan.record()
             for b in range(B):
                 pack(b)
+                pack_ev[b].record()
         else:
-            st, counts, L, bad = RS.send_fine_rows(bufs, rows, e, tmp, hist, n, seps_hi, B, W, fb)
+            # the send side round by round, as the overlapped exchange packs it (FineSend.pack(b)
+            # just before round b's all-to-all-v is queued)
+            plan = RS.FineSend(bufs, rows, e, tmp, hist, n, seps_hi, B, W, fb)
+            st, counts, L, bad = plan.st, plan.counts, plan.L, plan.bad
+            ev_plan.record()
+            for b in range(B):
+                plan.pack(b)
+                pack_ev[b].record()
         ev[2][1].record()
         off, fine = self._receive(seps_hi, L, fb)            # the all-to-all-v (not timed)
         acc = TS.check(bufs.recv_rows()[: off[-1]])
         ev[3][0].record()
-        out = RS.merge_received_rounds(bufs, off, fine, L, fb, B, me, [off[-1]] * B, 0)
+        # the receive side round by round (FineMerge, as the exchange merges each received round)
+        recv = bufs.recv_rows()
+        merger = RS.FineMerge(fine, L, fb, B, me, bufs.rows_out)
+        merge_ev = [torch.cuda.Event(enable_timing=True) for _ in range(B)]
+        for b in range(B):
+            merger.merge(b, recv, off[b], off[b], off[b + 1])
+            merge_ev[b].record()
         ev[3][1].record()
+        fl = merger.flags.tolist()
+        for b in range(B):                   # a bucket past LDS (heavy skew): the round re-sorted
+            if fl[b]:
+                a, z = off[b], off[b + 1]
+                ea, eb = RS._round_scratch(bufs, off[-1], a, z)
+                RS.local_sort_rows(recv[a:z], bufs.rows_out[a:z], ea, eb, 0, KEYLEN,
+                                   hi_bounds=RS.fine_hi_bounds(L, fb, me * B + b))
+        out = bufs.rows_out[: off[-1]]
         torch.cuda.synchronize(dev)
         if self.mode != "gen-fused" and int(bad.item()):
             raise RuntimeError("send-side pack: an entry named a row past the table")
@@ -554,10 +580,34 @@ class TeraSortLoopbackJob:
         self.bounds = RS.fine_hi_bounds([L[me * B], L[(me + 1) * B]], fb, 0)
         self.phases = {"input_ms": ev[0][0].elapsed_time(ev[0][1]),
                        "sample_ms": ev[0][1].elapsed_time(ev[1][0]),
-                       "separators_pack_ms": ev[2][0].elapsed_time(ev[2][1]),
+                       "separators_entry_sort_ms": ev[2][0].elapsed_time(ev_plan),
+                       "pack_ms": ev_plan.elapsed_time(ev[2][1]),
                        "receive_sort_ms": ev[3][0].elapsed_time(ev[3][1])}
+        pk = [ev_plan.elapsed_time(pack_ev[0])] + [pack_ev[b - 1].elapsed_time(pack_ev[b]) for b in range(1, B)]
+        mg = [ev[3][0].elapsed_time(merge_ev[0])] + [merge_ev[b - 1].elapsed_time(merge_ev[b]) for b in range(1, B)]
+        # bytes this rank moves over its links per round (its own slice stays on the GPU)
+        send_b = [(st[(b + 1) * W] - st[b * W] - (st[b * W + me + 1] - st[b * W + me])) * RECORD for b in range(B)]
+        recv_b = [(off[b + 1] - off[b] - self.recv_sizes[me][b]) * RECORD for b in range(B)]
+        self.rounds = dict(pack_ms=pk, merge_ms=mg, send_bytes=send_b, recv_bytes=recv_b, st=st, off=off)
         self.sent_rows = st[-1]
         return out
+
+    def model(self, link_GBps: float) -> dict:
+        """MODELLED step of this rank with the all-to-all-v on a link of ``link_GBps`` per GPU (each
+        round takes max(bytes out, bytes in) / link): the measured per-round pack and merge times
+        of the last step replayed in the overlapped exchange's queue order
+        (recordsort._overlapped_fine_exchange, ``overlap_model``), and in the bulk order (every
+        round packed before the first goes out).  Labelled modelled: no link is measured here."""
+        r, ph = self.rounds, self.phases
+        t_ready = ph["input_ms"] + ph["sample_ms"] + ph["separators_entry_sort_ms"]
+        wire = [max(a, b) / (link_GBps * 1e6) for a, b in zip(r["send_bytes"], r["recv_bytes"])]
+        sched = RS.overlap_schedule(r["st"], r["off"], self.B, self.W, r["st"][-1], RS.OVERLAP_SLOTS)
+        ov = RS.overlap_model(t_ready, r["pack_ms"], r["merge_ms"], wire, sched, RS.OVERLAP_SLOTS)
+        bulk = RS.overlap_model(t_ready, r["pack_ms"], r["merge_ms"], wire, sched, RS.OVERLAP_SLOTS, bulk=True)
+        return dict(link_GBps=link_GBps, modelled=True, wire_ms=round(sum(wire), 2),
+                    overlapped_step_ms=round(ov["step_ms"], 2), first_round_queued_ms=round(ov["first_queued_ms"], 2),
+                    wire_idle_ms=round(ov["wire_idle_ms"], 2), bulk_step_ms=round(bulk["step_ms"], 2),
+                    bulk_first_round_queued_ms=round(bulk["first_queued_ms"], 2))
 
     @property
     def ms(self) -> float:

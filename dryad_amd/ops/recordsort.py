@@ -35,6 +35,10 @@ from . import terasort as TSG
 # data size; tests set it) and the target bytes per (source, destination) pair and round
 PIPE_SUBS = 0
 PIPE_ROUND_BYTES = 1 << 30
+# fine-bucket exchange over a materialised table: rows a rank receives per round (~1 GiB: the
+# overlapped exchange receives each round into one of OVERLAP_SLOTS small slots) and the slots
+OVERLAP_ROUND_BYTES = 1 << 30
+OVERLAP_SLOTS = 3
 _M64 = (1 << 64) - 1
 
 
@@ -120,8 +124,10 @@ class SortStats:
     round_send_bytes: list = field(default_factory=list)
     round_recv_bytes: list = field(default_factory=list)
     # HIP events on the compute stream: before the first payload collective is queued, after
-    # round b's wait (its rows usable), after the receive side's last kernel
+    # round b's wait (its rows usable), after the receive side's last kernel; the overlapped
+    # exchange also records each round's pack ("pack")
     events: dict = field(default_factory=dict)
+    overlap: dict = field(default_factory=dict)       # the overlapped exchange's report
 
     def exchange_report(self) -> dict:
         """Per-round exchange bytes and arrival times (ms after the first payload round was queued:
@@ -141,8 +147,18 @@ class SortStats:
                 if "done" in ev:
                     out["receive_tail_ms"] = round(ev["arrive"][-1].elapsed_time(ev["done"]), 3)
                     out["exchange_to_done_ms"] = round(ev["start"].elapsed_time(ev["done"]), 3)
+                if ev.get("entry") is not None:
+                    out["send_side_before_exchange_ms"] = round(ev["entry"].elapsed_time(ev["start"]), 3)
+                if ev.get("pack"):
+                    # the overlapped exchange: round 0 queued once its send rows were packed
+                    pk = [ev["start"].elapsed_time(e) for e in ev["pack"]]
+                    t0 = ev["entry"].elapsed_time(ev["start"]) if ev.get("entry") is not None else 0.0
+                    out["first_round_queued_ms"] = round(t0 + pk[0], 3)
+                    out["round_packed_ms"] = [round(x, 3) for x in pk]
             except RuntimeError:          # events not recorded (gloo rehearsal on CPU tensors)
                 pass
+        if self.overlap:
+            out["overlap"] = self.overlap
         return out
 
 
@@ -260,6 +276,21 @@ def pipeline_subs(max_rank_bytes: int, world_size: int) -> int:
     return min(b, cap)
 
 
+def fine_subs(max_rank_bytes: int, world_size: int) -> int:
+    """Rounds (key sub-ranges per destination) of the fine-bucket exchange over a materialised
+    table: about OVERLAP_ROUND_BYTES received per rank and round (each round's send rows are packed
+    just before it goes out and it is received into a slot of that size), a power of two, at
+    least 4, and world * rounds <= 2048 key ranges."""
+    cap = max(1, 2048 // world_size)
+    if PIPE_SUBS:
+        return max(1, min(PIPE_SUBS, cap))
+    want = -(-max_rank_bytes // max(1, OVERLAP_ROUND_BYTES))
+    b = 4
+    while b < want:
+        b <<= 1
+    return min(b, cap)
+
+
 def _range_hi_bounds(seps_hi: list, g: int) -> tuple[int, int]:
     """(min, max) of the key ``hi`` words that key range ``g`` (between separators g-1 and g) holds."""
     lo = seps_hi[g - 1] if g > 0 else 0
@@ -363,6 +394,10 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     rec = bufs.rows_out.shape[1]
     pitch = bufs.pitch
     rows = bufs.rows_in[:n, :rec] if src is None else src[:n]
+    entry = None
+    if stats is not None and bufs.rows_out.is_cuda and w.collective:
+        entry = torch.cuda.Event(enable_timing=True)          # the send side's start (exchange_report)
+        entry.record()
     if src is not None:
         assert src.shape[1] == rec and gen is None and not keys_ready, "src: [n, record width] rows, no producer keys"
         pitch = rec
@@ -430,9 +465,10 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     except Exception as ex:  # noqa: BLE001
         err = ex
     nmax = max(_agree(err, w, "distributed OrderBy (entries)", n))
-    B = pipeline_subs(nmax * rec, W)
+    B = fine_subs(nmax * rec, W) if fine_rows else pipeline_subs(nmax * rec, W)
     pack = None
     fine = None
+    plan = None
     try:
         if gen_path or fine_rows:
             seps = separators_from_samples(shuffle.all_gather_varlen(samp, w), W * B)
@@ -443,6 +479,7 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
                 # the whole bucket to one rank; the E128 path splits runs of equal keys (key, rank,
                 # row) instead.  The separators are global, so every rank switches alike.
                 fine_rows = False
+                B = pipeline_subs(nmax * rec, W)        # (the E128 path: world * rounds <= 256)
                 ent = S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
                 ent[:, 0].bitwise_or_(lo_or)
                 seps = choose_separators(ent, n, w, part_mask, sample_target, seed, bufs.ent_b, parts=W * B)
@@ -450,8 +487,10 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
             elif gen_path:
                 st, pack, counts, L = pack_gen_fine(bufs, gen, n, seps_hi, B, W, fb)
             if fine_rows:
-                st, counts, L, bad = send_fine_rows(bufs, rows, e, tmp, hist, n, seps_hi, B, W, fb,
-                                                    rebuild=lambda: S.extract_keys64_tile(rows, key_off, key_len, 0, e)[0])
+                # the rows are packed round by round in the exchange below, each just before it goes out
+                plan = FineSend(bufs, rows, e, tmp, hist, n, seps_hi, B, W, fb,
+                                rebuild=lambda: S.extract_keys64_tile(rows, key_off, key_len, 0, e)[0])
+                st, counts, L = plan.st, plan.counts, plan.L
         else:
             seps = choose_separators(ent, n, w, part_mask, sample_target, seed, bufs.ent_b, parts=W * B)
             seps_hi = [int(x) & _M64 for x in seps[:, 1].tolist()]
@@ -487,13 +526,49 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
         except Exception:  # noqa: BLE001 (out of HBM: the capacity vote reports it)
             rb = bufs
     _check_capacity(n_recv, rb.capacity, w)
-    recv_rows = rb.recv_rows()
-    send_flat, recv_flat = bufs.rows_out.view(-1), recv_rows.view(-1)
     ev = {}
     if stats is not None and bufs.rows_out.is_cuda:
         ev = dict(start=torch.cuda.Event(enable_timing=True), done=torch.cuda.Event(enable_timing=True),
-                  arrive=[torch.cuda.Event(enable_timing=True) for _ in range(B)])
+                  arrive=[torch.cuda.Event(enable_timing=True) for _ in range(B)], entry=entry)
         ev["start"].record()
+    if plan is not None:
+        ov = _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, n_sent, ev, key_len)
+        if ov is None:                 # no room for the receive slots: pack everything, then exchange
+            for b in range(B):
+                plan.pack(b)
+        else:
+            out, ov_stats = ov
+    if plan is None or ov is None:
+        out = _bulk_exchange(bufs, rb, st, send, off, rc, B, W, w, pack, fine, L if fine is not None else None,
+                             fb if fine is not None else 0, n_sent, ev, seps_hi, key_off, key_len, descending)
+    if ev:
+        ev["done"].record()
+    if plan is not None and int(plan.bad.item()):
+        raise RuntimeError("fine-bucket send side: an entry named a row past the table (corrupt entries)")
+    if stats is not None:
+        stats.n_in, stats.n_out, stats.rounds = n, n_recv, B
+        stats.send_counts = [sum(send[b][r] for b in range(B)) for r in range(W)]
+        stats.recv_counts = [sum(rc[s]) for s in range(W)]
+        stats.path = ("fine-bucket exchange, records generated into the send rows" if gen_path else
+                      f"fine-bucket exchange over the table (pitch {pitch}), "
+                      + ("rounds packed as they go out, received into slots" if plan is not None and ov is not None
+                         else "table packed before the first round") if fine_rows else
+                      "E128 range partition + per-round radix sort")
+        stats.round_send_bytes = [(st[(b + 1) * W] - st[b * W] - send[b][w.rank]) * rec for b in range(B)]
+        stats.round_recv_bytes = [(off[b + 1] - off[b] - rc[w.rank][b]) * rec for b in range(B)]
+        stats.events = ev
+        if plan is not None and ov is not None:
+            stats.overlap = ov_stats
+    return out[:n_recv]
+
+
+def _bulk_exchange(bufs, rb, st, send, off, rc, B, W, w, pack, fine, L, fb, n_sent, ev, seps_hi, key_off, key_len,
+                   descending):
+    """Every payload round queued up front, the send rows complete before the first (the receive
+    buffer is the input table's memory, rows_in); each round ordered as it arrives."""
+    rec = bufs.rows_out.shape[1]
+    recv_rows = rb.recv_rows()
+    send_flat, recv_flat = bufs.rows_out.view(-1), recv_rows.view(-1)
     handles = []
     for b in range(B):
         if pack is not None:
@@ -508,25 +583,163 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
             ev["arrive"][b].record()
     sent_after = [st[(b + 1) * W] for b in range(B)]
     if fine is not None:
-        out = merge_received_rounds(rb, off, fine, L, fb, B, w.rank, sent_after, n_sent, wait=wait)
+        return merge_received_rounds(rb, off, fine, L, fb, B, w.rank, sent_after, n_sent, wait=wait)
+    return sort_received_rounds(rb, off, sent_after, n_sent, seps_hi, B, w.rank, key_off, key_len, wait=wait,
+                                descending=descending)
+
+
+def overlap_schedule(st: list, off: list, B: int, W: int, n_sent: int, slots: int):
+    """When each received round of the overlapped exchange may be merged: k[j] = the last payload
+    round that must have completed before round j's rows are written to out[off[j]:off[j+1]]
+    (its own arrival, and the send rows under that output having gone out; rows past ``n_sent``
+    never held send data).  None when some round would hold its slot past ``slots`` rounds (the
+    receive slots would be overwritten before the merge read them)."""
+    k = []
+    for j in range(B):
+        need = min(off[j + 1], n_sent)
+        kk = j
+        while kk < B - 1 and st[(kk + 1) * W] < need:
+            kk += 1
+        k.append(kk)
+        if kk > j + slots - 1:
+            return None
+    return k
+
+
+def overlap_model(t_ready: float, pack_ms: list, merge_ms: list, wire_ms: list, sched: list | None, slots: int,
+                  bulk: bool = False) -> dict:
+    """Timeline of the fine-bucket exchange from per-round kernel and link times (ms): one compute
+    stream (packs, merges) and one communicator stream (rounds in order; a round starts when
+    everything queued before it on the compute stream is done, as RCCL's stream waits on the
+    caller's).  ``bulk``: every round packed before the first goes out (the table is the
+    receive buffer).  Used to MODEL a node's step from one-GPU measurements (bench.py
+    --loopback-ranks --model-link-GBps)."""
+    B = len(pack_ms)
+    sched = sched if sched is not None else list(range(B))
+    comp, comm = t_ready, 0.0
+    end = [0.0] * B
+    first = None
+    idle, last_end = 0.0, None
+
+    def coll(i, ready):
+        nonlocal comm, idle, last_end
+        start = max(ready, comm)
+        if last_end is not None:
+            idle += max(0.0, start - last_end)
+        end[i] = start + wire_ms[i]
+        comm = last_end = end[i]
+
+    def merge(j):
+        nonlocal comp
+        comp = max(comp, end[sched[j]]) + merge_ms[j]
+    if bulk:
+        comp += sum(pack_ms)
+        first = comp
+        for i in range(B):
+            coll(i, comp)
+        for j in range(B):
+            merge(j)
     else:
-        out = sort_received_rounds(rb, off, sent_after, n_sent, seps_hi, B, w.rank, key_off, key_len, wait=wait,
-                                   descending=descending)
+        pending = list(range(B))
+        for i in range(B):
+            comp += pack_ms[i]
+            if first is None:
+                first = comp
+            coll(i, comp)
+            while pending and (sched[pending[0]] <= i - 1 or pending[0] <= i + 1 - slots):
+                merge(pending.pop(0))
+        while pending:
+            merge(pending.pop(0))
+    return dict(step_ms=comp, first_queued_ms=first, wire_idle_ms=idle, wire_end_ms=comm)
+
+
+def _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, n_sent, ev, key_len):
+    """The fine-bucket exchange with the send side overlapped: round i's send rows are packed
+    (plan.pack(i)) just before its all-to-all-v is queued, so the first round is on the wire after
+    1/B of the pack instead of all of it.  The input table must stay readable until the last pack,
+    so nothing is received into it: round i lands in receive slot i % OVERLAP_SLOTS (each the size
+    of the largest round) and is merged from there into its final place out[off[i]:off[i+1]] (the
+    output overlays the send rows: the merge waits until the rows under it have gone out,
+    ``overlap_schedule``).  Queue order per round i: pack(i), all-to-all-v(i) [the communicator's
+    stream waits for everything queued before it on the compute stream, so a slot is reused only
+    after the merge that read it], then the merges that are safe.  Returns (output rows, report),
+    or None when the slots do not fit in HBM (the caller packs everything and uses the bulk path)."""
+    rec = bufs.rows_out.shape[1]
+    NS = OVERLAP_SLOTS
+    out_buf = rb.rows_out
+    sched = overlap_schedule(plan.st, off, B, W, n_sent if rb is bufs else 0, NS)
+    if sched is None:
+        return None
+    slot_rows = max([off[b + 1] - off[b] for b in range(B)] + [1])
+    try:
+        slots = torch.empty((NS * slot_rows, rec), dtype=torch.uint8, device=out_buf.device)
+    except (torch.OutOfMemoryError, RuntimeError):
+        return None
+    merger = FineMerge(fine, plan.L, fb, B, w.rank, out_buf)
+    cuda = out_buf.is_cuda
+    flags_host = torch.zeros(B, dtype=torch.int32, pin_memory=cuda)
+    merged_ev = [None] * B
+    tev = dict(pack=[], queued=None) if ev else None
+    handles = [None] * B
+    pending = list(range(B))           # rounds not merged yet, in order
+    send_flat = bufs.rows_out.view(-1)
+    fixups = []
+
+    def merge(j: int):
+        for h in range(j, sched[j] + 1):
+            shuffle.wait(handles[h])
+        if ev:
+            ev["arrive"][j].record()
+        base = (j % NS) * slot_rows
+        merger.merge(j, slots, base, off[j], off[j + 1])
+        if cuda:
+            flags_host[j: j + 1].copy_(merger.flags[j: j + 1], non_blocking=True)
+            merged_ev[j] = torch.cuda.Event()
+            merged_ev[j].record()
+        else:
+            flags_host[j] = merger.flags[j]
+
+    def check(j: int):
+        """Before slot j % NS is received into again: a round whose bucket outgrew LDS is ordered
+        from the slot now (rare: heavy key skew), while its rows are still there."""
+        if merged_ev[j] is not None:
+            merged_ev[j].synchronize()
+        if int(flags_host[j]):
+            base = (j % NS) * slot_rows
+            a, z = off[j], off[j + 1]
+            ea = torch.empty((z - a, 2), dtype=torch.int64, device=out_buf.device)
+            eb = torch.empty_like(ea)
+            local_sort_rows(slots[base: base + z - a], out_buf[a:z], ea, eb, 0, key_len,
+                            hi_bounds=fine_hi_bounds(plan.L, fb, w.rank * B + j))
+            fixups.append(j)
+
+    for i in range(B):
+        plan.pack(i)
+        if ev:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            tev["pack"].append(e)
+        if i >= NS:
+            check(i - NS)
+        base = (i % NS) * slot_rows
+        a, z = plan.st[i * W], plan.st[(i + 1) * W]
+        handles[i] = shuffle.alltoallv_bytes_async(
+            send_flat[a * rec: z * rec], [c * rec for c in send[i]],
+            slots.view(-1)[base * rec: (base + off[i + 1] - off[i]) * rec], [rc[s][i] * rec for s in range(W)], w)
+        # merges whose inputs and output rows are ready without waiting for round i, and the one
+        # whose slot round i + 1 needs (which may wait for round i)
+        while pending and (sched[pending[0]] <= i - 1 or pending[0] <= i + 1 - NS):
+            merge(pending.pop(0))
+    while pending:
+        merge(pending.pop(0))
+    for j in range(max(0, B - NS), B):
+        check(j)
+    report = dict(mode="rounds packed as they go out", slots=NS, slot_GB=round(NS * slot_rows * rec / 1e9, 3),
+                  merge_after=[k - j for j, k in enumerate(sched)], skew_fixups=fixups)
     if ev:
-        ev["done"].record()
-    if fine_rows and int(bad.item()):
-        raise RuntimeError("fine-bucket send side: an entry named a row past the table (corrupt entries)")
-    if stats is not None:
-        stats.n_in, stats.n_out, stats.rounds = n, n_recv, B
-        stats.send_counts = [sum(send[b][r] for b in range(B)) for r in range(W)]
-        stats.recv_counts = [sum(rc[s]) for s in range(W)]
-        stats.path = ("fine-bucket exchange, records generated into the send rows" if gen_path else
-                      f"fine-bucket exchange over the table (pitch {pitch})" if fine_rows else
-                      "E128 range partition + per-round radix sort")
-        stats.round_send_bytes = [(st[(b + 1) * W] - st[b * W] - send[b][w.rank]) * rec for b in range(B)]
-        stats.round_recv_bytes = [(off[b + 1] - off[b] - rc[w.rank][b]) * rec for b in range(B)]
-        stats.events = ev
-    return out[:n_recv]
+        ev["pack"] = tev["pack"]
+    del slots
+    return out_buf[: off[-1]], report
 
 
 def _fine_collapsed(seps_hi: list, fb: int) -> bool:
@@ -548,50 +761,72 @@ def e64_samples(e: torch.Tensor, n: int, rank: int, sample_target: int, seed: in
     return samp
 
 
-def send_fine_rows(bufs: SortBuffers, rows: torch.Tensor, e: torch.Tensor, tmp: torch.Tensor, hist, n: int,
-                   seps_hi: list, B: int, W: int, fb: int, rebuild=None):
+class FineSend:
     """Send side of the fine-bucket exchange over a materialised table (``rows``: [n, 100] at a
     100- or 128-byte pitch): one look-back sort of the rows' E64 entries ``e`` (window = key bytes
     0..3, with the producer's / extraction's histograms ``hist``) on the top 8 * ceil(fb / 8) key
-    bits, the fine-bucket starts of the sorted order, then ONE gather of the rows into the
-    round-major send buffer ``bufs.rows_out`` (round b = key range r * B + b for every
-    destination r, each piece in fine-bucket order; ts_pack_rows: 16-byte loads, one HBM line per
-    row at pitch 128).  The pack runs to completion before the exchange: the receive buffer is
-    the table's own memory.  A failed look-back sort (``err``) keeps the pack from reading and
-    is redone with count + scatter passes over ``rebuild()``'s entries.  Returns (send-row starts
-    st[b * W + r], per-bucket row counts (device int32 [2^fb]), fine bounds L)."""
-    err = S.lookback_error()
-    win = 8 * ((fb + 7) // 8)
-    srt = S.sort_entries64(e, tmp, win, gen_hist=hist, err=err)
-    starts = TSG.fine_starts(srt, fb)
-    L = fine_bounds(seps_hi, fb)
-    Lt = torch.tensor(L, dtype=torch.int64, device=e.device)
-    host = torch.cat([starts.index_select(0, Lt).to(torch.int64), err.to(torch.int64)]).tolist()
-    Sg = host[:-1]
-    if host[-1]:                  # the look-back sort gave up: entries again, count + scatter passes
-        e2 = rebuild() if rebuild is not None else e
-        srt = S.sort_entries64(e2, tmp if e2.data_ptr() == e.data_ptr() else e, win, lookback=False)
+    bits, the fine-bucket starts of the sorted order, the send-row starts ``st[b * W + r]`` of the
+    round-major send buffer ``bufs.rows_out`` (round b = key range r * B + b for every destination
+    r, each piece in fine-bucket order), the per-bucket row counts ``counts`` (device int32 [2^fb])
+    and the fine bounds ``L``.  ``pack(b)`` gathers round b's rows from the table into the send
+    buffer (ts_pack_rows: 16-byte loads, one HBM line per row at pitch 128), so the exchange can
+    send round b while later rounds are still being packed.  A failed look-back sort is redone
+    with count + scatter passes over ``rebuild()``'s entries before anything is packed."""
+
+    def __init__(self, bufs: SortBuffers, rows: torch.Tensor, e: torch.Tensor, tmp: torch.Tensor, hist, n: int,
+                 seps_hi: list, B: int, W: int, fb: int, rebuild=None):
+        err = S.lookback_error()
+        win = 8 * ((fb + 7) // 8)
+        srt = S.sort_entries64(e, tmp, win, gen_hist=hist, err=err)
         starts = TSG.fine_starts(srt, fb)
-        Sg = starts.index_select(0, Lt).tolist()
-        err = None
-    counts = starts[1:] - starts[:-1]
-    st, acc = [], 0
+        L = fine_bounds(seps_hi, fb)
+        Lt = torch.tensor(L, dtype=torch.int64, device=e.device)
+        host = torch.cat([starts.index_select(0, Lt).to(torch.int64), err.to(torch.int64)]).tolist()
+        Sg = host[:-1]
+        if host[-1]:              # the look-back sort gave up: entries again, count + scatter passes
+            e2 = rebuild() if rebuild is not None else e
+            srt = S.sort_entries64(e2, tmp if e2.data_ptr() == e.data_ptr() else e, win, lookback=False)
+            starts = TSG.fine_starts(srt, fb)
+            Sg = starts.index_select(0, Lt).tolist()
+            err = None
+        self.counts = starts[1:] - starts[:-1]
+        st, acc = [], 0
+        for b in range(B):
+            for r in range(W):
+                st.append(acc)
+                acc += Sg[r * B + b + 1] - Sg[r * B + b]
+        st.append(acc)
+        if srt.data_ptr() == bufs.rows_out.data_ptr():
+            # (an even pass count left the entries in rows_out, which the pack writes: move them)
+            e64 = bufs.ent_a.view(-1)[:n] if bufs.ent_a.data_ptr() != srt.data_ptr() else None
+            if e64 is None or e64.numel() < n:
+                raise RuntimeError("send_fine_rows: no room for the sorted entries outside the send buffer")
+            e64.copy_(srt)
+            srt = e64
+        # per round: W segments {send row relative to the round's start, first sorted entry}
+        self.segs = torch.tensor([[st[b * W + r] - st[b * W], Sg[r * B + b]] for b in range(B) for r in range(W)],
+                                 dtype=torch.int64).to(e.device)
+        self.bufs, self.rows, self.srt, self.err = bufs, rows, srt, err
+        self.st, self.L, self.Sg, self.B, self.W = st, L, Sg, B, W
+        self.bad = torch.zeros(1, dtype=torch.int32, device=e.device)
+
+    def pack(self, b: int) -> None:
+        """Round b's send rows: out[st[b * W]: st[(b + 1) * W]] gathered from the table."""
+        W = self.W
+        a, z = self.st[b * W], self.st[(b + 1) * W]
+        if z > a:
+            TSG.pack_rows(self.bufs.rows_out[a:z], self.rows, self.srt, z - a, seg=self.segs[b * W: (b + 1) * W],
+                          err=self.err, bad=self.bad)
+
+
+def send_fine_rows(bufs: SortBuffers, rows: torch.Tensor, e: torch.Tensor, tmp: torch.Tensor, hist, n: int,
+                   seps_hi: list, B: int, W: int, fb: int, rebuild=None):
+    """The whole send side at once (FineSend, then every round packed): (send-row starts
+    st[b * W + r], per-bucket row counts, fine bounds L, the pack's bad-entry flag)."""
+    plan = FineSend(bufs, rows, e, tmp, hist, n, seps_hi, B, W, fb, rebuild=rebuild)
     for b in range(B):
-        for r in range(W):
-            st.append(acc)
-            acc += Sg[r * B + b + 1] - Sg[r * B + b]
-    st.append(acc)
-    if srt.data_ptr() == bufs.rows_out.data_ptr():
-        # (an even pass count left the entries in rows_out, which the pack writes: move them)
-        e64 = bufs.ent_a.view(-1)[:n] if bufs.ent_a.data_ptr() != srt.data_ptr() else None
-        if e64 is None or e64.numel() < n:
-            raise RuntimeError("send_fine_rows: no room for the sorted entries outside the send buffer")
-        e64.copy_(srt)
-        srt = e64
-    segs = torch.tensor([[st[b * W + r], Sg[r * B + b]] for b in range(B) for r in range(W)],
-                        dtype=torch.int64).to(e.device)
-    bad = TSG.pack_rows(bufs.rows_out, rows, srt, acc, seg=segs, err=err)
-    return st, counts, L, bad
+        plan.pack(b)
+    return plan.st, plan.counts, plan.L, plan.bad
 
 
 # Fine buckets of the gen:// exchange: the top ``fb`` key bits, about FINE_ROWS rows of the whole
@@ -694,50 +929,65 @@ def exchange_fine_counts(counts: torch.Tensor, L: list, B: int, W: int, world: W
     return recv.view(W, K)
 
 
+class FineMerge:
+    """Receive side of the fine-bucket exchange, one round at a time.  ``fine[s, k]`` = rows of
+    bucket L[rank * B] + k from source s; a received round b (key range g = rank * B + b) is W
+    source pieces in source order, each in bucket order.  ``merge(b, recv, base, a, z)``: the
+    round's rows are ``recv[base: base + z - a]``; the slices of every bucket are located on the
+    device (prefix sums of ``fine``) and ts_tile_merge orders each bucket in LDS into
+    ``out[a:z]``.  A bucket too large for LDS (heavy key skew) sets ``flags[b]``."""
+
+    def __init__(self, fine: torch.Tensor, L: list, fb: int, B: int, rank: int, out: torch.Tensor):
+        self.W, self.K = fine.shape
+        self.L, self.fb, self.B, self.rank, self.out = L, fb, B, rank, out
+        self.flags = torch.zeros(B, dtype=torch.int32, device=out.device)
+        self.base = L[rank * B]
+        # slice starts of every bucket from one flat scan of all sources' counts (a 1-D device
+        # scan; per round only elementwise differences): ex[s, k] = rows of source s before bucket k
+        fine = fine.contiguous()
+        ex = (torch.cumsum(fine.view(-1), 0, dtype=torch.int64).view(self.W, self.K) - fine)
+        self.ex = ex - ex[:, :1]
+        col = fine.sum(0, dtype=torch.int64)
+        self.cex = torch.cumsum(col, 0) - col
+        self.fine = fine
+
+    def merge(self, b: int, recv: torch.Tensor, base: int, a: int, z: int) -> None:
+        if z <= a:
+            return
+        g = self.rank * self.B + b
+        k0, k1 = self.L[g] - self.base, self.L[g + 1] - self.base
+        ex, fine, K = self.ex, self.fine, self.K
+        cnt = fine[:, k0:k1]
+        exr = ex[:, k0:k1] - ex[:, k0:k0 + 1]                       # within the range
+        rows_per_src = (ex[:, k1:k1 + 1] if k1 < K else (ex[:, -1:] + fine[:, -1:])) - ex[:, k0:k0 + 1]
+        pre = (exr + (torch.cumsum(rows_per_src, 0) - rows_per_src) + base).contiguous()
+        outoff = (self.cex[k0:k1] - self.cex[k0] + a).contiguous()
+        TSG.tile_merge(recv, self.out, pre, cnt.contiguous(), outoff, self.fb, self.flags[b:b + 1])
+
+
 def merge_received_rounds(bufs: SortBuffers, off: list, fine: torch.Tensor, L: list, fb: int, B: int, rank: int,
                           sent_after: list, n_sent: int, wait=None, key_len: int = 10) -> torch.Tensor:
-    """Receive side of the fine-bucket exchange: round b's block ``rows_in[off[b]:off[b+1]]`` holds
-    key range g = rank * B + b as W source pieces (source order), each in bucket order, and
-    ``fine[s, k]`` = rows of bucket L[rank * B] + k from source s.  Per round (``wait(b)``) the
-    slices of every bucket are located on the device (prefix sums of ``fine``) and ts_tile_merge
-    orders each bucket in LDS into ``rows_out[off[b]:...]``, deferred until the send rows under it
-    have gone out (``sent_after``, as in sort_received_rounds).  A bucket too large for LDS (heavy
-    key skew) flags its round, which is then sorted after the last round with local_sort_rows."""
+    """Receive side of the fine-bucket exchange when every round lands in place: round b's block
+    ``rows_in[off[b]:off[b+1]]`` (FineMerge) is ordered into ``rows_out[off[b]:...]``, deferred
+    until the send rows under it have gone out (``sent_after``, as in sort_received_rounds).  A
+    round whose bucket outgrew LDS is sorted after the last round with local_sort_rows."""
     out = bufs.rows_out
     recv = bufs.recv_rows()
-    W, Kme = fine.shape
-    flags = torch.zeros(B, dtype=torch.int32, device=out.device)
-    base = L[rank * B]
-    # slice starts of every bucket from one flat scan of all sources' counts (a 1-D device scan;
-    # per round only elementwise differences): ex[s, k] = rows of source s before bucket k
-    fine = fine.contiguous()
-    ex = (torch.cumsum(fine.view(-1), 0, dtype=torch.int64).view(W, Kme) - fine)
-    ex = ex - ex[:, :1]
-    col = fine.sum(0, dtype=torch.int64)
-    cex = torch.cumsum(col, 0) - col
+    m = FineMerge(fine, L, fb, B, rank, out)
     pending = []
     for b in range(B):
         if wait is not None:
             wait(b)
-        a, z = off[b], off[b + 1]
-        if z > a:
-            g = rank * B + b
-            k0, k1 = L[g] - base, L[g + 1] - base
-            cnt = fine[:, k0:k1]
-            exr = ex[:, k0:k1] - ex[:, k0:k0 + 1]                       # within the range
-            rows_per_src = (ex[:, k1:k1 + 1] if k1 < Kme else (ex[:, -1:] + fine[:, -1:])) - ex[:, k0:k0 + 1]
-            pre = (exr + (torch.cumsum(rows_per_src, 0) - rows_per_src) + a).contiguous()
-            outoff = (cex[k0:k1] - cex[k0] + a).contiguous()
-            pending.append((a, z, b, pre, cnt.contiguous(), outoff))
+        pending.append(b)
         keep = []
-        for item in pending:
-            a2, z2, b2, pre, cnt, outoff = item
+        for b2 in pending:
+            a2, z2 = off[b2], off[b2 + 1]
             if b == B - 1 or z2 <= sent_after[b] or a2 >= n_sent:
-                TSG.tile_merge(recv, out, pre, cnt, outoff, fb, flags[b2:b2 + 1])
+                m.merge(b2, recv, a2, a2, z2)
             else:
-                keep.append(item)
+                keep.append(b2)
         pending = keep
-    fl = flags.tolist()
+    fl = m.flags.tolist()
     for b in range(B):
         if fl[b]:
             a, z = off[b], off[b + 1]

@@ -50,8 +50,9 @@ log = get_logger("grace_stage")
 
 CHUNK_ROWS = 1 << 26
 _I64 = torch.int64
-# longest string a packed join row carries inline (a longer one fails the stage, non-retryable)
-MAX_INLINE_STRING_BYTES = 1 << 16
+# widest packed join row the grace partitioner takes (dr_grace_partition: kMaxStride bytes); a
+# row of longer strings is not packed: the stage is not chosen (vote) or fails non-retryably
+MAX_ROW_BYTES = 512
 
 
 class StreamedPart:
@@ -611,7 +612,27 @@ def vote(desc, runner):
         if 3 * max(v[0] for v in vals) <= budget:
             return None
     lens = [v[1] for v in vals]
-    return dict(lay, max_str=-1 if min(lens) < 0 else max(lens))
+    out = dict(lay, max_str=-1 if min(lens) < 0 else max(lens))
+    if row_bytes(out, runner, desc) > MAX_ROW_BYTES:
+        log.info("join %s: no grace stage (strings of %d bytes make rows past %d bytes)", desc["join"],
+                 out["max_str"], MAX_ROW_BYTES)
+        return None
+    return out
+
+
+def row_bytes(lay, runner, desc) -> int:
+    """Bytes of a packed join row for the voted layout (the widest side's: key word, fields,
+    strings of ``max(GraceJoinStringBytes, max_str)`` bytes inline)."""
+    s_bytes = max(int(runner.ctx._props.get("GraceJoinStringBytes") or 64), int(lay.get("max_str") or 0))
+    S = -(-s_bytes // 8)
+    me = runner.world.rank
+    P = runner.plan.stages[desc["join"]].partitions
+    part = next((p for p in range(P) if runner.owner(p) == me), 0)
+    words = []
+    for r, used in zip(desc["reads"], (lay["uo"], lay["ui"])):
+        side = _side(r, part)
+        words.append(1 + sum(side.field_words(f, S) for f in used) if side is not None else 1)
+    return 8 * max(words)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -696,11 +717,11 @@ def run(desc, runner, lay) -> dict:
                 break
             grace.release()
             grace = None
-            if need > MAX_INLINE_STRING_BYTES:
-                from ..errors import GangAgreementError
-                raise GangAgreementError(f"grace join: a {need}-byte string field is longer than the "
-                                         f"{MAX_INLINE_STRING_BYTES}-byte row limit", retryable=False)
             s_bytes = -(-need // 64) * 64
+            if 8 * layout(-(-s_bytes // 8))[0] > MAX_ROW_BYTES:
+                from ..errors import GangAgreementError
+                raise GangAgreementError(f"grace join: a {need}-byte string field makes the packed rows wider "
+                                         f"than {MAX_ROW_BYTES} bytes", retryable=False)
             widened += 1
             log.info("grace join %s: string of %d bytes, pass A again with %d inline bytes", desc["join"], need, s_bytes)
         grace.finish_partitioning()

@@ -60,6 +60,8 @@ def main():
         want = "records generated into the send rows" if gen_fused else "fine-bucket exchange over the table"
         assert ex is not None and want in ex["path"], ex
         assert ex["rounds"] == len(ex["round_send_MB"]) and ex["send_GB"] > 0, ex
+        if not gen_fused:     # the table's send side overlapped with the exchange, round by round
+            assert "rounds packed as they go out" in ex["path"] and "first_round_queued_ms" in ex, ex
     # 2. an hbm:// table (a previous job's output) read in place, and a stored partfile of rows
     g = D.DryadLinqContext(platform="gpu")
     g.PartitionCount = w.size

@@ -75,6 +75,10 @@ def main():
         assert out.shape[0] == n and int(acc[1]) == 0 and int(acc[0]) == int(acc_in[0]), (acc.tolist(), acc_in.tolist())
         rep = st.exchange_report()
         assert rep["rounds"] == 4 and "round_arrival_ms" in rep, rep
+        # the send side overlapped with the exchange: each round packed just before it went out,
+        # received into slots, merged from there
+        assert "rounds packed as they go out" in st.path and "first_round_queued_ms" in rep, rep
+        assert rep["overlap"]["slots"] == RS.OVERLAP_SLOTS and not rep["overlap"]["skew_fixups"], rep
         # 3. the E128 range-partition path, descending
         st2 = RS.SortStats()
         out2 = RS.distributed_sort_rows(bufs, n, 0, 10, w, stats=st2, src=src, descending=True)

@@ -23,3 +23,30 @@ def test_fine_bounds_cut_separators_to_bucket_edges():
     lo, hi = RS.fine_hi_bounds(L, fb, 1)
     assert lo == 1 << 63 and hi == ((3 << 18) + 1 << 44) - 1
     assert RS.fine_hi_bounds(L, fb, 2)[1] == (1 << 64) - 1
+
+
+def test_overlap_schedule_merges_once_the_rows_under_the_output_are_sent():
+    """overlap_schedule: round j's merge waits for its own arrival and for the payload round that
+    sends the last send rows under out[off[j]:off[j+1]]; a round that would hold its receive slot
+    longer than the slots allow makes the exchange fall back (None)."""
+    W, B = 2, 4
+    # send-row starts st[b * W + r]: 100 rows per round
+    st = [0, 50, 100, 150, 200, 250, 300, 350, 400]
+    # balanced receive: every merge waits only for its own round
+    assert RS.overlap_schedule(st, [0, 100, 200, 300, 400], B, W, 400, 3) == [0, 1, 2, 3]
+    # round 0 receives 130 rows: its output reaches into round 1's send rows
+    assert RS.overlap_schedule(st, [0, 130, 200, 300, 400], B, W, 400, 3) == [1, 1, 2, 3]
+    # rows past the sent ones never held data (n_sent), and with separate output buffers
+    # (n_sent = 0) nothing overlays the send rows
+    assert RS.overlap_schedule(st, [0, 130, 200, 300, 420], B, W, 400, 3) == [1, 1, 2, 3]
+    assert RS.overlap_schedule(st, [0, 330, 340, 350, 360], B, W, 0, 3) == [0, 1, 2, 3]
+    # round 0's output reaches round 3's rows: 3 rounds of lag do not fit 3 slots
+    assert RS.overlap_schedule(st, [0, 330, 340, 350, 400], B, W, 400, 3) is None
+    assert RS.overlap_schedule(st, [0, 330, 340, 350, 400], B, W, 400, 4) == [3, 3, 3, 3]
+
+
+def test_fine_subs_targets_one_gib_rounds():
+    assert RS.fine_subs(125 * 10**9, 8) == 128
+    assert RS.fine_subs(125 * 10**9, 1) == 128
+    assert RS.fine_subs(10**6, 2) == 4
+    assert RS.fine_subs(10**15, 8) == 256           # world * rounds <= 2048
