@@ -124,10 +124,13 @@ _DEFAULTS = dict(
     #                               (runtime/stream_agg.py; None: when a partition exceeds HbmBudgetBytes)
     StreamDenseState=True,        # ... a streamed GroupBy of one integer key keeps its running state
     #                               directly addressed by key while the keys' range fits the budget
+    StreamShuffle=None,           # multi-partition GroupBy / Distinct: partial side, exchange and final
+    #                               side as pipelined rounds with bounded channels (runtime/
+    #                               stream_shuffle.py; None: when a source partition exceeds the budget)
     GraceJoin=None,               # a Join as the partitioned grace join stage (runtime/grace_stage.py;
     #                               None: when its inputs would crowd the HBM budget; False: never)
-    GraceJoinStringBytes=64,      # ... inline bytes per string field in its packed bucket rows (longer
-    #                               strings: a voted GangAgreementError)
+    GraceJoinStringBytes=64,      # ... inline bytes per string field in its packed bucket rows, at least
+    #                               (longer strings widen the rows; past 512-byte rows the compiled join runs)
     LineAlignedSortInput=True,   # GPU executor: a table of 100-byte rows that only an OrderBy reads is
     #                               stored at a 128-byte pitch (one HBM line per record gather)
     GenFusedShuffle=False,        # multi-rank OrderBy over gen://terasort: generate the records straight

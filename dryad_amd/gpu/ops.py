@@ -275,7 +275,10 @@ def op_read(op, inputs, v):
     if scheme == "host":
         from ..io.hosttable import HostRows
         from ..ops.extsort import _copy
+        from ..io.hosttable import HostColumns
         b = provider_for(uri).get(uri)["local"].get(v.partition)
+        if isinstance(b, HostColumns):
+            return b.to_device(v.device)                # pinned host columns -> HBM
         if isinstance(b, HostRows):
             # pinned host tier -> HBM (one DMA; a following OrderBy sorts the pooled rows in place)
             rows = v.alloc_rows(b.n, b.stride)

@@ -153,3 +153,78 @@ class TieredRows:
 
     def __len__(self):
         return self.n
+
+
+class HostColumns:
+    """A columnar table (fixed-width columns, no string heaps) in page-locked host DRAM, built piece
+    by piece: the ``host://`` result of a streamed stage whose output outgrows HBM
+    (runtime/sinks.HostSink; a streamed Distinct / GroupBy result, runtime/stream_agg.py).  Each
+    piece is one device table's columns copied out by DMA into leased pinned buffers
+    (ops/_lib.pinned_lease: exact-size, reused across jobs).  Read back whole (``to_device``),
+    piece by piece (``device_pieces``, the chunk source of a later streamed stage) or as records."""
+
+    def __init__(self, shape):
+        self.shape = shape
+        self.pieces = []               # [(n, {column: pinned tensor [n, ...]}, [leases])]
+        self.n = 0
+
+    def append(self, t) -> None:
+        from ..ops._lib import pinned_lease
+        if t.rows is not None or t.heap is not None or t.strs:
+            raise ValueError("HostColumns holds fixed-width columnar tables")
+        if t.n == 0:
+            return
+        cols, leases = {}, []
+        for k, v in t.cols.items():
+            src = v[: t.n]
+            if not src.is_cuda:                 # a CPU run: plain host memory
+                cols[k] = src.clone()
+                continue
+            ls = pinned_lease(tuple(src.shape), src.dtype)
+            ls.tensor.copy_(src, non_blocking=True)
+            cols[k] = ls.tensor
+            leases.append(ls)
+        self.pieces.append((t.n, cols, leases))
+        self.n += t.n
+
+    @property
+    def nbytes(self) -> int:
+        return sum(v.numel() * v.element_size() for _, cols, _ in self.pieces for v in cols.values())
+
+    def columns(self) -> list:
+        return list(self.pieces[0][1]) if self.pieces else list(self.shape.fields)
+
+    def device_pieces(self, device, max_rows: int | None = None):
+        """Yield the table as device tables of at most ``max_rows`` rows, in row order."""
+        from ..gpu.table import DeviceTable
+        for n, cols, _ in self.pieces:
+            step = n if not max_rows else max(1, int(max_rows))
+            for a in range(0, n, step):
+                b = min(n, a + step)
+                yield DeviceTable(b - a, self.shape, {k: v[a:b].to(device, non_blocking=True) for k, v in cols.items()})
+
+    def to_device(self, device):
+        from ..gpu.table import DeviceTable
+        if not self.pieces:
+            return DeviceTable(0, self.shape, {})
+        names = self.columns()
+        return DeviceTable(self.n, self.shape, {k: torch.cat([c[k] for _, c, _ in self.pieces]).to(device)
+                                                for k in names})
+
+    def to_objects(self) -> list:
+        from ..gpu.table import DeviceTable
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()            # the pieces' DMAs are complete
+        out = []
+        for n, cols, _ in self.pieces:
+            out += DeviceTable(n, self.shape, dict(cols)).to_objects()
+        return out
+
+    def release(self):
+        for _, _, leases in self.pieces:
+            for ls in leases:
+                ls.release()
+        self.pieces, self.n = [], 0
+
+    def __len__(self):
+        return self.n

@@ -230,27 +230,81 @@ def _set_received_bounds(have: list, colspecs, out_cols: dict, offset_cols: set)
 def exchange(world: World, sends: list, stats: ExchangeStats | None = None) -> list:
     """``sends[r]``: DeviceTables (pieces) for rank r, in order.  Returns ``recv[s]``: the pieces
     rank s sent to this rank, in its order.  Collective: every rank calls it with W send lists.
-    Raises SchemaMismatch (on every rank) when the ranks' tables are structurally different.
+    Raises SchemaMismatch (on every rank) when the ranks' tables are structurally different."""
+    return exchange_start(world, sends, stats).finish()
 
-    The manifest is two tensor collectives (``_manifest``); the payload columns are queued as
-    asynchronous all-to-all-v collectives back to back (RCCL runs them in order on its stream
-    while the host prepares the next) and waited for together; a partition's received pieces are
-    adjacent slices of one buffer per column (DeviceTable.concat takes them as one view)."""
+
+def _structure(world: World, have_rank: int, proto):
+    """The table structure from rank ``have_rank`` (the first rank holding a piece), for ranks
+    that hold none: its repr-free pickle broadcast as one uint8 tensor (length, then bytes) -- no
+    object collective."""
+    import pickle
+    dev = world.device if world.backend == "nccl" else torch.device("cpu")
+    me = world.rank
+    blob = pickle.dumps(signature(proto)[0]) if me == have_rank else b""
+    ln = torch.tensor([len(blob)], dtype=torch.int64, device=dev)
+    dist.broadcast(ln, src=have_rank)
+    buf = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev) if me == have_rank else \
+        torch.empty(int(ln.item()), dtype=torch.uint8, device=dev)
+    dist.broadcast(buf, src=have_rank)
+    return pickle.loads(buf.cpu().numpy().tobytes())     # this framework's own structure tuple
+
+
+class PendingExchange:
+    """An exchange whose payload collectives are queued (asynchronous all-to-all-v per column and
+    per string heap) but not yet waited for; ``finish()`` makes the caller's stream wait and
+    returns the received pieces.  The send buffers stay referenced until then."""
+
+    def __init__(self, W, recv_pieces, big_args, handles, strs, keep):
+        self.W, self.recv_pieces, self.big_args = W, recv_pieces, big_args
+        self.handles, self.strs, self.keep = handles, strs, keep
+
+    def finish(self) -> list:
+        if self.big_args is None:
+            return [[] for _ in range(self.W)]
+        for h in self.handles:
+            shuffle.wait(h)
+        total_r, shape, out_cols, heaps, have, colspecs, offset_cols = self.big_args
+        for oc, lc, hk, recv in self.strs:         # offsets rebuilt from the received lengths
+            ln = out_cols[lc].to(torch.int64)
+            out_cols[oc] = (torch.cumsum(ln, 0) - ln).to(out_cols[oc])
+            heaps[hk] = recv
+        _set_received_bounds(have, colspecs, out_cols, offset_cols)
+        if "__rows__" in out_cols:
+            big = DeviceTable(total_r, shape, rows=out_cols["__rows__"])
+        else:
+            big = DeviceTable(total_r, shape, out_cols, heap=heaps.get(None),
+                              strs={k: v for k, v in heaps.items() if k is not None})
+        res, a = [], 0
+        for s in range(self.W):
+            lst = []
+            for n, _ in self.recv_pieces[s]:
+                lst.append(big.slice(a, a + n))
+                a += n
+            res.append(lst)
+        self.keep = None
+        return res
+
+
+def exchange_start(world: World, sends: list, stats: ExchangeStats | None = None) -> PendingExchange:
+    """Queue an exchange (see ``exchange``).  The manifest is two tensor collectives
+    (``_manifest``); the payload columns and string heaps are queued as asynchronous all-to-all-v
+    collectives back to back (RCCL runs them in order on its stream while the host prepares the
+    next, and while the caller computes); a partition's received pieces are adjacent slices of one
+    buffer per column (DeviceTable.concat takes them as one view)."""
     W, me = world.size, world.rank
     assert len(sends) == W
     proto = next((p for lst in sends for p in lst if p is not None), None)
     heads, recv_pieces = _manifest(world, sends, proto)
     have = [h for h in heads if h[0]]
     if not have:                      # nobody holds a piece
-        return [[] for _ in range(W)]
+        return PendingExchange(W, recv_pieces, None, [], [], None)
     if len({h[1] for h in have}) != 1 or len({h[2] for h in have}) != 1:
         raise SchemaMismatch("ranks hold different table structures")
     if len(have) < W:
-        # a rank without source pieces learns the structure from the others (rare: fewer source
-        # partitions than ranks); every rank sees the same headers, so all take this branch
-        objs = [None] * W
-        dist.all_gather_object(objs, signature(proto)[0] if proto is not None else None)
-        struct = next(o for o in objs if o is not None)
+        # a rank without source pieces learns the structure from the first rank that has one (rare:
+        # fewer source partitions than ranks); every rank sees the same headers, so all take this branch
+        struct = _structure(world, next(r for r, h in enumerate(heads) if h[0]), proto)
     else:
         struct = signature(proto)[0]
     kind, fields, pytype, key_off, key_len, colspecs, strspecs = struct
@@ -267,7 +321,7 @@ def exchange(world: World, sends: list, stats: ExchangeStats | None = None) -> l
     total_r = sum(recv_rows)
     out_cols = {name: None for name, _ in colspecs}
     offset_cols = {oc for oc, _, _ in strspecs}        # rebuilt from the lengths on arrival
-    handles = []
+    handles, keep = [], []
     for (name, tail), dt in zip(colspecs, dtypes):
         if name in offset_cols:
             out_cols[name] = dt
@@ -282,14 +336,13 @@ def exchange(world: World, sends: list, stats: ExchangeStats | None = None) -> l
         recv = torch.empty(total_r * per, dtype=torch.uint8, device=dev)
         handles.append(shuffle.alltoallv_bytes_async(send, [c * per for c in send_rows], recv,
                                                      [c * per for c in recv_rows], world))
+        keep.append(send)
         out_cols[name] = recv.view(dt).view((total_r,) + tuple(tail))
         if stats is not None:
             stats.bytes_sent += sum(send_rows) * per
             stats.bytes_received += total_r * per
             stats.collectives += 1
-    for h in handles:
-        shuffle.wait(h)
-    heaps = {}
+    heaps, strs = {}, []
     for j, (oc, lc, hk) in enumerate(strspecs):
         parts, send_b = [], []
         for lst in sends:
@@ -306,25 +359,12 @@ def exchange(world: World, sends: list, stats: ExchangeStats | None = None) -> l
         send = torch.cat(parts) if len(parts) > 1 else (parts[0] if parts else torch.empty(0, dtype=torch.uint8,
                                                                                                 device=dev))
         recv = torch.empty(sum(recv_b), dtype=torch.uint8, device=dev)
-        shuffle.alltoallv_bytes(send, send_b, recv, recv_b, world)
-        ln = out_cols[lc].to(torch.int64)
-        out_cols[oc] = (torch.cumsum(ln, 0) - ln).to(out_cols[oc])
-        heaps[hk] = recv
+        handles.append(shuffle.alltoallv_bytes_async(send, send_b, recv, recv_b, world))
+        keep.append(send)
+        strs.append((oc, lc, hk, recv))
         if stats is not None:
             stats.bytes_sent += sum(send_b)
             stats.bytes_received += recv.numel()
             stats.collectives += 1
-    _set_received_bounds(have, colspecs, out_cols, offset_cols)
-    if "__rows__" in out_cols:
-        big = DeviceTable(total_r, shape, rows=out_cols["__rows__"])
-    else:
-        big = DeviceTable(total_r, shape, out_cols, heap=heaps.get(None),
-                          strs={k: v for k, v in heaps.items() if k is not None})
-    res, a = [], 0
-    for s in range(W):
-        lst = []
-        for n, _ in recv_pieces[s]:
-            lst.append(big.slice(a, a + n))
-            a += n
-        res.append(lst)
-    return res
+    return PendingExchange(W, recv_pieces, (total_r, shape, out_cols, heaps, have, colspecs, offset_cols),
+                           handles, strs, keep)

@@ -38,6 +38,7 @@ from ..ops import extsort as EX
 from ..io.providers import parse_uri, provider_for
 from . import checkpoint as CK
 from . import stream_agg as SA
+from . import stream_shuffle as SSH
 from ..native import runtime as native_runtime
 from ..parallel import shuffle
 from ..parallel.comm import World, get_world, init_world
@@ -1081,6 +1082,8 @@ class GpuJobRunner:
         self.fused_joins = FJ.find(self.plan) if self.gpu_ok else {}
         self.grace_joins = GS.find(self.plan) if self.gpu_ok else {}
         join_first = {min(d["stages"]): jid for jid, d in list(self.fused_joins.items()) + list(self.grace_joins.items())}
+        self.stream_shuffles = SSH.find(self.plan) if self.gpu_ok else {}
+        shuffle_first = {d["a"]: bid for bid, d in self.stream_shuffles.items()}
         precomputed = {}
         stage_events = []          # (timing key, host seconds, start event, end event)
         t_stages = time.time()
@@ -1111,6 +1114,18 @@ class GpuJobRunner:
                     self.precomputed_bodies[jid] = (body, rest)
                     self.skipped.update((self.fused_joins.get(jid) or self.grace_joins[jid])["stages"])
                     self.timings[f"{jid}:Join({how})"] = time.time() - t0
+            if s.id in shuffle_first:
+                bid = shuffle_first[s.id]
+                desc = self.stream_shuffles[bid]
+                lay = SSH.vote(desc, self)
+                if lay is not None:
+                    body = (lambda d=desc, ly=lay: SSH.run(d, self, ly))
+                    out = self._attempt_stage(self.plan.stages[bid], body)
+                    if out is not None:
+                        precomputed[bid] = (out, [])
+                        self.precomputed_bodies[bid] = (body, [])
+                        self.skipped.update(desc["stages"])
+                        self.timings[f"{bid}:{self.plan.stages[bid].name}(streamed shuffle)"] = time.time() - t0
             if s.id in precomputed:
                 refresh()
                 outs, rest = precomputed.pop(s.id)
@@ -1631,9 +1646,10 @@ class GpuJobRunner:
                                             "pins": pins, "pool": self.pool})
                 committed[uri] = s.partitions
             elif scheme == "host":
+                from ..io.hosttable import HostColumns
                 tabs = {}
                 for p, v in local.items():
-                    if isinstance(v, HostRows):
+                    if isinstance(v, (HostRows, HostColumns)):        # streamed into the host tier
                         tabs[p] = v
                     elif isinstance(v, DeviceTable) and v.rows is not None and v.device.type == "cuda":
                         tabs[p] = HostRows.from_tensor(v.rows, v.shape.key_off, v.shape.key_len)

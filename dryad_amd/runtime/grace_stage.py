@@ -773,92 +773,39 @@ def run(desc, runner, lay) -> dict:
 
 class _Sink:
     """Where the buckets' results go: folded (decomposable aggregate), appended to the output part
-    file (partfile:// output, first local partition), or concatenated."""
+    file(s) through runtime/sinks.PartfileSink (partfile:// output, first local partition), or
+    concatenated."""
 
     def __init__(self, runner, stage, parts, desc):
         self.runner, self.stage, self.parts, self.desc = runner, stage, parts, desc
         self.agg = desc["agg"]
         self.chunks, self.partials = [], []
-        self.writer, self.dtype, self.n, self.written = None, None, 0, 0
-        self.written_bytes, self.index = 0, []          # (string records) block index of the stream
-        self.stream = False
-        self.paths, self.fbytes = None, None            # a split output: its part files and their sizes
-        self.frecs, self.findex = None, None            # ... their record counts and block indexes
-        self.split = int(runner.ctx.PartFileSplitBytes or 0) > 0
+        self.written = 0
+        self.pf = None
         if stage.is_output and not self.agg and not desc["after"]:
-            scheme, path, _ = parse_uri(stage.output["uri"])
-            self.stream = scheme in ("partfile", "file") and runner.ctx.OutputDataCompressionScheme.value == 0
-            if self.stream:
-                from ..io import partfile as PF
-                base = PF.default_base(path)
-                os.makedirs(os.path.dirname(base) or ".", exist_ok=True)
-                self.tmp = f"{base}.{parts[0]:08X}---{runner.vids[stage.id][parts[0]]}_0_stream.tmp"
+            from .sinks import PartfileSink
+            if PartfileSink.applicable(runner, stage):
+                self.pf = PartfileSink(runner, stage, parts[0])
 
     def add(self, data):
         if self.agg:
             self.partials.append(data)
             return
-        if self.stream and isinstance(data, DeviceTable):
-            from ..ops import codec as CD
-            if self.dtype is None:
-                self.dtype = _table_dtype(data)
-            enc = CD.encode(data, self.dtype) if self.dtype is not None else None
-            offs = None
-            if enc is None and self.dtype is not None and CD.var_layout(self.dtype) is not None:
-                got = CD.encode_var(data, self.dtype, full_offsets=True)
-                if got is not None:
-                    enc, offs = got
-            if enc is not None:
-                B = CD.BLOCK
-                if self.writer is None:
-                    from ..io.writer import SPLIT_MAX, PartWriter
-                    if self.split:
-                        # PartFileSplitBytes: the buckets' results go to SPLIT_MAX part files at
-                        # once (page-cache writes serialise per inode); string records keep one
-                        # block index per file
-                        self.paths = [f"{self.tmp}.{j}" for j in range(SPLIT_MAX)]
-                        self.fbytes, self.frecs = [0] * SPLIT_MAX, [0] * SPLIT_MAX
-                        self.findex = [[] for _ in range(SPLIT_MAX)]
-                        self.writer = PartWriter(self.paths, data.device, self.runner.write_stats)
-                    else:
-                        self.writer = PartWriter(self.tmp, data.device, self.runner.write_stats)
-                if self.paths is not None:
-                    j = min(range(len(self.fbytes)), key=self.fbytes.__getitem__)
-                    if offs is not None:          # block index of file j: its records n, n + B, ...
-                        j0 = (-self.frecs[j]) % B
-                        if data.n > j0:
-                            self.findex[j].append(offs[j0::B] + self.fbytes[j])
-                    self.writer.write(enc, file=j)
-                    self.fbytes[j] += enc.numel()
-                    self.frecs[j] += data.n
-                else:
-                    if offs is not None:          # block index of the stream: records n, n + B, ...
-                        j0 = (-self.n) % B
-                        if data.n > j0:
-                            self.index.append(offs[j0::B] + self.written_bytes)
-                    self.writer.write(enc)
-                self.n += data.n
-                self.written_bytes += enc.numel()
+        if self.pf is not None and isinstance(data, DeviceTable):
+            if self.pf.add(data):
                 return
-            if self.writer is None:
-                self.stream = False
-        if self.writer is not None:
+            if self.pf.started:
+                raise RuntimeError("grace join stage: a bucket result could not be encoded like the others")
+            self.pf = None                     # no device encoding: the results are concatenated
+        elif self.pf is not None and self.pf.started:
             raise RuntimeError("grace join stage: a bucket result could not be encoded like the others")
         self.chunks.append(data)
 
     def abort(self):
         """An attempt failed mid-stream: stop the writer (its threads, the ring lock) and remove
-        the partial part file."""
-        w, self.writer = self.writer, None
-        if w is not None:
-            try:
-                w.abort()
-            finally:
-                for f in self.paths or [self.tmp]:
-                    try:
-                        os.remove(f)
-                    except OSError:
-                        pass
+        the partial part files."""
+        if self.pf is not None:
+            self.pf.abort()
         self.chunks, self.partials = [], []
 
     def finish(self, V):
@@ -883,29 +830,8 @@ class _Sink:
             for p in parts[1:]:
                 out[p] = empty
             return out
-        if self.writer is not None and self.paths is not None:
-            sizes = self.writer.close()
-            self.written = sum(sizes)
-            keep = []
-            from ..io import partfile as PF
-            from ..ops import codec as CD
-            for j, (f, b) in enumerate(zip(self.paths, sizes)):
-                if b:
-                    keep.append(f)
-                    if self.findex[j]:
-                        PF.write_index(f, self.frecs[j], b, torch.cat(self.findex[j]).cpu().numpy(), CD.BLOCK)
-                else:
-                    os.remove(f)
-            out[parts[0]] = StreamedPart(keep or self.paths[:1], self.n, self.written, self.dtype)
-            self.writer = None
-        elif self.writer is not None:
-            self.written = self.writer.close()
-            if self.index:
-                from ..io import partfile as PF
-                from ..ops import codec as CD
-                PF.write_index(self.tmp, self.n, self.written, torch.cat(self.index).cpu().numpy(), CD.BLOCK)
-            out[parts[0]] = StreamedPart(self.tmp, self.n, self.written, self.dtype)
-            self.writer = None
+        if self.pf is not None and self.pf.started:
+            out[parts[0]], self.written = self.pf.finish()
         else:
             tabs = [c for c in self.chunks if isinstance(c, DeviceTable)]
             if tabs and len(tabs) == len(self.chunks):

@@ -426,7 +426,23 @@ class StreamAggregator:
             data = self.runner._run_op(op, [data], self.v, self.s)
         if data is None or data.n == 0:
             return
-        part = self._partial(data)
+        self._fold_in(self._partial(data), t.n)
+
+    def add_partial(self, part: DeviceTable):
+        """Fold in a table of partial rows another stage produced (the received rounds of a
+        streamed shuffle, runtime/stream_shuffle.py): GroupBy partials go straight into the running
+        state; records of a Distinct are deduplicated first."""
+        if part is None or part.n == 0:
+            return
+        self.stats["chunks"] += 1
+        self.stats["records_in"] += part.n
+        if "chunk_bytes_first" not in self.p:
+            self.p["chunk_bytes_first"] = _nbytes(part)
+        if self.kind == "distinct":
+            part = G.op_distinct(self.agg, [part], self.v)
+        self._fold_in(part, part.n)
+
+    def _fold_in(self, part: DeviceTable, rows_in: int):
         if self.dense is not None:
             if DenseState.eligible(part) and self.dense.add(part):
                 self.stats["dense_state_GB"] = round(self.dense.nbytes() / 1e9, 2)
@@ -435,8 +451,8 @@ class StreamAggregator:
             prior, self.dense = self.dense.to_partial(), None
             self.stats["dense_fallback"] = True
             if prior is not None and prior.n:
-                self._add_partial(prior, rows_in=t.n)
-        self._add_partial(part, rows_in=t.n)
+                self._add_partial(prior, rows_in=rows_in)
+        self._add_partial(part, rows_in=rows_in)
 
     def _add_partial(self, part: DeviceTable, rows_in: int):
         if self.K is None:
@@ -483,18 +499,47 @@ def run(runner, s, p, version, vctx, splan):
         agg.add_chunk(chunk)
     t1 = time.perf_counter()
     final = splan["agg"]["op"] != "group_partial"
-    pieces = list(agg.bucket_results(final))
-    if pieces:
-        out = DeviceTable.concat(pieces)
-    else:
-        out = _empty_result(runner, s, vctx, splan)
-    for op in splan["rest"]:
-        out = runner._run_op(op, [out], vctx, s)
+    out, written = finish(runner, s, p, vctx, agg, final, splan["rest"])
     runner.stream_stats[(s.id, p)] = dict(agg.stats, buckets=agg.K, spilled_buckets=len(agg.spilled),
                                            stream_s=round(t1 - t0, 3),
                                            finish_s=round(time.perf_counter() - t1, 3),
-                                           budget_bytes=agg.budget, kind="streamed aggregation")
+                                           budget_bytes=agg.budget, kind="streamed aggregation",
+                                           result=("streamed to the output store" if written is not None
+                                                   else "concatenated in HBM"),
+                                           result_bytes=written)
     return out
+
+
+def finish(runner, s, p, vctx, agg: StreamAggregator, final: bool, rest: list):
+    """The aggregator's bucket results -> the stage's output value.  A result the stage only
+    writes (``rest`` = its output op, a partfile:// or host:// store) goes to the store bucket by
+    bucket through runtime/sinks.py, never concatenated in HBM; otherwise the buckets are
+    concatenated and the rest of the program runs on them.  Returns (value, bytes streamed or
+    None)."""
+    from . import sinks
+    sink = sinks.for_stage(runner, s, p, rest)
+    pending = []
+    if sink is not None:
+        try:
+            for t in agg.bucket_results(final):
+                if not pending and sink.add(t):
+                    continue
+                if sink.started:
+                    raise RuntimeError("streamed aggregation: a bucket result could not be written like the others")
+                pending.append(t)            # no device encoding: concatenated below
+        except BaseException:
+            sink.abort()
+            raise
+        if sink.started:
+            value, written = sink.finish()
+            return value, written
+        pieces = pending
+    else:
+        pieces = list(agg.bucket_results(final))
+    out = DeviceTable.concat(pieces) if pieces else _empty_result(runner, s, vctx, None)
+    for op in rest:
+        out = runner._run_op(op, [out], vctx, s)
+    return out, None
 
 
 def _empty_result(runner, s, vctx, splan):

@@ -1,0 +1,201 @@
+"""Streamed shuffle: a multi-partition GroupBy / Distinct whose partial side and final side run as
+one pipelined gang stage with bounded channels (SURVEY C-1, §2.4 CrossProduct).
+
+The planner emits a decomposable GroupBy (or a Distinct) over P partitions as two stages:
+
+    A: read -> (Select | Where)* -> group_partial | distinct -> hash_partition     (no inputs)
+    B: group_final | distinct -> ...                                               (cross from A)
+
+Run stage by stage, A's whole partition of partial rows is hash-partitioned, exchanged in one
+all-to-all-v per column, and B's partition receives every source's partials at once: the final
+GroupBy's input must fit HBM.  The reference never holds it: a vertex consumes its input channels
+as streams (RChannelReader, DryadVertex/VertexHost/system/channel/include/channelinterface.h:212;
+DryadLinqVertexReader.cs:41-257) and its partial accumulation folds records as they arrive
+(ParallelHashGroupByPartialAccumulate, LinqToDryad/DryadLinqVertex.cs:5718).
+
+Here the pair runs as rounds.  Round r: each rank reads its next source chunk
+(runtime/streaming._chunks: generator ranges, stored rows, fixed-width parts, host:// tables),
+runs A's record-wise operators and partial aggregation on it, hash-partitions the partial rows and
+queues them as one asynchronous exchange (parallel/exchange.exchange_start: all-to-all-v per column
+and string heap); then it waits for round r-1's pieces and folds them into the running state of
+each of its B partitions (runtime/stream_agg.StreamAggregator.add_partial: the directly addressed
+dense state of an integer key, or hash buckets spilled to pinned host memory past
+``HbmBudgetBytes``).  Round r's transfer overlaps round r+1's partial aggregation and round r-1's
+fold.  After the last round each B partition's state is reduced bucket by bucket and streamed to
+its output store (runtime/sinks.py) or concatenated for the rest of B's program.
+
+Chosen when ``StreamShuffle=True`` (context property; False forbids it), or when a source partition
+exceeds the HBM budget (the pair could not run stage by stage).  Every rank votes alike.
+"""
+from __future__ import annotations
+
+import time
+
+
+from ..gpu.table import DeviceTable, Ported
+from ..gpu.trace import NotTraceable
+from ..parallel import exchange as EXC
+from ..parallel import shuffle
+from ..utils.log import get_logger
+from . import stream_agg as SA
+from . import streaming as ST
+
+log = get_logger("stream_shuffle")
+
+PARTIAL_OPS = {"group_partial", "distinct"}
+FINAL_OPS = {"group_final", "distinct"}
+
+
+def find(plan) -> dict:
+    """{B stage id: descriptor} for every (A, B) pair of the idiom in the module docstring."""
+    out = {}
+    st = plan.stages
+    for b in st:
+        if len(b.inputs) != 1 or b.inputs[0].kind != "cross" or not b.ops or b.ops[0]["op"] not in FINAL_OPS:
+            continue
+        a = st[b.inputs[0].src]
+        ops = [o["op"] for o in a.ops]
+        if a.inputs or len(ops) < 3 or ops[0] != "read" or ops[-1] != "hash_partition" or ops[-2] not in PARTIAL_OPS:
+            continue
+        if any(o not in SA.PRE_OPS for o in ops[1:-2]) or a.is_output or plan.consumers(a.id) != [b.id]:
+            continue
+        if a.partitions != b.partitions or a.ops[-1].get("count", a.partitions) != b.partitions:
+            continue
+        pa, fb = a.ops[-2], b.ops[0]
+        if (pa["op"] == "distinct") != (fb["op"] == "distinct"):
+            continue
+        if pa.get("comparer") is not None or fb.get("comparer") is not None:
+            continue
+        if pa["op"] == "group_partial" and (pa.get("decomp") is None or pa.get("elem") is not None):
+            continue
+        out[b.id] = dict(a=a.id, b=b.id, stages=[a.id])
+    return out
+
+
+def plan_local(desc, runner):
+    """This rank's source plan of stage A (kind, info, chunk bytes, ...) or None."""
+    if not runner.gpu_ok:
+        return None
+    a = runner.plan.stages[desc["a"]]
+    src = ST._source(runner, a)
+    if src is None:
+        return None
+    budget = SA._budget(runner)
+    me = runner.world.rank
+    mine = [p for p in range(a.partitions) if runner.owner(p, a.id) == me]
+    big = max((ST._partition_bytes(src[0], src[1], p) for p in mine), default=0)
+    props = runner.ctx._props
+    chunk = int(props.get("StreamChunkBytes") or ST.DEFAULT_CHUNK_BYTES)
+    chunk = max(1 << 20, min(chunk, budget // 8))
+    return dict(kind=src[0], info=src[1], chunk=chunk, budget=budget, source_bytes=big)
+
+
+def vote(desc, runner):
+    """Collective (one tensor all-gather): the pair runs streamed iff every rank can and it is
+    forced (StreamShuffle=True) or some rank's source partition exceeds its HBM budget."""
+    force = runner.ctx._props.get("StreamShuffle")
+    lay = None if force is False else plan_local(desc, runner)
+    agree, vals = shuffle.vote(lay is not None, None, runner.world,
+                               values=(0 if lay is None else int(lay["source_bytes"] > lay["budget"]),))
+    if not agree:
+        return None
+    if force is not True and not any(v[0] for v in vals):
+        return None
+    return lay
+
+
+def run(desc, runner, lay) -> dict:
+    """Execute the pair on this rank -> {local partition of B: its output value}."""
+    from .gpu_executor import GpuVertexContext
+    w, dev = runner.world, runner.dev
+    W, me = w.size, w.rank
+    A, B = runner.plan.stages[desc["a"]], runner.plan.stages[desc["b"]]
+    parts_a = [p for p in range(A.partitions) if runner.owner(p, A.id) == me]
+    owned = {r: [p for p in range(B.partitions) if runner.owner(p, B.id) == r] for r in range(W)}
+    parts_b = owned[me]
+    vctx_a = {p: GpuVertexContext(p, A.partitions, runner.vids[A.id][p], 0, A, dev, w, runner) for p in parts_a}
+    vctx_b = {p: GpuVertexContext(p, B.partitions, runner.vids[B.id][p], 0, B, dev, w, runner) for p in parts_b}
+    splan = dict(lay, pre=A.ops[1:-2], agg=A.ops[-2], rest=A.ops[-1:])
+    bplan = dict(agg=B.ops[0], pre=[], rest=B.ops[1:], budget=lay["budget"], source_bytes=lay["source_bytes"],
+                 chunk=lay["chunk"])
+    aggs = {p: SA.StreamAggregator(runner, B, vctx_b[p], dict(bplan)) for p in parts_b}
+
+    def chunks():
+        for p in parts_a:
+            for t in ST._chunks(splan, p, dev, vctx_a[p]):
+                yield p, t
+    it = chunks()
+    proto = None
+    pending = None
+    rounds, sent_rows, recv_rows = 0, 0, 0
+    stats = EXC.ExchangeStats()
+    t0 = time.perf_counter()
+    wait_s = 0.0
+
+    def fold(ex):
+        nonlocal recv_rows, wait_s
+        tw = time.perf_counter()
+        got = ex.finish()
+        wait_s += time.perf_counter() - tw
+        for i, q in enumerate(parts_b):
+            pieces = [lst[i] for lst in got if len(lst) > i and lst[i].n]
+            if not pieces:
+                continue
+            tab = DeviceTable.concat(pieces) if len(pieces) > 1 else pieces[0]
+            recv_rows += tab.n
+            aggs[q].add_partial(tab)
+
+    while True:
+        err, sends, item = None, None, None
+        try:
+            item = next(it, None)
+            if item is not None:
+                p, t = item
+                data = t
+                for op in splan["pre"]:
+                    data = runner._run_op(op, [data], vctx_a[p], A)
+                part = runner._run_op(splan["agg"], [data], vctx_a[p], A)
+                ported = runner._run_op(splan["rest"][0], [part], vctx_a[p], A)
+                if not isinstance(ported, Ported) or not isinstance(ported.table, DeviceTable):
+                    raise NotTraceable("streamed shuffle: the partial rows left the device")
+                sends = [[ported.port(q) for q in owned[r]] for r in range(W)]
+                proto = ported.port(0).slice(0, 0)
+                sent_rows += ported.table.n
+        except Exception as e:  # noqa: BLE001
+            err = e
+        # one small tensor collective per round: every rank's status and whether it had a chunk;
+        # a rank whose round failed stops every rank alike (no rank left inside an exchange)
+        st = shuffle.gang_status(err is None, int(item is not None), w)
+        bad = [r for r, (ok, _) in enumerate(st) if not ok]
+        if bad:
+            from ..errors import GangAgreementError
+            raise GangAgreementError(f"streamed shuffle: rank(s) {bad} failed in round {rounds}"
+                                     + (f" ({type(err).__name__}: {err})" if err is not None else ""), ranks=bad) \
+                from err
+        if not any(v for _, v in st):
+            break
+        if sends is None:
+            # this rank's chunks are done: empty pieces of its layout (or none before its first)
+            sends = [[proto for _ in owned[r]] for r in range(W)] if proto is not None else [[] for _ in range(W)]
+        ex = EXC.exchange_start(w, sends, stats)      # queued; round r-1 is folded meanwhile
+        if pending is not None:
+            fold(pending)
+        pending = ex
+        rounds += 1
+    if pending is not None:
+        fold(pending)
+    t1 = time.perf_counter()
+    out, written = {}, 0
+    for q in parts_b:
+        value, nb = SA.finish(runner, B, q, vctx_b[q], aggs[q], True, B.ops[1:])
+        out[q] = value
+        written += nb or 0
+    st = [a.stats for a in aggs.values()]
+    runner.stream_stats[(B.id, me)] = dict(
+        kind="streamed shuffle", rounds=rounds, sent_rows=sent_rows, received_rows=recv_rows,
+        exchanged_GB=round((stats.bytes_sent + stats.bytes_received) / 2e9, 3), collectives=stats.collectives,
+        exchange_wait_s=round(wait_s, 3), stream_s=round(t1 - t0, 3), finish_s=round(time.perf_counter() - t1, 3),
+        spilled_bytes=sum(x.get("spilled_bytes", 0) for x in st), combines=sum(x.get("combines", 0) for x in st),
+        dense_state=any("dense_state_GB" in x for x in st), budget_bytes=lay["budget"],
+        result="streamed to the output store" if written else "concatenated in HBM", result_bytes=written)
+    return out

@@ -45,6 +45,19 @@ def _source(runner, s):
         if kind in ("terasort", "records64", "range", "names"):
             return kind, dict(q=q, uri=uri)
         return None
+    if scheme == "host":
+        # the pinned host tier: row tables (an out-of-core sort's output) and column tables (a
+        # streamed result), read back chunk by chunk
+        from ..io.hosttable import HostColumns, HostRows
+        prov = provider_for(uri)
+        if not prov.exists(uri):
+            return None
+        local = prov.get(uri)["local"]
+        if local and all(isinstance(v, HostRows) for v in local.values()):
+            return "hostrows", dict(uri=uri, local=local)
+        if local and all(isinstance(v, HostColumns) for v in local.values()):
+            return "hostcols", dict(uri=uri, local=local)
+        return None
     if scheme in ("partfile", "file"):
         prov = provider_for(uri)
         sch = prov.schema(uri) or {}
@@ -58,6 +71,9 @@ def _source(runner, s):
 
 
 def _partition_bytes(kind, info, p) -> int:
+    if kind in ("hostrows", "hostcols"):
+        v = info["local"].get(p)
+        return v.nbytes if v is not None else 0
     if kind in ("rows", "fixed"):
         from ..io import partfile as PF
         m = PF.read_meta(parse_uri(info["uri"])[1])
@@ -99,6 +115,24 @@ class NotStreamable(Exception):
 def _chunks(plan, p, device, vctx):
     """Yield the DeviceTable of each chunk of partition p of the source."""
     kind, info, chunk = plan["kind"], plan["info"], plan["chunk"]
+    if kind == "hostrows":
+        h = info["local"].get(p)
+        if h is None or h.n == 0:
+            return
+        per = max(1, chunk // h.stride)
+        for a in range(0, h.n, per):
+            m = min(per, h.n - a)
+            buf = torch.empty((m, h.stride), dtype=torch.uint8, device=device)
+            buf.copy_(h.rows[a: a + m], non_blocking=h.pinned)
+            yield DeviceTable(m, Shape("rows", key_off=h.key_off, key_len=h.key_len), rows=buf)
+        return
+    if kind == "hostcols":
+        h = info["local"].get(p)
+        if h is None or h.n == 0:
+            return
+        per_row = max(1, h.nbytes // max(h.n, 1))
+        yield from h.device_pieces(device, max(1, chunk // per_row))
+        return
     if kind == "rows":
         from ..io import reader as RD
         mm, ko, kl = info["prov"].rows_part(info["uri"], p)

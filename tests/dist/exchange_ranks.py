@@ -98,6 +98,22 @@ def main():
             merged = DeviceTable.concat([x for lst in got for x in lst])
             if merged is not None and merged.n != sum(x.n for lst in got for x in lst):
                 bad.append((kind, nports, "concat"))
+    # a rank holding no piece at all (fewer source partitions than ranks): it learns the table
+    # structure from the first rank that has one (a tensor broadcast, no object collective)
+    if W > 1:
+        t = make_table("tuple_str_vec", me, dev, 50 + me)
+        sends = [[] for _ in range(W)] if me == 0 else [[t.slice(0, 25 + me)] if r == 0 else [t.slice(25 + me, t.n)]
+                                                         for r in range(W)]
+        got = EXC.exchange(w, sends)
+        for s_ in range(W):
+            want = 0 if s_ == 0 else 1
+            if len(got[s_]) != want:
+                bad.append(("no-piece", s_, len(got[s_])))
+            elif want:
+                src = make_table("tuple_str_vec", s_, dev, 50 + s_)
+                exp = src.slice(0, 25 + s_) if me == 0 else src.slice(25 + s_, src.n)
+                if got[s_][0].to_objects() != exp.to_objects():
+                    bad.append(("no-piece", s_, "data"))
     # strided entry columns (views into one [n, 2] tensor, one-row pieces): the merge / broadcast
     # edges of the sampler send such tables unpartitioned
     def ent_table(r, n):
