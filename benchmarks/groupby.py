@@ -11,7 +11,10 @@ shuffle moves most of it).  The timed step is one DryadLINQ job through the GPU 
 
 i.e. generate (the "read" of the input) -> partial GroupBy (radix sort + segmented reduce) ->
 hash partition -> RCCL all-to-all-v -> final GroupBy -> HBM table.  Validated outside the timed
-region (group counts and V1 sums against column totals).
+region group by group: an order-independent fingerprint of every output group (key, count, sum,
+min, max) against the same fingerprint of a reference GroupBy computed by torch sort + scatter ops
+over the regenerated input, one key range at a time (dryad_amd/utils/validate.py); plus the
+count / V1 totals.
 """
 from __future__ import annotations
 
@@ -83,22 +86,34 @@ def main():
         times.append(dt)
     ex = ctx._get_executor()
     fallbacks = [f"{s}:{op}" for s, op, _ in ex.last_result.get("fallbacks", [])]
-    valid = None
+    valid, fpv = None, None
     if not a.no_validate:
+        from dryad_amd.utils import validate as V
         tab = provider_for(out).get(out)["local"]
         cnt = sum(int(t.col(1).sum()) for t in tab.values())
         s1 = sum(int(t.col(2).sum()) for t in tab.values())
         groups = sum(t.n for t in tab.values())
+        got_fp = V.combine([V.group_fingerprint([t.col(j) for j in range(5)]) for t in tab.values()])
+        del tab
+        torch.cuda.empty_cache()
         from dryad_amd.ops import relational as R
         lo = (n * w.rank) // w.size
         hi = (n * (w.rank + 1)) // w.size
         cols = [torch.empty(hi - lo, dtype=torch.int64, device=w.device) for _ in range(2)]
         R.gen_records64(cols, lo, int(a.keys), 4242)
-        tot = torch.tensor([cnt, s1, int(cols[1].sum()), groups], dtype=torch.int64, device=w.device)
+        s_in = int(cols[1].sum())
+        del cols
+        exp_fp = _expected_groups(n, int(a.keys), w.size, w.rank, w.device)
+        i64 = lambda x: x - (1 << 64) if x >= (1 << 63) else x  # noqa: E731
+        tot = torch.tensor([cnt, s1, s_in, groups, got_fp[0], i64(got_fp[1]), exp_fp[0], i64(exp_fp[1])],
+                           dtype=torch.int64, device=w.device)
         if w.size > 1:
             torch.distributed.all_reduce(tot)
-        cnt, s1, s_in, groups = tot.tolist()
-        valid = cnt == n and s1 == s_in
+        cnt, s1, s_in, groups, gn, gf, en, ef = tot.tolist()
+        fpv = dict(groups=gn, expected_groups=en, fingerprint=gf & ((1 << 64) - 1),
+                   expected_fingerprint=ef & ((1 << 64) - 1))
+        fpv["ok"] = gn == en and (gf - ef) % (1 << 64) == 0
+        valid = cnt == n and s1 == s_in and fpv["ok"]
     med = sorted(times)[len(times) // 2]
     streamed = [v for v in (ex.last_result.get("streamed") or {}).values() if v.get("kind") == "streamed aggregation"]
     report(w, {
@@ -107,6 +122,8 @@ def main():
         "warmup": a.warmup, "ms_per_step": round(med * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int64", "data": "synthetic gen://records64 (uniform keys)",
         "validated": valid, "groups": groups if valid is not None else None, "host_fallback_ops": fallbacks,
+        "validation": None if fpv is None else dict(fpv, method="per-group fingerprint vs a torch sort + scatter "
+                                                           "GroupBy of the regenerated input (utils/validate.py)"),
         "all_step_ms": [round(t * 1e3, 2) for t in times],
         "config": {"model": "GroupBy(Key) -> Count/Sum/Min/Max (decomposable, hash shuffle)",
                    "records": n, "record_bytes": 64, "keys": int(a.keys), "parallelism": f"dp{w.size}",
@@ -148,22 +165,18 @@ def loopback(a):
             ph.append(p)
     valid = None
     if not a.no_validate:
+        from dryad_amd.utils import validate as V
         out = job.out
         cnt, s1, groups = int(out.col(1).sum()), int(out.col(2).sum()), out.n
-        # the input rows hashed to rank r, from every source partition: count and V1 sum
-        from dryad_amd.ops import relational as R
-        exp_cnt = exp_s1 = 0
-        for s_ in range(W):
-            lo, hi = (n * s_) // W, (n * (s_ + 1)) // W
-            for c0 in range(lo, hi, 1 << 27):
-                c1 = min(hi, c0 + (1 << 27))
-                cols = [torch.empty(c1 - c0, dtype=torch.int64, device="cuda") for _ in range(2)]
-                R.gen_records64(cols, c0, int(a.keys), 4242)
-                dest = _dest_of(cols[0], W)
-                m = dest == r
-                exp_cnt += int(m.sum())
-                exp_s1 += int(cols[1][m].sum())
-        valid = dict(ok=cnt == exp_cnt and s1 == exp_s1, records=cnt, expected_records=exp_cnt, groups=groups)
+        got = V.group_fingerprint([out.col(j) for j in range(5)])
+        job.out = out = None
+        torch.cuda.empty_cache()
+        # the groups of the keys hashed to rank r, from every source partition: the reference
+        # GroupBy (torch sort + scatter) of the regenerated rows, one key range at a time
+        exp = _expected_groups(n, int(a.keys), W, r, "cuda", keep=lambda k: _dest_of(k, W) == r)
+        valid = dict(ok=got == exp, records=cnt, groups=groups, expected_groups=exp[0],
+                     fingerprint_match=got[1] == exp[1],
+                     method="per-group fingerprint vs a torch sort + scatter GroupBy of the regenerated input")
     mean = sum(ms) / len(ms)
     print(json.dumps({
         "metric": f"GroupBy-Aggregate per-rank step of a {W}-rank job (loopback on one GPU: all-to-all-v replaced)",
@@ -178,6 +191,30 @@ def loopback(a):
                    "exchange": {k: v for k, v in job.bytes.items()},
                    "per_rank_input_GBps": round(int(a.records_per_gpu) * 64 / 1e6 / mean, 1),
                    "validated": valid}}), flush=True)
+
+
+def _gen_chunks(n: int, keys: int, step: int = 1 << 27):
+    """Callable -> iterator over [Key, V1, V2, V3] int64 chunks of gen://records64 rows 0..n-1."""
+    import torch
+    from dryad_amd.ops import relational as R
+
+    def it():
+        for c0 in range(0, n, step):
+            c1 = min(n, c0 + step)
+            cols = [torch.empty(c1 - c0, dtype=torch.int64, device="cuda") for _ in range(4)]
+            R.gen_records64(cols, c0, keys, 4242)
+            yield cols
+    return it
+
+
+def _expected_groups(n: int, keys: int, W: int, rank: int, dev, keep=None):
+    """(groups, fingerprint) of the reference GroupBy over this rank's share of the key ranges (every
+    rank regenerates all n rows per range; ``keep`` selects rows of the groups it validates)."""
+    from dryad_amd.utils import validate as V
+    pieces = max(16, 8 * W) if keep is None else 16
+    ranges = V.key_ranges(0, keys - 1, pieces)
+    mine = ranges if keep is not None else [r for i, r in enumerate(ranges) if i % W == rank]
+    return V.expected_fingerprint(_gen_chunks(n, keys), ["count", "sum", "min", "max"], mine, keep=keep)
 
 
 def _dest_of(keys, W):

@@ -72,13 +72,15 @@ def main():
         return None
 
     def store_check():
-        """(pairs, sum of r.V1 + s.V1) over the written part files, streamed back through HBM."""
+        """(pairs, sum of r.V1 + s.V1, pair fingerprint) over the written part files, streamed back
+        through HBM (the fingerprint: utils/validate.group_fingerprint of every output record)."""
         import torch
         from dryad_amd.io import partfile as PF
         from dryad_amd.io import reader as RD
         from dryad_amd.io.providers import parse_uri
+        from dryad_amd.utils import validate as V
         meta = PF.read_meta(parse_uri(a.to_store)[1])
-        n, tot = 0, 0
+        n, tot, fps = 0, 0, []
         for p in range(meta.count):
             if p % w.size != w.rank:
                 continue
@@ -89,11 +91,13 @@ def main():
                 m = min(step_rows, rows - r0)
                 buf = RD.read_to_device(path, w.device, offset=r0 * 24, length=m * 24).view(torch.int64).view(m, 3)
                 tot += int((buf[:, 1] + buf[:, 2]).sum().item())
+                fps.append(V.group_fingerprint([buf[:, 0], buf[:, 1], buf[:, 2]]))
                 n += m
-        t = torch.tensor([n, tot], dtype=torch.int64, device=w.device)
+        fp = V.combine(fps)[1]
+        t = torch.tensor([n, tot, fp - (1 << 64) if fp >= (1 << 63) else fp], dtype=torch.int64, device=w.device)
         if w.size > 1:
             torch.distributed.all_reduce(t)
-        return [int(t[0].item()), int(t[1].item())]
+        return [int(t[0].item()), int(t[1].item()), int(t[2].item()) & ((1 << 64) - 1)]
 
     step = job.step if a.direct else (store_step if a.to_store else api_step)
     if a.direct:
@@ -109,9 +113,12 @@ def main():
         if job is None:
             job = HashJoinJob(w, cfg)
         exp = job.expected()
+        fp_ok = None
         if a.to_store:
             res = store_check()
-        ok = res[0] == exp[0] and res[1] == exp[1]
+            pairs_fp = job.expected_pairs("v2" if a.names else "key")
+            fp_ok = res[2] == pairs_fp[1] and res[0] == pairs_fp[0]
+        ok = res[0] == exp[0] and res[1] == exp[1] and fp_ok is not False
     med = sorted(times)[len(times) // 2]
     if a.names:                 # Name bytes ("u" + decimal key, keys < rows) + V1 + V2 per record
         lo = lambda d: 10 ** (d - 1) if d > 1 else 0  # noqa: E731  (first key with d digits)
@@ -137,6 +144,7 @@ def main():
         "data": ("synthetic gen://names tables (string key, dimension x fact; input bytes = Name + 2 x int64)"
                  if a.names else "synthetic gen://records64 row tables (dimension x fact)"),
         "validated": ok, "matches": res[0] if res else None, "all_step_ms": [round(t * 1e3, 1) for t in times],
+        "pair_fingerprint_ok": fp_ok if not a.no_validate else None,
         "path": "direct (models/hashjoin.py)" if a.direct else (
             f"DryadLINQ query -> grace join stage -> {a.to_store}" if a.to_store else
             "DryadLINQ query -> fused grace join stage"),

@@ -126,6 +126,26 @@ class HashJoinJob:
                          buckets=self.grace.B, in_hbm=self.grace.in_hbm)
         return res
 
+    def expected_pairs(self, first: str = "key") -> tuple[int, int]:
+        """(pairs, fingerprint) of the join's output records (first, r.V1, s.V1) from S alone, as
+        utils/validate.group_fingerprint hashes them (an order-independent multiset hash): every S
+        row meets exactly one R row, whose fields are functions of the key.  ``first``: "key"
+        (r.Key) or "v2" (r.V2, the string-key variant's first field)."""
+        from ..utils import validate as V
+        parts = []
+        for a, b in self._chunks(self.s_lo, self.s_hi):
+            rows = self._produce("S", a, b).view(torch.int64).reshape(-1, 8)
+            key = rows[:, 0]
+            f1 = _lsr(mix64_t(_i64(SEED_R + KH) ^ key), 33)
+            c0 = key if first == "key" else _lsr(mix64_t(_i64(SEED_R + 2 * KH) ^ key), 33)
+            parts.append(V.group_fingerprint([c0, f1, rows[:, 1]]))
+        n, fp = V.combine(parts)
+        if self.w.size > 1:
+            t = torch.tensor([n, _i64(fp)], dtype=torch.int64, device=self.w.device)
+            shuffle.all_reduce_(t, "sum", self.w)
+            n, fp = int(t[0]), int(t[1]) & ((1 << 64) - 1)
+        return n, fp
+
     def expected(self):
         """(matches, sum) from S alone: every S key hits exactly one R row whose V1 = f(key)."""
         acc = torch.zeros(2, dtype=torch.int64, device=self.w.device)

@@ -86,15 +86,25 @@ def test_streamed_distinct_matches_oracle():
     assert got == sorted(q(_loc()))
 
 
-def test_streamed_partial_side_of_a_two_partition_groupby():
-    """Two partitions on one rank: the partial side (read -> group_partial -> hash_partition)
-    streams, the folded partials go through the exchange and the final GroupBy."""
+@pytest.mark.parametrize("shuffle", [None, False])
+def test_streamed_partial_side_of_a_two_partition_groupby(shuffle):
+    """Two partitions on one rank, each past the budget: by default the pair (partial side, final
+    side) runs as the streamed shuffle (runtime/stream_shuffle.py: rounds of partial -> exchange ->
+    fold); with StreamShuffle=False the partial side (read -> group_partial -> hash_partition)
+    streams on its own and the folded partials go through the exchange and the final GroupBy."""
     src = SRC.format(n=400_000, P=2, k=50_000)
     q = lambda c: c.FromStore(src).GroupBy(lambda r: r[0], lambda k, g: (k, g.Count(), g.Sum(lambda r: r[1])))  # noqa
     g = _ctx(P=2, budget=8 << 20)             # each partition (12.8 MB) past the budget
+    if shuffle is not None:
+        g.StreamShuffle = shuffle
     got = sorted(q(g))
-    res, st = _stats(g)
-    assert len(st) == 2 and all(x["chunks"] > 4 for x in st), st
+    res = g._get_executor().last_result
+    if shuffle is None:
+        st = [v for v in (res.get("streamed") or {}).values() if v.get("kind") == "streamed shuffle"]
+        assert st and st[0]["rounds"] > 4, res.get("streamed")
+    else:
+        _, st = _stats(g)
+        assert len(st) == 2 and all(x["chunks"] > 4 for x in st), st
     assert res["fallbacks"] == [], res["fallbacks"]
     assert got == sorted(q(_loc()))
 
