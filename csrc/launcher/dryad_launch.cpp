@@ -17,7 +17,9 @@
 // DRYAD_GANG_RESTARTS=K, DRYAD_CHECKPOINT_DIR (the persisted stage outputs it resumes from,
 // runtime/checkpoint.py) and MASTER_PORT = P + e (a fresh rendezvous).  The checkpoint directory
 // is launcher-owned: <--checkpoint-dir>/dryad-ckpt-<launcher pid>, created at start and removed
-// when the launcher exits; nothing else under --checkpoint-dir is ever touched.  Nothing is ever re-exec'd
+// when the launcher exits; nothing else under --checkpoint-dir is ever touched.  Without
+// --checkpoint-dir a relaunching launcher (--max-restarts > 0) uses /dev/shm (host memory that
+// outlives the ranks; the native part writer fills it at page-cache speed).  Nothing is ever re-exec'd
 // in place: a process that initialised the GPU only exits.  A rank that fails with an ordinary
 // error code (a deterministic job failure) ends the job as before.  The reference re-executes a
 // failed vertex process from its persisted inputs the same way (DrVertex.cpp:1042-1171,
@@ -205,6 +207,13 @@ int main(int argc, char** argv) {
   if (i >= argc || o.n < 1 || o.n > 64 || o.max_restarts < 0) return usage();
   o.prog = argv + i;
   if (!o.log_dir.empty()) mkdir(o.log_dir.c_str(), 0755);
+  if (o.ckpt_dir.empty() && o.max_restarts > 0) {
+    // relaunches need the persisted stage outputs of the lost gang: by default they go to host
+    // memory that outlives the rank processes (tmpfs), else next to the logs
+    struct stat shm {};
+    if (stat("/dev/shm", &shm) == 0 && S_ISDIR(shm.st_mode) && access("/dev/shm", W_OK) == 0) o.ckpt_dir = "/dev/shm";
+    else if (!o.log_dir.empty()) o.ckpt_dir = o.log_dir;
+  }
   if (!o.ckpt_dir.empty()) {
     struct stat st {};
     if (stat(o.ckpt_dir.c_str(), &st) != 0) {

@@ -143,6 +143,8 @@ _DEFAULTS = dict(
     PersistStageOutputs=None,     # GPU executor: copy completed stage outputs to a checkpoint store so a
     #                               relaunched gang resumes there (None: under a relaunching launcher;
     #                               a directory or True: always; False: never; runtime/checkpoint.py)
+    CheckpointBudgetBytes=None,   # ... bytes the persisted outputs may take (None: 90% of the checkpoint
+    #                               file system's free space); a stage past it is not persisted
     PartFileSplitBytes=0,         # GPU executor: a fixed-width partfile:// output partition of at least
     #                               this many bytes is written as several part files at once (0: one
     #                               part file per partition, as the reference; io/writer.split_count)

@@ -230,6 +230,7 @@ class GpuJobRunner:
                 self.gang_stages.add(s.id)
         self.recovery: list = []         # recovery actions taken (tests / statistics)
         self.ckpt = None                 # runtime/checkpoint.StageCheckpoint of a resumable job
+        self.persist_stats: dict = {}    # stage name -> persisted bytes / ms (or why it was not)
         self.persist_seconds = 0.0
         self.precomputed_bodies: dict = {}   # fused join stage id -> (attempt body, program after it)
 
@@ -1010,14 +1011,40 @@ class GpuJobRunner:
     # ------------------------------------------------------------------ gang relaunch / resume
     def _persist_stage(self, s):
         """Copy this rank's outputs of a completed stage to the checkpoint store (persist policy
-        of a job run under a relaunching launcher, runtime/checkpoint.py)."""
+        of a job run under a relaunching launcher, runtime/checkpoint.py): written by the native
+        part writer, timed per stage (a ``stage_persisted`` job event), skipped when it would pass
+        the store's budget (``persist_skipped``) and dropped when it fails (``persist_failed``):
+        persistence only saves work after a relaunch, it never fails a job."""
         me = self.world.rank
         t0 = time.time()
+        mine = [p for p in range(s.partitions) if self.owner(p, s.id) == me and (s.id, p) in self.channels]
+        if self.gpu_ok:
+            torch.cuda.synchronize(self.dev)          # the stage's kernels are not part of the cost
+        t0 = time.time()
+        need = sum(CK.StageCheckpoint.nbytes(self.channels[(s.id, p)]) for p in mine)
+        ev = dict(stage=s.name, rank=me, bytes=need, budget=self.ckpt.budget, used=self.ckpt.used)
+        if self.ckpt.used + need > self.ckpt.budget:
+            self.persist_stats[s.name] = dict(skipped="budget", bytes=need)
+            self.g.event(json.dumps(dict(ev, ev="persist_skipped", reason="checkpoint budget")))
+            log.warning("stage %s not persisted: %d bytes past the checkpoint budget (%d of %d used)",
+                        s.name, need, self.ckpt.used, self.ckpt.budget)
+            return
         saved = 0
-        for p in range(s.partitions):
-            if self.owner(p, s.id) == me and (s.id, p) in self.channels:
-                saved += int(self.ckpt.save(s.id, p, self.channels[(s.id, p)]))
-        self.persist_seconds += time.time() - t0
+        try:
+            for p in mine:
+                saved += self.ckpt.save(s.id, p, self.channels[(s.id, p)])
+        except Exception as e:  # noqa: BLE001 (a resume aid: the stage simply reruns after a relaunch)
+            for p in mine:
+                self.ckpt.drop(s.id, p)
+            self.persist_stats[s.name] = dict(failed=f"{type(e).__name__}: {e}")
+            self.g.event(json.dumps(dict(ev, ev="persist_failed", error=f"{type(e).__name__}: {e}")))
+            log.warning("stage %s not persisted: %s", s.name, e)
+            return
+        dt = time.time() - t0
+        self.persist_seconds += dt
+        self.persist_stats[s.name] = dict(bytes=saved, ms=round(dt * 1e3, 2),
+                                          GBps=round(saved / 1e9 / max(dt, 1e-9), 2), dir=self.ckpt.dir)
+        self.g.event(json.dumps(dict(ev, ev="stage_persisted", bytes=saved, ms=round(dt * 1e3, 2))))
 
     def _resume_stage(self, s, ready, refresh, now) -> bool:
         """A relaunched gang: when EVERY rank holds the persisted outputs of all its partitions of
@@ -1219,7 +1246,8 @@ class GpuJobRunner:
                     streamed={f"{k[0]}:{k[1]}": v for k, v in self.stream_stats.items()},
                     statistics=json.loads(g.statistics_json()), events=[json.loads(e) for e in g.drain_events()],
                     external_sort=getattr(self, "extsort_stats", None), join=getattr(self, "join_stats", None),
-                    recovery=self.recovery, persist_seconds=round(self.persist_seconds, 4))
+                    recovery=self.recovery, persist_seconds=round(self.persist_seconds, 4),
+                    persist=dict(self.persist_stats))
 
     # ------------------------------------------------------------------ fault-tolerant stage execution
     def _run_stage(self, s, ready, refresh, now):
@@ -1972,7 +2000,9 @@ class GpuExecutor(_BaseExecutor):
         root = CK.from_env(self.ctx)
         if root is not None:
             GpuExecutor._ckpt_seq += 1
-            runner.ckpt = CK.StageCheckpoint(root, CK.job_key(GpuExecutor._ckpt_seq, plan))
+            budget = self.ctx._props.get("CheckpointBudgetBytes")
+            runner.ckpt = CK.StageCheckpoint(root, CK.job_key(GpuExecutor._ckpt_seq, plan),
+                                             budget=int(budget) if budget else None)
         job_dir = self._job_dir(plan) if self.world.rank == 0 else None
         runner.job_dir = job_dir
         self.last_job_dir = job_dir

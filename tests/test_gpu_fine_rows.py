@@ -66,7 +66,14 @@ def test_loopback_rank_program(mode):
         v = job.validate()
         assert v["ok"], v
         assert 0.8 * job.n < v["records"] < 1.2 * job.n
-    assert set(job.phases) == {"input_ms", "sample_ms", "separators_pack_ms", "receive_sort_ms"}
+    assert set(job.phases) == {"input_ms", "sample_ms", "separators_entry_sort_ms", "pack_ms", "receive_sort_ms"}
+    assert len(job.rounds["merge_ms"]) == job.B
+    if mode == "table":
+        # the modelled node step: the overlapped exchange puts round 0 on the wire after one
+        # round's pack, the bulk order after all of them
+        m = job.model(300.0)
+        assert m["modelled"] and m["first_round_queued_ms"] < m["bulk_first_round_queued_ms"], m
+        assert m["overlapped_step_ms"] <= m["bulk_step_ms"] + 1e-6, m
 
 
 def test_loopback_rank_program_from_partfile(tmp_path):

@@ -57,8 +57,9 @@ def test_gang_relaunch_resumes_after_a_lost_rank(tmp_path):
     import json
     env = dict(os.environ, SPMD_DEVICE="cpu", PYTHONPATH=ROOT, DRYAD_HOME=str(tmp_path / "home"))
     logs = tmp_path / "logs"
+    # no --checkpoint-dir: a relaunching launcher persists to its own directory under /dev/shm
     out = subprocess.run([_launcher(), "--gpus", "2", "--master-port", "29641", "--grace-seconds", "3",
-                          "--max-restarts", "2", "--checkpoint-dir", str(tmp_path / "ckpt"), "--log-dir", str(logs),
+                          "--max-restarts", "2", "--log-dir", str(logs),
                           "--", sys.executable, os.path.join(ROOT, "tests", "dist", "gang_relaunch_job.py")],
                          capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:] + open(logs / "rank0.log").read()[-2000:]
@@ -70,6 +71,10 @@ def test_gang_relaunch_resumes_after_a_lost_rank(tmp_path):
     evs = [json.loads(x) for x in open(os.path.join(rep["job_dir"], "log", "events.jsonl"))]
     kinds = [e.get("ev") for e in evs]
     assert "gang_relaunch" in kinds and "stage_resumed" in kinds, kinds
+    ck = next(e for e in evs if e.get("ev") == "gang_relaunch")["checkpoint"]
+    assert ck.startswith("/dev/shm/dryad-ckpt-"), ck
+    assert not os.path.exists("/".join(ck.split("/")[:4])), ck     # the launcher removed its directory
+    assert "stage_persisted" in kinds, kinds
     relaunch = next(e for e in evs if e.get("ev") == "gang_relaunch")
     assert relaunch["epoch"] == 1 and "rank 1 lost" in relaunch["reason"], relaunch
     launcher = [json.loads(x) for x in open(logs / "launcher.jsonl")]
