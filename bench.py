@@ -69,6 +69,8 @@ def main():
                     help="run the per-rank program of a W-rank job on this one GPU, the all-to-all-v replaced by "
                          "generating the exact bytes this rank would receive (not timed); reports per-rank ms")
     ap.add_argument("--loopback-rank", type=int, default=0, help="which rank of the --loopback-ranks job to run")
+    ap.add_argument("--pack-group", type=int, default=1,
+                    help="with --loopback-ranks (A/B): send rounds packed per launch")
     ap.add_argument("--model-link-GBps", type=float, nargs="*", default=[300.0, 450.0],
                     help="with --loopback-ranks: MODELLED per-rank step with the all-to-all-v on a link of this many "
                          "GB/s per GPU (measured per-round pack / merge times replayed in the exchange's queue order; "
@@ -229,7 +231,7 @@ def loopback(args, env):
         sys.exit(2)
     mode = "gen-fused" if args.gen_fused else "table"
     job = TeraSortLoopbackJob(TeraSortConfig(records_per_rank=args.records_per_gpu), W, r, mode=mode,
-                              input_uri=args.input)
+                              input_uri=args.input, pack_group=args.pack_group)
     for i in range(args.warmup):
         job.step()
         print(f"[bench] warmup {i}: {job.ms:.2f} ms {job.phases}", file=sys.stderr, flush=True)

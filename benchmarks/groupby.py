@@ -52,6 +52,13 @@ def main():
     ap.add_argument("--hbm-budget-gb", type=float, default=None,
                     help="HbmBudgetBytes: a partition past it is aggregated chunk by chunk (runtime/stream_agg.py), "
                          "e.g. --records-per-gpu 6.25e9 (400 GB) --hbm-budget-gb 60")
+    ap.add_argument("--stream-shuffle", action="store_true",
+                    help="with --loopback-ranks: the pipelined streamed shuffle (runtime/stream_shuffle.py: rounds "
+                         "of chunk partial -> exchange -> fold); per-round times measured, the node step modelled")
+    ap.add_argument("--chunk-gb", type=float, default=4.0, help="StreamChunkBytes of --stream-shuffle")
+    ap.add_argument("--model-link-GBps", type=float, nargs="*", default=[300.0, 450.0],
+                    help="with --loopback-ranks: MODELLED per-rank step with the exchange on a link of this many "
+                         "GB/s per GPU (labelled modelled)")
     ap.add_argument("--raw-shuffle", action="store_true",
                     help="with --loopback-ranks: shuffle the pruned raw rows (Select -> HashPartition -> GroupBy) "
                          "instead of partial aggregation before the shuffle")
@@ -153,13 +160,25 @@ def loopback(a):
         q = q.Select(lambda x: (x[0], x[1], x[2], x[3])).HashPartition(lambda x: x[0], W).GroupBy(lambda x: x[0], res)
     else:
         q = q.GroupBy(lambda x: x[0], res)
+    if a.stream_shuffle:
+        ctx.StreamShuffle = True
+        ctx.StreamChunkBytes = int(a.chunk_gb * 1e9)
+        if a.hbm_budget_gb:
+            ctx.HbmBudgetBytes = int(a.hbm_budget_gb * 1e9)
     plan = compile_queries(ctx, [q.ToStore("hbm://groupby_lb", delete_if_exists=True)])
-    job = LoopbackRank(plan, W, r)
+    if a.stream_shuffle:
+        from dryad_amd.runtime.loopback import LoopbackStreamShuffle
+        job = LoopbackStreamShuffle(plan, W, r, ctx)
+        job.bytes = {}
+    else:
+        job = LoopbackRank(plan, W, r)
     ms, ph = [], []
     for i in range(a.warmup + a.steps):
         p = job.step()
         print(f"[groupby-lb] {'warmup' if i < a.warmup else 'step'} {i}: {job.ms:.2f} ms {p} {job.bytes}",
               flush=True)
+        if a.stream_shuffle and i >= a.warmup:
+            print(f"[groupby-lb] modelled: {[job.model(x) for x in a.model_link_GBps]}", flush=True)
         if i >= a.warmup:
             ms.append(job.ms)
             ph.append(p)
@@ -186,11 +205,22 @@ def loopback(a):
         "config": {"model": "GroupBy(Key) -> Count/Sum/Min/Max", "records_per_rank": int(a.records_per_gpu),
                    "keys": int(a.keys), "ranks": W, "rank": r,
                    "plan": "Select(4 cols) -> HashPartition -> GroupBy (raw rows shuffled)" if a.raw_shuffle else
-                   "partial GroupBy -> HashPartition -> final GroupBy",
+                   "streamed shuffle: rounds of chunk partial -> HashPartition -> exchange -> fold (pipelined)"
+                   if a.stream_shuffle else "partial GroupBy -> HashPartition -> final GroupBy",
                    "phases_ms": {k: round(sum(p[k] for p in ph) / len(ph), 3) for k in ph[0]},
                    "exchange": {k: v for k, v in job.bytes.items()},
+                   # the exchange is not run here: MODELLED node steps from the measured compute and an
+                   # assumed per-GPU link rate
+                   "modelled_exchange": ([job.model(x) for x in a.model_link_GBps] if a.stream_shuffle else
+                                         [_bulk_model(job, x) for x in a.model_link_GBps]),
+                   "stream": getattr(job, "stats", None),
                    "per_rank_input_GBps": round(int(a.records_per_gpu) * 64 / 1e6 / mean, 1),
                    "validated": valid}}), flush=True)
+
+
+def _bulk_model(job, link):
+    from dryad_amd.runtime.loopback import bulk_model
+    return bulk_model(job.phases, job.bytes, link)
 
 
 def _gen_chunks(n: int, keys: int, step: int = 1 << 27):

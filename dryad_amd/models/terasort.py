@@ -404,8 +404,9 @@ class TeraSortLoopbackJob:
     received records (hash sum and count), and its keys lie inside this rank's separator bounds."""
 
     def __init__(self, cfg: TeraSortConfig, W: int, rank: int = 0, device=None, mode: str = "table",
-                 input_uri: str | None = None):
+                 input_uri: str | None = None, pack_group: int = 1):
         self.cfg, self.W, self.rank = cfg, W, rank
+        self.pack_group = pack_group
         self.n = cfg.records_per_rank
         self.dev = torch.device(device or "cuda")
         self.mode = mode
@@ -547,7 +548,7 @@ class TeraSortLoopbackJob:
         else:
             # the send side round by round, as the overlapped exchange packs it (FineSend.pack(b)
             # just before round b's all-to-all-v is queued)
-            plan = RS.FineSend(bufs, rows, e, tmp, hist, n, seps_hi, B, W, fb)
+            plan = RS.FineSend(bufs, rows, e, tmp, hist, n, seps_hi, B, W, fb, group=self.pack_group)
             st, counts, L, bad = plan.st, plan.counts, plan.L, plan.bad
             ev_plan.record()
             for b in range(B):

@@ -215,7 +215,8 @@ class PinnedHostBuffer:
 # registered once per process and leased by every job that needs it (the executor's HbmPool does
 # the same for HBM).
 _PINNED_FREE: list = []
-PINNED_KEEP = 2
+PINNED_KEEP = 2                    # free buffers kept for reuse (at least) ...
+PINNED_KEEP_BYTES = 16 << 30       # ... and as many more as fit this many bytes (spill pieces)
 
 
 class PinnedLease:
@@ -232,7 +233,8 @@ class PinnedLease:
     def release(self):
         if self._buf is not None:
             _PINNED_FREE.append(self._buf)
-            while len(_PINNED_FREE) > PINNED_KEEP:
+            while len(_PINNED_FREE) > PINNED_KEEP and \
+                    sum(b.tensor.numel() for b in _PINNED_FREE) > PINNED_KEEP_BYTES:
                 _PINNED_FREE.pop(0).release()
             self._buf = None
         self.tensor = None

@@ -38,7 +38,7 @@ PIPE_ROUND_BYTES = 1 << 30
 # fine-bucket exchange over a materialised table: rows a rank receives per round (~1 GiB: the
 # overlapped exchange receives each round into one of OVERLAP_SLOTS small slots) and the slots
 OVERLAP_ROUND_BYTES = 1 << 30
-OVERLAP_SLOTS = 3
+OVERLAP_SLOTS = 2
 _M64 = (1 << 64) - 1
 
 
@@ -658,7 +658,7 @@ def _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, 
     (plan.pack(i)) just before its all-to-all-v is queued, so the first round is on the wire after
     1/B of the pack instead of all of it.  The input table must stay readable until the last pack,
     so nothing is received into it: round i lands in receive slot i % OVERLAP_SLOTS (each the size
-    of the largest round) and is merged from there into its final place out[off[i]:off[i+1]] (the
+    of the largest round; the table's free tail holds what fits, the rest is allocated) and is merged from there into its final place out[off[i]:off[i+1]] (the
     output overlays the send rows: the merge waits until the rows under it have gone out,
     ``overlap_schedule``).  Queue order per round i: pack(i), all-to-all-v(i) [the communicator's
     stream waits for everything queued before it on the compute stream, so a slot is reused only
@@ -671,10 +671,20 @@ def _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, 
     if sched is None:
         return None
     slot_rows = max([off[b + 1] - off[b] for b in range(B)] + [1])
+    # receive slots: the buffer set's free input memory holds as many as fit (rows_in past the
+    # table: the capacity slack, ~1.6 GB at 125 GB per rank; all of rows_in when the table is read
+    # in place from elsewhere), the rest are allocated
+    flat_in = bufs.rows_in.view(-1)
+    tail = flat_in[plan.rows.shape[0] * bufs.rows_in.shape[1]:] if plan.rows.data_ptr() == flat_in.data_ptr() \
+        else flat_in
+    in_tail = min(NS, tail.numel() // max(1, slot_rows * rec))
     try:
-        slots = torch.empty((NS * slot_rows, rec), dtype=torch.uint8, device=out_buf.device)
+        extra = torch.empty(((NS - in_tail) * slot_rows, rec), dtype=torch.uint8, device=out_buf.device) \
+            if in_tail < NS else None
     except (torch.OutOfMemoryError, RuntimeError):
         return None
+    slot_t = [tail[i * slot_rows * rec: (i + 1) * slot_rows * rec].view(slot_rows, rec) for i in range(in_tail)]
+    slot_t += [extra[i * slot_rows: (i + 1) * slot_rows] for i in range(NS - in_tail)]
     merger = FineMerge(fine, plan.L, fb, B, w.rank, out_buf)
     cuda = out_buf.is_cuda
     flags_host = torch.zeros(B, dtype=torch.int32, pin_memory=cuda)
@@ -690,8 +700,7 @@ def _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, 
             shuffle.wait(handles[h])
         if ev:
             ev["arrive"][j].record()
-        base = (j % NS) * slot_rows
-        merger.merge(j, slots, base, off[j], off[j + 1])
+        merger.merge(j, slot_t[j % NS], 0, off[j], off[j + 1])
         if cuda:
             flags_host[j: j + 1].copy_(merger.flags[j: j + 1], non_blocking=True)
             merged_ev[j] = torch.cuda.Event()
@@ -705,11 +714,10 @@ def _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, 
         if merged_ev[j] is not None:
             merged_ev[j].synchronize()
         if int(flags_host[j]):
-            base = (j % NS) * slot_rows
             a, z = off[j], off[j + 1]
             ea = torch.empty((z - a, 2), dtype=torch.int64, device=out_buf.device)
             eb = torch.empty_like(ea)
-            local_sort_rows(slots[base: base + z - a], out_buf[a:z], ea, eb, 0, key_len,
+            local_sort_rows(slot_t[j % NS][: z - a], out_buf[a:z], ea, eb, 0, key_len,
                             hi_bounds=fine_hi_bounds(plan.L, fb, w.rank * B + j))
             fixups.append(j)
 
@@ -721,11 +729,10 @@ def _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, 
             tev["pack"].append(e)
         if i >= NS:
             check(i - NS)
-        base = (i % NS) * slot_rows
         a, z = plan.st[i * W], plan.st[(i + 1) * W]
         handles[i] = shuffle.alltoallv_bytes_async(
             send_flat[a * rec: z * rec], [c * rec for c in send[i]],
-            slots.view(-1)[base * rec: (base + off[i + 1] - off[i]) * rec], [rc[s][i] * rec for s in range(W)], w)
+            slot_t[i % NS].view(-1)[: (off[i + 1] - off[i]) * rec], [rc[s][i] * rec for s in range(W)], w)
         # merges whose inputs and output rows are ready without waiting for round i, and the one
         # whose slot round i + 1 needs (which may wait for round i)
         while pending and (sched[pending[0]] <= i - 1 or pending[0] <= i + 1 - NS):
@@ -734,11 +741,11 @@ def _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, 
         merge(pending.pop(0))
     for j in range(max(0, B - NS), B):
         check(j)
-    report = dict(mode="rounds packed as they go out", slots=NS, slot_GB=round(NS * slot_rows * rec / 1e9, 3),
-                  merge_after=[k - j for j, k in enumerate(sched)], skew_fixups=fixups)
+    report = dict(mode="rounds packed as they go out", slots=NS, slot_GB=round(slot_rows * rec / 1e9, 3),
+                  slots_in_table_tail=in_tail, merge_after=[k - j for j, k in enumerate(sched)], skew_fixups=fixups)
     if ev:
         ev["pack"] = tev["pack"]
-    del slots
+    del slot_t, extra
     return out_buf[: off[-1]], report
 
 
@@ -774,7 +781,7 @@ class FineSend:
     with count + scatter passes over ``rebuild()``'s entries before anything is packed."""
 
     def __init__(self, bufs: SortBuffers, rows: torch.Tensor, e: torch.Tensor, tmp: torch.Tensor, hist, n: int,
-                 seps_hi: list, B: int, W: int, fb: int, rebuild=None):
+                 seps_hi: list, B: int, W: int, fb: int, rebuild=None, group: int = 1):
         err = S.lookback_error()
         win = 8 * ((fb + 7) // 8)
         srt = S.sort_entries64(e, tmp, win, gen_hist=hist, err=err)
@@ -809,14 +816,24 @@ class FineSend:
         self.bufs, self.rows, self.srt, self.err = bufs, rows, srt, err
         self.st, self.L, self.Sg, self.B, self.W = st, L, Sg, B, W
         self.bad = torch.zeros(1, dtype=torch.int32, device=e.device)
+        # rounds per pack launch (``group``): round b is packed with the first round of its group
+        self.group = max(1, min(int(group), 256 // max(W, 1)))
+        if self.group > 1:
+            g = self.group
+            self.gsegs = torch.tensor([[st[b * W + r] - st[(b // g) * g * W], Sg[r * B + b]]
+                                       for b in range(B) for r in range(W)], dtype=torch.int64).to(e.device)
 
     def pack(self, b: int) -> None:
-        """Round b's send rows: out[st[b * W]: st[(b + 1) * W]] gathered from the table."""
-        W = self.W
-        a, z = self.st[b * W], self.st[(b + 1) * W]
+        """Round b's send rows: out[st[b * W]: st[(b + 1) * W]] gathered from the table (with
+        ``group`` > 1, rounds b .. b + group - 1 in one launch when b starts a group)."""
+        W, g = self.W, self.group
+        if b % g:
+            return
+        e = min(self.B, b + g)
+        a, z = self.st[b * W], self.st[e * W]
         if z > a:
-            TSG.pack_rows(self.bufs.rows_out[a:z], self.rows, self.srt, z - a, seg=self.segs[b * W: (b + 1) * W],
-                          err=self.err, bad=self.bad)
+            segs = self.segs[b * W: e * W] if g == 1 else self.gsegs[b * W: e * W]
+            TSG.pack_rows(self.bufs.rows_out[a:z], self.rows, self.srt, z - a, seg=segs, err=self.err, bad=self.bad)
 
 
 def send_fine_rows(bufs: SortBuffers, rows: torch.Tensor, e: torch.Tensor, tmp: torch.Tensor, hist, n: int,
@@ -939,30 +956,49 @@ class FineMerge:
 
     def __init__(self, fine: torch.Tensor, L: list, fb: int, B: int, rank: int, out: torch.Tensor):
         self.W, self.K = fine.shape
+        W, K = self.W, self.K
         self.L, self.fb, self.B, self.rank, self.out = L, fb, B, rank, out
-        self.flags = torch.zeros(B, dtype=torch.int32, device=out.device)
+        dev = out.device
+        self.flags = torch.zeros(B, dtype=torch.int32, device=dev)
         self.base = L[rank * B]
-        # slice starts of every bucket from one flat scan of all sources' counts (a 1-D device
-        # scan; per round only elementwise differences): ex[s, k] = rows of source s before bucket k
+        # Every round's merge arguments computed once, up front, in a handful of device passes
+        # (per round only slices remain: one kernel launch per round).  Round b holds buckets
+        # [k0_b, k1_b); a bucket's slice from source s starts at
+        #   pre[s, k] = (rows of s before k in the round) + (rows of sources < s in the round)
+        # relative to the round's first received row, and its output at
+        #   outoff[k] = (rows of all sources before k in the round) relative to the round's output.
+        # Both are laid out round-major ([W, k1_b - k0_b] blocks back to back), so a round's
+        # arguments are contiguous slices.
         fine = fine.contiguous()
-        ex = (torch.cumsum(fine.view(-1), 0, dtype=torch.int64).view(self.W, self.K) - fine)
-        self.ex = ex - ex[:, :1]
+        ex = torch.cumsum(fine.view(-1), 0, dtype=torch.int64).view(W, K) - fine
+        ex = ex - ex[:, :1]                                   # rows of source s before bucket k
+        ext = torch.cat([ex, (ex[:, -1:] + fine[:, -1:].to(torch.int64))], 1)      # [W, K + 1]
+        kb = torch.tensor([L[rank * B + b] - self.base for b in range(B + 1)], dtype=torch.int64, device=dev)
+        rid = torch.bucketize(torch.arange(K, dtype=torch.int64, device=dev), kb[1:], right=True)
+        rows_per_src = ext[:, kb[1:]] - ext[:, kb[:-1]]                              # [W, B]
+        src_base = torch.cumsum(rows_per_src, 0) - rows_per_src                     # [W, B]
+        pre_rel = ex - ext[:, kb[:-1]][:, rid] + src_base[:, rid]                   # [W, K]
         col = fine.sum(0, dtype=torch.int64)
-        self.cex = torch.cumsum(col, 0) - col
-        self.fine = fine
+        cex = torch.cumsum(col, 0) - col
+        self.outoff = (cex - cex[kb[:-1]][rid]).contiguous()                          # [K]
+        # round-major blocks: element (s, k) of round b at W * k0_b + s * (k1_b - k0_b) + (k - k0_b)
+        k0 = kb[:-1][rid]
+        width = (kb[1:] - kb[:-1])[rid]
+        kk = torch.arange(K, dtype=torch.int64, device=dev)
+        pos = (W * k0 + (kk - k0)).unsqueeze(0) + torch.arange(W, dtype=torch.int64, device=dev).unsqueeze(1) * width
+        self.pre = torch.empty(W * K, dtype=torch.int64, device=dev).scatter_(0, pos.view(-1), pre_rel.view(-1))
+        self.cnt = torch.empty(W * K, dtype=fine.dtype, device=dev).scatter_(0, pos.view(-1), fine.view(-1))
+        self.kb = kb.tolist()
 
     def merge(self, b: int, recv: torch.Tensor, base: int, a: int, z: int) -> None:
+        """Round b: its rows ``recv[base: base + z - a]`` -> ``out[a:z]`` (one kernel launch)."""
         if z <= a:
             return
-        g = self.rank * self.B + b
-        k0, k1 = self.L[g] - self.base, self.L[g + 1] - self.base
-        ex, fine, K = self.ex, self.fine, self.K
-        cnt = fine[:, k0:k1]
-        exr = ex[:, k0:k1] - ex[:, k0:k0 + 1]                       # within the range
-        rows_per_src = (ex[:, k1:k1 + 1] if k1 < K else (ex[:, -1:] + fine[:, -1:])) - ex[:, k0:k0 + 1]
-        pre = (exr + (torch.cumsum(rows_per_src, 0) - rows_per_src) + base).contiguous()
-        outoff = (self.cex[k0:k1] - self.cex[k0] + a).contiguous()
-        TSG.tile_merge(recv, self.out, pre, cnt.contiguous(), outoff, self.fb, self.flags[b:b + 1])
+        k0, k1 = self.kb[b], self.kb[b + 1]
+        W = self.W
+        pre = self.pre[W * k0: W * k1].view(W, k1 - k0)
+        cnt = self.cnt[W * k0: W * k1].view(W, k1 - k0)
+        TSG.tile_merge(recv[base:], self.out[a:], pre, cnt, self.outoff[k0:k1], self.fb, self.flags[b:b + 1])
 
 
 def merge_received_rounds(bufs: SortBuffers, off: list, fine: torch.Tensor, L: list, fb: int, B: int, rank: int,

@@ -131,3 +131,146 @@ class LoopbackRank:
     @property
     def ms(self) -> float:
         return sum(self.phases.values())
+
+
+def bulk_model(phases: dict, nbytes: dict, link_GBps: float) -> dict:
+    """MODELLED step of the bulk plan (stage A, one exchange, stage B) on a link of ``link_GBps``
+    per GPU: the exchange takes max(bytes out, bytes in) / link between the two stages."""
+    wire = max(nbytes["sent_bytes"], nbytes["received_bytes"]) / (link_GBps * 1e6)
+    return dict(link_GBps=link_GBps, modelled=True, wire_ms=round(wire, 2),
+                step_ms=round(phases["stage_a_ms"] + wire + phases["stage_b_ms"], 2))
+
+
+class LoopbackStreamShuffle:
+    """Rank ``rank`` of a W-rank streamed shuffle (runtime/stream_shuffle.py) on one GPU: per round,
+    this rank's chunk through stage A's program (read chunk, record-wise ops, partial aggregation,
+    hash partition) and the fold of the round's received pieces into stage B's running state are
+    timed; the pieces the other W - 1 sources would send it in that round are produced untimed by
+    running their chunk of the round.  ``model(link)`` replays the measured per-round times in the
+    streamed shuffle's queue order with each round's exchange taking max(bytes out, bytes in) /
+    link (MODELLED: no link is measured here)."""
+
+    def __init__(self, plan, W: int, rank: int, ctx, device=None):
+        from . import stream_shuffle as SSH
+        self.plan, self.W, self.rank, self.ctx = plan, W, rank, ctx
+        self.dev = torch.device(device or "cuda")
+        self.A, self.B = shuffle_stages(plan)
+        if self.A.partitions != W:
+            raise ValueError("loopback: compile the plan with PartitionCount = W")
+        d = SSH.find(plan).get(self.B.id)
+        if d is None:
+            raise ValueError("loopback: the plan is not a streamed-shuffle pair")
+        self.world = World(rank=rank, size=W, local_rank=0, device=self.dev, backend=None)
+        self.out = None
+        self.rounds = []
+
+    def _splan(self):
+        from . import stream_agg as SA
+        from . import streaming as ST
+        props = self.ctx._props
+
+        class _R:                      # the minimal runner surface streaming._source / budget read
+            pass
+        r = _R()
+        r.ctx, r.dev = self.ctx, self.dev
+        src = ST._source(r, self.A)
+        budget = int(props.get("HbmBudgetBytes") or torch.cuda.mem_get_info(self.dev)[0] * 0.8)
+        chunk = max(1 << 20, min(int(props.get("StreamChunkBytes") or ST.DEFAULT_CHUNK_BYTES), budget // 8))
+        big = ST._partition_bytes(src[0], src[1], self.rank)
+        return dict(kind=src[0], info=src[1], chunk=chunk, budget=budget, source_bytes=big,
+                    pre=self.A.ops[1:-2], agg=self.A.ops[-2], rest=self.A.ops[-1:]), SA
+
+    def _a_round(self, s, t):
+        v = GpuVertexContext(s, self.A.partitions, 0, 0, self.A, self.dev, self.world, None)
+        data = t
+        for op in self.A.ops[1:]:
+            data = G.OPS[op["op"]](op, [data], v)
+        return data                  # Ported
+
+    def step(self) -> dict:
+        from . import streaming as ST
+        W, me = self.W, self.rank
+        self.out = None
+        splan, SA = self._splan()
+        vb = GpuVertexContext(me, self.B.partitions, 0, 0, self.B, self.dev, self.world, None)
+
+        class _Runner:               # what StreamAggregator and finish() use of the executor
+            pass
+        run = _Runner()
+        run.ctx, run.dev, run.stream_stats = self.ctx, self.dev, {}
+        run._run_op = lambda op, ins, v, s: G.OPS[op["op"]](op, ins, v)
+        bplan = dict(agg=self.B.ops[0], pre=[], rest=[], budget=splan["budget"], source_bytes=splan["source_bytes"],
+                     chunk=splan["chunk"])
+        agg = SA.StreamAggregator(run, self.B, vb, bplan)
+        gens = [ST._chunks(splan, s, self.dev, None) for s in range(W)]
+        self.rounds = []
+        t_all = torch.cuda.Event(enable_timing=True)
+        t_all.record()
+        while True:
+            mine = next(gens[me], None)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            ev[0].record()
+            ported = self._a_round(me, mine) if mine is not None else None
+            ev[1].record()
+            pieces = []
+            sent = 0
+            if ported is not None:
+                sent = sum(_nbytes(ported.port(p)) for p in range(ported.nports) if p != me)
+                pieces.append((me, _copy_table(ported.port(me))))
+            others = False
+            for s in range(W):               # the round's pieces from the other sources (untimed)
+                if s == me:
+                    continue
+                t = next(gens[s], None)
+                if t is None:
+                    continue
+                others = True
+                pieces.append((s, _copy_table(self._a_round(s, t).port(me))))
+            if mine is None and not others:
+                break
+            pieces.sort(key=lambda x: x[0])
+            tabs = [p for _, p in pieces if p.n]
+            recv = DeviceTable.concat(tabs) if len(tabs) > 1 else (tabs[0] if tabs else None)
+            rb = _nbytes(recv) - (_nbytes(pieces[0][1]) if pieces and pieces[0][0] == me else 0) if recv else 0
+            torch.cuda.synchronize(self.dev)
+            ev[2].record()
+            if recv is not None:
+                agg.add_partial(recv)
+            ev[3].record()
+            torch.cuda.synchronize(self.dev)
+            self.rounds.append(dict(a_ms=ev[0].elapsed_time(ev[1]), fold_ms=ev[2].elapsed_time(ev[3]),
+                                    sent_bytes=sent, recv_bytes=rb))
+            del pieces, recv, ported
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        res = list(agg.bucket_results(True))
+        self.out = DeviceTable.concat(res) if len(res) > 1 else (res[0] if res else None)
+        e1.record()
+        torch.cuda.synchronize(self.dev)
+        self.finish_ms = e0.elapsed_time(e1)
+        self.stats = dict(agg.stats, buckets=agg.K, spilled_buckets=len(agg.spilled))
+        self.phases = {"rounds": len(self.rounds), "stage_a_ms": sum(r["a_ms"] for r in self.rounds),
+                       "fold_ms": sum(r["fold_ms"] for r in self.rounds), "finish_ms": self.finish_ms}
+        return self.phases
+
+    @property
+    def ms(self) -> float:
+        return self.phases["stage_a_ms"] + self.phases["fold_ms"] + self.phases["finish_ms"]
+
+    def model(self, link_GBps: float) -> dict:
+        """Queue order of stream_shuffle.run: A(r), exchange(r) queued, fold(r - 1) (waits for
+        round r - 1), ..., fold(R - 1), finish; one compute stream, one link."""
+        comp = comm = 0.0
+        end = []
+        for r, rd in enumerate(self.rounds):
+            comp += rd["a_ms"]
+            start = max(comp, comm)
+            end.append(start + max(rd["sent_bytes"], rd["recv_bytes"]) / (link_GBps * 1e6))
+            comm = end[-1]
+            if r >= 1:
+                comp = max(comp, end[r - 1]) + self.rounds[r - 1]["fold_ms"]
+        if self.rounds:
+            comp = max(comp, end[-1]) + self.rounds[-1]["fold_ms"]
+        comp += self.finish_ms
+        wire = sum(max(r["sent_bytes"], r["recv_bytes"]) for r in self.rounds) / (link_GBps * 1e6)
+        return dict(link_GBps=link_GBps, modelled=True, wire_ms=round(wire, 2), step_ms=round(comp, 2))

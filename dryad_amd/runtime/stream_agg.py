@@ -91,25 +91,39 @@ def _nbytes(t) -> int:
 
 
 class HostPiece:
-    """A table's columns in pinned host memory (a spilled bucket state or piece)."""
+    """A table's columns in pinned host memory (a spilled bucket state or piece), in leased
+    exact-size page-locked buffers (ops/_lib.pinned_lease: reused by later spills and by the
+    streamed result, not rounded up to a power of two like torch's pinned allocator).  Every copy
+    in and out is ordered on the current stream, so ``release()`` may hand the buffers on as soon
+    as the copy out is queued."""
 
     def __init__(self, t: DeviceTable):
+        from ..ops._lib import pinned_lease
         self.n, self.shape, self.strs = t.n, t.shape, t.strs
         self.rows = None
         self.cols = {}
+        self.leases = []
+
+        def out(v):
+            ls = pinned_lease(tuple(v.shape), v.dtype)
+            ls.tensor.copy_(v, non_blocking=True)
+            self.leases.append(ls)
+            return ls.tensor
         if t.rows is not None:
-            self.rows = torch.empty(t.rows[: t.n].shape, dtype=t.rows.dtype, pin_memory=True)
-            self.rows.copy_(t.rows[: t.n], non_blocking=True)
+            self.rows = out(t.rows[: t.n])
         for k, v in t.cols.items():
-            h = torch.empty(v[: t.n].shape, dtype=v.dtype, pin_memory=True)
-            h.copy_(v[: t.n], non_blocking=True)
-            self.cols[k] = h
+            self.cols[k] = out(v[: t.n])
         self.nbytes = _nbytes(t)
 
     def to_device(self, dev) -> DeviceTable:
         if self.rows is not None:
             return DeviceTable(self.n, self.shape, rows=self.rows.to(dev, non_blocking=True))
         return DeviceTable(self.n, self.shape, {k: v.to(dev, non_blocking=True) for k, v in self.cols.items()})
+
+    def release(self):
+        for ls in self.leases:
+            ls.release()
+        self.leases, self.rows, self.cols = [], None, {}
 
 
 def _key_fields(t: DeviceTable, agg_kind: str):
@@ -366,6 +380,9 @@ class StreamAggregator:
     def _fold(self, pieces: list) -> DeviceTable:
         dev = self.v.device
         tabs = [x.to_device(dev) if isinstance(x, HostPiece) else x for x in pieces if x is not None]
+        for x in pieces:                 # (their copies to HBM are queued: the buffers go back to the pool)
+            if isinstance(x, HostPiece):
+                x.release()
         tabs = [x for x in tabs if x.n]
         if not tabs:
             return None

@@ -50,3 +50,26 @@ def test_fine_subs_targets_one_gib_rounds():
     assert RS.fine_subs(125 * 10**9, 1) == 128
     assert RS.fine_subs(10**6, 2) == 4
     assert RS.fine_subs(10**15, 8) == 256           # world * rounds <= 2048
+
+
+def test_fine_merge_arguments_match_the_per_round_formula():
+    """FineMerge computes every round's (slice starts, counts, output offsets) up front, round-major;
+    each round's slices equal the per-round prefix-sum formula."""
+    import torch
+    torch.manual_seed(0)
+    W, B, base, K, rank = 4, 5, 37, 200, 1
+    kb0 = sorted(torch.randint(0, K, (B - 1,)).tolist())
+    L = [0] * (rank * B) + [base] + [base + x for x in kb0] + [base + K] + [base + K] * (B * 2 - rank * B - B)
+    fine = torch.randint(0, 5, (W, K), dtype=torch.int32)
+    m = RS.FineMerge(fine, L, 16, B, rank, torch.empty((10, 100), dtype=torch.uint8))
+    ex = torch.cumsum(fine.view(-1).long(), 0).view(W, K) - fine
+    ex = ex - ex[:, :1]
+    col = fine.sum(0, dtype=torch.int64)
+    cex = torch.cumsum(col, 0) - col
+    for b in range(B):
+        k0, k1 = L[rank * B + b] - base, L[rank * B + b + 1] - base
+        rps = (ex[:, k1:k1 + 1] if k1 < K else (ex[:, -1:] + fine[:, -1:])) - ex[:, k0:k0 + 1]
+        pre = ex[:, k0:k1] - ex[:, k0:k0 + 1] + (torch.cumsum(rps, 0) - rps)
+        assert torch.equal(m.pre[W * k0: W * k1].view(W, k1 - k0), pre), b
+        assert torch.equal(m.cnt[W * k0: W * k1].view(W, k1 - k0), fine[:, k0:k1]), b
+        assert torch.equal(m.outoff[k0:k1], cex[k0:k1] - cex[k0]), b
