@@ -288,7 +288,7 @@ def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | N
                   budget: int | None = None, keep_ties: bool = False, sample_target: int = 1 << 20,
                   seed: int = 314159, stats: ExtSortStats | None = None,
                   out: HostRows | None = None, out_factory=None, resident: bool = False,
-                  work_fraction: float = HYBRID_WORK_FRACTION):
+                  work_fraction: float = HYBRID_WORK_FRACTION, descending: bool = False):
     """Globally sort the rows of ``src`` (this rank's partition) by the byte-string key
     [key_off, key_off + key_len) (memcmp order, key_len <= 12).  Rank r returns the r-th key range
     as a ``HostRows`` table in pinned host memory.  ``budget``: HBM bytes the sort may use
@@ -296,7 +296,11 @@ def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | N
     enough (the result is then a view of its first rows); ``out_factory(n_out)``: builds the
     output table once this rank's row count is known (e.g. a memory-mapped part file,
     ``HostRows.mapped``, for outputs larger than host memory).  ``resident``: hybrid mode (module
-    docstring); returns a ``TieredRows`` table when some buckets stayed in HBM."""
+    docstring); returns a ``TieredRows`` table when some buckets stayed in HBM.  ``descending``
+    (OrderByDescending, the reference's ParallelSort with isDescending, DryadLinqVertex.cs:
+    9330-9335): the key bits of every entry are inverted (recordsort.invert_keys) before sampling,
+    range destination and each bucket's sort, so rank 0 / bucket 0 hold the largest keys; the tie
+    tags are not inverted, so equal keys keep the source order (a stable descending sort)."""
     w = world or get_world()
     W, me = w.size, w.rank
     dev = w.device if w.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
@@ -338,6 +342,8 @@ def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | N
         idx = torch.arange(off, n, stride_s, dtype=torch.int64)[:m]
         srows = src.sample_rows(idx, scratch, chunk_rows)
         samp = S.extract_keys(srows.contiguous(), key_off, key_len, 0)
+        if descending:
+            RS.invert_keys(samp, key_len)
         if split:
             c_idx = idx // chunk_rows
             tag = ((me * C + c_idx) << 32) | (idx - c_idx * chunk_rows)
@@ -356,6 +362,8 @@ def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | N
 
     def entries(c, rows_c, out_e):
         e = S.extract_keys(rows_c, key_off, key_len, 0, out=out_e)
+        if descending:
+            RS.invert_keys(e, key_len)
         if split:
             e[:, 0].bitwise_or_(tag_of(c))
         S.range_dest(e, seps, part_mask)
@@ -568,13 +576,14 @@ def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | N
                     comp.wait_event(ev_down[0])
                     comp.wait_event(ev_down[1])
                 res = RS.local_sort_rows(rows_r, rtmp if rtmp is not None else bout[0], ea, eb, key_off, key_len,
-                                         hi_bounds=hb)
+                                         hi_bounds=hb, descending=descending)
                 rows_r.copy_(res[:mb])
                 continue
             k = j % 2
             comp.wait_event(ev_down[k])        # slot k's previous output has left for the host
             comp.wait_event(ev_up.pop(j))
-            res = RS.local_sort_rows(bin_[k][:mb], bout[k], ea, eb, key_off, key_len, hi_bounds=hb)
+            res = RS.local_sort_rows(bin_[k][:mb], bout[k], ea, eb, key_off, key_len, hi_bounds=hb,
+                                     descending=descending)
             ev_sorted[k].record(comp)
             d2h.wait_event(ev_sorted[k])
             _copy(out.rows[offs[b]: offs[b] + mb], res[:mb], d2h)

@@ -970,10 +970,17 @@ class FineMerge:
         # Both are laid out round-major ([W, k1_b - k0_b] blocks back to back), so a round's
         # arguments are contiguous slices.
         fine = fine.contiguous()
+        kb = torch.tensor([L[rank * B + b] - self.base for b in range(B + 1)], dtype=torch.int64, device=dev)
+        self.kb = [L[rank * B + b] - self.base for b in range(B + 1)]
+        if K == 0:                       # this rank's key ranges hold no bucket (e.g. all keys equal)
+            self.pre = torch.zeros(0, dtype=torch.int64, device=dev)
+            self.cnt = torch.zeros(0, dtype=fine.dtype, device=dev)
+            self.outoff = torch.zeros(0, dtype=torch.int64, device=dev)
+            return
+        assert self.kb[0] == 0 and self.kb[-1] == K, (self.kb[0], self.kb[-1], K)
         ex = torch.cumsum(fine.view(-1), 0, dtype=torch.int64).view(W, K) - fine
         ex = ex - ex[:, :1]                                   # rows of source s before bucket k
-        ext = torch.cat([ex, (ex[:, -1:] + fine[:, -1:].to(torch.int64))], 1)      # [W, K + 1]
-        kb = torch.tensor([L[rank * B + b] - self.base for b in range(B + 1)], dtype=torch.int64, device=dev)
+        ext = torch.cat([ex, fine.sum(1, keepdim=True, dtype=torch.int64)], 1)     # [W, K + 1]
         rid = torch.bucketize(torch.arange(K, dtype=torch.int64, device=dev), kb[1:], right=True)
         rows_per_src = ext[:, kb[1:]] - ext[:, kb[:-1]]                              # [W, B]
         src_base = torch.cumsum(rows_per_src, 0) - rows_per_src                     # [W, B]
@@ -988,7 +995,6 @@ class FineMerge:
         pos = (W * k0 + (kk - k0)).unsqueeze(0) + torch.arange(W, dtype=torch.int64, device=dev).unsqueeze(1) * width
         self.pre = torch.empty(W * K, dtype=torch.int64, device=dev).scatter_(0, pos.view(-1), pre_rel.view(-1))
         self.cnt = torch.empty(W * K, dtype=fine.dtype, device=dev).scatter_(0, pos.view(-1), fine.view(-1))
-        self.kb = kb.tolist()
 
     def merge(self, b: int, recv: torch.Tensor, base: int, a: int, z: int) -> None:
         """Round b: its rows ``recv[base: base + z - a]`` -> ``out[a:z]`` (one kernel launch)."""

@@ -602,8 +602,7 @@ class GpuJobRunner:
         out = {}
         for sid, c in sorted(cands.items()):
             sort = c["sort"]
-            ok = parse_uri(st[sid].output["uri"])[0] in ("host", "partfile", "file") and sort.get("comparer") is None \
-                and not sort.get("descending", False)
+            ok = parse_uri(st[sid].output["uri"])[0] in ("host", "partfile", "file") and sort.get("comparer") is None
             src = self._chunk_source(c["read"]) if ok else None
             spec = None
             if src is not None:
@@ -660,7 +659,8 @@ class GpuJobRunner:
         st = EX.ExtSortStats()
         factory = self._disk_output(s, e["source"], off, ln)
         out = EX.external_sort(e["source"], off, ln, self.world, budget=self.ctx._props.get("HbmBudgetBytes"),
-                               keep_ties=e["keep_ties"], stats=st, out_factory=factory)
+                               keep_ties=e["keep_ties"], stats=st, out_factory=factory,
+                               descending=bool(e["sort"].get("descending", False)))
         self.extsort_stats = st
         return out
 

@@ -73,3 +73,13 @@ def test_fine_merge_arguments_match_the_per_round_formula():
         assert torch.equal(m.pre[W * k0: W * k1].view(W, k1 - k0), pre), b
         assert torch.equal(m.cnt[W * k0: W * k1].view(W, k1 - k0), fine[:, k0:k1]), b
         assert torch.equal(m.outoff[k0:k1], cex[k0:k1] - cex[k0]), b
+
+
+def test_fine_merge_of_a_rank_without_buckets():
+    """A rank whose key ranges hold no fine bucket (all keys equal, kept together on another rank):
+    no merge arguments, nothing indexed."""
+    import torch
+    L = [0, 0, 0, 0, 0, 65536, 65536, 65536, 65536]        # W = 2, B = 4: rank 0 owns nothing
+    m = RS.FineMerge(torch.zeros((2, 0), dtype=torch.int32), L, 16, 4, 0, torch.empty((4, 100), dtype=torch.uint8))
+    assert m.kb == [0] * 5 and m.pre.numel() == 0
+    m.merge(0, torch.empty((0, 100), dtype=torch.uint8), 0, 0, 0)

@@ -148,3 +148,37 @@ def test_query_out_of_core_orderby_to_disk_partfile(tmp_path):
     assert (off, ln) == (0, 10)
     assert np.array_equal(np.asarray(mm), _in_hbm_sorted(_gen_rows(n, 0, 5)).numpy())
     assert not [f for f in os.listdir(tmp_path) if ".extsort." in f]
+
+
+@pytest.mark.parametrize("resident", [False, True])
+def test_extsort_descending_is_a_stable_reverse_order(resident):
+    """OrderByDescending out of core: inverted key bits for the sample, the range destinations and
+    every bucket sort; equal keys keep the source order (stable) -- against numpy."""
+    from dryad_amd.io.hosttable import HostRows
+    from dryad_amd.ops import extsort as EX
+    n, stride = 400_003, 24
+    g = np.random.default_rng(5)
+    a = g.integers(0, 256, size=(n, stride), dtype=np.uint8)
+    a[:, 2] = 7                                    # many equal 3-byte keys (ties)
+    src = HostRows.from_tensor(torch.from_numpy(a), key_off=0, key_len=3)
+    out = EX.external_sort(EX.HostRowsSource(src), 0, 3, budget=4 << 20, resident=resident, descending=True)
+    got = out.rows.numpy() if hasattr(out, "rows") else np.concatenate([x.cpu().numpy() for x in out.segments])
+    k_int = a[:, 0].astype(np.int64) << 16 | a[:, 1].astype(np.int64) << 8 | a[:, 2].astype(np.int64)
+    np.testing.assert_array_equal(got, a[np.argsort(-k_int, kind="stable")])
+
+
+def test_query_out_of_core_orderby_descending_to_host_table():
+    import dryad_amd as D
+    from dryad_amd.io.providers import provider_for
+    n = 800_000
+    ctx = D.DryadLinqContext(platform="gpu")
+    ctx.HbmBudgetBytes = 48 << 20
+    src = f"gen://terasort?records={n}&partitions=1&seed=11"
+    ctx.FromStore(src).OrderByDescending(lambda r: r[0:10]).ToStore("host://ooc_desc", delete_if_exists=True) \
+        .SubmitAndWait()
+    res = ctx._get_executor().last_result
+    assert res["external_sort"] is not None and res["external_sort"].buckets > 1 and not res["fallbacks"]
+    h = provider_for("host://ooc_desc").local_rows("host://ooc_desc", 0)
+    ref = _in_hbm_sorted(_gen_rows(n))
+    assert torch.equal(h.rows, ref.flip(0))        # distinct TeraSort keys: exactly the reverse
+    provider_for("host://ooc_desc").delete("host://ooc_desc")
