@@ -19,7 +19,6 @@ namespace {
 
 constexpr uint32_t kTmCap = 1024;                  // rows of one bucket a workgroup orders
 constexpr uint32_t kTmMaxW = 64;                   // sources
-constexpr uint32_t kTmWords = 25;                  // 100-byte rows
 constexpr uint32_t kTmThreads = 512;
 constexpr uint32_t kTmRows = kTmCap / kTmThreads;  // rows per lane, held in registers (2 x 25 dwords)
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(4)));   // 16-byte access, 4-byte aligned
@@ -68,18 +67,44 @@ __global__ __launch_bounds__(256) void ts_fine_starts_kernel(const E64* __restri
   }
 }
 
-// Key bits [fb, 80) of a 100-byte row (fb >= 16: they fit 64 bits), left-aligned.
+// Key bits [fb, 80) of a row whose first 10 bytes are the key (fb >= 16: they fit 64 bits),
+// left-aligned.
 __device__ __forceinline__ uint64_t tm_key(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t fb) {
   const uint64_t k0 = ((uint64_t)bswap32(w0) << 32) | bswap32(w1);
   const uint64_t k1 = (uint64_t)(bswap32(w2) >> 16);                  // key bytes 8, 9
   return (k0 << fb) | ((k1 << 48) >> (64 - fb));
 }
 
-// Rows of one bucket staged in LDS at the record pitch (two workgroups per CU: 79.4 KB each).
+// The same key for a row whose key is `klen` <= 10 bytes at byte `koff` (read byte by byte, the
+// missing bytes zero: equal keys compare equal, so ties keep their (source, position) order), its
+// bits inverted for a descending sort (`desc`): the order the window-sorted E64 entries and the fine
+// buckets of an inverted key define.
+__device__ __forceinline__ uint64_t tm_key_at(const uint8_t* r, uint32_t koff, uint32_t klen, bool desc, uint32_t fb) {
+  uint64_t k0 = 0;
+  uint32_t k1 = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 10; ++j) {
+    uint32_t b = j < klen ? (uint32_t)r[koff + j] : 0u;
+    if (desc && j < klen) b ^= 0xFFu;
+    if (j < 8) k0 = (k0 << 8) | b;
+    else k1 = (k1 << 8) | b;
+  }
+  return (k0 << fb) | (((uint64_t)k1 << 48) >> (64 - fb));
+}
+
+// Key of staged / loaded row `r`: the TeraSort layout (10-byte key at byte 0, ascending) from its
+// first three words, any other key spec (kspec = koff | klen << 8 | desc << 16) byte by byte.
+template <bool GEN>
+__device__ __forceinline__ uint64_t tm_row_key(const uint32_t* r, uint32_t kspec, uint32_t fb) {
+  if (!GEN) return tm_key(r[0], r[1], r[2], fb);
+  return tm_key_at(reinterpret_cast<const uint8_t*>(r), kspec & 0xFFu, (kspec >> 8) & 0xFFu, (kspec >> 16) & 1u, fb);
+}
+
+// Rows of one bucket staged in LDS at the record pitch (100-byte rows: two workgroups per CU,
+// 79.4 KB each; 128-byte rows: one, 99 KB).
 constexpr uint32_t kTsStage = 736;
 constexpr uint32_t kTsBins = 256;                  // staged path: next 8 key bits
 constexpr uint32_t kTsPasses = (kTsStage + 63) / 64;
-constexpr uint32_t kTsPoolWords = kTsStage * kTmWords + kTsStage + 2 * kTsBins;
 
 // pre[s * K + k] = row (of `rows`) where bucket k's slice from source s starts, cnt[s * K + k] its
 // rows; bucket k's output rows start at out row outoff[k].  A workgroup orders buckets
@@ -98,14 +123,18 @@ constexpr uint32_t kTsPoolWords = kTsStage * kTmWords + kTsStage + 2 * kTsBins;
 // kTsStage < nt <= kTmCap (a rare large bucket): left to ts_tile_merge_big_kernel.  A bucket of
 // more than kTmCap rows is skipped and flagged (*overflow); the caller orders that key range
 // another way.
-__global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4))) void ts_tile_merge_kernel(const uint32_t* __restrict__ rows,
+template <uint32_t RW, bool GEN>
+__global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(RW <= 25 ? 4 : 2))) void ts_tile_merge_kernel(const uint32_t* __restrict__ rows,
                                                                    uint32_t* __restrict__ out,
                                                                    const int64_t* __restrict__ pre,
                                                                    const int32_t* __restrict__ cnt,
                                                                    const int64_t* __restrict__ outoff, uint32_t W,
                                                                    uint32_t K, uint32_t fb,
-                                                                   uint32_t* __restrict__ overflow) {
-  __shared__ __attribute__((aligned(16))) uint32_t pool[kTsPoolWords];
+                                                                   uint32_t* __restrict__ overflow, uint32_t kspec) {
+  constexpr uint32_t P = (RW + 3) / 4;              // 16-byte pieces per row (the last may be partial)
+  constexpr uint32_t kPoolWords = kTsStage * RW + kTsStage + 2 * kTsBins;
+  static_assert(P <= 8, "rows of at most 128 bytes");
+  __shared__ __attribute__((aligned(16))) uint32_t pool[kPoolWords];
   __shared__ int64_t sbase[2][kTmMaxW];
   __shared__ uint32_t spre[2][kTmMaxW + 1];
   __shared__ int64_t sout[2];
@@ -113,9 +142,9 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
   const uint32_t t = threadIdx.x;
   const uint32_t G = gridDim.x;
   uint32_t* stage = pool;
-  uint16_t* member = reinterpret_cast<uint16_t*>(pool + kTsStage * kTmWords);
+  uint16_t* member = reinterpret_cast<uint16_t*>(pool + kTsStage * RW);
   uint16_t* perm = member + kTsStage;
-  uint32_t* bcnt = pool + kTsStage * kTmWords + kTsStage;
+  uint32_t* bcnt = pool + kTsStage * RW + kTsStage;
   uint32_t* bcur = bcnt + kTsBins;
   const uint32_t g = t >> 3, sub = t & 7;
 
@@ -146,11 +175,16 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
     for (uint32_t p = 0; p < kTsPasses; ++p) {
       const uint32_t i = g + 64 * p;
-      if (i < nt && sub < 7) {
+      if (i < nt && sub < P) {
         while (spre[buf][s + 1] <= i) ++s;
-        const uint32_t* src = rows + (uint64_t)(sbase[buf][s] + (int64_t)(i - spre[buf][s])) * kTmWords + sub * 4;
-        if (sub < 6) v[p] = *reinterpret_cast<const u32x4u*>(src);
-        else v[p].x = src[0];
+        const uint32_t* src = rows + (uint64_t)(sbase[buf][s] + (int64_t)(i - spre[buf][s])) * RW + sub * 4;
+        if ((sub + 1) * 4 <= RW) {
+          v[p] = *reinterpret_cast<const u32x4u*>(src);
+        } else {                                   // the row's last, partial piece: never read past it
+          v[p].x = src[0];
+          if (RW % 4 > 1) v[p].y = src[1];
+          if (RW % 4 > 2) v[p].z = src[2];
+        }
       }
     }
   };
@@ -177,13 +211,16 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
       for (uint32_t p = 0; p < kTsPasses; ++p) {
         const uint32_t i = g + 64 * p;
-        if (i < nt && sub < 7) {
-          uint32_t* d = stage + i * kTmWords + sub * 4;
+        if (i < nt && sub < P) {
+          uint32_t* d = stage + i * RW + sub * 4;
           d[0] = v[p].x;
-          if (sub < 6) {
+          if ((sub + 1) * 4 <= RW) {
             d[1] = v[p].y;
             d[2] = v[p].z;
             d[3] = v[p].w;
+          } else {
+            if (RW % 4 > 1) d[1] = v[p].y;
+            if (RW % 4 > 2) d[2] = v[p].z;
           }
         }
       }
@@ -193,10 +230,10 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
     if (k + G < K && nt2 <= kTsStage) rows_load(b ^ 1, nt2);     // in flight while bucket k is ordered
     if (nt > kTmCap && t == 0) atomicOr(overflow, 1u);
     if (staged) {
-      uint32_t* o = out + (uint64_t)ob * kTmWords;
+      uint32_t* o = out + (uint64_t)ob * RW;
       for (uint32_t i = t; i < nt; i += kTmThreads) {
-        const uint32_t* r = stage + i * kTmWords;
-        atomicAdd(&bcnt[(uint32_t)(tm_key(r[0], r[1], r[2], fb) >> 56)], 1u);
+        const uint32_t* r = stage + i * RW;
+        atomicAdd(&bcnt[(uint32_t)(tm_row_key<GEN>(r, kspec, fb) >> 56)], 1u);
       }
       __syncthreads();
       uint32_t c = 0, inc = 0;
@@ -213,19 +250,19 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
       }
       __syncthreads();
       for (uint32_t i = t; i < nt; i += kTmThreads) {
-        const uint32_t* r = stage + i * kTmWords;
-        member[atomicAdd(&bcur[(uint32_t)(tm_key(r[0], r[1], r[2], fb) >> 56)], 1u)] = (uint16_t)i;
+        const uint32_t* r = stage + i * RW;
+        member[atomicAdd(&bcur[(uint32_t)(tm_row_key<GEN>(r, kspec, fb) >> 56)], 1u)] = (uint16_t)i;
       }
       __syncthreads();
       for (uint32_t i = t; i < nt; i += kTmThreads) {   // slot = bin start + smaller (key, index) in the bin
-        const uint32_t* r = stage + i * kTmWords;
-        const uint64_t a = tm_key(r[0], r[1], r[2], fb);
+        const uint32_t* r = stage + i * RW;
+        const uint64_t a = tm_row_key<GEN>(r, kspec, fb);
         const uint32_t d = (uint32_t)(a >> 56), end = bcur[d], beg = end - bcnt[d];
         uint32_t slot = beg;
         for (uint32_t m = beg; m < end; ++m) {
           const uint32_t x = member[m];
-          const uint32_t* q = stage + x * kTmWords;
-          const uint64_t bb = tm_key(q[0], q[1], q[2], fb);
+          const uint32_t* q = stage + x * RW;
+          const uint64_t bb = tm_row_key<GEN>(q, kspec, fb);
           slot += (bb < a || (bb == a && x < i)) ? 1u : 0u;
         }
         perm[slot] = (uint16_t)i;
@@ -234,13 +271,18 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll 4
       for (uint32_t p = 0; p < kTsPasses; ++p) {
         const uint32_t jj = g + 64 * p;
-        if (jj < nt && sub < 7) {
-          const uint32_t* sr = stage + (uint32_t)perm[jj] * kTmWords + sub * 4;
-          uint32_t* dst = o + jj * kTmWords + sub * 4;
+        if (jj < nt && sub < P) {
+          const uint32_t* sr = stage + (uint32_t)perm[jj] * RW + sub * 4;
+          uint32_t* dst = o + jj * RW + sub * 4;
           // plain stores: the bucket's first and last lines are partial, completed in L2 by the
           // neighbouring buckets (nontemporal stores write partial lines through)
-          if (sub < 6) *reinterpret_cast<u32x4u*>(dst) = u32x4u{sr[0], sr[1], sr[2], sr[3]};
-          else dst[0] = sr[0];
+          if ((sub + 1) * 4 <= RW) {
+            *reinterpret_cast<u32x4u*>(dst) = u32x4u{sr[0], sr[1], sr[2], sr[3]};
+          } else {
+            dst[0] = sr[0];
+            if (RW % 4 > 1) dst[1] = sr[1];
+            if (RW % 4 > 2) dst[2] = sr[2];
+          }
         }
       }
     }
@@ -253,9 +295,11 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
 // FINE_ROWS) that ts_tile_merge_kernel leaves: each workgroup scans 512 buckets' sizes, lists the
 // large ones in LDS and orders them with the register path -- lane t holds tile rows t and t + 512
 // (6 x 16 + 4 bytes each), ranks by the next 10 key bits, rows stored to their slots.
+template <uint32_t RW, bool GEN>
 __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4))) void ts_tile_merge_big_kernel(
     const uint32_t* __restrict__ rows, uint32_t* __restrict__ out, const int64_t* __restrict__ pre,
-    const int32_t* __restrict__ cnt, const int64_t* __restrict__ outoff, uint32_t W, uint32_t K, uint32_t fb) {
+    const int32_t* __restrict__ cnt, const int64_t* __restrict__ outoff, uint32_t W, uint32_t K, uint32_t fb,
+    uint32_t kspec) {
   __shared__ uint64_t key[kTmCap];
   __shared__ uint16_t member[kTmCap];
   __shared__ uint16_t rnk[kTmCap];
@@ -292,21 +336,25 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
     }
     __syncthreads();
     const uint32_t nt = spre[W];
-    uint32_t* o = out + (uint64_t)outoff[k] * kTmWords;
+    constexpr uint32_t F = RW / 4, T = RW % 4;       // full 16-byte pieces, tail words per row
+    uint32_t* o = out + (uint64_t)outoff[k] * RW;
     bcnt[t] = 0;
     bcnt[t + kTmThreads] = 0;
-    u32x4u v[kTmRows][6];
-    uint32_t tail[kTmRows];
+    u32x4u v[kTmRows][F > 0 ? F : 1];
+    uint32_t tail[kTmRows][T > 0 ? T : 1];
+    uint64_t gkey[kTmRows];                          // GEN: the key read from the row in HBM
 #pragma unroll
     for (uint32_t h = 0; h < kTmRows; ++h) {
       const uint32_t i = t + h * kTmThreads;        // tile row: source-major = stable
       if (i < nt) {
         uint32_t s = 0;
         while (spre[s + 1] <= i) ++s;
-        const uint32_t* src = rows + (uint64_t)(sbase[s] + (int64_t)(i - spre[s])) * kTmWords;
+        const uint32_t* src = rows + (uint64_t)(sbase[s] + (int64_t)(i - spre[s])) * RW;
 #pragma unroll
-        for (int q = 0; q < 6; ++q) v[h][q] = *reinterpret_cast<const u32x4u*>(src + 4 * q);
-        tail[h] = src[24];
+        for (uint32_t q = 0; q < F; ++q) v[h][q] = *reinterpret_cast<const u32x4u*>(src + 4 * q);
+#pragma unroll
+        for (uint32_t q = 0; q < T; ++q) tail[h][q] = src[4 * F + q];
+        if (GEN) gkey[h] = tm_row_key<true>(src, kspec, fb);
       }
     }
     __syncthreads();
@@ -314,7 +362,9 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
     for (uint32_t h = 0; h < kTmRows; ++h) {
       const uint32_t i = t + h * kTmThreads;
       if (i < nt) {
-        const uint64_t kv = tm_key(v[h][0].x, v[h][0].y, v[h][0].z, fb);   // the top 10 bits pick the bin
+        const uint64_t kv = GEN ? gkey[h]                  // the top 10 bits pick the bin
+                                : F > 0 ? tm_key(v[h][0].x, v[h][0].y, v[h][0].z, fb)
+                                        : tm_key(tail[h][0], tail[h][T > 1 ? 1 : 0], tail[h][T > 2 ? 2 : 0], fb);
         key[i] = kv;
         atomicAdd(&bcnt[(uint32_t)(kv >> 54)], 1u);
       }
@@ -349,10 +399,11 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
     for (uint32_t h = 0; h < kTmRows; ++h) {
       const uint32_t i = t + h * kTmThreads;
       if (i < nt) {
-        uint32_t* dst = o + (uint32_t)rnk[i] * kTmWords;
+        uint32_t* dst = o + (uint32_t)rnk[i] * RW;
 #pragma unroll
-        for (int q = 0; q < 6; ++q) *reinterpret_cast<u32x4u*>(dst + 4 * q) = v[h][q];
-        dst[24] = tail[h];
+        for (uint32_t q = 0; q < F; ++q) *reinterpret_cast<u32x4u*>(dst + 4 * q) = v[h][q];
+#pragma unroll
+        for (uint32_t q = 0; q < T; ++q) dst[4 * F + q] = tail[h][q];
       }
     }
     __syncthreads();
@@ -370,13 +421,15 @@ __global__ __launch_bounds__(kTmThreads) __attribute__((amdgpu_waves_per_eu(4)))
 // tile leaves as contiguous 16-byte nontemporal stores.  ``err`` (nullable): the look-back sort's
 // error word; non-zero means the entries are not a permutation, and nothing is read.  An index
 // past n_in (a broken caller) is not dereferenced: the row is zero-filled and *bad is set.
-template <int PW>
+template <int PW, int OW>
 __global__ __launch_bounds__(256) void ts_pack_rows_kernel(const uint32_t* __restrict__ rows, uint64_t n_in,
                                                            const E64* __restrict__ ent, uint64_t n,
                                                            const int64_t* __restrict__ seg, uint32_t nseg,
                                                            uint32_t* __restrict__ out, const int32_t* __restrict__ err,
                                                            uint32_t* __restrict__ bad) {
-  __shared__ __attribute__((aligned(16))) uint32_t stage[256 * kTmWords];
+  constexpr uint32_t P = (OW + 3) / 4;             // 16-byte pieces per row (the last may be partial)
+  static_assert(P <= 8 && PW >= OW, "rows of at most 128 bytes");
+  __shared__ __attribute__((aligned(16))) uint32_t stage[256 * OW];
   __shared__ uint32_t sidx[256];
   __shared__ int64_t sseg[256][2];
   const uint32_t t = threadIdx.x;
@@ -408,38 +461,43 @@ __global__ __launch_bounds__(256) void ts_pack_rows_kernel(const uint32_t* __res
       for (int k = 0; k < 8; ++k) {
         const uint32_t r = g + 32 * k;
         buf[k] = u32x4u{0u, 0u, 0u, 0u};
-        if (r < rows_here && sub < 7 && sidx[r] != 0xFFFFFFFFu) {
+        if (r < rows_here && sub < P && sidx[r] != 0xFFFFFFFFu) {
           const uint32_t* src = rows + (uint64_t)sidx[r] * PW + sub * 4;
-          if (PW == 32) {
+          if (PW == 32) {                      // line-aligned input: whole 16-byte pieces are there
             const uint4* s4 = reinterpret_cast<const uint4*>(src);
             buf[k].x = __builtin_nontemporal_load(&s4->x);
             buf[k].y = __builtin_nontemporal_load(&s4->y);
             buf[k].z = __builtin_nontemporal_load(&s4->z);
             buf[k].w = __builtin_nontemporal_load(&s4->w);
-          } else if (sub < 6) {
+          } else if ((sub + 1) * 4 <= (uint32_t)OW) {
             buf[k] = *reinterpret_cast<const u32x4u*>(src);
-          } else {
-            buf[k].x = src[0];                 // word 24: never read past the row
+          } else {                             // the row's last, partial piece: never read past it
+            buf[k].x = src[0];
+            if (OW % 4 > 1) buf[k].y = src[1];
+            if (OW % 4 > 2) buf[k].z = src[2];
           }
         }
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const uint32_t r = g + 32 * k;
-        if (r < rows_here && sub < 7) {
-          uint32_t* d = stage + r * kTmWords + sub * 4;
+        if (r < rows_here && sub < P) {
+          uint32_t* d = stage + r * OW + sub * 4;
           d[0] = buf[k].x;
-          if (sub < 6) {
+          if ((sub + 1) * 4 <= (uint32_t)OW) {
             d[1] = buf[k].y;
             d[2] = buf[k].z;
             d[3] = buf[k].w;
+          } else {
+            if (OW % 4 > 1) d[1] = buf[k].y;
+            if (OW % 4 > 2) d[2] = buf[k].z;
           }
         }
       }
     }
     __syncthreads();
-    uint32_t* o = out + row0 * kTmWords;
-    const uint32_t words = rows_here * kTmWords;
+    uint32_t* o = out + row0 * OW;
+    const uint32_t words = rows_here * OW;
     uint32_t head = (4u - (uint32_t)((reinterpret_cast<uintptr_t>(o) >> 2) & 3u)) & 3u;
     head = head < words ? head : words;
     if (t < head) o[t] = stage[t];
@@ -472,25 +530,47 @@ __global__ __launch_bounds__(256) void ts_pack_rows_kernel(const uint32_t* __res
 // alignment); out: n rows of 100 bytes; seg: nseg <= 256 segments {out row, entry} (device int64
 // [nseg][2], seg[0].out = 0, ascending), or nseg = 0 for q(p) = p; err: look-back error word
 // (nullable); bad: set when an entry's row index is out of range.
-DR_API int dr_ts_pack_rows(const uint8_t* rows, uint64_t n_in, uint32_t pitch, const E64* ent, uint64_t n,
-                           const int64_t* seg, uint32_t nseg, uint8_t* out, const int32_t* err, uint32_t* bad,
-                           hipStream_t s) {
+namespace {
+
+// Rows of 4 * RW bytes, RW = 2 .. 32 (8-byte to 128-byte records), dispatched to their template.
+#define DR_TS_WIDTHS(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) \
+  X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
+
+int pack_rows_w(const uint8_t* rows, uint64_t n_in, uint32_t pitch, const E64* ent, uint64_t n, const int64_t* seg,
+                uint32_t nseg, uint8_t* out, uint32_t rec, const int32_t* err, uint32_t* bad, hipStream_t s) {
   if (n == 0) return 0;
   if (nseg > 256 || (nseg > 0 && seg == nullptr) || bad == nullptr) return (int)hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(rows)) & 3) return (int)hipErrorInvalidValue;
+  if (rec % 4 || rec < 8 || rec > 128 || (pitch != rec && pitch != 128)) return (int)hipErrorInvalidValue;
+  if (pitch == 128 && (reinterpret_cast<uintptr_t>(rows) & 15)) return (int)hipErrorInvalidValue;
   const unsigned g = grid_for(n, 256, 32768);
-  if (pitch == 128) {
-    if (reinterpret_cast<uintptr_t>(rows) & 15) return (int)hipErrorInvalidValue;
-    ts_pack_rows_kernel<32><<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows), n_in, ent, n, seg, nseg,
-                                              reinterpret_cast<uint32_t*>(out), err, bad);
-  } else if (pitch == 100) {
-    ts_pack_rows_kernel<25><<<g, 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows), n_in, ent, n, seg, nseg,
-                                              reinterpret_cast<uint32_t*>(out), err, bad);
-  } else {
-    return (int)hipErrorInvalidValue;
+  const uint32_t* in = reinterpret_cast<const uint32_t*>(rows);
+  uint32_t* o = reinterpret_cast<uint32_t*>(out);
+  const uint32_t ow = rec / 4;
+#define DR_TS_PACK(w)                                                                             \
+  if (ow == (w)) {                                                                                \
+    if (pitch == 128) ts_pack_rows_kernel<32, (w)><<<g, 256, 0, s>>>(in, n_in, ent, n, seg, nseg, o, err, bad); \
+    else ts_pack_rows_kernel<(w), (w)><<<g, 256, 0, s>>>(in, n_in, ent, n, seg, nseg, o, err, bad);            \
   }
+  DR_TS_WIDTHS(DR_TS_PACK)
+#undef DR_TS_PACK
   DR_LAUNCH_CHECK();
   return 0;
+}
+
+}  // namespace
+
+DR_API int dr_ts_pack_rows(const uint8_t* rows, uint64_t n_in, uint32_t pitch, const E64* ent, uint64_t n,
+                           const int64_t* seg, uint32_t nseg, uint8_t* out, const int32_t* err, uint32_t* bad,
+                           hipStream_t s) {
+  return pack_rows_w(rows, n_in, pitch, ent, n, seg, nseg, out, 100, err, bad, s);
+}
+
+// dr_ts_pack_rows for records of `rec` bytes (a multiple of 4, 8..128) at `pitch` (rec or 128).
+DR_API int dr_ts_pack_rows_w(const uint8_t* rows, uint64_t n_in, uint32_t pitch, const E64* ent, uint64_t n,
+                             const int64_t* seg, uint32_t nseg, uint8_t* out, uint32_t rec, const int32_t* err,
+                             uint32_t* bad, hipStream_t s) {
+  return pack_rows_w(rows, n_in, pitch, ent, n, seg, nseg, out, rec, err, bad, s);
 }
 
 // starts: (1 << fb) + 1 uint32 = for each fine bucket k the first position of `ent` (sorted on
@@ -510,18 +590,45 @@ DR_API uint32_t dr_ts_tile_cap() { return kTmCap; }
 
 // rows / out: 100-byte rows (4-byte aligned); pre, cnt: [W][K]; outoff: [K]; 16 <= fb <= 24 (the
 // caller's FINE_MIN_BITS..FINE_MAX_BITS).  A bucket past kTmCap rows is flagged, never ordered.
+// dr_ts_tile_merge for records of `rec` bytes (a multiple of 4, 12..128) ordered by the key of
+// `key_len` <= 10 bytes at byte `key_off` (descending: `desc`).  The TeraSort layout (10-byte key
+// at byte 0, ascending) reads the key as three words; any other as bytes.
+DR_API int dr_ts_tile_merge_w(const uint8_t* rows, uint8_t* out, const int64_t* pre, const int32_t* cnt,
+                              const int64_t* outoff, uint32_t W, uint32_t K, uint32_t fb, uint32_t* overflow,
+                              uint32_t rec, uint32_t key_off, uint32_t key_len, uint32_t desc, hipStream_t s) {
+  if (W == 0 || W > kTmMaxW || fb < 16 || fb > 24) return (int)hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(out)) & 3) return (int)hipErrorInvalidValue;
+  if (rec % 4 || rec < 12 || rec > 128) return (int)hipErrorInvalidValue;
+  if (key_len < 1 || key_len > 10 || key_off + key_len > rec) return (int)hipErrorInvalidValue;
+  if (K == 0) return 0;
+  const unsigned g = K < 65536u ? K : 65536u;
+  const uint32_t* in = reinterpret_cast<const uint32_t*>(rows);
+  uint32_t* o = reinterpret_cast<uint32_t*>(out);
+  const uint32_t rw = rec / 4;
+  const unsigned gb = (K + kTmThreads - 1) / kTmThreads;
+  const bool gen = !(key_off == 0 && key_len == 10 && !desc);
+  const uint32_t kspec = key_off | (key_len << 8) | ((desc ? 1u : 0u) << 16);
+#define DR_TS_MERGE(w)                                                                               \
+  if (rw == (w) && (w) >= 3) {                                                                       \
+    constexpr uint32_t RWC = (w) >= 3 ? (w) : 3;                                                     \
+    if (gen) {                                                                                       \
+      ts_tile_merge_kernel<RWC, true><<<g, kTmThreads, 0, s>>>(in, o, pre, cnt, outoff, W, K, fb, overflow, kspec); \
+      DR_LAUNCH_CHECK();                                                                             \
+      ts_tile_merge_big_kernel<RWC, true><<<gb, kTmThreads, 0, s>>>(in, o, pre, cnt, outoff, W, K, fb, kspec);      \
+    } else {                                                                                         \
+      ts_tile_merge_kernel<RWC, false><<<g, kTmThreads, 0, s>>>(in, o, pre, cnt, outoff, W, K, fb, overflow, kspec); \
+      DR_LAUNCH_CHECK();                                                                             \
+      ts_tile_merge_big_kernel<RWC, false><<<gb, kTmThreads, 0, s>>>(in, o, pre, cnt, outoff, W, K, fb, kspec);     \
+    }                                                                                                \
+    DR_LAUNCH_CHECK();                                                                               \
+  }
+  DR_TS_WIDTHS(DR_TS_MERGE)
+#undef DR_TS_MERGE
+  return 0;
+}
+
 DR_API int dr_ts_tile_merge(const uint8_t* rows, uint8_t* out, const int64_t* pre, const int32_t* cnt,
                             const int64_t* outoff, uint32_t W, uint32_t K, uint32_t fb, uint32_t* overflow,
                             hipStream_t s) {
-  if (W == 0 || W > kTmMaxW || fb < 16 || fb > 24) return (int)hipErrorInvalidValue;
-  if ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(out)) & 3) return (int)hipErrorInvalidValue;
-  if (K == 0) return 0;
-  const unsigned g = K < 65536u ? K : 65536u;
-  ts_tile_merge_kernel<<<g, kTmThreads, 0, s>>>(reinterpret_cast<const uint32_t*>(rows),
-                                                reinterpret_cast<uint32_t*>(out), pre, cnt, outoff, W, K, fb, overflow);
-  DR_LAUNCH_CHECK();
-  ts_tile_merge_big_kernel<<<(K + kTmThreads - 1) / kTmThreads, kTmThreads, 0, s>>>(
-      reinterpret_cast<const uint32_t*>(rows), reinterpret_cast<uint32_t*>(out), pre, cnt, outoff, W, K, fb);
-  DR_LAUNCH_CHECK();
-  return 0;
+  return dr_ts_tile_merge_w(rows, out, pre, cnt, outoff, W, K, fb, overflow, 100, 0, 10, 0, s);
 }

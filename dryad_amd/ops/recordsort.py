@@ -341,11 +341,30 @@ def _check_capacity(n_recv: int, cap: int, w: World):
 
 
 def fine_rows_ok(rec: int, pitch: int, key_off: int, key_len: int, W: int, n: int, one_rank: bool = False) -> bool:
-    """The fine-bucket exchange applies: 100-byte records keyed by bytes 0..9 (TeraSort rows),
-    stored at a 100- or 128-byte pitch, 2..64 ranks (sources per merged bucket; ``one_rank``: a
-    one-rank world that still exchanges through its communicator)."""
-    return ((1 < W or (one_rank and W == 1)) and W <= 64 and key_off == 0 and key_len == TSG.KEY_BYTES and rec == TSG.RECORD_BYTES
-            and pitch in (TSG.RECORD_BYTES, 128) and n < (1 << 31))
+    """The fine-bucket exchange applies: fixed-width records of 12..128 bytes (a multiple of 4)
+    keyed by a byte string of at most 10 bytes anywhere in the record (TeraSort rows: 100 bytes,
+    key bytes 0..9), stored back to back or at a 128-byte pitch, 2..64 ranks (sources per merged
+    bucket; ``one_rank``: a one-rank world that still exchanges through its communicator)."""
+    return ((1 < W or (one_rank and W == 1)) and W <= 64 and rec % 4 == 0 and 12 <= rec <= 128
+            and 1 <= key_len <= TSG.KEY_BYTES and 0 <= key_off and key_off + key_len <= rec
+            and pitch in (rec, 128) and n < (1 << 31))
+
+
+_WINDOW = _as_i64(0xFFFFFFFF00000000)
+
+
+def fine_entries(rows: torch.Tensor, key_off: int, key_len: int, e: torch.Tensor, descending: bool = False,
+                 hist: bool = True):
+    """E64 entries (key window << 32 | row) of ``rows`` for the fine-bucket exchange, with the
+    look-back sort's window histograms; ``descending``: the window bits inverted (and the
+    histograms mirrored), so the ascending sort, the separators and the fine buckets of the
+    inverted key order the rows descending (ts_tile_merge inverts the key alike)."""
+    e, h = S.extract_keys64_tile(rows, key_off, key_len, 0, e, hist=hist)
+    if descending:
+        e.bitwise_xor_(_WINDOW)
+        if h is not None:
+            h.copy_(h.view(-1, 4, 256).flip(-1).reshape(-1))
+    return e, h
 
 
 def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int, world: World | None = None,
@@ -404,7 +423,7 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
     if descending:
         hi_bounds = None              # bounds of the ascending keys
     gen_path = gen is not None and fine_rows_ok(rec, pitch, key_off, key_len, W, n, w.force_collectives) \
-        and pitch == rec and not descending
+        and pitch == rec and not descending and (rec, key_off, key_len) == (TSG.RECORD_BYTES, 0, TSG.KEY_BYTES)
     if gen is not None and not gen_path:
         TSG.generate(bufs.rows_in[:n], gen[0], gen[1])       # the records are needed after all
         gen = None
@@ -427,8 +446,9 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
             stats.n_in = stats.n_out = n
             stats.path = "local"
         return out
-    fine_rows = gen is None and fine_rows_ok(rec, pitch, key_off, key_len, W, n, w.force_collectives) \
-        and not descending
+    fine_rows = gen is None and fine_rows_ok(rec, pitch, key_off, key_len, W, n, w.force_collectives)
+    if descending and keys_fmt != "e128":
+        keys_ready = False              # a producer's entries hold the ascending key
     if pitch != bufs.pitch and not fine_rows:
         raise ValueError("distributed_sort_rows: a src table needs a buffer set at its record width")
     if pitch != rec and not fine_rows:
@@ -452,7 +472,7 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
             e, tmp = bufs.entry_pair(n, in_out=in_out)
             hist = S.take_gen_hist(e) if keys_ready and keys_fmt in ("e64", "e64@out") else None
             if hist is None and not (keys_ready and keys_fmt in ("e64", "e64@out")):
-                e, hist = S.extract_keys64_tile(rows, key_off, key_len, 0, e, hist=True)
+                e, hist = fine_entries(rows, key_off, key_len, e, descending)
             samp = e64_samples(e, n, w.rank, sample_target, seed)
         else:
             if keys_fmt != "e128":
@@ -474,13 +494,15 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
             seps = separators_from_samples(shuffle.all_gather_varlen(samp, w), W * B)
             fb = fine_bits(nmax * W)
             seps_hi = [int(x) & _M64 for x in seps[:, 1].tolist()]
-            if fine_rows and split and _fine_collapsed(seps_hi, fb) and bufs.ent_b.numel() >= 2 * n:
+            if fine_rows and split and _fine_collapsed(seps_hi, fb) and bufs.ent_b.numel() >= 2 * n and pitch == rec:
                 # heavy duplication: two separators inside one fine bucket.  The fine cut would give
                 # the whole bucket to one rank; the E128 path splits runs of equal keys (key, rank,
                 # row) instead.  The separators are global, so every rank switches alike.
                 fine_rows = False
                 B = pipeline_subs(nmax * rec, W)        # (the E128 path: world * rounds <= 256)
                 ent = S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])
+                if descending:
+                    invert_keys(ent, key_len)
                 ent[:, 0].bitwise_or_(lo_or)
                 seps = choose_separators(ent, n, w, part_mask, sample_target, seed, bufs.ent_b, parts=W * B)
                 seps_hi = [int(x) & _M64 for x in seps[:, 1].tolist()]
@@ -489,7 +511,7 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
             if fine_rows:
                 # the rows are packed round by round in the exchange below, each just before it goes out
                 plan = FineSend(bufs, rows, e, tmp, hist, n, seps_hi, B, W, fb,
-                                rebuild=lambda: S.extract_keys64_tile(rows, key_off, key_len, 0, e)[0])
+                                rebuild=lambda: fine_entries(rows, key_off, key_len, e, descending, hist=False)[0])
                 st, counts, L = plan.st, plan.counts, plan.L
         else:
             seps = choose_separators(ent, n, w, part_mask, sample_target, seed, bufs.ent_b, parts=W * B)
@@ -532,7 +554,8 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
                   arrive=[torch.cuda.Event(enable_timing=True) for _ in range(B)], entry=entry)
         ev["start"].record()
     if plan is not None:
-        ov = _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, n_sent, ev, key_len)
+        ov = _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, n_sent, ev, key_off, key_len,
+                                       descending)
         if ov is None:                 # no room for the receive slots: pack everything, then exchange
             for b in range(B):
                 plan.pack(b)
@@ -583,7 +606,8 @@ def _bulk_exchange(bufs, rb, st, send, off, rc, B, W, w, pack, fine, L, fb, n_se
             ev["arrive"][b].record()
     sent_after = [st[(b + 1) * W] for b in range(B)]
     if fine is not None:
-        return merge_received_rounds(rb, off, fine, L, fb, B, w.rank, sent_after, n_sent, wait=wait)
+        return merge_received_rounds(rb, off, fine, L, fb, B, w.rank, sent_after, n_sent, wait=wait, key_off=key_off,
+                                     key_len=key_len, descending=descending)
     return sort_received_rounds(rb, off, sent_after, n_sent, seps_hi, B, w.rank, key_off, key_len, wait=wait,
                                 descending=descending)
 
@@ -653,7 +677,8 @@ def overlap_model(t_ready: float, pack_ms: list, merge_ms: list, wire_ms: list, 
     return dict(step_ms=comp, first_queued_ms=first, wire_idle_ms=idle, wire_end_ms=comm)
 
 
-def _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, n_sent, ev, key_len):
+def _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, n_sent, ev, key_off, key_len,
+                              descending=False):
     """The fine-bucket exchange with the send side overlapped: round i's send rows are packed
     (plan.pack(i)) just before its all-to-all-v is queued, so the first round is on the wire after
     1/B of the pack instead of all of it.  The input table must stay readable until the last pack,
@@ -685,7 +710,7 @@ def _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, 
         return None
     slot_t = [tail[i * slot_rows * rec: (i + 1) * slot_rows * rec].view(slot_rows, rec) for i in range(in_tail)]
     slot_t += [extra[i * slot_rows: (i + 1) * slot_rows] for i in range(NS - in_tail)]
-    merger = FineMerge(fine, plan.L, fb, B, w.rank, out_buf)
+    merger = FineMerge(fine, plan.L, fb, B, w.rank, out_buf, key_off, key_len, descending)
     cuda = out_buf.is_cuda
     flags_host = torch.zeros(B, dtype=torch.int32, pin_memory=cuda)
     merged_ev = [None] * B
@@ -717,8 +742,8 @@ def _overlapped_fine_exchange(plan, rb, bufs, off, send, rc, fine, fb, B, W, w, 
             a, z = off[j], off[j + 1]
             ea = torch.empty((z - a, 2), dtype=torch.int64, device=out_buf.device)
             eb = torch.empty_like(ea)
-            local_sort_rows(slot_t[j % NS][: z - a], out_buf[a:z], ea, eb, 0, key_len,
-                            hi_bounds=fine_hi_bounds(plan.L, fb, w.rank * B + j))
+            local_sort_rows(slot_t[j % NS][: z - a], out_buf[a:z], ea, eb, key_off, key_len, descending=descending,
+                            hi_bounds=None if descending else fine_hi_bounds(plan.L, fb, w.rank * B + j))
             fixups.append(j)
 
     for i in range(B):
@@ -952,11 +977,14 @@ class FineMerge:
     source pieces in source order, each in bucket order.  ``merge(b, recv, base, a, z)``: the
     round's rows are ``recv[base: base + z - a]``; the slices of every bucket are located on the
     device (prefix sums of ``fine``) and ts_tile_merge orders each bucket in LDS into
-    ``out[a:z]``.  A bucket too large for LDS (heavy key skew) sets ``flags[b]``."""
+    ``out[a:z]`` by the key spec (``key_off``, ``key_len``, ``descending``).  A bucket too large
+    for LDS (heavy key skew) sets ``flags[b]``."""
 
-    def __init__(self, fine: torch.Tensor, L: list, fb: int, B: int, rank: int, out: torch.Tensor):
+    def __init__(self, fine: torch.Tensor, L: list, fb: int, B: int, rank: int, out: torch.Tensor,
+                 key_off: int = 0, key_len: int = 10, descending: bool = False):
         self.W, self.K = fine.shape
         W, K = self.W, self.K
+        self.key = dict(key_off=key_off, key_len=key_len, descending=descending)
         self.L, self.fb, self.B, self.rank, self.out = L, fb, B, rank, out
         dev = out.device
         self.flags = torch.zeros(B, dtype=torch.int32, device=dev)
@@ -1004,18 +1032,20 @@ class FineMerge:
         W = self.W
         pre = self.pre[W * k0: W * k1].view(W, k1 - k0)
         cnt = self.cnt[W * k0: W * k1].view(W, k1 - k0)
-        TSG.tile_merge(recv[base:], self.out[a:], pre, cnt, self.outoff[k0:k1], self.fb, self.flags[b:b + 1])
+        TSG.tile_merge(recv[base:], self.out[a:], pre, cnt, self.outoff[k0:k1], self.fb, self.flags[b:b + 1],
+                       **self.key)
 
 
 def merge_received_rounds(bufs: SortBuffers, off: list, fine: torch.Tensor, L: list, fb: int, B: int, rank: int,
-                          sent_after: list, n_sent: int, wait=None, key_len: int = 10) -> torch.Tensor:
+                          sent_after: list, n_sent: int, wait=None, key_off: int = 0, key_len: int = 10,
+                          descending: bool = False) -> torch.Tensor:
     """Receive side of the fine-bucket exchange when every round lands in place: round b's block
     ``rows_in[off[b]:off[b+1]]`` (FineMerge) is ordered into ``rows_out[off[b]:...]``, deferred
     until the send rows under it have gone out (``sent_after``, as in sort_received_rounds).  A
     round whose bucket outgrew LDS is sorted after the last round with local_sort_rows."""
     out = bufs.rows_out
     recv = bufs.recv_rows()
-    m = FineMerge(fine, L, fb, B, rank, out)
+    m = FineMerge(fine, L, fb, B, rank, out, key_off, key_len, descending)
     pending = []
     for b in range(B):
         if wait is not None:
@@ -1034,7 +1064,8 @@ def merge_received_rounds(bufs: SortBuffers, off: list, fine: torch.Tensor, L: l
         if fl[b]:
             a, z = off[b], off[b + 1]
             ea, eb = _round_scratch(bufs, off[-1], a, z)
-            local_sort_rows(recv[a:z], out[a:z], ea, eb, 0, key_len, hi_bounds=fine_hi_bounds(L, fb, rank * B + b))
+            local_sort_rows(recv[a:z], out[a:z], ea, eb, key_off, key_len, descending=descending,
+                            hi_bounds=None if descending else fine_hi_bounds(L, fb, rank * B + b))
     return out[: off[-1]]
 
 

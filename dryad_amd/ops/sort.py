@@ -457,7 +457,9 @@ def extract_keys64_tile(rows: torch.Tensor, key_off: int, key_len: int, prefix_b
     the window-digit histograms a following look-back sort takes instead of its histogram read.
     Returns (entries, histograms or None)."""
     _lib.require_gpu_tensor(rows, "extract_keys64_tile")
-    n, stride = rows.shape
+    n = rows.shape[0]
+    stride = rows.stride(0) if n > 1 else rows.shape[1]     # (a [n, rec] view of 128-byte-pitch rows)
+    assert rows.stride(1) == 1 and key_off + key_len <= rows.shape[1]
     part = None
     if hist and n >= ONESWEEP_MIN:
         part = gen_hist_buffer(int(_lib.lib().dr_extract_keys64_tile_parts(c_u64(n))), rows.device)

@@ -168,36 +168,48 @@ def tile_cap() -> int:
 
 
 def tile_merge(rows: torch.Tensor, out: torch.Tensor, pre: torch.Tensor, cnt: torch.Tensor, outoff: torch.Tensor,
-               fb: int, overflow: torch.Tensor) -> None:
+               fb: int, overflow: torch.Tensor, key_off: int = 0, key_len: int = 10, descending: bool = False) -> None:
     """Order the received fine buckets: bucket k's rows are the W slices ``rows[pre[s, k] :
     pre[s, k] + cnt[s, k]]`` (all sharing their top ``fb`` key bits), written in key order (ties by
-    source, then slice position) to ``out[outoff[k]:]``.  A bucket past tile_cap() rows is left
-    out and flags ``overflow``."""
+    source, then slice position) to ``out[outoff[k]:]``.  The key is the ``key_len`` <= 10 bytes at
+    byte ``key_off`` (memcmp order; its bits inverted with ``descending``, matching entries whose
+    window was inverted).  A bucket past tile_cap() rows is left out and flags ``overflow``."""
     W, K = cnt.shape
     assert pre.shape == (W, K) and pre.dtype == torch.int64 and cnt.dtype == torch.int32 and outoff.shape == (K,)
-    assert rows.shape[1] == RECORD_BYTES and out.shape[1] == RECORD_BYTES
-    _lib.call("dr_ts_tile_merge", ptr(rows), ptr(out), ptr(pre.contiguous()), ptr(cnt.contiguous()),
-              ptr(outoff.contiguous()), c_u32(W), c_u32(K), c_u32(fb), ptr(overflow), stream_of(rows))
+    rec = rows.shape[1]
+    # rows of any width (a multiple of 4 bytes, 12..128)
+    assert out.shape[1] == rec and rec % 4 == 0 and 12 <= rec <= 128 and rows.stride(0) == rec
+    assert 1 <= key_len <= 10 and 0 <= key_off and key_off + key_len <= rec
+    _lib.call("dr_ts_tile_merge_w", ptr(rows), ptr(out), ptr(pre.contiguous()), ptr(cnt.contiguous()),
+              ptr(outoff.contiguous()), c_u32(W), c_u32(K), c_u32(fb), ptr(overflow), c_u32(rec),
+              c_u32(key_off), c_u32(key_len), c_u32(int(bool(descending))), stream_of(rows))
     _lib.written(out)
 
 
 _lib.register_signatures({
-    "dr_ts_pack_rows": (ctypes.c_int, [ctypes.c_void_p, c_u64, c_u32, ctypes.c_void_p, c_u64, ctypes.c_void_p, c_u32,
-                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "dr_ts_pack_rows_w": (ctypes.c_int, [ctypes.c_void_p, c_u64, c_u32, ctypes.c_void_p, c_u64, ctypes.c_void_p,
+                                         c_u32, ctypes.c_void_p, c_u32, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
+    "dr_ts_tile_merge_w": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, c_u32, c_u32, c_u32, ctypes.c_void_p, c_u32,
+                                          c_u32, c_u32, c_u32, ctypes.c_void_p]),
 })
 
 
 def pack_rows(out: torch.Tensor, rows: torch.Tensor, ent: torch.Tensor, n: int, seg: torch.Tensor | None = None,
               err: torch.Tensor | None = None, bad: torch.Tensor | None = None) -> torch.Tensor:
     """Send rows of a materialised table: ``out[p]`` := ``rows[ent[q(p)] & 0xFFFFFFFF]`` for p < n
-    (``rows`` [n_in, 100] or [n_in, 128] uint8 holding 100-byte records, ``out`` [>= n, 100]);
+    (``rows`` [n_in, rec] or [n_in, 128] uint8 holding rec-byte records, rec a multiple of 4 in
+    8..128, ``out`` [>= n, rec]);
     q(p) = p, or through ``seg`` (device int64 [nseg <= 256, 2] of {out row, entry}, ascending,
     seg[0, 0] = 0).  ``err``: the look-back sort's error word (nothing is read when it is set);
     ``bad`` (int32 [1]) is set when an entry names a row past n_in.  Returns ``bad``."""
     _lib.require_gpu_tensor(out, "terasort.pack_rows")
     pitch = rows.stride(0)
-    assert rows.dtype == torch.uint8 and pitch in (100, 128) and rows.stride(1) == 1
-    assert out.dtype == torch.uint8 and out.shape[1] == RECORD_BYTES and out.is_contiguous() and out.shape[0] >= n
+    rec = out.shape[1]
+    assert rows.dtype == torch.uint8 and pitch in (rec, 128) and rows.stride(1) == 1
+    assert rec % 4 == 0 and 8 <= rec <= 128 and rows.shape[1] >= rec
+    assert out.dtype == torch.uint8 and out.is_contiguous() and out.shape[0] >= n
     assert ent.dtype == torch.int64 and ent.is_contiguous()
     nseg = 0
     if seg is not None:
@@ -208,7 +220,7 @@ def pack_rows(out: torch.Tensor, rows: torch.Tensor, ent: torch.Tensor, n: int, 
         assert ent.shape[0] >= n
     if bad is None:
         bad = torch.zeros(1, dtype=torch.int32, device=out.device)
-    _lib.call("dr_ts_pack_rows", ptr(rows), c_u64(rows.shape[0]), c_u32(pitch), ptr(ent), c_u64(n), ptr(seg),
-              c_u32(nseg), ptr(out), ptr(err), ptr(bad), stream_of(out))
+    _lib.call("dr_ts_pack_rows_w", ptr(rows), c_u64(rows.shape[0]), c_u32(pitch), ptr(ent), c_u64(n), ptr(seg),
+              c_u32(nseg), ptr(out), c_u32(rec), ptr(err), ptr(bad), stream_of(out))
     _lib.written(out)
     return bad

@@ -44,6 +44,42 @@ def _valsort(rows, w, expect_hash, expect_n):
     assert int(acc[0]) == expect_hash and int(acc[1]) == 0 and int(cnt) == expect_n, (acc.tolist(), int(cnt))
 
 
+def _rows64(w, base):
+    import numpy as np
+    from dryad_amd.io.providers import provider_for
+    from dryad_amd.runtime.jobmanager import write_schema
+    n, W = 250_000, w.size
+    g = np.random.default_rng(64)
+    rows = g.integers(0, 256, size=(W * n, 64), dtype=np.uint8)
+    key = g.integers(0, 1 << 63, size=W * n, dtype=np.uint64) * np.uint64(2) + np.uint64(1)
+    key[::50] = key[7]                                      # runs of equal keys
+    idx = np.arange(W * n, dtype=np.uint64)
+    rows[:, 8:16] = key.astype(">u8").view(np.uint8).reshape(-1, 8)
+    rows[:, 16:24] = idx.astype(">u8").view(np.uint8).reshape(-1, 8)
+    uri = f"partfile://{base}/rows64"
+    if w.rank == 0:
+        prov = provider_for(uri)
+        prov.write_table(uri, [rows[p * n: (p + 1) * n].tobytes() for p in range(W)], None)
+        write_schema(prov._path(uri), None, "rows", stride=64, key_off=8, key_len=8)
+    w.barrier()
+    ctx = D.DryadLinqContext(platform="gpu")
+    ctx.PartitionCount = W
+    for desc in (False, True):
+        q = ctx.FromStore(uri)
+        q = q.OrderByDescending(lambda r: r[8:16]) if desc else q.OrderBy(lambda r: r[8:16])
+        q.ToStore("hbm://rows64_out", delete_if_exists=True).SubmitAndWait()
+        res = ctx._get_executor().last_result
+        ex = res["exchange"]
+        assert ex is not None and "fine-bucket exchange over the table (pitch 64)" in ex["path"], (desc, ex)
+        got = provider_for("hbm://rows64_out").get("hbm://rows64_out")["local"][w.rank].rows.cpu().numpy()
+        counts = shuffle.all_gather_tensor(torch.tensor([got.shape[0]], dtype=torch.int64, device=w.device), w)
+        counts = counts.view(-1).tolist()
+        assert sum(counts) == W * n, counts
+        order = np.lexsort((idx, ~key if desc else key))
+        a = sum(counts[: w.rank])
+        assert np.array_equal(got, rows[order[a: a + got.shape[0]]]), (w.rank, desc)
+
+
 def main():
     w = init_world(device="cuda")
     n = int(os.environ.get("TS_RECORDS", "1500000"))
@@ -130,6 +166,11 @@ def main():
     out = RS.distributed_sort_rows(bufs, 200_000, 0, 10, w, stats=stt)
     assert "E128" in stt.path and abs(stt.n_out - 200_000) <= 2_000, (stt.path, stt.n_out)
     assert torch.equal(out[:, :10], torch.full_like(out[:, :10], 42))
+    # 5. a table of 64-byte rows keyed by bytes 8..15 (not the TeraSort layout), OrderBy and
+    # OrderByDescending through the query API: the fine-bucket exchange with the key read at its
+    # offset (inverted for the descending sort); every rank's output is its exact slice of the
+    # stable global order (ties by source rank, then row)
+    _rows64(w, base)
     w.barrier()
     if w.rank == 0:
         print("FINE_ROWS_OK", w.size, flush=True)

@@ -83,3 +83,17 @@ def test_fine_merge_of_a_rank_without_buckets():
     m = RS.FineMerge(torch.zeros((2, 0), dtype=torch.int32), L, 16, 4, 0, torch.empty((4, 100), dtype=torch.uint8))
     assert m.kb == [0] * 5 and m.pre.numel() == 0
     m.merge(0, torch.empty((0, 100), dtype=torch.uint8), 0, 0, 0)
+
+
+def test_fine_rows_ok_any_width_and_key():
+    from dryad_amd.ops import recordsort as RS
+    ok = lambda rec, pitch, ko, kl: RS.fine_rows_ok(rec, pitch, ko, kl, 8, 1000)  # noqa: E731
+    assert ok(100, 100, 0, 10) and ok(100, 128, 0, 10)            # TeraSort rows
+    assert ok(64, 64, 8, 8) and ok(12, 12, 0, 2) and ok(128, 128, 118, 10) and ok(64, 128, 0, 4)
+    assert not ok(64, 64, 8, 12)          # keys past 10 bytes: the E128 path
+    assert not ok(66, 66, 0, 8)           # rows not a multiple of 4 bytes
+    assert not ok(8, 8, 0, 4) and not ok(132, 132, 0, 10)
+    assert not ok(64, 64, 60, 8)          # key past the row
+    assert not ok(64, 80, 0, 8)           # other pitches
+    assert not RS.fine_rows_ok(64, 64, 8, 8, 1, 1000) and RS.fine_rows_ok(64, 64, 8, 8, 1, 1000, one_rank=True)
+    assert not RS.fine_rows_ok(64, 64, 8, 8, 65, 1000)

@@ -169,3 +169,47 @@ def test_merge_received_rounds_falls_back_on_a_skewed_bucket():
         key = [bytes(x[:10]) for x in blk]
         exp.append(blk[sorted(range(len(blk)), key=lambda i: (key[i], i))])
     assert np.array_equal(got, np.concatenate(exp))
+
+
+@pytest.mark.parametrize("rec,key_off,key_len,desc", [
+    (100, 0, 10, False), (64, 8, 8, False), (64, 8, 8, True), (68, 3, 5, True), (128, 120, 8, False),
+    (12, 0, 2, False), (16, 6, 10, True), (40, 0, 10, True)])
+def test_tile_merge_any_width_and_key(rec, key_off, key_len, desc):
+    """ts_tile_merge over rows of other widths, a key of <= 10 bytes anywhere in the row, ascending
+    or descending: every bucket in the stable order (key, source, slot) of a numpy reference; a hot
+    bucket takes the register-path kernel."""
+    g = np.random.default_rng(rec * 31 + key_off)
+    W, fb, n = 3, 16, 60_000
+    rows = g.integers(0, 256, size=(n, rec), dtype=np.uint8)
+    rows[: 900, key_off: key_off + 2] = 0x5A            # one hot bucket (~900 rows > the LDS stage)
+    rows[1000::200, key_off: key_off + key_len] = rows[950, key_off: key_off + key_len]    # equal keys
+    key = np.zeros((n, 10), dtype=np.uint8)
+    key[:, :key_len] = rows[:, key_off: key_off + key_len]
+    if desc:
+        key[:, :key_len] ^= 0xFF
+    bucket = ((key[:, 0].astype(np.int64) << 8) | key[:, 1]) >> (16 - fb)
+    src = g.integers(0, W, size=n)
+    pieces = []
+    cnt = np.zeros((W, 1 << fb), dtype=np.int32)
+    for s in range(W):
+        sel = np.nonzero(src == s)[0]
+        sel = sel[np.argsort(bucket[sel], kind="stable")]       # the send side's bucket order
+        pieces.append(sel)
+        cnt[s] = np.bincount(bucket[sel], minlength=1 << fb)
+    order_in = np.concatenate(pieces)
+    recv = rows[order_in]
+    pre = np.zeros_like(cnt, dtype=np.int64)
+    base = 0
+    for s in range(W):
+        pre[s] = base + np.cumsum(cnt[s]) - cnt[s]
+        base += int(cnt[s].sum())
+    col = cnt.sum(0).astype(np.int64)
+    outoff = np.cumsum(col) - col
+    out = torch.zeros((n, rec), dtype=torch.uint8, device="cuda")
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    TS.tile_merge(torch.from_numpy(recv).cuda(), out, torch.from_numpy(pre).cuda(), torch.from_numpy(cnt).cuda(),
+                  torch.from_numpy(outoff).cuda(), fb, flag, key_off=key_off, key_len=key_len, descending=desc)
+    assert int(flag.item()) == 0
+    k = key[order_in]
+    exp = recv[np.lexsort([np.arange(n)] + [k[:, j] for j in range(9, -1, -1)])]
+    assert np.array_equal(out.cpu().numpy(), exp)
