@@ -494,10 +494,12 @@ def distributed_sort_rows(bufs: SortBuffers, n: int, key_off: int, key_len: int,
             seps = separators_from_samples(shuffle.all_gather_varlen(samp, w), W * B)
             fb = fine_bits(nmax * W)
             seps_hi = [int(x) & _M64 for x in seps[:, 1].tolist()]
-            if fine_rows and split and _fine_collapsed(seps_hi, fb) and bufs.ent_b.numel() >= 2 * n and pitch == rec:
-                # heavy duplication: two separators inside one fine bucket.  The fine cut would give
-                # the whole bucket to one rank; the E128 path splits runs of equal keys (key, rank,
-                # row) instead.  The separators are global, so every rank switches alike.
+            if fine_rows and _fine_collapsed(seps_hi, fb) and bufs.ent_b.numel() >= 2 * n and pitch == rec:
+                # two separators inside one fine bucket: heavy duplication, or keys whose leading
+                # bits hardly vary.  The fine cut would give the whole bucket to one rank (and
+                # overflow the LDS merge); the E128 path cuts at full key resolution and, with
+                # split ties, splits runs of equal keys (key, rank, row).  The separators are
+                # global, so every rank switches alike.
                 fine_rows = False
                 B = pipeline_subs(nmax * rec, W)        # (the E128 path: world * rounds <= 256)
                 ent = S.extract_keys(rows, key_off, key_len, 0, out=bufs.ent_a[:n])

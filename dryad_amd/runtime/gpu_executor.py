@@ -69,6 +69,13 @@ class VertexCancelled(Exception):
     """A losing speculative attempt stopped at an operator boundary (its duplicate won)."""
 
 
+class _ColSpec:
+    """Vote spec of a columnar fused OrderBy: off -1, length = the packed row bytes."""
+
+    def __init__(self, off: int, length: int):
+        self.off, self.length = off, length
+
+
 class GpuVertexContext(V.VertexContext):
     def __init__(self, partition, partitions, vertex_id, version, stage, device, world, runner=None):
         super().__init__(partition, partitions, vertex_id, version, stage)
@@ -316,6 +323,8 @@ class GpuJobRunner:
 
     def _fused_applicable(self, f) -> bool:
         from ..gpu import trace as TR
+        from ..ops import rowpack as RP
+        colvals = []
         ok = self.gpu_ok and f["comparer"] is None and self.plan.stages[f["x"]].partitions == self.world.size
         spec = None
         if ok:
@@ -332,8 +341,30 @@ class GpuJobRunner:
                     ok = False
                 if not ok:
                     spec = None
+            elif isinstance(t, DeviceTable) and t.rows is None and self.pool is not None:
+                # a columnar table with numeric key parts: packed into byte-keyed rows
+                # (ops/rowpack.py) for the same exchange, each part cut to the job's value range
+                # (the bounds travel in the vote); spec (-1, key parts)
+                try:
+                    kind, keys = TR.key_columns(TR.call(f["key"], t), t)
+                    pre = RP.plan(t, keys, [(0, 0)] * len(keys)) \
+                        if kind == "cols" and len(keys) <= RP.MAX_KEY_BYTES else None
+                    if pre is not None:
+                        colvals = RP.key_bounds(keys, t.n)
+                except Exception:  # noqa: BLE001
+                    pre = None
+                if pre is not None:
+                    ok = True
+                    spec = _ColSpec(-1, len(keys))
         mine = None if spec is None else (spec.off, spec.length)
-        agree, _ = shuffle.vote(bool(ok), mine, self.world)      # one tensor all-gather, no pickles
+        pad = list(colvals) + [(1 << 63) - 1, -(1 << 63)] * RP.MAX_KEY_BYTES
+        agree, vals = shuffle.vote(bool(ok), mine, self.world, values=pad[: 2 * RP.MAX_KEY_BYTES])
+        if agree and mine is not None and mine[0] < 0:
+            f["colbounds"] = RP.merge_bounds(vals, mine[1])
+            lay = RP.plan(t, keys, f["colbounds"])         # the same decision on every rank
+            if lay is None:
+                return False
+            mine = (-1, lay.rec)
         if agree:
             f["spec"] = mine
             return True
@@ -430,6 +461,8 @@ class GpuJobRunner:
         off, ln = f["spec"]
         stats = RS.SortStats()
         src = None
+        if off < 0:
+            return self._run_fused_columns(m, f, t, stats)
         if bs is None:
             # the input table is not ours to clobber: its rows are read in place (entries, the
             # send-side pack) and the exchange works in a buffer set of its own
@@ -457,6 +490,36 @@ class GpuJobRunner:
         # the rest of the merge stage's program after the sort
         vctx = GpuVertexContext(me, m.partitions, self.vids[m.id][me], 0, m, self.dev, self.world, self)
         data = table
+        for op in m.ops[1:]:
+            data = self._run_op(op, [data], vctx, m)
+        return data
+
+    def _run_fused_columns(self, m, f, t, stats):
+        """The fused OrderBy of a columnar table: its rows packed with the byte-comparable key
+        first into a buffer set of their own (the input stays intact), the fine-bucket exchange,
+        the received rows unpacked into columns that live in the set's input memory (free once
+        the exchange has merged every round)."""
+        from ..gpu import trace as TR
+        from ..ops import recordsort as RS
+        from ..ops import rowpack as RP
+        me = self.world.rank
+        _, keys = TR.key_columns(TR.call(f["key"], t), t)
+        lay = RP.plan(t, keys, f["colbounds"])
+        if lay is None or lay.rec != f["spec"][1]:
+            raise RuntimeError("fused columnar OrderBy: the row layout changed after the vote")
+        slack = self.ctx._props.get("ShuffleSlack", 0.01)
+        bs = self.pool.acquire(int(t.n * (1 + slack)) + 1024, lay.rec)
+        RP.pack(t, keys, lay, bs.bufs.rows_in[: t.n])
+        out = RS.distributed_sort_rows(bs.bufs, t.n, 0, lay.key_len, self.world, stats=stats,
+                                       split_ties=not f.get("keep_ties", False),
+                                       descending=bool(f.get("desc", False)))
+        mem = bs.bufs.rows_in.view(-1) if out.data_ptr() == bs.bufs.rows_out.data_ptr() else None
+        cols = RP.unpack(out, lay, mem)
+        stats.path = f"columns packed into {lay.rec}-byte rows, " + (stats.path or "")
+        self.row_sets[(m.id, me)] = bs
+        self.last_sort_stats = stats
+        vctx = GpuVertexContext(me, m.partitions, self.vids[m.id][me], 0, m, self.dev, self.world, self)
+        data = DeviceTable(out.shape[0], t.shape, cols)
         for op in m.ops[1:]:
             data = self._run_op(op, [data], vctx, m)
         return data

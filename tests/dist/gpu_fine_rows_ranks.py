@@ -80,6 +80,33 @@ def _rows64(w, base):
         assert np.array_equal(got, rows[order[a: a + got.shape[0]]]), (w.rank, desc)
 
 
+def _records64(w):
+    from dryad_amd.io.providers import provider_for
+    W, n = w.size, 200_000
+    ctx = D.DryadLinqContext(platform="gpu")
+    ctx.PartitionCount = W
+    ctx.FromStore(f"gen://records64?count={W * n}&partitions={W}&keys=5000&seed=9") \
+        .ToStore("hbm://r64_in", delete_if_exists=True).SubmitAndWait()
+    t = provider_for("hbm://r64_in").get("hbm://r64_in")["local"][w.rank]
+    names = list(t.cols)
+    mine = torch.stack([t.cols[c][: t.n] for c in names], 1)
+    allin = shuffle.all_gather_varlen(mine, w)               # rank order = the ties' order
+    for field, desc in (("V1", False), ("Key", True), ("V1", True)):
+        q = ctx.FromStore("hbm://r64_in")
+        sel = (lambda r: r.V1) if field == "V1" else (lambda r: r.Key)
+        q = q.OrderByDescending(sel) if desc else q.OrderBy(sel)
+        q.ToStore("hbm://r64_out", delete_if_exists=True).SubmitAndWait()
+        ex = ctx._get_executor().last_result["exchange"]
+        assert ex is not None and "columns packed into" in ex["path"] and "fine-bucket" in ex["path"], (field, desc, ex)
+        o = provider_for("hbm://r64_out").get("hbm://r64_out")["local"][w.rank]
+        got = torch.stack([o.cols[c][: o.n] for c in names], 1)
+        counts = shuffle.all_gather_tensor(torch.tensor([o.n], dtype=torch.int64, device=w.device), w).tolist()
+        assert sum(counts) == W * n, counts
+        _, order = torch.sort(allin[:, names.index(field)], descending=desc, stable=True)
+        a = sum(counts[: w.rank])
+        assert torch.equal(got, allin[order[a: a + o.n]]), (w.rank, field, desc)
+
+
 def main():
     w = init_world(device="cuda")
     n = int(os.environ.get("TS_RECORDS", "1500000"))
@@ -171,6 +198,9 @@ def main():
     # offset (inverted for the descending sort); every rank's output is its exact slice of the
     # stable global order (ties by source rank, then row)
     _rows64(w, base)
+    # 6. a COLUMNAR table (gen://records64: 8 int64 columns) by r.V1 (31-bit values) and
+    # descending by r.Key (few distinct keys: long runs of ties), packed into byte-keyed rows
+    _records64(w)
     w.barrier()
     if w.rank == 0:
         print("FINE_ROWS_OK", w.size, flush=True)
