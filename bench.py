@@ -69,6 +69,12 @@ def main():
                     help="run the per-rank program of a W-rank job on this one GPU, the all-to-all-v replaced by "
                          "generating the exact bytes this rank would receive (not timed); reports per-rank ms")
     ap.add_argument("--loopback-rank", type=int, default=0, help="which rank of the --loopback-ranks job to run")
+    ap.add_argument("--loopback-table", choices=["terasort", "records64"], default="terasort",
+                    help="with --loopback-ranks: records64 = a COLUMNAR table of 64-byte records (8 int64 columns) "
+                         "ordered by --sort-key (packed into byte-keyed rows for the fine-bucket exchange)")
+    ap.add_argument("--loopback-gb", type=float, default=80.0, help="with --loopback-table records64: GB per rank")
+    ap.add_argument("--sort-key", default="V1", help="with --loopback-table records64: the key column")
+    ap.add_argument("--descending", action="store_true", help="with --loopback-table records64: OrderByDescending")
     ap.add_argument("--pack-group", type=int, default=1,
                     help="with --loopback-ranks (A/B): send rounds packed per launch")
     ap.add_argument("--model-link-GBps", type=float, nargs="*", default=[300.0, 450.0],
@@ -229,6 +235,8 @@ def loopback(args, env):
     if W < 2 or not 0 <= r < W:
         print("[bench] --loopback-ranks needs W >= 2 and 0 <= --loopback-rank < W", file=sys.stderr)
         sys.exit(2)
+    if args.loopback_table == "records64":
+        return loopback_records64(args, env)
     mode = "gen-fused" if args.gen_fused else "table"
     job = TeraSortLoopbackJob(TeraSortConfig(records_per_rank=args.records_per_gpu), W, r, mode=mode,
                               input_uri=args.input, pack_group=args.pack_group)
@@ -265,6 +273,47 @@ def loopback(args, env):
                    "modelled_exchange": ([job.model(x) for x in args.model_link_GBps]
                                          if mode == "table" and args.model_link_GBps else None),
                    "round_pack_ms": [round(x, 3) for x in job.rounds["pack_ms"]] if mode == "table" else None,
+                   "round_merge_ms": [round(x, 3) for x in job.rounds["merge_ms"]],
+                   "validated": None if val is None else val["ok"], "validation": val, "env": env},
+    }
+    print(json.dumps(line), flush=True)
+    if val is not None and not val["ok"]:
+        sys.exit(3)
+
+
+def loopback_records64(args, env):
+    """``--loopback-ranks W --loopback-table records64``: one rank's share of a W-GPU OrderBy over
+    a columnar table of 64-byte records (models/records_sort.py), timed phase by phase."""
+    from dryad_amd.models.records_sort import Records64LoopbackJob
+    W, r = args.loopback_ranks, args.loopback_rank
+    n = int(args.loopback_gb * 1e9) // 64
+    job = Records64LoopbackJob(W, r, n, key=args.sort_key, descending=args.descending, pack_group=args.pack_group)
+    for i in range(args.warmup):
+        job.step()
+        print(f"[bench] warmup {i}: {job.ms:.2f} ms {job.phases}", file=sys.stderr, flush=True)
+    ms, phases = [], []
+    for i in range(args.steps):
+        job.step()
+        ms.append(job.ms)
+        phases.append(job.phases)
+        print(f"[bench] step {i}: {job.ms:.2f} ms {job.phases}", file=sys.stderr, flush=True)
+    val = None if args.no_validate else job.validate()
+    mean = sum(ms) / len(ms)
+    order = "OrderByDescending" if args.descending else "OrderBy"
+    line = {
+        "metric": f"{order}(r => r.{args.sort_key}) per-rank step of a {W}-rank job over a columnar table "
+                  f"(loopback on one GPU: all-to-all-v replaced)",
+        "value": round(mean, 3), "unit": "ms", "higher_is_better": False, "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(mean, 3), "dtype": "int64",
+        "data": "synthetic gen://records64 (8 int64 columns: Key uniform in [0, 2^20), V1..V7 31-bit)",
+        "config": {"model": f"records64 {order} by {args.sort_key}", "rows_per_rank": n,
+                   "bytes_per_rank": job.bytes_per_rank, "row_bytes": job.rec, "key_bytes": job.lay.key_len,
+                   "ranks": W, "rank": r, "rounds": job.B, "received_rows": int(job.out_cols[args.sort_key].shape[0]),
+                   "phases_ms": {k: round(sum(p[k] for p in phases) / len(phases), 3) for k in phases[0]},
+                   "per_rank_GBps": round(job.bytes_per_rank / 1e6 / mean, 1),
+                   "input": "the rank's columnar table generated before the step (an existing hbm:// table), untimed",
+                   "modelled_exchange": [job.model(x) for x in args.model_link_GBps] if args.model_link_GBps else None,
+                   "round_pack_ms": [round(x, 3) for x in job.rounds["pack_ms"]],
                    "round_merge_ms": [round(x, 3) for x in job.rounds["merge_ms"]],
                    "validated": None if val is None else val["ok"], "validation": val, "env": env},
     }

@@ -116,3 +116,18 @@ def test_gather_fixup_reads_nothing_after_a_failed_lookback_sort():
                               torch.empty(n, dtype=torch.int64, device=dev), 0, 10)
     keys = got[:, :10].cpu().numpy()
     assert all(bytes(keys[i]) <= bytes(keys[i + 1]) for i in range(0, n - 1, 997))
+
+
+@pytest.mark.parametrize("key,desc", [("V1", False), ("Key", True)])
+def test_records64_loopback_rank_program(key, desc):
+    """The per-rank program of a columnar OrderBy (models/records_sort.py) at a small size: packed
+    rows through the fine-bucket send side and LDS merge, unpacked, validated (order, fingerprint
+    of the received rows, range)."""
+    from dryad_amd.models.records_sort import Records64LoopbackJob
+    job = Records64LoopbackJob(4, 2, 300_000, key=key, descending=desc, nkeys=50_000)
+    job.step()
+    v = job.validate()
+    assert v["ok"], v
+    assert job.rec == 64 and set(job.phases) >= {"pack_columns_ms", "receive_merge_ms", "unpack_ms"}
+    m = job.model(300.0)
+    assert m["overlapped_step_ms"] > 0 and m["modelled"]

@@ -7,6 +7,10 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_rowpack.py tests/test_gpu_tsmerge.py tests/test_gpu_fine_rows.py tests/test_gpu_multirank.py tests/test_gpu_extsort.py -x -q --timeout 580 --timeout-method thread > gpurun_out/r6d_tests.log 2>&1 || { tail -60 gpurun_out/r6d_tests.log; exit 1; }
 tail -1 gpurun_out/r6d_tests.log
+timeout -k 10 400 python -u bench.py --loopback-ranks 8 --loopback-table records64 --loopback-gb 80 --steps 2 --warmup 1 > gpurun_out/r6d_r64_lb8.log 2>&1 || { tail -20 gpurun_out/r6d_r64_lb8.log; exit 1; }
+tail -1 gpurun_out/r6d_r64_lb8.log | cut -c1-1800
+timeout -k 10 400 python -u bench.py --loopback-ranks 8 --loopback-table records64 --loopback-gb 80 --sort-key Key --descending --steps 2 --warmup 1 > gpurun_out/r6d_r64_lb8_desc.log 2>&1 || { tail -20 gpurun_out/r6d_r64_lb8_desc.log; exit 1; }
+tail -1 gpurun_out/r6d_r64_lb8_desc.log | cut -c1-1800
 for g in 1 2; do
 timeout -k 10 300 python -u bench.py --loopback-ranks 8 --steps 3 --warmup 1 --pack-group $g > gpurun_out/r6d_lb8_g$g.log 2>&1 || { tail -20 gpurun_out/r6d_lb8_g$g.log; exit 1; }
 tail -1 gpurun_out/r6d_lb8_g$g.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['config']; print('group $g', d['value'], c['phases_ms'], c['validated'], c['modelled_exchange'])"
