@@ -124,7 +124,7 @@ def test_records64_loopback_rank_program(key, desc):
     rows through the fine-bucket send side and LDS merge, unpacked, validated (order, fingerprint
     of the received rows, range)."""
     from dryad_amd.models.records_sort import Records64LoopbackJob
-    job = Records64LoopbackJob(4, 2, 300_000, key=key, descending=desc, nkeys=50_000)
+    job = Records64LoopbackJob(4, 2, 300_000, key=key, descending=desc, nkeys=50_000, slack=0.2)   # ~300 samples a rank
     job.step()
     v = job.validate()
     assert v["ok"], v
