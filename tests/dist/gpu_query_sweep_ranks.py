@@ -55,7 +55,8 @@ def queries():
                       True),
         "terasort_bytes": (lambda c, W: c.FromStore(ts % W).OrderBy(lambda r: r[0:10]).Select(lambda r: r[0:10]),
                            True),
-        # the fused distributed OrderBy, descending: inverted E128 keys, ties in (partition, row) order
+        # the fused distributed OrderBy, descending: inverted key windows (fine buckets; the 1-byte key
+        # collapses the fine cut: the E128 path), ties in (partition, row) order
         "terasort_bytes_desc": (lambda c, W: c.FromStore(ts % W).OrderByDescending(lambda r: r[0:10]).Select(
             lambda r: r[0:10]), True),
         "terasort_desc_ties": (lambda c, W: c.FromStore(ts % W).OrderByDescending(lambda r: r[0:1]).Select(

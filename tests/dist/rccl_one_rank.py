@@ -79,15 +79,22 @@ def main():
         # received into slots, merged from there
         assert "rounds packed as they go out" in st.path and "first_round_queued_ms" in rep, rep
         assert rep["overlap"]["slots"] == RS.OVERLAP_SLOTS and not rep["overlap"]["skew_fixups"], rep
-        # 3. the E128 range-partition path, descending
+        # 3. descending: the fine-bucket exchange with inverted key windows
         st2 = RS.SortStats()
         out2 = RS.distributed_sort_rows(bufs, n, 0, 10, w, stats=st2, src=src, descending=True)
         asc = out2.flip(0).contiguous()
         acc2 = TS.check(asc)
         torch.cuda.synchronize()
-        assert st2.path.startswith("E128"), st2.path
+        assert st2.path.startswith("fine-bucket exchange over the table"), st2.path
         assert out2.shape[0] == n and int(acc2[1]) == 0 and int(acc2[0]) == int(acc_in[0]), acc2.tolist()
-        del bufs, src, out, out2
+        # 3b. a 12-byte key (past the fine path's 10): the E128 range-partition path
+        st3 = RS.SortStats()
+        out3 = RS.distributed_sort_rows(bufs, n, 0, 12, w, stats=st3, src=src)
+        acc3 = TS.check(out3)
+        torch.cuda.synchronize()
+        assert st3.path.startswith("E128"), st3.path
+        assert out3.shape[0] == n and int(acc3[1]) == 0 and int(acc3[0]) == int(acc_in[0]), acc3.tolist()
+        del bufs, src, out, out2, out3
         torch.cuda.empty_cache()
         # 4. the bench's N > 1 program: the DryadLINQ query through the executor's fused OrderBy gang
         #    stage (ExchangeOneRank plans the sampled range shuffle for the one partition), validated
