@@ -590,6 +590,56 @@ DR_API uint32_t dr_ts_tile_cap() { return kTmCap; }
 
 // rows / out: 100-byte rows (4-byte aligned); pre, cnt: [W][K]; outoff: [K]; 16 <= fb <= 24 (the
 // caller's FINE_MIN_BITS..FINE_MAX_BITS).  A bucket past kTmCap rows is flagged, never ordered.
+namespace {
+// Fine buckets that each hold ONE key (every key bit is a bucket bit, e.g. a 2-byte key at
+// fb >= 16): the merge is the W slices of a bucket copied in source order, at any bucket size
+// (the LDS merge would flag a bucket past its 1024 rows).  One wave per bucket.
+__global__ __launch_bounds__(256) void ts_bucket_copy_kernel(const uint8_t* __restrict__ rows,
+                                                             uint8_t* __restrict__ out,
+                                                             const int64_t* __restrict__ pre,
+                                                             const int32_t* __restrict__ cnt,
+                                                             const int64_t* __restrict__ outoff, uint32_t W,
+                                                             uint32_t K, uint32_t rec) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t waves = (gridDim.x * blockDim.x) >> 6;
+  for (uint32_t k = wave; k < K; k += waves) {
+    uint64_t dst = (uint64_t)outoff[k] * rec;
+    for (uint32_t s = 0; s < W; ++s) {
+      const int32_t c = cnt[(uint64_t)s * K + k];
+      if (c <= 0) continue;
+      const uint64_t src = (uint64_t)pre[(uint64_t)s * K + k] * rec;
+      const uint64_t bytes = (uint64_t)c * rec;
+      const uint8_t* a = rows + src;
+      uint8_t* b = out + dst;
+      if (((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) | bytes) & 15) == 0) {
+        const uint4* a4 = reinterpret_cast<const uint4*>(a);
+        uint4* b4 = reinterpret_cast<uint4*>(b);
+        for (uint64_t i = lane; i < bytes / 16; i += 64) b4[i] = a4[i];
+      } else {
+        const uint32_t* a1 = reinterpret_cast<const uint32_t*>(a);
+        uint32_t* b1 = reinterpret_cast<uint32_t*>(b);
+        for (uint64_t i = lane; i < bytes / 4; i += 64) b1[i] = a1[i];
+      }
+      dst += bytes;
+    }
+  }
+}
+}  // namespace
+
+// The merge of fine buckets that each hold one key: bucket k's W slices rows[pre[s, k] ..
+// + cnt[s, k]) copied in source order to out[outoff[k]:] (records of `rec` bytes, a multiple of 4).
+DR_API int dr_ts_bucket_copy(const uint8_t* rows, uint8_t* out, const int64_t* pre, const int32_t* cnt,
+                             const int64_t* outoff, uint32_t W, uint32_t K, uint32_t rec, hipStream_t s) {
+  if (W == 0 || rec % 4 || rec == 0) return (int)hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(out)) & 3) return (int)hipErrorInvalidValue;
+  if (K == 0) return 0;
+  const unsigned g = (unsigned)((K + 3) / 4 < 65536 ? (K + 3) / 4 : 65536);
+  ts_bucket_copy_kernel<<<g, 256, 0, s>>>(rows, out, pre, cnt, outoff, W, K, rec);
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
 // dr_ts_tile_merge for records of `rec` bytes (a multiple of 4, 12..128) ordered by the key of
 // `key_len` <= 10 bytes at byte `key_off` (descending: `desc`).  The TeraSort layout (10-byte key
 // at byte 0, ascending) reads the key as three words; any other as bytes.

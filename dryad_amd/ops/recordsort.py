@@ -987,6 +987,9 @@ class FineMerge:
         self.W, self.K = fine.shape
         W, K = self.W, self.K
         self.key = dict(key_off=key_off, key_len=key_len, descending=descending)
+        # every key bit is a bucket bit: a bucket holds one key, its merge is a copy in source
+        # order at any size (long runs of equal keys would overflow the LDS merge)
+        self.whole = 8 * key_len <= fb
         self.L, self.fb, self.B, self.rank, self.out = L, fb, B, rank, out
         dev = out.device
         self.flags = torch.zeros(B, dtype=torch.int32, device=dev)
@@ -1034,8 +1037,11 @@ class FineMerge:
         W = self.W
         pre = self.pre[W * k0: W * k1].view(W, k1 - k0)
         cnt = self.cnt[W * k0: W * k1].view(W, k1 - k0)
-        TSG.tile_merge(recv[base:], self.out[a:], pre, cnt, self.outoff[k0:k1], self.fb, self.flags[b:b + 1],
-                       **self.key)
+        if self.whole:
+            TSG.bucket_copy(recv[base:], self.out[a:], pre, cnt, self.outoff[k0:k1])
+        else:
+            TSG.tile_merge(recv[base:], self.out[a:], pre, cnt, self.outoff[k0:k1], self.fb, self.flags[b:b + 1],
+                           **self.key)
 
 
 def merge_received_rounds(bufs: SortBuffers, off: list, fine: torch.Tensor, L: list, fb: int, B: int, rank: int,

@@ -186,7 +186,23 @@ def tile_merge(rows: torch.Tensor, out: torch.Tensor, pre: torch.Tensor, cnt: to
     _lib.written(out)
 
 
+def bucket_copy(rows: torch.Tensor, out: torch.Tensor, pre: torch.Tensor, cnt: torch.Tensor,
+                outoff: torch.Tensor) -> None:
+    """tile_merge for fine buckets that each hold ONE key (no key bit below the bucket bits):
+    bucket k's W slices ``rows[pre[s, k] : pre[s, k] + cnt[s, k]]`` copied in source order to
+    ``out[outoff[k]:]``, whatever the bucket's size (runs of equal keys past tile_cap())."""
+    W, K = cnt.shape
+    rec = rows.shape[1]
+    assert pre.shape == (W, K) and pre.dtype == torch.int64 and cnt.dtype == torch.int32 and outoff.shape == (K,)
+    assert out.shape[1] == rec and rec % 4 == 0 and rows.stride(0) == rec and out.stride(0) == rec
+    _lib.call("dr_ts_bucket_copy", ptr(rows), ptr(out), ptr(pre.contiguous()), ptr(cnt.contiguous()),
+              ptr(outoff.contiguous()), c_u32(W), c_u32(K), c_u32(rec), stream_of(rows))
+    _lib.written(out)
+
+
 _lib.register_signatures({
+    "dr_ts_bucket_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, c_u32, c_u32, c_u32, ctypes.c_void_p]),
     "dr_ts_pack_rows_w": (ctypes.c_int, [ctypes.c_void_p, c_u64, c_u32, ctypes.c_void_p, c_u64, ctypes.c_void_p,
                                          c_u32, ctypes.c_void_p, c_u32, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),

@@ -213,3 +213,32 @@ def test_tile_merge_any_width_and_key(rec, key_off, key_len, desc):
     k = key[order_in]
     exp = recv[np.lexsort([np.arange(n)] + [k[:, j] for j in range(9, -1, -1)])]
     assert np.array_equal(out.cpu().numpy(), exp)
+
+
+def test_bucket_copy_orders_one_key_buckets_of_any_size():
+    """Fine buckets that each hold one key (2-byte keys, fb = 16): the merge is the W slices in
+    source order, including buckets far past the LDS merge's 1024 rows."""
+    g = np.random.default_rng(5)
+    W, fb, n, rec = 3, 16, 90_000, 20
+    rows = g.integers(0, 256, size=(n, rec), dtype=np.uint8)
+    rows[:, :2] = g.integers(0, 40, size=(n, 2), dtype=np.uint8)       # 1600 keys, ~56 rows each
+    rows[:5000, :2] = 7                                               # one key of 5000+ rows
+    bucket = (rows[:, 0].astype(np.int64) << 8) | rows[:, 1]
+    src = g.integers(0, W, size=n)
+    pieces = [np.nonzero(src == s)[0] for s in range(W)]
+    pieces = [p[np.argsort(bucket[p], kind="stable")] for p in pieces]
+    cnt = np.stack([np.bincount(bucket[p], minlength=1 << fb) for p in pieces]).astype(np.int32)
+    order_in = np.concatenate(pieces)
+    recv = rows[order_in]
+    pre = np.zeros_like(cnt, dtype=np.int64)
+    base = 0
+    for s in range(W):
+        pre[s] = base + np.cumsum(cnt[s]) - cnt[s]
+        base += int(cnt[s].sum())
+    col = cnt.sum(0).astype(np.int64)
+    outoff = np.cumsum(col) - col
+    out = torch.zeros((n, rec), dtype=torch.uint8, device="cuda")
+    TS.bucket_copy(torch.from_numpy(recv).cuda(), out, torch.from_numpy(pre).cuda(), torch.from_numpy(cnt).cuda(),
+                   torch.from_numpy(outoff).cuda())
+    exp = recv[np.lexsort([np.arange(n), bucket[order_in]])]
+    assert np.array_equal(out.cpu().numpy(), exp)
