@@ -74,7 +74,8 @@ def main():
                          "ordered by --sort-key (packed into byte-keyed rows for the fine-bucket exchange)")
     ap.add_argument("--loopback-gb", type=float, default=80.0, help="with --loopback-table records64: GB per rank")
     ap.add_argument("--sort-key", default="V1", help="with --loopback-table records64: the key column")
-    ap.add_argument("--descending", action="store_true", help="with --loopback-table records64: OrderByDescending")
+    ap.add_argument("--descending", action="store_true",
+                    help="OrderByDescending: with --loopback-table records64, or the out-of-core TeraSort (past HBM)")
     ap.add_argument("--pack-group", type=int, default=1,
                     help="with --loopback-ranks (A/B): send rounds packed per launch")
     ap.add_argument("--model-link-GBps", type=float, nargs="*", default=[300.0, 450.0],
@@ -130,7 +131,7 @@ def main():
             print(f"[bench] input table: {prep}", file=sys.stderr, flush=True)
     elif ooc:
         budget = None if args.hbm_budget_gb is None else int(args.hbm_budget_gb * 1e9)
-        job = TeraSortOOCJob(cfg, world, budget=budget)
+        job = TeraSortOOCJob(cfg, world, budget=budget, descending=args.descending)
     else:
         job = TeraSortJob(cfg, world) if args.direct else TeraSortQueryJob(cfg, world, gen_fused=args.gen_fused)
     if world.rank == 0:
@@ -214,6 +215,9 @@ def main():
             line["config"]["stored"] = job.report()
         elif ooc:
             line["config"]["out_of_core"] = job.report()
+            if args.descending:
+                line["metric"] = METRIC + " [OrderByDescending]"
+                line["config"]["model"] = "TeraSort 100-byte records / 10-byte key, OrderByDescending"
             line["config"]["input"] = "gen://terasort, generated chunk by chunk in the timed step (count + partition passes)"
         elif not args.direct and not stored:
             rep = job.executor_report()

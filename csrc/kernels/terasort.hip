@@ -140,6 +140,7 @@ __device__ __forceinline__ void ts_key(const uint32_t* r, uint64_t& hi, uint32_t
 }
 
 // out[0] += sum of record hashes (mod 2^64), out[1] += #i with key(i-1) > key(i).
+template <bool DESC>
 __global__ __launch_bounds__(256) void ts_check_kernel(const uint32_t* __restrict__ rows, uint64_t n,
                                                        unsigned long long* __restrict__ out) {
   uint64_t hsum = 0, bad = 0;
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(256) void ts_check_kernel(const uint32_t* __restric
       uint64_t h0, h1; uint32_t l0, l1;
       ts_key(r - 25, h0, l0);
       ts_key(r, h1, l1);
-      if (h0 > h1 || (h0 == h1 && l0 > l1)) ++bad;
+      if (DESC ? (h0 < h1 || (h0 == h1 && l0 < l1)) : (h0 > h1 || (h0 == h1 && l0 > l1))) ++bad;
     }
   }
   hsum = wave_sum64(hsum);
@@ -326,8 +327,17 @@ DR_API int dr_terasort_gen_entries64(E64* keys, uint64_t n, uint64_t first_index
 // Accumulates [hash_sum, order_violations] into out2 (2 x uint64, device; caller zeroes it).
 DR_API int dr_terasort_check(const uint8_t* rows, uint64_t n, uint64_t* out2, hipStream_t s) {
   if (n == 0) return 0;
-  ts_check_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows), n,
-                                                         reinterpret_cast<unsigned long long*>(out2));
+  ts_check_kernel<false><<<grid_for(n, 256, 8192), 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows), n,
+                                                                reinterpret_cast<unsigned long long*>(out2));
+  DR_LAUNCH_CHECK();
+  return 0;
+}
+
+// dr_terasort_check of a descending order (OrderByDescending output).
+DR_API int dr_terasort_check_desc(const uint8_t* rows, uint64_t n, uint64_t* out2, hipStream_t s) {
+  if (n == 0) return 0;
+  ts_check_kernel<true><<<grid_for(n, 256, 8192), 256, 0, s>>>(reinterpret_cast<const uint32_t*>(rows), n,
+                                                               reinterpret_cast<unsigned long long*>(out2));
   DR_LAUNCH_CHECK();
   return 0;
 }

@@ -297,8 +297,10 @@ class TeraSortOOCJob:
     in HBM, the others go through pinned host DRAM (allocated once per job, like a job's spill
     tier), so only the overflow crosses PCIe.  The output is a ``TieredRows`` table per rank."""
 
-    def __init__(self, cfg: TeraSortConfig, world: World | None = None, budget: int | None = None):
+    def __init__(self, cfg: TeraSortConfig, world: World | None = None, budget: int | None = None,
+                 descending: bool = False):
         from ..io.hosttable import HostRows
+        self.descending = descending
         from ..ops import extsort as EX
         self.EX = EX
         self.cfg = cfg
@@ -326,7 +328,7 @@ class TeraSortOOCJob:
         st = self.EX.ExtSortStats()
         self.out = None              # the previous output's HBM buckets are this step's to reuse
         self.out = self.EX.external_sort(self.src, 0, KEYLEN, self.world, budget=self.budget, stats=st,
-                                         out=self.host, resident=True)
+                                         out=self.host, resident=True, descending=self.descending)
         self.stats = st
         return self.out
 
@@ -344,7 +346,7 @@ class TeraSortOOCJob:
 
     def validate(self, expect_hash: int, expect_records: int) -> dict:
         m64 = (1 << 64) - 1
-        h, bad, first, last = self.EX.check_terasort_host(self.out)
+        h, bad, first, last = self.EX.check_terasort_host(self.out, descending=self.descending)
         s64 = (h & m64) - (1 << 64) if (h & m64) >= (1 << 63) else (h & m64)
         dev = self.world.device
         tot = torch.tensor([s64, self.out.n, bad], dtype=torch.int64, device=dev)
@@ -359,7 +361,8 @@ class TeraSortOOCJob:
         for row in allends:
             if row[0] == 0:
                 continue
-            if prev_last is not None and prev_last > bytes(row[1:1 + KEYLEN]):
+            k0 = bytes(row[1:1 + KEYLEN])
+            if prev_last is not None and (prev_last < k0 if self.descending else prev_last > k0):
                 boundary_ok = False
             prev_last = bytes(row[1 + KEYLEN:])
         hv = int(tot[0]) & m64

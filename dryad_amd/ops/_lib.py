@@ -39,6 +39,7 @@ _SIGS = {
     "dr_bucket_scatter_rows": (c_i32, [vp, vp, vp, c_u64, c_u32, vp, vp, vp]),
     "dr_terasort_gen": (c_i32, [vp, c_u64, c_u64, c_u64, vp]),
     "dr_terasort_check": (c_i32, [vp, c_u64, vp, vp]),
+    "dr_terasort_check_desc": (c_i32, [vp, c_u64, vp, vp]),
     "dr_terasort_gen_keys": (c_i32, [vp, c_u64, c_u64, c_u64, vp, c_u32, vp, vp]),
     "dr_terasort_gen_keys64": (c_i32, [vp, c_u64, c_u64, c_u64, vp, c_u32, vp, vp]),
     "dr_terasort_gen_keys64_pitch128": (c_i32, [vp, c_u64, c_u64, c_u64, vp, c_u32, vp, vp, vp]),

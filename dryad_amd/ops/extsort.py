@@ -603,7 +603,7 @@ def external_sort(src: ChunkSource, key_off: int, key_len: int, world: World | N
     return out
 
 
-def check_terasort_host(out, chunk_rows: int = 1 << 24) -> tuple[int, int, bytes, bytes]:
+def check_terasort_host(out, chunk_rows: int = 1 << 24, descending: bool = False) -> tuple[int, int, bytes, bytes]:
     """valsort over a host (``HostRows``) or tiered (``TieredRows``) TeraSort table: (hash sum mod
     2^64, order violations incl. chunk and segment boundaries, first key, last key); host rows are
     streamed through HBM in chunks, HBM-resident segments checked in place."""
@@ -624,11 +624,11 @@ def check_terasort_host(out, chunk_rows: int = 1 << 24) -> tuple[int, int, bytes
                     buf = torch.empty((chunk_rows, seg.shape[1]), dtype=torch.uint8, device=dev)
                 _copy(buf[: b - a], seg[a:b], None)
                 rows = buf[: b - a]
-            TS.check(rows, acc)
+            TS.check(rows, acc, descending=descending)
             k0 = bytes(seg[a, :TS.KEY_BYTES].cpu().numpy())
             if first is None:
                 first = k0
-            if prev is not None and prev > k0:
+            if prev is not None and (prev < k0 if descending else prev > k0):
                 bad += 1
             prev = bytes(seg[b - 1, :TS.KEY_BYTES].cpu().numpy())
     torch.cuda.synchronize(dev)

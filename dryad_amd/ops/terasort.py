@@ -74,12 +74,14 @@ def generate_with_keys64_pitch128(out: torch.Tensor, first_index: int, seed: int
     return out
 
 
-def check(rows: torch.Tensor, acc: torch.Tensor | None = None) -> torch.Tensor:
-    """Accumulate [sum of record hashes mod 2^64, #adjacent order violations] into ``acc``."""
+def check(rows: torch.Tensor, acc: torch.Tensor | None = None, descending: bool = False) -> torch.Tensor:
+    """Accumulate [sum of record hashes mod 2^64, #adjacent order violations] into ``acc``
+    (``descending``: violations of the descending order)."""
     _lib.require_gpu_tensor(rows, "terasort.check")
     if acc is None:
         acc = torch.zeros(2, dtype=torch.int64, device=rows.device)
-    _lib.call("dr_terasort_check", ptr(rows), c_u64(rows.shape[0]), ptr(acc), stream_of(rows))
+    _lib.call("dr_terasort_check_desc" if descending else "dr_terasort_check", ptr(rows), c_u64(rows.shape[0]),
+              ptr(acc), stream_of(rows))
     return acc
 
 
