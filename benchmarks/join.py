@@ -37,6 +37,9 @@ def main():
                     help="string keys: both tables are gen://names (Name = \"u\" + decimal(Key), V1, V2 from the same "
                          "generator), joined on Name; with --to-store the result is (r.V2, r.V1, s.V1), so the "
                          "validation of the integer-key join applies unchanged")
+    ap.add_argument("--name-len", type=int, default=0,
+                    help="with --names: every Name padded to this many bytes (> 20; e.g. 200: longer than "
+                         "GraceJoinStringBytes, so the join widens its string slots or moves them out of line)")
     ap.add_argument("--string-bytes", type=int, default=24,
                     help="GraceJoinStringBytes: inline bytes per string field in the packed bucket rows")
     a = ap.parse_args()
@@ -54,8 +57,9 @@ def main():
     if a.to_store:
         ctx.PartFileSplitBytes = 1 << 30      # a rank's output partition over 8 part files at once
     gen = "names" if a.names else "records64"
-    R = f"gen://{gen}?count={rows}&partitions={w.size}&keys={rows}&seed={SEED_R}&mode=dim"
-    S = f"gen://{gen}?count={rows}&partitions={w.size}&keys={rows}&seed={SEED_S}"
+    nl = f"&namelen={a.name_len}" if a.names and a.name_len else ""
+    R = f"gen://{gen}?count={rows}&partitions={w.size}&keys={rows}&seed={SEED_R}&mode=dim{nl}"
+    S = f"gen://{gen}?count={rows}&partitions={w.size}&keys={rows}&seed={SEED_S}{nl}"
     if a.names:
         ctx.GraceJoin = True
         ctx.GraceJoinStringBytes = a.string_bytes
@@ -120,7 +124,9 @@ def main():
             fp_ok = res[2] == pairs_fp[1] and res[0] == pairs_fp[0]
         ok = res[0] == exp[0] and res[1] == exp[1] and fp_ok is not False
     med = sorted(times)[len(times) // 2]
-    if a.names:                 # Name bytes ("u" + decimal key, keys < rows) + V1 + V2 per record
+    if a.names and a.name_len:
+        total = 2 * rows * (a.name_len + 16)
+    elif a.names:                 # Name bytes ("u" + decimal key, keys < rows) + V1 + V2 per record
         lo = lambda d: 10 ** (d - 1) if d > 1 else 0  # noqa: E731  (first key with d digits)
         ndig = sum(d * (min(rows, 10 ** d) - lo(d)) for d in range(1, 20) if lo(d) < rows)
         total = 2 * (rows * 17 + ndig)
@@ -154,6 +160,8 @@ def main():
                              else "R.Join(S, Key, (r, s) => (r.Key, r.V1, s.V1)).ToStore(partfile)" if a.to_store else
                              "R.Join(S, Key).Select(r.V1 + s.V1).Sum()") + " (grace hash join)", "rows_per_table": rows,
                    "row_bytes": None if a.names else 64, "input_GB": round(total / 1e9, 2),
+                   "name_bytes": (a.name_len or "natural") if a.names else None,
+                   "grace_join_string_bytes": a.string_bytes if a.names else None,
                    "hbm_budget_gb": a.hbm_budget_gb, "parallelism": f"dp{w.size}"}})
 
 

@@ -14,3 +14,8 @@ free -g > gpurun_out/r6e_free.txt
 cd benchmarks
 timeout -k 10 600 python3 -u distinct.py --gb 150 --hbm-budget-gb 60 > ../gpurun_out/r6e_distinct150.log 2>&1 || { tail -20 ../gpurun_out/r6e_distinct150.log; exit 1; }
 tail -1 ../gpurun_out/r6e_distinct150.log | cut -c1-2500
+timeout -k 10 600 python3 -u join.py --to-store partfile:///tmp/dryad_jout --steps 2 --warmup 1 > ../gpurun_out/r6e_join_store.log 2>&1 || { tail -20 ../gpurun_out/r6e_join_store.log; exit 1; }
+tail -1 ../gpurun_out/r6e_join_store.log | cut -c1-2500
+rm -rf /tmp/dryad_jout*
+timeout -k 10 600 python3 -u join.py --names --name-len 200 --table-gb 20 --to-store partfile:///tmp/dryad_jnames --steps 2 --warmup 1 > ../gpurun_out/r6e_join_names200.log 2>&1 || { tail -20 ../gpurun_out/r6e_join_names200.log; exit 1; }
+tail -1 ../gpurun_out/r6e_join_names200.log | cut -c1-2500
