@@ -200,6 +200,7 @@ class LoopbackStreamShuffle:
         run.ctx, run.dev, run.stream_stats = self.ctx, self.dev, {}
         run._run_op = lambda op, ins, v, s: G.OPS[op["op"]](op, ins, v)
         bplan = dict(agg=self.B.ops[0], pre=[], rest=[], budget=splan["budget"], source_bytes=splan["source_bytes"],
+                     hold_bytes=splan["budget"] // 4,
                      chunk=splan["chunk"])
         agg = SA.StreamAggregator(run, self.B, vb, bplan)
         gens = [ST._chunks(splan, s, self.dev, None) for s in range(W)]

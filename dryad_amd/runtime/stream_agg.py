@@ -367,6 +367,12 @@ class StreamAggregator:
         # GroupBy of one integer key: the directly addressed running state while it fits
         use = runner.ctx._props.get("StreamDenseState", True) and self.kind == "group"
         self.dense = DenseState(self.d, self.budget) if use else None
+        # received partials of a streamed shuffle (add_partial) held in HBM up to ``hold_bytes`` and
+        # combined once per batch by the partition + LDS aggregation of a final GroupBy (the bulk
+        # path's kernels) instead of folded round by round into the running state with per-row
+        # atomics: with one batch the whole fold is one final reduce after the last round
+        self.hold_budget = int(splan.get("hold_bytes") or 0) if self.kind == "group" else 0
+        self.held, self.held_bytes, self.direct = [], 0, None
 
     # ------------------------------------------------------------------ per chunk
     def _partial(self, t: DeviceTable) -> DeviceTable:
@@ -457,7 +463,39 @@ class StreamAggregator:
             self.p["chunk_bytes_first"] = _nbytes(part)
         if self.kind == "distinct":
             part = G.op_distinct(self.agg, [part], self.v)
+        if self.hold_budget:
+            nb = _nbytes(part)
+            if self.held_bytes + nb > self.hold_budget:
+                self._flush_held()
+            if nb <= self.hold_budget:
+                self.held.append(part)
+                self.held_bytes += nb
+                return
         self._fold_in(part, part.n)
+
+    def _state_only_direct(self) -> bool:
+        return self.K is None and (self.dense is None or self.dense.nbytes() == 0)
+
+    def _state_empty(self) -> bool:
+        return self.K is None and (self.dense is None or self.dense.nbytes() == 0) and self.direct is None
+
+    def _flush_held(self):
+        """The held partials combined into one partial row per key: kept as is while nothing else
+        is held (the common case: every received round fits), else folded into the state."""
+        if not self.held:
+            return
+        t = DeviceTable.concat(self.held) if len(self.held) > 1 else self.held[0]
+        self.held, self.held_bytes = [], 0
+        self.stats["held_batches"] = self.stats.get("held_batches", 0) + 1
+        comb = G.combine_partials(t, self.d)
+        del t
+        if self._state_empty():
+            self.direct = comb
+            return
+        if self.direct is not None:
+            prev, self.direct = self.direct, None
+            self._fold_in(prev, prev.n)
+        self._fold_in(comb, comb.n)
 
     def _fold_in(self, part: DeviceTable, rows_in: int):
         if self.dense is not None:
@@ -492,6 +530,21 @@ class StreamAggregator:
     # ------------------------------------------------------------------ end of stream
     def bucket_results(self, final: bool):
         """Yield each bucket's folded state (``final``: reduced to the GroupBy's result)."""
+        if self.held and self._state_empty():
+            # every received partial held: ONE final reduce over them (the bulk stage's kernels)
+            t = DeviceTable.concat(self.held) if len(self.held) > 1 else self.held[0]
+            self.held, self.held_bytes = [], 0
+            self.stats["held_batches"] = self.stats.get("held_batches", 0) + 1
+            yield G.final_reduce(t, self.d) if final else G.combine_partials(t, self.d)
+            return
+        self._flush_held()
+        if self.direct is not None and self._state_only_direct():
+            t, self.direct = self.direct, None
+            yield G.final_reduce(t, self.d) if final else t
+            return
+        if self.direct is not None:
+            t, self.direct = self.direct, None
+            self._fold_in(t, t.n)
         if self.dense is not None:
             t = self.dense.to_partial()
             self.dense = None

@@ -116,7 +116,10 @@ def run(desc, runner, lay) -> dict:
     vctx_a = {p: GpuVertexContext(p, A.partitions, runner.vids[A.id][p], 0, A, dev, w, runner) for p in parts_a}
     vctx_b = {p: GpuVertexContext(p, B.partitions, runner.vids[B.id][p], 0, B, dev, w, runner) for p in parts_b}
     splan = dict(lay, pre=A.ops[1:-2], agg=A.ops[-2], rest=A.ops[-1:])
+    # received partials held up to a quarter of the budget (their concatenation doubles it) and
+    # reduced once (StreamAggregator.hold_budget)
     bplan = dict(agg=B.ops[0], pre=[], rest=B.ops[1:], budget=lay["budget"], source_bytes=lay["source_bytes"],
+                 hold_bytes=lay["budget"] // (4 * max(1, len(parts_b))),
                  chunk=lay["chunk"])
     aggs = {p: SA.StreamAggregator(runner, B, vctx_b[p], dict(bplan)) for p in parts_b}
 
@@ -197,5 +200,6 @@ def run(desc, runner, lay) -> dict:
         exchange_wait_s=round(wait_s, 3), stream_s=round(t1 - t0, 3), finish_s=round(time.perf_counter() - t1, 3),
         spilled_bytes=sum(x.get("spilled_bytes", 0) for x in st), combines=sum(x.get("combines", 0) for x in st),
         dense_state=any("dense_state_GB" in x for x in st), budget_bytes=lay["budget"],
+        held_batches=sum(x.get("held_batches", 0) for x in st),
         result="streamed to the output store" if written else "concatenated in HBM", result_bytes=written)
     return out

@@ -64,6 +64,20 @@ def test_streamed_shuffle_groupby_matches_oracle(keys, dense):
     _close(got, sorted(q(_loc())))
 
 
+def test_streamed_shuffle_holds_received_partials_and_reduces_once():
+    """A budget the received partials fit: every round is held in HBM and each final partition
+    reduces them ONCE after the last round (the bulk stage's kernels), no per-round folds."""
+    src = SRC.format(n=600_000, P=2, k=40_000)
+    q = lambda c: c.FromStore(src).GroupBy(lambda r: r[0], lambda k, g: (k, g.Count(), g.Sum(lambda r: r[1]),  # noqa: E731
+                                                                          g.Max(lambda r: r[4])))
+    g = _ctx(2, budget=1 << 30)
+    got = sorted(q(g))
+    res, st = _shuffle_stats(g)
+    assert st and st[0]["rounds"] > 2 and st[0]["held_batches"] == 2 and st[0]["spilled_bytes"] == 0, st
+    assert res["fallbacks"] == [], res["fallbacks"]
+    assert got == sorted(q(_loc()))
+
+
 def test_streamed_shuffle_distinct_to_host_table():
     """Distinct over two partitions, the result streamed bucket by bucket into pinned host columns
     (host://), read back oracle-equal."""
