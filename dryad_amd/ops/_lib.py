@@ -185,15 +185,22 @@ def memcpy_async(dst: torch.Tensor, src: torch.Tensor, stream) -> None:
                                        ctypes.c_void_p(stream.cuda_stream)), "hipMemcpyAsync")
 
 
+PREFAULT_MIN_BYTES = 64 << 20
+
+
 class PinnedHostBuffer:
     """Exact-size page-locked host memory: a plain CPU tensor registered with hipHostRegister
     (torch's pinned allocator rounds requests up to a power of two, which for 100 GB spill
     buffers would double the host footprint)."""
 
-    def __init__(self, shape, dtype=torch.uint8):
+    def __init__(self, shape, dtype=torch.uint8, prefault: bool = True):
         self.tensor = torch.empty(shape, dtype=dtype)
         nbytes = self.tensor.numel() * self.tensor.element_size()
         self.registered = False
+        if prefault and nbytes >= PREFAULT_MIN_BYTES:
+            # first touch by torch's CPU threads: the kernel zeroes the fresh pages in parallel, and
+            # hipHostRegister then only locks resident pages instead of faulting them in one by one
+            self.tensor.view(-1).view(torch.uint8).zero_()
         if nbytes:
             check(hip_runtime().hipHostRegister(ctypes.c_void_p(self.tensor.data_ptr()), nbytes, 0), "hipHostRegister")
             self.registered = True
