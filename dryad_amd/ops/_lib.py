@@ -193,13 +193,13 @@ class PinnedHostBuffer:
     (torch's pinned allocator rounds requests up to a power of two, which for 100 GB spill
     buffers would double the host footprint)."""
 
-    def __init__(self, shape, dtype=torch.uint8, prefault: bool = True):
+    def __init__(self, shape, dtype=torch.uint8, prefault: bool = False):
         self.tensor = torch.empty(shape, dtype=dtype)
         nbytes = self.tensor.numel() * self.tensor.element_size()
         self.registered = False
         if prefault and nbytes >= PREFAULT_MIN_BYTES:
-            # first touch by torch's CPU threads: the kernel zeroes the fresh pages in parallel, and
-            # hipHostRegister then only locks resident pages instead of faulting them in one by one
+            # first touch by torch's CPU threads before hipHostRegister; measured no faster on the
+            # box (~15 GB/s of fresh pages either way, profiles/r6/r6f_pinned.log), so off by default
             self.tensor.view(-1).view(torch.uint8).zero_()
         if nbytes:
             check(hip_runtime().hipHostRegister(ctypes.c_void_p(self.tensor.data_ptr()), nbytes, 0), "hipHostRegister")
