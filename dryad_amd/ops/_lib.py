@@ -197,6 +197,7 @@ class PinnedHostBuffer:
         self.tensor = torch.empty(shape, dtype=dtype)
         nbytes = self.tensor.numel() * self.tensor.element_size()
         self.registered = False
+        self.pending = None            # event after the last queued copy of the last lease
         if prefault and nbytes >= PREFAULT_MIN_BYTES:
             # first touch by torch's CPU threads before hipHostRegister; measured no faster on the
             # box (~15 GB/s of fresh pages either way, profiles/r6/r6f_pinned.log), so off by default
@@ -205,8 +206,15 @@ class PinnedHostBuffer:
             check(hip_runtime().hipHostRegister(ctypes.c_void_p(self.tensor.data_ptr()), nbytes, 0), "hipHostRegister")
             self.registered = True
 
+    def wait(self):
+        """Block until the copies queued on the buffer by its last lease are done."""
+        if self.pending is not None:
+            self.pending.synchronize()
+            self.pending = None
+
     def release(self):
         if self.registered:
+            self.wait()                # a DMA still queued on the pages must finish before they unlock
             hip_runtime().hipHostUnregister(ctypes.c_void_p(self.tensor.data_ptr()))
             self.registered = False
         self.tensor = None
@@ -239,7 +247,14 @@ class PinnedLease:
         self.tensor = buf.tensor[: n * esz].view(dtype).view(*shape)
 
     def release(self):
+        """Back to the pool, possibly with copies still queued on it (e.g. a spilled piece's copy to
+        HBM): an event on the current stream marks them, and the buffer is neither unlocked nor
+        handed to another lease before it has passed."""
         if self._buf is not None:
+            if torch.cuda.is_available() and torch.cuda.is_initialized():
+                ev = torch.cuda.Event()
+                ev.record()
+                self._buf.pending = ev
             _PINNED_FREE.append(self._buf)
             while len(_PINNED_FREE) > PINNED_KEEP and \
                     sum(b.tensor.numel() for b in _PINNED_FREE) > PINNED_KEEP_BYTES:
@@ -259,6 +274,7 @@ def pinned_lease(shape, dtype=torch.uint8) -> PinnedLease:
             best = b
     if best is not None:
         _PINNED_FREE.remove(best)
+        best.wait()
     else:
         best = PinnedHostBuffer((max(n, 1),))
     return PinnedLease(best, shape, dtype)
