@@ -33,6 +33,17 @@ def main():
     q2 = lambda c: c.FromStore(src).Select(lambda r: r[0] % 90_001).Distinct()  # noqa: E731
     got2 = sorted(q2(g))
     assert got2 == sorted(q2(loc)), "Distinct differs from the oracle"
+    # a repartition written to a partfile table as rounds (one part writer per rank)
+    out = os.environ.get("SS_TMP", "/tmp") + f"/ss_rep_{W}.pt"
+    q3 = lambda c: c.FromStore(src).HashPartition(lambda r: r[1], W).Select(lambda r: (r[1], r[0] * 3))  # noqa: E731
+    q3(g).ToStore("partfile://" + out, delete_if_exists=True).SubmitAndWait()
+    res3 = g._get_executor().last_result
+    st3 = [v for v in (res3.get("streamed") or {}).values() if v.get("kind") == "streamed shuffle"]
+    assert st3 and st3[0]["mode"] == "repartition" and st3[0]["result_bytes"] > 0, res3.get("streamed")
+    assert res3["fallbacks"] == [], res3["fallbacks"]
+    if w.rank == 0:
+        assert sorted(loc.FromStore("partfile://" + out)) == sorted(q3(loc)), "repartition differs from the oracle"
+    w.barrier()
     print(f"STREAM_SHUFFLE_OK {W} rounds={st[0]['rounds']} exchanged_GB={st[0]['exchanged_GB']}", flush=True)
     shutdown()
 

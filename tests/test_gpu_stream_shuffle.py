@@ -92,6 +92,23 @@ def test_streamed_shuffle_distinct_to_host_table():
     assert got == sorted(q(_loc()))
 
 
+@pytest.mark.parametrize("P,store", [(2, "host"), (1, "partfile")])
+def test_streamed_repartition_to_store(P, store, tmp_path):
+    """HashPartition -> Select -> ToStore as rounds: each received round through B's Select and
+    straight into the output sink, never a whole partition in HBM; oracle-equal."""
+    src = SRC.format(n=500_000, P=P, k=1 << 20)
+    uri = "host://ss_rep" if store == "host" else "partfile://" + str(tmp_path / "rep.pt")
+    q = lambda c: c.FromStore(src).Where(lambda r: r[2] % 3 != 0).HashPartition(lambda r: r[0], P).Select(  # noqa: E731
+        lambda r: (r[0], r[1] + r[3]))
+    g = _ctx(P)
+    q(g).ToStore(uri, delete_if_exists=True).SubmitAndWait()
+    res, st = _shuffle_stats(g)
+    assert st and st[0]["mode"] == "repartition" and st[0]["rounds"] > 4, st
+    assert st[0]["result"] == "streamed to the output store" and st[0]["result_bytes"] > 0, st
+    assert res["fallbacks"] == [], res["fallbacks"]
+    assert sorted(g.FromStore(uri)) == sorted(q(_loc()))
+
+
 def test_streamed_groupby_result_to_partfile(tmp_path):
     """A leaf streamed GroupBy (one partition past the budget) writes its buckets' results straight
     into the output part files (PartFileSplitBytes: several at once) instead of concatenating them."""
