@@ -58,19 +58,6 @@ __device__ __forceinline__ uint32_t popc_below(uint64_t mask) {
 
 __device__ __forceinline__ uint64_t ballot64(bool p) { return __ballot(p); }
 
-// Lanes of the wave whose 8-bit digit equals this lane's (among lanes with `valid`): eight
-// ballots, no LDS traffic (the multisplit match of a radix rank).
-__device__ __forceinline__ uint64_t match_digit8(uint32_t d, bool valid) {
-  uint64_t m = __ballot(valid);
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    const bool bit = (d >> b) & 1u;
-    const uint64_t bb = __ballot(bit);
-    m &= bit ? bb : ~bb;
-  }
-  return m;
-}
-
 // Inclusive wave-level scan (64 lanes) of a 32-bit value.
 __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
   const int l = lane_id();

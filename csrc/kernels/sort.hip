@@ -1817,7 +1817,7 @@ __global__ __launch_bounds__(256) void os_hist_scan_kernel(uint32_t* __restrict_
   if (t == 0 && (uint64_t)total != n) atomicOr(err, 2u);
 }
 
-template <int ITEMS, int LB, bool MATCH>
+template <int ITEMS, int LB>
 __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__ in, E64* __restrict__ out,
                                                          uint64_t n, int shift, const uint32_t* __restrict__ gbase,
                                                          unsigned long long* granules, uint32_t* ticket,
@@ -1855,21 +1855,15 @@ __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__
       const uint32_t pos = w * (kTile / 4) + r * 64 + l;
       const bool valid = pos < cnt;
       const uint32_t d = valid ? digit_of(cur[r], shift) : 0u;
-      unsigned long long peers;
-      if constexpr (MATCH) {
-        const unsigned long long m = match_digit8(d, valid);   // (every lane takes part in the ballots)
-        peers = valid ? m : 0ull;
-      } else {
-        if (valid) atomicOr(&wmask[w][d], lanebit);
-        __builtin_amdgcn_wave_barrier();
-        peers = valid ? wmask[w][d] : 0ull;
-      }
+      if (valid) atomicOr(&wmask[w][d], lanebit);
+      __builtin_amdgcn_wave_barrier();
+      const unsigned long long peers = valid ? wmask[w][d] : 0ull;
       const uint32_t below = popc_below(peers);
       const uint32_t prior = wcnt[w][d];
       __builtin_amdgcn_wave_barrier();
       if (valid && below == 0) {
         wcnt[w][d] = prior + (uint32_t)__popcll(peers);
-        if constexpr (!MATCH) wmask[w][d] = 0ull;
+        wmask[w][d] = 0ull;
       }
       __builtin_amdgcn_wave_barrier();
       rk[r] = prior + below;
@@ -1958,11 +1952,6 @@ DR_API uint64_t dr_sort_u64_onesweep_workspace(uint64_t n) { return os_workspace
 // hist_part (nullable; sorts of bits [32 + 8k, 64) only): `parts` per-workgroup [4][256]
 // histograms of the digits of bits [32, 64) the producer of the entries wrote
 // (dr_terasort_gen_keys64_pitch128), used instead of the histogram read.
-static int g_os_match = 0;        // ranking variant of the scatter passes (A/B: dr_sort_onesweep_set_match)
-
-// A/B switch of the look-back scatter's in-wave ranking: 0 LDS atomicOr masks, 1 ballot match.
-DR_API void dr_sort_onesweep_set_match(int m) { g_os_match = m; }
-
 DR_API int dr_sort_u64_onesweep(E64* keys, E64* tmp, uint64_t n, int begin_bit, int end_bit, void* ws,
                                 uint64_t ws_bytes, const uint32_t* hist_part, uint32_t parts, uint32_t* err_out,
                                 hipStream_t s, int* result_in_tmp) {
@@ -1992,14 +1981,9 @@ DR_API int dr_sort_u64_onesweep(E64* keys, E64* tmp, uint64_t n, int begin_bit, 
   E64* dst = tmp;
   int flips = 0;
   for (int p = 0; p < P; ++p) {
-    if (g_os_match)
-      os_scatter_kernel<kOsItems, 4, true><<<(unsigned)tiles, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p,
-                                                                         gbase + p * kBins, granules, tickets + p, err,
-                                                                         2u * (p + 1), (uint32_t)tiles);
-    else
-      os_scatter_kernel<kOsItems, 4, false><<<(unsigned)tiles, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p,
-                                                                          gbase + p * kBins, granules, tickets + p, err,
-                                                                          2u * (p + 1), (uint32_t)tiles);
+    os_scatter_kernel<kOsItems, 4><<<(unsigned)tiles, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
+                                                                   granules, tickets + p, err, 2u * (p + 1),
+                                                                   (uint32_t)tiles);
     E64* x = src; src = dst; dst = x;
     flips ^= 1;
   }
