@@ -197,6 +197,24 @@ def all_gather_varlen(t: torch.Tensor, world: World | None = None) -> torch.Tens
     return torch.cat(parts, 0)
 
 
+def gather_json(obj, world: World | None = None) -> list:
+    """Every rank's JSON-serialisable ``obj`` (per-rank control data: part-file paths, report
+    records, error strings), as UTF-8 JSON bytes in one variable-length tensor all-gather.  Peers'
+    data is parsed, never unpickled (dict keys come back as strings, tuples as lists)."""
+    import json
+    w = world or get_world()
+    if not w.collective:
+        return [json.loads(json.dumps(obj))]
+    raw = json.dumps(obj).encode()
+    t = torch.frombuffer(bytearray(raw), dtype=torch.uint8) if raw else torch.zeros(0, dtype=torch.uint8)
+    n = torch.tensor([t.numel()], dtype=torch.int64)
+    ns = [int(x) for x in all_gather_tensor(n, w).view(-1).tolist()]
+    pad = torch.zeros(max(ns), dtype=torch.uint8)
+    pad[: t.numel()] = t
+    g = all_gather_tensor(pad, w).view(w.size, -1).cpu()
+    return [json.loads(bytes(g[r, : ns[r]].numpy()).decode()) for r in range(w.size)]
+
+
 def all_reduce_(t: torch.Tensor, op: str = "sum", world: World | None = None) -> torch.Tensor:
     w = world or get_world()
     if not w.collective:

@@ -603,7 +603,7 @@ class GpuJobRunner:
     def _gather_if_any(self, obj):
         """None when every rank passes None (one tensor all-gather of a flag, no pickling: the
         per-stage votes of an iterative job stay off the host's object path), else every rank's
-        object (all_gather_object, only when some rank has something to say)."""
+        record (JSON over a tensor all-gather, only when some rank has something to say)."""
         from ..parallel import shuffle
         st = shuffle.gang_status(obj is None, 0, self.world)
         if all(ok for ok, _ in st):
@@ -611,9 +611,8 @@ class GpuJobRunner:
         return self._gather_objects(obj)
 
     def _gather_objects(self, obj):
-        got = [None] * self.world.size
-        dist.all_gather_object(got, obj)
-        return got
+        """Every rank's outcome records (ints, strings), as JSON over a tensor all-gather."""
+        return shuffle.gather_json(obj, self.world)
 
     def _restore_fused_input(self, f, reread: bool = False):
         """Before a retry of a fused distributed OrderBy: its input table again.  A gen://terasort
@@ -1495,8 +1494,7 @@ class GpuJobRunner:
                 started = []
                 reps = [rep]
                 if W > 1:
-                    reps = [None] * W
-                    dist.all_gather_object(reps, rep)
+                    reps = shuffle.gather_json(rep, self.world)
                 T = max(r["t"] for r in reps)
                 for r, x in enumerate(reps):
                     for vid, ver, dup in x["started"]:
@@ -1637,8 +1635,7 @@ class GpuJobRunner:
                 ok, err = False, f"{type(e).__name__}: {e}"
         oks = [(ok, err)]
         if self.world.size > 1:
-            oks = [None] * self.world.size
-            dist.all_gather_object(oks, (ok, err))
+            oks = shuffle.gather_json([ok, err], self.world)
         bad = next((x for x in oks if not x[0]), None)
         if bad is not None:
             raise DryadLinqJobException(ErrorCode.JobToCreateTableFailed,
@@ -1807,8 +1804,7 @@ def _commit_partfile_impl(runner, s, uri, path, local):
         dt = streamed[0].dtype
     if W > 1 and (dt is None or dt == T.Pickle):
         # the record type one rank learnt from its streamed part (ranks without rows have none)
-        allts = [None] * W
-        dist.all_gather_object(allts, None if dt is None or dt == T.Pickle else T.dtype_to_json(dt))
+        allts = shuffle.gather_json(None if dt is None or dt == T.Pickle else T.dtype_to_json(dt), runner.world)
         got = next((x for x in allts if x is not None), None)
         dt = T.dtype_from_json(got) if got is not None else dt
     if not rows_fmt and (dt is None or dt == T.Pickle):
@@ -1908,8 +1904,10 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     gathered = [None] * W
     gathered_fmt = [None] * W
     if W > 1:
-        dist.all_gather_object(gathered, mine)
-        dist.all_gather_object(gathered_fmt, fmt_extra)
+        # part-file paths and the rows format (JSON over one tensor all-gather, no pickles)
+        got = shuffle.gather_json([[[int(p), v] for p, v in mine.items()], fmt_extra], runner.world)
+        gathered = [{p: v for p, v in x[0]} for x in got]
+        gathered_fmt = [x[1] for x in got]
     else:
         gathered = [mine]
     if me == 0:

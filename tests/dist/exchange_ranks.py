@@ -144,6 +144,13 @@ def main():
             (min(100 * r - 5 for r in senders), max(100 * r + 60 for r in senders))
         if ST.known(merged.cols["v"]) != want:
             bad.append(("bounds", unknown_rank, ST.known(merged.cols["v"]), want))
+    # per-rank control records as JSON over a tensor all-gather (no pickles), uneven sizes
+    from dryad_amd.parallel import shuffle as SHF
+    got = SHF.gather_json({"rank": me, "paths": [f"/tmp/p{me}.{j}" for j in range(me + 1)], "t": 0.5 * me,
+                           "err": None if me else "é boom"}, w)
+    if [g["rank"] for g in got] != list(range(W)) or got[W - 1]["paths"][-1] != f"/tmp/p{W - 1}.{W - 1}" \
+            or got[0]["err"] != "é boom" or got[1]["t"] != 0.5:
+        bad.append(("gather_json", got))
     w.barrier()
     assert not bad, (me, bad[:5])
     if me == 0:
