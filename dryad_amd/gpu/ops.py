@@ -354,6 +354,12 @@ def op_read(op, inputs, v):
                     torch.zeros(0, dtype=torch.uint8, device=v.device)
             if CD.layout(dt) is not None:
                 t = CD.decode(buf, dt)
+                # column bounds the writer measured (runtime/gpu_executor._commit_partfile_impl)
+                from . import stats as GST
+                for f, (lo, hi) in (sch.get("bounds") or {}).items():
+                    c = t.cols.get(f) if t is not None else None
+                    if c is not None and c.dtype in (torch.int64, torch.int32, torch.int16, torch.int8):
+                        GST.set_bounds(c, int(lo), int(hi))
             else:
                 from ..io import partfile as PF
                 idx = PF.read_index(path) if path is not None else None

@@ -1823,7 +1823,23 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     base = PF.default_base(path)
     os.makedirs(os.path.dirname(base) or ".", exist_ok=True)
     mine = {}
-    state = dict(fmt_extra=None)
+    state = dict(fmt_extra=None, bounds={}, noted=0)
+
+    def note_bounds(v):
+        """Union of the integer columns' [min, max] over this rank's written partitions (kept in
+        the table's schema, so a later read knows them as a generator's columns do: a GroupBy or
+        join packing by value width skips its min / max pass)."""
+        from ..gpu import stats as GST
+        state["noted"] += 1
+        for f, c in v.cols.items():
+            if c.dtype not in (torch.int64, torch.int32, torch.int16, torch.int8) or v.n == 0:
+                continue
+            kb = GST.known(c)
+            if kb is None:
+                mn, mx = torch.aminmax(c[: v.n])
+                kb = (int(mn.item()), int(mx.item()))
+            old = state["bounds"].get(f)
+            state["bounds"][f] = [kb[0], kb[1]] if old is None else [min(old[0], kb[0]), max(old[1], kb[1])]
 
     def write_parts():
         for p, v in local.items():
@@ -1877,6 +1893,7 @@ def _commit_partfile_impl(runner, s, uri, path, local):
             elif data is not None:
                 # device-encoded records: HBM -> pinned ring -> native writer threads
                 if index is None and v.n and data.numel() % v.n == 0:      # fixed-width records
+                    note_bounds(v)
                     mine[p] = _write_split(runner, tmp, data, v.n, data.numel() // v.n)
                     continue
                 WR.write_device(tmp, data, stats=runner.write_stats)
@@ -1901,15 +1918,20 @@ def _commit_partfile_impl(runner, s, uri, path, local):
                     pass
         raise
     fmt_extra = state["fmt_extra"]
+    empty = sum(1 for v in local.values() if (isinstance(v, DeviceTable) and v.n == 0) or (isinstance(v, list) and not v))
+    # the bounds hold for the table only when every non-empty partition was measured
+    bounds = state["bounds"] if state["noted"] + empty == len(local) else None
     gathered = [None] * W
     gathered_fmt = [None] * W
     if W > 1:
-        # part-file paths and the rows format (JSON over one tensor all-gather, no pickles)
-        got = shuffle.gather_json([[[int(p), v] for p, v in mine.items()], fmt_extra], runner.world)
+        # part-file paths, the rows format and the column bounds (JSON over one tensor all-gather)
+        got = shuffle.gather_json([[[int(p), v] for p, v in mine.items()], fmt_extra, bounds], runner.world)
         gathered = [{p: v for p, v in x[0]} for x in got]
         gathered_fmt = [x[1] for x in got]
+        allb = [x[2] for x in got]
     else:
         gathered = [mine]
+        allb = [bounds]
     if me == 0:
         parts = {}
         for d in gathered:
@@ -1922,7 +1944,15 @@ def _commit_partfile_impl(runner, s, uri, path, local):
             extras = [x for x in gathered_fmt if x] if W > 1 else [fmt_extra]
             write_schema(path, dt, "rows", **(extras[0] if extras and extras[0] else {}))
         else:
-            write_schema(path, dt, "binary")
+            extra = {}
+            if all(b is not None for b in allb) and any(allb):
+                union = {}
+                for b in allb:
+                    for f, (lo, hi) in b.items():
+                        u = union.get(f)
+                        union[f] = [lo, hi] if u is None else [min(u[0], lo), max(u[1], hi)]
+                extra["bounds"] = union
+            write_schema(path, dt, "binary", **extra)
     if W > 1:
         runner.world.barrier()
     if me == 0:

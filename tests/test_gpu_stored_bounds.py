@@ -1,0 +1,39 @@
+"""Column bounds travel with a stored table: the GPU executor's partfile writer records each
+integer column's [min, max] in the schema sidecar and a device read registers them, so a GroupBy
+over the stored table packs by value width without a min / max pass."""
+import json
+
+import pytest
+import torch
+
+import dryad_amd as D
+
+pytestmark = pytest.mark.gpu
+
+
+def test_partfile_schema_keeps_column_bounds(tmp_path):
+    from dryad_amd.gpu import stats as GST
+    from dryad_amd.runtime.jobmanager import schema_path
+    uri = "partfile://" + str(tmp_path / "r64.pt")
+    g = D.DryadLinqContext(platform="gpu")
+    g.PartitionCount = 2
+    src = "gen://records64?count=200000&partitions=2&keys=5000&seed=3&cols=4"
+    g.FromStore(src).Select(lambda r: (r[0], r[1] - 7, r[2])).ToStore(uri, delete_if_exists=True).SubmitAndWait()
+    sch = json.load(open(schema_path(str(tmp_path / "r64.pt"))))
+    b = sch.get("bounds")
+    assert b is not None and len(b) == 3, sch
+    loc = D.DryadLinqContext(1)
+    loc.LocalDebug = True
+    rows = list(loc.FromStore(src).Select(lambda r: (r[0], r[1] - 7, r[2])))
+    exp = [[min(x[j] for x in rows), max(x[j] for x in rows)] for j in range(3)]
+    assert sorted(b.values()) == sorted(exp), (b, exp)
+    # a device read of a part registers them on its columns
+    from types import SimpleNamespace
+    from dryad_amd.gpu.ops import OPS
+    v = SimpleNamespace(partition=0, device=torch.device("cuda"), runner=None, stage=None)
+    t = OPS["read"](dict(op="read", uri=uri), [], v)
+    assert t.n > 0 and sorted(GST.known(c) for c in t.cols.values()) == sorted(tuple(x) for x in b.values())
+    got = sorted(g.FromStore(uri).GroupBy(lambda r: r[0], lambda k, grp: (k, grp.Count())))
+    assert len(got) == len({x[0] for x in rows}) and sum(c for _, c in got) == len(rows)
+    res = g._get_executor().last_result
+    assert res["fallbacks"] == [], res["fallbacks"]
