@@ -166,6 +166,7 @@ class HostColumns:
     def __init__(self, shape):
         self.shape = shape
         self.pieces = []               # [(n, {column: pinned tensor [n, ...]}, [leases])]
+        self.bounds = []               # per piece: {column: (lo, hi)} of the columns that had them
         self.n = 0
 
     def append(self, t) -> None:
@@ -174,7 +175,9 @@ class HostColumns:
             raise ValueError("HostColumns holds fixed-width columnar tables")
         if t.n == 0:
             return
+        from ..gpu import stats as GST
         cols, leases = {}, []
+        self.bounds.append({k: b for k, b in ((k, GST.known(v)) for k, v in t.cols.items()) if b is not None})
         for k, v in t.cols.items():
             src = v[: t.n]
             if not src.is_cuda:                 # a CPU run: plain host memory
@@ -196,20 +199,31 @@ class HostColumns:
 
     def device_pieces(self, device, max_rows: int | None = None):
         """Yield the table as device tables of at most ``max_rows`` rows, in row order."""
+        from ..gpu import stats as GST
         from ..gpu.table import DeviceTable
-        for n, cols, _ in self.pieces:
+        for i, (n, cols, _) in enumerate(self.pieces):
             step = n if not max_rows else max(1, int(max_rows))
+            bnd = self.bounds[i] if i < len(self.bounds) else {}
             for a in range(0, n, step):
                 b = min(n, a + step)
-                yield DeviceTable(b - a, self.shape, {k: v[a:b].to(device, non_blocking=True) for k, v in cols.items()})
+                t = DeviceTable(b - a, self.shape, {k: v[a:b].to(device, non_blocking=True) for k, v in cols.items()})
+                for k, (lo, hi) in bnd.items():       # the bounds the piece's columns had on the device
+                    GST.set_bounds(t.cols[k], lo, hi)
+                yield t
 
     def to_device(self, device):
         from ..gpu.table import DeviceTable
         if not self.pieces:
             return DeviceTable(0, self.shape, {})
+        from ..gpu import stats as GST
         names = self.columns()
-        return DeviceTable(self.n, self.shape, {k: torch.cat([c[k] for _, c, _ in self.pieces]).to(device)
-                                                for k in names})
+        t = DeviceTable(self.n, self.shape, {k: torch.cat([c[k] for _, c, _ in self.pieces]).to(device)
+                                             for k in names})
+        for k in names:                           # bounds every piece knew: their union
+            bs = [b.get(k) for b in self.bounds]
+            if bs and len(bs) == len(self.pieces) and all(x is not None for x in bs):
+                GST.set_bounds(t.cols[k], min(x[0] for x in bs), max(x[1] for x in bs))
+        return t
 
     def to_objects(self) -> list:
         from ..gpu.table import DeviceTable
@@ -224,7 +238,7 @@ class HostColumns:
         for _, _, leases in self.pieces:
             for ls in leases:
                 ls.release()
-        self.pieces, self.n = [], 0
+        self.pieces, self.bounds, self.n = [], [], 0
 
     def __len__(self):
         return self.n
