@@ -57,3 +57,37 @@ def bounds(cols: list) -> list:
             out[i] = (int(got[2 * j]), int(got[2 * j + 1]))
             set_bounds(cols[i], *out[i])
     return out
+
+
+class BoundsAcc:
+    """Union of the integer columns' [min, max] over the pieces of a table written piece by piece
+    (a stored table keeps them in its schema, runtime/gpu_executor._commit_partfile_impl).
+    ``result()`` is None once a piece was not a columnar device table (nothing known then)."""
+
+    _INT = (torch.int64, torch.int32, torch.int16, torch.int8)
+
+    def __init__(self):
+        self.bounds, self.ok = {}, True
+
+    def add(self, t) -> None:
+        if not self.ok:
+            return
+        cols = getattr(t, "cols", None)
+        if cols is None or getattr(t, "rows", None) is not None or getattr(t, "strs", None):
+            if getattr(t, "n", len(t) if isinstance(t, list) else 1):
+                self.ok = False
+            return
+        if t.n == 0:
+            return
+        for f, c in cols.items():
+            if c.dtype not in self._INT:
+                continue
+            kb = known(c)
+            if kb is None:
+                mn, mx = torch.aminmax(c[: t.n])
+                kb = (int(mn.item()), int(mx.item()))
+            o = self.bounds.get(f)
+            self.bounds[f] = [kb[0], kb[1]] if o is None else [min(o[0], kb[0]), max(o[1], kb[1])]
+
+    def result(self):
+        return dict(self.bounds) if self.ok else None

@@ -1825,25 +1825,28 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     mine = {}
     state = dict(fmt_extra=None, bounds={}, noted=0)
 
-    def note_bounds(v):
+    def note_bounds(v=None, measured=None):
         """Union of the integer columns' [min, max] over this rank's written partitions (kept in
         the table's schema, so a later read knows them as a generator's columns do: a GroupBy or
-        join packing by value width skips its min / max pass)."""
-        from ..gpu import stats as GST
+        join packing by value width skips its min / max pass).  ``measured``: a streamed part's
+        own union (its writer measured every chunk)."""
+        from ..gpu.stats import BoundsAcc
+        if measured is None:
+            acc = BoundsAcc()
+            acc.add(v)
+            measured = acc.result()
+        if measured is None:
+            return
         state["noted"] += 1
-        for f, c in v.cols.items():
-            if c.dtype not in (torch.int64, torch.int32, torch.int16, torch.int8) or v.n == 0:
-                continue
-            kb = GST.known(c)
-            if kb is None:
-                mn, mx = torch.aminmax(c[: v.n])
-                kb = (int(mn.item()), int(mx.item()))
+        for f, (lo, hi) in measured.items():
             old = state["bounds"].get(f)
-            state["bounds"][f] = [kb[0], kb[1]] if old is None else [min(old[0], kb[0]), max(old[1], kb[1])]
+            state["bounds"][f] = [lo, hi] if old is None else [min(old[0], lo), max(old[1], hi)]
 
     def write_parts():
         for p, v in local.items():
             tmp = PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, 0)
+            if isinstance(v, GS.StreamedPart) and v.bounds is not None and v.rows is None:
+                note_bounds(measured=v.bounds)
             if isinstance(v, GS.StreamedPart) and isinstance(v.path, list):    # split over part files
                 mine[p] = []
                 for j, f in enumerate(v.path):

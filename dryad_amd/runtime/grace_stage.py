@@ -60,9 +60,10 @@ class StreamedPart:
     split over several part files) by a streaming stage; the output commit renames it into place
     (runtime/gpu_executor._commit_partfile_impl)."""
 
-    def __init__(self, path: str, n: int, nbytes: int, dtype, rows: dict | None = None):
+    def __init__(self, path: str, n: int, nbytes: int, dtype, rows: dict | None = None, bounds: dict | None = None):
         self.path, self.n, self.nbytes, self.dtype = path, n, nbytes, dtype
         self.rows = rows                  # raw fixed-width rows: {stride, key_off, key_len}
+        self.bounds = bounds              # integer columns' {field: [min, max]} when measured
 
 
 # ------------------------------------------------------------------------------------------------

@@ -34,6 +34,8 @@ class PartfileSink:
         self.writer, self.dtype = None, None
         self.n, self.written_bytes, self.index = 0, 0, []
         self.paths = self.fbytes = self.frecs = self.findex = None
+        from ..gpu.stats import BoundsAcc
+        self.acc = BoundsAcc()
 
     @staticmethod
     def applicable(runner, stage) -> bool:
@@ -82,6 +84,7 @@ class PartfileSink:
                 if data.n > j0:
                     self.index.append(offs[j0::B] + self.written_bytes)
             self.writer.write(enc)
+        self.acc.add(data)
         self.n += data.n
         self.written_bytes += enc.numel()
         return True
@@ -108,12 +111,13 @@ class PartfileSink:
                 else:
                     os.remove(f)
             self.writer = None
-            return StreamedPart(keep or self.paths[:1], self.n, sum(sizes), self.dtype), sum(sizes)
+            return StreamedPart(keep or self.paths[:1], self.n, sum(sizes), self.dtype,
+                                bounds=self.acc.result()), sum(sizes)
         written = self.writer.close()
         if self.index:
             PF.write_index(self.tmp, self.n, written, torch.cat(self.index).cpu().numpy(), CD.BLOCK)
         self.writer = None
-        return StreamedPart(self.tmp, self.n, written, self.dtype), written
+        return StreamedPart(self.tmp, self.n, written, self.dtype, bounds=self.acc.result()), written
 
     def abort(self):
         """Stop the writer (its threads, the process-wide ring) and remove the partial files."""

@@ -238,7 +238,9 @@ def run(runner, s, p, version, vctx, plan, cancel=None):
     tmp = f"{PF.tmp_part_path(base, p, runner.vids[s.id][p], 0, version)}.stream"
     from .grace_stage import _table_dtype
     from .. import types as T
+    from ..gpu.stats import BoundsAcc
     n, rows_fmt, chunks = 0, None, 0
+    acc = BoundsAcc()
     dtype = None if s.dtype in (None, T.Pickle) else s.dtype    # unknown: the first chunk decides
     with WR.PartWriter(tmp, vctx.device, runner.write_stats) as w:
         for t in _chunks(plan, p, vctx.device, vctx):
@@ -256,11 +258,12 @@ def run(runner, s, p, version, vctx, plan, cancel=None):
                     raise NotStreamable(f"{s.name}: no fixed record layout to stream")
             b, rf = _encode(data, dtype)
             rows_fmt = rows_fmt or rf
+            acc.add(data)
             w.write(b)
             n += data.n if isinstance(data, DeviceTable) else len(data)
             chunks += 1
     runner.stream_stats[(s.id, p)] = dict(chunks=chunks, records=n, bytes=w.off)
-    return StreamedPart(tmp, n, w.off, dtype, rows=rows_fmt)
+    return StreamedPart(tmp, n, w.off, dtype, rows=rows_fmt, bounds=acc.result())
 
 
 def partition_plan(runner, s):
@@ -305,7 +308,9 @@ def run_partitioned(runner, s, p, version, vctx, plan):
     os.makedirs(os.path.dirname(base) or ".", exist_ok=True)
     paths = [f"{PF.tmp_part_path(base, k, runner.vids[B.id][k], 0, version)}.stream" for k in range(nparts)]
     dtype = None if B.dtype in (None, T.Pickle) else B.dtype
+    from ..gpu.stats import BoundsAcc
     counts, rows_fmt, chunks = [0] * nparts, None, 0
+    accs = [BoundsAcc() for _ in range(nparts)]
     w = WR.PartWriter(paths, vctx.device, runner.write_stats)
     try:
         for t in _chunks(plan, p, vctx.device, vctx):
@@ -323,6 +328,7 @@ def run_partitioned(runner, s, p, version, vctx, plan):
                         raise NotStreamable(f"{s.name}: no fixed record layout to stream")
                 b, rf = _encode(piece, dtype)
                 rows_fmt = rows_fmt or rf
+                accs[k].add(piece)
                 w.write(b, file=k)
                 counts[k] += piece.n if isinstance(piece, DeviceTable) else len(piece)
             chunks += 1
@@ -337,4 +343,5 @@ def run_partitioned(runner, s, p, version, vctx, plan):
         raise
     runner.stream_stats[(s.id, p)] = dict(chunks=chunks, records=sum(counts), bytes=sum(sizes), ports=nparts,
                                           kind="streamed partition to store")
-    return [StreamedPart(paths[k], counts[k], sizes[k], dtype, rows=rows_fmt) for k in range(nparts)]
+    return [StreamedPart(paths[k], counts[k], sizes[k], dtype, rows=rows_fmt, bounds=accs[k].result())
+            for k in range(nparts)]
