@@ -1895,8 +1895,8 @@ def _commit_partfile_impl(runner, s, uri, path, local):
                     f.write(gzip.compress(raw, compresslevel=6))
             elif data is not None:
                 # device-encoded records: HBM -> pinned ring -> native writer threads
+                note_bounds(v)
                 if index is None and v.n and data.numel() % v.n == 0:      # fixed-width records
-                    note_bounds(v)
                     mine[p] = _write_split(runner, tmp, data, v.n, data.numel() // v.n)
                     continue
                 WR.write_device(tmp, data, stats=runner.write_stats)

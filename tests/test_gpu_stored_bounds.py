@@ -19,6 +19,8 @@ def test_partfile_schema_keeps_column_bounds(tmp_path):
     g.PartitionCount = 2
     src = "gen://records64?count=200000&partitions=2&keys=5000&seed=3&cols=4"
     g.FromStore(src).Select(lambda r: (r[0], r[1] - 7, r[2])).ToStore(uri, delete_if_exists=True).SubmitAndWait()
+    res0 = g._get_executor().last_result
+    assert res0["fallbacks"] == [], res0["fallbacks"]
     sch = json.load(open(schema_path(str(tmp_path / "r64.pt"))))
     b = sch.get("bounds")
     assert b is not None and len(b) == 3, sch
