@@ -217,8 +217,16 @@ class HostColumns:
             return DeviceTable(0, self.shape, {})
         from ..gpu import stats as GST
         names = self.columns()
-        t = DeviceTable(self.n, self.shape, {k: torch.cat([c[k] for _, c, _ in self.pieces]).to(device)
-                                             for k in names})
+        cols = {}
+        for k in names:                           # piece by piece into one device column (no host copy)
+            first = self.pieces[0][1][k]
+            dst = torch.empty((self.n,) + tuple(first.shape[1:]), dtype=first.dtype, device=device)
+            a = 0
+            for n, c, _ in self.pieces:
+                dst[a: a + n].copy_(c[k], non_blocking=True)
+                a += n
+            cols[k] = dst
+        t = DeviceTable(self.n, self.shape, cols)
         for k in names:                           # bounds every piece knew: their union
             bs = [b.get(k) for b in self.bounds]
             if bs and len(bs) == len(self.pieces) and all(x is not None for x in bs):

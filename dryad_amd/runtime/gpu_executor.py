@@ -1741,6 +1741,10 @@ class GpuJobRunner:
                         tabs[p] = v
                     elif isinstance(v, DeviceTable) and v.rows is not None and v.device.type == "cuda":
                         tabs[p] = HostRows.from_tensor(v.rows, v.shape.key_off, v.shape.key_len)
+                    elif isinstance(v, DeviceTable) and v.device.type == "cuda" and v.heap is None and not v.strs:
+                        h = HostColumns(v.shape)            # columns DMA'd into pinned host memory
+                        h.append(v)
+                        tabs[p] = h
                     else:
                         tabs[p] = _to_objects(v) if not isinstance(v, list) else v
                 provider_for(uri).put(uri, {"dtype": s.dtype, "partitions": s.partitions, "local": tabs,

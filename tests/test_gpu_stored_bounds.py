@@ -11,9 +11,16 @@ import dryad_amd as D
 pytestmark = pytest.mark.gpu
 
 
-def test_partfile_schema_keeps_column_bounds(tmp_path):
+def test_partfile_schema_keeps_column_bounds(tmp_path, monkeypatch):
     from dryad_amd.gpu import stats as GST
+    from dryad_amd.runtime import gpu_executor as GE
     from dryad_amd.runtime.jobmanager import schema_path
+    seen = []
+
+    def spy(self, s, uri, path, local):
+        seen.append({p: (type(v).__name__, getattr(v, "bounds", "-")) for p, v in local.items()})
+        return GE._commit_partfile_impl(self, s, uri, path, local)
+    monkeypatch.setattr(GE.GpuJobRunner, "_commit_partfile", spy)
     uri = "partfile://" + str(tmp_path / "r64.pt")
     g = D.DryadLinqContext(platform="gpu")
     g.PartitionCount = 2
@@ -23,7 +30,7 @@ def test_partfile_schema_keeps_column_bounds(tmp_path):
     assert res0["fallbacks"] == [], res0["fallbacks"]
     sch = json.load(open(schema_path(str(tmp_path / "r64.pt"))))
     b = sch.get("bounds")
-    assert b is not None and len(b) == 3, sch
+    assert b is not None and len(b) == 3, (sch, seen, res0.get("streamed"))
     loc = D.DryadLinqContext(1)
     loc.LocalDebug = True
     rows = list(loc.FromStore(src).Select(lambda r: (r[0], r[1] - 7, r[2])))
@@ -39,3 +46,22 @@ def test_partfile_schema_keeps_column_bounds(tmp_path):
     assert len(got) == len({x[0] for x in rows}) and sum(c for _, c in got) == len(rows)
     res = g._get_executor().last_result
     assert res["fallbacks"] == [], res["fallbacks"]
+
+
+def test_columnar_result_to_host_table_stays_columnar():
+    """A columnar device result written to host:// is DMA'd into pinned host columns (not turned
+    into Python records) and read back to the device with its bounds."""
+    from dryad_amd.gpu import stats as GST
+    from dryad_amd.io.hosttable import HostColumns
+    from dryad_amd.io.providers import provider_for
+    g = D.DryadLinqContext(platform="gpu")
+    src = "gen://records64?count=300000&partitions=1&keys=7000&seed=9&cols=3"
+    g.FromStore(src).ToStore("host://cols_src", delete_if_exists=True).SubmitAndWait()
+    h = provider_for("host://cols_src").get("host://cols_src")["local"][0]
+    assert isinstance(h, HostColumns) and h.n == 300000
+    t = h.to_device(torch.device("cuda"))
+    assert GST.known(t.cols[list(t.cols)[0]]) == (0, 6999)
+    got = sorted(g.FromStore("host://cols_src").GroupBy(lambda r: r[0], lambda k, grp: (k, grp.Count())))
+    loc = D.DryadLinqContext(1)
+    loc.LocalDebug = True
+    assert got == sorted(loc.FromStore(src).GroupBy(lambda r: r[0], lambda k, grp: (k, grp.Count())))
