@@ -21,6 +21,14 @@ def test_partfile_schema_keeps_column_bounds(tmp_path, monkeypatch):
         seen.append({p: (type(v).__name__, getattr(v, "bounds", "-")) for p, v in local.items()})
         return GE._commit_partfile_impl(self, s, uri, path, local)
     monkeypatch.setattr(GE.GpuJobRunner, "_commit_partfile", spy)
+    calls = []
+    orig_add = GST.BoundsAcc.add
+
+    def add(self, t):
+        orig_add(self, t)
+        calls.append((type(t).__name__, getattr(t, "n", None), self.ok, dict(self.bounds),
+                      {k: str(v.dtype) for k, v in (getattr(t, "cols", None) or {}).items()}))
+    monkeypatch.setattr(GST.BoundsAcc, "add", add)
     uri = "partfile://" + str(tmp_path / "r64.pt")
     g = D.DryadLinqContext(platform="gpu")
     g.PartitionCount = 2
@@ -30,7 +38,7 @@ def test_partfile_schema_keeps_column_bounds(tmp_path, monkeypatch):
     assert res0["fallbacks"] == [], res0["fallbacks"]
     sch = json.load(open(schema_path(str(tmp_path / "r64.pt"))))
     b = sch.get("bounds")
-    assert b is not None and len(b) == 3, (sch, seen, res0.get("streamed"))
+    assert b is not None and len(b) == 3, (sch, seen, calls, res0.get("streamed"))
     loc = D.DryadLinqContext(1)
     loc.LocalDebug = True
     rows = list(loc.FromStore(src).Select(lambda r: (r[0], r[1] - 7, r[2])))
