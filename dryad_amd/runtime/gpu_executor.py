@@ -1806,8 +1806,18 @@ def _commit_partfile_impl(runner, s, uri, path, local):
     streamed = [v for v in local.values() if isinstance(v, GS.StreamedPart)]
     if streamed and (dt is None or dt == T.Pickle):
         dt = streamed[0].dtype
-    if W > 1 and (dt is None or dt == T.Pickle):
-        # the record type one rank learnt from its streamed part (ranks without rows have none)
+    if dt is None or dt == T.Pickle:
+        # a plan that does not know the record type (e.g. a Select to tuples): the device tables'
+        # columns define it, so the parts are device-encoded instead of going through host records
+        for v in local.values():
+            if isinstance(v, DeviceTable) and v.device.type == "cuda":
+                got = GS._table_dtype(v)
+                if got is not None:
+                    dt = got
+                    break
+    if W > 1 and (s.dtype is None or s.dtype == T.Pickle):
+        # every rank takes the record type the first rank that knows one learnt (ranks without
+        # rows have none); the plan-level condition keeps every rank in this collective
         allts = shuffle.gather_json(None if dt is None or dt == T.Pickle else T.dtype_to_json(dt), runner.world)
         got = next((x for x in allts if x is not None), None)
         dt = T.dtype_from_json(got) if got is not None else dt
