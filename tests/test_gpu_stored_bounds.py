@@ -43,13 +43,17 @@ def test_partfile_schema_keeps_column_bounds(tmp_path, monkeypatch):
     loc.LocalDebug = True
     rows = list(loc.FromStore(src).Select(lambda r: (r[0], r[1] - 7, r[2])))
     exp = [[min(x[j] for x in rows), max(x[j] for x in rows)] for j in range(3)]
-    assert sorted(b.values()) == sorted(exp), (b, exp)
+    # bounds, not extremes: a column the generator declared keeps its declared range, a computed
+    # one is measured exactly
+    got_b = [b[f"Item{j + 1}"] for j in range(3)]
+    assert all(lo <= e[0] and e[1] <= hi for (lo, hi), e in zip(got_b, exp)), (b, exp)
+    assert got_b[1] == exp[1], (b, exp)
     # a device read of a part registers them on its columns
     from types import SimpleNamespace
     from dryad_amd.gpu.ops import OPS
     v = SimpleNamespace(partition=0, device=torch.device("cuda"), runner=None, stage=None)
     t = OPS["read"](dict(op="read", uri=uri), [], v)
-    assert t.n > 0 and sorted(GST.known(c) for c in t.cols.values()) == sorted(tuple(x) for x in b.values())
+    assert t.n > 0 and [GST.known(t.cols[f]) for f in sorted(b)] == [tuple(b[f]) for f in sorted(b)]
     got = sorted(g.FromStore(uri).GroupBy(lambda r: r[0], lambda k, grp: (k, grp.Count())))
     assert len(got) == len({x[0] for x in rows}) and sum(c for _, c in got) == len(rows)
     res = g._get_executor().last_result
