@@ -146,6 +146,29 @@ def exists(meta_path: str) -> bool:
 # by a daemon thread (and by the next delete's sweep, after a restart).
 RECYCLE_DIR = ".recycle"
 RECYCLE_TTL = 60.0
+_MINE: set = set()            # recycled files this process created (unlinked at exit if unclaimed)
+_ATEXIT = False
+
+
+def _remember(path: str) -> None:
+    """Track a recycled file; the first one registers the exit hook that unlinks what nobody
+    claimed (a short script, or a failed write whose commit never dropped them, exits before the
+    daemon thread's TTL)."""
+    global _ATEXIT
+    _MINE.add(path)
+    if not _ATEXIT:
+        import atexit
+        atexit.register(_drop_mine)
+        _ATEXIT = True
+
+
+def _drop_mine() -> None:
+    for q in list(_MINE):
+        try:
+            os.remove(q)                 # claimed ones were renamed away: nothing to remove
+        except OSError:
+            pass
+    _MINE.clear()
 
 
 def _recycle_dir(path: str) -> str:
@@ -234,6 +257,7 @@ def delete(meta_path: str, background: bool = False, recycle: bool = True):
                     q = os.path.join(rdir, f"r-{stamp}-{uuid.uuid4().hex[:8]}-{i}")
                     os.replace(p, q)
                     recycled.append(q)
+                    _remember(q)
                 elif os.path.exists(p):
                     os.replace(p, p + tag)
                     moved.append(p + tag)
