@@ -85,8 +85,8 @@ def test_fault_kinds_on_gpu_ranks(ranks):
     assert f"FAULTS_OK {ranks}" in out.stdout
 
 
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("ranks", [2, 4])
+@pytest.mark.timeout(960)
+@pytest.mark.parametrize("ranks", [2, 4, 8])
 def test_fine_rows_ranks_share_one_gpu(ranks, tmp_path):
     """The fine-bucket exchange over materialised tables (generated at a 128-byte pitch, hbm://,
     partfile://) and the GenFusedShuffle variant, validated; skew past capacity stops every rank
@@ -96,7 +96,7 @@ def test_fine_rows_ranks_share_one_gpu(ranks, tmp_path):
     out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
                           "--master-addr", "127.0.0.1", "--master-port", str(29700 + ranks),
                           os.path.join(ROOT, "tests", "dist", "gpu_fine_rows_ranks.py")],
-                         capture_output=True, text=True, timeout=560, env=env, cwd=ROOT)
+                         capture_output=True, text=True, timeout=920, env=env, cwd=ROOT)
     _dump(os.path.basename(out.args[-1]) + str(ranks), out)
     assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
     assert f"FINE_ROWS_OK {ranks}" in out.stdout
