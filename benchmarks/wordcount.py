@@ -52,6 +52,7 @@ def main():
     print(json.dumps({
         "metric": "WordCount MB/s of text (LocalJobSubmission on CPU)" if not a.gpu else "WordCount MB/s of text (GPU executor)",
         "value": round(size / med / 1e6, 2), "unit": "MB/s", "steps": a.steps, "seconds_per_step": round(med, 3),
+        "all_step_s": [round(t, 4) for t in times],
         "higher_is_better": True, "validated": ok, "words": len(res), "bytes": size,
         "data": "synthetic Zipf-ish corpus (models/wordcount.synthetic_corpus)",
         "config": {"executor": "gpu" if a.gpu else f"process x{a.procs}", "partitions": a.partitions}}))
