@@ -250,6 +250,34 @@ def _structure(world: World, have_rank: int, proto):
     return pickle.loads(buf.cpu().numpy().tobytes())     # this framework's own structure tuple
 
 
+class RecvArena:
+    """Receive buffers of consecutive exchanges laid back to back, one region per column: the
+    pieces a partition receives over many rounds (a streamed shuffle holding them for one final
+    reduce, runtime/stream_shuffle.py) then concatenate as ONE view (DeviceTable._adjacent) instead
+    of a copy.  ``nbytes`` is split over the columns by their row widths at the first round; a
+    round that no longer fits gets fresh buffers (its pieces are then copied when concatenated)."""
+
+    def __init__(self, nbytes: int, device):
+        self.nbytes, self.dev = int(nbytes), device
+        self.bufs, self.used, self.rows = None, None, 0
+
+    def take(self, widths: dict, rows: int):
+        """{column: uint8 buffer of rows * width bytes} for the next round, or None when the
+        arena's column layout differs or it has no room left."""
+        if self.bufs is None:
+            per = sum(widths.values())
+            if per <= 0:
+                return None
+            self.rows = self.nbytes // per
+            self.bufs = {k: torch.empty(self.rows * w, dtype=torch.uint8, device=self.dev) for k, w in widths.items()}
+            self.widths, self.used = dict(widths), 0
+        if widths != self.widths or self.used + rows > self.rows:
+            return None
+        out = {k: self.bufs[k][self.used * w: (self.used + rows) * w] for k, w in widths.items()}
+        self.used += rows
+        return out
+
+
 class PendingExchange:
     """An exchange whose payload collectives are queued (asynchronous all-to-all-v per column and
     per string heap) but not yet waited for; ``finish()`` makes the caller's stream wait and
@@ -286,7 +314,8 @@ class PendingExchange:
         return res
 
 
-def exchange_start(world: World, sends: list, stats: ExchangeStats | None = None) -> PendingExchange:
+def exchange_start(world: World, sends: list, stats: ExchangeStats | None = None,
+                   arena: RecvArena | None = None) -> PendingExchange:
     """Queue an exchange (see ``exchange``).  The manifest is two tensor collectives
     (``_manifest``); the payload columns and string heaps are queued as asynchronous all-to-all-v
     collectives back to back (RCCL runs them in order on its stream while the host prepares the
@@ -322,6 +351,15 @@ def exchange_start(world: World, sends: list, stats: ExchangeStats | None = None
     out_cols = {name: None for name, _ in colspecs}
     offset_cols = {oc for oc, _, _ in strspecs}        # rebuilt from the lengths on arrival
     handles, keep = [], []
+    slots = None
+    if arena is not None and not strspecs:
+        widths = {}
+        for (name, tail), dt in zip(colspecs, dtypes):
+            per = torch.empty((0,) + tuple(tail), dtype=dt).element_size()
+            for d in tail:
+                per *= d
+            widths[name] = per
+        slots = arena.take(widths, total_r)
     for (name, tail), dt in zip(colspecs, dtypes):
         if name in offset_cols:
             out_cols[name] = dt
@@ -333,7 +371,7 @@ def exchange_start(world: World, sends: list, stats: ExchangeStats | None = None
         pieces = [x if x.dtype == dt else x.to(dt) for x in pieces]
         like = torch.empty((0,) + tuple(tail), dtype=dt, device=dev)
         send = _bytes(_cat(pieces, like)) if pieces else torch.empty(0, dtype=torch.uint8, device=dev)
-        recv = torch.empty(total_r * per, dtype=torch.uint8, device=dev)
+        recv = slots[name] if slots is not None else torch.empty(total_r * per, dtype=torch.uint8, device=dev)
         handles.append(shuffle.alltoallv_bytes_async(send, [c * per for c in send_rows], recv,
                                                      [c * per for c in recv_rows], world))
         keep.append(send)

@@ -133,6 +133,38 @@ class LoopbackRank:
         return sum(self.phases.values())
 
 
+def _arena_table(arena, tabs: list):
+    """The round's received pieces laid into the next region of the receive arena (what the
+    exchange's all-to-all-v writes there in a real run), or None (strings, rows, no room)."""
+    if not tabs or any(t.rows is not None or t.heap is not None or t.strs for t in tabs):
+        return None
+    t0 = tabs[0]
+    n = sum(t.n for t in tabs)
+    dts, widths = {}, {}
+    for k, v in t0.cols.items():
+        dt = v.dtype
+        for t in tabs[1:]:
+            dt = torch.promote_types(dt, t.cols[k].dtype)
+        dts[k] = (dt, tuple(v.shape[1:]))
+        w = torch.empty((0,) + tuple(v.shape[1:]), dtype=dt).element_size()
+        for d in v.shape[1:]:
+            w *= d
+        widths[k] = w
+    slots = arena.take(widths, n)
+    if slots is None:
+        return None
+    cols = {}
+    for k, (dt, tail) in dts.items():
+        dst = slots[k].view(dt).view((n,) + tail)
+        a = 0
+        for t in tabs:
+            dst[a: a + t.n].copy_(t.cols[k][: t.n])
+            a += t.n
+        stats.union(dst, [t.cols[k] for t in tabs])
+        cols[k] = dst
+    return DeviceTable(n, t0.shape, cols)
+
+
 def bulk_model(phases: dict, nbytes: dict, link_GBps: float) -> dict:
     """MODELLED step of the bulk plan (stage A, one exchange, stage B) on a link of ``link_GBps``
     per GPU: the exchange takes max(bytes out, bytes in) / link between the two stages."""
@@ -203,6 +235,8 @@ class LoopbackStreamShuffle:
                      hold_bytes=splan["budget"] // 4,
                      chunk=splan["chunk"])
         agg = SA.StreamAggregator(run, self.B, vb, bplan)
+        from ..parallel import exchange as EXC
+        arena = EXC.RecvArena(bplan["hold_bytes"], self.dev)      # as stream_shuffle.run receives
         gens = [ST._chunks(splan, s, self.dev, None) for s in range(W)]
         self.rounds = []
         t_all = torch.cuda.Event(enable_timing=True)
@@ -231,7 +265,9 @@ class LoopbackStreamShuffle:
                 break
             pieces.sort(key=lambda x: x[0])
             tabs = [p for _, p in pieces if p.n]
-            recv = DeviceTable.concat(tabs) if len(tabs) > 1 else (tabs[0] if tabs else None)
+            recv = _arena_table(arena, tabs)
+            if recv is None:
+                recv = DeviceTable.concat(tabs) if len(tabs) > 1 else (tabs[0] if tabs else None)
             rb = _nbytes(recv) - (_nbytes(pieces[0][1]) if pieces and pieces[0][0] == me else 0) if recv else 0
             torch.cuda.synchronize(self.dev)
             ev[2].record()

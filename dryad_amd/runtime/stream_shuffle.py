@@ -167,6 +167,9 @@ def run(desc, runner, lay) -> dict:
                  hold_bytes=lay["budget"] // (4 * max(1, len(parts_b))),
                  chunk=lay["chunk"])
     aggs = {} if rep_mode else {p: SA.StreamAggregator(runner, B, vctx_b[p], dict(bplan)) for p in parts_b}
+    # one final partition on this rank: its rounds are received back to back into an arena of the
+    # hold budget, so the held partials concatenate as one view for the final reduce
+    arena = EXC.RecvArena(bplan["hold_bytes"], dev) if not rep_mode and len(parts_b) == 1 else None
     from . import sinks as SK
     outs = {p: SK.for_stage(runner, B, p, B.ops[-1:]) for p in parts_b} if rep_mode else {}
     held = {p: [] for p in parts_b}          # repartition pieces no sink could take (run at the end)
@@ -246,7 +249,7 @@ def run(desc, runner, lay) -> dict:
         if sends is None:
             # this rank's chunks are done: empty pieces of its layout (or none before its first)
             sends = [[proto for _ in owned[r]] for r in range(W)] if proto is not None else [[] for _ in range(W)]
-        ex = EXC.exchange_start(w, sends, stats)      # queued; round r-1 is folded meanwhile
+        ex = EXC.exchange_start(w, sends, stats, arena=arena)   # queued; round r-1 is folded meanwhile
         if pending is not None:
             try:
                 fold(pending)
