@@ -1533,25 +1533,49 @@ def op_agg_partial(op, inputs, v):
 class _AccFold:
     """Symbolic accumulator of a user ``Aggregate(seed, func)``: tracing ``func(acc, x)`` with
     ``acc`` bound to this object records ``acc + T(x)`` (or ``acc - T(x)``, ``T(x) + acc``, ``acc
-    + T(x) + c``, ...).  A fold whose step only adds a per-record term is ``seed + sum_i T(x_i)``,
-    so the sequential vertex becomes one device reduction.  Any other use of ``acc`` (products,
-    comparisons, branches, attribute access) is not a sum fold and raises NotTraceable."""
-    __slots__ = ("term",)
+    + T(x) + c``, ...), or a bitwise fold ``acc ^ T(x)`` / ``acc | T(x)`` / ``acc & T(x)`` of
+    integers (checksums, flag unions).  Such a fold is ``seed OP reduce_i T(x_i)`` (the operators
+    are associative and commutative), so the sequential vertex becomes one device reduction.  Any
+    other use of ``acc`` (products, comparisons, branches, attribute access, mixed operators) is
+    not such a fold and raises NotTraceable."""
+    __slots__ = ("term", "kind")
 
-    def __init__(self, term=0):
-        self.term = term
+    def __init__(self, term=0, kind="sum"):
+        self.term, self.kind = term, kind
 
-    def __add__(self, o):
+    @staticmethod
+    def _operand(o):
         if isinstance(o, _AccFold):
             raise NotTraceable("accumulator used twice in the fold step")
-        return _AccFold(self.term + (o if isinstance(o, (TR.Col, int, float)) else TR.Col(o)))
+        return o if isinstance(o, (TR.Col, int, float)) else TR.Col(o)
+
+    def __add__(self, o):
+        if self.kind != "sum":
+            raise NotTraceable("mixed fold operators")
+        return _AccFold(self.term + self._operand(o))
 
     __radd__ = __add__
 
     def __sub__(self, o):
-        if isinstance(o, _AccFold):
-            raise NotTraceable("accumulator used twice in the fold step")
-        return _AccFold(self.term - (o if isinstance(o, (TR.Col, int, float)) else TR.Col(o)))
+        if self.kind != "sum":
+            raise NotTraceable("mixed fold operators")
+        return _AccFold(self.term - self._operand(o))
+
+    def _bitwise(self, o, kind):
+        if self.kind != "sum" or not (isinstance(self.term, int) and self.term == 0):
+            raise NotTraceable("mixed fold operators")
+        return _AccFold(self._operand(o), kind)
+
+    def __xor__(self, o):
+        return self._bitwise(o, "xor")
+
+    def __or__(self, o):
+        return self._bitwise(o, "or")
+
+    def __and__(self, o):
+        return self._bitwise(o, "and")
+
+    __rxor__, __ror__, __rand__ = __xor__, __or__, __and__
 
     def __getattr__(self, name):
         raise NotTraceable(f"accumulator used as {name}: not a sum fold")
@@ -1563,8 +1587,20 @@ class _AccFold:
         raise NotTraceable("accumulator in a non-additive expression")
 
     __mul__ = __rmul__ = __rsub__ = __truediv__ = __rtruediv__ = __floordiv__ = __mod__ = __pow__ = _no
-    __and__ = __or__ = __xor__ = __lt__ = __le__ = __gt__ = __ge__ = __eq__ = __ne__ = __neg__ = _no
+    __lt__ = __le__ = __gt__ = __ge__ = __eq__ = __ne__ = __neg__ = _no
     __hash__ = None
+
+
+def _bitwise_reduce(col: torch.Tensor, kind: str) -> int:
+    """XOR / OR / AND of an integer column by halving folds (log2(n) passes over shrinking
+    halves: about two reads of the column)."""
+    fn = {"xor": torch.bitwise_xor, "or": torch.bitwise_or, "and": torch.bitwise_and}[kind]
+    x = col.to(torch.int64)
+    while x.numel() > 1:
+        h = x.numel() // 2
+        y = fn(x[:h], x[h: 2 * h])
+        x = torch.cat([y, x[2 * h:]]) if x.numel() % 2 else y
+    return int(x[0].item())
 
 
 def op_aggregate_seq(op, inputs, v):
@@ -1601,6 +1637,25 @@ def op_aggregate_seq(op, inputs, v):
     if not isinstance(res, _AccFold):
         raise NotTraceable("Aggregate step is not acc + f(x)")
     term = res.term
+    if res.kind != "sum":
+        # bitwise fold of integers: seed OP (T(x_1) OP ... OP T(x_n)) (Python ints: exact as long as
+        # the seed and the terms are int64 values)
+        if isinstance(seed, float) or (isinstance(term, TR.Col) and not isinstance(term.t, torch.Tensor)):
+            raise NotTraceable("bitwise Aggregate of non-integers")
+        if isinstance(term, bool) or isinstance(term, float):
+            raise NotTraceable("bitwise Aggregate of non-integers")
+        if isinstance(term, int):
+            col = torch.full((rows.n,), term, dtype=torch.int64, device=t.device)
+        else:
+            col = term.t.expand(rows.n) if term.t.dim() == 0 else term.t
+            if col.dim() != 1 or col.is_floating_point() or col.is_complex():
+                raise NotTraceable("bitwise Aggregate of non-integers")
+        if not -(1 << 63) <= int(seed) < (1 << 63):
+            raise NotTraceable("Aggregate seed past int64")
+        red = _bitwise_reduce(col[: rows.n].contiguous(), res.kind)
+        acc = {"xor": int(seed) ^ red, "or": int(seed) | red, "and": int(seed) & red}[res.kind]
+        r = s.get("result_selector")
+        return [r(acc) if r else acc]
     if isinstance(term, (int, float)) and not isinstance(term, bool):
         acc = seed + term * rows.n
     else:

@@ -103,7 +103,8 @@ def test_aggregates_on_device_match_localdebug(parts):
 
 @pytest.mark.parametrize("parts", [1, 3])
 def test_user_aggregate_sum_fold_on_device(parts):
-    """Aggregate(seed, func) whose step is acc + f(x) folds on the device (one reduction);
+    """Aggregate(seed, func) whose step is acc + f(x), or a bitwise acc ^ / | / & f(x), folds on
+    the device (one reduction);
     any other step still runs on the host and gives the oracle's answer."""
     cases = {
         "seed": (lambda c: c.FromEnumerable(INTS).Aggregate(5, lambda a, x: a + x * 3 - 1), True),
@@ -113,6 +114,10 @@ def test_user_aggregate_sum_fold_on_device(parts):
             0.5, lambda a, p: a + p[1] * 2, lambda a: round(a, 6)), True),
         "seedless": (lambda c: c.FromEnumerable(INTS).Aggregate(lambda a, x: a + x), True),
         "bool_term": (lambda c: c.FromEnumerable(INTS).Aggregate(0, lambda a, x: a + (x > 0)), True),
+        "xor": (lambda c: c.FromEnumerable(INTS).Aggregate(12345, lambda a, x: a ^ (x * 2654435761)), True),
+        "or_term_first": (lambda c: c.FromEnumerable(INTS).Aggregate(0, lambda a, x: (x & 0xFF0) | a), True),
+        "and_seedless": (lambda c: c.FromEnumerable(INTS).Aggregate(lambda a, x: a & (x | 1)), True),
+        "mixed_host": (lambda c: c.FromEnumerable(INTS).Aggregate(0, lambda a, x: (a ^ x) + 1), False),
         "product_host": (lambda c: c.FromEnumerable(INTS[:50]).Aggregate(1, lambda a, x: a * (x % 3 + 1)), False),
         "max_host": (lambda c: c.FromEnumerable(INTS).Aggregate(0, lambda a, x: a if a > x else x), False),
     }
