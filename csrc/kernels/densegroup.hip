@@ -40,6 +40,9 @@ constexpr int kDgWaves = kDgThreads / 64;
 #ifndef DR_DG_GMAX
 #define DR_DG_GMAX 1536
 #endif
+#ifndef DR_DG_LDS_MATCH
+#define DR_DG_LDS_MATCH 0     // in-wave digit match: 0 ballots per digit bit, 1 LDS atomicOr masks
+#endif
 constexpr int kDgTile = DR_DG_TILE;   // build-time constants: tools/micro/dg_tile_ab.sh measures variants
 constexpr int kDgItems = kDgTile / kDgThreads; // rows per thread per tile
 constexpr int kDgMaxDigit = 10;               // digit bits per pass (1024 buckets)
@@ -185,6 +188,10 @@ __global__ __launch_bounds__(kDgThreads) __attribute__((amdgpu_waves_per_eu(DR_D
     // of the next tile would need ~150-180 VGPRs, one workgroup per CU)
     load_raw(base);
     for (uint32_t i = t; i < kDgWaves * nb; i += kDgThreads) (&wcnt[0][0])[i] = 0;
+#if DR_DG_LDS_MATCH
+    static_assert(kDgWaves * nb * 8 <= kDgTile * 16, "the digit masks fit the row stage");
+    for (uint32_t i = t; i < kDgWaves * nb; i += kDgThreads) reinterpret_cast<unsigned long long*>(tile)[i] = 0ull;
+#endif
     uint4 rv[kDgItems];
 #pragma unroll
     for (int r = 0; r < kDgItems; ++r) {
@@ -211,6 +218,14 @@ __global__ __launch_bounds__(kDgThreads) __attribute__((amdgpu_waves_per_eu(DR_D
       const bool valid = pos < cnt;
       const uint64_t ko = (((uint64_t)rv[r].y << 32) | rv[r].x) & kmask;
       const uint32_t d = valid ? (uint32_t)((ko >> shift) & mask) : 0u;
+#if DR_DG_LDS_MATCH
+      // wave64 multisplit by per-wave digit masks in LDS (aliasing the row stage, which is only
+      // written after the ranking): one ds_or_b64 per lane, the mask read back, cleared by the leader
+      unsigned long long* wm = reinterpret_cast<unsigned long long*>(tile) + (uint32_t)w * nb;
+      if (valid) atomicOr(&wm[d], 1ull << l);
+      __builtin_amdgcn_wave_barrier();
+      const uint64_t peers = valid ? wm[d] : 0ull;
+#else
       // wave64 multisplit: the lanes holding the same digit, by one ballot per digit bit
       uint64_t peers = ballot64(valid);
 #pragma unroll
@@ -219,10 +234,16 @@ __global__ __launch_bounds__(kDgThreads) __attribute__((amdgpu_waves_per_eu(DR_D
         const uint64_t b = ballot64(bit);
         peers &= bit ? b : ~b;
       }
+#endif
       const uint32_t below = popc_below(peers);
       const uint32_t prior = wcnt[w][d];
       __builtin_amdgcn_wave_barrier();
-      if (valid && below == 0) wcnt[w][d] = (uint16_t)(prior + (uint32_t)__popcll(peers));
+      if (valid && below == 0) {
+        wcnt[w][d] = (uint16_t)(prior + (uint32_t)__popcll(peers));
+#if DR_DG_LDS_MATCH
+        wm[d] = 0ull;
+#endif
+      }
       __builtin_amdgcn_wave_barrier();
       rk[r] = prior + below;
       dg[r] = d;
