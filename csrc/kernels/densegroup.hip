@@ -41,7 +41,7 @@ constexpr int kDgWaves = kDgThreads / 64;
 #define DR_DG_GMAX 1536
 #endif
 #ifndef DR_DG_LDS_MATCH
-#define DR_DG_LDS_MATCH 0     // in-wave digit match: 0 ballots per digit bit, 1 LDS atomicOr masks
+#define DR_DG_LDS_MATCH 1     // in-wave digit match: 1 LDS atomicOr masks (~1 % faster per pass, profiles/r6/kernels/dg_ab_*), 0 ballots per digit bit
 #endif
 constexpr int kDgTile = DR_DG_TILE;   // build-time constants: tools/micro/dg_tile_ab.sh measures variants
 constexpr int kDgItems = kDgTile / kDgThreads; // rows per thread per tile
