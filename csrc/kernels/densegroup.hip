@@ -21,19 +21,17 @@
 //                id changes (global output cursor)
 //
 // Each partition pass is count (per-workgroup histograms, bucket-major) + exclusive scan (host
-// side, torch) + scatter: a workgroup ranks a 4096-row tile by digit with wave64 ballot
-// multisplits, writes the rows into LDS in bucket order and stores every bucket's run contiguously.
+// side, torch) + scatter: a workgroup ranks an 8192-row tile (4096 at 10-bit digits) by digit with
+// wave64 multisplits, writes the rows into LDS in bucket order and stores every bucket's run
+// contiguously.
 #include "common.h"
 
 namespace {
-// Scatter and aggregate workgroups are 512 threads (8 waves), one per CU: a 4096-row tile puts
-// 8 rows (128 bytes, a full line) per bucket per tile at 512 buckets; scattered 16-byte rows
-// (2048-row tiles into 1024 buckets) measured 2.5-2.8x the written bytes at the memory side.
+// Aggregate workgroups are 512 threads (8 waves); partition passes see DgSc.  Scattered 16-byte
+// rows (2048-row tiles into 1024 buckets) measured 2.5-2.8x the written bytes at the memory side,
+// so a tile holds as many rows per bucket as the LDS allows.
 constexpr int kDgThreads = 512;
 constexpr int kDgWaves = kDgThreads / 64;
-#ifndef DR_DG_TILE
-#define DR_DG_TILE 4096
-#endif
 #ifndef DR_DG_WPE
 #define DR_DG_WPE 4
 #endif
@@ -43,8 +41,23 @@ constexpr int kDgWaves = kDgThreads / 64;
 #ifndef DR_DG_LDS_MATCH
 #define DR_DG_LDS_MATCH 1     // in-wave digit match: 1 LDS atomicOr masks (~1 % faster per pass, profiles/r6/kernels/dg_ab_*), 0 ballots per digit bit
 #endif
-constexpr int kDgTile = DR_DG_TILE;   // build-time constants: tools/micro/dg_tile_ab.sh measures variants
-constexpr int kDgItems = kDgTile / kDgThreads; // rows per thread per tile
+#ifndef DR_DG_BIG_TILE
+#define DR_DG_BIG_TILE 8192   // rows per tile of the <= 9-bit-digit passes (profiles/r6/kernels/dg_tile8k_ab.txt)
+#endif
+// Partition-pass shape per digit width: <= 512 buckets stage 8192-row tiles (128 KB of LDS, one
+// 1024-thread workgroup per CU, 16 rows = 256 bytes per bucket per tile on average); 1024 buckets
+// keep 4096-row tiles in 512-thread workgroups (two per CU) for the LDS of their wave counts.
+// Fewer, longer bucket runs per tile are fewer partial lines at the memory side: 8192-row tiles cut
+// the two passes of the 2^30-key GroupBy from 16.5 + 12.7 to 15.0 + 11.2 ms.
+template <int DB>
+struct DgSc {
+  static constexpr int tile = DB <= 9 ? DR_DG_BIG_TILE : 4096;
+  static constexpr int threads = tile >= 8192 ? 1024 : 512;
+  static constexpr int waves = threads / 64;
+  static constexpr int items = tile / threads;     // rows per thread per tile
+  static constexpr int wpe = DB <= 9 ? DR_DG_WPE : 2;  // 10-bit digits: one workgroup per CU by LDS
+};
+constexpr int kDgGridTile = DR_DG_BIG_TILE > 4096 ? DR_DG_BIG_TILE : 4096;  // per_block granule
 constexpr int kDgMaxDigit = 10;               // digit bits per pass (1024 buckets)
 constexpr int kDgTableBits = 12;              // LDS table slots per run: 4096
 constexpr int kDgSlots = 1 << kDgTableBits;
@@ -62,7 +75,8 @@ struct DgPack {
   uint32_t ncols;
 };
 
-// Exclusive scan across the 512-thread workgroup; scratch holds kDgWaves words of LDS.
+// Exclusive scan across a workgroup of NW waves; scratch holds NW words of LDS.
+template <int NW = kDgWaves>
 __device__ __forceinline__ uint32_t dg_block_scan(uint32_t v, uint32_t* scratch, uint32_t& total) {
   const int w = wave_id(), l = lane_id();
   const uint32_t inc = wave_inclusive_scan(v);
@@ -70,7 +84,7 @@ __device__ __forceinline__ uint32_t dg_block_scan(uint32_t v, uint32_t* scratch,
   __syncthreads();
   uint32_t base = 0, tot = 0;
 #pragma unroll
-  for (int k = 0; k < kDgWaves; ++k) {
+  for (int k = 0; k < NW; ++k) {
     const uint32_t x = scratch[k];
     base += k < w ? x : 0u;
     tot += x;
@@ -145,32 +159,33 @@ __global__ __launch_bounds__(256) void dg_count_kernel(const int64_t* __restrict
 // Stable partition of rows [beg, end) of each workgroup by digit; offsets[d * G + b] = first output
 // row of workgroup b's bucket d (exclusive prefix of the bucket-major counts).
 template <bool FROM_COLS, int DB>
-__global__ __launch_bounds__(kDgThreads) __attribute__((amdgpu_waves_per_eu(DR_DG_WPE))) void dg_scatter_kernel(DgPack pk, const uint4* __restrict__ in, uint64_t n,
+__global__ __launch_bounds__(DgSc<DB>::threads) __attribute__((amdgpu_waves_per_eu(DgSc<DB>::wpe))) void dg_scatter_kernel(DgPack pk, const uint4* __restrict__ in, uint64_t n,
                                                          uint32_t shift, const int64_t* __restrict__ offsets, uint32_t G,
                                                          uint64_t per_block, uint4* __restrict__ out) {
   constexpr uint32_t nb = 1u << DB, mask = nb - 1;
-  constexpr int kPer = (nb + kDgThreads - 1) / kDgThreads;   // buckets per thread in the scans
-  // 16-bit wave counts and bucket starts (<= kDgTile) and no per-slot digit array (recomputed from
-  // the staged row): 77 KB of LDS at DB = 9, two workgroups per CU
-  __shared__ uint4 tile[kDgTile];
-  __shared__ uint16_t wcnt[kDgWaves][nb];
+  constexpr int kT = DgSc<DB>::tile, kTh = DgSc<DB>::threads, kNW = DgSc<DB>::waves, kIt = DgSc<DB>::items;
+  constexpr int kPer = (nb + kTh - 1) / kTh;   // buckets per thread in the scans
+  // 16-bit wave counts and bucket starts (<= kT) and no per-slot digit array (recomputed from
+  // the staged row): 149 KB of LDS at DB = 9 (one workgroup per CU), 85 KB at DB = 10 (two)
+  __shared__ uint4 tile[kT];
+  __shared__ uint16_t wcnt[kNW][nb];
   __shared__ int64_t goff[nb];
   __shared__ uint16_t bstart[nb];
-  __shared__ uint32_t sc[kDgWaves];
+  __shared__ uint32_t sc[kNW];
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   const uint64_t beg = (uint64_t)blockIdx.x * per_block;
   const uint64_t end = beg + per_block < n ? beg + per_block : n;
   if (beg >= end) return;                              // uniform: the whole workgroup leaves
   const uint64_t kmask = pk.kbits >= 64 ? ~0ull : ((1ull << pk.kbits) - 1);
-  for (uint32_t i = t; i < nb; i += kDgThreads) goff[i] = offsets[(uint64_t)i * G + blockIdx.x];
+  for (uint32_t i = t; i < nb; i += kTh) goff[i] = offsets[(uint64_t)i * G + blockIdx.x];
   // raw inputs of one tile: the key and value columns (FROM_COLS) or the packed rows
   constexpr int kRaw = FROM_COLS ? 1 + kDgMaxCols : 1;
-  int64_t rawc[FROM_COLS ? kDgItems : 1][kRaw];
-  uint4 rawr[FROM_COLS ? 1 : kDgItems];
+  int64_t rawc[FROM_COLS ? kIt : 1][kRaw];
+  uint4 rawr[FROM_COLS ? 1 : kIt];
   auto load_raw = [&](uint64_t tb) {
 #pragma unroll
-    for (int r = 0; r < kDgItems; ++r) {
-      const uint64_t i = tb + w * (kDgTile / kDgWaves) + r * 64 + l;
+    for (int r = 0; r < kIt; ++r) {
+      const uint64_t i = tb + w * (kT / kNW) + r * 64 + l;
       const bool ok = i < end;
       if constexpr (FROM_COLS) {
         rawc[r][0] = ok ? pk.key[i] : pk.kmin;
@@ -182,19 +197,19 @@ __global__ __launch_bounds__(kDgThreads) __attribute__((amdgpu_waves_per_eu(DR_D
       }
     }
   };
-  for (uint64_t base = beg; base < end; base += kDgTile) {
-    const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kDgTile ? (end - base) : kDgTile);
-    // two workgroups per CU: the other one's tile overlaps this one's loads (a register prefetch
-    // of the next tile would need ~150-180 VGPRs, one workgroup per CU)
+  for (uint64_t base = beg; base < end; base += kT) {
+    const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kT ? (end - base) : kT);
+    // 16 waves per CU either way: while some waves rank or store, others' loads are in flight (a
+    // register prefetch of the next tile would need ~150-180 VGPRs)
     load_raw(base);
-    for (uint32_t i = t; i < kDgWaves * nb; i += kDgThreads) (&wcnt[0][0])[i] = 0;
+    for (uint32_t i = t; i < kNW * nb; i += kTh) (&wcnt[0][0])[i] = 0;
 #if DR_DG_LDS_MATCH
-    static_assert(kDgWaves * nb * 8 <= kDgTile * 16, "the digit masks fit the row stage");
-    for (uint32_t i = t; i < kDgWaves * nb; i += kDgThreads) reinterpret_cast<unsigned long long*>(tile)[i] = 0ull;
+    static_assert(kNW * nb * 8 <= kT * 16, "the digit masks fit the row stage");
+    for (uint32_t i = t; i < kNW * nb; i += kTh) reinterpret_cast<unsigned long long*>(tile)[i] = 0ull;
 #endif
-    uint4 rv[kDgItems];
+    uint4 rv[kIt];
 #pragma unroll
-    for (int r = 0; r < kDgItems; ++r) {
+    for (int r = 0; r < kIt; ++r) {
       if constexpr (FROM_COLS) {
         u128 v = (u128)(uint64_t)(rawc[r][0] - pk.kmin);
         uint32_t off = pk.kbits;
@@ -211,10 +226,10 @@ __global__ __launch_bounds__(kDgThreads) __attribute__((amdgpu_waves_per_eu(DR_D
       }
     }
     __syncthreads();
-    uint32_t rk[kDgItems], dg[kDgItems];
+    uint32_t rk[kIt], dg[kIt];
 #pragma unroll
-    for (int r = 0; r < kDgItems; ++r) {
-      const uint32_t pos = w * (kDgTile / kDgWaves) + r * 64 + l;
+    for (int r = 0; r < kIt; ++r) {
+      const uint32_t pos = w * (kT / kNW) + r * 64 + l;
       const bool valid = pos < cnt;
       const uint64_t ko = (((uint64_t)rv[r].y << 32) | rv[r].x) & kmask;
       const uint32_t d = valid ? (uint32_t)((ko >> shift) & mask) : 0u;
@@ -258,7 +273,7 @@ __global__ __launch_bounds__(kDgThreads) __attribute__((amdgpu_waves_per_eu(DR_D
       if (b < nb) {
         uint32_t acc = 0;
 #pragma unroll
-        for (int k = 0; k < kDgWaves; ++k) {
+        for (int k = 0; k < kNW; ++k) {
           const uint32_t c = wcnt[k][b];
           wcnt[k][b] = (uint16_t)acc;
           acc += c;
@@ -268,7 +283,7 @@ __global__ __launch_bounds__(kDgThreads) __attribute__((amdgpu_waves_per_eu(DR_D
       run += tot[q];
     }
     uint32_t all;
-    uint32_t pre = dg_block_scan(run, sc, all);
+    uint32_t pre = dg_block_scan<kNW>(run, sc, all);
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const uint32_t b = t * kPer + q;
@@ -277,8 +292,8 @@ __global__ __launch_bounds__(kDgThreads) __attribute__((amdgpu_waves_per_eu(DR_D
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kDgItems; ++r) {
-      const uint32_t pos = w * (kDgTile / kDgWaves) + r * 64 + l;
+    for (int r = 0; r < kIt; ++r) {
+      const uint32_t pos = w * (kT / kNW) + r * 64 + l;
       if (pos < cnt) {
         const uint32_t slot = (uint32_t)bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
         tile[slot] = rv[r];
@@ -287,7 +302,7 @@ __global__ __launch_bounds__(kDgThreads) __attribute__((amdgpu_waves_per_eu(DR_D
     __syncthreads();
     // consecutive slots of one bucket are consecutive output rows
 #pragma unroll 4
-    for (uint32_t j = t; j < cnt; j += kDgThreads) {
+    for (uint32_t j = t; j < cnt; j += kTh) {
       const uint4 v = tile[j];
       const uint32_t d = (uint32_t)((((((uint64_t)v.y << 32) | v.x) & kmask) >> shift) & mask);
       out[goff[d] + (int64_t)(j - bstart[d])] = v;
@@ -466,10 +481,10 @@ DR_API uint32_t dr_dg_max_digit() { return kDgMaxDigit; }
 
 // Workgroups and rows per workgroup of a partition pass (counts are sized (1 << dbits) * G).
 DR_API uint32_t dr_dg_grid(uint64_t n, uint64_t* per_block) {
-  uint64_t tiles = (n + kDgTile - 1) / kDgTile;
+  uint64_t tiles = (n + kDgGridTile - 1) / kDgGridTile;
   if (tiles < 1) tiles = 1;
   const uint64_t G = tiles < DR_DG_GMAX ? tiles : DR_DG_GMAX;
-  *per_block = ((tiles + G - 1) / G) * kDgTile;
+  *per_block = ((tiles + G - 1) / G) * kDgGridTile;
   return (uint32_t)G;
 }
 
@@ -519,14 +534,14 @@ DR_API int dr_dg_scatter(const int64_t* key, const int64_t* const* cols, const i
   if (dg_pack_from(&p, key, cols, vmin, vbits, ncols, kmin, kbits)) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
 #define DG_SC(FC, DBV)                                                                                \
-  dg_scatter_kernel<FC, DBV><<<G, kDgThreads, 0, s>>>(p, static_cast<const uint4*>(in), n, shift, offsets, G, per_block, \
+  dg_scatter_kernel<FC, DBV><<<G, DgSc<DBV>::threads, 0, s>>>(p, static_cast<const uint4*>(in), n, shift, offsets, G, per_block, \
                                                static_cast<uint4*>(out))
 #define DG_SC_ALL(FC)                                                                                 \
   switch (dbits) {                                                                                    \
     case 1: DG_SC(FC, 1); break; case 2: DG_SC(FC, 2); break; case 3: DG_SC(FC, 3); break;            \
     case 4: DG_SC(FC, 4); break; case 5: DG_SC(FC, 5); break; case 6: DG_SC(FC, 6); break;            \
     case 7: DG_SC(FC, 7); break; case 8: DG_SC(FC, 8); break; case 9: DG_SC(FC, 9); break;            \
-    default: DG_SC(FC, 10); break;                                                                    \
+    default: DG_SC(FC, 10); break;                                                                            \
   }
   if (in) {
     DG_SC_ALL(false);

@@ -33,7 +33,8 @@ _lib.register_signatures({
 TABLE_BITS = 12
 # aggregation workgroups (one per CU by LDS: 1024 = four rounds over the 256 CUs)
 AGG_GRID = 1024
-MAX_DIGIT = 10
+MAX_DIGIT = 10                   # the library's dr_dg_max_digit() when it is loaded
+_MAXD = None
 MIN_ROWS = 1 << 20
 _INT = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8)
 _OP = {"sum": 0, "min": 1, "max": 2}
@@ -42,10 +43,14 @@ _OP = {"sum": 0, "min": 1, "max": 2}
 def plan(kspan_bits: int, vbits: list) -> list | None:
     """Digit widths of the partition passes (low digit first) for a key offset of ``kspan_bits``
     bits, or None when the dense path does not apply."""
+    global _MAXD
+    if _MAXD is None:
+        _MAXD = int(_lib.lib().dr_dg_max_digit()) if torch.cuda.is_available() else MAX_DIGIT
+    m = _MAXD
     d = kspan_bits - TABLE_BITS
-    if d < 1 or d > 2 * MAX_DIGIT or kspan_bits + sum(vbits) > 128:
+    if d < 1 or d > 2 * m or kspan_bits + sum(vbits) > 128:
         return None
-    if d <= MAX_DIGIT:
+    if d <= m:
         return [d]
     lo = (d + 1) // 2
     return [lo, d - lo]
