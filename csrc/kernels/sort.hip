@@ -1719,7 +1719,7 @@ DR_API int dr_sort_u64_expand(E64* keys, E64* tmp, E128* out, uint64_t n, int be
 // on the order, so here ONE read (os_hist_kernel) builds the histograms of every pass, and each
 // scatter pass finds a tile's per-digit output offset from the tiles before it instead of from a
 // count matrix:
-//   * tiles (4096 entries) are claimed in order from a per-pass ticket counter, so every tile a
+//   * tiles (16384 entries) are claimed in order from a per-pass ticket counter, so every tile a
 //     workgroup waits for belongs to a workgroup that is already running;
 //   * a tile publishes its 256 digit counts as 8-byte {tag, value} granules (one agent-scope
 //     atomic store each: the granule is its own flag), first tagged "aggregate of this tile", then,
@@ -1733,9 +1733,20 @@ DR_API int dr_sort_u64_expand(E64* keys, E64* tmp, E128* out, uint64_t n, int be
 // so every store stays inside the output); the caller checks that word.
 namespace {
 
-constexpr int kOsItems = 32;                   // 8192-entry tiles: 78 KB of LDS, 2 workgroups per CU
-                                               // (A/B at 1.25e9: 16 items 33.9 ms / 4 passes, 20: 32.7,
-                                               //  24: 29.3, 32: 25.1, 40: 34.6, 48: 32.9, 64: 30.2)
+#ifndef DR_OS_NT
+#define DR_OS_NT 1024                          // look-back scatter workgroup: 16 waves, one per CU by LDS
+#endif
+#ifndef DR_OS_ITEMS
+#define DR_OS_ITEMS 16                         // entries per thread: 16384-entry tiles (128 KB stage)
+#endif
+#ifndef DR_OS_LB
+#define DR_OS_LB 4                             // look-back granules per round trip
+#endif
+// Tile shape A/B at 1.25e9 entries (profiles/r6/kernels/os_shape_ab.txt, per pass): 256 threads x 32
+// 6.00 ms, 512 x 16 5.80, 512 x 32 6.12, 768 x 20 6.07, 1024 x 12 6.47, 1024 x 16 5.74 (LB 8: 5.86).
+// Round 5's 256-thread sweep: 16 items 33.9 ms / 4 passes, 20: 32.7, 24: 29.3, 32: 25.1, 40: 34.6.
+constexpr int kOsThreads = DR_OS_NT;
+constexpr int kOsItems = DR_OS_ITEMS;
 constexpr int kOsMaxPasses = 8;
 constexpr uint32_t kOsHistGrid = 1024;
 constexpr uint32_t kOsSpinLimit = 1u << 22;
@@ -1743,8 +1754,8 @@ constexpr uint64_t kOsHeader = 256;            // tickets[8] at 0, error word at
 typedef __attribute__((address_space(1))) unsigned long long os_gu64;
 typedef __attribute__((address_space(1))) unsigned int os_gu32;
 
-inline uint64_t os_tiles(uint64_t n, int items = kOsItems) {
-  const uint64_t tile = (uint64_t)kBlock * items;
+inline uint64_t os_tiles(uint64_t n) {
+  const uint64_t tile = (uint64_t)kOsThreads * kOsItems;
   return (n + tile - 1) / tile;
 }
 
@@ -1817,80 +1828,97 @@ __global__ __launch_bounds__(256) void os_hist_scan_kernel(uint32_t* __restrict_
   if (t == 0 && (uint64_t)total != n) atomicOr(err, 2u);
 }
 
-template <int ITEMS, int LB>
-__global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__ in, E64* __restrict__ out,
-                                                         uint64_t n, int shift, const uint32_t* __restrict__ gbase,
-                                                         unsigned long long* granules, uint32_t* ticket,
-                                                         uint32_t* err, uint32_t tag_agg, uint32_t tiles) {
-  constexpr int kTile = kBlock * ITEMS;
+// One pass: NT threads (NT / 64 waves), ITEMS entries per thread, a tile of NT * ITEMS entries,
+// each wave ranking a contiguous kTile / NW of them (stable).  16 waves over a 16384-entry tile:
+// 64 entries (512 bytes) per digit per tile on average, and fewer serial ranking steps per wave
+// than 4 waves over 8192 entries.  The per-wave digit masks alias the stage (written only after the
+// ranking); digit-indexed work stays on threads < 256.
+template <int ITEMS, int LB, int NT>
+__global__ __launch_bounds__(NT) void os_scatter_kernel(const E64* __restrict__ in, E64* __restrict__ out,
+                                                              uint64_t n, int shift, const uint32_t* __restrict__ gbase,
+                                                              unsigned long long* granules, uint32_t* ticket,
+                                                              uint32_t* err, uint32_t tag_agg, uint32_t tiles) {
+  constexpr int kTile = NT * ITEMS, kNW = NT / 64;
+  static_assert(NT >= kBins && kNW * kBins <= kTile, "bins on the first 256 threads; masks fit the stage");
   __shared__ E64 stage[kTile];
-  __shared__ uint32_t wcnt[4][kBins];
-  __shared__ unsigned long long wmask[4][kBins];
+  __shared__ uint32_t wcnt[kNW][kBins];
   __shared__ uint32_t bstart[kBins];
   __shared__ uint32_t goff[kBins];
   __shared__ uint32_t sc[4];
   __shared__ uint32_t tile_sh;
+  unsigned long long* wmask = reinterpret_cast<unsigned long long*>(stage);   // [kNW][kBins]
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   const unsigned long long tag_inc = tag_agg + 1u;
-  if (*err & 2u) return;                         // refused histogram (os_hist_scan_kernel): uniform exit
+  if (*err & 2u) return;
   if (t == 0) tile_sh = __hip_atomic_fetch_add((os_gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  wmask[0][t] = 0ull; wmask[1][t] = 0ull; wmask[2][t] = 0ull; wmask[3][t] = 0ull;
-  wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+  for (int i = t; i < kNW * kBins; i += NT) {
+    wmask[i] = 0ull;
+    (&wcnt[0][0])[i] = 0;
+  }
   __syncthreads();
-  const uint32_t tile = tile_sh;                 // the grid has exactly one workgroup per tile
+  const uint32_t tile = tile_sh;
   if (tile >= tiles) return;
   const uint64_t base = (uint64_t)tile * kTile;
   const uint32_t cnt = (uint32_t)((n - base) < (uint64_t)kTile ? (n - base) : kTile);
   E64 cur[ITEMS];
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
-    const uint32_t pos = w * (kTile / 4) + r * 64 + l;
+    const uint32_t pos = w * (kTile / kNW) + r * 64 + l;
     if (pos < cnt) cur[r] = in[base + pos];
   }
   const unsigned long long lanebit = 1ull << l;
-  {
-    uint32_t rk[ITEMS], dg[ITEMS];
+  uint32_t rk[ITEMS], dg[ITEMS];
 #pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
-      const bool valid = pos < cnt;
-      const uint32_t d = valid ? digit_of(cur[r], shift) : 0u;
-      if (valid) atomicOr(&wmask[w][d], lanebit);
-      __builtin_amdgcn_wave_barrier();
-      const unsigned long long peers = valid ? wmask[w][d] : 0ull;
-      const uint32_t below = popc_below(peers);
-      const uint32_t prior = wcnt[w][d];
-      __builtin_amdgcn_wave_barrier();
-      if (valid && below == 0) {
-        wcnt[w][d] = prior + (uint32_t)__popcll(peers);
-        wmask[w][d] = 0ull;
-      }
-      __builtin_amdgcn_wave_barrier();
-      rk[r] = prior + below;
-      dg[r] = d;
+  for (int r = 0; r < ITEMS; ++r) {
+    const uint32_t pos = w * (kTile / kNW) + r * 64 + l;
+    const bool valid = pos < cnt;
+    const uint32_t d = valid ? digit_of(cur[r], shift) : 0u;
+    unsigned long long* wm = wmask + w * kBins;
+    if (valid) atomicOr(&wm[d], lanebit);
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long peers = valid ? wm[d] : 0ull;
+    const uint32_t below = popc_below(peers);
+    const uint32_t prior = wcnt[w][d];
+    __builtin_amdgcn_wave_barrier();
+    if (valid && below == 0) {
+      wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+      wm[d] = 0ull;
     }
-    __syncthreads();
-    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
-    const uint32_t tot = c0 + c1 + c2 + c3;
-    // publish this tile's count of digit t before anything else, so successors can move past it
-    os_gu64* mine = (os_gu64*)(granules + (uint64_t)tile * kBins + t);
+    __builtin_amdgcn_wave_barrier();
+    rk[r] = prior + below;
+    dg[r] = d;
+  }
+  __syncthreads();
+  uint32_t tot = 0;
+  os_gu64* mine = (os_gu64*)(granules + (uint64_t)tile * kBins + (t < kBins ? t : 0));
+  if (t < kBins) {
+#pragma unroll
+    for (int k = 0; k < kNW; ++k) {
+      const uint32_t c = wcnt[k][t];
+      wcnt[k][t] = tot;
+      tot += c;
+    }
     __hip_atomic_store(mine, ((tile == 0 ? tag_inc : (unsigned long long)tag_agg) << 32) | tot, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-    wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
-    uint32_t all;
-    bstart[t] = block_exclusive_scan256(tot, sc, all);
+  }
+  {
+    // exclusive scan of the 256 digit totals (waves 0..3); the other waves only meet the barriers
+    const uint32_t inc = wave_inclusive_scan(tot);
+    if (l == 63 && w < 4) sc[w] = inc;
     __syncthreads();
+    const uint32_t b = (w > 0 ? sc[0] : 0) + (w > 1 ? sc[1] : 0) + (w > 2 ? sc[2] : 0);
+    if (t < kBins) bstart[t] = b + inc - tot;
+    __syncthreads();
+  }
 #pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-      const uint32_t pos = w * (kTile / 4) + r * 64 + l;
-      if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
-    }
-    // look-back for digit t: LB predecessors per round trip, nearest first; aggregates
-    // are summed up to the first inclusive prefix, or up to the first granule not yet published
-    // (then that one is polled again)
+  for (int r = 0; r < ITEMS; ++r) {
+    const uint32_t pos = w * (kTile / kNW) + r * 64 + l;
+    if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
+  }
+  if (t < kBins) {
     uint32_t excl = 0;
     if (tile > 0) {
-      uint64_t j = tile;                         // granules of tiles < j are still to be summed
+      uint64_t j = tile;
       uint32_t spins = 0;
       for (;;) {
         unsigned long long g[LB];
@@ -1904,7 +1932,7 @@ __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__
         int used = 0;
 #pragma unroll
         for (int k = 0; k < LB; ++k) {
-          if (done || used < k) continue;        // stopped at an earlier granule
+          if (done || used < k) continue;
           const uint32_t tag = (uint32_t)(g[k] >> 32);
           if (tag == (uint32_t)tag_inc) {
             excl += (uint32_t)g[k];
@@ -1915,7 +1943,7 @@ __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__
           }
         }
         if (done) break;
-        j -= (uint64_t)used;                     // tile 0 always publishes an inclusive prefix
+        j -= (uint64_t)used;
         if (used == 0) {
           if (++spins > kOsSpinLimit) {
             __hip_atomic_fetch_or((os_gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1927,13 +1955,13 @@ __global__ __launch_bounds__(256) void os_scatter_kernel(const E64* __restrict__
       __hip_atomic_store(mine, (tag_inc << 32) | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     goff[t] = gbase[t] + excl;
-    __syncthreads();
+  }
+  __syncthreads();
 #pragma unroll 4
-    for (uint32_t j = t; j < cnt; j += kBlock) {
-      const E64 v = stage[j];
-      const uint32_t d = digit_of(v, shift);
-      out[(uint64_t)goff[d] + (j - bstart[d])] = v;    // plain stores (nontemporal: slower, onesweep_nt_ab.log)
-    }
+  for (uint32_t j = t; j < cnt; j += NT) {
+    const E64 v = stage[j];
+    const uint32_t d = digit_of(v, shift);
+    out[(uint64_t)goff[d] + (j - bstart[d])] = v;
   }
 }
 
@@ -1981,9 +2009,8 @@ DR_API int dr_sort_u64_onesweep(E64* keys, E64* tmp, uint64_t n, int begin_bit, 
   E64* dst = tmp;
   int flips = 0;
   for (int p = 0; p < P; ++p) {
-    os_scatter_kernel<kOsItems, 4><<<(unsigned)tiles, 256, 0, s>>>(src, dst, n, begin_bit + 8 * p, gbase + p * kBins,
-                                                                   granules, tickets + p, err, 2u * (p + 1),
-                                                                   (uint32_t)tiles);
+    os_scatter_kernel<kOsItems, DR_OS_LB, kOsThreads><<<(unsigned)tiles, kOsThreads, 0, s>>>(
+        src, dst, n, begin_bit + 8 * p, gbase + p * kBins, granules, tickets + p, err, 2u * (p + 1), (uint32_t)tiles);
     E64* x = src; src = dst; dst = x;
     flips ^= 1;
   }
