@@ -612,7 +612,14 @@ namespace {
 // 32 KiB tiles (2048 16-byte rows): ~42 KiB of LDS per workgroup, three workgroups per CU to
 // hide each one's load / rank / store latency chain (one 64 KiB-tile workgroup per CU ran at half
 // the rate); 16 rows per digit run at 7-bit digits.
-constexpr uint32_t kRpTileBytes = 32768;
+#ifndef DR_RP_TILE_BYTES
+#define DR_RP_TILE_BYTES 32768
+#endif
+#ifndef DR_RP_NT
+#define DR_RP_NT 256
+#endif
+constexpr uint32_t kRpTileBytes = DR_RP_TILE_BYTES;
+constexpr int kRpThreads = DR_RP_NT;              // rp_scatter workgroup
 constexpr uint64_t kRjEmpty = 0xFFFFFFFFFFFFFFFFull;
 constexpr uint32_t kRjCap = 2048;                 // LDS slots (16 B each: 32 KiB, 4 workgroups per CU)
 constexpr int kRjPer = 6;                         // rows per thread held in registers (1536 >= 0.75 cap)
@@ -706,20 +713,23 @@ __global__ __launch_bounds__(256) void rp_scan_kernel(const int64_t* __restrict_
 }
 
 template <int RW>
-__global__ __launch_bounds__(256) void rp_scatter_kernel(const uint32_t* __restrict__ rows, uint32_t* __restrict__ out,
+__global__ __launch_bounds__(kRpThreads) void rp_scatter_kernel(const uint32_t* __restrict__ rows, uint32_t* __restrict__ out,
                                                          const int64_t* __restrict__ seg_begin,
                                                          const int64_t* __restrict__ seg_len,
                                                          const int64_t* __restrict__ tile_base, uint32_t nseg,
                                                          uint64_t ntiles, uint32_t kw, int key_len, uint64_t seed,
                                                          int shift, int bits, const uint32_t* __restrict__ offsets) {
+  constexpr int NT = kRpThreads, NW = NT / 64;
   constexpr uint32_t TILE = kRpTileBytes / (4 * RW);
-  constexpr int ITEMS = TILE / kBlock;
+  constexpr int ITEMS = TILE / NT;
   constexpr uint32_t C = RW / 4;                    // 16-byte pieces per row
+  constexpr int PIECES = TILE * C / NT;             // staged 16-byte pieces per thread
+  static_assert(PIECES >= 1 && PIECES <= 8 && NT >= 256, "tile shape");
   const uint32_t D = 1u << bits, dmask = D - 1;
   __shared__ __attribute__((aligned(16))) uint4 srow[TILE * C];
   __shared__ uint16_t perm[TILE];
   __shared__ uint8_t dslot[TILE];
-  __shared__ uint32_t wcnt[4][256];
+  __shared__ uint32_t wcnt[NW][256];
   __shared__ uint32_t bstart[256];
   __shared__ uint32_t goff[256];
   __shared__ uint32_t sc[4];
@@ -731,15 +741,14 @@ __global__ __launch_bounds__(256) void rp_scatter_kernel(const uint32_t* __restr
     cnt = left < TILE ? (uint32_t)left : TILE;
     return reinterpret_cast<const uint4*>(rows + ((uint64_t)seg_begin[s] + r0) * RW);
   };
-  static_assert(TILE * C / kBlock == 8, "8 staged 16-byte pieces per thread");
-  // the next tile's 8 pieces per thread live in 8 named registers across the loop (an array here
-  // was placed in scratch)
+  // the next tile's pieces live in named registers across the loop (an array here was placed in
+  // scratch)
   uint4 p0, p1, p2, p3, p4, p5, p6, p7;
   const uint4* nsrc = nullptr;
   uint32_t ncnt = 0;
   auto issue = [&](const uint4* src, uint32_t pieces) {
     const uint32_t last = pieces ? pieces - 1 : 0;
-#define DR_RP_LD(I, P) { const uint32_t q = t + (I) * kBlock; P = src[q < pieces ? q : last]; }
+#define DR_RP_LD(I, P) if (PIECES > (I)) { const uint32_t q = t + (I) * NT; P = src[q < pieces ? q : last]; }
     DR_RP_LD(0, p0) DR_RP_LD(1, p1) DR_RP_LD(2, p2) DR_RP_LD(3, p3)
     DR_RP_LD(4, p4) DR_RP_LD(5, p5) DR_RP_LD(6, p6) DR_RP_LD(7, p7)
 #undef DR_RP_LD
@@ -752,7 +761,7 @@ __global__ __launch_bounds__(256) void rp_scatter_kernel(const uint32_t* __restr
     const uint32_t cnt = ncnt;
     {
       const uint32_t pieces = cnt * C;
-#define DR_RP_ST(I, P) { const uint32_t q = t + (I) * kBlock; if (q < pieces) srow[q] = P; }
+#define DR_RP_ST(I, P) if (PIECES > (I)) { const uint32_t q = t + (I) * NT; if (q < pieces) srow[q] = P; }
       DR_RP_ST(0, p0) DR_RP_ST(1, p1) DR_RP_ST(2, p2) DR_RP_ST(3, p3)
       DR_RP_ST(4, p4) DR_RP_ST(5, p5) DR_RP_ST(6, p6) DR_RP_ST(7, p7)
 #undef DR_RP_ST
@@ -761,13 +770,13 @@ __global__ __launch_bounds__(256) void rp_scatter_kernel(const uint32_t* __restr
       nsrc = locate(tile + gridDim.x, ncnt);
       issue(nsrc, ncnt * C);
     }
-    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    for (int i = t; i < NW * 256; i += NT) (&wcnt[0][0])[i] = 0;
     if ((uint32_t)t < D) goff[t] = offsets[tile * D + t];
     __syncthreads();
     uint32_t rk[ITEMS], dg[ITEMS];
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
-      const uint32_t pos = w * (TILE / 4) + r * 64 + l;
+      const uint32_t pos = w * (TILE / NW) + r * 64 + l;
       const bool valid = pos < cnt;
       const uint32_t d = valid ? rp_digit<RW>(reinterpret_cast<const uint32_t*>(srow) + pos * RW + kw, key_len, seed,
                                               shift, dmask)
@@ -787,14 +796,27 @@ __global__ __launch_bounds__(256) void rp_scatter_kernel(const uint32_t* __restr
       dg[r] = d;
     }
     __syncthreads();
-    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
-    wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
-    uint32_t all;
-    bstart[t] = block_exclusive_scan256(c0 + c1 + c2 + c3, sc, all);
-    __syncthreads();
+    uint32_t tot = 0;
+    if (t < 256) {
+#pragma unroll
+      for (int k = 0; k < NW; ++k) {
+        const uint32_t c = wcnt[k][t];
+        wcnt[k][t] = tot;
+        tot += c;
+      }
+    }
+    {
+      // exclusive scan of the 256 digit totals (waves 0..3; the other waves meet the barriers)
+      const uint32_t inc = wave_inclusive_scan(tot);
+      if (l == 63 && w < 4) sc[w] = inc;
+      __syncthreads();
+      const uint32_t b = (w > 0 ? sc[0] : 0) + (w > 1 ? sc[1] : 0) + (w > 2 ? sc[2] : 0);
+      if (t < 256) bstart[t] = b + inc - tot;
+      __syncthreads();
+    }
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
-      const uint32_t pos = w * (TILE / 4) + r * 64 + l;
+      const uint32_t pos = w * (TILE / NW) + r * 64 + l;
       if (pos < cnt) {
         const uint32_t slot = bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
         perm[slot] = (uint16_t)pos;
@@ -803,7 +825,7 @@ __global__ __launch_bounds__(256) void rp_scatter_kernel(const uint32_t* __restr
     }
     __syncthreads();
     uint4* o4 = reinterpret_cast<uint4*>(out);
-    for (uint32_t q = t; q < cnt * C; q += kBlock) {
+    for (uint32_t q = t; q < cnt * C; q += NT) {
       const uint32_t j = q / C, c = q - j * C;
       const uint32_t d = dslot[j];
       o4[((uint64_t)goff[d] + (j - bstart[d])) * C + c] = srow[(uint32_t)perm[j] * C + c];
@@ -953,13 +975,13 @@ DR_API int dr_radix_partition(const uint8_t* rows, uint8_t* out, uint32_t row_by
     rp_count_kernel<4><<<g, 256, 0, s>>>(in, seg_begin, seg_len, tile_base, nseg, ntiles, kw, (int)key_len, seed,
                                          shift, bits, counts);
     rp_scan_kernel<<<nseg, 256, 0, s>>>(seg_begin, tile_base, bits, counts, part_start, part_len);
-    rp_scatter_kernel<4><<<g, 256, 0, s>>>(in, o, seg_begin, seg_len, tile_base, nseg, ntiles, kw, (int)key_len, seed,
+    rp_scatter_kernel<4><<<g, kRpThreads, 0, s>>>(in, o, seg_begin, seg_len, tile_base, nseg, ntiles, kw, (int)key_len, seed,
                                            shift, bits, counts);
   } else {
     rp_count_kernel<8><<<g, 256, 0, s>>>(in, seg_begin, seg_len, tile_base, nseg, ntiles, kw, (int)key_len, seed,
                                          shift, bits, counts);
     rp_scan_kernel<<<nseg, 256, 0, s>>>(seg_begin, tile_base, bits, counts, part_start, part_len);
-    rp_scatter_kernel<8><<<g, 256, 0, s>>>(in, o, seg_begin, seg_len, tile_base, nseg, ntiles, kw, (int)key_len, seed,
+    rp_scatter_kernel<8><<<g, kRpThreads, 0, s>>>(in, o, seg_begin, seg_len, tile_base, nseg, ntiles, kw, (int)key_len, seed,
                                            shift, bits, counts);
   }
   DR_LAUNCH_CHECK();
