@@ -609,14 +609,16 @@ DR_API int dr_ht_probe_pairs(const uint8_t* prow, uint64_t np, uint32_t stride_p
 //              too large for the LDS table (key skew) are listed for the global-table path.
 namespace {
 
-// 32 KiB tiles (2048 16-byte rows): ~42 KiB of LDS per workgroup, three workgroups per CU to
-// hide each one's load / rank / store latency chain (one 64 KiB-tile workgroup per CU ran at half
-// the rate); 16 rows per digit run at 7-bit digits.
+// 64 KiB tiles (4096 16-byte rows) in 1024-thread workgroups: ~94 KiB of LDS, one workgroup of 16
+// waves per CU, 32 rows per digit run at 7-bit digits.  Join step 190.3 vs 201.5 ms against 32 KiB
+// tiles at three 256-thread workgroups per CU (rp_scatter 13.8 vs 15.1 ms per pass, fewer tiles
+// for rp_scan: profiles/r6/kernels/rp_shape_ab.txt); a 64 KiB tile in ONE 256-thread workgroup
+// per CU ran at half the rate (round 3): the 16 waves keep loads in flight while others rank.
 #ifndef DR_RP_TILE_BYTES
-#define DR_RP_TILE_BYTES 32768
+#define DR_RP_TILE_BYTES 65536
 #endif
 #ifndef DR_RP_NT
-#define DR_RP_NT 256
+#define DR_RP_NT 1024
 #endif
 constexpr uint32_t kRpTileBytes = DR_RP_TILE_BYTES;
 constexpr int kRpThreads = DR_RP_NT;              // rp_scatter workgroup
