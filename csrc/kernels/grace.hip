@@ -176,8 +176,9 @@ __global__ __launch_bounds__(256) void gp_offsets_kernel(uint32_t* __restrict__ 
 // ATOMIC (every destination appends at its fill counter, row order inside a destination free):
 // no count pass; each tile reserves its rows per destination with one atomicAdd on the fill
 // counter (a join's buckets do not need the input order).  Rows past cap are dropped and flagged.
-template <int ITEMS, int WC, int OWC, bool VEC, bool STAGE_PROJ = false, bool ATOMIC = false, int LDSW = 16384>
-__global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restrict__ rows, uint64_t n, uint32_t Wdyn,
+template <int ITEMS, int WC, int OWC, bool VEC, bool STAGE_PROJ = false, bool ATOMIC = false, int LDSW = 16384,
+          int NT = 256>
+__global__ __launch_bounds__(NT) void gp_scatter_kernel(const uint32_t* __restrict__ rows, uint64_t n, uint32_t Wdyn,
                                                          uint32_t kw, int key_len, uint64_t seed, int shift, uint32_t nb,
                                                          const uint32_t* __restrict__ prefix,
                                                          const int64_t* __restrict__ base,
@@ -186,11 +187,12 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
                                                          uint32_t G, uint64_t per_block, uint32_t OWdyn, uint32_t PO,
                                                          int64_t* __restrict__ fill = nullptr,
                                                          uint32_t* __restrict__ overflow = nullptr) {
-  constexpr int TILE = kBlock * ITEMS;
-  // projected tiles: 32 KiB, three workgroups per CU; rows of 129..512 bytes: one row per thread
-  // in a 128 KiB tile (one workgroup per CU)
-  constexpr int LDS_DW = STAGE_PROJ ? 8192 : LDSW;
+  constexpr int TILE = NT * ITEMS, NW = NT / 64;
+  // projected tiles: one 16-byte piece per row (kGpProjNT x kGpProjItems rows); rows of 129..512
+  // bytes: one row per thread in a 128 KiB tile (one workgroup per CU)
+  constexpr int LDS_DW = STAGE_PROJ ? TILE * 4 : LDSW;
   static_assert(STAGE_PROJ || LDS_DW >= kBlock * ITEMS, "tile");
+  static_assert(NT == kBlock || STAGE_PROJ, "wider workgroups stage projections only");
   static_assert(!STAGE_PROJ || OWC == 4, "staged projections are one 16-byte piece per row");
   const uint32_t W = WC > 0 ? (uint32_t)WC : Wdyn;
   const uint32_t OW = OWC > 0 ? (uint32_t)OWC : OWdyn;
@@ -200,7 +202,7 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
   __shared__ __attribute__((aligned(16))) uint32_t srow[LDS_DW];
   __shared__ uint16_t perm[TILE];
   __shared__ uint8_t dslot[TILE];
-  __shared__ uint32_t wcnt[4][kMaxBuckets];
+  __shared__ uint32_t wcnt[NW][kMaxBuckets];
   __shared__ int64_t goff[kMaxBuckets];
   __shared__ uint32_t bstart[kMaxBuckets];
   __shared__ uint64_t sptr[kMaxBuckets];
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
   const uint64_t end = beg + per_block < n ? beg + per_block : n;
   // STAGE_PROJ: one 16-byte piece per row, ITEMS per thread, the next tile's loads in flight
   // while this tile is ranked and written out
-  static_assert(!STAGE_PROJ || ITEMS == 8, "staged projections: 8 pieces per thread");
+  static_assert(!STAGE_PROJ || ITEMS <= 8, "staged projections: at most 8 pieces per thread");
   // STAGE_PROJ: the next tile's 8 pieces per thread in 8 named registers (an array is placed in
   // scratch), in flight while this tile is ranked and written out
   uint4 p0, p1, p2, p3, p4, p5, p6, p7;
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
     const uint32_t pieces = (uint32_t)((end - tb2) < (uint64_t)TILE ? (end - tb2) : TILE);
     const uint32_t last = pieces ? pieces - 1 : 0;
     const uint4* src = reinterpret_cast<const uint4*>(rows + tb2 * W);
-#define DR_GP_LD(I, P) { const uint32_t q = t + (I) * kBlock; P = src[(uint64_t)(q < pieces ? q : last) * pC + pP4]; }
+#define DR_GP_LD(I, P) if (ITEMS > (I)) { const uint32_t q = t + (I) * NT; P = src[(uint64_t)(q < pieces ? q : last) * pC + pP4]; }
     DR_GP_LD(0, p0) DR_GP_LD(1, p1) DR_GP_LD(2, p2) DR_GP_LD(3, p3)
     DR_GP_LD(4, p4) DR_GP_LD(5, p5) DR_GP_LD(6, p6) DR_GP_LD(7, p7)
 #undef DR_GP_LD
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
     const uint32_t cnt = (uint32_t)((end - tb) < (uint64_t)TILE ? (end - tb) : TILE);
     if (STAGE_PROJ) {
       uint4* s4 = reinterpret_cast<uint4*>(srow);
-#define DR_GP_ST(I, P) { const uint32_t q = t + (I) * kBlock; if (q < cnt) s4[q] = P; }
+#define DR_GP_ST(I, P) if (ITEMS > (I)) { const uint32_t q = t + (I) * NT; if (q < cnt) s4[q] = P; }
       DR_GP_ST(0, p0) DR_GP_ST(1, p1) DR_GP_ST(2, p2) DR_GP_ST(3, p3)
       DR_GP_ST(4, p4) DR_GP_ST(5, p5) DR_GP_ST(6, p6) DR_GP_ST(7, p7)
 #undef DR_GP_ST
@@ -246,14 +248,14 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
     } else {
       const uint32_t words = cnt * W;
       const uint32_t* src = rows + tb * W;
-      for (uint32_t j = t; j < words; j += kBlock) srow[j] = src[j];
+      for (uint32_t j = t; j < words; j += NT) srow[j] = src[j];
     }
-    wcnt[0][t] = 0; wcnt[1][t] = 0; wcnt[2][t] = 0; wcnt[3][t] = 0;
+    for (int i = t; i < NW * kMaxBuckets; i += NT) (&wcnt[0][0])[i] = 0;
     __syncthreads();
     uint32_t rk[ITEMS], dg[ITEMS];
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
-      const uint32_t pos = w * (TILE / 4) + r * 64 + l;
+      const uint32_t pos = w * (TILE / NW) + r * 64 + l;
       const bool valid = pos < cnt;
       uint32_t d = 0;
       if (valid) {
@@ -278,17 +280,30 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
       dg[r] = d;
     }
     __syncthreads();
-    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
-    const uint32_t tot = c0 + c1 + c2 + c3;
-    wcnt[0][t] = 0; wcnt[1][t] = c0; wcnt[2][t] = c0 + c1; wcnt[3][t] = c0 + c1 + c2;
-    uint32_t all;
-    bstart[t] = block_exclusive_scan256(tot, sc, all);
+    uint32_t tot = 0;
+    if (t < kMaxBuckets) {
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const uint32_t c = wcnt[q][t];
+        wcnt[q][t] = tot;
+        tot += c;
+      }
+    }
+    {
+      // exclusive scan of the 256 bucket totals (waves 0..3; other waves only meet the barriers)
+      const uint32_t inc = wave_inclusive_scan(tot);
+      if (l == 63 && w < 4) sc[w] = inc;
+      __syncthreads();
+      const uint32_t b0 = (w > 0 ? sc[0] : 0) + (w > 1 ? sc[1] : 0) + (w > 2 ? sc[2] : 0);
+      if (t < kMaxBuckets) bstart[t] = b0 + inc - tot;
+      __syncthreads();
+    }
     if (ATOMIC && (uint32_t)t < nb && tot)
       goff[t] = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(fill + t), (unsigned long long)tot);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
-      const uint32_t pos = w * (TILE / 4) + r * 64 + l;
+      const uint32_t pos = w * (TILE / NW) + r * 64 + l;
       if (pos < cnt) {
         const uint32_t slot = bstart[dg[r]] + wcnt[w][dg[r]] + rk[r];
         perm[slot] = (uint16_t)pos;
@@ -303,7 +318,7 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
       const uint32_t LC = LW / 4, OC = OW / 4, P4 = LPO / 4;
       const uint32_t chunks = cnt * OC;
       const uint4* s4 = reinterpret_cast<const uint4*>(srow);
-      for (uint32_t q = t; q < chunks; q += kBlock) {
+      for (uint32_t q = t; q < chunks; q += NT) {
         const uint32_t j = q / OC, c = q - j * OC;
         const uint32_t d = dslot[j];
         const int64_t row = goff[d] + (int64_t)(j - bstart[d]);
@@ -312,7 +327,7 @@ __global__ __launch_bounds__(256) void gp_scatter_kernel(const uint32_t* __restr
       }
     } else {
       const uint32_t words = cnt * OW;
-      for (uint32_t q = t; q < words; q += kBlock) {
+      for (uint32_t q = t; q < words; q += NT) {
         const uint32_t j = q / OW, c = q - j * OW;
         const uint32_t d = dslot[j];
         const int64_t row = goff[d] + (int64_t)(j - bstart[d]);
@@ -452,6 +467,18 @@ bool key_ok(uint32_t stride, uint32_t key_off, uint32_t key_len) {
 
 }  // namespace
 
+// Staged 16-byte projections: workgroup threads x pieces per thread (tile rows = product).  512 x 8
+// (4096-row 64 KiB tiles, one workgroup per CU) vs 256 x 8 (2048 rows, three per CU): 2.29 vs 2.64 ms
+// per 130M-row chunk of the 2 x 100 GB join, 1024 x 4 2.32 (profiles/r6/kernels/gp_shape_ab.txt).
+#ifndef DR_GP_PROJ_NT
+#define DR_GP_PROJ_NT 512
+#endif
+#ifndef DR_GP_PROJ_ITEMS
+#define DR_GP_PROJ_ITEMS 8
+#endif
+constexpr int kGpProjNT = DR_GP_PROJ_NT;
+constexpr int kGpProjItems = DR_GP_PROJ_ITEMS;
+
 // Rows up to this many bytes are partitioned (wide rows: one per thread, kWideLdsDw dwords of LDS).
 constexpr uint32_t kMaxStride = 512;
 constexpr int kWideLdsDw = 256 * (kMaxStride / 4);
@@ -492,14 +519,15 @@ DR_API int dr_grace_partition(const uint8_t* rows, uint64_t n, uint32_t stride, 
   const bool stage_proj = vec0 && out_stride == 16 && stride > 16 && key_off >= proj_off &&
                           key_off + key_len <= proj_off + out_stride;
   uint32_t G; uint64_t per_block;
-  geometry(n, stage_proj ? 2048 : (small ? 1024 : wide ? 256 : 512), G, per_block);
+  geometry(n, stage_proj ? kGpProjNT * kGpProjItems : (small ? 1024 : wide ? 256 : 512), G, per_block);
   uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
   uint64_t* totals = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(ws) + (((uint64_t)nb * G * 4 + 15) & ~15ull));
   const uint32_t W = stride / 4, kw = key_off / 4;
   const uint32_t* in = reinterpret_cast<const uint32_t*>(rows);
   if (unordered && stage_proj && contig_from >= nb) {
     // every destination appends at its fill counter: no count pass, one reservation per tile
-    gp_scatter_kernel<8, 0, 4, true, true, true><<<G, 256, 0, s>>>(in, n, W, kw, (int)key_len, seed, shift, nb,
+    gp_scatter_kernel<kGpProjItems, 0, 4, true, true, true, 16384, kGpProjNT><<<G, kGpProjNT, 0, s>>>(
+                                                                    in, n, W, kw, (int)key_len, seed, shift, nb,
                                                                     nullptr, nullptr, dst_ptr, cap, contig_from, G,
                                                                     per_block, out_stride / 4, proj_off / 4, fill,
                                                                     overflow);
@@ -515,7 +543,8 @@ DR_API int dr_grace_partition(const uint8_t* rows, uint64_t n, uint32_t stride, 
   gp_scatter_kernel<IT, WCV, OWCV, VECV><<<G, 256, 0, s>>>(in, n, W, kw, (int)key_len, seed, shift, nb, counts, \
                                                            bases, dst_ptr, cap, contig_from, G, per_block, OW, PO)
   if (stage_proj) {
-    gp_scatter_kernel<8, 0, 4, true, true><<<G, 256, 0, s>>>(in, n, W, kw, (int)key_len, seed, shift, nb, counts,
+    gp_scatter_kernel<kGpProjItems, 0, 4, true, true, false, 16384, kGpProjNT><<<G, kGpProjNT, 0, s>>>(
+                                                             in, n, W, kw, (int)key_len, seed, shift, nb, counts,
                                                              bases, dst_ptr, cap, contig_from, G, per_block, OW, PO);
   } else if (wide) {
     if (vec)
