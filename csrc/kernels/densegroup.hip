@@ -27,7 +27,7 @@
 #include "common.h"
 
 namespace {
-// Aggregate workgroups are 512 threads (8 waves); partition passes see DgSc.  Scattered 16-byte
+// Aggregate workgroups are kAgThreads (16 waves); partition passes see DgSc.  Scattered 16-byte
 // rows (2048-row tiles into 1024 buckets) measured 2.5-2.8x the written bytes at the memory side,
 // so a tile holds as many rows per bucket as the LDS allows.
 constexpr int kDgThreads = 512;
@@ -316,6 +316,15 @@ __global__ __launch_bounds__(DgSc<DB>::threads) __attribute__((amdgpu_waves_per_
   }
 }
 
+#ifndef DR_DG_AGG_NT
+#define DR_DG_AGG_NT 1024     // 16 waves per CU: 9.86 vs 11.92 ms at 512 (profiles/r6/kernels/dg_agg_ab.txt)
+#endif
+#ifndef DR_DG_AGG_U
+#define DR_DG_AGG_U 4
+#endif
+constexpr int kAgThreads = DR_DG_AGG_NT;      // aggregation workgroup (one per CU by its 112 KB table)
+constexpr int kAgWaves = kAgThreads / 64;
+
 struct DgAgg {
   uint32_t nacc;
   uint32_t pack;                 // PACK: the Sum accumulator that carries the count
@@ -327,13 +336,13 @@ struct DgAgg {
 
 // The rows are sorted by run id (key offset >> table bits); rstart[r] .. rstart[r + 1] are run r's
 // rows.  Workgroup b folds the runs [wrun[b], wrun[b + 1]) (equal row shares) into its LDS table,
-// kU * 512 rows per step with the next step's rows (possibly of the next run) in flight, and
+// kU * kAgThreads rows per step with the next step's rows (possibly of the next run) in flight, and
 // emits the table at the end of each run: no barrier inside a run.
 //
 // PACK (a Sum aggregate ag.pack of a field of <= 32 bits, runs of < 2^16 rows): the count rides
 // in the top 16 bits of that sum's 64-bit slot, one LDS atomic per row fewer.
 //
-// Emission: slot q * 512 + t is thread t's in round q.  Each wave compacts its occupied slots of a
+// Emission: slot q * kAgThreads + t is thread t's in round q.  Each wave compacts its occupied slots of a
 // round with a ballot, so every wave store writes one contiguous range of each output column (the
 // slot-major assignment wrote 8 scattered elements per thread and cost ~2.5x the bytes written).
 template <bool PACK>
@@ -344,9 +353,9 @@ __device__ __forceinline__ void dg_agg_body(const uint4* __restrict__ rows, cons
                                             unsigned long long (*acc)[kDgSlots], uint32_t* wtot,
                                             unsigned long long* obase) {
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
-  constexpr int kRounds = kDgSlots / kDgThreads;
-  constexpr int kU = 4;                                 // rows per thread per step
-  constexpr uint64_t kStep = (uint64_t)kU * kDgThreads;
+  constexpr int kRounds = kDgSlots / kAgThreads;
+  constexpr int kU = DR_DG_AGG_U;                       // rows per thread per step
+  constexpr uint64_t kStep = (uint64_t)kU * kAgThreads;
   constexpr unsigned long long kOne = 1ull << 48, kLow = kOne - 1;
   const int64_t r1 = wrun[blockIdx.x + 1];
   auto reset = [&](int sl) {
@@ -355,34 +364,34 @@ __device__ __forceinline__ void dg_agg_body(const uint4* __restrict__ rows, cons
     for (int a = 0; a < kDgMaxCols; ++a)
       if (a < (int)ag.nacc) acc[a][sl] = ag.op[a] == 1 ? ~0ull : 0ull;
   };
-  for (int q = 0; q < kRounds; ++q) reset(q * kDgThreads + t);
+  for (int q = 0; q < kRounds; ++q) reset(q * kAgThreads + t);
   auto emit = [&](uint64_t run) {
     uint32_t pos[kRounds];
     uint32_t mine = 0;
 #pragma unroll
     for (int q = 0; q < kRounds; ++q) {
-      const int sl = q * kDgThreads + t;
+      const int sl = q * kAgThreads + t;
       const bool occ = PACK ? acc[ag.pack][sl] != 0ull : cnt[sl] != 0u;
       const uint64_t bal = ballot64(occ);
       pos[q] = popc_below(bal);
       mine |= (uint32_t)occ << q;
-      if (l == 0) wtot[q * kDgWaves + w] = (uint32_t)__popcll(bal);
+      if (l == 0) wtot[q * kAgWaves + w] = (uint32_t)__popcll(bal);
     }
     __syncthreads();
-    static_assert(kRounds * kDgWaves <= 64, "one wave scans the per-(round, wave) counts");
+    static_assert(kRounds * kAgWaves <= 64, "one wave scans the per-(round, wave) counts");
     if (w == 0) {                        // exclusive scan of the (round, wave) counts, one lane each
-      const uint32_t c = l < kRounds * kDgWaves ? wtot[l] : 0u;
+      const uint32_t c = l < kRounds * kAgWaves ? wtot[l] : 0u;
       const uint32_t inc = wave_inclusive_scan(c);
-      if (l < kRounds * kDgWaves) wtot[l] = inc - c;
+      if (l < kRounds * kAgWaves) wtot[l] = inc - c;
       if (l == 63) *obase = atomicAdd(head, (unsigned long long)inc);
     }
     __syncthreads();
     uint64_t o = *obase;
 #pragma unroll
     for (int q = 0; q < kRounds; ++q) {
-      const uint32_t before = wtot[q * kDgWaves + w];
+      const uint32_t before = wtot[q * kAgWaves + w];
       if ((mine >> q) & 1u) {
-        const int sl = q * kDgThreads + t;
+        const int sl = q * kAgThreads + t;
         const uint64_t oo = o + before + pos[q];
         const uint32_t c = PACK ? (uint32_t)(acc[ag.pack][sl] >> 48) : cnt[sl];
         okey[oo] = kmin + (int64_t)((run << kDgTableBits) | (uint64_t)sl);
@@ -411,7 +420,7 @@ __device__ __forceinline__ void dg_agg_body(const uint4* __restrict__ rows, cons
   auto load = [&](uint64_t b, uint64_t e, uint4* dst) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const uint64_t i = b + (uint64_t)u * kDgThreads + t;
+      const uint64_t i = b + (uint64_t)u * kAgThreads + t;
       dst[u] = i < e ? rows[i] : make_uint4(0u, 0u, 0u, 0u);
     }
   };
@@ -427,7 +436,7 @@ __device__ __forceinline__ void dg_agg_body(const uint4* __restrict__ rows, cons
     if (more) load(nbg, ne, nbuf);                       // the next step in flight
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const uint64_t i = b + (uint64_t)u * kDgThreads + t;
+      const uint64_t i = b + (uint64_t)u * kAgThreads + t;
       if (i < e) {
         const uint4 rr = buf[u];
         const u128 v = (u128)rr.x | ((u128)rr.y << 32) | ((u128)rr.z << 64) | ((u128)rr.w << 96);
@@ -457,7 +466,7 @@ __device__ __forceinline__ void dg_agg_body(const uint4* __restrict__ rows, cons
   }
 }
 
-__global__ __launch_bounds__(kDgThreads) void dg_agg_kernel(const uint4* __restrict__ rows,
+__global__ __launch_bounds__(kAgThreads) void dg_agg_kernel(const uint4* __restrict__ rows,
                                                             const int64_t* __restrict__ rstart,
                                                             const int64_t* __restrict__ wrun, uint32_t kbits,
                                                             int64_t kmin, DgAgg ag, unsigned long long* __restrict__ head,
@@ -466,7 +475,7 @@ __global__ __launch_bounds__(kDgThreads) void dg_agg_kernel(const uint4* __restr
                                                             int64_t* __restrict__ oacc2, int pack) {
   __shared__ uint32_t cnt[kDgSlots];
   __shared__ unsigned long long acc[kDgMaxCols][kDgSlots];
-  __shared__ uint32_t wtot[(kDgSlots / kDgThreads) * kDgWaves];
+  __shared__ uint32_t wtot[(kDgSlots / kAgThreads) * kAgWaves];
   __shared__ unsigned long long obase;
   int64_t* const oacc[3] = {oacc0, oacc1, oacc2};
   if (pack)
@@ -578,7 +587,7 @@ DR_API int dr_dg_aggregate(const void* rows, const int64_t* rstart, const int64_
   ag.pack = pack > 0 ? (uint32_t)(pack - 1) : 0;
   if (pack && (ag.pack >= nacc || ag.op[ag.pack] != 0 || ag.field_bits[ag.pack] > 32)) return (int)hipErrorInvalidValue;
   if (G == 0) return 0;
-  dg_agg_kernel<<<G, kDgThreads, 0, s>>>(static_cast<const uint4*>(rows), rstart, wrun, kbits, kmin, ag, head, okey,
+  dg_agg_kernel<<<G, kAgThreads, 0, s>>>(static_cast<const uint4*>(rows), rstart, wrun, kbits, kmin, ag, head, okey,
                                          ocnt, nacc > 0 ? oacc[0] : nullptr, nacc > 1 ? oacc[1] : nullptr,
                                          nacc > 2 ? oacc[2] : nullptr, pack);
   DR_LAUNCH_CHECK();
