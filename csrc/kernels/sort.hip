@@ -243,8 +243,114 @@ __global__ __launch_bounds__(256) void rs_scatter_v3(const T* __restrict__ in, T
 }
 
 
+// Wide-workgroup pass for the count-matrix sorts: NT threads (NT / 64 waves, up to 16), ITEMS
+// entries per thread, the per-wave digit masks aliasing the stage (written only after the
+// ranking), digit-indexed work on threads < 256.  No register prefetch: the other waves' loads
+// are in flight while some rank or store.
+template <typename T, int ITEMS, int NT>
+__global__ __launch_bounds__(NT) void rs_scatter_w(const T* __restrict__ in, T* __restrict__ out, uint64_t n,
+                                                   int shift, const uint32_t* __restrict__ offsets, uint32_t G,
+                                                   uint64_t per_block) {
+  constexpr int kT = NT * ITEMS, kNW = NT / 64;
+  static_assert(NT >= kBins && kNW * kBins * 8 <= kT * (int)sizeof(T), "bins on 256 threads; masks fit the stage");
+  __shared__ T stage[kT];
+  __shared__ uint32_t wcnt[kNW][kBins];
+  __shared__ uint32_t goff[kBins];
+  __shared__ uint32_t bstart[kBins];
+  __shared__ uint32_t sc[4];
+  unsigned long long* wmask = reinterpret_cast<unsigned long long*>(stage);   // [kNW][kBins]
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const uint64_t beg = (uint64_t)blockIdx.x * per_block;
+  const uint64_t end = beg + per_block < n ? beg + per_block : n;
+  if (beg >= end) return;                                   // uniform
+  if (t < kBins) goff[t] = offsets[(uint64_t)t * G + blockIdx.x];
+  const unsigned long long lanebit = 1ull << l;
+  for (uint64_t base = beg; base < end; base += kT) {
+    const uint32_t cnt = (uint32_t)((end - base) < (uint64_t)kT ? (end - base) : kT);
+    T cur[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kT / kNW) + r * 64 + l;
+      if (pos < cnt) cur[r] = in[base + pos];
+    }
+    for (int i = t; i < kNW * kBins; i += NT) {
+      wmask[i] = 0ull;
+      (&wcnt[0][0])[i] = 0;
+    }
+    __syncthreads();
+    uint32_t rk[ITEMS], dg[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kT / kNW) + r * 64 + l;
+      const bool valid = pos < cnt;
+      const uint32_t d = valid ? digit_of(cur[r], shift) : 0u;
+      unsigned long long* wm = wmask + w * kBins;
+      if (valid) atomicOr(&wm[d], lanebit);
+      __builtin_amdgcn_wave_barrier();
+      const unsigned long long peers = valid ? wm[d] : 0ull;
+      const uint32_t below = popc_below(peers);
+      const uint32_t prior = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) {
+        wcnt[w][d] = prior + (uint32_t)__popcll(peers);
+        wm[d] = 0ull;
+      }
+      __builtin_amdgcn_wave_barrier();
+      rk[r] = prior + below;
+      dg[r] = d;
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+    if (t < kBins) {
+#pragma unroll
+      for (int k = 0; k < kNW; ++k) {
+        const uint32_t c = wcnt[k][t];
+        wcnt[k][t] = tot;
+        tot += c;
+      }
+    }
+    {
+      const uint32_t inc = wave_inclusive_scan(tot);
+      if (l == 63 && w < 4) sc[w] = inc;
+      __syncthreads();
+      const uint32_t b = (w > 0 ? sc[0] : 0) + (w > 1 ? sc[1] : 0) + (w > 2 ? sc[2] : 0);
+      if (t < kBins) bstart[t] = b + inc - tot;
+      __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t pos = w * (kT / kNW) + r * 64 + l;
+      if (pos < cnt) stage[bstart[dg[r]] + wcnt[w][dg[r]] + rk[r]] = cur[r];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (uint32_t j = t; j < cnt; j += NT) {
+      const T v = stage[j];
+      const uint32_t d = digit_of(v, shift);
+      out[(uint64_t)goff[d] + (j - bstart[d])] = v;
+    }
+    __syncthreads();
+    if (t < kBins) goff[t] += tot;
+  }
+}
+
+// E128 count-matrix sort pass: 1024 threads x 8 entries (8192-entry, 128 KB tiles): 4.24 vs 5.72 ms per
+// pass of 5e8 entries for rs_scatter_v2 at 256 x 8 (profiles/r6/kernels/sort_shape_ab.txt)
+#ifndef DR_SORT_NT
+#define DR_SORT_NT 1024                        // 256: rs_scatter_v2
+#endif
+#ifndef DR_SORT_ITEMS
+#define DR_SORT_ITEMS 8
+#endif
+// E64 dr_sort_u64 pass: 512 threads x 16 (8192-entry tiles): 6.74 vs 7.48 ms per 10 GB pass for
+// rs_scatter_v3 at 256 x 16; 1024 x 16 6.87 (two VGPRs spill)
+#ifndef DR_SORT64_NT
+#define DR_SORT64_NT 512                       // 256: rs_scatter_v3 x 16
+#endif
+constexpr uint64_t kSortTile = (uint64_t)DR_SORT_NT * DR_SORT_ITEMS;
+
 inline void sort_geometry(uint64_t n, uint32_t& G, uint64_t& per_block) {
-  const uint64_t tile = (uint64_t)kTile;
+  const uint64_t tile = kSortTile;
   uint64_t tiles = (n + tile - 1) / tile;
   if (tiles < 1) tiles = 1;
   G = (uint32_t)(tiles < (uint64_t)kMaxGrid ? tiles : (uint64_t)kMaxGrid);
@@ -253,7 +359,11 @@ inline void sort_geometry(uint64_t n, uint32_t& G, uint64_t& per_block) {
 
 void launch_scatter(const E128* in, E128* out, uint64_t n, int shift, const uint32_t* offsets, uint32_t G,
                     uint64_t per_block, hipStream_t s) {
+#if DR_SORT_NT == 256
   rs_scatter_v2<E128, kItems><<<G, 256, 0, s>>>(in, out, n, shift, offsets, G, per_block);
+#else
+  rs_scatter_w<E128, DR_SORT_ITEMS, DR_SORT_NT><<<G, DR_SORT_NT, 0, s>>>(in, out, n, shift, offsets, G, per_block);
+#endif
 }
 
 }  // namespace
@@ -1654,7 +1764,7 @@ DR_API int dr_sort_u64(E64* keys, E64* tmp, uint64_t n, int begin_bit, int end_b
   if (end_bit > 64 || begin_bit < 0 || (begin_bit & 7) || (end_bit & 7)) return (int)hipErrorInvalidValue;
   if (n >= (1ull << 32)) return (int)hipErrorInvalidValue;
   constexpr int ITEMS = 16;
-  const uint64_t tile = (uint64_t)kBlock * ITEMS;
+  const uint64_t tile = (uint64_t)DR_SORT64_NT * ITEMS;
   uint64_t tiles = (n + tile - 1) / tile;
   if (tiles < 1) tiles = 1;
   const uint32_t G = (uint32_t)(tiles < (uint64_t)kMaxGrid ? tiles : (uint64_t)kMaxGrid);
@@ -1667,7 +1777,11 @@ DR_API int dr_sort_u64(E64* keys, E64* tmp, uint64_t n, int begin_bit, int end_b
   for (int shift = begin_bit; shift < end_bit; shift += kRadixBits) {
     rs_count<<<G, 256, 0, s>>>(src, n, shift, counts, G, per_block);
     scan_inplace(counts, kBins * G, partial, s);
+#if DR_SORT64_NT == 256
     rs_scatter_v3<E64, ITEMS><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+#else
+    rs_scatter_w<E64, ITEMS, DR_SORT64_NT><<<G, DR_SORT64_NT, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+#endif
     E64* x = src; src = dst; dst = x;
     flips ^= 1;
   }
