@@ -650,6 +650,8 @@ namespace {
 #define DR_RP_NT 1024
 #endif
 constexpr uint32_t kRpTileBytes = DR_RP_TILE_BYTES;
+constexpr uint32_t kRaTileBytes = 32768;          // radix-aggregation pass A (ra_cols_*): 256-thread
+                                                  // workgroups, the next tile's columns in registers
 constexpr int kRpThreads = DR_RP_NT;              // rp_scatter workgroup
 constexpr uint64_t kRjEmpty = 0xFFFFFFFFFFFFFFFFull;
 constexpr uint32_t kRjCap = 2048;                 // LDS slots (16 B each: 32 KiB, 4 workgroups per CU)
@@ -1124,7 +1126,7 @@ template <int RW>
 __global__ __launch_bounds__(256) void ra_cols_count_kernel(const uint64_t* __restrict__ key, uint64_t n,
                                                             uint64_t ntiles, uint64_t seed, int shift, int bits,
                                                             uint32_t* __restrict__ counts) {
-  constexpr uint32_t TILE = kRpTileBytes / (4 * RW);
+  constexpr uint32_t TILE = kRaTileBytes / (4 * RW);
   const uint32_t D = 1u << bits, dmask = D - 1;
   __shared__ uint32_t hist[4][256];
   const int t = threadIdx.x, w = wave_id();
@@ -1150,7 +1152,7 @@ template <int RW>
 __global__ __launch_bounds__(256) void ra_cols_scatter_kernel(RaCols in, uint64_t n, uint64_t ntiles, uint64_t seed,
                                                               int shift, int bits, const uint32_t* __restrict__ offsets,
                                                               uint32_t* __restrict__ out) {
-  constexpr uint32_t TILE = kRpTileBytes / (4 * RW);
+  constexpr uint32_t TILE = kRaTileBytes / (4 * RW);
   constexpr int ITEMS = TILE / kBlock;
   constexpr uint32_t C = RW / 4;
   const uint32_t D = 1u << bits, dmask = D - 1;
@@ -1435,7 +1437,7 @@ DR_API int dr_radix_agg_pack(const int64_t* key, const void* const* vals, int nv
   in.key = reinterpret_cast<const uint64_t*>(key);
   for (int j = 0; j < nval; ++j) in.val[j] = reinterpret_cast<const uint64_t*>(vals[j]);
   in.nval = nval;
-  const uint32_t tile = kRpTileBytes / row_bytes;
+  const uint32_t tile = kRaTileBytes / row_bytes;
   const uint64_t ntiles = (n + tile - 1) / tile;
   const unsigned g = (unsigned)(ntiles < kRpGrid ? ntiles : kRpGrid);
   // counts / offsets per workgroup (its contiguous tile range), so rp_scan's "tiles" are the g
@@ -1456,7 +1458,7 @@ DR_API int dr_radix_agg_pack(const int64_t* key, const void* const* vals, int nv
 }
 
 DR_API uint32_t dr_radix_agg_pack_grid(uint64_t n, uint32_t row_bytes) {
-  const uint64_t ntiles = (n + kRpTileBytes / row_bytes - 1) / (kRpTileBytes / row_bytes);
+  const uint64_t ntiles = (n + kRaTileBytes / row_bytes - 1) / (kRaTileBytes / row_bytes);
   return (uint32_t)(ntiles < kRpGrid ? (ntiles ? ntiles : 1) : kRpGrid);
 }
 
