@@ -369,11 +369,14 @@ void launch_scatter(const E128* in, E128* out, uint64_t n, int shift, const uint
 }  // namespace
 
 // Workspace needed by dr_sort_u128 (bytes).
+// Sized for the finest workgroup geometry of any sort that takes this workspace: kTile (2048-entry)
+// tiles, finer than dr_sort_u64_expand's 4096 and the E128 / E64 passes' 8192 (a workspace sized
+// by the coarser sort_geometry let the expand sort's count matrix overrun it).
 DR_API uint64_t dr_sort_u128_workspace(uint64_t n) {
-  uint32_t G; uint64_t per_block;
-  sort_geometry(n, G, per_block);
-  const uint64_t M = (uint64_t)kBins * G;
-  return (M + 1024) * sizeof(uint32_t);
+  uint64_t tiles = (n + kTile - 1) / kTile;
+  if (tiles < 1) tiles = 1;
+  const uint64_t G = tiles < (uint64_t)kMaxGrid ? tiles : (uint64_t)kMaxGrid;
+  return ((uint64_t)kBins * G + 1024) * sizeof(uint32_t);
 }
 
 // Stable LSD radix sort of `n` entries on composite key bits [begin_bit, end_bit) (multiples of 8;
