@@ -214,7 +214,12 @@ class PinnedHostBuffer:
 
     def release(self):
         if self.registered:
-            self.wait()                # a DMA still queued on the pages must finish before they unlock
+            # a DMA still queued on the pages must finish before they unlock: the last lease's event,
+            # or (a buffer dropped without a lease release, its copies untracked) the whole device
+            if self.pending is not None:
+                self.wait()
+            elif torch.cuda.is_available() and torch.cuda.is_initialized():
+                torch.cuda.synchronize()
             hip_runtime().hipHostUnregister(ctypes.c_void_p(self.tensor.data_ptr()))
             self.registered = False
         self.tensor = None
@@ -236,7 +241,8 @@ PINNED_KEEP_BYTES = 16 << 30       # ... and as many more as fit this many bytes
 
 
 class PinnedLease:
-    """A ``shape`` view into a pooled page-locked buffer; ``release()`` returns it to the pool."""
+    """A ``shape`` view into a pooled page-locked buffer; ``release()`` returns it to the pool (a
+    lease dropped without it is released when collected, so its queued copies stay covered)."""
 
     def __init__(self, buf: PinnedHostBuffer, shape, dtype):
         self._buf = buf
@@ -261,6 +267,12 @@ class PinnedLease:
                 _PINNED_FREE.pop(0).release()
             self._buf = None
         self.tensor = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:  # noqa: BLE001
+            pass
 
 
 def pinned_lease(shape, dtype=torch.uint8) -> PinnedLease:

@@ -210,3 +210,12 @@ def test_sort_rows_compact_recovers_from_failed_lookback(monkeypatch):
     assert calls == [True, False] and "look-back failed" in info["path"]
     acc = TS.check(got)
     assert int(acc[1].item()) == 0 and int(acc[0].item()) == int(TS.check(rows)[0].item())
+
+
+def test_sort_workspace_covers_every_geometry():
+    """dr_sort_u128_workspace must hold the count matrix of the finest-grained sort that takes it
+    (dr_sort_u64_expand: 4096-entry tiles), not only the E128 passes' 8192-entry geometry."""
+    from dryad_amd.ops import _lib
+    for n in (1, 5000, 500_000, 3_000_000, 1 << 31):
+        g = min((n + 4095) // 4096, 1024)
+        assert int(_lib.lib().dr_sort_u128_workspace(n)) >= (256 * g + 1024) * 4, n
