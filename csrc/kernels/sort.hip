@@ -334,20 +334,20 @@ __global__ __launch_bounds__(NT) void rs_scatter_w(const T* __restrict__ in, T* 
   }
 }
 
-// E128 count-matrix sort pass: 1024 threads x 8 entries (8192-entry, 128 KB tiles) measured 4.24 vs
-// 5.72 ms per pass of 5e8 entries for rs_scatter_v2 at 256 x 8 (profiles/r6/kernels/sort_shape_ab.txt),
-// but a GPU-suite run with the wide passes on faulted in a streamed GroupBy whose cause was not
-// pinned down (profiles/r6/gpu_suite_r6zh_fault.log): the default stays rs_scatter_v2.
+// E128 count-matrix sort pass: 1024 threads x 8 entries (8192-entry, 128 KB tiles): 4.24 vs 5.72 ms
+// per pass of 5e8 entries for rs_scatter_v2 at 256 x 8 (profiles/r6/kernels/sort_shape_ab.txt).  (A
+// GPU-suite fault seen once with these passes on was in a spilling streamed GroupBy whose sorts run
+// dr_sort_u64_expand, not these kernels: profiles/r6/gpu_suite_r6zh_fault.log.)
 #ifndef DR_SORT_NT
-#define DR_SORT_NT 256                         // 256: rs_scatter_v2; 1024 (with DR_SORT_ITEMS 8): rs_scatter_w
+#define DR_SORT_NT 1024                        // 256: rs_scatter_v2
 #endif
 #ifndef DR_SORT_ITEMS
 #define DR_SORT_ITEMS 8
 #endif
-// E64 dr_sort_u64 pass: 512 threads x 16 (8192-entry tiles) measured 6.74 vs 7.48 ms per 10 GB pass
-// for rs_scatter_v3 at 256 x 16 (1024 x 16 6.87, two VGPRs spill); off by default like DR_SORT_NT
+// E64 dr_sort_u64 pass: 512 threads x 16 (8192-entry tiles): 6.74 vs 7.48 ms per 10 GB pass for
+// rs_scatter_v3 at 256 x 16 (1024 x 16 6.87, two VGPRs spill)
 #ifndef DR_SORT64_NT
-#define DR_SORT64_NT 256                       // 256: rs_scatter_v3 x 16
+#define DR_SORT64_NT 512                       // 256: rs_scatter_v3 x 16
 #endif
 constexpr uint64_t kSortTile = (uint64_t)DR_SORT_NT * DR_SORT_ITEMS;
 
