@@ -1176,11 +1176,21 @@ DR_API int dr_hi_flags(const uint64_t* entries, uint32_t words, uint64_t n, int6
 
 namespace {
 
-// ITEMS entries per thread per tile: E256 8 (2048-entry tile, 64 KiB LDS stage, ~256 contiguous
-// output bytes per digit run), E320 4 (40 KiB stage, three workgroups per CU)
-template <typename T, int ITEMS>
+// NT = 1024 (rs_scatter_w): one wide workgroup per CU with a 4096-entry E256 tile (128 KiB) or a
+// 3072-entry E320 tile (120 KiB): E256 pass 3.21 vs 4.47 ms for rs_scatter_v2 at 256 threads x 8
+// (2048-entry, 64 KiB tiles; profiles/r6/kernels/sortwide_ab.txt).  NT = 256 selects rs_scatter_v2.
+#ifndef DR_SORTW_NT
+#define DR_SORTW_NT 1024
+#endif
+#ifndef DR_SORTW_ITEMS256
+#define DR_SORTW_ITEMS256 4
+#endif
+#ifndef DR_SORTW_ITEMS320
+#define DR_SORTW_ITEMS320 3
+#endif
+template <typename T, int ITEMS, int NT>
 int sort_wide(T* keys, T* tmp, uint64_t n, int begin_bit, int end_bit, void* ws, hipStream_t s, int* result_in_tmp) {
-  const uint64_t tile = (uint64_t)kBlock * ITEMS;
+  const uint64_t tile = (uint64_t)NT * ITEMS;
   uint64_t tiles = (n + tile - 1) / tile;
   if (tiles < 1) tiles = 1;
   const uint32_t G = (uint32_t)(tiles < (uint64_t)kMaxGrid ? tiles : (uint64_t)kMaxGrid);
@@ -1193,7 +1203,10 @@ int sort_wide(T* keys, T* tmp, uint64_t n, int begin_bit, int end_bit, void* ws,
   for (int shift = begin_bit; shift < end_bit; shift += kRadixBits) {
     rs_count<<<G, 256, 0, s>>>(src, n, shift, counts, G, per_block);
     scan_inplace(counts, kBins * G, partial, s);
-    rs_scatter_v2<T, ITEMS><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+    if constexpr (NT == 256)
+      rs_scatter_v2<T, ITEMS><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+    else
+      rs_scatter_w<T, ITEMS, NT><<<G, NT, 0, s>>>(src, dst, n, shift, counts, G, per_block);
     T* x = src; src = dst; dst = x;
     flips ^= 1;
   }
@@ -1215,11 +1228,11 @@ DR_API int dr_sort_wide(int words, void* keys, void* tmp, uint64_t n, int begin_
   if ((begin_bit & 7) && begin_bit < 64) return (int)hipErrorInvalidValue;
   if (n >= (1ull << 32)) return (int)hipErrorInvalidValue;
   if (words == 4)
-    return sort_wide<E256, 8>(static_cast<E256*>(keys), static_cast<E256*>(tmp), n, begin_bit, end_bit, ws, s,
-                              result_in_tmp);
+    return sort_wide<E256, DR_SORTW_ITEMS256, DR_SORTW_NT>(static_cast<E256*>(keys), static_cast<E256*>(tmp), n,
+                                                           begin_bit, end_bit, ws, s, result_in_tmp);
   if (words == 5)
-    return sort_wide<E320, 4>(static_cast<E320*>(keys), static_cast<E320*>(tmp), n, begin_bit, end_bit, ws, s,
-                              result_in_tmp);
+    return sort_wide<E320, DR_SORTW_ITEMS320, DR_SORTW_NT>(static_cast<E320*>(keys), static_cast<E320*>(tmp), n,
+                                                           begin_bit, end_bit, ws, s, result_in_tmp);
   return (int)hipErrorInvalidValue;
 }
 
