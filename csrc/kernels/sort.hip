@@ -1819,7 +1819,9 @@ DR_API int dr_sort_u64_expand(E64* keys, E64* tmp, E128* out, uint64_t n, int be
     return (int)hipErrorInvalidValue;
   if (n >= (1ull << 32)) return (int)hipErrorInvalidValue;
   constexpr int ITEMS = 16;
-  const uint64_t tile = (uint64_t)kBlock * ITEMS;
+  // the dr_sort_u64 geometry (DR_SORT64_NT x 16 entries per tile); the last, expanding pass keeps
+  // rs_scatter_v2 (256 threads walk the workgroup's slice in 4096-entry tiles)
+  const uint64_t tile = (uint64_t)DR_SORT64_NT * ITEMS;
   uint64_t tiles = (n + tile - 1) / tile;
   if (tiles < 1) tiles = 1;
   const uint32_t G = (uint32_t)(tiles < (uint64_t)kMaxGrid ? tiles : (uint64_t)kMaxGrid);
@@ -1835,7 +1837,11 @@ DR_API int dr_sort_u64_expand(E64* keys, E64* tmp, E128* out, uint64_t n, int be
       rs_scatter_v2<E64, ITEMS, true><<<G, 256, 0, s>>>(src, reinterpret_cast<E64*>(out), n, shift, counts, G,
                                                         per_block, bias);
     } else {
+#if DR_SORT64_NT == 256
       rs_scatter_v2<E64, ITEMS><<<G, 256, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+#else
+      rs_scatter_w<E64, ITEMS, DR_SORT64_NT><<<G, DR_SORT64_NT, 0, s>>>(src, dst, n, shift, counts, G, per_block);
+#endif
       E64* x = src; src = dst; dst = x;
     }
   }
