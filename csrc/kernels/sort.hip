@@ -334,20 +334,21 @@ __global__ __launch_bounds__(NT) void rs_scatter_w(const T* __restrict__ in, T* 
   }
 }
 
-// E128 count-matrix sort pass: 1024 threads x 8 entries (8192-entry, 128 KB tiles): 4.24 vs 5.72 ms
-// per pass of 5e8 entries for rs_scatter_v2 at 256 x 8 (profiles/r6/kernels/sort_shape_ab.txt).  (A
-// GPU-suite fault seen once with these passes on was in a spilling streamed GroupBy whose sorts run
-// dr_sort_u64_expand, not these kernels: profiles/r6/gpu_suite_r6zh_fault.log.)
+// E128 count-matrix sort pass: 1024 threads x 8 entries (8192-entry, 128 KB tiles) measured 4.24 vs
+// 5.72 ms per pass of 5e8 entries for rs_scatter_v2 at 256 x 8 (profiles/r6/kernels/sort_shape_ab.txt),
+// but two of three GPU-suite runs with the wide sort passes on hit an illegal address in a streamed
+// GroupBy (profiles/r6/gpu_suite_r6zh_fault.log, gpu_suite_r6zm_fault.log) and none with them off:
+// every count-matrix sort stays on its 256-thread kernel until that is understood.
 #ifndef DR_SORT_NT
-#define DR_SORT_NT 1024                        // 256: rs_scatter_v2
+#define DR_SORT_NT 256                         // 256: rs_scatter_v2; 1024 (DR_SORT_ITEMS 8): rs_scatter_w
 #endif
 #ifndef DR_SORT_ITEMS
 #define DR_SORT_ITEMS 8
 #endif
-// E64 dr_sort_u64 pass: 512 threads x 16 (8192-entry tiles): 6.74 vs 7.48 ms per 10 GB pass for
-// rs_scatter_v3 at 256 x 16 (1024 x 16 6.87, two VGPRs spill)
+// E64 dr_sort_u64 pass: 512 threads x 16 (8192-entry tiles) measured 6.74 vs 7.48 ms per 10 GB pass
+// for rs_scatter_v3 at 256 x 16 (1024 x 16 6.87, two VGPRs spill); off, as DR_SORT_NT
 #ifndef DR_SORT64_NT
-#define DR_SORT64_NT 512                       // 256: rs_scatter_v3 x 16
+#define DR_SORT64_NT 256                       // 256: rs_scatter_v3 x 16 (and v2 in the expand sort)
 #endif
 constexpr uint64_t kSortTile = (uint64_t)DR_SORT_NT * DR_SORT_ITEMS;
 
@@ -1179,14 +1180,15 @@ namespace {
 // NT = 1024 (rs_scatter_w): one wide workgroup per CU with a 4096-entry E256 tile (128 KiB) or a
 // 3072-entry E320 tile (120 KiB): E256 pass 3.21 vs 4.47 ms for rs_scatter_v2 at 256 threads x 8
 // (2048-entry, 64 KiB tiles; profiles/r6/kernels/sortwide_ab.txt).  NT = 256 selects rs_scatter_v2.
+// Off by default like DR_SORT_NT (256 threads x 8 E256 / x 4 E320 through rs_scatter_v2).
 #ifndef DR_SORTW_NT
-#define DR_SORTW_NT 1024
+#define DR_SORTW_NT 256
 #endif
 #ifndef DR_SORTW_ITEMS256
-#define DR_SORTW_ITEMS256 4
+#define DR_SORTW_ITEMS256 8
 #endif
 #ifndef DR_SORTW_ITEMS320
-#define DR_SORTW_ITEMS320 3
+#define DR_SORTW_ITEMS320 4
 #endif
 template <typename T, int ITEMS, int NT>
 int sort_wide(T* keys, T* tmp, uint64_t n, int begin_bit, int end_bit, void* ws, hipStream_t s, int* result_in_tmp) {
